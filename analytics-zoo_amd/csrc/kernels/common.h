@@ -1,0 +1,94 @@
+// Shared device helpers for the zoo CDNA4 (gfx950) kernel library.
+//
+// Everything here is written for MI355X directly: 64-lane wavefronts,
+// v_mfma_f32_16x16x32_bf16 matrix cores, 160 KiB LDS per CU and 8 XCDs.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define ZOO_DEV __device__ __forceinline__
+
+namespace zoo {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef uint16_t bf16_t;  // raw storage type for bf16 in global memory
+
+constexpr int kWave = 64;
+
+ZOO_DEV float bf2f(bf16_t v) {
+  return __uint_as_float(((uint32_t)v) << 16);
+}
+
+// Round-to-nearest-even f32 -> bf16. Plain cast lowers to v_cvt_pk_bf16_f32 on
+// gfx950 and keeps NaNs NaN (MI355X_MICROARCH.md "Correctness boundaries").
+ZOO_DEV bf16_t f2bf(float f) {
+  __bf16 b = (__bf16)f;
+  return __builtin_bit_cast(bf16_t, b);
+}
+
+ZOO_DEV uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+
+ZOO_DEV void unpack8(const uint4& v, float* f) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+ZOO_DEV uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2bf(f[0], f[1]);
+  r.y = pack2bf(f[2], f[3]);
+  r.z = pack2bf(f[4], f[5]);
+  r.w = pack2bf(f[6], f[7]);
+  return r;
+}
+
+ZOO_DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+ZOO_DEV float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware block remap (cdna_hip_programming.md §5 "XCD swizzle must
+// be bijective"): blocks b and b+8 share an XCD under round-robin dispatch, so
+// give each XCD group a contiguous range of logical tiles -> neighbouring tiles
+// (which share operand panels) hit the same L2.
+ZOO_DEV int xcd_remap(int orig, int nwg) {
+  if (nwg <= 8) return orig;
+  const int q = nwg / 8, r = nwg % 8;
+  const int xcd = orig % 8;
+  const int base = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+  return base + orig / 8;
+}
+
+ZOO_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// Activation codes shared with the Python side (zoo/ops/_codes.py).
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SIGMOID = 3, ACT_TANH = 4 };
+
+ZOO_DEV float apply_act(float x, int act) {
+  switch (act) {
+    case ACT_RELU: return x > 0.f ? x : 0.f;
+    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
+    case ACT_TANH: return tanhf(x);
+    default: return x;
+  }
+}
+
+}  // namespace zoo

@@ -1,0 +1,395 @@
+// Implicit-GEMM convolution / GEMM on CDNA4 matrix cores (gfx950).
+//
+// One kernel template covers every "K-contiguous" GEMM in the framework:
+//   * conv forward (NHWC activations, weights [Cout][R][S][Cin])
+//   * conv data-gradient (a transposed conv: input dilation = forward stride,
+//     weights pre-flipped to [Cin][R][S][Cout] by `flip_weights_kernel`)
+//   * 1x1 convs and Linear layers (A is a plain row-major [M][K] matrix)
+//
+// Replaces the reference's MKL im2col+sgemm / MKL-DNN conv primitives
+// (BigDL SpatialConvolution, used by Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110
+// and Dense.scala) — see SURVEY.md §2.16 HK1/HK3/HK5.
+//
+// Tiling: BM=128 rows (output pixels) x BN={64,128} cols (output channels) x
+// BK=64, 256 threads = 4 waves in a 2x2 grid, each wave owns a 64 x BN/2 tile
+// computed with v_mfma_f32_16x16x32_bf16 (8 bf16 per lane per operand).
+// A/B tiles are register-staged (the im2col gather needs per-lane addresses and
+// zero-fill for padding) into a double-buffered, XOR-swizzled LDS image; the
+// global loads of tile k+1 are in flight while tile k is on the MFMA pipe.
+// The epilogue stages the fp32 accumulators through LDS so that every global
+// store is a full 16-byte row segment, and optionally fuses bias, residual add,
+// activation and per-channel BatchNorm statistics (sum, sum of squares).
+#include "common.h"
+
+namespace zoo {
+
+struct ConvGeom {
+  int N, H, W, C;        // input activation, NHWC
+  int K;                 // output channels (GEMM N dimension)
+  int R, S;              // filter
+  int P, Q;              // output spatial
+  int sh, sw, ph, pw;    // stride / padding (in the possibly-dilated input space)
+  int dh, dw;            // filter dilation
+  int lh, lw;            // input dilation (1 = plain conv; >1 = transposed conv)
+  int M;                 // N*P*Q
+  int Ktot;              // R*S*C (logical reduction length)
+  int ldb;               // leading dim of the weight matrix (>= Ktot, %8 == 0)
+};
+
+constexpr int IG_BM = 128, IG_BK = 64, IG_NT = 256;
+
+ZOO_DEV int ig_swz(int row) { return (row >> 1) & 7; }
+
+template <int VEC, bool IS1x1, bool LDIL, int BN>
+__global__ __launch_bounds__(256, 2) void igemm_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y,
+    float* __restrict__ Yf, const float* __restrict__ bias, const bf16_t* __restrict__ resid,
+    float* __restrict__ stats, ConvGeom g, int act) {
+  constexpr int BM = IG_BM, BK = IG_BK;
+  constexpr int WN = BN / 2;      // wave tile width
+  constexpr int NJ = WN / 16;     // 16-wide n tiles per wave
+  constexpr int NI = 4;           // 16-high m tiles per wave (wave tile height 64)
+  constexpr int B_ROWS_PER_THREAD = BN / 32;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* Bs = As + 2 * BM * BK;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int ntn = (g.K + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  // ---- staging assignment: thread -> (16-byte k-chunk, rows) ----
+  const int cc = tid & 7;
+  const int rbase = tid >> 3;  // 0..31
+
+  // per-row precompute for the A (activation) gather
+  int a_base[4], a_ih[4], a_iw[4];
+  bool a_ok[4];
+  const int PQ = g.P * g.Q;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + rbase + 32 * i;
+    a_ok[i] = m < g.M;
+    const int mm = a_ok[i] ? m : 0;
+    if constexpr (IS1x1) {
+      a_base[i] = mm * g.C;
+      a_ih[i] = a_iw[i] = 0;
+    } else {
+      const int n = mm / PQ;
+      const int pq = mm - n * PQ;
+      const int p = pq / g.Q;
+      const int q = pq - p * g.Q;
+      a_base[i] = n * g.H * g.W * g.C;
+      a_ih[i] = p * g.sh - g.ph;
+      a_iw[i] = q * g.sw - g.pw;
+    }
+  }
+  // k position of this thread's chunk (VEC==8 path): (kr, ks, kc)
+  int kr = 0, ks = 0, kc = cc * 8;
+  if constexpr (!IS1x1 && VEC == 8) {
+    while (kc >= g.C) { kc -= g.C; if (++ks == g.S) { ks = 0; ++kr; } }
+  }
+
+  uint4 ra[4], rb[B_ROWS_PER_THREAD];
+  const int nk = (g.ldb + BK - 1) / BK;
+
+  auto load_tile = [&](int kt) {
+    const int k = kt * BK + cc * 8;
+    // ---- A ----
+    if constexpr (IS1x1) {
+      const bool kok = k < g.Ktot;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        ra[i] = (a_ok[i] && kok) ? *reinterpret_cast<const uint4*>(X + a_base[i] + k)
+                                 : make_uint4(0, 0, 0, 0);
+      }
+    } else if constexpr (VEC == 8) {
+      const bool kok = kr < g.R;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ih = a_ih[i] + kr * g.dh, iw = a_iw[i] + ks * g.dw;
+        bool ok = a_ok[i] && kok;
+        if constexpr (LDIL) {
+          ok = ok && ih >= 0 && iw >= 0 && (ih % g.lh) == 0 && (iw % g.lw) == 0;
+          ih /= g.lh; iw /= g.lw;
+          ok = ok && ih < g.H && iw < g.W;
+        } else {
+          ok = ok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        }
+        ra[i] = ok ? *reinterpret_cast<const uint4*>(X + a_base[i] + (ih * g.W + iw) * g.C + kc)
+                   : make_uint4(0, 0, 0, 0);
+      }
+    } else {  // VEC == 4: C == 4, each 8-element chunk spans two filter taps
+      const int pos0 = k >> 2;
+      uint2 lo[4], hi[4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int pos = pos0 + h;
+        const int r = pos / g.S, s = pos - (pos / g.S) * g.S;
+        const bool kok = r < g.R;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int ih = a_ih[i] + r * g.dh, iw = a_iw[i] + s * g.dw;
+          const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          const uint2 v = ok ? *reinterpret_cast<const uint2*>(X + a_base[i] + (ih * g.W + iw) * 4)
+                             : make_uint2(0, 0);
+          if (h == 0) lo[i] = v; else hi[i] = v;
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ra[i] = make_uint4(lo[i].x, lo[i].y, hi[i].x, hi[i].y);
+    }
+    // ---- B (weights, row-major [K][ldb]) ----
+    const bool kokb = k < g.ldb;
+#pragma unroll
+    for (int i = 0; i < B_ROWS_PER_THREAD; ++i) {
+      const int n = n0 + rbase + 32 * i;
+      rb[i] = (n < g.K && kokb) ? *reinterpret_cast<const uint4*>(Wm + (size_t)n * g.ldb + k)
+                                : make_uint4(0, 0, 0, 0);
+    }
+    // advance the incremental k decode for the next tile
+    if constexpr (!IS1x1 && VEC == 8) {
+      kc += BK;
+      while (kc >= g.C) { kc -= g.C; if (++ks == g.S) { ks = 0; ++kr; } }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16_t* a = As + buf * BM * BK;
+    bf16_t* b = Bs + buf * BN * BK;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rbase + 32 * i;
+      *reinterpret_cast<uint4*>(a + row * BK + ((cc ^ ig_swz(row)) << 3)) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_ROWS_PER_THREAD; ++i) {
+      const int row = rbase + 32 * i;
+      *reinterpret_cast<uint4*>(b + row * BK + ((cc ^ ig_swz(row)) << 3)) = rb[i];
+    }
+  };
+
+  f32x4 acc[NI][NJ];
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fq = lane >> 4;
+
+  auto compute = [&](int buf) {
+    const bf16_t* a = As + buf * BM * BK;
+    const bf16_t* b = Bs + buf * BN * BK;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int chunk = kk * 4 + fq;
+      bf16x8 af[NI], bfg[NJ];
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(a + row * BK + ((chunk ^ ig_swz(row)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = wn * WN + j * 16 + fr;
+        bfg[j] = *reinterpret_cast<const bf16x8*>(b + row * BK + ((chunk ^ ig_swz(row)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j] = mfma16(af[i], bfg[j], acc[i][j]);
+    }
+  };
+
+  // ---- main loop: one barrier per K tile, loads of tile k+1 overlap MFMA on tile k ----
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load_tile(kt + 1);
+    compute(cur);
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue: stage fp32 tile in LDS, then row-contiguous 16-byte stores ----
+  constexpr int EPI_LD = BN + 4;  // fp32 pitch: rows r and r+4 land 16 banks apart
+  float* Cs = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int i = 0; i < NI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + fq * 4 + r;
+        const int col = wn * WN + j * 16 + fr;
+        Cs[row * EPI_LD + col] = acc[i][j][r];
+      }
+  __syncthreads();
+
+  constexpr int CPR = BN / 8;            // 8-column chunks per row
+  constexpr int RSTEP = IG_NT / CPR;     // rows handled per pass
+  const int ch = tid % CPR;
+  const int rr0 = tid / CPR;
+  const int col0 = n0 + ch * 8;
+  const bool col_ok = col0 < g.K;        // K % 8 == 0 is required by the launcher
+  float bsv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bsv[e] = (bias && col_ok) ? bias[col0 + e] : 0.f;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+
+  for (int rr = rr0; rr < BM; rr += RSTEP) {
+    const int m = m0 + rr;
+    if (m >= g.M || !col_ok) continue;
+    float v[8];
+    const float4 lo = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8);
+    const float4 hi = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8 + 4);
+    v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+    v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+    const size_t off = (size_t)m * g.K + col0;
+    if (resid) {
+      float rv[8];
+      unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += rv[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e] + bsv[e], act);
+    if (Yf) {
+      *reinterpret_cast<float4*>(Yf + off) = make_float4(v[0], v[1], v[2], v[3]);
+      *reinterpret_cast<float4*>(Yf + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    }
+    if (Y) {
+      const uint4 pk = pack8(v);
+      *reinterpret_cast<uint4*>(Y + off) = pk;
+      if (stats) {  // statistics of the values actually stored (bf16-rounded)
+        float q[8];
+        unpack8(pk, q);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
+      }
+    }
+  }
+
+  if (stats) {
+    // threads sharing a column chunk: tid % CPR equal. Reduce within the wave
+    // (lanes differing in bits >= log2(CPR)), then across waves through LDS.
+    __syncthreads();
+    float* red = Cs;  // reuse: [4 waves][BN][2]
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) {
+        s1[e] += __shfl_xor(s1[e], o, 64);
+        s2[e] += __shfl_xor(s2[e], o, 64);
+      }
+    }
+    if (lane < CPR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        red[(wid * BN + ch * 8 + e) * 2 + 0] = s1[e];
+        red[(wid * BN + ch * 8 + e) * 2 + 1] = s2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int col = n0 + tid;
+      if (col < g.K) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
+        atomicAdd(stats + col, a);
+        atomicAdd(stats + g.K + col, b);
+      }
+    }
+  }
+}
+
+// Wt[c][r][s][k] = W[k][R-1-r][S-1-s][c]  (dgrad weights for the transposed conv)
+__global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt,
+                                    int K, int R, int S, int C) {
+  const int total = K * R * S * C;
+  for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
+    int t = idx;
+    const int k = t % K; t /= K;
+    const int s = t % S; t /= S;
+    const int r = t % R; t /= R;
+    const int c = t;
+    Wt[idx] = W[((k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+  }
+}
+
+size_t igemm_smem_bytes(int BN) {
+  const size_t main_bytes = (size_t)2 * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
+  const size_t epi_bytes = (size_t)IG_BM * (BN + 4) * sizeof(float);
+  return main_bytes > epi_bytes ? main_bytes : epi_bytes;
+}
+
+template <int VEC, bool IS1x1, bool LDIL, int BN>
+static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                            const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                            hipStream_t st) {
+  const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
+  const size_t smem = igemm_smem_bytes(BN);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
+                     Yf, bias, resid, stats, g, act);
+  return hipGetLastError();
+}
+
+template <int VEC, bool IS1x1, bool LDIL>
+static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                               const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                               hipStream_t st) {
+  // narrow output-channel counts waste half of a 128-wide tile: use BN=64 there
+  if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, st);
+  const long tiles128 = (long)((g.M + IG_BM - 1) / IG_BM) * ((g.K + 127) / 128);
+  if (tiles128 < 512)  // not enough workgroups to fill 256 CUs twice -> smaller tiles
+    return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, st);
+  return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, st);
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
+                                const void* resid, float* stats, const ConvGeom* g, int act,
+                                hipStream_t st) {
+  const bf16_t* x = (const bf16_t*)X;
+  const bf16_t* w = (const bf16_t*)W;
+  bf16_t* y = (bf16_t*)Y;
+  const bf16_t* rs = (const bf16_t*)resid;
+  const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
+                     g->lh == 1 && g->lw == 1 && g->H == g->P && g->W == g->Q;
+  const bool ldil = g->lh > 1 || g->lw > 1;
+  if (g->C == 4) return launch_ig_bn<4, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
+  if (is1x1) return launch_ig_bn<8, true, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
+  if (ldil) return launch_ig_bn<8, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, st);
+  return launch_ig_bn<8, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
+}
+
+extern "C" hipError_t zoo_flip_weights(const void* W, void* Wt, int K, int R, int S, int C,
+                                       hipStream_t st) {
+  const int total = K * R * S * C;
+  const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
+  hipLaunchKernelGGL(flip_weights_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)W, (bf16_t*)Wt, K,
+                     R, S, C);
+  return hipGetLastError();
+}

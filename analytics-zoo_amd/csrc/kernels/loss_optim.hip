@@ -1,0 +1,286 @@
+// Losses, fused optimizer updates and small utility kernels (gfx950).
+//
+//  * softmax + cross-entropy (fused fwd+bwd), with the padding/ignore label of
+//    ZooClassNLLCriterion (Zs/pipeline/api/keras/objectives/ZooClassNLLCriterion.scala:28-100)
+//  * SGD (momentum / dampening / nesterov / weight decay, BigDL SGD semantics)
+//    and Adam (Zs/pipeline/api/keras/optimizers/Adam.scala:59-106, bias corrected)
+//    / AdamWeightDecay (AdamWeightDecay.scala:75-124) over ONE flat fp32 master
+//    buffer: a single launch updates every parameter of the model and writes
+//    the bf16 compute copy in the same pass
+//  * global L2-norm partial sums and constant clipping (HK19)
+//  * layout/cast helpers (input NCHW fp32 -> NHWC bf16 with channel padding)
+#include "common.h"
+
+namespace zoo {
+
+// one wave per row; logits fp32 or bf16
+template <typename T>
+ZOO_DEV float ld(const T* p, size_t i);
+template <>
+ZOO_DEV float ld<float>(const float* p, size_t i) { return p[i]; }
+template <>
+ZOO_DEV float ld<bf16_t>(const bf16_t* p, size_t i) { return bf2f(p[i]); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__ logits,
+                                                           const int64_t* __restrict__ labels,
+                                                           float* __restrict__ loss_sum,
+                                                           float* __restrict__ count,
+                                                           T* __restrict__ dlogits, int B, int NC,
+                                                           float grad_scale, int ignore_index) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= B) return;
+  const T* x = logits + (size_t)row * NC;
+  float mx = -INFINITY;
+  for (int j = lane; j < NC; j += 64) mx = fmaxf(mx, ld(x, j));
+  mx = warp_max(mx);
+  float s = 0.f;
+  for (int j = lane; j < NC; j += 64) s += __expf(ld(x, j) - mx);
+  s = warp_sum(s);
+  const float lse = mx + __logf(s);
+  const int64_t lab = labels[row];
+  const bool valid = lab != ignore_index && lab >= 0 && lab < NC;
+  if (lane == 0 && valid) {
+    atomicAdd(loss_sum, lse - ld(x, lab));
+    atomicAdd(count, 1.f);
+  }
+  if (dlogits) {
+    const float inv_s = 1.f / s;
+    for (int j = lane; j < NC; j += 64) {
+      float p = __expf(ld(x, j) - mx) * inv_s;
+      if (j == lab) p -= 1.f;
+      const float gv = valid ? p * grad_scale : 0.f;
+      if constexpr (sizeof(T) == 4) dlogits[(size_t)row * NC + j] = gv;
+      else dlogits[(size_t)row * NC + j] = f2bf(gv);
+    }
+  }
+}
+
+// ---------------- optimizers over flat buffers ----------------
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                  float* __restrict__ mom, bf16_t* __restrict__ pbf, size_t n,
+                                                  float lr, float momentum, float dampening, float wd,
+                                                  int nesterov, float gscale, int first_step) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    if (momentum != 0.f) {
+      float b = first_step ? gi : momentum * mom[i] + (1.f - dampening) * gi;
+      mom[i] = b;
+      gi = nesterov ? gi + momentum * b : b;
+    }
+    pi -= lr * gi;
+    p[i] = pi;
+    if (pbf) pbf[i] = f2bf(pi);
+  }
+}
+
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                   float* __restrict__ m, float* __restrict__ v,
+                                                   bf16_t* __restrict__ pbf, size_t n, float lr, float b1,
+                                                   float b2, float eps, float wd, float bc1, float bc2,
+                                                   float gscale, int decoupled) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    float pi = p[i];
+    if (wd != 0.f && !decoupled) gi += wd * pi;
+    const float mi = b1 * m[i] + (1.f - b1) * gi;
+    const float vi = b2 * v[i] + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    // Zoo Adam (Adam.scala:93-99): step = lr*sqrt(bc2)/bc1, update = m/(sqrt(v)+eps)
+    float upd = mi / (sqrtf(vi) + eps) * (sqrtf(bc2) / bc1);
+    if (wd != 0.f && decoupled) upd += wd * pi;
+    pi -= lr * upd;
+    p[i] = pi;
+    if (pbf) pbf[i] = f2bf(pi);
+  }
+}
+
+// generic "RMSprop / Adagrad / Adadelta / Adamax" family in one kernel
+// kind: 0 rmsprop, 1 adagrad, 2 adadelta, 3 adamax
+__global__ __launch_bounds__(256) void adaptive_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                       float* __restrict__ s1, float* __restrict__ s2,
+                                                       bf16_t* __restrict__ pbf, size_t n, int kind, float lr,
+                                                       float rho, float rho2, float eps, float wd, float bc1,
+                                                       float gscale) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float gi = g[i] * gscale;
+    float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    float upd;
+    if (kind == 0) {  // rmsprop
+      const float a = rho * s1[i] + (1.f - rho) * gi * gi;
+      s1[i] = a;
+      upd = lr * gi / (sqrtf(a) + eps);
+    } else if (kind == 1) {  // adagrad
+      const float a = s1[i] + gi * gi;
+      s1[i] = a;
+      upd = lr * gi / (sqrtf(a) + eps);
+    } else if (kind == 2) {  // adadelta
+      const float a = rho * s1[i] + (1.f - rho) * gi * gi;
+      const float d = sqrtf(s2[i] + eps) / sqrtf(a + eps) * gi;
+      s1[i] = a;
+      s2[i] = rho * s2[i] + (1.f - rho) * d * d;
+      upd = lr * d;
+    } else {  // adamax: s1 = m, s2 = u
+      const float mi = rho * s1[i] + (1.f - rho) * gi;  // rho = beta1 here
+      const float ui = fmaxf(rho2 * s2[i], fabsf(gi));
+      s1[i] = mi;
+      s2[i] = ui;
+      upd = lr / bc1 * mi / (ui + eps);
+    }
+    pi -= upd;
+    p[i] = pi;
+    if (pbf) pbf[i] = f2bf(pi);
+  }
+}
+
+// sum of squares (global L2 norm) -> atomicAdd into out[0]
+__global__ __launch_bounds__(256) void sumsq_kernel(const float* __restrict__ g, size_t n, float* __restrict__ out) {
+  float s = 0.f;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const float v = g[i];
+    s += v * v;
+  }
+  s = warp_sum(s);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(out, red[0] + red[1] + red[2] + red[3]);
+}
+
+__global__ __launch_bounds__(256) void clip_kernel(float* __restrict__ g, size_t n, float lo, float hi,
+                                                   const float* __restrict__ norm_sq, float max_norm) {
+  float sc = 1.f;
+  if (norm_sq) {
+    const float nrm = sqrtf(*norm_sq);
+    sc = nrm > max_norm ? max_norm / (nrm + 1e-6f) : 1.f;
+  }
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    float v = g[i] * sc;
+    g[i] = fminf(fmaxf(v, lo), hi);
+  }
+}
+
+// ---------------- layout / cast helpers ----------------
+// NCHW float -> NHWC bf16 with channels padded to Cp (zero fill)
+__global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restrict__ X, bf16_t* __restrict__ Y,
+                                                           int N, int C, int H, int W, int Cp) {
+  const size_t total = (size_t)N * H * W * Cp;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % Cp);
+    size_t t = i / Cp;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    const float v = c < C ? X[(((size_t)n * C + c) * H + h) * W + w] : 0.f;
+    Y[i] = f2bf(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void bf16_to_f32_accum_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
+                                                                 size_t n, int accumulate) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = accumulate ? y[i] + bf2f(x[i]) : bf2f(x[i]);
+}
+
+__global__ __launch_bounds__(256) void f32_to_bf16_kernel(const float* __restrict__ x, bf16_t* __restrict__ y, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = f2bf(x[i]);
+}
+
+// bf16 elementwise add (8 per lane), y = a + b
+__global__ __launch_bounds__(256) void add_bf16_kernel(const bf16_t* __restrict__ a, const bf16_t* __restrict__ b,
+                                                       bf16_t* __restrict__ y, size_t n8) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    float x[8], z[8];
+    unpack8(reinterpret_cast<const uint4*>(a)[i], x);
+    unpack8(reinterpret_cast<const uint4*>(b)[i], z);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) x[e] += z[e];
+    reinterpret_cast<uint4*>(y)[i] = pack8(x);
+  }
+}
+
+static int egrid(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 4096) b = 4096;
+  return (int)(b ? b : 1);
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" hipError_t zoo_softmax_xent(const void* logits, int is_f32, const int64_t* labels, float* loss_sum,
+                                       float* count, void* dlogits, int B, int NC, float grad_scale,
+                                       int ignore_index, hipStream_t st) {
+  const int blocks = (B + 3) / 4;
+  if (is_f32)
+    hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)logits, labels,
+                       loss_sum, count, (float*)dlogits, B, NC, grad_scale, ignore_index);
+  else
+    hipLaunchKernelGGL(softmax_xent_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)logits, labels,
+                       loss_sum, count, (bf16_t*)dlogits, B, NC, grad_scale, ignore_index);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_sgd(float* p, const float* g, float* mom, void* pbf, size_t n, float lr, float momentum,
+                              float dampening, float wd, int nesterov, float gscale, int first_step,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(sgd_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, mom, (bf16_t*)pbf, n, lr, momentum,
+                     dampening, wd, nesterov, gscale, first_step);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_adam(float* p, const float* g, float* m, float* v, void* pbf, size_t n, float lr, float b1,
+                               float b2, float eps, float wd, float bc1, float bc2, float gscale, int decoupled,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(adam_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd,
+                     bc1, bc2, gscale, decoupled);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_adaptive(float* p, const float* g, float* s1, float* s2, void* pbf, size_t n, int kind,
+                                   float lr, float rho, float rho2, float eps, float wd, float bc1, float gscale,
+                                   hipStream_t st) {
+  hipLaunchKernelGGL(adaptive_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, s1, s2, (bf16_t*)pbf, n, kind, lr, rho,
+                     rho2, eps, wd, bc1, gscale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_sumsq(const float* g, size_t n, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(egrid(n) > 1024 ? 1024 : egrid(n)), dim3(256), 0, st, g, n, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_clip(float* g, size_t n, float lo, float hi, const float* norm_sq, float max_norm,
+                               hipStream_t st) {
+  hipLaunchKernelGGL(clip_kernel, dim3(egrid(n)), dim3(256), 0, st, g, n, lo, hi, norm_sq, max_norm);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_nchw_to_nhwc(const float* X, void* Y, int N, int C, int H, int W, int Cp, hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(egrid((size_t)N * H * W * Cp)), dim3(256), 0, st, X, (bf16_t*)Y, N, C,
+                     H, W, Cp);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_bf16_to_f32(const void* x, float* y, size_t n, int accumulate, hipStream_t st) {
+  hipLaunchKernelGGL(bf16_to_f32_accum_kernel, dim3(egrid(n)), dim3(256), 0, st, (const bf16_t*)x, y, n, accumulate);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_f32_to_bf16(const float* x, void* y, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(f32_to_bf16_kernel, dim3(egrid(n)), dim3(256), 0, st, x, (bf16_t*)y, n);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_add_bf16(const void* a, const void* b, void* y, size_t n, hipStream_t st) {
+  hipLaunchKernelGGL(add_bf16_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, (const bf16_t*)a, (const bf16_t*)b,
+                     (bf16_t*)y, n / 8);
+  return hipGetLastError();
+}

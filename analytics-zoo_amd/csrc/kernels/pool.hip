@@ -1,0 +1,167 @@
+// Pooling for NHWC bf16 activations (gfx950).
+//
+// Reference: BigDL SpatialMaxPooling / SpatialAveragePooling behind
+// Zs/pipeline/api/keras/layers/{MaxPooling2D,AveragePooling2D,GlobalAveragePooling2D}.scala
+// (SURVEY.md §2.16 HK6). Max pooling records the winning tap (0..R*S-1) as one
+// byte per output so the backward pass is a race-free gather (no atomics).
+#include "common.h"
+
+namespace zoo {
+
+__global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                          uint8_t* __restrict__ arg, int N, int H, int W, int C,
+                                                          int P, int Q, int R, int S, int sh, int sw, int ph,
+                                                          int pw) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * P * Q * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    for (int r = 0; r < R; ++r) {
+      const int ih = p * sh - ph + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < S; ++s) {
+        const int iw = q * sw - pw + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(X + (((size_t)n * H + ih) * W + iw) * C + chunk * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * S + s); }
+      }
+    }
+    *reinterpret_cast<uint4*>(Y + i * 8) = pack8(best);
+    if (arg) {
+      uint2 pk;
+      pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *reinterpret_cast<uint2*>(arg + i * 8) = pk;
+    }
+  }
+}
+
+// gather form: every input pixel sums the gradients of the windows whose argmax it is
+__global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restrict__ dY,
+                                                          const uint8_t* __restrict__ arg, bf16_t* __restrict__ dX,
+                                                          int N, int H, int W, int C, int P, int Q, int R, int S,
+                                                          int sh, int sw, int ph, int pw) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * H * W * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    // output rows p with p*sh - ph <= h <= p*sh - ph + R - 1
+    const int p_lo = max(0, (h + ph - R + sh) / sh);
+    const int p_hi = min(P - 1, (h + ph) / sh);
+    const int q_lo = max(0, (w + pw - S + sw) / sw);
+    const int q_hi = min(Q - 1, (w + pw) / sw);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * sh - ph);
+      if (r < 0 || r >= R) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * sw - pw);
+        if (s < 0 || s >= S) continue;
+        const uint8_t tap = (uint8_t)(r * S + s);
+        const size_t o = (((size_t)n * P + p) * Q + q) * C + chunk * 8;
+        const uint2 ab = *reinterpret_cast<const uint2*>(arg + o);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dY + o), g);
+        const uint8_t a8[8] = {(uint8_t)(ab.x), (uint8_t)(ab.x >> 8), (uint8_t)(ab.x >> 16), (uint8_t)(ab.x >> 24),
+                               (uint8_t)(ab.y), (uint8_t)(ab.y >> 8), (uint8_t)(ab.y >> 16), (uint8_t)(ab.y >> 24)};
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (a8[e] == tap) acc[e] += g[e];
+      }
+    }
+    *reinterpret_cast<uint4*>(dX + i * 8) = pack8(acc);
+  }
+}
+
+// global average pool [N][HW][C] -> [N][C] (fp32 accumulate, bf16 or fp32 out)
+__global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                      int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const int total = N * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int chunk = i % cpr, n = i / cpr;
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    const bf16_t* base = X + (size_t)n * HW * C + chunk * 8;
+    for (int s = 0; s < HW; ++s) {
+      float v[8];
+      unpack8(*reinterpret_cast<const uint4*>(base + (size_t)s * C), v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+    const float inv = 1.f / (float)HW;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<uint4*>(Y + (size_t)n * C + chunk * 8) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16_t* __restrict__ dY, bf16_t* __restrict__ dX,
+                                                      int N, int HW, int C) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * HW * cpr;
+  const float inv = 1.f / (float)HW;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % cpr);
+    const int n = (int)(i / ((size_t)cpr * HW));
+    float g[8];
+    unpack8(*reinterpret_cast<const uint4*>(dY + (size_t)n * C + chunk * 8), g);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) g[e] *= inv;
+    *reinterpret_cast<uint4*>(dX + i * 8) = pack8(g);
+  }
+}
+
+static int pgrid(size_t work) {
+  size_t b = (work + 255) / 256;
+  if (b > 4096) b = 4096;
+  return (int)(b ? b : 1);
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" hipError_t zoo_maxpool_fwd(const void* X, void* Y, void* arg, int N, int H, int W, int C, int P, int Q,
+                                      int R, int S, int sh, int sw, int ph, int pw, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(pgrid((size_t)N * P * Q * (C / 8))), dim3(256), 0, st,
+                     (const bf16_t*)X, (bf16_t*)Y, (uint8_t*)arg, N, H, W, C, P, Q, R, S, sh, sw, ph, pw);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_maxpool_bwd(const void* dY, const void* arg, void* dX, int N, int H, int W, int C, int P,
+                                      int Q, int R, int S, int sh, int sw, int ph, int pw, hipStream_t st) {
+  hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(pgrid((size_t)N * H * W * (C / 8))), dim3(256), 0, st,
+                     (const bf16_t*)dY, (const uint8_t*)arg, (bf16_t*)dX, N, H, W, C, P, Q, R, S, sh, sw, ph, pw);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_gap_fwd(const void* X, void* Y, int N, int HW, int C, hipStream_t st) {
+  hipLaunchKernelGGL(gap_fwd_kernel, dim3(pgrid((size_t)N * (C / 8))), dim3(256), 0, st, (const bf16_t*)X,
+                     (bf16_t*)Y, N, HW, C);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_gap_bwd(const void* dY, void* dX, int N, int HW, int C, hipStream_t st) {
+  hipLaunchKernelGGL(gap_bwd_kernel, dim3(pgrid((size_t)N * HW * (C / 8))), dim3(256), 0, st, (const bf16_t*)dY,
+                     (bf16_t*)dX, N, HW, C);
+  return hipGetLastError();
+}

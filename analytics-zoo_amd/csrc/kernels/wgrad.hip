@@ -1,0 +1,235 @@
+// Convolution / Linear weight gradient on CDNA4 matrix cores (gfx950).
+//
+//   dW[k][(r,s,c)] += sum_m dY[m][k] * im2col(X)[m][(r,s,c)]
+//
+// The reduction runs over output pixels m, and BOTH operands are stored
+// m-major (NHWC), i.e. not K-contiguous per lane as the MFMA operand maps
+// want. Instead of an explicit transpose pass, the tiles are staged [m][col]
+// in LDS and read with gfx950's hardware transposing read ds_read_b64_tr_b16
+// (cdna_hip_programming.md T10): two 4x16 transposed reads give a lane the 8
+// consecutive-k values of its v_mfma_f32_16x16x32_bf16 operand fragment.
+//
+// The pixel dimension (up to N*P*Q = 802816 for ResNet-50 stage 1 at batch 256)
+// is split over workgroups; each adds its fp32 partial tile into dW with
+// global float atomics (shaped 64 B per 16-lane row segment).
+//
+// Reference parity: the weight-gradient half of BigDL SpatialConvolution /
+// Linear accGradParameters.
+#include "common.h"
+
+namespace zoo {
+
+struct WgradGeom {
+  int N, H, W, C;      // input activation (NHWC)
+  int K;               // output channels
+  int R, S, P, Q;
+  int sh, sw, ph, pw, dh, dw;
+  int M;               // N*P*Q (reduction length)
+  int Ktot;            // R*S*C (GEMM columns)
+  int ldw;             // leading dim of dW (>= Ktot)
+  int m_per_split;     // multiple of 64
+};
+
+constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 64;
+
+// XOR swizzle on 16-column (32-byte) blocks; rows {0..3, 8..11} (one
+// half-wave of transposed reads) map to 8 distinct bank groups.
+ZOO_DEV int wg_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
+ZOO_DEV int wg_off(int row, int col) {  // element offset in a [64][128] bf16 tile
+  return row * 128 + ((((col >> 4) ^ wg_f(row)) & 7) << 4) + (col & 15);
+}
+
+template <int VEC>
+__global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ X,
+                                                        const bf16_t* __restrict__ dY,
+                                                        float* __restrict__ dW, WgradGeom g) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64 m][128 k-out]
+  bf16_t* Bs = As + 2 * WG_BK * WG_BM;           // [2][64 m][128 (r,s,c)]
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  const int tiles_m = (g.K + WG_BM - 1) / WG_BM;
+  const int tiles_n = (g.Ktot + WG_BN - 1) / WG_BN;
+  const int tiles = tiles_m * tiles_n;
+  const int split = blockIdx.x / tiles;
+  const int tile = blockIdx.x - split * tiles;
+  const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
+  const int k0 = tm * WG_BM, c0 = tn * WG_BN;
+  const int mstart = split * g.m_per_split;
+  const int mend = min(g.M, mstart + g.m_per_split);
+  if (mstart >= mend) return;
+  const int nk = (mend - mstart + WG_BK - 1) / WG_BK;
+
+  // staging: thread -> 8-column chunk `ch` (16 per 128-wide row), rows rb + 16*i
+  const int ch = tid & 15;
+  const int rb = tid >> 4;  // 0..15
+
+  // dY columns (output channels) for this thread's chunk
+  const int ycol = k0 + ch * 8;
+  const bool ycol_ok = ycol < g.K;
+  // im2col column decode for the X chunk (fixed for the whole block)
+  const int xcol = c0 + ch * 8;
+  int xr[2], xs[2], xc[2];
+  bool xok[2];
+  if constexpr (VEC == 8) {
+    const int rs = xcol / g.C;
+    xc[0] = xcol - rs * g.C;
+    xr[0] = rs / g.S;
+    xs[0] = rs - xr[0] * g.S;
+    xok[0] = xcol < g.Ktot;
+  } else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pos = (xcol >> 2) + h;
+      xr[h] = pos / g.S;
+      xs[h] = pos - xr[h] * g.S;
+      xc[h] = 0;
+      xok[h] = pos * 4 < g.Ktot;
+    }
+  }
+
+  uint4 ra[4], rbv[4];
+  const int PQ = g.P * g.Q;
+
+  auto load_tile = [&](int kt) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mstart + kt * WG_BK + rb + 16 * i;
+      const bool mok = m < mend;
+      ra[i] = (mok && ycol_ok) ? *reinterpret_cast<const uint4*>(dY + (size_t)m * g.K + ycol)
+                               : make_uint4(0, 0, 0, 0);
+      const int mm = mok ? m : 0;
+      const int n = mm / PQ;
+      const int pq = mm - n * PQ;
+      const int p = pq / g.Q;
+      const int q = pq - p * g.Q;
+      const bf16_t* xb = X + (size_t)n * g.H * g.W * g.C;
+      if constexpr (VEC == 8) {
+        const int ih = p * g.sh - g.ph + xr[0] * g.dh;
+        const int iw = q * g.sw - g.pw + xs[0] * g.dw;
+        const bool ok = mok && xok[0] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        rbv[i] = ok ? *reinterpret_cast<const uint4*>(xb + (ih * g.W + iw) * g.C + xc[0])
+                    : make_uint4(0, 0, 0, 0);
+      } else {
+        uint2 v[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int ih = p * g.sh - g.ph + xr[h] * g.dh;
+          const int iw = q * g.sw - g.pw + xs[h] * g.dw;
+          const bool ok = mok && xok[h] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          v[h] = ok ? *reinterpret_cast<const uint2*>(xb + (ih * g.W + iw) * 4) : make_uint2(0, 0);
+        }
+        rbv[i] = make_uint4(v[0].x, v[0].y, v[1].x, v[1].y);
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    bf16_t* a = As + buf * WG_BK * WG_BM;
+    bf16_t* b = Bs + buf * WG_BK * WG_BN;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = rb + 16 * i;
+      *reinterpret_cast<uint4*>(a + wg_off(row, ch * 8)) = ra[i];
+      *reinterpret_cast<uint4*>(b + wg_off(row, ch * 8)) = rbv[i];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // transposed-read addressing: group gq = lane>>4 holds k = 8*gq..8*gq+7 of a
+  // 32-deep k-step; lane i = 4q+p of the group addresses row q, columns 4p..4p+3
+  const int gq = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+
+  auto read_frag = [&](const bf16_t* base, int kk, int colbase) -> bf16x8 {
+    const int row0 = kk * 32 + gq * 8 + tq;
+    typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4*)(base + wg_off(row0, colbase + 4 * tp)));
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_i16x4*)(base + wg_off(row0 + 4, colbase + 4 * tp)));
+    typedef short i16x8 __attribute__((ext_vector_type(8)));
+    i16x8 v;
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    return __builtin_bit_cast(bf16x8, v);
+  };
+
+  auto compute = [&](int buf) {
+    const bf16_t* a = As + buf * WG_BK * WG_BM;
+    const bf16_t* b = Bs + buf * WG_BK * WG_BN;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfg[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(a, kk, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfg[j] = read_frag(b, kk, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfg[j], acc[i][j]);
+    }
+  };
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load_tile(kt + 1);
+    compute(cur);
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map of 16x16x32 -> row = 4*(lane>>4)+reg (k-out), col = lane&15
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = c0 + wn * 64 + j * 16 + fr;
+      if (col >= g.Ktot) continue;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = k0 + wm * 64 + i * 16 + fq * 4 + r;
+        if (row < g.K) atomicAdd(dW + (size_t)row * g.ldw + col, acc[i][j][r]);
+      }
+    }
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const WgradGeom* gin,
+                                hipStream_t st) {
+  WgradGeom g = *gin;
+  const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
+  // split the pixel reduction so that ~1024 workgroups are in flight, >= 512 pixels each
+  int splits = (1024 + tiles - 1) / tiles;
+  const int max_splits = (g.M + 511) / 512;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int mps = (g.M + splits - 1) / splits;
+  mps = (mps + WG_BK - 1) / WG_BK * WG_BK;
+  splits = (g.M + mps - 1) / mps;
+  g.m_per_split = mps;
+  const size_t smem = (size_t)2 * WG_BK * (WG_BM + WG_BN) * sizeof(bf16_t);
+  if (g.C == 4) {
+    hipLaunchKernelGGL(wgrad_kernel<4>, dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+                       (const bf16_t*)dY, dW, g);
+  } else {
+    hipLaunchKernelGGL(wgrad_kernel<8>, dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+                       (const bf16_t*)dY, dW, g);
+  }
+  return hipGetLastError();
+}

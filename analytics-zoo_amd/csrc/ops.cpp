@@ -1,0 +1,450 @@
+// Python bindings for the zoo gfx950 kernel library (`zoo._C`).
+//
+// Every entry validates dtype / device / contiguity / shape on the host BEFORE
+// launching, because the kernels index raw pointers with the geometry they are
+// given (an out-of-bounds access on the GPU can take the whole node down).
+// Kernels run on PyTorch's current HIP stream, so they order correctly with
+// any other torch work and are capturable into hipGraphs.
+#include <torch/extension.h>
+#include <ATen/hip/HIPContext.h>
+#include <hip/hip_runtime.h>
+
+namespace zoo {
+struct ConvGeom {
+  int N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, lh, lw, M, Ktot, ldb;
+};
+struct WgradGeom {
+  int N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, M, Ktot, ldw, m_per_split;
+};
+}  // namespace zoo
+
+using zoo::ConvGeom;
+using zoo::WgradGeom;
+
+extern "C" {
+hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
+                     hipStream_t);
+hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t zoo_wgrad(const void*, const void*, float*, const WgradGeom*, hipStream_t);
+hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int,
+                         hipStream_t);
+hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
+                            float*, float*, int, int, float, float, int, int, hipStream_t);
+hipError_t zoo_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*,
+                            const float*, void*, void*, float*, float*, int, int, hipStream_t);
+hipError_t zoo_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                           hipStream_t);
+hipError_t zoo_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                           hipStream_t);
+hipError_t zoo_gap_fwd(const void*, void*, int, int, int, hipStream_t);
+hipError_t zoo_gap_bwd(const void*, void*, int, int, int, hipStream_t);
+hipError_t zoo_softmax_xent(const void*, int, const int64_t*, float*, float*, void*, int, int, float, int,
+                            hipStream_t);
+hipError_t zoo_sgd(float*, const float*, float*, void*, size_t, float, float, float, float, int, float, int,
+                   hipStream_t);
+hipError_t zoo_adam(float*, const float*, float*, float*, void*, size_t, float, float, float, float, float, float,
+                    float, float, int, hipStream_t);
+hipError_t zoo_adaptive(float*, const float*, float*, float*, void*, size_t, int, float, float, float, float, float,
+                        float, float, hipStream_t);
+hipError_t zoo_sumsq(const float*, size_t, float*, hipStream_t);
+hipError_t zoo_clip(float*, size_t, float, float, const float*, float, hipStream_t);
+hipError_t zoo_nchw_to_nhwc(const float*, void*, int, int, int, int, int, hipStream_t);
+hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
+hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
+hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
+}
+
+namespace {
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "zoo HIP kernel launch failed in ", what, ": ", hipGetErrorString(e));
+}
+
+void req(const torch::Tensor& t, at::ScalarType dt, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+template <typename T>
+T* opt_ptr(const c10::optional<torch::Tensor>& t) {
+  return t.has_value() && t->defined() ? reinterpret_cast<T*>(t->data_ptr()) : nullptr;
+}
+
+ConvGeom make_geom(const torch::Tensor& x, int K, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
+                   int lh, int lw, int ldb) {
+  ConvGeom g;
+  g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
+  g.K = K; g.R = R; g.S = S;
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dw; g.lh = lh; g.lw = lw;
+  const int Hd = (g.H - 1) * lh + 1, Wd = (g.W - 1) * lw + 1;  // extent of the (dilated) input
+  g.P = (Hd + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  g.Q = (Wd + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+  g.M = g.N * g.P * g.Q;
+  g.Ktot = R * S * g.C;
+  g.ldb = ldb;
+  return g;
+}
+
+// x: [N,H,W,C] bf16; w: [K, ldb] bf16 (logical [K][R][S][C] rows, zero padded to ldb)
+torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
+                       int lh, int lw, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
+                       c10::optional<torch::Tensor> stats, int act, bool out_f32, bool out_bf16, int out_h,
+                       int out_w) {
+  req(x, at::kBFloat16, "x");
+  req(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
+  const int C = x.size(3), K = w.size(0), ldb = w.size(1);
+  TORCH_CHECK(C == 4 || C % 8 == 0, "conv_fwd: input channels must be 4 or a multiple of 8, got ", C);
+  TORCH_CHECK(K % 8 == 0, "conv_fwd: output channels must be a multiple of 8, got ", K);
+  TORCH_CHECK(ldb % 8 == 0 && ldb >= R * S * C, "conv_fwd: bad weight leading dim ", ldb);
+  TORCH_CHECK(R >= 1 && S >= 1 && sh >= 1 && sw >= 1 && dh >= 1 && dw >= 1 && lh >= 1 && lw >= 1 && ph >= 0 && pw >= 0,
+              "conv_fwd: bad geometry");
+  ConvGeom g = make_geom(x, K, R, S, sh, sw, ph, pw, dh, dw, lh, lw, ldb);
+  // transposed convs (dgrad) may need one extra output row/col (asymmetric padding):
+  // the loader zero-fills taps that fall outside the input, so a larger P/Q is safe.
+  if (out_h > 0) { TORCH_CHECK(out_h >= g.P && out_h <= g.P + sh, "conv_fwd: out_h"); g.P = out_h; }
+  if (out_w > 0) { TORCH_CHECK(out_w >= g.Q && out_w <= g.Q + sw, "conv_fwd: out_w"); g.Q = out_w; }
+  g.M = g.N * g.P * g.Q;
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "conv_fwd: empty output");
+  TORCH_CHECK((int64_t)g.N * g.H * g.W * g.C < (1LL << 31) && (int64_t)g.M * K < (1LL << 31),
+              "conv_fwd: tensor too large for 32-bit indexing");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == K, "bias size mismatch");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (resid.has_value() && resid->defined()) {
+    req(*resid, at::kBFloat16, "resid");
+    TORCH_CHECK(resid->numel() == (int64_t)g.M * K, "resid size mismatch");
+    rp = resid->data_ptr();
+  }
+  float* sp = nullptr;
+  if (stats.has_value() && stats->defined()) {
+    req(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->numel() == 2 * K, "stats must hold 2*K floats");
+    TORCH_CHECK(out_bf16, "stats require the bf16 output");
+    sp = stats->data_ptr<float>();
+  }
+  torch::Tensor y, yf;
+  if (out_bf16) y = torch::empty({g.N, g.P, g.Q, K}, x.options());
+  if (out_f32) yf = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(at::kFloat));
+  check_hip(zoo_igemm(x.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
+                      out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, cur_stream()),
+            "igemm");
+  return out_bf16 ? y : yf;
+}
+
+torch::Tensor flip_weights(torch::Tensor w, int K, int R, int S, int C) {
+  req(w, at::kBFloat16, "w");
+  TORCH_CHECK(w.numel() == (int64_t)K * R * S * C, "flip_weights: size mismatch");
+  auto wt = torch::empty({C, R * S * K}, w.options());
+  check_hip(zoo_flip_weights(w.data_ptr(), wt.data_ptr(), K, R, S, C, cur_stream()), "flip_weights");
+  return wt;
+}
+
+// dW (fp32, [K, ldw]) += wgrad(x, dy)
+void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int S, int sh, int sw, int ph, int pw,
+                int dh, int dil_w) {
+  req(x, at::kBFloat16, "x");
+  req(dy, at::kBFloat16, "dy");
+  req(dw, at::kFloat, "dw");
+  TORCH_CHECK(x.dim() == 4 && dy.dim() == 4, "conv_wgrad: NHWC inputs expected");
+  WgradGeom g;
+  g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
+  g.K = dy.size(3); g.R = R; g.S = S; g.P = dy.size(1); g.Q = dy.size(2);
+  g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dil_w;
+  TORCH_CHECK(dy.size(0) == g.N, "conv_wgrad: batch mismatch");
+  TORCH_CHECK(g.C == 4 || g.C % 8 == 0, "conv_wgrad: C must be 4 or a multiple of 8");
+  TORCH_CHECK(g.K % 8 == 0, "conv_wgrad: K must be a multiple of 8");
+  const int P = (g.H + 2 * ph - dh * (R - 1) - 1) / sh + 1, Q = (g.W + 2 * pw - dil_w * (S - 1) - 1) / sw + 1;
+  TORCH_CHECK(P == g.P && Q == g.Q, "conv_wgrad: dy spatial shape does not match the geometry");
+  g.M = g.N * g.P * g.Q;
+  g.Ktot = R * S * g.C;
+  g.ldw = dw.size(-1);
+  TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
+  g.m_per_split = 0;
+  check_hip(zoo_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), &g, cur_stream()), "wgrad");
+}
+
+void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<torch::Tensor> x,
+               c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> invstd, torch::Tensor out, int mode) {
+  req(a, at::kBFloat16, "a");
+  req(out, at::kFloat, "out");
+  const int C = a.size(-1);
+  const int64_t M = a.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_reduce: C must be a multiple of 8");
+  TORCH_CHECK(out.numel() == 2 * C, "bn_reduce: out must be [2*C]");
+  if (mode == 1) {
+    TORCH_CHECK(x.has_value() && mean.has_value() && invstd.has_value(), "bn_reduce mode 1 needs x/mean/invstd");
+    req(*x, at::kBFloat16, "x");
+    TORCH_CHECK(x->numel() == a.numel(), "bn_reduce: x shape");
+    if (z.has_value() && z->defined()) {
+      req(*z, at::kBFloat16, "z");
+      TORCH_CHECK(z->numel() == a.numel(), "bn_reduce: z shape");
+    }
+  }
+  check_hip(zoo_bn_reduce(a.data_ptr(), opt_ptr<void>(z), opt_ptr<void>(x), opt_ptr<float>(mean),
+                          opt_ptr<float>(invstd), out.data_ptr<float>(), (int)M, C, mode, cur_stream()),
+            "bn_reduce");
+}
+
+torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<torch::Tensor> gamma,
+                           c10::optional<torch::Tensor> beta, c10::optional<torch::Tensor> resid,
+                           c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
+                           torch::Tensor smean, torch::Tensor sinv, double eps, double momentum, bool relu,
+                           bool training) {
+  req(x, at::kBFloat16, "x");
+  const int C = x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn: C must be a multiple of 8");
+  req(smean, at::kFloat, "save_mean");
+  req(sinv, at::kFloat, "save_invstd");
+  TORCH_CHECK(smean.numel() == C && sinv.numel() == C, "bn: save buffers must be [C]");
+  if (training) {
+    req(stats, at::kFloat, "stats");
+    TORCH_CHECK(stats.numel() == 2 * C, "bn: stats must be [2*C]");
+  } else {
+    TORCH_CHECK(rmean.has_value() && rvar.has_value(), "bn eval needs running stats");
+  }
+  if (resid.has_value() && resid->defined()) {
+    req(*resid, at::kBFloat16, "resid");
+    TORCH_CHECK(resid->numel() == x.numel(), "bn: resid shape");
+  }
+  auto y = torch::empty_like(x);
+  check_hip(zoo_bn_fwd_apply(x.data_ptr(), training ? stats.data_ptr<float>() : nullptr, opt_ptr<float>(gamma),
+                             opt_ptr<float>(beta), opt_ptr<void>(resid), y.data_ptr(), opt_ptr<float>(rmean),
+                             opt_ptr<float>(rvar), smean.data_ptr<float>(), sinv.data_ptr<float>(), (int)M, C,
+                             (float)eps, (float)momentum, relu, training, cur_stream()),
+            "bn_fwd_apply");
+  return y;
+}
+
+std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dz, c10::optional<torch::Tensor> z, torch::Tensor x,
+                                        torch::Tensor smean, torch::Tensor sinv, c10::optional<torch::Tensor> gamma,
+                                        torch::Tensor sums, bool want_dresid, c10::optional<torch::Tensor> dgamma,
+                                        c10::optional<torch::Tensor> dbeta) {
+  req(dz, at::kBFloat16, "dz");
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(dz.numel() == x.numel(), "bn_bwd: shape mismatch");
+  const int C = x.size(-1);
+  const int64_t M = x.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "bn_bwd: C must be a multiple of 8");
+  req(sums, at::kFloat, "sums");
+  TORCH_CHECK(sums.numel() == 2 * C, "bn_bwd: sums must be [2*C]");
+  if (z.has_value() && z->defined()) {
+    req(*z, at::kBFloat16, "z");
+    TORCH_CHECK(z->numel() == x.numel(), "bn_bwd: z shape");
+  }
+  auto dx = torch::empty_like(x);
+  torch::Tensor dr;
+  if (want_dresid) dr = torch::empty_like(x);
+  check_hip(zoo_bn_bwd_apply(dz.data_ptr(), opt_ptr<void>(z), x.data_ptr(), smean.data_ptr<float>(),
+                             sinv.data_ptr<float>(), opt_ptr<float>(gamma), sums.data_ptr<float>(), dx.data_ptr(),
+                             want_dresid ? dr.data_ptr() : nullptr, opt_ptr<float>(dgamma), opt_ptr<float>(dbeta),
+                             (int)M, C, cur_stream()),
+            "bn_bwd_apply");
+  if (want_dresid) return {dx, dr};
+  return {dx};
+}
+
+std::vector<torch::Tensor> maxpool_fwd(torch::Tensor x, int R, int S, int sh, int sw, int ph, int pw, bool save_arg) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool: NHWC with C%8==0");
+  TORCH_CHECK(R * S <= 256, "maxpool: window too large");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = (H + 2 * ph - R) / sh + 1, Q = (W + 2 * pw - S) / sw + 1;
+  auto y = torch::empty({N, P, Q, C}, x.options());
+  torch::Tensor arg;
+  if (save_arg) arg = torch::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  check_hip(zoo_maxpool_fwd(x.data_ptr(), y.data_ptr(), save_arg ? arg.data_ptr() : nullptr, N, H, W, C, P, Q, R, S,
+                            sh, sw, ph, pw, cur_stream()),
+            "maxpool_fwd");
+  if (save_arg) return {y, arg};
+  return {y};
+}
+
+torch::Tensor maxpool_bwd(torch::Tensor dy, torch::Tensor arg, int H, int W, int R, int S, int sh, int sw, int ph,
+                          int pw) {
+  req(dy, at::kBFloat16, "dy");
+  req(arg, at::kByte, "arg");
+  TORCH_CHECK(dy.sizes() == arg.sizes(), "maxpool_bwd: arg shape");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(P == (H + 2 * ph - R) / sh + 1 && Q == (W + 2 * pw - S) / sw + 1, "maxpool_bwd: geometry");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  check_hip(zoo_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, R, S, sh, sw, ph, pw,
+                            cur_stream()),
+            "maxpool_bwd");
+  return dx;
+}
+
+torch::Tensor gap_fwd(torch::Tensor x) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap: NHWC with C%8==0");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = torch::empty({N, C}, x.options());
+  check_hip(zoo_gap_fwd(x.data_ptr(), y.data_ptr(), N, HW, C, cur_stream()), "gap_fwd");
+  return y;
+}
+
+torch::Tensor gap_bwd(torch::Tensor dy, int H, int W) {
+  req(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(dy.dim() == 2 && dy.size(1) % 8 == 0, "gap_bwd: [N,C] with C%8==0");
+  const int N = dy.size(0), C = dy.size(1);
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  check_hip(zoo_gap_bwd(dy.data_ptr(), dx.data_ptr(), N, H * W, C, cur_stream()), "gap_bwd");
+  return dx;
+}
+
+// returns (loss_sum[1], count[1], dlogits or empty)
+std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labels, bool want_grad, double grad_scale,
+                                        int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "softmax_xent: 2-D GPU logits");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "logits dtype");
+  req(labels, at::kLong, "labels");
+  TORCH_CHECK(labels.numel() == logits.size(0), "labels size");
+  const int B = logits.size(0), NC = logits.size(1);
+  auto loss = torch::zeros({2}, logits.options().dtype(at::kFloat));
+  torch::Tensor dl;
+  if (want_grad) dl = torch::empty_like(logits);
+  const bool f32 = logits.scalar_type() == at::kFloat;
+  check_hip(zoo_softmax_xent(logits.data_ptr(), f32, labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
+                             loss.data_ptr<float>() + 1, want_grad ? dl.data_ptr() : nullptr, B, NC,
+                             (float)grad_scale, (int)ignore_index, cur_stream()),
+            "softmax_xent");
+  if (want_grad) return {loss, dl};
+  return {loss};
+}
+
+void check_flat(const torch::Tensor& t, const char* n, int64_t numel) {
+  req(t, at::kFloat, n);
+  TORCH_CHECK(t.numel() == numel, n, " numel mismatch");
+}
+
+void sgd(torch::Tensor p, torch::Tensor g, c10::optional<torch::Tensor> mom, c10::optional<torch::Tensor> pbf,
+         double lr, double momentum, double dampening, double wd, bool nesterov, double gscale, bool first_step) {
+  req(p, at::kFloat, "p");
+  check_flat(g, "g", p.numel());
+  if (momentum != 0.0) {
+    TORCH_CHECK(mom.has_value(), "sgd: momentum buffer required");
+    check_flat(*mom, "mom", p.numel());
+  }
+  if (pbf.has_value() && pbf->defined()) {
+    req(*pbf, at::kBFloat16, "pbf");
+    TORCH_CHECK(pbf->numel() == p.numel(), "pbf numel");
+  }
+  check_hip(zoo_sgd(p.data_ptr<float>(), g.data_ptr<float>(), opt_ptr<float>(mom), opt_ptr<void>(pbf), p.numel(),
+                    lr, momentum, dampening, wd, nesterov, gscale, first_step, cur_stream()),
+            "sgd");
+}
+
+void adam(torch::Tensor p, torch::Tensor g, torch::Tensor m, torch::Tensor v, c10::optional<torch::Tensor> pbf,
+          double lr, double b1, double b2, double eps, double wd, double bc1, double bc2, double gscale,
+          bool decoupled) {
+  req(p, at::kFloat, "p");
+  check_flat(g, "g", p.numel());
+  check_flat(m, "m", p.numel());
+  check_flat(v, "v", p.numel());
+  if (pbf.has_value() && pbf->defined()) {
+    req(*pbf, at::kBFloat16, "pbf");
+    TORCH_CHECK(pbf->numel() == p.numel(), "pbf numel");
+  }
+  check_hip(zoo_adam(p.data_ptr<float>(), g.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(),
+                     opt_ptr<void>(pbf), p.numel(), lr, b1, b2, eps, wd, bc1, bc2, gscale, decoupled, cur_stream()),
+            "adam");
+}
+
+void adaptive(torch::Tensor p, torch::Tensor g, torch::Tensor s1, c10::optional<torch::Tensor> s2,
+              c10::optional<torch::Tensor> pbf, int kind, double lr, double rho, double rho2, double eps, double wd,
+              double bc1, double gscale) {
+  req(p, at::kFloat, "p");
+  check_flat(g, "g", p.numel());
+  check_flat(s1, "s1", p.numel());
+  if (kind >= 2) {
+    TORCH_CHECK(s2.has_value(), "adaptive: second state required");
+    check_flat(*s2, "s2", p.numel());
+  }
+  if (pbf.has_value() && pbf->defined()) {
+    req(*pbf, at::kBFloat16, "pbf");
+    TORCH_CHECK(pbf->numel() == p.numel(), "pbf numel");
+  }
+  check_hip(zoo_adaptive(p.data_ptr<float>(), g.data_ptr<float>(), s1.data_ptr<float>(), opt_ptr<float>(s2),
+                         opt_ptr<void>(pbf), p.numel(), kind, lr, rho, rho2, eps, wd, bc1, gscale, cur_stream()),
+            "adaptive");
+}
+
+torch::Tensor sumsq(torch::Tensor g) {
+  req(g, at::kFloat, "g");
+  auto out = torch::zeros({1}, g.options());
+  check_hip(zoo_sumsq(g.data_ptr<float>(), g.numel(), out.data_ptr<float>(), cur_stream()), "sumsq");
+  return out;
+}
+
+void clip(torch::Tensor g, double lo, double hi, c10::optional<torch::Tensor> norm_sq, double max_norm) {
+  req(g, at::kFloat, "g");
+  check_hip(zoo_clip(g.data_ptr<float>(), g.numel(), lo, hi, opt_ptr<float>(norm_sq), max_norm, cur_stream()),
+            "clip");
+}
+
+torch::Tensor nchw_to_nhwc(torch::Tensor x, int cpad) {
+  req(x, at::kFloat, "x");
+  TORCH_CHECK(x.dim() == 4, "nchw_to_nhwc: 4-D input");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  TORCH_CHECK(cpad >= C, "nchw_to_nhwc: cpad < C");
+  auto y = torch::empty({N, H, W, cpad}, x.options().dtype(at::kBFloat16));
+  check_hip(zoo_nchw_to_nhwc(x.data_ptr<float>(), y.data_ptr(), N, C, H, W, cpad, cur_stream()), "nchw_to_nhwc");
+  return y;
+}
+
+void bf16_to_f32(torch::Tensor x, torch::Tensor y, bool accumulate) {
+  req(x, at::kBFloat16, "x");
+  req(y, at::kFloat, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "bf16_to_f32 numel");
+  check_hip(zoo_bf16_to_f32(x.data_ptr(), y.data_ptr<float>(), x.numel(), accumulate, cur_stream()), "bf16_to_f32");
+}
+
+void f32_to_bf16(torch::Tensor x, torch::Tensor y) {
+  req(x, at::kFloat, "x");
+  req(y, at::kBFloat16, "y");
+  TORCH_CHECK(x.numel() == y.numel(), "f32_to_bf16 numel");
+  check_hip(zoo_f32_to_bf16(x.data_ptr<float>(), y.data_ptr(), x.numel(), cur_stream()), "f32_to_bf16");
+}
+
+torch::Tensor add_bf16(torch::Tensor a, torch::Tensor b) {
+  req(a, at::kBFloat16, "a");
+  req(b, at::kBFloat16, "b");
+  TORCH_CHECK(a.numel() == b.numel() && a.numel() % 8 == 0, "add_bf16: equal sizes, multiple of 8");
+  auto y = torch::empty_like(a);
+  check_hip(zoo_add_bf16(a.data_ptr(), b.data_ptr(), y.data_ptr(), a.numel(), cur_stream()), "add_bf16");
+  return y;
+}
+
+}  // namespace
+
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "zoo native gfx950 (MI355X) kernel library";
+  m.def("conv_fwd", &conv_fwd);
+  m.def("flip_weights", &flip_weights);
+  m.def("conv_wgrad", &conv_wgrad);
+  m.def("bn_reduce", &bn_reduce);
+  m.def("bn_fwd_apply", &bn_fwd_apply);
+  m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("gap_fwd", &gap_fwd);
+  m.def("gap_bwd", &gap_bwd);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("sgd", &sgd);
+  m.def("adam", &adam);
+  m.def("adaptive", &adaptive);
+  m.def("sumsq", &sumsq);
+  m.def("clip", &clip);
+  m.def("nchw_to_nhwc", &nchw_to_nhwc);
+  m.def("bf16_to_f32", &bf16_to_f32);
+  m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("add_bf16", &add_bf16);
+}

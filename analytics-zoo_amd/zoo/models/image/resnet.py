@@ -1,0 +1,144 @@
+"""ResNet (v1.5, NHWC, bf16) built on the zoo gfx950 kernels.
+
+The reference trains ResNet-50 through BigDL's MKL-DNN graph
+(Zs/examples/resnet/TrainImageNet.scala, `nn.mkldnn.ResNet.graph`) and serves
+it through ImageClassifier configs (Zs/models/image/imageclassification/
+ImageClassificationConfig.scala:56-190). Here every conv is fused with its
+BatchNorm (+ residual + ReLU) into the conv_bn_act op (implicit-GEMM conv with
+BN statistics in the epilogue, then one apply pass), activations stay NHWC
+bf16 end-to-end, and weights are stored in the packed [K, ceil8(R*S*C)]
+layout the MFMA kernels read directly.
+"""
+import math
+
+import torch
+import torch.nn as nn
+
+from zoo import ops
+
+
+class ConvBN(nn.Module):
+    """conv(KxK) -> BatchNorm -> (+residual) -> (ReLU), NHWC."""
+
+    def __init__(self, cin, cout, k, stride=1, pad=0, relu=True, zero_gamma=False, eps=1e-5, momentum=0.1):
+        super().__init__()
+        self.cin, self.cout, self.k, self.stride, self.pad, self.relu = cin, cout, k, stride, pad, relu
+        self.eps, self.momentum = eps, momentum
+        w4 = torch.empty(cout, k, k, cin)
+        fan_out = cout * k * k
+        nn.init.normal_(w4, 0.0, math.sqrt(2.0 / fan_out))
+        self.weight = nn.Parameter(ops.pack_weight(w4))
+        self.gamma = nn.Parameter(torch.zeros(cout) if zero_gamma else torch.ones(cout))
+        self.beta = nn.Parameter(torch.zeros(cout))
+        self.register_buffer("running_mean", torch.zeros(cout))
+        self.register_buffer("running_var", torch.ones(cout))
+
+    def forward(self, x, resid=None):
+        return ops.conv_bn_act(x, self.weight, self.gamma, self.beta, self.running_mean, self.running_var,
+                               kernel=(self.k, self.k), stride=(self.stride, self.stride),
+                               pad=(self.pad, self.pad), eps=self.eps, momentum=self.momentum, relu=self.relu,
+                               resid=resid, training=self.training)
+
+
+class Bottleneck(nn.Module):
+    expansion = 4
+
+    def __init__(self, cin, width, stride=1):
+        super().__init__()
+        cout = width * self.expansion
+        self.conv1 = ConvBN(cin, width, 1)
+        self.conv2 = ConvBN(width, width, 3, stride=stride, pad=1)
+        self.conv3 = ConvBN(width, cout, 1, relu=True, zero_gamma=False)
+        self.down = ConvBN(cin, cout, 1, stride=stride, relu=False) if (stride != 1 or cin != cout) else None
+
+    def forward(self, x):
+        sc = self.down(x) if self.down is not None else x
+        h = self.conv1(x)
+        h = self.conv2(h)
+        return self.conv3(h, resid=sc)
+
+
+class BasicBlock(nn.Module):
+    expansion = 1
+
+    def __init__(self, cin, width, stride=1):
+        super().__init__()
+        self.conv1 = ConvBN(cin, width, 3, stride=stride, pad=1)
+        self.conv2 = ConvBN(width, width, 3, pad=1, relu=True)
+        self.down = ConvBN(cin, width, 1, stride=stride, relu=False) if (stride != 1 or cin != width) else None
+
+    def forward(self, x):
+        sc = self.down(x) if self.down is not None else x
+        return self.conv2(self.conv1(x), resid=sc)
+
+
+class Dense(nn.Module):
+    """Final classifier on the MFMA GEMM (fp32 logits)."""
+
+    def __init__(self, cin, cout):
+        super().__init__()
+        w = torch.empty(cout, cin)
+        nn.init.normal_(w, 0.0, 0.01)
+        self.weight = nn.Parameter(w)
+        self.bias = nn.Parameter(torch.zeros(cout))
+
+    def forward(self, x):
+        if x.is_cuda:
+            y = ops.conv2d_nhwc(x.reshape(x.shape[0], 1, 1, x.shape[1]), self.weight, self.bias, out_f32=True)
+            return y.reshape(x.shape[0], -1)
+        return torch.nn.functional.linear(x.float(), self.weight, self.bias)
+
+
+class ResNet(nn.Module):
+    def __init__(self, block, layers, num_classes=1000, width=64, in_channels=3):
+        super().__init__()
+        self.in_channels = in_channels
+        self.cin_pad = 4 if in_channels <= 4 else ops.ceil8(in_channels)
+        self.stem = ConvBN(self.cin_pad, width, 7, stride=2, pad=3)
+        cin = width
+        stages = []
+        for i, n in enumerate(layers):
+            w = width * (2 ** i)
+            blocks = []
+            for j in range(n):
+                blocks.append(block(cin, w, stride=(2 if (j == 0 and i > 0) else 1)))
+                cin = w * block.expansion
+            stages.append(nn.Sequential(*blocks))
+        self.stages = nn.Sequential(*stages)
+        self.fc = Dense(cin, num_classes)
+        self.num_classes = num_classes
+
+    def to_nhwc(self, x):
+        """NCHW fp32 images -> NHWC bf16 with channels zero-padded for 16-byte loads."""
+        if x.dim() == 4 and x.shape[1] == self.in_channels:
+            if x.is_cuda:
+                return ops.native().nchw_to_nhwc(x.float().contiguous(), self.cin_pad)
+            x = x.permute(0, 2, 3, 1)
+        pad = self.cin_pad - x.shape[-1]
+        if pad:
+            x = torch.nn.functional.pad(x, (0, pad))
+        return x.contiguous()
+
+    def forward(self, x):
+        x = self.to_nhwc(x)
+        x = self.stem(x)
+        x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+        x = self.stages(x)
+        x = ops.global_avg_pool_nhwc(x)
+        return self.fc(x)
+
+
+def resnet50(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 6, 3], num_classes=num_classes, **kw)
+
+
+def resnet18(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [2, 2, 2, 2], num_classes=num_classes, **kw)
+
+
+def resnet34(num_classes=1000, **kw):
+    return ResNet(BasicBlock, [3, 4, 6, 3], num_classes=num_classes, **kw)
+
+
+def resnet101(num_classes=1000, **kw):
+    return ResNet(Bottleneck, [3, 4, 23, 3], num_classes=num_classes, **kw)

@@ -1,0 +1,51 @@
+"""Loader for the in-tree HIP kernel library ``zoo._C``.
+
+GPU tensors ALWAYS go through the native gfx950 kernels: if the extension is
+missing on a machine with a GPU, the first op raises instead of silently
+falling back to an eager PyTorch path. CPU tensors use the PyTorch reference
+implementations in each op module (these double as the numerics oracles in
+tests/).
+"""
+import importlib
+import os
+
+_C = None
+_err = None
+
+
+def _load():
+    global _C, _err
+    if _C is not None or _err is not None:
+        return _C
+    try:
+        _C = importlib.import_module("zoo._C")
+    except ImportError as e:  # pragma: no cover - depends on build state
+        if os.environ.get("ZOO_AUTOBUILD", "1") == "1":
+            try:
+                from zoo.utils.build import build_native
+                build_native()
+                _C = importlib.import_module("zoo._C")
+                return _C
+            except Exception as e2:  # noqa: BLE001
+                _err = e2
+                return None
+        _err = e
+    return _C
+
+
+def native():
+    """Return the native module, raising loudly if it cannot be loaded."""
+    m = _load()
+    if m is None:
+        raise RuntimeError(
+            "zoo native HIP library (zoo._C) is not available: %r. Build it with "
+            "`python analytics-zoo_amd/tools/build_native.py`." % (_err,))
+    return m
+
+
+def available():
+    return _load() is not None
+
+
+def on_gpu(t):
+    return t is not None and t.is_cuda

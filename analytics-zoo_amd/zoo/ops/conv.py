@@ -1,0 +1,166 @@
+"""NHWC convolution / linear ops on the gfx950 implicit-GEMM kernels.
+
+Weights are kept in the native *packed* layout ``[K, ldb]`` where a row is the
+logical ``[R][S][C]`` filter flattened and zero padded to ``ldb = ceil8(R*S*C)``
+(16-byte aligned rows for the MFMA B-operand loads). The fp32 master weight and
+its bf16 compute copy both use this layout, so the fused optimizer can update
+master + copy in one pass over flat buffers.
+
+Backward:
+  * dX  = transposed conv of dY with flipped weights (``flip_weights`` + igemm
+    with input dilation = stride)
+  * dW += wgrad(X, dY) accumulated in fp32 straight into the parameter's
+    gradient (``param._zoo_grad`` when the engine owns a flat gradient buffer).
+
+Reference: BigDL SpatialConvolution / Linear behind
+Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110 and Dense.scala:97
+(SURVEY.md §2.16 HK1/HK3/HK5).
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+from zoo.ops._native import native
+
+ACT_CODES = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
+
+
+def ceil8(v):
+    return (v + 7) // 8 * 8
+
+
+def conv_out_size(h, r, stride, pad, dil=1):
+    return (h + 2 * pad - dil * (r - 1) - 1) // stride + 1
+
+
+def bf16_weight(w):
+    """bf16 compute copy of a packed weight (engine-maintained if present)."""
+    c = getattr(w, "_zoo_bf16", None)
+    if c is not None:
+        return c
+    return w.detach().to(torch.bfloat16)
+
+
+def accumulate_grad(param, g):
+    """Return the gradient autograd should accumulate, or None if the kernel
+    already accumulated into the engine-owned flat gradient buffer."""
+    return g
+
+
+def _ref_act(y, act):
+    if act in (None, "linear"):
+        return y
+    if act == "relu":
+        return torch.relu(y)
+    if act == "gelu":
+        return F.gelu(y)
+    if act == "sigmoid":
+        return torch.sigmoid(y)
+    if act == "tanh":
+        return torch.tanh(y)
+    raise ValueError(act)
+
+
+def unpack_weight(w2, K, R, S, C):
+    return w2[:, : R * S * C].reshape(K, R, S, C)
+
+
+def pack_weight(w4):
+    K, R, S, C = w4.shape
+    ldb = ceil8(R * S * C)
+    out = torch.zeros(K, ldb, dtype=w4.dtype, device=w4.device)
+    out[:, : R * S * C] = w4.reshape(K, R * S * C)
+    return out
+
+
+def conv2d_ref(x, w2, geom, bias=None):
+    """fp32 PyTorch reference: x NHWC, packed weight -> NHWC."""
+    R, S, C, stride, pad, dil = geom
+    K = w2.shape[0]
+    w4 = unpack_weight(w2.float(), K, R, S, C).permute(0, 3, 1, 2)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w4, bias=None if bias is None else bias.float(), stride=stride,
+                 padding=pad, dilation=dil)
+    return y.permute(0, 2, 3, 1)
+
+
+class _Conv2dFn(torch.autograd.Function):
+    """y = act(conv(x, w) + b) on NHWC bf16 with the native kernels."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, R, S, stride, pad, dil, act, out_f32):
+        C_ = native()
+        wb = bf16_weight(w)
+        y = C_.conv_fwd(x, wb, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], 1, 1,
+                        None if bias is None else bias.detach().float().contiguous(), None, None,
+                        ACT_CODES[act], out_f32, not out_f32, 0, 0)
+        ctx.save_for_backward(x, w, y if act not in (None, "linear") else None)
+        ctx.geom = (R, S, stride, pad, dil, act, x.shape, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = native()
+        x, w, y = ctx.saved_tensors
+        R, S, stride, pad, dil, act, xshape, has_bias = ctx.geom
+        dy = dy.contiguous()
+        if act == "relu":
+            dy = dy * (y > 0).to(dy.dtype)
+        elif act not in (None, "linear"):
+            yf = y.float()
+            if act == "sigmoid":
+                dy = dy * (yf * (1 - yf)).to(dy.dtype)
+            elif act == "tanh":
+                dy = dy * (1 - yf * yf).to(dy.dtype)
+            else:
+                raise NotImplementedError("backward through fused %s epilogue" % act)
+        dyb = dy.to(torch.bfloat16).contiguous()
+        K = w.shape[0]
+        Cin = xshape[3]
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            wt = C_.flip_weights(bf16_weight(w)[:, : R * S * Cin].contiguous(), K, R, S, Cin)
+            if wt.shape[1] % 8:
+                wt = F.pad(wt, (0, ceil8(wt.shape[1]) - wt.shape[1]))
+            dx = C_.conv_fwd(dyb, wt, R, S, 1, 1, dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1], dil[0],
+                             dil[1], stride[0], stride[1], None, None, None, 0, False, True, xshape[1], xshape[2])
+        if ctx.needs_input_grad[1]:
+            gbuf = getattr(w, "_zoo_grad", None)
+            target = gbuf if gbuf is not None else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+            C_.conv_wgrad(x, dyb, target, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
+            if gbuf is None:
+                dw = target.to(w.dtype)
+            else:
+                hook = getattr(w, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(w)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().reshape(-1, K).sum(0)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def conv2d_nhwc(x, w, bias=None, kernel=(1, 1), stride=(1, 1), pad=(0, 0), dil=(1, 1), act=None, out_f32=False):
+    """NHWC conv with a packed weight [K, ldb]. x: [N,H,W,C]."""
+    R, S = kernel
+    Cin = x.shape[3]
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        return _Conv2dFn.apply(x.contiguous(), w, bias, R, S, tuple(stride), tuple(pad), tuple(dil), act, out_f32)
+    y = conv2d_ref(x, w, (R, S, Cin, tuple(stride), tuple(pad), tuple(dil)), bias)
+    y = _ref_act(y, act)
+    return y if out_f32 or x.dtype == torch.float32 else y.to(x.dtype)
+
+
+def linear(x, w, bias=None, act=None):
+    """y = act(x @ w^T + b). Uses the MFMA GEMM when features are 8-aligned and
+    the input is on the GPU; otherwise the plain library GEMM (hipBLASLt)."""
+    K, Cin = w.shape
+    lead = x.shape[:-1]
+    if x.is_cuda and Cin % 8 == 0 and K % 8 == 0 and w.shape[1] == Cin:
+        x2 = x.reshape(-1, 1, 1, Cin)
+        out_f32 = x.dtype == torch.float32
+        y = conv2d_nhwc(x2, w, bias, act=act, out_f32=out_f32)
+        return y.reshape(*lead, K).to(x.dtype)
+    y = F.linear(x, w.to(x.dtype), None if bias is None else bias.to(x.dtype))
+    return _ref_act(y, act)

@@ -1,0 +1,36 @@
+"""Fused softmax + cross-entropy (ClassNLL over log-softmax) on gfx950.
+
+Forward and backward are computed by ONE kernel launch: the gradient w.r.t.
+the logits, ``(softmax - onehot) * scale``, is produced in the forward pass and
+returned from backward (scaled by the incoming grad), so the loss costs one
+read of the logits. Honours the padding label of ZooClassNLLCriterion
+(Zs/pipeline/api/keras/objectives/ZooClassNLLCriterion.scala:28-100).
+"""
+import torch
+import torch.nn.functional as F
+
+from zoo.ops._native import native
+
+
+class _SoftmaxXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        B = logits.shape[0]
+        outs = native().softmax_xent(logits, labels, True, 1.0, ignore_index)
+        acc, dl = outs[0], outs[1]
+        count = acc[1].clamp_min(1.0)
+        ctx.save_for_backward(dl, count)
+        return acc[0] / count
+
+    @staticmethod
+    def backward(ctx, g):
+        dl, count = ctx.saved_tensors
+        return dl * (g / count).to(dl.dtype), None, None
+
+
+def softmax_cross_entropy(logits, labels, ignore_index=-100):
+    """Mean cross-entropy of raw logits [B, C] against int64 labels [B]."""
+    labels = labels.long()
+    if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16):
+        return _SoftmaxXentFn.apply(logits.contiguous(), labels.contiguous(), int(ignore_index))
+    return F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)

@@ -1,0 +1,17 @@
+"""Programmatic access to the native build (used by __graft_entry__.build and autobuild)."""
+import importlib.util
+import os
+
+_TOOLS = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "tools",
+                      "build_native.py")
+
+
+def _mod():
+    spec = importlib.util.spec_from_file_location("zoo_build_native", _TOOLS)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def build_native(force=False, jobs=8, verbose=False):
+    return _mod().build_all(force=force, jobs=jobs, verbose=verbose)
