@@ -1,0 +1,213 @@
+"""Runtime bring-up: ``init_nncontext`` and the typed engine configuration.
+
+Reference: Py/common/nncontext.py:104-124 (init_nncontext -> SparkContext +
+BigDL Engine.init) and Zs/common/NNContext.scala:133-246. On MI355X the
+"context" is one process per GPU:
+
+  * device from ``LOCAL_RANK`` (``torch.cuda.set_device``)
+  * ``torch.distributed`` process group over RCCL ("nccl" backend on ROCm) when
+    ``WORLD_SIZE > 1`` (gloo on CPU-only hosts, used by the CPU test suite)
+  * the native kernel library is loaded eagerly so a missing build fails here
+  * a typed :class:`ZooConfig` assembled from defaults < env (``ZOO_*`` and the
+    honoured legacy ``bigdl.failure.*`` / ``OMP_NUM_THREADS`` names) < kwargs
+    
+
+``init_nncontext`` returns a :class:`ZooContext`; it never starts Spark. Spark
+integration (NNFrames) is optional and only used when pyspark is importable.
+"""
+import dataclasses
+import datetime
+import logging
+import os
+import socket
+
+import torch
+
+log = logging.getLogger("zoo")
+
+
+@dataclasses.dataclass
+class ZooConfig:
+    # engine
+    dtype: str = "bf16"
+    bucket_mb: float = 64.0
+    overlap_comm: bool = True
+    sharded_optimizer: bool = False
+    hip_graph: bool = False
+    # failure handling (bigdl.failure.retryTimes / retryTimeInterval, Topology.scala:1181-1182)
+    failure_retry_times: int = 5
+    failure_retry_interval_s: float = 120.0
+    fault_inject_step: int = -1          # ZOO_FAULT_INJECT_STEP: raise at this iteration (tests the retry path)
+    # data
+    num_workers: int = 4
+    pin_memory: bool = True
+    # logging / tracing
+    log_every: int = 50
+    roctx: bool = False
+    seed: int = 1
+    backend: str = ""                    # "", "nccl" (RCCL), "gloo"
+    timeout_s: float = 1800.0
+
+    _ENV = {
+        "dtype": "ZOO_DTYPE", "bucket_mb": "ZOO_BUCKET_MB", "overlap_comm": "ZOO_OVERLAP_COMM",
+        "sharded_optimizer": "ZOO_SHARDED_OPTIM", "hip_graph": "ZOO_HIP_GRAPH",
+        "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
+        "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
+        "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",
+        "backend": "ZOO_DIST_BACKEND", "timeout_s": "ZOO_DIST_TIMEOUT",
+    }
+    _LEGACY = {"failure_retry_times": "bigdl.failure.retryTimes",
+               "failure_retry_interval_s": "bigdl.failure.retryTimeInterval"}
+
+    @classmethod
+    def from_sources(cls, conf=None, **kw):
+        c = cls()
+        sources = {}
+        for f in dataclasses.fields(cls):
+            for key in (cls._LEGACY.get(f.name), cls._ENV.get(f.name)):
+                if key and key in os.environ:
+                    sources[f.name] = os.environ[key]
+        if isinstance(conf, dict):
+            for k, v in conf.items():
+                name = k
+                for f, legacy in cls._LEGACY.items():
+                    if k == legacy:
+                        name = f
+                sources[name] = v
+        sources.update(kw)
+        for k, v in sources.items():
+            if not hasattr(c, k):
+                continue
+            cur = getattr(c, k)
+            if isinstance(cur, bool):
+                v = v if isinstance(v, bool) else str(v).lower() in ("1", "true", "yes", "on")
+            elif isinstance(cur, int):
+                v = int(v)
+            elif isinstance(cur, float):
+                v = float(v)
+            setattr(c, k, v)
+        return c
+
+
+class ZooContext:
+    """Handle returned by :func:`init_nncontext` (replaces the SparkContext)."""
+
+    def __init__(self, config, device, rank, world_size, local_rank, group=None, app_name="zoo"):
+        self.config = config
+        self.device = device
+        self.rank = rank
+        self.world_size = world_size
+        self.local_rank = local_rank
+        self.group = group
+        self.app_name = app_name
+        self.start_time = datetime.datetime.now()
+
+    # spark-like helpers used by the reference APIs
+    @property
+    def defaultParallelism(self):  # noqa: N802 (reference name)
+        return self.world_size
+
+    @property
+    def node_number(self):
+        return int(os.environ.get("ZOO_NUM_NODES", os.environ.get("NNODES", "1")))
+
+    @property
+    def core_number(self):
+        return int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+
+    @property
+    def is_distributed(self):
+        return self.world_size > 1
+
+    def barrier(self):
+        if self.world_size > 1:
+            import torch.distributed as dist
+            dist.barrier(group=self.group)
+
+    def stop(self):
+        global _CTX
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            dist.destroy_process_group()
+        _CTX = None
+
+    def __repr__(self):
+        return "ZooContext(rank=%d/%d, device=%s, backend=%s)" % (self.rank, self.world_size, self.device,
+                                                                  self.config.backend or "none")
+
+
+_CTX = None
+
+
+def _env_int(*names, default=0):
+    for n in names:
+        if n in os.environ:
+            return int(os.environ[n])
+    return default
+
+
+def init_nncontext(conf=None, redirect_spark_log=True, app_name=None, **kw):
+    """Create (or return) the process-wide :class:`ZooContext`.
+
+    ``conf`` may be an app-name string (as in the reference) or a dict of
+    config keys; keyword arguments override everything.
+    """
+    global _CTX
+    if _CTX is not None:
+        return _CTX
+    if isinstance(conf, str):
+        app_name, conf = conf, None
+    cfg = ZooConfig.from_sources(conf, **kw)
+    rank = _env_int("RANK", default=0)
+    world = _env_int("WORLD_SIZE", default=1)
+    local_rank = _env_int("LOCAL_RANK", default=rank)
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        ndev = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank % max(ndev, 1))
+        device = torch.device("cuda", local_rank % max(ndev, 1))
+        from zoo.ops._native import native
+        native()  # fail early and loudly if the kernel library is missing
+    else:
+        device = torch.device("cpu")
+    group = None
+    if world > 1:
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            backend = cfg.backend or ("nccl" if use_gpu else "gloo")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29500")
+            dist.init_process_group(backend=backend, rank=rank, world_size=world,
+                                    timeout=datetime.timedelta(seconds=cfg.timeout_s),
+                                    device_id=device if use_gpu else None)
+            cfg.backend = backend
+        else:
+            cfg.backend = dist.get_backend()
+    torch.manual_seed(cfg.seed + rank)
+    if "OMP_NUM_THREADS" in os.environ:
+        try:
+            torch.set_num_threads(int(os.environ["OMP_NUM_THREADS"]))
+        except ValueError:
+            pass
+    logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING,
+                        format="%(asctime)s zoo[%(process)d] %(levelname)s %(message)s")
+    _CTX = ZooContext(cfg, device, rank, world, local_rank, group, app_name or "zoo")
+    log.info("init_nncontext: %r on %s", _CTX, socket.gethostname())
+    return _CTX
+
+
+def get_nncontext():
+    return _CTX if _CTX is not None else init_nncontext()
+
+
+def init_spark_on_local(cores=2, conf=None, python_location=None, spark_log_level="WARN",
+                        redirect_spark_log=True):
+    """Reference launcher (Py/common/nncontext.py:23). Local mode == one process."""
+    os.environ.setdefault("OMP_NUM_THREADS", str(cores))
+    return init_nncontext(conf)
+
+
+def init_spark_on_yarn(*args, **kwargs):
+    """YARN is not part of the MI355X deployment model; use torchrun / the zoo launcher."""
+    raise NotImplementedError("init_spark_on_yarn: launch one process per GPU with "
+                              "`python -m torch.distributed.run` and call init_nncontext() instead")

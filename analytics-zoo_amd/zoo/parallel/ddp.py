@@ -1,0 +1,228 @@
+"""Data-parallel gradient synchronisation over RCCL (xGMI) — one process per GPU.
+
+This replaces BigDL's Spark-BlockManager ``AllReduceParameter`` (SURVEY.md
+§2.4 "DistriOptimizer iteration", §2.17 CC1-CC4; Topology.scala:1128-1206):
+
+* ``mode="allreduce"`` (default): gradients live in ONE flat fp32 buffer
+  (:class:`FlatParams`) laid out in backward order. The buffer is cut into
+  contiguous buckets (``bucket_mb``, default 64 MB — few, large messages suit
+  xGMI's 7 point-to-point links and 288 GB HBM; ResNet-50's 102 MB of fp32
+  gradients is 2 buckets). A bucket is launched the moment the backward
+  kernels of all its parameters have been *enqueued*: the comm stream waits on
+  an event recorded on the compute stream, so the all-reduce of late layers
+  overlaps the backward of early layers.
+* ``mode="sharded"``: BigDL's exact algorithm, ZeRO-1 style: reduce-scatter
+  the flat gradient, each rank runs the fused optimizer on its 1/N shard
+  (optimizer state sharded N ways), then all-gather the updated bf16 compute
+  weights (CC2 + CC3 + CC1 in one step).
+
+Gradient averaging (1/N) is folded into the optimizer kernel's ``gscale``.
+On CPU (gloo) the same code runs synchronously — that is what the multi-process
+CPU tests exercise.
+"""
+import threading
+
+import torch
+import torch.distributed as dist
+
+from zoo.parallel.flat import FlatParams
+
+
+class _Bucket:
+    __slots__ = ("lo", "hi", "params", "pending", "work", "launched")
+
+    def __init__(self, lo, hi):
+        self.lo, self.hi = lo, hi
+        self.params = set()
+        self.pending = 0
+        self.work = None
+        self.launched = False
+
+
+class GradSync:
+    def __init__(self, flat: FlatParams, group=None, bucket_mb=64.0, mode="allreduce", overlap=True):
+        self.flat = flat
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if self.world > 1 else 0
+        self.mode = mode
+        self.overlap = overlap and flat.grad.is_cuda and self.world > 1 and mode == "allreduce"
+        self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (flat.grad.is_cuda and self.world > 1) \
+            else None
+        self._lock = threading.Lock()
+        # -- buckets over contiguous parameter ranges --------------------------
+        cap = max(int(bucket_mb * 1024 * 1024 / 4), 1)
+        self.buckets = []
+        cur = None
+        self.param_bucket = {}
+        for p, (lo, hi) in zip(flat.params, flat.ranges()):
+            if cur is None or (hi - cur.lo) > cap and cur.params:
+                cur = _Bucket(lo, hi)
+                self.buckets.append(cur)
+            cur.hi = hi
+            cur.params.add(id(p))
+            self.param_bucket[id(p)] = cur
+        if self.buckets:
+            self.buckets[-1].hi = flat.numel  # include alignment tail
+            self.buckets[0].lo = 0
+            for a, b in zip(self.buckets, self.buckets[1:]):
+                b.lo = a.hi
+        # -- shard bounds for the sharded mode (equal, 64-element aligned) -----
+        n = flat.numel
+        per = (n + self.world - 1) // self.world
+        per = (per + 63) // 64 * 64
+        self.shard_size = per
+        self.padded = per * self.world
+        self._seen = set()
+        self._install_hooks()
+        self.reset()
+
+    # ------------------------------------------------------------------
+    def _install_hooks(self):
+        for p in self.flat.params:
+            p._zoo_grad_ready = self._ready
+            if hasattr(p, "register_post_accumulate_grad_hook"):
+                p.register_post_accumulate_grad_hook(self._ready)
+
+    def reset(self):
+        self._seen = set()
+        for b in self.buckets:
+            b.pending = len(b.params)
+            b.work = None
+            b.launched = False
+
+    def _ready(self, p):
+        if not self.overlap:
+            return
+        with self._lock:
+            if id(p) in self._seen:
+                return
+            self._seen.add(id(p))
+            b = self.param_bucket.get(id(p))
+            if b is None:
+                return
+            b.pending -= 1
+            if b.pending == 0 and not b.launched:
+                self._launch(b)
+
+    def _launch(self, b):
+        b.launched = True
+        g = self.flat.grad[b.lo:b.hi]
+        if self.comm_stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(g.device))
+            with torch.cuda.stream(self.comm_stream):
+                self.comm_stream.wait_event(ev)
+                b.work = dist.all_reduce(g, group=self.group, async_op=True)
+        else:
+            b.work = dist.all_reduce(g, group=self.group, async_op=True)
+
+    # ------------------------------------------------------------------
+    def broadcast_parameters(self, src=0):
+        """CC5: model weights from rank 0 to every rank (RCCL broadcast)."""
+        if self.world > 1:
+            dist.broadcast(self.flat.master, src, group=self.group)
+            self.flat.refresh_bf16()
+
+    def finish(self):
+        """Called after backward: launch what is left, wait for every bucket."""
+        if self.world <= 1:
+            return
+        if self.mode == "sharded":
+            return
+        for b in self.buckets:
+            if not b.launched:
+                self._launch(b)
+        for b in self.buckets:
+            if b.work is not None:
+                b.work.wait()
+        if self.comm_stream is not None:
+            torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.comm_stream)
+
+    def step(self, optim, clip=None):
+        """finish comm, (clip), run the optimizer. Returns nothing."""
+        flat = self.flat
+        gscale = 1.0 / self.world
+        if self.mode == "sharded" and self.world > 1:
+            self._sharded_step(optim, gscale, clip)
+        else:
+            self.finish()
+            if clip is not None:
+                clip(flat.grad, gscale, self)
+            optim.step(flat.master, flat.grad, flat.bf16, gscale)
+        self.reset()
+
+    def _sharded_step(self, optim, gscale, clip):
+        flat = self.flat
+        per = self.shard_size
+        lo = self.rank * per
+        hi = min(lo + per, flat.numel)
+        gpad = flat.grad
+        if self.padded != flat.numel:
+            gpad = torch.zeros(self.padded, dtype=flat.grad.dtype, device=flat.grad.device)
+            gpad[: flat.numel].copy_(flat.grad)
+        shard = torch.empty(per, dtype=flat.grad.dtype, device=flat.grad.device)
+        if dist.get_backend(self.group) == "gloo":
+            dist.all_reduce(gpad, group=self.group)
+            shard.copy_(gpad[lo:lo + per])
+        else:
+            dist.reduce_scatter_tensor(shard, gpad, group=self.group)
+        if clip is not None:
+            clip(shard[: hi - lo], gscale, self)
+        if hi > lo:
+            optim.step(flat.master[lo:hi], shard[: hi - lo], None, gscale)
+        # all-gather the updated fp32 master shards, then refresh the bf16 copy
+        mpad = torch.zeros(self.padded, dtype=flat.master.dtype, device=flat.master.device)
+        mine = mpad[lo:lo + per].clone()
+        mine[: hi - lo].copy_(flat.master[lo:hi])
+        if dist.get_backend(self.group) == "gloo":
+            parts = [torch.empty_like(mine) for _ in range(self.world)]
+            dist.all_gather(parts, mine, group=self.group)
+            mpad = torch.cat(parts)
+        else:
+            dist.all_gather_into_tensor(mpad, mine, group=self.group)
+        flat.master.copy_(mpad[: flat.numel])
+        flat.refresh_bf16()
+
+    def all_reduce_scalars(self, values):
+        """CC4/CC6: batch small metric/loss reductions into ONE all-reduce."""
+        t = torch.as_tensor(values, dtype=torch.float64, device=self.flat.grad.device)
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+
+def global_norm_clip(max_norm):
+    """L2-norm gradient clipping across ranks (Estimator.scala:137-150, CC4)."""
+    from zoo.ops._native import native
+
+    def _clip(g, gscale, sync):
+        if g.is_cuda:
+            ss = native().sumsq(g)
+        else:
+            ss = (g.float() ** 2).sum().reshape(1)
+        if sync.world > 1 and sync.mode == "sharded":
+            dist.all_reduce(ss, group=sync.group)
+        # gradients are summed over ranks; the optimizer applies gscale later
+        scale_sq = gscale * gscale
+        ss = ss * scale_sq
+        if g.is_cuda:
+            native().clip(g, -3.4e38, 3.4e38, ss, float(max_norm))
+        else:
+            nrm = ss.sqrt().item()
+            if nrm > max_norm:
+                g.mul_(max_norm / (nrm + 1e-6))
+    return _clip
+
+
+def constant_clip(lo, hi):
+    from zoo.ops._native import native
+
+    def _clip(g, gscale, sync):
+        # bounds apply to the averaged gradient: scale them to the summed buffer
+        s = 1.0 / gscale
+        if g.is_cuda:
+            native().clip(g, lo * s, hi * s, None, 0.0)
+        else:
+            g.clamp_(lo * s, hi * s)
+    return _clip

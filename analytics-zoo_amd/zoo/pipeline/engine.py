@@ -1,0 +1,273 @@
+"""The training / evaluation engine (MI355X replacement of Zoo's
+InternalDistriOptimizer + BigDL DistriOptimizer, SURVEY.md §2.4 E1-E3, E5;
+call stack §3.2).
+
+One process per GPU. Per iteration:
+  1. ``flat.grad`` zeroed (one memset over the flat fp32 gradient buffer)
+  2. forward on the native kernels (bf16 activations, bf16 weight copies)
+  3. loss (+ fused loss gradient) and backward; conv/BN backward kernels
+     accumulate straight into the flat gradient buffer and each finished
+     parameter triggers its RCCL bucket on the comm stream (overlap)
+  4. optional clipping (constant / global L2 with one all-reduce), then ONE
+     fused optimizer launch over the flat master buffer, which also rewrites
+     the bf16 compute copy (or the ZeRO-1 sharded variant)
+No host synchronisation happens inside the iteration; loss values stay on the
+device until a trigger (logging / validation / checkpoint) needs them.
+
+Failure handling mirrors Topology.scala:1180-1262: any exception inside the
+loop (other than ValueError, the analogue of IllegalArgumentException) is
+retried up to ``failure_retry_times`` within ``failure_retry_interval_s`` by
+reloading the latest checkpoint, if one is configured. ``ZOO_FAULT_INJECT_STEP``
+injects a failure at a chosen iteration to exercise that path.
+"""
+import glob
+import logging
+import math
+import os
+import time
+
+import torch
+
+from zoo.common.triggers import EveryEpoch, MaxEpoch, Trigger
+from zoo.parallel.ddp import GradSync
+from zoo.parallel.flat import FlatParams
+
+log = logging.getLogger("zoo.engine")
+
+
+class InjectedFault(RuntimeError):
+    pass
+
+
+def _move(batch, device, non_blocking=True):
+    if isinstance(batch, torch.Tensor):
+        return batch.to(device, non_blocking=non_blocking)
+    if isinstance(batch, (list, tuple)):
+        return type(batch)(_move(b, device, non_blocking) for b in batch)
+    if isinstance(batch, dict):
+        return {k: _move(v, device, non_blocking) for k, v in batch.items()}
+    return batch
+
+
+class TrainingEngine:
+    def __init__(self, model, criterion, optim_method, device=None, ctx=None, clip=None, sharded=None,
+                 bucket_mb=None, model_forward=None):
+        from zoo.common.nncontext import get_nncontext
+        self.ctx = ctx or get_nncontext()
+        cfg = self.ctx.config
+        self.device = torch.device(device) if device is not None else self.ctx.device
+        self.model = model.to(self.device)
+        self.criterion = criterion
+        self.optim = optim_method
+        self.flat = FlatParams(list(self.model.parameters()), device=self.device,
+                               bf16_copy=self.device.type == "cuda")
+        self.sync = GradSync(self.flat, bucket_mb=bucket_mb or cfg.bucket_mb,
+                             mode="sharded" if (cfg.sharded_optimizer if sharded is None else sharded)
+                             else "allreduce", overlap=cfg.overlap_comm)
+        self.sync.broadcast_parameters(0)
+        self.clip = clip
+        self.forward_fn = model_forward or (lambda m, x: m(x))
+        self.state = {"epoch": 1, "neval": 1, "Loss": float("nan"), "score": None, "records": 0}
+        self._pending_loss = []
+        self.train_summary = None
+        self.val_summary = None
+        self.checkpoint_path = None
+        self.checkpoint_trigger = None
+        self.checkpoint_overwrite = True
+        self.fault_step = cfg.fault_inject_step
+        self._fault_fired = False
+
+    # ------------------------------------------------------------------
+    def train_step(self, inputs, target):
+        """One synchronous-DP iteration. Returns the (device) loss tensor."""
+        if self.fault_step >= 0 and self.state["neval"] == self.fault_step and not self._fault_fired:
+            self._fault_fired = True
+            raise InjectedFault("injected fault at iteration %d" % self.fault_step)
+        self.model.train()
+        self.flat.grad.zero_()
+        out = self.forward_fn(self.model, inputs)
+        loss = self.criterion(out, target)
+        loss.backward()
+        self.sync.step(self.optim, self.clip)
+        self.state["neval"] += 1
+        return loss.detach()
+
+    # ------------------------------------------------------------------
+    def fit(self, data, end_trigger=None, validation=None, val_methods=None, val_trigger=None,
+            batch_size=None, log_every=None, callbacks=()):
+        """Train over an iterable of (x, y) minibatches until ``end_trigger``.
+
+        ``data`` is anything with ``data(train=True)`` (a FeatureSet) or a
+        re-iterable of batches (one pass = one epoch).
+        """
+        end_trigger = end_trigger or MaxEpoch(1)
+        val_trigger = val_trigger or EveryEpoch()
+        log_every = log_every or self.ctx.config.log_every
+        cfg = self.ctx.config
+        retries = []
+        while True:
+            try:
+                self._fit_loop(data, end_trigger, validation, val_methods, val_trigger, log_every, callbacks)
+                break
+            except (ValueError, KeyboardInterrupt):
+                raise
+            except Exception as e:  # noqa: BLE001 - mirrors Topology.scala:1229 catch Throwable
+                now = time.time()
+                retries = [t for t in retries if now - t < cfg.failure_retry_interval_s] + [now]
+                ck = self.latest_checkpoint()
+                if ck is None or len(retries) > cfg.failure_retry_times:
+                    raise
+                log.warning("training failed (%s); retry %d/%d from checkpoint %s", e, len(retries),
+                            cfg.failure_retry_times, ck)
+                self.load_checkpoint(ck)
+        return self
+
+    def _iter_epoch(self, data):
+        if hasattr(data, "data"):
+            return data.data(train=True, epoch=self.state["epoch"])
+        return iter(data)
+
+    def _fit_loop(self, data, end_trigger, validation, val_methods, val_trigger, log_every, callbacks):
+        state = self.state
+        while not end_trigger(state):
+            t_epoch = time.time()
+            recs = 0
+            t_last = time.time()
+            n_since = 0
+            for batch in self._iter_epoch(data):
+                x, y = batch[0], batch[1]
+                x = _move(x, self.device)
+                y = _move(y, self.device)
+                loss = self.train_step(x, y)
+                bs = (x[0] if isinstance(x, (list, tuple)) else x).shape[0] * self.sync.world
+                recs += bs
+                n_since += bs
+                state["records"] += bs
+                self._pending_loss.append(loss)
+                if (state["neval"] - 1) % log_every == 0:
+                    lval = self.flush_loss()
+                    dt = time.time() - t_last
+                    thr = n_since / dt if dt > 0 else 0.0
+                    state["Throughput"] = thr
+                    log.info("Epoch %d iter %d loss %.5f throughput %.1f records/s lr %.6g", state["epoch"],
+                             state["neval"] - 1, lval, thr, self.optim.current_lr())
+                    if self.train_summary is not None:
+                        self.train_summary.add_scalar("Loss", lval, state["neval"] - 1)
+                        self.train_summary.add_scalar("Throughput", thr, state["neval"] - 1)
+                        self.train_summary.add_scalar("LearningRate", self.optim.current_lr(), state["neval"] - 1)
+                    t_last, n_since = time.time(), 0
+                for cb in callbacks:
+                    cb(self, state)
+                if end_trigger.iteration_based and end_trigger(state):
+                    break
+                if self.checkpoint_trigger is not None and self.checkpoint_trigger.iteration_based and \
+                        self.checkpoint_trigger(state):
+                    self.save_checkpoint()
+            self.flush_loss()
+            log.info("Epoch %d finished: %d records in %.2fs", state["epoch"], recs, time.time() - t_epoch)
+            state["epoch"] += 1
+            self.optim.update_epoch(state["epoch"])
+            state["epoch_end"] = True
+            if validation is not None and val_methods and val_trigger(state):
+                res = self.evaluate(validation, val_methods)
+                state["score"] = res[0][1] if res else None
+                self.optim.state["score"] = state["score"]
+                if self.val_summary is not None:
+                    for name, v in res:
+                        self.val_summary.add_scalar(name, v, state["neval"] - 1)
+            if self.checkpoint_trigger is not None and self.checkpoint_trigger(state):
+                self.save_checkpoint()
+            state["epoch_end"] = False
+
+    def flush_loss(self):
+        if not self._pending_loss:
+            return self.state["Loss"]
+        vals = torch.stack([l.float() for l in self._pending_loss])
+        v = self.sync.all_reduce_scalars([vals.mean().item()]) / self.sync.world
+        self._pending_loss = []
+        self.state["Loss"] = float(v[0])
+        self.optim.state["Loss"] = self.state["Loss"]
+        return self.state["Loss"]
+
+    # ------------------------------------------------------------------
+    @torch.no_grad()
+    def predict(self, data, batch_size=None):
+        self.model.eval()
+        outs = []
+        for batch in (data.data(train=False) if hasattr(data, "data") else data):
+            x = batch[0] if isinstance(batch, (list, tuple)) else batch
+            out = self.forward_fn(self.model, _move(x, self.device))
+            outs.append(out.float() if isinstance(out, torch.Tensor) else out)
+        return outs
+
+    @torch.no_grad()
+    def evaluate(self, data, val_methods):
+        """Distributed validation: per-rank partial results, ONE all-reduce of a
+        small vector (Topology.scala:1459-1519, CC6)."""
+        self.model.eval()
+        accs = [m.new_accumulator() for m in val_methods]
+        for batch in (data.data(train=False) if hasattr(data, "data") else data):
+            x, y = _move(batch[0], self.device), _move(batch[1], self.device)
+            out = self.forward_fn(self.model, x)
+            for m, a in zip(val_methods, accs):
+                m.update(a, out, y, self.criterion)
+        flat = []
+        for a in accs:
+            flat.extend(a)
+        red = self.sync.all_reduce_scalars(flat).tolist()
+        res = []
+        i = 0
+        for m, a in zip(val_methods, accs):
+            n = len(a)
+            res.append((m.name, m.result(red[i:i + n])))
+            i += n
+        self.model.train()
+        return res
+
+    # ------------------------------------------------------------------
+    # checkpoint / resume: model.<neval> + optimMethod-<name>.<neval>
+    def set_checkpoint(self, path, trigger=None, overwrite=True):
+        self.checkpoint_path = path
+        self.checkpoint_trigger = trigger or EveryEpoch()
+        self.checkpoint_overwrite = overwrite
+        os.makedirs(path, exist_ok=True)
+
+    def save_checkpoint(self):
+        if self.checkpoint_path is None or self.ctx.rank != 0:
+            if self.sync.world > 1:
+                self.ctx.barrier()
+            return
+        from zoo.utils.checkpoint import save_object
+        it = self.state["neval"] - 1
+        suffix = "" if self.checkpoint_overwrite else ".%d" % it
+        name = type(self.optim).__name__
+        save_object({"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+                     "engine_state": dict(self.state), "neval": it},
+                    os.path.join(self.checkpoint_path, "model" + suffix), True)
+        save_object(self.optim.state_dict(), os.path.join(self.checkpoint_path, "optimMethod-%s%s" % (name, suffix)),
+                    True)
+        if self.sync.world > 1:
+            self.ctx.barrier()
+
+    def latest_checkpoint(self):
+        if self.checkpoint_path is None:
+            return None
+        cands = glob.glob(os.path.join(self.checkpoint_path, "model*"))
+        if not cands:
+            return None
+        return max(cands, key=os.path.getmtime)
+
+    def load_checkpoint(self, model_file):
+        from zoo.utils.checkpoint import load_object
+        d = load_object(model_file)
+        self.model.load_state_dict(d["model"])
+        self.flat.refresh_bf16()
+        self.state.update(d.get("engine_state", {}))
+        suffix = os.path.basename(model_file)[len("model"):]
+        name = type(self.optim).__name__
+        opath = os.path.join(os.path.dirname(model_file), "optimMethod-%s%s" % (name, suffix))
+        if os.path.exists(opath):
+            self.optim.load_state_dict(load_object(opath))
+            self.optim.to(self.device)
+        self.sync.broadcast_parameters(0)
+        self.sync.reset()

@@ -1,0 +1,40 @@
+"""Checkpoint object IO.
+
+Objects (state dicts of tensors, numbers, strings, lists, dicts) are written
+with ``torch.save`` and read back with ``torch.load(weights_only=True)`` so
+loading a checkpoint never executes code from the file. Paths may be local or
+``file://`` URIs; writes are atomic (temp file + rename) so a crash never
+leaves a torn ``model.<n>`` that the failure-retry path would pick up.
+"""
+import os
+import tempfile
+
+import torch
+
+
+def _local(path):
+    if path.startswith("file://"):
+        return path[len("file://"):]
+    if "://" in path:
+        raise NotImplementedError("remote filesystem %s: mount it locally" % path.split("://")[0])
+    return path
+
+
+def save_object(obj, path, overwrite=True):
+    path = _local(path)
+    if os.path.exists(path) and not overwrite:
+        raise FileExistsError(path)
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(dir=d, prefix=".tmp_")
+    os.close(fd)
+    try:
+        torch.save(obj, tmp)
+        os.replace(tmp, path)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+
+
+def load_object(path):
+    return torch.load(_local(path), map_location="cpu", weights_only=True)

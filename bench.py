@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""Headline benchmark: ResNet-50 (224x224, bf16) synchronous data-parallel
+training throughput in images/sec for the whole node; ``--model ncf`` gives
+the NCF records/sec metric (BASELINE.json).
+
+  python bench.py --gpus N --steps K --warmup W [--batch 256] [--model resnet50|ncf]
+
+For N > 1 launch one rank per GPU:
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+      --master-port P bench.py --gpus N --steps K --warmup W
+
+Each step = synthetic batch -> NCHW->NHWC bf16 conversion -> forward ->
+softmax cross-entropy -> backward -> RCCL gradient all-reduce (bucketed,
+overlapped) -> fused SGD-momentum update of the fp32 master weights + bf16
+copy. Weak scaling: the per-GPU batch is fixed, global batch = batch * N.
+Timing: W untimed warmup steps, then barrier + device sync, K timed steps,
+barrier + device sync; the max elapsed time over ranks is reported.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "analytics-zoo_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BASELINE_METRIC = "images/sec (whole node) ResNet-50 bf16"
+BASELINE_VALUE = None  # BASELINE.json "published" is empty -> vs_baseline null
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "ncf"])
+    ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer (BigDL AllReduceParameter)")
+    ap.add_argument("--profile-steps", type=int, default=0)
+    return ap.parse_args()
+
+
+def build_resnet50(ctx, batch):
+    from zoo.models.image.resnet import resnet50
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+
+    torch.manual_seed(1234)
+    model = resnet50(num_classes=1000)
+    optim = SGD(learningrate=0.1, momentum=0.9, weightdecay=1e-4, dampening=0.0)
+    eng = TrainingEngine(model, softmax_cross_entropy, optim)
+    dev = ctx.device
+    g = torch.Generator(device=dev)
+    g.manual_seed(ctx.rank)
+    x = torch.randn(batch, 3, 224, 224, device=dev, generator=g)
+    y = torch.randint(0, 1000, (batch,), device=dev, generator=g)
+    return eng, (x, y), "ResNet-50", {"image_size": 224, "optimizer": "SGD(momentum=0.9, wd=1e-4)"}
+
+
+def build_ncf(ctx, batch):
+    from zoo.models.recommendation.neuralcf import NeuralCF
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.pipeline.engine import TrainingEngine
+
+    torch.manual_seed(1234)
+    users, items = 138493, 26744  # ml-20m shape
+    model = NeuralCF(users, items, 5, user_embed=20, item_embed=20, hidden_layers=(40, 20, 10), include_mf=True,
+                     mf_embed=20)
+    eng = TrainingEngine(model, softmax_cross_entropy, Adam(lr=1e-3))
+    dev = ctx.device
+    g = torch.Generator(device=dev)
+    g.manual_seed(ctx.rank)
+    u = torch.randint(1, users + 1, (batch,), device=dev, generator=g)
+    i = torch.randint(1, items + 1, (batch,), device=dev, generator=g)
+    x = torch.stack([u, i], 1)
+    y = torch.randint(0, 5, (batch,), device=dev, generator=g)
+    return eng, (x, y), "NCF", {"users": users, "items": items, "embed": 20, "hidden": [40, 20, 10]}
+
+
+def main():
+    a = parse()
+    from zoo.common.nncontext import init_nncontext
+    ctx = init_nncontext("bench", sharded_optimizer=a.sharded)
+    world = ctx.world_size
+    if a.model == "resnet50":
+        batch = a.batch
+        eng, (x, y), model_name, extra = build_resnet50(ctx, batch)
+        metric, unit = BASELINE_METRIC, "images/sec"
+    else:
+        batch = a.batch if a.batch != 256 else 65536
+        eng, (x, y), model_name, extra = build_ncf(ctx, batch)
+        metric, unit = "records/sec (whole node) NCF", "records/sec"
+
+    for _ in range(a.warmup):
+        eng.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = eng.train_step(x, y)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    t = torch.tensor([elapsed], dtype=torch.float64, device=ctx.device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    final_loss = float(loss.float().item())
+    total = batch * world * a.steps
+    value = total / elapsed
+    if ctx.rank == 0:
+        out = {
+            "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16", "data": "synthetic (random-init weights, random inputs/labels)",
+            "config": dict({"model": model_name, "global_batch": batch * world, "per_gpu_batch": batch,
+                            "seq_len": None, "parallelism": "dp%d" % world,
+                            "grad_sync": "sharded(ZeRO-1)" if a.sharded else "allreduce(bucketed,overlapped)"},
+                           **extra),
+            "final_loss": round(final_loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
