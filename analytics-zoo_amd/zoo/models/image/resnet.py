@@ -73,20 +73,26 @@ class BasicBlock(nn.Module):
 
 
 class Dense(nn.Module):
-    """Final classifier on the MFMA GEMM (fp32 logits)."""
+    """Final classifier on the MFMA GEMM (fp32 logits). The class dimension is
+    padded to a multiple of 8 (16-byte rows for the kernel); padded rows stay
+    exactly zero (their logits are sliced off, so their gradient is zero)."""
 
     def __init__(self, cin, cout):
         super().__init__()
-        w = torch.empty(cout, cin)
-        nn.init.normal_(w, 0.0, 0.01)
+        self.cout = cout
+        cpad = ops.ceil8(cout)
+        w = torch.zeros(cpad, cin)
+        nn.init.normal_(w[:cout], 0.0, 0.01)
         self.weight = nn.Parameter(w)
-        self.bias = nn.Parameter(torch.zeros(cout))
+        self.bias = nn.Parameter(torch.zeros(cpad))
 
     def forward(self, x):
         if x.is_cuda:
             y = ops.conv2d_nhwc(x.reshape(x.shape[0], 1, 1, x.shape[1]), self.weight, self.bias, out_f32=True)
-            return y.reshape(x.shape[0], -1)
-        return torch.nn.functional.linear(x.float(), self.weight, self.bias)
+            y = y.reshape(x.shape[0], -1)
+        else:
+            y = torch.nn.functional.linear(x.float(), self.weight, self.bias)
+        return y if self.cout == y.shape[1] else y[:, : self.cout].contiguous()
 
 
 class ResNet(nn.Module):

@@ -1,0 +1,271 @@
+"""Numerics of every native gfx950 kernel against a plain PyTorch fp32 reference.
+
+Run on a real MI355X with ``pytest -m gpu``. bf16 outputs are compared with
+relative-to-max tolerances sized for bf16 rounding (8 mantissa bits).
+"""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float(), b.float()
+    return ((a - b).abs().max() / b.abs().max().clamp_min(1e-6)).item()
+
+
+def nrel(a, b):
+    """norm-relative error: robust to a few ReLU-mask flips between bf16 and fp32"""
+    a, b = a.float().flatten(), b.float().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+CONV_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad
+    (2, 8, 8, 16, 32, 1, 1, 0),
+    (2, 9, 7, 24, 40, 3, 1, 1),
+    (3, 15, 15, 32, 64, 3, 2, 1),
+    (2, 14, 14, 64, 128, 1, 2, 0),
+    (2, 19, 19, 4, 64, 7, 2, 3),
+    (1, 5, 5, 136, 200, 3, 1, 0),
+    (4, 12, 12, 128, 136, 5, 1, 2),
+]
+
+
+@pytest.mark.parametrize("shape", CONV_SHAPES)
+def test_conv_fwd_dgrad_wgrad(gpu, shape):
+    from zoo.ops import native, pack_weight
+    C = native()
+    N, H, W, Cin, Cout, R, st, pad = shape
+    x = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
+    w4 = (torch.randn(Cout, R, R, Cin, device=gpu) / math.sqrt(R * R * Cin)).bfloat16()
+    w2 = pack_weight(w4)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w4.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad)
+    P, Q = yr.shape[2], yr.shape[3]
+    stats = torch.zeros(2 * Cout, device=gpu)
+    y = C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0)
+    assert y.shape == (N, P, Q, Cout)
+    assert rel(y, yr.detach().permute(0, 2, 3, 1)) < 1e-2
+    yf = y.float()
+    ref_stats = torch.cat([yf.sum((0, 1, 2)), (yf * yf).sum((0, 1, 2))])
+    assert rel(stats, ref_stats) < 1e-3
+    dy = torch.randn(N, P, Q, Cout, device=gpu).bfloat16()
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    dw = torch.zeros(Cout, w2.shape[1], device=gpu)
+    C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, 1, 1)
+    ref_dw = wr.grad.permute(0, 2, 3, 1).reshape(Cout, -1)
+    assert rel(dw[:, : R * R * Cin], ref_dw) < 1e-3
+    if dw.shape[1] > R * R * Cin:
+        assert dw[:, R * R * Cin:].abs().max().item() == 0.0
+    if Cin % 8 == 0:
+        wt = C.flip_weights(w4.contiguous(), Cout, R, R, Cin)
+        dx = C.conv_fwd(dy, wt, R, R, 1, 1, R - 1 - pad, R - 1 - pad, 1, 1, st, st, None, None, None, 0, False,
+                        True, H, W)
+        assert dx.shape == x.shape
+        assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
+def test_conv_epilogue_bias_resid_act(gpu):
+    from zoo.ops import native, pack_weight
+    C = native()
+    x = torch.randn(2, 6, 6, 32, device=gpu).bfloat16()
+    w4 = (torch.randn(48, 3, 3, 32, device=gpu) * 0.1).bfloat16()
+    b = torch.randn(48, device=gpu)
+    r = torch.randn(2, 6, 6, 48, device=gpu).bfloat16()
+    y = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, r, None, 1, False, True, 0, 0)
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2), b, padding=1).permute(0, 2, 3, 1)
+    ref = torch.relu(ref + r.float())
+    assert rel(y, ref) < 1e-2
+    yf = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, None, None, 0, True, False, 0, 0)
+    assert yf.dtype == torch.float32
+    ref2 = F.conv2d(x.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2), b, padding=1).permute(0, 2, 3, 1)
+    assert rel(yf, ref2) < 1e-3
+
+
+def test_linear_mfma(gpu):
+    from zoo.ops import linear
+    x = torch.randn(37, 96, device=gpu)
+    w = torch.randn(40, 96, device=gpu) * 0.1
+    b = torch.randn(40, device=gpu)
+    y = linear(x, w, b, act="relu")
+    assert rel(y, torch.relu(x @ w.t() + b)) < 2e-2
+
+
+def _bf(t):
+    return t.bfloat16().float()
+
+
+def _conv_bn_reference(x, w4, g, b, r, relu, dz, eps=1e-5):
+    """fp32 math with bf16 rounding exactly where the native path stores bf16."""
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = _bf(w4.float()).permute(0, 3, 1, 2)
+    y = _bf(F.conv2d(xr, wr, padding=1).permute(0, 2, 3, 1))          # conv output stored bf16
+    C = y.shape[-1]
+    yf = y.reshape(-1, C)
+    mean = yf.mean(0)
+    var = (yf * yf).mean(0) - mean * mean
+    inv = torch.rsqrt(var + eps)
+    xhat = (y - mean) * inv
+    z = xhat * g + b
+    if r is not None:
+        z = z + r.float()
+    if relu:
+        z = torch.relu(z)
+    z = _bf(z)
+    dzf = dz.float()
+    dy = dzf * (z > 0).float() if relu else dzf
+    M = yf.shape[0]
+    s1 = dy.reshape(-1, C).sum(0)
+    s2 = (dy * xhat).reshape(-1, C).sum(0)
+    dyc = _bf(g * inv * (dy - s1 / M - xhat * s2 / M))                   # BN-backward output stored bf16
+    dx = torch.nn.grad.conv2d_input(xr.shape, wr, dyc.permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    dw = torch.nn.grad.conv2d_weight(xr, wr.shape, dyc.permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    return {"z": z, "dx": dx, "dw": dw.reshape(dw.shape[0], -1), "dgamma": s2, "dbeta": s1,
+            "dresid": _bf(dy) if r is not None else None}
+
+
+@pytest.mark.parametrize("relu,resid", [(True, False), (True, True), (False, False)])
+def test_conv_bn_act_autograd_vs_reference(gpu, relu, resid):
+    from zoo.ops import conv_bn_act, pack_weight
+    torch.manual_seed(0)
+    N, H, Cin, Cout = 4, 10, 16, 32
+    x = torch.randn(N, H, H, Cin, device=gpu).bfloat16().requires_grad_(True)
+    w4 = torch.randn(Cout, 3, 3, Cin, device=gpu) * 0.2
+    w = pack_weight(w4).requires_grad_(True)
+    g = (torch.rand(Cout, device=gpu) + 0.5).requires_grad_(True)
+    bt = (torch.randn(Cout, device=gpu) * 0.1).requires_grad_(True)
+    r = torch.randn(N, H, H, Cout, device=gpu).bfloat16().requires_grad_(True) if resid else None
+    rm, rv = torch.zeros(Cout, device=gpu), torch.ones(Cout, device=gpu)
+    z = conv_bn_act(x, w, g, bt, rm, rv, kernel=(3, 3), pad=(1, 1), relu=relu, resid=r)
+    dz = torch.randn(z.shape, device=gpu).bfloat16()
+    z.backward(dz)
+    ref = _conv_bn_reference(x.detach(), w4, g.detach(), bt.detach(), None if r is None else r.detach(), relu, dz)
+    got = {"z": z, "dx": x.grad, "dw": w.grad[:, : 9 * Cin], "dgamma": g.grad, "dbeta": bt.grad,
+           "dresid": r.grad if resid else None}
+    errs = {k: nrel(got[k], ref[k]) for k in got if ref[k] is not None}
+    assert all(e < 1e-2 for e in errs.values()), errs
+    # running statistics: momentum 0.1 update with the unbiased batch variance
+    y = F.conv2d(x.detach().float().permute(0, 3, 1, 2), _bf(w4).permute(0, 3, 1, 2), padding=1)
+    assert rel(rm, 0.1 * y.mean((0, 2, 3))) < 2e-2
+
+
+def test_pooling(gpu):
+    from zoo.ops import max_pool2d_nhwc, global_avg_pool_nhwc
+    x = torch.randn(2, 13, 11, 24, device=gpu).bfloat16().requires_grad_(True)
+    y = max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+    xr = x.detach().float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, 3, 2, 1)
+    assert rel(y, yr.permute(0, 2, 3, 1)) < 1e-6
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel(x.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    x2 = torch.randn(3, 7, 7, 64, device=gpu).bfloat16().requires_grad_(True)
+    g = global_avg_pool_nhwc(x2)
+    assert rel(g, x2.detach().float().mean((1, 2))) < 1e-2
+    g.float().sum().backward()
+    assert rel(x2.grad, torch.full_like(x2.grad.float(), 1 / 49)) < 1e-2
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_softmax_xent(gpu, dt):
+    from zoo.ops import softmax_cross_entropy
+    logits = (torch.randn(33, 1000, device=gpu) * 3).to(dt).requires_grad_(True)
+    lab = torch.randint(0, 1000, (33,), device=gpu)
+    lab[3] = -100
+    l = softmax_cross_entropy(logits, lab)
+    lr_ = logits.detach().float().requires_grad_(True)
+    ref = F.cross_entropy(lr_, lab, ignore_index=-100)
+    assert abs(l.item() - ref.item()) < 1e-3 * max(1.0, ref.item())
+    l.backward()
+    ref.backward()
+    assert rel(logits.grad, lr_.grad) < 2e-2
+
+
+def test_fused_optimizers_match_cpu(gpu):
+    from zoo.pipeline.api.keras.optimizers import SGD, Adam, AdamWeightDecay, RMSprop, Adagrad, Adadelta, Adamax
+    for make in [lambda: SGD(learningrate=0.1, momentum=0.9, weightdecay=1e-3),
+                 lambda: SGD(learningrate=0.1, momentum=0.9, nesterov=True),
+                 lambda: Adam(lr=1e-2), lambda: AdamWeightDecay(lr=1e-2, weight_decay=0.01),
+                 lambda: RMSprop(learningrate=1e-2), lambda: Adagrad(learningrate=1e-1),
+                 lambda: Adadelta(), lambda: Adamax()]:
+        p0 = torch.randn(1000)
+        gs = [torch.randn(1000) for _ in range(3)]
+        res = []
+        for dev in ("cpu", gpu):
+            o = make()
+            p = p0.clone().to(dev)
+            bf = torch.empty(1000, dtype=torch.bfloat16, device=dev)
+            for g in gs:
+                o.step(p, g.to(dev), bf, 0.5)
+            res.append((p.cpu(), bf.float().cpu()))
+        assert rel(res[1][0], res[0][0]) < 1e-4, type(make()).__name__
+        assert rel(res[1][1], res[1][0]) < 1e-2
+
+
+def test_resnet_step_gpu_matches_cpu_reference(gpu):
+    """A small ResNet: one training step on the native kernels vs the fp32 CPU path."""
+    from zoo.models.image.resnet import ResNet, Bottleneck
+    from zoo.ops import softmax_cross_entropy
+    torch.manual_seed(0)
+    m_cpu = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=16, width=16)
+    m_gpu = ResNet(Bottleneck, [1, 1, 1, 1], num_classes=16, width=16)
+    m_gpu.load_state_dict(m_cpu.state_dict())
+    m_gpu = m_gpu.to(gpu)
+    # 128x128 input, batch 8: the last stage's BN still sees 128 values per channel
+    x = torch.randn(8, 3, 128, 128)
+    y = torch.randint(0, 16, (8,))
+    l_cpu = softmax_cross_entropy(m_cpu(x), y)
+    l_cpu.backward()
+    l_gpu = softmax_cross_entropy(m_gpu(x.to(gpu)), y.to(gpu))
+    l_gpu.backward()
+    assert abs(l_gpu.item() - l_cpu.item()) < 0.05 * max(1.0, l_cpu.item())
+    pc = dict(m_cpu.named_parameters())
+    cos = {}
+    for n, p in m_gpu.named_parameters():
+        assert p.grad is not None, n
+        cos[n] = F.cosine_similarity(p.grad.cpu().flatten().double(), pc[n].grad.flatten().double(), dim=0).item()
+    # Random data/labels give a noise-dominated gradient: merely rounding the CPU
+    # model's activations to bf16 moves stage-0 gradients to cosine ~0.95
+    # (tools/diag_resnet_grads.py). Exactness is tested per op above; here the
+    # directions must agree at that same scale and the head must match tightly.
+    bad = {n: c for n, c in cos.items() if c < 0.85}
+    assert not bad, bad
+    assert sum(cos.values()) / len(cos) > 0.93, cos
+    assert cos["fc.weight"] > 0.999 and cos["fc.bias"] > 0.999
+
+
+def test_resnet_learns_synthetic_task(gpu):
+    """End-to-end learnability through the engine: 4-way 'which quadrant is bright'."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.resnet import resnet18
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext()
+    torch.manual_seed(0)
+    eng = TrainingEngine(resnet18(num_classes=4), softmax_cross_entropy, SGD(learningrate=0.05, momentum=0.9))
+
+    def batch(n):
+        y = torch.randint(0, 4, (n,), device=gpu)
+        x = torch.randn(n, 3, 64, 64, device=gpu) * 0.5
+        for q in range(4):
+            sel = y == q
+            r0, c0 = (q // 2) * 32, (q % 2) * 32
+            x[sel, :, r0:r0 + 32, c0:c0 + 32] += 1.5
+        return x, y
+    losses = []
+    for _ in range(60):
+        x, y = batch(64)
+        losses.append(eng.train_step(x, y).item())
+    assert sum(losses[-10:]) / 10 < 0.25 * sum(losses[:5]) / 5, losses
+    eng.model.eval()
+    x, y = batch(256)
+    with torch.no_grad():
+        acc = (eng.model(x).argmax(1) == y).float().mean().item()
+    assert acc > 0.9, acc
