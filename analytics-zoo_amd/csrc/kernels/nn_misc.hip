@@ -1,0 +1,216 @@
+// LayerNorm and embedding kernels (gfx950).
+//
+// * LayerNorm forward/backward over the last dimension (InternalLayerNorm,
+//   Zs/pipeline/api/keras/layers/internal/InternalLayerNorm.scala:26-97; BERT's
+//   normalisation). One wave per row, 8 elements per lane
+//   per step (16-byte vector loads of bf16), fp32 statistics, gamma/beta grads
+//   reduced per workgroup in LDS and added with one fp32 atomic per column.
+// * Embedding gather (LookupTable forward, Embedding.scala:82-100) and sorted-
+//   free scatter-add backward with fp32 atomics into the (flat) gradient buffer
+//   (HK9). Rows are gathered 16 bytes per lane; each row's gradient add is a
+//   contiguous row segment (Guideline 12 atomic shaping).
+#include "common.h"
+
+namespace zoo {
+
+template <typename T>
+ZOO_DEV void ld8(const T* p, float* f);
+template <>
+ZOO_DEV void ld8<bf16_t>(const bf16_t* p, float* f) { unpack8(*reinterpret_cast<const uint4*>(p), f); }
+template <>
+ZOO_DEV void ld8<float>(const float* p, float* f) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w; f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+}
+template <typename T>
+ZOO_DEV void st8(T* p, const float* f);
+template <>
+ZOO_DEV void st8<bf16_t>(bf16_t* p, const float* f) { *reinterpret_cast<uint4*>(p) = pack8(f); }
+template <>
+ZOO_DEV void st8<float>(float* p, const float* f) {
+  *reinterpret_cast<float4*>(p) = make_float4(f[0], f[1], f[2], f[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
+}
+
+// ---------------------------------------------------------------- LayerNorm
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_fwd_kernel(const T* __restrict__ X, const float* __restrict__ g,
+                                                            const float* __restrict__ b, T* __restrict__ Y,
+                                                            float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                            int rows, int D, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* x = X + (size_t)row * D;
+  float s = 0.f, ss = 0.f;
+  for (int c = lane * 8; c < D; c += 512) {
+    float v[8];
+    ld8(x + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s += v[e]; ss += v[e] * v[e]; }
+  }
+  s = warp_sum(s);
+  ss = warp_sum(ss);
+  const float mu = s / D;
+  const float var = fmaxf(ss / D - mu * mu, 0.f);
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+  T* y = Y + (size_t)row * D;
+  for (int c = lane * 8; c < D; c += 512) {
+    float v[8];
+    ld8(x + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (v[e] - mu) * rs * (g ? g[c + e] : 1.f) + (b ? b[c + e] : 0.f);
+    st8(y + c, v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ dY, const T* __restrict__ X,
+                                                            const float* __restrict__ g, const float* __restrict__ mean,
+                                                            const float* __restrict__ rstd, T* __restrict__ dX,
+                                                            float* __restrict__ dg, float* __restrict__ db, int rows,
+                                                            int D, int rows_per_block) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* sdg = reinterpret_cast<float*>(smem);  // [D]
+  float* sdb = sdg + D;                          // [D]
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) sdg[i] = 0.f;
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  for (int row = r0 + wid; row < r1; row += 4) {
+    const T* x = X + (size_t)row * D;
+    const T* dy = dY + (size_t)row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float a = 0.f, bsum = 0.f;  // sum(dy*g*xhat), sum(dy*g)
+    for (int c = lane * 8; c < D; c += 512) {
+      float xv[8], gv[8];
+      ld8(x + c, xv);
+      ld8(dy + c, gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (xv[e] - mu) * rs;
+        const float gg = gv[e] * (g ? g[c + e] : 1.f);
+        a += gg * xh;
+        bsum += gg;
+        atomicAdd(&sdg[c + e], gv[e] * xh);  // LDS atomics
+        atomicAdd(&sdb[c + e], gv[e]);
+      }
+    }
+    a = warp_sum(a) / D;
+    bsum = warp_sum(bsum) / D;
+    T* dx = dX + (size_t)row * D;
+    for (int c = lane * 8; c < D; c += 512) {
+      float xv[8], gv[8], o[8];
+      ld8(x + c, xv);
+      ld8(dy + c, gv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float xh = (xv[e] - mu) * rs;
+        o[e] = rs * (gv[e] * (g ? g[c + e] : 1.f) - bsum - xh * a);
+      }
+      st8(dx + c, o);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    if (dg) atomicAdd(dg + i, sdg[i]);
+    if (db) atomicAdd(db + i, sdb[i]);
+  }
+}
+
+// ---------------------------------------------------------------- Embedding
+// out[i][:] = table[idx[i]][:]   (rows with idx < 0 or == padding produce zeros)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_fwd_kernel(const T* __restrict__ table, const int64_t* __restrict__ idx,
+                                                            T* __restrict__ out, int n, int D, int V, int64_t pad) {
+  const int vec = 16 / sizeof(T);
+  const int cpr = D / vec;
+  const size_t total = (size_t)n * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / cpr), c = (int)(i % cpr);
+    const int64_t id = idx[r];
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (id >= 0 && id < V && id != pad) v = reinterpret_cast<const uint4*>(table + (size_t)id * D)[c];
+    reinterpret_cast<uint4*>(out + (size_t)r * D)[c] = v;
+  }
+}
+
+// grad_table[idx[i]][:] += dout[i][:]  (fp32 accumulate)
+template <typename T>
+__global__ __launch_bounds__(256) void embedding_bwd_kernel(const T* __restrict__ dout, const int64_t* __restrict__ idx,
+                                                            float* __restrict__ gtable, int n, int D, int V,
+                                                            int64_t pad, float scale) {
+  const size_t total = (size_t)n * D;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int r = (int)(i / D), c = (int)(i % D);
+    const int64_t id = idx[r];
+    if (id < 0 || id >= V || id == pad) continue;
+    float v;
+    if constexpr (sizeof(T) == 4) v = dout[i];
+    else v = bf2f(dout[i]);
+    atomicAdd(gtable + (size_t)id * D + c, v * scale);
+  }
+}
+
+static int mgrid(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 8192) b = 8192;
+  return (int)(b ? b : 1);
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, const float* b, void* Y, float* mean,
+                                        float* rstd, int rows, int D, float eps, hipStream_t st) {
+  const int blocks = (rows + 3) / 4;
+  if (f32)
+    hipLaunchKernelGGL(layernorm_fwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)X, g, b, (float*)Y,
+                       mean, rstd, rows, D, eps);
+  else
+    hipLaunchKernelGGL(layernorm_fwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X, g, b,
+                       (bf16_t*)Y, mean, rstd, rows, D, eps);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
+                                        const float* rstd, void* dX, float* dg, float* db, int rows, int D,
+                                        hipStream_t st) {
+  int rpb = (rows + 511) / 512;
+  if (rpb < 4) rpb = 4;
+  const int blocks = (rows + rpb - 1) / rpb;
+  const size_t smem = (size_t)2 * D * sizeof(float);
+  if (f32)
+    hipLaunchKernelGGL(layernorm_bwd_kernel<float>, dim3(blocks), dim3(256), smem, st, (const float*)dY,
+                       (const float*)X, g, mean, rstd, (float*)dX, dg, db, rows, D, rpb);
+  else
+    hipLaunchKernelGGL(layernorm_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dY,
+                       (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, dg, db, rows, D, rpb);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_embedding_fwd(const void* table, int f32, const int64_t* idx, void* out, int n, int D, int V,
+                                        int64_t pad, hipStream_t st) {
+  const int vec = f32 ? 4 : 8;
+  if (f32)
+    hipLaunchKernelGGL(embedding_fwd_kernel<float>, dim3(mgrid((size_t)n * D / vec)), dim3(256), 0, st,
+                       (const float*)table, idx, (float*)out, n, D, V, pad);
+  else
+    hipLaunchKernelGGL(embedding_fwd_kernel<bf16_t>, dim3(mgrid((size_t)n * D / vec)), dim3(256), 0, st,
+                       (const bf16_t*)table, idx, (bf16_t*)out, n, D, V, pad);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_embedding_bwd(const void* dout, int f32, const int64_t* idx, float* gtable, int n, int D,
+                                        int V, int64_t pad, float scale, hipStream_t st) {
+  if (f32)
+    hipLaunchKernelGGL(embedding_bwd_kernel<float>, dim3(mgrid((size_t)n * D)), dim3(256), 0, st, (const float*)dout,
+                       idx, gtable, n, D, V, pad, scale);
+  else
+    hipLaunchKernelGGL(embedding_bwd_kernel<bf16_t>, dim3(mgrid((size_t)n * D)), dim3(256), 0, st,
+                       (const bf16_t*)dout, idx, gtable, n, D, V, pad, scale);
+  return hipGetLastError();
+}

@@ -52,6 +52,12 @@ hipError_t zoo_nchw_to_nhwc(const float*, void*, int, int, int, int, int, hipStr
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
+hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
+                             hipStream_t);
+hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
+                             float*, int, int, hipStream_t);
+hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, int, int64_t, hipStream_t);
+hipError_t zoo_embedding_bwd(const void*, int, const int64_t*, float*, int, int, int, int64_t, float, hipStream_t);
 }
 
 namespace {
@@ -423,6 +429,74 @@ torch::Tensor add_bf16(torch::Tensor a, torch::Tensor b) {
   return y;
 }
 
+bool is_f32(const torch::Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, "expected float32 or bfloat16");
+  return t.scalar_type() == at::kFloat;
+}
+
+std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, c10::optional<torch::Tensor> g,
+                                         c10::optional<torch::Tensor> b, double eps) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "layernorm: contiguous GPU input");
+  const bool f32 = is_f32(x);
+  const int D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0, "layernorm: last dim must be a multiple of 8");
+  if (g.has_value() && g->defined()) { req(*g, at::kFloat, "gamma"); TORCH_CHECK(g->numel() == D, "gamma size"); }
+  if (b.has_value() && b->defined()) { req(*b, at::kFloat, "beta"); TORCH_CHECK(b->numel() == D, "beta size"); }
+  auto y = torch::empty_like(x);
+  auto mean = torch::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = torch::empty({rows}, x.options().dtype(at::kFloat));
+  check_hip(zoo_layernorm_fwd(x.data_ptr(), f32, opt_ptr<float>(g), opt_ptr<float>(b), y.data_ptr(),
+                              mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)rows, D, (float)eps, cur_stream()),
+            "layernorm_fwd");
+  return {y, mean, rstd};
+}
+
+torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> g, torch::Tensor mean,
+                            torch::Tensor rstd, c10::optional<torch::Tensor> dg, c10::optional<torch::Tensor> db) {
+  TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous(), "layernorm_bwd: contiguous GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel(), "layernorm_bwd: dy/x mismatch");
+  const bool f32 = is_f32(x);
+  const int D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && mean.numel() == rows && rstd.numel() == rows, "layernorm_bwd: shapes");
+  if (dg.has_value() && dg->defined()) { req(*dg, at::kFloat, "dgamma"); TORCH_CHECK(dg->numel() == D, "dg"); }
+  if (db.has_value() && db->defined()) { req(*db, at::kFloat, "dbeta"); TORCH_CHECK(db->numel() == D, "db"); }
+  auto dx = torch::empty_like(x);
+  check_hip(zoo_layernorm_bwd(dy.data_ptr(), x.data_ptr(), f32, opt_ptr<float>(g), mean.data_ptr<float>(),
+                              rstd.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dg), opt_ptr<float>(db),
+                              (int)rows, D, cur_stream()),
+            "layernorm_bwd");
+  return dx;
+}
+
+torch::Tensor embedding_fwd(torch::Tensor table, torch::Tensor idx, int64_t pad) {
+  TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.dim() == 2, "embedding: 2-D GPU table");
+  req(idx, at::kLong, "indices");
+  const bool f32 = is_f32(table);
+  const int D = table.size(1), V = table.size(0);
+  TORCH_CHECK((f32 ? D % 4 : D % 8) == 0, "embedding: row must be a multiple of 16 bytes");
+  auto out_shape = idx.sizes().vec();
+  out_shape.push_back(D);
+  auto out = torch::empty(out_shape, table.options());
+  check_hip(zoo_embedding_fwd(table.data_ptr(), f32, idx.data_ptr<int64_t>(), out.data_ptr(), (int)idx.numel(), D, V,
+                              pad, cur_stream()),
+            "embedding_fwd");
+  return out;
+}
+
+void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor gtable, int64_t pad, double scale) {
+  TORCH_CHECK(dout.is_cuda() && dout.is_contiguous(), "embedding_bwd: contiguous GPU grad");
+  req(idx, at::kLong, "indices");
+  req(gtable, at::kFloat, "grad table");
+  const bool f32 = is_f32(dout);
+  const int D = gtable.size(1), V = gtable.size(0);
+  TORCH_CHECK(dout.numel() == idx.numel() * (int64_t)D, "embedding_bwd: shape");
+  check_hip(zoo_embedding_bwd(dout.data_ptr(), f32, idx.data_ptr<int64_t>(), gtable.data_ptr<float>(),
+                              (int)idx.numel(), D, V, pad, (float)scale, cur_stream()),
+            "embedding_bwd");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -447,4 +521,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bf16_to_f32", &bf16_to_f32);
   m.def("f32_to_bf16", &f32_to_bf16);
   m.def("add_bf16", &add_bf16);
+  m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("embedding_fwd", &embedding_fwd);
+  m.def("embedding_bwd", &embedding_bwd);
 }

@@ -1,0 +1,1 @@
+"""zoo.feature — FeatureSet (memory tiers, sharding), preprocessing, image/text pipelines."""

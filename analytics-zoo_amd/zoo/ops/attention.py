@@ -1,0 +1,66 @@
+"""Scaled dot-product attention (TransformerLayer.attn, TransformerLayer.scala:163-181).
+
+``attention(q, k, v, mask=None, causal=False, dropout_p=0.0)`` with q/k/v
+shaped [batch, heads, seq, head_dim]. On the GPU with bf16 and head_dim in
+{64, 128}, no dropout and an additive/causal mask, the fused native HIP kernel
+(online softmax, O(L) memory; ``zoo._C.attn_fwd``/``attn_bwd``) is used when it
+has been built; otherwise the materialised reference path (two batched GEMMs
+around a softmax) runs. The reference path is also the CPU implementation.
+"""
+import math
+
+import torch
+
+from zoo.ops._native import available, native
+
+
+def _reference(q, k, v, mask, causal, dropout_p, training):
+    scale = 1.0 / math.sqrt(q.shape[-1])
+    w = torch.matmul(q, k.transpose(-1, -2)) * scale
+    if causal:
+        L, S = w.shape[-2], w.shape[-1]
+        tri = torch.ones(L, S, dtype=torch.bool, device=w.device).tril(S - L)
+        w = w.masked_fill(~tri, float("-inf"))
+    if mask is not None:
+        w = w + mask.to(w.dtype)
+    p = torch.softmax(w.float(), dim=-1).to(q.dtype)
+    if dropout_p > 0 and training:
+        p = torch.nn.functional.dropout(p, dropout_p)
+    return torch.matmul(p, v)
+
+
+class _FlashAttnFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, mask, causal):
+        o, lse = native().attn_fwd(q, k, v, mask, causal)
+        ctx.save_for_backward(q, k, v, mask, o, lse)
+        ctx.causal = causal
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, mask, o, lse = ctx.saved_tensors
+        dq, dk, dv = native().attn_bwd(do.contiguous(), q, k, v, mask, o, lse, ctx.causal)
+        return dq, dk, dv, None, None
+
+
+def _native_ok(q, k, v, mask, dropout_p, training):
+    if not (q.is_cuda and available() and hasattr(native(), "attn_fwd")):
+        return False
+    if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128) or (dropout_p > 0 and training):
+        return False
+    if mask is not None and (mask.dtype != torch.float32 or mask.dim() != 2):
+        return False
+    return q.shape[-2] % 64 == 0 and k.shape[-2] % 64 == 0
+
+
+def attention(q, k, v, mask=None, causal=False, dropout_p=0.0, training=False):
+    """mask: additive float mask broadcastable to [B, H, L, S]; a [B, S] key
+    mask (0 keep / -10000 drop, BERT style) takes the fused path."""
+    if _native_ok(q, k, v, mask, dropout_p, training):
+        return _FlashAttnFn.apply(q.contiguous(), k.contiguous(), v.contiguous(),
+                                  None if mask is None else mask.contiguous(), bool(causal))
+    m = mask
+    if m is not None and m.dim() == 2:
+        m = m[:, None, None, :]
+    return _reference(q, k, v, m, causal, dropout_p, training)

@@ -164,3 +164,56 @@ def linear(x, w, bias=None, act=None):
         return y.reshape(*lead, K).to(x.dtype)
     y = F.linear(x, w.to(x.dtype), None if bias is None else bias.to(x.dtype))
     return _ref_act(y, act)
+
+
+class _ConvTranspose2dFn(torch.autograd.Function):
+    """Transposed conv (Deconvolution2D) = data-gradient of the conv F whose
+    packed weight is ``wf`` [Cin_deconv, R*S*Cout_deconv]. Forward runs the
+    dgrad kernel path (input dilation = stride); backward is a plain forward
+    conv (dX) and a wgrad with the operands' roles swapped (dW)."""
+
+    @staticmethod
+    def forward(ctx, x, wf, R, S, stride, pad, out_hw, cout):
+        C_ = native()
+        cin = x.shape[3]
+        wfb = bf16_weight(wf)[:, : R * S * cout].contiguous()
+        wt = C_.flip_weights(wfb, cin, R, S, cout)
+        if wt.shape[1] % 8:
+            wt = F.pad(wt, (0, ceil8(wt.shape[1]) - wt.shape[1]))
+        y = C_.conv_fwd(x, wt, R, S, 1, 1, R - 1 - pad[0], S - 1 - pad[1], 1, 1, stride[0], stride[1], None, None,
+                        None, 0, False, True, out_hw[0], out_hw[1])
+        ctx.save_for_backward(x, wf)
+        ctx.g = (R, S, stride, pad, cout)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = native()
+        x, wf = ctx.saved_tensors
+        R, S, stride, pad, cout = ctx.g
+        dyb = dy.contiguous().to(torch.bfloat16)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            dx = C_.conv_fwd(dyb, bf16_weight(wf), R, S, stride[0], stride[1], pad[0], pad[1], 1, 1, 1, 1, None,
+                             None, None, 0, False, True, x.shape[1], x.shape[2])
+        if ctx.needs_input_grad[1]:
+            gw = torch.zeros(wf.shape, dtype=torch.float32, device=wf.device)
+            C_.conv_wgrad(dyb, x, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
+            dw = gw.to(wf.dtype)
+        return dx, dw, None, None, None, None, None, None
+
+
+def conv_transpose2d_nhwc(x, wf, kernel, stride, pad, out_hw, cout):
+    """x: [N,H,W,Cin]; wf: packed [Cin, ceil8(R*S*Cout)] (Wf[ci][r][s][co] = Wd[ci][co][r][s])."""
+    R, S = kernel
+    if x.is_cuda:
+        return _ConvTranspose2dFn.apply(x.to(torch.bfloat16).contiguous(), wf, R, S, tuple(stride), tuple(pad),
+                                        tuple(out_hw), cout)
+    cin = x.shape[3]
+    wd = unpack_weight(wf.float(), cin, R, S, cout).permute(0, 3, 1, 2)  # [ci][co][r][s]
+    H, W = x.shape[1], x.shape[2]
+    oh = (H - 1) * stride[0] - 2 * pad[0] + R
+    ow = (W - 1) * stride[1] - 2 * pad[1] + S
+    y = F.conv_transpose2d(x.float().permute(0, 3, 1, 2), wd, stride=stride, padding=pad,
+                           output_padding=(out_hw[0] - oh, out_hw[1] - ow))
+    return y.permute(0, 2, 3, 1).to(x.dtype)

@@ -1,0 +1,205 @@
+"""Recurrent layers: SimpleRNN, LSTM, GRU, ConvLSTM2D, ConvLSTM3D
+(Py/pipeline/api/keras/layers/recurrent.py, convolutional_recurrent.py;
+Zs LSTM.scala:71-80, GRU, SimpleRNN, InternalRecurrent.scala:80-140).
+
+The input projection of ALL timesteps is one GEMM on the native MFMA kernel
+(``zoo.ops.linear`` over [batch*steps, input_dim]); the recurrence then does
+one [batch, hidden] x [hidden, gates*hidden] GEMM per step plus the gate math.
+Gate order follows Keras 1: LSTM (i, f, c, o), GRU (z, r, h).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from zoo import ops
+from zoo.pipeline.api.keras.base import Layer, apply_activation, init_tensor
+
+
+class _RNNBase(Layer):
+    n_gates = 1
+
+    def __init__(self, output_dim, activation="tanh", inner_activation="hard_sigmoid", return_sequences=False,
+                 go_backwards=False, W_regularizer=None, U_regularizer=None, b_regularizer=None, input_shape=None,
+                 init="glorot_uniform", inner_init="orthogonal", **kwargs):
+        super().__init__(input_shape=input_shape, **kwargs)
+        self.output_dim = int(output_dim)
+        self.activation, self.inner_activation = activation, inner_activation
+        self.return_sequences, self.go_backwards = return_sequences, go_backwards
+        self.init, self.inner_init = init, inner_init
+        self.add_regularizer(W_regularizer, "W")
+        self.add_regularizer(U_regularizer, "U")
+        self.add_regularizer(b_regularizer, "b")
+
+    def build(self, input_shape):
+        d, h, g = input_shape[-1], self.output_dim, self.n_gates
+        self.W = nn.Parameter(init_tensor(torch.empty(g * h, d), self.init, fan_in=d, fan_out=h))
+        U = torch.empty(g * h, h)
+        for i in range(g):
+            if self.inner_init == "orthogonal":
+                nn.init.orthogonal_(U[i * h:(i + 1) * h])
+            else:
+                init_tensor(U[i * h:(i + 1) * h], self.inner_init)
+        self.U = nn.Parameter(U)
+        b = torch.zeros(g * h)
+        if isinstance(self, LSTM):
+            b[h:2 * h] = 1.0  # forget-gate bias (Keras unit_forget_bias)
+        self.b = nn.Parameter(b)
+
+    def compute_output_shape(self, input_shape):
+        if self.return_sequences:
+            return (None, input_shape[1], self.output_dim)
+        return (None, self.output_dim)
+
+    def _step(self, xt, state):
+        raise NotImplementedError
+
+    def _init_state(self, x):
+        h = x.new_zeros(x.shape[0], self.output_dim)
+        return (h,)
+
+    def call(self, x):
+        B, T, D = x.shape
+        xw = ops.linear(x.reshape(B * T, D), self.W, self.b).reshape(B, T, -1)
+        state = self._init_state(x)
+        outs = []
+        steps = range(T - 1, -1, -1) if self.go_backwards else range(T)
+        for t in steps:
+            state = self._step(xw[:, t], state)
+            if self.return_sequences:
+                outs.append(state[0])
+        if self.return_sequences:
+            return torch.stack(outs, dim=1)
+        return state[0]
+
+
+class SimpleRNN(_RNNBase):
+    n_gates = 1
+
+    def __init__(self, output_dim, activation="tanh", return_sequences=False, go_backwards=False,
+                 W_regularizer=None, U_regularizer=None, b_regularizer=None, input_shape=None, **kwargs):
+        super().__init__(output_dim, activation, None, return_sequences, go_backwards, W_regularizer, U_regularizer,
+                         b_regularizer, input_shape, **kwargs)
+
+    def _step(self, xt, state):
+        (h,) = state
+        return (apply_activation(xt + ops.linear(h, self.U), self.activation),)
+
+
+class LSTM(_RNNBase):
+    n_gates = 4
+
+    def _init_state(self, x):
+        z = x.new_zeros(x.shape[0], self.output_dim)
+        return (z, z.clone())
+
+    def _step(self, xt, state):
+        h, c = state
+        H = self.output_dim
+        g = xt + ops.linear(h, self.U)
+        i = apply_activation(g[:, :H], self.inner_activation)
+        f = apply_activation(g[:, H:2 * H], self.inner_activation)
+        cc = apply_activation(g[:, 2 * H:3 * H], self.activation)
+        o = apply_activation(g[:, 3 * H:], self.inner_activation)
+        c = f * c + i * cc
+        h = o * apply_activation(c, self.activation)
+        return (h, c)
+
+
+class GRU(_RNNBase):
+    n_gates = 3
+
+    def _step(self, xt, state):
+        (h,) = state
+        H = self.output_dim
+        uh = ops.linear(h, self.U[: 2 * H])
+        z = apply_activation(xt[:, :H] + uh[:, :H], self.inner_activation)
+        r = apply_activation(xt[:, H:2 * H] + uh[:, H:], self.inner_activation)
+        hh = apply_activation(xt[:, 2 * H:] + ops.linear(r * h, self.U[2 * H:]), self.activation)
+        return (z * h + (1 - z) * hh,)
+
+
+class ConvLSTM2D(Layer):
+    """Convolutional LSTM over (batch, time, channels, rows, cols) ('th')."""
+
+    def __init__(self, nb_filter, nb_row, nb_col, activation="tanh", inner_activation="hard_sigmoid",
+                 dim_ordering="th", border_mode="same", subsample=(1, 1), W_regularizer=None, U_regularizer=None,
+                 b_regularizer=None, return_sequences=False, go_backwards=False, input_shape=None, **kwargs):
+        super().__init__(input_shape=input_shape, **kwargs)
+        self.nb_filter, self.k = int(nb_filter), (nb_row, nb_col)
+        self.activation, self.inner_activation = activation, inner_activation
+        self.return_sequences, self.go_backwards = return_sequences, go_backwards
+        self.subsample = tuple(subsample) if isinstance(subsample, (tuple, list)) else (subsample, subsample)
+
+    def build(self, input_shape):
+        c = input_shape[2]
+        f = self.nb_filter
+        self.Wx = nn.Parameter(init_tensor(torch.empty(4 * f, c, *self.k), "glorot_uniform"))
+        self.Wh = nn.Parameter(init_tensor(torch.empty(4 * f, f, *self.k), "glorot_uniform"))
+        self.b = nn.Parameter(torch.zeros(4 * f))
+
+    def compute_output_shape(self, s):
+        h = (s[3] + self.subsample[0] - 1) // self.subsample[0]
+        w = (s[4] + self.subsample[1] - 1) // self.subsample[1]
+        if self.return_sequences:
+            return (None, s[1], self.nb_filter, h, w)
+        return (None, self.nb_filter, h, w)
+
+    def call(self, x):
+        B, T = x.shape[:2]
+        pad = (self.k[0] // 2, self.k[1] // 2)
+        xs = F.conv2d(x.reshape(B * T, *x.shape[2:]), self.Wx.to(x.dtype), self.b.to(x.dtype), self.subsample, pad)
+        xs = xs.reshape(B, T, *xs.shape[1:])
+        f = self.nb_filter
+        h = x.new_zeros(B, f, xs.shape[3], xs.shape[4])
+        c = h.clone()
+        outs = []
+        for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):
+            g = xs[:, t] + F.conv2d(h, self.Wh.to(h.dtype), None, 1, pad)
+            i = apply_activation(g[:, :f], self.inner_activation)
+            fg = apply_activation(g[:, f:2 * f], self.inner_activation)
+            cc = apply_activation(g[:, 2 * f:3 * f], self.activation)
+            o = apply_activation(g[:, 3 * f:], self.inner_activation)
+            c = fg * c + i * cc
+            h = o * apply_activation(c, self.activation)
+            outs.append(h)
+        return torch.stack(outs, 1) if self.return_sequences else h
+
+
+class ConvLSTM3D(Layer):
+    """Convolutional LSTM over (batch, time, channels, d1, d2, d3)."""
+
+    def __init__(self, nb_filter, nb_kernel, dim_ordering="th", border_mode="same", subsample=(1, 1, 1),
+                 W_regularizer=None, U_regularizer=None, b_regularizer=None, return_sequences=False,
+                 go_backwards=False, input_shape=None, **kwargs):
+        super().__init__(input_shape=input_shape, **kwargs)
+        self.nb_filter, self.k = int(nb_filter), int(nb_kernel)
+        self.return_sequences, self.go_backwards = return_sequences, go_backwards
+
+    def build(self, input_shape):
+        c, f, k = input_shape[2], self.nb_filter, self.k
+        self.Wx = nn.Parameter(init_tensor(torch.empty(4 * f, c, k, k, k), "glorot_uniform"))
+        self.Wh = nn.Parameter(init_tensor(torch.empty(4 * f, f, k, k, k), "glorot_uniform"))
+        self.b = nn.Parameter(torch.zeros(4 * f))
+
+    def compute_output_shape(self, s):
+        if self.return_sequences:
+            return (None, s[1], self.nb_filter) + tuple(s[3:])
+        return (None, self.nb_filter) + tuple(s[3:])
+
+    def call(self, x):
+        B, T = x.shape[:2]
+        p = self.k // 2
+        xs = F.conv3d(x.reshape(B * T, *x.shape[2:]), self.Wx.to(x.dtype), self.b.to(x.dtype), 1, p)
+        xs = xs.reshape(B, T, *xs.shape[1:])
+        f = self.nb_filter
+        h = x.new_zeros(B, f, *xs.shape[3:])
+        c = h.clone()
+        outs = []
+        for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):
+            g = xs[:, t] + F.conv3d(h, self.Wh.to(h.dtype), None, 1, p)
+            i, fg = torch.sigmoid(g[:, :f]), torch.sigmoid(g[:, f:2 * f])
+            cc, o = torch.tanh(g[:, 2 * f:3 * f]), torch.sigmoid(g[:, 3 * f:])
+            c = fg * c + i * cc
+            h = o * torch.tanh(c)
+            outs.append(h)
+        return torch.stack(outs, 1) if self.return_sequences else h

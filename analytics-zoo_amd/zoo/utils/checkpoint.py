@@ -26,7 +26,7 @@ def save_object(obj, path, overwrite=True):
         raise FileExistsError(path)
     d = os.path.dirname(os.path.abspath(path))
     os.makedirs(d, exist_ok=True)
-    fd, tmp = tempfile.mkstemp(dir=d, prefix=".tmp_")
+    fd, tmp = tempfile.mkstemp(dir=d, prefix="zoo_tmp_", suffix=".part")
     os.close(fd)
     try:
         torch.save(obj, tmp)
