@@ -270,9 +270,7 @@ class Layer(nn.Module):
     def __init_subclass__(cls, **kw):
         # record constructor arguments (outermost __init__ only) for save/load
         super().__init_subclass__(**kw)
-        orig = cls.__dict__.get("__init__")
-        if orig is None:
-            return
+        orig = cls.__init__  # own or inherited (an inherited wrapper skips itself)
 
         def init(self, *a, **k):
             if "_init_args" not in self.__dict__:

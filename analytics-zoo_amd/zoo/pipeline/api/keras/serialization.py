@@ -90,7 +90,9 @@ def layer_config(layer):
     _cls, a, k = layer._init_args
     k = dict(k)
     k.setdefault("name", layer.name)
+    gis = layer._given_input_shape
     return {"class": [mod, qual], "args": [_enc(x) for x in a], "kwargs": {kk: _enc(vv) for kk, vv in k.items()},
+            "given_input_shape": None if gis is None else _enc(list(gis)) if not isinstance(gis, list) else _enc(gis),
             "built_shape": _enc(list(layer.get_input_shape())) if isinstance(layer.get_input_shape(), tuple) else None}
 
 
@@ -118,12 +120,19 @@ def build_layer(cfg):
     cls = _resolve(*cfg["class"])
     if "sequential" in cfg:
         m = cls(name=cfg.get("name"))
-        for c in cfg["sequential"]:
-            m.add(build_layer(c))
+        for i, c in enumerate(cfg["sequential"]):
+            l = build_layer(c)
+            if i == 0 and l._given_input_shape is None and cfg.get("input_shape") is not None:
+                l._given_input_shape = tuple(cfg["input_shape"])
+            m.add(l)
         return m
     if "graph" in cfg:
         return build_graph(cfg["graph"], cls, cfg.get("name"))
     layer = cls(*[_dec(x) for x in cfg["args"]], **{k: _dec(v) for k, v in cfg["kwargs"].items()})
+    gis = cfg.get("given_input_shape")
+    if gis is not None and layer._given_input_shape is None:
+        g = _dec(gis)
+        layer._given_input_shape = tuple(g) if g and not isinstance(g[0], (list, tuple)) else g
     bs = cfg.get("built_shape")
     if bs is not None and not layer.built:
         shape = _dec(bs)

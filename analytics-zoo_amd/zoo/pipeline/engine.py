@@ -143,7 +143,7 @@ class TrainingEngine:
                 recs += bs
                 n_since += bs
                 state["records"] += bs
-                self._pending_loss.append(loss)
+                self._pending_loss.append((state["neval"] - 1, loss))
                 if (state["neval"] - 1) % log_every == 0:
                     lval = self.flush_loss()
                     dt = time.time() - t_last
@@ -152,7 +152,6 @@ class TrainingEngine:
                     log.info("Epoch %d iter %d loss %.5f throughput %.1f records/s lr %.6g", state["epoch"],
                              state["neval"] - 1, lval, thr, self.optim.current_lr())
                     if self.train_summary is not None:
-                        self.train_summary.add_scalar("Loss", lval, state["neval"] - 1)
                         self.train_summary.add_scalar("Throughput", thr, state["neval"] - 1)
                         self.train_summary.add_scalar("LearningRate", self.optim.current_lr(), state["neval"] - 1)
                     t_last, n_since = time.time(), 0
@@ -180,12 +179,18 @@ class TrainingEngine:
             state["epoch_end"] = False
 
     def flush_loss(self):
+        """Bring the device-side per-iteration losses to the host (one sync),
+        average over ranks (one all-reduce) and log them to TensorBoard."""
         if not self._pending_loss:
             return self.state["Loss"]
-        vals = torch.stack([l.float() for l in self._pending_loss])
-        v = self.sync.all_reduce_scalars([vals.mean().item()]) / self.sync.world
+        its = [i for i, _ in self._pending_loss]
+        vals = torch.stack([l.float().reshape(()) for _, l in self._pending_loss])
+        red = self.sync.all_reduce_scalars(vals.detach().cpu().tolist()) / self.sync.world
         self._pending_loss = []
-        self.state["Loss"] = float(v[0])
+        if self.train_summary is not None:
+            for it, v in zip(its, red.tolist()):
+                self.train_summary.add_scalar("Loss", v, it)
+        self.state["Loss"] = float(red[-1])
         self.optim.state["Loss"] = self.state["Loss"]
         return self.state["Loss"]
 
