@@ -64,7 +64,7 @@ def build_resnet50(ctx, batch):
 
 def build_ncf(ctx, batch):
     from zoo.models.recommendation.neuralcf import NeuralCF
-    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
     from zoo.pipeline.api.keras.optimizers import Adam
     from zoo.pipeline.engine import TrainingEngine
 
@@ -72,7 +72,7 @@ def build_ncf(ctx, batch):
     users, items = 138493, 26744  # ml-20m shape
     model = NeuralCF(users, items, 5, user_embed=20, item_embed=20, hidden_layers=(40, 20, 10), include_mf=True,
                      mf_embed=20)
-    eng = TrainingEngine(model, softmax_cross_entropy, Adam(lr=1e-3))
+    eng = TrainingEngine(model, SparseCategoricalCrossEntropy(), Adam(lr=1e-3))
     dev = ctx.device
     g = torch.Generator(device=dev)
     g.manual_seed(ctx.rank)

@@ -11,6 +11,8 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
+sys_path_hack = None
+
 
 def rel(a, b):
     a, b = a.float(), b.float()
@@ -269,3 +271,84 @@ def test_resnet_learns_synthetic_task(gpu):
     with torch.no_grad():
         acc = (eng.model(x).argmax(1) == y).float().mean().item()
     assert acc > 0.9, acc
+
+
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_layernorm_kernel(gpu, dt):
+    from zoo.ops import layer_norm
+    x = torch.randn(37, 768, device=gpu).to(dt).requires_grad_(True)
+    g = (torch.rand(768, device=gpu) + 0.5).requires_grad_(True)
+    b = torch.randn(768, device=gpu).requires_grad_(True)
+    y = layer_norm(x, g, b, 1e-5)
+    xr = x.detach().float().requires_grad_(True)
+    gr, br = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    yr = F.layer_norm(xr, (768,), gr, br, 1e-5)
+    assert nrel(y, yr) < (1e-5 if dt == torch.float32 else 1e-2)
+    dy = torch.randn_like(yr)
+    y.backward(dy.to(dt))
+    yr.backward(dy)
+    tol = 1e-4 if dt == torch.float32 else 2e-2
+    assert nrel(x.grad, xr.grad) < tol and nrel(g.grad, gr.grad) < tol and nrel(b.grad, br.grad) < tol
+
+
+@pytest.mark.parametrize("dt,D", [(torch.float32, 20), (torch.bfloat16, 64)])
+def test_embedding_kernel(gpu, dt, D):
+    from zoo.ops import embedding
+    table = torch.randn(1000, D, device=gpu).requires_grad_(True)
+    idx = torch.randint(0, 1000, (257, 3), device=gpu)
+    idx[0, 0] = idx[1, 1]  # duplicate ids must accumulate
+    out = embedding(idx, table, compute_dtype=dt)
+    ref = F.embedding(idx, table.detach())
+    assert out.shape == (257, 3, D) and nrel(out, ref) < (1e-7 if dt == torch.float32 else 1e-2)
+    g = torch.randn(out.shape, device=gpu)
+    out.backward(g.to(out.dtype))
+    tr = table.detach().clone().requires_grad_(True)
+    F.embedding(idx, tr).backward(g)
+    assert nrel(table.grad, tr.grad) < (1e-6 if dt == torch.float32 else 1e-2)
+
+
+KERAS_GPU_CASES = ["Dense", "Convolution2D", "Convolution1D", "AtrousConvolution2D", "Deconvolution2D",
+                   "BatchNormalization", "LayerNorm", "Embedding", "LSTM", "GRU", "MaxPooling2D",
+                   "GlobalAveragePooling2D", "TimeDistributed", "Highway"]
+
+
+@pytest.mark.parametrize("name", KERAS_GPU_CASES)
+def test_keras_layer_gpu_matches_cpu(gpu, name):
+    """Same weights, GPU (native kernels, bf16 compute) vs CPU (fp32 reference)."""
+    from test_keras_layers import CASES, _input
+    from zoo.pipeline.api.keras.engine.topology import Sequential
+    case = CASES[name]
+    torch.manual_seed(0)
+    m = Sequential()
+    l = case[0]()
+    l._given_input_shape = case[1]
+    m.add(l)
+    m.eval()
+    x = _input(case[1], case[2] if len(case) > 2 else None, batch=16)
+    y_cpu = m(x)
+    m_gpu = m.to(gpu)
+    y_gpu = m_gpu(x.to(gpu))
+    assert y_gpu.is_cuda
+    assert nrel(y_gpu.float().cpu(), y_cpu.float()) < 2e-2, name
+
+
+def test_tf_ordering_conv_bn_pool_runs_native(gpu):
+    """Channels-last Keras conv/BN/pool/GAP stack on the GPU trains through the native path."""
+    from zoo.pipeline.api.keras import layers as L
+    from zoo.pipeline.api.keras.models import Sequential
+    from zoo.common.nncontext import init_nncontext
+    init_nncontext()
+    m = Sequential()
+    m.add(L.Convolution2D(16, 3, 3, border_mode="same", dim_ordering="tf", input_shape=(16, 16, 8)))
+    m.add(L.BatchNormalization(dim_ordering="tf"))
+    m.add(L.Activation("relu"))
+    m.add(L.MaxPooling2D((2, 2), dim_ordering="tf"))
+    m.add(L.GlobalAveragePooling2D(dim_ordering="tf"))
+    m.add(L.Dense(8, activation="softmax"))
+    m.compile("adam", "sparse_categorical_crossentropy", ["accuracy"])
+    y = torch.randint(0, 2, (256,)) * 3
+    x = torch.randn(256, 16, 16, 8)
+    x[y == 3, :, :, 0] += 1.0  # class 3 has a bright channel 0
+    m.fit(x.numpy(), y.numpy(), batch_size=64, nb_epoch=15)
+    acc = m.evaluate(x.numpy(), y.numpy(), batch_size=64)[0]
+    assert acc > 0.8, acc
