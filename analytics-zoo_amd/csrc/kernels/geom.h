@@ -1,0 +1,46 @@
+// Geometry structs shared by the HIP kernels and the host binding layer.
+#pragma once
+
+namespace zoo {
+
+// Implicit-GEMM conv / GEMM geometry (igemm.hip).
+struct ConvGeom {
+  int N, H, W, C;        // input activation, NHWC
+  int K;                 // output channels (GEMM N dimension)
+  int R, S;              // filter
+  int P, Q;              // output spatial (GEMM rows = N*P*Q)
+  int sh, sw, ph, pw;    // stride / padding (in the possibly-dilated input space)
+  int dh, dw;            // filter dilation
+  int lh, lw;            // input dilation (1 = plain conv; >1 = transposed conv)
+  int M;                 // N*P*Q
+  int Ktot;              // R*S*C (logical reduction length)
+  int ldb;               // leading dim of the weight matrix (>= Ktot, %8 == 0)
+  // optional output-row remap (strided scatter into a larger NHWC tensor):
+  // row (n,p,q) -> ((n*oH + oh0 + osh*p)*oW + ow0 + osw*q)*K
+  int omap, oH, oW, osh, osw, oh0, ow0;
+};
+
+// Fused BatchNorm-backward statistics in a dgrad epilogue: the conv computing
+// dL/dz of a conv->BN->ReLU unit writes dy = dz * [z > 0] instead of dz and
+// accumulates sums[c] += dy, sums[K + c] += dy * (y - mean[c]) * inv[c].
+struct BwdStats {
+  const void* z;      // ReLU output of the producing unit (nullptr: no ReLU mask)
+  const void* y;      // its pre-BN conv output
+  const float* mean;
+  const float* inv;
+  float* sums;        // [2*K]
+};
+
+// Weight-gradient geometry (wgrad.hip).
+struct WgradGeom {
+  int N, H, W, C;      // input activation (NHWC)
+  int K;               // output channels
+  int R, S, P, Q;
+  int sh, sw, ph, pw, dh, dw;
+  int M;               // N*P*Q (reduction length)
+  int Ktot;            // R*S*C (GEMM columns)
+  int ldw;             // leading dim of dW (>= Ktot)
+  int m_per_split;     // multiple of 64
+};
+
+}  // namespace zoo

@@ -20,21 +20,11 @@
 // store is a full 16-byte row segment, and optionally fuses bias, residual add,
 // activation and per-channel BatchNorm statistics (sum, sum of squares).
 #include "common.h"
+#include "geom.h"
 
 namespace zoo {
 
-struct ConvGeom {
-  int N, H, W, C;        // input activation, NHWC
-  int K;                 // output channels (GEMM N dimension)
-  int R, S;              // filter
-  int P, Q;              // output spatial
-  int sh, sw, ph, pw;    // stride / padding (in the possibly-dilated input space)
-  int dh, dw;            // filter dilation
-  int lh, lw;            // input dilation (1 = plain conv; >1 = transposed conv)
-  int M;                 // N*P*Q
-  int Ktot;              // R*S*C (logical reduction length)
-  int ldb;               // leading dim of the weight matrix (>= Ktot, %8 == 0)
-};
+
 
 constexpr int IG_BM = 128, IG_BK = 64, IG_NT = 256;
 
@@ -44,7 +34,7 @@ template <int VEC, bool IS1x1, bool LDIL, int BN>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y,
     float* __restrict__ Yf, const float* __restrict__ bias, const bf16_t* __restrict__ resid,
-    float* __restrict__ stats, ConvGeom g, int act) {
+    float* __restrict__ stats, ConvGeom g, int act, BwdStats bs) {
   constexpr int BM = IG_BM, BK = IG_BK;
   constexpr int WN = BN / 2;      // wave tile width
   constexpr int NJ = WN / 16;     // 16-wide n tiles per wave
@@ -257,7 +247,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     const float4 hi = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8 + 4);
     v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
     v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
-    const size_t off = (size_t)m * g.K + col0;
+    size_t off;
+    if (g.omap) {
+      const int n = m / PQ, pq = m - (m / PQ) * PQ;
+      const int p = pq / g.Q, q = pq - (pq / g.Q) * g.Q;
+      off = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
+    } else {
+      off = (size_t)m * g.K + col0;
+    }
     if (resid) {
       float rv[8];
       unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
@@ -270,6 +267,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
       *reinterpret_cast<float4*>(Yf + off) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(Yf + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
     }
+    if (bs.sums) {  // fused BN-backward: mask with the producer's ReLU, accumulate (dy, dy*xhat)
+      if (bs.z) {
+        float zz[8];
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+      }
+    }
     if (Y) {
       const uint4 pk = pack8(v);
       *reinterpret_cast<uint4*>(Y + off) = pk;
@@ -278,11 +283,21 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
         unpack8(pk, q);
 #pragma unroll
         for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
+      } else if (bs.sums) {
+        float q[8], yy[8];
+        unpack8(pk, q);
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += q[e];
+          s2[e] += q[e] * (yy[e] - bs.mean[col0 + e]) * bs.inv[col0 + e];
+        }
       }
     }
   }
 
-  if (stats) {
+  float* const sacc = stats ? stats : bs.sums;
+  if (sacc) {
     // threads sharing a column chunk: tid % CPR equal. Reduce within the wave
     // (lanes differing in bits >= log2(CPR)), then across waves through LDS.
     __syncthreads();
@@ -309,24 +324,27 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
-        atomicAdd(stats + col, a);
-        atomicAdd(stats + g.K + col, b);
+        atomicAdd(sacc + col, a);
+        atomicAdd(sacc + g.K + col, b);
       }
     }
   }
 }
 
-// Wt[c][r][s][k] = W[k][R-1-r][S-1-s][c]  (dgrad weights for the transposed conv)
-__global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt,
-                                    int K, int R, int S, int C) {
-  const int total = K * R * S * C;
+// Wt[c][t][u][k] = W[k][r0 + sh*(Ra-1-t)][s0 + sw*(Sb-1-u)][c]
+// (flipped sub-filter of one output-parity class of a strided conv's dgrad;
+//  r0=s0=0, sh=sw=1, Ra=R, Sb=S is the plain flipped filter). W rows have leading dim ldw.
+__global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __restrict__ Wt, int K, int R, int S,
+                                    int C, int ldw, int r0, int s0, int Ra, int Sb, int sh, int sw, int ldt) {
+  const int total = C * Ra * Sb * K;
   for (int idx = blockIdx.x * blockDim.x + threadIdx.x; idx < total; idx += gridDim.x * blockDim.x) {
     int t = idx;
     const int k = t % K; t /= K;
-    const int s = t % S; t /= S;
-    const int r = t % R; t /= R;
+    const int u = t % Sb; t /= Sb;
+    const int v = t % Ra; t /= Ra;
     const int c = t;
-    Wt[idx] = W[((k * R + (R - 1 - r)) * S + (S - 1 - s)) * C + c];
+    const int r = r0 + sh * (Ra - 1 - v), s = s0 + sw * (Sb - 1 - u);
+    Wt[(size_t)c * ldt + (v * Sb + u) * K + k] = W[(size_t)k * ldw + (r * S + s) * C + c];
   }
 }
 
@@ -338,7 +356,7 @@ size_t igemm_smem_bytes(int BN) {
 
 template <int VEC, bool IS1x1, bool LDIL, int BN>
 static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
-                            const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                            const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                             hipStream_t st) {
   const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
   const size_t smem = igemm_smem_bytes(BN);
@@ -349,20 +367,20 @@ static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* 
     attr_set = true;
   }
   hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
-                     Yf, bias, resid, stats, g, act);
+                     Yf, bias, resid, stats, g, act, bs);
   return hipGetLastError();
 }
 
 template <int VEC, bool IS1x1, bool LDIL>
 static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
-                               const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                               const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                                hipStream_t st) {
   // narrow output-channel counts waste half of a 128-wide tile: use BN=64 there
-  if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, st);
+  if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   const long tiles128 = (long)((g.M + IG_BM - 1) / IG_BM) * ((g.K + 127) / 128);
   if (tiles128 < 512)  // not enough workgroups to fill 256 CUs twice -> smaller tiles
-    return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, st);
-  return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, st);
+    return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 
 }  // namespace zoo
@@ -370,8 +388,9 @@ static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, floa
 using namespace zoo;
 
 extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
-                                const void* resid, float* stats, const ConvGeom* g, int act,
+                                const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
+  BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
   bf16_t* y = (bf16_t*)Y;
@@ -379,17 +398,17 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
   const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
                      g->lh == 1 && g->lw == 1 && g->H == g->P && g->W == g->Q;
   const bool ldil = g->lh > 1 || g->lw > 1;
-  if (g->C == 4) return launch_ig_bn<4, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
-  if (is1x1) return launch_ig_bn<8, true, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
-  if (ldil) return launch_ig_bn<8, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, st);
-  return launch_ig_bn<8, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, st);
+  if (g->C == 4) return launch_ig_bn<4, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  if (is1x1) return launch_ig_bn<8, true, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  if (ldil) return launch_ig_bn<8, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  return launch_ig_bn<8, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
 }
 
-extern "C" hipError_t zoo_flip_weights(const void* W, void* Wt, int K, int R, int S, int C,
-                                       hipStream_t st) {
-  const int total = K * R * S * C;
+extern "C" hipError_t zoo_flip_weights(const void* W, void* Wt, int K, int R, int S, int C, int ldw, int r0,
+                                       int s0, int Ra, int Sb, int sh, int sw, int ldt, hipStream_t st) {
+  const int total = C * Ra * Sb * K;
   const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
-  hipLaunchKernelGGL(flip_weights_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)W, (bf16_t*)Wt, K,
-                     R, S, C);
+  hipLaunchKernelGGL(flip_weights_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const bf16_t*)W,
+                     (bf16_t*)Wt, K, R, S, C, ldw, r0, s0, Ra, Sb, sh, sw, ldt);
   return hipGetLastError();
 }

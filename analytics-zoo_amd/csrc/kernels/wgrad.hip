@@ -16,19 +16,11 @@
 // Reference parity: the weight-gradient half of BigDL SpatialConvolution /
 // Linear accGradParameters.
 #include "common.h"
+#include "geom.h"
 
 namespace zoo {
 
-struct WgradGeom {
-  int N, H, W, C;      // input activation (NHWC)
-  int K;               // output channels
-  int R, S, P, Q;
-  int sh, sw, ph, pw, dh, dw;
-  int M;               // N*P*Q (reduction length)
-  int Ktot;            // R*S*C (GEMM columns)
-  int ldw;             // leading dim of dW (>= Ktot)
-  int m_per_split;     // multiple of 64
-};
+
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 64;
 

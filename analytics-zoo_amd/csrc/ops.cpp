@@ -9,22 +9,17 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
-namespace zoo {
-struct ConvGeom {
-  int N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, lh, lw, M, Ktot, ldb;
-};
-struct WgradGeom {
-  int N, H, W, C, K, R, S, P, Q, sh, sw, ph, pw, dh, dw, M, Ktot, ldw, m_per_split;
-};
-}  // namespace zoo
+#include "kernels/geom.h"
 
 using zoo::ConvGeom;
 using zoo::WgradGeom;
+using zoo::BwdStats;
 
 extern "C" {
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
-                     hipStream_t);
-hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, hipStream_t);
+                     const zoo::BwdStats*, hipStream_t);
+hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
+                            hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, const WgradGeom*, hipStream_t);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int,
                          hipStream_t);
@@ -98,7 +93,10 @@ ConvGeom make_geom(const torch::Tensor& x, int K, int R, int S, int sh, int sw, 
 torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
                        int lh, int lw, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> stats, int act, bool out_f32, bool out_bf16, int out_h,
-                       int out_w) {
+                       int out_w, c10::optional<torch::Tensor> out, std::vector<int64_t> omap,
+                       c10::optional<torch::Tensor> bz, c10::optional<torch::Tensor> by,
+                       c10::optional<torch::Tensor> bmean, c10::optional<torch::Tensor> binv,
+                       c10::optional<torch::Tensor> bsums) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -111,9 +109,20 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   ConvGeom g = make_geom(x, K, R, S, sh, sw, ph, pw, dh, dw, lh, lw, ldb);
   // transposed convs (dgrad) may need one extra output row/col (asymmetric padding):
   // the loader zero-fills taps that fall outside the input, so a larger P/Q is safe.
-  if (out_h > 0) { TORCH_CHECK(out_h >= g.P && out_h <= g.P + sh, "conv_fwd: out_h"); g.P = out_h; }
-  if (out_w > 0) { TORCH_CHECK(out_w >= g.Q && out_w <= g.Q + sw, "conv_fwd: out_w"); g.Q = out_w; }
+  if (out_h > 0) { TORCH_CHECK(out_h <= g.P + sh, "conv_fwd: out_h"); g.P = out_h; }
+  if (out_w > 0) { TORCH_CHECK(out_w <= g.Q + sw, "conv_fwd: out_w"); g.Q = out_w; }
   g.M = g.N * g.P * g.Q;
+  g.omap = 0; g.oH = g.P; g.oW = g.Q; g.osh = 1; g.osw = 1; g.oh0 = 0; g.ow0 = 0;
+  if (!omap.empty()) {
+    // omap = {oH, oW, osh, osw, oh0, ow0}: write row (n,p,q) to (n, oh0+osh*p, ow0+osw*q) of [N,oH,oW,K]
+    TORCH_CHECK(omap.size() == 6, "conv_fwd: omap needs 6 entries");
+    g.omap = 1; g.oH = omap[0]; g.oW = omap[1]; g.osh = omap[2]; g.osw = omap[3]; g.oh0 = omap[4]; g.ow0 = omap[5];
+    TORCH_CHECK(g.osh >= 1 && g.osw >= 1 && g.oh0 >= 0 && g.ow0 >= 0 &&
+                g.oh0 + g.osh * (g.P - 1) < g.oH && g.ow0 + g.osw * (g.Q - 1) < g.oW,
+                "conv_fwd: omap writes outside the output");
+    TORCH_CHECK(out.has_value() && out->defined(), "conv_fwd: omap requires an explicit output tensor");
+    TORCH_CHECK(!stats.has_value() || !stats->defined(), "conv_fwd: omap does not support stats");
+  }
   TORCH_CHECK(g.P > 0 && g.Q > 0, "conv_fwd: empty output");
   TORCH_CHECK((int64_t)g.N * g.H * g.W * g.C < (1LL << 31) && (int64_t)g.M * K < (1LL << 31),
               "conv_fwd: tensor too large for 32-bit indexing");
@@ -126,7 +135,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   const void* rp = nullptr;
   if (resid.has_value() && resid->defined()) {
     req(*resid, at::kBFloat16, "resid");
-    TORCH_CHECK(resid->numel() == (int64_t)g.M * K, "resid size mismatch");
+    TORCH_CHECK(resid->numel() == (g.omap ? (int64_t)g.N * g.oH * g.oW * K : (int64_t)g.M * K),
+                "resid size mismatch");
     rp = resid->data_ptr();
   }
   float* sp = nullptr;
@@ -136,20 +146,59 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     TORCH_CHECK(out_bf16, "stats require the bf16 output");
     sp = stats->data_ptr<float>();
   }
+  BwdStats bs{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (bsums.has_value() && bsums->defined()) {
+    req(*bsums, at::kFloat, "bn sums");
+    TORCH_CHECK(bsums->numel() == 2 * K, "bn sums must be [2*K]");
+    TORCH_CHECK(by.has_value() && bmean.has_value() && binv.has_value(), "fused bn-backward needs y/mean/inv");
+    req(*by, at::kBFloat16, "bn y");
+    req(*bmean, at::kFloat, "bn mean");
+    req(*binv, at::kFloat, "bn inv");
+    TORCH_CHECK(bmean->numel() == K && binv->numel() == K, "bn mean/inv must be [K]");
+    const int64_t full = g.omap ? (int64_t)g.N * g.oH * g.oW * K : (int64_t)g.M * K;
+    TORCH_CHECK(by->numel() == full, "bn y must match the output");
+    if (bz.has_value() && bz->defined()) {
+      req(*bz, at::kBFloat16, "bn z");
+      TORCH_CHECK(bz->numel() == full, "bn z must match the output");
+      bs.z = bz->data_ptr();
+    }
+    TORCH_CHECK(!stats.has_value() || !stats->defined(), "stats and fused bn-backward are exclusive");
+    TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
+    bs.y = by->data_ptr();
+    bs.mean = bmean->data_ptr<float>();
+    bs.inv = binv->data_ptr<float>();
+    bs.sums = bsums->data_ptr<float>();
+  }
   torch::Tensor y, yf;
-  if (out_bf16) y = torch::empty({g.N, g.P, g.Q, K}, x.options());
+  if (out.has_value() && out->defined()) {
+    TORCH_CHECK(out_bf16 && !out_f32, "conv_fwd: explicit output must be bf16");
+    req(*out, at::kBFloat16, "out");
+    TORCH_CHECK(out->dim() == 4 && out->size(0) == g.N && out->size(1) == g.oH && out->size(2) == g.oW &&
+                    out->size(3) == K, "conv_fwd: explicit output shape mismatch");
+    y = *out;
+  } else {
+    if (out_bf16) y = torch::empty({g.N, g.P, g.Q, K}, x.options());
+  }
   if (out_f32) yf = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(at::kFloat));
   check_hip(zoo_igemm(x.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
-                      out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, cur_stream()),
+                      out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, &bs, cur_stream()),
             "igemm");
   return out_bf16 ? y : yf;
 }
 
-torch::Tensor flip_weights(torch::Tensor w, int K, int R, int S, int C) {
+// w: [K, ldw] packed rows of [R][S][C]; returns [C, ceil8(Ra*Sb*K)] flipped sub-filter
+// Wt[c][t][u][k] = W[k][r0 + sh*(Ra-1-t)][s0 + sw*(Sb-1-u)][c]
+torch::Tensor flip_weights(torch::Tensor w, int K, int R, int S, int C, int r0, int s0, int Ra, int Sb, int sh,
+                           int sw) {
   req(w, at::kBFloat16, "w");
-  TORCH_CHECK(w.numel() == (int64_t)K * R * S * C, "flip_weights: size mismatch");
-  auto wt = torch::empty({C, R * S * K}, w.options());
-  check_hip(zoo_flip_weights(w.data_ptr(), wt.data_ptr(), K, R, S, C, cur_stream()), "flip_weights");
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == K && w.size(1) >= R * S * C, "flip_weights: w must be [K, >=R*S*C]");
+  TORCH_CHECK(Ra >= 1 && Sb >= 1 && r0 >= 0 && s0 >= 0 && sh >= 1 && sw >= 1 && r0 + sh * (Ra - 1) < R &&
+                  s0 + sw * (Sb - 1) < S, "flip_weights: sub-filter outside the filter");
+  const int ldt = (Ra * Sb * K + 7) / 8 * 8;
+  auto wt = (ldt == Ra * Sb * K) ? torch::empty({C, ldt}, w.options()) : torch::zeros({C, ldt}, w.options());
+  check_hip(zoo_flip_weights(w.data_ptr(), wt.data_ptr(), K, R, S, C, (int)w.size(1), r0, s0, Ra, Sb, sh, sw, ldt,
+                             cur_stream()),
+            "flip_weights");
   return wt;
 }
 

@@ -83,17 +83,17 @@ def check_one(N, H, Cin, Cout, R, st, pad, dev, do_time=True):
     res = {"shape": [N, H, Cin, Cout, R, st, pad]}
 
     stats = torch.zeros(2 * Cout, device=dev)
-    y = C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0)
+    y = C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0, None, [], None, None, None, None, None)
     yref = yr.detach().permute(0, 2, 3, 1)
     res["fwd_err"] = rel_err(y, yref)
     s_ref = torch.stack([y.float().sum((0, 1, 2)), (y.float() ** 2).sum((0, 1, 2))]).flatten()
     res["stats_err"] = rel_err(stats, s_ref)
 
     # dgrad: transposed conv with flipped weights
-    wt = C.flip_weights(w4.contiguous(), Cout, R, R, Cin)
+    wt = C.flip_weights(w4.reshape(Cout, -1).contiguous(), Cout, R, R, Cin, 0, 0, R, R, 1, 1)
     if Cin != 4:  # the stem's input never needs a gradient
         dx = C.conv_fwd(dy, wt, R, R, 1, 1, R - 1 - pad, R - 1 - pad, 1, 1, st, st, None, None, None, 0, False, True,
-                        H, H)
+                        H, H, None, [], None, None, None, None, None)
         res["dgrad_err"] = rel_err(dx, xr.grad.permute(0, 2, 3, 1))
     dw = torch.zeros(Cout, ktot, device=dev)
     C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, 1, 1)
@@ -101,9 +101,9 @@ def check_one(N, H, Cin, Cout, R, st, pad, dev, do_time=True):
 
     if do_time:
         flops = 2.0 * N * P * P * Cout * ktot
-        t_f = timeit(lambda: C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0))
+        t_f = timeit(lambda: C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0, None, [], None, None, None, None, None))
         t_d = timeit(lambda: C.conv_fwd(dy, wt, R, R, 1, 1, R - 1 - pad, R - 1 - pad, 1, 1, st, st, None, None, None, 0,
-                                        False, True, H, H)) if Cin != 4 else float("nan")
+                                        False, True, H, H, None, [], None, None, None, None, None)) if Cin != 4 else float("nan")
         t_w = timeit(lambda: (dw.zero_(), C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, 1, 1)))
         xt = x.permute(0, 3, 1, 2)  # channels_last view
         wt4 = w4.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)

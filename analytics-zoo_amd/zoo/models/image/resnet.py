@@ -15,6 +15,7 @@ import torch
 import torch.nn as nn
 
 from zoo import ops
+from zoo.ops.bn import BNProducer, GradHandoff
 
 
 class ConvBN(nn.Module):
@@ -33,11 +34,25 @@ class ConvBN(nn.Module):
         self.register_buffer("running_mean", torch.zeros(cout))
         self.register_buffer("running_var", torch.ones(cout))
 
-    def forward(self, x, resid=None):
+    def forward(self, x, resid=None, resid_handoff=None, grad_add=None, producer_in=None, producer_out=None):
         return ops.conv_bn_act(x, self.weight, self.gamma, self.beta, self.running_mean, self.running_var,
                                kernel=(self.k, self.k), stride=(self.stride, self.stride),
                                pad=(self.pad, self.pad), eps=self.eps, momentum=self.momentum, relu=self.relu,
-                               resid=resid, training=self.training)
+                               resid=resid, training=self.training, resid_handoff=resid_handoff, grad_add=grad_add,
+                               producer_in=producer_in, producer_out=producer_out)
+
+
+# cross-unit BN-backward fusion (BNProducer); the switch exists for A/B numerics tests
+FUSE_BN_BACKWARD = True
+
+
+def _bp():
+    return BNProducer(None, None, None, None) if FUSE_BN_BACKWARD else None
+
+
+def _fusing(x):
+    """Cross-unit backward fusion applies to GPU training with autograd on."""
+    return x.is_cuda and torch.is_grad_enabled()
 
 
 class Bottleneck(nn.Module):
@@ -51,11 +66,24 @@ class Bottleneck(nn.Module):
         self.conv3 = ConvBN(width, cout, 1, relu=True, zero_gamma=False)
         self.down = ConvBN(cin, cout, 1, stride=stride, relu=False) if (stride != 1 or cin != cout) else None
 
-    def forward(self, x):
-        sc = self.down(x) if self.down is not None else x
-        h = self.conv1(x)
-        h = self.conv2(h)
-        return self.conv3(h, resid=sc)
+    def forward(self, x, prod=None):
+        """``prod``: BNProducer of ``x`` (the previous block's last unit). Returns
+        (out, BNProducer of out) when fusing, else out."""
+        if not (self.training and _fusing(x)):
+            sc = self.down(x) if self.down is not None else x
+            return self.conv3(self.conv2(self.conv1(x)), resid=sc)
+        p1, p2, p3 = _bp(), _bp(), _bp()
+        if self.down is None:
+            # identity shortcut: conv3's residual gradient is added in conv1's dgrad epilogue, which makes
+            # conv1 the sole consumer of x -> it also fuses the previous block's BN-backward reduction
+            ho = GradHandoff()
+            h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
+            h = self.conv2(h, producer_in=p1, producer_out=p2)
+            return self.conv3(h, resid=x, resid_handoff=ho, producer_in=p2, producer_out=p3), p3
+        sc = self.down(x)
+        h = self.conv1(x, producer_out=p1)  # x also feeds `down`: no producer fusion across this edge
+        h = self.conv2(h, producer_in=p1, producer_out=p2)
+        return self.conv3(h, resid=sc, producer_in=p2, producer_out=p3), p3
 
 
 class BasicBlock(nn.Module):
@@ -67,9 +95,18 @@ class BasicBlock(nn.Module):
         self.conv2 = ConvBN(width, width, 3, pad=1, relu=True)
         self.down = ConvBN(cin, width, 1, stride=stride, relu=False) if (stride != 1 or cin != width) else None
 
-    def forward(self, x):
-        sc = self.down(x) if self.down is not None else x
-        return self.conv2(self.conv1(x), resid=sc)
+    def forward(self, x, prod=None):
+        if not (self.training and _fusing(x)):
+            sc = self.down(x) if self.down is not None else x
+            return self.conv2(self.conv1(x), resid=sc)
+        p1, p2 = _bp(), _bp()
+        if self.down is None:
+            ho = GradHandoff()
+            h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
+            return self.conv2(h, resid=x, resid_handoff=ho, producer_in=p1, producer_out=p2), p2
+        sc = self.down(x)
+        h = self.conv1(x, producer_out=p1)
+        return self.conv2(h, resid=sc, producer_in=p1, producer_out=p2), p2
 
 
 class Dense(nn.Module):
@@ -129,7 +166,13 @@ class ResNet(nn.Module):
         x = self.to_nhwc(x)
         x = self.stem(x)
         x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
-        x = self.stages(x)
+        if self.training and _fusing(x):
+            prod = None
+            for stage in self.stages:
+                for blk in stage:
+                    x, prod = blk(x, prod)
+        else:
+            x = self.stages(x)
         x = ops.global_avg_pool_nhwc(x)
         return self.fc(x)
 

@@ -6,7 +6,7 @@ suite and as numerics oracles).
 """
 from zoo.ops._native import native, available
 from zoo.ops.conv import conv2d_nhwc, linear, pack_weight, unpack_weight, ceil8, conv_out_size
-from zoo.ops.bn import conv_bn_act, batch_norm_nhwc
+from zoo.ops.bn import conv_bn_act, batch_norm_nhwc, GradHandoff, BNProducer
 from zoo.ops.pool import max_pool2d_nhwc, global_avg_pool_nhwc
 from zoo.ops.loss import softmax_cross_entropy
 from zoo.ops.nn import layer_norm, embedding

@@ -1,0 +1,81 @@
+"""Thin keyword wrappers over the raw ``zoo._C`` conv entry points, plus the
+convolution data-gradient driver.
+
+``conv_dgrad`` computes dX of an NHWC conv:
+  * stride 1: ONE transposed-conv launch (flipped filter, pad R-1-p).
+  * stride s > 1: the transposed conv would waste (s^2-1)/s^2 of the MFMA work
+    on zero-inserted rows, so the output is split into its s_h x s_w parity
+    classes; each class is a stride-1 conv of dY with a flipped SUB-filter
+    (the taps r = r0 + s*t that reach that class), written straight to its
+    strided output positions by the igemm epilogue's row remap. Classes no
+    tap reaches are zero.
+"""
+import math
+
+import torch
+
+from zoo.ops._native import native
+
+
+def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
+             act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None):
+    """``bstats = (z or None, y, mean, inv, sums)`` fuses the producing unit's
+    BN-backward reduction (and ReLU mask) into this conv's epilogue."""
+    bz = by = bm = bi = bsum = None
+    if bstats is not None:
+        bz, by, bm, bi, bsum = bstats
+    return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
+                             bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
+                             list(omap) if omap else [], bz, by, bm, bi, bsum)
+
+
+def flip_weights(w, K, R, S, C, r0=0, s0=0, Ra=None, Sb=None, sh=1, sw=1):
+    return native().flip_weights(w, K, R, S, C, r0, s0, Ra or R, Sb or S, sh, sw)
+
+
+def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None):
+    """dX [N,H,W,C] of y = conv(x, w) given dY [N,P,Q,K] and the bf16 packed weight.
+    ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer)."""
+    sh, sw = stride
+    if (sh, sw) == (1, 1) or dil != (1, 1):
+        wt = flip_weights(wb, K, R, S, C)
+        return conv_fwd(dy, wt, R, S, (1, 1), (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1]), dil, stride,
+                        resid=resid, out_hw=(H, W), bstats=bstats)
+    N = dy.shape[0]
+    classes = []
+    for a in range(sh):
+        r0 = (a + pad[0]) % sh
+        Ra = (R - r0 + sh - 1) // sh
+        Ha = len(range(a, H, sh))
+        for b in range(sw):
+            s0 = (b + pad[1]) % sw
+            Sb = (S - s0 + sw - 1) // sw
+            Wb = len(range(b, W, sw))
+            if Ha == 0 or Wb == 0:
+                continue
+            classes.append((a, b, r0, s0, Ra, Sb, Ha, Wb))
+    full = all(c[4] > 0 and c[5] > 0 for c in classes) and len(classes) == sh * sw
+    if bstats is not None and resid is not None and not full:
+        raise NotImplementedError("fused bn-backward with zero parity classes and a residual")
+    if resid is not None:
+        dx = resid.clone() if not full else torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    else:
+        dx = (torch.empty if full else torch.zeros)(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+    for (a, b, r0, s0, Ra, Sb, Ha, Wb) in classes:
+        if Ra <= 0 or Sb <= 0:
+            continue
+        ca = (a + pad[0] - r0) // sh
+        cb = (b + pad[1] - s0) // sw
+        pa, pb = Ra - 1 - ca, Sb - 1 - cb
+        if pa < 0 or pb < 0:  # unusual geometry: fall back to the dilated transposed conv
+            wt = flip_weights(wb, K, R, S, C)
+            return conv_fwd(dy, wt, R, S, (1, 1), (R - 1 - pad[0], S - 1 - pad[1]), (1, 1), stride, resid=resid,
+                            out_hw=(H, W), bstats=bstats)
+        wt = flip_weights(wb, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+        # with zero classes dx starts as a copy of resid and is updated in place
+        # (the epilogue reads and writes each element from the same lane)
+        add = None if resid is None else (resid if full else dx)
+        conv_fwd(dy, wt, Ra, Sb, (1, 1), (pa, pb), (1, 1), (1, 1), resid=add, out_hw=(Ha, Wb), out=dx,
+                 omap=(H, W, sh, sw, a, b), bstats=bstats)
+    # (with bstats, positions no tap reaches stay 0: dy = 0 there and they add nothing to the sums)
+    return dx

@@ -19,6 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
+from zoo.ops import _kern, workspace
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
 
 
@@ -35,16 +36,47 @@ def _grad_target(p):
     return torch.zeros(p.shape, dtype=torch.float32, device=p.device), False
 
 
+class GradHandoff:
+    """Carries the residual-branch gradient of a bottleneck's last conv to the
+    block's FIRST conv, whose dgrad epilogue adds it (identity shortcut: both
+    consume the block input). Replaces autograd's separate add kernel."""
+
+    __slots__ = ("grad",)
+
+    def __init__(self):
+        self.grad = None
+
+
+class BNProducer:
+    """Handle attached to a conv->BN->ReLU unit's output. The single consumer
+    conv of that output fuses this unit's BN-backward reduction (sum dy,
+    sum dy*xhat) and ReLU mask into its dgrad epilogue (igemm BwdStats) and
+    marks ``fused``; this unit's backward then skips its reduction pass."""
+
+    __slots__ = ("z", "y", "mean", "inv", "sums", "fused")
+
+    def __init__(self, z, y, mean, inv):
+        self.z, self.y, self.mean, self.inv = z, y, mean, inv
+        self.sums = None
+        self.fused = False
+
+    def bstats(self):
+        self.sums = workspace.zeros(2 * self.y.shape[-1], self.y.device)
+        self.fused = True
+        return (self.z, self.y, self.mean, self.inv, self.sums)
+
+
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
-                relu, training):
+                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None):
         C_ = native()
         K = w.shape[0]
+        ctx.handoff_out, ctx.handoff_in = handoff_out, handoff_in
+        ctx.producer_in = producer_in
         wb = bf16_weight(w)
-        stats = torch.zeros(2 * K, device=x.device, dtype=torch.float32) if training else None
-        y = C_.conv_fwd(x, wb, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1, 1, 1, None, None, stats, 0,
-                        False, True, 0, 0)
+        stats = workspace.zeros(2 * K, x.device) if training else None
+        y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
         smean = torch.empty(K, device=x.device, dtype=torch.float32)
         sinv = torch.empty(K, device=x.device, dtype=torch.float32)
         z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
@@ -52,6 +84,9 @@ class _ConvBNActFn(torch.autograd.Function):
                             training)
         ctx.save_for_backward(x, w, gamma, y, z if relu else None, smean, sinv)
         ctx.meta = (R, S, stride, pad, relu, resid is not None, x.shape)
+        ctx.producer_out = producer_out
+        if producer_out is not None:
+            producer_out.z, producer_out.y, producer_out.mean, producer_out.inv = (z if relu else None), y, smean, sinv
         return z
 
     @staticmethod
@@ -64,20 +99,37 @@ class _ConvBNActFn(torch.autograd.Function):
             dz = dz.to(torch.bfloat16)
         K = w.shape[0]
         Cin = xshape[3]
-        sums = torch.zeros(2 * K, device=dz.device, dtype=torch.float32)
-        C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
         dgam, own_g = _grad_target(gamma)
         dbet, own_b = _grad_target(ctx.beta_ref) if hasattr(ctx, "beta_ref") else (None, False)
-        outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, has_resid, dgam, dbet)
-        dy = outs[0]
-        dresid = outs[1] if has_resid else None
+        po = ctx.producer_out
+        if po is not None and po.fused:
+            # dz arrived already ReLU-masked with its (dy, dy*xhat) sums from the consumer's epilogue
+            sums = po.sums
+            outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dgam, dbet)
+            dy = outs[0]
+            dresid = dz if has_resid else None
+            po.fused, po.sums = False, None
+        else:
+            sums = workspace.zeros(2 * K, dz.device)
+            C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
+            outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, has_resid, dgam, dbet)
+            dy = outs[0]
+            dresid = outs[1] if has_resid else None
+        if dresid is not None and ctx.handoff_out is not None:
+            ctx.handoff_out.grad = dresid   # consumed by the block's first conv (fused add)
+            dresid = None
         dx = None
         if ctx.needs_input_grad[0]:
-            wt = C_.flip_weights(bf16_weight(w)[:, : R * S * Cin].contiguous(), K, R, S, Cin)
-            if wt.shape[1] % 8:
-                wt = F.pad(wt, (0, ceil8(wt.shape[1]) - wt.shape[1]))
-            dx = C_.conv_fwd(dy, wt, R, S, 1, 1, R - 1 - pad[0], S - 1 - pad[1], 1, 1, stride[0], stride[1], None,
-                             None, None, 0, False, True, xshape[1], xshape[2])
+            add = None
+            if ctx.handoff_in is not None:
+                add = ctx.handoff_in.grad
+                ctx.handoff_in.grad = None
+                if add is None:
+                    raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
+            pin = ctx.producer_in
+            bst = pin.bstats() if (pin is not None and pin.y is not None) else None
+            dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, resid=add,
+                                  bstats=bst)
         gw, own_w = _grad_target(w)
         C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
         if own_w:
@@ -87,7 +139,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if own_b:
             _notify(ctx.beta_ref)
         return (dx, None if own_w else gw.to(w.dtype), None if own_g else dgam, None if own_b else dbet, dresid,
-                None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 class _ConvBNActFnB(_ConvBNActFn):
@@ -95,10 +147,11 @@ class _ConvBNActFnB(_ConvBNActFn):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
-                relu, training):
+                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None):
         ctx.beta_ref = beta
         return _ConvBNActFn.forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad,
-                                    eps, momentum, relu, training)
+                                    eps, momentum, relu, training, handoff_out, handoff_in, producer_in,
+                                    producer_out)
 
 
 def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
@@ -122,8 +175,17 @@ def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
 
 
 def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0),
-                eps=1e-5, momentum=0.1, relu=True, resid=None, training=True):
-    """z = relu?(BN(conv(x)) + resid) for NHWC input with a packed weight."""
+                eps=1e-5, momentum=0.1, relu=True, resid=None, training=True, resid_handoff=None, grad_add=None,
+                producer_in=None, producer_out=None):
+    """z = relu?(BN(conv(x)) + resid) for NHWC input with a packed weight.
+
+    ``resid_handoff``/``grad_add``: a shared :class:`GradHandoff` that routes the
+    residual gradient of the unit with ``resid`` into the dgrad epilogue of the
+    unit that consumes the same input first (GPU only).
+    ``producer_in``: the :class:`BNProducer` of the unit that produced ``x``,
+    when this unit is its ONLY consumer (fuses that unit's BN-backward
+    reduction into this unit's dgrad). ``producer_out``: a fresh BNProducer
+    to be filled for this unit's own output."""
     R, S = kernel
     if x.is_cuda:
         if x.dtype != torch.bfloat16:
@@ -132,7 +194,7 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
             resid = resid.to(torch.bfloat16).contiguous()
         return _ConvBNActFnB.apply(x.contiguous(), w, gamma, beta, resid, running_mean, running_var, R, S,
                                    tuple(stride), tuple(pad), float(eps), float(momentum), bool(relu),
-                                   bool(training))
+                                   bool(training), resid_handoff, grad_add, producer_in, producer_out)
     y = conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1)))
     z = bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training)
     if resid is not None:
@@ -149,7 +211,7 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, y, gamma, beta, resid, running_mean, running_var, eps, momentum, relu, training):
         C_ = native()
         K = y.shape[-1]
-        stats = torch.zeros(2 * K, device=y.device, dtype=torch.float32)
+        stats = workspace.zeros(2 * K, y.device)
         if training:
             C_.bn_reduce(y, None, None, None, None, stats, 0)
         smean = torch.empty(K, device=y.device, dtype=torch.float32)
@@ -166,7 +228,7 @@ class _BNActFn(torch.autograd.Function):
         y, gamma, beta, z, smean, sinv = ctx.saved_tensors
         dz = dz.contiguous().to(torch.bfloat16)
         K = y.shape[-1]
-        sums = torch.zeros(2 * K, device=dz.device, dtype=torch.float32)
+        sums = workspace.zeros(2 * K, dz.device)
         C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
         dgam, own_g = _grad_target(gamma)
         dbet, own_b = _grad_target(beta)

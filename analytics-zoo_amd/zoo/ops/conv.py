@@ -22,6 +22,7 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
+from zoo.ops import _kern
 
 ACT_CODES = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
 
@@ -89,11 +90,9 @@ class _Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, bias, R, S, stride, pad, dil, act, out_f32):
-        C_ = native()
         wb = bf16_weight(w)
-        y = C_.conv_fwd(x, wb, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], 1, 1,
-                        None if bias is None else bias.detach().float().contiguous(), None, None,
-                        ACT_CODES[act], out_f32, not out_f32, 0, 0)
+        y = _kern.conv_fwd(x, wb, R, S, stride, pad, dil, bias=None if bias is None else bias.detach().float().contiguous(),
+                           act=ACT_CODES[act], out_f32=out_f32, out_bf16=not out_f32)
         ctx.save_for_backward(x, w, y if act not in (None, "linear") else None)
         ctx.geom = (R, S, stride, pad, dil, act, x.shape, bias is not None)
         return y
@@ -119,11 +118,8 @@ class _Conv2dFn(torch.autograd.Function):
         Cin = xshape[3]
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            wt = C_.flip_weights(bf16_weight(w)[:, : R * S * Cin].contiguous(), K, R, S, Cin)
-            if wt.shape[1] % 8:
-                wt = F.pad(wt, (0, ceil8(wt.shape[1]) - wt.shape[1]))
-            dx = C_.conv_fwd(dyb, wt, R, S, 1, 1, dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1], dil[0],
-                             dil[1], stride[0], stride[1], None, None, None, 0, False, True, xshape[1], xshape[2])
+            dx = _kern.conv_dgrad(dyb, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, dil,
+                                  resid=getattr(ctx, "grad_add", None))
         if ctx.needs_input_grad[1]:
             gbuf = getattr(w, "_zoo_grad", None)
             target = gbuf if gbuf is not None else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
@@ -174,14 +170,8 @@ class _ConvTranspose2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wf, R, S, stride, pad, out_hw, cout):
-        C_ = native()
         cin = x.shape[3]
-        wfb = bf16_weight(wf)[:, : R * S * cout].contiguous()
-        wt = C_.flip_weights(wfb, cin, R, S, cout)
-        if wt.shape[1] % 8:
-            wt = F.pad(wt, (0, ceil8(wt.shape[1]) - wt.shape[1]))
-        y = C_.conv_fwd(x, wt, R, S, 1, 1, R - 1 - pad[0], S - 1 - pad[1], 1, 1, stride[0], stride[1], None, None,
-                        None, 0, False, True, out_hw[0], out_hw[1])
+        y = _kern.conv_dgrad(x, bf16_weight(wf), cin, R, S, cout, out_hw[0], out_hw[1], stride, pad)
         ctx.save_for_backward(x, wf)
         ctx.g = (R, S, stride, pad, cout)
         return y
@@ -194,8 +184,7 @@ class _ConvTranspose2dFn(torch.autograd.Function):
         dyb = dy.contiguous().to(torch.bfloat16)
         dx = dw = None
         if ctx.needs_input_grad[0]:
-            dx = C_.conv_fwd(dyb, bf16_weight(wf), R, S, stride[0], stride[1], pad[0], pad[1], 1, 1, 1, 1, None,
-                             None, None, 0, False, True, x.shape[1], x.shape[2])
+            dx = _kern.conv_fwd(dyb, bf16_weight(wf), R, S, stride, pad, out_hw=(x.shape[1], x.shape[2]))
         if ctx.needs_input_grad[1]:
             gw = torch.zeros(wf.shape, dtype=torch.float32, device=wf.device)
             C_.conv_wgrad(dyb, x, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)

@@ -31,6 +31,7 @@ import torch
 from zoo.common.triggers import EveryEpoch, MaxEpoch, Trigger
 from zoo.parallel.ddp import GradSync
 from zoo.parallel.flat import FlatParams
+from zoo.ops import workspace
 
 log = logging.getLogger("zoo.engine")
 
@@ -85,9 +86,13 @@ class TrainingEngine:
             raise InjectedFault("injected fault at iteration %d" % self.fault_step)
         self.model.train()
         self.flat.grad.zero_()
-        out = self.forward_fn(self.model, inputs)
-        loss = self.criterion(out, target)
-        loss.backward()
+        workspace.begin_step(self.device)
+        try:
+            out = self.forward_fn(self.model, inputs)
+            loss = self.criterion(out, target)
+            loss.backward()
+        finally:
+            workspace.end_step()
         self.sync.step(self.optim, self.clip)
         self.state["neval"] += 1
         return loss.detach()

@@ -50,7 +50,7 @@ def test_conv_fwd_dgrad_wgrad(gpu, shape):
     yr = F.conv2d(xr, wr, stride=st, padding=pad)
     P, Q = yr.shape[2], yr.shape[3]
     stats = torch.zeros(2 * Cout, device=gpu)
-    y = C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0)
+    y = C.conv_fwd(x, w2, R, R, st, st, pad, pad, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0, None, [], None, None, None, None, None)
     assert y.shape == (N, P, Q, Cout)
     assert rel(y, yr.detach().permute(0, 2, 3, 1)) < 1e-2
     yf = y.float()
@@ -65,9 +65,9 @@ def test_conv_fwd_dgrad_wgrad(gpu, shape):
     if dw.shape[1] > R * R * Cin:
         assert dw[:, R * R * Cin:].abs().max().item() == 0.0
     if Cin % 8 == 0:
-        wt = C.flip_weights(w4.contiguous(), Cout, R, R, Cin)
+        wt = C.flip_weights(w4.reshape(Cout, -1).contiguous(), Cout, R, R, Cin, 0, 0, R, R, 1, 1)
         dx = C.conv_fwd(dy, wt, R, R, 1, 1, R - 1 - pad, R - 1 - pad, 1, 1, st, st, None, None, None, 0, False,
-                        True, H, W)
+                        True, H, W, None, [], None, None, None, None, None)
         assert dx.shape == x.shape
         assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
@@ -79,11 +79,11 @@ def test_conv_epilogue_bias_resid_act(gpu):
     w4 = (torch.randn(48, 3, 3, 32, device=gpu) * 0.1).bfloat16()
     b = torch.randn(48, device=gpu)
     r = torch.randn(2, 6, 6, 48, device=gpu).bfloat16()
-    y = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, r, None, 1, False, True, 0, 0)
+    y = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, r, None, 1, False, True, 0, 0, None, [], None, None, None, None, None)
     ref = F.conv2d(x.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2), b, padding=1).permute(0, 2, 3, 1)
     ref = torch.relu(ref + r.float())
     assert rel(y, ref) < 1e-2
-    yf = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, None, None, 0, True, False, 0, 0)
+    yf = C.conv_fwd(x, pack_weight(w4), 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, b, None, None, 0, True, False, 0, 0, None, [], None, None, None, None, None)
     assert yf.dtype == torch.float32
     ref2 = F.conv2d(x.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2), b, padding=1).permute(0, 2, 3, 1)
     assert rel(yf, ref2) < 1e-3
@@ -242,6 +242,36 @@ def test_resnet_step_gpu_matches_cpu_reference(gpu):
     assert cos["fc.weight"] > 0.999 and cos["fc.bias"] > 0.999
 
 
+@pytest.mark.parametrize("block", ["bottleneck", "basic"])
+def test_resnet_bn_backward_fusion_matches_unfused(gpu, block):
+    """BN-backward reduction fused into the consumer's dgrad epilogue must give
+    the same gradients as the separate reduction pass. fp32 atomics make two
+    UNFUSED runs differ already (random labels at init give a noise-dominated
+    gradient, tools/diag_fusion.py), so fused-vs-unfused is held to that
+    run-to-run distance."""
+    import zoo.models.image.resnet as R
+    from zoo.ops import softmax_cross_entropy
+    torch.manual_seed(0)
+    blk = R.Bottleneck if block == "bottleneck" else R.BasicBlock
+    m = R.ResNet(blk, [2, 2, 1, 1], num_classes=16, width=16).to(gpu)
+    x = torch.randn(8, 3, 96, 96, device=gpu)
+    y = torch.randint(0, 16, (8,), device=gpu)
+    grads = []
+    try:
+        for fuse in (False, False, True):
+            R.FUSE_BN_BACKWARD = fuse
+            m.zero_grad(set_to_none=True)
+            softmax_cross_entropy(m(x), y).backward()
+            grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.parameters()]).double())
+    finally:
+        R.FUSE_BN_BACKWARD = True
+    u1, u2, f = grads
+    noise = (u1 - u2).norm().item() / u1.norm().item()
+    err = (u1 - f).norm().item() / u1.norm().item()
+    assert err < 2.0 * noise + 0.02, (err, noise)
+    assert F.cosine_similarity(u1, f, dim=0).item() > 0.98
+
+
 def test_resnet_learns_synthetic_task(gpu):
     """End-to-end learnability through the engine: 4-way 'which quadrant is bright'."""
     from zoo.common.nncontext import init_nncontext
@@ -262,7 +292,7 @@ def test_resnet_learns_synthetic_task(gpu):
             x[sel, :, r0:r0 + 32, c0:c0 + 32] += 1.5
         return x, y
     losses = []
-    for _ in range(60):
+    for _ in range(100):
         x, y = batch(64)
         losses.append(eng.train_step(x, y).item())
     assert sum(losses[-10:]) / 10 < 0.25 * sum(losses[:5]) / 5, losses
@@ -352,3 +382,26 @@ def test_tf_ordering_conv_bn_pool_runs_native(gpu):
     m.fit(x.numpy(), y.numpy(), batch_size=64, nb_epoch=15)
     acc = m.evaluate(x.numpy(), y.numpy(), batch_size=64)[0]
     assert acc > 0.8, acc
+
+
+@pytest.mark.parametrize("shape", [(2, 12, 12, 16, 32, 3, 2, 1), (2, 13, 11, 24, 16, 3, 2, 1),
+                                   (2, 14, 14, 32, 64, 1, 2, 0), (2, 15, 15, 16, 24, 5, 2, 2),
+                                   (1, 17, 17, 8, 16, 3, 3, 1)])
+def test_parity_decomposed_dgrad(gpu, shape):
+    """Strided dgrad through the output-parity decomposition (sub-filters +
+    epilogue row remap), incl. the fused residual add, vs the fp32 reference."""
+    from zoo.ops import pack_weight
+    from zoo.ops._kern import conv_dgrad
+    N, H, W, Cin, Cout, R, st, pad = shape
+    w4 = (torch.randn(Cout, R, R, Cin, device=gpu) / math.sqrt(R * R * Cin)).bfloat16()
+    xr = torch.zeros(N, Cin, H, W, device=gpu, requires_grad=True)
+    yr = F.conv2d(xr, w4.float().permute(0, 3, 1, 2), stride=st, padding=pad)
+    dy = torch.randn(yr.shape, device=gpu).bfloat16()
+    yr.backward(dy.float())
+    ref = xr.grad.permute(0, 2, 3, 1)
+    dx = conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), pack_weight(w4), Cout, R, R, Cin, H, W, (st, st), (pad, pad))
+    assert rel(dx, ref) < 1e-2
+    add = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
+    dx2 = conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), pack_weight(w4), Cout, R, R, Cin, H, W, (st, st),
+                     (pad, pad), resid=add)
+    assert rel(dx2, ref + add.float()) < 1e-2
