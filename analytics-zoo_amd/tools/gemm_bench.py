@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""GEMM throughput: the zoo implicit-GEMM kernel used as a plain GEMM
+(1x1 conv) vs torch.matmul (hipBLASLt) on the same bf16 shapes.
+
+  python analytics-zoo_amd/tools/gemm_bench.py
+"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import zoo._C as C  # noqa: E402
+
+SHAPES = [  # (M, N, K): Y[M,N] = X[M,K] @ W[N,K]^T
+    (4096, 4096, 4096), (8192, 8192, 8192), (802816, 64, 64), (802816, 256, 64), (802816, 64, 256),
+    (200704, 512, 128), (200704, 128, 512), (50176, 1024, 256), (50176, 256, 1024), (12544, 2048, 512),
+    (12544, 512, 2048),
+]
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    dev = torch.device("cuda:0")
+    rows = []
+    for M, N, K in SHAPES:
+        x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+        w = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
+        x4 = x.view(1, M, 1, K)
+        f = 2.0 * M * N * K
+        t_z = timeit(lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0,
+                                        None, [], None, None, None, None, None))
+        t_t = timeit(lambda: torch.matmul(x, w.t()))
+        byts = 2.0 * (M * K + N * K + M * N)
+        rows.append({"M": M, "N": N, "K": K, "zoo_TF": round(f / t_z / 1e12, 1), "torch_TF": round(f / t_t / 1e12, 1),
+                     "zoo_us": round(t_z * 1e6, 1), "torch_us": round(t_t * 1e6, 1),
+                     "zoo_TBps": round(byts / t_z / 1e12, 2)})
+        print(json.dumps(rows[-1]), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -170,7 +170,10 @@ class GradSync:
         if clip is not None:
             clip(shard[: hi - lo], gscale, self)
         if hi > lo:
-            optim.step(flat.master[lo:hi], shard[: hi - lo], None, gscale)
+            if getattr(optim, "parts", None) is not None:   # MultiOptimMethod: ranges are global offsets
+                optim.step(flat.master[lo:hi], shard[: hi - lo], None, gscale, base=lo)
+            else:
+                optim.step(flat.master[lo:hi], shard[: hi - lo], None, gscale)
         # all-gather the updated fp32 master shards, then refresh the bf16 copy
         mpad = torch.zeros(self.padded, dtype=flat.master.dtype, device=flat.master.device)
         mine = mpad[lo:lo + per].clone()

@@ -219,6 +219,8 @@ def to_metrics(metrics, criterion=None):
     """Metric strings -> ValidationMethods (KerasUtils.toBigDLMetrics)."""
     if metrics is None:
         return []
+    if isinstance(metrics, (ValidationMethod, str)):
+        metrics = [metrics]
     out = []
     for m in metrics:
         if isinstance(m, ValidationMethod):
