@@ -1,0 +1,46 @@
+"""Net: model loaders (Zs/pipeline/api/Net.scala:44-260; Py/pipeline/api/net/net_load.py).
+
+  Net.load(path)                 zoo Keras / ZooModel file
+  Net.load_bigdl(path, weights)  BigDL protobuf ``.model`` -> GraphNet
+  Net.load_caffe(def, model)     Caffe prototxt + caffemodel -> GraphNet
+  Net.load_onnx(path)            ONNX ModelProto -> GraphNet
+  Net.load_torch(path)           TorchScript -> TorchNet
+  Net.load_tf / load_keras       not available (no TF / Keras runtime here)
+"""
+
+
+class Net:
+    @staticmethod
+    def load(model_path, weight_path=None):
+        from zoo.pipeline.api.keras.serialization import load_model
+        return load_model(model_path)
+
+    @staticmethod
+    def load_bigdl(model_path, weight_path=None, bigdl_type="float"):
+        from zoo.pipeline.api.net.bigdl_loader import load_bigdl
+        return load_bigdl(model_path, weight_path)
+
+    @staticmethod
+    def load_caffe(def_path, model_path, bigdl_type="float"):
+        from zoo.pipeline.api.net.caffe_loader import load_caffe
+        return load_caffe(def_path, model_path)
+
+    @staticmethod
+    def load_onnx(model_path):
+        from zoo.pipeline.api.onnx.onnx_loader import load_onnx
+        return load_onnx(model_path)
+
+    @staticmethod
+    def load_torch(path, bigdl_type="float"):
+        from zoo.pipeline.api.net.torch_net import TorchNet
+        return TorchNet.load(path)
+
+    @staticmethod
+    def load_tf(path, inputs=None, outputs=None, **kw):
+        raise NotImplementedError("TensorFlow graphs cannot be executed here (no TF runtime); export the graph "
+                                  "to ONNX and use Net.load_onnx")
+
+    @staticmethod
+    def load_keras(json_path=None, hdf5_path=None, by_name=False):
+        raise NotImplementedError("Keras 1.2 json/hdf5 import needs h5py/keras; rebuild the model with "
+                                  "zoo.pipeline.api.keras layers or go through ONNX")
