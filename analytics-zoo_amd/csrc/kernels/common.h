@@ -50,6 +50,17 @@ ZOO_DEV uint4 pack8(const float* f) {
   return r;
 }
 
+// zero a loaded vector on a predicate without a branch or an aggregate select
+// (an aggregate `ok ? v : zero` lowers to a scratch-memory select on hipcc)
+ZOO_DEV uint4 mask4(uint4 v, bool ok) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_uint4(v.x & m, v.y & m, v.z & m, v.w & m);
+}
+ZOO_DEV uint2 mask2(uint2 v, bool ok) {
+  const uint32_t m = ok ? 0xffffffffu : 0u;
+  return make_uint2(v.x & m, v.y & m);
+}
+
 ZOO_DEV float warp_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

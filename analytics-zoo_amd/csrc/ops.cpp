@@ -52,6 +52,8 @@ hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*
 hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
                              float*, int, int, hipStream_t);
 hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, int, int64_t, hipStream_t);
+hipError_t zoo_resize_normalize(const void*, void*, int, int, int, int, int, int, const float*, const float*, int, int,
+                                hipStream_t);
 hipError_t zoo_embedding_bwd(const void*, int, const int64_t*, float*, int, int, int, int64_t, float, hipStream_t);
 }
 
@@ -546,10 +548,38 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor gtable, 
             "embedding_bwd");
 }
 
+
+// uint8 [N, Hi, Wi, C] (C in 1..4) -> resized + normalized image batch:
+// layout 0 -> fp32 [N, C, Ho, Wo]; layout 1 -> bf16 [N, Ho, Wo, 4] (zero-padded channels)
+torch::Tensor resize_normalize(torch::Tensor in, int64_t Ho, int64_t Wo, std::vector<double> mean,
+                               std::vector<double> stdv, bool swap_rb, int64_t layout) {
+  req(in, at::kByte, "image");
+  TORCH_CHECK(in.dim() == 4, "image batch must be [N, H, W, C]");
+  const int N = in.size(0), Hi = in.size(1), Wi = in.size(2), C = in.size(3);
+  TORCH_CHECK(C >= 1 && C <= 4, "1..4 channels supported");
+  TORCH_CHECK(Ho > 0 && Wo > 0 && Hi > 0 && Wi > 0, "bad image size");
+  TORCH_CHECK(layout == 0 || layout == 1, "layout must be 0 (NCHW f32) or 1 (NHWC4 bf16)");
+  float m[3] = {0.f, 0.f, 0.f}, sd[3] = {1.f, 1.f, 1.f};
+  for (size_t i = 0; i < 3 && i < mean.size(); ++i) m[i] = (float)mean[i];
+  for (size_t i = 0; i < 3 && i < stdv.size(); ++i) sd[i] = (float)stdv[i];
+  if (mean.size() == 1) m[1] = m[2] = m[0];
+  if (stdv.size() == 1) sd[1] = sd[2] = sd[0];
+  for (int i = 0; i < 3; ++i) TORCH_CHECK(sd[i] != 0.f, "std must be non-zero");
+  torch::Tensor out = layout == 0
+      ? torch::empty({N, C, Ho, Wo}, in.options().dtype(at::kFloat))
+      : torch::empty({N, Ho, Wo, 4}, in.options().dtype(at::kBFloat16));
+  if (N == 0) return out;
+  check_hip(zoo_resize_normalize(in.data_ptr(), out.data_ptr(), N, Hi, Wi, C, (int)Ho, (int)Wo, m, sd,
+                                 swap_rb ? 1 : 0, (int)layout, cur_stream()),
+            "resize_normalize");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "zoo native gfx950 (MI355X) kernel library";
+  m.def("resize_normalize", &resize_normalize);
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);
   m.def("conv_wgrad", &conv_wgrad);

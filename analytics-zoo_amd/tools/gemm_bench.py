@@ -33,16 +33,22 @@ def timeit(fn, iters=20):
 
 
 def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default=None, help="comma-separated indices into SHAPES")
+    ap.add_argument("--zoo-only", action="store_true")
+    a = ap.parse_args()
+    shapes = SHAPES if a.shapes is None else [SHAPES[int(i)] for i in a.shapes.split(",")]
     dev = torch.device("cuda:0")
     rows = []
-    for M, N, K in SHAPES:
+    for M, N, K in shapes:
         x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
         w = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
         x4 = x.view(1, M, 1, K)
         f = 2.0 * M * N * K
         t_z = timeit(lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0,
                                         None, [], None, None, None, None, None))
-        t_t = timeit(lambda: torch.matmul(x, w.t()))
+        t_t = float("nan") if a.zoo_only else timeit(lambda: torch.matmul(x, w.t()))
         byts = 2.0 * (M * K + N * K + M * N)
         rows.append({"M": M, "N": N, "K": K, "zoo_TF": round(f / t_z / 1e12, 1), "torch_TF": round(f / t_t / 1e12, 1),
                      "zoo_us": round(t_z * 1e6, 1), "torch_us": round(t_t * 1e6, 1),
