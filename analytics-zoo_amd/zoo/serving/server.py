@@ -1,0 +1,248 @@
+"""Cluster Serving worker (Zs/serving/ClusterServing.scala:38-300, ClusterServingHelper.scala,
+PreProcessing.scala, PostProcessing.scala; config scripts/cluster-serving/config.yaml).
+
+One worker process per GPU. Each worker:
+  1. joins consumer group ``serving`` on stream ``image_stream`` (XREADGROUP),
+  2. takes up to ``batch_size`` records (``uri`` + base64 ``image`` — an
+     encoded image — or ``tensor``: base64 float32 bytes with a ``shape`` field),
+  3. decodes images on a CPU thread pool, then does resize + normalize +
+     layout on the GPU in ONE fused HIP kernel (csrc/kernels/image.hip),
+  4. runs the model through InferenceModel (HIP stream + captured hipGraph
+     per batch shape, bf16/fp32),
+  5. post-processes (``topN(k)`` filter or the full nested-list string) and
+     writes ``result:<uri>`` hashes, then XACK + XDEL the consumed entries.
+Back-pressure: records are trimmed when the stream exceeds ``max_queue``.
+Throughput / record counts go to TensorBoard ("Serving Throughput",
+"Total Records Number", InferenceSummary.scala).
+"""
+import base64
+import io
+import logging
+import os
+import socket
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import torch
+
+log = logging.getLogger("zoo.serving")
+
+STREAM = "image_stream"
+GROUP = "serving"
+
+MODEL_EXTS = {".caffemodel": "caffe", ".prototxt": "caffe", ".model": "bigdl", ".onnx": "onnx", ".pt": "torch",
+              ".zoo": "zoo", ".keras": "zoo", ".pb": "tensorflow", ".xml": "openvino", ".bin": "openvino"}
+
+
+def load_config(path):
+    import yaml
+    with open(path) as f:
+        cfg = yaml.safe_load(f) or {}
+    model = cfg.get("model") or {}
+    data = cfg.get("data") or {}
+    params = cfg.get("params") or {}
+    src = data.get("src") or "localhost:6379"
+    host, _, port = src.partition(":")
+    shape = data.get("image_shape") or "3,224,224"
+    shape = [int(s) for s in str(shape).split(",")]
+    out = {
+        "model_path": model.get("path") or "model",
+        "host": "127.0.0.1" if host in ("", "localhost") else host,
+        "port": int(port or 6379),
+        "image_shape": shape,
+        "filter": data.get("filter") or "None",
+        "batch_size": int(params.get("batch_size") or 4),
+        "performance_mode": str(params.get("performance_mode") or "OFF").upper() in ("ON", "TRUE", "1"),
+        "mean": [float(x) for x in str(params.get("mean", "0,0,0")).split(",")],
+        "std": [float(x) for x in str(params.get("std", "1,1,1")).split(",")],
+        "to_rgb": str(params.get("to_rgb", "false")).lower() in ("true", "1", "on"),
+        "concurrent_num": int(params.get("concurrent_num") or 1),
+        "max_queue": int(params.get("max_queue") or 100000),
+        "tensorboard": params.get("tensorboard"),
+        "maxmem": (cfg.get("redis") or {}).get("maxmem") or "4g",
+    }
+    return out
+
+
+def discover_model(path):
+    """Model type from the file extensions in ``path`` (ClusterServingHelper.parseModelType)."""
+    files = [path] if os.path.isfile(path) else [os.path.join(path, f) for f in sorted(os.listdir(path))]
+    found = {}
+    for f in files:
+        ext = os.path.splitext(f)[1].lower()
+        if ext in MODEL_EXTS:
+            found.setdefault(MODEL_EXTS[ext], []).append(f)
+    for kind in ("caffe", "bigdl", "onnx", "torch", "zoo", "tensorflow", "openvino"):
+        if kind in found:
+            return kind, found[kind]
+    raise ValueError("no model file found in %s" % path)
+
+
+def load_model_into(im, path):
+    kind, files = discover_model(path)
+    if kind == "caffe":
+        proto = next(f for f in files if f.endswith(".prototxt"))
+        weights = next((f for f in files if f.endswith(".caffemodel")), None)
+        return im.load_caffe(proto, weights)
+    if kind == "bigdl":
+        return im.load_bigdl(files[0])
+    if kind == "onnx":
+        return im.load_onnx(files[0])
+    if kind == "torch":
+        return im.load_torch(files[0])
+    if kind == "zoo":
+        return im.load(files[0])
+    if kind == "tensorflow":
+        return im.load_tensorflow(files[0])
+    return im.load_openvino(*files[:2])
+
+
+# ---- pre / post processing -------------------------------------------------------------------
+def decode_record(fields):
+    """-> ("image", HWC uint8 BGR) or ("tensor", float32 array)."""
+    g = {(k.decode() if isinstance(k, bytes) else k): v for k, v in fields.items()}
+    if "image" in g:
+        from zoo.pipeline.nnframes.nn_image_reader import decode_image
+        raw = base64.b64decode(g["image"])
+        return "image", decode_image(raw)
+    if "tensor" in g:
+        shape = [int(s) for s in (g["shape"].decode() if isinstance(g["shape"], bytes) else g["shape"]).split(",")]
+        return "tensor", np.frombuffer(base64.b64decode(g["tensor"]), np.float32).reshape(shape)
+    raise ValueError("record has neither image nor tensor")
+
+
+def tensor_to_ndarray_string(t):
+    """PostProcessing.tensorToNdArrayString: nested brackets, comma separated."""
+    return np.array2string(np.asarray(t, np.float32), separator=",", threshold=1 << 30,
+                           max_line_width=1 << 30, formatter={"float_kind": lambda x: repr(float(x))}).replace(
+        " ", "").replace("\n", "")
+
+
+def top_n(t, n):
+    """PostProcessing.topN: ``[[index,value],...]`` over the flattened output, descending."""
+    flat = np.asarray(t, np.float32).reshape(-1)
+    idx = np.argsort(-flat, kind="stable")[:n]
+    return "[" + "".join("[%d,%s]" % (i, repr(float(flat[i]))) for i in idx) + "]"
+
+
+def post_process(t, flt="None"):
+    if flt and flt != "None":
+        if not flt.endswith(")") or len(flt.split("(")) != 2:
+            raise ValueError("please check your filter format, should be filter_name(filter_args)")
+        name, args = flt.split("(")
+        args = args[:-1].split(",")
+        if name == "topN":
+            if len(args) != 1:
+                raise ValueError("topN filter only support 1 argument")
+            return top_n(t, int(args[0]))
+        return ""
+    return tensor_to_ndarray_string(t)
+
+
+class ClusterServing:
+    def __init__(self, config, model=None, consumer=None, device=None):
+        from zoo.pipeline.inference import InferenceModel
+        from zoo.serving.resp import connect
+        self.cfg = load_config(config) if isinstance(config, str) else dict(config)
+        self.db = connect(self.cfg["host"], self.cfg["port"])
+        try:
+            self.db.xgroup_create(STREAM, GROUP, id="0", mkstream=True)
+        except Exception:  # noqa: BLE001 - BUSYGROUP: group exists
+            pass
+        self.consumer = consumer or "%s-%d" % (socket.gethostname(), os.getpid())
+        self.im = InferenceModel(self.cfg["concurrent_num"], device=device)
+        if model is not None:
+            self.im.load_module(model)
+        else:
+            load_model_into(self.im, self.cfg["model_path"])
+        self.pool = ThreadPoolExecutor(8)
+        self.stop_flag = threading.Event()
+        self.records = 0
+        self.summary = None
+        if self.cfg.get("tensorboard"):
+            from zoo.tensorboard import FileWriter
+            self.summary = FileWriter(self.cfg["tensorboard"])
+        self._t0 = time.time()
+
+    def _images_to_batch(self, imgs):
+        c, h, w = self.cfg["image_shape"]
+        mean, std = self.cfg["mean"], self.cfg["std"]
+        dev = self.im.device
+        if dev.type == "cuda" and len({im.shape for im in imgs}) == 1:
+            from zoo.feature.image.transforms import gpu_resize_normalize
+            return gpu_resize_normalize(np.stack(imgs), h, w, mean, std, self.cfg["to_rgb"], "NCHW", dev)
+        from zoo.feature.image.transforms import resize_bilinear
+        out = []
+        for im in imgs:
+            m = resize_bilinear(im.astype(np.float32), h, w)
+            if self.cfg["to_rgb"]:
+                m = m[..., ::-1]
+            m = (m - np.asarray(mean[:m.shape[2]], np.float32)) / np.asarray(std[:m.shape[2]], np.float32)
+            out.append(m.transpose(2, 0, 1))
+        return torch.from_numpy(np.stack(out).astype(np.float32))
+
+    def serve_once(self, block_ms=100):
+        """One micro-batch; returns the number of records served."""
+        res = self.db.xreadgroup(GROUP, self.consumer, {STREAM: ">"}, count=self.cfg["batch_size"], block=block_ms)
+        if not res:
+            return 0
+        msgs = res[0][1]
+        ids = [sid for sid, _ in msgs]
+        uris = [(f.get(b"uri", f.get("uri", b"")) if isinstance(f, dict) else b"") for _, f in msgs]
+        uris = [u.decode() if isinstance(u, bytes) else str(u) for u in uris]
+        decoded = list(self.pool.map(lambda m: decode_record(m[1]), msgs))
+        kinds = {k for k, _ in decoded}
+        if kinds == {"image"}:
+            batch = self._images_to_batch([a for _, a in decoded])
+        elif kinds == {"tensor"}:
+            batch = torch.from_numpy(np.stack([a for _, a in decoded]).astype(np.float32))
+        else:  # mixed micro-batch: images are brought to the configured tensor shape first
+            img_pos = [i for i, (k, _) in enumerate(decoded) if k == "image"]
+            imgs = self._images_to_batch([decoded[i][1] for i in img_pos]).float().cpu()
+            rows = [torch.from_numpy(np.asarray(a, np.float32)) for _, a in decoded]
+            for j, i in enumerate(img_pos):
+                rows[i] = imgs[j]
+            batch = torch.stack(rows)
+        out = self.im.predict(batch)
+        outs = out if isinstance(out, np.ndarray) else out[0]
+        flt = self.cfg["filter"]
+        for uri, row in zip(uris, outs):
+            self.db.hset("result:" + uri, "value", post_process(row, flt))
+        self.db.xack(STREAM, GROUP, *ids)
+        self.db.xdel(STREAM, *ids)
+        self.records += len(ids)
+        if self.summary is not None:
+            dt = max(time.time() - self._t0, 1e-9)
+            self.summary.add_scalar("Serving Throughput", self.records / dt, self.records)
+            self.summary.add_scalar("Total Records Number", self.records, self.records)
+        return len(ids)
+
+    def _trim(self):
+        try:
+            if self.db.xlen(STREAM) > self.cfg["max_queue"]:
+                self.db.xtrim(STREAM, self.cfg["max_queue"])
+        except Exception:  # noqa: BLE001
+            pass
+
+    def run(self, running_flag=None, max_records=None, idle_timeout=None):
+        """Serve until ``running_flag`` (a file path) disappears, ``max_records``
+        are served, or nothing arrives for ``idle_timeout`` seconds."""
+        last = time.time()
+        while not self.stop_flag.is_set():
+            if running_flag is not None and not os.path.exists(running_flag):
+                break
+            n = self.serve_once()
+            if n:
+                last = time.time()
+            elif idle_timeout is not None and time.time() - last > idle_timeout:
+                break
+            if max_records is not None and self.records >= max_records:
+                break
+            if self.records and self.records % 1000 < self.cfg["batch_size"]:
+                self._trim()
+        return self.records
+
+    def stop(self):
+        self.stop_flag.set()

@@ -1,0 +1,94 @@
+"""Cluster Serving (ClusterServingSpec / PreProcessingSpec / PostProcessingSpec /
+test_serving client analogues): the RESP queue server, the end-to-end
+enqueue -> batch -> infer -> result path, pre/post processing formats."""
+import numpy as np
+import pytest
+import torch
+
+from zoo.common.nncontext import init_nncontext
+
+
+@pytest.fixture(scope="module", autouse=True)
+def ctx():
+    return init_nncontext()
+
+
+@pytest.fixture()
+def server():
+    from zoo.serving.resp import RespServer
+    srv = RespServer("127.0.0.1", 0, maxmemory=1 << 20).start()
+    yield srv
+    srv.shutdown()
+    srv.server_close()
+
+
+def test_resp_streams_hashes_groups(server):
+    from zoo.serving.resp import RespClient
+    c = RespClient("127.0.0.1", server.port)
+    assert c.ping()
+    c.xgroup_create("s", "g", id="0", mkstream=True)
+    ids = [c.xadd("s", {"uri": "u%d" % i, "v": str(i)}) for i in range(5)]
+    assert c.xlen("s") == 5
+    got = c.xreadgroup("g", "c1", {"s": ">"}, count=3, block=10)
+    msgs = got[0][1]
+    assert [m[1][b"uri"] for m in msgs] == [b"u0", b"u1", b"u2"]
+    got2 = c.xreadgroup("g", "c2", {"s": ">"}, count=10, block=10)
+    assert [m[1][b"uri"] for m in got2[0][1]] == [b"u3", b"u4"]  # consumer group: no re-delivery
+    assert c.xreadgroup("g", "c1", {"s": ">"}, count=1, block=20) == []
+    assert c.xack("s", "g", *ids) == 5 and c.xdel("s", *ids) == 5 and c.xlen("s") == 0
+    c.hset("result:a", "value", "[1,2]")
+    assert c.hgetall("result:a") == {b"value": b"[1,2]"}
+    assert c.keys("result:*") == [b"result:a"]
+    assert c.delete("result:a") == 1 and c.exists("result:a") == 0
+    info = c.info()
+    assert info["maxmemory"] == 1 << 20
+    # back-pressure: the server refuses writes beyond maxmemory
+    with pytest.raises(Exception):
+        for i in range(10000):
+            c.xadd("big", {"x": "y" * 4096})
+
+
+def test_post_processing_formats():
+    from zoo.serving.server import post_process
+    t = np.array([0.1, 0.7, 0.2], np.float32)
+    assert post_process(t, "topN(2)") == "[[1,%r][2,%r]]" % (float(np.float32(0.7)), float(np.float32(0.2)))
+    s = post_process(np.array([[1.0, 2.0], [3.0, 4.0]], np.float32))
+    assert s == "[[1.0,2.0],[3.0,4.0]]"
+    with pytest.raises(ValueError):
+        post_process(t, "topN(2")
+
+
+def test_serving_end_to_end_tensors_and_images(server, tmp_path):
+    from zoo.serving import ClusterServing, InputQueue, OutputQueue
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Flatten(), torch.nn.Linear(3 * 8 * 8, 5), torch.nn.Softmax(-1))
+    cfg = tmp_path / "config.yaml"
+    cfg.write_text("model:\n  path: m\ndata:\n  src: 127.0.0.1:%d\n  image_shape: 3,8,8\n  filter: topN(2)\n"
+                   "params:\n  batch_size: 4\n" % server.port)
+    serving = ClusterServing(str(cfg), model=model)
+    inq, outq = InputQueue(str(cfg)), OutputQueue(str(cfg))
+    rng = np.random.default_rng(0)
+    xs = {("t%d" % i): rng.random((3, 8, 8)).astype(np.float32) for i in range(6)}
+    for k, v in xs.items():
+        inq.enqueue_tensor(k, v)
+    img = rng.integers(0, 255, (10, 12, 3)).astype(np.uint8)
+    inq.enqueue_image("img0", img)
+    served = serving.run(max_records=7, idle_timeout=5)
+    assert served == 7
+    res = outq.dequeue()
+    assert set(res) == set(xs) | {"img0"}
+    with torch.no_grad():
+        ref = model(torch.from_numpy(xs["t3"][None]))[0].numpy()
+    top = np.argsort(-ref)[:2]
+    assert res["t3"].startswith("[[%d," % top[0]) and ("[%d," % top[1]) in res["t3"]
+    assert outq.dequeue() == {}
+
+
+def test_model_discovery(tmp_path):
+    from zoo.serving.server import discover_model
+    (tmp_path / "a.prototxt").write_text("x")
+    (tmp_path / "a.caffemodel").write_bytes(b"")
+    kind, files = discover_model(str(tmp_path))
+    assert kind == "caffe" and len(files) == 2
+    (tmp_path / "m.onnx").write_bytes(b"")
+    assert discover_model(str(tmp_path / "m.onnx"))[0] == "onnx"
