@@ -1,0 +1,102 @@
+"""Wide & Deep (Zs/models/recommendation/WideAndDeep.scala:54-365, Py wide_and_deep.py:29-239).
+
+Wide part: a linear model over the (base + crossed) categorical columns. The
+reference feeds a sparse multi-hot tensor to ``SparseDense``; here the wide
+input is the per-column GLOBAL index (column offset + value), ``[batch,
+n_wide_cols]`` int, and the linear layer is an embedding-bag sum over the
+weight rows (SparseEmbedding, the HK10 gather) — the same math without
+materialising a [batch, sum(wide_dims)] multi-hot matrix in HBM.
+Deep part: multi-hot indicator columns + per-column embeddings +
+continuous columns -> MLP. ``model_type`` in {wide, deep, wide_n_deep}.
+"""
+from zoo.models.recommendation.recommender import Recommender
+from zoo.pipeline.api.keras.engine.topology import Model, merge
+from zoo.pipeline.api.keras.layers import (Activation, CAdd, Dense, Embedding, Flatten, Input, Select,
+                                           SparseEmbedding)
+
+
+class ColumnFeatureInfo:
+    def __init__(self, wide_base_cols=None, wide_base_dims=None, wide_cross_cols=None, wide_cross_dims=None,
+                 indicator_cols=None, indicator_dims=None, embed_cols=None, embed_in_dims=None, embed_out_dims=None,
+                 continuous_cols=None, label="label"):
+        self.wide_base_cols = list(wide_base_cols or [])
+        self.wide_base_dims = [int(d) for d in (wide_base_dims or [])]
+        self.wide_cross_cols = list(wide_cross_cols or [])
+        self.wide_cross_dims = [int(d) for d in (wide_cross_dims or [])]
+        self.indicator_cols = list(indicator_cols or [])
+        self.indicator_dims = [int(d) for d in (indicator_dims or [])]
+        self.embed_cols = list(embed_cols or [])
+        self.embed_in_dims = [int(d) for d in (embed_in_dims or [])]
+        self.embed_out_dims = [int(d) for d in (embed_out_dims or [])]
+        self.continuous_cols = list(continuous_cols or [])
+        self.label = label
+
+    def __str__(self):
+        return ("ColumnFeatureInfo {wide_base_cols: %s, wide_base_dims: %s, wide_cross_cols: %s, wide_cross_dims: %s, "
+                "indicator_cols: %s, indicator_dims: %s, embed_cols: %s, embed_in_dims: %s, embed_out_dims: %s, "
+                "continuous_cols: %s, label: '%s'}" % (
+                    self.wide_base_cols, self.wide_base_dims, self.wide_cross_cols, self.wide_cross_dims,
+                    self.indicator_cols, self.indicator_dims, self.embed_cols, self.embed_in_dims,
+                    self.embed_out_dims, self.continuous_cols, self.label))
+
+
+class WideAndDeep(Recommender):
+    def __init__(self, class_num, column_info, model_type="wide_n_deep", hidden_layers=(40, 20, 10), **kwargs):
+        super().__init__(**kwargs)
+        ci = column_info
+        if len(ci.wide_base_cols) != len(ci.wide_base_dims) or len(ci.wide_cross_cols) != len(ci.wide_cross_dims):
+            raise ValueError("size of wide columns and dims should match")
+        if len(ci.indicator_cols) != len(ci.indicator_dims):
+            raise ValueError("size of indicator columns and dims should match")
+        if not (len(ci.embed_cols) == len(ci.embed_in_dims) == len(ci.embed_out_dims)):
+            raise ValueError("size of embed columns and dims should match")
+        if model_type not in ("wide", "deep", "wide_n_deep"):
+            raise TypeError("Unsupported model_type: %s" % model_type)
+        self.class_num = int(class_num)
+        self.column_info = ci
+        self.model_type = model_type
+        self.hidden_layers = [int(u) for u in hidden_layers]
+        self._init_model()
+
+    def _wide(self):
+        ci = self.column_info
+        n = len(ci.wide_base_cols) + len(ci.wide_cross_cols)
+        dims = sum(ci.wide_base_dims) + sum(ci.wide_cross_dims)
+        inp = Input(shape=(n,))
+        lin = SparseEmbedding(dims, self.class_num, combiner="sum", init="zero")(inp)
+        return inp, CAdd((self.class_num,))(lin)
+
+    def _deep(self):
+        ci = self.column_info
+        inputs, parts = [], []
+        if ci.indicator_dims:
+            ind = Input(shape=(sum(ci.indicator_dims),))
+            inputs.append(ind)
+            parts.append(ind)
+        if ci.embed_in_dims:
+            emb_in = Input(shape=(len(ci.embed_in_dims),))
+            inputs.append(emb_in)
+            for i, (din, dout) in enumerate(zip(ci.embed_in_dims, ci.embed_out_dims)):
+                sel = Flatten()(Select(1, i)(emb_in))
+                parts.append(Flatten()(Embedding(din + 1, dout, init="normal")(sel)))
+        if ci.continuous_cols:
+            cont = Input(shape=(len(ci.continuous_cols),))
+            inputs.append(cont)
+            parts.append(cont)
+        if not parts:
+            raise TypeError("Empty deep tensors")
+        h = parts[0] if len(parts) == 1 else merge(parts, mode="concat")
+        for u in self.hidden_layers:
+            h = Dense(u, activation="relu")(h)
+        return inputs, Dense(self.class_num, activation="relu")(h)
+
+    def build_model(self):
+        if self.model_type == "wide":
+            inp, lin = self._wide()
+            return Model(inp, Activation("softmax")(lin))
+        if self.model_type == "deep":
+            ins, deep = self._deep()
+            return Model(ins if len(ins) > 1 else ins[0], Activation("softmax")(deep))
+        winp, wide = self._wide()
+        ins, deep = self._deep()
+        return Model([winp] + ins, Activation("softmax")(merge([wide, deep], mode="sum")))

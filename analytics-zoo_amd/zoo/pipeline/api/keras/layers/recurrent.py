@@ -20,9 +20,10 @@ class _RNNBase(Layer):
 
     def __init__(self, output_dim, activation="tanh", inner_activation="hard_sigmoid", return_sequences=False,
                  go_backwards=False, W_regularizer=None, U_regularizer=None, b_regularizer=None, input_shape=None,
-                 init="glorot_uniform", inner_init="orthogonal", **kwargs):
+                 init="glorot_uniform", inner_init="orthogonal", return_state=False, **kwargs):
         super().__init__(input_shape=input_shape, **kwargs)
         self.output_dim = int(output_dim)
+        self.return_state = return_state
         self.activation, self.inner_activation = activation, inner_activation
         self.return_sequences, self.go_backwards = return_sequences, go_backwards
         self.init, self.inner_init = init, inner_init
@@ -45,10 +46,20 @@ class _RNNBase(Layer):
             b[h:2 * h] = 1.0  # forget-gate bias (Keras unit_forget_bias)
         self.b = nn.Parameter(b)
 
+    def build_shapes(self, input_shape):
+        return input_shape[0] if isinstance(input_shape, list) else input_shape
+
+    def _ensure_built(self, input_shape):
+        super()._ensure_built(self.build_shapes(input_shape))
+
     def compute_output_shape(self, input_shape):
-        if self.return_sequences:
-            return (None, input_shape[1], self.output_dim)
-        return (None, self.output_dim)
+        input_shape = self.build_shapes(input_shape)
+        out = (None, input_shape[1], self.output_dim) if self.return_sequences else (None, self.output_dim)
+        if self.return_state:
+            return [out] + [(None, self.output_dim)] * self._n_state
+        return out
+
+    _n_state = 1
 
     def _step(self, xt, state):
         raise NotImplementedError
@@ -58,18 +69,22 @@ class _RNNBase(Layer):
         return (h,)
 
     def call(self, x):
+        init = None
+        if isinstance(x, (list, tuple)):  # [sequence, initial states...] (Seq2seq decoder / bridge)
+            x, init = x[0], tuple(x[1:])
         B, T, D = x.shape
         xw = ops.linear(x.reshape(B * T, D), self.W, self.b).reshape(B, T, -1)
-        state = self._init_state(x)
+        state = self._init_state(x) if not init else tuple(t.to(xw.dtype) for t in init)
         outs = []
         steps = range(T - 1, -1, -1) if self.go_backwards else range(T)
         for t in steps:
             state = self._step(xw[:, t], state)
             if self.return_sequences:
                 outs.append(state[0])
-        if self.return_sequences:
-            return torch.stack(outs, dim=1)
-        return state[0]
+        out = torch.stack(outs, dim=1) if self.return_sequences else state[0]
+        if self.return_state:
+            return [out] + list(state)
+        return out
 
 
 class SimpleRNN(_RNNBase):
@@ -87,6 +102,7 @@ class SimpleRNN(_RNNBase):
 
 class LSTM(_RNNBase):
     n_gates = 4
+    _n_state = 2
 
     def _init_state(self, x):
         z = x.new_zeros(x.shape[0], self.output_dim)
