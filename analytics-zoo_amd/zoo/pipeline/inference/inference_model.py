@@ -43,6 +43,9 @@ class _Replica:
         self.idx = idx
         dev = owner.device
         self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
+        # a private memory pool: graphs of different replicas replay concurrently,
+        # so their static buffers must never alias
+        self.pool = torch.cuda.graph_pool_handle() if dev.type == "cuda" else None
         self.graphs = {}
 
     def _forward(self, xs):
@@ -55,17 +58,20 @@ class _Replica:
         if g is not None:
             return g
         dev = self.owner.device
-        static_in = [torch.zeros(t.shape, dtype=t.dtype, device=dev) for t in xs]
-        for s, t in zip(static_in, xs):
-            s.copy_(t)
-        # warm up on the side stream (lazy allocations, kernel attributes), then capture
-        with torch.cuda.stream(self.stream):
-            for _ in range(2):
-                self._forward(static_in)
-        self.stream.synchronize()
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph, stream=self.stream, pool=self.owner._pool):
-            static_out = self._forward(static_in)
+        # one capture at a time per process; thread-local capture mode lets the
+        # other replicas keep replaying / copying on their own streams meanwhile
+        with self.owner._capture_lock:
+            static_in = [torch.zeros(t.shape, dtype=t.dtype, device=dev) for t in xs]
+            for s, t in zip(static_in, xs):
+                s.copy_(t)
+            # warm up on the side stream (lazy allocations, kernel attributes), then capture
+            with torch.cuda.stream(self.stream):
+                for _ in range(2):
+                    self._forward(static_in)
+            self.stream.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graph, stream=self.stream, pool=self.pool, capture_error_mode="thread_local"):
+                static_out = self._forward(static_in)
         g = (graph, static_in, static_out)
         self.graphs[key] = g
         return g
@@ -108,8 +114,8 @@ class InferenceModel:
         self.max_batch = max_batch
         self.model = None
         self._queue = None
-        self._pool = None
         self._lock = threading.Lock()
+        self._capture_lock = threading.Lock()
         self._n_replicas = 0
         self.summary = None
         self._records = 0
@@ -124,7 +130,6 @@ class InferenceModel:
         for p in model.parameters():
             p.requires_grad_(False)
         self.model = model
-        self._pool = torch.cuda.graph_pool_handle() if self.device.type == "cuda" else None
         self._queue = queue.Queue(maxsize=max(self.concurrent_num, 1) if not self.auto_scaling else 0)
         self._n_replicas = 0
         if not self.auto_scaling:

@@ -5,6 +5,8 @@ relative-to-max tolerances sized for bf16 rounding (8 mantissa bits).
 """
 import math
 
+import numpy as np
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -405,3 +407,57 @@ def test_parity_decomposed_dgrad(gpu, shape):
     dx2 = conv_dgrad(dy.permute(0, 2, 3, 1).contiguous(), pack_weight(w4), Cout, R, R, Cin, H, W, (st, st),
                      (pad, pad), resid=add)
     assert rel(dx2, ref + add.float()) < 1e-2
+
+
+def test_inference_model_hipgraph_replicas(gpu):
+    """InferenceModel on the GPU: per-replica HIP streams + captured hipGraph per
+    input shape; concurrent predictions from several threads match eager."""
+    import threading
+    from zoo.models.image.resnet import resnet18
+    from zoo.pipeline.inference import InferenceModel
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).to(gpu).eval()
+    x = torch.randn(4, 3, 64, 64)
+    with torch.no_grad():
+        ref = m(x.to(gpu)).float().cpu().numpy()
+    im = InferenceModel(2, device=gpu).load_module(m)
+    assert im.use_graph
+    outs = [None] * 4
+
+    def work(i):
+        outs[i] = im.predict(x.numpy())
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(4)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    for o in outs:
+        assert np.allclose(o, ref, atol=2e-2, rtol=2e-2)
+    # a second shape gets its own graph
+    assert im.predict(x[:2].numpy()).shape == (2, 10)
+
+
+def test_serving_worker_on_gpu(gpu):
+    from zoo.serving import ClusterServing, InputQueue, OutputQueue
+    from zoo.serving.resp import RespServer
+    import tempfile
+    srv = RespServer("127.0.0.1", 0).start()
+    try:
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3), torch.nn.Flatten(), torch.nn.LazyLinear(6))
+        model(torch.zeros(1, 3, 16, 16))
+        with tempfile.TemporaryDirectory() as d:
+            cfg = d + "/config.yaml"
+            open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,16,16\n  filter: topN(1)\n"
+                                 "params:\n  batch_size: 4\n" % srv.port)
+            s = ClusterServing(cfg, model=model, device=gpu)
+            inq, outq = InputQueue(cfg), OutputQueue(cfg)
+            rng = np.random.default_rng(0)
+            for i in range(5):
+                inq.enqueue_image("im%d" % i, rng.integers(0, 255, (20, 24, 3)).astype(np.uint8))
+            assert s.run(max_records=5, idle_timeout=10) == 5
+            res = outq.dequeue()
+            assert len(res) == 5 and all(v.startswith("[[") for v in res.values())
+    finally:
+        srv.shutdown()
+        srv.server_close()
