@@ -1,0 +1,117 @@
+"""TFPark API on the engine (test_tf_optimizer.py / test_tfpark_model.py /
+test_gan_estimator.py / GanOptimMethodSpec analogues)."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from zoo.common import triggers as T
+from zoo.common.nncontext import init_nncontext
+
+
+@pytest.fixture(scope="module", autouse=True)
+def ctx():
+    return init_nncontext()
+
+
+def _data(n=128):
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((n, 5)).astype(np.float32)
+    return x, (x[:, :1] * 2 - x[:, 1:2]).astype(np.float32)
+
+
+def _net():
+    from zoo.pipeline.api.keras.layers import Dense
+    from zoo.pipeline.api.keras.models import Sequential
+    torch.manual_seed(0)
+    m = Sequential()
+    m.add(Dense(16, activation="relu", input_shape=(5,)))
+    m.add(Dense(1))
+    return m
+
+
+def test_keras_model_fit_evaluate_predict_batches(tmp_path):
+    from zoo.tfpark import KerasModel, TFDataset
+    x, y = _data()
+    from zoo.pipeline.api.keras.optimizers import Adam
+    km = KerasModel(_net(), optimizer=Adam(lr=0.01), loss="mse")
+    before = km.evaluate(x, y)[0]
+    km.fit(TFDataset.from_ndarrays((x, y), batch_size=16, val_tensors=(x, y)), epochs=15)
+    assert km.evaluate(x, y)[0] < 0.3 * before
+    assert km.predict(x).shape == (128, 1)
+    l0 = km.train_on_batch(x[:16], y[:16])
+    assert np.isfinite(l0)
+    km.save_weights(str(tmp_path / "w"))
+    w = km.get_weights()
+    km.set_weights([np.zeros_like(a) for a in w])
+    km.load_weights(str(tmp_path / "w"))
+    assert all(np.allclose(a, b) for a, b in zip(km.get_weights(), w))
+
+
+def test_tfoptimizer_from_keras_and_dataframe():
+    from zoo.tfpark import KerasModel, TFDataset, TFOptimizer
+    x, y = _data(64)
+    df = pd.DataFrame({"f": list(x), "label": y[:, 0]})
+    ds = TFDataset.from_dataframe(df, ["f"], ["label"], batch_size=16)
+    m = _net()
+    m.compile("sgd", "mse")
+    before = m.evaluate(x, y[:, 0])[0]
+    opt = TFOptimizer.from_keras(m, ds, optim_method="adam")
+    opt.set_gradient_clipping_by_l2_norm(10.0)
+    opt.optimize(T.MaxEpoch(10))
+    assert m.evaluate(x, y[:, 0])[0] < before
+    with pytest.raises(NotImplementedError):
+        TFOptimizer.from_loss(None, None)
+
+
+def test_tfestimator_model_fn():
+    from zoo.tfpark import TFEstimator, TFEstimatorSpec
+    x, y = _data(64)
+    lin = torch.nn.Linear(5, 1)
+
+    def model_fn(features, labels, mode, params):
+        pred = lin(features)
+        loss = None if labels is None else torch.nn.functional.mse_loss(pred, labels)
+        return TFEstimatorSpec(mode, pred, loss)
+
+    def input_fn():
+        for i in range(0, 64, 16):
+            yield torch.from_numpy(x[i:i + 16]), torch.from_numpy(y[i:i + 16])
+    from zoo.pipeline.api.keras.optimizers import Adam
+    est = TFEstimator.from_model_fn(model_fn, [lin], optimizer=Adam(lr=0.05))
+    before = est.evaluate(input_fn)["loss"]
+    est.train(input_fn, steps=200)
+    assert est.evaluate(input_fn)["loss"] < 0.2 * before
+    assert est.predict(input_fn).shape == (64, 1)
+
+
+def test_gan_optim_method_schedule():
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.tfpark import GanOptimMethod
+    om = GanOptimMethod(SGD(learningrate=1.0), SGD(learningrate=1.0), d_steps=2, g_steps=1, g_param_size=3)
+    master = torch.zeros(8)
+    for k in range(3):
+        om.step(master, torch.ones(8))
+    # two D steps moved the tail, one G step the head
+    assert torch.allclose(master[:3], -torch.ones(3)) and torch.allclose(master[3:], -2 * torch.ones(5))
+
+
+def test_gan_estimator_learns_mean():
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.tfpark import GANEstimator
+    torch.manual_seed(0)
+    G = torch.nn.Sequential(torch.nn.Linear(2, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+    D = torch.nn.Sequential(torch.nn.Linear(1, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+    bce = torch.nn.functional.binary_cross_entropy_with_logits
+
+    def g_loss(fake_logits):
+        return bce(fake_logits, torch.ones_like(fake_logits))
+
+    def d_loss(real_logits, fake_logits):
+        return bce(real_logits, torch.ones_like(real_logits)) + bce(fake_logits, torch.zeros_like(fake_logits))
+    est = GANEstimator(G, D, g_loss, d_loss, Adam(lr=5e-3), Adam(lr=5e-3), noise_dim=2)
+    real = torch.randn(4096, 1) * 0.5 + 3.0
+    data = [real[i:i + 64] for i in range(0, 4096, 64)]
+    est.train(data, 1200)
+    gen = est.generate(2000)
+    assert abs(float(gen.mean()) - 3.0) < 0.6, float(gen.mean())
