@@ -1,0 +1,116 @@
+"""AutoML / Zouwu / XShards (test_time_sequence_predictor.py, test_forecast.py,
+test_shard.py analogues). Reference fixture: pyzoo/test/zoo/resources/xshard/*.csv."""
+import os
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from zoo.common.nncontext import init_nncontext
+
+XS = "/root/reference/pyzoo/test/zoo/resources/xshard"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def ctx():
+    return init_nncontext()
+
+
+def _ts(n=300):
+    dt = pd.date_range("2020-01-01", periods=n, freq="h")
+    v = np.sin(np.arange(n) / 6.0) + 0.05 * np.random.default_rng(0).standard_normal(n)
+    return pd.DataFrame({"datetime": dt, "value": v})
+
+
+def test_metrics():
+    from zoo.automl.common.metrics import Evaluator
+    y = np.array([1.0, 2.0, 4.0])
+    p = np.array([1.0, 2.5, 3.0])
+    assert Evaluator.evaluate("mse", y, p, "uniform_average") == pytest.approx((0.25 + 1) / 3)
+    assert Evaluator.evaluate("mae", y, p, "uniform_average") == pytest.approx(0.5)
+    assert Evaluator.evaluate("r2", y, y, "uniform_average") == pytest.approx(1.0)
+    assert Evaluator.evaluate("smape", y, y, "uniform_average") == pytest.approx(0.0)
+
+
+def test_feature_transformer_rolling():
+    from zoo.automl.feature.time_sequence import TimeSequenceFeatureTransformer
+    df = _ts(50)
+    ft = TimeSequenceFeatureTransformer(future_seq_len=2)
+    x, y = ft.fit_transform(df, past_seq_len=4, selected_features=["HOUR", "IS_WEEKEND"])
+    assert x.shape == (45, 4, 3) and y.shape == (45, 2)
+    # target column is first; y is the scaled target of the next 2 steps
+    assert np.allclose(x[1, -1, 0], y[0, 0])
+    back = ft.post_processing(df, y, True)
+    assert np.allclose(back[:, 0], df["value"].values[4:49], atol=1e-6)
+
+
+def test_search_expand_grid_random():
+    from zoo.automl.search import GridSearch, RandomSample, expand
+    cfgs = expand({"a": GridSearch([1, 2]), "b": RandomSample(lambda s: s["a"] * 10), "c": 5}, num_samples=2)
+    assert len(cfgs) == 4 and {c["b"] for c in cfgs} == {10, 20} and all(c["c"] == 5 for c in cfgs)
+
+
+def test_time_sequence_predictor_fit_predict_save(tmp_path):
+    from zoo.automl.config.recipe import LSTMGridRandomRecipe
+    from zoo.automl.pipeline import load_ts_pipeline
+    from zoo.automl.regression import TimeSequencePredictor
+    df = _ts()
+    train, val = df[:240], df[240:]
+    tsp = TimeSequencePredictor(future_seq_len=1)
+    recipe = LSTMGridRandomRecipe(num_rand_samples=1, epochs=3, training_iteration=2, look_back=6,
+                                  lstm_1_units=[16], lstm_2_units=[8, 16], batch_size=[32])
+    ppl = tsp.fit(train, val, metric="mse", recipe=recipe)
+    assert len(tsp.trials) == 2
+    mse = ppl.evaluate(val, ["mse"], "uniform_average")[0]
+    assert mse < np.var(val["value"].values)
+    pred = ppl.predict(val)
+    assert list(pred.columns) == ["datetime", "value"] and len(pred) == len(val) - 6 + 1
+    p = ppl.save(str(tmp_path / "ppl"))
+    ppl2 = load_ts_pipeline(p)
+    assert np.allclose(ppl2.predict(val)["value"].values, pred["value"].values, atol=1e-5)
+    mean, unc = ppl.predict_with_uncertainty(val, n_iter=5)
+    assert unc.shape[0] == len(mean)
+
+
+def test_mtnet_and_seq2seq_models_forward():
+    import torch
+    from zoo.automl.model import LSTMSeq2Seq, MTNet
+    x = torch.randn(4, 9, 3)
+    assert MTNet(3, 2, time_step=3, long_num=2, ar_window=2)(x).shape == (4, 2)
+    assert LSTMSeq2Seq(3, 3, latent_dim=8)(x).shape == (4, 3)
+
+
+def test_zouwu_forecasters_and_autots(tmp_path):
+    from zoo.automl.config.recipe import SmokeRecipe
+    from zoo.zouwu.autots import AutoTSTrainer, TSPipeline
+    from zoo.zouwu.model import LSTMForecaster, MTNetForecaster
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((64, 6, 2)).astype(np.float32)
+    y = x[:, -1, :1] * 0.5
+    f = LSTMForecaster(target_dim=1, feature_dim=2, lr=0.01)
+    before = f.evaluate(x, y)[0]
+    f.fit(x, y, batch_size=16, epochs=20)
+    assert f.evaluate(x, y)[0] < before
+    m = MTNetForecaster(target_dim=1, feature_dim=2, long_series_num=2, series_length=2, ar_window_size=2,
+                        cnn_height=2)
+    assert m.predict(m.preprocess_input(x)).shape == (64, 1)
+    df = _ts(120)
+    ppl = AutoTSTrainer(horizon=1).fit(df[:100], df[100:], recipe=SmokeRecipe())
+    assert isinstance(ppl, TSPipeline) and len(ppl.predict(df[100:])) == 19
+    ppl.save(str(tmp_path / "p"))
+    assert len(TSPipeline.load(str(tmp_path / "p")).predict(df[100:])) == 19
+
+
+def test_xshards_read_apply_repartition(tmp_path):
+    from zoo import xshard
+    if os.path.isdir(XS):
+        shards = xshard.read_csv(XS)
+        assert shards.num_partitions() >= 1 and len(shards.concat()) > 0
+    for i in range(3):
+        pd.DataFrame({"a": np.arange(i * 10, i * 10 + 10), "b": 1.0}).to_csv(tmp_path / ("p%d.csv" % i), index=False)
+    s = xshard.read_csv(str(tmp_path))
+    assert s.num_partitions() == 3
+    s2 = s.apply(lambda df, k: df.assign(c=df["a"] * k), 2)
+    assert s2.concat()["c"].sum() == 2 * np.arange(30).sum()
+    r = s2.repartition(2)
+    assert r.num_partitions() == 2 and len(r.concat()) == 30
