@@ -31,6 +31,12 @@ struct BwdStats {
   float* sums;        // [2*K]
 };
 
+// Plain GEMM geometry (gemm256.hip): Y[M, N] = A[M, K] . B[N, K]^T
+struct GemmGeom {
+  int M, N, K;
+  int lda, ldb, ldy;   // leading dims (elements), all % 8 == 0
+};
+
 // Weight-gradient geometry (wgrad.hip).
 struct WgradGeom {
   int N, H, W, C;      // input activation (NHWC)

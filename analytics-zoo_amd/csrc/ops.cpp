@@ -14,10 +14,13 @@
 using zoo::ConvGeom;
 using zoo::WgradGeom;
 using zoo::BwdStats;
+using zoo::GemmGeom;
 
 extern "C" {
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
                      const zoo::BwdStats*, hipStream_t);
+hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, const void*, float*, const GemmGeom*,
+                       int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                             hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, const WgradGeom*, hipStream_t);
@@ -575,11 +578,64 @@ torch::Tensor resize_normalize(torch::Tensor in, int64_t Ho, int64_t Wo, std::ve
   return out;
 }
 
+
+// Y[M, N] = epilogue(A[M, K] . B[N, K]^T) on the 256x256 LDS-DMA kernel (gemm256.hip).
+torch::Tensor gemm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
+                   c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> stats, int64_t act, bool out_f32,
+                   bool out_bf16, c10::optional<torch::Tensor> bz, c10::optional<torch::Tensor> by,
+                   c10::optional<torch::Tensor> bmean, c10::optional<torch::Tensor> binv,
+                   c10::optional<torch::Tensor> bsums) {
+  req(a, at::kBFloat16, "a");
+  req(b, at::kBFloat16, "b");
+  TORCH_CHECK(a.dim() == 2 && b.dim() == 2, "gemm: 2-D operands");
+  const int M = a.size(0), K = a.size(1), N = b.size(0);
+  TORCH_CHECK(b.size(1) == K, "gemm: K mismatch");
+  TORCH_CHECK(K % 8 == 0 && N % 8 == 0, "gemm: K and N must be multiples of 8");
+  TORCH_CHECK(out_f32 || out_bf16, "gemm: no output requested");
+  GemmGeom g{M, N, K, K, K, N};
+  torch::Tensor y, yf;
+  if (out_bf16) y = torch::empty({M, N}, a.options());
+  if (out_f32) yf = torch::empty({M, N}, a.options().dtype(at::kFloat));
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == N, "gemm: bias shape");
+  }
+  if (resid.has_value() && resid->defined()) {
+    req(*resid, at::kBFloat16, "resid");
+    TORCH_CHECK(resid->numel() == (int64_t)M * N, "gemm: resid shape");
+  }
+  if (stats.has_value() && stats->defined()) {
+    req(*stats, at::kFloat, "stats");
+    TORCH_CHECK(stats->numel() == 2 * N && out_bf16, "gemm: stats must be [2*N] with bf16 output");
+  }
+  BwdStats bs{nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (bsums.has_value() && bsums->defined()) {
+    req(*bsums, at::kFloat, "bsums");
+    TORCH_CHECK(bsums->numel() == 2 * N && out_bf16, "gemm: bsums must be [2*N] with bf16 output");
+    TORCH_CHECK(by.has_value() && bmean.has_value() && binv.has_value(), "gemm: bstats needs y/mean/inv");
+    req(*by, at::kBFloat16, "by");
+    TORCH_CHECK(by->numel() == (int64_t)M * N, "gemm: by shape");
+    if (bz.has_value() && bz->defined()) {
+      req(*bz, at::kBFloat16, "bz");
+      TORCH_CHECK(bz->numel() == (int64_t)M * N, "gemm: bz shape");
+    }
+    bs = BwdStats{opt_ptr<void>(bz), by->data_ptr(), bmean->data_ptr<float>(), binv->data_ptr<float>(),
+                  bsums->data_ptr<float>()};
+  }
+  if (M == 0) return out_bf16 ? y : yf;
+  check_hip(zoo_gemm256(a.data_ptr(), b.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
+                        out_f32 ? yf.data_ptr<float>() : nullptr, opt_ptr<float>(bias), opt_ptr<void>(resid),
+                        opt_ptr<float>(stats), &g, (int)act, bs.sums ? &bs : nullptr, cur_stream()),
+            "gemm256");
+  return out_bf16 ? y : yf;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "zoo native gfx950 (MI355X) kernel library";
   m.def("resize_normalize", &resize_normalize);
+  m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);
   m.def("conv_wgrad", &conv_wgrad);

@@ -49,8 +49,12 @@ def main():
         t_z = timeit(lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0,
                                         None, [], None, None, None, None, None))
         t_t = float("nan") if a.zoo_only else timeit(lambda: torch.matmul(x, w.t()))
+        t_g = timeit(lambda: C.gemm(x, w, None, None, None, 0, False, True, None, None, None, None, None))
+        err = float((C.gemm(x, w, None, None, None, 0, True, False, None, None, None, None, None) -
+                     x.float() @ w.float().t()).abs().max() / (x.float() @ w.float().t()).abs().max())
         byts = 2.0 * (M * K + N * K + M * N)
-        rows.append({"M": M, "N": N, "K": K, "zoo_TF": round(f / t_z / 1e12, 1), "torch_TF": round(f / t_t / 1e12, 1),
+        rows.append({"M": M, "N": N, "K": K, "gemm256_TF": round(f / t_g / 1e12, 1), "gemm256_err": err,
+                     "zoo_TF": round(f / t_z / 1e12, 1), "torch_TF": round(f / t_t / 1e12, 1),
                      "zoo_us": round(t_z * 1e6, 1), "torch_us": round(t_t * 1e6, 1),
                      "zoo_TBps": round(byts / t_z / 1e12, 2)})
         print(json.dumps(rows[-1]), flush=True)

@@ -461,3 +461,24 @@ def test_serving_worker_on_gpu(gpu):
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+@pytest.mark.parametrize("mnk", [(256, 256, 64), (300, 264, 128), (1000, 512, 200), (512, 1024, 1024),
+                                 (77, 40, 24)])
+def test_gemm256_numerics_and_epilogue(gpu, mnk):
+    from zoo.ops import native
+    C = native()
+    M, N, K = mnk
+    a = (torch.randn(M, K, device=gpu) * 0.5).bfloat16()
+    b = (torch.randn(N, K, device=gpu) * 0.5).bfloat16()
+    ref = a.float() @ b.float().t()
+    y = C.gemm(a, b, None, None, None, 0, True, False, None, None, None, None, None)
+    assert rel(y, ref) < 2e-3
+    bias = torch.randn(N, device=gpu)
+    r = torch.randn(M, N, device=gpu).bfloat16()
+    stats = torch.zeros(2 * N, device=gpu)
+    yb = C.gemm(a, b, bias, r, stats, 1, False, True, None, None, None, None, None)
+    ref2 = torch.relu(ref + bias + r.float())
+    assert rel(yb, ref2) < 1e-2
+    q = yb.float()
+    assert rel(stats, torch.cat([q.sum(0), (q * q).sum(0)])) < 1e-3
