@@ -58,6 +58,10 @@ hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, 
 hipError_t zoo_resize_normalize(const void*, void*, int, int, int, int, int, int, const float*, const float*, int, int,
                                 hipStream_t);
 hipError_t zoo_embedding_bwd(const void*, int, const int64_t*, float*, int, int, int, int64_t, float, hipStream_t);
+hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
+                        float, int, hipStream_t);
+hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
+                        float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
 
 namespace {
@@ -630,6 +634,63 @@ torch::Tensor gemm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor
   return out_bf16 ? y : yf;
 }
 
+
+// ---- fused attention: q [B,H,L,D], k/v [B,H,S,D] bf16, optional additive key mask [B,S] fp32 ----
+void attn_check(const torch::Tensor& q, const torch::Tensor& k, const torch::Tensor& v,
+                const c10::optional<torch::Tensor>& mask) {
+  req(q, at::kBFloat16, "q");
+  req(k, at::kBFloat16, "k");
+  req(v, at::kBFloat16, "v");
+  TORCH_CHECK(q.dim() == 4 && k.dim() == 4 && v.dim() == 4, "attention: q/k/v must be [B,H,T,D]");
+  TORCH_CHECK(k.sizes() == v.sizes(), "attention: k and v shapes differ");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(1) == k.size(1) && q.size(3) == k.size(3),
+              "attention: q/k batch, heads or head_dim differ");
+  const int64_t D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(q.size(0) * q.size(1) < 65536, "attention: B*H must be < 65536");
+  if (mask.has_value() && mask->defined()) {
+    req(*mask, at::kFloat, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == q.size(0) && mask->size(1) == k.size(2),
+                "attention: mask must be [B, S]");
+  }
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v,
+                                    c10::optional<torch::Tensor> mask, bool causal) {
+  attn_check(q, k, v, mask);
+  const int B = q.size(0), H = q.size(1), L = q.size(2), S = k.size(2), D = q.size(3);
+  auto o = torch::empty_like(q);
+  auto lse = torch::empty({B, H, L}, q.options().dtype(at::kFloat));
+  if (q.numel() == 0) return {o, lse};
+  check_hip(zoo_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask), o.data_ptr(),
+                         lse.data_ptr<float>(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal,
+                         cur_stream()),
+            "attn_fwd");
+  return {o, lse};
+}
+
+std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
+                                    c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor lse,
+                                    bool causal) {
+  attn_check(q, k, v, mask);
+  req(dout, at::kBFloat16, "dout");
+  req(o, at::kBFloat16, "o");
+  req(lse, at::kFloat, "lse");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes(), "attn_bwd: dout/o shape");
+  const int B = q.size(0), H = q.size(1), L = q.size(2), S = k.size(2), D = q.size(3);
+  TORCH_CHECK(lse.numel() == (int64_t)B * H * L, "attn_bwd: lse shape");
+  auto dq = torch::empty_like(q);
+  auto dk = torch::empty_like(k);
+  auto dv = torch::empty_like(v);
+  auto delta = torch::empty({B, H, L}, q.options().dtype(at::kFloat));
+  if (q.numel() == 0 || k.numel() == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
+  check_hip(zoo_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask),
+                         o.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                         dv.data_ptr(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, cur_stream()),
+            "attn_bwd");
+  return {dq, dk, dv};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -660,4 +721,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
+  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_bwd", &attn_bwd);
 }

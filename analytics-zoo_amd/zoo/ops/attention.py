@@ -1,11 +1,12 @@
 """Scaled dot-product attention (TransformerLayer.attn, TransformerLayer.scala:163-181).
 
 ``attention(q, k, v, mask=None, causal=False, dropout_p=0.0)`` with q/k/v
-shaped [batch, heads, seq, head_dim]. On the GPU with bf16 and head_dim in
-{64, 128}, no dropout and an additive/causal mask, the fused native HIP kernel
-(online softmax, O(L) memory; ``zoo._C.attn_fwd``/``attn_bwd``) is used when it
-has been built; otherwise the materialised reference path (two batched GEMMs
-around a softmax) runs. The reference path is also the CPU implementation.
+shaped [batch, heads, seq, head_dim]. On the GPU with head_dim in {64, 128},
+no dropout and a causal and/or additive [B, S] key mask, the fused native HIP
+kernel runs (csrc/kernels/attention.hip: online softmax, O(L) memory, bf16
+MFMA; ``zoo._C.attn_fwd``/``attn_bwd``). Other configurations (dropout on the
+probabilities, general masks) take the materialised path (two batched GEMMs
+around a softmax), which is also the CPU implementation.
 """
 import math
 
@@ -40,26 +41,31 @@ class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, do):
         q, k, v, mask, o, lse = ctx.saved_tensors
-        dq, dk, dv = native().attn_bwd(do.contiguous(), q, k, v, mask, o, lse, ctx.causal)
+        dq, dk, dv = native().attn_bwd(do.to(torch.bfloat16).contiguous(), q, k, v, mask, o, lse, ctx.causal)
         return dq, dk, dv, None, None
 
 
 def _native_ok(q, k, v, mask, dropout_p, training):
-    if not (q.is_cuda and available() and hasattr(native(), "attn_fwd")):
+    if not q.is_cuda:
         return False
-    if q.dtype != torch.bfloat16 or q.shape[-1] not in (64, 128) or (dropout_p > 0 and training):
+    if q.shape[-1] not in (64, 128) or (dropout_p > 0 and training) or q.dim() != 4:
         return False
-    if mask is not None and (mask.dtype != torch.float32 or mask.dim() != 2):
+    if mask is not None and (mask.dim() != 2 or tuple(mask.shape) != (q.shape[0], k.shape[-2])):
         return False
-    return q.shape[-2] % 64 == 0 and k.shape[-2] % 64 == 0
+    if not available():
+        raise RuntimeError("zoo native kernels are not built: run tools/build_native.py (fused attention)")
+    return True
 
 
 def attention(q, k, v, mask=None, causal=False, dropout_p=0.0, training=False):
     """mask: additive float mask broadcastable to [B, H, L, S]; a [B, S] key
     mask (0 keep / -10000 drop, BERT style) takes the fused path."""
     if _native_ok(q, k, v, mask, dropout_p, training):
-        return _FlashAttnFn.apply(q.contiguous(), k.contiguous(), v.contiguous(),
-                                  None if mask is None else mask.contiguous(), bool(causal))
+        dt = q.dtype
+        bf = torch.bfloat16
+        o = _FlashAttnFn.apply(q.to(bf).contiguous(), k.to(bf).contiguous(), v.to(bf).contiguous(),
+                               None if mask is None else mask.float().contiguous(), bool(causal))
+        return o if dt == bf else o.to(dt)
     m = mask
     if m is not None and m.dim() == 2:
         m = m[:, None, None, :]
