@@ -10,15 +10,14 @@
 // Layouts: q/o [B][H][L][D], k/v [B][H][S][D] bf16, D in {64, 128};
 // lse [B][H][L] fp32 = ln sum_k exp(logit) (saved for the backward pass).
 //
-// MFMA orientation (v_mfma_f32_16x16x32_bf16; A lane l: row l&15, k 8(l>>4)+j;
-// B lane l: k 8(l>>4)+j, col l&15; C: row 4(l>>4)+r, col l&15):
-//   forward  S^T = K Q^T   -> a lane owns ONE query row (col) and 16 keys
-//                              (rows), so row max / sum need only 2 shuffles
+// All products run on v_mfma_f32_32x32x16_bf16 (A lane l: row l&31, k 8(l>>5)+j;
+// B lane l: k 8(l>>5)+j, col l&31; C reg i: row 8(i>>2)+4(l>>5)+(i&3), col l&31):
+//   forward  S^T = K Q^T   -> a lane owns ONE query row (col) and 32 keys
+//                              (rows): row max needs one cross-half shuffle
 //            O^T = V^T P^T -> P^T comes straight from the S^T accumulators
-//                              (k order permuted identically on both sides:
-//                              k-slot (g, j) = key 4g+j (j<4) / 16+4g+j-4),
-//                              V^T is read from the row-major V tile with the
-//                              hardware transposing ds_read_b64_tr_b16.
+//                              (k-step s = regs 8s..8s+7, a permuted key order
+//                              that the transposed V^T read reproduces with
+//                              the hardware ds_read_b64_tr_b16)
 //   dK/dV    S = Q K^T, dP = dO V^T (key on the lane, K/V in registers),
 //            dV^T += dO^T P, dK^T += Q^T dS  (Q/dO tiles transposed-read)
 //   dQ       S^T, dP^T as in the forward, dQ^T += K^T dS^T
@@ -31,13 +30,26 @@ namespace zoo {
 constexpr float kLog2e = 1.4426950408889634f;
 constexpr float kLn2 = 0.6931471805599453f;
 
-// [64][D] bf16 tile, 16-byte chunks XOR-swizzled by row so that the 16 rows of
-// a half-wave's row read land in distinct bank groups.
+// [64][D] bf16 tile, 16-byte chunks XOR-swizzled by row. The swizzle is chosen
+// for BOTH reads of the tile (MI355X_MICROARCH.md §LDS lane groups):
+//  * ds_read_b128 row fragments (16 rows of a lane group, one logical chunk):
+//    the 16 rows must hit 16 distinct 16-byte bank slots;
+//  * ds_read_b64_tr_b16 (4 consecutive rows x 4 consecutive chunks per 32-lane
+//    half): the 4 rows' chunk groups must land on disjoint bank slots.
+// D = 128 (256-B rows): chunk ^= ((row&3)<<2) | ((row>>2)&3)
+// D = 64 (128-B rows, two rows per bank line): chunk ^= (((row>>1)&1)<<2) | ((row>>2)&3)
+template <int D>
+ZOO_DEV int swz(int row) {
+  return D == 128 ? (((row & 3) << 2) | ((row >> 2) & 3)) : ((((row >> 1) & 1) << 2) | ((row >> 2) & 3));
+}
 template <int D>
 ZOO_DEV int t_off(int row, int col) {
-  constexpr int NCH = D / 8;
-  return row * D + ((((col >> 3) ^ row) & (NCH - 1)) << 3) + (col & 7);
+  return row * D + ((((col >> 3) ^ swz<D>(row)) & (D / 8 - 1)) << 3) + (col & 7);
 }
+
+// exp2 straight to v_exp_f32 (no denormal range fix-up: softmax terms that
+// small are zero at bf16 anyway)
+ZOO_DEV float fexp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // 16-byte row fragment: A/B operand with k along the tile's columns
 template <int D>
@@ -45,218 +57,246 @@ ZOO_DEV bf16x8 row_frag(const bf16_t* tile, int row, int col) {
   return *reinterpret_cast<const bf16x8*>(tile + t_off<D>(row, col));
 }
 
-// transposed fragment: operand element j of lane-group g = tile[rowk(g,j)][col0 + (l&15)]
-// with the permuted k order rowk = base + 4g + j (j<4), base + 16 + 4g + j-4 (j>=4)
-template <int D>
-ZOO_DEV bf16x8 tr_frag(const bf16_t* tile, int base, int col0, int lane) {
-  const int g = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
-  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_i16x4*)(tile + t_off<D>(base + 4 * g + tq, col0 + 4 * tp)));
-  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (lds_i16x4*)(tile + t_off<D>(base + 16 + 4 * g + tq, col0 + 4 * tp)));
-  typedef short i16x8 __attribute__((ext_vector_type(8)));
-  i16x8 v;
-  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
-  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
-  return __builtin_bit_cast(bf16x8, v);
-}
-
-// two accumulator tiles (k = 4g+r and 16+4g+r) -> one bf16 operand fragment
-ZOO_DEV bf16x8 pack_frag(const f32x4& a, const f32x4& b) {
-  bf16x8 r;
-  r[0] = (__bf16)a[0]; r[1] = (__bf16)a[1]; r[2] = (__bf16)a[2]; r[3] = (__bf16)a[3];
-  r[4] = (__bf16)b[0]; r[5] = (__bf16)b[1]; r[6] = (__bf16)b[2]; r[7] = (__bf16)b[3];
-  return r;
-}
-
 ZOO_DEV bf16x8 load_frag(const bf16_t* p, bool ok) {
   uint4 v = ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0, 0, 0, 0);
   return __builtin_bit_cast(bf16x8, v);
 }
 
-// Register-staged double-buffered copy of `NT` [64][D] tiles (rows r0.., bounded by nrows)
-template <int D, int NT>
-struct TileStage {
-  static constexpr int PER = 64 * D / 8 / 256;  // 16-byte chunks per thread per tile
-  uint4 reg[NT][PER];
-  ZOO_DEV void load(const bf16_t* const* src, int r0, int nrows) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int idx = threadIdx.x + 256 * i;
-        const int row = idx / (D / 8), ch = idx % (D / 8);
-        const int r = r0 + row;
-        reg[t][i] = r < nrows ? *reinterpret_cast<const uint4*>(src[t] + (size_t)r * D + ch * 8)
-                              : make_uint4(0, 0, 0, 0);
-      }
-  }
-  ZOO_DEV void store(bf16_t* const* dst) {
-#pragma unroll
-    for (int t = 0; t < NT; ++t)
-#pragma unroll
-      for (int i = 0; i < PER; ++i) {
-        const int idx = threadIdx.x + 256 * i;
-        const int row = idx / (D / 8), ch = idx % (D / 8);
-        *reinterpret_cast<uint4*>(dst[t] + t_off<D>(row, ch * 8)) = reg[t][i];
-      }
-  }
-};
+// ---------------------------------------------------------------------------
+// forward: NW waves x 32 query rows per block on v_mfma_f32_32x32x16_bf16
+// (a 32x32x16 MFMA blocks vector issue for 8 of its 32 cycles, leaving 3x the
+// room of 16x16x32 for the softmax VALU work, MI355X_MICROARCH.md constants).
+//   S^T[key][q] = K Q^T: A = K rows (LDS), B = Q (registers); accumulator reg
+//   i of tile kt holds key 32kt + 8(i>>2) + 4h + (i&3) for query q0 + (l&31).
+//   O^T[d][q] += V^T P^T: B = P^T packed straight from the accumulators
+//   (k-step s = regs 8s..8s+7), A = V^T via ds_read_b64_tr_b16 in the same
+//   permuted key order.
+// Online softmax in the log2 domain with a deferred max: the running max only
+// moves when a tile's max exceeds it by > kDeferTh (P <= 2^kDeferTh stays exact
+// in fp32 sums and bf16 operands), so the O rescale is rare and wave-uniform.
+// ---------------------------------------------------------------------------
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-// ---------------------------------------------------------------------------
-// forward: block = 4 waves x 32 query rows; 64-key K/V tiles double-buffered
-// ---------------------------------------------------------------------------
+ZOO_DEV f32x16 mfma32(const bf16x8& a, const bf16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+constexpr float kDeferTh = 8.0f;
+
+// A operand of a 32x32x16 MFMA = tile^T: lane (row d = col0 + (l&31), half h) gets
+// keys kbase + 8(j>>2) + 4h + (j&3), j = 0..7, of column d
 template <int D>
-__global__ __launch_bounds__(256, D == 128 ? 1 : 2) void attn_fwd_kernel(const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K,
-                                                          const bf16_t* __restrict__ V,
-                                                          const float* __restrict__ mask, bf16_t* __restrict__ O,
-                                                          float* __restrict__ LSE, int H, int L, int S, float scale,
-                                                          int causal) {
+ZOO_DEV bf16x8 tr_frag32(const bf16_t* tile, int kbase, int col0, int lane) {
+  const int gq = lane >> 4, h = gq >> 1, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int col = col0 + 16 * (gq & 1) + 4 * tp;
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + t_off<D>(kbase + 4 * h + tq, col)));
+  const i16x4 hi =
+      __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(tile + t_off<D>(kbase + 8 + 4 * h + tq, col)));
+  const uint2 a = __builtin_bit_cast(uint2, lo), b = __builtin_bit_cast(uint2, hi);
+  return __builtin_bit_cast(bf16x8, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+ZOO_DEV bf16x8 pack8_acc(const f32x16& a, int base) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)a[base + j];
+  return r;
+}
+
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(1))) const void gl_void;
+ZOO_DEV void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Stage two [64][D] tiles (rows r0.., clamped to nrows-1: rows past the end
+// only ever meet zero probabilities) with LDS-DMA: one wave-instruction writes a
+// lane-linear 1-KiB piece, the swizzle is applied on the per-lane SOURCE address
+// (position (row, pc) receives logical chunk pc ^ swz(row)). The NW waves of the
+// block split the pieces; no staging registers, no ds_write.
+template <int D, int NW>
+ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf16_t* dst1, int r0, int nrows) {
+  constexpr int PPT = D / 8;            // 1-KiB pieces per tile
+  constexpr int PPW = 2 * PPT / NW;     // pieces per wave
+  static_assert((2 * PPT) % NW == 0, "pieces must split evenly over the waves");
+  constexpr int RP = 512 / D;           // tile rows per piece
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int rsub = lane / (D / 8), pc = lane % (D / 8);
+#pragma unroll
+  for (int i = 0; i < PPW; ++i) {
+    const int gp = wid * PPW + i;
+    const bool second = gp >= PPT;
+    const int pp = second ? gp - PPT : gp;
+    const int row = pp * RP + rsub;
+    const int r = min(r0 + row, nrows - 1);
+    const bf16_t* sp = (second ? src1 : src0) + (size_t)r * D + ((pc ^ swz<D>(row)) << 3);
+    bf16_t* dp = (second ? dst1 : dst0) + pp * 512;
+    __builtin_amdgcn_global_load_lds((gl_void*)sp, (lds_void*)dp, 16, 0, 0);
+  }
+}
+
+template <int D, int NW, bool HAS_MASK>
+__global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const float* __restrict__ mask, bf16_t* __restrict__ O, float* __restrict__ LSE, int H, int L, int S,
+    float scale, int causal) {
+  constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);  // [2][64][D]
   bf16_t* Vs = Ks + 2 * 64 * D;                  // [2][64][D]
-  constexpr int DC = D / 32, DT = D / 16;
+  float* Ms = reinterpret_cast<float*>(Vs + 2 * 64 * D);  // [2][64] additive mask (log2 units)
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int bh = blockIdx.y, b = bh / H;
-  const bf16_t* Qp = Q + (size_t)bh * L * D;
   const bf16_t* Kp = K + (size_t)bh * S * D;
   const bf16_t* Vp = V + (size_t)bh * S * D;
-  const float* mrow = mask ? mask + (size_t)b * S : nullptr;
-  const int qblk = blockIdx.x * 128, q0 = qblk + wid * 32;
+  const float* mrow = HAS_MASK ? mask + (size_t)b * S : nullptr;
+  // causal: heaviest query blocks (largest index) first
+  const int qb = causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int qblk = qb * 32 * NW, q0 = qblk + wid * 32, q = q0 + lr;
   const int coff = S - L;  // causal: key allowed iff key <= q + coff
   const float c2 = scale * kLog2e;
 
-  bf16x8 qf[2][DC];
+  bf16x8 qf[KS];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
-#pragma unroll
-    for (int dc = 0; dc < DC; ++dc) {
-      const int q = q0 + 16 * s + li;
-      qf[s][dc] = load_frag(Qp + (size_t)q * D + 32 * dc + 8 * g, q < L);
-    }
+  for (int ks = 0; ks < KS; ++ks) qf[ks] = load_frag(Q + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q < L);
 
-  f32x4 o[2][DT];
+  f32x16 o[DT];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
+  for (int i = 0; i < DT; ++i)
 #pragma unroll
-    for (int i = 0; i < DT; ++i) o[s][i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[2] = {-INFINITY, -INFINITY}, lsum[2] = {0.f, 0.f};
+    for (int r = 0; r < 16; ++r) o[i][r] = 0.f;
+  float m = -INFINITY, lsum = 0.f;
 
   int kv_end = S;
-  if (causal) kv_end = min(S, qblk + 127 + coff + 1);
+  if (causal) kv_end = min(S, qblk + 32 * NW - 1 + coff + 1);
   const int ntiles = kv_end > 0 ? (kv_end + 63) / 64 : 0;
 
-  TileStage<D, 2> st;
-  const bf16_t* srcs[2] = {Kp, Vp};
+  float mreg = 0.f;
+  auto load_mask = [&](int kv0) {
+    if (HAS_MASK && threadIdx.x < 64) {
+      const int key = kv0 + threadIdx.x;
+      mreg = key < S ? mrow[key] * kLog2e : -INFINITY;
+    }
+  };
+  auto store_mask = [&](int buf) {
+    if (HAS_MASK && threadIdx.x < 64) Ms[buf * 64 + threadIdx.x] = mreg;
+  };
   if (ntiles > 0) {
-    st.load(srcs, 0, S);
-    bf16_t* d0[2] = {Ks, Vs};
-    st.store(d0);
+    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S);
+    load_mask(0);
+    wait_vm0();
+    store_mask(0);
   }
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1, kv0 = t * 64;
-    if (t + 1 < ntiles) st.load(srcs, kv0 + 64, S);
+    if (t + 1 < ntiles) {
+      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S);
+      load_mask(kv0 + 64);
+    }
     const bf16_t* kt_ = Ks + buf * 64 * D;
     const bf16_t* vt_ = Vs + buf * 64 * D;
-    // wave-uniform skip of tiles entirely above this wave's causal diagonal
-    const bool active = !(causal && kv0 > q0 + 31 + coff) && q0 < L;
-    if (active) {
-      f32x4 sc[2][4];
+    // wave-uniform: skip tiles entirely above this wave's causal diagonal
+    if (q0 < L && !(causal && kv0 > q0 + 31 + coff)) {
+      f32x16 s[2];
+      const f32x16 z16 = {};
+      // K fragments one k-step ahead of their MFMAs (keeps LDS latency off the chain)
+      bf16x8 ka[2][2];
+      ka[0][0] = row_frag<D>(kt_, lr, 8 * h);
+      ka[0][1] = row_frag<D>(kt_, 32 + lr, 8 * h);
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4) sc[s][k4] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int dc = 0; dc < DC; ++dc) {
-          const bf16x8 a = row_frag<D>(kt_, 16 * k4 + li, 32 * dc + 8 * g);
-          sc[0][k4] = mfma16(a, qf[0][dc], sc[0][k4]);
-          sc[1][k4] = mfma16(a, qf[1][dc], sc[1][k4]);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
+          ka[(ks + 1) & 1][0] = row_frag<D>(kt_, lr, 16 * (ks + 1) + 8 * h);
+          ka[(ks + 1) & 1][1] = row_frag<D>(kt_, 32 + lr, 16 * (ks + 1) + 8 * h);
         }
-      // additive key mask for this lane's 16 keys (same for both query subtiles)
-      float madd[4][4];
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + 16 * k4 + 4 * g + r;
-          madd[k4][r] = key < S ? (mrow ? mrow[key] * kLog2e : 0.f) : -INFINITY;
-        }
-      bf16x8 pf[2][2];
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int q = q0 + 16 * s + li;
-        float mx = -INFINITY;
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int key = kv0 + 16 * k4 + 4 * g + r;
-            float x = sc[s][k4][r] * c2 + madd[k4][r];
-            if (causal && key > q + coff) x = -INFINITY;
-            sc[s][k4][r] = x;
-            mx = fmaxf(mx, x);
-          }
-        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-        const float mnew = fmaxf(m[s], mx);
-        const float base = mnew == -INFINITY ? 0.f : mnew;
-        const float alpha = exp2f(m[s] - base);
-        float sum = 0.f;
-#pragma unroll
-        for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const float p = exp2f(sc[s][k4][r] - base);
-            sc[s][k4][r] = p;
-            sum += p;
-          }
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        lsum[s] = lsum[s] * alpha + sum;
-        m[s] = mnew;
-#pragma unroll
-        for (int i = 0; i < DT; ++i) o[s][i] *= alpha;
-        pf[s][0] = pack_frag(sc[s][0], sc[s][1]);
-        pf[s][1] = pack_frag(sc[s][2], sc[s][3]);
+        s[0] = mfma32(ka[ks & 1][0], qf[ks], ks == 0 ? z16 : s[0]);
+        s[1] = mfma32(ka[ks & 1][1], qf[ks], ks == 0 ? z16 : s[1]);
       }
+
+      // logits in log2 units: x = s*c2 (+ mask); -inf outside [0, S) / above the diagonal
+      const bool edge = (kv0 + 64 > S) || (causal && kv0 + 63 > q0 + coff);
+      if (HAS_MASK) {
+        const float* mk = Ms + buf * 64;
 #pragma unroll
-      for (int i = 0; i < DT; ++i)
+        for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-          const bf16x8 a = tr_frag<D>(vt_, 32 * c, 16 * i, lane);
-          o[0][i] = mfma16(a, pf[0][c], o[0][i]);
-          o[1][i] = mfma16(a, pf[1][c], o[1][i]);
+          for (int i4 = 0; i4 < 4; ++i4) {
+            const float4 mv = *reinterpret_cast<const float4*>(mk + 32 * kt + 8 * i4 + 4 * h);
+            s[kt][4 * i4 + 0] = s[kt][4 * i4 + 0] * c2 + mv.x;
+            s[kt][4 * i4 + 1] = s[kt][4 * i4 + 1] * c2 + mv.y;
+            s[kt][4 * i4 + 2] = s[kt][4 * i4 + 2] * c2 + mv.z;
+            s[kt][4 * i4 + 3] = s[kt][4 * i4 + 3] * c2 + mv.w;
+          }
+      }
+      if (edge) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const int key = kv0 + 32 * kt + 8 * (i >> 2) + 4 * h + (i & 3);
+            if (key >= S || (causal && key > q + coff)) s[kt][i] = -INFINITY;
+          }
+      }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mx = fmaxf(mx, s[kt][i]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if (!HAS_MASK) mx *= c2;
+      const bool upd = mx > m + kDeferTh;
+      if (__ballot(upd)) {
+        const float mnew = upd ? mx : m;
+        const float alpha = mnew == m ? 1.f : fexp2(m - mnew);
+        lsum *= alpha;
+#pragma unroll
+        for (int i = 0; i < DT; ++i) o[i] *= alpha;
+        m = mnew;
+      }
+      const float base = m == -INFINITY ? 0.f : m;
+      float ps[4] = {0.f, 0.f, 0.f, 0.f};  // independent partial sums (no serial add chain)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const float p = HAS_MASK ? fexp2(s[kt][i] - base) : fexp2(s[kt][i] * c2 - base);
+          s[kt][i] = p;
+          ps[i & 3] += p;
         }
+      lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      bf16x8 pf[4];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) pf[k4] = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(tr_frag32<D>(vt_, 16 * k4, 32 * dt, lane), pf[k4], o[dt]);
     }
     if (t + 1 < ntiles) {
-      bf16_t* dn[2] = {Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D};
-      st.store(dn);
+      wait_vm0();
+      store_mask(buf ^ 1);
     }
     __syncthreads();
   }
 
-  // epilogue: lane owns query row q, d = 16i + 4g .. +3 of every d-tile
+  // epilogue: reg i of o[dt] = O[q][32dt + 8(i>>2) + 4h + (i&3)]
+  lsum += __shfl_xor(lsum, 32, 64);
+  if (q >= L) return;
+  const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
+  bf16_t* orow = O + ((size_t)bh * L + q) * D;
 #pragma unroll
-  for (int s = 0; s < 2; ++s) {
-    const int q = q0 + 16 * s + li;
-    if (q >= L) continue;
-    const float inv = lsum[s] > 0.f ? 1.f / lsum[s] : 0.f;
-    bf16_t* orow = O + ((size_t)bh * L + q) * D;
+  for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
-    for (int i = 0; i < DT; ++i) {
+    for (int i4 = 0; i4 < 4; ++i4) {
       uint2 w;
-      w.x = pack2bf(o[s][i][0] * inv, o[s][i][1] * inv);
-      w.y = pack2bf(o[s][i][2] * inv, o[s][i][3] * inv);
-      *reinterpret_cast<uint2*>(orow + 16 * i + 4 * g) = w;
+      w.x = pack2bf(o[dt][4 * i4 + 0] * inv, o[dt][4 * i4 + 1] * inv);
+      w.y = pack2bf(o[dt][4 * i4 + 2] * inv, o[dt][4 * i4 + 3] * inv);
+      *reinterpret_cast<uint2*>(orow + 32 * dt + 8 * i4 + 4 * h) = w;
     }
-    if (g == 0) LSE[(size_t)bh * L + q] = lsum[s] > 0.f ? (m[s] + __log2f(lsum[s])) * kLn2 : INFINITY;
-  }
+  if (h == 0) LSE[(size_t)bh * L + q] = lsum > 0.f ? (m + __log2f(lsum)) * kLn2 : INFINITY;
 }
 
 // delta[row] = sum_d dO[row][d] * O[row][d]  (fp32), 16 lanes per row
@@ -280,53 +320,58 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// backward dK/dV: block = 4 waves x 16 keys (64 keys); 64-query Q/dO tiles
+// backward dK/dV on 32x32x16 MFMAs: block = 4 waves x 32 keys (128 keys), one
+// wave per SIMD (the dK/dV accumulators live in AGPRs); 64-query Q/dO tiles.
+//   S = Q K^T, dP = dO V^T with the key on the lane (K/V fragments in registers,
+//   Q/dO row fragments from LDS); reg i of tile qt <-> q = 32qt + 8(i>>2) + 4h + (i&3)
+//   dV^T += dO^T P, dK^T += Q^T dS: P / dS packed from the accumulators, dO^T /
+//   Q^T transposed-read from the same LDS tiles in that permuted q order.
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(
+template <int D, bool HAS_MASK>
+__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
     float scale, int causal) {
+  constexpr int KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);  // [2][64][D]
-  bf16_t* dOs = Qs + 2 * 64 * D;                 // [2][64][D]
-  float* lse_s = reinterpret_cast<float*>(dOs + 2 * 64 * D);  // [2][64] (log2 domain)
-  float* del_s = lse_s + 2 * 64;                               // [2][64]
-  constexpr int DC = D / 32, DT = D / 16;
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);                 // [2][64][D]
+  bf16_t* dOs = Qs + 2 * 64 * D;                                // [2][64][D]
+  float* lse_s = reinterpret_cast<float*>(dOs + 2 * 64 * D);    // [2][64] (log2 units)
+  float* del_s = lse_s + 2 * 64;                                // [2][64]
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int bh = blockIdx.y, b = bh / H;
   const bf16_t* Qp = Q + (size_t)bh * L * D;
   const bf16_t* dOp = dO + (size_t)bh * L * D;
   const float* lp = LSE + (size_t)bh * L;
   const float* dp_ = delta + (size_t)bh * L;
-  const int kblk = blockIdx.x * 64, key = kblk + wid * 16 + li;
+  const int kblk = blockIdx.x * 128, kw0 = kblk + wid * 32, key = kw0 + lr;
   const int coff = S - L;
   const float c2 = scale * kLog2e;
   const bool key_ok = key < S;
-  const float madd = !key_ok ? -INFINITY : (mask ? mask[(size_t)b * S + key] * kLog2e : 0.f);
+  const float madd = !key_ok ? -INFINITY : (HAS_MASK ? mask[(size_t)b * S + key] * kLog2e : 0.f);
 
-  bf16x8 kf[DC], vf[DC];
+  bf16x8 kf[KS], vf[KS];
 #pragma unroll
-  for (int dc = 0; dc < DC; ++dc) {
-    kf[dc] = load_frag(K + ((size_t)bh * S + key) * D + 32 * dc + 8 * g, key_ok);
-    vf[dc] = load_frag(V + ((size_t)bh * S + key) * D + 32 * dc + 8 * g, key_ok);
+  for (int ks = 0; ks < KS; ++ks) {
+    kf[ks] = load_frag(K + ((size_t)bh * S + key) * D + 16 * ks + 8 * h, key_ok);
+    vf[ks] = load_frag(V + ((size_t)bh * S + key) * D + 16 * ks + 8 * h, key_ok);
   }
-  f32x4 dk[DT], dv[DT];
+  f32x16 dk[DT], dv[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) dk[i] = dv[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dk[i][r] = dv[i][r] = 0.f;
 
-  // causal: query q sees key iff key <= q + coff  ->  first useful q = kblk - coff
+  // causal: query q sees key iff key <= q + coff -> first useful q = kblk - coff
   int qstart = 0;
   if (causal) qstart = max(0, (kblk - coff) / 64 * 64);
   const int ntiles = qstart < L ? (L - qstart + 63) / 64 : 0;
 
-  TileStage<D, 2> st;
-  const bf16_t* srcs[2] = {Qp, dOp};
   float lse_r = 0.f, del_r = 0.f;
-  auto load_rows = [&](int q0) {
-    st.load(srcs, q0, L);
+  auto load_rows = [&](int q0, int buf) {
+    dma_tiles<D, 4>(Qp, dOp, Qs + buf * 64 * D, dOs + buf * 64 * D, q0, L);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
       lse_r = q < L ? lp[q] * kLog2e : INFINITY;
@@ -334,206 +379,303 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkdv_kernel(
     }
   };
   auto store_rows = [&](int buf) {
-    bf16_t* d[2] = {Qs + buf * 64 * D, dOs + buf * 64 * D};
-    st.store(d);
     if (threadIdx.x < 64) {
       lse_s[buf * 64 + threadIdx.x] = lse_r;
       del_s[buf * 64 + threadIdx.x] = del_r;
     }
   };
   if (ntiles > 0) {
-    load_rows(qstart);
+    load_rows(qstart, 0);
+    wait_vm0();
     store_rows(0);
   }
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1, q0 = qstart + t * 64;
-    if (t + 1 < ntiles) load_rows(q0 + 64);
+    if (t + 1 < ntiles) load_rows(q0 + 64, buf ^ 1);
     const bf16_t* qt_ = Qs + buf * 64 * D;
     const bf16_t* ot_ = dOs + buf * 64 * D;
     const float* ls = lse_s + buf * 64;
     const float* ds_ = del_s + buf * 64;
-    const bool active = !(causal && kblk + wid * 16 > q0 + 63 + coff);
-    if (active) {
-      f32x4 sc[4], dp[4];
+    if (kw0 < S && !(causal && kw0 > q0 + 63 + coff)) {
+      f32x16 s[2], dp[2];
+      const f32x16 z16 = {};
+      bf16x8 qa[2][2], oa[2][2];
+      qa[0][0] = row_frag<D>(qt_, lr, 8 * h);
+      qa[0][1] = row_frag<D>(qt_, 32 + lr, 8 * h);
+      oa[0][0] = row_frag<D>(ot_, lr, 8 * h);
+      oa[0][1] = row_frag<D>(ot_, 32 + lr, 8 * h);
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4) sc[q4] = dp[q4] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-        for (int dc = 0; dc < DC; ++dc) {
-          sc[q4] = mfma16(row_frag<D>(qt_, 16 * q4 + li, 32 * dc + 8 * g), kf[dc], sc[q4]);
-          dp[q4] = mfma16(row_frag<D>(ot_, 16 * q4 + li, 32 * dc + 8 * g), vf[dc], dp[q4]);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
+          const int c = 16 * (ks + 1) + 8 * h;
+          qa[(ks + 1) & 1][0] = row_frag<D>(qt_, lr, c);
+          qa[(ks + 1) & 1][1] = row_frag<D>(qt_, 32 + lr, c);
+          oa[(ks + 1) & 1][0] = row_frag<D>(ot_, lr, c);
+          oa[(ks + 1) & 1][1] = row_frag<D>(ot_, 32 + lr, c);
         }
-      // P = exp2(s*c2 + mask - lse2), dS = P * (dP - delta); row q = 16q4 + 4g + r
 #pragma unroll
-      for (int q4 = 0; q4 < 4; ++q4)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qr = 16 * q4 + 4 * g + r;
-          float p = exp2f(sc[q4][r] * c2 + madd - ls[qr]);
-          if (causal && key > q0 + qr + coff) p = 0.f;
-          sc[q4][r] = p;
-          dp[q4][r] = p * (dp[q4][r] - ds_[qr]);
+        for (int qt = 0; qt < 2; ++qt) {
+          s[qt] = mfma32(qa[ks & 1][qt], kf[ks], ks == 0 ? z16 : s[qt]);
+          dp[qt] = mfma32(oa[ks & 1][qt], vf[ks], ks == 0 ? z16 : dp[qt]);
         }
-      const bf16x8 pf0 = pack_frag(sc[0], sc[1]), pf1 = pack_frag(sc[2], sc[3]);
-      const bf16x8 sf0 = pack_frag(dp[0], dp[1]), sf1 = pack_frag(dp[2], dp[3]);
+      }
+      const bool diag = causal && kw0 + 31 > q0 + coff;
 #pragma unroll
-      for (int i = 0; i < DT; ++i) {
-        dv[i] = mfma16(tr_frag<D>(ot_, 0, 16 * i, lane), pf0, dv[i]);
-        dv[i] = mfma16(tr_frag<D>(ot_, 32, 16 * i, lane), pf1, dv[i]);
-        dk[i] = mfma16(tr_frag<D>(qt_, 0, 16 * i, lane), sf0, dk[i]);
-        dk[i] = mfma16(tr_frag<D>(qt_, 32, 16 * i, lane), sf1, dk[i]);
+      for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int qr = 32 * qt + 8 * i4 + 4 * h;
+          const float4 l4 = *reinterpret_cast<const float4*>(ls + qr);
+          const float4 d4 = *reinterpret_cast<const float4*>(ds_ + qr);
+          const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 4 * i4 + r;
+            float p = fexp2(s[qt][i] * c2 + (madd - lv[r]));
+            if (diag && key > q0 + qr + r + coff) p = 0.f;
+            s[qt][i] = p;
+            dp[qt][i] = p * (dp[qt][i] - dv4[r]);
+          }
+        }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 pf = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
+        const bf16x8 sf = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) {
+          dv[dt] = mfma32(tr_frag32<D>(ot_, 16 * k4, 32 * dt, lane), pf, dv[dt]);
+          dk[dt] = mfma32(tr_frag32<D>(qt_, 16 * k4, 32 * dt, lane), sf, dk[dt]);
+        }
       }
     }
-    if (t + 1 < ntiles) store_rows(buf ^ 1);
+    if (t + 1 < ntiles) {
+      wait_vm0();
+      store_rows(buf ^ 1);
+    }
     __syncthreads();
   }
 
   if (!key_ok) return;
+  // reg i of dk[dt] = dK[key][32dt + 8(i>>2) + 4h + (i&3)]
   bf16_t* dkr = dK + ((size_t)bh * S + key) * D;
   bf16_t* dvr = dV + ((size_t)bh * S + key) * D;
 #pragma unroll
-  for (int i = 0; i < DT; ++i) {
-    uint2 w;
-    w.x = pack2bf(dk[i][0] * scale, dk[i][1] * scale);
-    w.y = pack2bf(dk[i][2] * scale, dk[i][3] * scale);
-    *reinterpret_cast<uint2*>(dkr + 16 * i + 4 * g) = w;
-    w.x = pack2bf(dv[i][0], dv[i][1]);
-    w.y = pack2bf(dv[i][2], dv[i][3]);
-    *reinterpret_cast<uint2*>(dvr + 16 * i + 4 * g) = w;
-  }
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      const int d = 32 * dt + 8 * i4 + 4 * h;
+      uint2 w;
+      w.x = pack2bf(dk[dt][4 * i4 + 0] * scale, dk[dt][4 * i4 + 1] * scale);
+      w.y = pack2bf(dk[dt][4 * i4 + 2] * scale, dk[dt][4 * i4 + 3] * scale);
+      *reinterpret_cast<uint2*>(dkr + d) = w;
+      w.x = pack2bf(dv[dt][4 * i4 + 0], dv[dt][4 * i4 + 1]);
+      w.y = pack2bf(dv[dt][4 * i4 + 2], dv[dt][4 * i4 + 3]);
+      *reinterpret_cast<uint2*>(dvr + d) = w;
+    }
 }
 
 // ---------------------------------------------------------------------------
-// backward dQ: block = 4 waves x 16 query rows (64 rows); K/V tiles as forward
+// backward dQ on 32x32x16 MFMAs: NW waves x 32 query rows; K/V tiles as forward
+//   S^T = K Q^T, dP^T = V dO^T (query on the lane: LSE and delta are per-lane
+//   scalars), dQ^T += K^T dS^T with K^T transposed-read from the K tile.
 // ---------------------------------------------------------------------------
-template <int D>
-__global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(
+template <int D, int NW, bool HAS_MASK>
+__global__ __launch_bounds__(NW * 64, 4 / NW) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dQ, int H, int L, int S, float scale, int causal) {
+  constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
   bf16_t* Vs = Ks + 2 * 64 * D;
-  constexpr int DC = D / 32, DT = D / 16;
+  float* Ms = reinterpret_cast<float*>(Vs + 2 * 64 * D);
 
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, g = lane >> 4, li = lane & 15;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int bh = blockIdx.y, b = bh / H;
   const bf16_t* Kp = K + (size_t)bh * S * D;
   const bf16_t* Vp = V + (size_t)bh * S * D;
-  const float* mrow = mask ? mask + (size_t)b * S : nullptr;
-  const int qblk = blockIdx.x * 64, q0 = qblk + wid * 16, q = q0 + li;
+  const float* mrow = HAS_MASK ? mask + (size_t)b * S : nullptr;
+  // causal: heaviest query blocks (largest index) first
+  const int qb = causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
+  const int qblk = qb * 32 * NW, q0 = qblk + wid * 32, q = q0 + lr;
   const int coff = S - L;
   const float c2 = scale * kLog2e;
   const bool q_ok = q < L;
 
-  bf16x8 qf[DC], of[DC];
+  bf16x8 qf[KS], of[KS];
 #pragma unroll
-  for (int dc = 0; dc < DC; ++dc) {
-    qf[dc] = load_frag(Q + ((size_t)bh * L + q) * D + 32 * dc + 8 * g, q_ok);
-    of[dc] = load_frag(dO + ((size_t)bh * L + q) * D + 32 * dc + 8 * g, q_ok);
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = load_frag(Q + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q_ok);
+    of[ks] = load_frag(dO + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q_ok);
   }
   const float lse2 = q_ok ? LSE[(size_t)bh * L + q] * kLog2e : INFINITY;
   const float del = q_ok ? delta[(size_t)bh * L + q] : 0.f;
-  f32x4 dq[DT];
+  f32x16 dq[DT];
 #pragma unroll
-  for (int i = 0; i < DT; ++i) dq[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < DT; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) dq[i][r] = 0.f;
 
   int kv_end = S;
-  if (causal) kv_end = min(S, qblk + 63 + coff + 1);
+  if (causal) kv_end = min(S, qblk + 32 * NW - 1 + coff + 1);
   const int ntiles = kv_end > 0 ? (kv_end + 63) / 64 : 0;
-  TileStage<D, 2> st;
-  const bf16_t* srcs[2] = {Kp, Vp};
+  float mreg = 0.f;
+  auto load_mask = [&](int kv0) {
+    if (threadIdx.x < 64) {
+      const int key = kv0 + threadIdx.x;
+      mreg = key < S ? (HAS_MASK ? mrow[key] * kLog2e : 0.f) : -INFINITY;
+    }
+  };
+  auto store_mask = [&](int buf) {
+    if (threadIdx.x < 64) Ms[buf * 64 + threadIdx.x] = mreg;
+  };
   if (ntiles > 0) {
-    st.load(srcs, 0, S);
-    bf16_t* d0[2] = {Ks, Vs};
-    st.store(d0);
+    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S);
+    load_mask(0);
+    wait_vm0();
+    store_mask(0);
   }
   __syncthreads();
 
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1, kv0 = t * 64;
-    if (t + 1 < ntiles) st.load(srcs, kv0 + 64, S);
+    if (t + 1 < ntiles) {
+      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S);
+      load_mask(kv0 + 64);
+    }
     const bf16_t* kt_ = Ks + buf * 64 * D;
     const bf16_t* vt_ = Vs + buf * 64 * D;
-    const bool active = !(causal && kv0 > q0 + 15 + coff) && q0 < L;
-    if (active) {
-      f32x4 sc[4], dp[4];
+    if (q0 < L && !(causal && kv0 > q0 + 31 + coff)) {
+      f32x16 s[2], dp[2];
+      const f32x16 z16 = {};
+      bf16x8 ka[2][2], va[2][2];
+      ka[0][0] = row_frag<D>(kt_, lr, 8 * h);
+      ka[0][1] = row_frag<D>(kt_, 32 + lr, 8 * h);
+      va[0][0] = row_frag<D>(vt_, lr, 8 * h);
+      va[0][1] = row_frag<D>(vt_, 32 + lr, 8 * h);
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) sc[k4] = dp[k4] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int dc = 0; dc < DC; ++dc) {
-          sc[k4] = mfma16(row_frag<D>(kt_, 16 * k4 + li, 32 * dc + 8 * g), qf[dc], sc[k4]);
-          dp[k4] = mfma16(row_frag<D>(vt_, 16 * k4 + li, 32 * dc + 8 * g), of[dc], dp[k4]);
+      for (int ks = 0; ks < KS; ++ks) {
+        if (ks + 1 < KS) {
+          const int c = 16 * (ks + 1) + 8 * h;
+          ka[(ks + 1) & 1][0] = row_frag<D>(kt_, lr, c);
+          ka[(ks + 1) & 1][1] = row_frag<D>(kt_, 32 + lr, c);
+          va[(ks + 1) & 1][0] = row_frag<D>(vt_, lr, c);
+          va[(ks + 1) & 1][1] = row_frag<D>(vt_, 32 + lr, c);
         }
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int key = kv0 + 16 * k4 + 4 * g + r;
-          const float madd = key < S ? (mrow ? mrow[key] * kLog2e : 0.f) : -INFINITY;
-          float p = exp2f(sc[k4][r] * c2 + madd - lse2);
-          if (causal && key > q + coff) p = 0.f;
-          dp[k4][r] = p * (dp[k4][r] - del);
+        for (int kt = 0; kt < 2; ++kt) {
+          s[kt] = mfma32(ka[ks & 1][kt], qf[ks], ks == 0 ? z16 : s[kt]);
+          dp[kt] = mfma32(va[ks & 1][kt], of[ks], ks == 0 ? z16 : dp[kt]);
         }
-      const bf16x8 sf0 = pack_frag(dp[0], dp[1]), sf1 = pack_frag(dp[2], dp[3]);
+      }
+      const bool diag = causal && kv0 + 63 > q0 + coff;
+      const float* mk = Ms + buf * 64;
 #pragma unroll
-      for (int i = 0; i < DT; ++i) {
-        dq[i] = mfma16(tr_frag<D>(kt_, 0, 16 * i, lane), sf0, dq[i]);
-        dq[i] = mfma16(tr_frag<D>(kt_, 32, 16 * i, lane), sf1, dq[i]);
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int kr = 32 * kt + 8 * i4 + 4 * h;
+          const float4 mv = *reinterpret_cast<const float4*>(mk + kr);
+          const float ma[4] = {mv.x, mv.y, mv.z, mv.w};
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int i = 4 * i4 + r;
+            float p = fexp2(s[kt][i] * c2 + (ma[r] - lse2));
+            if (diag && kv0 + kr + r > q + coff) p = 0.f;
+            dp[kt][i] = p * (dp[kt][i] - del);
+          }
+        }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const bf16x8 sf = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_frag32<D>(kt_, 16 * k4, 32 * dt, lane), sf, dq[dt]);
       }
     }
     if (t + 1 < ntiles) {
-      bf16_t* dn[2] = {Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D};
-      st.store(dn);
+      wait_vm0();
+      store_mask(buf ^ 1);
     }
     __syncthreads();
   }
   if (!q_ok) return;
   bf16_t* dqr = dQ + ((size_t)bh * L + q) * D;
 #pragma unroll
-  for (int i = 0; i < DT; ++i) {
-    uint2 w;
-    w.x = pack2bf(dq[i][0] * scale, dq[i][1] * scale);
-    w.y = pack2bf(dq[i][2] * scale, dq[i][3] * scale);
-    *reinterpret_cast<uint2*>(dqr + 16 * i + 4 * g) = w;
-  }
+  for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+    for (int i4 = 0; i4 < 4; ++i4) {
+      uint2 w;
+      w.x = pack2bf(dq[dt][4 * i4 + 0] * scale, dq[dt][4 * i4 + 1] * scale);
+      w.y = pack2bf(dq[dt][4 * i4 + 2] * scale, dq[dt][4 * i4 + 3] * scale);
+      *reinterpret_cast<uint2*>(dqr + 32 * dt + 8 * i4 + 4 * h) = w;
+    }
 }
 
 }  // namespace zoo
 
 using namespace zoo;
 
-// D = 128 tiles need more than the default 64 KiB of dynamic LDS per block
-#define ATTN_LAUNCH(kern, grid, smem, ...)                                                              \
-  do {                                                                                                  \
-    static const bool lds_ok_ = [] {                                                                    \
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&kern), hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          96 * 1024);                                                                   \
-      return true;                                                                                      \
-    }();                                                                                                \
-    (void)lds_ok_;                                                                                      \
-    hipLaunchKernelGGL(kern, grid, dim3(256), smem, st, __VA_ARGS__);                                   \
-  } while (0)
+template <int D, int NW, bool HM>
+static void launch_fwd(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
+                       int H, int L, int S, float scale, int causal, hipStream_t st) {
+  const dim3 grid((L + 32 * NW - 1) / (32 * NW), B * H);
+  const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 2 * 64 * sizeof(float);
+  static const bool lds_ok_ = [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_fwd_kernel<D, NW, HM>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    return true;
+  }();
+  (void)lds_ok_;
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, HM>), grid, dim3(NW * 64), smem, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal);
+}
+
+template <int D>
+static void launch_fwd_d(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
+                         int H, int L, int S, float scale, int causal, hipStream_t st) {
+  // 8 waves (256 query rows) share each K/V tile when there are enough rows
+  if (L >= 256) {
+    if (mask) launch_fwd<D, 8, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    else launch_fwd<D, 8, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+  } else {
+    if (mask) launch_fwd<D, 4, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    else launch_fwd<D, 4, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+  }
+}
 
 extern "C" hipError_t zoo_attn_fwd(const void* q, const void* k, const void* v, const float* mask, void* o,
                                    float* lse, int B, int H, int L, int S, int D, float scale, int causal,
                                    hipStream_t st) {
-  const dim3 grid((L + 127) / 128, B * H);
-  const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t);
   if (D == 64)
-    ATTN_LAUNCH(attn_fwd_kernel<64>, grid, smem, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal);
+    launch_fwd_d<64>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
   else if (D == 128)
-    ATTN_LAUNCH(attn_fwd_kernel<128>, grid, smem, (const bf16_t*)q, (const bf16_t*)k,
-                       (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal);
+    launch_fwd_d<128>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+template <int D, bool HM>
+static void launch_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
+                       const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int H, int L, int S,
+                       float scale, int causal, hipStream_t st) {
+  static const bool lds_ok_ = [] {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D, HM>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D, 4, HM>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    return true;
+  }();
+  (void)lds_ok_;
+  const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 4 * 64 * sizeof(float);
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, HM>), dim3((S + 127) / 128, B * H), dim3(256), smem, st,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
+                     (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, HM>), dim3((L + 127) / 128, B * H), dim3(256), smem, st,
+                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
+                     (bf16_t*)dq, H, L, S, scale, causal);
 }
 
 extern "C" hipError_t zoo_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
@@ -541,26 +683,16 @@ extern "C" hipError_t zoo_attn_bwd(const void* dout, const void* q, const void* 
                                    int H, int L, int S, int D, float scale, int causal, hipStream_t st) {
   const int rows = B * H * L;
   const int dblocks = (rows * (D / 8) + 255) / 256;
-  const size_t smem_kv = (size_t)4 * 64 * D * sizeof(bf16_t);
-  const size_t smem_q = smem_kv + 4 * 64 * sizeof(float);
   if (D == 64) {
     hipLaunchKernelGGL(attn_delta_kernel<64>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
                        (const bf16_t*)o, delta, rows);
-    ATTN_LAUNCH(attn_bwd_dkdv_kernel<64>, dim3((S + 63) / 64, B * H), smem_q,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal);
-    ATTN_LAUNCH(attn_bwd_dq_kernel<64>, dim3((L + 63) / 64, B * H), smem_kv,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dq, H, L, S, scale, causal);
+    if (mask) launch_bwd<64, true>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+    else launch_bwd<64, false>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
   } else if (D == 128) {
     hipLaunchKernelGGL(attn_delta_kernel<128>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
                        (const bf16_t*)o, delta, rows);
-    ATTN_LAUNCH(attn_bwd_dkdv_kernel<128>, dim3((S + 63) / 64, B * H), smem_q,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal);
-    ATTN_LAUNCH(attn_bwd_dq_kernel<128>, dim3((L + 63) / 64, B * H), smem_kv,
-                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                       (bf16_t*)dq, H, L, S, scale, causal);
+    if (mask) launch_bwd<128, true>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+    else launch_bwd<128, false>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
   } else {
     return hipErrorInvalidValue;
   }
