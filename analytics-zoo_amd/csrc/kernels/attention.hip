@@ -270,10 +270,14 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
       bf16x8 pf[4];
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) pf[k4] = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
+      constexpr int NSTEP = 4 * DT;
+      bf16x8 fv[2];
+      fv[0] = tr_frag32<D>(vt_, 0, 0, lane);
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4)
-#pragma unroll
-        for (int dt = 0; dt < DT; ++dt) o[dt] = mfma32(tr_frag32<D>(vt_, 16 * k4, 32 * dt, lane), pf[k4], o[dt]);
+      for (int idx = 0; idx < NSTEP; ++idx) {
+        if (idx + 1 < NSTEP) fv[(idx + 1) & 1] = tr_frag32<D>(vt_, 16 * ((idx + 1) / DT), 32 * ((idx + 1) % DT), lane);
+        o[idx % DT] = mfma32(fv[idx & 1], pf[idx / DT], o[idx % DT]);
+      }
     }
     if (t + 1 < ntiles) {
       wait_vm0();
@@ -320,20 +324,22 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 }
 
 // ---------------------------------------------------------------------------
-// backward dK/dV on 32x32x16 MFMAs: block = 4 waves x 32 keys (128 keys), one
-// wave per SIMD (the dK/dV accumulators live in AGPRs); 64-query Q/dO tiles.
+// backward dK/dV on 32x32x16 MFMAs: block = 128 keys (4 key groups of 32) x
+// QW query halves; 64-query Q/dO tiles double-buffered by LDS-DMA.
 //   S = Q K^T, dP = dO V^T with the key on the lane (K/V fragments in registers,
 //   Q/dO row fragments from LDS); reg i of tile qt <-> q = 32qt + 8(i>>2) + 4h + (i&3)
 //   dV^T += dO^T P, dK^T += Q^T dS: P / dS packed from the accumulators, dO^T /
 //   Q^T transposed-read from the same LDS tiles in that permuted q order.
 // ---------------------------------------------------------------------------
-template <int D, bool HAS_MASK>
-__global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
+template <int D, int QW, bool HAS_MASK>
+__global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
     float scale, int causal) {
-  constexpr int KS = D / 16, DT = D / 32;
+  // QW = 2: 8 waves; wave w owns keys 32(w&3).. and query rows 32(w>>2).. of every
+  // 64-row tile (two waves per SIMD); the two q-halves are summed through LDS at the end
+  constexpr int KS = D / 16, DT = D / 32, NQT = 2 / QW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);                 // [2][64][D]
   bf16_t* dOs = Qs + 2 * 64 * D;                                // [2][64][D]
@@ -341,12 +347,13 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
   float* del_s = lse_s + 2 * 64;                                // [2][64]
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
+  const int kg = wid & 3, qh = QW == 2 ? wid >> 2 : 0;
   const int bh = blockIdx.y, b = bh / H;
   const bf16_t* Qp = Q + (size_t)bh * L * D;
   const bf16_t* dOp = dO + (size_t)bh * L * D;
   const float* lp = LSE + (size_t)bh * L;
   const float* dp_ = delta + (size_t)bh * L;
-  const int kblk = blockIdx.x * 128, kw0 = kblk + wid * 32, key = kw0 + lr;
+  const int kblk = blockIdx.x * 128, kw0 = kblk + kg * 32, key = kw0 + lr;
   const int coff = S - L;
   const float c2 = scale * kLog2e;
   const bool key_ok = key < S;
@@ -371,7 +378,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 
   float lse_r = 0.f, del_r = 0.f;
   auto load_rows = [&](int q0, int buf) {
-    dma_tiles<D, 4>(Qp, dOp, Qs + buf * 64 * D, dOs + buf * 64 * D, q0, L);
+    dma_tiles<D, 4 * QW>(Qp, dOp, Qs + buf * 64 * D, dOs + buf * 64 * D, q0, L);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
       lse_r = q < L ? lp[q] * kLog2e : INFINITY;
@@ -398,35 +405,38 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* ot_ = dOs + buf * 64 * D;
     const float* ls = lse_s + buf * 64;
     const float* ds_ = del_s + buf * 64;
-    if (kw0 < S && !(causal && kw0 > q0 + 63 + coff)) {
-      f32x16 s[2], dp[2];
+    const int qlo = 32 * qh;  // first tile row of this wave (QW = 2) or 0
+    if (kw0 < S && !(causal && kw0 > q0 + qlo + 32 * NQT - 1 + coff)) {
+      f32x16 s[NQT], dp[NQT];
       const f32x16 z16 = {};
-      bf16x8 qa[2][2], oa[2][2];
-      qa[0][0] = row_frag<D>(qt_, lr, 8 * h);
-      qa[0][1] = row_frag<D>(qt_, 32 + lr, 8 * h);
-      oa[0][0] = row_frag<D>(ot_, lr, 8 * h);
-      oa[0][1] = row_frag<D>(ot_, 32 + lr, 8 * h);
+      bf16x8 qa[2][NQT], oa[2][NQT];
+#pragma unroll
+      for (int qt = 0; qt < NQT; ++qt) {
+        qa[0][qt] = row_frag<D>(qt_, qlo + 32 * qt + lr, 8 * h);
+        oa[0][qt] = row_frag<D>(ot_, qlo + 32 * qt + lr, 8 * h);
+      }
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         if (ks + 1 < KS) {
           const int c = 16 * (ks + 1) + 8 * h;
-          qa[(ks + 1) & 1][0] = row_frag<D>(qt_, lr, c);
-          qa[(ks + 1) & 1][1] = row_frag<D>(qt_, 32 + lr, c);
-          oa[(ks + 1) & 1][0] = row_frag<D>(ot_, lr, c);
-          oa[(ks + 1) & 1][1] = row_frag<D>(ot_, 32 + lr, c);
+#pragma unroll
+          for (int qt = 0; qt < NQT; ++qt) {
+            qa[(ks + 1) & 1][qt] = row_frag<D>(qt_, qlo + 32 * qt + lr, c);
+            oa[(ks + 1) & 1][qt] = row_frag<D>(ot_, qlo + 32 * qt + lr, c);
+          }
         }
 #pragma unroll
-        for (int qt = 0; qt < 2; ++qt) {
+        for (int qt = 0; qt < NQT; ++qt) {
           s[qt] = mfma32(qa[ks & 1][qt], kf[ks], ks == 0 ? z16 : s[qt]);
           dp[qt] = mfma32(oa[ks & 1][qt], vf[ks], ks == 0 ? z16 : dp[qt]);
         }
       }
-      const bool diag = causal && kw0 + 31 > q0 + coff;
+      const bool diag = causal && kw0 + 31 > q0 + qlo + coff;
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < NQT; ++qt)
 #pragma unroll
         for (int i4 = 0; i4 < 4; ++i4) {
-          const int qr = 32 * qt + 8 * i4 + 4 * h;
+          const int qr = qlo + 32 * qt + 8 * i4 + 4 * h;
           const float4 l4 = *reinterpret_cast<const float4*>(ls + qr);
           const float4 d4 = *reinterpret_cast<const float4*>(ds_ + qr);
           const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
@@ -439,15 +449,27 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
             dp[qt][i] = p * (dp[qt][i] - dv4[r]);
           }
         }
+      bf16x8 pf[2 * NQT], sf[2 * NQT];
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const bf16x8 pf = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
-        const bf16x8 sf = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+      for (int k4 = 0; k4 < 2 * NQT; ++k4) {
+        pf[k4] = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
+        sf[k4] = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+      }
+      // dO^T / Q^T fragments one step ahead of their MFMAs
+      constexpr int NSTEP = 2 * NQT * DT;
+      bf16x8 fo[2], fq[2];
+      fo[0] = tr_frag32<D>(ot_, qlo, 0, lane);
+      fq[0] = tr_frag32<D>(qt_, qlo, 0, lane);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) {
-          dv[dt] = mfma32(tr_frag32<D>(ot_, 16 * k4, 32 * dt, lane), pf, dv[dt]);
-          dk[dt] = mfma32(tr_frag32<D>(qt_, 16 * k4, 32 * dt, lane), sf, dk[dt]);
+      for (int idx = 0; idx < NSTEP; ++idx) {
+        if (idx + 1 < NSTEP) {
+          const int k4n = (idx + 1) / DT, dtn = (idx + 1) % DT;
+          fo[(idx + 1) & 1] = tr_frag32<D>(ot_, qlo + 16 * k4n, 32 * dtn, lane);
+          fq[(idx + 1) & 1] = tr_frag32<D>(qt_, qlo + 16 * k4n, 32 * dtn, lane);
         }
+        const int k4 = idx / DT, dt = idx % DT;
+        dv[dt] = mfma32(fo[idx & 1], pf[k4], dv[dt]);
+        dk[dt] = mfma32(fq[idx & 1], sf[k4], dk[dt]);
       }
     }
     if (t + 1 < ntiles) {
@@ -457,6 +479,29 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
     __syncthreads();
   }
 
+  if (QW == 2) {
+    // sum the two query halves: waves 4..7 park their partials in the (now idle) tile LDS
+    float* red = reinterpret_cast<float*>(smem);  // [4 key groups][DT][16][64 lanes]
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      f32x16* acc = pass == 0 ? dk : dv;
+      if (qh == 1) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) red[((kg * DT + dt) * 16 + r) * 64 + lane] = acc[dt][r];
+      }
+      __syncthreads();
+      if (qh == 0) {
+#pragma unroll
+        for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) acc[dt][r] += red[((kg * DT + dt) * 16 + r) * 64 + lane];
+      }
+      __syncthreads();
+    }
+    if (qh == 1) return;
+  }
   if (!key_ok) return;
   // reg i of dk[dt] = dK[key][32dt + 8(i>>2) + 4h + (i&3)]
   bf16_t* dkr = dK + ((size_t)bh * S + key) * D;
@@ -482,7 +527,7 @@ __global__ __launch_bounds__(256, 1) void attn_bwd_dkdv_kernel(
 //   scalars), dQ^T += K^T dS^T with K^T transposed-read from the K tile.
 // ---------------------------------------------------------------------------
 template <int D, int NW, bool HAS_MASK>
-__global__ __launch_bounds__(NW * 64, 4 / NW) void attn_bwd_dq_kernel(
+__global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dQ, int H, int L, int S, float scale, int causal) {
@@ -587,11 +632,16 @@ __global__ __launch_bounds__(NW * 64, 4 / NW) void attn_bwd_dq_kernel(
             dp[kt][i] = p * (dp[kt][i] - del);
           }
         }
+      bf16x8 sf[4];
 #pragma unroll
-      for (int k4 = 0; k4 < 4; ++k4) {
-        const bf16x8 sf = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+      for (int k4 = 0; k4 < 4; ++k4) sf[k4] = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+      constexpr int NSTEP = 4 * DT;
+      bf16x8 fk[2];
+      fk[0] = tr_frag32<D>(kt_, 0, 0, lane);
 #pragma unroll
-        for (int dt = 0; dt < DT; ++dt) dq[dt] = mfma32(tr_frag32<D>(kt_, 16 * k4, 32 * dt, lane), sf, dq[dt]);
+      for (int idx = 0; idx < NSTEP; ++idx) {
+        if (idx + 1 < NSTEP) fk[(idx + 1) & 1] = tr_frag32<D>(kt_, 16 * ((idx + 1) / DT), 32 * ((idx + 1) % DT), lane);
+        dq[idx % DT] = mfma32(fk[idx & 1], sf[idx / DT], dq[idx % DT]);
       }
     }
     if (t + 1 < ntiles) {
@@ -657,25 +707,38 @@ extern "C" hipError_t zoo_attn_fwd(const void* q, const void* k, const void* v, 
   return hipGetLastError();
 }
 
-template <int D, bool HM>
+template <int D, bool HM, int QW, int NWQ>
 static void launch_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
                        const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int H, int L, int S,
                        float scale, int causal, hipStream_t st) {
   static const bool lds_ok_ = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D, HM>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D, 4, HM>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    return true;
+    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D, QW, HM>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D, NWQ, HM>),
+                                        hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
+    return e1 == hipSuccess && e2 == hipSuccess;
   }();
   (void)lds_ok_;
   const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 4 * 64 * sizeof(float);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, HM>), dim3((S + 127) / 128, B * H), dim3(256), smem, st,
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM>), dim3((S + 127) / 128, B * H), dim3(256 * QW), smem, st,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
                      (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, 4, HM>), dim3((L + 127) / 128, B * H), dim3(256), smem, st,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                     (bf16_t*)dq, H, L, S, scale, causal);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NWQ, HM>), dim3((L + 32 * NWQ - 1) / (32 * NWQ), B * H),
+                     dim3(64 * NWQ), smem, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask,
+                     (const bf16_t*)dout, lse, delta, (bf16_t*)dq, H, L, S, scale, causal);
+}
+
+template <int D>
+static void launch_bwd_d(const void* dout, const void* q, const void* k, const void* v, const float* mask,
+                         const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int H, int L,
+                         int S, float scale, int causal, hipStream_t st) {
+  // D = 64 fits two waves per SIMD (8-wave blocks); D = 128 keeps one wave per
+  // SIMD with the accumulators in AGPRs (the 8-wave form would spill)
+  constexpr int QW = D == 64 ? 2 : 1, NWQ = D == 64 ? 8 : 4;
+  if (mask)
+    launch_bwd<D, true, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+  else
+    launch_bwd<D, false, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
 }
 
 extern "C" hipError_t zoo_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
@@ -686,13 +749,11 @@ extern "C" hipError_t zoo_attn_bwd(const void* dout, const void* q, const void* 
   if (D == 64) {
     hipLaunchKernelGGL(attn_delta_kernel<64>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
                        (const bf16_t*)o, delta, rows);
-    if (mask) launch_bwd<64, true>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
-    else launch_bwd<64, false>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+    launch_bwd_d<64>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
   } else if (D == 128) {
     hipLaunchKernelGGL(attn_delta_kernel<128>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
                        (const bf16_t*)o, delta, rows);
-    if (mask) launch_bwd<128, true>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
-    else launch_bwd<128, false>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+    launch_bwd_d<128>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
   } else {
     return hipErrorInvalidValue;
   }

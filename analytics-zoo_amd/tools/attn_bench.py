@@ -49,8 +49,11 @@ def main():
         # torch SDPA for comparison (math/flash backend chosen by torch)
         qs, ks, vs = (t.clone().requires_grad_(True) for t in (q, k, v))
         tt = timeit(lambda: torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=causal), a.iters)
+        ot = torch.nn.functional.scaled_dot_product_attention(qs, ks, vs, is_causal=causal)
+        ttb = timeit(lambda: torch.autograd.grad(ot, (qs, ks, vs), do, retain_graph=True), a.iters)
         print("B%d H%d L%d D%d causal=%d  fwd %.3f ms %.0f TF | bwd %.3f ms %.0f TF | torch sdpa fwd %.3f ms %.0f TF"
-              % (B, H, L, D, causal, tf, fl / tf / 1e9, tb, 2.5 * fl / tb / 1e9, tt, fl / tt / 1e9), flush=True)
+              " bwd %.3f ms %.0f TF" % (B, H, L, D, causal, tf, fl / tf / 1e9, tb, 2.5 * fl / tb / 1e9, tt,
+                                       fl / tt / 1e9, ttb, 2.5 * fl / ttb / 1e9), flush=True)
 
 
 if __name__ == "__main__":
