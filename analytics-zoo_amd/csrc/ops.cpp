@@ -58,6 +58,11 @@ hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, 
 hipError_t zoo_resize_normalize(const void*, void*, int, int, int, int, int, int, const float*, const float*, int, int,
                                 hipStream_t);
 hipError_t zoo_embedding_bwd(const void*, int, const int64_t*, float*, int, int, int, int64_t, float, hipStream_t);
+hipError_t zoo_absmax(const void*, int, size_t, float*, hipStream_t);
+hipError_t zoo_im2col_q8(const void*, int, const float*, void*, int, int, int, int, int, int, int, int, int, int, int,
+                         int, int, hipStream_t);
+hipError_t zoo_qgemm(const void*, const void*, const float*, const float*, const float*, const void*, void*, int, int,
+                     int, int, int, hipStream_t);
 hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
                         float, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
@@ -691,6 +696,59 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::
   return {dq, dk, dv};
 }
 
+
+// ---- int8 quantized inference ----
+torch::Tensor absmax(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "absmax: contiguous GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "absmax: fp32 or bf16");
+  auto out = torch::zeros({1}, x.options().dtype(at::kFloat));
+  if (x.numel() == 0) return out;
+  check_hip(zoo_absmax(x.data_ptr(), x.scalar_type() == at::kFloat, (size_t)x.numel(), out.data_ptr<float>(),
+                       cur_stream()),
+            "absmax");
+  return out;
+}
+
+torch::Tensor im2col_q8(torch::Tensor x, torch::Tensor amax, int R, int S, int sh, int sw, int ph, int pw, int P,
+                        int Q, int Kp) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() == 4, "im2col_q8: contiguous NHWC GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "im2col_q8: fp32 or bf16");
+  req(amax, at::kFloat, "amax");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK(Kp % 16 == 0 && Kp >= R * S * C, "im2col_q8: Kp must be a multiple of 16 covering R*S*C");
+  TORCH_CHECK(P > 0 && Q > 0 && R > 0 && S > 0 && sh > 0 && sw > 0, "im2col_q8: bad geometry");
+  auto q = torch::empty({(int64_t)N * P * Q, Kp}, x.options().dtype(at::kChar));
+  if (q.numel() == 0) return q;
+  check_hip(zoo_im2col_q8(x.data_ptr(), x.scalar_type() == at::kFloat, amax.data_ptr<float>(), q.data_ptr(), N, H,
+                          W, C, R, S, P, Q, sh, sw, ph, pw, Kp, cur_stream()),
+            "im2col_q8");
+  return q;
+}
+
+torch::Tensor qgemm(torch::Tensor a, torch::Tensor w, torch::Tensor amax, torch::Tensor wscale,
+                    c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid, bool relu, bool out_f32) {
+  req(a, at::kChar, "a");
+  req(w, at::kChar, "w");
+  req(amax, at::kFloat, "amax");
+  req(wscale, at::kFloat, "wscale");
+  TORCH_CHECK(a.dim() == 2 && w.dim() == 2 && a.size(1) == w.size(1), "qgemm: a [M,Kp], w [N,Kp]");
+  const int M = a.size(0), N = w.size(0), Kp = a.size(1);
+  TORCH_CHECK(Kp % 16 == 0, "qgemm: Kp must be a multiple of 16");
+  TORCH_CHECK(wscale.numel() == N, "qgemm: wscale [N]");
+  if (bias.has_value() && bias->defined()) { req(*bias, at::kFloat, "bias"); TORCH_CHECK(bias->numel() == N, "bias"); }
+  if (resid.has_value() && resid->defined()) {
+    req(*resid, at::kBFloat16, "resid");
+    TORCH_CHECK(resid->numel() == (int64_t)M * N, "qgemm: resid [M,N]");
+  }
+  auto y = torch::empty({M, N}, a.options().dtype(out_f32 ? at::kFloat : at::kBFloat16));
+  if (M == 0 || N == 0) return y;
+  check_hip(zoo_qgemm(a.data_ptr(), w.data_ptr(), amax.data_ptr<float>(), wscale.data_ptr<float>(),
+                      opt_ptr<float>(bias), opt_ptr<void>(resid), y.data_ptr(), M, N, Kp, relu, out_f32,
+                      cur_stream()),
+            "qgemm");
+  return y;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -722,5 +780,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("absmax", &absmax);
+  m.def("im2col_q8", &im2col_q8);
+  m.def("qgemm", &qgemm);
   m.def("attn_bwd", &attn_bwd);
 }

@@ -49,6 +49,12 @@ class ZooModel(KerasNet):
         from zoo.pipeline.api.keras.serialization import load_model
         return load_model(path)
 
+    def quantize(self):
+        """int8 inference copy of the model in place (AbstractModule.quantize,
+        ImageModel.scala:133-145): see zoo.ops.quant."""
+        from zoo.ops.quant import quantize
+        return quantize(self)
+
     def get_model(self):
         return self.model
 

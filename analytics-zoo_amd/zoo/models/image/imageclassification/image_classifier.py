@@ -70,6 +70,10 @@ class ImageModel(ZooModel):
     @torch.no_grad()
     def predict_image_set(self, image_set, configure=None, batch_size=32):
         cfg = configure or self.config
+        if getattr(self, "int8", False):
+            from zoo.ops.quant import is_quantized
+            if not is_quantized(self):
+                self.quantize()  # "*-int8" / "*-quantize" configs serve the int8 model
         s = image_set.transform(cfg.pre_processor) if cfg is not None and cfg.pre_processor else image_set
         x = np.stack([f["imageTensor"] for f in s.features]).astype(np.float32)
         out = self.predict(x, batch_size=batch_size)
@@ -86,6 +90,7 @@ class ImageClassifier(ImageModel):
         self.num_classes = int(num_classes)
         self.config = ImageConfigure.for_model(model_name, label_map)
         self.net = nets.build(model_name, num_classes)
+        self.int8 = model_name.lower().endswith(("-int8", "-quantize"))
         self.built = True
 
     def build_model(self):

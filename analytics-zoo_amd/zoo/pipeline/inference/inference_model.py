@@ -122,11 +122,14 @@ class InferenceModel:
         self._t0 = None
 
     # ------------------------------------------------------------------ loading
-    def _install(self, model):
+    def _install(self, model, quantize=False):
         model = model.to(self.device)
         if self.dtype is not None:
             model = model.to(self.dtype)
         model.eval()
+        if quantize:  # blas=false in the reference loaders -> BigDL quantize() (int8)
+            from zoo.ops.quant import quantize as _q
+            model = _q(model)
         for p in model.parameters():
             p.requires_grad_(False)
         self.model = model
@@ -143,24 +146,31 @@ class InferenceModel:
             self._n_replicas += 1
         return r
 
-    def load_module(self, module):
-        """Serve an in-memory torch.nn.Module (the PyTorch loader, doLoadPyTorch)."""
-        return self._install(module)
+    def load_module(self, module, blas=True):
+        """Serve an in-memory torch.nn.Module (the PyTorch loader, doLoadPyTorch).
+        ``blas=False`` quantizes to int8 as the reference loaders do."""
+        return self._install(module, quantize=not blas)
 
-    def load(self, model_path, weight_path=None):
+    def load(self, model_path, weight_path=None, blas=True):
         """Zoo Keras/ZooModel file (doLoad, InferenceModel.scala:97-110)."""
         from zoo.pipeline.api.keras.serialization import load_model
-        return self._install(load_model(model_path))
+        return self._install(load_model(model_path), quantize=not blas)
 
-    def load_bigdl(self, model_path, weight_path=None):
+    def load_bigdl(self, model_path, weight_path=None, blas=True):
         """BigDL protobuf ``.model`` (doLoadBigDL, InferenceModel.scala:81-95)."""
         from zoo.pipeline.api.net import Net
-        return self._install(Net.load_bigdl(model_path, weight_path))
+        return self._install(Net.load_bigdl(model_path, weight_path), quantize=not blas)
 
-    def load_caffe(self, model_path, weight_path):
+    def load_caffe(self, model_path, weight_path, blas=True):
         """Caffe prototxt + caffemodel (doLoadCaffe, InferenceModel.scala:112-124)."""
         from zoo.pipeline.api.net import Net
-        return self._install(Net.load_caffe(model_path, weight_path))
+        return self._install(Net.load_caffe(model_path, weight_path), quantize=not blas)
+
+    def quantize(self):
+        """Re-install the loaded model as its int8 version (InferenceModelFactory.scala:33,47)."""
+        if self.model is None:
+            raise RuntimeError("load a model first")
+        return self._install(self.model, quantize=True)
 
     def load_onnx(self, model_path):
         from zoo.pipeline.api.onnx import load_onnx
