@@ -31,8 +31,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
                                                         const bf16_t* __restrict__ Xin,  // conv output x (mode 1)
                                                         const float* __restrict__ mean,
                                                         const float* __restrict__ invstd,
-                                                        float* __restrict__ out,  // [2][C]
-                                                        int M, int C, int rows_per_block) {
+                                                        float* __restrict__ out,  // [2][C] (+ slots)
+                                                        int M, int C, int rows_per_block, int nslot) {
   const int cpr = C >> 3;  // 8-channel chunks per row
   const int tid = threadIdx.x;
   // threads are laid out [row_lane][chunk]; if C/8 > 256 a thread walks several chunks
@@ -87,7 +87,8 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
     }
   }
   __syncthreads();
-  for (int i = tid; i < 2 * C; i += blockDim.x) atomicAdd(out + i, red[i]);
+  float* const dst = nslot > 0 ? slot_ptr(out, 2 * C, nslot) : out;
+  for (int i = tid; i < 2 * C; i += blockDim.x) atomicAdd(dst + i, red[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -252,6 +253,15 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
+// fold the statistic slots: buf[i] = sum_k buf[n2*(1+k) + i]
+__global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__ buf, int n2, int nslot) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n2) return;
+  float s = 0.f;
+  for (int k = 0; k < nslot; ++k) s += buf[(size_t)n2 * (1 + k) + i];
+  buf[i] = s;
+}
+
 // contiguous row range per block: ~1024 blocks, at least 8 rows per thread-row
 static int apply_rows_per_block(int M, int C) {
   const int cpr = C / 8;
@@ -266,8 +276,13 @@ static int apply_rows_per_block(int M, int C) {
 
 using namespace zoo;
 
+extern "C" hipError_t zoo_stats_finalize(float* buf, int n2, int nslot, hipStream_t st) {
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2 + 255) / 256), dim3(256), 0, st, buf, n2, nslot);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X, const float* mean,
-                                    const float* invstd, float* out, int M, int C, int mode,
+                                    const float* invstd, float* out, int M, int C, int mode, int nslot,
                                     hipStream_t st) {
   // ~1024 blocks, each owning a contiguous row range
   int blocks = 1024;
@@ -277,10 +292,11 @@ extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X,
   const size_t smem = (size_t)2 * C * sizeof(float);
   if (mode == 0)
     hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)A,
-                       (const bf16_t*)Z, (const bf16_t*)X, mean, invstd, out, M, C, rpb);
+                       (const bf16_t*)Z, (const bf16_t*)X, mean, invstd, out, M, C, rpb, nslot);
   else
     hipLaunchKernelGGL(bn_reduce_kernel<1>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)A,
-                       (const bf16_t*)Z, (const bf16_t*)X, mean, invstd, out, M, C, rpb);
+                       (const bf16_t*)Z, (const bf16_t*)X, mean, invstd, out, M, C, rpb, nslot);
+  if (nslot > 0) return zoo_stats_finalize(out, 2 * C, nslot, st);
   return hipGetLastError();
 }
 

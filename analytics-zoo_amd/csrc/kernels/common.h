@@ -85,6 +85,15 @@ ZOO_DEV int xcd_remap(int orig, int nwg) {
   return base + orig / 8;
 }
 
+// Contention-spreading per-channel sums (MI355X_MICROARCH.md "Global float
+// atomics": every workgroup adding into ONE row runs ~14x below the atomic
+// rate). buf = [n2 final][nslot x n2 partial][pad], zero-initialised; a block
+// adds its partials into slot blockIdx % nslot and zoo_stats_finalize (a tiny
+// follow-up kernel on the same stream) folds the slots into buf[0..n2).
+ZOO_DEV float* slot_ptr(float* buf, int n2, int nslot) {
+  return buf + (size_t)n2 * (1 + (int)(blockIdx.x % (unsigned)nslot));
+}
+
 ZOO_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

@@ -4,6 +4,9 @@
 namespace zoo {
 
 // Implicit-GEMM conv / GEMM geometry (igemm.hip).
+// Per-channel statistics buffers in slotted form: [2C final][slots x 2C][counter]
+constexpr int kStatSlots = 16;
+
 struct ConvGeom {
   int N, H, W, C;        // input activation, NHWC
   int K;                 // output channels (GEMM N dimension)
@@ -18,6 +21,9 @@ struct ConvGeom {
   // optional output-row remap (strided scatter into a larger NHWC tensor):
   // row (n,p,q) -> ((n*oH + oh0 + osh*p)*oW + ow0 + osw*q)*K
   int omap, oH, oW, osh, osw, oh0, ow0;
+  // >0: per-channel statistics go through `stat_slots` contention-spreading slots
+  // (see slotted_stats in common.h); 0: direct atomics into the [2*K] buffer
+  int stat_slots;
 };
 
 // Fused BatchNorm-backward statistics in a dgrad epilogue: the conv computing

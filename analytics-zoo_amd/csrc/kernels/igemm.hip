@@ -318,14 +318,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
       }
     }
     __syncthreads();
+    float* const dst = g.stat_slots > 0 ? slot_ptr(sacc, 2 * g.K, g.stat_slots) : sacc;
     if (tid < BN) {
       const int col = n0 + tid;
       if (col < g.K) {
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
-        atomicAdd(sacc + col, a);
-        atomicAdd(sacc + g.K + col, b);
+        atomicAdd(dst + col, a);
+        atomicAdd(dst + g.K + col, b);
       }
     }
   }

@@ -24,7 +24,8 @@ hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, co
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                             hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, const WgradGeom*, hipStream_t);
-hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int,
+hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
+hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
                             float*, float*, int, int, float, float, int, int, hipStream_t);
@@ -77,6 +78,9 @@ void check_hip(hipError_t e, const char* what) {
   TORCH_CHECK(e == hipSuccess, "zoo HIP kernel launch failed in ", what, ": ", hipGetErrorString(e));
 }
 
+// slotted per-channel statistics buffer: [2C final][kStatSlots x 2C][counter, padded to 4 floats]
+int64_t stat_len(int64_t C) { return 2 * C * (zoo::kStatSlots + 1) + 4; }
+
 void req(const torch::Tensor& t, at::ScalarType dt, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
   TORCH_CHECK(t.scalar_type() == dt, name, " has dtype ", t.scalar_type(), ", expected ", dt);
@@ -90,7 +94,7 @@ T* opt_ptr(const c10::optional<torch::Tensor>& t) {
 
 ConvGeom make_geom(const torch::Tensor& x, int K, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
                    int lh, int lw, int ldb) {
-  ConvGeom g;
+  ConvGeom g{};
   g.N = x.size(0); g.H = x.size(1); g.W = x.size(2); g.C = x.size(3);
   g.K = K; g.R = R; g.S = S;
   g.sh = sh; g.sw = sw; g.ph = ph; g.pw = pw; g.dh = dh; g.dw = dw; g.lh = lh; g.lw = lw;
@@ -156,14 +160,18 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   float* sp = nullptr;
   if (stats.has_value() && stats->defined()) {
     req(*stats, at::kFloat, "stats");
-    TORCH_CHECK(stats->numel() == 2 * K, "stats must hold 2*K floats");
+    TORCH_CHECK(stats->numel() == 2 * K || stats->numel() == stat_len(K),
+                "stats must hold 2*K floats (or the slotted stat_len(K))");
+    g.stat_slots = stats->numel() == 2 * K ? 0 : zoo::kStatSlots;
     TORCH_CHECK(out_bf16, "stats require the bf16 output");
     sp = stats->data_ptr<float>();
   }
   BwdStats bs{nullptr, nullptr, nullptr, nullptr, nullptr};
   if (bsums.has_value() && bsums->defined()) {
     req(*bsums, at::kFloat, "bn sums");
-    TORCH_CHECK(bsums->numel() == 2 * K, "bn sums must be [2*K]");
+    TORCH_CHECK(bsums->numel() == 2 * K || bsums->numel() == stat_len(K),
+                "bn sums must be [2*K] (or the slotted stat_len(K))");
+    g.stat_slots = bsums->numel() == 2 * K ? 0 : zoo::kStatSlots;
     TORCH_CHECK(by.has_value() && bmean.has_value() && binv.has_value(), "fused bn-backward needs y/mean/inv");
     req(*by, at::kBFloat16, "bn y");
     req(*bmean, at::kFloat, "bn mean");
@@ -197,6 +205,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   check_hip(zoo_igemm(x.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
                       out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, &bs, cur_stream()),
             "igemm");
+  if (g.stat_slots > 0)
+    check_hip(zoo_stats_finalize(sp ? sp : bs.sums, 2 * K, g.stat_slots, cur_stream()), "stats_finalize");
   return out_bf16 ? y : yf;
 }
 
@@ -247,7 +257,8 @@ void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<to
   const int C = a.size(-1);
   const int64_t M = a.numel() / C;
   TORCH_CHECK(C % 8 == 0, "bn_reduce: C must be a multiple of 8");
-  TORCH_CHECK(out.numel() == 2 * C, "bn_reduce: out must be [2*C]");
+  TORCH_CHECK(out.numel() == 2 * C || out.numel() == stat_len(C), "bn_reduce: out must be [2*C] or stat_len(C)");
+  const int nslot = out.numel() == 2 * C ? 0 : zoo::kStatSlots;
   if (mode == 1) {
     TORCH_CHECK(x.has_value() && mean.has_value() && invstd.has_value(), "bn_reduce mode 1 needs x/mean/invstd");
     req(*x, at::kBFloat16, "x");
@@ -258,7 +269,7 @@ void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<to
     }
   }
   check_hip(zoo_bn_reduce(a.data_ptr(), opt_ptr<void>(z), opt_ptr<void>(x), opt_ptr<float>(mean),
-                          opt_ptr<float>(invstd), out.data_ptr<float>(), (int)M, C, mode, cur_stream()),
+                          opt_ptr<float>(invstd), out.data_ptr<float>(), (int)M, C, mode, nslot, cur_stream()),
             "bn_reduce");
 }
 
@@ -276,7 +287,7 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
   TORCH_CHECK(smean.numel() == C && sinv.numel() == C, "bn: save buffers must be [C]");
   if (training) {
     req(stats, at::kFloat, "stats");
-    TORCH_CHECK(stats.numel() == 2 * C, "bn: stats must be [2*C]");
+    TORCH_CHECK(stats.numel() >= 2 * C, "bn: stats must hold [2*C]");
   } else {
     TORCH_CHECK(rmean.has_value() && rvar.has_value(), "bn eval needs running stats");
   }
@@ -304,7 +315,7 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dz, c10::optional<torch::T
   const int64_t M = x.numel() / C;
   TORCH_CHECK(C % 8 == 0, "bn_bwd: C must be a multiple of 8");
   req(sums, at::kFloat, "sums");
-  TORCH_CHECK(sums.numel() == 2 * C, "bn_bwd: sums must be [2*C]");
+  TORCH_CHECK(sums.numel() >= 2 * C, "bn_bwd: sums must hold [2*C]");
   if (z.has_value() && z->defined()) {
     req(*z, at::kBFloat16, "z");
     TORCH_CHECK(z->numel() == x.numel(), "bn_bwd: z shape");
@@ -759,6 +770,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("flip_weights", &flip_weights);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("bn_reduce", &bn_reduce);
+  m.def("stat_len", &stat_len);
   m.def("bn_fwd_apply", &bn_fwd_apply);
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);

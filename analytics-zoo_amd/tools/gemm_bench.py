@@ -48,6 +48,9 @@ def main():
         f = 2.0 * M * N * K
         t_z = timeit(lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0,
                                         None, [], None, None, None, None, None))
+        st = torch.zeros(C.stat_len(N), device=dev)  # slotted statistics (as the BN path uses)
+        t_zs = timeit(lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, st, 0, False, True, 0, 0,
+                                         None, [], None, None, None, None, None))
         t_t = float("nan") if a.zoo_only else timeit(lambda: torch.matmul(x, w.t()))
         t_g = timeit(lambda: C.gemm(x, w, None, None, None, 0, False, True, None, None, None, None, None))
         err = float((C.gemm(x, w, None, None, None, 0, True, False, None, None, None, None, None) -
@@ -55,7 +58,7 @@ def main():
         byts = 2.0 * (M * K + N * K + M * N)
         rows.append({"M": M, "N": N, "K": K, "gemm256_TF": round(f / t_g / 1e12, 1), "gemm256_err": err,
                      "zoo_TF": round(f / t_z / 1e12, 1), "torch_TF": round(f / t_t / 1e12, 1),
-                     "zoo_us": round(t_z * 1e6, 1), "torch_us": round(t_t * 1e6, 1),
+                     "zoo_us": round(t_z * 1e6, 1), "zoo_stats_us": round(t_zs * 1e6, 1), "torch_us": round(t_t * 1e6, 1),
                      "zoo_TBps": round(byts / t_z / 1e12, 2)})
         print(json.dumps(rows[-1]), flush=True)
 

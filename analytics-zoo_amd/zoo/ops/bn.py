@@ -22,6 +22,15 @@ from zoo.ops._native import native
 from zoo.ops import _kern, workspace
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
 
+# Per-channel statistics buffers are "slotted" ([2C final][STAT_SLOTS x 2C][counter]):
+# producers spread their atomics over the slots and the last block folds them
+# (csrc/kernels/common.h slotted_finalize). Must match zoo::kStatSlots.
+STAT_SLOTS = 16
+
+
+def stat_len(c):
+    return 2 * int(c) * (STAT_SLOTS + 1) + 4
+
 
 def _notify(p):
     hook = getattr(p, "_zoo_grad_ready", None)
@@ -61,7 +70,7 @@ class BNProducer:
         self.fused = False
 
     def bstats(self):
-        self.sums = workspace.zeros(2 * self.y.shape[-1], self.y.device)
+        self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
         self.fused = True
         return (self.z, self.y, self.mean, self.inv, self.sums)
 
@@ -75,7 +84,7 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.handoff_out, ctx.handoff_in = handoff_out, handoff_in
         ctx.producer_in = producer_in
         wb = bf16_weight(w)
-        stats = workspace.zeros(2 * K, x.device) if training else None
+        stats = workspace.zeros(stat_len(K), x.device) if training else None
         y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
         smean = torch.empty(K, device=x.device, dtype=torch.float32)
         sinv = torch.empty(K, device=x.device, dtype=torch.float32)
@@ -110,7 +119,7 @@ class _ConvBNActFn(torch.autograd.Function):
             dresid = dz if has_resid else None
             po.fused, po.sums = False, None
         else:
-            sums = workspace.zeros(2 * K, dz.device)
+            sums = workspace.zeros(stat_len(K), dz.device)
             C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
             outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, has_resid, dgam, dbet)
             dy = outs[0]
@@ -211,7 +220,7 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, y, gamma, beta, resid, running_mean, running_var, eps, momentum, relu, training):
         C_ = native()
         K = y.shape[-1]
-        stats = workspace.zeros(2 * K, y.device)
+        stats = workspace.zeros(stat_len(K), y.device)
         if training:
             C_.bn_reduce(y, None, None, None, None, stats, 0)
         smean = torch.empty(K, device=y.device, dtype=torch.float32)
@@ -228,7 +237,7 @@ class _BNActFn(torch.autograd.Function):
         y, gamma, beta, z, smean, sinv = ctx.saved_tensors
         dz = dz.contiguous().to(torch.bfloat16)
         K = y.shape[-1]
-        sums = workspace.zeros(2 * K, dz.device)
+        sums = workspace.zeros(stat_len(K), dz.device)
         C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
         dgam, own_g = _grad_target(gamma)
         dbet, own_b = _grad_target(beta)
