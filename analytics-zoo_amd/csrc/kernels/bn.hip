@@ -253,13 +253,17 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   }
 }
 
-// fold the statistic slots: buf[i] = sum_k buf[n2*(1+k) + i]
+// fold the statistic slots: buf[i] = sum_k buf[n2*(1+k) + i]; a block owns 64
+// columns, its 4 waves split the slots and meet in LDS
 __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__ buf, int n2, int nslot) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n2) return;
+  __shared__ float part[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
   float s = 0.f;
-  for (int k = 0; k < nslot; ++k) s += buf[(size_t)n2 * (1 + k) + i];
-  buf[i] = s;
+  if (c < n2)
+    for (int k = w; k < nslot; k += 4) s += buf[(size_t)n2 * (1 + k) + c];
+  part[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && c < n2) buf[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
 // contiguous row range per block: ~1024 blocks, at least 8 rows per thread-row
@@ -277,7 +281,7 @@ static int apply_rows_per_block(int M, int C) {
 using namespace zoo;
 
 extern "C" hipError_t zoo_stats_finalize(float* buf, int n2, int nslot, hipStream_t st) {
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2 + 255) / 256), dim3(256), 0, st, buf, n2, nslot);
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2 + 63) / 64), dim3(256), 0, st, buf, n2, nslot);
   return hipGetLastError();
 }
 

@@ -19,6 +19,8 @@
 // The epilogue stages the fp32 accumulators through LDS so that every global
 // store is a full 16-byte row segment, and optionally fuses bias, residual add,
 // activation and per-channel BatchNorm statistics (sum, sum of squares).
+#include <stdlib.h>
+
 #include "common.h"
 #include "geom.h"
 
@@ -214,6 +216,35 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   // ---- epilogue: stage fp32 tile in LDS, then row-contiguous 16-byte stores ----
   constexpr int EPI_LD = BN + 4;  // fp32 pitch: rows r and r+4 land 16 banks apart
   float* Cs = reinterpret_cast<float*>(smem);
+  // Plain forward conv with BN statistics (no bias/residual/activation): reduce the
+  // statistics straight from the accumulators (bf16-rounded, as stored) -- column
+  // sums over the wave's 64 rows need two cross-lane steps -- and park the two
+  // row-waves' partials next to the staging tile; no extra barrier is needed.
+  const bool reg_stats = stats && !bias && !resid && act == 0 && !Yf && !g.omap;
+  float* wstat = Cs + BM * EPI_LD;  // [2 wm][BN][2]
+  if (reg_stats) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float q = bf2f(f2bf(acc[i][j][r]));
+          a += q;
+          b += q * q;
+        }
+      a += __shfl_xor(a, 16, 64);
+      b += __shfl_xor(b, 16, 64);
+      a += __shfl_xor(a, 32, 64);
+      b += __shfl_xor(b, 32, 64);
+      if (fq == 0) {
+        const int col = wn * WN + j * 16 + fr;
+        wstat[(wm * BN + col) * 2 + 0] = a;
+        wstat[(wm * BN + col) * 2 + 1] = b;
+      }
+    }
+  }
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
@@ -278,7 +309,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     if (Y) {
       const uint4 pk = pack8(v);
       *reinterpret_cast<uint4*>(Y + off) = pk;
-      if (stats) {  // statistics of the values actually stored (bf16-rounded)
+      if (stats && !reg_stats) {  // statistics of the values actually stored (bf16-rounded)
         float q[8];
         unpack8(pk, q);
 #pragma unroll
@@ -296,6 +327,14 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     }
   }
 
+  if (reg_stats) {
+    float* const dst = g.stat_slots > 0 ? slot_ptr(stats, 2 * g.K, g.stat_slots) : stats;
+    if (tid < BN && n0 + tid < g.K) {
+      atomicAdd(dst + n0 + tid, wstat[tid * 2] + wstat[(BN + tid) * 2]);
+      atomicAdd(dst + g.K + n0 + tid, wstat[tid * 2 + 1] + wstat[(BN + tid) * 2 + 1]);
+    }
+    return;
+  }
   float* const sacc = stats ? stats : bs.sums;
   if (sacc) {
     // threads sharing a column chunk: tid % CPR equal. Reduce within the wave
@@ -351,7 +390,7 @@ __global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __rest
 
 size_t igemm_smem_bytes(int BN) {
   const size_t main_bytes = (size_t)2 * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
-  const size_t epi_bytes = (size_t)IG_BM * (BN + 4) * sizeof(float);
+  const size_t epi_bytes = (size_t)IG_BM * (BN + 4) * sizeof(float) + (size_t)2 * BN * 2 * sizeof(float);
   return main_bytes > epi_bytes ? main_bytes : epi_bytes;
 }
 
@@ -376,11 +415,18 @@ template <int VEC, bool IS1x1, bool LDIL>
 static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                                const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                                hipStream_t st) {
-  // narrow output-channel counts waste half of a 128-wide tile: use BN=64 there
+  static const int force_bn = [] {
+    const char* e = getenv("ZOO_IGEMM_BN");
+    return e ? atoi(e) : 0;
+  }();
+  if (force_bn == 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (force_bn == 128) return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  // BN=64 tiles (lower VGPR/LDS footprint, more workgroups in flight) win while
+  // there are plenty of them; few large tiles win when the grid is small
+  // (tools/gemm_bench.py sweep on ResNet-50 shapes)
   if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  const long tiles128 = (long)((g.M + IG_BM - 1) / IG_BM) * ((g.K + 127) / 128);
-  if (tiles128 < 512)  // not enough workgroups to fill 256 CUs twice -> smaller tiles
-    return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  const long tiles64 = (long)((g.M + IG_BM - 1) / IG_BM) * ((g.K + 63) / 64);
+  if (tiles64 >= 1536) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 

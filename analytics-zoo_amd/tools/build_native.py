@@ -68,7 +68,7 @@ def build_kernels(force=False, jobs=8, verbose=True):
     bsrc = os.path.join(CSRC, "ops.cpp")
     bobj = os.path.join(BUILD, "ops.cpp.o")
     objs.append(bobj)
-    if force or _newer([bsrc], bobj):
+    if force or _newer([bsrc] + headers, bobj):
         tasks.append(["g++", "-O2", "-fPIC", "-std=c++17", "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1",
                       "-DTORCH_EXTENSION_NAME=_C", "-DTORCH_API_INCLUDE_EXTENSION_H",
                       "-D_GLIBCXX_USE_CXX11_ABI=1"] + ["-I" + p for p in tinc] +
