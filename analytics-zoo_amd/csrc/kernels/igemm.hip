@@ -44,8 +44,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   constexpr int B_ROWS_PER_THREAD = BN / 32;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // single-K-tile GEMMs (1x1 convs with C <= 64) need no second stage buffer:
+  // the launcher then sizes LDS for one stage, which raises occupancy
+  const int nbuf = g.ldb > BK ? 2 : 1;
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);
-  bf16_t* Bs = As + 2 * BM * BK;
+  bf16_t* Bs = As + nbuf * BM * BK;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -388,8 +391,8 @@ __global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __rest
   }
 }
 
-size_t igemm_smem_bytes(int BN) {
-  const size_t main_bytes = (size_t)2 * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
+size_t igemm_smem_bytes(int BN, int nbuf = 2) {
+  const size_t main_bytes = (size_t)nbuf * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
   const size_t epi_bytes = (size_t)IG_BM * (BN + 4) * sizeof(float) + (size_t)2 * BN * 2 * sizeof(float);
   return main_bytes > epi_bytes ? main_bytes : epi_bytes;
 }
@@ -399,11 +402,11 @@ static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* 
                             const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                             hipStream_t st) {
   const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
-  const size_t smem = igemm_smem_bytes(BN);
+  const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1);
   static bool attr_set = false;
   if (!attr_set) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN));
     attr_set = true;
   }
   hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
