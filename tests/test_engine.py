@@ -220,7 +220,8 @@ def _dp_worker(rank, world, port, mode, out_q):
     for step in range(3):
         sl = slice(rank * 8 + step * 16, rank * 8 + step * 16 + 8)  # each rank: its half of a 16-batch
         eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
-    out_q.put((rank, eng.flat.master.clone()))
+    # numpy, not a shared-memory tensor: the fd-backed storage dies with this process
+    out_q.put((rank, eng.flat.master.detach().cpu().numpy().copy()))
     ctx.stop()
 
 
@@ -232,7 +233,7 @@ def test_data_parallel_gloo_matches_single_process(mode):
     procs = [ctx_mp.Process(target=_dp_worker, args=(r, 2, port, mode, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = {r: torch.from_numpy(v) for r, v in (q.get(timeout=240) for _ in range(2))}
     for p in procs:
         p.join(timeout=60)
     assert torch.allclose(res[0], res[1], atol=1e-6), "ranks diverged"
