@@ -55,4 +55,25 @@ struct WgradGeom {
   int m_per_split;     // multiple of 64
 };
 
+// Recurrent cells (rnn.hip). Activation codes shared with zoo/ops/rnn.py.
+enum RnnAct : int { RA_LINEAR = 0, RA_TANH = 1, RA_SIGMOID = 2, RA_HSIG = 3, RA_RELU = 4 };
+enum RnnCell : int { CELL_RNN = 0, CELL_LSTM = 1, CELL_GRU = 2 };
+
+struct RnnArgs {
+  const float* xw;     // [B, T, G*H] input projections (bias included)
+  const void* u;       // bf16: U [G*H, H] (forward) or U^T [H, G*H] (backward)
+  const float* h0;     // [B, H] or null (zeros)
+  const float* c0;     // [B, H] or null (LSTM)
+  float* hseq;         // [B, T, H] (forward output; backward input)
+  float* cseq;         // [B, T, H] LSTM cell states or null
+  float* gates;        // [B, T, G*H] activated gates or null
+  float* cT;           // [B, H] final LSTM cell state or null
+  const float* dhseq;  // [B, T, H] or null (backward)
+  const float* dcT;    // [B, H] or null (backward, LSTM)
+  float* dgates;       // [B, T, G*H] (backward)
+  float* dh0;          // [B, H] or null (backward)
+  float* dc0;          // [B, H] or null (backward, LSTM)
+  int B, T, act, iact;
+};
+
 }  // namespace zoo

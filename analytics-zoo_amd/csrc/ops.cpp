@@ -66,6 +66,7 @@ hipError_t zoo_qgemm(const void*, const void*, const float*, const float*, const
                      int, int, int, hipStream_t);
 hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
                         float, int, hipStream_t);
+hipError_t zoo_rnn(const zoo::RnnArgs*, int, int, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
@@ -760,6 +761,113 @@ torch::Tensor qgemm(torch::Tensor a, torch::Tensor w, torch::Tensor amax, torch:
   return y;
 }
 
+
+// ---- persistent recurrent cells (rnn.hip): cell 0 SimpleRNN, 1 LSTM, 2 GRU ----
+int rnn_gates(int64_t cell) {
+  TORCH_CHECK(cell >= 0 && cell <= 2, "rnn: cell must be 0 (SimpleRNN), 1 (LSTM) or 2 (GRU)");
+  return cell == 1 ? 4 : (cell == 2 ? 3 : 1);
+}
+
+void rnn_check_state(const c10::optional<torch::Tensor>& s, int64_t B, int64_t H, const char* name) {
+  if (s.has_value() && s->defined()) {
+    req(*s, at::kFloat, name);
+    TORCH_CHECK(s->dim() == 2 && s->size(0) == B && s->size(1) == H, "rnn: ", name, " must be [B, H]");
+  }
+}
+
+void rnn_check_acts(int64_t act, int64_t iact) {
+  TORCH_CHECK(act >= 0 && act <= 4 && iact >= 0 && iact <= 4, "rnn: unsupported activation code");
+}
+
+// xw [B, T, G*H] fp32 (bias included), u [G*H, H] bf16 -> {hseq [B,T,H], cT [B,H] (LSTM), cseq, gates}
+std::vector<torch::Tensor> rnn_fwd(torch::Tensor xw, torch::Tensor u, c10::optional<torch::Tensor> h0,
+                                   c10::optional<torch::Tensor> c0, int64_t cell, int64_t act, int64_t iact,
+                                   bool save) {
+  req(xw, at::kFloat, "xw");
+  req(u, at::kBFloat16, "u");
+  const int G = rnn_gates(cell);
+  rnn_check_acts(act, iact);
+  TORCH_CHECK(u.dim() == 2 && u.size(0) == G * u.size(1), "rnn_fwd: u must be [G*H, H]");
+  const int64_t H = u.size(1);
+  TORCH_CHECK(H == 32 || H == 64 || H == 128 || H == 256, "rnn_fwd: hidden size must be 32/64/128/256 (pad it)");
+  TORCH_CHECK(xw.dim() == 3 && xw.size(2) == G * H, "rnn_fwd: xw must be [B, T, G*H]");
+  const int64_t B = xw.size(0), T = xw.size(1);
+  rnn_check_state(h0, B, H, "h0");
+  rnn_check_state(c0, B, H, "c0");
+  auto f32 = xw.options();
+  auto hseq = torch::empty({B, T, H}, f32);
+  torch::Tensor cT, cseq, gates;
+  if (cell == 1) cT = torch::empty({B, H}, f32);
+  if (save && cell == 1) cseq = torch::empty({B, T, H}, f32);
+  if (save && cell != 0) gates = torch::empty({B, T, G * H}, f32);
+  zoo::RnnArgs a{};
+  a.xw = xw.data_ptr<float>();
+  a.u = u.data_ptr();
+  a.h0 = opt_ptr<float>(h0);
+  a.c0 = opt_ptr<float>(c0);
+  a.hseq = hseq.data_ptr<float>();
+  a.cseq = cseq.defined() ? cseq.data_ptr<float>() : nullptr;
+  a.gates = gates.defined() ? gates.data_ptr<float>() : nullptr;
+  a.cT = cT.defined() ? cT.data_ptr<float>() : nullptr;
+  a.B = (int)B; a.T = (int)T; a.act = (int)act; a.iact = (int)iact;
+  check_hip(zoo_rnn(&a, (int)cell, (int)H, 0, cur_stream()), "rnn_fwd");
+  return {hseq, cT, cseq, gates};
+}
+
+// ut = U^T [H, G*H] bf16 -> {dgates [B,T,G*H] (= d xw), dh0 [B,H], dc0 [B,H] (LSTM)}
+std::vector<torch::Tensor> rnn_bwd(c10::optional<torch::Tensor> dhseq, c10::optional<torch::Tensor> dcT,
+                                   torch::Tensor ut, torch::Tensor hseq, c10::optional<torch::Tensor> cseq,
+                                   c10::optional<torch::Tensor> gates, c10::optional<torch::Tensor> h0,
+                                   c10::optional<torch::Tensor> c0, int64_t cell, int64_t act, int64_t iact) {
+  req(ut, at::kBFloat16, "ut");
+  req(hseq, at::kFloat, "hseq");
+  const int G = rnn_gates(cell);
+  rnn_check_acts(act, iact);
+  TORCH_CHECK(ut.dim() == 2 && ut.size(1) == G * ut.size(0), "rnn_bwd: ut must be [H, G*H]");
+  const int64_t H = ut.size(0);
+  TORCH_CHECK(H == 32 || H == 64 || H == 128 || H == 256, "rnn_bwd: hidden size must be 32/64/128/256");
+  TORCH_CHECK(hseq.dim() == 3 && hseq.size(2) == H, "rnn_bwd: hseq must be [B, T, H]");
+  const int64_t B = hseq.size(0), T = hseq.size(1);
+  if (dhseq.has_value() && dhseq->defined()) {
+    req(*dhseq, at::kFloat, "dhseq");
+    TORCH_CHECK(dhseq->sizes() == hseq.sizes(), "rnn_bwd: dhseq shape");
+  }
+  rnn_check_state(dcT, B, H, "dcT");
+  rnn_check_state(h0, B, H, "h0");
+  rnn_check_state(c0, B, H, "c0");
+  if (cell == 1) {
+    TORCH_CHECK(cseq.has_value() && cseq->defined(), "rnn_bwd: LSTM needs the saved cell states");
+    req(*cseq, at::kFloat, "cseq");
+    TORCH_CHECK(cseq->sizes() == hseq.sizes(), "rnn_bwd: cseq shape");
+  }
+  if (cell != 0) {
+    TORCH_CHECK(gates.has_value() && gates->defined(), "rnn_bwd: saved gates required");
+    req(*gates, at::kFloat, "gates");
+    TORCH_CHECK(gates->dim() == 3 && gates->size(0) == B && gates->size(1) == T && gates->size(2) == G * H,
+                "rnn_bwd: gates shape");
+  }
+  auto f32 = hseq.options();
+  auto dgates = torch::empty({B, T, G * H}, f32);
+  auto dh0 = torch::empty({B, H}, f32);
+  torch::Tensor dc0;
+  if (cell == 1) dc0 = torch::empty({B, H}, f32);
+  zoo::RnnArgs a{};
+  a.u = ut.data_ptr();
+  a.h0 = opt_ptr<float>(h0);
+  a.c0 = opt_ptr<float>(c0);
+  a.hseq = hseq.data_ptr<float>();
+  a.cseq = opt_ptr<float>(cseq);
+  a.gates = opt_ptr<float>(gates);
+  a.dhseq = opt_ptr<float>(dhseq);
+  a.dcT = opt_ptr<float>(dcT);
+  a.dgates = dgates.data_ptr<float>();
+  a.dh0 = dh0.data_ptr<float>();
+  a.dc0 = dc0.defined() ? dc0.data_ptr<float>() : nullptr;
+  a.B = (int)B; a.T = (int)T; a.act = (int)act; a.iact = (int)iact;
+  check_hip(zoo_rnn(&a, (int)cell, (int)H, 1, cur_stream()), "rnn_bwd");
+  return {dgates, dh0, dc0};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -796,4 +904,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("im2col_q8", &im2col_q8);
   m.def("qgemm", &qgemm);
   m.def("attn_bwd", &attn_bwd);
+  m.def("rnn_fwd", &rnn_fwd);
+  m.def("rnn_bwd", &rnn_bwd);
 }

@@ -3,8 +3,11 @@
 Zs LSTM.scala:71-80, GRU, SimpleRNN, InternalRecurrent.scala:80-140).
 
 The input projection of ALL timesteps is one GEMM on the native MFMA kernel
-(``zoo.ops.linear`` over [batch*steps, input_dim]); the recurrence then does
-one [batch, hidden] x [hidden, gates*hidden] GEMM per step plus the gate math.
+(``zoo.ops.linear`` over [batch*steps, input_dim]). On the GPU the whole
+recurrence (forward and BPTT) is then ONE persistent HIP kernel launch
+(``zoo.ops.rnn``, csrc/kernels/rnn.hip) for hidden sizes up to 256; the
+per-step path below (one [batch, hidden] x [hidden, gates*hidden] GEMM per step
+plus the gate math) is the CPU reference and the fallback for wider layers.
 Gate order follows Keras 1: LSTM (i, f, c, o), GRU (z, r, h).
 """
 import torch
@@ -12,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.ops import rnn as rnn_ops
 from zoo.pipeline.api.keras.base import Layer, apply_activation, init_tensor
 
 
@@ -60,6 +64,23 @@ class _RNNBase(Layer):
         return out
 
     _n_state = 1
+    _cell = None  # zoo.ops.rnn cell name of the fused GPU path
+
+    def _fused_ok(self, x):
+        acts = (self.activation,) if self._cell == "rnn" else (self.activation, self.inner_activation)
+        return self._cell is not None and rnn_ops.supported(x, self.output_dim, *acts)
+
+    def _call_fused(self, x, init):
+        h0 = init[0] if init else None
+        c0 = init[1] if (init and len(init) > 1) else None
+        hseq, hT, cT = rnn_ops.recurrent(x, self.W, self.b, self.U, self._cell, self.activation,
+                                         self.inner_activation if self._cell != "rnn" else None, h0=h0, c0=c0,
+                                         go_backwards=self.go_backwards)
+        dt = x.dtype if x.is_floating_point() else hseq.dtype
+        out = (hseq if self.return_sequences else hT).to(dt)
+        if self.return_state:
+            return [out, hT.to(dt)] + ([cT.to(dt)] if cT is not None else [])
+        return out
 
     def _step(self, xt, state):
         raise NotImplementedError
@@ -72,6 +93,8 @@ class _RNNBase(Layer):
         init = None
         if isinstance(x, (list, tuple)):  # [sequence, initial states...] (Seq2seq decoder / bridge)
             x, init = x[0], tuple(x[1:])
+        if self._fused_ok(x):
+            return self._call_fused(x, init)
         B, T, D = x.shape
         xw = ops.linear(x.reshape(B * T, D), self.W, self.b).reshape(B, T, -1)
         state = self._init_state(x) if not init else tuple(t.to(xw.dtype) for t in init)
@@ -89,6 +112,7 @@ class _RNNBase(Layer):
 
 class SimpleRNN(_RNNBase):
     n_gates = 1
+    _cell = "rnn"
 
     def __init__(self, output_dim, activation="tanh", return_sequences=False, go_backwards=False,
                  W_regularizer=None, U_regularizer=None, b_regularizer=None, input_shape=None, **kwargs):
@@ -103,6 +127,7 @@ class SimpleRNN(_RNNBase):
 class LSTM(_RNNBase):
     n_gates = 4
     _n_state = 2
+    _cell = "lstm"
 
     def _init_state(self, x):
         z = x.new_zeros(x.shape[0], self.output_dim)
@@ -123,6 +148,7 @@ class LSTM(_RNNBase):
 
 class GRU(_RNNBase):
     n_gates = 3
+    _cell = "gru"
 
     def _step(self, xt, state):
         (h,) = state
