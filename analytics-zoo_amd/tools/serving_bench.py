@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Serving benchmark (BASELINE.json config "Cluster Serving batched inference:
+ResNet-50 + BERT-base, throughput + p50 latency").
+
+  serving_bench.py model [--iters N]   InferenceModel (hipGraph replica) throughput and
+                                       p50/p99 latency per batch size: ResNet-50 bf16,
+                                       ResNet-50 int8, BERT-base (seq 128)
+  serving_bench.py e2e [--images N]    end-to-end Cluster Serving: JPEG images through the
+                                       RESP (Redis-protocol) queue -> batching worker ->
+                                       GPU resize/normalize -> ResNet-50 -> top-N results
+
+Random-init weights, synthetic inputs. Prints one JSON line per measurement.
+"""
+import argparse
+import io
+import json
+import os
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+
+def _pct(v, q):
+    return float(np.percentile(np.asarray(v), q))
+
+
+def bench_model(name, im, make_input, batches, iters):
+    for bs in batches:
+        x = make_input(bs)
+        for _ in range(3):
+            im.predict(x)
+        lat = []
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            t = time.perf_counter()
+            im.predict(x)
+            lat.append((time.perf_counter() - t) * 1e3)
+        el = time.perf_counter() - t0
+        print(json.dumps({"bench": "serving-model", "model": name, "batch": bs, "throughput": round(bs * iters / el, 1),
+                          "unit": "records/sec", "p50_ms": round(_pct(lat, 50), 3), "p99_ms": round(_pct(lat, 99), 3),
+                          "n_gpus": 1, "data": "synthetic"}), flush=True)
+
+
+def run_models(a):
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.resnet import resnet50
+    from zoo.pipeline.api.keras.layers import BERT
+    from zoo.pipeline.inference import InferenceModel
+    init_nncontext("serving-bench")
+    torch.manual_seed(0)
+    rn = resnet50()
+    im = InferenceModel(1).load_module(rn)
+    bench_model("ResNet-50 bf16", im, lambda b: torch.randn(b, 3, 224, 224), [1, 8, 32, 128, 256], a.iters)
+    im8 = InferenceModel(1).load_module(resnet50(), blas=False)
+    bench_model("ResNet-50 int8", im8, lambda b: torch.randn(b, 3, 224, 224), [1, 32, 256], a.iters)
+    L = 128
+    bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512, intermediate_size=3072,
+                output_all_block=False)
+
+    class Head(torch.nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.m = m
+
+        def forward(self, xs):
+            return self.m(xs)[1]  # pooled output [B, 768]
+
+    imb = InferenceModel(1).load_module(Head(bert))
+
+    def bert_in(b):
+        tok = torch.randint(0, 30522, (b, L))
+        return [tok, torch.zeros(b, L, dtype=torch.long), torch.arange(L).repeat(b, 1), torch.ones(b, L)]
+    bench_model("BERT-base seq128", imb, bert_in, [1, 8, 32, 128], a.iters)
+
+
+def run_e2e(a):
+    from PIL import Image
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.resnet import resnet50
+    from zoo.serving import ClusterServing, InputQueue, OutputQueue
+    from zoo.serving.resp import RespServer
+    import tempfile
+    init_nncontext("serving-e2e")
+    srv = RespServer("127.0.0.1", 0).start()
+    rng = np.random.default_rng(0)
+    jpgs = []
+    for _ in range(16):
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
+        jpgs.append(buf.getvalue())
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            cfg = os.path.join(d, "config.yaml")
+            open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,224,224\n  filter: topN(5)\n"
+                                 "params:\n  batch_size: %d\n" % (srv.port, a.batch))
+            s = ClusterServing(cfg, model=resnet50(), device="cuda")
+            inq, outq = InputQueue(cfg), OutputQueue(cfg)
+            # warm-up (graph capture for the batch shape)
+            for i in range(a.batch):
+                inq.enqueue_encoded("warm%d" % i, jpgs[i % len(jpgs)])
+            s.run(max_records=a.batch, idle_timeout=30)
+            outq.dequeue()
+            s.records = 0
+            sent = {}
+
+            def producer():
+                for i in range(a.images):
+                    sent["im%d" % i] = time.perf_counter()
+                    inq.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+            th = threading.Thread(target=producer)
+            t0 = time.perf_counter()
+            th.start()
+            done = {}
+            worker = threading.Thread(target=s.run, kwargs={"max_records": a.images, "idle_timeout": 30})
+            worker.start()
+            while len(done) < a.images and time.perf_counter() - t0 < 300:
+                for k in outq.dequeue():
+                    done.setdefault(k, time.perf_counter())
+                time.sleep(0.002)
+            worker.join()
+            th.join()
+            el = time.perf_counter() - t0
+            lat = [(done[k] - sent[k]) * 1e3 for k in done if k in sent]
+            print(json.dumps({"bench": "cluster-serving-e2e", "model": "ResNet-50 bf16", "batch": a.batch,
+                              "images": len(done), "throughput": round(len(done) / el, 1), "unit": "images/sec",
+                              "p50_ms": round(_pct(lat, 50), 2), "p99_ms": round(_pct(lat, 99), 2), "n_gpus": 1,
+                              "data": "synthetic 256x256 JPEG"}), flush=True)
+    finally:
+        srv.shutdown()
+        srv.server_close()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("mode", choices=["model", "e2e"])
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--images", type=int, default=2048)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
+    run_models(a) if a.mode == "model" else run_e2e(a)
+
+
+if __name__ == "__main__":
+    main()

@@ -78,6 +78,10 @@ class InputQueue(API):
         im.save(buf, format="JPEG", quality=95)
         return self._push({"uri": uri, "image": base64.b64encode(buf.getvalue()).decode()})
 
+    def enqueue_encoded(self, uri, jpeg_bytes):
+        """Enqueue an already-encoded JPEG/PNG (skips the client-side resize)."""
+        return self._push({"uri": uri, "image": base64.b64encode(bytes(jpeg_bytes)).decode()})
+
     def enqueue_tensor(self, uri, data):
         a = np.ascontiguousarray(np.asarray(data, np.float32))
         return self._push({"uri": uri, "tensor": base64.b64encode(a.tobytes()).decode(),
