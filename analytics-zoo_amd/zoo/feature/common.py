@@ -240,15 +240,23 @@ class ArrayFeatureSet(FeatureSet):
                 outs.append(o)
             return outs, tickets, idx
 
-        for b in range(min(depth, nb)):
-            pending.append(launch(b))
-        for b in range(nb):
-            outs, tickets, _idx = pending.pop(0)
-            for t in tickets:
-                g.wait(t)
-            if b + depth < nb:
-                pending.append(launch(b + depth))
-            yield self._split(outs)
+        try:
+            for b in range(min(depth, nb)):
+                pending.append(launch(b))
+            for b in range(nb):
+                outs, tickets, _idx = pending.pop(0)
+                for t in tickets:
+                    g.wait(t)
+                if b + depth < nb:
+                    pending.append(launch(b + depth))
+                yield self._split(outs)
+        finally:
+            # an abandoned epoch (exception / early break) must not free the
+            # destination buffers and index arrays while gather workers still
+            # write into / read from them
+            for _outs, tickets, _idx in pending:
+                for t in tickets:
+                    g.wait(t)
 
 
 class DataLoaderFeatureSet(FeatureSet):
