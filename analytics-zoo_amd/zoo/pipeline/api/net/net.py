@@ -5,7 +5,8 @@
   Net.load_caffe(def, model)     Caffe prototxt + caffemodel -> GraphNet
   Net.load_onnx(path)            ONNX ModelProto -> GraphNet
   Net.load_torch(path)           TorchScript -> TorchNet
-  Net.load_tf / load_keras       not available (no TF / Keras runtime here)
+  Net.load_tf(path, in, out)     TF frozen graph / SavedModel -> TFNet
+  Net.load_keras                 not available (no Keras runtime here)
 """
 
 
@@ -37,8 +38,10 @@ class Net:
 
     @staticmethod
     def load_tf(path, inputs=None, outputs=None, **kw):
-        raise NotImplementedError("TensorFlow graphs cannot be executed here (no TF runtime); export the graph "
-                                  "to ONNX and use Net.load_onnx")
+        """Frozen GraphDef / export folder / SavedModel -> TFNet (torch executor
+        of the TF graph, zoo.pipeline.api.net.tf_graph)."""
+        from zoo.tfpark.tfnet import TFNet
+        return TFNet(path, inputs, outputs, **kw)
 
     @staticmethod
     def load_keras(json_path=None, hdf5_path=None, by_name=False):

@@ -82,8 +82,16 @@ class _Replica:
         if dev.type != "cuda":
             return self._forward([t.to(dev) for t in xs])
         with torch.cuda.stream(self.stream):
+            g = None
             if self.owner.use_graph:
-                graph, sin, sout = self._graph_for(xs)
+                try:
+                    g = self._graph_for(xs)
+                except RuntimeError as e:  # model does host syncs inside forward: serve it eagerly
+                    log.warning("hipGraph capture failed (%s); serving this model without graphs", e)
+                    self.owner.use_graph = False
+                    self.graphs.clear()
+            if g is not None:
+                graph, sin, sout = g
                 for s, t in zip(sin, xs):
                     s.copy_(t, non_blocking=True)
                 graph.replay()
@@ -184,9 +192,13 @@ class InferenceModel:
         raise NotImplementedError("OpenVINO IR is a CPU runtime format; convert the model to ONNX / Caffe / a "
                                   "zoo model and use load_onnx / load_caffe / load")
 
-    def load_tensorflow(self, model_path, model_type="frozenModel", **kw):
-        raise NotImplementedError("TensorFlow graphs are not executed on this framework (no TF runtime on "
-                                  "ROCm here); export to ONNX and use load_onnx")
+    def load_tensorflow(self, model_path, model_type="frozenModel", inputs=None, outputs=None, **kw):
+        """TF frozen graph / export folder / SavedModel (doLoadTensorflow,
+        InferenceModel.scala:126-244) executed by TFNet on this device."""
+        from zoo.tfpark.tfnet import TFNet
+        sig = kw.get("signature")
+        tag = kw.get("tag") or "serve"
+        return self._install(TFNet(model_path, inputs, outputs, tag=tag, signature=sig))
 
     load_tf = load_tensorflow
 

@@ -14,10 +14,14 @@ front-end API is kept and backed by the framework itself:
                         (module-output, loss) spec, run by the engine
   * ``GanOptimMethod`` / ``GANEstimator`` -> alternating D / G steps over two
                         slices of ONE flat parameter buffer (generator first)
-Graph-import paths (``from_loss``, ``from_train_op``, frozen ``.pb``) need TF
-and raise; export such graphs to ONNX and use zoo.pipeline.api.onnx.
+  * ``TFNet``        -> a TF frozen graph / export_tf folder / SavedModel decoded
+                        from protobuf and executed op-by-op on torch (tfnet.py)
+Graph-building paths that need a live TF session (``from_loss``,
+``from_train_op``, ``TFNet.from_session``) raise: save the graph and load it
+with TFNet instead.
 """
 from zoo.tfpark.gan import GANEstimator, GanOptimMethod  # noqa: F401
 from zoo.tfpark.model import KerasModel  # noqa: F401
 from zoo.tfpark.tf_dataset import TFDataset  # noqa: F401
 from zoo.tfpark.tf_optimizer import TFEstimator, TFEstimatorSpec, TFOptimizer, ZooOptimizer  # noqa: F401
+from zoo.tfpark.tfnet import TFNet  # noqa: F401
