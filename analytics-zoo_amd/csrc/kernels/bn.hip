@@ -18,9 +18,18 @@
 //   apply  = dx = scale*(dy - mean(dy) - xhat*mean(dy*xhat)); optionally also
 //            emits dy for the residual branch; workgroup 0 writes dgamma/dbeta.
 // All passes move 8 bf16 per lane (16-byte vector loads, Guideline 13).
+#include <stdlib.h>
+
 #include "common.h"
 
 namespace zoo {
+
+ZOO_DEV void load8f(const float* __restrict__ p, int chunk, float* v) {
+  const float4 a = reinterpret_cast<const float4*>(p)[2 * chunk];
+  const float4 b = reinterpret_cast<const float4*>(p)[2 * chunk + 1];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
 
 // ---------------------------------------------------------------------------
 // channel reduction over [M][C]; mode 0: (x, x^2); mode 1: (dy, dy*xhat)
@@ -52,9 +61,10 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
       float s1[8], s2[8];
       float mu[8], is[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        s1[e] = 0.f; s2[e] = 0.f;
-        if (MODE == 1) { mu[e] = mean[chunk * 8 + e]; is[e] = invstd[chunk * 8 + e]; }
+      for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+      if (MODE == 1) {
+        load8f(mean, chunk, mu);
+        load8f(invstd, chunk, is);
       }
       for (int r = r0 + my_row; r < r1; r += row_step) {
         const size_t off = (size_t)r * C + chunk * 8;
@@ -137,30 +147,44 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
   const int cpr = C >> 3;
   const RowSplit rs = row_split(cpr);
   if (rs.rsub >= rs.rstep) return;
-  const int r0 = blockIdx.x * rows_per_block + rs.rsub, r1 = min(M, blockIdx.x * rows_per_block + rows_per_block);
+  // rows_per_block > 0: the block streams one contiguous row range; == 0: tiles of
+  // 4*rstep rows are dealt round-robin over the grid (concurrent blocks touch
+  // neighbouring memory)
+  const int tile = 4 * rs.rstep;
+  const bool inter = rows_per_block == 0;
+  const int r0 = (inter ? blockIdx.x * tile : blockIdx.x * rows_per_block) + rs.rsub;
+  const int r1 = inter ? M : min(M, blockIdx.x * rows_per_block + rows_per_block);
+  const int rstride = inter ? gridDim.x * tile : tile;
   for (int chunk = rs.chunk0; chunk < cpr; chunk += rs.lpr) {
     float sc[8], sh[8];
+    {
+      // per-channel coefficients with 16-byte loads (all vectors are 8-channel aligned)
+      float s1[8], s2[8], g8[8], b8[8];
+      load8f(training ? stats : running_mean, chunk, s1);
+      load8f(training ? stats + C : running_var, chunk, s2);
+      if (gamma) load8f(gamma, chunk, g8);
+      if (beta) load8f(beta, chunk, b8);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int c = chunk * 8 + e;
-      float mu, is;
-      if (training) {
-        mu = stats[c] * invM;
-        is = rsqrtf(fmaxf(stats[C + c] * invM - mu * mu, 0.f) + eps);
-      } else {
-        mu = running_mean[c];
-        is = rsqrtf(running_var[c] + eps);
+      for (int e = 0; e < 8; ++e) {
+        float mu, is;
+        if (training) {
+          mu = s1[e] * invM;
+          is = rsqrtf(fmaxf(s2[e] * invM - mu * mu, 0.f) + eps);
+        } else {
+          mu = s1[e];
+          is = rsqrtf(s2[e] + eps);
+        }
+        sc[e] = gamma ? g8[e] * is : is;
+        sh[e] = (beta ? b8[e] : 0.f) - mu * sc[e];
       }
-      sc[e] = gamma ? gamma[c] * is : is;
-      sh[e] = (beta ? beta[c] : 0.f) - mu * sc[e];
     }
     // 4 rows per step: four independent 16-byte loads (x 2 with a residual) in flight per thread
-    for (int rb = r0; rb < r1; rb += 4 * rs.rstep) {
+    for (int rb = r0; rb < r1; rb += rstride) {
       uint4 xv[4], rv[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int r = rb + u * rs.rstep;
-        const size_t off = (size_t)(r < r1 ? r : r0) * C + chunk * 8;
+        const size_t off = (size_t)(r < r1 ? r : rb) * C + chunk * 8;
         xv[u] = *reinterpret_cast<const uint4*>(X + off);
         if (resid) rv[u] = *reinterpret_cast<const uint4*>(resid + off);
       }
@@ -206,25 +230,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int cpr = C >> 3;
   const RowSplit rs = row_split(cpr);
   if (rs.rsub >= rs.rstep) return;
-  const int r0 = blockIdx.x * rows_per_block + rs.rsub, r1 = min(M, blockIdx.x * rows_per_block + rows_per_block);
+  const int tile = 2 * rs.rstep;
+  const bool inter = rows_per_block == 0;
+  const int r0 = (inter ? blockIdx.x * tile : blockIdx.x * rows_per_block) + rs.rsub;
+  const int r1 = inter ? M : min(M, blockIdx.x * rows_per_block + rows_per_block);
+  const int rstride = inter ? gridDim.x * tile : tile;
   for (int chunk = rs.chunk0; chunk < cpr; chunk += rs.lpr) {
     float ka[8], kb[8], kd[8];
+    float is8[8], mu8[8], g8[8], q1[8], q2[8];
+    load8f(save_invstd, chunk, is8);
+    load8f(save_mean, chunk, mu8);
+    load8f(sums, chunk, q1);
+    load8f(sums + C, chunk, q2);
+    if (gamma) load8f(gamma, chunk, g8);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const int c = chunk * 8 + e;
-      const float is = save_invstd[c], mu = save_mean[c];
-      const float a = (gamma ? gamma[c] : 1.f) * is;
-      const float m1 = sums[c] * invM, m2 = sums[C + c] * invM;
+      const float is = is8[e], mu = mu8[e];
+      const float a = (gamma ? g8[e] : 1.f) * is;
+      const float m1 = q1[e] * invM, m2 = q2[e] * invM;
       ka[e] = a;
       kb[e] = -a * is * m2;
       kd[e] = a * (mu * is * m2 - m1);
     }
-    for (int rb = r0; rb < r1; rb += 2 * rs.rstep) {
+    for (int rb = r0; rb < r1; rb += rstride) {
       uint4 dv[2], xv[2], zv[2];
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int r = rb + u * rs.rstep;
-        const size_t off = (size_t)(r < r1 ? r : r0) * C + chunk * 8;
+        const size_t off = (size_t)(r < r1 ? r : rb) * C + chunk * 8;
         dv[u] = *reinterpret_cast<const uint4*>(dZ + off);
         xv[u] = *reinterpret_cast<const uint4*>(X + off);
         if (Z) zv[u] = *reinterpret_cast<const uint4*>(Z + off);
@@ -266,12 +299,20 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
   if (w == 0 && c < n2) buf[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
-// contiguous row range per block: ~1024 blocks, at least 8 rows per thread-row
+// contiguous row range per block: ~kApplyBlocks blocks, at least kMinRows rows per thread-row
 static int apply_rows_per_block(int M, int C) {
+  static const int target = [] {
+    const char* e = getenv("ZOO_BN_BLOCKS");
+    return e ? atoi(e) : 1024;
+  }();
+  static const int min_rows = [] {
+    const char* e = getenv("ZOO_BN_MINROWS");
+    return e ? atoi(e) : 8;
+  }();
   const int cpr = C / 8;
   const int rstep = 256 / (cpr < 256 ? cpr : 256);
-  int rpb = (M + 1023) / 1024;
-  if (rpb < 8 * rstep) rpb = 8 * rstep;
+  int rpb = (M + target - 1) / target;
+  if (rpb < min_rows * rstep) rpb = min_rows * rstep;
   return rpb;
 }
 
@@ -304,12 +345,36 @@ extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X,
   return hipGetLastError();
 }
 
+// grid for the apply kernels: interleaved tiles (default) or contiguous ranges (ZOO_BN_INTERLEAVE=0)
+static void apply_grid(int M, int C, int tile_units, int* blocks, int* rpb) {
+  static const int inter = [] {
+    const char* e = getenv("ZOO_BN_INTERLEAVE");
+    return e ? atoi(e) : 1;
+  }();
+  // 512 blocks x 256 threads: 2 blocks per CU; tools/bn_bench.py sweep on the
+  // ResNet-50 shapes (more blocks only repeat the coefficient prologue)
+  static const int target = [] {
+    const char* e = getenv("ZOO_BN_BLOCKS");
+    return e ? atoi(e) : 512;
+  }();
+  if (inter) {
+    const int cpr = C / 8;
+    const int rstep = 256 / (cpr < 256 ? cpr : 256);
+    const int tiles = (M + tile_units * rstep - 1) / (tile_units * rstep);
+    *blocks = tiles < target ? (tiles > 0 ? tiles : 1) : target;
+    *rpb = 0;
+    return;
+  }
+  *rpb = apply_rows_per_block(M, C);
+  *blocks = M > 0 ? (M + *rpb - 1) / *rpb : 1;
+}
+
 extern "C" hipError_t zoo_bn_fwd_apply(const void* X, const float* stats, const float* gamma,
                                        const float* beta, const void* resid, void* Y, float* rmean,
                                        float* rvar, float* smean, float* sinv, int M, int C, float eps,
                                        float momentum, int relu, int training, hipStream_t st) {
-  const int rpb = apply_rows_per_block(M, C);
-  const int blocks = M > 0 ? (M + rpb - 1) / rpb : 1;
+  int rpb, blocks;
+  apply_grid(M, C, 4, &blocks, &rpb);
   hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X,
                      stats, gamma, beta, (const bf16_t*)resid, (bf16_t*)Y, rmean, rvar, smean, sinv, M, C, eps,
                      momentum, relu, training, rpb);
@@ -320,8 +385,8 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                                        const float* sinv, const float* gamma, const float* sums, void* dX,
                                        void* dResid, float* dgamma, float* dbeta, int M, int C,
                                        hipStream_t st) {
-  const int rpb = apply_rows_per_block(M, C);
-  const int blocks = M > 0 ? (M + rpb - 1) / rpb : 1;
+  int rpb, blocks;
+  apply_grid(M, C, 2, &blocks, &rpb);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dZ,
                      (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
                      dgamma, dbeta, M, C, rpb);

@@ -251,6 +251,10 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   check_hip(zoo_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), &g, cur_stream()), "wgrad");
 }
 
+static void check_al16(const void* p, const char* what) {
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(p) & 15) == 0, what, " must be 16-byte aligned");
+}
+
 void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<torch::Tensor> x,
                c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> invstd, torch::Tensor out, int mode) {
   req(a, at::kBFloat16, "a");
@@ -268,6 +272,10 @@ void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<to
       req(*z, at::kBFloat16, "z");
       TORCH_CHECK(z->numel() == a.numel(), "bn_reduce: z shape");
     }
+  }
+  if (mode == 1) {
+    check_al16(opt_ptr<float>(mean), "mean");
+    check_al16(opt_ptr<float>(invstd), "invstd");
   }
   check_hip(zoo_bn_reduce(a.data_ptr(), opt_ptr<void>(z), opt_ptr<void>(x), opt_ptr<float>(mean),
                           opt_ptr<float>(invstd), out.data_ptr<float>(), (int)M, C, mode, nslot, cur_stream()),
@@ -296,6 +304,12 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
     req(*resid, at::kBFloat16, "resid");
     TORCH_CHECK(resid->numel() == x.numel(), "bn: resid shape");
   }
+  // the apply kernels read per-channel vectors with 16-byte loads
+  check_al16(training ? stats.data_ptr<float>() : nullptr, "stats");
+  check_al16(opt_ptr<float>(gamma), "gamma");
+  check_al16(opt_ptr<float>(beta), "beta");
+  check_al16(opt_ptr<float>(rmean), "running_mean");
+  check_al16(opt_ptr<float>(rvar), "running_var");
   auto y = torch::empty_like(x);
   check_hip(zoo_bn_fwd_apply(x.data_ptr(), training ? stats.data_ptr<float>() : nullptr, opt_ptr<float>(gamma),
                              opt_ptr<float>(beta), opt_ptr<void>(resid), y.data_ptr(), opt_ptr<float>(rmean),
@@ -321,6 +335,10 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dz, c10::optional<torch::T
     req(*z, at::kBFloat16, "z");
     TORCH_CHECK(z->numel() == x.numel(), "bn_bwd: z shape");
   }
+  check_al16(sums.data_ptr<float>(), "sums");
+  check_al16(smean.data_ptr<float>(), "save_mean");
+  check_al16(sinv.data_ptr<float>(), "save_invstd");
+  check_al16(opt_ptr<float>(gamma), "gamma");
   auto dx = torch::empty_like(x);
   torch::Tensor dr;
   if (want_dresid) dr = torch::empty_like(x);

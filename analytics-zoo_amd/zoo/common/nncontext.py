@@ -30,7 +30,10 @@ log = logging.getLogger("zoo")
 class ZooConfig:
     # engine
     dtype: str = "bf16"
-    bucket_mb: float = 64.0
+    # gradient bucket size: the last bucket (the earliest layers) is launched only
+    # when backward ends and is exposed; 16 MB keeps that tail short while each
+    # message is still large enough for full xGMI ring bandwidth
+    bucket_mb: float = 16.0
     overlap_comm: bool = True
     sharded_optimizer: bool = False
     hip_graph: bool = False

@@ -47,7 +47,7 @@ FUSE_BN_BACKWARD = True
 
 
 def _bp():
-    return BNProducer(None, None, None, None) if FUSE_BN_BACKWARD else None
+    return BNProducer(False, None, None, None) if FUSE_BN_BACKWARD else None
 
 
 def _fusing(x):

@@ -62,17 +62,25 @@ class BNProducer:
     sum dy*xhat) and ReLU mask into its dgrad epilogue (igemm BwdStats) and
     marks ``fused``; this unit's backward then skips its reduction pass."""
 
-    __slots__ = ("z", "y", "mean", "inv", "sums", "fused")
+    # The producer's OUTPUT z is deliberately not held here: z -> grad_fn -> ctx ->
+    # producer -> z would be a reference cycle that keeps every step's
+    # activations alive until the cyclic GC runs. The consumer passes its own
+    # saved input (which is z) to bstats() instead.
+    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused")
 
-    def __init__(self, z, y, mean, inv):
-        self.z, self.y, self.mean, self.inv = z, y, mean, inv
+    def __init__(self, relu, y, mean, inv):
+        self.relu, self.y, self.mean, self.inv = relu, y, mean, inv
         self.sums = None
         self.fused = False
 
-    def bstats(self):
+    def bstats(self, z):
         self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
         self.fused = True
-        return (self.z, self.y, self.mean, self.inv, self.sums)
+        return (z if self.relu else None, self.y, self.mean, self.inv, self.sums)
+
+    def release(self):
+        self.y = self.mean = self.inv = self.sums = None
+        self.fused = False
 
 
 class _ConvBNActFn(torch.autograd.Function):
@@ -95,7 +103,7 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.meta = (R, S, stride, pad, relu, resid is not None, x.shape)
         ctx.producer_out = producer_out
         if producer_out is not None:
-            producer_out.z, producer_out.y, producer_out.mean, producer_out.inv = (z if relu else None), y, smean, sinv
+            producer_out.relu, producer_out.y, producer_out.mean, producer_out.inv = bool(relu), y, smean, sinv
         return z
 
     @staticmethod
@@ -117,7 +125,7 @@ class _ConvBNActFn(torch.autograd.Function):
             outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dgam, dbet)
             dy = outs[0]
             dresid = dz if has_resid else None
-            po.fused, po.sums = False, None
+            po.release()
         else:
             sums = workspace.zeros(stat_len(K), dz.device)
             C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
@@ -136,7 +144,7 @@ class _ConvBNActFn(torch.autograd.Function):
                 if add is None:
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
             pin = ctx.producer_in
-            bst = pin.bstats() if (pin is not None and pin.y is not None) else None
+            bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
             dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, resid=add,
                                   bstats=bst)
         gw, own_w = _grad_target(w)

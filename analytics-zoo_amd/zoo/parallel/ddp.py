@@ -5,9 +5,10 @@ This replaces BigDL's Spark-BlockManager ``AllReduceParameter`` (SURVEY.md
 
 * ``mode="allreduce"`` (default): gradients live in ONE flat fp32 buffer
   (:class:`FlatParams`) laid out in backward order. The buffer is cut into
-  contiguous buckets (``bucket_mb``, default 64 MB — few, large messages suit
-  xGMI's 7 point-to-point links and 288 GB HBM; ResNet-50's 102 MB of fp32
-  gradients is 2 buckets). A bucket is launched the moment the backward
+  contiguous buckets (``bucket_mb``, default 16 MB from ZooConfig: messages
+  big enough for full ring bandwidth over xGMI's point-to-point links, small
+  enough that the final bucket — launched only when backward ends — is a short
+  exposed tail; ResNet-50's 102 MB of fp32 gradients is ~7 buckets). A bucket is launched the moment the backward
   kernels of all its parameters have been *enqueued*: the comm stream waits on
   an event recorded on the compute stream, so the all-reduce of late layers
   overlaps the backward of early layers.
@@ -40,7 +41,7 @@ class _Bucket:
 
 
 class GradSync:
-    def __init__(self, flat: FlatParams, group=None, bucket_mb=64.0, mode="allreduce", overlap=True):
+    def __init__(self, flat: FlatParams, group=None, bucket_mb=16.0, mode="allreduce", overlap=True):
         self.flat = flat
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
