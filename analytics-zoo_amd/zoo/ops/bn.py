@@ -21,6 +21,7 @@ import torch.nn.functional as F
 from zoo.ops._native import native
 from zoo.ops import _kern, workspace
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
+from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
 
 # Per-channel statistics buffers are "slotted" ([2C final][STAT_SLOTS x 2C][counter]):
 # producers spread their atomics over the slots and the last block folds them
@@ -83,6 +84,19 @@ class BNProducer:
         self.fused = False
 
 
+def _sync_bwd(ctx, sums, K, m_local, dgam, dbet):
+    """SyncBN backward: dgamma/dbeta take the LOCAL sums (the DP gradient sync
+    combines ranks), then (sum dy, sum dy*xhat) are all-reduced for dx."""
+    if not getattr(ctx, "sync", False):
+        return dgam, dbet
+    if dgam is not None:
+        dgam.add_(sums[K:2 * K])
+    if dbet is not None:
+        dbet.add_(sums[:K])
+    all_reduce_stats(sums[:2 * K], m_local)
+    return None, None
+
+
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
@@ -94,6 +108,9 @@ class _ConvBNActFn(torch.autograd.Function):
         wb = bf16_weight(w)
         stats = workspace.zeros(stat_len(K), x.device) if training else None
         y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
+        ctx.sync = bool(training) and sync_bn_active()
+        if ctx.sync:  # SyncBN (P5): global statistics over the data-parallel group
+            all_reduce_stats(stats[:2 * K], y.numel() // K)
         smean = torch.empty(K, device=x.device, dtype=torch.float32)
         sinv = torch.empty(K, device=x.device, dtype=torch.float32)
         z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
@@ -122,14 +139,16 @@ class _ConvBNActFn(torch.autograd.Function):
         if po is not None and po.fused:
             # dz arrived already ReLU-masked with its (dy, dy*xhat) sums from the consumer's epilogue
             sums = po.sums
-            outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dgam, dbet)
+            dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
+            outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dg, db)
             dy = outs[0]
             dresid = dz if has_resid else None
             po.release()
         else:
             sums = workspace.zeros(stat_len(K), dz.device)
             C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
-            outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, has_resid, dgam, dbet)
+            dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
+            outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, has_resid, dg, db)
             dy = outs[0]
             dresid = outs[1] if has_resid else None
         if dresid is not None and ctx.handoff_out is not None:
@@ -213,7 +232,10 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
                                    tuple(stride), tuple(pad), float(eps), float(momentum), bool(relu),
                                    bool(training), resid_handoff, grad_add, producer_in, producer_out)
     y = conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1)))
-    z = bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training)
+    if training and sync_bn_active():
+        z = sync_batch_norm(y.float(), gamma, beta, running_mean, running_var, eps, momentum)
+    else:
+        z = bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training)
     if resid is not None:
         z = z + resid.float()
     if relu:
@@ -229,8 +251,11 @@ class _BNActFn(torch.autograd.Function):
         C_ = native()
         K = y.shape[-1]
         stats = workspace.zeros(stat_len(K), y.device)
+        ctx.sync = bool(training) and sync_bn_active()
         if training:
             C_.bn_reduce(y, None, None, None, None, stats, 0)
+            if ctx.sync:
+                all_reduce_stats(stats[:2 * K], y.numel() // K)
         smean = torch.empty(K, device=y.device, dtype=torch.float32)
         sinv = torch.empty(K, device=y.device, dtype=torch.float32)
         z = C_.bn_fwd_apply(y, stats, gamma.detach(), beta.detach(), resid, running_mean, running_var, smean,
@@ -249,7 +274,8 @@ class _BNActFn(torch.autograd.Function):
         C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
         dgam, own_g = _grad_target(gamma)
         dbet, own_b = _grad_target(beta)
-        outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, ctx.has_resid, dgam, dbet)
+        dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
+        outs = C_.bn_bwd_apply(dz, z, y, smean, sinv, gamma.detach(), sums, ctx.has_resid, dg, db)
         if own_g:
             _notify(gamma)
         if own_b:
@@ -267,7 +293,10 @@ def batch_norm_nhwc(y, gamma, beta, running_mean, running_var, eps=1e-5, momentu
         out = _BNActFn.apply(yb, gamma, beta, r, running_mean, running_var, float(eps), float(momentum), bool(relu),
                              bool(training))
         return out if y.dtype == torch.bfloat16 else out.to(y.dtype)
-    z = bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training)
+    if training and sync_bn_active():
+        z = sync_batch_norm(y.float(), gamma, beta, running_mean, running_var, eps, momentum)
+    else:
+        z = bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training)
     if resid is not None:
         z = z + resid.float()
     if relu:

@@ -11,7 +11,9 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.parallel.sync_bn import sync_batch_norm, sync_bn_active
 from zoo.pipeline.api.keras.base import Layer, init_tensor
+
 
 
 class BatchNormalization(Layer):
@@ -34,6 +36,10 @@ class BatchNormalization(Layer):
 
     def call(self, x):
         channels_last = x.dim() == 2 or (x.dim() == 4 and self.dim_ordering == "tf") or x.dim() == 3
+        if self.training and sync_bn_active():  # SyncBN across data-parallel ranks (P5)
+            cdim = -1 if channels_last else 1
+            return sync_batch_norm(x, self.gamma, self.beta, self.running_mean, self.running_var, self.epsilon,
+                                   self.momentum, channel_dim=cdim)
         if channels_last and x.is_cuda and self.nc % 8 == 0:
             y = ops.batch_norm_nhwc(x, self.gamma, self.beta, self.running_mean, self.running_var, self.epsilon,
                                     self.momentum, relu=False, training=self.training)
