@@ -22,6 +22,22 @@ def _free_port():
     return p
 
 
+def _collect(q, procs, n, timeout):
+    """Results from n workers; fail fast (instead of waiting out the timeout) if one dies."""
+    import queue
+    import time
+    out, t0 = {}, time.time()
+    while len(out) < n:
+        try:
+            r, v = q.get(timeout=1.0)
+            out[r] = v
+        except queue.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, "worker died with exit code %s" % dead
+            assert time.time() - t0 < timeout, "workers timed out"
+    return out
+
+
 def _data():
     g = torch.Generator().manual_seed(7)
     return (torch.randn(8, 6, 5, 5, generator=g) * 2 + 1, torch.randn(8, 6, 5, 5, generator=g),
@@ -83,7 +99,7 @@ def test_sync_bn_two_ranks_match_full_batch():
     procs = [ctx_mp.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=240) for _ in range(2))
+    res = _collect(q, procs, 2, 240)
     for p in procs:
         p.join(timeout=60)
     x, dy, xc, dyc = _data()
@@ -108,8 +124,8 @@ def _gpu_unit(xc, dyc):
     xr = xc.to(dev, torch.bfloat16).requires_grad_(True)
     z = ops.conv_bn_act(xr, w, gam, bet, rm, rv, kernel=(3, 3), pad=(1, 1), relu=True, training=True)
     z.backward(dyc.to(dev, torch.bfloat16))
-    return {"z": z.float().cpu(), "dx": xr.grad.float().cpu(), "dgam": gam.grad.cpu(), "dbet": bet.grad.cpu(),
-            "rm": rm.cpu(), "rv": rv.cpu()}
+    return {"z": z.detach().float().cpu(), "dx": xr.grad.float().cpu(), "dgam": gam.grad.cpu(),
+            "dbet": bet.grad.cpu(), "rm": rm.cpu(), "rv": rv.cpu()}
 
 
 def _gpu_data():
@@ -144,7 +160,7 @@ def test_sync_bn_native_gpu_path_two_ranks(gpu):
     procs = [ctx_mp.Process(target=_gpu_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    res = dict(q.get(timeout=100) for _ in range(2))
+    res = _collect(q, procs, 2, 100)
     for p in procs:
         p.join(timeout=60)
     xc, dyc = _gpu_data()
