@@ -332,7 +332,11 @@ extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X,
   // ~1024 blocks, each owning a contiguous row range
   int blocks = 1024;
   int rpb = (M + blocks - 1) / blocks;
-  if (rpb < 8) rpb = 8;
+  // at least 16 rows per thread-row: small tensors (bias gradients) then use few
+  // blocks instead of 1024 nearly idle ones each paying 2C slot atomics
+  const int cpr = C >> 3;
+  const int row_step = 256 / (cpr < 256 ? cpr : 256);
+  if (rpb < 16 * row_step) rpb = 16 * row_step;
   blocks = (M + rpb - 1) / rpb;
   const size_t smem = (size_t)2 * C * sizeof(float);
   if (mode == 0)

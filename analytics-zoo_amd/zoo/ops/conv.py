@@ -131,7 +131,12 @@ class _Conv2dFn(torch.autograd.Function):
                 if hook is not None:
                     hook(w)
         if has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().reshape(-1, K).sum(0)
+            if K % 8 == 0:  # native channel reduction (16-byte loads, ~1024 blocks) instead of torch's sum
+                st = torch.zeros(C_.stat_len(K), dtype=torch.float32, device=dyb.device)  # slotted atomics
+                C_.bn_reduce(dyb, None, None, None, None, st, 0)
+                db = st[:K]
+            else:
+                db = dy.float().reshape(-1, K).sum(0)
         return dx, dw, db, None, None, None, None, None, None, None
 
 
@@ -153,6 +158,14 @@ def linear(x, w, bias=None, act=None):
     the input is on the GPU; otherwise the plain library GEMM (hipBLASLt)."""
     K, Cin = w.shape
     lead = x.shape[:-1]
+    if x.is_cuda and (Cin % 8 or K % 8) and x.shape[-1] == Cin:
+        # zero-pad features to the MFMA kernels' 8-element granule (keeps small
+        # layers such as NCF's 30->10->5 off hipBLASLt's tall-skinny fp32 wgrad)
+        pc, pk = (-Cin) % 8, (-K) % 8
+        xp = F.pad(x, (0, pc))
+        wp = F.pad(w, (0, pc, 0, pk))
+        bp = None if bias is None else F.pad(bias, (0, pk))
+        return linear(xp, wp, bp, act)[..., :K]
     if x.is_cuda and Cin % 8 == 0 and K % 8 == 0 and w.shape[1] == Cin:
         x2 = x.reshape(-1, 1, 1, Cin)
         out_f32 = x.dtype == torch.float32

@@ -52,7 +52,7 @@ def _move(batch, device, non_blocking=True):
 
 class TrainingEngine:
     def __init__(self, model, criterion, optim_method, device=None, ctx=None, clip=None, sharded=None,
-                 bucket_mb=None, model_forward=None):
+                 bucket_mb=None, model_forward=None, hip_graph=None):
         from zoo.common.nncontext import get_nncontext
         self.ctx = ctx or get_nncontext()
         cfg = self.ctx.config
@@ -77,6 +77,12 @@ class TrainingEngine:
         self.checkpoint_overwrite = True
         self.fault_step = cfg.fault_inject_step
         self._fault_fired = False
+        # hipGraph capture of forward+backward (launch-bound models, e.g. NCF):
+        # the graph replays every kernel of the step with one launch; the
+        # gradient all-reduce and the optimizer stay eager after the replay
+        self.hip_graph = (cfg.hip_graph if hip_graph is None else bool(hip_graph)) and self.device.type == "cuda"
+        self._graphs = {}
+        self._graph_warm = {}
 
     # ------------------------------------------------------------------
     def train_step(self, inputs, target):
@@ -85,6 +91,15 @@ class TrainingEngine:
             self._fault_fired = True
             raise InjectedFault("injected fault at iteration %d" % self.fault_step)
         self.model.train()
+        if self.hip_graph and torch.is_tensor(target):
+            loss = self._graph_fwd_bwd(inputs, target)
+        else:
+            loss = self._fwd_bwd(inputs, target)
+        self.sync.step(self.optim, self.clip)
+        self.state["neval"] += 1
+        return loss
+
+    def _fwd_bwd(self, inputs, target):
         self.flat.grad.zero_()
         workspace.begin_step(self.device)
         try:
@@ -93,9 +108,53 @@ class TrainingEngine:
             loss.backward()
         finally:
             workspace.end_step()
-        self.sync.step(self.optim, self.clip)
-        self.state["neval"] += 1
         return loss.detach()
+
+    def _graph_fwd_bwd(self, inputs, target):
+        """Replay a captured forward+backward for this input signature. Two eager
+        warm-up steps per signature settle lazy allocations (workspace high-water
+        mark, kernel attributes) before the capture."""
+        xs = list(inputs) if isinstance(inputs, (list, tuple)) else [inputs]
+        if not all(torch.is_tensor(t) for t in xs):
+            return self._fwd_bwd(inputs, target)
+        key = tuple((tuple(t.shape), t.dtype) for t in xs + [target])
+        g = self._graphs.get(key)
+        if g is None:
+            n = self._graph_warm.get(key, 0)
+            if n < 2:
+                self._graph_warm[key] = n + 1
+                return self._fwd_bwd(inputs, target)
+            try:
+                g = self._capture(key, xs, target, isinstance(inputs, (list, tuple)))
+            except RuntimeError as e:  # a host sync inside the step: stay eager for this model
+                log.warning("hipGraph capture failed (%s); training eagerly", e)
+                self.hip_graph = False
+                torch.cuda.synchronize(self.device)
+                return self._fwd_bwd(inputs, target)
+        graph, sx, sy, sloss = g
+        for s_, t in zip(sx, xs):
+            s_.copy_(t, non_blocking=True)
+        sy.copy_(target, non_blocking=True)
+        graph.replay()
+        return sloss.clone()
+
+    def _capture(self, key, xs, target, as_list):
+        sx = [t.detach().clone() for t in xs]
+        sy = target.detach().clone()
+        overlap = self.sync.overlap
+        self.sync.overlap = False  # no collectives inside the capture: finish() launches them after replay
+        torch.cuda.synchronize(self.device)
+        graph = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(graph):
+                sloss = self._fwd_bwd(sx if as_list else sx[0], sy)
+        finally:
+            self.sync.overlap = overlap
+        self.sync.reset()
+        g = (graph, sx, sy, sloss)
+        self._graphs[key] = g
+        log.info("captured forward+backward as a hipGraph for inputs %s", key)
+        return g
 
     # ------------------------------------------------------------------
     def fit(self, data, end_trigger=None, validation=None, val_methods=None, val_trigger=None,

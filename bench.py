@@ -72,7 +72,8 @@ def build_ncf(ctx, batch):
     users, items = 138493, 26744  # ml-20m shape
     model = NeuralCF(users, items, 5, user_embed=20, item_embed=20, hidden_layers=(40, 20, 10), include_mf=True,
                      mf_embed=20)
-    eng = TrainingEngine(model, SparseCategoricalCrossEntropy(), Adam(lr=1e-3))
+    # NCF's step is ~130 small kernels: capture forward+backward as one hipGraph
+    eng = TrainingEngine(model, SparseCategoricalCrossEntropy(), Adam(lr=1e-3), hip_graph=True)
     dev = ctx.device
     g = torch.Generator(device=dev)
     g.manual_seed(ctx.rank)

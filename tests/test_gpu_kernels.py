@@ -100,6 +100,27 @@ def test_linear_mfma(gpu):
     assert rel(y, torch.relu(x @ w.t() + b)) < 2e-2
 
 
+@pytest.mark.parametrize("rows,cin,k,act", [(4096, 30, 5, None), (4096, 20, 10, "relu"), (513, 40, 20, "relu"),
+                                             (300, 96, 40, "sigmoid")])
+def test_linear_native_fwd_bwd_any_dims(gpu, rows, cin, k, act):
+    """Unaligned feature dims are zero-padded onto the MFMA kernels (NCF's 30->10->5
+    layers); forward and all three gradients vs fp32 autograd on bf16-rounded inputs."""
+    from zoo.ops import linear
+    torch.manual_seed(0)
+    x = _bf(torch.randn(rows, cin, device=gpu)).requires_grad_(True)
+    w = _bf(torch.randn(k, cin, device=gpu) * 0.2).requires_grad_(True)
+    b = torch.randn(k, device=gpu).requires_grad_(True)
+    y = linear(x, w, b, act=act)
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr.t() + br
+    yr = {"relu": torch.relu, "sigmoid": torch.sigmoid, None: lambda v: v}[act](yr)
+    yr.backward(dy)
+    assert rel(y, yr) < 2e-2
+    assert rel(x.grad, xr.grad) < 3e-2 and rel(w.grad, wr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
+
+
 def _bf(t):
     return t.bfloat16().float()
 
@@ -514,3 +535,32 @@ def test_gemm256_numerics_and_epilogue(gpu, mnk):
     assert rel(yb, ref2) < 1e-2
     q = yb.float()
     assert rel(stats, torch.cat([q.sum(0), (q * q).sum(0)])) < 1e-3
+
+
+def test_engine_hipgraph_matches_eager(gpu):
+    """Captured forward+backward (TrainingEngine(hip_graph=True)) trains like the
+    eager engine: same losses and parameters after several steps (NCF model)."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.recommendation.neuralcf import NeuralCF
+    from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext()
+    g = torch.Generator(device=gpu)
+    g.manual_seed(3)
+    x = torch.stack([torch.randint(1, 501, (1024,), device=gpu, generator=g),
+                     torch.randint(1, 301, (1024,), device=gpu, generator=g)], 1)
+    y = torch.randint(0, 5, (1024,), device=gpu, generator=g)
+    res = []
+    for graph in (False, True):
+        torch.manual_seed(0)
+        m = NeuralCF(500, 300, 5, user_embed=16, item_embed=16, hidden_layers=(40, 20, 10), include_mf=True,
+                     mf_embed=16)
+        eng = TrainingEngine(m, SparseCategoricalCrossEntropy(), Adam(lr=1e-2), hip_graph=graph)
+        losses = [float(eng.train_step(x, y)) for _ in range(6)]
+        res.append((losses, eng.flat.master.clone()))
+        if graph:
+            assert eng._graphs, "no graph was captured"
+    (l0, p0), (l1, p1) = res
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3, (l0, l1)
+    assert rel(p1, p0) < 1e-3
