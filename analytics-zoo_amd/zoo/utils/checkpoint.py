@@ -2,8 +2,8 @@
 
 Objects (state dicts of tensors, numbers, strings, lists, dicts) are written
 with ``torch.save`` and read back with ``torch.load(weights_only=True)`` so
-loading a checkpoint never executes code from the file. Paths may be local or
-``file://`` URIs; writes are atomic (temp file + rename) so a crash never
+loading a checkpoint never executes code from the file. Paths may be local,
+``file://`` or (through zoo.utils.file) ``hdfs://`` URIs; writes are atomic (temp file + rename) so a crash never
 leaves a torn ``model.<n>`` that the failure-retry path would pick up.
 """
 import os
@@ -15,12 +15,13 @@ import torch
 def _local(path):
     if path.startswith("file://"):
         return path[len("file://"):]
-    if "://" in path:
-        raise NotImplementedError("remote filesystem %s: mount it locally" % path.split("://")[0])
     return path
 
 
 def save_object(obj, path, overwrite=True):
+    if "://" in path and not path.startswith("file://"):  # hdfs:// etc.: write locally, then upload
+        from zoo.common.utils import save_file
+        return save_file(lambda p: save_object(obj, p, True), path)
     path = _local(path)
     if os.path.exists(path) and not overwrite:
         raise FileExistsError(path)
@@ -37,4 +38,7 @@ def save_object(obj, path, overwrite=True):
 
 
 def load_object(path):
+    if "://" in path and not path.startswith("file://"):
+        from zoo.common.utils import load_from_file
+        return load_from_file(load_object, path)
     return torch.load(_local(path), map_location="cpu", weights_only=True)

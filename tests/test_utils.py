@@ -1,0 +1,74 @@
+"""Utility surfaces of the reference: Py/util/nest.py, Py/common/utils.py
+(paths, remote files, JTensor, Sample), Zs/utils/File.scala (FS helpers)."""
+import collections
+import os
+
+import numpy as np
+import pytest
+
+from zoo.util import nest
+from zoo.utils import file as zfile
+from zoo.common import utils as cu
+
+
+def test_nest_flatten_and_pack_roundtrip():
+    Pt = collections.namedtuple("Pt", "x y")
+    s = {"b": [1, (2, 3)], "a": Pt(4, {"z": 5, "y": 6})}
+    flat = nest.flatten(s)
+    assert flat == [4, 6, 5, 1, 2, 3]   # dicts flatten in sorted-key order
+    back = nest.pack_sequence_as(s, [v * 10 for v in flat])
+    assert back == {"b": [10, (20, 30)], "a": Pt(40, {"z": 50, "y": 60})}
+    assert nest.flatten(7) == [7] and nest.pack_sequence_as(0, [9]) == 9
+    with pytest.raises(ValueError):
+        nest.pack_sequence_as([1, 2], [1])
+
+
+def test_file_helpers_local_and_file_uri(tmp_path):
+    p = str(tmp_path / "d" / "x.bin")
+    zfile.save_bytes(b"abc", p)
+    assert zfile.exists(p) and zfile.read_bytes("file://" + p) == b"abc"
+    with pytest.raises(FileExistsError):
+        zfile.save_bytes(b"zz", p)
+    zfile.save_bytes(b"zz", "file://" + p, overwrite=True)
+    assert zfile.read_bytes(p) == b"zz"
+    assert zfile.list_files(str(tmp_path / "d")) == [p]
+    q = str(tmp_path / "copy.bin")
+    zfile.get_remote_file_to_local("file://" + p, q)
+    assert open(q, "rb").read() == b"zz"
+    zfile.delete(str(tmp_path / "d"))
+    assert not os.path.exists(p)
+    assert zfile.is_local_path("/a/b") and zfile.is_local_path("file:///a") and not zfile.is_local_path("hdfs://n/a")
+
+
+def test_remote_scheme_without_client_is_explicit(monkeypatch):
+    monkeypatch.setenv("PATH", "")
+    with pytest.raises(NotImplementedError):
+        zfile.exists("hdfs://namenode:9000/x")
+    with pytest.raises(NotImplementedError):
+        zfile.exists("s3://bucket/x")
+
+
+def test_common_utils_save_load_and_carriers(tmp_path):
+    p = str(tmp_path / "m.npy")
+    cu.save_file(lambda f: np.save(f, np.arange(3)), p)
+    assert cu.load_from_file(np.load, p).tolist() == [0, 1, 2]
+    assert cu.append_suffix("abc", "hdfs://x/y/model.npy") == "abc.npy"
+    assert [a.tolist() for a in cu.to_list_of_numpy([1, np.ones(2)])] == [1, [1.0, 1.0]]
+    with pytest.raises(ValueError):
+        cu.to_list_of_numpy("nope")
+    a = np.arange(6, dtype=np.float32).reshape(2, 3)
+    assert np.array_equal(cu.JTensor.from_ndarray(a).to_ndarray(), a)
+    sp = cu.JTensor.sparse(np.array([1.0, 2.0]), np.array([0, 1, 2, 0]), (2, 3))
+    assert sp.to_ndarray().tolist() == [[0, 0, 1.0], [2.0, 0, 0]]
+    s = cu.Sample.from_ndarray(a, np.array(1))
+    assert s.feature.shape == (2, 3) and int(s.label) == 1
+    with pytest.raises(NotImplementedError):
+        cu.callZooFunc("float", "anything")
+
+
+def test_checkpoint_file_uri(tmp_path):
+    from zoo.utils.checkpoint import load_object, save_object
+    import torch
+    uri = "file://" + str(tmp_path / "ck" / "model.1")
+    save_object({"w": torch.ones(2)}, uri)
+    assert load_object(uri)["w"].tolist() == [1.0, 1.0]
