@@ -55,7 +55,7 @@ def test_common_utils_save_load_and_carriers(tmp_path):
     assert cu.append_suffix("abc", "hdfs://x/y/model.npy") == "abc.npy"
     assert [a.tolist() for a in cu.to_list_of_numpy([1, np.ones(2)])] == [1, [1.0, 1.0]]
     with pytest.raises(ValueError):
-        cu.to_list_of_numpy("nope")
+        cu.to_list_of_numpy({"a": 1})
     a = np.arange(6, dtype=np.float32).reshape(2, 3)
     assert np.array_equal(cu.JTensor.from_ndarray(a).to_ndarray(), a)
     sp = cu.JTensor.sparse(np.array([1.0, 2.0]), np.array([0, 1, 2, 0]), (2, 3))
