@@ -15,6 +15,8 @@
 //
 // Reference parity: the weight-gradient half of BigDL SpatialConvolution /
 // Linear accGradParameters.
+#include <stdlib.h>
+
 #include "common.h"
 #include "geom.h"
 
@@ -206,9 +208,17 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const 
                                 hipStream_t st) {
   WgradGeom g = *gin;
   const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
-  // split the pixel reduction so that ~1024 workgroups are in flight, >= 512 pixels each
-  int splits = (1024 + tiles - 1) / tiles;
-  const int max_splits = (g.M + 511) / 512;
+  // split the pixel reduction so that ~kTarget workgroups are in flight, >= kMinPix pixels each
+  static const int target = [] {
+    const char* e = getenv("ZOO_WGRAD_WG");
+    return e ? atoi(e) : 1024;
+  }();
+  static const int min_pix = [] {
+    const char* e = getenv("ZOO_WGRAD_MINPIX");
+    return e ? atoi(e) : 512;
+  }();
+  int splits = (target + tiles - 1) / tiles;
+  const int max_splits = (g.M + min_pix - 1) / min_pix;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int mps = (g.M + splits - 1) / splits;

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Whole-network conv time of ResNet-50 (batch N, bf16 NHWC) per op, weighted by
+how often each conv shape occurs: one number per op for A/B-ing kernel knobs
+(env vars such as ZOO_IGEMM_BN) on the GPU.
+
+  python analytics-zoo_amd/tools/conv_sweep.py [--batch 256] [--ops fwd,dgrad,wgrad] [--detail]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import zoo._C as C  # noqa: E402
+from zoo.ops import _kern  # noqa: E402
+from tools.kernel_check import RESNET50_CONVS  # noqa: E402
+
+# occurrences of each RESNET50_CONVS shape in ResNet-50 v1.5 (53 convs)
+COUNTS = [1, 1, 3, 4, 2, 1, 1, 4, 1, 3, 3, 1, 1, 6, 1, 5, 5, 1, 1, 3, 1, 2, 2]
+
+
+def timeit(fn, iters=10):
+    for _ in range(2):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=256)
+    ap.add_argument("--ops", default="fwd,dgrad,wgrad")
+    ap.add_argument("--detail", action="store_true")
+    a = ap.parse_args()
+    ops = a.ops.split(",")
+    dev = torch.device("cuda")
+    tot = {o: 0.0 for o in ops}
+    assert len(COUNTS) == len(RESNET50_CONVS)
+    for (H, Cin, Cout, R, st, pad), cnt in zip(RESNET50_CONVS, COUNTS):
+        N = a.batch
+        x = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+        ktot = R * R * Cin
+        w2 = torch.zeros(Cout, (ktot + 7) // 8 * 8, device=dev, dtype=torch.bfloat16)
+        w2[:, :ktot] = (torch.randn(Cout, ktot, device=dev) / ktot ** 0.5).bfloat16()
+        P = (H + 2 * pad - R) // st + 1
+        dy = torch.randn(N, P, P, Cout, device=dev).bfloat16()
+        stats = torch.zeros(C.stat_len(Cout), device=dev)
+        row = {"shape": [H, Cin, Cout, R, st, pad], "n": cnt}
+        if "fwd" in ops:
+            row["fwd"] = timeit(lambda: _kern.conv_fwd(x, w2, R, R, (st, st), (pad, pad), stats=stats))
+        if "dgrad" in ops and Cin != 4:
+            row["dgrad"] = timeit(lambda: _kern.conv_dgrad(dy, w2, Cout, R, R, Cin, H, H, (st, st), (pad, pad)))
+        if "wgrad" in ops:
+            dw = torch.zeros(Cout, ktot, device=dev)
+            row["wgrad"] = timeit(lambda: C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, 1, 1))
+        for o in ops:
+            tot[o] += row.get(o, 0.0) * cnt
+        if a.detail:
+            print(json.dumps({k: (round(v, 4) if isinstance(v, float) else v) for k, v in row.items()}), flush=True)
+        del x, dy, w2
+    print(json.dumps({"batch": a.batch, "ms_per_step": {o: round(v, 3) for o, v in tot.items()},
+                      "knobs": {k: v for k, v in os.environ.items() if k.startswith("ZOO_")}}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
