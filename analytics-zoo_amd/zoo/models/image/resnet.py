@@ -34,12 +34,13 @@ class ConvBN(nn.Module):
         self.register_buffer("running_mean", torch.zeros(cout))
         self.register_buffer("running_var", torch.ones(cout))
 
-    def forward(self, x, resid=None, resid_handoff=None, grad_add=None, producer_in=None, producer_out=None):
+    def forward(self, x, resid=None, resid_handoff=None, grad_add=None, producer_in=None, producer_out=None,
+                dx_handoff=None):
         return ops.conv_bn_act(x, self.weight, self.gamma, self.beta, self.running_mean, self.running_var,
                                kernel=(self.k, self.k), stride=(self.stride, self.stride),
                                pad=(self.pad, self.pad), eps=self.eps, momentum=self.momentum, relu=self.relu,
                                resid=resid, training=self.training, resid_handoff=resid_handoff, grad_add=grad_add,
-                               producer_in=producer_in, producer_out=producer_out)
+                               producer_in=producer_in, producer_out=producer_out, dx_handoff=dx_handoff)
 
 
 # cross-unit BN-backward fusion (BNProducer); the switch exists for A/B numerics tests
@@ -80,8 +81,11 @@ class Bottleneck(nn.Module):
             h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
             h = self.conv2(h, producer_in=p1, producer_out=p2)
             return self.conv3(h, resid=x, resid_handoff=ho, producer_in=p2, producer_out=p3), p3
-        sc = self.down(x)
-        h = self.conv1(x, producer_out=p1)  # x also feeds `down`: no producer fusion across this edge
+        # x feeds both `down` and conv1: conv1 (created later, so its backward runs first) hands its dx
+        # to down's dgrad epilogue, which adds it -- no separate gradient-add pass over x
+        dh = GradHandoff()
+        sc = self.down(x, grad_add=dh)
+        h = self.conv1(x, producer_out=p1, dx_handoff=dh)
         h = self.conv2(h, producer_in=p1, producer_out=p2)
         return self.conv3(h, resid=sc, producer_in=p2, producer_out=p3), p3
 
@@ -104,8 +108,9 @@ class BasicBlock(nn.Module):
             ho = GradHandoff()
             h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
             return self.conv2(h, resid=x, resid_handoff=ho, producer_in=p1, producer_out=p2), p2
-        sc = self.down(x)
-        h = self.conv1(x, producer_out=p1)
+        dh = GradHandoff()
+        sc = self.down(x, grad_add=dh)
+        h = self.conv1(x, producer_out=p1, dx_handoff=dh)
         return self.conv2(h, resid=sc, producer_in=p1, producer_out=p2), p2
 
 

@@ -100,10 +100,11 @@ def _sync_bwd(ctx, sums, K, m_local, dgam, dbet):
 class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
-                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None):
+                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None,
+                dx_out=None):
         C_ = native()
         K = w.shape[0]
-        ctx.handoff_out, ctx.handoff_in = handoff_out, handoff_in
+        ctx.handoff_out, ctx.handoff_in, ctx.dx_out = handoff_out, handoff_in, dx_out
         ctx.producer_in = producer_in
         wb = bf16_weight(w)
         stats = workspace.zeros(stat_len(K), x.device) if training else None
@@ -166,6 +167,10 @@ class _ConvBNActFn(torch.autograd.Function):
             bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
             dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, resid=add,
                                   bstats=bst)
+            if ctx.dx_out is not None:
+                # another consumer of x adds this gradient in its own dgrad epilogue
+                ctx.dx_out.grad = dx
+                dx = None
         gw, own_w = _grad_target(w)
         C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
         if own_w:
@@ -175,7 +180,7 @@ class _ConvBNActFn(torch.autograd.Function):
         if own_b:
             _notify(ctx.beta_ref)
         return (dx, None if own_w else gw.to(w.dtype), None if own_g else dgam, None if own_b else dbet, dresid,
-                None, None, None, None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None, None, None, None)
 
 
 class _ConvBNActFnB(_ConvBNActFn):
@@ -183,11 +188,12 @@ class _ConvBNActFnB(_ConvBNActFn):
 
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
-                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None):
+                relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None,
+                dx_out=None):
         ctx.beta_ref = beta
         return _ConvBNActFn.forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad,
                                     eps, momentum, relu, training, handoff_out, handoff_in, producer_in,
-                                    producer_out)
+                                    producer_out, dx_out)
 
 
 def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
@@ -212,7 +218,7 @@ def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
 
 def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0),
                 eps=1e-5, momentum=0.1, relu=True, resid=None, training=True, resid_handoff=None, grad_add=None,
-                producer_in=None, producer_out=None):
+                producer_in=None, producer_out=None, dx_handoff=None):
     """z = relu?(BN(conv(x)) + resid) for NHWC input with a packed weight.
 
     ``resid_handoff``/``grad_add``: a shared :class:`GradHandoff` that routes the
@@ -221,7 +227,10 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
     ``producer_in``: the :class:`BNProducer` of the unit that produced ``x``,
     when this unit is its ONLY consumer (fuses that unit's BN-backward
     reduction into this unit's dgrad). ``producer_out``: a fresh BNProducer
-    to be filled for this unit's own output."""
+    to be filled for this unit's own output. ``dx_handoff``: this unit's input
+    gradient is handed to the unit whose ``grad_add`` is the same GradHandoff
+    (which must run its backward later) instead of being returned — two
+    consumers of one tensor then need no separate gradient-add pass."""
     R, S = kernel
     if x.is_cuda:
         if x.dtype != torch.bfloat16:
@@ -230,7 +239,7 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
             resid = resid.to(torch.bfloat16).contiguous()
         return _ConvBNActFnB.apply(x.contiguous(), w, gamma, beta, resid, running_mean, running_var, R, S,
                                    tuple(stride), tuple(pad), float(eps), float(momentum), bool(relu),
-                                   bool(training), resid_handoff, grad_add, producer_in, producer_out)
+                                   bool(training), resid_handoff, grad_add, producer_in, producer_out, dx_handoff)
     y = conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1)))
     if training and sync_bn_active():
         z = sync_batch_norm(y.float(), gamma, beta, running_mean, running_var, eps, momentum)
