@@ -31,8 +31,10 @@ def _normal(shape, std):
 
 
 class _Block(nn.Module):
-    def __init__(self, hidden, n_head, inter, hidden_drop, attn_drop, init_range, post_ln=True, gelu="erf"):
+    def __init__(self, hidden, n_head, inter, hidden_drop, attn_drop, init_range, post_ln=True, gelu="erf",
+                 ln_eps=1e-5):
         super().__init__()
+        self.ln_eps = float(ln_eps)
         self.h, self.n_head = hidden, n_head
         self.qkv_w = nn.Parameter(_normal((3 * hidden, hidden), init_range))
         self.qkv_b = nn.Parameter(torch.zeros(3 * hidden))
@@ -55,13 +57,13 @@ class _Block(nn.Module):
                           training=self.training)
         a = a.transpose(1, 2).reshape(B, L, H)
         a = F.dropout(ops.linear(a, self.proj_w, self.proj_b), self.hidden_drop, self.training)
-        n = ops.layer_norm(x + a, self.ln1_g, self.ln1_b, 1e-5)
+        n = ops.layer_norm(x + a, self.ln1_g, self.ln1_b, self.ln_eps)
         act = "gelu" if self.gelu == "erf" else None
         m = ops.linear(n, self.fc1_w, self.fc1_b, act=act)
         if self.gelu != "erf":  # GPT tanh approximation
             m = 0.5 * m * (1 + torch.tanh(math.sqrt(2 / math.pi) * (m + 0.044715 * m * m * m)))
         m = F.dropout(ops.linear(m, self.fc2_w, self.fc2_b), self.hidden_drop, self.training)
-        return ops.layer_norm(n + m, self.ln2_g, self.ln2_b, 1e-5)
+        return ops.layer_norm(n + m, self.ln2_g, self.ln2_b, self.ln_eps)
 
 
 class TransformerLayer(Layer):
@@ -119,18 +121,21 @@ class TransformerLayer(Layer):
 class BERT(Layer):
     def __init__(self, vocab=40990, hidden_size=768, n_block=12, n_head=12, max_position_len=512,
                  intermediate_size=3072, hidden_drop=0.1, attn_drop=0.1, initializer_range=0.02,
-                 output_all_block=True, input_shape=None, seq_len=None, **kwargs):
+                 output_all_block=True, input_shape=None, seq_len=None, type_vocab_size=2, layer_norm_eps=1e-5,
+                 **kwargs):
         super().__init__(input_shape=None, **kwargs)
         self.vocab, self.hidden, self.n_block, self.n_head = vocab, hidden_size, n_block, n_head
         self.max_position_len, self.output_all_block = max_position_len, output_all_block
         self.seq_len = seq_len
         self.word = nn.Parameter(_normal((vocab, hidden_size), initializer_range))
         self.position = nn.Parameter(_normal((max_position_len, hidden_size), initializer_range))
-        self.token_type = nn.Parameter(_normal((2, hidden_size), initializer_range))
+        self.token_type = nn.Parameter(_normal((type_vocab_size, hidden_size), initializer_range))
+        self.layer_norm_eps = float(layer_norm_eps)
         self.emb_ln_g, self.emb_ln_b = nn.Parameter(torch.ones(hidden_size)), nn.Parameter(torch.zeros(hidden_size))
         self.hidden_drop = hidden_drop
         self.blocks = nn.ModuleList([_Block(hidden_size, n_head, intermediate_size, hidden_drop, attn_drop,
-                                            initializer_range, gelu="erf") for _ in range(n_block)])
+                                            initializer_range, gelu="erf", ln_eps=layer_norm_eps)
+                                     for _ in range(n_block)])
         self.pool_w = nn.Parameter(_normal((hidden_size, hidden_size), initializer_range))
         self.pool_b = nn.Parameter(torch.zeros(hidden_size))
         self.built = True
@@ -152,7 +157,7 @@ class BERT(Layer):
         tok, typ, pos = xs[0].long(), xs[1].long(), xs[2].long()
         amask = xs[3] if len(xs) > 3 else None
         e = ops.embedding(tok, self.word) + ops.embedding(typ, self.token_type) + ops.embedding(pos, self.position)
-        x = F.dropout(ops.layer_norm(e, self.emb_ln_g, self.emb_ln_b, 1e-12 if False else 1e-5), self.hidden_drop,
+        x = F.dropout(ops.layer_norm(e, self.emb_ln_g, self.emb_ln_b, self.layer_norm_eps), self.hidden_drop,
                       self.training)
         mask = None
         if amask is not None:

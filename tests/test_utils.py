@@ -72,3 +72,35 @@ def test_checkpoint_file_uri(tmp_path):
     uri = "file://" + str(tmp_path / "ck" / "model.1")
     save_object({"w": torch.ones(2)}, uri)
     assert load_object(uri)["w"].tolist() == [1.0, 1.0]
+
+
+REFERENCE_IMPORT_PATHS = [
+    "zoo.automl.model.Seq2Seq", "zoo.automl.model.VanillaLSTM", "zoo.feature.image.imagePreprocessing",
+    "zoo.feature.text.text_feature", "zoo.feature.text.transformer", "zoo.models.image.common.image_config",
+    "zoo.models.image.common.image_model", "zoo.models.image.imageclassification.image_classification",
+    "zoo.models.image.objectdetection.object_detector", "zoo.pipeline.api.keras.layers.convolutional_recurrent",
+    "zoo.pipeline.api.keras.layers.local", "zoo.pipeline.api.keras.layers.noise",
+    "zoo.pipeline.api.keras.layers.torch", "zoo.pipeline.api.keras2.layers.convolutional",
+    "zoo.pipeline.api.keras2.layers.core", "zoo.pipeline.api.keras2.layers.merge",
+    "zoo.pipeline.api.keras2.layers.pooling", "zoo.pipeline.api.net.net_load", "zoo.pipeline.api.net.torch_criterion",
+    "zoo.pipeline.nnframes.nn_image_schema", "zoo.ray.mxnet.mxnet_trainer", "zoo.tfpark.estimator",
+    "zoo.tfpark.zoo_optimizer", "zoo.tfpark.text.estimator", "zoo.tfpark.text.keras", "zoo.util.nest",
+    "zoo.common.utils", "zoo.automl.search.abstract",
+]
+
+
+@pytest.mark.parametrize("mod", REFERENCE_IMPORT_PATHS)
+def test_reference_import_paths(mod):
+    """A user of the reference can keep its import paths (Py/<path>.py)."""
+    import importlib
+    m = importlib.import_module(mod)
+    assert [n for n in dir(m) if not n.startswith("_")]
+
+
+def test_layers_star_import_does_not_shadow_torch():
+    import torch
+    import zoo.pipeline.api.keras.layers.torch  # noqa: F401  (reference-named submodule)
+    ns = {}
+    exec("from zoo.pipeline.api.keras.layers import *", ns)
+    assert "torch" not in ns and "Dense" in ns
+    assert torch.zeros(1).numel() == 1
