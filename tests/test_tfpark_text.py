@@ -219,3 +219,63 @@ def test_intent_entity_and_sequence_tagger():
     pp, pc = st.predict(words)
     assert pp.shape == (32, 6, 4) and pc.shape == (32, 6, 3)
     assert np.isfinite(st.evaluate(words, [words % 4, tags])["loss"])
+
+
+def test_tf_predictor_over_dataset():
+    from zoo.tfpark import TFDataset
+    from zoo.tfpark.tf_predictor import TFPredictor
+    from zoo.pipeline.api.keras.layers import Dense
+    from zoo.pipeline.api.keras.models import Sequential
+    m = Sequential()
+    m.add(Dense(3, input_shape=(4,)))
+    x = np.random.rand(10, 4).astype(np.float32)
+    ds = TFDataset.from_ndarrays(x, batch_per_thread=4)
+    out = TFPredictor.from_keras(m, ds).predict()
+    with torch.no_grad():
+        ref = m(torch.from_numpy(x)).numpy()
+    np.testing.assert_allclose(out, ref, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_bert_encoder_gpu_matches_numpy_reference(gpu, monkeypatch):
+    """The checkpoint-loaded encoder on the native GPU path (MFMA GEMMs, fused
+    attention, native LayerNorm; bf16 compute) against the fp32 numpy BERT."""
+    from zoo.pipeline.api.net import tf_graph
+    from zoo.tfpark.text.estimator import BertEncoder, load_bert_checkpoint
+    v = _fake_google_ckpt(H=64, nh=4, inter=128, vocab=50, maxpos=32)
+    monkeypatch.setattr(tf_graph, "read_tensor_bundle", lambda prefix: v)
+    enc = BertEncoder(_cfg(hidden_size=64, intermediate_size=128, max_position_embeddings=32))
+    load_bert_checkpoint(enc.bert, "unused")
+    enc = enc.to(gpu).eval()
+    rng = np.random.default_rng(2)
+    ids = rng.integers(0, 50, (4, 32))
+    tt = rng.integers(0, 2, (4, 32))
+    mask = np.ones((4, 32), np.float32)
+    mask[2, 20:] = 0
+    with torch.no_grad():
+        seq, pooled = enc({"input_ids": torch.from_numpy(ids).to(gpu), "token_type_ids": torch.from_numpy(tt).to(gpu),
+                           "input_mask": torch.from_numpy(mask).to(gpu)})
+    rs, rp = _numpy_google_bert(v, ids, tt, mask, 64, 4, 2)
+    err = np.abs(seq.float().cpu().numpy() - rs).max() / np.abs(rs).max()
+    assert err < 5e-2, err
+    assert np.abs(pooled.float().cpu().numpy() - rp).max() < 5e-2
+
+
+@pytest.mark.gpu
+def test_bert_classifier_and_ner_train_on_gpu(gpu):
+    from zoo.tfpark.text.estimator import BERTClassifier, bert_input_fn
+    from zoo.tfpark.text.keras import NER
+    from zoo.pipeline.api.keras.optimizers import Adam
+    torch.manual_seed(0)
+    rows = _bert_rows(64, 16, lambda ids: int(ids[0] > 25))
+    est = BERTClassifier(2, _cfg(hidden_size=64, intermediate_size=128), optimizer=Adam(lr=2e-3))
+    fn = bert_input_fn(rows, 16, 16)
+    before = est.evaluate(fn)["loss"]
+    est.train(fn, steps=60)
+    after = est.evaluate(fn)
+    assert after["loss"] < before and after["acc"] > 0.8, (before, after)
+    words, chars, tags = _tag_data()
+    m = NER(3, 30, 20, word_length=4, word_emb_dim=16, char_emb_dim=8, tagger_lstm_dim=16, dropout=0.0,
+            optimizer=Adam(lr=1e-2))
+    hist = m.fit([words, chars], np.eye(3)[tags], batch_size=16, epochs=5)
+    assert np.isfinite(hist[-1]) and hist[-1] < hist[0]
