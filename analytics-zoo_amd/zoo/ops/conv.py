@@ -147,6 +147,12 @@ def conv2d_nhwc(x, w, bias=None, kernel=(1, 1), stride=(1, 1), pad=(0, 0), dil=(
     if x.is_cuda:
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
+        if act == "gelu" and torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or
+                                                          (bias is not None and bias.requires_grad)):
+            # GELU's derivative needs the pre-activation, which the fused epilogue does not keep:
+            # training runs the GEMM with a plain epilogue and GELU as a separate op
+            y = _Conv2dFn.apply(x.contiguous(), w, bias, R, S, tuple(stride), tuple(pad), tuple(dil), None, out_f32)
+            return F.gelu(y)
         return _Conv2dFn.apply(x.contiguous(), w, bias, R, S, tuple(stride), tuple(pad), tuple(dil), act, out_f32)
     y = conv2d_ref(x, w, (R, S, Cin, tuple(stride), tuple(pad), tuple(dil)), bias)
     y = _ref_act(y, act)
