@@ -114,8 +114,14 @@ ZOO_DEV void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 // lane-linear 1-KiB piece, the swizzle is applied on the per-lane SOURCE address
 // (position (row, pc) receives logical chunk pc ^ swz(row)). The NW waves of the
 // block split the pieces; no staging registers, no ds_write.
+// element strides of the forward kernel's operands: [batch, head, row]
+struct AttnStrides {
+  long qb, qh, ql, kb, kh, kl, vb, vh, vl, ob, oh, ol;
+};
+
 template <int D, int NW>
-ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf16_t* dst1, int r0, int nrows) {
+ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf16_t* dst1, int r0, int nrows,
+                       long ld0 = D, long ld1 = D) {
   constexpr int PPT = D / 8;            // 1-KiB pieces per tile
   constexpr int PPW = 2 * PPT / NW;     // pieces per wave
   static_assert((2 * PPT) % NW == 0, "pieces must split evenly over the waves");
@@ -129,7 +135,7 @@ ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf1
     const int pp = second ? gp - PPT : gp;
     const int row = pp * RP + rsub;
     const int r = min(r0 + row, nrows - 1);
-    const bf16_t* sp = (second ? src1 : src0) + (size_t)r * D + ((pc ^ swz<D>(row)) << 3);
+    const bf16_t* sp = (second ? src1 : src0) + (size_t)r * (second ? ld1 : ld0) + ((pc ^ swz<D>(row)) << 3);
     bf16_t* dp = (second ? dst1 : dst0) + pp * 512;
     __builtin_amdgcn_global_load_lds((gl_void*)sp, (lds_void*)dp, 16, 0, 0);
   }
@@ -139,7 +145,7 @@ template <int D, int NW, bool HAS_MASK>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, bf16_t* __restrict__ O, float* __restrict__ LSE, int H, int L, int S,
-    float scale, int causal) {
+    float scale, int causal, AttnStrides sd) {
   constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);  // [2][64][D]
@@ -147,9 +153,11 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
   float* Ms = reinterpret_cast<float*>(Vs + 2 * 64 * D);  // [2][64] additive mask (log2 units)
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
-  const int bh = blockIdx.y, b = bh / H;
-  const bf16_t* Kp = K + (size_t)bh * S * D;
-  const bf16_t* Vp = V + (size_t)bh * S * D;
+  const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+  // element strides (batch, head, row); rows are D-contiguous. Contiguous [B,H,T,D]
+  // tensors and views into a packed [B,T,3,H,D] QKV projection both come through here.
+  const bf16_t* Kp = K + b * sd.kb + hd * sd.kh;
+  const bf16_t* Vp = V + b * sd.vb + hd * sd.vh;
   const float* mrow = HAS_MASK ? mask + (size_t)b * S : nullptr;
   // causal: heaviest query blocks (largest index) first
   const int qb = causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
@@ -159,7 +167,8 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
 
   bf16x8 qf[KS];
 #pragma unroll
-  for (int ks = 0; ks < KS; ++ks) qf[ks] = load_frag(Q + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q < L);
+  for (int ks = 0; ks < KS; ++ks)
+    qf[ks] = load_frag(Q + b * sd.qb + hd * sd.qh + (long)min(q, L - 1) * sd.ql + 16 * ks + 8 * h, q < L);
 
   f32x16 o[DT];
 #pragma unroll
@@ -183,7 +192,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
     if (HAS_MASK && threadIdx.x < 64) Ms[buf * 64 + threadIdx.x] = mreg;
   };
   if (ntiles > 0) {
-    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S);
+    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S, sd.kl, sd.vl);
     load_mask(0);
     wait_vm0();
     store_mask(0);
@@ -193,7 +202,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1, kv0 = t * 64;
     if (t + 1 < ntiles) {
-      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S);
+      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S, sd.kl, sd.vl);
       load_mask(kv0 + 64);
     }
     const bf16_t* kt_ = Ks + buf * 64 * D;
@@ -290,7 +299,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
   lsum += __shfl_xor(lsum, 32, 64);
   if (q >= L) return;
   const float inv = lsum > 0.f ? 1.f / lsum : 0.f;
-  bf16_t* orow = O + ((size_t)bh * L + q) * D;
+  bf16_t* orow = O + b * sd.ob + hd * sd.oh + (long)q * sd.ol;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -669,7 +678,7 @@ using namespace zoo;
 
 template <int D, int NW, bool HM>
 static void launch_fwd(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
-                       int H, int L, int S, float scale, int causal, hipStream_t st) {
+                       int H, int L, int S, float scale, int causal, const AttnStrides& sd, hipStream_t st) {
   const dim3 grid((L + 32 * NW - 1) / (32 * NW), B * H);
   const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 2 * 64 * sizeof(float);
   static const bool lds_ok_ = [] {
@@ -679,29 +688,38 @@ static void launch_fwd(const void* q, const void* k, const void* v, const float*
   }();
   (void)lds_ok_;
   hipLaunchKernelGGL((attn_fwd_kernel<D, NW, HM>), grid, dim3(NW * 64), smem, st, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal);
+                     (const bf16_t*)k, (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal, sd);
 }
 
 template <int D>
 static void launch_fwd_d(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
-                         int H, int L, int S, float scale, int causal, hipStream_t st) {
+                         int H, int L, int S, float scale, int causal, const AttnStrides& sd, hipStream_t st) {
   // 8 waves (256 query rows) share each K/V tile when there are enough rows
   if (L >= 256) {
-    if (mask) launch_fwd<D, 8, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
-    else launch_fwd<D, 8, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    if (mask) launch_fwd<D, 8, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    else launch_fwd<D, 8, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
   } else {
-    if (mask) launch_fwd<D, 4, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
-    else launch_fwd<D, 4, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    if (mask) launch_fwd<D, 4, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    else launch_fwd<D, 4, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
   }
 }
 
+// strides: 12 element strides (q, k, v, o) x (batch, head, row); nullptr = contiguous [B,H,T,D]
 extern "C" hipError_t zoo_attn_fwd(const void* q, const void* k, const void* v, const float* mask, void* o,
                                    float* lse, int B, int H, int L, int S, int D, float scale, int causal,
-                                   hipStream_t st) {
+                                   const long* strides, hipStream_t st) {
+  AttnStrides sd;
+  if (strides) {
+    sd = AttnStrides{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
+                     strides[6], strides[7], strides[8], strides[9], strides[10], strides[11]};
+  } else {
+    sd = AttnStrides{(long)H * L * D, (long)L * D, D, (long)H * S * D, (long)S * D, D,
+                     (long)H * S * D, (long)S * D, D, (long)H * L * D, (long)L * D, D};
+  }
   if (D == 64)
-    launch_fwd_d<64>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    launch_fwd_d<64>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
   else if (D == 128)
-    launch_fwd_d<128>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, st);
+    launch_fwd_d<128>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

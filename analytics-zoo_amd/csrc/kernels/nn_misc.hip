@@ -65,6 +65,66 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const T* __restrict_
   }
 }
 
+// Row-resident variant for D <= NCH*512: one wave per row keeps its NCH x 8
+// values in registers between the statistics and the normalise pass (the row
+// is read once), and gamma/beta are read with 16-byte vector loads.
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void layernorm_fwd_reg_kernel(const T* __restrict__ X, const float* __restrict__ g,
+                                                                const float* __restrict__ b, T* __restrict__ Y,
+                                                                float* __restrict__ mean_out,
+                                                                float* __restrict__ rstd_out, int rows, int D,
+                                                                float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const T* x = X + (size_t)row * D;
+  float v[NCH][8];
+  float s = 0.f, ss = 0.f;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c < D) {
+      ld8(x + c, v[k]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[k][e] = 0.f;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { s += v[k][e]; ss += v[k][e] * v[k][e]; }
+  }
+  s = warp_sum(s);
+  ss = warp_sum(ss);
+  const float mu = s / D;
+  const float var = fmaxf(ss / D - mu * mu, 0.f);
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) { mean_out[row] = mu; rstd_out[row] = rs; }
+  T* y = Y + (size_t)row * D;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c >= D) continue;
+    float gg[8], bb[8];
+    if (g) {
+      const float4 g0 = *reinterpret_cast<const float4*>(g + c), g1 = *reinterpret_cast<const float4*>(g + c + 4);
+      gg[0] = g0.x; gg[1] = g0.y; gg[2] = g0.z; gg[3] = g0.w; gg[4] = g1.x; gg[5] = g1.y; gg[6] = g1.z; gg[7] = g1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) gg[e] = 1.f;
+    }
+    if (b) {
+      const float4 b0 = *reinterpret_cast<const float4*>(b + c), b1 = *reinterpret_cast<const float4*>(b + c + 4);
+      bb[0] = b0.x; bb[1] = b0.y; bb[2] = b0.z; bb[3] = b0.w; bb[4] = b1.x; bb[5] = b1.y; bb[6] = b1.z; bb[7] = b1.w;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bb[e] = 0.f;
+    }
+    float o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (v[k][e] - mu) * rs * gg[e] + bb[e];
+    st8(y + c, o);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ dY, const T* __restrict__ X,
                                                             const float* __restrict__ g, const float* __restrict__ mean,
@@ -167,6 +227,24 @@ using namespace zoo;
 extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, const float* b, void* Y, float* mean,
                                         float* rstd, int rows, int D, float eps, hipStream_t st) {
   const int blocks = (rows + 3) / 4;
+  // gamma/beta are read as float4 by the register-resident kernels
+  const bool al = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
+#define ZOO_LN_REG(T, NCH)                                                                                   \
+  hipLaunchKernelGGL((layernorm_fwd_reg_kernel<T, NCH>), dim3(blocks), dim3(256), 0, st, (const T*)X, g, b, \
+                     (T*)Y, mean, rstd, rows, D, eps)
+  if (al && D <= 2048) {
+    if (f32) {
+      if (D <= 512) ZOO_LN_REG(float, 1);
+      else if (D <= 1024) ZOO_LN_REG(float, 2);
+      else ZOO_LN_REG(float, 4);
+    } else {
+      if (D <= 512) ZOO_LN_REG(bf16_t, 1);
+      else if (D <= 1024) ZOO_LN_REG(bf16_t, 2);
+      else ZOO_LN_REG(bf16_t, 4);
+    }
+    return hipGetLastError();
+  }
+#undef ZOO_LN_REG
   if (f32)
     hipLaunchKernelGGL(layernorm_fwd_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)X, g, b, (float*)Y,
                        mean, rstd, rows, D, eps);

@@ -65,7 +65,7 @@ hipError_t zoo_im2col_q8(const void*, int, const float*, void*, int, int, int, i
 hipError_t zoo_qgemm(const void*, const void*, const float*, const float*, const float*, const void*, void*, int, int,
                      int, int, int, hipStream_t);
 hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
-                        float, int, hipStream_t);
+                        float, int, const long*, hipStream_t);
 hipError_t zoo_rnn(const zoo::RnnArgs*, int, int, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
@@ -699,8 +699,44 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
   if (q.numel() == 0) return {o, lse};
   check_hip(zoo_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask), o.data_ptr(),
                          lse.data_ptr<float>(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal,
-                         cur_stream()),
+                         nullptr, cur_stream()),
             "attn_fwd");
+  return {o, lse};
+}
+
+// Forward attention on strided [B, H, T, D] views (D contiguous, 16-byte aligned rows), e.g. the
+// q/k/v slices of one packed [B, T, 3, H, D] projection, so no per-head copies are made. With
+// out_blhd the output is written as [B, L, H, D] (the layout the output projection reads).
+std::vector<torch::Tensor> attn_fwd_strided(torch::Tensor q, torch::Tensor k, torch::Tensor v,
+                                            c10::optional<torch::Tensor> mask, bool causal, bool out_blhd) {
+  for (const torch::Tensor* t : {&q, &k, &v}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "attention: q/k/v must be bf16 GPU tensors");
+    TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1, "attention: head_dim must be the contiguous dim");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 && t->stride(2) % 8 == 0 &&
+                    t->stride(1) % 8 == 0 && t->stride(0) % 8 == 0,
+                "attention: rows must be 16-byte aligned");
+  }
+  TORCH_CHECK(k.sizes() == v.sizes(), "attention: k and v shapes differ");
+  TORCH_CHECK(q.size(0) == k.size(0) && q.size(1) == k.size(1) && q.size(3) == k.size(3),
+              "attention: q/k batch, heads or head_dim differ");
+  const int B = q.size(0), H = q.size(1), L = q.size(2), S = k.size(2), D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(B * H < 65536, "attention: B*H must be < 65536");
+  if (mask.has_value() && mask->defined()) {
+    req(*mask, at::kFloat, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == B && mask->size(1) == S, "attention: mask must be [B, S]");
+  }
+  auto o = out_blhd ? torch::empty({B, L, H, D}, q.options()) : torch::empty({B, H, L, D}, q.options());
+  auto lse = torch::empty({B, H, L}, q.options().dtype(at::kFloat));
+  if (q.numel() == 0) return {o, lse};
+  const long st[12] = {(long)q.stride(0), (long)q.stride(1), (long)q.stride(2), (long)k.stride(0),
+                       (long)k.stride(1), (long)k.stride(2), (long)v.stride(0), (long)v.stride(1),
+                       (long)v.stride(2), (long)o.stride(0), (long)(out_blhd ? o.stride(2) : o.stride(1)),
+                       (long)(out_blhd ? o.stride(1) : o.stride(2))};
+  check_hip(zoo_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask), o.data_ptr(),
+                         lse.data_ptr<float>(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, st,
+                         cur_stream()),
+            "attn_fwd_strided");
   return {o, lse};
 }
 
@@ -918,6 +954,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd_strided", &attn_fwd_strided);
   m.def("absmax", &absmax);
   m.def("im2col_q8", &im2col_q8);
   m.def("qgemm", &qgemm);

@@ -37,8 +37,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--shapes", default=None, help="comma-separated indices into SHAPES")
     ap.add_argument("--zoo-only", action="store_true")
+    ap.add_argument("--bert", action="store_true", help="BERT-base b128 x L128 linear-layer shapes")
     a = ap.parse_args()
     shapes = SHAPES if a.shapes is None else [SHAPES[int(i)] for i in a.shapes.split(",")]
+    if a.bert:  # (M, N, K) of QKV, attention output, FFN1, FFN2 at 16384 tokens
+        shapes = [(16384, 2304, 768), (16384, 768, 768), (16384, 3072, 768), (16384, 768, 3072),
+                  (4096, 2304, 768), (4096, 768, 3072)]
     dev = torch.device("cuda:0")
     rows = []
     for M, N, K in shapes:

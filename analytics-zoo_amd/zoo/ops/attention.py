@@ -57,6 +57,25 @@ def _native_ok(q, k, v, mask, dropout_p, training):
     return True
 
 
+def attention_packed(qkv, n_head, mask=None, causal=False):
+    """Inference attention straight from a packed [B, L, 3*H*D] QKV projection:
+    the fused kernel reads q/k/v through strides and writes [B, L, H*D], so the
+    per-head permute copies disappear. Returns None when the fused kernel does
+    not apply (caller falls back to :func:`attention`)."""
+    B, L, three_h = qkv.shape
+    hd = three_h // (3 * n_head)
+    if not (qkv.is_cuda and qkv.dtype == torch.bfloat16 and hd in (64, 128) and qkv.is_contiguous()):
+        return None
+    if torch.is_grad_enabled() and qkv.requires_grad:
+        return None
+    if mask is not None and (mask.dim() != 2 or tuple(mask.shape) != (B, L)):
+        return None
+    v5 = qkv.view(B, L, 3, n_head, hd).permute(2, 0, 3, 1, 4)   # [3, B, H, L, hd] strided views
+    o, _ = native().attn_fwd_strided(v5[0], v5[1], v5[2], None if mask is None else mask.float().contiguous(),
+                                     bool(causal), True)
+    return o.view(B, L, n_head * hd)
+
+
 def attention(q, k, v, mask=None, causal=False, dropout_p=0.0, training=False):
     """mask: additive float mask broadcastable to [B, H, L, S]; a [B, S] key
     mask (0 keep / -10000 drop, BERT style) takes the fused path."""

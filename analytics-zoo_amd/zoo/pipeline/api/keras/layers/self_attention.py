@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.ops.attention import attention_packed
 from zoo.pipeline.api.keras.base import Layer
 
 
@@ -52,10 +53,14 @@ class _Block(nn.Module):
         B, L, H = x.shape
         nh, hd = self.n_head, H // self.n_head
         qkv = ops.linear(x, self.qkv_w, self.qkv_b)                   # [B, L, 3H]
-        qkv = qkv.reshape(B, L, 3, nh, hd).permute(2, 0, 3, 1, 4)     # [3, B, nh, L, hd]
-        a = ops.attention(qkv[0], qkv[1], qkv[2], mask=mask, causal=causal, dropout_p=self.attn_drop,
-                          training=self.training)
-        a = a.transpose(1, 2).reshape(B, L, H)
+        a = None
+        if not (self.training and self.attn_drop > 0):
+            a = attention_packed(qkv, nh, mask=mask, causal=causal)     # strided, no head copies
+        if a is None:
+            qkv = qkv.reshape(B, L, 3, nh, hd).permute(2, 0, 3, 1, 4)  # [3, B, nh, L, hd]
+            a = ops.attention(qkv[0], qkv[1], qkv[2], mask=mask, causal=causal, dropout_p=self.attn_drop,
+                              training=self.training)
+            a = a.transpose(1, 2).reshape(B, L, H)
         a = F.dropout(ops.linear(a, self.proj_w, self.proj_b), self.hidden_drop, self.training)
         n = ops.layer_norm(x + a, self.ln1_g, self.ln1_b, self.ln_eps)
         act = "gelu" if self.gelu == "erf" else None
@@ -106,6 +111,8 @@ class TransformerLayer(Layer):
             return self.embedding_layer([xs[0], xs[1]])
         # reference: one table shared by word and position ids, summed
         e = ops.embedding(tok, self.tok) + ops.embedding(pos, self.tok)
+        if e.is_cuda:
+            e = e.to(torch.bfloat16)
         return F.dropout(e, self.embedding_drop, self.training)
 
     def call(self, xs):
@@ -157,6 +164,8 @@ class BERT(Layer):
         tok, typ, pos = xs[0].long(), xs[1].long(), xs[2].long()
         amask = xs[3] if len(xs) > 3 else None
         e = ops.embedding(tok, self.word) + ops.embedding(typ, self.token_type) + ops.embedding(pos, self.position)
+        if e.is_cuda:  # bf16 activations end to end on the GPU (LayerNorm / attention / GEMMs all take bf16)
+            e = e.to(torch.bfloat16)
         x = F.dropout(ops.layer_norm(e, self.emb_ln_g, self.emb_ln_b, self.layer_norm_eps), self.hidden_drop,
                       self.training)
         mask = None

@@ -82,3 +82,25 @@ def test_fused_attention_lse_and_fully_masked_rows():
     o2, _ = native().attn_fwd(q2, k[:, :1], v[:, :1], None, True)
     assert o2[:, :, :64].abs().max().item() == 0.0
     assert torch.isfinite(o2.float()).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hd,causal", [(64, False), (64, True), (128, False)])
+def test_attention_packed_strided_matches_reference(hd, causal):
+    """Fused forward reading q/k/v through strides of one packed [B, L, 3*H*hd]
+    projection and writing [B, L, H*hd] (inference path, no head copies)."""
+    from zoo.ops.attention import _reference, attention_packed
+    torch.manual_seed(0)
+    B, L, H = 2, 200, 4
+    dev = torch.device("cuda")
+    qkv = (torch.randn(B, L, 3 * H * hd, device=dev) * 0.5).bfloat16()
+    mask = torch.zeros(B, L, device=dev)
+    mask[1, 150:] = -10000.0
+    with torch.no_grad():
+        out = attention_packed(qkv, H, mask=mask, causal=causal)
+    assert out is not None and out.shape == (B, L, H * hd)
+    v5 = qkv.float().view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4)
+    ref = _reference(v5[0], v5[1], v5[2], mask[:, None, None, :], causal, 0.0, False)
+    ref = ref.transpose(1, 2).reshape(B, L, H * hd)
+    err = (out.float() - ref).abs().max() / ref.abs().max()
+    assert err < 2e-2, err

@@ -564,3 +564,28 @@ def test_engine_hipgraph_matches_eager(gpu):
     (l0, p0), (l1, p1) = res
     assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3, (l0, l1)
     assert rel(p1, p0) < 1e-3
+
+
+@pytest.mark.parametrize("act", [None, "relu", "gelu"])
+def test_linear_blas_path_fwd_bwd(gpu, act):
+    """Transformer-size linear layers (hipBLASLt bf16 path): forward and the three
+    gradients vs fp32 autograd on bf16-rounded operands."""
+    from zoo.ops import linear
+    from zoo.ops.conv import _use_blas
+    torch.manual_seed(0)
+    x = _bf(torch.randn(2048, 256, device=gpu)).requires_grad_(True)
+    w = _bf(torch.randn(512, 256, device=gpu) * 0.05).requires_grad_(True)
+    b = torch.randn(512, device=gpu).requires_grad_(True)
+    assert _use_blas(x, 256, 512, act)
+    y = linear(x.bfloat16(), w, b, act=act).float()
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
+    yr = xr @ wr.t() + br
+    if act == "relu":  # the ReLU mask of the bf16 output (entries at ~0 may round either way)
+        yr = yr * (y.detach() > 0).float()
+    else:
+        yr = {"gelu": torch.nn.functional.gelu, None: lambda v: v}[act](yr)
+    yr.backward(dy)
+    assert rel(y, yr) < 2e-2
+    assert rel(x.grad, xr.grad) < 3e-2 and rel(w.grad, wr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
