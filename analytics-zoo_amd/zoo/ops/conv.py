@@ -37,11 +37,25 @@ def conv_out_size(h, r, stride, pad, dil=1):
 
 
 def bf16_weight(w):
-    """bf16 compute copy of a packed weight (engine-maintained if present)."""
+    """bf16 compute copy of a packed weight: engine-maintained (``_zoo_bf16``, a
+    view into the flat bf16 buffer the optimizer rewrites) when training;
+    otherwise converted once and cached on the parameter until it is modified
+    (in-place updates bump ``_version``), so inference pays no per-call cast."""
     c = getattr(w, "_zoo_bf16", None)
     if c is not None:
         return c
-    return w.detach().to(torch.bfloat16)
+    if w.dtype == torch.bfloat16:
+        return w.detach()
+    cc = getattr(w, "_zoo_bf16_cache", None)
+    if cc is not None and cc[0] == w._version and cc[1] == w.data_ptr():
+        return cc[2]
+    b = w.detach().to(torch.bfloat16)
+    if not torch.is_grad_enabled() or not w.requires_grad:
+        try:
+            w._zoo_bf16_cache = (w._version, w.data_ptr(), b)
+        except (AttributeError, RuntimeError):
+            pass
+    return b
 
 
 def accumulate_grad(param, g):
