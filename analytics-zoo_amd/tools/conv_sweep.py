@@ -60,6 +60,16 @@ def main():
         if "wgrad" in ops:
             dw = torch.zeros(Cout, ktot, device=dev)
             row["wgrad"] = timeit(lambda: C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, 1, 1))
+            if R == 1 and st == 1:  # library GEMM for comparison: dW = dY^T X, fp32 output
+                x2, dy2 = x.reshape(-1, Cin), dy.reshape(-1, Cout)
+                row["wgrad_blas"] = timeit(lambda: torch.mm(dy2.t(), x2, out_dtype=torch.float32))
+        if "fwd" in ops and R == 1 and st == 1:
+            x2 = x.reshape(-1, Cin)
+            row["fwd_blas"] = timeit(lambda: torch.mm(x2, w2[:, :Cin].t()))
+        if "dgrad" in ops and R == 1 and st == 1:
+            dy2 = dy.reshape(-1, Cout)
+            wt = w2[:, :Cin].contiguous()
+            row["dgrad_blas"] = timeit(lambda: torch.mm(dy2, wt))
         for o in ops:
             tot[o] += row.get(o, 0.0) * cnt
         if a.detail:
