@@ -46,7 +46,9 @@ class ZooConfig:
     pin_memory: bool = True
     # logging / tracing
     log_every: int = 50
-    roctx: bool = False
+    roctx: bool = False                  # ZOO_ROCTX: roctx ranges around engine phases (rocprofv3 --marker-trace)
+    phase_timing: bool = False           # ZOO_PHASE_TIMING: per-phase device timings (fwd+bwd / comm / optim)
+    debug_sync: bool = False             # ZOO_DEBUG_SYNC: synchronise + check for non-finite loss every step
     seed: int = 1
     backend: str = ""                    # "", "nccl" (RCCL), "gloo"
     timeout_s: float = 1800.0
@@ -57,6 +59,7 @@ class ZooConfig:
         "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
         "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
         "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",
+        "phase_timing": "ZOO_PHASE_TIMING", "debug_sync": "ZOO_DEBUG_SYNC",
         "backend": "ZOO_DIST_BACKEND", "timeout_s": "ZOO_DIST_TIMEOUT",
     }
     _LEGACY = {"failure_retry_times": "bigdl.failure.retryTimes",

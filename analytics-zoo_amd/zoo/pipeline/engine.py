@@ -40,6 +40,57 @@ class InjectedFault(RuntimeError):
     pass
 
 
+class _Phases:
+    """roctx ranges (``torch.cuda.nvtx`` is roctx on ROCm: visible with
+    ``rocprofv3 --marker-trace``) and optional device-side phase timings with
+    HIP events. Both are off unless configured, and neither
+    synchronises inside a step: event pairs are resolved at the next report."""
+
+    def __init__(self, roctx, timing, device):
+        self.roctx = roctx and device.type == "cuda"
+        self.timing = timing and device.type == "cuda"
+        self.pending = []
+        self.totals = {}
+        self.counts = {}
+
+    def range(self, name):
+        return _PhaseRange(self, name)
+
+    def resolve(self):
+        keep = []
+        for name, a, b in self.pending:
+            if b.query():
+                self.totals[name] = self.totals.get(name, 0.0) + a.elapsed_time(b)
+                self.counts[name] = self.counts.get(name, 0) + 1
+            else:
+                keep.append((name, a, b))
+        self.pending = keep
+        return {k: self.totals[k] / max(self.counts[k], 1) for k in self.totals}
+
+
+class _PhaseRange:
+    __slots__ = ("ph", "name", "ev")
+
+    def __init__(self, ph, name):
+        self.ph, self.name, self.ev = ph, name, None
+
+    def __enter__(self):
+        if self.ph.roctx:
+            torch.cuda.nvtx.range_push("zoo." + self.name)
+        if self.ph.timing:
+            self.ev = torch.cuda.Event(enable_timing=True)
+            self.ev.record()
+        return self
+
+    def __exit__(self, *exc):
+        if self.ph.timing:
+            end = torch.cuda.Event(enable_timing=True)
+            end.record()
+            self.ph.pending.append((self.name, self.ev, end))
+        if self.ph.roctx:
+            torch.cuda.nvtx.range_pop()
+
+
 def _move(batch, device, non_blocking=True):
     if isinstance(batch, torch.Tensor):
         return batch.to(device, non_blocking=non_blocking)
@@ -80,6 +131,8 @@ class TrainingEngine:
         # hipGraph capture of forward+backward (launch-bound models, e.g. NCF):
         # the graph replays every kernel of the step with one launch; the
         # gradient all-reduce and the optimizer stay eager after the replay
+        self.phases = _Phases(cfg.roctx, cfg.phase_timing, self.device)
+        self.debug_sync = cfg.debug_sync
         self.hip_graph = (cfg.hip_graph if hip_graph is None else bool(hip_graph)) and self.device.type == "cuda"
         self._graphs = {}
         self._graph_warm = {}
@@ -91,13 +144,25 @@ class TrainingEngine:
             self._fault_fired = True
             raise InjectedFault("injected fault at iteration %d" % self.fault_step)
         self.model.train()
-        if self.hip_graph and torch.is_tensor(target):
-            loss = self._graph_fwd_bwd(inputs, target)
-        else:
-            loss = self._fwd_bwd(inputs, target)
-        self.sync.step(self.optim, self.clip)
+        ph = self.phases
+        with ph.range("fwd_bwd"):
+            if self.hip_graph and torch.is_tensor(target):
+                loss = self._graph_fwd_bwd(inputs, target)
+            else:
+                loss = self._fwd_bwd(inputs, target)
+        with ph.range("comm_optim"):
+            self.sync.step(self.optim, self.clip)
         self.state["neval"] += 1
+        if self.debug_sync:  # debug mode: surface asynchronous HIP errors / divergence at the failing step
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            if not torch.isfinite(loss).all():
+                raise FloatingPointError("non-finite loss at iteration %d" % (self.state["neval"] - 1))
         return loss
+
+    def phase_times(self):
+        """Mean device milliseconds per phase so far (needs ``phase_timing``)."""
+        return self.phases.resolve()
 
     def _fwd_bwd(self, inputs, target):
         self.flat.grad.zero_()
@@ -218,6 +283,8 @@ class TrainingEngine:
                     if self.train_summary is not None:
                         self.train_summary.add_scalar("Throughput", thr, state["neval"] - 1)
                         self.train_summary.add_scalar("LearningRate", self.optim.current_lr(), state["neval"] - 1)
+                        for name, ms in self.phase_times().items():
+                            self.train_summary.add_scalar("StepTime/%s_ms" % name, ms, state["neval"] - 1)
                     t_last, n_since = time.time(), 0
                 for cb in callbacks:
                     cb(self, state)
@@ -317,6 +384,43 @@ class TrainingEngine:
                     True)
         if self.sync.world > 1:
             self.ctx.barrier()
+
+    def save_flat_checkpoint(self, path):
+        """Fast native snapshot: the flat fp32 master buffer and the
+        optimizer state buffers as one safetensors file per rank (ZeRO-1 ranks each
+        hold their shard's state), plus the engine counters in the metadata."""
+        from safetensors.torch import save_file
+        import json as _json
+        t = {"master": self.flat.master.detach().cpu().contiguous()}
+        for i, b in enumerate(self.optim._buffers or []):
+            t["optim_state_%d" % i] = b.detach().cpu().contiguous()
+        meta = {"engine_state": _json.dumps({k: v for k, v in self.state.items()
+                                             if isinstance(v, (int, float, str, type(None)))}),
+                "optim_state": _json.dumps({k: v for k, v in self.optim.state.items()
+                                            if isinstance(v, (int, float, str))}),
+                "rank": str(self.ctx.rank), "world": str(self.sync.world)}
+        p = path if self.sync.world == 1 else "%s.rank%d" % (path, self.ctx.rank)
+        os.makedirs(os.path.dirname(os.path.abspath(p)), exist_ok=True)
+        save_file(t, p, metadata=meta)
+        return p
+
+    def load_flat_checkpoint(self, path):
+        from safetensors import safe_open
+        import json as _json
+        p = path if self.sync.world == 1 else "%s.rank%d" % (path, self.ctx.rank)
+        with safe_open(p, framework="pt", device="cpu") as f:
+            meta = f.metadata() or {}
+            self.flat.master.copy_(f.get_tensor("master").to(self.flat.master.device))
+            keys = sorted(k for k in f.keys() if k.startswith("optim_state_"))
+            if keys:
+                bufs = [f.get_tensor(k).to(self.device) for k in keys]
+                self.optim._buffers = bufs
+                self.optim._key = (bufs[0].numel(), str(self.device))
+        self.flat.refresh_bf16()
+        self.state.update(_json.loads(meta.get("engine_state", "{}")))
+        self.optim.state.update(_json.loads(meta.get("optim_state", "{}")))
+        self.sync.reset()
+        return self
 
     def latest_checkpoint(self):
         if self.checkpoint_path is None:

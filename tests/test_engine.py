@@ -247,3 +247,34 @@ def test_data_parallel_gloo_matches_single_process(mode):
         sl = slice(step * 16, step * 16 + 16)
         eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
     assert torch.allclose(res[0], eng.flat.master, atol=1e-5)
+
+
+def test_flat_safetensors_checkpoint_roundtrip(tmp_path):
+    """Fast native snapshot: master + optimizer state restored exactly; training
+    continues identically to an uninterrupted run."""
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import Adam
+    x, y = _toy(64)
+    xs, ys = torch.from_numpy(x), torch.from_numpy(y)
+    a = TrainingEngine(_mlp(seed=3), MeanSquaredError(), Adam(lr=0.01))
+    for _ in range(3):
+        a.train_step(xs[:32], ys[:32])
+    p = a.save_flat_checkpoint(str(tmp_path / "snap.safetensors"))
+    b = TrainingEngine(_mlp(seed=9), MeanSquaredError(), Adam(lr=0.01))
+    b.load_flat_checkpoint(p)
+    assert torch.equal(a.flat.master, b.flat.master) and b.state["neval"] == a.state["neval"]
+    la = a.train_step(xs[32:], ys[32:])
+    lb = b.train_step(xs[32:], ys[32:])
+    assert torch.allclose(a.flat.master, b.flat.master, atol=1e-7) and torch.allclose(la, lb)
+
+
+def test_phase_timing_and_debug_sync_are_inert_on_cpu():
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    x, y = _toy(32)
+    eng = TrainingEngine(_mlp(), MeanSquaredError(), SGD(learningrate=0.01))
+    eng.debug_sync = True
+    eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
+    assert eng.phase_times() == {}

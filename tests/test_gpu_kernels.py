@@ -589,3 +589,23 @@ def test_linear_blas_path_fwd_bwd(gpu, act):
     yr.backward(dy)
     assert rel(y, yr) < 2e-2
     assert rel(x.grad, xr.grad) < 3e-2 and rel(w.grad, wr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
+
+
+def test_engine_phase_timing_and_roctx_on_gpu(gpu):
+    """roctx ranges + HIP-event phase timings around the engine phases."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.resnet import resnet18
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine, _Phases
+    init_nncontext()
+    eng = TrainingEngine(resnet18(num_classes=10), softmax_cross_entropy, SGD(learningrate=0.01))
+    eng.phases = _Phases(True, True, torch.device("cuda"))
+    eng.debug_sync = True
+    x = torch.randn(8, 3, 64, 64, device=gpu)
+    y = torch.randint(0, 10, (8,), device=gpu)
+    for _ in range(3):
+        eng.train_step(x, y)
+    torch.cuda.synchronize()
+    t = eng.phase_times()
+    assert set(t) == {"fwd_bwd", "comm_optim"} and t["fwd_bwd"] > 0
