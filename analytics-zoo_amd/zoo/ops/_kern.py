@@ -33,9 +33,12 @@ def flip_weights(w, K, R, S, C, r0=0, s0=0, Ra=None, Sb=None, sh=1, sw=1):
     return native().flip_weights(w, K, R, S, C, r0, s0, Ra or R, Sb or S, sh, sw)
 
 
-def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None):
+def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None,
+               resid_inplace=False):
     """dX [N,H,W,C] of y = conv(x, w) given dY [N,P,Q,K] and the bf16 packed weight.
-    ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer)."""
+    ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer).
+    ``resid_inplace``: ``resid`` is a temporary the caller gives away; strided dgrads
+    with tap-less parity classes accumulate into it instead of a copy of it."""
     sh, sw = stride
     if (sh, sw) == (1, 1) or dil != (1, 1):
         wt = flip_weights(wb, K, R, S, C)
@@ -58,7 +61,10 @@ def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), 
     if bstats is not None and resid is not None and not full:
         raise NotImplementedError("fused bn-backward with zero parity classes and a residual")
     if resid is not None:
-        dx = resid.clone() if not full else torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+        if full:
+            dx = torch.empty(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
+        else:
+            dx = resid if (resid_inplace and resid.is_contiguous()) else resid.clone()
     else:
         dx = (torch.empty if full else torch.zeros)(N, H, W, C, dtype=torch.bfloat16, device=dy.device)
     for (a, b, r0, s0, Ra, Sb, Ha, Wb) in classes:

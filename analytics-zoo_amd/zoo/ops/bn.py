@@ -165,8 +165,9 @@ class _ConvBNActFn(torch.autograd.Function):
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
             pin = ctx.producer_in
             bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
+            # a handed-off gradient is a temporary owned by this unit now: accumulate into it in place
             dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, resid=add,
-                                  bstats=bst)
+                                  bstats=bst, resid_inplace=add is not None)
             if ctx.dx_out is not None:
                 # another consumer of x adds this gradient in its own dgrad epilogue
                 ctx.dx_out.grad = dx
