@@ -67,6 +67,7 @@ hipError_t zoo_qgemm(const void*, const void*, const float*, const float*, const
 hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
                         float, int, const long*, hipStream_t);
 hipError_t zoo_rnn(const zoo::RnnArgs*, int, int, int, hipStream_t);
+hipError_t zoo_nms_mask(const float*, int, float, unsigned long long*, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
@@ -670,6 +671,35 @@ torch::Tensor gemm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor
 }
 
 
+// ---- greedy NMS: boxes [N, 4] (x1, y1, x2, y2) fp32 already sorted by descending score ----
+// The suppression bitmask is built on the GPU (detect.hip); the sequential greedy
+// pass walks it on the host. Returns the kept row indices (int64, ascending = score order).
+torch::Tensor nms_sorted(torch::Tensor boxes, double thresh, int64_t max_keep) {
+  req(boxes, at::kFloat, "boxes");
+  TORCH_CHECK(boxes.dim() == 2 && boxes.size(1) == 4, "nms: boxes must be [N, 4]");
+  const int n = boxes.size(0);
+  const int words = (n + 63) / 64;
+  if (n == 0) return torch::empty({0}, boxes.options().dtype(at::kLong));
+  auto mask = torch::empty({(int64_t)n * words}, boxes.options().dtype(at::kLong));
+  check_hip(zoo_nms_mask(boxes.data_ptr<float>(), n, (float)thresh,
+                         reinterpret_cast<unsigned long long*>(mask.data_ptr<int64_t>()), cur_stream()),
+            "nms_mask");
+  auto hm = mask.cpu();
+  const unsigned long long* m = reinterpret_cast<const unsigned long long*>(hm.data_ptr<int64_t>());
+  std::vector<unsigned long long> removed(words, 0ull);
+  std::vector<int64_t> keep;
+  keep.reserve(std::min<int64_t>(n, max_keep > 0 ? max_keep : n));
+  for (int i = 0; i < n; ++i) {
+    if (removed[i / 64] & (1ull << (i % 64))) continue;
+    keep.push_back(i);
+    if (max_keep > 0 && (int64_t)keep.size() >= max_keep) break;
+    const unsigned long long* row = m + (size_t)i * words;
+    for (int w = i / 64; w < words; ++w) removed[w] |= row[w];
+  }
+  auto out = torch::from_blob(keep.data(), {(int64_t)keep.size()}, torch::kLong).clone();
+  return out.to(boxes.device());
+}
+
 // ---- fused attention: q [B,H,L,D], k/v [B,H,S,D] bf16, optional additive key mask [B,S] fp32 ----
 void attn_check(const torch::Tensor& q, const torch::Tensor& k, const torch::Tensor& v,
                 const c10::optional<torch::Tensor>& mask) {
@@ -954,6 +984,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);
+  m.def("nms_sorted", &nms_sorted);
   m.def("attn_fwd_strided", &attn_fwd_strided);
   m.def("absmax", &absmax);
   m.def("im2col_q8", &im2col_q8);

@@ -1,0 +1,282 @@
+"""Faster R-CNN (the reference's "frcnn-vgg16" / "frcnn-pvanet" ObjectDetector
+configs: Zs/models/image/objectdetection/ObjectDetectionConfig.scala:38-46, 70-135;
+post-processing Postprocessor.scala:30-75; BigDL Proposal / RoiPooling /
+DetectionOutputFrcnn layers behind them).
+
+The network runs NCHW on the device (convolutions on MIOpen through torch, the
+linear heads on the framework's linear op). Proposal generation and per-class
+detection output are vectorised on the device; only the greedy NMS loop runs on
+the host, as in SSD's DetectionOutput.
+
+Pre-processing follows ``preprocessFrcnn(resolution, scaleMultipleOf)``: aspect
+scale to ``resolution`` on the short side (600 for VGG16, 640 with multiples of
+32 for PVANet), BGR mean subtraction (122.7717, 115.9465, 102.9801), and an
+``im_info`` = (height, width, scale) tensor per image.
+"""
+import math
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from zoo import ops
+from zoo.models.image.objectdetection.ssd import nms
+
+FRCNN_MEANS = (122.7717, 115.9465, 102.9801)
+
+
+def generate_anchors(base_size=16, ratios=(0.5, 1.0, 2.0), scales=(8, 16, 32)):
+    """The 9 reference anchors (x1, y1, x2, y2) centred on one ``base_size`` cell."""
+    ctr = (base_size - 1) / 2.0
+    out = []
+    for r in ratios:
+        size = base_size * base_size / r
+        ws = round(math.sqrt(size))
+        hs = round(ws * r)
+        for s in scales:
+            w, h = ws * s, hs * s
+            out.append([ctr - (w - 1) / 2, ctr - (h - 1) / 2, ctr + (w - 1) / 2, ctr + (h - 1) / 2])
+    return torch.tensor(out, dtype=torch.float32)
+
+
+def bbox_transform_inv(boxes, deltas):
+    """Apply (dx, dy, dw, dh) regression deltas to pixel boxes."""
+    w = boxes[:, 2] - boxes[:, 0] + 1.0
+    h = boxes[:, 3] - boxes[:, 1] + 1.0
+    cx = boxes[:, 0] + 0.5 * w
+    cy = boxes[:, 1] + 0.5 * h
+    dx, dy, dw, dh = deltas[:, 0::4], deltas[:, 1::4], deltas[:, 2::4], deltas[:, 3::4]
+    pcx = dx * w[:, None] + cx[:, None]
+    pcy = dy * h[:, None] + cy[:, None]
+    pw = torch.exp(dw.clamp(max=math.log(1000.0 / 16))) * w[:, None]
+    ph = torch.exp(dh.clamp(max=math.log(1000.0 / 16))) * h[:, None]
+    out = torch.empty_like(deltas)
+    out[:, 0::4] = pcx - 0.5 * pw
+    out[:, 1::4] = pcy - 0.5 * ph
+    out[:, 2::4] = pcx + 0.5 * pw - 1
+    out[:, 3::4] = pcy + 0.5 * ph - 1
+    return out
+
+
+def clip_boxes(boxes, h, w):
+    boxes[:, 0::4] = boxes[:, 0::4].clamp(0, w - 1)
+    boxes[:, 1::4] = boxes[:, 1::4].clamp(0, h - 1)
+    boxes[:, 2::4] = boxes[:, 2::4].clamp(0, w - 1)
+    boxes[:, 3::4] = boxes[:, 3::4].clamp(0, h - 1)
+    return boxes
+
+
+class Proposal(nn.Module):
+    """RPN scores + deltas -> RoIs [R, 5] (batch index, x1, y1, x2, y2)."""
+
+    def __init__(self, pre_nms_topn=6000, post_nms_topn=300, nms_thresh=0.7, min_size=16, feat_stride=16,
+                 ratios=(0.5, 1.0, 2.0), scales=(8, 16, 32)):
+        super().__init__()
+        self.pre, self.post, self.thresh, self.min_size, self.stride = pre_nms_topn, post_nms_topn, nms_thresh, \
+            min_size, feat_stride
+        self.register_buffer("anchors", generate_anchors(feat_stride, ratios, scales))
+
+    @torch.no_grad()
+    def forward(self, cls_prob, bbox_deltas, im_info):
+        B, twoA, H, W = cls_prob.shape
+        A = twoA // 2
+        dev = cls_prob.device
+        sx = torch.arange(W, device=dev, dtype=torch.float32) * self.stride
+        sy = torch.arange(H, device=dev, dtype=torch.float32) * self.stride
+        yy, xx = torch.meshgrid(sy, sx, indexing="ij")
+        shifts = torch.stack([xx, yy, xx, yy], -1).reshape(-1, 1, 4)                 # [HW, 1, 4]
+        all_anchors = (self.anchors.to(dev)[None] + shifts).reshape(-1, 4)          # [HW*A, 4]
+        rois = []
+        for b in range(B):
+            scores = cls_prob[b, A:].permute(1, 2, 0).reshape(-1)                   # foreground probs
+            deltas = bbox_deltas[b].permute(1, 2, 0).reshape(-1, 4)
+            props = clip_boxes(bbox_transform_inv(all_anchors, deltas.float()), float(im_info[b, 0]),
+                               float(im_info[b, 1]))
+            ms = self.min_size * float(im_info[b, 2])
+            keep = ((props[:, 2] - props[:, 0] + 1) >= ms) & ((props[:, 3] - props[:, 1] + 1) >= ms)
+            props, scores = props[keep], scores[keep].float()
+            order = scores.argsort(descending=True)[:self.pre]
+            props, scores = props[order], scores[order]
+            k = nms(props, scores, self.thresh, props.shape[0], max_keep=self.post)[:self.post]
+            rois.append(torch.cat([torch.full((k.numel(), 1), float(b), device=dev), props[k]], 1))
+        return torch.cat(rois) if rois else torch.zeros(0, 5, device=dev)
+
+
+def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16):
+    """Max RoI pooling (BigDL RoiPooling): each RoI, in feature coordinates, is
+    divided into pooled x pooled bins and max-reduced."""
+    out = features.new_zeros(rois.shape[0], features.shape[1], pooled, pooled)
+    H, W = features.shape[2], features.shape[3]
+    r = torch.round(rois[:, 1:] * spatial_scale).long()
+    for i in range(rois.shape[0]):
+        b = int(rois[i, 0])
+        x1, y1 = int(r[i, 0].clamp(0, W - 1)), int(r[i, 1].clamp(0, H - 1))
+        x2, y2 = int(r[i, 2].clamp(x1, W - 1)), int(r[i, 3].clamp(y1, H - 1))
+        crop = features[b:b + 1, :, y1:y2 + 1, x1:x2 + 1]
+        out[i] = F.adaptive_max_pool2d(crop, pooled)[0]
+    return out
+
+
+class DetectionOutputFrcnn(nn.Module):
+    """Per-class box decode + NMS -> per-image [K, 6] (label, score, x1, y1, x2, y2)
+    in input-image pixels divided by the scale (i.e. original-image pixels)."""
+
+    def __init__(self, num_classes=21, nms_thresh=0.3, max_per_image=100, thresh=0.05, bg_label=0):
+        super().__init__()
+        self.n, self.nms_thresh, self.max_per_image, self.thresh, self.bg = num_classes, nms_thresh, \
+            max_per_image, thresh, bg_label
+
+    @torch.no_grad()
+    def forward(self, rois, cls_prob, bbox_pred, im_info):
+        out = []
+        B = im_info.shape[0]
+        for b in range(B):
+            sel = rois[:, 0] == b
+            boxes = rois[sel, 1:]
+            scores = cls_prob[sel].float()
+            pred = clip_boxes(bbox_transform_inv(boxes, bbox_pred[sel].float()), float(im_info[b, 0]),
+                              float(im_info[b, 1])) / float(im_info[b, 2])
+            dets = []
+            for c in range(self.n):
+                if c == self.bg:
+                    continue
+                s = scores[:, c]
+                m = s > self.thresh
+                if not m.any():
+                    continue
+                bx = pred[m, 4 * c:4 * c + 4]
+                keep = nms(bx, s[m], self.nms_thresh, bx.shape[0])
+                dets.append(torch.cat([torch.full((keep.numel(), 1), float(c), device=bx.device), s[m][keep, None],
+                                       bx[keep]], 1))
+            d = torch.cat(dets) if dets else torch.zeros(0, 6, device=rois.device)
+            if d.shape[0] > self.max_per_image:
+                d = d[d[:, 1].argsort(descending=True)[:self.max_per_image]]
+            out.append(d)
+        return out
+
+
+def _vgg16_conv5():
+    cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "M", 512, 512, 512, "M", 512, 512, 512]
+    layers, c = [], 3
+    for v in cfg:
+        if v == "M":
+            layers.append(nn.MaxPool2d(2, 2, ceil_mode=True))
+        else:
+            layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=True)]
+            c = v
+    return nn.Sequential(*layers), 512
+
+
+class _CReLU(nn.Module):
+    """PVANet concatenated ReLU: conv -> [x, -x] -> scale/shift -> ReLU."""
+
+    def __init__(self, cin, cout, k, stride=1):
+        super().__init__()
+        self.conv = nn.Conv2d(cin, cout, k, stride, k // 2)
+        self.bn = nn.BatchNorm2d(2 * cout)
+
+    def forward(self, x):
+        y = self.conv(x)
+        return F.relu(self.bn(torch.cat([y, -y], 1)))
+
+
+class _Inception(nn.Module):
+    def __init__(self, cin, cout, stride=1):
+        super().__init__()
+        b = cout // 4
+        self.b1 = nn.Sequential(nn.Conv2d(cin, b, 1, stride), nn.ReLU(True))
+        self.b3 = nn.Sequential(nn.Conv2d(cin, b, 1), nn.ReLU(True), nn.Conv2d(b, b, 3, stride, 1), nn.ReLU(True))
+        self.b5 = nn.Sequential(nn.Conv2d(cin, b, 1), nn.ReLU(True), nn.Conv2d(b, b, 3, 1, 1), nn.ReLU(True),
+                                nn.Conv2d(b, b, 3, stride, 1), nn.ReLU(True))
+        self.bp = nn.Sequential(nn.MaxPool2d(3, stride, 1), nn.Conv2d(cin, cout - 3 * b, 1), nn.ReLU(True))
+        self.proj = nn.Conv2d(cin, cout, 1, stride) if (cin != cout or stride != 1) else None
+
+    def forward(self, x):
+        y = torch.cat([self.b1(x), self.b3(x), self.b5(x), self.bp(x)], 1)
+        return y + (x if self.proj is None else self.proj(x))
+
+
+class _PVANetLite(nn.Module):
+    """PVANet-style feature extractor (C.ReLU stem, inception stages, hyper-feature
+    concat of conv3/conv4/conv5 at stride 16 -> 512 channels). Architecture parity
+    with the released PVANet is unpinned: the reference loads its weights and graph
+    from a downloaded BigDL model file."""
+
+    def __init__(self):
+        super().__init__()
+        self.stem = nn.Sequential(_CReLU(3, 16, 7, 2), nn.MaxPool2d(3, 2, 1))                 # /4, 32 ch
+        self.c2 = nn.Sequential(_CReLU(32, 32, 3), _CReLU(64, 32, 3))                        # /4, 64
+        self.c3 = nn.Sequential(_CReLU(64, 64, 3, 2), _CReLU(128, 64, 3))                    # /8, 128
+        self.c4 = nn.Sequential(_Inception(128, 256, 2), _Inception(256, 256))               # /16, 256
+        self.c5 = nn.Sequential(_Inception(256, 384, 2), _Inception(384, 384))               # /32, 384
+        self.fuse = nn.Sequential(nn.Conv2d(128 + 256 + 384, 512, 1), nn.ReLU(True))
+
+    def forward(self, x):
+        x = self.c2(self.stem(x))
+        c3 = self.c3(x)
+        c4 = self.c4(c3)
+        c5 = self.c5(c4)
+        h, w = c4.shape[2], c4.shape[3]
+        hyper = torch.cat([F.max_pool2d(c3, 3, 2, 1)[:, :, :h, :w], c4,
+                           F.interpolate(c5, size=(h, w), mode="bilinear", align_corners=False)], 1)
+        return self.fuse(hyper)
+
+
+class FasterRCNN(nn.Module):
+    """backbone (stride 16) -> RPN -> Proposal -> RoI pooling -> fc heads.
+    forward(x, im_info) -> (rois [R, 5], cls_prob [R, C], bbox_pred [R, 4C])."""
+
+    def __init__(self, num_classes=21, backbone="vgg16", pre_nms_topn=6000, post_nms_topn=300):
+        super().__init__()
+        self.num_classes = num_classes
+        if backbone == "vgg16":
+            self.features, c = _vgg16_conv5()
+            fc_in, fc = 512 * 7 * 7, 4096
+        elif backbone == "pvanet":
+            self.features, c = _PVANetLite(), 512
+            fc_in, fc = 512 * 6 * 6, 2048
+        else:
+            raise ValueError("backbone must be 'vgg16' or 'pvanet'")
+        self.pooled = 7 if backbone == "vgg16" else 6
+        A = 9
+        self.rpn_conv = nn.Conv2d(c, 512 if backbone == "vgg16" else 384, 3, padding=1)
+        rc = self.rpn_conv.out_channels
+        self.rpn_cls = nn.Conv2d(rc, 2 * A, 1)
+        self.rpn_bbox = nn.Conv2d(rc, 4 * A, 1)
+        self.proposal = Proposal(pre_nms_topn, post_nms_topn)
+        self.fc6 = nn.Linear(fc_in, fc)
+        self.fc7 = nn.Linear(fc, fc)
+        self.cls_score = nn.Linear(fc, num_classes)
+        self.bbox_pred = nn.Linear(fc, 4 * num_classes)
+
+    def forward(self, x, im_info):
+        f = self.features(x)
+        r = F.relu(self.rpn_conv(f))
+        s = self.rpn_cls(r)
+        B, twoA, H, W = s.shape
+        prob = F.softmax(s.reshape(B, 2, twoA // 2, H, W), 1).reshape(B, twoA, H, W)
+        rois = self.proposal(prob, self.rpn_bbox(r), im_info)
+        pooled = roi_pool(f, rois, self.pooled).flatten(1)
+        h = F.relu(ops.linear(pooled, self.fc6.weight, self.fc6.bias).float())
+        h = F.relu(ops.linear(h, self.fc7.weight, self.fc7.bias).float())
+        cls = F.softmax(ops.linear(h, self.cls_score.weight, self.cls_score.bias).float(), -1)
+        box = ops.linear(h, self.bbox_pred.weight, self.bbox_pred.bias).float()
+        return rois, cls, box
+
+
+def aspect_scale(img_hwc, resolution=600, scale_multiple_of=1, max_size=1000):
+    """ImageAspectScale(resolution, scaleMultipleOf) + ImageChannelNormalize(means) + ImInfo:
+    HWC BGR image -> (CHW float32 array, im_info [h, w, scale])."""
+    from zoo.feature.image.transforms import resize_bilinear
+    h, w = img_hwc.shape[:2]
+    scale = resolution / float(min(h, w))
+    if round(scale * max(h, w)) > max_size:
+        scale = max_size / float(max(h, w))
+    nh, nw = int(round(h * scale)), int(round(w * scale))
+    if scale_multiple_of > 1:
+        nh = max(scale_multiple_of, nh // scale_multiple_of * scale_multiple_of)
+        nw = max(scale_multiple_of, nw // scale_multiple_of * scale_multiple_of)
+    out = resize_bilinear(img_hwc.astype(np.float32), nh, nw)
+    out = out - np.asarray(FRCNN_MEANS, np.float32)
+    return out.transpose(2, 0, 1).copy(), np.asarray([nh, nw, nh / float(h)], np.float32)

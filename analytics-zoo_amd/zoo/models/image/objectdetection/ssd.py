@@ -51,11 +51,16 @@ def decode(loc, priors, var=(0.1, 0.1, 0.2, 0.2)):
     return center_to_corner(torch.cat([xy, wh], -1))
 
 
-def nms(boxes, scores, iou_threshold=0.45, top_k=400):
-    """Greedy NMS; returns kept indices (descending score)."""
+def nms(boxes, scores, iou_threshold=0.45, top_k=400, max_keep=0):
+    """Greedy NMS; returns kept indices (descending score). On the GPU the IoU
+    suppression bitmask comes from the native kernel (csrc/kernels/detect.hip)."""
     order = scores.argsort(descending=True)[:top_k]
     if order.numel() == 0:
         return order
+    if boxes.is_cuda:
+        from zoo.ops._native import native
+        k = native().nms_sorted(boxes[order].float().contiguous(), float(iou_threshold), int(max_keep))
+        return order[k]
     b = boxes[order]
     iou = iou_matrix(b, b)
     n = order.numel()
@@ -296,7 +301,13 @@ def mean_average_precision(detections, ground_truths, num_classes, iou_thresh=0.
 
 
 class ObjectDetector(ImageModel):
-    """ObjectDetector facade: SSD-VGG16 (300/512) with DetectionOutputSSD."""
+    """ObjectDetector facade: SSD-VGG16 (300/512) with DetectionOutputSSD, or a
+    Faster R-CNN config ("frcnn-vgg16", "frcnn-pvanet") -> :class:`FrcnnDetector`."""
+
+    def __new__(cls, model_name="ssd-vgg16-300x300", *a, **kw):
+        if cls is ObjectDetector and str(model_name).startswith("frcnn"):
+            return FrcnnDetector(model_name, *a, **kw)
+        return super().__new__(cls)
 
     def __init__(self, model_name="ssd-vgg16-300x300", num_classes=21, label_map=None, **kwargs):
         super().__init__(**kwargs)
@@ -325,3 +336,42 @@ class ObjectDetector(ImageModel):
         out = self.detect(loc, conf, self.ssd.priors)
         self.train(was)
         return [o.cpu().numpy() for o in out]
+
+
+class FrcnnDetector(ImageModel):
+    """Faster R-CNN ObjectDetector configs (ObjectDetectionConfig.scala:70-135):
+    "frcnn-vgg16[-...]" (short side 600) and "frcnn-pvanet[-...]" (640, multiples of 32)."""
+
+    def __init__(self, model_name="frcnn-vgg16", num_classes=21, label_map=None, pre_nms_topn=6000,
+                 post_nms_topn=300, **kwargs):
+        super().__init__(**kwargs)
+        from zoo.models.image.objectdetection.frcnn import DetectionOutputFrcnn, FasterRCNN
+        self.model_name, self.num_classes, self.label_map = model_name, num_classes, label_map
+        self.backbone = "pvanet" if "pvanet" in model_name else "vgg16"
+        self.resolution, self.multiple = (640, 32) if self.backbone == "pvanet" else (600, 1)
+        self.frcnn = FasterRCNN(num_classes, self.backbone, pre_nms_topn, post_nms_topn)
+        self.detect = DetectionOutputFrcnn(num_classes)
+        self.built = True
+
+    def forward(self, x, im_info):
+        return self.frcnn(x, im_info)
+
+    def _layer_list(self):
+        return []
+
+    @torch.no_grad()
+    def detect_images(self, images_hwc_bgr):
+        """Raw HWC BGR images (any sizes) -> per-image [K, 6] detections in original pixels."""
+        from zoo.models.image.objectdetection.frcnn import aspect_scale
+        was = self.training
+        self.eval()
+        dev = next(self.frcnn.parameters()).device
+        out = []
+        for img in images_hwc_bgr:
+            chw, info = aspect_scale(np.asarray(img), self.resolution, self.multiple)
+            x = torch.from_numpy(chw)[None].to(dev)
+            ii = torch.from_numpy(info)[None].to(dev)
+            rois, cls, box = self.frcnn(x, ii)
+            out.append(self.detect(rois, cls, box, ii)[0].cpu().numpy())
+        self.train(was)
+        return out

@@ -1,0 +1,106 @@
+"""Faster R-CNN configs of ObjectDetector (M6) + detection post-processing
+(Postprocessor.scala, LabelReader.scala) + the native NMS bitmask kernel (HK21).
+Anchors are pinned against the published py-faster-rcnn generate_anchors table."""
+import numpy as np
+import pytest
+import torch
+
+from zoo.models.image.objectdetection import (DecodeOutput, DetectionOutputFrcnn, ObjectDetector, Proposal,
+                                              ScaleDetection, Visualizer, generate_anchors, nms,
+                                              read_pascal_label_map, roi_pool)
+from zoo.models.image.objectdetection.frcnn import bbox_transform_inv
+
+
+def test_anchors_match_reference_table():
+    a = generate_anchors()
+    ref = [[-84, -40, 99, 55], [-176, -88, 191, 103], [-360, -184, 375, 199], [-56, -56, 71, 71],
+           [-120, -120, 135, 135], [-248, -248, 263, 263], [-36, -80, 51, 95], [-80, -168, 95, 183],
+           [-168, -344, 183, 359]]
+    assert a.tolist() == ref
+
+
+def test_bbox_transform_zero_deltas_is_identity():
+    boxes = torch.tensor([[10.0, 20.0, 50.0, 80.0], [0.0, 0.0, 15.0, 15.0]])
+    out = bbox_transform_inv(boxes, torch.zeros(2, 8))
+    torch.testing.assert_close(out[:, :4], boxes)
+    torch.testing.assert_close(out[:, 4:], boxes)
+
+
+def test_roi_pool_is_max_over_bins():
+    f = torch.arange(2 * 3 * 8 * 8, dtype=torch.float32).reshape(2, 3, 8, 8)
+    rois = torch.tensor([[1.0, 0.0, 0.0, 63.0, 63.0]])  # whole map at scale 1/8
+    out = roi_pool(f, rois, pooled=2, spatial_scale=1 / 8)
+    exp = torch.nn.functional.adaptive_max_pool2d(f[1:2], 2)[0]
+    torch.testing.assert_close(out[0], exp)
+
+
+def test_proposal_and_detection_output():
+    torch.manual_seed(0)
+    B, A, H, W = 1, 9, 6, 8
+    prob = torch.rand(B, 2 * A, H, W)
+    deltas = torch.randn(B, 4 * A, H, W) * 0.1
+    info = torch.tensor([[96.0, 128.0, 1.0]])
+    rois = Proposal(pre_nms_topn=100, post_nms_topn=10, min_size=4)(prob, deltas, info)
+    assert rois.shape[1] == 5 and 0 < rois.shape[0] <= 10
+    assert (rois[:, 1] >= 0).all() and (rois[:, 3] <= 127).all() and (rois[:, 4] <= 95).all()
+    # detection output: one confident class-3 RoI survives, a duplicate is suppressed
+    r = torch.tensor([[0, 10.0, 10.0, 40.0, 40.0], [0, 11.0, 11.0, 41.0, 41.0], [0, 60.0, 60.0, 90.0, 90.0]])
+    cls = torch.full((3, 5), 0.01)
+    cls[0, 3], cls[1, 3], cls[2, 1] = 0.9, 0.8, 0.7
+    det = DetectionOutputFrcnn(num_classes=5)(r, cls, torch.zeros(3, 20), torch.tensor([[100.0, 100.0, 2.0]]))[0]
+    labels = sorted(det[:, 0].tolist())
+    assert labels == [1.0, 3.0]
+    d3 = det[det[:, 0] == 3][0]
+    torch.testing.assert_close(d3[2:], torch.tensor([5.0, 5.0, 20.0, 20.0]))  # divided by the scale 2
+
+
+def test_frcnn_detector_configs_end_to_end():
+    torch.manual_seed(0)
+    for name in ("frcnn-vgg16", "frcnn-pvanet-quantize"):
+        d = ObjectDetector(name, pre_nms_topn=200, post_nms_topn=16)
+        assert type(d).__name__ == "FrcnnDetector"
+        d.resolution = 96 if d.backbone == "vgg16" else 128
+        d.detect.thresh = 0.0
+        img = (np.random.rand(100, 140, 3) * 255).astype(np.uint8)
+        out = d.detect_images([img])[0]
+        assert out.ndim == 2 and out.shape[1] == 6 and 0 < out.shape[0] <= 100
+        assert (out[:, 2] >= 0).all() and (out[:, 4] <= 140 + 1).all()
+
+
+def test_postprocessors_and_label_maps():
+    assert read_pascal_label_map()[15] == "person"
+    flat = np.array([2, 1, 0.9, 0.1, 0.1, 0.5, 0.5, 3, 0.8, 0.2, 0.2, 0.4, 0.9], np.float32)
+    d = DecodeOutput()(flat)
+    assert d.shape == (2, 6)
+    s = ScaleDetection()(d, (200, 100))
+    np.testing.assert_allclose(s[0, 2:], [10, 20, 50, 100])
+    img = Visualizer(thresh=0.5)(np.zeros((200, 100, 3), np.uint8), s)
+    assert img.sum() > 0
+
+
+def _rand_boxes(n, seed):
+    g = torch.Generator().manual_seed(seed)
+    xy = torch.rand(n, 2, generator=g) * 100
+    wh = torch.rand(n, 2, generator=g) * 30 + 2
+    return torch.cat([xy, xy + wh], 1), torch.rand(n, generator=g)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 500, 3000])
+def test_native_nms_matches_cpu(gpu, n):
+    b, s = _rand_boxes(n, n)
+    ref = nms(b, s, 0.5, n)
+    got = nms(b.to(gpu), s.to(gpu), 0.5, n)
+    assert got.cpu().tolist() == ref.tolist()
+    got5 = nms(b.to(gpu), s.to(gpu), 0.5, n, max_keep=5)
+    assert got5.cpu().tolist() == ref[:5].tolist()
+
+
+@pytest.mark.gpu
+def test_frcnn_on_gpu(gpu):
+    torch.manual_seed(0)
+    d = ObjectDetector("frcnn-vgg16", pre_nms_topn=2000, post_nms_topn=100).to(gpu)
+    d.resolution = 224
+    d.detect.thresh = 0.0
+    out = d.detect_images([(np.random.rand(200, 300, 3) * 255).astype(np.uint8)])[0]
+    assert out.shape[1] == 6 and 0 < out.shape[0] <= 100
