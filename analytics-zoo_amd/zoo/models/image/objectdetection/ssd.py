@@ -172,6 +172,50 @@ class SSD(nn.Module):
         return loc, conf
 
 
+class SSDMobileNet(nn.Module):
+    """SSD-MobileNet-300 ("ssd-mobilenet-300x300", ObjectDetectionConfig.scala:64-69): MobileNet v1
+    taps at conv11 (19x19, 512) and conv13 (10x10, 1024) plus four extra 1x1/3x3-s2
+    stages. forward -> (loc [B, P, 4], conf [B, P, C])."""
+
+    CONFIG = dict(resolution=300, feature_maps=(19, 10, 5, 3, 2, 1), steps=(16, 32, 64, 100, 150, 300),
+                  min_sizes=(60, 105, 150, 195, 240, 285), max_sizes=(105, 150, 195, 240, 285, 300),
+                  aspect_ratios=((2,), (2, 3), (2, 3), (2, 3), (2, 3), (2, 3)))
+
+    def __init__(self, num_classes=21):
+        super().__init__()
+        from zoo.models.image.imageclassification.nets import MobileNet
+        self.cfg = SSDConfig(**self.CONFIG)
+        self.num_classes = num_classes
+        self.base = MobileNet(1000).features          # classifier head dropped
+        self.tap = 22                                 # conv11 pointwise output (stride 16)
+
+        def extra(cin, mid, cout):
+            return nn.Sequential(nn.Conv2d(cin, mid, 1), nn.ReLU(True), nn.Conv2d(mid, cout, 3, 2, 1), nn.ReLU(True))
+        self.extras = nn.ModuleList([extra(1024, 256, 512), extra(512, 128, 256), extra(256, 128, 256),
+                                     extra(256, 64, 128)])
+        chans = [512, 1024, 512, 256, 256, 128]
+        nb = self.cfg.boxes_per_location()
+        self.loc = nn.ModuleList([nn.Conv2d(c, n * 4, 3, padding=1) for c, n in zip(chans, nb)])
+        self.conf = nn.ModuleList([nn.Conv2d(c, n * num_classes, 3, padding=1) for c, n in zip(chans, nb)])
+        self.register_buffer("priors", prior_boxes(self.cfg))
+
+    def forward(self, x):
+        feats = []
+        for i, l in enumerate(self.base):
+            x = l(x)
+            if i == self.tap:
+                feats.append(x)
+        feats.append(x)
+        for e in self.extras:
+            x = e(x)
+            feats.append(x)
+        B = x.shape[0]
+        loc = torch.cat([l(f).permute(0, 2, 3, 1).reshape(B, -1, 4) for l, f in zip(self.loc, feats)], 1)
+        conf = torch.cat([c(f).permute(0, 2, 3, 1).reshape(B, -1, self.num_classes) for c, f in zip(self.conf, feats)],
+                         1)
+        return loc, conf
+
+
 class DetectionOutputSSD(nn.Module):
     """Decode + per-class threshold + NMS + keep_top_k -> list of [K, 6] (label, score, x1, y1, x2, y2)."""
 
@@ -316,7 +360,7 @@ class ObjectDetector(ImageModel):
             512, (64, 32, 16, 8, 4, 2, 1)[:6], (8, 16, 32, 64, 128, 256), (35.84, 76.8, 153.6, 230.4, 307.2, 384.0),
             (76.8, 153.6, 230.4, 307.2, 384.0, 460.8))
         self.model_name, self.num_classes, self.label_map = model_name, num_classes, label_map
-        self.ssd = SSD(num_classes, cfg)
+        self.ssd = SSDMobileNet(num_classes) if "mobilenet" in model_name else SSD(num_classes, cfg)
         self.detect = DetectionOutputSSD(num_classes)
         self.criterion = MultiBoxLoss(num_classes)
         self.built = True

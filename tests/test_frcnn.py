@@ -104,3 +104,15 @@ def test_frcnn_on_gpu(gpu):
     d.detect.thresh = 0.0
     out = d.detect_images([(np.random.rand(200, 300, 3) * 255).astype(np.uint8)])[0]
     assert out.shape[1] == 6 and 0 < out.shape[0] <= 100
+
+
+def test_ssd_mobilenet_config_shapes():
+    from zoo.models.image.objectdetection import SSDMobileNet
+    d = ObjectDetector("ssd-mobilenet-300x300")
+    assert isinstance(d.ssd, SSDMobileNet)
+    loc, conf = d.ssd(torch.randn(1, 3, 300, 300))
+    P = d.ssd.priors.shape[0]
+    assert loc.shape == (1, P, 4) and conf.shape == (1, P, 21)
+    assert P == 19 * 19 * 4 + (100 + 25 + 9 + 4 + 1) * 6
+    dets = d.detect_batch(np.random.rand(1, 3, 300, 300).astype(np.float32))
+    assert dets[0].shape[1] == 6
