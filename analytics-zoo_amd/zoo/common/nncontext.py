@@ -35,6 +35,7 @@ class ZooConfig:
     # message is still large enough for full xGMI ring bandwidth
     bucket_mb: float = 16.0
     overlap_comm: bool = True
+    grad_compression: str = ""          # ZOO_GRAD_COMPRESSION=bf16: 16-bit gradient transfer
     sharded_optimizer: bool = False
     hip_graph: bool = False
     # failure handling (bigdl.failure.retryTimes / retryTimeInterval, Topology.scala:1181-1182)
@@ -56,6 +57,7 @@ class ZooConfig:
     _ENV = {
         "dtype": "ZOO_DTYPE", "bucket_mb": "ZOO_BUCKET_MB", "overlap_comm": "ZOO_OVERLAP_COMM",
         "sharded_optimizer": "ZOO_SHARDED_OPTIM", "hip_graph": "ZOO_HIP_GRAPH",
+        "grad_compression": "ZOO_GRAD_COMPRESSION",
         "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
         "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
         "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",

@@ -30,7 +30,7 @@ from zoo.parallel.flat import FlatParams
 
 
 class _Bucket:
-    __slots__ = ("lo", "hi", "params", "pending", "work", "launched")
+    __slots__ = ("lo", "hi", "params", "pending", "work", "launched", "packed")
 
     def __init__(self, lo, hi):
         self.lo, self.hi = lo, hi
@@ -38,11 +38,17 @@ class _Bucket:
         self.pending = 0
         self.work = None
         self.launched = False
+        self.packed = None
 
 
 class GradSync:
-    def __init__(self, flat: FlatParams, group=None, bucket_mb=16.0, mode="allreduce", overlap=True):
+    def __init__(self, flat: FlatParams, group=None, bucket_mb=16.0, mode="allreduce", overlap=True,
+                 compress=None):
+        """``compress="bf16"``: gradients travel as bf16 (half the xGMI bytes, the
+        16-bit transfer of BigDL's AllReduceParameter) and are
+        unpacked back into the fp32 flat buffer after the reduction."""
         self.flat = flat
+        self.compress = compress if compress in ("bf16",) else None
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if self.world > 1 else 0
@@ -114,9 +120,15 @@ class GradSync:
             ev.record(torch.cuda.current_stream(g.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
-                b.work = dist.all_reduce(g, group=self.group, async_op=True)
+                t = g
+                if self.compress:
+                    t = b.packed = g.to(torch.bfloat16)
+                b.work = dist.all_reduce(t, group=self.group, async_op=True)
         else:
-            b.work = dist.all_reduce(g, group=self.group, async_op=True)
+            t = g
+            if self.compress:
+                t = b.packed = g.to(torch.bfloat16)
+            b.work = dist.all_reduce(t, group=self.group, async_op=True)
 
     # ------------------------------------------------------------------
     def broadcast_parameters(self, src=0):
@@ -137,6 +149,13 @@ class GradSync:
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
+                if b.packed is not None:  # unpack the bf16 sum into the fp32 flat gradient
+                    if self.comm_stream is not None:
+                        with torch.cuda.stream(self.comm_stream):
+                            self.flat.grad[b.lo:b.hi].copy_(b.packed)
+                    else:
+                        self.flat.grad[b.lo:b.hi].copy_(b.packed)
+                    b.packed = None
         if self.comm_stream is not None:
             torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.comm_stream)
 

@@ -115,7 +115,7 @@ class TrainingEngine:
                                bf16_copy=self.device.type == "cuda")
         self.sync = GradSync(self.flat, bucket_mb=bucket_mb or cfg.bucket_mb,
                              mode="sharded" if (cfg.sharded_optimizer if sharded is None else sharded)
-                             else "allreduce", overlap=cfg.overlap_comm)
+                             else "allreduce", overlap=cfg.overlap_comm, compress=cfg.grad_compression or None)
         self.sync.broadcast_parameters(0)
         self.clip = clip
         self.forward_fn = model_forward or (lambda m, x: m(x))

@@ -204,6 +204,49 @@ def _free_port():
     return p
 
 
+def _dp_worker_compressed(rank, world, port, out_q):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "ZOO_GRAD_COMPRESSION": "bf16"})
+    import zoo.common.nncontext as nc
+    nc._CTX = None
+    ctx = nc.init_nncontext(backend="gloo")
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(64)
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9), ctx=ctx,
+                         bucket_mb=0.0001)
+    assert eng.sync.compress == "bf16"
+    for step in range(3):
+        sl = slice(rank * 8 + step * 16, rank * 8 + step * 16 + 8)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    out_q.put((rank, eng.flat.master.detach().cpu().numpy().copy()))
+    ctx.stop()
+
+
+def test_data_parallel_bf16_gradient_compression():
+    """16-bit gradient transfer (HK24): ranks stay identical and track the fp32 run closely."""
+    ctx_mp = mp.get_context("spawn")
+    q = ctx_mp.Queue()
+    port = _free_port()
+    procs = [ctx_mp.Process(target=_dp_worker_compressed, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = {r: torch.from_numpy(v) for r, v in (q.get(timeout=240) for _ in range(2))}
+    for p in procs:
+        p.join(timeout=60)
+    assert torch.equal(res[0], res[1])
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(64)
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9))
+    for step in range(3):
+        sl = slice(step * 16, step * 16 + 16)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    assert (res[0] - eng.flat.master).abs().max() < 2e-2 * eng.flat.master.abs().max()
+
+
 def _dp_worker(rank, world, port, mode, out_q):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
