@@ -181,6 +181,35 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restri
   }
 }
 
+// NCHW fp32 images -> zero-padded space-to-depth(2) NHWC bf16: Y[n][i][j][(dy*2+dx)*Cp + c] =
+// X[n][c][2i+dy-pad][2j+dx-pad]. A 7x7 stride-2 stem conv on X equals a 4x4 stride-1 conv
+// on Y (16 channels instead of 4 -> the 16-byte-vector implicit-GEMM path). One thread
+// writes the 8 channels of one (pixel, dy): 16 bytes.
+__global__ __launch_bounds__(256) void nchw_to_s2d_kernel(const float* __restrict__ X, bf16_t* __restrict__ Y,
+                                                          int N, int C, int H, int W, int Cp, int pad, int Hs,
+                                                          int Ws) {
+  const size_t total = (size_t)N * Hs * Ws * 2;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int dy = (int)(i & 1);
+    size_t t = i >> 1;
+    const int j = (int)(t % Ws); t /= Ws;
+    const int ii = (int)(t % Hs);
+    const int n = (int)(t / Hs);
+    const int h = 2 * ii + dy - pad;
+    float v[8];
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int w = 2 * j + dx - pad;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        v[dx * 4 + c] = (ok && c < C) ? X[(((size_t)n * C + c) * H + h) * W + w] : 0.f;
+    }
+    // Cp == 4: the 8 values of (dy, dx=0..1, c=0..3) are contiguous in the output pixel
+    *reinterpret_cast<uint4*>(Y + ((((size_t)n * Hs + ii) * Ws + j) * 4 * Cp) + dy * 2 * Cp) = pack8(v);
+  }
+}
+
 __global__ __launch_bounds__(256) void bf16_to_f32_accum_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
                                                                  size_t n, int accumulate) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -266,6 +295,13 @@ extern "C" hipError_t zoo_clip(float* g, size_t n, float lo, float hi, const flo
 extern "C" hipError_t zoo_nchw_to_nhwc(const float* X, void* Y, int N, int C, int H, int W, int Cp, hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_nhwc_kernel, dim3(egrid((size_t)N * H * W * Cp)), dim3(256), 0, st, X, (bf16_t*)Y, N, C,
                      H, W, Cp);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_nchw_to_s2d(const float* X, void* Y, int N, int C, int H, int W, int pad, int Hs, int Ws,
+                                       hipStream_t st) {
+  hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(egrid((size_t)N * Hs * Ws * 2)), dim3(256), 0, st, X, (bf16_t*)Y, N, C,
+                     H, W, 4, pad, Hs, Ws);
   return hipGetLastError();
 }
 

@@ -48,6 +48,7 @@ hipError_t zoo_adaptive(float*, const float*, float*, float*, void*, size_t, int
 hipError_t zoo_sumsq(const float*, size_t, float*, hipStream_t);
 hipError_t zoo_clip(float*, size_t, float, float, const float*, float, hipStream_t);
 hipError_t zoo_nchw_to_nhwc(const float*, void*, int, int, int, int, int, hipStream_t);
+hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
@@ -488,6 +489,19 @@ void clip(torch::Tensor g, double lo, double hi, c10::optional<torch::Tensor> no
   req(g, at::kFloat, "g");
   check_hip(zoo_clip(g.data_ptr<float>(), g.numel(), lo, hi, opt_ptr<float>(norm_sq), max_norm, cur_stream()),
             "clip");
+}
+
+// [N, C<=4, H, W] fp32 -> [N, Hs, Ws, 16] bf16 space-to-depth(2) of the input zero-padded by `pad`
+torch::Tensor nchw_to_s2d(torch::Tensor x, int pad) {
+  req(x, at::kFloat, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(1) <= 4, "nchw_to_s2d: [N, C<=4, H, W] input");
+  const int N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int Hs = (H + 2 * pad + 1) / 2, Ws = (W + 2 * pad + 1) / 2;
+  auto y = torch::empty({N, Hs, Ws, 16}, x.options().dtype(at::kBFloat16));
+  if (y.numel() == 0) return y;
+  check_hip(zoo_nchw_to_s2d(x.data_ptr<float>(), y.data_ptr(), N, C, H, W, pad, Hs, Ws, cur_stream()),
+            "nchw_to_s2d");
+  return y;
 }
 
 torch::Tensor nchw_to_nhwc(torch::Tensor x, int cpad) {
@@ -985,6 +999,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("attn_fwd", &attn_fwd);
   m.def("nms_sorted", &nms_sorted);
+  m.def("nchw_to_s2d", &nchw_to_s2d);
   m.def("attn_fwd_strided", &attn_fwd_strided);
   m.def("absmax", &absmax);
   m.def("im2col_q8", &im2col_q8);

@@ -11,6 +11,8 @@ layout the MFMA kernels read directly.
 """
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -45,6 +47,8 @@ class ConvBN(nn.Module):
 
 # cross-unit BN-backward fusion (BNProducer); the switch exists for A/B numerics tests
 FUSE_BN_BACKWARD = True
+# 7x7/2 stem computed as a 4x4/1 conv on a space-to-depth(2) input (GPU)
+S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
 
 
 def _bp():
@@ -167,9 +171,31 @@ class ResNet(nn.Module):
             x = torch.nn.functional.pad(x, (0, pad))
         return x.contiguous()
 
+    def _stem_s2d_ok(self, x):
+        return x.is_cuda and x.dim() == 4 and x.shape[1] == self.in_channels and self.cin_pad == 4 and \
+            self.stem.k == 7 and self.stem.stride == 2 and self.stem.pad == 3 and S2D_STEM
+
+    def _s2d_weight(self):
+        """7x7x4 stem weight -> the equivalent 4x4x16 space-to-depth weight (differentiable:
+        the gradient flows back to the 7x7 parameter). Tap (r, s) = (2R+dy, 2S+dx); r = s = 7
+        are the zero pad row/column."""
+        K = self.stem.cout
+        w7 = self.stem.weight[:, :7 * 7 * 4].reshape(K, 7, 7, 4)
+        w8 = torch.nn.functional.pad(w7, (0, 0, 0, 1, 0, 1))                 # [K, 8, 8, 4]
+        return w8.reshape(K, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(K, 256).contiguous()
+
     def forward(self, x):
-        x = self.to_nhwc(x)
-        x = self.stem(x)
+        if self._stem_s2d_ok(x):
+            # stem as a 4x4 stride-1 conv on the space-to-depth(2) image: 16 input channels
+            # take the vector implicit-GEMM path; the NCHW->NHWC pass becomes the s2d pass
+            xs = ops.native().nchw_to_s2d(x.float().contiguous(), 3)
+            st = self.stem
+            x = ops.conv_bn_act(xs, self._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
+                                kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
+                                relu=True, training=st.training)
+        else:
+            x = self.to_nhwc(x)
+            x = self.stem(x)
         x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
         if self.training and _fusing(x):
             prod = None

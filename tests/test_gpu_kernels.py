@@ -300,6 +300,40 @@ def test_resnet_bn_backward_fusion_matches_unfused(gpu, block):
     assert F.cosine_similarity(u[0], f[0], dim=0).item() > 0.98
 
 
+def test_resnet_s2d_stem_matches_7x7_stem(gpu):
+    """The space-to-depth stem (4x4/1 conv on the s2d image) must equal the 7x7/2
+    conv+BN+ReLU stem: output, input-free weight gradient and BN parameter grads."""
+    import zoo.models.image.resnet as R
+    from zoo import ops
+    torch.manual_seed(0)
+    m = R.resnet50(num_classes=10).to(gpu).train()
+    x = torch.randn(4, 3, 64, 64, device=gpu)
+    st = m.stem
+    outs = []
+    for s2d in (False, True):
+        st.zero_grad(set_to_none=True)
+        if s2d:
+            xs = ops.native().nchw_to_s2d(x, 3)
+            assert tuple(xs.shape) == (4, 35, 35, 16)
+            z = ops.conv_bn_act(xs, m._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
+                                kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
+                                relu=True, training=True)
+        else:
+            z = st(m.to_nhwc(x))
+        g = torch.randn(z.shape, generator=torch.Generator().manual_seed(5)).to(gpu, z.dtype)
+        z.backward(g)
+        outs.append((z.detach().float(), st.weight.grad.detach().clone(), st.gamma.grad.clone(),
+                     st.beta.grad.clone()))
+    (z0, w0, g0, b0), (z1, w1, g1, b1) = outs
+    assert z0.shape == z1.shape == (4, 32, 32, 64)
+    assert (z0 - z1).abs().max().item() <= 3e-2 * z0.abs().max().item()
+    for a, b in ((w0, w1), (g0, g1), (b0, b1)):
+        assert F.cosine_similarity(a.flatten(), b.flatten(), dim=0).item() > 0.999
+        assert (a - b).norm().item() <= 2e-2 * a.norm().item()
+    # the pad taps (r = 7 or s = 7) of the s2d weight must receive no gradient path
+    assert torch.count_nonzero(w1[:, 196:]).item() == 0
+
+
 def test_resnet_step_memory_is_stable_without_gc(gpu):
     """No reference cycle may hold a step's activations: with the cyclic GC off,
     allocated memory stays flat from step 3 to step 6 (one step's activations
