@@ -81,11 +81,142 @@ class TFDataset:
                          batch_per_thread)
 
     @staticmethod
-    def from_tf_data_dataset(*a, **k):
-        raise NotImplementedError("tf.data needs TensorFlow; build the pipeline with FeatureSet / DataLoader")
+    def from_tf_data_dataset(dataset, batch_size=-1, batch_per_thread=-1, hard_code_batch_size=False,
+                             validation_dataset=None, sequential_order=False, shuffle=True):
+        """Py/tfpark/tf_dataset.py:TFDataDataset (T4 TFDataFeatureSet). Without TensorFlow the
+        dataset is any iterable of UNBATCHED elements -- ``x`` or ``(x, y)`` numpy-convertible
+        (a ``tf.data.Dataset`` exposing ``as_numpy_iterator`` works as is); it is materialised
+        once into host arrays and served by the native FeatureSet gather."""
+        bs = TFDataset._bs(batch_size, batch_per_thread)
+        train = _iterable_featureset(dataset, bs, shuffle and not sequential_order and batch_size > 0)
+        val = _iterable_featureset(validation_dataset, bs, False) if validation_dataset is not None else None
+        return TFDataset(train, val, batch_size, batch_per_thread)
 
     @staticmethod
-    def from_tfrecord_file(*a, **k):
-        raise NotImplementedError("TFRecord decoding of tf.Example needs TensorFlow protos; use FeatureSet")
+    def from_tfrecord_file(file_path, batch_size=-1, batch_per_thread=-1, hard_code_batch_size=False,
+                           validation_file_path=None, parse_fn=None, feature_keys=None, label_key=None):
+        """Py/tfpark/tf_dataset.py:TFRecordDataset. Records are read with the native TFRecord
+        framing and decoded as ``tf.train.Example`` protos (:func:`parse_example`). ``parse_fn``
+        maps the decoded ``{name: ndarray}`` dict to ``x`` or ``(x, y)`` (the reference maps
+        the serialized string with TF ops instead); by default the ``feature_keys`` features
+        are concatenated into x and ``label_key`` is y."""
+        bs = TFDataset._bs(batch_size, batch_per_thread)
+
+        def elements(path):
+            paths = path if isinstance(path, (list, tuple)) else [path]
+            for pth in paths:
+                for rec in read_tfrecord(pth):
+                    ex = parse_example(rec)
+                    if parse_fn is not None:
+                        yield parse_fn(ex)
+                        continue
+                    keys = feature_keys or sorted(k for k in ex if k != label_key)
+                    x = np.concatenate([np.asarray(ex[k], np.float32).reshape(-1) for k in keys])
+                    yield (x, ex[label_key]) if label_key is not None else x
+        train = _iterable_featureset(elements(file_path), bs, batch_size > 0)
+        val = _iterable_featureset(elements(validation_file_path), bs, False) \
+            if validation_file_path is not None else None
+        return TFDataset(train, val, batch_size, batch_per_thread)
 
     from_rdd = from_feature_set
+
+
+def _iterable_featureset(dataset, batch_size, shuffle):
+    it = dataset.as_numpy_iterator() if hasattr(dataset, "as_numpy_iterator") else iter(dataset)
+    xs, ys = [], []
+    for el in it:
+        if isinstance(el, dict):
+            raise TypeError("dict elements: map them to x or (x, y) first")
+        if isinstance(el, (tuple, list)) and len(el) == 2:
+            xs.append(np.asarray(el[0]))
+            ys.append(np.asarray(el[1]))
+        else:
+            xs.append(np.asarray(el))
+    if not xs:
+        raise ValueError("the dataset is empty")
+    x = np.stack(xs)
+    y = None
+    if ys:
+        y = np.stack(ys)
+        if y.ndim == 2 and y.shape[1] == 1:
+            y = y[:, 0]
+    return FeatureSet.from_ndarrays(x, y, batch_size, shuffle=shuffle)
+
+
+# ---- tf.train.Example (example.proto / feature.proto) codec, no TensorFlow needed ----
+def _packed(v, wt, kind):
+    if wt != 2:  # unpacked scalar element
+        if kind == "f":
+            return [np.frombuffer(int(v).to_bytes(4, "little"), np.float32)[0]]
+        return [v - (1 << 64) if v >= 1 << 63 else v]
+    if kind == "f":
+        return list(np.frombuffer(v, np.float32))
+    from zoo.utils.protobuf import _varint
+    out, i = [], 0
+    while i < len(v):
+        x, i = _varint(v, i)
+        out.append(x - (1 << 64) if x >= 1 << 63 else x)
+    return out
+
+
+def parse_example(record):
+    """Serialized ``tf.train.Example`` -> {name: ndarray} (bytes_list -> object array of
+    bytes, float_list -> float32, int64_list -> int64)."""
+    from zoo.utils.protobuf import fields
+    out = {}
+    for f, _, feats in fields(record):
+        if f != 1:
+            continue
+        for ff, _, entry in fields(feats):
+            if ff != 1:
+                continue
+            key, feat = "", b""
+            for ef, _, ev in fields(entry):
+                if ef == 1:
+                    key = ev.decode("utf-8")
+                elif ef == 2:
+                    feat = ev
+            arr = np.zeros((0,), np.float32)
+            for kind, _, lst in fields(feat):
+                vals = [(wt, v) for vf, wt, v in fields(lst) if vf == 1]
+                if kind == 1:
+                    arr = np.array([v for _, v in vals], dtype=object)
+                elif kind == 2:
+                    arr = np.array([x for wt, v in vals for x in _packed(v, wt, "f")], np.float32)
+                elif kind == 3:
+                    arr = np.array([x for wt, v in vals for x in _packed(v, wt, "i")], np.int64)
+            out[key] = arr
+    return out
+
+
+def encode_example(features):
+    """{name: bytes | str | float/int array} -> serialized ``tf.train.Example``."""
+    from zoo.tensorboard import _field, _varint
+    entries = b""
+    for key in sorted(features):
+        v = features[key]
+        if isinstance(v, (bytes, str)) or (isinstance(v, (list, tuple)) and v and isinstance(v[0], (bytes, str))):
+            items = [v] if isinstance(v, (bytes, str)) else list(v)
+            lst = b"".join(_field(1, 2, x.encode() if isinstance(x, str) else x) for x in items)
+            feat = _field(1, 2, lst)
+        else:
+            a = np.asarray(v).reshape(-1)
+            if np.issubdtype(a.dtype, np.floating):
+                feat = _field(2, 2, _field(1, 2, a.astype("<f4").tobytes()))
+            else:
+                packed = b"".join(_varint(int(x) & ((1 << 64) - 1)) for x in a)
+                feat = _field(3, 2, _field(1, 2, packed))
+        entries += _field(1, 2, _field(1, 2, key.encode()) + _field(2, 2, feat))
+    return _field(1, 2, entries)
+
+
+def read_tfrecord(path):
+    from zoo.tensorboard import read_records
+    return read_records(path)
+
+
+def write_tfrecord(path, records):
+    from zoo.tensorboard import _frame
+    with open(path, "wb") as f:
+        for r in records:
+            f.write(_frame(r))

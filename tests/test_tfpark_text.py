@@ -279,3 +279,29 @@ def test_bert_classifier_and_ner_train_on_gpu(gpu):
             optimizer=Adam(lr=1e-2))
     hist = m.fit([words, chars], np.eye(3)[tags], batch_size=16, epochs=5)
     assert np.isfinite(hist[-1]) and hist[-1] < hist[0]
+
+
+def test_tfdataset_from_tfrecord_and_iterable(tmp_path):
+    """TFDataset.from_tfrecord_file (tf.train.Example codec over TFRecord framing) and
+    from_tf_data_dataset (any iterable of unbatched elements)."""
+    from zoo.tfpark.tf_dataset import TFDataset, encode_example, parse_example, write_tfrecord
+    rng = np.random.RandomState(0)
+    xs, ys = rng.randn(10, 3).astype(np.float32), rng.randint(0, 5, 10)
+    recs = [encode_example({"a": xs[i, :2], "b": xs[i, 2:], "label": [ys[i]], "name": "r%d" % i,
+                            "neg": [-3, 7]}) for i in range(10)]
+    ex = parse_example(recs[4])
+    np.testing.assert_allclose(ex["a"], xs[4, :2])
+    assert ex["label"].dtype == np.int64 and ex["label"][0] == ys[4]
+    assert list(ex["neg"]) == [-3, 7] and ex["name"][0] == b"r4"
+    p = str(tmp_path / "d.tfrecord")
+    write_tfrecord(p, recs)
+    ds = TFDataset.from_tfrecord_file(p, batch_size=5, feature_keys=["a", "b"], label_key="label")
+    got_x, got_y = [], []
+    for b in ds.get_training_data().data(train=False):
+        got_x.append(np.asarray(b[0]))
+        got_y.append(np.asarray(b[1]))
+    np.testing.assert_allclose(np.concatenate(got_x), xs, rtol=1e-6)
+    np.testing.assert_array_equal(np.concatenate(got_y).reshape(-1), ys)
+    ds2 = TFDataset.from_tf_data_dataset([(xs[i], ys[i]) for i in range(10)], batch_size=4)
+    n = sum(np.asarray(b[0]).shape[0] for b in ds2.get_training_data().data(train=False))
+    assert n == 10
