@@ -104,3 +104,24 @@ def test_layers_star_import_does_not_shadow_torch():
     exec("from zoo.pipeline.api.keras.layers import *", ns)
     assert "torch" not in ns and "Dense" in ns
     assert torch.zeros(1).numel() == 1
+
+
+def test_xshard_reference_import_paths(tmp_path):
+    import pandas as pd
+    import zoo.xshard.pandas
+    from zoo.xshard.shard import RayDataShards, RayPartition
+    from zoo.xshard.pandas.preprocessing import RayPandasShard, read_file_ray
+    from zoo.xshard.utils import chunk, flatten
+    for i in range(3):
+        pd.DataFrame({"a": [i, i + 1], "b": [1.0, 2.0]}).to_csv(tmp_path / ("p%d.csv" % i), index=False)
+    sh = zoo.xshard.pandas.read_csv(str(tmp_path), None)
+    assert isinstance(sh, RayDataShards) and len(sh.collect()) == 3
+    out = sh.apply(lambda df, k: df.assign(c=df.a * k), 2).collect()
+    assert list(out[2].c) == [4, 6]
+    assert len(read_file_ray(None, str(tmp_path), "csv").collect()) == 3
+    s = RayPandasShard()
+    s.read_file_partitions([str(tmp_path / "p0.csv")], "csv")
+    s.apply(lambda df: df[df.a > 0])
+    assert len(s.get_data()) == 1
+    assert RayPartition([s]).get_data()[0] is s.get_data()
+    assert chunk(list(range(7)), 3) == [[0, 1, 2], [3, 4], [5, 6]] and flatten([[1], [2, 3]]) == [1, 2, 3]
