@@ -172,7 +172,8 @@ class ResNet(nn.Module):
         return x.contiguous()
 
     def _stem_s2d_ok(self, x):
-        return x.is_cuda and x.dim() == 4 and x.shape[1] == self.in_channels and self.cin_pad == 4 and \
+        return x.is_cuda and type(self.stem) is ConvBN and x.dim() == 4 and x.shape[1] == self.in_channels and \
+            self.cin_pad == 4 and \
             self.stem.k == 7 and self.stem.stride == 2 and self.stem.pad == 3 and S2D_STEM
 
     def _s2d_weight(self):
