@@ -30,9 +30,14 @@ namespace zoo {
 
 constexpr int IG_BM = 128, IG_BK = 64, IG_NT = 256;
 
+typedef __attribute__((address_space(3))) void ig_lds_void;
+typedef __attribute__((address_space(1))) const void ig_gl_void;
+// zero page for LDS-DMA of out-of-range rows / padding taps
+__device__ __attribute__((aligned(16))) bf16_t ig_zero_page[8];
+
 ZOO_DEV int ig_swz(int row) { return (row >> 1) & 7; }
 
-template <int VEC, bool IS1x1, bool LDIL, int BN>
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y,
     float* __restrict__ Yf, const float* __restrict__ bias, const bf16_t* __restrict__ resid,
@@ -61,8 +66,11 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- staging assignment: thread -> (16-byte k-chunk, rows) ----
-  const int cc = tid & 7;
+  // DMA staging writes LDS lane-linearly (lane -> 16-byte slot lane&7 of row lane>>3 of the
+  // wave's 8-row group), so the XOR swizzle is applied by choosing which k-chunk each lane
+  // loads; ig_swz depends on row bits 1..3 only, so it is the same for all rows of a thread
   const int rbase = tid >> 3;  // 0..31
+  const int cc = DMA ? ((tid & 7) ^ ig_swz(rbase)) : (tid & 7);
 
   // per-row precompute for the A (activation) gather
   int a_base[4], a_ih[4], a_iw[4];
@@ -95,15 +103,27 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   uint4 ra[4], rb[B_ROWS_PER_THREAD];
   const int nk = (g.ldb + BK - 1) / BK;
 
+  // LDS-DMA: per-lane 16-byte global source, wave-uniform LDS base (lane-linear image)
+  auto dma16 = [&](const bf16_t* src, bf16_t* dst) {
+    __builtin_amdgcn_global_load_lds((ig_gl_void*)src, (ig_lds_void*)dst, 16, 0, 0);
+  };
   auto load_tile = [&](int kt) {
     const int k = kt * BK + cc * 8;
+    // wave-uniform LDS row-group bases of this tile's buffer (DMA path)
+    bf16_t* adst = As + (kt & 1) * BM * BK + (wid * 8) * BK;
+    bf16_t* bdst = Bs + (kt & 1) * BN * BK + (wid * 8) * BK;
+    (void)adst; (void)bdst;
     // ---- A ----
     if constexpr (IS1x1) {
       const bool kok = k < g.Ktot;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        ra[i] = (a_ok[i] && kok) ? *reinterpret_cast<const uint4*>(X + a_base[i] + k)
-                                 : make_uint4(0, 0, 0, 0);
+        if constexpr (DMA) {
+          dma16(a_ok[i] && kok ? X + a_base[i] + k : ig_zero_page, adst + (32 * i) * BK);
+        } else {
+          ra[i] = (a_ok[i] && kok) ? *reinterpret_cast<const uint4*>(X + a_base[i] + k)
+                                   : make_uint4(0, 0, 0, 0);
+        }
       }
     } else if constexpr (VEC == 8) {
       const bool kok = kr < g.R;
@@ -118,8 +138,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
         } else {
           ok = ok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
         }
-        ra[i] = ok ? *reinterpret_cast<const uint4*>(X + a_base[i] + (ih * g.W + iw) * g.C + kc)
-                   : make_uint4(0, 0, 0, 0);
+        if constexpr (DMA) {
+          dma16(ok ? X + a_base[i] + (ih * g.W + iw) * g.C + kc : ig_zero_page, adst + (32 * i) * BK);
+        } else {
+          ra[i] = ok ? *reinterpret_cast<const uint4*>(X + a_base[i] + (ih * g.W + iw) * g.C + kc)
+                     : make_uint4(0, 0, 0, 0);
+        }
       }
     } else {  // VEC == 4: C == 4, each 8-element chunk spans two filter taps
       const int pos0 = k >> 2;
@@ -146,8 +170,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 #pragma unroll
     for (int i = 0; i < B_ROWS_PER_THREAD; ++i) {
       const int n = n0 + rbase + 32 * i;
-      rb[i] = (n < g.K && kokb) ? *reinterpret_cast<const uint4*>(Wm + (size_t)n * g.ldb + k)
-                                : make_uint4(0, 0, 0, 0);
+      if constexpr (DMA) {
+        dma16(n < g.K && kokb ? Wm + (size_t)n * g.ldb + k : ig_zero_page, bdst + (32 * i) * BK);
+      } else {
+        rb[i] = (n < g.K && kokb) ? *reinterpret_cast<const uint4*>(Wm + (size_t)n * g.ldb + k)
+                                  : make_uint4(0, 0, 0, 0);
+      }
     }
     // advance the incremental k decode for the next tile
     if constexpr (!IS1x1 && VEC == 8) {
@@ -204,16 +232,31 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   };
 
   // ---- main loop: one barrier per K tile, loads of tile k+1 overlap MFMA on tile k ----
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load_tile(kt + 1);
-    compute(cur);
-    if (more) store_tile(cur ^ 1);
+  if constexpr (DMA) {
+    // tile k+1 streams into the other LDS buffer (free since the previous barrier)
+    // while tile k is on the MFMA pipe; vmcnt(0) + barrier publish it
+    load_tile(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(kt + 1);
+      compute(kt & 1);
+      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(kt + 1);
+      compute(cur);
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage fp32 tile in LDS, then row-contiguous 16-byte stores ----
@@ -397,7 +440,7 @@ size_t igemm_smem_bytes(int BN, int nbuf = 2) {
   return main_bytes > epi_bytes ? main_bytes : epi_bytes;
 }
 
-template <int VEC, bool IS1x1, bool LDIL, int BN>
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA>
 static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                             const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                             hipStream_t st) {
@@ -405,16 +448,16 @@ static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* 
   const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN, DMA>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN));
     attr_set = true;
   }
-  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
+  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN, DMA>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
                      Yf, bias, resid, stats, g, act, bs);
   return hipGetLastError();
 }
 
-template <int VEC, bool IS1x1, bool LDIL>
+template <int VEC, bool IS1x1, bool LDIL, bool DMA>
 static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                                const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                                hipStream_t st) {
@@ -422,15 +465,15 @@ static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, floa
     const char* e = getenv("ZOO_IGEMM_BN");
     return e ? atoi(e) : 0;
   }();
-  if (force_bn == 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  if (force_bn == 128) return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (force_bn == 64) return launch_ig<VEC, IS1x1, LDIL, 64, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (force_bn == 128) return launch_ig<VEC, IS1x1, LDIL, 128, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   // BN=64 tiles (lower VGPR/LDS footprint, more workgroups in flight) win while
   // there are plenty of them; few large tiles win when the grid is small
   // (tools/gemm_bench.py sweep on ResNet-50 shapes)
-  if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (g.K <= 64) return launch_ig<VEC, IS1x1, LDIL, 64, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   const long tiles64 = (long)((g.M + IG_BM - 1) / IG_BM) * ((g.K + 63) / 64);
-  if (tiles64 >= 1536) return launch_ig<VEC, IS1x1, LDIL, 64>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  return launch_ig<VEC, IS1x1, LDIL, 128>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (tiles64 >= 1536) return launch_ig<VEC, IS1x1, LDIL, 64, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  return launch_ig<VEC, IS1x1, LDIL, 128, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 
 }  // namespace zoo
@@ -448,10 +491,21 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
   const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
                      g->lh == 1 && g->lw == 1 && g->H == g->P && g->W == g->Q;
   const bool ldil = g->lh > 1 || g->lw > 1;
-  if (g->C == 4) return launch_ig_bn<4, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
-  if (is1x1) return launch_ig_bn<8, true, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
-  if (ldil) return launch_ig_bn<8, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
-  return launch_ig_bn<8, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  // LDS-DMA staging (global_load_lds) for the 16-byte-vector paths; ZOO_IGEMM_DMA=0 selects
+  // the register-staged variant
+  static const bool dma = [] {
+    const char* e = getenv("ZOO_IGEMM_DMA");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (g->C == 4) return launch_ig_bn<4, false, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  if (dma) {
+    if (is1x1) return launch_ig_bn<8, true, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+    if (ldil) return launch_ig_bn<8, false, true, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+    return launch_ig_bn<8, false, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  }
+  if (is1x1) return launch_ig_bn<8, true, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  if (ldil) return launch_ig_bn<8, false, true, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
+  return launch_ig_bn<8, false, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
 }
 
 extern "C" hipError_t zoo_flip_weights(const void* W, void* Wt, int K, int R, int S, int C, int ldw, int r0,
