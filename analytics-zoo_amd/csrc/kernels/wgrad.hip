@@ -26,6 +26,10 @@ namespace zoo {
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 64;
 
+typedef __attribute__((address_space(3))) void wg_lds_void;
+typedef __attribute__((address_space(1))) const void wg_gl_void;
+__device__ __attribute__((aligned(16))) bf16_t wg_zero_page[8];
+
 // XOR swizzle on 16-column (32-byte) blocks; rows {0..3, 8..11} (one
 // half-wave of transposed reads) map to 8 distinct bank groups.
 ZOO_DEV int wg_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
@@ -33,7 +37,7 @@ ZOO_DEV int wg_off(int row, int col) {  // element offset in a [64][128] bf16 ti
   return row * 128 + ((((col >> 4) ^ wg_f(row)) & 7) << 4) + (col & 15);
 }
 
-template <int VEC>
+template <int VEC, bool DMA>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ X,
                                                         const bf16_t* __restrict__ dY,
                                                         float* __restrict__ dW, WgradGeom g) {
@@ -57,8 +61,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   const int nk = (mend - mstart + WG_BK - 1) / WG_BK;
 
   // staging: thread -> 8-column chunk `ch` (16 per 128-wide row), rows rb + 16*i
-  const int ch = tid & 15;
+  // LDS-DMA (VEC 8): a wave writes 4 rows x 256 B lane-linearly (lane -> 16-byte slot lane&15
+  // of row lane>>4), so each lane loads the logical 8-column chunk that the swizzle puts in
+  // its slot; wg_f depends on row bits 0,1,3 only -> one chunk per thread for all its rows
   const int rb = tid >> 4;  // 0..15
+  const int ch = DMA ? 2 * ((((tid & 15) >> 1) ^ wg_f(rb)) & 7) + (tid & 1) : (tid & 15);
 
   // dY columns (output channels) for this thread's chunk
   const int ycol = k0 + ch * 8;
@@ -87,13 +94,23 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   uint4 ra[4], rbv[4];
   const int PQ = g.P * g.Q;
 
+  auto dma16 = [&](const bf16_t* src, bf16_t* dst) {
+    __builtin_amdgcn_global_load_lds((wg_gl_void*)src, (wg_lds_void*)dst, 16, 0, 0);
+  };
   auto load_tile = [&](int kt) {
+    bf16_t* adst = As + (kt & 1) * WG_BK * WG_BM + (wid * 4) * WG_BM;
+    bf16_t* bdst = Bs + (kt & 1) * WG_BK * WG_BN + (wid * 4) * WG_BN;
+    (void)adst; (void)bdst;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = mstart + kt * WG_BK + rb + 16 * i;
       const bool mok = m < mend;
-      ra[i] = (mok && ycol_ok) ? *reinterpret_cast<const uint4*>(dY + (size_t)m * g.K + ycol)
-                               : make_uint4(0, 0, 0, 0);
+      if constexpr (DMA) {
+        dma16(mok && ycol_ok ? dY + (size_t)m * g.K + ycol : wg_zero_page, adst + 16 * i * WG_BM);
+      } else {
+        ra[i] = (mok && ycol_ok) ? *reinterpret_cast<const uint4*>(dY + (size_t)m * g.K + ycol)
+                                 : make_uint4(0, 0, 0, 0);
+      }
       const int mm = mok ? m : 0;
       const int n = mm / PQ;
       const int pq = mm - n * PQ;
@@ -104,8 +121,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
         const int ih = p * g.sh - g.ph + xr[0] * g.dh;
         const int iw = q * g.sw - g.pw + xs[0] * g.dw;
         const bool ok = mok && xok[0] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        rbv[i] = ok ? *reinterpret_cast<const uint4*>(xb + (ih * g.W + iw) * g.C + xc[0])
-                    : make_uint4(0, 0, 0, 0);
+        if constexpr (DMA) {
+          dma16(ok ? xb + (ih * g.W + iw) * g.C + xc[0] : wg_zero_page, bdst + 16 * i * WG_BN);
+        } else {
+          rbv[i] = ok ? *reinterpret_cast<const uint4*>(xb + (ih * g.W + iw) * g.C + xc[0])
+                      : make_uint4(0, 0, 0, 0);
+        }
       } else {
         uint2 v[2];
 #pragma unroll
@@ -172,16 +193,29 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
     }
   };
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load_tile(kt + 1);
-    compute(cur);
-    if (more) store_tile(cur ^ 1);
+  if constexpr (DMA) {
+    load_tile(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(kt + 1);
+      compute(kt & 1);
+      if (more) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(kt + 1);
+      compute(cur);
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: C/D map of 16x16x32 -> row = 4*(lane>>4)+reg (k-out), col = lane&15
@@ -226,11 +260,20 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const 
   splits = (g.M + mps - 1) / mps;
   g.m_per_split = mps;
   const size_t smem = (size_t)2 * WG_BK * (WG_BM + WG_BN) * sizeof(bf16_t);
+  static const bool dma = [] {
+    // measured slower than register staging for the weight gradient (conv_sweep wgrad
+    // 7.34 vs 6.99 ms/step, bench 8912 vs 9045 img/s): opt-in until re-tuned
+    const char* e = getenv("ZOO_WGRAD_DMA");
+    return e ? atoi(e) != 0 : false;
+  }();
   if (g.C == 4) {
-    hipLaunchKernelGGL(wgrad_kernel<4>, dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+    hipLaunchKernelGGL((wgrad_kernel<4, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+                       (const bf16_t*)dY, dW, g);
+  } else if (dma) {
+    hipLaunchKernelGGL((wgrad_kernel<8, true>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
                        (const bf16_t*)dY, dW, g);
   } else {
-    hipLaunchKernelGGL(wgrad_kernel<8>, dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+    hipLaunchKernelGGL((wgrad_kernel<8, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
                        (const bf16_t*)dY, dW, g);
   }
   return hipGetLastError();
