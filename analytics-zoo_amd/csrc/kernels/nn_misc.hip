@@ -125,6 +125,94 @@ __global__ __launch_bounds__(256) void layernorm_fwd_reg_kernel(const T* __restr
   }
 }
 
+// Register-resident LayerNorm backward (D <= 64*8*NCH): each wave keeps its row of x/dy in
+// registers for both passes, gamma once per thread (float4), and the dgamma/dbeta partials
+// of every row the wave visits in registers; the 4 waves fold them through LDS once and
+// the block adds [D] partials to global with one atomic per column. Replaces per-element
+// LDS atomics (the generic kernel below).
+template <typename T, int NCH>
+__global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(const T* __restrict__ dY, const T* __restrict__ X,
+                                                                const float* __restrict__ g,
+                                                                const float* __restrict__ mean,
+                                                                const float* __restrict__ rstd, T* __restrict__ dX,
+                                                                float* __restrict__ dg, float* __restrict__ db,
+                                                                int rows, int D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* part = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  float gg[NCH][8], pg[NCH][8], pb[NCH][8];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { gg[k][e] = 1.f; pg[k][e] = 0.f; pb[k][e] = 0.f; }
+    if (g && c < D) {
+      const float4 g0 = *reinterpret_cast<const float4*>(g + c), g1 = *reinterpret_cast<const float4*>(g + c + 4);
+      gg[k][0] = g0.x; gg[k][1] = g0.y; gg[k][2] = g0.z; gg[k][3] = g0.w;
+      gg[k][4] = g1.x; gg[k][5] = g1.y; gg[k][6] = g1.z; gg[k][7] = g1.w;
+    }
+  }
+  for (int row = blockIdx.x * 4 + wid; row < rows; row += gridDim.x * 4) {
+    const T* x = X + (size_t)row * D;
+    const T* dy = dY + (size_t)row * D;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NCH][8], gv[NCH][8];
+    float a = 0.f, bsum = 0.f;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c < D) {
+        ld8(x + c, xh[k]);
+        ld8(dy + c, gv[k]);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) { xh[k][e] = 0.f; gv[k][e] = 0.f; }
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        xh[k][e] = c < D ? (xh[k][e] - mu) * rs : 0.f;
+        const float gy = gv[k][e] * gg[k][e];
+        a += gy * xh[k][e];
+        bsum += gy;
+        pg[k][e] += gv[k][e] * xh[k][e];
+        pb[k][e] += gv[k][e];
+      }
+    }
+    a = warp_sum(a) / D;
+    bsum = warp_sum(bsum) / D;
+    T* dx = dX + (size_t)row * D;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      const int c = (k * 64 + lane) * 8;
+      if (c >= D) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = rs * (gv[k][e] * gg[k][e] - bsum - xh[k][e] * a);
+      st8(dx + c, o);
+    }
+  }
+  if (!dg && !db) return;
+  // fold the 4 waves' partials, one global atomic per column per block
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 8;
+    if (c >= D) continue;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      part[(wid * 2) * D + c + e] = pg[k][e];
+      part[(wid * 2 + 1) * D + c + e] = pb[k][e];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D; i += blockDim.x) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) { sg += part[(w * 2) * D + i]; sb += part[(w * 2 + 1) * D + i]; }
+    if (dg) atomicAdd(dg + i, sg);
+    if (db) atomicAdd(db + i, sb);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ dY, const T* __restrict__ X,
                                                             const float* __restrict__ g, const float* __restrict__ mean,
@@ -257,6 +345,28 @@ extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, 
 extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
                                         const float* rstd, void* dX, float* dg, float* db, int rows, int D,
                                         hipStream_t st) {
+  const bool al = (reinterpret_cast<uintptr_t>(g) & 15) == 0 && (f32 ? D % 4 == 0 : D % 8 == 0);
+  if (al && D <= 2048 && (f32 ? D % 8 == 0 : true)) {
+    // ~512 blocks of 4 waves; each wave loops over rows, so the dgamma/dbeta partials are
+    // folded once per block instead of once per row
+    int blocks = (rows + 3) / 4;
+    if (blocks > 512) blocks = 512;
+    const size_t psm = (size_t)8 * D * sizeof(float);
+#define ZOO_LNB_REG(TT, NCH)                                                                                   \
+  hipLaunchKernelGGL((layernorm_bwd_reg_kernel<TT, NCH>), dim3(blocks), dim3(256), psm, st, (const TT*)dY,   \
+                     (const TT*)X, g, mean, rstd, (TT*)dX, dg, db, rows, D)
+    if (f32) {
+      if (D <= 512) ZOO_LNB_REG(float, 1);
+      else if (D <= 1024) ZOO_LNB_REG(float, 2);
+      else ZOO_LNB_REG(float, 4);
+    } else {
+      if (D <= 512) ZOO_LNB_REG(bf16_t, 1);
+      else if (D <= 1024) ZOO_LNB_REG(bf16_t, 2);
+      else ZOO_LNB_REG(bf16_t, 4);
+    }
+#undef ZOO_LNB_REG
+    return hipGetLastError();
+  }
   int rpb = (rows + 511) / 512;
   if (rpb < 4) rpb = 4;
   const int blocks = (rows + rpb - 1) / rpb;

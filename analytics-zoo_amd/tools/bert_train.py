@@ -1,0 +1,58 @@
+#!/usr/bin/env python3
+"""BERT-base fine-tuning step throughput (random init, sequence classification head,
+AdamWeightDecay, bf16 compute with fp32 master weights, dropout on), for profiling:
+  python analytics-zoo_amd/tools/bert_train.py [--batch 32] [--seq 128] [--iters 20]"""
+import argparse
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+import torch.nn as nn  # noqa: E402
+
+
+class _Classifier(nn.Module):
+    def __init__(self, bert, n_cls=2):
+        super().__init__()
+        self.bert = bert
+        self.fc = nn.Linear(768, n_cls)
+
+    def forward(self, xs):
+        return self.fc(self.bert(xs)[1].float())
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--seq", type=int, default=128)
+    a = ap.parse_args()
+    from zoo.common.nncontext import init_nncontext
+    from zoo.pipeline.api.keras.layers import BERT
+    from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.ops import softmax_cross_entropy
+    init_nncontext("bert-train")
+    dev = torch.device("cuda")
+    bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512, intermediate_size=3072,
+                output_all_block=False)
+    eng = TrainingEngine(_Classifier(bert), softmax_cross_entropy, AdamWeightDecay(lr=2e-5))
+    B, L = a.batch, a.seq
+    xs = [torch.randint(0, 30522, (B, L), device=dev), torch.zeros(B, L, dtype=torch.long, device=dev),
+          torch.arange(L, device=dev).repeat(B, 1), torch.ones(B, L, device=dev)]
+    y = torch.randint(0, 2, (B,), device=dev)
+    for _ in range(3):
+        eng.train_step(xs, y)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.iters):
+        loss = eng.train_step(xs, y)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.iters
+    print('{"bench": "bert-base-finetune-train", "batch": %d, "seq": %d, "ms_per_step": %.3f, "seq_per_s": %.1f, '
+          '"tokens_per_s": %.0f, "loss": %.4f}' % (B, L, dt * 1e3, B / dt, B * L / dt, float(loss)))
+
+
+if __name__ == "__main__":
+    main()

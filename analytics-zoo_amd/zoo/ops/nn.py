@@ -48,6 +48,10 @@ def layer_norm(x, gamma=None, beta=None, eps=1e-5):
     D = x.shape[-1]
     if x.is_cuda and D % 8 == 0 and x.dtype in (torch.float32, torch.bfloat16):
         return _LayerNormFn.apply(x.contiguous(), gamma, beta, float(eps))
+    if (gamma is not None and gamma.dtype != x.dtype) or (beta is not None and beta.dtype != x.dtype):
+        # fp32 affine parameters with a low-precision input: normalise in fp32
+        return F.layer_norm(x.float(), (D,), None if gamma is None else gamma.float(),
+                            None if beta is None else beta.float(), eps).to(x.dtype)
     return F.layer_norm(x, (D,), gamma, beta, eps)
 
 

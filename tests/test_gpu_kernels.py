@@ -393,15 +393,17 @@ def test_resnet_learns_synthetic_task(gpu):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_layernorm_kernel(gpu, dt):
+@pytest.mark.parametrize("rows,D", [(37, 768), (4099, 768), (515, 1000), (300, 2048), (64, 100)])
+def test_layernorm_kernel(gpu, dt, rows, D):
+    """register-resident (D % 8 == 0, D <= 2048) and generic paths, fwd + bwd"""
     from zoo.ops import layer_norm
-    x = torch.randn(37, 768, device=gpu).to(dt).requires_grad_(True)
-    g = (torch.rand(768, device=gpu) + 0.5).requires_grad_(True)
-    b = torch.randn(768, device=gpu).requires_grad_(True)
+    x = torch.randn(rows, D, device=gpu).to(dt).requires_grad_(True)
+    g = (torch.rand(D, device=gpu) + 0.5).requires_grad_(True)
+    b = torch.randn(D, device=gpu).requires_grad_(True)
     y = layer_norm(x, g, b, 1e-5)
     xr = x.detach().float().requires_grad_(True)
     gr, br = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
-    yr = F.layer_norm(xr, (768,), gr, br, 1e-5)
+    yr = F.layer_norm(xr, (D,), gr, br, 1e-5)
     assert nrel(y, yr) < (1e-5 if dt == torch.float32 else 1e-2)
     dy = torch.randn_like(yr)
     y.backward(dy.to(dt))
