@@ -202,7 +202,7 @@ class _LinearBlasFn(torch.autograd.Function):
             elif act == "gelu":
                 y = F.gelu(y)
         ctx.save_for_backward(x2, w, y if act == "relu" else None, pre)
-        ctx.act, ctx.has_bias = act, bias is not None
+        ctx.act, ctx.has_bias, ctx.bias_ref = act, bias is not None, bias
         return y
 
     @staticmethod
@@ -217,18 +217,43 @@ class _LinearBlasFn(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, bf16_weight(w))
         if ctx.needs_input_grad[1]:
-            g = torch.mm(dy.t(), x2, out_dtype=torch.float32)
             gbuf = getattr(w, "_zoo_grad", None)
             if gbuf is not None:
-                gbuf.add_(g.reshape(gbuf.shape))
+                # accumulate straight into the flat fp32 gradient (hipBLASLt beta=1, bf16 in, fp32 out)
+                g2 = gbuf.view(dy.shape[1], x2.shape[1])
+                if not _blas_accumulate(g2, dy, x2):
+                    g2.add_(torch.mm(dy.t(), x2, out_dtype=torch.float32))
                 hook = getattr(w, "_zoo_grad_ready", None)
                 if hook is not None:
                     hook(w)
             else:
-                dw = g.to(w.dtype)
+                dw = torch.mm(dy.t(), x2, out_dtype=torch.float32).to(w.dtype)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            db = dy.float().sum(0)
+            bias = ctx.bias_ref
+            db = torch.sum(dy, 0, dtype=torch.float32)   # fp32 accumulation, no fp32 copy of dy
+            bbuf = getattr(bias, "_zoo_grad", None) if bias is not None else None
+            if bbuf is not None:
+                bbuf.add_(db)
+                hook = getattr(bias, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(bias)
+                db = None
         return dx, dw, db, None, None
+
+
+_ADDMM_DTYPE_OK = [True]
+
+
+def _blas_accumulate(g2, dy, x2):
+    """g2 (fp32) += dy^T x2 (bf16) in one hipBLASLt call; False if unsupported here."""
+    if not _ADDMM_DTYPE_OK[0]:
+        return False
+    try:
+        torch.ops.aten.addmm.dtype_out(g2, dy.t(), x2, torch.float32, beta=1, alpha=1, out=g2)
+        return True
+    except (RuntimeError, TypeError, AttributeError):
+        _ADDMM_DTYPE_OK[0] = False
+        return False
 
 
 def _bf16_bias(bias):
