@@ -213,6 +213,32 @@ __global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(const T* __restr
   }
 }
 
+// ---------------------------------------------------------------- Dropout (+ residual add)
+// out = x + keep(i) * a * scale  (x optional). keep(i) is a counter-based hash of (seed, i),
+// so backward regenerates the mask instead of storing it: da = keep(i) * dout * scale.
+ZOO_DEV uint32_t drop_fmix(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+__global__ __launch_bounds__(256) void dropout_add_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ X,
+                                                          bf16_t* __restrict__ Out, size_t n8, uint32_t thresh,
+                                                          float scale, uint32_t s0, uint32_t s1) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    float a[8], o[8];
+    unpack8(reinterpret_cast<const uint4*>(A)[i], a);
+    if (X) unpack8(reinterpret_cast<const uint4*>(X)[i], o);
+    const uint32_t base = drop_fmix((uint32_t)(i >> 29) ^ s1);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const uint32_t h = drop_fmix(((uint32_t)(i << 3) + e) * 0x9E3779B1u ^ s0 ^ base);
+      const float v = h >= thresh ? a[e] * scale : 0.f;
+      o[e] = X ? o[e] + v : v;
+    }
+    reinterpret_cast<uint4*>(Out)[i] = pack8(o);
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void layernorm_bwd_kernel(const T* __restrict__ dY, const T* __restrict__ X,
                                                             const float* __restrict__ g, const float* __restrict__ mean,
@@ -400,5 +426,19 @@ extern "C" hipError_t zoo_embedding_bwd(const void* dout, int f32, const int64_t
   else
     hipLaunchKernelGGL(embedding_bwd_kernel<bf16_t>, dim3(mgrid((size_t)n * D)), dim3(256), 0, st,
                        (const bf16_t*)dout, idx, gtable, n, D, V, pad, scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_dropout_add(const void* A, const void* X, void* Out, size_t n, float p, uint64_t seed,
+                                      hipStream_t st) {
+  const double t = (double)p * 4294967296.0;
+  const uint32_t thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  const float scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  const size_t n8 = n / 8;
+  size_t blocks = (n8 + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(dropout_add_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)A,
+                     (const bf16_t*)X, (bf16_t*)Out, n8, thresh, scale, (uint32_t)seed, (uint32_t)(seed >> 32));
   return hipGetLastError();
 }

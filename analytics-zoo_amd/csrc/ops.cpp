@@ -48,6 +48,7 @@ hipError_t zoo_adaptive(float*, const float*, float*, float*, void*, size_t, int
 hipError_t zoo_sumsq(const float*, size_t, float*, hipStream_t);
 hipError_t zoo_clip(float*, size_t, float, float, const float*, float, hipStream_t);
 hipError_t zoo_nchw_to_nhwc(const float*, void*, int, int, int, int, int, hipStream_t);
+hipError_t zoo_dropout_add(const void*, const void*, void*, size_t, float, uint64_t, hipStream_t);
 hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
@@ -489,6 +490,27 @@ void clip(torch::Tensor g, double lo, double hi, c10::optional<torch::Tensor> no
   req(g, at::kFloat, "g");
   check_hip(zoo_clip(g.data_ptr<float>(), g.numel(), lo, hi, opt_ptr<float>(norm_sq), max_norm, cur_stream()),
             "clip");
+}
+
+static bool xp_defined(const c10::optional<torch::Tensor>& x) { return x.has_value() && x->defined(); }
+
+// out = x + dropout(a, p) (x optional), bf16, mask regenerated from `seed` (counter-based hash)
+torch::Tensor dropout_add(torch::Tensor a, c10::optional<torch::Tensor> x, double p, int64_t seed) {
+  req(a, at::kBFloat16, "a");
+  TORCH_CHECK(a.numel() % 8 == 0, "dropout_add: numel must be a multiple of 8");
+  if (x.has_value() && x->defined()) {
+    req(*x, at::kBFloat16, "x");
+    TORCH_CHECK(x->sizes() == a.sizes(), "dropout_add: shape mismatch");
+  }
+  TORCH_CHECK(a.is_contiguous() && (!xp_defined(x) || x->is_contiguous()), "dropout_add: contiguous inputs");
+  check_al16(a.data_ptr(), "a");
+  if (xp_defined(x)) check_al16(x->data_ptr(), "x");
+  auto out = torch::empty_like(a);
+  const void* xp = (x.has_value() && x->defined()) ? x->data_ptr() : nullptr;
+  check_hip(zoo_dropout_add(a.data_ptr(), xp, out.data_ptr(), (size_t)a.numel(), (float)p, (uint64_t)seed,
+                            cur_stream()),
+            "dropout_add");
+  return out;
 }
 
 // [N, C<=4, H, W] fp32 -> [N, Hs, Ws, 16] bf16 space-to-depth(2) of the input zero-padded by `pad`
@@ -1000,6 +1022,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("nms_sorted", &nms_sorted);
   m.def("nchw_to_s2d", &nchw_to_s2d);
+  m.def("dropout_add", &dropout_add, py::arg("a"), py::arg("x") = py::none(), py::arg("p"), py::arg("seed"));
   m.def("attn_fwd_strided", &attn_fwd_strided);
   m.def("absmax", &absmax);
   m.def("im2col_q8", &im2col_q8);

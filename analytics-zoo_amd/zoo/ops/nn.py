@@ -44,6 +44,42 @@ class _LayerNormFn(torch.autograd.Function):
         return dx, (None if own_g else dg), (None if own_b else db), None
 
 
+_DROP_RNG = []
+
+
+def _drop_rng():
+    if not _DROP_RNG:
+        import random
+        _DROP_RNG.append(random.Random(torch.initial_seed()))
+    return _DROP_RNG[0]
+
+
+class _DropoutAddFn(torch.autograd.Function):
+    """out = x + dropout(a): one native pass; the keep-mask is a counter-based hash of a
+    per-call seed, so backward regenerates it (no mask tensor is stored)."""
+
+    @staticmethod
+    def forward(ctx, a, x, p):
+        seed = _drop_rng().getrandbits(62)   # host RNG: no device sync, no tensor op
+        ctx.p, ctx.seed = p, seed
+        return native().dropout_add(a, x, p, seed)
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        return native().dropout_add(g, None, ctx.p, ctx.seed), g, None
+
+
+def dropout_add(a, x, p, training=True):
+    """``x + F.dropout(a, p, training)`` (Transformer residual branch)."""
+    if not training or p <= 0:
+        return x + a
+    if a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and a.shape == x.shape and \
+            a.numel() % 8 == 0 and not torch.cuda.is_current_stream_capturing():
+        return _DropoutAddFn.apply(a.contiguous(), x.contiguous(), float(p))
+    return x + F.dropout(a, p, True)
+
+
 def layer_norm(x, gamma=None, beta=None, eps=1e-5):
     D = x.shape[-1]
     if x.is_cuda and D % 8 == 0 and x.dtype in (torch.float32, torch.bfloat16):

@@ -22,6 +22,7 @@ import torch.nn.functional as F
 
 from zoo import ops
 from zoo.ops.attention import attention_packed
+from zoo.ops.nn import dropout_add
 from zoo.pipeline.api.keras.base import Layer
 
 
@@ -61,14 +62,15 @@ class _Block(nn.Module):
             a = ops.attention(qkv[0], qkv[1], qkv[2], mask=mask, causal=causal, dropout_p=self.attn_drop,
                               training=self.training)
             a = a.transpose(1, 2).reshape(B, L, H)
-        a = F.dropout(ops.linear(a, self.proj_w, self.proj_b), self.hidden_drop, self.training)
-        n = ops.layer_norm(x + a, self.ln1_g, self.ln1_b, self.ln_eps)
+        a = ops.linear(a, self.proj_w, self.proj_b)
+        n = ops.layer_norm(dropout_add(a, x, self.hidden_drop, self.training), self.ln1_g, self.ln1_b, self.ln_eps)
         act = "gelu" if self.gelu == "erf" else None
         m = ops.linear(n, self.fc1_w, self.fc1_b, act=act)
         if self.gelu != "erf":  # GPT tanh approximation
             m = 0.5 * m * (1 + torch.tanh(math.sqrt(2 / math.pi) * (m + 0.044715 * m * m * m)))
-        m = F.dropout(ops.linear(m, self.fc2_w, self.fc2_b), self.hidden_drop, self.training)
-        return ops.layer_norm(n + m, self.ln2_g, self.ln2_b, self.ln_eps)
+        m = ops.linear(m, self.fc2_w, self.fc2_b)
+        return ops.layer_norm(dropout_add(m, n, self.hidden_drop, self.training), self.ln2_g, self.ln2_b,
+                              self.ln_eps)
 
 
 class TransformerLayer(Layer):

@@ -645,3 +645,29 @@ def test_engine_phase_timing_and_roctx_on_gpu(gpu):
     torch.cuda.synchronize()
     t = eng.phase_times()
     assert set(t) == {"fwd_bwd", "comm_optim"} and t["fwd_bwd"] > 0
+
+
+def test_dropout_add_kernel(gpu):
+    """x + dropout(a): drop rate ~p, kept values scaled by 1/(1-p), and the backward mask
+    (regenerated from the seed) equals the forward one."""
+    from zoo.ops import dropout_add
+    p = 0.1
+    a = (torch.rand(64, 128, 768, device=gpu) + 0.5).bfloat16().requires_grad_(True)
+    x = torch.randn(64, 128, 768, device=gpu).bfloat16().requires_grad_(True)
+    out = dropout_add(a, x, p, True)
+    d = (out.float() - x.float())
+    keep = d.abs() > 1e-3
+    rate = 1.0 - keep.float().mean().item()
+    assert abs(rate - p) < 0.005, rate
+    ratio = (d[keep] / a.float()[keep])
+    assert (ratio - 1.0 / (1.0 - p)).abs().max().item() < 0.03
+    g = torch.randn_like(out)
+    out.backward(g)
+    assert torch.equal(x.grad, g)
+    ga = a.grad.float()
+    assert torch.equal(ga == 0, ~keep | (g == 0))
+    assert (ga[keep] - g.float()[keep] / (1 - p)).abs().max().item() < 0.05
+    # two calls draw different masks
+    out2 = dropout_add(a.detach(), x.detach(), p, True)
+    assert not torch.equal(out2, out.detach())
+    assert torch.equal(dropout_add(a.detach(), x.detach(), p, False), x.detach() + a.detach())
