@@ -45,6 +45,7 @@ class _LayerNormFn(torch.autograd.Function):
 
 
 _DROP_RNG = []
+_DROP_FUSE_MIN = 1 << 22
 
 
 def _drop_rng():
@@ -75,7 +76,8 @@ def dropout_add(a, x, p, training=True):
     if not training or p <= 0:
         return x + a
     if a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and a.shape == x.shape and \
-            a.numel() % 8 == 0 and not torch.cuda.is_current_stream_capturing():
+            a.numel() % 8 == 0 and a.numel() >= _DROP_FUSE_MIN and not torch.cuda.is_current_stream_capturing():
+        # small tensors are launch/host-bound: the C++ dropout path has less per-call overhead
         return _DropoutAddFn.apply(a.contiguous(), x.contiguous(), float(p))
     return x + F.dropout(a, p, True)
 
