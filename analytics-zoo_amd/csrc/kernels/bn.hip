@@ -21,6 +21,7 @@
 #include <stdlib.h>
 
 #include "common.h"
+#include "geom.h"
 
 namespace zoo {
 
@@ -46,16 +47,16 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
   const int tid = threadIdx.x;
   // threads are laid out [row_lane][chunk]; if C/8 > 256 a thread walks several chunks
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* red = reinterpret_cast<float*>(smem);  // [2][C]
-  for (int i = tid; i < 2 * C; i += blockDim.x) red[i] = 0.f;
-  __syncthreads();
-
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
   const int lanes_per_row = cpr < 256 ? cpr : 256;
   const int row_step = 256 / lanes_per_row;
   const int my_row = tid / lanes_per_row;
   const int my_chunk0 = tid - my_row * lanes_per_row;
+  // per-row-lane partials [row_step][2][C]: every (row lane, channel) slot has exactly one
+  // writer, and the fold below adds the row lanes in a fixed order (no LDS float atomics,
+  // so the block's sums are bit-reproducible)
+  float* red = reinterpret_cast<float*>(smem);
   if (my_row < row_step) {
     for (int chunk = my_chunk0; chunk < cpr; chunk += lanes_per_row) {
       float s1[8], s2[8];
@@ -89,16 +90,30 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
           }
         }
       }
+      float* rr = red + (size_t)my_row * 2 * C;
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        atomicAdd(&red[chunk * 8 + e], s1[e]);  // LDS atomics: cheap, few per thread
-        atomicAdd(&red[C + chunk * 8 + e], s2[e]);
+        rr[chunk * 8 + e] = s1[e];
+        rr[C + chunk * 8 + e] = s2[e];
       }
     }
   }
   __syncthreads();
+  if (nslot == kStatPartial) {  // out = [gridDim.x][2C] partials, folded by stats_part_finalize
+    float* const dst = out + (size_t)blockIdx.x * 2 * C;
+    for (int i = tid; i < 2 * C; i += blockDim.x) {
+      float a = 0.f;
+      for (int r = 0; r < row_step; ++r) a += red[(size_t)r * 2 * C + i];
+      dst[i] = a;
+    }
+    return;
+  }
   float* const dst = nslot > 0 ? slot_ptr(out, 2 * C, nslot) : out;
-  for (int i = tid; i < 2 * C; i += blockDim.x) atomicAdd(dst + i, red[i]);
+  for (int i = tid; i < 2 * C; i += blockDim.x) {
+    float a = 0.f;
+    for (int r = 0; r < row_step; ++r) a += red[(size_t)r * 2 * C + i];
+    atomicAdd(dst + i, a);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -299,6 +314,36 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
   if (w == 0 && c < n2) buf[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
+// Deterministic fold of per-workgroup partials: out[c] += sum_p part[p][c], p in order.
+// Level 1 (nparts > kPartGroup): block (column chunk, group g) sums the group's parts,
+// 4 waves x 16 parts each then the waves in order, into lvl1[g][c]; level 2 sums the
+// groups in order and adds into out.
+constexpr int kPartGroup = 64;
+__global__ __launch_bounds__(256) void stats_part_lvl1_kernel(const float* __restrict__ part,
+                                                             float* __restrict__ lvl1, int n2, int nparts) {
+  __shared__ float w4[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), w = threadIdx.x >> 6;
+  const int p0 = blockIdx.y * kPartGroup + w * (kPartGroup / 4);
+  const int p1 = min(nparts, p0 + kPartGroup / 4);
+  float s = 0.f;
+  if (c < n2)
+    for (int p = p0; p < p1; ++p) s += part[(size_t)p * n2 + c];
+  w4[w][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (w == 0 && c < n2)
+    lvl1[(size_t)blockIdx.y * n2 + c] = ((w4[0][threadIdx.x] + w4[1][threadIdx.x]) + w4[2][threadIdx.x]) +
+                                        w4[3][threadIdx.x];
+}
+
+__global__ __launch_bounds__(256) void stats_part_lvl2_kernel(const float* __restrict__ part, float* __restrict__ out,
+                                                             int n2, int nparts) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= n2) return;
+  float s = 0.f;
+  for (int p = 0; p < nparts; ++p) s += part[(size_t)p * n2 + c];
+  out[c] += s;
+}
+
 // contiguous row range per block: ~kApplyBlocks blocks, at least kMinRows rows per thread-row
 static int apply_rows_per_block(int M, int C) {
   static const int target = [] {
@@ -326,19 +371,49 @@ extern "C" hipError_t zoo_stats_finalize(float* buf, int n2, int nslot, hipStrea
   return hipGetLastError();
 }
 
+// scratch floats zoo_stats_part_finalize needs for `nparts` partial rows of n2 columns
+extern "C" size_t zoo_stats_part_scratch(int n2, int nparts) {
+  return nparts > kPartGroup ? (size_t)((nparts + kPartGroup - 1) / kPartGroup) * n2 : 0;
+}
+
+extern "C" hipError_t zoo_stats_part_finalize(float* out, const float* part, float* scratch, int n2, int nparts,
+                                              hipStream_t st) {
+  if (nparts > kPartGroup) {
+    const int groups = (nparts + kPartGroup - 1) / kPartGroup;
+    hipLaunchKernelGGL(stats_part_lvl1_kernel, dim3((n2 + 63) / 64, groups), dim3(256), 0, st, part, scratch, n2,
+                       nparts);
+    part = scratch;
+    nparts = groups;
+  }
+  hipLaunchKernelGGL(stats_part_lvl2_kernel, dim3((n2 + 255) / 256), dim3(256), 0, st, part, out, n2, nparts);
+  return hipGetLastError();
+}
+
+// grid of zoo_bn_reduce: ~1024 blocks owning contiguous row ranges, at least 16 rows per
+// thread-row (small tensors such as bias gradients use few blocks)
+static void bn_reduce_grid(int M, int C, int* blocks, int* rpb) {
+  *blocks = 1024;
+  *rpb = (M + *blocks - 1) / *blocks;
+  const int cpr = C >> 3;
+  const int row_step = 256 / (cpr < 256 ? cpr : 256);
+  if (*rpb < 16 * row_step) *rpb = 16 * row_step;
+  *blocks = (M + *rpb - 1) / *rpb;
+}
+
+extern "C" int zoo_bn_reduce_blocks(int M, int C) {
+  int blocks, rpb;
+  bn_reduce_grid(M, C, &blocks, &rpb);
+  return blocks;
+}
+
 extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X, const float* mean,
                                     const float* invstd, float* out, int M, int C, int mode, int nslot,
                                     hipStream_t st) {
-  // ~1024 blocks, each owning a contiguous row range
-  int blocks = 1024;
-  int rpb = (M + blocks - 1) / blocks;
-  // at least 16 rows per thread-row: small tensors (bias gradients) then use few
-  // blocks instead of 1024 nearly idle ones each paying 2C slot atomics
+  int blocks, rpb;
+  bn_reduce_grid(M, C, &blocks, &rpb);
   const int cpr = C >> 3;
   const int row_step = 256 / (cpr < 256 ? cpr : 256);
-  if (rpb < 16 * row_step) rpb = 16 * row_step;
-  blocks = (M + rpb - 1) / rpb;
-  const size_t smem = (size_t)2 * C * sizeof(float);
+  const size_t smem = (size_t)row_step * 2 * C * sizeof(float);
   if (mode == 0)
     hipLaunchKernelGGL(bn_reduce_kernel<0>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)A,
                        (const bf16_t*)Z, (const bf16_t*)X, mean, invstd, out, M, C, rpb, nslot);

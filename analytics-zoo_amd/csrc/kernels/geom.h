@@ -6,6 +6,7 @@ namespace zoo {
 // Implicit-GEMM conv / GEMM geometry (igemm.hip).
 // Per-channel statistics buffers in slotted form: [2C final][slots x 2C][counter]
 constexpr int kStatSlots = 16;
+constexpr int kStatPartial = -1;
 
 struct ConvGeom {
   int N, H, W, C;        // input activation, NHWC
@@ -22,7 +23,10 @@ struct ConvGeom {
   // row (n,p,q) -> ((n*oH + oh0 + osh*p)*oW + ow0 + osw*q)*K
   int omap, oH, oW, osh, osw, oh0, ow0;
   // >0: per-channel statistics go through `stat_slots` contention-spreading slots
-  // (see slotted_stats in common.h); 0: direct atomics into the [2*K] buffer
+  // (see slotted_stats in common.h); 0: direct atomics into the [2*K] buffer;
+  // kStatPartial: no atomics -- the stats pointer is a [tiles_m][2*K] partials buffer,
+  // each workgroup STORES its column sums into row tm, and zoo_stats_part_finalize
+  // folds the rows in a fixed order (deterministic, contention-free)
   int stat_slots;
 };
 

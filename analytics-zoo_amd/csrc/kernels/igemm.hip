@@ -374,10 +374,18 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   }
 
   if (reg_stats) {
-    float* const dst = g.stat_slots > 0 ? slot_ptr(stats, 2 * g.K, g.stat_slots) : stats;
     if (tid < BN && n0 + tid < g.K) {
-      atomicAdd(dst + n0 + tid, wstat[tid * 2] + wstat[(BN + tid) * 2]);
-      atomicAdd(dst + g.K + n0 + tid, wstat[tid * 2 + 1] + wstat[(BN + tid) * 2 + 1]);
+      const float a = wstat[tid * 2] + wstat[(BN + tid) * 2];
+      const float b = wstat[tid * 2 + 1] + wstat[(BN + tid) * 2 + 1];
+      if (g.stat_slots == kStatPartial) {
+        float* const dst = stats + (size_t)tm * 2 * g.K;
+        dst[n0 + tid] = a;
+        dst[g.K + n0 + tid] = b;
+      } else {
+        float* const dst = g.stat_slots > 0 ? slot_ptr(stats, 2 * g.K, g.stat_slots) : stats;
+        atomicAdd(dst + n0 + tid, a);
+        atomicAdd(dst + g.K + n0 + tid, b);
+      }
     }
     return;
   }
@@ -403,15 +411,21 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
       }
     }
     __syncthreads();
-    float* const dst = g.stat_slots > 0 ? slot_ptr(sacc, 2 * g.K, g.stat_slots) : sacc;
     if (tid < BN) {
       const int col = n0 + tid;
       if (col < g.K) {
         float a = 0.f, b = 0.f;
 #pragma unroll
         for (int w = 0; w < 4; ++w) { a += red[(w * BN + tid) * 2]; b += red[(w * BN + tid) * 2 + 1]; }
-        atomicAdd(dst + col, a);
-        atomicAdd(dst + g.K + col, b);
+        if (g.stat_slots == kStatPartial) {
+          float* const dst = sacc + (size_t)tm * 2 * g.K;
+          dst[col] = a;
+          dst[g.K + col] = b;
+        } else {
+          float* const dst = g.stat_slots > 0 ? slot_ptr(sacc, 2 * g.K, g.stat_slots) : sacc;
+          atomicAdd(dst + col, a);
+          atomicAdd(dst + g.K + col, b);
+        }
       }
     }
   }

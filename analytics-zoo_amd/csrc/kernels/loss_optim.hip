@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__
                                                            float* __restrict__ loss_sum,
                                                            float* __restrict__ count,
                                                            T* __restrict__ dlogits, int B, int NC,
-                                                           float grad_scale, int ignore_index) {
+                                                           float grad_scale, int ignore_index, int per_row) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= B) return;
@@ -41,9 +41,14 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__
   const float lse = mx + __logf(s);
   const int64_t lab = labels[row];
   const bool valid = lab != ignore_index && lab >= 0 && lab < NC;
-  if (lane == 0 && valid) {
-    atomicAdd(loss_sum, lse - ld(x, lab));
-    atomicAdd(count, 1.f);
+  if (lane == 0) {
+    if (per_row) {  // deterministic mode: per-row terms, summed by the caller in a fixed order
+      loss_sum[row] = valid ? lse - ld(x, lab) : 0.f;
+      count[row] = valid ? 1.f : 0.f;
+    } else if (valid) {
+      atomicAdd(loss_sum, lse - ld(x, lab));
+      atomicAdd(count, 1.f);
+    }
   }
   if (dlogits) {
     const float inv_s = 1.f / s;
@@ -246,14 +251,14 @@ using namespace zoo;
 
 extern "C" hipError_t zoo_softmax_xent(const void* logits, int is_f32, const int64_t* labels, float* loss_sum,
                                        float* count, void* dlogits, int B, int NC, float grad_scale,
-                                       int ignore_index, hipStream_t st) {
+                                       int ignore_index, int per_row, hipStream_t st) {
   const int blocks = (B + 3) / 4;
   if (is_f32)
     hipLaunchKernelGGL(softmax_xent_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)logits, labels,
-                       loss_sum, count, (float*)dlogits, B, NC, grad_scale, ignore_index);
+                       loss_sum, count, (float*)dlogits, B, NC, grad_scale, ignore_index, per_row);
   else
     hipLaunchKernelGGL(softmax_xent_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)logits, labels,
-                       loss_sum, count, (bf16_t*)dlogits, B, NC, grad_scale, ignore_index);
+                       loss_sum, count, (bf16_t*)dlogits, B, NC, grad_scale, ignore_index, per_row);
   return hipGetLastError();
 }
 

@@ -40,7 +40,8 @@ ZOO_DEV int wg_off(int row, int col) {  // element offset in a [64][128] bf16 ti
 template <int VEC, bool DMA>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ X,
                                                         const bf16_t* __restrict__ dY,
-                                                        float* __restrict__ dW, WgradGeom g) {
+                                                        float* __restrict__ dW, float* __restrict__ part,
+                                                        WgradGeom g) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64 m][128 k-out]
   bf16_t* Bs = As + 2 * WG_BK * WG_BM;           // [2][64 m][128 (r,s,c)]
@@ -218,8 +219,12 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
     }
   }
 
-  // epilogue: C/D map of 16x16x32 -> row = 4*(lane>>4)+reg (k-out), col = lane&15
+  // epilogue: C/D map of 16x16x32 -> row = 4*(lane>>4)+reg (k-out), col = lane&15.
+  // part != null: plain stores of this split's tile into part[split][K][Ktot] (folded in a
+  // fixed order by wgrad_fold_kernel: deterministic, no atomics); otherwise fp32 atomics
+  // into dW (a single split is one adder per element, hence also deterministic)
   const int fr = lane & 15, fq = lane >> 4;
+  float* const pdst = part ? part + (size_t)split * g.K * g.Ktot : nullptr;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -229,18 +234,40 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int row = k0 + wm * 64 + i * 16 + fq * 4 + r;
-        if (row < g.K) atomicAdd(dW + (size_t)row * g.ldw + col, acc[i][j][r]);
+        if (row < g.K) {
+          if (pdst) pdst[(size_t)row * g.Ktot + col] = acc[i][j][r];
+          else atomicAdd(dW + (size_t)row * g.ldw + col, acc[i][j][r]);
+        }
       }
     }
+}
+
+// dW[k][c] += sum_s part[s][k][c] (s in order); 4 columns per thread (Ktot % 4 == 0)
+__global__ __launch_bounds__(256) void wgrad_fold_kernel(const float* __restrict__ part, float* __restrict__ dW,
+                                                        int K, int Ktot, int ldw, int splits) {
+  const int q = Ktot >> 2;
+  const size_t n4 = (size_t)K * q;
+  const size_t stride = (size_t)K * Ktot;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i / q), c4 = (int)(i - (size_t)k * q) * 4;
+    const float* p = part + (size_t)k * Ktot + c4;
+    float4 s = *reinterpret_cast<const float4*>(p);
+    for (int sp = 1; sp < splits; ++sp) {
+      const float4 v = *reinterpret_cast<const float4*>(p + sp * stride);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+    float* d = dW + (size_t)k * ldw + c4;
+    d[0] += s.x; d[1] += s.y; d[2] += s.z; d[3] += s.w;
+  }
 }
 
 }  // namespace zoo
 
 using namespace zoo;
 
-extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const WgradGeom* gin,
-                                hipStream_t st) {
-  WgradGeom g = *gin;
+// split plan of the pixel reduction: sets g->m_per_split, returns the number of splits
+extern "C" int zoo_wgrad_plan(WgradGeom* gp) {
+  WgradGeom& g = *gp;
   const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
   // split the pixel reduction so that ~kTarget workgroups are in flight, >= kMinPix pixels each
   static const int target = [] {
@@ -259,6 +286,16 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const 
   mps = (mps + WG_BK - 1) / WG_BK * WG_BK;
   splits = (g.M + mps - 1) / mps;
   g.m_per_split = mps;
+  return splits;
+}
+
+// part: null (fp32 atomics into dW) or [splits][K][Ktot] scratch from zoo_wgrad_plan
+extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float* part, const WgradGeom* gin,
+                                hipStream_t st) {
+  WgradGeom g = *gin;
+  const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
+  const int splits = zoo_wgrad_plan(&g);
+  if (splits <= 1) part = nullptr;
   const size_t smem = (size_t)2 * WG_BK * (WG_BM + WG_BN) * sizeof(bf16_t);
   static const bool dma = [] {
     // measured slower than register staging for the weight gradient (conv_sweep wgrad
@@ -268,13 +305,18 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, const 
   }();
   if (g.C == 4) {
     hipLaunchKernelGGL((wgrad_kernel<4, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
-                       (const bf16_t*)dY, dW, g);
+                       (const bf16_t*)dY, dW, part, g);
   } else if (dma) {
     hipLaunchKernelGGL((wgrad_kernel<8, true>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
-                       (const bf16_t*)dY, dW, g);
+                       (const bf16_t*)dY, dW, part, g);
   } else {
     hipLaunchKernelGGL((wgrad_kernel<8, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
-                       (const bf16_t*)dY, dW, g);
+                       (const bf16_t*)dY, dW, part, g);
+  }
+  if (part) {
+    const size_t n4 = (size_t)g.K * (g.Ktot / 4);
+    const int blocks = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
+    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, part, dW, g.K, g.Ktot, g.ldw, splits);
   }
   return hipGetLastError();
 }

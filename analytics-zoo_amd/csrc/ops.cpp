@@ -23,8 +23,12 @@ hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, co
                        int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                             hipStream_t);
-hipError_t zoo_wgrad(const void*, const void*, float*, const WgradGeom*, hipStream_t);
+hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
+int zoo_wgrad_plan(WgradGeom*);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
+size_t zoo_stats_part_scratch(int, int);
+hipError_t zoo_stats_part_finalize(float*, const float*, float*, int, int, hipStream_t);
+int zoo_bn_reduce_blocks(int, int);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
@@ -37,7 +41,7 @@ hipError_t zoo_maxpool_bwd(const void*, const void*, void*, int, int, int, int, 
                            hipStream_t);
 hipError_t zoo_gap_fwd(const void*, void*, int, int, int, hipStream_t);
 hipError_t zoo_gap_bwd(const void*, void*, int, int, int, hipStream_t);
-hipError_t zoo_softmax_xent(const void*, int, const int64_t*, float*, float*, void*, int, int, float, int,
+hipError_t zoo_softmax_xent(const void*, int, const int64_t*, float*, float*, void*, int, int, float, int, int,
                             hipStream_t);
 hipError_t zoo_sgd(float*, const float*, float*, void*, size_t, float, float, float, float, int, float, int,
                    hipStream_t);
@@ -84,6 +88,32 @@ void check_hip(hipError_t e, const char* what) {
 
 // slotted per-channel statistics buffer: [2C final][kStatSlots x 2C][counter, padded to 4 floats]
 int64_t stat_len(int64_t C) { return 2 * C * (zoo::kStatSlots + 1) + 4; }
+
+// Reduction modes.
+//  * deterministic: every cross-workgroup float reduction of the conv/BN/loss path goes through
+//    per-workgroup partials folded in a fixed order (no float atomics): identical inputs give
+//    bit-identical outputs run to run. ZOO_DETERMINISTIC=1 or set_deterministic(True).
+//  * stats_partial / wgrad_partial: the same partial-buffer reductions used for speed (no atomic
+//    contention) -- on by default where they measured faster.
+bool env_flag(const char* name, bool dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) != 0 : dflt;
+}
+bool g_deterministic = env_flag("ZOO_DETERMINISTIC", false);
+bool g_stats_partial = env_flag("ZOO_STATS_PARTIAL", false);
+bool g_wgrad_partial = env_flag("ZOO_WGRAD_PARTIAL", false);
+bool stats_partial() { return g_deterministic || g_stats_partial; }
+bool wgrad_partial() { return g_deterministic || g_wgrad_partial; }
+
+// out[0..n2) += ordered fold of part [nparts][n2]
+void fold_partials(float* out, const torch::Tensor& part, int n2, int nparts) {
+  const size_t scr = zoo_stats_part_scratch(n2, nparts);
+  torch::Tensor s;
+  if (scr) s = torch::empty({(int64_t)scr}, part.options());
+  check_hip(zoo_stats_part_finalize(out, part.data_ptr<float>(), scr ? s.data_ptr<float>() : nullptr, n2, nparts,
+                                    cur_stream()),
+            "stats_part_finalize");
+}
 
 void req(const torch::Tensor& t, at::ScalarType dt, const char* name) {
   TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -195,6 +225,17 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     bs.inv = binv->data_ptr<float>();
     bs.sums = bsums->data_ptr<float>();
   }
+  // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
+  // they are folded in order into the caller's buffer (its first 2K floats)
+  float* const stat_dst = sp ? sp : bs.sums;
+  torch::Tensor part;
+  const int tiles_m = (g.M + 127) / 128;  // IG_BM
+  if (stat_dst && stats_partial()) {
+    part = torch::empty({(int64_t)tiles_m, 2 * (int64_t)K}, x.options().dtype(at::kFloat));
+    g.stat_slots = zoo::kStatPartial;
+    if (sp) sp = part.data_ptr<float>();
+    else bs.sums = part.data_ptr<float>();
+  }
   torch::Tensor y, yf;
   if (out.has_value() && out->defined()) {
     TORCH_CHECK(out_bf16 && !out_f32, "conv_fwd: explicit output must be bf16");
@@ -209,8 +250,9 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   check_hip(zoo_igemm(x.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
                       out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, &bs, cur_stream()),
             "igemm");
-  if (g.stat_slots > 0)
-    check_hip(zoo_stats_finalize(sp ? sp : bs.sums, 2 * K, g.stat_slots, cur_stream()), "stats_finalize");
+  if (g.stat_slots == zoo::kStatPartial) fold_partials(stat_dst, part, 2 * K, tiles_m);
+  else if (g.stat_slots > 0)
+    check_hip(zoo_stats_finalize(stat_dst, 2 * K, g.stat_slots, cur_stream()), "stats_finalize");
   return out_bf16 ? y : yf;
 }
 
@@ -251,7 +293,15 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
   g.m_per_split = 0;
-  check_hip(zoo_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), &g, cur_stream()), "wgrad");
+  torch::Tensor part;
+  if (wgrad_partial()) {
+    WgradGeom gp = g;
+    const int splits = zoo_wgrad_plan(&gp);
+    if (splits > 1) part = torch::empty({(int64_t)splits, (int64_t)g.K * g.Ktot}, dw.options());
+  }
+  check_hip(zoo_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), part.defined() ? part.data_ptr<float>() : nullptr,
+                      &g, cur_stream()),
+            "wgrad");
 }
 
 static void check_al16(const void* p, const char* what) {
@@ -266,7 +316,7 @@ void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<to
   const int64_t M = a.numel() / C;
   TORCH_CHECK(C % 8 == 0, "bn_reduce: C must be a multiple of 8");
   TORCH_CHECK(out.numel() == 2 * C || out.numel() == stat_len(C), "bn_reduce: out must be [2*C] or stat_len(C)");
-  const int nslot = out.numel() == 2 * C ? 0 : zoo::kStatSlots;
+  int nslot = out.numel() == 2 * C ? 0 : zoo::kStatSlots;
   if (mode == 1) {
     TORCH_CHECK(x.has_value() && mean.has_value() && invstd.has_value(), "bn_reduce mode 1 needs x/mean/invstd");
     req(*x, at::kBFloat16, "x");
@@ -280,9 +330,19 @@ void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<to
     check_al16(opt_ptr<float>(mean), "mean");
     check_al16(opt_ptr<float>(invstd), "invstd");
   }
+  float* dst = out.data_ptr<float>();
+  torch::Tensor part;
+  int blocks = 0;
+  if (stats_partial()) {
+    blocks = zoo_bn_reduce_blocks((int)M, C);
+    part = torch::empty({(int64_t)blocks, 2 * (int64_t)C}, out.options());
+    dst = part.data_ptr<float>();
+    nslot = zoo::kStatPartial;
+  }
   check_hip(zoo_bn_reduce(a.data_ptr(), opt_ptr<void>(z), opt_ptr<void>(x), opt_ptr<float>(mean),
-                          opt_ptr<float>(invstd), out.data_ptr<float>(), (int)M, C, mode, nslot, cur_stream()),
+                          opt_ptr<float>(invstd), dst, (int)M, C, mode, nslot, cur_stream()),
             "bn_reduce");
+  if (nslot == zoo::kStatPartial) fold_partials(out.data_ptr<float>(), part, 2 * C, blocks);
 }
 
 torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<torch::Tensor> gamma,
@@ -410,14 +470,17 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
   req(labels, at::kLong, "labels");
   TORCH_CHECK(labels.numel() == logits.size(0), "labels size");
   const int B = logits.size(0), NC = logits.size(1);
-  auto loss = torch::zeros({2}, logits.options().dtype(at::kFloat));
+  const bool per_row = g_deterministic;
+  auto loss = per_row ? torch::empty({2, B}, logits.options().dtype(at::kFloat))
+                      : torch::zeros({2}, logits.options().dtype(at::kFloat));
   torch::Tensor dl;
   if (want_grad) dl = torch::empty_like(logits);
   const bool f32 = logits.scalar_type() == at::kFloat;
   check_hip(zoo_softmax_xent(logits.data_ptr(), f32, labels.data_ptr<int64_t>(), loss.data_ptr<float>(),
-                             loss.data_ptr<float>() + 1, want_grad ? dl.data_ptr() : nullptr, B, NC,
-                             (float)grad_scale, (int)ignore_index, cur_stream()),
+                             loss.data_ptr<float>() + (per_row ? B : 1), want_grad ? dl.data_ptr() : nullptr, B, NC,
+                             (float)grad_scale, (int)ignore_index, per_row ? 1 : 0, cur_stream()),
             "softmax_xent");
+  if (per_row) loss = loss.sum(1);
   if (want_grad) return {loss, dl};
   return {loss};
 }
@@ -997,6 +1060,13 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("set_deterministic", [](bool on) { g_deterministic = on; });
+  m.def("get_deterministic", []() { return g_deterministic; });
+  m.def("set_reduce_modes", [](bool stats_part, bool wgrad_part) {
+    g_stats_partial = stats_part;
+    g_wgrad_partial = wgrad_part;
+  });
+  m.def("get_reduce_modes", []() { return std::make_tuple(g_stats_partial, g_wgrad_partial); });
   m.def("bn_reduce", &bn_reduce);
   m.def("stat_len", &stat_len);
   m.def("bn_fwd_apply", &bn_fwd_apply);

@@ -50,6 +50,7 @@ class ZooConfig:
     roctx: bool = False                  # ZOO_ROCTX: roctx ranges around engine phases (rocprofv3 --marker-trace)
     phase_timing: bool = False           # ZOO_PHASE_TIMING: per-phase device timings (fwd+bwd / comm / optim)
     debug_sync: bool = False             # ZOO_DEBUG_SYNC: synchronise + check for non-finite loss every step
+    deterministic: bool = False          # ZOO_DETERMINISTIC: ordered (atomic-free) reductions, bit-reproducible
     seed: int = 1
     backend: str = ""                    # "", "nccl" (RCCL), "gloo"
     timeout_s: float = 1800.0
@@ -61,7 +62,7 @@ class ZooConfig:
         "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
         "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
         "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",
-        "phase_timing": "ZOO_PHASE_TIMING", "debug_sync": "ZOO_DEBUG_SYNC",
+        "phase_timing": "ZOO_PHASE_TIMING", "debug_sync": "ZOO_DEBUG_SYNC", "deterministic": "ZOO_DETERMINISTIC",
         "backend": "ZOO_DIST_BACKEND", "timeout_s": "ZOO_DIST_TIMEOUT",
     }
     _LEGACY = {"failure_retry_times": "bigdl.failure.retryTimes",
@@ -176,6 +177,8 @@ def init_nncontext(conf=None, redirect_spark_log=True, app_name=None, **kw):
         device = torch.device("cuda", local_rank % max(ndev, 1))
         from zoo.ops._native import native
         native()  # fail early and loudly if the kernel library is missing
+        if cfg.deterministic:
+            native().set_deterministic(True)
     else:
         device = torch.device("cpu")
     group = None

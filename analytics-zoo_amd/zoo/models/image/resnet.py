@@ -63,12 +63,12 @@ def _fusing(x):
 class Bottleneck(nn.Module):
     expansion = 4
 
-    def __init__(self, cin, width, stride=1):
+    def __init__(self, cin, width, stride=1, zero_init_residual=False):
         super().__init__()
         cout = width * self.expansion
         self.conv1 = ConvBN(cin, width, 1)
         self.conv2 = ConvBN(width, width, 3, stride=stride, pad=1)
-        self.conv3 = ConvBN(width, cout, 1, relu=True, zero_gamma=False)
+        self.conv3 = ConvBN(width, cout, 1, relu=True, zero_gamma=zero_init_residual)
         self.down = ConvBN(cin, cout, 1, stride=stride, relu=False) if (stride != 1 or cin != cout) else None
 
     def forward(self, x, prod=None):
@@ -97,10 +97,10 @@ class Bottleneck(nn.Module):
 class BasicBlock(nn.Module):
     expansion = 1
 
-    def __init__(self, cin, width, stride=1):
+    def __init__(self, cin, width, stride=1, zero_init_residual=False):
         super().__init__()
         self.conv1 = ConvBN(cin, width, 3, stride=stride, pad=1)
-        self.conv2 = ConvBN(width, width, 3, pad=1, relu=True)
+        self.conv2 = ConvBN(width, width, 3, pad=1, relu=True, zero_gamma=zero_init_residual)
         self.down = ConvBN(cin, width, 1, stride=stride, relu=False) if (stride != 1 or cin != width) else None
 
     def forward(self, x, prod=None):
@@ -142,7 +142,9 @@ class Dense(nn.Module):
 
 
 class ResNet(nn.Module):
-    def __init__(self, block, layers, num_classes=1000, width=64, in_channels=3):
+    def __init__(self, block, layers, num_classes=1000, width=64, in_channels=3, zero_init_residual=False):
+        """``zero_init_residual``: the last BN gamma of every residual block starts at 0 (each block
+        is the identity at init; the standard large-batch ImageNet recipe)."""
         super().__init__()
         self.in_channels = in_channels
         self.cin_pad = 4 if in_channels <= 4 else ops.ceil8(in_channels)
@@ -153,7 +155,8 @@ class ResNet(nn.Module):
             w = width * (2 ** i)
             blocks = []
             for j in range(n):
-                blocks.append(block(cin, w, stride=(2 if (j == 0 and i > 0) else 1)))
+                blocks.append(block(cin, w, stride=(2 if (j == 0 and i > 0) else 1),
+                                    zero_init_residual=zero_init_residual))
                 cin = w * block.expansion
             stages.append(nn.Sequential(*blocks))
         self.stages = nn.Sequential(*stages)

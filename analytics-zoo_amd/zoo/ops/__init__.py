@@ -4,7 +4,7 @@ GPU tensors run on the native kernels in ``zoo._C`` (fail loudly if missing);
 CPU tensors run on PyTorch reference implementations (used by the CPU test
 suite and as numerics oracles).
 """
-from zoo.ops._native import native, available
+from zoo.ops._native import native, available, set_deterministic, deterministic
 from zoo.ops.conv import conv2d_nhwc, linear, pack_weight, unpack_weight, ceil8, conv_out_size
 from zoo.ops.bn import conv_bn_act, batch_norm_nhwc, GradHandoff, BNProducer
 from zoo.ops.pool import max_pool2d_nhwc, global_avg_pool_nhwc

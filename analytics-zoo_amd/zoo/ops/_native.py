@@ -49,3 +49,15 @@ def available():
 
 def on_gpu(t):
     return t is not None and t.is_cuda
+
+
+def set_deterministic(on=True):
+    """Bit-reproducible reductions on the conv / BN / loss path:
+    every cross-workgroup float sum goes through per-workgroup partials folded in
+    a fixed order instead of fp32 atomics. Also set by ``ZOO_DETERMINISTIC=1``."""
+    native().set_deterministic(bool(on))
+
+
+def deterministic():
+    m = _load()
+    return bool(m.get_deterministic()) if m is not None else False
