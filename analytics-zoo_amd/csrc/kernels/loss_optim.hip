@@ -320,6 +320,39 @@ extern "C" hipError_t zoo_f32_to_bf16(const float* x, void* y, size_t n, hipStre
   return hipGetLastError();
 }
 
+// Reduce-scatter epilogue of the all-to-all gradient exchange (zoo/parallel/ddp.py): rank r
+// received chunk r of every peer's bf16 bucket, recv = [nchunks][cb]; the sum is accumulated in
+// fp32 (one bf16 rounding per input instead of one per ring hop) and written as fp32 (sharded
+// optimizer input) and/or bf16 (the all-gather payload). 8 elements per thread, cb % 8 == 0.
+__global__ __launch_bounds__(256) void sum_chunks_bf16_kernel(const bf16_t* __restrict__ recv, int nchunks,
+                                                             size_t cb, float* __restrict__ out32,
+                                                             bf16_t* __restrict__ out16, float scale) {
+  const size_t n8 = cb / 8;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < nchunks; ++c) {
+      float v[8];
+      unpack8(reinterpret_cast<const uint4*>(recv + (size_t)c * cb)[i], v);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] += v[e];
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= scale;
+    if (out32) {
+      reinterpret_cast<float4*>(out32)[2 * i] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+      reinterpret_cast<float4*>(out32)[2 * i + 1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+    if (out16) reinterpret_cast<uint4*>(out16)[i] = pack8(acc);
+  }
+}
+
+extern "C" hipError_t zoo_sum_chunks_bf16(const void* recv, int nchunks, size_t cb, float* out32, void* out16,
+                                          float scale, hipStream_t st) {
+  hipLaunchKernelGGL(sum_chunks_bf16_kernel, dim3(egrid(cb / 8)), dim3(256), 0, st, (const bf16_t*)recv, nchunks, cb,
+                     out32, (bf16_t*)out16, scale);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t zoo_add_bf16(const void* a, const void* b, void* y, size_t n, hipStream_t st) {
   hipLaunchKernelGGL(add_bf16_kernel, dim3(egrid(n / 8)), dim3(256), 0, st, (const bf16_t*)a, (const bf16_t*)b,
                      (bf16_t*)y, n / 8);

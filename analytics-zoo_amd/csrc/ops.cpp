@@ -56,6 +56,7 @@ hipError_t zoo_dropout_add(const void*, const void*, void*, size_t, float, uint6
 hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
+hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, hipStream_t);
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
@@ -606,6 +607,33 @@ void bf16_to_f32(torch::Tensor x, torch::Tensor y, bool accumulate) {
   check_hip(zoo_bf16_to_f32(x.data_ptr(), y.data_ptr<float>(), x.numel(), accumulate, cur_stream()), "bf16_to_f32");
 }
 
+// out32 / out16 [cb] = scale * sum_c recv[c][:] with fp32 accumulation (recv bf16 [nchunks * cb])
+void sum_chunks_bf16(torch::Tensor recv, int64_t nchunks, c10::optional<torch::Tensor> out32,
+                     c10::optional<torch::Tensor> out16, double scale) {
+  req(recv, at::kBFloat16, "recv");
+  TORCH_CHECK(nchunks >= 1 && recv.numel() % nchunks == 0, "sum_chunks_bf16: recv not divisible into chunks");
+  const int64_t cb = recv.numel() / nchunks;
+  TORCH_CHECK(cb % 8 == 0, "sum_chunks_bf16: chunk must be a multiple of 8");
+  check_al16(recv.data_ptr(), "recv");
+  float* o32 = nullptr;
+  void* o16 = nullptr;
+  if (out32.has_value() && out32->defined()) {
+    req(*out32, at::kFloat, "out32");
+    TORCH_CHECK(out32->numel() == cb, "out32 size");
+    check_al16(out32->data_ptr(), "out32");
+    o32 = out32->data_ptr<float>();
+  }
+  if (out16.has_value() && out16->defined()) {
+    req(*out16, at::kBFloat16, "out16");
+    TORCH_CHECK(out16->numel() == cb, "out16 size");
+    check_al16(out16->data_ptr(), "out16");
+    o16 = out16->data_ptr();
+  }
+  TORCH_CHECK(o32 || o16, "sum_chunks_bf16: no output");
+  check_hip(zoo_sum_chunks_bf16(recv.data_ptr(), (int)nchunks, (size_t)cb, o32, o16, (float)scale, cur_stream()),
+            "sum_chunks_bf16");
+}
+
 void f32_to_bf16(torch::Tensor x, torch::Tensor y) {
   req(x, at::kFloat, "x");
   req(y, at::kBFloat16, "y");
@@ -1084,6 +1112,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("nchw_to_nhwc", &nchw_to_nhwc);
   m.def("bf16_to_f32", &bf16_to_f32);
   m.def("f32_to_bf16", &f32_to_bf16);
+  m.def("sum_chunks_bf16", &sum_chunks_bf16);
   m.def("add_bf16", &add_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd);

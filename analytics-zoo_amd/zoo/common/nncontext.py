@@ -42,6 +42,9 @@ class ZooConfig:
     failure_retry_times: int = 5
     failure_retry_interval_s: float = 120.0
     fault_inject_step: int = -1          # ZOO_FAULT_INJECT_STEP: raise at this iteration (tests the retry path)
+    fault_inject_rank: int = -1          # ZOO_FAULT_INJECT_RANK: only this rank raises (-1: every rank)
+    auto_resume: bool = False            # ZOO_AUTO_RESUME: fit() resumes from the latest checkpoint (launcher restarts)
+    force_comm: bool = False             # ZOO_FORCE_COMM: run the collective path on a world-size-1 process group
     # data
     num_workers: int = 4
     pin_memory: bool = True
@@ -61,6 +64,8 @@ class ZooConfig:
         "grad_compression": "ZOO_GRAD_COMPRESSION",
         "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
         "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
+        "fault_inject_rank": "ZOO_FAULT_INJECT_RANK", "auto_resume": "ZOO_AUTO_RESUME",
+        "force_comm": "ZOO_FORCE_COMM",
         "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",
         "phase_timing": "ZOO_PHASE_TIMING", "debug_sync": "ZOO_DEBUG_SYNC", "deterministic": "ZOO_DETERMINISTIC",
         "backend": "ZOO_DIST_BACKEND", "timeout_s": "ZOO_DIST_TIMEOUT",
@@ -182,6 +187,17 @@ def init_nncontext(conf=None, redirect_spark_log=True, app_name=None, **kw):
     else:
         device = torch.device("cpu")
     group = None
+    if world == 1 and cfg.force_comm:
+        # one-rank process group (RCCL on a GPU): exercises the bucketed / overlapped collective
+        # path of the data-parallel engine on a single device; an in-memory store needs no network
+        import torch.distributed as dist
+        if not dist.is_initialized():
+            backend = cfg.backend or ("nccl" if use_gpu else "gloo")
+            dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                                    device_id=device if use_gpu else None)
+            cfg.backend = backend
+        else:
+            cfg.backend = dist.get_backend()
     if world > 1:
         import torch.distributed as dist
         if not dist.is_initialized():

@@ -91,6 +91,8 @@ def _shard(n, world, rank):
 
 
 class ColumnParallelLinear(nn.Module):
+    tensor_parallel = True  # TrainingEngine: data-parallel sync only over replicas of this shard
+
     def __init__(self, in_features, out_features, bias=True, gather_output=False, group=None, init_weight=None,
                  init_bias=None, activation=None):
         super().__init__()
@@ -112,6 +114,8 @@ class ColumnParallelLinear(nn.Module):
 
 
 class RowParallelLinear(nn.Module):
+    tensor_parallel = True
+
     def __init__(self, in_features, out_features, bias=True, input_is_parallel=True, group=None, init_weight=None,
                  init_bias=None):
         super().__init__()

@@ -40,6 +40,48 @@ class InjectedFault(RuntimeError):
     pass
 
 
+class CommFailure(RuntimeError):
+    """A collective failed (RCCL/gloo error or timeout). The process group cannot be
+    trusted any more: the engine exits non-zero so the launcher (torchrun
+    ``--max-restarts``) restarts every rank, which then auto-resume from the latest
+    checkpoint (``ZooConfig.auto_resume``)."""
+
+
+class CoordinatedFailure(RuntimeError):
+    """Every rank agreed that some rank failed locally: all of them reload the
+    latest checkpoint together (Topology.scala:1229-1262 retry, made collective)."""
+
+
+def _tp_groups(model):
+    """Process group of the tensor-parallel layers in ``model`` (None if none)."""
+    groups = {id(m.group): m.group for m in model.modules() if getattr(m, "tensor_parallel", False)}
+    if not groups:
+        return None, False
+    if len(groups) > 1:
+        raise ValueError("TrainingEngine: tensor-parallel layers must share one process group")
+    return next(iter(groups.values())), True
+
+
+def data_parallel_group(model):
+    """The data-parallel group for a model with tensor-parallel layers: the ranks
+    holding the SAME shard (same TP rank), TP groups being contiguous rank blocks.
+    Without TP layers: None (the world)."""
+    import torch.distributed as dist
+    tpg, has_tp = _tp_groups(model)
+    if not has_tp or not (dist.is_available() and dist.is_initialized()):
+        return None
+    world = dist.get_world_size()
+    tp = dist.get_world_size(tpg)
+    if world % tp:
+        raise ValueError("world size %d is not a multiple of the tensor-parallel size %d" % (world, tp))
+    mine = None
+    for t in range(tp):  # every rank creates every group, in the same order
+        g = dist.new_group(list(range(t, world, tp)))
+        if dist.get_rank() % tp == t:
+            mine = g
+    return mine
+
+
 class _Phases:
     """roctx ranges (``torch.cuda.nvtx`` is roctx on ROCm: visible with
     ``rocprofv3 --marker-trace``) and optional device-side phase timings with
@@ -103,7 +145,7 @@ def _move(batch, device, non_blocking=True):
 
 class TrainingEngine:
     def __init__(self, model, criterion, optim_method, device=None, ctx=None, clip=None, sharded=None,
-                 bucket_mb=None, model_forward=None, hip_graph=None):
+                 bucket_mb=None, model_forward=None, hip_graph=None, dp_group=None):
         from zoo.common.nncontext import get_nncontext
         self.ctx = ctx or get_nncontext()
         cfg = self.ctx.config
@@ -113,10 +155,13 @@ class TrainingEngine:
         self.optim = optim_method
         self.flat = FlatParams(list(self.model.parameters()), device=self.device,
                                bf16_copy=self.device.type == "cuda")
-        self.sync = GradSync(self.flat, bucket_mb=bucket_mb or cfg.bucket_mb,
+        self.dp_group = dp_group if dp_group is not None else data_parallel_group(self.model)
+        self.sync = GradSync(self.flat, group=self.dp_group, bucket_mb=bucket_mb or cfg.bucket_mb,
                              mode="sharded" if (cfg.sharded_optimizer if sharded is None else sharded)
-                             else "allreduce", overlap=cfg.overlap_comm, compress=cfg.grad_compression or None)
-        self.sync.broadcast_parameters(0)
+                             else "allreduce", overlap=cfg.overlap_comm, compress=cfg.grad_compression or None,
+                             force_comm=cfg.force_comm)
+        self.sync.broadcast_parameters()
+        self._local_failure = None
         self.clip = clip
         self.forward_fn = model_forward or (lambda m, x: m(x))
         self.state = {"epoch": 1, "neval": 1, "Loss": float("nan"), "score": None, "records": 0}
@@ -138,20 +183,52 @@ class TrainingEngine:
         self._graph_warm = {}
 
     # ------------------------------------------------------------------
-    def train_step(self, inputs, target):
-        """One synchronous-DP iteration. Returns the (device) loss tensor."""
-        if self.fault_step >= 0 and self.state["neval"] == self.fault_step and not self._fault_fired:
+    def _maybe_inject_fault(self):
+        cfg = self.ctx.config
+        if self.fault_step >= 0 and self.state["neval"] == self.fault_step and not self._fault_fired and \
+                (cfg.fault_inject_rank < 0 or cfg.fault_inject_rank == self.ctx.rank):
             self._fault_fired = True
             raise InjectedFault("injected fault at iteration %d" % self.fault_step)
+
+    def train_step(self, inputs, target):
+        """One synchronous-DP iteration. Returns the (device) loss tensor.
+
+        Multi-rank failure protocol: an exception in this rank's forward/backward
+        does not leave the other ranks blocked in a collective. The rank turns into
+        a "zombie" that keeps taking part in every collective with a zero gradient
+        until the next agreement point (:meth:`flush_loss`, checkpoints), where all
+        ranks learn of the failure together and reload the latest checkpoint.
+        A failing collective raises :class:`CommFailure` (restart by the launcher)."""
+        multi = self.sync.comm and self.sync.world > 1
         self.model.train()
         ph = self.phases
-        with ph.range("fwd_bwd"):
-            if self.hip_graph and torch.is_tensor(target):
-                loss = self._graph_fwd_bwd(inputs, target)
-            else:
-                loss = self._fwd_bwd(inputs, target)
+        loss = None
+        if self._local_failure is None:
+            try:
+                self._maybe_inject_fault()
+                with ph.range("fwd_bwd"):
+                    if self.hip_graph and torch.is_tensor(target):
+                        loss = self._graph_fwd_bwd(inputs, target)
+                    else:
+                        loss = self._fwd_bwd(inputs, target)
+            except (ValueError, KeyboardInterrupt):
+                raise
+            except Exception as e:  # noqa: BLE001
+                if not multi:
+                    raise
+                log.warning("rank %d: step failed (%s); continuing with zero gradients until the ranks agree",
+                            self.ctx.rank, e)
+                self._local_failure = e
+        if loss is None:  # zombie step: contribute nothing, stay in lock-step
+            self.flat.grad.zero_()
+            loss = torch.zeros((), device=self.device)
         with ph.range("comm_optim"):
-            self.sync.step(self.optim, self.clip)
+            try:
+                self.sync.step(self.optim, self.clip)
+            except Exception as e:  # noqa: BLE001
+                if multi and not isinstance(e, (ValueError, KeyboardInterrupt)):
+                    raise CommFailure("gradient synchronisation failed on rank %d: %s" % (self.ctx.rank, e)) from e
+                raise
         self.state["neval"] += 1
         if self.debug_sync:  # debug mode: surface asynchronous HIP errors / divergence at the failing step
             if self.device.type == "cuda":
@@ -234,13 +311,20 @@ class TrainingEngine:
         log_every = log_every or self.ctx.config.log_every
         cfg = self.ctx.config
         retries = []
+        if cfg.auto_resume and self.latest_checkpoint() is not None and self.state["neval"] == 1:
+            log.info("auto-resume from %s", self.latest_checkpoint())
+            self.load_checkpoint(self.latest_checkpoint())
+        multi = self.sync.comm and self.sync.world > 1
         while True:
             try:
                 self._fit_loop(data, end_trigger, validation, val_methods, val_trigger, log_every, callbacks)
+                self.flush_loss()  # final agreement point
                 break
-            except (ValueError, KeyboardInterrupt):
+            except (ValueError, KeyboardInterrupt, CommFailure):
                 raise
             except Exception as e:  # noqa: BLE001 - mirrors Topology.scala:1229 catch Throwable
+                if multi and not isinstance(e, CoordinatedFailure):
+                    raise  # a local failure outside train_step: no safe way to keep the ranks in step
                 now = time.time()
                 retries = [t for t in retries if now - t < cfg.failure_retry_interval_s] + [now]
                 ck = self.latest_checkpoint()
@@ -248,7 +332,10 @@ class TrainingEngine:
                     raise
                 log.warning("training failed (%s); retry %d/%d from checkpoint %s", e, len(retries),
                             cfg.failure_retry_times, ck)
+                self._local_failure = None
+                self._pending_loss = []
                 self.load_checkpoint(ck)
+        self.sync.sync_master()
         return self
 
     def _iter_epoch(self, data):
@@ -312,12 +399,22 @@ class TrainingEngine:
     def flush_loss(self):
         """Bring the device-side per-iteration losses to the host (one sync),
         average over ranks (one all-reduce) and log them to TensorBoard."""
-        if not self._pending_loss:
+        multi = self.sync.comm and self.sync.world > 1
+        if not self._pending_loss and not multi:
             return self.state["Loss"]
         its = [i for i, _ in self._pending_loss]
-        vals = torch.stack([l.float().reshape(()) for _, l in self._pending_loss])
-        red = self.sync.all_reduce_scalars(vals.detach().cpu().tolist()) / self.sync.world
+        vals = torch.stack([l.float().reshape(()) for _, l in self._pending_loss]) if self._pending_loss \
+            else torch.zeros(0)
+        # the failure flag rides in the same all-reduce as the losses (no extra collective)
+        red = self.sync.all_reduce_scalars(vals.detach().cpu().tolist() + [1.0 if self._local_failure else 0.0])
         self._pending_loss = []
+        if red[-1] > 0:
+            cause = self._local_failure
+            raise CoordinatedFailure("%d rank(s) failed before iteration %d%s" % (
+                int(red[-1]), self.state["neval"] - 1, (": %s" % cause) if cause else ""))
+        red = red[:-1] / self.sync.world
+        if not its:
+            return self.state["Loss"]
         if self.train_summary is not None:
             for it, v in zip(its, red.tolist()):
                 self.train_summary.add_scalar("Loss", v, it)
@@ -368,21 +465,35 @@ class TrainingEngine:
         self.checkpoint_overwrite = overwrite
         os.makedirs(path, exist_ok=True)
 
+    def _sharded(self):
+        return self.sync.mode == "sharded" and self.sync.comm
+
     def save_checkpoint(self):
-        if self.checkpoint_path is None or self.ctx.rank != 0:
-            if self.sync.world > 1:
-                self.ctx.barrier()
+        """``model<suffix>`` (rank 0) + ``optimMethod-<name><suffix>``; with the ZeRO-1
+        sharded optimizer every rank writes its own state shard as
+        ``optimMethod-<name><suffix>.rank<r>``. Collective: every rank calls it."""
+        if self.checkpoint_path is None:
             return
+        multi = self.sync.comm and self.sync.world > 1
+        if multi:
+            self.flush_loss()  # agreement point: never checkpoint a state a failed rank diverged from
+        self.sync.sync_master()
         from zoo.utils.checkpoint import save_object
         it = self.state["neval"] - 1
         suffix = "" if self.checkpoint_overwrite else ".%d" % it
         name = type(self.optim).__name__
-        save_object({"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
-                     "engine_state": dict(self.state), "neval": it},
-                    os.path.join(self.checkpoint_path, "model" + suffix), True)
-        save_object(self.optim.state_dict(), os.path.join(self.checkpoint_path, "optimMethod-%s%s" % (name, suffix)),
-                    True)
-        if self.sync.world > 1:
+        opath = os.path.join(self.checkpoint_path, "optimMethod-%s%s" % (name, suffix))
+        if self._sharded():
+            save_object(self.optim.state_dict(), "%s.rank%d" % (opath, self.sync.rank), True)
+        if self.ctx.rank == 0:
+            if not self._sharded():
+                save_object(self.optim.state_dict(), opath, True)
+            # the model file goes last: latest_checkpoint() only sees complete checkpoints
+            save_object({"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
+                         "engine_state": dict(self.state), "neval": it,
+                         "world": self.sync.world, "sharded": self._sharded()},
+                        os.path.join(self.checkpoint_path, "model" + suffix), True)
+        if multi:
             self.ctx.barrier()
 
     def save_flat_checkpoint(self, path):
@@ -431,6 +542,7 @@ class TrainingEngine:
         return max(cands, key=os.path.getmtime)
 
     def load_checkpoint(self, model_file):
+        """Collective in multi-rank runs (every rank loads, then one broadcast)."""
         from zoo.utils.checkpoint import load_object
         d = load_object(model_file)
         self.model.load_state_dict(d["model"])
@@ -439,8 +551,16 @@ class TrainingEngine:
         suffix = os.path.basename(model_file)[len("model"):]
         name = type(self.optim).__name__
         opath = os.path.join(os.path.dirname(model_file), "optimMethod-%s%s" % (name, suffix))
-        if os.path.exists(opath):
+        if self._sharded():
+            if d.get("world", self.sync.world) != self.sync.world:
+                log.warning("checkpoint written by %s ranks, running on %d: optimizer state shards reset",
+                            d.get("world"), self.sync.world)
+                self.optim.clear_history()
+            elif os.path.exists("%s.rank%d" % (opath, self.sync.rank)):
+                self.optim.load_state_dict(load_object("%s.rank%d" % (opath, self.sync.rank)))
+                self.optim.to(self.device)
+        elif os.path.exists(opath):
             self.optim.load_state_dict(load_object(opath))
             self.optim.to(self.device)
-        self.sync.broadcast_parameters(0)
+        self.sync.broadcast_parameters()
         self.sync.reset()

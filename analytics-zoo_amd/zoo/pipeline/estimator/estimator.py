@@ -45,6 +45,15 @@ class MultiOptimMethod:
                 o.step(master[a:b], grad[a:b], None if bf16 is None else bf16[a:b], gscale)
         self.state["neval"] += 1
 
+    def step_ranges(self, ranges, master, grad, bf16=None, gscale=1.0):
+        """ZeRO-1 shard update: ``ranges`` = [((lo, hi) in shard coordinates or None, optim)]."""
+        for r, o in ranges:
+            if r is None:
+                continue
+            a, b = r
+            o.step(master[a:b], grad[a:b], None if bf16 is None else bf16[a:b], gscale)
+        self.state["neval"] += 1
+
     def current_lr(self):
         return self.parts[0][1].current_lr() if self.parts else 0.0
 

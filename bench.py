@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "ncf"])
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer (BigDL AllReduceParameter)")
+    ap.add_argument("--force-comm", action="store_true",
+                    help="run the bucketed RCCL path even at world size 1 (implied by --sharded)")
+    ap.add_argument("--grad-compression", default="", choices=["", "bf16"])
     ap.add_argument("--profile-steps", type=int, default=0)
     return ap.parse_args()
 
@@ -93,7 +96,8 @@ def build_ncf(ctx, batch):
 def main():
     a = parse()
     from zoo.common.nncontext import init_nncontext
-    ctx = init_nncontext("bench", sharded_optimizer=a.sharded)
+    ctx = init_nncontext("bench", sharded_optimizer=a.sharded, force_comm=a.force_comm or a.sharded,
+                         grad_compression=a.grad_compression)
     world = ctx.world_size
     if a.model == "resnet50":
         batch = a.batch
@@ -136,7 +140,8 @@ def main():
             "dtype": "bf16", "data": "synthetic (random-init weights, random inputs/labels)",
             "config": dict({"model": model_name, "global_batch": batch * world, "per_gpu_batch": batch,
                             "seq_len": None, "parallelism": "dp%d" % world,
-                            "grad_sync": "sharded(ZeRO-1)" if a.sharded else "allreduce(bucketed,overlapped)"},
+                            "grad_sync": ("sharded(ZeRO-1)" if a.sharded else "allreduce(bucketed,overlapped)") +
+                            ("+bf16-wire" if a.grad_compression else "")},
                            **extra),
             "first_loss": round(float(first_loss.float().item()), 4) if first_loss is not None else None,
             "final_loss": round(final_loss, 4),

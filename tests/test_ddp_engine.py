@@ -1,0 +1,268 @@
+"""Data-parallel engine correctness (round 2): shared-parameter bucket launch,
+ZeRO-1 with per-part optimizers and 16-bit wire format, per-rank sharded
+checkpoints, cross-rank failure agreement, tensor parallelism through the engine.
+All multi-rank cases run over gloo with world_size 2 (CPU)."""
+import multiprocessing as mp
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _mlp(seed=0):
+    torch.manual_seed(seed)
+    return nn.Sequential(nn.Linear(6, 16), nn.Tanh(), nn.Linear(16, 8), nn.Tanh(), nn.Linear(8, 1))
+
+
+def _toy(n=64, seed=1):
+    r = np.random.RandomState(seed)
+    x = r.randn(n, 6).astype(np.float32)
+    y = (np.sin(x[:, :1]) + 0.1 * x[:, 1:2]).astype(np.float32)
+    return x, y
+
+
+def _init(rank, world, port, **env):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    for k, v in env.items():
+        os.environ[k] = str(v)
+    import zoo.common.nncontext as nc
+    nc._CTX = None
+    return nc.init_nncontext(backend="gloo")
+
+
+def _run(target, *args, world=2, timeout=240):
+    ctx_mp = mp.get_context("spawn")
+    q = ctx_mp.Queue()
+    port = _free_port()
+    procs = [ctx_mp.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = dict(q.get(timeout=timeout) for _ in range(world))
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    return res
+
+
+# ---------------------------------------------------------------------------
+# shared parameters: a bucket launches only after the LAST contribution
+# ---------------------------------------------------------------------------
+def test_shared_parameter_bucket_waits_for_every_contribution():
+    import torch.distributed as dist
+    from zoo.parallel.ddp import GradSync
+    from zoo.parallel.flat import FlatParams
+    dist.init_process_group("gloo", store=dist.HashStore(), rank=0, world_size=1)
+    try:
+        lin, other = nn.Linear(4, 4), nn.Linear(4, 2)
+        flat = FlatParams(list(lin.parameters()) + list(other.parameters()))
+        sync = GradSync(flat, bucket_mb=1.0, force_comm=True)
+        sync.overlap = True  # the CPU path is synchronous; drive the launch logic directly
+        launches = []
+        sync._issue = lambda b: launches.append(b.idx)
+        assert len(sync.buckets) == 1
+
+        def backward_pass():
+            # lin.weight is used twice (a shared layer): two contributions
+            for p in (other.weight, other.bias, lin.weight, lin.bias, lin.weight):
+                sync._ready(p)
+        backward_pass()                     # calibration step: nothing launches early
+        assert launches == []
+        sync.finish()
+        assert launches == [0]
+        sync.reset()
+        launches.clear()
+        for p in (other.weight, other.bias, lin.weight, lin.bias):
+            sync._ready(p)
+        assert launches == [], "bucket launched before the shared weight's second contribution"
+        sync._ready(lin.weight)
+        assert launches == [0]
+        sync.finish()                       # nothing left to launch
+        assert launches == [0]
+        sync.reset()
+        # a step with MORE contributions than calibrated after the launch must fail loudly
+        launches.clear()
+        for p in (other.weight, other.bias, lin.weight, lin.bias, lin.weight):
+            sync._ready(p)
+        with pytest.raises(RuntimeError, match="calibration"):
+            sync._ready(lin.weight)
+    finally:
+        dist.destroy_process_group()
+
+
+# ---------------------------------------------------------------------------
+# ZeRO-1: per-submodule optimizers and the bf16 all-to-all wire format
+# ---------------------------------------------------------------------------
+def _zero1_worker(rank, world, port, q, compress, multi):
+    ctx = _init(rank, world, port, ZOO_GRAD_COMPRESSION=compress)
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD, Adam
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.pipeline.estimator.estimator import MultiOptimMethod
+    x, y = _toy(64)
+    m = _mlp(seed=0)
+    eng = TrainingEngine(m, MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9), ctx=ctx, sharded=True,
+                         bucket_mb=0.0003)
+    if multi:
+        from zoo.pipeline.estimator.estimator import _resolve_optim
+        eng.optim = _resolve_optim(m, {"0": Adam(lr=0.01), "2": SGD(learningrate=0.1), "4": SGD(learningrate=0.05)},
+                                   eng.flat)
+        assert isinstance(eng.optim, MultiOptimMethod)
+    for step in range(4):
+        sl = slice(rank * 8 + step * 16, rank * 8 + step * 16 + 8)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    eng.sync.sync_master()
+    q.put((rank, eng.flat.master.detach().numpy().copy()))
+    ctx.stop()
+
+
+@pytest.mark.parametrize("compress,multi", [("", True), ("bf16", False), ("bf16", True)])
+def test_zero1_matches_single_process(compress, multi):
+    res = _run(_zero1_worker, compress, multi)
+    r0, r1 = torch.from_numpy(res[0]), torch.from_numpy(res[1])
+    assert torch.allclose(r0, r1, atol=1e-6), "ranks diverged"
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD, Adam
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.pipeline.estimator.estimator import _resolve_optim
+    x, y = _toy(64)
+    m = _mlp(seed=0)
+    eng = TrainingEngine(m, MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9))
+    if multi:
+        eng.optim = _resolve_optim(m, {"0": Adam(lr=0.01), "2": SGD(learningrate=0.1), "4": SGD(learningrate=0.05)},
+                                   eng.flat)
+    for step in range(4):
+        sl = slice(step * 16, step * 16 + 16)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    tol = 2e-2 * eng.flat.master.abs().max() if compress else 1e-5
+    assert (r0 - eng.flat.master).abs().max() < tol
+
+
+# ---------------------------------------------------------------------------
+# per-rank ZeRO-1 optimizer shards in checkpoints: resume == uninterrupted
+# ---------------------------------------------------------------------------
+def _ckpt_worker(rank, world, port, q, path):
+    ctx = _init(rank, world, port)
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(128)
+
+    def batch(step):
+        sl = slice(rank * 8 + step * 16, rank * 8 + step * 16 + 8)
+        return torch.from_numpy(x[sl]), torch.from_numpy(y[sl])
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), Adam(lr=0.02), ctx=ctx, sharded=True, bucket_mb=0.0003)
+    for s in range(3):
+        eng.train_step(*batch(s))
+    eng.set_checkpoint(path)
+    eng.save_checkpoint()
+    for s in range(3, 6):
+        eng.train_step(*batch(s))
+    eng.sync.sync_master()
+    a = eng.flat.master.detach().numpy().copy()
+    files = sorted(os.listdir(path))
+    # a fresh engine (different init) resumes from the checkpoint
+    eng2 = TrainingEngine(_mlp(seed=7), MeanSquaredError(), Adam(lr=0.02), ctx=ctx, sharded=True, bucket_mb=0.0003)
+    eng2.set_checkpoint(path)
+    eng2.load_checkpoint(eng2.latest_checkpoint())
+    for s in range(3, 6):
+        eng2.train_step(*batch(s))
+    eng2.sync.sync_master()
+    q.put((rank, (a, eng2.flat.master.detach().numpy().copy(), files)))
+    ctx.stop()
+
+
+def test_zero1_checkpoint_saves_every_rank_shard(tmp_path):
+    res = _run(_ckpt_worker, str(tmp_path / "ck"))
+    for r in (0, 1):
+        a, b, files = res[r]
+        np.testing.assert_allclose(a, b, rtol=0, atol=1e-6)
+    files = res[0][2]
+    assert "optimMethod-Adam.rank0" in files and "optimMethod-Adam.rank1" in files and "model" in files
+
+
+# ---------------------------------------------------------------------------
+# a local failure on ONE rank: all ranks agree and reload together (no hang)
+# ---------------------------------------------------------------------------
+def _fail_worker(rank, world, port, q, path):
+    ctx = _init(rank, world, port, ZOO_FAULT_INJECT_STEP=5, ZOO_FAULT_INJECT_RANK=1)
+    from zoo.common import triggers as T
+    from zoo.feature.common import FeatureSet
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(128)
+    xs, ys = x[rank::2], y[rank::2]
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), SGD(learningrate=0.05), ctx=ctx, bucket_mb=0.0003)
+    eng.set_checkpoint(path, T.SeveralIteration(2))
+    eng.fit(FeatureSet.from_ndarrays(xs, ys, 8), end_trigger=T.MaxIteration(12), log_every=3)
+    q.put((rank, (eng.flat.master.detach().numpy().copy(), eng._fault_fired, eng.state["neval"])))
+    ctx.stop()
+
+
+def test_failure_on_one_rank_is_agreed_and_retried(tmp_path):
+    res = _run(_fail_worker, str(tmp_path / "ck"))
+    (m0, f0, n0), (m1, f1, n1) = res[0], res[1]
+    assert f1 and not f0
+    assert n0 == n1 >= 12
+    np.testing.assert_allclose(m0, m1, rtol=0, atol=1e-6)
+
+
+# ---------------------------------------------------------------------------
+# tensor parallelism through the engine: shards are not averaged across TP ranks
+# ---------------------------------------------------------------------------
+def _tp_worker(rank, world, port, q):
+    ctx = _init(rank, world, port)
+    from zoo.parallel.tensor_parallel import ParallelMLP
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    g = torch.Generator().manual_seed(3)
+    w1, b1 = torch.randn(16, 6, generator=g) * 0.3, torch.randn(16, generator=g) * 0.1
+    w2, b2 = torch.randn(6, 16, generator=g) * 0.3, torch.randn(6, generator=g) * 0.1
+    mlp = ParallelMLP(6, 16, activation="relu", fc1=(w1, b1), fc2=(w2, b2))
+    eng = TrainingEngine(mlp, MeanSquaredError(), SGD(learningrate=0.1), ctx=ctx)
+    assert eng.sync.world == 1  # DP group: this rank alone (TP spans the world)
+    x = torch.randn(8, 6, generator=g)
+    y = torch.randn(8, 6, generator=g)
+    for _ in range(3):
+        eng.train_step(x, y)
+    q.put((rank, (mlp.fc1.weight.detach().numpy().copy(), mlp.fc2.weight.detach().numpy().copy(),
+                  mlp.fc2.bias.detach().numpy().copy())))
+    ctx.stop()
+
+
+def test_tensor_parallel_mlp_trains_through_engine():
+    res = _run(_tp_worker)
+    g = torch.Generator().manual_seed(3)
+    w1, b1 = torch.randn(16, 6, generator=g) * 0.3, torch.randn(16, generator=g) * 0.1
+    w2, b2 = torch.randn(6, 16, generator=g) * 0.3, torch.randn(6, generator=g) * 0.1
+    x = torch.randn(8, 6, generator=g)
+    y = torch.randn(8, 6, generator=g)
+    full = nn.Sequential(nn.Linear(6, 16), nn.ReLU(), nn.Linear(16, 6))
+    with torch.no_grad():
+        full[0].weight.copy_(w1); full[0].bias.copy_(b1); full[2].weight.copy_(w2); full[2].bias.copy_(b2)
+    opt = torch.optim.SGD(full.parameters(), lr=0.1)
+    for _ in range(3):
+        opt.zero_grad()
+        ((full(x) - y) ** 2).mean().backward()
+        opt.step()
+    fc1 = np.concatenate([res[0][0], res[1][0]], 0)
+    fc2 = np.concatenate([res[0][1], res[1][1]], 1)
+    np.testing.assert_allclose(fc1, full[0].weight.detach().numpy(), atol=1e-5)
+    np.testing.assert_allclose(fc2, full[2].weight.detach().numpy(), atol=1e-5)
+    np.testing.assert_allclose(res[0][2], full[2].bias.detach().numpy(), atol=1e-5)

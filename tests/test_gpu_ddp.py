@@ -1,0 +1,91 @@
+"""The data-parallel engine's collective path on a real GPU: a world-size-1 RCCL
+process group with ``force_comm`` runs the bucketed, comm-stream, event-ordered
+path (all_reduce / reduce_scatter_tensor / all_to_all_single /
+all_gather_into_tensor) and must reproduce the local (no-comm) step bit for bit
+under the deterministic reduction mode."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def rccl_world1():
+    import torch.distributed as dist
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from zoo.common.nncontext import init_nncontext
+    ctx = init_nncontext("ddp-test")
+    created = False
+    if not dist.is_initialized():
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1,
+                                device_id=torch.device("cuda", torch.cuda.current_device()))
+        created = True
+    yield ctx
+    if created:
+        dist.destroy_process_group()
+
+
+def _model():
+    from zoo.models.image.resnet import Bottleneck, ResNet
+    torch.manual_seed(3)
+    return ResNet(Bottleneck, [1, 1, 1, 1], num_classes=16, width=16)
+
+
+def _train(ctx, force, sharded=False, compress=None, steps=4):
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    old = (ctx.config.force_comm, ctx.config.grad_compression)
+    ctx.config.force_comm, ctx.config.grad_compression = force, compress or ""
+    try:
+        eng = TrainingEngine(_model(), softmax_cross_entropy, SGD(learningrate=0.05, momentum=0.9), ctx=ctx,
+                             sharded=sharded, bucket_mb=0.05)
+    finally:
+        ctx.config.force_comm, ctx.config.grad_compression = old
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0)
+    x = torch.randn(8, 3, 64, 64, device="cuda", generator=g)
+    y = torch.randint(0, 16, (8,), device="cuda", generator=g)
+    early = []
+    fin = eng.sync.finish
+
+    def finish():
+        early.append(sum(b.launched for b in eng.sync.buckets))
+        fin()
+    eng.sync.finish = finish
+    losses = [eng.train_step(x, y).float().item() for _ in range(steps)]
+    torch.cuda.synchronize()
+    eng.sync.sync_master()
+    return eng, losses, early
+
+
+@pytest.mark.parametrize("sharded", [False, True])
+def test_forced_comm_matches_local_bitwise(gpu, rccl_world1, sharded):
+    from zoo.ops import deterministic, set_deterministic
+    prev = deterministic()
+    set_deterministic(True)
+    try:
+        e0, l0, _ = _train(rccl_world1, force=False)
+        e1, l1, early = _train(rccl_world1, force=True, sharded=sharded)
+    finally:
+        set_deterministic(prev)
+    assert e1.sync.comm and len(e1.sync.buckets) > 2
+    assert early[0] == 0, "calibration step must not launch early"
+    assert max(early[1:]) > 0, "no bucket overlapped with backward"
+    assert l0 == l1
+    assert torch.equal(e0.flat.bf16, e1.flat.bf16)
+    assert torch.equal(e0.flat.master, e1.flat.master)
+
+
+def test_forced_comm_bf16_wire_tracks_fp32(gpu, rccl_world1):
+    e0, l0, _ = _train(rccl_world1, force=False)
+    e1, l1, _ = _train(rccl_world1, force=True, compress="bf16")
+    e2, l2, _ = _train(rccl_world1, force=True, sharded=True, compress="bf16")
+    for a, b, c in zip(l0, l1, l2):
+        assert abs(a - b) < 0.05 and abs(a - c) < 0.05
+    for e in (e1, e2):  # bf16 gradient rounding: a small relative perturbation of the update
+        d = (e0.flat.master - e.flat.master).norm() / e0.flat.master.norm()
+        assert d.item() < 0.01
