@@ -3,8 +3,8 @@ KerasZooModel.scala:32-183; Py/models/common/zoo_model.py).
 
 A ZooModel owns a Keras graph built by ``build_model()`` and exposes the
 KerasNet API (compile/fit/evaluate/predict/summary/save) by delegation.
-``save_model``/``load_model`` use the safe zoo-keras format (config + weights;
-loaded with ``torch.load(weights_only=True)``).
+``save_model``/``load_model`` write/read the reference's BigDL/Zoo ``.model``
+protobuf (zoo.utils.bigdl_model: constructor config + every tensor).
 """
 from zoo.pipeline.api.keras.engine.topology import KerasNet
 

@@ -1,6 +1,10 @@
 """Keras model persistence (KerasNet.saveModel / Net.load, Topology.scala:708-825).
 
-A saved model is ONE file written with ``torch.save`` that contains only
+``save_model`` writes the reference's BigDL/Zoo ``.model`` protobuf by default
+(zoo.utils.bigdl_model); ``load_model`` reads both that and the framework's
+torch-file format below.
+
+A torch-file model is ONE file written with ``torch.save`` that contains only
 primitives and tensors, so it is loaded back with ``torch.load(weights_only=True)``
 (nothing in the file is executed):
 
@@ -157,16 +161,26 @@ def build_graph(g, cls=None, name=None):
     return cls(ins if len(ins) > 1 else ins[0], outs if g["multi_out"] else outs[0], name=name)
 
 
-def save_model(model, path, over_write=False):
+def save_model(model, path, over_write=False, format="bigdl"):
+    """``format="bigdl"`` (default): the reference's BigDL/Zoo ``.model`` protobuf
+    (zoo.utils.bigdl_model); ``"zoo"``: the framework's torch-file config format."""
     import os
-    from zoo.utils.checkpoint import save_object
     if os.path.exists(path) and not over_write:
         raise FileExistsError("%s exists; pass over_write=True" % path)
+    if format == "bigdl":
+        from zoo.utils.bigdl_model import save_bigdl_model
+        save_bigdl_model(model, path, over_write=True)
+        return
+    from zoo.utils.checkpoint import save_object
     state = {k: v.detach().cpu() for k, v in model.state_dict().items()}
     save_object({"format": FORMAT, "arch": layer_config(model), "state": state}, path, True)
 
 
 def load_model(path):
+    """Reads both the BigDL/Zoo ``.model`` protobuf and the torch-file format."""
+    from zoo.utils.bigdl_model import is_bigdl_model_file, load_bigdl_model
+    if is_bigdl_model_file(path):
+        return load_bigdl_model(path)
     from zoo.utils.checkpoint import load_object
     d = load_object(path)
     if not isinstance(d, dict) or d.get("format") != FORMAT:

@@ -488,11 +488,15 @@ class TrainingEngine:
         if self.ctx.rank == 0:
             if not self._sharded():
                 save_object(self.optim.state_dict(), opath, True)
-            # the model file goes last: latest_checkpoint() only sees complete checkpoints
-            save_object({"model": {k: v.detach().cpu() for k, v in self.model.state_dict().items()},
-                         "engine_state": dict(self.state), "neval": it,
-                         "world": self.sync.world, "sharded": self._sharded()},
-                        os.path.join(self.checkpoint_path, "model" + suffix), True)
+            # the model file goes last: latest_checkpoint() only sees complete checkpoints. It is a
+            # BigDL/Zoo ``.model`` protobuf (Net.load / KerasNet.loadModel read it), with the engine
+            # counters as top-level attributes
+            import json as _json
+            from zoo.utils.bigdl_model import save_bigdl_model
+            eng = {k: v for k, v in self.state.items() if isinstance(v, (int, float, str, bool, type(None)))}
+            save_bigdl_model(self.model, os.path.join(self.checkpoint_path, "model" + suffix), True,
+                             extra_attr={"zoo_engine_state": _json.dumps(eng), "zoo_neval": int(it),
+                                         "zoo_world": int(self.sync.world), "zoo_sharded": bool(self._sharded())})
         if multi:
             self.ctx.barrier()
 
@@ -543,9 +547,16 @@ class TrainingEngine:
 
     def load_checkpoint(self, model_file):
         """Collective in multi-rank runs (every rank loads, then one broadcast)."""
+        import json as _json
+        from zoo.utils.bigdl_model import is_bigdl_model_file, load_bigdl_model, read_attr
         from zoo.utils.checkpoint import load_object
-        d = load_object(model_file)
-        self.model.load_state_dict(d["model"])
+        if is_bigdl_model_file(model_file):
+            load_bigdl_model(model_file, model=self.model)
+            d = {"engine_state": _json.loads(read_attr(model_file, "zoo_engine_state", "{}") or "{}"),
+                 "world": read_attr(model_file, "zoo_world", self.sync.world)}
+        else:  # round-1 torch-file checkpoints
+            d = load_object(model_file)
+            self.model.load_state_dict(d["model"])
         self.flat.refresh_bf16()
         self.state.update(d.get("engine_state", {}))
         suffix = os.path.basename(model_file)[len("model"):]

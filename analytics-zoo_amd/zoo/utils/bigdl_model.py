@@ -1,0 +1,620 @@
+"""BigDL / Analytics-Zoo ``.model`` protobuf files for zoo models: write and read.
+
+The reference persists every model (``KerasNet.saveModel``, ``Net.load``,
+``ZooModel.saveModel``, DistriOptimizer checkpoints ``model.<n>``) with BigDL's
+module serializer: one ``BigDLModule`` protobuf per module, the Zoo-Keras layer
+as the outer module (``com.intel.analytics.zoo.pipeline.api.keras.layers.X``,
+its constructor arguments as ``attr``) wrapping the BigDL ``nn`` module that
+does the work (the "labor") and owns the weights, all tensor data stored once
+in the top module's ``global_storage`` (Topology.scala:708-825, Net.scala:136-193,
+KerasLayerSerializer).
+
+This module writes that structure for the framework's Keras layers and reads it
+back, including the reference's own fixtures
+(zoo/src/test/resources/models/zoo_keras/small_seq.model, small_model.model):
+
+* known labors are written in BigDL layout: ``Linear`` (weight [out, in]),
+  ``SpatialConvolution`` (weight [nGroup, out, in, kH, kW]; the framework's
+  packed NHWC weight is converted), ``(Spatial)BatchNormalization`` (weight,
+  bias, runningMean/runningVar), ``LookupTable`` (weight [n, d]);
+* every other layer keeps its tensors as ``parameters`` of a generic labor with
+  the parameter names in ``attr["zoo_param_names"]``, so all layers round-trip;
+* a non-Keras ``nn.Module`` (e.g. the native ResNet used by the engine) is
+  written as a ``com.intel.analytics.zoo.pipeline.api.net.TorchModel`` whose
+  ``parameters`` are its state dict (named), which is how the training engine's
+  ``model.<n>`` checkpoints are stored.
+
+Decoding never executes anything from the file: it only builds classes of the
+``zoo`` package named by a fixed registry.
+"""
+import inspect
+import re
+
+import numpy as np
+import torch
+
+from zoo.utils import bigdl_proto as P
+from zoo.utils.protobuf import enc_bytes, enc_float, enc_int, enc_packed_floats, enc_packed_ints
+
+ZOO_KERAS = "com.intel.analytics.zoo.pipeline.api.keras.layers."
+ZOO_MODELS = "com.intel.analytics.zoo.pipeline.api.keras.models."
+BIGDL_NN = "com.intel.analytics.bigdl.nn."
+BIGDL_KERAS_INPUT = "com.intel.analytics.bigdl.nn.keras.Input"
+TORCH_MODEL = "com.intel.analytics.zoo.pipeline.api.net.TorchModel"
+ZOO_MODEL_PKG = "com.intel.analytics.zoo.models."
+VERSION = "0.5.0"
+
+# python-API argument name <-> reference (Scala) constructor attribute name where the
+# generic snake_case <-> camelCase rule does not apply
+_ALIASES = {"W_regularizer": "wRegularizer", "b_regularizer": "bRegularizer", "U_regularizer": "uRegularizer",
+            "input_shape": "inputShape", "bias": "bias"}
+_REV_ALIASES = {v: k for k, v in _ALIASES.items()}
+
+
+def _camel(name):
+    if name in _ALIASES:
+        return _ALIASES[name]
+    parts = name.split("_")
+    return parts[0] + "".join(p[:1].upper() + p[1:] for p in parts[1:])
+
+
+def _snake(name):
+    if name in _REV_ALIASES:
+        return _REV_ALIASES[name]
+    return re.sub(r"(?<=[a-z0-9])([A-Z])", lambda m: "_" + m.group(1).lower(), name)
+
+
+# ---------------------------------------------------------------------------
+# encoder
+# ---------------------------------------------------------------------------
+class _Writer:
+    def __init__(self):
+        self.storages = []   # (tensor id, storage id, float32 array)
+        self._next = 1
+
+    def _id(self):
+        self._next += 1
+        return self._next
+
+    def tensor(self, arr):
+        """BigDLTensor referencing a global-storage entry."""
+        arr = np.ascontiguousarray(np.asarray(arr, dtype=np.float32))
+        tid, sid = self._id(), self._id()
+        self.storages.append((tid, sid, arr))
+        body = enc_int(1, P.FLOAT) + enc_packed_ints(2, arr.shape)
+        strides = [s // 4 for s in arr.strides] if arr.ndim else []
+        body += enc_packed_ints(3, strides) + enc_int(4, 1) + enc_int(5, arr.ndim) + enc_int(6, arr.size)
+        body += enc_bytes(8, enc_int(1, P.FLOAT) + enc_int(9, sid)) + enc_int(9, tid)
+        return body
+
+    def shape(self, dims):
+        return enc_int(1, 0) + enc_int(2, len(dims)) + enc_packed_ints(3, [-1 if d is None else int(d) for d in dims])
+
+    def attr(self, v):
+        """AttrValue bytes, or None when the value is not representable (skipped)."""
+        if isinstance(v, bool):
+            return enc_int(1, P.BOOL) + enc_int(8, int(v))
+        if isinstance(v, (int, np.integer)):
+            return enc_int(1, P.INT32) + enc_int(3, int(v))
+        if isinstance(v, (float, np.floating)):
+            return enc_int(1, P.FLOAT) + enc_float(5, float(v))
+        if isinstance(v, str):
+            return enc_int(1, P.STRING) + enc_bytes(7, v)
+        if isinstance(v, _ShapeAttr):
+            return enc_int(1, P.SHAPE) + enc_bytes(18, self.shape(v.dims))
+        if isinstance(v, (np.ndarray, torch.Tensor)):
+            a = v.detach().cpu().numpy() if isinstance(v, torch.Tensor) else v
+            return enc_int(1, P.TENSOR) + enc_bytes(10, self.tensor(a))
+        if isinstance(v, dict) and "__module__" in v:
+            return enc_int(1, P.MODULE) + enc_bytes(13, self.module(v["__module__"], top=False))
+        if isinstance(v, (list, tuple)):
+            flat = list(v)
+            if all(isinstance(x, (bool, np.bool_)) for x in flat) and flat:
+                arr = enc_int(1, len(flat)) + enc_int(2, P.BOOL) + enc_packed_ints(8, [int(x) for x in flat])
+            elif all(isinstance(x, (int, np.integer)) and not isinstance(x, bool) for x in flat):
+                arr = enc_int(1, len(flat)) + enc_int(2, P.INT32) + enc_packed_ints(3, flat)
+            elif all(isinstance(x, (int, float, np.integer, np.floating)) for x in flat):
+                arr = enc_int(1, len(flat)) + enc_int(2, P.FLOAT) + enc_packed_floats(5, flat)
+            elif all(isinstance(x, str) for x in flat):
+                arr = enc_int(1, len(flat)) + enc_int(2, P.STRING) + b"".join(enc_bytes(7, x) for x in flat)
+            else:
+                return None
+            return enc_int(1, P.ARRAY_VALUE) + enc_bytes(15, arr)
+        return None
+
+    def module(self, spec, top=True):
+        """spec: dict(name, type, attr{}, weight, bias, parameters[], submodules[], pre[], next[])."""
+        out = enc_bytes(1, spec.get("name", ""))
+        for s in spec.get("submodules", []):
+            out += enc_bytes(2, self.module(s, top=False))
+        if spec.get("weight") is not None:
+            out += enc_bytes(3, self.tensor(spec["weight"]))
+        if spec.get("bias") is not None:
+            out += enc_bytes(4, self.tensor(spec["bias"]))
+        for p in spec.get("pre", []):
+            out += enc_bytes(5, p)
+        for p in spec.get("next", []):
+            out += enc_bytes(6, p)
+        out += enc_bytes(7, spec["type"])
+        attrs = dict(spec.get("attr", {}))
+        for k, v in list(attrs.items()):
+            # nested numeric sequences (e.g. Cropping2D ((1, 1), (1, 0))): flattened + row lengths
+            if isinstance(v, (list, tuple)) and v and all(isinstance(e, (list, tuple)) for e in v):
+                attrs[k] = [x for e in v for x in e]
+                attrs[k + "__nest"] = [len(e) for e in v]
+        for k, v in attrs.items():
+            if v is None:
+                continue
+            if isinstance(v, dict) and "__edges__" in v:
+                body = enc_bytes(1, v["name"])
+                for pre in v["__edges__"]:
+                    body += enc_bytes(2, enc_bytes(1, pre) + enc_bytes(2, enc_int(1, P.INT32) + enc_int(3, -1)))
+                av = enc_int(1, P.NAME_ATTR_LIST) + enc_bytes(14, body)
+            else:
+                av = self.attr(v)
+            if av is not None:
+                out += enc_bytes(8, enc_bytes(1, k) + enc_bytes(2, av))
+        out += enc_bytes(9, VERSION) + enc_int(10, 1)
+        for p in spec.get("parameters", []):
+            out += enc_bytes(16, self.tensor(p))
+        if top:
+            body = enc_bytes(1, "global_storage")
+            for tid, sid, arr in self.storages:
+                st = enc_int(1, P.FLOAT) + enc_packed_floats(2, arr.reshape(-1)) + enc_int(9, sid)
+                t = enc_int(1, P.FLOAT) + enc_packed_ints(2, arr.shape) + enc_int(4, 1) + enc_int(6, arr.size) + \
+                    enc_bytes(8, st) + enc_int(9, tid)
+                body += enc_bytes(2, enc_bytes(1, str(tid)) + enc_bytes(2, enc_int(1, P.TENSOR) + enc_bytes(10, t)))
+            out += enc_bytes(8, enc_bytes(1, "global_storage") + enc_bytes(2, enc_int(1, P.NAME_ATTR_LIST) +
+                                                                          enc_bytes(14, body)))
+        return out
+
+
+class _ShapeAttr:
+    def __init__(self, dims):
+        self.dims = list(dims)
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy()
+
+
+def _ctor_kwargs(layer):
+    """Bound constructor arguments of a Keras layer (recorded by Layer.__init_subclass__)."""
+    cls, a, k = layer._init_args
+    init = getattr(cls.__init__, "__wrapped__", cls.__init__)
+    try:
+        bound = inspect.signature(init).bind(None, *a, **k)
+        args = dict(bound.arguments)
+        args.pop("self", None)
+        extra = args.pop("kwargs", {}) or {}
+        args.update(extra)
+    except TypeError:
+        args = dict(k)
+    return args
+
+
+def _labor(layer):
+    """The BigDL nn module carrying ``layer``'s weights (BigDL layout where known)."""
+    from zoo.pipeline.api.keras.layers import core, convolutional, normalization, embeddings
+    t = type(layer)
+    if t is core.Dense and layer.built:
+        return {"type": BIGDL_NN + "Linear", "name": layer.name + "_linear",
+                "attr": {"inputSize": int(layer.weight.shape[1]), "outputSize": int(layer.weight.shape[0]),
+                         "withBias": layer.bias is not None},
+                "weight": _np(layer.weight), "bias": None if layer.bias is None else _np(layer.bias)}
+    if t is convolutional.Convolution2D and layer.built:
+        R, S = layer.kernel
+        K, C = layer.nb_filter, layer.cin
+        w = layer.weight.detach().float().cpu()[:K, :R * S * layer.cin_p].reshape(K, R, S, layer.cin_p)[..., :C]
+        w = w.permute(0, 3, 1, 2).reshape(1, K, C, R, S).numpy()
+        if layer.border_mode == "same":
+            pad_hw = (-1, -1)   # BigDL's SAME padding marker
+        else:
+            pp = layer._pads((None, None))
+            pad_hw = (pp[0][0], pp[1][0])
+        attr = {"nInputPlane": C, "nOutputPlane": K, "kernelW": S, "kernelH": R,
+                "strideW": layer.subsample[1], "strideH": layer.subsample[0], "nGroup": 1,
+                "withBias": layer.bias is not None, "format": "NCHW" if layer.dim_ordering == "th" else "NHWC"}
+        attr["padH"], attr["padW"] = pad_hw
+        return {"type": BIGDL_NN + "SpatialConvolution", "name": layer.name + "_conv", "attr": attr, "weight": w,
+                "bias": None if layer.bias is None else _np(layer.bias)[:K]}
+    if t is normalization.BatchNormalization and layer.built:
+        return {"type": BIGDL_NN + "SpatialBatchNormalization", "name": layer.name + "_bn",
+                "attr": {"nOutput": int(layer.gamma.numel()), "eps": float(layer.epsilon),
+                         "momentum": float(1.0 - layer.momentum) if layer.momentum > 0.5 else float(layer.momentum),
+                         "affine": True, "runningMean": _np(layer.running_mean), "runningVar": _np(layer.running_var)},
+                "weight": _np(layer.gamma), "bias": _np(layer.beta)}
+    if t is embeddings.Embedding and layer.built:
+        return {"type": BIGDL_NN + "LookupTable", "name": layer.name + "_lookup",
+                "attr": {"nIndex": int(layer.embeddings.shape[0]), "nOutput": int(layer.embeddings.shape[1])},
+                "weight": _np(layer.embeddings)}
+    # generic labor: every tensor of the layer, named
+    sd = layer.state_dict()
+    if not sd:
+        return None
+    names = list(sd.keys())
+    return {"type": BIGDL_NN + "Sequential", "name": layer.name + "_labor",
+            "attr": {"zoo_param_names": names}, "parameters": [_np(sd[n]) for n in names]}
+
+
+def _zoo_model_type(layer):
+    mod = type(layer).__module__                       # zoo.models.recommendation.neuralcf
+    pkg = mod.split(".")[2:-1]                          # ["recommendation"]
+    return ZOO_MODEL_PKG + ".".join(pkg + [type(layer).__name__])
+
+
+def _keras_spec(layer):
+    from zoo.models.common.zoo_model import ZooModel
+    from zoo.pipeline.api.keras.engine.topology import Model, Sequential
+    if isinstance(layer, ZooModel):
+        # ZooModel (Zs/models/common/ZooModel.scala): constructor config + every tensor of the model
+        attr = {"is_keras_module": True}
+        for k, v in _ctor_kwargs(layer).items():
+            if k != "name" and not hasattr(v, "_init_args"):
+                attr[_camel(k)] = v
+        sd = layer.state_dict()
+        names = list(sd.keys())
+        return {"type": _zoo_model_type(layer), "name": layer.name, "attr": attr,
+                "submodules": [{"type": BIGDL_NN + "Sequential", "name": layer.name + "_labor",
+                                "attr": {"zoo_param_names": names}, "parameters": [_np(sd[n]) for n in names]}]}
+    if isinstance(layer, Sequential):
+        inner = {"type": BIGDL_NN + "Sequential", "name": layer.name + "_seq",
+                 "submodules": [_keras_spec(l) for l in layer.stack]}
+        attr = {"is_keras_module": True}
+        ins = layer.get_input_shape()
+        if isinstance(ins, tuple):
+            attr["inputShape"] = _ShapeAttr(ins[1:])
+        return {"type": ZOO_MODELS + "Sequential", "name": layer.name, "attr": attr, "submodules": [inner]}
+    if isinstance(layer, Model) and type(layer).__name__ == "Model":
+        return _graph_spec(layer)
+    args = _ctor_kwargs(layer)
+    attr = {"is_keras_module": True}
+    for k, v in args.items():
+        if k in ("name",):
+            continue
+        if k == "input_shape" and v is not None:
+            attr["inputShape"] = _ShapeAttr(v if isinstance(v, (list, tuple)) else (v,))
+            continue
+        if hasattr(v, "_init_args"):  # a wrapped layer (TimeDistributed(Dense(...)))
+            attr[_camel(k)] = {"__module__": _keras_spec(v)}
+            continue
+        attr[_camel(k)] = v
+    built = layer.get_input_shape()
+    if isinstance(built, tuple) and "inputShape" not in attr:
+        attr["zoo_built_shape"] = _ShapeAttr(built[1:])
+    spec = {"type": ZOO_KERAS + type(layer).__name__, "name": layer.name, "attr": attr}
+    lab = _labor(layer)
+    if lab is not None:
+        spec["submodules"] = [lab]
+    return spec
+
+
+def _graph_spec(model):
+    from zoo.pipeline.api.keras.base import InputLayer
+    subs, names = [], {}
+    for n in model._nodes:
+        if id(n) in names:
+            continue
+        if isinstance(n.layer, InputLayer):
+            nm = n.layer.name
+            spec = {"type": BIGDL_KERAS_INPUT, "name": nm,
+                    "attr": {"inputShape": _ShapeAttr(n.output_shapes[0][1:]), "is_keras_module": True},
+                    "submodules": [{"type": BIGDL_NN + "Input", "name": nm + "_input"}]}
+        else:
+            nm = n.layer.name if n.layer.name not in names.values() else "%s_%d" % (n.layer.name, len(names))
+            spec = _keras_spec(n.layer)
+            spec["name"] = nm
+            spec["pre"] = [names[id(i.node)] for i in n.inputs]
+        names[id(n)] = nm
+        subs.append(spec)
+    attr = {}
+    for s in subs:
+        attr[s["name"] + "_edges"] = {"__edges__": s.get("pre", []), "name": s["name"]}
+    attr["inputNames"] = [names[id(v.node)] for v in model.inputs]
+    attr["outputNames"] = [names[id(v.node)] for v in model.outputs]
+    graph = {"type": BIGDL_NN + "StaticGraph", "name": model.name + "_graph", "attr": attr, "submodules": subs}
+    return {"type": ZOO_MODELS + "Model", "name": model.name, "attr": {"is_keras_module": True},
+            "submodules": [graph]}
+
+
+def _torch_spec(model):
+    sd = model.state_dict()
+    names = list(sd.keys())
+    return {"type": TORCH_MODEL, "name": type(model).__name__,
+            "attr": {"zoo_param_names": names, "zoo_class": type(model).__module__ + "." + type(model).__qualname__},
+            "parameters": [_np(sd[n]) for n in names]}
+
+
+def model_to_bytes(model, extra_attr=None):
+    from zoo.pipeline.api.keras.base import Layer
+    spec = _keras_spec(model) if isinstance(model, Layer) and hasattr(model, "_init_args") or \
+        type(model).__name__ in ("Sequential", "Model") and isinstance(model, Layer) else _torch_spec(model)
+    if extra_attr:
+        spec.setdefault("attr", {}).update(extra_attr)
+    return _Writer().module(spec)
+
+
+def save_bigdl_model(model, path, over_write=True, extra_attr=None):
+    """Write ``model`` as a BigDL/Zoo ``.model`` protobuf (KerasNet.saveModel).
+    ``extra_attr``: additional top-level attributes (the engine stores its
+    iteration/epoch counters there for ``model.<n>`` checkpoints)."""
+    import os
+    if os.path.exists(path) and not over_write:
+        raise FileExistsError("%s exists; pass over_write=True" % path)
+    data = model_to_bytes(model, extra_attr)
+    # the temporary name must not match the engine's ``model*`` checkpoint glob
+    tmp = os.path.join(os.path.dirname(os.path.abspath(path)), "." + os.path.basename(path) + ".tmp")
+    with open(tmp, "wb") as f:
+        f.write(data)
+    os.replace(tmp, path)
+    return path
+
+
+# ---------------------------------------------------------------------------
+# decoder
+# ---------------------------------------------------------------------------
+def _keras_registry():
+    from zoo.pipeline.api.keras import layers as L
+    from zoo.pipeline.api.keras.engine import topology
+    reg = {n: getattr(L, n) for n in dir(L) if isinstance(getattr(L, n), type)}
+    reg["Sequential"] = topology.Sequential
+    reg["Model"] = topology.Model
+    return reg
+
+
+def _find(spec, short):
+    if spec.short_type == short:
+        return spec
+    for s in spec.submodules:
+        r = _find(s, short)
+        if r is not None:
+            return r
+    return None
+
+
+def _shape_of(v):
+    if isinstance(v, dict) and "shape" in v:
+        return tuple(None if d == -1 else d for d in v["shape"])
+    return None
+
+
+def _kwargs_for(cls, spec, st):
+    init = getattr(cls.__init__, "__wrapped__", cls.__init__)
+    sig = inspect.signature(init)
+    accepts_kw = any(p.kind == p.VAR_KEYWORD for p in sig.parameters.values())
+    kw = {}
+    for k, v in spec.attr.items():
+        if k in ("module_tags", "module_numerics", "is_keras_module", "global_storage", "zoo_built_shape") or \
+                k.endswith("_edges") or k.endswith("__nest"):
+            continue
+        nest = spec.attr.get(k + "__nest")
+        if nest and isinstance(v, list):
+            rows, i = [], 0
+            for n in nest:
+                rows.append(tuple(v[i:i + n]))
+                i += n
+            v = tuple(rows)
+        name = _snake(k)
+        if name not in sig.parameters and not accepts_kw:
+            continue
+        if name not in sig.parameters and accepts_kw and name not in ("input_shape", "input_dim"):
+            continue
+        if isinstance(v, tuple) and v and v[0] == "opaque":  # InitMethod / Regularizer protos: defaults
+            continue
+        if k == "inputShape":
+            v = _shape_of(v)
+            if v is None:
+                continue
+        elif isinstance(v, P.BigDLModuleSpec):
+            v = _keras_layer(v, st)
+        elif isinstance(v, P.TensorRef):
+            v = v.materialize(st)
+        elif isinstance(v, dict) and "shape" in v:
+            v = _shape_of(v)
+        kw[name] = v
+    return kw
+
+
+def _load_weights(layer, spec, st):
+    """Copy the labor's tensors into the built layer."""
+    from zoo.pipeline.api.keras.layers import core, convolutional, normalization, embeddings
+    t = type(layer)
+    with torch.no_grad():
+        if t is core.Dense:
+            lin = _find(spec, "Linear")
+            if lin is not None and lin.weight is not None:
+                layer.weight.copy_(torch.from_numpy(lin.weight.materialize(st)).reshape(layer.weight.shape))
+                if layer.bias is not None and lin.bias is not None:
+                    layer.bias.copy_(torch.from_numpy(lin.bias.materialize(st)).reshape(-1))
+                return
+        if t is convolutional.Convolution2D:
+            cv = _find(spec, "SpatialConvolution")
+            if cv is not None and cv.weight is not None:
+                R, S = layer.kernel
+                K, C = layer.nb_filter, layer.cin
+                w = torch.from_numpy(cv.weight.materialize(st)).reshape(K, C, R, S).permute(0, 2, 3, 1)
+                w4 = torch.zeros(layer.weight.shape[0], R, S, layer.cin_p)
+                w4[:K, :, :, :C] = w
+                from zoo import ops
+                layer.weight.copy_(ops.pack_weight(w4).to(layer.weight.dtype))
+                if layer.bias is not None and cv.bias is not None:
+                    layer.bias.zero_()
+                    layer.bias[:K].copy_(torch.from_numpy(cv.bias.materialize(st)).reshape(-1))
+                return
+        if t is normalization.BatchNormalization:
+            bn = _find(spec, "SpatialBatchNormalization") or _find(spec, "BatchNormalization")
+            if bn is not None and bn.weight is not None:
+                layer.gamma.copy_(torch.from_numpy(bn.weight.materialize(st)).reshape(-1))
+                layer.beta.copy_(torch.from_numpy(bn.bias.materialize(st)).reshape(-1))
+                for key, buf in (("runningMean", layer.running_mean), ("runningVar", layer.running_var)):
+                    v = bn.attr.get(key)
+                    if isinstance(v, P.TensorRef):
+                        buf.copy_(torch.from_numpy(v.materialize(st)).reshape(-1))
+                return
+        if t is embeddings.Embedding:
+            lt = _find(spec, "LookupTable")
+            if lt is not None and lt.weight is not None:
+                layer.embeddings.copy_(torch.from_numpy(lt.weight.materialize(st)).reshape(layer.embeddings.shape))
+                return
+        gen = next((s for s in spec.submodules if "zoo_param_names" in s.attr), None)
+        if gen is not None:
+            sd = {n: torch.from_numpy(tr.materialize(st)) for n, tr in zip(gen.attr["zoo_param_names"],
+                                                                          gen.parameters)}
+            cur = layer.state_dict()
+            layer.load_state_dict({k: v.reshape(cur[k].shape).to(cur[k].dtype) for k, v in sd.items()})
+
+
+def _keras_layer(spec, st):
+    reg = _keras_registry()
+    short = spec.short_type
+    if short not in reg:
+        raise ValueError("unsupported Zoo-Keras layer type %s" % spec.type)
+    cls = reg[short]
+    layer = cls(**_kwargs_for(cls, spec, st))
+    layer.name = spec.effective_name or layer.name
+    return layer
+
+
+def _build_keras_layer(spec, st):
+    layer = _keras_layer(spec, st)
+    bs = _shape_of(spec.attr.get("zoo_built_shape"))
+    if bs is not None and not layer.built:
+        layer._ensure_built((None,) + tuple(bs))
+    return layer
+
+
+def _finish_weights(model, pairs, st):
+    for layer, spec in pairs:
+        if not layer.built:
+            raise ValueError("layer %s was not built from the recorded shapes" % layer.name)
+        _load_weights(layer, spec, st)
+
+
+def _sequential_from(spec, st):
+    from zoo.pipeline.api.keras.engine.topology import Sequential
+    inner = spec.submodules[0] if spec.submodules else None
+    layers = inner.submodules if inner is not None else []
+    m = Sequential(name=spec.effective_name)
+    pairs = []
+    for i, ls in enumerate(layers):
+        l = _any_keras(ls, st)
+        if i == 0 and l._given_input_shape is None:
+            shp = _shape_of(spec.attr.get("inputShape"))
+            if shp is not None:
+                l._given_input_shape = shp
+        m.add(l)
+        pairs.append((l, ls))
+    _finish_weights(m, [(l, s) for l, s in pairs if not _is_container(s)], st)
+    return m
+
+
+def _is_container(spec):
+    return spec.type.startswith(ZOO_MODELS)
+
+
+def _graph_from(spec, st):
+    from zoo.pipeline.api.keras.base import Input
+    from zoo.pipeline.api.keras.engine.topology import Model
+    g = spec.submodules[0]
+    by_name = {s.effective_name: s for s in g.submodules}
+    vals, pairs = {}, []
+
+    def value(name):
+        if name in vals:
+            return vals[name]
+        s = by_name[name]
+        if s.type == BIGDL_KERAS_INPUT or s.short_type == "Input":
+            v = Input(shape=_shape_of(s.attr.get("inputShape")), name=name)
+        else:
+            edges = g.attr.get(name + "_edges")
+            pre = list(edges["attr"].keys()) if isinstance(edges, dict) else list(s.pre)
+            args = [value(p) for p in pre]
+            layer = _any_keras(s, st)
+            v = layer(args if len(args) > 1 else args[0])
+            if not _is_container(s):
+                pairs.append((layer, s))
+        vals[name] = v
+        return v
+    ins = [value(n) for n in g.attr.get("inputNames", [])]
+    outs = [value(n) for n in g.attr.get("outputNames", [])]
+    m = Model(ins if len(ins) > 1 else ins[0], outs if len(outs) > 1 else outs[0], name=spec.effective_name)
+    _finish_weights(m, pairs, st)
+    return m
+
+
+def _zoo_model_registry():
+    import importlib
+    import pkgutil
+    import zoo.models as zm
+    from zoo.models.common.zoo_model import ZooModel
+    reg = {}
+    for m in pkgutil.walk_packages(zm.__path__, "zoo.models."):
+        try:
+            mod = importlib.import_module(m.name)
+        except Exception:  # noqa: BLE001 - optional model families
+            continue
+        for n, o in vars(mod).items():
+            if isinstance(o, type) and issubclass(o, ZooModel) and o is not ZooModel:
+                reg.setdefault(n, o)
+    return reg
+
+
+def _zoo_model_from(spec, st):
+    reg = _zoo_model_registry()
+    cls = reg.get(spec.short_type)
+    if cls is None:
+        raise ValueError("unsupported Zoo model type %s" % spec.type)
+    m = cls(**_kwargs_for(cls, spec, st))
+    gen = next((s for s in spec.submodules if "zoo_param_names" in s.attr), None)
+    if gen is not None:
+        cur = m.state_dict()
+        m.load_state_dict({n: torch.from_numpy(tr.materialize(st)).reshape(cur[n].shape).to(cur[n].dtype)
+                           for n, tr in zip(gen.attr["zoo_param_names"], gen.parameters)})
+    return m
+
+
+def _any_keras(spec, st):
+    if spec.type.startswith(ZOO_MODEL_PKG):
+        return _zoo_model_from(spec, st)
+    if spec.type == ZOO_MODELS + "Sequential":
+        return _sequential_from(spec, st)
+    if spec.type == ZOO_MODELS + "Model":
+        return _graph_from(spec, st)
+    return _build_keras_layer(spec, st)
+
+
+def load_bigdl_model(path, model=None):
+    """Read a ``.model`` file: Zoo-Keras models come back as framework Keras
+    models; a ``TorchModel`` entry is loaded into ``model`` (state dict); plain
+    BigDL ``nn`` graphs go through Net.loadBigDL's GraphNet converter."""
+    root, st = P.load_bigdl_spec(path)
+    if root.type.startswith(ZOO_MODELS) or root.type.startswith(ZOO_KERAS) or root.type.startswith(ZOO_MODEL_PKG):
+        loaded = _any_keras(root, st)
+        if model is not None:
+            model.load_state_dict(loaded.state_dict())
+            return model
+        return loaded
+    if root.type == TORCH_MODEL:
+        sd = {n: torch.from_numpy(tr.materialize(st)) for n, tr in zip(root.attr["zoo_param_names"], root.parameters)}
+        if model is None:
+            return sd
+        cur = model.state_dict()
+        model.load_state_dict({k: v.reshape(cur[k].shape).to(cur[k].dtype) for k, v in sd.items()})
+        return model
+    from zoo.pipeline.api.net.bigdl_loader import load_bigdl
+    return load_bigdl(path)
+
+
+def is_bigdl_model_file(path):
+    try:
+        with open(path, "rb") as f:
+            head = f.read(4096)
+    except OSError:
+        return False
+    return b"com.intel.analytics" in head or b"global_storage" in head
+
+
+def read_attr(path, key, default=None):
+    """One top-level attribute of a ``.model`` file (e.g. the engine counters)."""
+    root, _ = P.load_bigdl_spec(path)
+    return root.attr.get(key, default)

@@ -172,6 +172,12 @@ class BigDLModuleSpec:
         self.attr = {}
         self.train = False
         self.version = ""
+        self.name_postfix = ""
+
+    @property
+    def effective_name(self):
+        """BigDL's default module name: class name + namePostfix when ``name`` is empty."""
+        return self.name or (self.short_type + self.name_postfix)
 
     @property
     def short_type(self):
@@ -206,6 +212,8 @@ def decode_module(b):
             m.version = as_str(v)
         elif f == 10:
             m.train = bool(v)
+        elif f == 11:
+            m.name_postfix = as_str(v)
         elif f == 16:
             m.parameters.append(decode_tensor(v))
     return m

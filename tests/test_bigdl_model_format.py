@@ -1,0 +1,161 @@
+"""BigDL / Zoo ``.model`` protobuf: the reference's own Zoo-Keras fixtures load
+and compute what their decoded weights say (NetSpec.scala "net load model"),
+and the framework writes the same format (KerasNet.saveModel / ZooModel /
+engine ``model.<n>`` checkpoints) with BigDL tensor layouts for the standard
+labors. Layer-by-layer round trips of every Keras layer run through this codec
+in tests/test_keras_layers.py (save_model defaults to it)."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from zoo.utils import bigdl_proto as P
+from zoo.utils.bigdl_model import load_bigdl_model, save_bigdl_model
+
+FIX = "/root/reference/zoo/src/test/resources/models/zoo_keras"
+needs_fixtures = pytest.mark.skipif(not os.path.isdir(FIX), reason="reference fixtures not present")
+
+
+def _linear_of(path):
+    root, st = P.load_bigdl_spec(path)
+
+    def find(m):
+        if m.short_type == "Linear":
+            return m
+        for s in m.submodules:
+            r = find(s)
+            if r is not None:
+                return r
+    lin = find(root)
+    return lin.weight.materialize(st), lin.bias.materialize(st)
+
+
+@needs_fixtures
+def test_reference_small_seq_fixture_loads_and_matches_decoded_weights():
+    m = load_bigdl_model(os.path.join(FIX, "small_seq.model"))
+    w, b = _linear_of(os.path.join(FIX, "small_seq.model"))
+    assert w.shape == (3, 3)
+    x = torch.rand(2, 2, 3)
+    y = m(x)
+    ref = x.numpy() @ w.T + b
+    np.testing.assert_allclose(y.detach().numpy(), ref, rtol=1e-5, atol=1e-6)
+    assert tuple(m.get_output_shape()) == (None, 2, 3)
+
+
+@needs_fixtures
+def test_reference_small_model_graph_fixture_loads_and_matches_decoded_weights():
+    m = load_bigdl_model(os.path.join(FIX, "small_model.model"))
+    w, b = _linear_of(os.path.join(FIX, "small_model.model"))
+    assert w.shape == (7, 5)
+    x = torch.rand(2, 3, 5)
+    y = m(x)
+    np.testing.assert_allclose(y.detach().numpy(), x.numpy() @ w.T + b, rtol=1e-5, atol=1e-6)
+
+
+def test_written_file_uses_bigdl_layouts(tmp_path):
+    from zoo.pipeline.api.keras import layers as L
+    from zoo.pipeline.api.keras.engine.topology import Sequential
+    m = Sequential()
+    m.add(L.Convolution2D(5, 3, 3, border_mode="same", input_shape=(3, 8, 8)))
+    m.add(L.BatchNormalization())
+    m.add(L.Flatten())
+    m.add(L.Dense(4))
+    m.eval()
+    x = torch.randn(2, 3, 8, 8)
+    y = m(x)
+    p = str(tmp_path / "m.model")
+    save_bigdl_model(m, p)
+    root, st = P.load_bigdl_spec(p)
+    assert root.type == "com.intel.analytics.zoo.pipeline.api.keras.models.Sequential"
+    layers = root.submodules[0].submodules
+    assert [l.short_type for l in layers] == ["Convolution2D", "BatchNormalization", "Flatten", "Dense"]
+    conv = layers[0].submodules[0]
+    assert conv.short_type == "SpatialConvolution" and conv.attr["padH"] == -1
+    wc = conv.weight.materialize(st)
+    assert wc.shape == (1, 5, 3, 3, 3)
+    # the packed NHWC weight, unpacked to [out, in, kh, kw], equals the stored BigDL tensor
+    lw = m.stack[0].weight.detach()[:5, :3 * 3 * m.stack[0].cin_p].reshape(5, 3, 3, -1)[..., :3]
+    np.testing.assert_allclose(wc[0], lw.permute(0, 3, 1, 2).numpy(), rtol=0, atol=0)
+    bn = layers[1].submodules[0]
+    assert bn.short_type == "SpatialBatchNormalization" and bn.attr["runningVar"].size == [5]
+    lin = layers[3].submodules[0]
+    assert lin.short_type == "Linear" and lin.weight.size == [4, 5 * 8 * 8]
+    m2 = load_bigdl_model(p)
+    m2.eval()
+    np.testing.assert_allclose(m2(x).detach().numpy(), y.detach().numpy(), rtol=1e-5, atol=1e-5)
+
+
+def test_functional_model_roundtrip(tmp_path):
+    from zoo.pipeline.api.keras import layers as L
+    from zoo.pipeline.api.keras.base import Input
+    from zoo.pipeline.api.keras.engine.topology import Model
+    a, b = Input(shape=(4,)), Input(shape=(4,))
+    h = L.Dense(6, activation="relu")(a)
+    g = L.Dense(6)(b)
+    out = L.Dense(2)(L.merge([h, g], mode="concat"))
+    m = Model([a, b], out)
+    xa, xb = torch.randn(3, 4), torch.randn(3, 4)
+    y = m([xa, xb])
+    p = str(tmp_path / "g.model")
+    save_bigdl_model(m, p)
+    m2 = load_bigdl_model(p)
+    np.testing.assert_allclose(m2([xa, xb]).detach().numpy(), y.detach().numpy(), rtol=1e-5, atol=1e-6)
+    root, _ = P.load_bigdl_spec(p)
+    assert root.submodules[0].short_type == "StaticGraph"
+
+
+def test_zoo_model_roundtrip(tmp_path):
+    from zoo.models.recommendation.neuralcf import NeuralCF
+    m = NeuralCF(50, 40, 5, user_embed=4, item_embed=4, hidden_layers=(8, 4), include_mf=True, mf_embed=3)
+    m.eval()
+    x = torch.stack([torch.randint(1, 51, (6,)), torch.randint(1, 41, (6,))], 1)
+    y = m(x)
+    p = str(tmp_path / "ncf.model")
+    m.save_model(p, over_write=True)
+    root, _ = P.load_bigdl_spec(p)
+    assert root.type == "com.intel.analytics.zoo.models.recommendation.NeuralCF"
+    m2 = NeuralCF.load_model(p)
+    m2.eval()
+    np.testing.assert_allclose(m2(x).detach().numpy(), y.detach().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_torch_module_and_engine_checkpoint_are_bigdl_files(tmp_path):
+    import torch.nn as nn
+    from zoo.common import triggers as T
+    from zoo.feature.common import FeatureSet
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    from zoo.utils.bigdl_model import is_bigdl_model_file, read_attr
+    torch.manual_seed(0)
+    net = nn.Sequential(nn.Linear(4, 8), nn.Tanh(), nn.Linear(8, 1))
+    x = np.random.RandomState(0).randn(64, 4).astype(np.float32)
+    y = x[:, :1] * 0.5
+    eng = TrainingEngine(net, MeanSquaredError(), SGD(learningrate=0.05))
+    eng.set_checkpoint(str(tmp_path / "ck"), T.EveryEpoch(), overwrite=False)
+    eng.fit(FeatureSet.from_ndarrays(x, y, 16), end_trigger=T.MaxEpoch(2))
+    ck = eng.latest_checkpoint()
+    assert is_bigdl_model_file(ck)
+    root, _ = P.load_bigdl_spec(ck)
+    assert root.type == "com.intel.analytics.zoo.pipeline.api.net.TorchModel"
+    assert read_attr(ck, "zoo_neval") == 8
+    net2 = nn.Sequential(nn.Linear(4, 8), nn.Tanh(), nn.Linear(8, 1))
+    eng2 = TrainingEngine(net2, MeanSquaredError(), SGD(learningrate=0.05))
+    eng2.set_checkpoint(str(tmp_path / "ck"))
+    eng2.load_checkpoint(ck)
+    assert eng2.state["neval"] == eng.state["neval"]
+    for p1, p2 in zip(net.parameters(), net2.parameters()):
+        assert torch.equal(p1.detach(), p2.detach())
+
+
+def test_legacy_torch_format_still_loads(tmp_path):
+    from zoo.pipeline.api.keras import layers as L
+    from zoo.pipeline.api.keras.engine.topology import Sequential
+    from zoo.pipeline.api.keras.serialization import load_model, save_model
+    m = Sequential()
+    m.add(L.Dense(3, input_shape=(4,)))
+    p = str(tmp_path / "old.model")
+    save_model(m, p, over_write=True, format="zoo")
+    x = torch.randn(2, 4)
+    np.testing.assert_allclose(load_model(p)(x).detach().numpy(), m(x).detach().numpy(), rtol=1e-6)
