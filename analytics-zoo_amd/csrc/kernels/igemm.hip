@@ -37,7 +37,13 @@ __device__ __attribute__((aligned(16))) bf16_t ig_zero_page[8];
 
 ZOO_DEV int ig_swz(int row) { return (row >> 1) & 7; }
 
-template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA>
+// LEAN: the plain-conv epilogue (bf16 output, optional BN statistics; no bias / residual /
+// activation / fp32 output / row remap / fused BN-backward): the tile is staged through LDS
+// as bf16 (half the LDS of the fp32 staging, so 6 instead of 4 workgroups fit per CU) and
+// stored with precomputed row pointers. The general epilogue was instruction-issue bound on
+// the memory-bound 1x1 convolutions (rocprofv3: SQ_ACTIVE_INST_ANY ~ the whole wave lifetime
+// at 3.4 resident waves per SIMD, profiles/conv1x1_r2.md).
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, bool LEAN>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y,
     float* __restrict__ Yf, const float* __restrict__ bias, const bf16_t* __restrict__ resid,
@@ -259,6 +265,71 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     }
   }
 
+  if constexpr (LEAN) {
+    // bf16 staging, pitch BN+4 elements: the 4 row groups of a ds_write_b16 land 8 banks apart
+    constexpr int LD16 = BN + 4;
+    bf16_t* C16 = reinterpret_cast<bf16_t*>(smem);
+    float* wst = reinterpret_cast<float*>(smem + ((BM * LD16 * 2 + 15) / 16) * 16);  // [2 wm][BN][2]
+    if (stats) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int i = 0; i < NI; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float q = bf2f(f2bf(acc[i][j][r]));
+            a += q;
+            b += q * q;
+          }
+        a += __shfl_xor(a, 16, 64);
+        b += __shfl_xor(b, 16, 64);
+        a += __shfl_xor(a, 32, 64);
+        b += __shfl_xor(b, 32, 64);
+        if (fq == 0) {
+          const int col = wn * WN + j * 16 + fr;
+          wst[(wm * BN + col) * 2 + 0] = a;
+          wst[(wm * BN + col) * 2 + 1] = b;
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          C16[(wm * 64 + i * 16 + fq * 4 + r) * LD16 + wn * WN + j * 16 + fr] = f2bf(acc[i][j][r]);
+    __syncthreads();
+    constexpr int CPR = BN / 8, RSTEP = IG_NT / CPR;
+    const int ch = tid % CPR, rr0 = tid / CPR;
+    const int col0 = n0 + ch * 8;
+    if (col0 < g.K) {
+      const int rend = min(BM, g.M - m0);
+      bf16_t* yp = Y + (size_t)(m0 + rr0) * g.K + col0;
+      const bf16_t* cp = C16 + rr0 * LD16 + ch * 8;
+      for (int rr = rr0; rr < rend; rr += RSTEP, yp += (size_t)RSTEP * g.K, cp += RSTEP * LD16) {
+        const uint2 lo = *reinterpret_cast<const uint2*>(cp);
+        const uint2 hi = *reinterpret_cast<const uint2*>(cp + 4);
+        *reinterpret_cast<uint4*>(yp) = make_uint4(lo.x, lo.y, hi.x, hi.y);
+      }
+    }
+    if (stats && tid < BN && n0 + tid < g.K) {
+      const float a = wst[tid * 2] + wst[(BN + tid) * 2];
+      const float b = wst[tid * 2 + 1] + wst[(BN + tid) * 2 + 1];
+      if (g.stat_slots == kStatPartial) {
+        float* const dst = stats + (size_t)tm * 2 * g.K;
+        dst[n0 + tid] = a;
+        dst[g.K + n0 + tid] = b;
+      } else {
+        float* const dst = g.stat_slots > 0 ? slot_ptr(stats, 2 * g.K, g.stat_slots) : stats;
+        atomicAdd(dst + n0 + tid, a);
+        atomicAdd(dst + g.K + n0 + tid, b);
+      }
+    }
+    return;
+  }
+
   // ---- epilogue: stage fp32 tile in LDS, then row-contiguous 16-byte stores ----
   constexpr int EPI_LD = BN + 4;  // fp32 pitch: rows r and r+4 land 16 banks apart
   float* Cs = reinterpret_cast<float*>(smem);
@@ -448,27 +519,42 @@ __global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __rest
   }
 }
 
-size_t igemm_smem_bytes(int BN, int nbuf = 2) {
+size_t igemm_smem_bytes(int BN, int nbuf = 2, bool lean = false) {
   const size_t main_bytes = (size_t)nbuf * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
-  const size_t epi_bytes = (size_t)IG_BM * (BN + 4) * sizeof(float) + (size_t)2 * BN * 2 * sizeof(float);
+  const size_t epi_bytes = lean ? ((size_t)IG_BM * (BN + 4) * sizeof(bf16_t) + 15) / 16 * 16 +
+                                      (size_t)2 * BN * 2 * sizeof(float)
+                                : (size_t)IG_BM * (BN + 4) * sizeof(float) + (size_t)2 * BN * 2 * sizeof(float);
   return main_bytes > epi_bytes ? main_bytes : epi_bytes;
+}
+
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, bool LEAN>
+static hipError_t launch_ig1(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                             const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
+                             hipStream_t st) {
+  const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
+  const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1, LEAN);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, LEAN>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN, 2, LEAN));
+    attr_set = true;
+  }
+  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, LEAN>), dim3(tiles), dim3(IG_NT), smem, st, X, W,
+                     Y, Yf, bias, resid, stats, g, act, bs);
+  return hipGetLastError();
 }
 
 template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA>
 static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                             const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                             hipStream_t st) {
-  const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
-  const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1);
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN, DMA>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN));
-    attr_set = true;
-  }
-  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN, DMA>), dim3(tiles), dim3(IG_NT), smem, st, X, W, Y,
-                     Yf, bias, resid, stats, g, act, bs);
-  return hipGetLastError();
+  static const bool lean_ok = [] {
+    const char* e = getenv("ZOO_IGEMM_LEAN");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool lean = lean_ok && Y && !Yf && !bias && !resid && act == 0 && !g.omap && !bs.sums;
+  if (lean) return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, true>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, false>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 
 template <int VEC, bool IS1x1, bool LDIL, bool DMA>
