@@ -43,7 +43,10 @@ ZOO_DEV int ig_swz(int row) { return (row >> 1) & 7; }
 // stored with precomputed row pointers. The general epilogue was instruction-issue bound on
 // the memory-bound 1x1 convolutions (rocprofv3: SQ_ACTIVE_INST_ANY ~ the whole wave lifetime
 // at 3.4 resident waves per SIMD, profiles/conv1x1_r2.md).
-template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, bool LEAN>
+// EPI: 0 general epilogue; 1 LEAN (above); 2 backward epilogue (no bias / activation / fp32
+// output: residual-gradient add, producer ReLU mask and fused BN-backward sums) with the
+// per-column BN constants hoisted out of the row loop.
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, int EPI>
 __global__ __launch_bounds__(256, 2) void igemm_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y,
     float* __restrict__ Yf, const float* __restrict__ bias, const bf16_t* __restrict__ resid,
@@ -265,7 +268,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     }
   }
 
-  if constexpr (LEAN) {
+  if constexpr (EPI == 1) {
     // bf16 staging, pitch BN+4 elements: the 4 row groups of a ds_write_b16 land 8 banks apart
     constexpr int LD16 = BN + 4;
     bf16_t* C16 = reinterpret_cast<bf16_t*>(smem);
@@ -387,6 +390,54 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
 
+  if constexpr (EPI == 2) {
+    float mu[8], iv[8];
+    if (bs.sums && col_ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
+    }
+    const int rend = min(BM, g.M - m0);
+    for (int rr = rr0; col_ok && rr < rend; rr += RSTEP) {
+      const int m = m0 + rr;
+      float v[8];
+      const float4 lo = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8 + 4);
+      v[0] = lo.x; v[1] = lo.y; v[2] = lo.z; v[3] = lo.w;
+      v[4] = hi.x; v[5] = hi.y; v[6] = hi.z; v[7] = hi.w;
+      size_t off;
+      if (g.omap) {
+        const int n = m / PQ, pq = m - n * PQ;
+        const int p = pq / g.Q, q = pq - p * g.Q;
+        off = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
+      } else {
+        off = (size_t)m * g.K + col0;
+      }
+      if (resid) {
+        float rv[8];
+        unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += rv[e];
+      }
+      if (bs.z) {
+        float zz[8];
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+      }
+      const uint4 pk = pack8(v);
+      *reinterpret_cast<uint4*>(Y + off) = pk;
+      if (bs.sums) {
+        float q[8], yy[8];
+        unpack8(pk, q);
+        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          s1[e] += q[e];
+          s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+        }
+      }
+    }
+  } else
   for (int rr = rr0; rr < BM; rr += RSTEP) {
     const int m = m0 + rr;
     if (m >= g.M || !col_ok) continue;
@@ -527,19 +578,19 @@ size_t igemm_smem_bytes(int BN, int nbuf = 2, bool lean = false) {
   return main_bytes > epi_bytes ? main_bytes : epi_bytes;
 }
 
-template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, bool LEAN>
+template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA, int EPI>
 static hipError_t launch_ig1(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                              const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                              hipStream_t st) {
   const int tiles = ((g.M + IG_BM - 1) / IG_BM) * ((g.K + BN - 1) / BN);
-  const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1, LEAN);
+  const size_t smem = igemm_smem_bytes(BN, g.ldb > IG_BK ? 2 : 1, EPI == 1);
   static bool attr_set = false;
   if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, LEAN>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN, 2, LEAN));
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, EPI>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)igemm_smem_bytes(BN, 2, EPI == 1));
     attr_set = true;
   }
-  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, LEAN>), dim3(tiles), dim3(IG_NT), smem, st, X, W,
+  hipLaunchKernelGGL((igemm_kernel<VEC, IS1x1, LDIL, BN, DMA, EPI>), dim3(tiles), dim3(IG_NT), smem, st, X, W,
                      Y, Yf, bias, resid, stats, g, act, bs);
   return hipGetLastError();
 }
@@ -553,8 +604,10 @@ static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* 
     return e ? atoi(e) != 0 : true;
   }();
   const bool lean = lean_ok && Y && !Yf && !bias && !resid && act == 0 && !g.omap && !bs.sums;
-  if (lean) return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, true>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, false>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (lean) return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  const bool bwd = lean_ok && Y && !Yf && !bias && act == 0 && !stats;
+  if (bwd) return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, 2>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, 0>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 
 template <int VEC, bool IS1x1, bool LDIL, bool DMA>
