@@ -36,26 +36,36 @@ ZOO_DEV int wg_f(int row) { return (row & 3) | (((row >> 3) & 1) << 2); }
 ZOO_DEV int wg_off(int row, int col) {  // element offset in a [64][128] bf16 tile
   return row * 128 + ((((col >> 4) ^ wg_f(row)) & 7) << 4) + (col & 15);
 }
+// [64][64] tile (the dY tile of K <= 64 convs): two 128-byte rows per 64-bank row, so the
+// even and the odd rows of {0..3, 8..11} each need 4 distinct 32-byte slots
+ZOO_DEV int wg_f64(int row) { return ((row >> 1) & 1) | (((row >> 3) & 1) << 1); }
+ZOO_DEV int wg_off64(int row, int col) {
+  return row * 64 + ((((col >> 4) ^ wg_f64(row)) & 3) << 4) + (col & 15);
+}
 
-template <int VEC, bool DMA>
+// BMT: output-channel tile (128, or 64 for K <= 64 convs, which would waste half of a
+// 128-row tile's MFMA work).
+template <int VEC, bool DMA, int BMT>
 __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict__ X,
                                                         const bf16_t* __restrict__ dY,
                                                         float* __restrict__ dW, float* __restrict__ part,
                                                         WgradGeom g) {
+  static_assert(BMT == 128 || (BMT == 64 && !DMA), "64-row tiles use register staging");
+  constexpr int NIW = BMT / 32;  // 16-row MFMA tiles per wave (wave tile BMT/2 x 64)
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64 m][128 k-out]
-  bf16_t* Bs = As + 2 * WG_BK * WG_BM;           // [2][64 m][128 (r,s,c)]
+  bf16_t* As = reinterpret_cast<bf16_t*>(smem);  // [2][64 m][BMT k-out]
+  bf16_t* Bs = As + 2 * WG_BK * BMT;             // [2][64 m][128 (r,s,c)]
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
 
-  const int tiles_m = (g.K + WG_BM - 1) / WG_BM;
+  const int tiles_m = (g.K + BMT - 1) / BMT;
   const int tiles_n = (g.Ktot + WG_BN - 1) / WG_BN;
   const int tiles = tiles_m * tiles_n;
   const int split = blockIdx.x / tiles;
   const int tile = blockIdx.x - split * tiles;
   const int tm = tile / tiles_n, tn = tile - tm * tiles_n;
-  const int k0 = tm * WG_BM, c0 = tn * WG_BN;
+  const int k0 = tm * BMT, c0 = tn * WG_BN;
   const int mstart = split * g.m_per_split;
   const int mend = min(g.M, mstart + g.m_per_split);
   if (mstart >= mend) return;
@@ -68,8 +78,11 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   const int rb = tid >> 4;  // 0..15
   const int ch = DMA ? 2 * ((((tid & 15) >> 1) ^ wg_f(rb)) & 7) + (tid & 1) : (tid & 15);
 
-  // dY columns (output channels) for this thread's chunk
-  const int ycol = k0 + ch * 8;
+  // dY columns (output channels) for this thread's chunk; 64-row tiles: 8 chunks per row,
+  // rows arb + 32*i (i < 2)
+  const int ach = BMT == 128 ? ch : (tid & 7);
+  const int arb = BMT == 128 ? rb : (tid >> 3);
+  const int ycol = k0 + ach * 8;
   const bool ycol_ok = ycol < g.K;
   // im2col column decode for the X chunk (fixed for the whole block)
   const int xcol = c0 + ch * 8;
@@ -94,29 +107,56 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
 
   uint4 ra[4], rbv[4];
   const int PQ = g.P * g.Q;
+  // incremental pixel decode: row i of the staging pattern sits at pixel
+  // m = mstart + kt*BK + rb + 16i; each k-tile advances it by BK = dn*PQ + dp*Q + dq
+  // (no integer division inside the loop)
+  const int dn = WG_BK / PQ, dp = (WG_BK % PQ) / g.Q, dq = (WG_BK % PQ) % g.Q;
+  int pn[4], pp[4], pqq[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = mstart + rb + 16 * i;
+    const int mm = m < g.M ? m : 0;
+    pn[i] = mm / PQ;
+    const int pq = mm - pn[i] * PQ;
+    pp[i] = pq / g.Q;
+    pqq[i] = pq - pp[i] * g.Q;
+  }
+  auto advance = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      pqq[i] += dq; pp[i] += dp; pn[i] += dn;
+      if (pqq[i] >= g.Q) { pqq[i] -= g.Q; ++pp[i]; }
+      if (pp[i] >= g.P) { pp[i] -= g.P; ++pn[i]; }
+    }
+  };
 
   auto dma16 = [&](const bf16_t* src, bf16_t* dst) {
     __builtin_amdgcn_global_load_lds((wg_gl_void*)src, (wg_lds_void*)dst, 16, 0, 0);
   };
   auto load_tile = [&](int kt) {
-    bf16_t* adst = As + (kt & 1) * WG_BK * WG_BM + (wid * 4) * WG_BM;
+    bf16_t* adst = As + (kt & 1) * WG_BK * BMT + (wid * 4) * BMT;
     bf16_t* bdst = Bs + (kt & 1) * WG_BK * WG_BN + (wid * 4) * WG_BN;
     (void)adst; (void)bdst;
+    if constexpr (BMT == 64) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = mstart + kt * WG_BK + arb + 32 * i;
+        ra[i] = (m < mend && ycol_ok) ? *reinterpret_cast<const uint4*>(dY + (size_t)m * g.K + ycol)
+                                      : make_uint4(0, 0, 0, 0);
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int m = mstart + kt * WG_BK + rb + 16 * i;
       const bool mok = m < mend;
-      if constexpr (DMA) {
-        dma16(mok && ycol_ok ? dY + (size_t)m * g.K + ycol : wg_zero_page, adst + 16 * i * WG_BM);
+      if constexpr (BMT == 64) {
+      } else if constexpr (DMA) {
+        dma16(mok && ycol_ok ? dY + (size_t)m * g.K + ycol : wg_zero_page, adst + 16 * i * BMT);
       } else {
         ra[i] = (mok && ycol_ok) ? *reinterpret_cast<const uint4*>(dY + (size_t)m * g.K + ycol)
                                  : make_uint4(0, 0, 0, 0);
       }
-      const int mm = mok ? m : 0;
-      const int n = mm / PQ;
-      const int pq = mm - n * PQ;
-      const int p = pq / g.Q;
-      const int q = pq - p * g.Q;
+      const int n = mok ? pn[i] : 0, p = mok ? pp[i] : 0, q = mok ? pqq[i] : 0;
       const bf16_t* xb = X + (size_t)n * g.H * g.W * g.C;
       if constexpr (VEC == 8) {
         const int ih = p * g.sh - g.ph + xr[0] * g.dh;
@@ -140,22 +180,28 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
         rbv[i] = make_uint4(v[0].x, v[0].y, v[1].x, v[1].y);
       }
     }
+    advance();
   };
 
   auto store_tile = [&](int buf) {
-    bf16_t* a = As + buf * WG_BK * WG_BM;
+    bf16_t* a = As + buf * WG_BK * BMT;
     bf16_t* b = Bs + buf * WG_BK * WG_BN;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = rb + 16 * i;
-      *reinterpret_cast<uint4*>(a + wg_off(row, ch * 8)) = ra[i];
+      if constexpr (BMT == 128) *reinterpret_cast<uint4*>(a + wg_off(row, ch * 8)) = ra[i];
       *reinterpret_cast<uint4*>(b + wg_off(row, ch * 8)) = rbv[i];
+    }
+    if constexpr (BMT == 64) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        *reinterpret_cast<uint4*>(a + wg_off64(arb + 32 * i, ach * 8)) = ra[i];
     }
   };
 
-  f32x4 acc[4][4];
+  f32x4 acc[NIW][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NIW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -163,13 +209,13 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   // 32-deep k-step; lane i = 4q+p of the group addresses row q, columns 4p..4p+3
   const int gq = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
 
-  auto read_frag = [&](const bf16_t* base, int kk, int colbase) -> bf16x8 {
+  auto read_frag = [&](const bf16_t* base, int kk, int colbase, bool narrow) -> bf16x8 {
     const int row0 = kk * 32 + gq * 8 + tq;
     typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
-    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_i16x4*)(base + wg_off(row0, colbase + 4 * tp)));
-    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_i16x4*)(base + wg_off(row0 + 4, colbase + 4 * tp)));
+    const int o0 = narrow ? wg_off64(row0, colbase + 4 * tp) : wg_off(row0, colbase + 4 * tp);
+    const int o1 = narrow ? wg_off64(row0 + 4, colbase + 4 * tp) : wg_off(row0 + 4, colbase + 4 * tp);
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + o0));
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + o1));
     typedef short i16x8 __attribute__((ext_vector_type(8)));
     i16x8 v;
     v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
@@ -178,17 +224,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   };
 
   auto compute = [&](int buf) {
-    const bf16_t* a = As + buf * WG_BK * WG_BM;
+    const bf16_t* a = As + buf * WG_BK * BMT;
     const bf16_t* b = Bs + buf * WG_BK * WG_BN;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[4], bfg[4];
+      bf16x8 af[NIW], bfg[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag(a, kk, wm * 64 + i * 16);
+      for (int i = 0; i < NIW; ++i) af[i] = read_frag(a, kk, wm * (BMT / 2) + i * 16, BMT == 64);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfg[j] = read_frag(b, kk, wn * 64 + j * 16);
+      for (int j = 0; j < 4; ++j) bfg[j] = read_frag(b, kk, wn * 64 + j * 16, false);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NIW; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = mfma16(af[i], bfg[j], acc[i][j]);
     }
@@ -226,14 +272,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
   const int fr = lane & 15, fq = lane >> 4;
   float* const pdst = part ? part + (size_t)split * g.K * g.Ktot : nullptr;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NIW; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int col = c0 + wn * 64 + j * 16 + fr;
       if (col >= g.Ktot) continue;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = k0 + wm * 64 + i * 16 + fq * 4 + r;
+        const int row = k0 + wm * (BMT / 2) + i * 16 + fq * 4 + r;
         if (row < g.K) {
           if (pdst) pdst[(size_t)row * g.Ktot + col] = acc[i][j][r];
           else atomicAdd(dW + (size_t)row * g.ldw + col, acc[i][j][r]);
@@ -266,9 +312,18 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const float* __restrict
 using namespace zoo;
 
 // split plan of the pixel reduction: sets g->m_per_split, returns the number of splits
+static int wgrad_bm(const WgradGeom& g) {
+  static const int narrow = [] {
+    const char* e = getenv("ZOO_WGRAD_BM64");
+    return e ? atoi(e) : 1;
+  }();
+  return (narrow && g.K <= 64) ? 64 : 128;
+}
+
 extern "C" int zoo_wgrad_plan(WgradGeom* gp) {
   WgradGeom& g = *gp;
-  const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
+  const int bm = wgrad_bm(g);
+  const int tiles = ((g.K + bm - 1) / bm) * ((g.Ktot + WG_BN - 1) / WG_BN);
   // split the pixel reduction so that ~kTarget workgroups are in flight, >= kMinPix pixels each
   static const int target = [] {
     const char* e = getenv("ZOO_WGRAD_WG");
@@ -293,10 +348,11 @@ extern "C" int zoo_wgrad_plan(WgradGeom* gp) {
 extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float* part, const WgradGeom* gin,
                                 hipStream_t st) {
   WgradGeom g = *gin;
-  const int tiles = ((g.K + WG_BM - 1) / WG_BM) * ((g.Ktot + WG_BN - 1) / WG_BN);
+  const int bm = wgrad_bm(g);
+  const int tiles = ((g.K + bm - 1) / bm) * ((g.Ktot + WG_BN - 1) / WG_BN);
   const int splits = zoo_wgrad_plan(&g);
   if (splits <= 1) part = nullptr;
-  const size_t smem = (size_t)2 * WG_BK * (WG_BM + WG_BN) * sizeof(bf16_t);
+  const size_t smem = (size_t)2 * WG_BK * (bm + WG_BN) * sizeof(bf16_t);
   static const bool dma = [] {
     // measured slower than register staging for the weight gradient (conv_sweep wgrad
     // 7.34 vs 6.99 ms/step, bench 8912 vs 9045 img/s): opt-in until re-tuned
@@ -304,13 +360,20 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
     return e ? atoi(e) != 0 : false;
   }();
   if (g.C == 4) {
-    hipLaunchKernelGGL((wgrad_kernel<4, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+    if (bm == 64)
+      hipLaunchKernelGGL((wgrad_kernel<4, false, 64>), dim3(tiles * splits), dim3(256), smem, st,
+                         (const bf16_t*)X, (const bf16_t*)dY, dW, part, g);
+    else
+      hipLaunchKernelGGL((wgrad_kernel<4, false, 128>), dim3(tiles * splits), dim3(256), smem, st,
+                         (const bf16_t*)X, (const bf16_t*)dY, dW, part, g);
+  } else if (bm == 64) {
+    hipLaunchKernelGGL((wgrad_kernel<8, false, 64>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
                        (const bf16_t*)dY, dW, part, g);
   } else if (dma) {
-    hipLaunchKernelGGL((wgrad_kernel<8, true>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+    hipLaunchKernelGGL((wgrad_kernel<8, true, 128>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
                        (const bf16_t*)dY, dW, part, g);
   } else {
-    hipLaunchKernelGGL((wgrad_kernel<8, false>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
+    hipLaunchKernelGGL((wgrad_kernel<8, false, 128>), dim3(tiles * splits), dim3(256), smem, st, (const bf16_t*)X,
                        (const bf16_t*)dY, dW, part, g);
   }
   if (part) {
