@@ -288,18 +288,35 @@ __global__ __launch_bounds__(256, 2) void wgrad_kernel(const bf16_t* __restrict_
     }
 }
 
-// dW[k][c] += sum_s part[s][k][c] (s in order); 4 columns per thread (Ktot % 4 == 0)
+// Ordered fold of the per-split partials. Level 1 (splits > kFoldGroup): blockIdx.y = group g
+// sums splits [g*G, (g+1)*G) in order into lvl1[g]; level 2 sums the groups in order and adds
+// into dW. 4 columns per thread (Ktot % 4 == 0). Parallel over splits as well as elements, so
+// layers with hundreds of splits and small weights (ResNet stage 1) fold in microseconds.
+constexpr int kFoldGroup = 16;
+__global__ __launch_bounds__(256) void wgrad_fold1_kernel(const float* __restrict__ part, float* __restrict__ lvl1,
+                                                         size_t n4, int splits) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int s0 = blockIdx.y * kFoldGroup, s1 = min(splits, s0 + kFoldGroup);
+  const float4* p = reinterpret_cast<const float4*>(part) + i;
+  float4 s = p[(size_t)s0 * n4];
+  for (int sp = s0 + 1; sp < s1; ++sp) {
+    const float4 v = p[(size_t)sp * n4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  reinterpret_cast<float4*>(lvl1)[(size_t)blockIdx.y * n4 + i] = s;
+}
+
 __global__ __launch_bounds__(256) void wgrad_fold_kernel(const float* __restrict__ part, float* __restrict__ dW,
                                                         int K, int Ktot, int ldw, int splits) {
   const int q = Ktot >> 2;
   const size_t n4 = (size_t)K * q;
-  const size_t stride = (size_t)K * Ktot;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const int k = (int)(i / q), c4 = (int)(i - (size_t)k * q) * 4;
-    const float* p = part + (size_t)k * Ktot + c4;
-    float4 s = *reinterpret_cast<const float4*>(p);
+    const float4* p = reinterpret_cast<const float4*>(part) + i;
+    float4 s = p[0];
     for (int sp = 1; sp < splits; ++sp) {
-      const float4 v = *reinterpret_cast<const float4*>(p + sp * stride);
+      const float4 v = p[(size_t)sp * n4];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
     float* d = dW + (size_t)k * ldw + c4;
@@ -379,7 +396,17 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
   if (part) {
     const size_t n4 = (size_t)g.K * (g.Ktot / 4);
     const int blocks = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
-    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, part, dW, g.K, g.Ktot, g.ldw, splits);
+    const float* src = part;
+    int n = splits;
+    if (splits > kFoldGroup) {  // level 1 in place of the first groups' slots: group g -> slot g
+      const int groups = (splits + kFoldGroup - 1) / kFoldGroup;
+      float* lvl1 = part + (size_t)splits * g.K * g.Ktot;  // scratch after the partials
+      hipLaunchKernelGGL(wgrad_fold1_kernel, dim3((unsigned)((n4 + 255) / 256), groups), dim3(256), 0, st, part,
+                         lvl1, n4, splits);
+      src = lvl1;
+      n = groups;
+    }
+    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, src, dW, g.K, g.Ktot, g.ldw, n);
   }
   return hipGetLastError();
 }

@@ -294,11 +294,24 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
   g.m_per_split = 0;
+  // split-K reduction: fp32 atomics into dW, or per-split partials + an ordered fold. Atomics
+  // run at ~1.3 TB/s of added bytes, plain stores + the fold's reads at ~5 TB/s: the partials
+  // win once the split output is larger than ~ZOO_WGRAD_PARTIAL_MB (and are always used in
+  // deterministic mode)
+  static const double auto_mb = [] {
+    const char* e = getenv("ZOO_WGRAD_PARTIAL_MB");
+    return e ? atof(e) : 16.0;
+  }();
   torch::Tensor part;
-  if (wgrad_partial()) {
+  {
     WgradGeom gp = g;
     const int splits = zoo_wgrad_plan(&gp);
-    if (splits > 1) part = torch::empty({(int64_t)splits, (int64_t)g.K * g.Ktot}, dw.options());
+    const double mb = (double)splits * g.K * g.Ktot * 4 / 1e6;
+    if (splits > 1 && (wgrad_partial() || (auto_mb > 0 && mb >= auto_mb))) {
+      const int groups = (splits + 15) / 16;
+      const int64_t extra = splits > 16 ? (int64_t)groups : 0;  // level-1 fold scratch
+      part = torch::empty({(int64_t)splits + extra, (int64_t)g.K * g.Ktot}, dw.options());
+    }
   }
   check_hip(zoo_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), part.defined() ? part.data_ptr<float>() : nullptr,
                       &g, cur_stream()),
