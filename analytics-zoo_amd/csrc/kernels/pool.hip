@@ -130,6 +130,82 @@ __global__ __launch_bounds__(256) void gap_bwd_kernel(const bf16_t* __restrict__
   }
 }
 
+// average pooling (AveragePooling2D / SpatialAveragePooling): the divisor is the window
+// clipped to the padded input (count_include_pad) or to the valid taps; ceil-mode output
+// sizes come in through P / Q
+ZOO_DEV int avg_div(int p, int q, int H, int W, int R, int S, int sh, int sw, int ph, int pw, int inc_pad) {
+  int h0 = p * sh - ph, w0 = q * sw - pw;
+  int h1 = min(h0 + R, H + ph), w1 = min(w0 + S, W + pw);
+  if (!inc_pad) {
+    h0 = max(h0, 0); w0 = max(w0, 0);
+    h1 = min(h1, H); w1 = min(w1, W);
+  }
+  const int d = (h1 - h0) * (w1 - w0);
+  return d > 0 ? d : 1;
+}
+
+__global__ __launch_bounds__(256) void avgpool_fwd_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                          int N, int H, int W, int C, int P, int Q, int R, int S,
+                                                          int sh, int sw, int ph, int pw, int inc_pad) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * P * Q * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int q = (int)(t % Q); t /= Q;
+    const int p = (int)(t % P);
+    const int n = (int)(t / P);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int r = 0; r < R; ++r) {
+      const int ih = p * sh - ph + r;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int s = 0; s < S; ++s) {
+        const int iw = q * sw - pw + s;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(X + (((size_t)n * H + ih) * W + iw) * C + chunk * 8), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += v[e];
+      }
+    }
+    const float inv = 1.f / (float)avg_div(p, q, H, W, R, S, sh, sw, ph, pw, inc_pad);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] *= inv;
+    *reinterpret_cast<uint4*>(Y + i * 8) = pack8(acc);
+  }
+}
+
+__global__ __launch_bounds__(256) void avgpool_bwd_kernel(const bf16_t* __restrict__ dY, bf16_t* __restrict__ dX,
+                                                          int N, int H, int W, int C, int P, int Q, int R, int S,
+                                                          int sh, int sw, int ph, int pw, int inc_pad) {
+  const int cpr = C >> 3;
+  const size_t total = (size_t)N * H * W * cpr;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int chunk = (int)(i % cpr);
+    size_t t = i / cpr;
+    const int w = (int)(t % W); t /= W;
+    const int h = (int)(t % H);
+    const int n = (int)(t / H);
+    float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    const int p_lo = max(0, (h + ph - R + sh) / sh), p_hi = min(P - 1, (h + ph) / sh);
+    const int q_lo = max(0, (w + pw - S + sw) / sw), q_hi = min(Q - 1, (w + pw) / sw);
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * sh - ph);
+      if (r < 0 || r >= R) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * sw - pw);
+        if (s < 0 || s >= S) continue;
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dY + (((size_t)n * P + p) * Q + q) * C + chunk * 8), g);
+        const float inv = 1.f / (float)avg_div(p, q, H, W, R, S, sh, sw, ph, pw, inc_pad);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) acc[e] += g[e] * inv;
+      }
+    }
+    *reinterpret_cast<uint4*>(dX + i * 8) = pack8(acc);
+  }
+}
+
 static int pgrid(size_t work) {
   size_t b = (work + 255) / 256;
   if (b > 4096) b = 4096;
@@ -163,5 +239,19 @@ extern "C" hipError_t zoo_gap_fwd(const void* X, void* Y, int N, int HW, int C, 
 extern "C" hipError_t zoo_gap_bwd(const void* dY, void* dX, int N, int HW, int C, hipStream_t st) {
   hipLaunchKernelGGL(gap_bwd_kernel, dim3(pgrid((size_t)N * HW * (C / 8))), dim3(256), 0, st, (const bf16_t*)dY,
                      (bf16_t*)dX, N, HW, C);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_avgpool_fwd(const void* X, void* Y, int N, int H, int W, int C, int P, int Q, int R, int S,
+                                      int sh, int sw, int ph, int pw, int inc_pad, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_fwd_kernel, dim3(pgrid((size_t)N * P * Q * (C / 8))), dim3(256), 0, st,
+                     (const bf16_t*)X, (bf16_t*)Y, N, H, W, C, P, Q, R, S, sh, sw, ph, pw, inc_pad);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_avgpool_bwd(const void* dY, void* dX, int N, int H, int W, int C, int P, int Q, int R,
+                                      int S, int sh, int sw, int ph, int pw, int inc_pad, hipStream_t st) {
+  hipLaunchKernelGGL(avgpool_bwd_kernel, dim3(pgrid((size_t)N * H * W * (C / 8))), dim3(256), 0, st,
+                     (const bf16_t*)dY, (bf16_t*)dX, N, H, W, C, P, Q, R, S, sh, sw, ph, pw, inc_pad);
   return hipGetLastError();
 }

@@ -40,6 +40,16 @@ hipError_t zoo_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, i
 hipError_t zoo_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                            hipStream_t);
 hipError_t zoo_gap_fwd(const void*, void*, int, int, int, hipStream_t);
+hipError_t zoo_avgpool_fwd(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                           hipStream_t);
+hipError_t zoo_avgpool_bwd(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                           hipStream_t);
+hipError_t zoo_dwconv_fwd(const void*, const void*, const float*, void*, const int*, int, hipStream_t);
+hipError_t zoo_dwconv_dgrad(const void*, const void*, void*, const int*, hipStream_t);
+hipError_t zoo_dwconv_wgrad(const void*, const void*, float*, const int*, hipStream_t);
+hipError_t zoo_softmax_rows(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t zoo_softmax_rows_bwd(const void*, const void*, void*, int, int, int, int, hipStream_t);
+hipError_t zoo_lrn(const void*, const void*, void*, size_t, int, int, float, float, float, int, int, hipStream_t);
 hipError_t zoo_gap_bwd(const void*, void*, int, int, int, hipStream_t);
 hipError_t zoo_softmax_xent(const void*, int, const int64_t*, float*, float*, void*, int, int, float, int, int,
                             hipStream_t);
@@ -89,6 +99,13 @@ void check_hip(hipError_t e, const char* what) {
 
 // slotted per-channel statistics buffer: [2C final][kStatSlots x 2C][counter, padded to 4 floats]
 int64_t stat_len(int64_t C) { return 2 * C * (zoo::kStatSlots + 1) + 4; }
+
+// pooled output size (floor or ceil mode; a ceil-mode window must start inside the padded input)
+int pool_out(int H, int R, int st, int pad, bool ceil_mode) {
+  int o = ceil_mode ? (H + 2 * pad - R + st - 1) / st + 1 : (H + 2 * pad - R) / st + 1;
+  if (ceil_mode && (o - 1) * st >= H + pad) --o;
+  return o;
+}
 
 // Reduction modes.
 //  * deterministic: every cross-workgroup float reduction of the conv/BN/loss path goes through
@@ -428,12 +445,14 @@ std::vector<torch::Tensor> bn_bwd_apply(torch::Tensor dz, c10::optional<torch::T
   return {dx};
 }
 
-std::vector<torch::Tensor> maxpool_fwd(torch::Tensor x, int R, int S, int sh, int sw, int ph, int pw, bool save_arg) {
+std::vector<torch::Tensor> maxpool_fwd(torch::Tensor x, int R, int S, int sh, int sw, int ph, int pw, bool save_arg,
+                                       bool ceil_mode) {
   req(x, at::kBFloat16, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "maxpool: NHWC with C%8==0");
   TORCH_CHECK(R * S <= 256, "maxpool: window too large");
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
-  const int P = (H + 2 * ph - R) / sh + 1, Q = (W + 2 * pw - S) / sw + 1;
+  const int P = pool_out(H, R, sh, ph, ceil_mode), Q = pool_out(W, S, sw, pw, ceil_mode);
+  TORCH_CHECK(P > 0 && Q > 0, "maxpool: empty output");
   auto y = torch::empty({N, P, Q, C}, x.options());
   torch::Tensor arg;
   if (save_arg) arg = torch::empty({N, P, Q, C}, x.options().dtype(at::kByte));
@@ -450,12 +469,150 @@ torch::Tensor maxpool_bwd(torch::Tensor dy, torch::Tensor arg, int H, int W, int
   req(arg, at::kByte, "arg");
   TORCH_CHECK(dy.sizes() == arg.sizes(), "maxpool_bwd: arg shape");
   const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
-  TORCH_CHECK(P == (H + 2 * ph - R) / sh + 1 && Q == (W + 2 * pw - S) / sw + 1, "maxpool_bwd: geometry");
+  TORCH_CHECK((P == pool_out(H, R, sh, ph, false) || P == pool_out(H, R, sh, ph, true)) &&
+                  (Q == pool_out(W, S, sw, pw, false) || Q == pool_out(W, S, sw, pw, true)),
+              "maxpool_bwd: geometry");
   auto dx = torch::empty({N, H, W, C}, dy.options());
   check_hip(zoo_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, R, S, sh, sw, ph, pw,
                             cur_stream()),
             "maxpool_bwd");
   return dx;
+}
+
+
+std::vector<int64_t> pool_shape(int H, int W, int R, int S, int sh, int sw, int ph, int pw, bool ceil_mode) {
+  return {pool_out(H, R, sh, ph, ceil_mode), pool_out(W, S, sw, pw, ceil_mode)};
+}
+
+torch::Tensor avgpool_fwd(torch::Tensor x, int R, int S, int sh, int sw, int ph, int pw, bool ceil_mode,
+                          bool count_include_pad) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "avgpool: NHWC with C%8==0");
+  TORCH_CHECK(R >= 1 && S >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && ph * 2 <= R && pw * 2 <= S,
+              "avgpool: bad geometry");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = pool_out(H, R, sh, ph, ceil_mode), Q = pool_out(W, S, sw, pw, ceil_mode);
+  TORCH_CHECK(P > 0 && Q > 0, "avgpool: empty output");
+  auto y = torch::empty({N, P, Q, C}, x.options());
+  check_hip(zoo_avgpool_fwd(x.data_ptr(), y.data_ptr(), N, H, W, C, P, Q, R, S, sh, sw, ph, pw, count_include_pad,
+                            cur_stream()),
+            "avgpool_fwd");
+  return y;
+}
+
+torch::Tensor avgpool_bwd(torch::Tensor dy, int H, int W, int R, int S, int sh, int sw, int ph, int pw,
+                          bool count_include_pad) {
+  req(dy, at::kBFloat16, "dy");
+  TORCH_CHECK(dy.dim() == 4 && dy.size(3) % 8 == 0, "avgpool_bwd: NHWC with C%8==0");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK((P - 1) * sh - ph < H && (Q - 1) * sw - pw < W, "avgpool_bwd: geometry");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  check_hip(zoo_avgpool_bwd(dy.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, R, S, sh, sw, ph, pw, count_include_pad,
+                            cur_stream()),
+            "avgpool_bwd");
+  return dx;
+}
+
+// depthwise conv: x [N,H,W,C] bf16, w [R*S, C] bf16 (tap-major)
+std::vector<int> dw_geom(const torch::Tensor& x, int R, int S, int sh, int sw, int ph, int pw, int P, int Q) {
+  return {(int)x.size(0), (int)x.size(1), (int)x.size(2), (int)x.size(3), P, Q, R, S, sh, sw, ph, pw};
+}
+
+torch::Tensor dwconv_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, int R, int S, int sh,
+                         int sw, int ph, int pw, int act) {
+  req(x, at::kBFloat16, "x");
+  req(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "dwconv: NHWC with C%8==0");
+  const int C = x.size(3);
+  TORCH_CHECK(w.dim() == 2 && w.size(0) == R * S && w.size(1) == C, "dwconv: w must be [R*S, C]");
+  TORCH_CHECK(R >= 1 && S >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0, "dwconv: bad geometry");
+  const int P = (x.size(1) + 2 * ph - R) / sh + 1, Q = (x.size(2) + 2 * pw - S) / sw + 1;
+  TORCH_CHECK(P > 0 && Q > 0, "dwconv: empty output");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == C, "dwconv: bias size");
+    bp = bias->data_ptr<float>();
+  }
+  auto g = dw_geom(x, R, S, sh, sw, ph, pw, P, Q);
+  auto y = torch::empty({x.size(0), P, Q, C}, x.options());
+  check_hip(zoo_dwconv_fwd(x.data_ptr(), w.data_ptr(), bp, y.data_ptr(), g.data(), act, cur_stream()), "dwconv_fwd");
+  return y;
+}
+
+torch::Tensor dwconv_dgrad(torch::Tensor dy, torch::Tensor w, int H, int W, int R, int S, int sh, int sw, int ph,
+                           int pw) {
+  req(dy, at::kBFloat16, "dy");
+  req(w, at::kBFloat16, "w");
+  const int N = dy.size(0), P = dy.size(1), Q = dy.size(2), C = dy.size(3);
+  TORCH_CHECK(C % 8 == 0 && w.size(0) == R * S && w.size(1) == C, "dwconv_dgrad: shapes");
+  TORCH_CHECK(P == (H + 2 * ph - R) / sh + 1 && Q == (W + 2 * pw - S) / sw + 1, "dwconv_dgrad: geometry");
+  auto dx = torch::empty({N, H, W, C}, dy.options());
+  std::vector<int> g = {N, H, W, C, P, Q, R, S, sh, sw, ph, pw};
+  check_hip(zoo_dwconv_dgrad(dy.data_ptr(), w.data_ptr(), dx.data_ptr(), g.data(), cur_stream()), "dwconv_dgrad");
+  return dx;
+}
+
+// dw (fp32 [R*S, C]) += wgrad
+void dwconv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int S, int sh, int sw, int ph, int pw) {
+  req(x, at::kBFloat16, "x");
+  req(dy, at::kBFloat16, "dy");
+  req(dw, at::kFloat, "dw");
+  const int C = x.size(3);
+  TORCH_CHECK(R * S <= 9, "dwconv_wgrad: at most 9 taps (3x3)");
+  TORCH_CHECK(dw.numel() == (int64_t)R * S * C && dy.size(3) == C && dy.size(0) == x.size(0), "dwconv_wgrad: shapes");
+  const int P = dy.size(1), Q = dy.size(2);
+  TORCH_CHECK(P == (x.size(1) + 2 * ph - R) / sh + 1 && Q == (x.size(2) + 2 * pw - S) / sw + 1,
+              "dwconv_wgrad: geometry");
+  auto g = dw_geom(x, R, S, sh, sw, ph, pw, P, Q);
+  check_hip(zoo_dwconv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), g.data(), cur_stream()),
+            "dwconv_wgrad");
+}
+
+// row softmax / log-softmax over the last dim (fp32 or bf16)
+torch::Tensor softmax_rows(torch::Tensor x, bool log_out) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "softmax: contiguous GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "softmax: fp32 or bf16");
+  const int n = x.size(-1);
+  const int64_t rows = n ? x.numel() / n : 0;
+  TORCH_CHECK(rows < (1LL << 31), "softmax: too many rows");
+  auto y = torch::empty_like(x);
+  if (rows == 0) return y;
+  check_hip(zoo_softmax_rows(x.data_ptr(), y.data_ptr(), (int)rows, n, log_out, x.scalar_type() == at::kFloat,
+                             cur_stream()),
+            "softmax_rows");
+  return y;
+}
+
+torch::Tensor softmax_rows_bwd(torch::Tensor y, torch::Tensor dy, bool log_out) {
+  TORCH_CHECK(y.is_cuda() && y.is_contiguous() && dy.is_contiguous() && dy.sizes() == y.sizes() &&
+                  dy.scalar_type() == y.scalar_type(), "softmax_bwd: matching contiguous GPU tensors");
+  const int n = y.size(-1);
+  const int64_t rows = n ? y.numel() / n : 0;
+  auto dx = torch::empty_like(y);
+  if (rows == 0) return dx;
+  check_hip(zoo_softmax_rows_bwd(y.data_ptr(), dy.data_ptr(), dx.data_ptr(), (int)rows, n, log_out,
+                                 y.scalar_type() == at::kFloat, cur_stream()),
+            "softmax_rows_bwd");
+  return dx;
+}
+
+// cross-channel LRN over the last dim; backward when dy is given
+torch::Tensor lrn(torch::Tensor x, c10::optional<torch::Tensor> dy, int size, double alpha, double beta, double k) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "lrn: contiguous GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "lrn: fp32 or bf16");
+  TORCH_CHECK(size >= 1 && size <= 15, "lrn: window size 1..15");
+  const int C = x.size(-1);
+  const size_t rows = C ? x.numel() / C : 0;
+  auto out = torch::empty_like(x);
+  const bool bwd = dy.has_value() && dy->defined();
+  if (bwd) TORCH_CHECK(dy->is_contiguous() && dy->sizes() == x.sizes() && dy->scalar_type() == x.scalar_type(),
+                       "lrn: dy must match x");
+  if (rows == 0) return out;
+  check_hip(zoo_lrn(x.data_ptr(), bwd ? dy->data_ptr() : nullptr, out.data_ptr(), rows, C, size, (float)alpha,
+                    (float)beta, (float)k, bwd, x.scalar_type() == at::kFloat, cur_stream()),
+            "lrn");
+  return out;
 }
 
 torch::Tensor gap_fwd(torch::Tensor x) {
@@ -1101,6 +1258,15 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);
   m.def("conv_wgrad", &conv_wgrad);
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("pool_shape", &pool_shape);
+  m.def("dwconv_fwd", &dwconv_fwd);
+  m.def("dwconv_dgrad", &dwconv_dgrad);
+  m.def("dwconv_wgrad", &dwconv_wgrad);
+  m.def("softmax_rows", &softmax_rows);
+  m.def("softmax_rows_bwd", &softmax_rows_bwd);
+  m.def("lrn", &lrn);
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });
   m.def("get_deterministic", []() { return g_deterministic; });
   m.def("set_reduce_modes", [](bool stats_part, bool wgrad_part) {

@@ -130,3 +130,115 @@ def embedding(idx, table, padding_idx=None, compute_dtype=None):
         return _EmbeddingFn.apply(table, idx.contiguous(), pad, compute_dtype)
     out = F.embedding(idx, table, padding_idx=padding_idx)
     return out if compute_dtype is None else out.to(compute_dtype)
+
+
+# ---------------------------------------------------------------------------
+# depthwise convolution (NHWC bf16, tap-major weight [R*S, C])
+# ---------------------------------------------------------------------------
+class _DwConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, bias, R, S, stride, pad, act):
+        C_ = native()
+        wb = w.detach().to(torch.bfloat16).contiguous()
+        y = C_.dwconv_fwd(x, wb, None if bias is None else bias.detach().float().contiguous(), R, S, stride[0],
+                          stride[1], pad[0], pad[1], _ACT.get(act, 0))
+        ctx.save_for_backward(x, w, y if act == "relu" else None)
+        ctx.g = (R, S, stride, pad, act, bias is not None, x.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = native()
+        x, w, y = ctx.saved_tensors
+        R, S, stride, pad, act, has_bias, xs = ctx.g
+        dy = dy.contiguous().to(torch.bfloat16)
+        if act == "relu":
+            dy = dy * (y > 0).to(dy.dtype)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = C_.dwconv_dgrad(dy, w.detach().to(torch.bfloat16).contiguous(), xs[1], xs[2], R, S, stride[0],
+                                 stride[1], pad[0], pad[1])
+        if ctx.needs_input_grad[1]:
+            tgt, own = _target(w)
+            C_.dwconv_wgrad(x, dy, tgt, R, S, stride[0], stride[1], pad[0], pad[1])
+            if own:
+                _ready(w)
+            else:
+                dw = tgt.to(w.dtype)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.float().reshape(-1, dy.shape[-1]).sum(0)
+        return dx, dw, db, None, None, None, None, None
+
+
+_ACT = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
+
+
+def depthwise_conv2d_nhwc(x, w, bias=None, kernel=(3, 3), stride=(1, 1), pad=(0, 0), act=None):
+    """Depthwise conv, x [N,H,W,C], w [R*S, C] (tap-major), optional fused bias + relu."""
+    R, S = kernel
+    C = x.shape[-1]
+    if x.is_cuda and C % 8 == 0 and R * S <= 9 and act in (None, "linear", "relu"):
+        return _DwConvFn.apply(x.to(torch.bfloat16).contiguous(), w, bias, R, S, tuple(stride), tuple(pad), act)
+    wt = w.float().t().reshape(C, 1, R, S)
+    y = F.conv2d(x.permute(0, 3, 1, 2).float(), wt, None if bias is None else bias.float(), stride, pad, groups=C)
+    if act == "relu":
+        y = torch.relu(y)
+    elif act not in (None, "linear"):
+        y = getattr(torch, act)(y)
+    return y.permute(0, 2, 3, 1).to(x.dtype)
+
+
+# ---------------------------------------------------------------------------
+# row softmax / log-softmax (last dim)
+# ---------------------------------------------------------------------------
+class _SoftmaxFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, log_out):
+        y = native().softmax_rows(x, log_out)
+        ctx.save_for_backward(y)
+        ctx.log_out = log_out
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        (y,) = ctx.saved_tensors
+        return native().softmax_rows_bwd(y, dy.contiguous().to(y.dtype), ctx.log_out), None
+
+
+def softmax(x, dim=-1, log=False):
+    """Softmax / LogSoftmax over ``dim`` on the native row kernel (fp32 or bf16)."""
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.numel() > 0:
+        moved = dim not in (-1, x.dim() - 1)
+        xt = x.movedim(dim, -1) if moved else x
+        y = _SoftmaxFn.apply(xt.contiguous(), bool(log))
+        return y.movedim(-1, dim) if moved else y
+    return F.log_softmax(x, dim) if log else F.softmax(x, dim)
+
+
+# ---------------------------------------------------------------------------
+# cross-channel LRN (channels last)
+# ---------------------------------------------------------------------------
+class _LRNFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, size, alpha, beta, k):
+        ctx.save_for_backward(x)
+        ctx.p = (size, alpha, beta, k)
+        return native().lrn(x, None, size, alpha, beta, k)
+
+    @staticmethod
+    def backward(ctx, dy):
+        (x,) = ctx.saved_tensors
+        size, alpha, beta, k = ctx.p
+        return native().lrn(x, dy.contiguous().to(x.dtype), size, alpha, beta, k), None, None, None, None
+
+
+def lrn_channels_last(x, size=5, alpha=1e-4, beta=0.75, k=1.0):
+    """y = x * (k + alpha/size * sum_{window} x^2)^-beta over the LAST dim (BigDL
+    SpatialCrossMapLRN semantics; the window is centred, (size-1)/2 below)."""
+    if x.is_cuda and x.dtype in (torch.float32, torch.bfloat16) and x.numel() > 0:
+        return _LRNFn.apply(x.contiguous(), int(size), float(alpha), float(beta), float(k))
+    xc = x.float()
+    lo = (size - 1) // 2
+    sq = F.pad((xc * xc).unsqueeze(1), (lo, size - 1 - lo)).squeeze(1)
+    s = sq.unfold(-1, size, 1).sum(-1)
+    return (xc * (k + alpha / size * s) ** (-beta)).to(x.dtype)
