@@ -1,9 +1,12 @@
 """Image-classification backbones of the reference's ImageClassifier configs
 (Zs/models/image/imageclassification/ImageClassificationConfig.scala:56-190:
 alexnet, inception-v1, inception-v3, resnet-50, vgg-16/19, densenet-161,
-squeezenet, mobilenet, mobilenet-v2). NCHW PyTorch-ROCm modules (MIOpen /
-hipBLASLt) — ResNet-50 is the framework's native NHWC implementation
-(zoo.models.image.resnet) and is used for "resnet-50" instead.
+squeezenet, mobilenet, mobilenet-v2).
+
+``build(name)`` returns the framework's native NHWC bf16 implementation
+(zoo.models.image.native_nets, zoo.models.image.resnet). The plain NCHW
+``torch.nn`` definitions below are kept as the architecture reference
+(``build(name, native=False)``) for parity tests.
 """
 import torch
 import torch.nn as nn
@@ -236,11 +239,16 @@ class InceptionV3(nn.Module):
         return self.fc(F.adaptive_avg_pool2d(x, 1).flatten(1))
 
 
-def build(name, num_classes=1000):
+def build(name, num_classes=1000, native=True):
     n = name.lower()
     if n in ("resnet-50", "resnet-50-int8", "resnet-50-quantize"):
         from zoo.models.image.resnet import resnet50
         return resnet50(num_classes=num_classes)
+    if native:
+        from zoo.models.image.native_nets import TABLE
+        for k in sorted(TABLE, key=len, reverse=True):
+            if n.startswith(k):
+                return TABLE[k](num_classes)
     table = {"vgg-16": lambda: VGG(16, num_classes), "vgg-19": lambda: VGG(19, num_classes),
              "alexnet": lambda: AlexNet(num_classes), "squeezenet": lambda: SqueezeNet(num_classes),
              "mobilenet": lambda: MobileNet(num_classes), "mobilenet-v2": lambda: MobileNetV2(num_classes),

@@ -107,7 +107,8 @@ def prior_boxes(cfg):
 
 
 class NormalizeScale(nn.Module):
-    """Channel-wise L2 normalisation with a learnable per-channel scale (init 20)."""
+    """Channel-wise L2 normalisation with a learnable per-channel scale (init 20);
+    channels last (NHWC)."""
 
     def __init__(self, channels, scale=20.0, eps=1e-10):
         super().__init__()
@@ -115,67 +116,83 @@ class NormalizeScale(nn.Module):
         self.eps = eps
 
     def forward(self, x):
-        n = x.pow(2).sum(1, keepdim=True).sqrt() + self.eps
-        return x / n * self.weight.view(1, -1, 1, 1)
+        xf = x.float()
+        n = xf.pow(2).sum(-1, keepdim=True).sqrt() + self.eps
+        return (xf / n * self.weight).to(x.dtype)
 
 
 def _vgg16_base():
+    """SSD's VGG16 trunk on the native NHWC units (conv4_3 is index 12: its ReLU output
+    feeds the L2-normalised head; fc6 is the dilated 3x3, fc7 the 1x1)."""
+    from zoo.models.image.native_nets import CB, MaxPool
     cfg = [64, 64, "M", 128, 128, "M", 256, 256, 256, "C", 512, 512, 512, "M", 512, 512, 512]
-    layers, c = [], 3
+    layers, c = [], 4
     for v in cfg:
         if v == "M":
-            layers.append(nn.MaxPool2d(2, 2))
+            layers.append(MaxPool(2, 2))
         elif v == "C":
-            layers.append(nn.MaxPool2d(2, 2, ceil_mode=True))
+            layers.append(MaxPool(2, 2, ceil_mode=True))
         else:
-            layers += [nn.Conv2d(c, v, 3, padding=1), nn.ReLU(inplace=True)]
+            layers.append(CB(c, v, 3, 1, 1))
             c = v
-    layers += [nn.MaxPool2d(3, 1, 1), nn.Conv2d(512, 1024, 3, padding=6, dilation=6), nn.ReLU(True),
-               nn.Conv2d(1024, 1024, 1), nn.ReLU(True)]
+    layers += [MaxPool(3, 1, 1), CB(512, 1024, 3, 1, 6, dil=6), CB(1024, 1024, 1)]
     return nn.ModuleList(layers)
 
 
+def _heads(chans, nb, num_classes):
+    from zoo.models.image.native_nets import CB
+    loc = nn.ModuleList([CB(c, n * 4, 3, 1, 1, relu=False) for c, n in zip(chans, nb)])
+    conf = nn.ModuleList([CB(c, n * num_classes, 3, 1, 1, relu=False) for c, n in zip(chans, nb)])
+    return loc, conf
+
+
+def _multibox(loc_heads, conf_heads, feats, num_classes):
+    """NHWC head outputs [B, H, W, n*4] flatten straight into [B, H*W*n, 4]."""
+    B = feats[0].shape[0]
+    loc = torch.cat([l(f).reshape(B, -1, 4) for l, f in zip(loc_heads, feats)], 1).float()
+    conf = torch.cat([c(f).reshape(B, -1, num_classes) for c, f in zip(conf_heads, feats)], 1).float()
+    return loc, conf
+
+
 class SSD(nn.Module):
-    """SSD-VGG16 (300x300 by default). forward -> (loc [B, P, 4], conf [B, P, C])."""
+    """SSD-VGG16 (300x300 by default) on the native NHWC bf16 conv kernels.
+    forward(NCHW images) -> (loc [B, P, 4], conf [B, P, C]) in fp32."""
 
     def __init__(self, num_classes=21, cfg=None):
         super().__init__()
+        from zoo.models.image.native_nets import CB
         self.cfg = cfg or SSDConfig()
         self.num_classes = num_classes
         self.base = _vgg16_base()
         self.l2norm = NormalizeScale(512, 20.0)
         self.extras = nn.ModuleList([
-            nn.Sequential(nn.Conv2d(1024, 256, 1), nn.ReLU(True), nn.Conv2d(256, 512, 3, 2, 1), nn.ReLU(True)),
-            nn.Sequential(nn.Conv2d(512, 128, 1), nn.ReLU(True), nn.Conv2d(128, 256, 3, 2, 1), nn.ReLU(True)),
-            nn.Sequential(nn.Conv2d(256, 128, 1), nn.ReLU(True), nn.Conv2d(128, 256, 3), nn.ReLU(True)),
-            nn.Sequential(nn.Conv2d(256, 128, 1), nn.ReLU(True), nn.Conv2d(128, 256, 3), nn.ReLU(True))])
+            nn.Sequential(CB(1024, 256, 1), CB(256, 512, 3, 2, 1)),
+            nn.Sequential(CB(512, 128, 1), CB(128, 256, 3, 2, 1)),
+            nn.Sequential(CB(256, 128, 1), CB(128, 256, 3)),
+            nn.Sequential(CB(256, 128, 1), CB(128, 256, 3))])
         chans = [512, 1024, 512, 256, 256, 256]
-        nb = self.cfg.boxes_per_location()
-        self.loc = nn.ModuleList([nn.Conv2d(c, n * 4, 3, padding=1) for c, n in zip(chans, nb)])
-        self.conf = nn.ModuleList([nn.Conv2d(c, n * num_classes, 3, padding=1) for c, n in zip(chans, nb)])
+        self.loc, self.conf = _heads(chans, self.cfg.boxes_per_location(), num_classes)
         self.register_buffer("priors", prior_boxes(self.cfg))
 
     def forward(self, x):
+        from zoo.models.image.native_nets import to_nhwc
+        x = to_nhwc(x, 3, 4)
         feats = []
         for i, l in enumerate(self.base):
             x = l(x)
-            if i == 22:  # conv4_3 relu
+            if i == 12:  # conv4_3 (+ReLU)
                 feats.append(self.l2norm(x))
         feats.append(x)
         for e in self.extras:
             x = e(x)
             feats.append(x)
-        B = x.shape[0]
-        loc = torch.cat([l(f).permute(0, 2, 3, 1).reshape(B, -1, 4) for l, f in zip(self.loc, feats)], 1)
-        conf = torch.cat([c(f).permute(0, 2, 3, 1).reshape(B, -1, self.num_classes) for c, f in zip(self.conf, feats)],
-                         1)
-        return loc, conf
+        return _multibox(self.loc, self.conf, feats, self.num_classes)
 
 
 class SSDMobileNet(nn.Module):
     """SSD-MobileNet-300 ("ssd-mobilenet-300x300", ObjectDetectionConfig.scala:64-69): MobileNet v1
     taps at conv11 (19x19, 512) and conv13 (10x10, 1024) plus four extra 1x1/3x3-s2
-    stages. forward -> (loc [B, P, 4], conf [B, P, C])."""
+    stages, all on the native NHWC units. forward -> (loc [B, P, 4], conf [B, P, C])."""
 
     CONFIG = dict(resolution=300, feature_maps=(19, 10, 5, 3, 2, 1), steps=(16, 32, 64, 100, 150, 300),
                   min_sizes=(60, 105, 150, 195, 240, 285), max_sizes=(105, 150, 195, 240, 285, 300),
@@ -183,23 +200,23 @@ class SSDMobileNet(nn.Module):
 
     def __init__(self, num_classes=21):
         super().__init__()
-        from zoo.models.image.imageclassification.nets import MobileNet
+        from zoo.models.image.native_nets import CB, MobileNet
         self.cfg = SSDConfig(**self.CONFIG)
         self.num_classes = num_classes
         self.base = MobileNet(1000).features          # classifier head dropped
         self.tap = 22                                 # conv11 pointwise output (stride 16)
 
         def extra(cin, mid, cout):
-            return nn.Sequential(nn.Conv2d(cin, mid, 1), nn.ReLU(True), nn.Conv2d(mid, cout, 3, 2, 1), nn.ReLU(True))
+            return nn.Sequential(CB(cin, mid, 1), CB(mid, cout, 3, 2, 1))
         self.extras = nn.ModuleList([extra(1024, 256, 512), extra(512, 128, 256), extra(256, 128, 256),
                                      extra(256, 64, 128)])
         chans = [512, 1024, 512, 256, 256, 128]
-        nb = self.cfg.boxes_per_location()
-        self.loc = nn.ModuleList([nn.Conv2d(c, n * 4, 3, padding=1) for c, n in zip(chans, nb)])
-        self.conf = nn.ModuleList([nn.Conv2d(c, n * num_classes, 3, padding=1) for c, n in zip(chans, nb)])
+        self.loc, self.conf = _heads(chans, self.cfg.boxes_per_location(), num_classes)
         self.register_buffer("priors", prior_boxes(self.cfg))
 
     def forward(self, x):
+        from zoo.models.image.native_nets import to_nhwc
+        x = to_nhwc(x, 3, 4)
         feats = []
         for i, l in enumerate(self.base):
             x = l(x)
@@ -209,11 +226,7 @@ class SSDMobileNet(nn.Module):
         for e in self.extras:
             x = e(x)
             feats.append(x)
-        B = x.shape[0]
-        loc = torch.cat([l(f).permute(0, 2, 3, 1).reshape(B, -1, 4) for l, f in zip(self.loc, feats)], 1)
-        conf = torch.cat([c(f).permute(0, 2, 3, 1).reshape(B, -1, self.num_classes) for c, f in zip(self.conf, feats)],
-                         1)
-        return loc, conf
+        return _multibox(self.loc, self.conf, feats, self.num_classes)
 
 
 class DetectionOutputSSD(nn.Module):
