@@ -314,6 +314,57 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
   if (w == 0 && c < n2) buf[c] = (part[0][threadIdx.x] + part[1][threadIdx.x]) + (part[2][threadIdx.x] + part[3][threadIdx.x]);
 }
 
+// Backward of a conv epilogue's bias + ReLU: dy = dz * [z > 0] written out (bf16) and the
+// bias gradient sum(dy) per channel accumulated, in ONE pass (replaces a compare, a multiply,
+// a cast and a reduction launch). Z == null: no mask (bias only). Same row layout and
+// per-row-lane LDS fold as bn_reduce_kernel; out = [C] fp32 (+= per block) or partials.
+__global__ __launch_bounds__(256) void act_bwd_reduce_kernel(const bf16_t* __restrict__ dZ,
+                                                            const bf16_t* __restrict__ Z, bf16_t* __restrict__ dY,
+                                                            float* __restrict__ out, int M, int C,
+                                                            int rows_per_block, int partial) {
+  const int cpr = C >> 3;
+  const int tid = threadIdx.x;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int r0 = blockIdx.x * rows_per_block;
+  const int r1 = min(M, r0 + rows_per_block);
+  const int lanes_per_row = cpr < 256 ? cpr : 256;
+  const int row_step = 256 / lanes_per_row;
+  const int my_row = tid / lanes_per_row;
+  const int my_chunk0 = tid - my_row * lanes_per_row;
+  float* red = reinterpret_cast<float*>(smem);  // [row_step][C]
+  if (my_row < row_step) {
+    for (int chunk = my_chunk0; chunk < cpr; chunk += lanes_per_row) {
+      float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      for (int r = r0 + my_row; r < r1; r += row_step) {
+        const size_t off = (size_t)r * C + chunk * 8;
+        float a[8];
+        unpack8(*reinterpret_cast<const uint4*>(dZ + off), a);
+        if (Z) {
+          float z[8];
+          unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+          *reinterpret_cast<uint4*>(dY + off) = pack8(a);
+          unpack8(*reinterpret_cast<const uint4*>(dY + off), a);  // sum what is stored (bf16)
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) s1[e] += a[e];
+      }
+      float* rr = red + (size_t)my_row * C;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rr[chunk * 8 + e] = s1[e];
+    }
+  }
+  __syncthreads();
+  if (!out) return;
+  for (int i = tid; i < C; i += blockDim.x) {
+    float a = 0.f;
+    for (int r = 0; r < row_step; ++r) a += red[(size_t)r * C + i];
+    if (partial) out[(size_t)blockIdx.x * C + i] = a;
+    else atomicAdd(out + i, a);
+  }
+}
+
 // Deterministic fold of per-workgroup partials: out[c] += sum_p part[p][c], p in order.
 // Level 1 (nparts > kPartGroup): block (column chunk, group g) sums the group's parts,
 // 4 waves x 16 parts each then the waves in order, into lvl1[g][c]; level 2 sums the
@@ -470,4 +521,18 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                      (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
                      dgamma, dbeta, M, C, rpb);
   return hipGetLastError();
+}
+
+// dY = dZ * [Z > 0] (Z non-null) and out[c] += sum_rows dY (out non-null; partial: out is
+// [blocks][C] partials for an ordered fold by the caller). Returns the block count.
+extern "C" int zoo_act_bwd_reduce(const void* dZ, const void* Z, void* dY, float* out, int M, int C, int partial,
+                                  hipStream_t st) {
+  int blocks, rpb;
+  bn_reduce_grid(M, C, &blocks, &rpb);
+  const int cpr = C >> 3;
+  const int row_step = 256 / (cpr < 256 ? cpr : 256);
+  const size_t smem = (size_t)row_step * C * sizeof(float);
+  hipLaunchKernelGGL(act_bwd_reduce_kernel, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ, (const bf16_t*)Z,
+                     (bf16_t*)dY, out, M, C, rpb, partial);
+  return blocks;
 }

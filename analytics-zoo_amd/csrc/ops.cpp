@@ -29,6 +29,7 @@ hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
 size_t zoo_stats_part_scratch(int, int);
 hipError_t zoo_stats_part_finalize(float*, const float*, float*, int, int, hipStream_t);
 int zoo_bn_reduce_blocks(int, int);
+int zoo_act_bwd_reduce(const void*, const void*, void*, float*, int, int, int, hipStream_t);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
@@ -567,6 +568,47 @@ void dwconv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, in
   auto g = dw_geom(x, R, S, sh, sw, ph, pw, P, Q);
   check_hip(zoo_dwconv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), g.data(), cur_stream()),
             "dwconv_wgrad");
+}
+
+// conv-epilogue backward: returns dy = dz * [z > 0] (z given) and/or db (fp32 [C]) = column sums
+std::vector<torch::Tensor> act_bwd_reduce(torch::Tensor dz, c10::optional<torch::Tensor> z, bool want_db,
+                                          c10::optional<torch::Tensor> db_into) {
+  req(dz, at::kBFloat16, "dz");
+  const int C = dz.size(-1);
+  const int64_t M = dz.numel() / C;
+  TORCH_CHECK(C % 8 == 0, "act_bwd_reduce: C must be a multiple of 8");
+  TORCH_CHECK(M < (1LL << 31), "act_bwd_reduce: too many rows");
+  const bool mask = z.has_value() && z->defined();
+  if (mask) {
+    req(*z, at::kBFloat16, "z");
+    TORCH_CHECK(z->numel() == dz.numel(), "act_bwd_reduce: z shape");
+  }
+  torch::Tensor dy = mask ? torch::empty_like(dz) : dz;
+  torch::Tensor db;
+  const bool part = g_deterministic;
+  torch::Tensor partials;
+  float* out = nullptr;
+  if (want_db) {
+    if (db_into.has_value() && db_into->defined()) {  // accumulate into an existing fp32 [C] (flat grad view)
+      req(*db_into, at::kFloat, "db_into");
+      TORCH_CHECK(db_into->numel() == C, "act_bwd_reduce: db_into size");
+      db = *db_into;
+    } else {
+      db = torch::zeros({C}, dz.options().dtype(at::kFloat));
+    }
+    if (part) {
+      partials = torch::empty({(int64_t)zoo_bn_reduce_blocks((int)M, C), (int64_t)C}, db.options());
+      out = partials.data_ptr<float>();
+    } else {
+      out = db.data_ptr<float>();
+    }
+  }
+  const int blocks = zoo_act_bwd_reduce(dz.data_ptr(), mask ? z->data_ptr() : nullptr, dy.data_ptr(), out, (int)M, C,
+                                        part ? 1 : 0, cur_stream());
+  check_hip(hipGetLastError(), "act_bwd_reduce");
+  if (want_db && part) fold_partials(db.data_ptr<float>(), partials, C, blocks);
+  if (want_db) return {dy, db};
+  return {dy};
 }
 
 // row softmax / log-softmax over the last dim (fp32 or bf16)
@@ -1265,6 +1307,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_dgrad", &dwconv_dgrad);
   m.def("dwconv_wgrad", &dwconv_wgrad);
   m.def("softmax_rows", &softmax_rows);
+  m.def("act_bwd_reduce", &act_bwd_reduce);
   m.def("softmax_rows_bwd", &softmax_rows_bwd);
   m.def("lrn", &lrn);
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });

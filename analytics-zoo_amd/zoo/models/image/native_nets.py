@@ -104,7 +104,11 @@ class DWBR(nn.Module):
         self.register_buffer("running_var", torch.ones(c))
 
     def forward(self, x):
-        from zoo.ops.nn import depthwise_conv2d_nhwc
+        from zoo.ops.nn import depthwise_bn_act_eval, depthwise_conv2d_nhwc
+        if x.is_cuda and not self.training and not torch.is_grad_enabled() and x.shape[-1] % 8 == 0 and \
+                self.k[0] * self.k[1] <= 9:
+            return depthwise_bn_act_eval(x, self.weight, self.gamma, self.beta, self.running_mean, self.running_var,
+                                         self.k, self.stride, self.pad, relu=self.relu)
         y = depthwise_conv2d_nhwc(x, self.weight, None, self.k, self.stride, self.pad)
         return ops.batch_norm_nhwc(y, self.gamma, self.beta, self.running_mean, self.running_var, relu=self.relu,
                                    training=self.training)

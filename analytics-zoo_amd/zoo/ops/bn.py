@@ -217,6 +217,36 @@ def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
     return out.reshape(y.shape)
 
 
+def _folded(w, gamma, beta, running_mean, running_var, eps, cols=None):
+    """Inference-time BatchNorm folding: W' = W * gamma/sqrt(var+eps) (per output row),
+    b' = beta - mean * gamma/sqrt(var+eps). Cached on the weight parameter and rebuilt
+    when any of the five tensors changes (in-place updates bump ``_version``)."""
+    key = tuple((t.data_ptr(), t._version) for t in (w, gamma, beta, running_mean, running_var)) + (float(eps),)
+    c = getattr(w, "_zoo_bn_fold", None)
+    if c is not None and c[0] == key:
+        return c[1], c[2]
+    with torch.no_grad():
+        scale = gamma.float() * torch.rsqrt(running_var.float() + eps)
+        bias = (beta.float() - running_mean.float() * scale).contiguous()
+        shape = (-1,) + (1,) * (w.dim() - 1) if cols is None else (1, -1)
+        wf = (w.float() * scale.reshape(shape)).to(torch.bfloat16).contiguous()
+    try:
+        w._zoo_bn_fold = (key, wf, bias)
+    except (AttributeError, RuntimeError):
+        pass
+    return wf, bias
+
+
+def conv_bn_act_eval(x, w, gamma, beta, running_mean, running_var, kernel, stride, pad, eps, relu, resid=None):
+    """Eval-mode conv -> BN(running stats) -> (+resid) -> ReLU as ONE implicit-GEMM
+    launch: BN folded into the weights and a bias, residual add and ReLU in the epilogue
+    (no statistics, no separate apply pass)."""
+    wf, bf = _folded(w, gamma, beta, running_mean, running_var, eps)
+    r = None if resid is None else resid.to(torch.bfloat16).contiguous()
+    return _kern.conv_fwd(x.to(torch.bfloat16).contiguous(), wf, kernel[0], kernel[1], stride, pad, bias=bf,
+                          resid=r, act=1 if relu else 0)
+
+
 def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0),
                 eps=1e-5, momentum=0.1, relu=True, resid=None, training=True, resid_handoff=None, grad_add=None,
                 producer_in=None, producer_out=None, dx_handoff=None):
@@ -233,6 +263,9 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
     (which must run its backward later) instead of being returned — two
     consumers of one tensor then need no separate gradient-add pass."""
     R, S = kernel
+    if x.is_cuda and not training and not (torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)):
+        return conv_bn_act_eval(x, w, gamma, beta, running_mean, running_var, kernel, tuple(stride), tuple(pad),
+                                eps, relu, resid)
     if x.is_cuda:
         if x.dtype != torch.bfloat16:
             x = x.to(torch.bfloat16)
@@ -260,7 +293,7 @@ class _BNActFn(torch.autograd.Function):
     def forward(ctx, y, gamma, beta, resid, running_mean, running_var, eps, momentum, relu, training):
         C_ = native()
         K = y.shape[-1]
-        stats = workspace.zeros(stat_len(K), y.device)
+        stats = workspace.zeros(stat_len(K), y.device) if training else torch.empty(0, device=y.device)
         ctx.sync = bool(training) and sync_bn_active()
         if training:
             C_.bn_reduce(y, None, None, None, None, stats, 0)

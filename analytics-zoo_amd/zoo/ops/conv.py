@@ -105,6 +105,7 @@ class _Conv2dFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, w, bias, R, S, stride, pad, dil, act, out_f32):
+        ctx.bias_ref = bias
         wb = bf16_weight(w)
         y = _kern.conv_fwd(x, wb, R, S, stride, pad, dil, bias=None if bias is None else bias.detach().float().contiguous(),
                            act=ACT_CODES[act], out_f32=out_f32, out_bf16=not out_f32)
@@ -118,7 +119,25 @@ class _Conv2dFn(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         R, S, stride, pad, dil, act, xshape, has_bias = ctx.geom
         dy = dy.contiguous()
-        if act == "relu":
+        db_native = None
+        K = w.shape[0]
+        want_db = bool(has_bias and ctx.needs_input_grad[2])
+        if K % 8 == 0 and dy.is_cuda and ((act == "relu" and y.dtype == torch.bfloat16) or
+                                          (act in (None, "linear") and want_db)):
+            # ReLU mask + bias-gradient column sums in one native pass
+            # the bias gradient goes straight into the engine's flat gradient buffer when there is one
+            bref = getattr(ctx, "bias_ref", None)
+            into = getattr(bref, "_zoo_grad", None) if (want_db and bref is not None) else None
+            into = into if (into is not None and into.is_contiguous() and into.numel() == K) else None
+            outs = C_.act_bwd_reduce(dy.to(torch.bfloat16).contiguous(), y if act == "relu" else None, want_db, into)
+            dy = outs[0]
+            db_native = outs[1] if len(outs) > 1 else None
+            if into is not None:
+                hook = getattr(bref, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(bref)
+                db_native = "flat"
+        elif act == "relu":
             dy = dy * (y > 0).to(dy.dtype)
         elif act not in (None, "linear"):
             yf = y.float()
@@ -145,7 +164,9 @@ class _Conv2dFn(torch.autograd.Function):
                 hook = getattr(w, "_zoo_grad_ready", None)
                 if hook is not None:
                     hook(w)
-        if has_bias and ctx.needs_input_grad[2]:
+        if has_bias and ctx.needs_input_grad[2] and db_native is not None:
+            db = None if isinstance(db_native, str) else db_native
+        elif has_bias and ctx.needs_input_grad[2]:
             if K % 8 == 0:  # native channel reduction (16-byte loads, ~1024 blocks) instead of torch's sum
                 st = torch.zeros(C_.stat_len(K), dtype=torch.float32, device=dyb.device)  # slotted atomics
                 C_.bn_reduce(dyb, None, None, None, None, st, 0)

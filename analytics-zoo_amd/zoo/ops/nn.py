@@ -138,8 +138,9 @@ def embedding(idx, table, padding_idx=None, compute_dtype=None):
 class _DwConvFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, bias, R, S, stride, pad, act):
+        from zoo.ops.conv import bf16_weight
         C_ = native()
-        wb = w.detach().to(torch.bfloat16).contiguous()
+        wb = bf16_weight(w).contiguous()
         y = C_.dwconv_fwd(x, wb, None if bias is None else bias.detach().float().contiguous(), R, S, stride[0],
                           stride[1], pad[0], pad[1], _ACT.get(act, 0))
         ctx.save_for_backward(x, w, y if act == "relu" else None)
@@ -156,8 +157,9 @@ class _DwConvFn(torch.autograd.Function):
             dy = dy * (y > 0).to(dy.dtype)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = C_.dwconv_dgrad(dy, w.detach().to(torch.bfloat16).contiguous(), xs[1], xs[2], R, S, stride[0],
-                                 stride[1], pad[0], pad[1])
+            from zoo.ops.conv import bf16_weight
+            dx = C_.dwconv_dgrad(dy, bf16_weight(w).contiguous(), xs[1], xs[2], R, S, stride[0], stride[1], pad[0],
+                                 pad[1])
         if ctx.needs_input_grad[1]:
             tgt, own = _target(w)
             C_.dwconv_wgrad(x, dy, tgt, R, S, stride[0], stride[1], pad[0], pad[1])
@@ -171,6 +173,15 @@ class _DwConvFn(torch.autograd.Function):
 
 
 _ACT = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
+
+
+def depthwise_bn_act_eval(x, w, gamma, beta, running_mean, running_var, kernel, stride, pad, eps=1e-5, relu=True):
+    """Eval-mode depthwise conv -> BN(running stats) -> ReLU as one kernel (BN folded into
+    the per-channel taps and a bias)."""
+    from zoo.ops.bn import _folded
+    wf, bf = _folded(w, gamma, beta, running_mean, running_var, eps, cols=True)
+    return native().dwconv_fwd(x.to(torch.bfloat16).contiguous(), wf, bf, kernel[0], kernel[1], stride[0], stride[1],
+                               pad[0], pad[1], 1 if relu else 0)
 
 
 def depthwise_conv2d_nhwc(x, w, bias=None, kernel=(3, 3), stride=(1, 1), pad=(0, 0), act=None):
