@@ -113,12 +113,13 @@ def apply_activation(x, name):
     if callable(name):
         return name(x)
     n = name.lower()
-    if n == "softmax":
-        return torch.softmax(x, dim=-1) if x.dim() != 4 else torch.softmax(x, dim=1)
-    if n == "softmin":
-        return torch.softmax(-x, dim=-1)
-    if n == "log_softmax":
-        return torch.log_softmax(x, dim=-1)
+    if n in ("softmax", "softmin", "log_softmax"):
+        from zoo.ops.nn import softmax  # native row kernel on the GPU
+        if n == "softmax":
+            return softmax(x, -1 if x.dim() != 4 else 1)
+        if n == "softmin":
+            return softmax(-x, -1)
+        return softmax(x, -1, log=True)
     if n not in _ACTS:
         raise ValueError("Unsupported activation: %s" % name)
     return _ACTS[n](x)

@@ -116,8 +116,11 @@ class _Conv2DBase(Layer):
 
     def call(self, x):
         if self.dim_ordering == "th":
+            # channels-last propagation: the NCHW result is a view of the NHWC output
+            # (torch.channels_last memory), so the next th layer's permute back to NHWC is
+            # free; only the graph input pays one NCHW -> NHWC copy
             y = self._conv_nhwc(x.permute(0, 2, 3, 1))
-            return y.permute(0, 3, 1, 2).contiguous()
+            return y.permute(0, 3, 1, 2)
         return self._conv_nhwc(x).contiguous()
 
     # ---- weights in the reference layouts ----

@@ -44,14 +44,23 @@ class BatchNormalization(Layer):
             y = ops.batch_norm_nhwc(x, self.gamma, self.beta, self.running_mean, self.running_var, self.epsilon,
                                     self.momentum, relu=False, training=self.training)
             return y.to(x.dtype)
+        if x.dim() == 4 and x.is_cuda and self.nc % 8 == 0:
+            # th ordering on the native NHWC kernel (a free view for channels-last memory)
+            y = ops.batch_norm_nhwc(x.permute(0, 2, 3, 1).contiguous(), self.gamma, self.beta, self.running_mean,
+                                    self.running_var, self.epsilon, self.momentum, relu=False,
+                                    training=self.training)
+            return y.to(x.dtype).permute(0, 3, 1, 2)
         if x.dim() == 4 and self.dim_ordering == "tf":
             xc = x.permute(0, 3, 1, 2)
         elif x.dim() == 3:
             xc = x.transpose(1, 2)
         else:
             xc = x
-        y = F.batch_norm(xc, self.running_mean, self.running_var, self.gamma.to(xc.dtype), self.beta.to(xc.dtype),
-                         self.training, self.momentum, self.epsilon)
+        # generic fallback (channel counts the NHWC kernel does not take) on ATen's own kernels,
+        # not MIOpen's
+        with torch.backends.cudnn.flags(enabled=False):
+            y = F.batch_norm(xc, self.running_mean, self.running_var, self.gamma.to(xc.dtype),
+                             self.beta.to(xc.dtype), self.training, self.momentum, self.epsilon)
         if x.dim() == 4 and self.dim_ordering == "tf":
             y = y.permute(0, 2, 3, 1)
         elif x.dim() == 3:

@@ -58,11 +58,32 @@ class _Pool2D(Layer):
         fill = float("-inf") if self.kind == "max" else 0.0
         return F.pad(x, (pw[0], pw[1], ph[0], ph[1]), value=fill), (0, 0)
 
+    def _native(self, xn):
+        """NHWC x -> NHWC pooled on the native kernels; None if the geometry is unsupported."""
+        pad = (0, 0)
+        if self.border_mode == "same":
+            ph = _same_pad(xn.shape[1], self.pool_size[0], self.strides[0])
+            pw = _same_pad(xn.shape[2], self.pool_size[1], self.strides[1])
+            if ph[0] != ph[1] or pw[0] != pw[1]:
+                return None
+            pad = (ph[0], pw[0])
+        if self.kind == "max":
+            return ops.max_pool2d_nhwc(xn, self.pool_size, self.strides, pad)
+        from zoo.ops.pool import avg_pool2d_nhwc
+        if 2 * pad[0] > self.pool_size[0] or 2 * pad[1] > self.pool_size[1]:
+            return None
+        return avg_pool2d_nhwc(xn, self.pool_size, self.strides, pad, count_include_pad=self.count_include_pad)
+
     def call(self, x):
-        native_ok = (self.kind == "max" and self.dim_ordering == "tf" and x.is_cuda and x.shape[-1] % 8 == 0
-                     and self.border_mode != "same")
-        if native_ok:
-            return ops.max_pool2d_nhwc(x, self.pool_size, self.strides, (0, 0)).to(x.dtype)
+        if x.is_cuda and x.dim() == 4:
+            th = self.dim_ordering == "th"
+            xn = x.permute(0, 2, 3, 1) if th else x
+            c = xn.shape[-1]
+            xp = xn if c % 8 == 0 else F.pad(xn, (0, (-c) % 8))  # the kernels move 8 channels per lane
+            y = self._native(xp.contiguous())
+            if y is not None:
+                y = y.to(x.dtype)[..., :c]
+                return y.permute(0, 3, 1, 2) if th else y
         xc = x if self.dim_ordering == "th" else x.permute(0, 3, 1, 2)
         xc, pad = self._pad_nchw(xc)
         if self.kind == "max":
@@ -164,8 +185,11 @@ class GlobalAveragePooling2D(Layer):
         return (None, s[1] if self.dim_ordering == "th" else s[3])
 
     def call(self, x):
-        if self.dim_ordering == "tf" and x.is_cuda and x.shape[-1] % 8 == 0:
-            return ops.global_avg_pool_nhwc(x).to(x.dtype)
+        if x.is_cuda and x.dim() == 4:
+            xn = x.permute(0, 2, 3, 1) if self.dim_ordering == "th" else x
+            c = xn.shape[-1]
+            xp = xn if c % 8 == 0 else F.pad(xn, (0, (-c) % 8))
+            return ops.global_avg_pool_nhwc(xp.contiguous()).to(x.dtype)[:, :c]
         return x.mean(dim=(2, 3)) if self.dim_ordering == "th" else x.mean(dim=(1, 2))
 
 

@@ -108,7 +108,8 @@ class Softmax(Layer):
     """Softmax over the last dimension (max-shifted, InternalSoftmax)."""
 
     def call(self, x):
-        return torch.softmax(x, dim=-1)
+        from zoo.ops.nn import softmax
+        return softmax(x, -1)
 
 
 class Recurrent(Layer):

@@ -97,11 +97,13 @@ def _batch_mode(v):
 
 
 def _lsm(x):
-    return F.log_softmax(x, dim=-1)
+    from zoo.ops.nn import softmax
+    return softmax(x, -1, log=True)
 
 
 def _sm(x):
-    return F.softmax(x, dim=-1)
+    from zoo.ops.nn import softmax
+    return softmax(x, -1)
 
 
 def convert(spec, st):
