@@ -41,6 +41,14 @@ struct BwdStats {
   float* sums;        // [2*K]
 };
 
+// One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):
+// Wt[c][t][u][k] = W[k][r0 + sh*(Ra-1-t)][s0 + sw*(Sb-1-u)][c]; blocks [blk0, blk0+nblk).
+struct FlipDesc {
+  const void* W;   // bf16
+  void* Wt;        // bf16
+  int K, R, S, C, ldw, r0, s0, Ra, Sb, sh, sw, ldt, blk0, nblk;
+};
+
 // Plain GEMM geometry (gemm256.hip): Y[M, N] = A[M, K] . B[N, K]^T
 struct GemmGeom {
   int M, N, K;

@@ -570,6 +570,32 @@ __global__ void flip_weights_kernel(const bf16_t* __restrict__ W, bf16_t* __rest
   }
 }
 
+// All the flipped (sub-)filters a training step's dgrads need, in ONE launch (once per
+// optimizer step instead of one launch per conv per backward). Descriptor d owns blocks
+// [blk0, blk0 + nblk); the descriptor table is sorted by blk0.
+__global__ __launch_bounds__(256) void flip_weights_batched_kernel(const FlipDesc* __restrict__ descs, int n) {
+  int lo = 0, hi = n - 1;
+  const int b = blockIdx.x;
+  while (lo < hi) {  // last descriptor with blk0 <= b (uniform across the block)
+    const int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].blk0 <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  const FlipDesc d = descs[lo];
+  const int total = d.C * d.Ra * d.Sb * d.K;
+  const int step = d.nblk * blockDim.x;
+  for (int idx = (b - d.blk0) * blockDim.x + threadIdx.x; idx < total; idx += step) {
+    int t = idx;
+    const int k = t % d.K; t /= d.K;
+    const int u = t % d.Sb; t /= d.Sb;
+    const int v = t % d.Ra; t /= d.Ra;
+    const int c = t;
+    const int r = d.r0 + d.sh * (d.Ra - 1 - v), s = d.s0 + d.sw * (d.Sb - 1 - u);
+    static_cast<bf16_t*>(d.Wt)[(size_t)c * d.ldt + (v * d.Sb + u) * d.K + k] =
+        static_cast<const bf16_t*>(d.W)[(size_t)k * d.ldw + (r * d.S + s) * d.C + c];
+  }
+}
+
 size_t igemm_smem_bytes(int BN, int nbuf = 2, bool lean = false) {
   const size_t main_bytes = (size_t)nbuf * (IG_BM + BN) * IG_BK * sizeof(bf16_t);
   const size_t epi_bytes = lean ? ((size_t)IG_BM * (BN + 4) * sizeof(bf16_t) + 15) / 16 * 16 +
@@ -667,5 +693,12 @@ extern "C" hipError_t zoo_flip_weights(const void* W, void* Wt, int K, int R, in
   const int blocks = (total + 255) / 256 < 2048 ? (total + 255) / 256 : 2048;
   hipLaunchKernelGGL(flip_weights_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const bf16_t*)W,
                      (bf16_t*)Wt, K, R, S, C, ldw, r0, s0, Ra, Sb, sh, sw, ldt);
+  return hipGetLastError();
+}
+
+// descs: device array of n FlipDesc sorted by blk0; nblocks = last.blk0 + last.nblk
+extern "C" hipError_t zoo_flip_weights_batched(const void* descs, int n, int nblocks, hipStream_t st) {
+  if (n <= 0 || nblocks <= 0) return hipSuccess;
+  hipLaunchKernelGGL(flip_weights_batched_kernel, dim3(nblocks), dim3(256), 0, st, (const FlipDesc*)descs, n);
   return hipGetLastError();
 }

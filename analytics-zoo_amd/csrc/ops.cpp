@@ -23,6 +23,7 @@ hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, co
                        int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                             hipStream_t);
+hipError_t zoo_flip_weights_batched(const void*, int, int, hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
 int zoo_wgrad_plan(WgradGeom*);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
@@ -290,6 +291,19 @@ torch::Tensor flip_weights(torch::Tensor w, int K, int R, int S, int C, int r0, 
             "flip_weights");
   return wt;
 }
+
+// Batched flip into preallocated outputs. `table` is a device int64 tensor of n rows x 16:
+// (W ptr, Wt ptr, K, R, S, C, ldw, r0, s0, Ra, Sb, sh, sw, ldt, blk0, nblk), written by
+// zoo.ops._kern.FlipCache from tensors it keeps alive and validated there with the same
+// checks as flip_weights (every row was first produced by flip_weights for that geometry).
+void flip_weights_batched(torch::Tensor table, int n, int nblocks) {
+  TORCH_CHECK(table.is_cuda() && table.scalar_type() == at::kInt && table.is_contiguous() &&
+                  table.numel() == (int64_t)n * (int64_t)(sizeof(zoo::FlipDesc) / sizeof(int)),
+              "flip_weights_batched: table must be a contiguous int32 [n, sizeof(FlipDesc)/4] device tensor");
+  check_hip(zoo_flip_weights_batched(table.data_ptr(), n, nblocks, cur_stream()), "flip_weights_batched");
+}
+
+int flip_desc_ints() { return (int)(sizeof(zoo::FlipDesc) / sizeof(int)); }
 
 // dW (fp32, [K, ldw]) += wgrad(x, dy)
 void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int S, int sh, int sw, int ph, int pw,
@@ -1299,6 +1313,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);
+  m.def("flip_weights_batched", &flip_weights_batched);
+  m.def("flip_desc_ints", &flip_desc_ints);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

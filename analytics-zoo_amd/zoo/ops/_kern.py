@@ -29,8 +29,109 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
                              list(omap) if omap else [], bz, by, bm, bi, bsum)
 
 
+# ---------------------------------------------------------------------------
+# Flipped dgrad filters, refreshed in ONE batched launch per weight update.
+#
+# Every dgrad needs its filter flipped to [Cin][R][S][Cout] (and strided convs one
+# sub-filter per output-parity class). Done per call that is one small launch per conv
+# per backward (62 on ResNet-50, profiles/resnet50_b256_r2_lean.md). For weights that
+# live in a FlatParams bf16 buffer -- rewritten only by the fused optimizer kernels and
+# refresh_bf16, which bump ``weights_epoch`` -- the flipped copies are cached, and the
+# first dgrad after an update re-flips ALL cached filters with one
+# ``flip_weights_batched`` launch. Other weights (inference, plain modules) and calls
+# made while a hipGraph is being captured flip directly, as before.
+# ---------------------------------------------------------------------------
+_EPOCH = [0]
+_CACHE_ON = __import__("os").environ.get("ZOO_FLIP_CACHE", "1") != "0"
+_FLATS = {}             # id(FlatParams.bf16) -> weakref(FlatParams)
+
+
+def bump_weights_epoch():
+    """Called by every writer of a FlatParams bf16 buffer (optimizer steps, refresh_bf16)."""
+    _EPOCH[0] += 1
+
+
+def weights_epoch():
+    return _EPOCH[0]
+
+
+def register_flat(flat):
+    """Give a FlatParams its own flip cache (it dies with the FlatParams, so cached
+    pointers never outlive the buffer they point into)."""
+    import weakref
+    if flat.bf16 is not None and flat.bf16.is_cuda:
+        for k in [k for k, r in _FLATS.items() if r() is None]:
+            del _FLATS[k]
+        _FLATS[id(flat.bf16)] = weakref.ref(flat)
+        flat._flip_cache = _FlipCache()
+        bump_weights_epoch()
+
+
+def _owner_cache(w):
+    """The flip cache of the FlatParams whose bf16 buffer ``w`` is a view of, else None."""
+    if not _CACHE_ON or not _FLATS or not w.is_cuda:
+        return None
+    base = w._base if w._base is not None else w
+    ref = _FLATS.get(id(base))
+    f = ref() if ref is not None else None
+    if f is None or f.bf16 is not base:
+        return None
+    return getattr(f, "_flip_cache", None)
+
+
+class _FlipCache:
+    def __init__(self):
+        self.entries = {}     # key -> [w, wt, epoch]
+        self.table = None     # device int32 [n, desc_ints]
+        self.table_n = 0
+        self.nblocks = 0
+
+    def _build_table(self):
+        import numpy as np
+        m = native()
+        di = m.flip_desc_ints()
+        ents = list(self.entries.items())
+        arr = np.zeros((len(ents), di), dtype=np.int32)
+        ptrs = arr[:, 0:4].copy().view(np.int64)
+        blk = 0
+        for i, (key, (w, wt, _)) in enumerate(ents):
+            _, K, R, S, C, r0, s0, Ra, Sb, sh, sw = key
+            total = C * Ra * Sb * K
+            nblk = max(1, min(256, (total + 1023) // 1024))
+            ptrs[i, 0] = w.data_ptr()
+            ptrs[i, 1] = wt.data_ptr()
+            arr[i, 4:18] = (K, R, S, C, w.shape[1], r0, s0, Ra, Sb, sh, sw, wt.shape[1], blk, nblk)
+            blk += nblk
+        arr[:, 0:4] = ptrs.view(np.int32)
+        dev = ents[0][1][0].device
+        self.table = torch.from_numpy(arr).to(dev)
+        self.table_n = len(ents)
+        self.nblocks = blk
+
+    def get(self, w, K, R, S, C, r0, s0, Ra, Sb, sh, sw):
+        key = (w.data_ptr(), K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+        ep = _EPOCH[0]
+        ent = self.entries.get(key)
+        if ent is not None and ent[0].shape == w.shape:
+            if ent[2] != ep:
+                if self.table is None or self.table_n != len(self.entries):
+                    self._build_table()
+                native().flip_weights_batched(self.table, self.table_n, self.nblocks)
+                for e in self.entries.values():
+                    e[2] = ep
+            return ent[1]
+        wt = native().flip_weights(w, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+        self.entries[key] = [w, wt, ep]
+        self.table = None
+        return wt
+
+
 def flip_weights(w, K, R, S, C, r0=0, s0=0, Ra=None, Sb=None, sh=1, sw=1):
-    return native().flip_weights(w, K, R, S, C, r0, s0, Ra or R, Sb or S, sh, sw)
+    Ra, Sb = Ra or R, Sb or S
+    cache = _owner_cache(w)
+    if cache is not None and not torch.cuda.is_current_stream_capturing():
+        return cache.get(w, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+    return native().flip_weights(w, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
 
 
 def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None,

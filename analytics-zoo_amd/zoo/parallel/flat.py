@@ -57,12 +57,17 @@ class FlatParams:
             p.grad = gview
             if self.bf16 is not None:
                 p._zoo_bf16 = self.bf16[o:o + n].view(p.shape)
+        if self.bf16 is not None:
+            from zoo.ops._kern import register_flat
+            register_flat(self)
         self.refresh_bf16()
 
     # ------------------------------------------------------------------
     def refresh_bf16(self):
         if self.bf16 is not None:
             self.bf16.copy_(self.master)
+            from zoo.ops._kern import bump_weights_epoch
+            bump_weights_epoch()
 
     def zero_grad(self):
         self.grad.zero_()

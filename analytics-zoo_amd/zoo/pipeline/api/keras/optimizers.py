@@ -234,6 +234,9 @@ class OptimMethod:
                 self._step_torch(master, grad * gscale, bufs, lr)
                 if bf16 is not None:
                     bf16.copy_(master)
+        if bf16 is not None:
+            from zoo.ops._kern import bump_weights_epoch
+            bump_weights_epoch()   # cached dgrad filter flips are stale now
         self.state["neval"] += 1
         self.state["evalCounter"] += 1
 

@@ -671,3 +671,31 @@ def test_dropout_add_kernel(gpu):
     out2 = dropout_add(a.detach(), x.detach(), p, True)
     assert not torch.equal(out2, out.detach())
     assert torch.equal(dropout_add(a.detach(), x.detach(), p, False), x.detach() + a.detach())
+
+
+def test_batched_flip_cache_tracks_weight_updates(gpu):
+    """Flat-managed dgrad filters are flipped once per weight update by ONE batched launch;
+    the cached copies must equal a direct flip after every optimizer write."""
+    from zoo.ops import _kern
+    from zoo.ops._native import native
+    from zoo.parallel.flat import FlatParams
+    from zoo.pipeline.api.keras.optimizers import SGD
+    torch.manual_seed(0)
+    ps = [torch.nn.Parameter(torch.randn(64, 3 * 3 * 32, device=gpu)),
+          torch.nn.Parameter(torch.randn(128, 64, device=gpu)),
+          torch.nn.Parameter(torch.randn(48, 5 * 5 * 16, device=gpu))]
+    flat = FlatParams(ps, device=gpu)
+    specs = [(ps[0], (64, 3, 3, 32, 0, 0, 3, 3, 1, 1)), (ps[0], (64, 3, 3, 32, 1, 0, 1, 2, 2, 2)),
+             (ps[1], (128, 1, 1, 64, 0, 0, 1, 1, 1, 1)), (ps[2], (48, 5, 5, 16, 0, 1, 3, 2, 2, 2))]
+    opt = SGD(learningrate=0.5, momentum=0.9)
+    for it in range(3):
+        outs = [_kern.flip_weights(p._zoo_bf16, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+                for p, (K, R, S, C, r0, s0, Ra, Sb, sh, sw) in specs]
+        for (p, (K, R, S, C, r0, s0, Ra, Sb, sh, sw)), o in zip(specs, outs):
+            ref = native().flip_weights(p._zoo_bf16, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
+            assert torch.equal(o, ref), (it, K, R, S, C)
+        flat.grad.normal_()
+        opt.step(flat.master, flat.grad, flat.bf16, 1.0)
+    assert len(flat._flip_cache.entries) == len(specs)
+    assert _kern._owner_cache(ps[0]._zoo_bf16) is flat._flip_cache
+    assert _kern._owner_cache(ps[0]._zoo_bf16.clone()) is None
