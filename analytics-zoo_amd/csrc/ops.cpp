@@ -87,6 +87,14 @@ hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, voi
                         float, int, const long*, hipStream_t);
 hipError_t zoo_rnn(const zoo::RnnArgs*, int, int, int, hipStream_t);
 hipError_t zoo_nms_mask(const float*, int, float, unsigned long long*, hipStream_t);
+hipError_t zoo_embedding_bag_fwd(const float*, const int64_t*, const int64_t*, int, const float*, float*, float*, int,
+                                 int, int, int64_t, int64_t, int, float, hipStream_t);
+hipError_t zoo_embedding_bag_bwd(const float*, const float*, const int64_t*, const int64_t*, int, const float*,
+                                 const float*, float*, int, int, int, int64_t, int64_t, float, hipStream_t);
+hipError_t zoo_sparse_linear_fwd(const int64_t*, const int64_t*, const float*, const float*, const float*, float*, int,
+                                 int, int, int64_t, hipStream_t);
+hipError_t zoo_sparse_linear_bwd(const int64_t*, const int64_t*, const float*, const float*, float*, float*, int64_t,
+                                 int, int, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
@@ -945,6 +953,126 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor gtable, 
 }
 
 
+// ---- HK10: embedding bag / sparse linear (sparse.hip) ----
+// Bags: offsets [B+1] (CSR over ids) or, when offsets is empty, a dense [B, L] id matrix.
+// ids outside [0, V) or == pad are skipped in-kernel; offsets are clamped to [0, nnz).
+std::vector<torch::Tensor> embedding_bag_fwd(torch::Tensor table, torch::Tensor ids, torch::Tensor offsets, int64_t L,
+                                             c10::optional<torch::Tensor> wts, int64_t mode, double max_norm,
+                                             int64_t pad) {
+  req(table, at::kFloat, "table");
+  req(ids, at::kLong, "ids");
+  TORCH_CHECK(table.dim() == 2, "embedding_bag: 2-D table");
+  TORCH_CHECK(mode >= 0 && mode <= 2, "embedding_bag: mode 0 sum / 1 mean / 2 sqrtn");
+  const int64_t nnz = ids.numel();
+  int64_t B;
+  const int64_t* op = nullptr;
+  if (offsets.numel() > 0) {
+    req(offsets, at::kLong, "offsets");
+    B = offsets.numel() - 1;
+    op = offsets.data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(L > 0 && nnz % L == 0, "embedding_bag: dense ids need L > 0 dividing numel");
+    B = nnz / L;
+  }
+  const float* wp = nullptr;
+  if (wts.has_value() && wts->defined()) {
+    req(*wts, at::kFloat, "per-id weights");
+    TORCH_CHECK(wts->numel() == nnz, "embedding_bag: weights must match ids");
+    wp = wts->data_ptr<float>();
+  }
+  const int D = table.size(1), V = table.size(0);
+  TORCH_CHECK(B < (1LL << 31) && D > 0, "embedding_bag: shape");
+  auto out = torch::empty({B, (int64_t)D}, table.options());
+  auto scale = torch::empty({B}, table.options());
+  if (B > 0)
+    check_hip(zoo_embedding_bag_fwd(table.data_ptr<float>(), ids.data_ptr<int64_t>(), op, (int)L, wp,
+                                    out.data_ptr<float>(), scale.data_ptr<float>(), (int)B, D, V, nnz, pad, (int)mode,
+                                    (float)max_norm, cur_stream()),
+              "embedding_bag_fwd");
+  return {out, scale};
+}
+
+void embedding_bag_bwd(torch::Tensor dout, torch::Tensor table, torch::Tensor ids, torch::Tensor offsets, int64_t L,
+                       c10::optional<torch::Tensor> wts, torch::Tensor scale, torch::Tensor gtable, double max_norm,
+                       int64_t pad) {
+  req(dout, at::kFloat, "dout");
+  req(table, at::kFloat, "table");
+  req(ids, at::kLong, "ids");
+  req(scale, at::kFloat, "bag scale");
+  req(gtable, at::kFloat, "grad table");
+  TORCH_CHECK(gtable.sizes() == table.sizes(), "embedding_bag_bwd: grad table shape");
+  const int64_t B = dout.size(0);
+  const int D = table.size(1), V = table.size(0);
+  TORCH_CHECK(dout.dim() == 2 && dout.size(1) == D && scale.numel() == B, "embedding_bag_bwd: shapes");
+  const int64_t* op = nullptr;
+  if (offsets.numel() > 0) {
+    req(offsets, at::kLong, "offsets");
+    TORCH_CHECK(offsets.numel() == B + 1, "embedding_bag_bwd: offsets");
+    op = offsets.data_ptr<int64_t>();
+  } else {
+    TORCH_CHECK(ids.numel() == B * L, "embedding_bag_bwd: dense ids");
+  }
+  const float* wp = nullptr;
+  if (wts.has_value() && wts->defined()) {
+    req(*wts, at::kFloat, "per-id weights");
+    TORCH_CHECK(wts->numel() == ids.numel(), "embedding_bag_bwd: weights");
+    wp = wts->data_ptr<float>();
+  }
+  if (B > 0)
+    check_hip(zoo_embedding_bag_bwd(dout.data_ptr<float>(), table.data_ptr<float>(), ids.data_ptr<int64_t>(), op,
+                                    (int)L, wp, scale.data_ptr<float>(), gtable.data_ptr<float>(), (int)B, D, V,
+                                    ids.numel(), pad, (float)max_norm, cur_stream()),
+              "embedding_bag_bwd");
+}
+
+// y [B, O] = CSR(crow, col, val) [B, IN] . W[O, IN]^T + bias
+torch::Tensor sparse_linear_fwd(torch::Tensor crow, torch::Tensor col, torch::Tensor val, torch::Tensor W,
+                                c10::optional<torch::Tensor> bias) {
+  req(crow, at::kLong, "crow");
+  req(col, at::kLong, "col");
+  req(val, at::kFloat, "values");
+  req(W, at::kFloat, "weight");
+  TORCH_CHECK(W.dim() == 2 && col.numel() == val.numel(), "sparse_linear: shapes");
+  const int64_t B = crow.numel() - 1;
+  const int O = W.size(0), IN = W.size(1);
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == O, "sparse_linear: bias");
+    bp = bias->data_ptr<float>();
+  }
+  auto y = torch::empty({B, (int64_t)O}, W.options());
+  if (B > 0 && O > 0)
+    check_hip(zoo_sparse_linear_fwd(crow.data_ptr<int64_t>(), col.data_ptr<int64_t>(), val.data_ptr<float>(),
+                                    W.data_ptr<float>(), bp, y.data_ptr<float>(), (int)B, O, IN, col.numel(),
+                                    cur_stream()),
+              "sparse_linear_fwd");
+  return y;
+}
+
+// dW [O, IN] += sum_j val_j * dy[row_j] (x) e_{col_j};  db [O] += column sums of dy
+void sparse_linear_bwd(torch::Tensor row, torch::Tensor col, torch::Tensor val, torch::Tensor dy, torch::Tensor dW,
+                       c10::optional<torch::Tensor> db) {
+  req(row, at::kLong, "row");
+  req(col, at::kLong, "col");
+  req(val, at::kFloat, "values");
+  req(dy, at::kFloat, "dy");
+  req(dW, at::kFloat, "dW");
+  TORCH_CHECK(row.numel() == col.numel() && col.numel() == val.numel() && dy.dim() == 2 && dW.dim() == 2 &&
+                  dW.size(0) == dy.size(1), "sparse_linear_bwd: shapes");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    req(*db, at::kFloat, "db");
+    TORCH_CHECK(db->numel() == dy.size(1), "sparse_linear_bwd: db");
+    dbp = db->data_ptr<float>();
+  }
+  if (dy.size(0) > 0)
+    check_hip(zoo_sparse_linear_bwd(row.data_ptr<int64_t>(), col.data_ptr<int64_t>(), val.data_ptr<float>(),
+                                    dy.data_ptr<float>(), dW.data_ptr<float>(), dbp, col.numel(), (int)dy.size(0),
+                                    (int)dy.size(1), (int)dW.size(1), cur_stream()),
+              "sparse_linear_bwd");
+}
+
 // uint8 [N, Hi, Wi, C] (C in 1..4) -> resized + normalized image batch:
 // layout 0 -> fp32 [N, C, Ho, Wo]; layout 1 -> bf16 [N, Ho, Wo, 4] (zero-padded channels)
 torch::Tensor resize_normalize(torch::Tensor in, int64_t Ho, int64_t Wo, std::vector<double> mean,
@@ -1315,6 +1443,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
+  m.def("embedding_bag_fwd", &embedding_bag_fwd);
+  m.def("embedding_bag_bwd", &embedding_bag_bwd);
+  m.def("sparse_linear_fwd", &sparse_linear_fwd);
+  m.def("sparse_linear_bwd", &sparse_linear_bwd);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);

@@ -204,13 +204,9 @@ class SparseDense(Layer):
         return (None, self.output_dim)
 
     def call(self, x):
-        if x.is_sparse:
-            y = torch.sparse.mm(x, self.weight.t())
-            if self.bias is not None:
-                y = y + self.bias
-        else:
-            y = F.linear(x, self.weight, self.bias)
-        return apply_activation(y, self.activation)
+        # CSR/COO input runs the native sparse-linear kernel on GPU (zoo/ops/sparse.py)
+        from zoo.ops.sparse import sparse_linear
+        return apply_activation(sparse_linear(x, self.weight, self.bias), self.activation)
 
 
 class MaxoutDense(Layer):

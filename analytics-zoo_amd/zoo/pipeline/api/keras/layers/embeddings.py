@@ -103,28 +103,12 @@ class SparseEmbedding(Layer):
         return (None, self.output_dim)
 
     def call(self, x):
-        if x.is_sparse:
-            x = x.coalesce()
-            rows, cols = x.indices()
-            weights = x.values().float()
-            offsets_rows = rows
-        else:
-            ids = x.long()
-            mask = ids >= 0
-            rows = torch.arange(ids.shape[0], device=ids.device).unsqueeze(1).expand_as(ids)[mask]
-            cols = ids[mask]
-            weights = torch.ones_like(cols, dtype=torch.float32)
-            offsets_rows = rows
-        emb = self.embeddings[cols]
-        if self.max_norm > 0:
-            n = emb.norm(dim=1, keepdim=True).clamp_min(1e-12)
-            emb = emb * torch.clamp(self.max_norm / n, max=1.0)
-        emb = emb * weights.unsqueeze(1)
-        B = x.shape[0]
-        out = torch.zeros(B, self.output_dim, device=emb.device, dtype=emb.dtype).index_add_(0, offsets_rows, emb)
-        if self.combiner in ("mean", "sqrtn"):
-            cnt = torch.zeros(B, device=emb.device).index_add_(0, offsets_rows, weights if self.combiner == "mean"
-                                                               else weights * weights)
-            cnt = cnt.clamp_min(1e-12)
-            out = out / (cnt if self.combiner == "mean" else cnt.sqrt()).unsqueeze(1)
-        return out
+        # native embedding-bag kernel on GPU (zoo/ops/sparse.py, csrc/kernels/sparse.hip)
+        from zoo.ops.sparse import coo_to_bags, embedding_bag
+        if x.is_sparse or x.layout == torch.sparse_csr:
+            ids, offsets, vals = coo_to_bags(x)
+            return embedding_bag(self.embeddings, ids, offsets, vals, self.combiner, self.max_norm)
+        ids = x.long()
+        if ids.dim() == 1:
+            ids = ids.unsqueeze(1)
+        return embedding_bag(self.embeddings, ids, None, None, self.combiner, self.max_norm)
