@@ -13,6 +13,8 @@
 //    TensorBoard event writer (Zs/tensorboard/RecordWriter.scala:30-90).
 //  * pb_fields — a protobuf wire-format scanner used by the BigDL ``.model``
 //    codec (zoo/utils/bigdl_proto.py) to walk nested messages without protoc.
+//  * NativeStore (serving.cpp) — the Cluster Serving queue: Redis-protocol
+//    streams/hashes with a TCP front end and GIL-free worker fast paths.
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -238,8 +240,11 @@ py::list pb_fields(py::bytes b) {
 
 }  // namespace
 
+void register_serving(py::module& m);  // serving.cpp
+
 PYBIND11_MODULE(_runtime, m) {
-  m.doc() = "zoo native host runtime (batch gather, TFRecord/CRC32C, protobuf wire scanner)";
+  m.doc() = "zoo native host runtime (batch gather, TFRecord/CRC32C, protobuf wire scanner, serving queue)";
+  register_serving(m);
   py::class_<Gatherer>(m, "Gatherer")
       .def(py::init<int>(), py::arg("nthreads") = 4)
       .def("gather", &Gatherer::gather)

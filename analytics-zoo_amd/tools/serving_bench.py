@@ -77,6 +77,14 @@ def run_models(a):
     bench_model("BERT-base seq128", imb, bert_in, [1, 8, 32, 128], a.iters)
 
 
+def _producer_proc(cfg, p, n, images, jpgs):
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from zoo.serving import InputQueue
+    q = InputQueue(cfg)
+    for i in range(p, images, n):
+        q.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+
+
 def run_e2e(a):
     from PIL import Image
     from zoo.common.nncontext import init_nncontext
@@ -107,13 +115,44 @@ def run_e2e(a):
             s.records = 0
             sent = {}
 
-            def producer():
+            if a.drain:  # worker-only throughput: the queue is filled before the worker starts
                 for i in range(a.images):
-                    sent["im%d" % i] = time.perf_counter()
                     inq.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
-            th = threading.Thread(target=producer)
-            t0 = time.perf_counter()
-            th.start()
+                s.records = 0
+                td = time.perf_counter()
+                s.run(max_records=a.images, idle_timeout=30)
+                el = time.perf_counter() - td
+                got = outq.dequeue()
+                print(json.dumps({"bench": "cluster-serving-drain", "model": "ResNet-50 bf16", "batch": a.batch,
+                                  "images": len(got), "throughput": round(len(got) / el, 1), "unit": "images/sec",
+                                  "n_gpus": 1, "data": "synthetic 256x256 JPEG"}), flush=True)
+                return
+
+            if a.client_procs:  # producers in separate processes (spawned: no GPU state in them)
+                import multiprocessing as mp
+                ctxmp = mp.get_context("spawn")
+                t0 = time.perf_counter()
+                procs = [ctxmp.Process(target=_producer_proc, args=(cfg, p, a.client_procs, a.images, jpgs))
+                         for p in range(a.client_procs)]
+                for pr in procs:
+                    pr.start()
+                sent_q = None
+                ths = []
+                for i in range(a.images):
+                    sent["im%d" % i] = t0   # latency measured from the run start (send times live in the children)
+            else:
+                ths = None
+
+            def producer(p):
+                q = inq if p == 0 else InputQueue(cfg)   # one connection per producer thread
+                for i in range(p, a.images, a.producers):
+                    sent["im%d" % i] = time.perf_counter()
+                    q.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+            if ths is None:
+                ths = [threading.Thread(target=producer, args=(p,)) for p in range(a.producers)]
+                t0 = time.perf_counter()
+                for th in ths:
+                    th.start()
             done = {}
             worker = threading.Thread(target=s.run, kwargs={"max_records": a.images, "idle_timeout": 30})
             worker.start()
@@ -122,13 +161,30 @@ def run_e2e(a):
                     done.setdefault(k, time.perf_counter())
                 time.sleep(0.002)
             worker.join()
-            th.join()
+            for th in ths:
+                th.join()
+            if a.client_procs:
+                for pr in procs:
+                    pr.join()
             el = time.perf_counter() - t0
             lat = [(done[k] - sent[k]) * 1e3 for k in done if k in sent]
+            # the model alone at the same batch (same InferenceModel replica, input already on the GPU)
+            xm = torch.randn(a.batch, 3, 224, 224, device="cuda")
+            for _ in range(3):
+                s.im.predict(xm)
+            tm = time.perf_counter()
+            for _ in range(20):
+                s.im.predict(xm)
+            model_tp = 20 * a.batch / (time.perf_counter() - tm)
+            from zoo.serving.resp import NativeRespServer
             print(json.dumps({"bench": "cluster-serving-e2e", "model": "ResNet-50 bf16", "batch": a.batch,
                               "images": len(done), "throughput": round(len(done) / el, 1), "unit": "images/sec",
-                              "p50_ms": round(_pct(lat, 50), 2), "p99_ms": round(_pct(lat, 99), 2), "n_gpus": 1,
-                              "data": "synthetic 256x256 JPEG"}), flush=True)
+                              "p50_ms": round(_pct(lat, 50), 2), "p99_ms": round(_pct(lat, 99), 2),
+                              "model_only_throughput": round(model_tp, 1),
+                              "e2e_over_model": round(len(done) / el / model_tp, 3),
+                              "producers": ("%d processes" % a.client_procs) if a.client_procs else a.producers,
+                              "queue": "native" if isinstance(srv, NativeRespServer) else "python",
+                              "n_gpus": 1, "data": "synthetic 256x256 JPEG"}), flush=True)
     finally:
         srv.shutdown()
         srv.server_close()
@@ -140,6 +196,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--images", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--producers", type=int, default=4)
+    ap.add_argument("--client-procs", type=int, default=0, help="producers in N separate processes")
+    ap.add_argument("--drain", action="store_true", help="prefill the queue, time the worker alone")
     a = ap.parse_args()
     run_models(a) if a.mode == "model" else run_e2e(a)
 

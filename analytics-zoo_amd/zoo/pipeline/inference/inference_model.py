@@ -81,6 +81,8 @@ class _Replica:
         dev = self.owner.device
         if dev.type != "cuda":
             return self._forward([t.to(dev) for t in xs])
+        # inputs may have been produced on the caller's stream (e.g. GPU preprocessing): order them first
+        self.stream.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(self.stream):
             g = None
             if self.owner.use_graph:

@@ -12,6 +12,13 @@ against a real Redis server when one is available.
 Supported commands: PING, ECHO, XADD, XLEN, XRANGE, XGROUP CREATE/DESTROY,
 XREADGROUP, XACK, XDEL, XTRIM MAXLEN, HSET/HMSET, HGET, HGETALL, KEYS, DEL,
 EXISTS, INFO, CONFIG GET/SET maxmemory, DBSIZE, FLUSHALL, SHUTDOWN.
+
+``RespServer`` is the native C++ store + multi-threaded TCP server
+(``zoo._runtime.NativeStore``, csrc/runtime/serving.cpp) whenever the runtime is
+built; the pure-Python ``PyRespServer`` below is the fallback and the executable
+specification the native one is tested against. A worker in the same process as
+a native server gets a :class:`LocalClient` from :func:`connect` (``local=True``):
+no socket, no RESP codec, and the batch fast paths ``read_batch``/``finish``.
 """
 import fnmatch
 import socket
@@ -381,7 +388,7 @@ class _Handler(socketserver.BaseRequestHandler):
                 return
 
 
-class RespServer(socketserver.ThreadingTCPServer):
+class PyRespServer(socketserver.ThreadingTCPServer):
     daemon_threads = True
     allow_reuse_address = True
 
@@ -397,6 +404,55 @@ class RespServer(socketserver.ThreadingTCPServer):
         t = threading.Thread(target=self.serve_forever, daemon=True)
         t.start()
         return self
+
+
+_LOCAL = {}   # port -> NativeStore of native servers running in this process
+
+
+def _native_runtime():
+    import os
+    if os.environ.get("ZOO_SERVING_PY", "0") == "1":
+        return None
+    try:
+        from zoo import _runtime
+        return _runtime if hasattr(_runtime, "NativeStore") else None
+    except ImportError:
+        return None
+
+
+class NativeRespServer:
+    """The C++ queue server; binds at construction (``port`` 0 = ephemeral)."""
+
+    def __init__(self, host="127.0.0.1", port=6379, maxmemory=4 << 30):
+        rt = _native_runtime()
+        self.store = rt.NativeStore(int(maxmemory))
+        self._port = self.store.serve(host, int(port))
+        _LOCAL[self._port] = self.store
+
+    @property
+    def port(self):
+        return self._port
+
+    def start(self):
+        return self
+
+    def serve_forever(self):
+        while self.store.running():
+            time.sleep(0.2)
+
+    def shutdown(self):
+        _LOCAL.pop(self._port, None)
+        self.store.stop()
+
+    def server_close(self):
+        pass
+
+
+def RespServer(host="127.0.0.1", port=6379, maxmemory=4 << 30):  # noqa: N802 - class-like factory
+    """Native C++ queue server when the runtime is built, else the Python one."""
+    if _native_runtime() is not None:
+        return NativeRespServer(host, port, maxmemory)
+    return PyRespServer(host, port, maxmemory)
 
 
 # ---- client ------------------------------------------------------------------------------
@@ -499,8 +555,43 @@ class RespClient:
         self.sock.close()
 
 
-def connect(host="127.0.0.1", port=6379):
-    """A real redis-py client when installed, else the built-in RESP client."""
+class LocalClient(RespClient):
+    """RespClient over an in-process NativeStore: commands skip the socket and the
+    codec, and the serving worker gets the batch fast paths."""
+
+    def __init__(self, store):  # noqa: D107 - no socket
+        self.store = store
+        self.sock = None
+        self.lock = threading.Lock()
+
+    def execute_command(self, *args):
+        parts = [a if isinstance(a, bytes) else str(a).encode() for a in args]
+        try:
+            return self.store.execute(parts)
+        except RuntimeError as e:
+            raise RespError(str(e)) from None
+
+    def read_batch(self, stream, group, consumer, count, block_ms):
+        """[(id, uri, kind, decoded payload bytes, shape)]; blocks without the GIL."""
+        return self.store.read_batch(stream, group, consumer, int(count), int(block_ms))
+
+    def finish(self, stream, group, ids, results, field="value"):
+        """HSET every (key, value) result, then XACK + XDEL ``ids``, under one lock."""
+        self.store.finish(stream, group, list(ids), list(results), field)
+
+    def shutdown(self):
+        self.store.stop()
+
+    def close(self):
+        pass
+
+
+def connect(host="127.0.0.1", port=6379, local=False):
+    """``local``: an in-process native server on that port is used directly
+    (:class:`LocalClient`); otherwise a real redis-py client when installed, else
+    the built-in RESP client."""
+    if local and host in ("127.0.0.1", "localhost") and int(port) in _LOCAL:
+        return LocalClient(_LOCAL[int(port)])
     try:
         import redis  # noqa: F401
         return redis.StrictRedis(host=host, port=int(port), db=0)

@@ -547,6 +547,26 @@ def test_serving_worker_on_gpu(gpu):
             assert s.run(max_records=5, idle_timeout=10) == 5
             res = outq.dequeue()
             assert len(res) == 5 and all(v.startswith("[[") for v in res.values())
+            # the pinned-ring RGB decode path feeds the model exactly what the generic
+            # BGR decode + GPU resize/normalize path does (both channel orders)
+            import base64
+            import io
+            from PIL import Image
+            from zoo.pipeline.nnframes.nn_image_reader import decode_image
+            jp = []
+            for i in range(4):
+                b = io.BytesIO()
+                Image.fromarray(rng.integers(0, 255, (20, 24, 3)).astype(np.uint8)).save(b, format="JPEG")
+                jp.append(b.getvalue())
+            recs = [(b"%d-0" % i, "u%d" % i, "image", jp[i], "") for i in range(4)]
+            for to_rgb in (False, True):
+                s.cfg["to_rgb"] = to_rgb
+                s.cfg["mean"], s.cfg["std"] = [10.0, 20.0, 30.0], [2.0, 3.0, 4.0]
+                _, _, dec = s._decode_native(recs)
+                assert dec[0] == "rgb"
+                fast = s._to_batch(dec)
+                ref = s._images_to_batch([decode_image(j) for j in jp])
+                assert torch.allclose(fast.float(), ref.float(), atol=1e-4), to_rgb
     finally:
         srv.shutdown()
         srv.server_close()

@@ -13,10 +13,11 @@ def ctx():
     return init_nncontext()
 
 
-@pytest.fixture()
-def server():
-    from zoo.serving.resp import RespServer
-    srv = RespServer("127.0.0.1", 0, maxmemory=1 << 20).start()
+@pytest.fixture(params=["native", "python"])
+def server(request):
+    from zoo.serving.resp import NativeRespServer, PyRespServer
+    cls = NativeRespServer if request.param == "native" else PyRespServer
+    srv = cls("127.0.0.1", 0, maxmemory=1 << 20).start()
     yield srv
     srv.shutdown()
     srv.server_close()
@@ -77,8 +78,9 @@ def test_serving_end_to_end_tensors_and_images(server, tmp_path):
     assert served == 7
     res = outq.dequeue()
     assert set(res) == set(xs) | {"img0"}
-    with torch.no_grad():
-        ref = model(torch.from_numpy(xs["t3"][None]))[0].numpy()
+    import copy
+    with torch.no_grad():   # (serving moved the model to its device; the reference runs on the CPU)
+        ref = copy.deepcopy(model).cpu()(torch.from_numpy(xs["t3"][None]))[0].numpy()
     top = np.argsort(-ref)[:2]
     assert res["t3"].startswith("[[%d," % top[0]) and ("[%d," % top[1]) in res["t3"]
     assert outq.dequeue() == {}
@@ -92,3 +94,61 @@ def test_model_discovery(tmp_path):
     assert kind == "caffe" and len(files) == 2
     (tmp_path / "m.onnx").write_bytes(b"")
     assert discover_model(str(tmp_path / "m.onnx"))[0] == "onnx"
+
+
+def test_native_store_commands_and_concurrency(server):
+    """Both servers agree on XRANGE/KEYS globbing/DEL/FLUSHALL, and many concurrent
+    producers plus a blocking consumer group lose and duplicate nothing."""
+    import threading
+    from zoo.serving.resp import RespClient
+    c = RespClient("127.0.0.1", server.port)
+    c.xgroup_create("s", "g", id="0", mkstream=True)
+    ids = [c.xadd("s", {"k": str(i)}) for i in range(4)]
+    rng = c.execute_command("XRANGE", "s", "-", "+", "COUNT", 3)
+    assert [r[0] for r in rng] == ids[:3]
+    for k in ("result:a1", "result:b2", "other"):
+        c.hset(k, "value", "x")
+    assert sorted(c.keys("result:[a-b]?")) == [b"result:a1", b"result:b2"]
+    assert c.execute_command("DBSIZE") == 4
+    assert c.execute_command("FLUSHALL") in ("OK", b"OK")
+    assert c.keys("*") == []
+    c.xgroup_create("q", "g", id="0", mkstream=True)
+    n_prod, per = 4, 50
+
+    def prod(p):
+        cc = RespClient("127.0.0.1", server.port)
+        for i in range(per):
+            cc.xadd("q", {"uri": "p%d-%d" % (p, i)})
+    ths = [threading.Thread(target=prod, args=(p,)) for p in range(n_prod)]
+    for t in ths:
+        t.start()
+    seen = []
+    while len(seen) < n_prod * per:
+        got = c.xreadgroup("g", "w", {"q": ">"}, count=16, block=200)
+        for _, msgs in got:
+            seen += [m[1][b"uri"] for m in msgs]
+    for t in ths:
+        t.join()
+    assert len(seen) == len(set(seen)) == n_prod * per
+
+
+def test_native_local_client_fast_paths():
+    from zoo.serving.resp import NativeRespServer, RespClient, connect
+    import base64
+    srv = NativeRespServer("127.0.0.1", 0, 1 << 20)
+    try:
+        lc = connect("127.0.0.1", srv.port, local=True)
+        assert type(lc).__name__ == "LocalClient"
+        lc.xgroup_create("image_stream", "serving", id="0", mkstream=True)
+        rc = RespClient("127.0.0.1", srv.port)
+        rc.xadd("image_stream", {"uri": "a", "image": base64.b64encode(b"\x01\x02jpeg")})
+        rc.xadd("image_stream", {"uri": "b", "tensor": base64.b64encode(np.ones(3, np.float32).tobytes()),
+                                 "shape": "3"})
+        recs = lc.read_batch("image_stream", "serving", "w", 8, 50)
+        assert [(r[1], r[2]) for r in recs] == [("a", "image"), ("b", "tensor")]
+        assert recs[0][3] == b"\x01\x02jpeg" and np.frombuffer(recs[1][3], np.float32).tolist() == [1.0] * 3
+        lc.finish("image_stream", "serving", [r[0] for r in recs], [("result:a", "[1]"), ("result:b", "[2]")])
+        assert rc.xlen("image_stream") == 0 and rc.hgetall("result:b") == {b"value": b"[2]"}
+        assert lc.read_batch("image_stream", "serving", "w", 8, 10) == []
+    finally:
+        srv.shutdown()
