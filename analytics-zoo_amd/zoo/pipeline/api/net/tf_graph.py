@@ -161,10 +161,11 @@ def parse_attr(b):
 
 
 class Node:
-    __slots__ = ("name", "op", "inputs", "controls", "attr")
+    __slots__ = ("name", "op", "inputs", "controls", "attr", "raw")
 
-    def __init__(self, name, op, inputs, controls, attr):
+    def __init__(self, name, op, inputs, controls, attr, raw=None):
         self.name, self.op, self.inputs, self.controls, self.attr = name, op, inputs, controls, attr
+        self.raw = raw   # the serialized NodeDef (kept for re-export, zoo.util.tf.export_tf)
 
     def s(self, key, default=""):
         v = self.attr.get(key, default)
@@ -186,7 +187,7 @@ def parse_node(b):
     for _w, v in g.get(5, []):
         e = pb.group(v)
         attr[pb.as_str(e[1][0][1])] = parse_attr(e[2][0][1]) if 2 in e else None
-    return Node(name, op, inputs, controls, attr)
+    return Node(name, op, inputs, controls, attr, bytes(b))
 
 
 def parse_graph_def(b):

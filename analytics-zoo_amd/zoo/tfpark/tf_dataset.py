@@ -118,7 +118,70 @@ class TFDataset:
             if validation_file_path is not None else None
         return TFDataset(train, val, batch_size, batch_per_thread)
 
-    from_rdd = from_feature_set
+    @staticmethod
+    def from_rdd(rdd, names=None, shapes=None, types=None, batch_size=-1, batch_per_thread=-1,
+                 hard_code_batch_size=False, val_rdd=None, memory_type="DRAM", sequential_order=False,
+                 shuffle=True):
+        """Py/tfpark/tf_dataset.py:1016 (TFNdarrayDataset over an RDD of samples): ``rdd`` is any
+        collection of ``x`` or ``(x, y)`` samples -- a list / iterable, an XShards/``RayRDD``-like
+        object with ``collect()``, or a FeatureSet (then used as is)."""
+        if isinstance(rdd, FeatureSet):
+            return TFDataset.from_feature_set(rdd, batch_size=batch_size, batch_per_thread=batch_per_thread,
+                                              validation_dataset=val_rdd)
+        bs = TFDataset._bs(batch_size, batch_per_thread)
+        train = _iterable_featureset(_collect(rdd), bs, shuffle and not sequential_order and batch_size > 0)
+        val = _iterable_featureset(_collect(val_rdd), bs, False) if val_rdd is not None else None
+        return TFDataset(train, val, batch_size, batch_per_thread)
+
+    @staticmethod
+    def from_string_rdd(string_rdd, batch_size=-1, batch_per_thread=-1, hard_code_batch_size=False,
+                        validation_string_rdd=None):
+        """Py/tfpark/tf_dataset.py:528: a dataset of single strings (utf-8 encoded to bytes);
+        batches are ``(list_of_bytes,)`` -- the reference's one tf.string feature tensor of
+        shape (None,). Labels, if any, live inside the strings."""
+        enc = (lambda v: v.encode("utf-8") if isinstance(v, str) else bytes(v))
+        val = None if validation_string_rdd is None else [enc(v) for v in _collect(validation_string_rdd)]
+        return TFDataset.from_bytes_rdd([enc(v) for v in _collect(string_rdd)], batch_size, batch_per_thread,
+                                        hard_code_batch_size, val)
+
+    @staticmethod
+    def from_bytes_rdd(bytes_rdd, batch_size=-1, batch_per_thread=-1, hard_code_batch_size=False,
+                       validation_bytes_rdd=None):
+        """Py/tfpark/tf_dataset.py:553 (TFBytesDataset): a dataset of byte strings served in
+        batches of ``(list_of_bytes,)`` (shuffled per epoch for training)."""
+        bs = TFDataset._bs(batch_size, batch_per_thread)
+        train = BytesFeatureSet(list(_collect(bytes_rdd)), bs, shuffle=batch_size > 0,
+                                drop_last=hard_code_batch_size)
+        val = BytesFeatureSet(list(_collect(validation_bytes_rdd)), bs, shuffle=False) \
+            if validation_bytes_rdd is not None else None
+        return TFDataset(train, val, batch_size, batch_per_thread)
+
+
+def _collect(rdd):
+    """An 'RDD' here: a list/iterable, or anything with collect() (XShards, RayRDD)."""
+    if hasattr(rdd, "collect"):
+        rdd = rdd.collect()
+    return list(rdd)
+
+
+class BytesFeatureSet(FeatureSet):
+    """Variable-length byte records (TFBytesDataset): batches are ``(list_of_bytes,)``."""
+
+    def __init__(self, records, batch_size=32, shuffle=True, drop_last=False, seed=0):
+        self.records = [bytes(r) for r in records]
+        self.batch_size, self.shuffle, self.drop_last, self.seed = int(batch_size), shuffle, drop_last, seed
+
+    def size(self):
+        return len(self.records)
+
+    def data(self, train=True, epoch=None):
+        idx = np.arange(len(self.records))
+        if train and self.shuffle:
+            np.random.default_rng(self.seed + (epoch or 0)).shuffle(idx)
+        n = len(idx)
+        stop = n - n % self.batch_size if (self.drop_last and train) else n
+        for s in range(0, stop, self.batch_size):
+            yield ([self.records[i] for i in idx[s:s + self.batch_size]],)
 
 
 def _iterable_featureset(dataset, batch_size, shuffle):

@@ -180,3 +180,29 @@ def test_tfnet_on_gpu_matches_cpu(gpu):
     ref = net.forward_numpy(x)
     out = net.to(gpu).forward_numpy(x)
     np.testing.assert_allclose(out, ref, rtol=1e-4, atol=1e-5)
+
+
+def test_export_tf_freezes_trained_variables(tmp_path):
+    """zoo.util.tf.export_tf (Py/util/tf.py:50): a TFNet whose variables changed after
+    loading is frozen (variables -> Const with the current values, resource reads ->
+    Identity) into an export folder that loads back and computes the same outputs."""
+    import torch
+    from zoo.util.tf import export_tf
+    p = os.path.join(R, "saved-model-signature")
+    net = TFNet.from_saved_model(p, trainable=True)
+    with torch.no_grad():
+        for prm in net.parameters():
+            prm.mul_(1.5).add_(0.25)        # "training" moved the weights
+    x = np.random.rand(3, 4).astype(np.float32)
+    want = net.forward_numpy(x)
+    out = export_tf(net, str(tmp_path / "exp"), net.input_names, net.output_names)
+    back = TFNet.from_export_folder(out)
+    assert not list(back.parameters())      # nothing left to train: everything is a Const
+    np.testing.assert_allclose(back.forward_numpy(x), want, rtol=1e-6, atol=1e-6)
+    # a frozen export folder re-exports to an equivalent folder
+    net2 = TFNet.from_export_folder(os.path.join(PYR, "tfnet"))
+    out2 = export_tf(net2, str(tmp_path / "exp2"), net2.input_names, net2.output_names)
+    np.testing.assert_allclose(TFNet.from_export_folder(out2).forward_numpy(x[:, :4]), net2.forward_numpy(x[:, :4]),
+                               rtol=1e-6)
+    with pytest.raises(TypeError):
+        export_tf(object(), str(tmp_path / "bad"), [], [])

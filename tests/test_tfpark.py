@@ -115,3 +115,30 @@ def test_gan_estimator_learns_mean():
     est.train(data, 1200)
     gen = est.generate(2000)
     assert abs(float(gen.mean()) - 3.0) < 0.6, float(gen.mean())
+
+
+def test_tfdataset_string_bytes_and_rdd_sources():
+    """TFDataset.from_string_rdd / from_bytes_rdd (batches of byte strings, the reference's
+    single tf.string feature) and from_rdd over sample collections (list or collect())."""
+    import numpy as np
+    from zoo.tfpark import TFDataset
+    strs = ["s%d,%d" % (i, i % 3) for i in range(10)]
+    ds = TFDataset.from_string_rdd(strs, batch_per_thread=4)
+    batches = [b[0] for b in ds.get_prediction_data().data(train=False)]
+    assert [len(b) for b in batches] == [4, 4, 2] and batches[0][0] == b"s0,0"
+    tr = TFDataset.from_bytes_rdd([s.encode() for s in strs], batch_size=4, hard_code_batch_size=True,
+                                  validation_bytes_rdd=[b"v"])
+    got = [x for b in tr.get_training_data().data(train=True, epoch=1) for x in b[0]]
+    assert len(got) == 8 and set(got) <= {s.encode() for s in strs}   # shuffled, last partial dropped
+    assert [b[0] for b in tr.get_validation_data().data(train=False)] == [[b"v"]]
+
+    class FakeRDD:
+        def __init__(self, items):
+            self.items = items
+
+        def collect(self):
+            return list(self.items)
+    samples = [(np.full(3, i, np.float32), np.int64(i % 2)) for i in range(8)]
+    rd = TFDataset.from_rdd(FakeRDD(samples), batch_per_thread=8)
+    x, y = next(iter(rd.get_prediction_data().data(train=False)))
+    assert tuple(np.asarray(x).shape) == (8, 3) and list(np.asarray(y)) == [i % 2 for i in range(8)]
