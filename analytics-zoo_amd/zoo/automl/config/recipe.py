@@ -14,6 +14,15 @@ class Recipe:
     def runtime_params(self):
         return {"training_iteration": self.training_iteration, "num_samples": self.num_samples}
 
+    def fixed_params(self):
+        return {}
+
+    def search_algorithm(self):
+        return None
+
+    def search_algorithm_params(self):
+        return None
+
 
 def _past(look_back):
     if isinstance(look_back, (tuple, list)):
@@ -123,9 +132,40 @@ class RandomRecipe(Recipe):
                 "epochs": self.epochs, "past_seq_len": self.past}
 
 
-class BayesRecipe(RandomRecipe):
-    """Bayesian optimisation needs an external optimiser; this recipe samples the
-    same space randomly with more samples (documented deviation)."""
+class BayesRecipe(Recipe):
+    """Bayesian-optimisation recipe (Py/automl/config/recipe.py:423-518): a continuous box
+    space searched by GP-UCB (zoo.automl.search.BayesOptSearch). Feature selection is a
+    ``bayes_feature_<f>`` in (0.3, 1) thresholded at 0.5; integer knobs are ``*_float``
+    ranges truncated to int; the batch size is 2**``batch_size_log``."""
 
     def __init__(self, num_samples=1, look_back=2, epochs=5, reward_metric=-0.05, training_iteration=5):
-        super().__init__(max(num_samples, 1), look_back, epochs, reward_metric, training_iteration)
+        self.num_samples, self.reward_metric = int(num_samples), reward_metric
+        self.training_iteration, self.epochs = training_iteration, epochs
+        if isinstance(look_back, tuple) and len(look_back) == 2 and all(isinstance(v, int) for v in look_back):
+            if look_back[1] < 2:
+                raise ValueError("The max look back value should be at least 2")
+            self.bayes_past = {"past_seq_len_float": (max(2, look_back[0]), look_back[1])}
+            self.fixed_past = {}
+        elif isinstance(look_back, int):
+            if look_back < 2:
+                raise ValueError("look back value should not be smaller than 2")
+            self.bayes_past, self.fixed_past = {}, {"past_seq_len": look_back}
+        else:
+            raise ValueError("look_back should be either a tuple with 2 int values (min_len, max_len) "
+                             "or a single int")
+
+    def search_space(self, all_available_features):
+        space = {"bayes_feature_%s" % f: (0.3, 1) for f in all_available_features}
+        space.update({"lstm_1_units_float": (8, 128), "dropout_1": (0.2, 0.5), "lstm_2_units_float": (8, 128),
+                      "dropout_2": (0.2, 0.5), "lr": (0.001, 0.01), "batch_size_log": (5, 10)})
+        space.update(self.bayes_past)
+        return space
+
+    def fixed_params(self):
+        return dict({"epochs": self.epochs, "model": "LSTM"}, **self.fixed_past)
+
+    def search_algorithm_params(self):
+        return {"utility_kwargs": {"kind": "ucb", "kappa": 2.5, "xi": 0.0}}
+
+    def search_algorithm(self):
+        return "BayesOpt"

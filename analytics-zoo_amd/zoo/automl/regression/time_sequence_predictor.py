@@ -40,7 +40,10 @@ class TimeSequencePredictor:
 
         engine = SearchEngine(n_parallel=n_parallel)
         mode = "max" if Evaluator.higher_is_better(metric) else "min"
-        best_cfg, best = engine.run(trial, recipe.search_space(feats), recipe.num_samples, metric, mode)
+        best_cfg, best = engine.run(trial, recipe.search_space(feats), recipe.num_samples, metric, mode,
+                                    search_alg=recipe.search_algorithm(),
+                                    search_alg_params=recipe.search_algorithm_params(),
+                                    fixed_params=recipe.fixed_params())
         self.pipeline = best["pipeline"]
         self.trials = engine.trials
         return self.pipeline
