@@ -8,22 +8,26 @@
 
 namespace zoo {
 
+// 32-bit index math throughout (the launcher checks N*P*Q*C/8 and N*H*W*C/8 < 2^31): the
+// 64-bit div/mod of a size_t grid-stride index made the r1 kernels VALU-bound (~2 TB/s)
 __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
                                                           uint8_t* __restrict__ arg, int N, int H, int W, int C,
                                                           int P, int Q, int R, int S, int sh, int sw, int ph,
                                                           int pw) {
   const int cpr = C >> 3;
-  const size_t total = (size_t)N * P * Q * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int chunk = (int)(i % cpr);
-    size_t t = i / cpr;
-    const int q = (int)(t % Q); t /= Q;
-    const int p = (int)(t % P);
-    const int n = (int)(t / P);
+  const int total = N * P * Q * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int chunk = i % cpr;
+    int t = i / cpr;
+    const int q = t % Q;
+    t /= Q;
+    const int p = t % P;
+    const int n = t / P;
     float best[8];
     uint8_t bi[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    const bf16_t* xn = X + (size_t)n * H * W * C + chunk * 8;
     for (int r = 0; r < R; ++r) {
       const int ih = p * sh - ph + r;
       if ((unsigned)ih >= (unsigned)H) continue;
@@ -31,18 +35,18 @@ __global__ __launch_bounds__(256) void maxpool_fwd_kernel(const bf16_t* __restri
         const int iw = q * sw - pw + s;
         if ((unsigned)iw >= (unsigned)W) continue;
         float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(X + (((size_t)n * H + ih) * W + iw) * C + chunk * 8), v);
+        unpack8(*reinterpret_cast<const uint4*>(xn + (ih * W + iw) * C), v);
 #pragma unroll
         for (int e = 0; e < 8; ++e)
           if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * S + s); }
       }
     }
-    *reinterpret_cast<uint4*>(Y + i * 8) = pack8(best);
+    *reinterpret_cast<uint4*>(Y + (size_t)i * 8) = pack8(best);
     if (arg) {
       uint2 pk;
       pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
       pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
-      *reinterpret_cast<uint2*>(arg + i * 8) = pk;
+      *reinterpret_cast<uint2*>(arg + (size_t)i * 8) = pk;
     }
   }
 }
@@ -53,13 +57,14 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
                                                           int N, int H, int W, int C, int P, int Q, int R, int S,
                                                           int sh, int sw, int ph, int pw) {
   const int cpr = C >> 3;
-  const size_t total = (size_t)N * H * W * cpr;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
-    const int chunk = (int)(i % cpr);
-    size_t t = i / cpr;
-    const int w = (int)(t % W); t /= W;
-    const int h = (int)(t % H);
-    const int n = (int)(t / H);
+  const int total = N * H * W * cpr;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
+    const int chunk = i % cpr;
+    int t = i / cpr;
+    const int w = t % W;
+    t /= W;
+    const int h = t % H;
+    const int n = t / H;
     float acc[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[e] = 0.f;
@@ -68,25 +73,26 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
     const int p_hi = min(P - 1, (h + ph) / sh);
     const int q_lo = max(0, (w + pw - S + sw) / sw);
     const int q_hi = min(Q - 1, (w + pw) / sw);
+    const size_t nb = (size_t)n * P * Q * C + chunk * 8;
     for (int p = p_lo; p <= p_hi; ++p) {
       const int r = h - (p * sh - ph);
       if (r < 0 || r >= R) continue;
       for (int q = q_lo; q <= q_hi; ++q) {
         const int s = w - (q * sw - pw);
         if (s < 0 || s >= S) continue;
-        const uint8_t tap = (uint8_t)(r * S + s);
-        const size_t o = (((size_t)n * P + p) * Q + q) * C + chunk * 8;
+        const uint32_t tap = (uint32_t)(r * S + s);
+        const size_t o = nb + (size_t)(p * Q + q) * C;
         const uint2 ab = *reinterpret_cast<const uint2*>(arg + o);
         float g[8];
         unpack8(*reinterpret_cast<const uint4*>(dY + o), g);
-        const uint8_t a8[8] = {(uint8_t)(ab.x), (uint8_t)(ab.x >> 8), (uint8_t)(ab.x >> 16), (uint8_t)(ab.x >> 24),
-                               (uint8_t)(ab.y), (uint8_t)(ab.y >> 8), (uint8_t)(ab.y >> 16), (uint8_t)(ab.y >> 24)};
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-          if (a8[e] == tap) acc[e] += g[e];
+        for (int e = 0; e < 4; ++e) {
+          if (((ab.x >> (8 * e)) & 0xff) == tap) acc[e] += g[e];
+          if (((ab.y >> (8 * e)) & 0xff) == tap) acc[4 + e] += g[4 + e];
+        }
       }
     }
-    *reinterpret_cast<uint4*>(dX + i * 8) = pack8(acc);
+    *reinterpret_cast<uint4*>(dX + (size_t)i * 8) = pack8(acc);
   }
 }
 

@@ -476,6 +476,8 @@ std::vector<torch::Tensor> maxpool_fwd(torch::Tensor x, int R, int S, int sh, in
   const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
   const int P = pool_out(H, R, sh, ph, ceil_mode), Q = pool_out(W, S, sw, pw, ceil_mode);
   TORCH_CHECK(P > 0 && Q > 0, "maxpool: empty output");
+  TORCH_CHECK((int64_t)N * H * W * C < (1LL << 31) && (int64_t)N * P * Q * C < (1LL << 31),
+              "maxpool: tensor too large for 32-bit indexing");
   auto y = torch::empty({N, P, Q, C}, x.options());
   torch::Tensor arg;
   if (save_arg) arg = torch::empty({N, P, Q, C}, x.options().dtype(at::kByte));
@@ -495,6 +497,8 @@ torch::Tensor maxpool_bwd(torch::Tensor dy, torch::Tensor arg, int H, int W, int
   TORCH_CHECK((P == pool_out(H, R, sh, ph, false) || P == pool_out(H, R, sh, ph, true)) &&
                   (Q == pool_out(W, S, sw, pw, false) || Q == pool_out(W, S, sw, pw, true)),
               "maxpool_bwd: geometry");
+  TORCH_CHECK((int64_t)N * H * W * C < (1LL << 31) && (int64_t)N * P * Q * C < (1LL << 31),
+              "maxpool_bwd: tensor too large for 32-bit indexing");
   auto dx = torch::empty({N, H, W, C}, dy.options());
   check_hip(zoo_maxpool_bwd(dy.data_ptr(), arg.data_ptr(), dx.data_ptr(), N, H, W, C, P, Q, R, S, sh, sw, ph, pw,
                             cur_stream()),
