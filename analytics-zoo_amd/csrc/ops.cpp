@@ -95,6 +95,10 @@ hipError_t zoo_sparse_linear_fwd(const int64_t*, const int64_t*, const float*, c
                                  int, int, int64_t, hipStream_t);
 hipError_t zoo_sparse_linear_bwd(const int64_t*, const int64_t*, const float*, const float*, float*, float*, int64_t,
                                  int, int, int, hipStream_t);
+hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*, const void*, float, const ConvGeom*,
+                     int, int, hipStream_t);
+hipError_t zoo_quantize_i8(const void*, void*, size_t, float, hipStream_t);
+hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
@@ -957,6 +961,64 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor gtable, 
 }
 
 
+// ---- static-int8 implicit-GEMM conv (qconv.hip) ----
+// x: int8 NHWC [N,H,W,C] (C % 16 == 0); w: int8 [K, ldb] rows of [R][S][C]; colscale/bias fp32 [K]
+// (already divided by the output scale); resid: int8 [N,P,Q,K] scaled by rscale. Output int8
+// (saturating round) or bf16 (out_bf16).
+torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw,
+                    torch::Tensor colscale, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
+                    double rscale, bool relu, bool out_bf16) {
+  req(x, at::kChar, "x");
+  req(w, at::kChar, "w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "qconv: x NHWC 4-D, w 2-D [K, ldb]");
+  const int C = x.size(3), K = w.size(0), ldb = w.size(1);
+  TORCH_CHECK(C % 16 == 0, "qconv: input channels must be a multiple of 16, got ", C);
+  TORCH_CHECK(K % 8 == 0, "qconv: output channels must be a multiple of 8, got ", K);
+  TORCH_CHECK(ldb % 16 == 0 && ldb >= R * S * C, "qconv: bad weight leading dim ", ldb);
+  TORCH_CHECK(R >= 1 && S >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0, "qconv: bad geometry");
+  ConvGeom g = make_geom(x, K, R, S, sh, sw, ph, pw, 1, 1, 1, 1, ldb);
+  TORCH_CHECK(g.P > 0 && g.Q > 0, "qconv: empty output");
+  TORCH_CHECK((int64_t)g.N * g.H * g.W * g.C < (1LL << 31) && (int64_t)g.M * K < (1LL << 31),
+              "qconv: tensor too large for 32-bit indexing");
+  g.omap = 0; g.stat_slots = 0;
+  req(colscale, at::kFloat, "colscale");
+  TORCH_CHECK(colscale.numel() == K, "qconv: colscale must be [K]");
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == K, "qconv: bias must be [K]");
+    bp = bias->data_ptr<float>();
+  }
+  const void* rp = nullptr;
+  if (resid.has_value() && resid->defined()) {
+    req(*resid, at::kChar, "resid");
+    TORCH_CHECK(resid->numel() == (int64_t)g.M * K, "qconv: resid must match the output");
+    rp = resid->data_ptr();
+  }
+  auto y = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kChar));
+  check_hip(zoo_qconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), colscale.data_ptr<float>(), bp, rp, (float)rscale,
+                      &g, relu, out_bf16, cur_stream()),
+            "qconv");
+  return y;
+}
+
+torch::Tensor quantize_i8(torch::Tensor x, double inv_scale) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.numel() % 16 == 0, "quantize_i8: numel must be a multiple of 16");
+  auto q = torch::empty(x.sizes(), x.options().dtype(at::kChar));
+  check_hip(zoo_quantize_i8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, cur_stream()), "quantize_i8");
+  return q;
+}
+
+torch::Tensor gap_i8(torch::Tensor x, double scale) {
+  req(x, at::kChar, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap_i8: NHWC with C % 8 == 0");
+  const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  auto y = torch::empty({N, C}, x.options().dtype(at::kBFloat16));
+  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, cur_stream()), "gap_i8");
+  return y;
+}
+
 // ---- HK10: embedding bag / sparse linear (sparse.hip) ----
 // Bags: offsets [B+1] (CSR over ids) or, when offsets is empty, a dense [B, L] id matrix.
 // ids outside [0, V) or == pad are skipped in-kernel; offsets are clamped to [0, nnz).
@@ -1447,6 +1509,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
+  m.def("qconv", &qconv);
+  m.def("quantize_i8", &quantize_i8);
+  m.def("gap_i8", &gap_i8);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("sparse_linear_fwd", &sparse_linear_fwd);

@@ -1,6 +1,9 @@
-"""ResNet-50 inference throughput: bf16 (fused conv+BN kernels) vs int8 (zoo.ops.quant).
-python tools/quant_bench.py [--batch 64] [--iters 20]"""
+"""ResNet-50 inference throughput: bf16 (fused conv+BN kernels) vs static int8
+(zoo.ops.qresnet, implicit-GEMM int8 conv on the i8 matrix cores) vs the dynamic int8
+path of zoo.ops.quant (im2col + GEMM), plus the int8-vs-bf16 logit agreement.
+python tools/quant_bench.py [--batch 256] [--iters 20] [--no-dynamic]"""
 import argparse
+import json
 import os
 import sys
 import time
@@ -10,6 +13,7 @@ import torch  # noqa: E402
 
 from zoo.models.image.resnet import resnet50  # noqa: E402
 from zoo.ops import quant as Q  # noqa: E402
+from zoo.ops.qresnet import Int8ResNet  # noqa: E402
 
 
 def bench(m, x, iters):
@@ -26,16 +30,31 @@ def bench(m, x, iters):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--no-dynamic", action="store_true")
     a = ap.parse_args()
+    torch.manual_seed(0)
     m = resnet50().cuda().eval()
     x = torch.randn(a.batch, 3, 224, 224, device="cuda")
     tb = bench(m, x, a.iters)
-    Q.quantize(m)
-    tq = bench(m, x, a.iters)
-    print("resnet50 inference batch %d: bf16 %.2f ms (%.0f img/s) | int8 %.2f ms (%.0f img/s)"
-          % (a.batch, tb * 1e3, a.batch / tb, tq * 1e3, a.batch / tq), flush=True)
+    with torch.no_grad():
+        ref = m(x).float()
+    calib = torch.randn(64, 3, 224, 224, device="cuda")
+    q8 = Int8ResNet(m, calib)
+    ts = bench(q8, x, a.iters)
+    with torch.no_grad():
+        out = q8(x).float()
+    cos = torch.nn.functional.cosine_similarity(out.flatten(), ref.flatten(), dim=0).item()
+    top1 = (out.argmax(1) == ref.argmax(1)).float().mean().item()
+    res = {"bench": "resnet50-inference", "batch": a.batch, "bf16_img_s": round(a.batch / tb, 1),
+           "int8_static_img_s": round(a.batch / ts, 1), "int8_vs_bf16_logit_cos": round(cos, 4),
+           "int8_vs_bf16_top1_agree": round(top1, 4), "speedup": round(tb / ts, 3)}
+    if not a.no_dynamic:
+        Q.quantize(m)
+        td = bench(m, x, a.iters)
+        res["int8_dynamic_img_s"] = round(a.batch / td, 1)
+    print(json.dumps(res), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,174 @@
+"""Static-int8 ResNet inference on the int8 implicit-GEMM conv kernel (csrc/kernels/qconv.hip).
+
+BigDL's ``quantize()`` (InferenceModelFactory.scala:33,47; ImageModel.scala:133-145) runs
+calibrated int8 convolutions through MKL-DNN; this is the MI355X counterpart
+(SURVEY.md §2.16 HK23):
+
+* weights: BatchNorm folded in, symmetric int8 with one scale per output channel;
+* activations: int8 NHWC between layers with one calibrated per-tensor scale each
+  (absmax over a calibration batch run through the bf16 model, / 127);
+* every conv unit is ONE kernel: int8 x int8 on ``v_mfma_i32_16x16x64_i8`` (2x the bf16
+  MFMA rate, half the bytes), epilogue ``acc * s_in*s_w[c]/s_out + b[c]/s_out
+  (+ resid * s_r/s_out) -> ReLU -> saturating int8``;
+* the stem (3-channel input) and the classifier stay bf16; the last block's int8 output
+  is average-pooled and dequantised by one kernel.
+
+``qconv_ref`` is the float64 CPU model of the kernel (same rounding) used as the oracle.
+"""
+import torch
+import torch.nn as nn
+
+from zoo.ops._native import native
+
+
+def _q_weight(unit):
+    """ConvBN (eval) -> (int8 [K, R*S*C], per-channel scale [K], folded bias [K])."""
+    inv = torch.rsqrt(unit.running_var.float() + unit.eps)
+    g = unit.gamma.detach().float() * inv
+    w = unit.weight.detach().float()[:, :unit.k * unit.k * unit.cin] * g[:, None]
+    s = w.abs().amax(dim=1).clamp_min(1e-12) / 127.0
+    q = torch.round(w / s[:, None]).clamp_(-127, 127).to(torch.int8)
+    b = unit.beta.detach().float() - unit.running_mean.float() * g
+    return q.contiguous(), s, b
+
+
+def _sat(v):
+    return torch.clamp(torch.round(v), -127, 127)
+
+
+def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
+    """float64 CPU model of qconv: xq int8 NHWC, wq int8 [K, R*S*C]."""
+    import torch.nn.functional as F
+    N, H, W, C = xq.shape
+    K = wq.shape[0]
+    w4 = wq[:, :R * S * C].double().reshape(K, R, S, C).permute(0, 3, 1, 2)
+    acc = F.conv2d(xq.double().permute(0, 3, 1, 2), w4, stride=stride, padding=pad).permute(0, 2, 3, 1)
+    v = acc * colscale.double() + (bias.double() if bias is not None else 0.0)
+    if resid is not None:
+        v = v + resid.double() * rscale
+    if relu:
+        v = v.clamp_min(0)
+    return v.to(torch.bfloat16) if out_bf16 else _sat(v).to(torch.int8)
+
+
+def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
+    if xq.is_cuda:
+        return native().qconv(xq, wq, R, S, stride, stride, pad, pad, colscale, bias, resid, float(rscale),
+                              bool(relu), bool(out_bf16))
+    return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16)
+
+
+def quantize_act(x, scale):
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 16 == 0:
+        return native().quantize_i8(x.contiguous(), 1.0 / scale)
+    return _sat(x.double() / scale).to(torch.int8)
+
+
+class _QUnit:
+    """One conv unit: int8 weights and the epilogue constants for given in/out scales."""
+
+    def __init__(self, unit, device):
+        self.q, self.sw, self.b = (t.to(device) for t in _q_weight(unit))
+        self.k, self.stride, self.pad, self.relu = unit.k, unit.stride, unit.pad, unit.relu
+
+    def bind(self, s_in, s_out):
+        self.s_in, self.s_out = s_in, s_out
+        self.colscale = (self.sw * (s_in / s_out)).float().contiguous()
+        self.bias = (self.b / s_out).float().contiguous()
+
+    def __call__(self, xq, resid=None, s_resid=None):
+        return qconv(xq, self.q, self.k, self.k, self.stride, self.pad, self.colscale, self.bias, resid,
+                     0.0 if resid is None else s_resid / self.s_out, self.relu)
+
+
+class Int8ResNet(nn.Module):
+    """Calibrated static-int8 inference twin of a ``zoo.models.image.resnet.ResNet``."""
+
+    def __init__(self, model, calib_x):
+        super().__init__()
+        from zoo.models.image import resnet as R
+        model.eval()
+        self.model = model
+        dev = next(model.parameters()).device
+        self.blocks = []
+        for stage in model.stages:
+            for blk in stage:
+                units = {"conv1": _QUnit(blk.conv1, dev), "conv2": _QUnit(blk.conv2, dev)}
+                if isinstance(blk, R.Bottleneck):
+                    units["conv3"] = _QUnit(blk.conv3, dev)
+                if blk.down is not None:
+                    units["down"] = _QUnit(blk.down, dev)
+                self.blocks.append((blk, units))
+        self.calibrate(calib_x)
+
+    @torch.no_grad()
+    def _stem(self, x):
+        m = self.model
+        from zoo import ops
+        if m._stem_s2d_ok(x):
+            xs = ops.native().nchw_to_s2d(x.float().contiguous(), 3)
+            st = m.stem
+            x = ops.conv_bn_act(xs, m._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
+                                kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
+                                relu=True, training=False)
+        else:
+            x = m.stem(m.to_nhwc(x))
+        return ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+
+    @torch.no_grad()
+    def calibrate(self, x):
+        """Per-tensor absmax of every int8 tensor of the network on ``x`` (run in bf16)."""
+        amax = lambda t: max(float(t.float().abs().max()), 1e-6) / 127.0  # noqa: E731
+        h = self._stem(x)
+        self.s_in = amax(h)
+        s_x = self.s_in
+        for blk, u in self.blocks:
+            sc = blk.down(h) if blk.down is not None else h
+            s_sc = amax(sc) if blk.down is not None else s_x
+            h1 = blk.conv1(h)
+            s1 = amax(h1)
+            if "conv3" in u:
+                h2 = blk.conv2(h1)
+                s2 = amax(h2)
+                out = blk.conv3(h2, resid=sc)
+            else:
+                out = blk.conv2(h1, resid=sc)
+            s_o = amax(out)
+            u["conv1"].bind(s_x, s1)
+            if "conv3" in u:
+                u["conv2"].bind(s1, s2)
+                u["conv3"].bind(s2, s_o)
+            else:
+                u["conv2"].bind(s1, s_o)
+            if "down" in u:
+                u["down"].bind(s_x, s_sc)
+            blk._q_scales = (s_x, s_sc, s_o)
+            h, s_x = out, s_o
+        self.s_out = s_x
+        return self
+
+    @torch.no_grad()
+    def forward(self, x):
+        h = self._stem(x)
+        xq = quantize_act(h, self.s_in)
+        for blk, u in self.blocks:
+            s_x, s_sc, s_o = blk._q_scales
+            sc = u["down"](xq) if "down" in u else xq
+            h1 = u["conv1"](xq)
+            if "conv3" in u:
+                xq = u["conv3"](u["conv2"](h1), resid=sc, s_resid=s_sc)
+            else:
+                xq = u["conv2"](h1, resid=sc, s_resid=s_sc)
+        if xq.is_cuda:
+            feat = native().gap_i8(xq.contiguous(), self.s_out)
+        else:
+            feat = (xq.double() * self.s_out).mean((1, 2)).to(torch.bfloat16)
+        return self.model.fc(feat)
+
+
+def quantize_resnet(model, calib_x):
+    """Static-int8 inference twin of ``model`` (a zoo ResNet), calibrated on ``calib_x``."""
+    return Int8ResNet(model, calib_x)
+
+
+__all__ = ["Int8ResNet", "quantize_resnet", "qconv", "qconv_ref", "quantize_act"]

@@ -1,0 +1,46 @@
+"""Static-int8 implicit-GEMM conv (csrc/kernels/qconv.hip) against its float64 model
+(zoo.ops.qresnet.qconv_ref), and the calibrated int8 ResNet against the bf16 model."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [(2, 14, 64, 64, 1, 1, 0), (2, 14, 64, 128, 3, 1, 1),
+                                                  (3, 15, 32, 64, 3, 2, 1), (2, 16, 128, 256, 1, 2, 0),
+                                                  (1, 7, 512, 2048, 1, 1, 0), (4, 28, 16, 72, 3, 1, 1)])
+@pytest.mark.parametrize("resid,relu,out_bf16", [(False, True, False), (True, True, False), (True, False, True)])
+def test_qconv_matches_float64_model(gpu, N, H, C, K, R, stride, pad, resid, relu, out_bf16):
+    from zoo.ops.qresnet import qconv, qconv_ref
+    g = torch.Generator().manual_seed(N * 1000 + C + K)
+    xq = torch.randint(-127, 128, (N, H, H, C), generator=g, dtype=torch.int8)
+    wq = torch.randint(-127, 128, (K, R * R * C), generator=g, dtype=torch.int8)
+    cs = (torch.rand(K, generator=g) * 2e-4 + 1e-5).float()
+    b = (torch.randn(K, generator=g) * 3).float()
+    P = (H + 2 * pad - R) // stride + 1
+    rq = torch.randint(-127, 128, (N, P, P, K), generator=g, dtype=torch.int8) if resid else None
+    ref = qconv_ref(xq, wq, R, R, stride, pad, cs, b, rq, 0.37, relu, out_bf16)
+    out = qconv(xq.to(gpu), wq.to(gpu), R, R, stride, pad, cs.to(gpu), b.to(gpu),
+                None if rq is None else rq.to(gpu), 0.37, relu, out_bf16).cpu()
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    if out_bf16:
+        assert torch.allclose(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    else:
+        d = (out.int() - ref.int()).abs()
+        assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-3   # fp32 vs fp64 rounding ties
+
+
+def test_int8_resnet_tracks_bf16_model(gpu):
+    from zoo.models.image.resnet import resnet50
+    from zoo.ops.qresnet import Int8ResNet
+    torch.manual_seed(0)
+    m = resnet50(num_classes=100).to(gpu).eval()
+    x = torch.randn(16, 3, 224, 224, device=gpu)
+    with torch.no_grad():
+        ref = m(x).float()
+    q = Int8ResNet(m, torch.randn(16, 3, 224, 224, device=gpu))
+    with torch.no_grad():
+        out = q(x).float()
+    assert out.shape == ref.shape and torch.isfinite(out).all()
+    cos = torch.nn.functional.cosine_similarity(out.flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.95, cos
