@@ -13,10 +13,12 @@ classifier, zoo Keras ``Dense`` layers and ``torch.nn.Linear`` / ``Conv2d``.
 On the CPU the same integer arithmetic runs exactly in float64 (the reference
 path the GPU kernels are tested against).
 
-Status (tools/quant_bench.py, MI355X, ResNet-50 batch 64): int8 8.7k img/s vs
-the fused bf16 path 19.2k img/s -- the int8 conv is an explicit im2col plus a
-plain tiled GEMM, not yet an implicit-GEMM kernel with the epilogue fusions of
-the bf16 path; it exists for memory footprint / parity with quantize().
+This module is the DYNAMIC path (no calibration data: per-call activation absmax, im2col +
+GEMM; any model). With calibration data a zoo ResNet takes the STATIC path instead --
+``quantize(model, calib_data)`` returns a :class:`zoo.ops.qresnet.Int8ResNet`, whose
+convolutions are one implicit-GEMM int8 kernel each with the whole unit fused in the
+epilogue (tools/quant_bench.py, MI355X, ResNet-50 b256: static int8 60.2k img/s vs bf16
+41.1k vs this dynamic path 11.1k; profiles/resnet50_infer_int8_r2.md).
 """
 import torch
 import torch.nn as nn
@@ -156,11 +158,19 @@ def _quantizable_conv(m):
         isinstance(m.padding, tuple) and m.padding_mode == "zeros"
 
 
-def quantize(model):
-    """Convert supported layers of ``model`` to int8 in place; returns the model (eval mode)."""
+def quantize(model, calib_data=None):
+    """Convert supported layers of ``model`` to int8 in place; returns the model (eval mode).
+    With ``calib_data`` (an input batch) a zoo ResNet is instead returned as its calibrated
+    static-int8 twin (zoo.ops.qresnet.Int8ResNet; the original model is left as is)."""
     from zoo.models.image import resnet as R
     from zoo.pipeline.api.keras.layers.core import Dense as KDense
     model.eval()
+    if calib_data is not None and isinstance(model, R.ResNet):
+        from zoo.ops.qresnet import Int8ResNet
+        dev = next(model.parameters()).device
+        q = Int8ResNet(model, torch.as_tensor(calib_data).to(dev))
+        q._zoo_quantized = True
+        return q
 
     def convert(parent):
         for name, child in list(parent.named_children()):

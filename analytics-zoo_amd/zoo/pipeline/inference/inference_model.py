@@ -132,14 +132,14 @@ class InferenceModel:
         self._t0 = None
 
     # ------------------------------------------------------------------ loading
-    def _install(self, model, quantize=False):
+    def _install(self, model, quantize=False, calib_data=None):
         model = model.to(self.device)
         if self.dtype is not None:
             model = model.to(self.dtype)
         model.eval()
         if quantize:  # blas=false in the reference loaders -> BigDL quantize() (int8)
             from zoo.ops.quant import quantize as _q
-            model = _q(model)
+            model = _q(model, calib_data)
         for p in model.parameters():
             p.requires_grad_(False)
         self.model = model
@@ -156,10 +156,11 @@ class InferenceModel:
             self._n_replicas += 1
         return r
 
-    def load_module(self, module, blas=True):
+    def load_module(self, module, blas=True, calib_data=None):
         """Serve an in-memory torch.nn.Module (the PyTorch loader, doLoadPyTorch).
-        ``blas=False`` quantizes to int8 as the reference loaders do."""
-        return self._install(module, quantize=not blas)
+        ``blas=False`` quantizes to int8 as the reference loaders do; with ``calib_data`` a
+        zoo ResNet gets the calibrated static-int8 kernels (zoo.ops.qresnet)."""
+        return self._install(module, quantize=not blas, calib_data=calib_data)
 
     def load(self, model_path, weight_path=None, blas=True):
         """Zoo Keras/ZooModel file (doLoad, InferenceModel.scala:97-110)."""
@@ -176,11 +177,12 @@ class InferenceModel:
         from zoo.pipeline.api.net import Net
         return self._install(Net.load_caffe(model_path, weight_path), quantize=not blas)
 
-    def quantize(self):
-        """Re-install the loaded model as its int8 version (InferenceModelFactory.scala:33,47)."""
+    def quantize(self, calib_data=None):
+        """Re-install the loaded model as its int8 version (InferenceModelFactory.scala:33,47);
+        ``calib_data`` selects the calibrated static-int8 path where the model supports it."""
         if self.model is None:
             raise RuntimeError("load a model first")
-        return self._install(self.model, quantize=True)
+        return self._install(self.model, quantize=True, calib_data=calib_data)
 
     def load_onnx(self, model_path):
         from zoo.pipeline.api.onnx import load_onnx

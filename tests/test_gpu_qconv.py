@@ -44,3 +44,24 @@ def test_int8_resnet_tracks_bf16_model(gpu):
     assert out.shape == ref.shape and torch.isfinite(out).all()
     cos = torch.nn.functional.cosine_similarity(out.flatten(), ref.flatten(), dim=0).item()
     assert cos > 0.95, cos
+
+
+def test_inference_model_static_int8_with_hipgraph(gpu):
+    """InferenceModel.load_module(blas=False, calib_data=...) serves the calibrated int8
+    twin through the hipGraph replica path; predictions track the bf16 model."""
+    import numpy as np
+    from zoo.models.image.resnet import resnet18
+    from zoo.pipeline.inference import InferenceModel
+    torch.manual_seed(1)
+    m = resnet18(num_classes=10).to(gpu).eval()
+    x = torch.randn(8, 3, 64, 64)
+    with torch.no_grad():
+        ref = m(x.to(gpu)).float().cpu().numpy()
+    im = InferenceModel(2, device=gpu).load_module(m, blas=False, calib_data=torch.randn(8, 3, 64, 64))
+    from zoo.ops.qresnet import Int8ResNet
+    assert isinstance(im.model, Int8ResNet)
+    out = im.predict(x)
+    out2 = im.predict(x)       # graph replay
+    assert np.allclose(out, out2)
+    cos = float((out * ref).sum() / (np.linalg.norm(out) * np.linalg.norm(ref)))
+    assert cos > 0.95, cos
