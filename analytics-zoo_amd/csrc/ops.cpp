@@ -99,6 +99,11 @@ hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*
                      int, int, hipStream_t);
 hipError_t zoo_quantize_i8(const void*, void*, size_t, float, hipStream_t);
 hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, hipStream_t);
+hipError_t zoo_act(const void*, const void*, void*, size_t, int, int, float, hipStream_t);
+hipError_t zoo_dropout(const void*, void*, size_t, int, float, uint64_t, hipStream_t);
+hipError_t zoo_loss(const void*, const void*, void*, float*, size_t, int, int, float, float, hipStream_t);
+hipError_t zoo_auc_hist(const float*, const float*, float*, size_t, int, float, float, hipStream_t);
+hipError_t zoo_box_decode(const float*, const float*, float*, int, int, float, float, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
                         float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
 }
@@ -961,6 +966,83 @@ void embedding_bwd(torch::Tensor dout, torch::Tensor idx, torch::Tensor gtable, 
 }
 
 
+// ---- pointwise.hip: activations, dropout, elementwise objectives, AUC histogram, box decode ----
+static bool pw_f32(const torch::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), what, " must be a contiguous GPU tensor");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, what, " must be fp32 or bf16");
+  return t.scalar_type() == at::kFloat;
+}
+
+// dy empty: y = act(x); else dx = dy * act'(x)
+torch::Tensor act_fwd_bwd(torch::Tensor x, c10::optional<torch::Tensor> dy, int64_t kind, double alpha) {
+  const bool f32 = pw_f32(x, "x");
+  TORCH_CHECK(kind >= 0 && kind <= 15, "act: unknown activation code");
+  const void* dp = nullptr;
+  if (dy.has_value() && dy->defined()) {
+    TORCH_CHECK(pw_f32(*dy, "dy") == f32 && dy->numel() == x.numel(), "act: dy must match x");
+    dp = dy->data_ptr();
+  }
+  auto out = torch::empty_like(x);
+  if (x.numel() > 0)
+    check_hip(zoo_act(x.data_ptr(), dp, out.data_ptr(), x.numel(), f32, (int)kind, (float)alpha, cur_stream()),
+              "act");
+  return out;
+}
+
+torch::Tensor dropout_fwd(torch::Tensor x, double p, int64_t seed) {
+  const bool f32 = pw_f32(x, "x");
+  TORCH_CHECK(p >= 0.0 && p <= 1.0, "dropout: p must be in [0, 1]");
+  auto out = torch::empty_like(x);
+  if (x.numel() > 0)
+    check_hip(zoo_dropout(x.data_ptr(), out.data_ptr(), x.numel(), f32, (float)p, (uint64_t)seed, cur_stream()),
+              "dropout");
+  return out;
+}
+
+// -> (loss fp32 scalar, grad like pred); w = per-element weight (1/N for mean)
+std::vector<torch::Tensor> loss_fwd(torch::Tensor pred, torch::Tensor target, int64_t kind, double beta, double w,
+                                    bool want_grad) {
+  const bool f32 = pw_f32(pred, "pred");
+  TORCH_CHECK(pw_f32(target, "target") == f32 && target.numel() == pred.numel(), "loss: target must match pred");
+  TORCH_CHECK(kind >= 0 && kind <= 10, "loss: unknown loss code");
+  auto loss = torch::zeros({}, pred.options().dtype(at::kFloat));
+  torch::Tensor grad;
+  if (want_grad) grad = torch::empty_like(pred);
+  if (pred.numel() > 0)
+    check_hip(zoo_loss(pred.data_ptr(), target.data_ptr(), want_grad ? grad.data_ptr() : nullptr,
+                       loss.data_ptr<float>(), pred.numel(), f32, (int)kind, (float)beta, (float)w, cur_stream()),
+              "loss");
+  if (want_grad) return {loss, grad};
+  return {loss};
+}
+
+torch::Tensor auc_hist(torch::Tensor score, torch::Tensor label, int64_t nbins, double lo, double hi) {
+  req(score, at::kFloat, "score");
+  req(label, at::kFloat, "label");
+  TORCH_CHECK(score.numel() == label.numel(), "auc_hist: score/label size");
+  TORCH_CHECK(nbins >= 1 && nbins <= 16384, "auc_hist: 1 <= nbins <= 16384");
+  auto hist = torch::zeros({2, nbins}, score.options());
+  if (score.numel() > 0)
+    check_hip(zoo_auc_hist(score.data_ptr<float>(), label.data_ptr<float>(), hist.data_ptr<float>(), score.numel(),
+                           (int)nbins, (float)lo, (float)hi, cur_stream()),
+              "auc_hist");
+  return hist;
+}
+
+torch::Tensor box_decode(torch::Tensor loc, torch::Tensor priors, double v0, double v1, bool clip) {
+  req(loc, at::kFloat, "loc");
+  req(priors, at::kFloat, "priors");
+  TORCH_CHECK(loc.dim() == 3 && loc.size(2) == 4 && priors.dim() == 2 && priors.size(1) == 4 &&
+                  priors.size(0) == loc.size(1), "box_decode: loc [N,P,4], priors [P,4]");
+  TORCH_CHECK(loc.numel() < (1LL << 31), "box_decode: too large");
+  auto boxes = torch::empty_like(loc);
+  if (loc.numel() > 0)
+    check_hip(zoo_box_decode(loc.data_ptr<float>(), priors.data_ptr<float>(), boxes.data_ptr<float>(),
+                             (int)loc.size(0), (int)loc.size(1), (float)v0, (float)v1, clip, cur_stream()),
+              "box_decode");
+  return boxes;
+}
+
 // ---- static-int8 implicit-GEMM conv (qconv.hip) ----
 // x: int8 NHWC [N,H,W,C] (C % 16 == 0); w: int8 [K, ldb] rows of [R][S][C]; colscale/bias fp32 [K]
 // (already divided by the output scale); resid: int8 [N,P,Q,K] scaled by rscale. Output int8
@@ -1510,6 +1592,11 @@ PYBIND11_MODULE(_C, m) {
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
   m.def("qconv", &qconv);
+  m.def("act_fwd_bwd", &act_fwd_bwd);
+  m.def("dropout_fwd", &dropout_fwd);
+  m.def("loss_fwd", &loss_fwd);
+  m.def("auc_hist", &auc_hist);
+  m.def("box_decode", &box_decode);
   m.def("quantize_i8", &quantize_i8);
   m.def("gap_i8", &gap_i8);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);

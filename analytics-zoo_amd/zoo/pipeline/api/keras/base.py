@@ -122,6 +122,10 @@ def apply_activation(x, name):
         return softmax(x, -1, log=True)
     if n not in _ACTS:
         raise ValueError("Unsupported activation: %s" % name)
+    if x.is_cuda and n not in ("linear",):
+        from zoo.ops.pointwise import ACT_CODES, activation   # native fwd/bwd kernels (HK13)
+        if n in ACT_CODES:
+            return activation(x, n)
     return _ACTS[n](x)
 
 

@@ -61,7 +61,8 @@ class Dropout(Layer):
         self.p = float(p)
 
     def call(self, x):
-        return F.dropout(x, self.p, self.training)
+        from zoo.ops.pointwise import dropout   # native counter-hash mask on the GPU (HK16)
+        return dropout(x, self.p, self.training)
 
 
 class SpatialDropout1D(Layer):

@@ -133,6 +133,16 @@ class AUC(ValidationMethod):
         if output.dim() > 1 and output.shape[-1] == 2:
             p = output.float()[:, 1]
         t = target.to(output.device).float().reshape(-1)
+        if p.is_cuda and self.T > 1:
+            # one native histogram pass (HK14): bin i = [i/(T-1), (i+1)/(T-1)); TP/FP at threshold
+            # i are the suffix sums from bin i
+            from zoo.ops._native import native
+            h = native().auc_hist(p.contiguous(), t.contiguous(), self.T, 0.0, self.T / (self.T - 1.0))
+            suf = h.flip(1).cumsum(1).flip(1).double().cpu().numpy()
+            for i in range(self.T):
+                acc[i] += float(suf[0, i])
+                acc[self.T + i] += float(suf[1, i])
+            return
         th = torch.linspace(0, 1, self.T, device=p.device)
         predpos = p.unsqueeze(0) >= th.unsqueeze(1)        # [T, n]
         pos = (t > 0.5).unsqueeze(0)

@@ -14,6 +14,18 @@ from zoo import ops
 EPS = 1e-7
 
 
+def _native(y_pred, y_true, kind, size_average=True, beta=1.0, weight=None):
+    """The native one-pass loss+gradient kernel (zoo/ops/pointwise.py, HK20) for fp32/bf16 GPU
+    predictions whose target has the same shape; None otherwise."""
+    if not (torch.is_tensor(y_pred) and y_pred.is_cuda and torch.is_tensor(y_true) and
+            y_true.shape == y_pred.shape and y_pred.numel() > 0):
+        return None
+    from zoo.ops.pointwise import elementwise_loss
+    w = weight if weight is not None else (1.0 / y_pred.numel() if size_average else 1.0)
+    # fp32 math like the reference definitions (y_pred.float()): the cast is differentiable
+    return elementwise_loss(y_pred.float(), y_true.float(), kind, w, beta)
+
+
 class LossFunction:
     name = "loss"
 
@@ -97,6 +109,10 @@ class BinaryCrossEntropy(LossFunction):
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
         p = torch.clamp(y_pred.float(), EPS, 1.0 - EPS)
+        if self.weights is None:
+            r = _native(y_pred, y_true, "bce", self.size_average)
+            if r is not None:
+                return r
         w = None if self.weights is None else torch.as_tensor(self.weights, dtype=torch.float32, device=p.device)
         return F.binary_cross_entropy(p, y_true, weight=w, reduction="mean" if self.size_average else "sum")
 
@@ -107,6 +123,9 @@ class MeanSquaredError(LossFunction):
 
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred)
+        r = _native(y_pred, y_true, "mse", self.size_average)
+        if r is not None:
+            return r
         return F.mse_loss(y_pred.float(), y_true.float(), reduction="mean" if self.size_average else "sum")
 
 
@@ -116,12 +135,18 @@ class MeanAbsoluteError(LossFunction):
 
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred)
+        r = _native(y_pred, y_true, "mae", self.size_average)
+        if r is not None:
+            return r
         return F.l1_loss(y_pred.float(), y_true.float(), reduction="mean" if self.size_average else "sum")
 
 
 class MeanAbsolutePercentageError(LossFunction):
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
+        r = _native(y_pred, y_true, "mape", True)
+        if r is not None:
+            return r
         diff = (y_true - y_pred.float()).abs() / torch.clamp(y_true.abs(), EPS, float("inf"))
         return 100.0 * diff.mean()
 
@@ -129,6 +154,9 @@ class MeanAbsolutePercentageError(LossFunction):
 class MeanSquaredLogarithmicError(LossFunction):
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
+        r = _native(y_pred, y_true, "msle", True)
+        if r is not None:
+            return r
         a = torch.log(torch.clamp(y_pred.float(), EPS, float("inf")) + 1.0)
         b = torch.log(torch.clamp(y_true, EPS, float("inf")) + 1.0)
         return ((a - b) ** 2).mean()
@@ -140,6 +168,9 @@ class Hinge(LossFunction):
 
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
+        r = _native(y_pred, y_true, "hinge", self.size_average, self.margin)
+        if r is not None:
+            return r
         l = torch.clamp(self.margin - y_true * y_pred.float(), min=0)
         return l.mean() if self.size_average else l.sum()
 
@@ -150,12 +181,19 @@ class SquaredHinge(Hinge):
 
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
+        r = _native(y_pred, y_true, "squared_hinge", True, self.margin)
+        if r is not None:
+            return r
         l = torch.clamp(self.margin - y_true * y_pred.float(), min=0) ** 2
         return l.mean()
 
 
 class KullbackLeiblerDivergence(LossFunction):
     def forward(self, y_pred, y_true):
+        rows = y_pred.numel() // max(y_pred.shape[-1], 1) if y_pred.dim() else 1
+        r = _native(y_pred, _match(y_true, y_pred).float(), "kld", True, weight=1.0 / max(rows, 1))
+        if r is not None:
+            return r
         y_true = torch.clamp(_match(y_true, y_pred).float(), EPS, 1.0)
         y_pred = torch.clamp(y_pred.float(), EPS, 1.0)
         return (y_true * torch.log(y_true / y_pred)).sum(-1).mean()
@@ -172,6 +210,9 @@ class CosineProximity(LossFunction):
 class Poisson(LossFunction):
     def forward(self, y_pred, y_true):
         y_true = _match(y_true, y_pred).float()
+        r = _native(y_pred, y_true, "poisson", True)
+        if r is not None:
+            return r
         p = y_pred.float()
         return (p - y_true * torch.log(p + EPS)).mean()
 
