@@ -119,6 +119,37 @@ struct AttnStrides {
   long qb, qh, ql, kb, kh, kl, vb, vh, vl, ob, oh, ol;
 };
 
+// backward element strides (batch, head, row) of q, k, v, dO, O, dQ, dK, dV: the packed training
+// path reads q/k/v straight out of the [B, L, 3, H, D] projection and writes dq/dk/dv into its
+// gradient, dO / O being [B, L, H, D] (LSE and delta stay contiguous [B*H, L]).
+struct AttnBwdStrides {
+  long qb, qh, ql, kb, kh, kl, vb, vh, vl, gb, gh, gl, ob, oh, ol;
+  long dqb, dqh, dql, dkb, dkh, dkl, dvb, dvh, dvl;
+};
+
+// Dropout on the attention probabilities (BERT attention_probs dropout, TransformerLayer.scala
+// attnDrop): keep(bh, q, key) is a counter hash of the element coordinates and a per-call seed,
+// so the forward and both backward passes regenerate the same mask without storing it.
+//   forward   O = (1/l) sum_k keep*scale * exp(s - m) V     (l sums the UNdropped terms)
+//   backward  dV += P_drop^T dO ; dS = P * (keep*scale * dP_drop - delta), delta = rowsum(dO*O)
+struct AttnDrop {
+  uint32_t thresh;  // 0: no dropout
+  float scale;      // 1 / (1 - p)
+  uint32_t s0, s1;
+};
+
+ZOO_DEV uint32_t attn_fmix(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+
+// keep-factor (scale or 0) of probability (bh, q, key)
+ZOO_DEV float attn_keep(const AttnDrop& d, int bh, int q, int key) {
+  const uint32_t a = attn_fmix((uint32_t)bh * 0x9E3779B1u ^ d.s1);
+  const uint32_t hsh = attn_fmix(((uint32_t)q * 0x85EBCA77u + (uint32_t)key) ^ d.s0 ^ a);
+  return hsh >= d.thresh ? d.scale : 0.f;
+}
+
 template <int D, int NW>
 ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf16_t* dst1, int r0, int nrows,
                        long ld0 = D, long ld1 = D) {
@@ -141,11 +172,11 @@ ZOO_DEV void dma_tiles(const bf16_t* src0, const bf16_t* src1, bf16_t* dst0, bf1
   }
 }
 
-template <int D, int NW, bool HAS_MASK>
+template <int D, int NW, bool HAS_MASK, bool DROP>
 __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, bf16_t* __restrict__ O, float* __restrict__ LSE, int H, int L, int S,
-    float scale, int causal, AttnStrides sd) {
+    float scale, int causal, AttnStrides sd, AttnDrop dd) {
   constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);  // [2][64][D]
@@ -276,6 +307,13 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
           ps[i & 3] += p;
         }
       lsum += (ps[0] + ps[1]) + (ps[2] + ps[3]);
+      if (DROP) {  // dropout after the (undropped) normaliser sum
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            s[kt][i] *= attn_keep(dd, bh, q, kv0 + 32 * kt + 8 * (i >> 2) + 4 * h + (i & 3));
+      }
       bf16x8 pf[4];
 #pragma unroll
       for (int k4 = 0; k4 < 4; ++k4) pf[k4] = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
@@ -315,17 +353,19 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
 // delta[row] = sum_d dO[row][d] * O[row][d]  (fp32), 16 lanes per row
 template <int D>
 __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restrict__ dO, const bf16_t* __restrict__ O,
-                                                         float* __restrict__ delta, int rows) {
+                                                         float* __restrict__ delta, int rows, int H, int L,
+                                                         AttnBwdStrides sd) {
   constexpr int LPR = D / 8;  // lanes per row (8 or 16)
   const int tid = blockIdx.x * 256 + threadIdx.x;
   const int row = tid / LPR, part = tid % LPR;
   float acc = 0.f;
   if (row < rows) {
-    float a[8], b[8];
-    unpack8(*reinterpret_cast<const uint4*>(dO + (size_t)row * D + part * 8), a);
-    unpack8(*reinterpret_cast<const uint4*>(O + (size_t)row * D + part * 8), b);
+    const int bh = row / L, l = row - bh * L, b = bh / H, hd = bh - b * H;
+    float a[8], c[8];
+    unpack8(*reinterpret_cast<const uint4*>(dO + b * sd.gb + hd * sd.gh + (long)l * sd.gl + part * 8), a);
+    unpack8(*reinterpret_cast<const uint4*>(O + b * sd.ob + hd * sd.oh + (long)l * sd.ol + part * 8), c);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc += a[e] * b[e];
+    for (int e = 0; e < 8; ++e) acc += a[e] * c[e];
   }
 #pragma unroll
   for (int o = LPR / 2; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
@@ -340,12 +380,12 @@ __global__ __launch_bounds__(256) void attn_delta_kernel(const bf16_t* __restric
 //   dV^T += dO^T P, dK^T += Q^T dS: P / dS packed from the accumulators, dO^T /
 //   Q^T transposed-read from the same LDS tiles in that permuted q order.
 // ---------------------------------------------------------------------------
-template <int D, int QW, bool HAS_MASK>
+template <int D, int QW, bool HAS_MASK, bool DROP>
 __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
-    float scale, int causal) {
+    float scale, int causal, AttnBwdStrides sd, AttnDrop dd) {
   // QW = 2: 8 waves; wave w owns keys 32(w&3).. and query rows 32(w>>2).. of every
   // 64-row tile (two waves per SIMD); the two q-halves are summed through LDS at the end
   constexpr int KS = D / 16, DT = D / 32, NQT = 2 / QW;
@@ -357,9 +397,9 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
   const int kg = wid & 3, qh = QW == 2 ? wid >> 2 : 0;
-  const int bh = blockIdx.y, b = bh / H;
-  const bf16_t* Qp = Q + (size_t)bh * L * D;
-  const bf16_t* dOp = dO + (size_t)bh * L * D;
+  const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+  const bf16_t* Qp = Q + b * sd.qb + hd * sd.qh;
+  const bf16_t* dOp = dO + b * sd.gb + hd * sd.gh;
   const float* lp = LSE + (size_t)bh * L;
   const float* dp_ = delta + (size_t)bh * L;
   const int kblk = blockIdx.x * 128, kw0 = kblk + kg * 32, key = kw0 + lr;
@@ -371,8 +411,8 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
   bf16x8 kf[KS], vf[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    kf[ks] = load_frag(K + ((size_t)bh * S + key) * D + 16 * ks + 8 * h, key_ok);
-    vf[ks] = load_frag(V + ((size_t)bh * S + key) * D + 16 * ks + 8 * h, key_ok);
+    kf[ks] = load_frag(K + b * sd.kb + hd * sd.kh + (long)key * sd.kl + 16 * ks + 8 * h, key_ok);
+    vf[ks] = load_frag(V + b * sd.vb + hd * sd.vh + (long)key * sd.vl + 16 * ks + 8 * h, key_ok);
   }
   f32x16 dk[DT], dv[DT];
 #pragma unroll
@@ -387,7 +427,7 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
 
   float lse_r = 0.f, del_r = 0.f;
   auto load_rows = [&](int q0, int buf) {
-    dma_tiles<D, 4 * QW>(Qp, dOp, Qs + buf * 64 * D, dOs + buf * 64 * D, q0, L);
+    dma_tiles<D, 4 * QW>(Qp, dOp, Qs + buf * 64 * D, dOs + buf * 64 * D, q0, L, sd.ql, sd.gl);
     if (threadIdx.x < 64) {
       const int q = q0 + threadIdx.x;
       lse_r = q < L ? lp[q] * kLog2e : INFINITY;
@@ -454,8 +494,9 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
             const int i = 4 * i4 + r;
             float p = fexp2(s[qt][i] * c2 + (madd - lv[r]));
             if (diag && key > q0 + qr + r + coff) p = 0.f;
-            s[qt][i] = p;
-            dp[qt][i] = p * (dp[qt][i] - dv4[r]);
+            const float kf_ = DROP ? attn_keep(dd, bh, q0 + qr + r, key) : 1.f;
+            s[qt][i] = p * kf_;
+            dp[qt][i] = p * (dp[qt][i] * kf_ - dv4[r]);
           }
         }
       bf16x8 pf[2 * NQT], sf[2 * NQT];
@@ -513,8 +554,8 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
   }
   if (!key_ok) return;
   // reg i of dk[dt] = dK[key][32dt + 8(i>>2) + 4h + (i&3)]
-  bf16_t* dkr = dK + ((size_t)bh * S + key) * D;
-  bf16_t* dvr = dV + ((size_t)bh * S + key) * D;
+  bf16_t* dkr = dK + b * sd.dkb + hd * sd.dkh + (long)key * sd.dkl;
+  bf16_t* dvr = dV + b * sd.dvb + hd * sd.dvh + (long)key * sd.dvl;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -535,11 +576,12 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
 //   S^T = K Q^T, dP^T = V dO^T (query on the lane: LSE and delta are per-lane
 //   scalars), dQ^T += K^T dS^T with K^T transposed-read from the K tile.
 // ---------------------------------------------------------------------------
-template <int D, int NW, bool HAS_MASK>
+template <int D, int NW, bool HAS_MASK, bool DROP>
 __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
-    const float* __restrict__ delta, bf16_t* __restrict__ dQ, int H, int L, int S, float scale, int causal) {
+    const float* __restrict__ delta, bf16_t* __restrict__ dQ, int H, int L, int S, float scale, int causal,
+    AttnBwdStrides sd, AttnDrop dd) {
   constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
@@ -547,9 +589,9 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
   float* Ms = reinterpret_cast<float*>(Vs + 2 * 64 * D);
 
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
-  const int bh = blockIdx.y, b = bh / H;
-  const bf16_t* Kp = K + (size_t)bh * S * D;
-  const bf16_t* Vp = V + (size_t)bh * S * D;
+  const int bh = blockIdx.y, b = bh / H, hd = bh - b * H;
+  const bf16_t* Kp = K + b * sd.kb + hd * sd.kh;
+  const bf16_t* Vp = V + b * sd.vb + hd * sd.vh;
   const float* mrow = HAS_MASK ? mask + (size_t)b * S : nullptr;
   // causal: heaviest query blocks (largest index) first
   const int qb = causal ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x;
@@ -561,8 +603,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
   bf16x8 qf[KS], of[KS];
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = load_frag(Q + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q_ok);
-    of[ks] = load_frag(dO + ((size_t)bh * L + q) * D + 16 * ks + 8 * h, q_ok);
+    qf[ks] = load_frag(Q + b * sd.qb + hd * sd.qh + (long)q * sd.ql + 16 * ks + 8 * h, q_ok);
+    of[ks] = load_frag(dO + b * sd.gb + hd * sd.gh + (long)q * sd.gl + 16 * ks + 8 * h, q_ok);
   }
   const float lse2 = q_ok ? LSE[(size_t)bh * L + q] * kLog2e : INFINITY;
   const float del = q_ok ? delta[(size_t)bh * L + q] : 0.f;
@@ -586,7 +628,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
     if (threadIdx.x < 64) Ms[buf * 64 + threadIdx.x] = mreg;
   };
   if (ntiles > 0) {
-    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S);
+    dma_tiles<D, NW>(Kp, Vp, Ks, Vs, 0, S, sd.kl, sd.vl);
     load_mask(0);
     wait_vm0();
     store_mask(0);
@@ -596,7 +638,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1, kv0 = t * 64;
     if (t + 1 < ntiles) {
-      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S);
+      dma_tiles<D, NW>(Kp, Vp, Ks + (buf ^ 1) * 64 * D, Vs + (buf ^ 1) * 64 * D, kv0 + 64, S, sd.kl, sd.vl);
       load_mask(kv0 + 64);
     }
     const bf16_t* kt_ = Ks + buf * 64 * D;
@@ -638,7 +680,8 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
             const int i = 4 * i4 + r;
             float p = fexp2(s[kt][i] * c2 + (ma[r] - lse2));
             if (diag && kv0 + kr + r > q + coff) p = 0.f;
-            dp[kt][i] = p * (dp[kt][i] - del);
+            const float kf_ = DROP ? attn_keep(dd, bh, q, kv0 + kr + r) : 1.f;
+            dp[kt][i] = p * (dp[kt][i] * kf_ - del);
           }
         }
       bf16x8 sf[4];
@@ -660,7 +703,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
     __syncthreads();
   }
   if (!q_ok) return;
-  bf16_t* dqr = dQ + ((size_t)bh * L + q) * D;
+  bf16_t* dqr = dQ + b * sd.dqb + hd * sd.dqh + (long)q * sd.dql;
 #pragma unroll
   for (int dt = 0; dt < DT; ++dt)
 #pragma unroll
@@ -676,38 +719,55 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
 
 using namespace zoo;
 
-template <int D, int NW, bool HM>
+template <int D, int NW, bool HM, bool DR>
 static void launch_fwd(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
-                       int H, int L, int S, float scale, int causal, const AttnStrides& sd, hipStream_t st) {
+                       int H, int L, int S, float scale, int causal, const AttnStrides& sd, const AttnDrop& dd,
+                       hipStream_t st) {
   const dim3 grid((L + 32 * NW - 1) / (32 * NW), B * H);
   const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 2 * 64 * sizeof(float);
   static const bool lds_ok_ = [] {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_fwd_kernel<D, NW, HM>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_fwd_kernel<D, NW, HM, DR>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
     return true;
   }();
   (void)lds_ok_;
-  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, HM>), grid, dim3(NW * 64), smem, st, (const bf16_t*)q,
-                     (const bf16_t*)k, (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal, sd);
+  hipLaunchKernelGGL((attn_fwd_kernel<D, NW, HM, DR>), grid, dim3(NW * 64), smem, st, (const bf16_t*)q,
+                     (const bf16_t*)k, (const bf16_t*)v, mask, (bf16_t*)o, lse, H, L, S, scale, causal, sd, dd);
 }
 
 template <int D>
 static void launch_fwd_d(const void* q, const void* k, const void* v, const float* mask, void* o, float* lse, int B,
-                         int H, int L, int S, float scale, int causal, const AttnStrides& sd, hipStream_t st) {
-  // 8 waves (256 query rows) share each K/V tile when there are enough rows
+                         int H, int L, int S, float scale, int causal, const AttnStrides& sd, const AttnDrop& dd,
+                         hipStream_t st) {
+  // 8 waves (256 query rows) share each K/V tile when there are enough rows; dropout is a
+  // template flag so the plain kernels keep their register budget (occupancy)
+#define ZOO_ATTN_FWD(NW_, HM_, DR_) launch_fwd<D, NW_, HM_, DR_>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, dd, st)
+  const bool dr = dd.thresh != 0u;
   if (L >= 256) {
-    if (mask) launch_fwd<D, 8, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
-    else launch_fwd<D, 8, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    if (mask) { if (dr) ZOO_ATTN_FWD(8, true, true); else ZOO_ATTN_FWD(8, true, false); }
+    else { if (dr) ZOO_ATTN_FWD(8, false, true); else ZOO_ATTN_FWD(8, false, false); }
   } else {
-    if (mask) launch_fwd<D, 4, true>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
-    else launch_fwd<D, 4, false>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    if (mask) { if (dr) ZOO_ATTN_FWD(4, true, true); else ZOO_ATTN_FWD(4, true, false); }
+    else { if (dr) ZOO_ATTN_FWD(4, false, true); else ZOO_ATTN_FWD(4, false, false); }
   }
+#undef ZOO_ATTN_FWD
+}
+
+static AttnDrop make_drop(float p, uint64_t seed) {
+  AttnDrop d;
+  d.thresh = p <= 0.f ? 0u : (p >= 1.f ? 0xFFFFFFFFu : (uint32_t)((double)p * 4294967296.0));
+  if (p > 0.f && d.thresh == 0u) d.thresh = 1u;
+  d.scale = p >= 1.f ? 0.f : 1.f / (1.f - p);
+  d.s0 = (uint32_t)seed;
+  d.s1 = (uint32_t)(seed >> 32);
+  return d;
 }
 
 // strides: 12 element strides (q, k, v, o) x (batch, head, row); nullptr = contiguous [B,H,T,D]
 extern "C" hipError_t zoo_attn_fwd(const void* q, const void* k, const void* v, const float* mask, void* o,
                                    float* lse, int B, int H, int L, int S, int D, float scale, int causal,
-                                   const long* strides, hipStream_t st) {
+                                   const long* strides, float pdrop, uint64_t seed, hipStream_t st) {
+  const AttnDrop dd = make_drop(pdrop, seed);
   AttnStrides sd;
   if (strides) {
     sd = AttnStrides{strides[0], strides[1], strides[2], strides[3], strides[4], strides[5],
@@ -717,61 +777,76 @@ extern "C" hipError_t zoo_attn_fwd(const void* q, const void* k, const void* v, 
                      (long)H * S * D, (long)S * D, D, (long)H * L * D, (long)L * D, D};
   }
   if (D == 64)
-    launch_fwd_d<64>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    launch_fwd_d<64>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, dd, st);
   else if (D == 128)
-    launch_fwd_d<128>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, st);
+    launch_fwd_d<128>(q, k, v, mask, o, lse, B, H, L, S, scale, causal, sd, dd, st);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-template <int D, bool HM, int QW, int NWQ>
+template <int D, bool HM, bool DR, int QW, int NWQ>
 static void launch_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
                        const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int H, int L, int S,
-                       float scale, int causal, hipStream_t st) {
+                       float scale, int causal, const AttnBwdStrides& sd, const AttnDrop& dd, hipStream_t st) {
   static const bool lds_ok_ = [] {
-    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D, QW, HM>),
+    hipError_t e1 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dkdv_kernel<D, QW, HM, DR>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
-    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D, NWQ, HM>),
+    hipError_t e2 = hipFuncSetAttribute(reinterpret_cast<const void*>(&attn_bwd_dq_kernel<D, NWQ, HM, DR>),
                                         hipFuncAttributeMaxDynamicSharedMemorySize, 96 * 1024);
     return e1 == hipSuccess && e2 == hipSuccess;
   }();
   (void)lds_ok_;
   const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 4 * 64 * sizeof(float);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM>), dim3((S + 127) / 128, B * H), dim3(256 * QW), smem, st,
+  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM, DR>), dim3((S + 127) / 128, B * H), dim3(256 * QW), smem, st,
                      (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                     (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal);
-  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NWQ, HM>), dim3((L + 32 * NWQ - 1) / (32 * NWQ), B * H),
+                     (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal, sd, dd);
+  hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NWQ, HM, DR>), dim3((L + 32 * NWQ - 1) / (32 * NWQ), B * H),
                      dim3(64 * NWQ), smem, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask,
-                     (const bf16_t*)dout, lse, delta, (bf16_t*)dq, H, L, S, scale, causal);
+                     (const bf16_t*)dout, lse, delta, (bf16_t*)dq, H, L, S, scale, causal, sd, dd);
 }
 
 template <int D>
 static void launch_bwd_d(const void* dout, const void* q, const void* k, const void* v, const float* mask,
                          const float* lse, const float* delta, void* dq, void* dk, void* dv, int B, int H, int L,
-                         int S, float scale, int causal, hipStream_t st) {
+                         int S, float scale, int causal, const AttnBwdStrides& sd, const AttnDrop& dd,
+                         hipStream_t st) {
   // D = 64 fits two waves per SIMD (8-wave blocks); D = 128 keeps one wave per
   // SIMD with the accumulators in AGPRs (the 8-wave form would spill)
   constexpr int QW = D == 64 ? 2 : 1, NWQ = D == 64 ? 8 : 4;
-  if (mask)
-    launch_bwd<D, true, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
-  else
-    launch_bwd<D, false, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+#define ZOO_ATTN_BWD(HM_, DR_) \
+  launch_bwd<D, HM_, DR_, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, sd, dd, st)
+  const bool dr = dd.thresh != 0u;
+  if (mask) { if (dr) ZOO_ATTN_BWD(true, true); else ZOO_ATTN_BWD(true, false); }
+  else { if (dr) ZOO_ATTN_BWD(false, true); else ZOO_ATTN_BWD(false, false); }
+#undef ZOO_ATTN_BWD
 }
 
+// strides: 24 element strides (q, k, v, dO, O, dQ, dK, dV) x (batch, head, row); nullptr = contiguous
 extern "C" hipError_t zoo_attn_bwd(const void* dout, const void* q, const void* k, const void* v, const float* mask,
                                    const void* o, const float* lse, float* delta, void* dq, void* dk, void* dv, int B,
-                                   int H, int L, int S, int D, float scale, int causal, hipStream_t st) {
+                                   int H, int L, int S, int D, float scale, int causal, const long* strides,
+                                   float pdrop, uint64_t seed, hipStream_t st) {
+  const AttnDrop dd = make_drop(pdrop, seed);
+  AttnBwdStrides sd;
+  if (strides) {
+    long* f = &sd.qb;
+    for (int i = 0; i < 24; ++i) f[i] = strides[i];
+  } else {
+    const long lq[3] = {(long)H * L * D, (long)L * D, D}, lk[3] = {(long)H * S * D, (long)S * D, D};
+    sd = AttnBwdStrides{lq[0], lq[1], lq[2], lk[0], lk[1], lk[2], lk[0], lk[1], lk[2], lq[0], lq[1], lq[2],
+                        lq[0], lq[1], lq[2], lq[0], lq[1], lq[2], lk[0], lk[1], lk[2], lk[0], lk[1], lk[2]};
+  }
   const int rows = B * H * L;
   const int dblocks = (rows * (D / 8) + 255) / 256;
   if (D == 64) {
     hipLaunchKernelGGL(attn_delta_kernel<64>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
-                       (const bf16_t*)o, delta, rows);
-    launch_bwd_d<64>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+                       (const bf16_t*)o, delta, rows, H, L, sd);
+    launch_bwd_d<64>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, sd, dd, st);
   } else if (D == 128) {
     hipLaunchKernelGGL(attn_delta_kernel<128>, dim3(dblocks), dim3(256), 0, st, (const bf16_t*)dout,
-                       (const bf16_t*)o, delta, rows);
-    launch_bwd_d<128>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, st);
+                       (const bf16_t*)o, delta, rows, H, L, sd);
+    launch_bwd_d<128>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, sd, dd, st);
   } else {
     return hipErrorInvalidValue;
   }

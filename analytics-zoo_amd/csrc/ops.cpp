@@ -84,7 +84,7 @@ hipError_t zoo_im2col_q8(const void*, int, const float*, void*, int, int, int, i
 hipError_t zoo_qgemm(const void*, const void*, const float*, const float*, const float*, const void*, void*, int, int,
                      int, int, int, hipStream_t);
 hipError_t zoo_attn_fwd(const void*, const void*, const void*, const float*, void*, float*, int, int, int, int, int,
-                        float, int, const long*, hipStream_t);
+                        float, int, const long*, float, uint64_t, hipStream_t);
 hipError_t zoo_rnn(const zoo::RnnArgs*, int, int, int, hipStream_t);
 hipError_t zoo_nms_mask(const float*, int, float, unsigned long long*, hipStream_t);
 hipError_t zoo_embedding_bag_fwd(const float*, const int64_t*, const int64_t*, int, const float*, float*, float*, int,
@@ -105,7 +105,8 @@ hipError_t zoo_loss(const void*, const void*, void*, float*, size_t, int, int, f
 hipError_t zoo_auc_hist(const float*, const float*, float*, size_t, int, float, float, hipStream_t);
 hipError_t zoo_box_decode(const float*, const float*, float*, int, int, float, float, int, hipStream_t);
 hipError_t zoo_attn_bwd(const void*, const void*, const void*, const void*, const float*, const void*, const float*,
-                        float*, void*, void*, void*, int, int, int, int, int, float, int, hipStream_t);
+                        float*, void*, void*, void*, int, int, int, int, int, float, int, const long*, float, uint64_t,
+                        hipStream_t);
 }
 
 namespace {
@@ -1350,7 +1351,8 @@ void attn_check(const torch::Tensor& q, const torch::Tensor& k, const torch::Ten
 }
 
 std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Tensor v,
-                                    c10::optional<torch::Tensor> mask, bool causal) {
+                                    c10::optional<torch::Tensor> mask, bool causal, double pdrop, int64_t seed) {
+  TORCH_CHECK(pdrop >= 0.0 && pdrop < 1.0, "attn_fwd: dropout p must be in [0, 1)");
   attn_check(q, k, v, mask);
   const int B = q.size(0), H = q.size(1), L = q.size(2), S = k.size(2), D = q.size(3);
   auto o = torch::empty_like(q);
@@ -1358,7 +1360,7 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
   if (q.numel() == 0) return {o, lse};
   check_hip(zoo_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask), o.data_ptr(),
                          lse.data_ptr<float>(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal,
-                         nullptr, cur_stream()),
+                         nullptr, (float)pdrop, (uint64_t)seed, cur_stream()),
             "attn_fwd");
   return {o, lse};
 }
@@ -1367,7 +1369,9 @@ std::vector<torch::Tensor> attn_fwd(torch::Tensor q, torch::Tensor k, torch::Ten
 // q/k/v slices of one packed [B, T, 3, H, D] projection, so no per-head copies are made. With
 // out_blhd the output is written as [B, L, H, D] (the layout the output projection reads).
 std::vector<torch::Tensor> attn_fwd_strided(torch::Tensor q, torch::Tensor k, torch::Tensor v,
-                                            c10::optional<torch::Tensor> mask, bool causal, bool out_blhd) {
+                                            c10::optional<torch::Tensor> mask, bool causal, bool out_blhd,
+                                            double pdrop, int64_t seed) {
+  TORCH_CHECK(pdrop >= 0.0 && pdrop < 1.0, "attn_fwd_strided: dropout p must be in [0, 1)");
   for (const torch::Tensor* t : {&q, &k, &v}) {
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "attention: q/k/v must be bf16 GPU tensors");
     TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1, "attention: head_dim must be the contiguous dim");
@@ -1394,14 +1398,15 @@ std::vector<torch::Tensor> attn_fwd_strided(torch::Tensor q, torch::Tensor k, to
                        (long)(out_blhd ? o.stride(1) : o.stride(2))};
   check_hip(zoo_attn_fwd(q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask), o.data_ptr(),
                          lse.data_ptr<float>(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, st,
-                         cur_stream()),
+                         (float)pdrop, (uint64_t)seed, cur_stream()),
             "attn_fwd_strided");
   return {o, lse};
 }
 
 std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
                                     c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor lse,
-                                    bool causal) {
+                                    bool causal, double pdrop, int64_t seed) {
+  TORCH_CHECK(pdrop >= 0.0 && pdrop < 1.0, "attn_bwd: dropout p must be in [0, 1)");
   attn_check(q, k, v, mask);
   req(dout, at::kBFloat16, "dout");
   req(o, at::kBFloat16, "o");
@@ -1416,9 +1421,51 @@ std::vector<torch::Tensor> attn_bwd(torch::Tensor dout, torch::Tensor q, torch::
   if (q.numel() == 0 || k.numel() == 0) return {dq.zero_(), dk.zero_(), dv.zero_()};
   check_hip(zoo_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask),
                          o.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
-                         dv.data_ptr(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, cur_stream()),
+                         dv.data_ptr(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, nullptr,
+                         (float)pdrop, (uint64_t)seed, cur_stream()),
             "attn_bwd");
   return {dq, dk, dv};
+}
+
+// Backward on strided [B, H, T, D] views (the training counterpart of attn_fwd_strided): q/k/v
+// are slices of the packed projection, dout/o any [B, H, L, D] views, and dq/dk/dv are written
+// into caller-provided views (slices of the packed projection's gradient).
+void attn_bwd_strided(torch::Tensor dout, torch::Tensor q, torch::Tensor k, torch::Tensor v,
+                      c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor lse, torch::Tensor dq,
+                      torch::Tensor dk, torch::Tensor dv, bool causal, double pdrop, int64_t seed) {
+  TORCH_CHECK(pdrop >= 0.0 && pdrop < 1.0, "attn_bwd_strided: dropout p must be in [0, 1)");
+  for (const torch::Tensor* t : {&dout, &q, &k, &v, &o, &dq, &dk, &dv}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "attn_bwd_strided: bf16 GPU tensors");
+    TORCH_CHECK(t->dim() == 4 && t->stride(3) == 1, "attn_bwd_strided: head_dim must be the contiguous dim");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0 && t->stride(2) % 8 == 0 &&
+                    t->stride(1) % 8 == 0 && t->stride(0) % 8 == 0,
+                "attn_bwd_strided: rows must be 16-byte aligned");
+  }
+  const int B = q.size(0), H = q.size(1), L = q.size(2), S = k.size(2), D = q.size(3);
+  TORCH_CHECK(D == 64 || D == 128, "attention: head_dim must be 64 or 128");
+  TORCH_CHECK(B * H < 65536, "attention: B*H must be < 65536");
+  TORCH_CHECK(k.sizes() == v.sizes() && dk.sizes() == k.sizes() && dv.sizes() == k.sizes(),
+              "attn_bwd_strided: k/v/dk/dv shapes differ");
+  TORCH_CHECK(dout.sizes() == q.sizes() && o.sizes() == q.sizes() && dq.sizes() == q.sizes(),
+              "attn_bwd_strided: dout/o/dq shape");
+  TORCH_CHECK(k.size(0) == B && k.size(1) == H && k.size(3) == D, "attn_bwd_strided: q/k batch, heads or dim");
+  req(lse, at::kFloat, "lse");
+  TORCH_CHECK(lse.is_contiguous() && lse.numel() == (int64_t)B * H * L, "attn_bwd_strided: lse shape");
+  if (mask.has_value() && mask->defined()) {
+    req(*mask, at::kFloat, "mask");
+    TORCH_CHECK(mask->dim() == 2 && mask->size(0) == B && mask->size(1) == S, "attention: mask must be [B, S]");
+  }
+  if (q.numel() == 0 || k.numel() == 0) return;
+  auto delta = torch::empty({B, H, L}, q.options().dtype(at::kFloat));
+  long st[24];
+  int n = 0;
+  for (const torch::Tensor* t : {&q, &k, &v, &dout, &o, &dq, &dk, &dv})
+    for (int d = 0; d < 3; ++d) st[n++] = (long)t->stride(d);
+  check_hip(zoo_attn_bwd(dout.data_ptr(), q.data_ptr(), k.data_ptr(), v.data_ptr(), opt_ptr<float>(mask),
+                         o.data_ptr(), lse.data_ptr<float>(), delta.data_ptr<float>(), dq.data_ptr(), dk.data_ptr(),
+                         dv.data_ptr(), B, H, L, S, D, (float)(1.0 / std::sqrt((double)D)), causal, st,
+                         (float)pdrop, (uint64_t)seed, cur_stream()),
+            "attn_bwd_strided");
 }
 
 
@@ -1644,15 +1691,19 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("causal"),
+        py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("nms_sorted", &nms_sorted);
   m.def("nchw_to_s2d", &nchw_to_s2d);
   m.def("dropout_add", &dropout_add, py::arg("a"), py::arg("x") = py::none(), py::arg("p"), py::arg("seed"));
-  m.def("attn_fwd_strided", &attn_fwd_strided);
+  m.def("attn_fwd_strided", &attn_fwd_strided, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"),
+        py::arg("causal"), py::arg("out_blhd"), py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("absmax", &absmax);
   m.def("im2col_q8", &im2col_q8);
   m.def("qgemm", &qgemm);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"),
+        py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("pdrop") = 0.0, py::arg("seed") = 0);
+  m.def("attn_bwd_strided", &attn_bwd_strided);
   m.def("rnn_fwd", &rnn_fwd);
   m.def("rnn_bwd", &rnn_bwd);
 }

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Linear-layer weight gradient dW[N, K] (fp32) += dy[M, N]^T x[M, K] (bf16) at BERT-base
+b128 x s128 shapes: hipBLASLt (fp32-out addmm beta=1, and bf16-out mm + add) vs the zoo
+split-K wgrad kernel (csrc/kernels/wgrad.hip run as a 1x1 conv).
+
+  python analytics-zoo_amd/tools/wgrad_bench.py [--m 16384]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+import zoo._C as C  # noqa: E402
+
+
+def timeit(fn, iters=20):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--m", type=int, default=16384)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    M = a.m
+    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+        dy = (torch.randn(M, N, device=dev) * 0.1).bfloat16()
+        x = torch.randn(M, K, device=dev).bfloat16()
+        ref = dy.double().t() @ x.double()
+        g = torch.zeros(N, K, device=dev)
+        res = {"M": M, "N": N, "K": K}
+        flop = 2.0 * M * N * K
+
+        def lt_f32():
+            torch.ops.aten.addmm.dtype_out(g, dy.t(), x, torch.float32, beta=1, alpha=1, out=g)
+
+        def lt_bf16():
+            g.add_(torch.mm(dy.t(), x))
+
+        def zoo():
+            C.conv_wgrad(x.view(M, 1, 1, K), dy.view(M, 1, 1, N), g, 1, 1, 1, 1, 0, 0, 1, 1)
+
+        for name, fn in (("hipblaslt_f32out", lt_f32), ("hipblaslt_bf16out_add", lt_bf16), ("zoo_wgrad", zoo)):
+            g.zero_()
+            fn()
+            torch.cuda.synchronize()
+            err = ((g.double() - ref).norm() / ref.norm()).item()
+            t = timeit(fn)
+            res[name] = {"us": round(t * 1e6, 1), "tflops": round(flop / t / 1e12, 1), "rel_err": float("%.2e" % err)}
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -54,9 +54,8 @@ class _Block(nn.Module):
         B, L, H = x.shape
         nh, hd = self.n_head, H // self.n_head
         qkv = ops.linear(x, self.qkv_w, self.qkv_b)                   # [B, L, 3H]
-        a = None
-        if not (self.training and self.attn_drop > 0):
-            a = attention_packed(qkv, nh, mask=mask, causal=causal)     # strided, no head copies
+        # strided fused kernels (attention-probability dropout in-kernel), no head copies
+        a = attention_packed(qkv, nh, mask=mask, causal=causal, dropout_p=self.attn_drop, training=self.training)
         if a is None:
             qkv = qkv.reshape(B, L, 3, nh, hd).permute(2, 0, 3, 1, 4)  # [3, B, nh, L, hd]
             a = ops.attention(qkv[0], qkv[1], qkv[2], mask=mask, causal=causal, dropout_p=self.attn_drop,

@@ -104,3 +104,98 @@ def test_attention_packed_strided_matches_reference(hd, causal):
     ref = ref.transpose(1, 2).reshape(B, L, H * hd)
     err = (out.float() - ref).abs().max() / ref.abs().max()
     assert err < 2e-2, err
+
+
+def _keep_ref(BH, L, S, p, seed):
+    """numpy model of the kernel's dropout hash (attention.hip attn_keep): keep-factor [BH, L, S]."""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFF)
+
+    def fmix(h):
+        h = h ^ (h >> np.uint64(16))
+        h = (h * np.uint64(0x85EBCA6B)) & M
+        h = h ^ (h >> np.uint64(13))
+        h = (h * np.uint64(0xC2B2AE35)) & M
+        return h ^ (h >> np.uint64(16))
+
+    s0, s1 = np.uint64(seed & 0xFFFFFFFF), np.uint64(seed >> 32)
+    bh = np.arange(BH, dtype=np.uint64)[:, None, None]
+    q = np.arange(L, dtype=np.uint64)[None, :, None]
+    key = np.arange(S, dtype=np.uint64)[None, None, :]
+    a = fmix(((bh * np.uint64(0x9E3779B1)) & M) ^ s1)
+    h = fmix(((((q * np.uint64(0x85EBCA77)) & M) + key) & M) ^ s0 ^ a)
+    thresh = np.uint64(int(p * 4294967296.0))
+    return torch.from_numpy((h >= thresh).astype(np.float32) / (1.0 - p))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,causal,masked,p", [(64, False, True, 0.1), (64, True, False, 0.5), (128, False, True, 0.1)])
+def test_fused_attention_dropout_matches_masked_reference(D, causal, masked, p):
+    """In-kernel attention-probability dropout: forward and both backward passes regenerate
+    the same counter-hash mask; checked against fp32 autograd through softmax * keep @ V."""
+    from zoo.ops._native import native
+    dev = torch.device("cuda:0")
+    torch.manual_seed(3)
+    B, H, L, S = 2, 2, 160, 192
+    seed = 0x1234_5678_9ABC
+    q = torch.randn(B, H, L, D, device=dev).bfloat16()
+    k = torch.randn(B, H, S, D, device=dev).bfloat16()
+    v = torch.randn(B, H, S, D, device=dev).bfloat16()
+    mask = None
+    if masked:
+        mask = torch.zeros(B, S, device=dev)
+        mask[1, S - 50:] = -10000.0
+    keep = _keep_ref(B * H, L, S, p, seed).view(B, H, L, S).to(dev)
+    assert abs(float((keep > 0).float().mean()) - (1 - p)) < 0.01
+    o, lse = native().attn_fwd(q, k, v, mask, causal, p, seed)
+    qr, kr, vr = (t.float().requires_grad_(True) for t in (q, k, v))
+    w = qr @ kr.transpose(-1, -2) / math.sqrt(D)
+    if causal:
+        w = w.masked_fill(~torch.ones(L, S, dtype=torch.bool, device=dev).tril(S - L), float("-inf"))
+    if mask is not None:
+        w = w + mask[:, None, None, :]
+    ref = (torch.softmax(w, -1) * keep) @ vr
+    err = (o.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    dq, dk, dv = native().attn_bwd(g.bfloat16(), q, k, v, mask, o, lse, causal, p, seed)
+    for name, a, b in (("dq", dq, qr.grad), ("dk", dk, kr.grad), ("dv", dv, vr.grad)):
+        rel = (a.float() - b).norm().item() / max(b.norm().item(), 1e-6)
+        assert rel < 2e-2, (name, rel)
+    # a different seed gives a different output
+    o2, _ = native().attn_fwd(q, k, v, mask, causal, p, seed + 1)
+    assert (o2.float() - o.float()).abs().max().item() > 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hd,p", [(64, 0.0), (64, 0.1), (128, 0.1)])
+def test_attention_packed_training_grads(hd, p, monkeypatch):
+    """Packed training path: strided forward + strided backward writing the packed
+    [B, L, 3*H*hd] gradient, vs fp32 autograd of the per-head reference (same dropout mask)."""
+    import importlib
+    A = importlib.import_module("zoo.ops.attention")   # (zoo.ops.attention the attribute is the function)
+    seed = 987654321
+    monkeypatch.setattr(A, "_seed", lambda: seed)
+    torch.manual_seed(4)
+    B, L, H = 2, 136, 4
+    dev = torch.device("cuda")
+    qkv = (torch.randn(B, L, 3 * H * hd, device=dev) * 0.5).bfloat16().requires_grad_(True)
+    mask = torch.zeros(B, L, device=dev)
+    mask[0, 100:] = -10000.0
+    out = A.attention_packed(qkv, H, mask=mask, causal=False, dropout_p=p, training=True)
+    assert out is not None and out.shape == (B, L, H * hd)
+    ref_in = qkv.detach().float().requires_grad_(True)
+    v5 = ref_in.view(B, L, 3, H, hd).permute(2, 0, 3, 1, 4)
+    w = v5[0] @ v5[1].transpose(-1, -2) / math.sqrt(hd) + mask[:, None, None, :]
+    pr = torch.softmax(w, -1)
+    if p > 0:
+        pr = pr * _keep_ref(B * H, L, L, p, seed).view(B, H, L, L).to(dev)
+    ref = (pr @ v5[2]).transpose(1, 2).reshape(B, L, H * hd)
+    err = (out.float() - ref).abs().max().item() / ref.abs().max().item()
+    assert err < 2e-2, err
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    out.backward(g.bfloat16())
+    rel = (qkv.grad.float() - ref_in.grad).norm().item() / ref_in.grad.norm().item()
+    assert rel < 2e-2, rel
