@@ -318,6 +318,8 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
 // bias gradient sum(dy) per channel accumulated, in ONE pass (replaces a compare, a multiply,
 // a cast and a reduction launch). Z == null: no mask (bias only). Same row layout and
 // per-row-lane LDS fold as bn_reduce_kernel; out = [C] fp32 (+= per block) or partials.
+// ACT 1: dY = dZ * [Z > 0] (ReLU, Z = output); ACT 2: dY = dZ * gelu'(Z) (erf GELU, Z = pre-activation)
+template <int ACT>
 __global__ __launch_bounds__(256) void act_bwd_reduce_kernel(const bf16_t* __restrict__ dZ,
                                                             const bf16_t* __restrict__ Z, bf16_t* __restrict__ dY,
                                                             float* __restrict__ out, int M, int C,
@@ -342,8 +344,16 @@ __global__ __launch_bounds__(256) void act_bwd_reduce_kernel(const bf16_t* __res
         if (Z) {
           float z[8];
           unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
+          if (ACT == 2) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+            for (int e = 0; e < 8; ++e) {
+              const float x = z[e];
+              a[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+          }
           *reinterpret_cast<uint4*>(dY + off) = pack8(a);
           unpack8(*reinterpret_cast<const uint4*>(dY + off), a);  // sum what is stored (bf16)
         }
@@ -526,13 +536,17 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
 // dY = dZ * [Z > 0] (Z non-null) and out[c] += sum_rows dY (out non-null; partial: out is
 // [blocks][C] partials for an ordered fold by the caller). Returns the block count.
 extern "C" int zoo_act_bwd_reduce(const void* dZ, const void* Z, void* dY, float* out, int M, int C, int partial,
-                                  hipStream_t st) {
+                                  int gelu, hipStream_t st) {
   int blocks, rpb;
   bn_reduce_grid(M, C, &blocks, &rpb);
   const int cpr = C >> 3;
   const int row_step = 256 / (cpr < 256 ? cpr : 256);
   const size_t smem = (size_t)row_step * C * sizeof(float);
-  hipLaunchKernelGGL(act_bwd_reduce_kernel, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ, (const bf16_t*)Z,
-                     (bf16_t*)dY, out, M, C, rpb, partial);
+  if (gelu)
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<2>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ,
+                       (const bf16_t*)Z, (bf16_t*)dY, out, M, C, rpb, partial);
+  else
+    hipLaunchKernelGGL(act_bwd_reduce_kernel<1>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ,
+                       (const bf16_t*)Z, (bf16_t*)dY, out, M, C, rpb, partial);
   return blocks;
 }

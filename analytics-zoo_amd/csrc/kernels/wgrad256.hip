@@ -1,0 +1,336 @@
+// Linear / 1x1-conv weight gradient on CDNA4 matrix cores (gfx950), large-tile form:
+//
+//   dW[n][k] (fp32, row stride ldw) += sum_m dY[m][n] * X[m][k]      dY [M, N], X [M, K] bf16
+//
+// Both operands are m-major (the reduction runs down their rows), so neither is
+// K-contiguous per lane as the MFMA operand maps want. The tiles are staged into LDS
+// as-is with LDS-DMA (global_load_lds, 16 B per lane, no VGPRs) and read back with the
+// hardware transposing read ds_read_b64_tr_b16 (cdna_hip_programming.md T10): two 4x16
+// transposed reads give a lane the 8 consecutive-m values of its v_mfma_f32_16x16x32_bf16
+// operand fragment.
+//
+// Structure (the schedule of gemm256.hip, i.e. cdna_hip_programming.md §5 "256² 8-phase"):
+//   * 256 (n) x 256 (k) output tile, 64-row m-steps, 8 waves as 2 (n) x 4 (k); each wave
+//     owns 128 x 64 outputs = 8 x 4 tiles of 16x16 (128 accumulator registers).
+//   * each m-step is four 16 KiB half-tiles (A = dY halves by the waves' upper / lower
+//     64-row quadrant, B = X halves by their left / right 32-column quadrant), staged one
+//     per phase 5-6 phases ahead; counted `s_waitcnt vmcnt(8)` + one raw s_barrier per
+//     phase, never a drain inside the loop.
+//   * LDS image of a half-tile: blocks of [8 m-rows][16 columns] (256 B, rows 32 B apart);
+//     the 8-row blocks of odd m-block index store their rows 0-3 <-> 4-7 swapped, so the
+//     two 16-lane groups of a half-wave (m-blocks 2g, 2g+1) read opposite 128-byte halves
+//     of the bank row: conflict-free. The swizzle is applied through the per-lane DMA
+//     SOURCE row (the DMA image is lane-linear).
+//   * the reduction (M up to 10^6 for ResNet stage 1, 16384 for BERT) is split over
+//     workgroups so ~one wave of 256 workgroups fills the chip; each split stores its
+//     fp32 tile in MFMA-fragment order (1 KiB fully coalesced per wave store) and an
+//     ordered fold kernel sums the splits into dW (deterministic, no atomics). A single
+//     split accumulates straight into dW.
+//
+// Reference parity: the weight-gradient half of BigDL Linear / SpatialConvolution
+// accGradParameters, as wgrad.hip.
+#include "common.h"
+#include "geom.h"
+
+namespace zoo {
+
+typedef __attribute__((address_space(3))) void w2_lds_void;
+typedef __attribute__((address_space(1))) const void w2_gl_void;
+typedef __attribute__((address_space(3))) i16x4 w2_lds_i16x4;
+
+constexpr int W2_T = 256, W2_BM = 64, W2_NT = 512, W2_HALF = 16384;
+
+ZOO_DEV void w2_vm8() { asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); }
+ZOO_DEV void w2_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+ZOO_DEV void w2_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+struct W2Geom {
+  int M, N, K;        // reduction rows, dY columns (dW rows), X columns (dW cols)
+  int ldy, ldx, ldw;  // leading dims (elements); ldy, ldx % 8 == 0
+  int m_per_split, splits, tiles_n, tiles_k;
+};
+
+// one fragment = two transposed 4-row reads of an 8-row block (rows 0-3 -> elements 0-3)
+ZOO_DEV bf16x8 w2_frag(const char* blk, int lo_off, int hi_off) {
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w2_lds_i16x4*)(blk + lo_off));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w2_lds_i16x4*)(blk + hi_off));
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  i16x8 v;
+  v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+  v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+__global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __restrict__ dY,
+                                                            const bf16_t* __restrict__ X, float* __restrict__ dW,
+                                                            float* __restrict__ part, W2Geom g,
+                                                            const bf16_t* __restrict__ zpage) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+
+  const int tiles = g.tiles_n * g.tiles_k;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int split = bid / tiles, tile = bid - split * tiles;
+  const int n0 = (tile / g.tiles_k) * W2_T, k0 = (tile % g.tiles_k) * W2_T;
+  const int ms = split * g.m_per_split;
+  const int me = min(g.M, ms + g.m_per_split);
+  const int nk = (me - ms + W2_BM - 1) / W2_BM;
+
+  // ---- per-lane DMA source (lane-linear 1 KiB per wave instruction) ----
+  const int slot = (lane >> 1) & 7, c8 = (lane & 1) * 8;
+  // A (dY) half h, instruction j: LDS block (q = j, mb = w): [nb16 = lane>>4][slot][16]
+  const int a_mb = w;
+  const int a_row = a_mb * 8 + (slot ^ ((a_mb & 1) << 2));
+  int a_col[2][2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) a_col[h][j] = n0 + j * 128 + h * 64 + (lane >> 4) * 16 + c8;
+  // B (X) half h, instruction j: idx = j*8 + w -> wn' = idx>>2, m-block pair mbp = idx&3;
+  // [mb = 2 mbp + (lane>>5)][nb16 = (lane>>4)&1][slot][16]
+  int b_row[2], b_col[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int idx = j * 8 + w, mb = 2 * (idx & 3) + (lane >> 5);
+    b_row[j] = mb * 8 + (slot ^ ((mb & 1) << 2));
+#pragma unroll
+    for (int h = 0; h < 2; ++h) b_col[h][j] = k0 + (idx >> 2) * 64 + h * 32 + ((lane >> 4) & 1) * 16 + c8;
+  }
+
+  auto half_base = [&](int buf, int op, int h) -> char* {
+    return smem + (((buf * 2 + op) * 2 + h) * W2_HALF);
+  };
+
+  auto stage = [&](int kt, int op, int h) {
+    char* hb = half_base(kt & 1, op, h);
+    const int mrow0 = ms + kt * W2_BM;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const bf16_t* src;
+      if (op == 0) {
+        const int m = mrow0 + a_row, n = a_col[h][j];
+        src = (m < me && n < g.N) ? dY + (size_t)m * g.ldy + n : zpage;
+      } else {
+        const int m = mrow0 + b_row[j], k = b_col[h][j];
+        src = (m < me && k < g.K) ? X + (size_t)m * g.ldx + k : zpage;
+      }
+      __builtin_amdgcn_global_load_lds((w2_gl_void*)src, (w2_lds_void*)(hb + (j * 8 + w) * 1024), 16, 0, 0);
+    }
+  };
+
+  // ---- transposed fragment reads ----
+  // lane: group gq = lane>>4 takes m rows 8gq..8gq+7 of a 32-row k-step (= m-block 4kb+gq);
+  // inside the group lane 4tq+tp addresses row tq (and 4+tq) columns 4tp..4tp+3
+  const int gq = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+  const int sw = (gq & 1) << 2;  // odd m-blocks store rows 0-3 <-> 4-7 swapped
+  const int lo_off = ((tq ^ sw) * 32) + tp * 8, hi_off = (((4 + tq) ^ sw) * 32) + tp * 8;
+  // A frag (half h, wave row wm, 16-col block i, k-step kb): block wm*8 + 4kb+gq, column block i
+  auto read_a = [&](int buf, int h, int i, int kb) -> bf16x8 {
+    const char* blk = half_base(buf, 0, h) + (wm * 8 + 4 * kb + gq) * 1024 + i * 256;
+    return w2_frag(blk, lo_off, hi_off);
+  };
+  // B frag (half h, wave col wn, 16-col block j, k-step kb)
+  auto read_b = [&](int buf, int h, int j, int kb) -> bf16x8 {
+    const char* blk = half_base(buf, 1, h) + wn * 4096 + (4 * kb + gq) * 512 + j * 256;
+    return w2_frag(blk, lo_off, hi_off);
+  };
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  bf16x8 fa[4][2], fb0[2][2], fb1[2][2];
+
+  if (nk > 0) {
+    stage(0, 0, 0);
+    stage(0, 1, 0);
+    stage(0, 1, 1);
+    stage(0, 0, 1);
+    if (nk > 1) {
+      stage(1, 0, 0);
+      stage(1, 1, 0);
+      w2_vm8();
+    } else {
+      w2_vm0();
+    }
+  }
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) fa[i][kb] = read_a(buf, 0, i, kb);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) fb0[j][kb] = read_b(buf, 0, j, kb);
+      } else if (p == 1) {
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) fb1[j][kb] = read_b(buf, 1, j, kb);
+      } else if (p == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) fa[i][kb] = read_a(buf, 1, i, kb);
+      }
+      // stage one half-tile: P0 -> B1(kt+1), P1 -> A1(kt+1), P2 -> A0(kt+2), P3 -> B0(kt+2)
+      const int skt = p < 2 ? kt + 1 : kt + 2;
+      const bool valid = skt < nk;
+      if (valid) stage(skt, p == 1 || p == 2 ? 0 : 1, p == 0 || p == 1 ? 1 : 0);
+      if (valid) w2_vm8(); else w2_vm0();
+      __builtin_amdgcn_s_barrier();
+      w2_lgkm0();
+      const int qa = p >= 2 ? 1 : 0;
+      const int qb = (p == 1 || p == 2) ? 1 : 0;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qa][qb][i][j] = mfma16(fa[i][kb], qb ? fb1[j][kb] : fb0[j][kb], acc[qa][qb][i][j]);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+
+  // ---- epilogue ----
+  // fragment (qa, qb, i, j) reg r <-> dW row n0 + wm*128 + qa*64 + i*16 + 4*(lane>>4) + r,
+  //                                   col k0 + wn*64 + qb*32 + j*16 + (lane&15)
+  if (part) {
+    // fragment order: [split][tile][wave][qa][qb][i][j][lane] float4
+    f32x4* dst = reinterpret_cast<f32x4*>(part) + ((size_t)(split * tiles + tile) * 8 + w) * 32 * 64 + lane;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) dst[(((qa * 2 + qb) * 4 + i) * 2 + j) * 64] = acc[qa][qb][i][j];
+  } else {
+    const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+    for (int qa = 0; qa < 2; ++qa)
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const int col = k0 + wn * 64 + qb * 32 + j * 16 + fr;
+            const int row = n0 + wm * 128 + qa * 64 + i * 16 + fq * 4;
+            if (col < g.K) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (row + r < g.N) dW[(size_t)(row + r) * g.ldw + col] += acc[qa][qb][i][j][r];
+            }
+          }
+  }
+}
+
+// Ordered fold of the split partials into dW: thread = one fragment lane (float4) of one
+// tile; sums splits 0..S-1 in order, then adds its 4 rows x 1 column into dW.
+__global__ __launch_bounds__(256) void wgrad256_fold_kernel(const float* __restrict__ part, float* __restrict__ dW,
+                                                           W2Geom g) {
+  const int tiles = g.tiles_n * g.tiles_k;
+  const size_t per_tile = (size_t)8 * 32 * 64;  // float4 slots per tile
+  const size_t total = per_tile * tiles;
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= total) return;
+  const f32x4* p = reinterpret_cast<const f32x4*>(part) + idx;
+  f32x4 s = p[0];
+  for (int sp = 1; sp < g.splits; ++sp) s += p[(size_t)sp * total];
+  const int tile = (int)(idx / per_tile);
+  const int rem = (int)(idx - (size_t)tile * per_tile);
+  const int w = rem >> 11, f = (rem >> 6) & 31, lane = rem & 63;
+  const int j = f & 1, i = (f >> 1) & 3, qb = (f >> 3) & 1, qa = f >> 4;
+  const int wm = w >> 2, wn = w & 3;
+  const int n0 = (tile / g.tiles_k) * W2_T, k0 = (tile % g.tiles_k) * W2_T;
+  const int col = k0 + wn * 64 + qb * 32 + j * 16 + (lane & 15);
+  const int row = n0 + wm * 128 + qa * 64 + i * 16 + (lane >> 4) * 4;
+  if (col >= g.K) return;
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    if (row + r < g.N) dW[(size_t)(row + r) * g.ldw + col] += s[r];
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+static const bf16_t* w2_zero_page() {
+  static bf16_t* z = nullptr;
+  if (!z) {
+    hipMalloc(&z, 4096);
+    hipMemset(z, 0, 4096);
+  }
+  return z;
+}
+
+// split plan: ~one workgroup per CU (256), >= 4 m-steps per split. Returns the number of
+// splits and fills m_per_split; the caller provides part (splits * tiles * 256 KiB) when > 1.
+extern "C" int zoo_wgrad256_plan(int M, int N, int K, int* m_per_split) {
+  const int tiles = ((N + W2_T - 1) / W2_T) * ((K + W2_T - 1) / W2_T);
+  static const int target = [] {
+    const char* e = getenv("ZOO_WGRAD256_WG");
+    return e ? atoi(e) : 256;
+  }();
+  int splits = (target + tiles / 2) / tiles;
+  const int max_splits = (M + 4 * W2_BM - 1) / (4 * W2_BM);
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int mps = (M + splits - 1) / splits;
+  mps = (mps + W2_BM - 1) / W2_BM * W2_BM;
+  splits = (M + mps - 1) / mps;
+  *m_per_split = mps;
+  return splits;
+}
+
+extern "C" size_t zoo_wgrad256_part_floats(int M, int N, int K) {
+  int mps = 0;
+  const int splits = zoo_wgrad256_plan(M, N, K, &mps);
+  const size_t tiles = (size_t)((N + W2_T - 1) / W2_T) * ((K + W2_T - 1) / W2_T);
+  return splits > 1 ? (size_t)splits * tiles * W2_T * W2_T : 0;
+}
+
+// dW[N][K] (row stride ldw) += dY[M][N]^T X[M][K]; part: zoo_wgrad256_part_floats() fp32 scratch
+extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, float* part, int M, int N, int K,
+                                   int ldy, int ldx, int ldw, hipStream_t st) {
+  W2Geom g;
+  g.M = M; g.N = N; g.K = K; g.ldy = ldy; g.ldx = ldx; g.ldw = ldw;
+  g.tiles_n = (N + W2_T - 1) / W2_T;
+  g.tiles_k = (K + W2_T - 1) / W2_T;
+  g.splits = zoo_wgrad256_plan(M, N, K, &g.m_per_split);
+  if (g.splits > 1 && !part) return hipErrorInvalidValue;
+  const int tiles = g.tiles_n * g.tiles_k;
+  const size_t smem = 4 * 2 * W2_HALF;  // 2 buffers x (A, B) x 2 halves = 128 KiB
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                     (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
+  if (g.splits > 1) {
+    const size_t total = (size_t)tiles * 8 * 32 * 64;
+    hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);
+  }
+  return hipGetLastError();
+}

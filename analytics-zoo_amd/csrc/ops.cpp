@@ -26,11 +26,13 @@ hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, in
 hipError_t zoo_flip_weights_batched(const void*, int, int, hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
 int zoo_wgrad_plan(WgradGeom*);
+hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
+size_t zoo_wgrad256_part_floats(int, int, int);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
 size_t zoo_stats_part_scratch(int, int);
 hipError_t zoo_stats_part_finalize(float*, const float*, float*, int, int, hipStream_t);
 int zoo_bn_reduce_blocks(int, int);
-int zoo_act_bwd_reduce(const void*, const void*, void*, float*, int, int, int, hipStream_t);
+int zoo_act_bwd_reduce(const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
@@ -368,6 +370,32 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
             "wgrad");
 }
 
+// dW (fp32 [N, >=K], row stride dw.stride(0)) += dy[M, N]^T x[M, K] on the 256x256-tile
+// LDS-DMA + transposed-read kernel (wgrad256.hip); linear layers and 1x1 stride-1 convs
+void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dw.is_cuda(), "linear_wgrad: GPU tensors expected");
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "linear_wgrad: bf16 dy / x");
+  TORCH_CHECK(dw.scalar_type() == at::kFloat, "linear_wgrad: fp32 dw");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && dw.dim() == 2, "linear_wgrad: 2-D tensors expected");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && dw.stride(1) == 1, "linear_wgrad: rows must be contiguous");
+  const int64_t M = dy.size(0), N = dy.size(1), K = x.size(1);
+  TORCH_CHECK(x.size(0) == M, "linear_wgrad: dy / x row count differs");
+  TORCH_CHECK(dw.size(0) == N && dw.size(1) >= K, "linear_wgrad: dw must be [N, >=K]");
+  TORCH_CHECK(N % 8 == 0 && K % 8 == 0 && dy.stride(0) % 8 == 0 && x.stride(0) % 8 == 0,
+              "linear_wgrad: N, K and leading dims must be multiples of 8");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0,
+              "linear_wgrad: 16-byte aligned operands expected");
+  TORCH_CHECK(M < (1LL << 31) && N < (1 << 30) && K < (1 << 30) && M * dy.stride(0) < (1LL << 40),
+              "linear_wgrad: size out of range");
+  if (M == 0 || N == 0 || K == 0) return;
+  const size_t pf = zoo_wgrad256_part_floats((int)M, (int)N, (int)K);
+  torch::Tensor part;
+  if (pf) part = torch::empty({(int64_t)pf}, dw.options());
+  check_hip(zoo_wgrad256(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), pf ? part.data_ptr<float>() : nullptr,
+                         (int)M, (int)N, (int)K, (int)dy.stride(0), (int)x.stride(0), (int)dw.stride(0), cur_stream()),
+            "linear_wgrad");
+}
+
 static void check_al16(const void* p, const char* what) {
   TORCH_CHECK((reinterpret_cast<uintptr_t>(p) & 15) == 0, what, " must be 16-byte aligned");
 }
@@ -607,8 +635,9 @@ void dwconv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, in
 }
 
 // conv-epilogue backward: returns dy = dz * [z > 0] (z given) and/or db (fp32 [C]) = column sums
+// gelu: z is the pre-activation and dy = dz * gelu'(z) (erf form)
 std::vector<torch::Tensor> act_bwd_reduce(torch::Tensor dz, c10::optional<torch::Tensor> z, bool want_db,
-                                          c10::optional<torch::Tensor> db_into) {
+                                          c10::optional<torch::Tensor> db_into, bool gelu) {
   req(dz, at::kBFloat16, "dz");
   const int C = dz.size(-1);
   const int64_t M = dz.numel() / C;
@@ -639,8 +668,9 @@ std::vector<torch::Tensor> act_bwd_reduce(torch::Tensor dz, c10::optional<torch:
       out = db.data_ptr<float>();
     }
   }
+  TORCH_CHECK(!gelu || mask, "act_bwd_reduce: gelu needs the pre-activation z");
   const int blocks = zoo_act_bwd_reduce(dz.data_ptr(), mask ? z->data_ptr() : nullptr, dy.data_ptr(), out, (int)M, C,
-                                        part ? 1 : 0, cur_stream());
+                                        part ? 1 : 0, gelu ? 1 : 0, cur_stream());
   check_hip(hipGetLastError(), "act_bwd_reduce");
   if (want_db && part) fold_partials(db.data_ptr<float>(), partials, C, blocks);
   if (want_db) return {dy, db};
@@ -1658,7 +1688,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("dwconv_dgrad", &dwconv_dgrad);
   m.def("dwconv_wgrad", &dwconv_wgrad);
   m.def("softmax_rows", &softmax_rows);
-  m.def("act_bwd_reduce", &act_bwd_reduce);
+  m.def("act_bwd_reduce", &act_bwd_reduce, py::arg("dz"), py::arg("z"), py::arg("want_db"), py::arg("db_into"),
+        py::arg("gelu") = false);
   m.def("softmax_rows_bwd", &softmax_rows_bwd);
   m.def("lrn", &lrn);
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });
@@ -1691,6 +1722,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_bwd", &layernorm_bwd);
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
+  m.def("linear_wgrad", &linear_wgrad);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("causal"),
         py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("nms_sorted", &nms_sorted);

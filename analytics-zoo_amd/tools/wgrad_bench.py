@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Linear-layer weight gradient dW[N, K] (fp32) += dy[M, N]^T x[M, K] (bf16) at BERT-base
 b128 x s128 shapes: hipBLASLt (fp32-out addmm beta=1, and bf16-out mm + add) vs the zoo
-split-K wgrad kernel (csrc/kernels/wgrad.hip run as a 1x1 conv).
+split-K wgrad kernel (csrc/kernels/wgrad.hip run as a 1x1 conv) and the 256x256-tile
+LDS-DMA kernel (csrc/kernels/wgrad256.hip, ``zoo._C.linear_wgrad``).
 
   python analytics-zoo_amd/tools/wgrad_bench.py [--m 16384]
 """
@@ -31,10 +32,14 @@ def timeit(fn, iters=20):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=16384)
+    ap.add_argument("--more", action="store_true", help="also square / ResNet 1x1 shapes")
     a = ap.parse_args()
     dev = torch.device("cuda")
     M = a.m
-    for N, K in ((2304, 768), (768, 768), (3072, 768), (768, 3072)):
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
+    if a.more:
+        shapes += [(4096, 4096), (1000, 2048), (256, 64), (64, 256), (512, 128), (2048, 512)]
+    for N, K in shapes:
         dy = (torch.randn(M, N, device=dev) * 0.1).bfloat16()
         x = torch.randn(M, K, device=dev).bfloat16()
         ref = dy.double().t() @ x.double()
@@ -51,7 +56,11 @@ def main():
         def zoo():
             C.conv_wgrad(x.view(M, 1, 1, K), dy.view(M, 1, 1, N), g, 1, 1, 1, 1, 0, 0, 1, 1)
 
-        for name, fn in (("hipblaslt_f32out", lt_f32), ("hipblaslt_bf16out_add", lt_bf16), ("zoo_wgrad", zoo)):
+        def zoo256():
+            C.linear_wgrad(dy, x, g)
+
+        for name, fn in (("hipblaslt_f32out", lt_f32), ("hipblaslt_bf16out_add", lt_bf16), ("zoo_wgrad", zoo),
+                         ("zoo_wgrad256", zoo256)):
             g.zero_()
             fn()
             torch.cuda.synchronize()

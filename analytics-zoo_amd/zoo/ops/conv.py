@@ -229,27 +229,50 @@ class _LinearBlasFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, w, y, pre = ctx.saved_tensors
-        dy = dy.to(torch.bfloat16)
-        if ctx.act == "relu":
+        dy = dy.to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        bias_done = False
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            # one native pass: activation backward + fp32 bias-gradient column sums, accumulated
+            # straight into the flat gradient when the engine owns one (csrc/kernels/bn.hip
+            # act_bwd_reduce_kernel)
+            bias = ctx.bias_ref
+            bbuf = getattr(bias, "_zoo_grad", None) if bias is not None else None
+            z = y if ctx.act == "relu" else (pre if ctx.act == "gelu" else None)
+            outs = native().act_bwd_reduce(dy, z, True, bbuf, ctx.act == "gelu")
+            dy = outs[0]
+            if bbuf is not None:
+                hook = getattr(bias, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(bias)
+            else:
+                db = outs[1].to(bias.dtype)
+            bias_done = True
+        elif ctx.act == "relu":
             dy = dy * (y > 0).to(dy.dtype)
         elif ctx.act == "gelu":
             dy = torch.ops.aten.gelu_backward(dy, pre)
-        dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.mm(dy, bf16_weight(w))
         if ctx.needs_input_grad[1]:
             gbuf = getattr(w, "_zoo_grad", None)
             if gbuf is not None:
-                # accumulate straight into the flat fp32 gradient (hipBLASLt beta=1, bf16 in, fp32 out)
+                # accumulate straight into the flat fp32 gradient (bf16 in, fp32 out)
                 g2 = gbuf.view(dy.shape[1], x2.shape[1])
-                if not _blas_accumulate(g2, dy, x2):
+                if _use_wgrad256(dy, x2):
+                    native().linear_wgrad(dy.contiguous(), x2, g2)
+                elif not _blas_accumulate(g2, dy, x2):
                     g2.add_(torch.mm(dy.t(), x2, out_dtype=torch.float32))
                 hook = getattr(w, "_zoo_grad_ready", None)
                 if hook is not None:
                     hook(w)
+            elif _use_wgrad256(dy, x2):
+                g2 = torch.zeros(dy.shape[1], x2.shape[1], device=dy.device, dtype=torch.float32)
+                native().linear_wgrad(dy.contiguous(), x2, g2)
+                dw = g2.to(w.dtype)
             else:
                 dw = torch.mm(dy.t(), x2, out_dtype=torch.float32).to(w.dtype)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             bias = ctx.bias_ref
             db = torch.sum(dy, 0, dtype=torch.float32)   # fp32 accumulation, no fp32 copy of dy
             bbuf = getattr(bias, "_zoo_grad", None) if bias is not None else None
@@ -263,6 +286,18 @@ class _LinearBlasFn(torch.autograd.Function):
 
 
 _ADDMM_DTYPE_OK = [True]
+_WGRAD256 = os.environ.get("ZOO_WGRAD256", "1") != "0"
+
+
+def _use_wgrad256(dy, x2):
+    """The 256x256-tile LDS-DMA weight-gradient kernel (csrc/kernels/wgrad256.hip) beats
+    hipBLASLt's fp32-output GEMM 1.6-2.2x at transformer shapes (tall reduction, small
+    weight: tools/wgrad_bench.py); hipBLASLt keeps very large weights (>= 16M elements),
+    where the library's main loop is faster and no split of the reduction is needed."""
+    N, K = dy.shape[1], x2.shape[1]
+    return (_WGRAD256 and dy.dtype == torch.bfloat16 and x2.dtype == torch.bfloat16 and N % 8 == 0 and
+            K % 8 == 0 and N * K < (1 << 24) and N >= 128 and K >= 128 and x2.stride(1) == 1 and
+            x2.stride(0) % 8 == 0)
 
 
 def _blas_accumulate(g2, dy, x2):
