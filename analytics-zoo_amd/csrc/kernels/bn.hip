@@ -318,60 +318,64 @@ __global__ __launch_bounds__(256) void stats_finalize_kernel(float* __restrict__
 // bias gradient sum(dy) per channel accumulated, in ONE pass (replaces a compare, a multiply,
 // a cast and a reduction launch). Z == null: no mask (bias only). Same row layout and
 // per-row-lane LDS fold as bn_reduce_kernel; out = [C] fp32 (+= per block) or partials.
-// ACT 1: dY = dZ * [Z > 0] (ReLU, Z = output); ACT 2: dY = dZ * gelu'(Z) (erf GELU, Z = pre-activation)
-template <int ACT>
-__global__ __launch_bounds__(256) void act_bwd_reduce_kernel(const bf16_t* __restrict__ dZ,
-                                                            const bf16_t* __restrict__ Z, bf16_t* __restrict__ dY,
-                                                            float* __restrict__ out, int M, int C,
-                                                            int rows_per_block, int partial) {
+// Activation backward + column sums over a [M, C] row-major gradient (bias gradients of
+// linear / 1x1-conv layers). Block = CT column threads (8 columns each, one coalesced
+// CT*16-byte row segment) x RL = 256/CT row lanes; blockIdx = (row chunk, column group).
+// Partial column sums are reduced through LDS, then one fp32 atomic (or, for the ordered
+// deterministic fold, one partial row per row chunk) per column per block.
+// ACT 0: dY = dZ (sums only); 1: dY = dZ * [Z > 0] (ReLU, Z = output);
+// 2: dY = dZ * gelu'(Z) (erf GELU, Z = pre-activation). The sums are of the stored bf16 dY.
+template <int ACT, int CT>
+__global__ __launch_bounds__(256) void act_colsum_kernel(const bf16_t* __restrict__ dZ, const bf16_t* __restrict__ Z,
+                                                         bf16_t* __restrict__ dY, float* __restrict__ out, int M,
+                                                         int C, int rows_per_chunk, int col_groups, int partial) {
+  constexpr int RL = 256 / CT;
+  __shared__ float red[RL][CT * 8 + 4];
   const int cpr = C >> 3;
-  const int tid = threadIdx.x;
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int r0 = blockIdx.x * rows_per_block;
-  const int r1 = min(M, r0 + rows_per_block);
-  const int lanes_per_row = cpr < 256 ? cpr : 256;
-  const int row_step = 256 / lanes_per_row;
-  const int my_row = tid / lanes_per_row;
-  const int my_chunk0 = tid - my_row * lanes_per_row;
-  float* red = reinterpret_cast<float*>(smem);  // [row_step][C]
-  if (my_row < row_step) {
-    for (int chunk = my_chunk0; chunk < cpr; chunk += lanes_per_row) {
-      float s1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      for (int r = r0 + my_row; r < r1; r += row_step) {
-        const size_t off = (size_t)r * C + chunk * 8;
-        float a[8];
-        unpack8(*reinterpret_cast<const uint4*>(dZ + off), a);
-        if (Z) {
-          float z[8];
-          unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
-          if (ACT == 2) {
+  const int chunk = blockIdx.x / col_groups, cg = blockIdx.x - chunk * col_groups;
+  const int ct = threadIdx.x % CT, rl = threadIdx.x / CT;
+  const int c = cg * CT + ct;
+  const int r0 = chunk * rows_per_chunk, r1 = min(M, r0 + rows_per_chunk);
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (c < cpr) {
+#pragma unroll 4
+    for (int r = r0 + rl; r < r1; r += RL) {
+      const size_t off = (size_t)r * C + c * 8;
+      float a[8];
+      unpack8(*reinterpret_cast<const uint4*>(dZ + off), a);
+      if (ACT != 0) {
+        float z[8];
+        unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
+        if (ACT == 2) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float x = z[e];
-              a[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
-            }
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+          for (int e = 0; e < 8; ++e) {
+            const float x = z[e];
+            a[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
           }
-          *reinterpret_cast<uint4*>(dY + off) = pack8(a);
-          unpack8(*reinterpret_cast<const uint4*>(dY + off), a);  // sum what is stored (bf16)
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
         }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s1[e] += a[e];
+        const uint4 pk = pack8(a);
+        *reinterpret_cast<uint4*>(dY + off) = pk;
+        unpack8(pk, a);  // sum what is stored (bf16)
       }
-      float* rr = red + (size_t)my_row * C;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) rr[chunk * 8 + e] = s1[e];
+      for (int e = 0; e < 8; ++e) s[e] += a[e];
     }
   }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) red[rl][ct * 8 + e] = s[e];
   __syncthreads();
   if (!out) return;
-  for (int i = tid; i < C; i += blockDim.x) {
+  for (int i = threadIdx.x; i < CT * 8; i += 256) {
+    const int col = cg * CT * 8 + i;
+    if (col >= C) continue;
     float a = 0.f;
-    for (int r = 0; r < row_step; ++r) a += red[(size_t)r * C + i];
-    if (partial) out[(size_t)blockIdx.x * C + i] = a;
-    else atomicAdd(out + i, a);
+#pragma unroll
+    for (int r = 0; r < RL; ++r) a += red[r][i];
+    if (partial) out[(size_t)chunk * C + col] = a;
+    else atomicAdd(out + col, a);
   }
 }
 
@@ -533,20 +537,42 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
   return hipGetLastError();
 }
 
-// dY = dZ * [Z > 0] (Z non-null) and out[c] += sum_rows dY (out non-null; partial: out is
-// [blocks][C] partials for an ordered fold by the caller). Returns the block count.
+// grid of act_colsum_kernel: column groups of CT threads, row chunks of >= 32 rows, ~1024 blocks
+static void colsum_grid(int M, int C, int* ct, int* col_groups, int* chunks, int* rows_per_chunk) {
+  const int cpr = C >> 3;
+  *ct = (cpr % 64 == 0 || cpr > 256) ? 64 : 32;
+  *col_groups = (cpr + *ct - 1) / *ct;
+  int ch = 1024 / *col_groups;
+  const int max_ch = (M + 31) / 32;
+  if (ch > max_ch) ch = max_ch;
+  if (ch < 1) ch = 1;
+  *rows_per_chunk = (M + ch - 1) / ch;
+  *chunks = (M + *rows_per_chunk - 1) / *rows_per_chunk;
+}
+
+// number of partial rows the deterministic (partial) mode of zoo_act_bwd_reduce writes
+extern "C" int zoo_act_bwd_reduce_parts(int M, int C) {
+  int ct, cg, ch, rpc;
+  colsum_grid(M, C, &ct, &cg, &ch, &rpc);
+  return ch;
+}
+
+// dY = act'(dZ) (Z non-null: ReLU mask, or GELU derivative when gelu) and out[c] += sum_rows dY
+// (out non-null; partial: out is [parts][C] partials for an ordered fold by the caller).
+// Returns the number of partial rows.
 extern "C" int zoo_act_bwd_reduce(const void* dZ, const void* Z, void* dY, float* out, int M, int C, int partial,
                                   int gelu, hipStream_t st) {
-  int blocks, rpb;
-  bn_reduce_grid(M, C, &blocks, &rpb);
-  const int cpr = C >> 3;
-  const int row_step = 256 / (cpr < 256 ? cpr : 256);
-  const size_t smem = (size_t)row_step * C * sizeof(float);
-  if (gelu)
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<2>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ,
-                       (const bf16_t*)Z, (bf16_t*)dY, out, M, C, rpb, partial);
-  else
-    hipLaunchKernelGGL(act_bwd_reduce_kernel<1>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dZ,
-                       (const bf16_t*)Z, (bf16_t*)dY, out, M, C, rpb, partial);
-  return blocks;
+  int ct, cg, ch, rpc;
+  colsum_grid(M, C, &ct, &cg, &ch, &rpc);
+  const int act = Z ? (gelu ? 2 : 1) : 0;
+#define ZOO_COLSUM(A_, CT_)                                                                                   \
+  hipLaunchKernelGGL((act_colsum_kernel<A_, CT_>), dim3(ch * cg), dim3(256), 0, st, (const bf16_t*)dZ,       \
+                     (const bf16_t*)Z, (bf16_t*)dY, out, M, C, rpc, cg, partial)
+  if (ct == 64) {
+    if (act == 2) ZOO_COLSUM(2, 64); else if (act == 1) ZOO_COLSUM(1, 64); else ZOO_COLSUM(0, 64);
+  } else {
+    if (act == 2) ZOO_COLSUM(2, 32); else if (act == 1) ZOO_COLSUM(1, 32); else ZOO_COLSUM(0, 32);
+  }
+#undef ZOO_COLSUM
+  return ch;
 }

@@ -33,6 +33,7 @@ size_t zoo_stats_part_scratch(int, int);
 hipError_t zoo_stats_part_finalize(float*, const float*, float*, int, int, hipStream_t);
 int zoo_bn_reduce_blocks(int, int);
 int zoo_act_bwd_reduce(const void*, const void*, void*, float*, int, int, int, int, hipStream_t);
+int zoo_act_bwd_reduce_parts(int, int);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
@@ -325,6 +326,8 @@ void flip_weights_batched(torch::Tensor table, int n, int nblocks) {
 
 int flip_desc_ints() { return (int)(sizeof(zoo::FlipDesc) / sizeof(int)); }
 
+void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw);
+
 // dW (fp32, [K, ldw]) += wgrad(x, dy)
 void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int S, int sh, int sw, int ph, int pw,
                 int dh, int dil_w) {
@@ -345,6 +348,14 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.Ktot = R * S * g.C;
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
+  // 1x1 stride-1 convs with >= 256 input and output channels are plain GEMMs: the 256x256-tile
+  // kernel (wgrad256.hip) is 1.3-1.6x the implicit-GEMM wgrad there (tools/wgrad_bench.py --resnet)
+  static const bool use256 = env_flag("ZOO_WGRAD256", true);
+  if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= 256 && g.C >= 256 &&
+      x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
+    linear_wgrad(dy.view({(int64_t)g.M, g.K}), x.view({(int64_t)g.M, g.C}), dw);
+    return;
+  }
   g.m_per_split = 0;
   // split-K reduction: fp32 atomics into dW, or per-split partials + an ordered fold. Atomics
   // run at ~1.3 TB/s of added bytes, plain stores + the fold's reads at ~5 TB/s: the partials
@@ -662,7 +673,7 @@ std::vector<torch::Tensor> act_bwd_reduce(torch::Tensor dz, c10::optional<torch:
       db = torch::zeros({C}, dz.options().dtype(at::kFloat));
     }
     if (part) {
-      partials = torch::empty({(int64_t)zoo_bn_reduce_blocks((int)M, C), (int64_t)C}, db.options());
+      partials = torch::empty({(int64_t)zoo_act_bwd_reduce_parts((int)M, C), (int64_t)C}, db.options());
       out = partials.data_ptr<float>();
     } else {
       out = db.data_ptr<float>();

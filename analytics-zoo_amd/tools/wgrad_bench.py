@@ -33,16 +33,22 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--m", type=int, default=16384)
     ap.add_argument("--more", action="store_true", help="also square / ResNet 1x1 shapes")
+    ap.add_argument("--resnet", action="store_true", help="ResNet-50 b256 1x1 stride-1 conv shapes (M, Cout, Cin)")
     a = ap.parse_args()
     dev = torch.device("cuda")
     M = a.m
     shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
     if a.more:
         shapes += [(4096, 4096), (1000, 2048), (256, 64), (64, 256), (512, 128), (2048, 512)]
-    for N, K in shapes:
+    cases = [(M, N, K) for N, K in shapes]
+    if a.resnet:
+        cases = [(802816, 64, 64), (802816, 256, 64), (802816, 64, 256), (802816, 128, 256),
+                 (200704, 512, 128), (200704, 128, 512), (200704, 256, 512), (50176, 1024, 256),
+                 (50176, 256, 1024), (50176, 512, 1024), (12544, 2048, 512), (12544, 512, 2048)]
+    for M, N, K in cases:
         dy = (torch.randn(M, N, device=dev) * 0.1).bfloat16()
         x = torch.randn(M, K, device=dev).bfloat16()
-        ref = dy.double().t() @ x.double()
+        ref = (dy.float().t() @ x.float()).double()
         g = torch.zeros(N, K, device=dev)
         res = {"M": M, "N": N, "K": K}
         flop = 2.0 * M * N * K
@@ -59,8 +65,11 @@ def main():
         def zoo256():
             C.linear_wgrad(dy, x, g)
 
-        for name, fn in (("hipblaslt_f32out", lt_f32), ("hipblaslt_bf16out_add", lt_bf16), ("zoo_wgrad", zoo),
-                         ("zoo_wgrad256", zoo256)):
+        fns = (("hipblaslt_f32out", lt_f32), ("hipblaslt_bf16out_add", lt_bf16), ("zoo_wgrad", zoo),
+               ("zoo_wgrad256", zoo256))
+        if a.resnet:
+            fns = fns[2:]
+        for name, fn in fns:
             g.zero_()
             fn()
             torch.cuda.synchronize()
