@@ -213,7 +213,9 @@ class _LinearBlasFn(torch.autograd.Function):
         pre = None
         if act == "gelu" and need_grad:
             pre = torch.addmm(bb, x2, wb.t()) if bb is not None else torch.mm(x2, wb.t())
-            y = F.gelu(pre)
+            # GELU on the native pointwise kernel; the pre-activation is kept for the fused
+            # GELU-backward + bias-gradient pass (act_bwd_reduce)
+            y = native().act_fwd_bwd(pre, None, 4, 0.0) if pre.is_contiguous() else F.gelu(pre)
         elif act in ("gelu", "relu") and bb is not None:
             y = torch._addmm_activation(bb, x2, wb.t(), use_gelu=(act == "gelu"))
         else:

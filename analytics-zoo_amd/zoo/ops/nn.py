@@ -122,6 +122,9 @@ class _EmbeddingFn(torch.autograd.Function):
 def embedding(idx, table, padding_idx=None, compute_dtype=None):
     """Row gather ``table[idx]``; backward scatter-adds into the table gradient."""
     idx = idx.long()
+    if getattr(table, "_zoo_row_sparse", False):
+        from zoo.parallel.ddp import record_lookup
+        record_lookup(table, idx)
     D = table.shape[1]
     dt = compute_dtype or table.dtype
     aligned = (dt == torch.float32 and D % 4 == 0) or (dt == torch.bfloat16 and D % 8 == 0)

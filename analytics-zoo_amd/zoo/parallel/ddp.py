@@ -33,6 +33,15 @@ docs/docs/wp-bigdl.md:140-160):
   flat buffer (layers read some fp32 parameters directly, so every rank must
   hold identical fp32 values), followed by one cast pass for the bf16 copy.
 
+* Row-sparse embedding tables (``mark_row_sparse``; NCF / Wide&Deep lookups,
+  SURVEY.md §2.17 note, NeuralCF.scala:45-53) get buckets of their own that do
+  not all-reduce the dense table gradient: the ranks all-gather the ids they
+  looked up this step, and only the rows of the union are all-reduced (a table
+  of 138k users with 8k lookups per rank moves ~|union| x dim floats instead of
+  the whole table). The rows nobody touched are zero on every rank, so the
+  result equals the dense all-reduce (the table must get gradient only through
+  lookups: no dense regulariser on it).
+
 All persistent comm buffers are allocated once (chunk = ceil(bucket/N) rounded
 to 64 elements). ``force_comm`` runs the whole bucket / comm-stream / event
 path on a world-size-1 process group (RCCL with one rank), so the overlapped
@@ -50,11 +59,44 @@ import torch.distributed as dist
 from zoo.parallel.flat import FlatParams
 
 CHUNK_ALIGN = 64
+# step counter for the row-sparse id records (bumped by GradSync.reset): an embedding lookup
+# in a new step starts a new record list; a hipGraph replay runs no Python forward, so the
+# captured id tensors (rewritten by every replay) stay recorded
+_TOUCH_STEP = [0]
+
+
+def mark_row_sparse(*params):
+    """Sync these embedding tables' gradients row-sparsely (see module doc)."""
+    for p in params:
+        p._zoo_row_sparse = True
+        p._zoo_touched = []
+        p._zoo_touch_step = -1
+
+
+def mark_row_sparse_embeddings(module):
+    """Mark the table of every Keras ``Embedding`` layer inside ``module``."""
+    from zoo.pipeline.api.keras.layers.embeddings import Embedding
+    n = 0
+    for m in module.modules():
+        if isinstance(m, Embedding) and getattr(m, "embeddings", None) is not None:
+            mark_row_sparse(m.embeddings)
+            n += 1
+    return n
+
+
+def record_lookup(table, idx):
+    """Called by the embedding ops: remember the ids looked up in ``table`` this step."""
+    if not getattr(table, "_zoo_row_sparse", False):
+        return
+    if getattr(table, "_zoo_touch_step", -1) != _TOUCH_STEP[0]:
+        table._zoo_touched = []
+        table._zoo_touch_step = _TOUCH_STEP[0]
+    table._zoo_touched.append(idx.detach().reshape(-1))
 
 
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "params", "pending", "launched", "cb", "so", "pack", "recv", "gath",
-                 "works", "post")
+                 "works", "post", "sparse")
 
     def __init__(self, idx, lo, hi):
         self.idx, self.lo, self.hi = idx, lo, hi
@@ -66,6 +108,7 @@ class _Bucket:
         self.pack = self.recv = self.gath = None
         self.works = []
         self.post = None
+        self.sparse = []     # [(param, lo, hi)] when every parameter of the bucket is row-sparse
 
 
 class GradSync:
@@ -93,13 +136,18 @@ class GradSync:
         self.buckets = []
         self.param_bucket = {}
         cur = None
+        prev_sparse = False
         for p, (lo, hi) in zip(flat.params, flat.ranges()):
-            if cur is None or ((hi - cur.lo) > cap and cur.params):
+            sp = bool(getattr(p, "_zoo_row_sparse", False)) and p.dim() == 2
+            if cur is None or ((hi - cur.lo) > cap and cur.params) or sp or prev_sparse:
                 cur = _Bucket(len(self.buckets), lo, hi)
                 self.buckets.append(cur)
             cur.hi = hi
             cur.params.append(id(p))
+            if sp:
+                cur.sparse.append((p, lo, hi))
             self.param_bucket[id(p)] = cur
+            prev_sparse = sp
         if self.buckets:
             self.buckets[-1].hi = flat.numel  # include the alignment tail
             self.buckets[0].lo = 0
@@ -205,9 +253,10 @@ class GradSync:
 
     def reset(self):
         self._counts = {}
+        _TOUCH_STEP[0] += 1
         for b in self.buckets:
-            if self._expected is None:
-                b.pending = -1  # calibration step: nothing launches before finish()
+            if self._expected is None or b.sparse:
+                b.pending = -1  # calibration step / row-sparse bucket: launched by finish()
             else:
                 b.pending = sum(1 for pid in b.params if self._expected.get(pid, 0) > 0)
             b.launched = False
@@ -289,12 +338,43 @@ class GradSync:
         if out16 is not None:
             out16.copy_(s)
 
+    def _row_sparse_allreduce(self, p, lo, hi):
+        """Sum table p's gradient over the ranks through the union of looked-up rows
+        (False: no lookup was recorded, the caller reduces the dense range)."""
+        touched = getattr(p, "_zoo_touched", None)
+        if not touched:
+            return False
+        V, D = p.shape
+        g = self.flat.grad[lo:lo + V * D].view(V, D)
+        dev = g.device
+        ids = torch.cat([t.to(dev).long() for t in touched])
+        u = torch.unique(ids[(ids >= 0) & (ids < V)])
+        cnt = torch.tensor([u.numel()], device=dev, dtype=torch.long)
+        cnts = [torch.empty_like(cnt) for _ in range(self.world)]
+        dist.all_gather(cnts, cnt, group=self.group)
+        m = int(max(int(c.item()) for c in cnts))
+        if m == 0:
+            return True
+        pad = torch.full((m,), V, device=dev, dtype=torch.long)
+        pad[:u.numel()] = u
+        allids = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(allids, pad, group=self.group)
+        union = torch.unique(torch.cat(allids))
+        union = union[union < V]
+        rows = g.index_select(0, union)
+        dist.all_reduce(rows, group=self.group)
+        g.index_copy_(0, union, rows)
+        self.sparse_rows = getattr(self, "sparse_rows", 0) + int(union.numel())
+        return True
+
     def _issue(self, b):
         """Enqueue bucket b's reduction on the current (comm) stream. Every step
         after a collective that consumes its result waits on the device only."""
         g = self.flat.grad[b.lo:b.hi]
         n = b.hi - b.lo
         if self.mode == "allreduce" and not self.compress:
+            if b.sparse and all(self._row_sparse_allreduce(p, lo, hi) for p, lo, hi in b.sparse):
+                return
             dist.all_reduce(g, group=self.group)
             return
         lo, hi = self._chunk(b)

@@ -266,3 +266,37 @@ def test_tensor_parallel_mlp_trains_through_engine():
     np.testing.assert_allclose(fc1, full[0].weight.detach().numpy(), atol=1e-5)
     np.testing.assert_allclose(fc2, full[2].weight.detach().numpy(), atol=1e-5)
     np.testing.assert_allclose(res[0][2], full[2].bias.detach().numpy(), atol=1e-5)
+
+
+# ---------------------------------------------------------------------------
+# row-sparse embedding-gradient sync (NCF at DP): equals the dense all-reduce
+# ---------------------------------------------------------------------------
+def _ncf_worker(rank, world, port, q, sparse):
+    ctx = _init(rank, world, port)
+    from zoo.models.recommendation.neuralcf import NeuralCF
+    from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.pipeline.engine import TrainingEngine
+    torch.manual_seed(0)
+    m = NeuralCF(500, 300, 5, user_embed=8, item_embed=8, hidden_layers=(16, 8), mf_embed=8,
+                 row_sparse_sync=sparse)
+    eng = TrainingEngine(m, SparseCategoricalCrossEntropy(), Adam(lr=0.01), ctx=ctx, bucket_mb=0.001)
+    r = np.random.RandomState(100 + rank)
+    for step in range(3):
+        x = np.stack([r.randint(1, 60, 32), r.randint(1, 40, 32)], 1).astype(np.float32)
+        y = r.randint(0, 5, 32).astype(np.int64)
+        eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
+    nb = sum(1 for b in eng.sync.buckets if b.sparse)
+    q.put((rank, (eng.flat.master.detach().numpy().copy(), nb, getattr(eng.sync, "sparse_rows", 0))))
+    ctx.stop()
+
+
+def test_row_sparse_embedding_sync_matches_dense_allreduce():
+    dense = _run(_ncf_worker, False)
+    sparse = _run(_ncf_worker, True)
+    for rk in (0, 1):
+        assert np.allclose(dense[rk][0], sparse[rk][0], atol=1e-6), "row-sparse sync differs from dense"
+    assert np.allclose(sparse[0][0], sparse[1][0], atol=1e-7), "ranks diverged"
+    assert dense[0][1] == 0 and sparse[0][1] == 4        # four tables, one bucket each
+    rows = sparse[0][2]
+    assert 0 < rows < 3 * (2 * 501 + 2 * 301)            # only the looked-up union moved
