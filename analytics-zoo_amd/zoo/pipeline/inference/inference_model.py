@@ -192,9 +192,12 @@ class InferenceModel:
         """TorchScript file (doLoadPyTorch, InferenceModel.scala:246-266)."""
         return self._install(torch.jit.load(model_path, map_location="cpu"))
 
-    def load_openvino(self, model_path, weight_path, batch_size=0):
-        raise NotImplementedError("OpenVINO IR is a CPU runtime format; convert the model to ONNX / Caffe / a "
-                                  "zoo model and use load_onnx / load_caffe / load")
+    def load_openvino(self, model_path, weight_path=None, batch_size=0):
+        """OpenVINO IR xml + bin (doLoadOpenVINO, InferenceModel.scala; OpenVINOModel.scala):
+        the IR is decoded and executed by this framework (zoo.pipeline.inference.openvino),
+        convolutions / matmuls on the native kernels."""
+        from zoo.pipeline.inference.openvino import load_openvino
+        return self._install(load_openvino(model_path, weight_path, batch_size))
 
     def load_tensorflow(self, model_path, model_type="frozenModel", inputs=None, outputs=None, **kw):
         """TF frozen graph / export folder / SavedModel (doLoadTensorflow,
