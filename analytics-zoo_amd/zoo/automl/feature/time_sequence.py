@@ -9,10 +9,12 @@ import json
 import numpy as np
 import pandas as pd
 
+from zoo.automl.feature.abstract import BaseFeatureTransformer
+
 DT_FEATURES = ["MONTH", "WEEKDAY", "DAY", "HOUR", "IS_WEEKEND", "IS_AWAKE", "IS_BUSY_HOURS"]
 
 
-class TimeSequenceFeatureTransformer:
+class TimeSequenceFeatureTransformer(BaseFeatureTransformer):
     def __init__(self, future_seq_len=1, dt_col="datetime", target_col="value", extra_features_col=None,
                  drop_missing=True):
         self.future_seq_len = int(future_seq_len)
@@ -110,3 +112,20 @@ class TimeSequenceFeatureTransformer:
     def save(self, file_path, replace=False):
         with open(file_path, "w") as f:
             json.dump(self.state(), f)
+
+    def restore(self, **config):
+        """Restore from a saved state dict (``save`` file contents) merged into the config."""
+        s = config.get("ft_state", config)
+        if "file_path" in config:
+            with open(config["file_path"]) as f:
+                s = json.load(f)
+        t = TimeSequenceFeatureTransformer.from_state(dict(self.state(), **{k: v for k, v in s.items()
+                                                                             if k in self.state()}))
+        self.__dict__.update(t.__dict__)
+        return self
+
+    def _get_required_parameters(self):
+        return {"past_seq_len"}
+
+    def _get_optional_parameters(self):
+        return {"selected_features"}

@@ -10,6 +10,7 @@ import torch
 from zoo.automl.common.metrics import Evaluator
 from zoo.automl.feature.time_sequence import TimeSequenceFeatureTransformer
 from zoo.automl.model import build_model
+from zoo.automl.pipeline.abstract import Pipeline
 
 
 def _train(module, x, y, config, epochs=None):
@@ -22,7 +23,7 @@ def _train(module, x, y, config, epochs=None):
     return net
 
 
-class TimeSequencePipeline:
+class TimeSequencePipeline(Pipeline):
     def __init__(self, feature_transformers=None, model=None, config=None, name=None):
         self.ft, self.model, self.config, self.name = feature_transformers, model, dict(config or {}), name
         self.net = None

@@ -23,14 +23,8 @@ import numpy as np
 log = logging.getLogger("zoo.automl")
 
 
-class GridSearch:
-    def __init__(self, values):
-        self.values = list(values)
-
-
-class RandomSample:
-    def __init__(self, fn):
-        self.fn = fn
+from zoo.automl.search.abstract import (BayersianOpt, GoodError, GridSearch, RandomSample,  # noqa: F401
+                                       SearchEngine as _AbstractSearchEngine, TrialOutput)
 
 
 def expand(space, num_samples=1, seed=0):
@@ -48,7 +42,7 @@ def expand(space, num_samples=1, seed=0):
                     if isinstance(v, GridSearch):
                         cfg[k] = combo[keys.index(k)]
                     elif isinstance(v, RandomSample):
-                        cfg[k] = v.fn(cfg)
+                        cfg[k] = v.func(cfg)
                     else:
                         cfg[k] = v
                 out.append(cfg)
@@ -132,10 +126,21 @@ class BayesOptSearch:
         self.y.append(float(reward))
 
 
-class SearchEngine:
+class SearchEngine(_AbstractSearchEngine):
+    """The local counterpart of RayTuneSearchEngine (RayTuneSearchEngine.py:28-458):
+    trials in-process or in worker processes pinned one per GPU."""
+
     def __init__(self, n_parallel=1, logs_dir=None):
         self.n_parallel, self.logs_dir = max(1, int(n_parallel)), logs_dir
         self.trials = []
+        self._mode = "min"
+        self._metric = "mse"
+
+    def get_best_trials(self, k=1):
+        """Configs of the best ``k`` finished trials (by the last run's metric and mode)."""
+        sign = 1 if self._mode == "min" else -1
+        ranked = sorted(self.trials, key=lambda t: sign * t[1][self._metric])
+        return [c for c, _ in ranked[:k]]
 
     def _map(self, trial_fn, cfgs):
         if self.n_parallel > 1:
@@ -149,6 +154,7 @@ class SearchEngine:
         """Sequential GP Bayesian optimisation; ``space`` = {name: (low, high)}. Each point is
         turned into a trial config by ``convert_bayes_configs`` plus ``fixed_params``."""
         from zoo.automl.common.util import convert_bayes_configs
+        self._metric, self._mode = metric, mode
         opt = BayesOptSearch(space, utility_kwargs, seed=seed)
         sign = -1.0 if mode == "min" else 1.0
         self.trials = []
@@ -170,6 +176,7 @@ class SearchEngine:
         if search_alg == "BayesOpt":
             return self.run_bayes(trial_fn, space, num_samples, metric, mode, seed, fixed_params,
                                   (search_alg_params or {}).get("utility_kwargs"))
+        self._metric, self._mode = metric, mode
         if fixed_params:
             space = dict(space, **fixed_params)
         cfgs = expand(space, num_samples, seed)
@@ -179,3 +186,6 @@ class SearchEngine:
         best = min(self.trials, key=lambda t: sign * t[1][metric])
         log.info("best trial %s -> %s", best[0], best[1])
         return best
+
+
+RayTuneSearchEngine = SearchEngine  # the reference's engine name

@@ -3,7 +3,7 @@ MTNetForecaster over (x [N, past, F], y [N, horizon]) numpy windows."""
 import numpy as np
 import torch
 
-from zoo.automl.model import MTNet, VanillaLSTM
+from zoo.automl.model import MTNetNet as MTNet, VanillaLSTMNet as VanillaLSTM
 
 
 class Forecaster:

@@ -74,10 +74,10 @@ def test_time_sequence_predictor_fit_predict_save(tmp_path):
 
 def test_mtnet_and_seq2seq_models_forward():
     import torch
-    from zoo.automl.model import LSTMSeq2Seq, MTNet
+    from zoo.automl.model import LSTMSeq2SeqNet, MTNetNet
     x = torch.randn(4, 9, 3)
-    assert MTNet(3, 2, time_step=3, long_num=2, ar_window=2)(x).shape == (4, 2)
-    assert LSTMSeq2Seq(3, 3, latent_dim=8)(x).shape == (4, 3)
+    assert MTNetNet(3, 2, time_step=3, long_num=2, ar_window=2)(x).shape == (4, 2)
+    assert LSTMSeq2SeqNet(3, 3, latent_dim=8)(x).shape == (4, 3)
 
 
 def test_zouwu_forecasters_and_autots(tmp_path):
@@ -156,3 +156,43 @@ def test_time_sequence_predictor_with_bayes_recipe():
     assert len(tsp.trials) == 3
     assert all(2 <= c["past_seq_len"] <= 4 and c["model"] == "LSTM" for c, _ in tsp.trials)
     assert ppl.predict(df).shape[0] > 0
+
+
+def test_automl_base_models_fit_eval_save_restore(tmp_path):
+    """BaseModel contract (Py/automl/model/abstract.py): fit_eval returns the validation
+    metric, save/restore round-trips, TimeSequenceModel picks the model from the config."""
+    from zoo.automl.model import LSTMSeq2Seq, MTNetKeras, TimeSequenceModel, VanillaLSTM
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((96, 6, 2)).astype(np.float32)
+    y = (x[:, -1, :1] * 0.7 + 0.1).astype(np.float32)
+    m = VanillaLSTM(check_optional_config=False, future_seq_len=1)
+    first = m.fit_eval(x, y, validation_data=(x, y), lstm_1_units=8, lstm_2_units=4, lr=0.01, epochs=1)
+    later = m.fit_eval(x, y, validation_data=(x, y), epochs=15)
+    assert later < first
+    m.save(str(tmp_path / "m.pt"), str(tmp_path / "m.json"))
+    import json
+    cfg = json.load(open(tmp_path / "m.json"))
+    m2 = VanillaLSTM().restore(str(tmp_path / "m.pt"), **cfg)
+    assert np.allclose(m2.predict(x), m.predict(x), atol=1e-5)
+    mean, std = m.predict_with_uncertainty(x[:8], n_iter=4)
+    assert mean.shape == (8, 1) and std.shape == (8, 1)
+    with pytest.raises(ValueError, match="Missing required"):
+        MTNetKeras().fit_eval(x, y, epochs=1)
+    mt = MTNetKeras(future_seq_len=1)
+    assert mt.fit_eval(x, y, long_num=2, time_step=2, epochs=1) >= 0
+    tsm = TimeSequenceModel(future_seq_len=2)
+    y2 = np.concatenate([y, y], 1)
+    tsm.fit_eval(x, y2, latent_dim=8, epochs=1)
+    assert tsm.selected_model == "Seq2seq" and tsm.predict(x).shape == (96, 2)
+    assert isinstance(tsm.model, LSTMSeq2Seq)
+
+
+def test_search_engine_abstract_contract():
+    from zoo.automl.search import GridSearch, RandomSample, RayTuneSearchEngine, SearchEngine
+    from zoo.automl.search.abstract import SearchEngine as Abstract
+    assert issubclass(SearchEngine, Abstract) and RayTuneSearchEngine is SearchEngine
+    eng = SearchEngine()
+    space = {"a": GridSearch([1, 2, 3]), "b": RandomSample(lambda spec: spec["a"] * 10)}
+    best_cfg, best = eng.run(lambda c: {"mse": abs(c["a"] - 2) + 0.0 * c["b"]}, space)
+    assert best_cfg == {"a": 2, "b": 20}
+    assert [c["a"] for c in eng.get_best_trials(2)] in ([2, 1], [2, 3])
