@@ -49,6 +49,30 @@ class ImageSet:
         return klass(feats, label_map)
 
     @classmethod
+    def read_sequence_files(cls, path, sc=None, min_partitions=1, class_num=1000, distributed=False):
+        """Images with labels from Hadoop SequenceFiles in ``path`` (a file or a folder),
+        as written by BigDL's ImageNet sequence-file generator (ImageSet.scala:335-352):
+        records with label > ``class_num`` are dropped; pixels stay BGR like the reference."""
+        from zoo.feature.image.sequence_file import decode_image_record, read_sequence_file
+        files = [path] if os.path.isfile(path) else sorted(
+            os.path.join(path, f) for f in os.listdir(path) if not f.startswith((".", "_")))
+        if distributed:
+            from zoo.common.nncontext import get_nncontext
+            ctx = get_nncontext()
+            files = files[ctx.rank::ctx.world_size]
+        feats = []
+        for fp in files:
+            for k, v in read_sequence_file(fp):
+                label, name, img = decode_image_record(k, v)
+                if label > class_num:
+                    continue
+                feats.append({"uri": name, "mat": img.astype(np.float32), "originalSize": img.shape,
+                              "label": np.array([label], np.float32)})
+        return (DistributedImageSet if distributed else LocalImageSet)(feats)
+
+    readSequenceFiles = read_sequence_files
+
+    @classmethod
     def from_arrays(cls, images, labels=None):
         feats = []
         for i, im in enumerate(images):

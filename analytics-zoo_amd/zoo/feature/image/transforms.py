@@ -249,6 +249,8 @@ class _Crop(ImagePreprocessing):
         x1, y1 = max(0, int(x1)), max(0, int(y1))
         x2, y2 = min(w, int(x2)), min(h, int(y2))
         f["mat"] = f["mat"][y1:y2, x1:x2]
+        # the crop window in normalised coordinates of the pre-crop image (ImageRoiProject)
+        f["cropBbox"] = np.array([x1 / w, y1 / h, x2 / w, y2 / h], np.float32)
         return f
 
 
@@ -400,3 +402,161 @@ def gpu_resize_normalize(batch_u8, out_h, out_w, mean=(0.0, 0.0, 0.0), std=(1.0,
     t = torch.as_tensor(np.ascontiguousarray(batch_u8, dtype=np.uint8)).to(device, non_blocking=True)
     return native().resize_normalize(t, int(out_h), int(out_w), [float(m) for m in mean], [float(s) for s in std],
                                      bool(swap_rb), 0 if layout == "NCHW" else 1)
+
+
+# ---------------------------------------------------------------------------
+# Random cropper and region-of-interest transformers
+# (Zs/feature/image/ImageRandomCropper.scala, RoiTransformer.scala, RandomSampler.scala)
+#
+# A feature's ground-truth boxes live in ``f["roi"]`` = {"classes": [n] (or [2, n] with the
+# difficult flags as row 1), "bboxes": [n, 4] float (x1, y1, x2, y2)} -- BigDL's RoiLabel.
+# ---------------------------------------------------------------------------
+def _roi(f):
+    r = f.get("roi")
+    if r is None and isinstance(f.get("label"), dict):
+        r = f["roi"] = f["label"]
+    return r
+
+
+class ImageRandomCropper(_Crop):
+    """Crop ``crop_width`` x ``crop_height`` at a random (``cropper_method="random"``) or
+    centred position, then mirror horizontally with probability 1/2 when ``mirror``."""
+
+    def __init__(self, crop_width, crop_height, mirror=False, cropper_method="random", channels=3):
+        self.cw, self.ch = int(crop_width), int(crop_height)
+        self.mirror, self.method, self.channels = bool(mirror), str(cropper_method).lower(), int(channels)
+
+    def transform(self, f):
+        h, w = f["mat"].shape[:2]
+        if self.method in ("random", "croprandom"):
+            x1 = int(_RNG.integers(0, max(w - self.cw, 0) + 1))
+            y1 = int(_RNG.integers(0, max(h - self.ch, 0) + 1))
+        else:
+            x1, y1 = max(w - self.cw, 0) // 2, max(h - self.ch, 0) // 2
+        f = self._crop(f, x1, y1, x1 + self.cw, y1 + self.ch)
+        if self.mirror and _RNG.random() < 0.5:
+            f["mat"] = f["mat"][:, ::-1].copy()
+        return f
+
+
+class ImageRoiNormalize(ImagePreprocessing):
+    """Boxes from pixels to [0, 1] of the current image size."""
+
+    def transform(self, f):
+        r = _roi(f)
+        if r is not None and len(r["bboxes"]):
+            h, w = f["mat"].shape[:2]
+            r["bboxes"] = np.asarray(r["bboxes"], np.float32) / np.array([w, h, w, h], np.float32)
+        return f
+
+
+class ImageRoiHFlip(ImagePreprocessing):
+    """Mirror the boxes horizontally (pair with ImageHFlip)."""
+
+    def __init__(self, normalized=True):
+        self.normalized = normalized
+
+    def transform(self, f):
+        r = _roi(f)
+        if r is not None and len(r["bboxes"]):
+            b = np.asarray(r["bboxes"], np.float32).copy()
+            width = 1.0 if self.normalized else float(f["mat"].shape[1])
+            x1 = width - b[:, 2]
+            b[:, 2] = width - b[:, 0]
+            b[:, 0] = x1
+            r["bboxes"] = b
+        return f
+
+
+class ImageRoiResize(ImagePreprocessing):
+    """Scale pixel boxes by the resize from ``originalSize`` to the current size (a no-op
+    for normalised boxes)."""
+
+    def __init__(self, normalized=False):
+        self.normalized = normalized
+
+    def transform(self, f):
+        r = _roi(f)
+        if r is not None and len(r["bboxes"]) and not self.normalized:
+            oh, ow = f["originalSize"][:2]
+            h, w = f["mat"].shape[:2]
+            r["bboxes"] = np.asarray(r["bboxes"], np.float32) * np.array([w / ow, h / oh, w / ow, h / oh],
+                                                                          np.float32)
+        return f
+
+
+class ImageRoiProject(ImagePreprocessing):
+    """Project normalised boxes onto the last crop window (``f["cropBbox"]``): boxes whose
+    centre falls outside the window are dropped when ``need_meet_center_constraint``, the
+    rest are clipped to the window and re-normalised to it; empty boxes are dropped."""
+
+    def __init__(self, need_meet_center_constraint=True):
+        self.center = need_meet_center_constraint
+
+    def transform(self, f):
+        r = _roi(f)
+        crop = f.get("cropBbox")
+        if r is None or crop is None or not len(r["bboxes"]):
+            return f
+        b = np.asarray(r["bboxes"], np.float32)
+        cx1, cy1, cx2, cy2 = [float(v) for v in crop]
+        keep = np.ones(len(b), bool)
+        if self.center:
+            mx, my = (b[:, 0] + b[:, 2]) / 2, (b[:, 1] + b[:, 3]) / 2
+            keep &= (mx >= cx1) & (mx <= cx2) & (my >= cy1) & (my <= cy2)
+        cw, ch = max(cx2 - cx1, 1e-12), max(cy2 - cy1, 1e-12)
+        nb = np.stack([(np.clip(b[:, 0], cx1, cx2) - cx1) / cw, (np.clip(b[:, 1], cy1, cy2) - cy1) / ch,
+                       (np.clip(b[:, 2], cx1, cx2) - cx1) / cw, (np.clip(b[:, 3], cy1, cy2) - cy1) / ch], 1)
+        keep &= (nb[:, 2] > nb[:, 0]) & (nb[:, 3] > nb[:, 1])
+        r["bboxes"] = nb[keep]
+        cls = np.asarray(r["classes"])
+        r["classes"] = cls[..., keep] if cls.ndim == 2 else cls[keep]
+        return f
+
+
+def _iou(box, boxes):
+    ix1 = np.maximum(box[0], boxes[:, 0])
+    iy1 = np.maximum(box[1], boxes[:, 1])
+    ix2 = np.minimum(box[2], boxes[:, 2])
+    iy2 = np.minimum(box[3], boxes[:, 3])
+    inter = np.clip(ix2 - ix1, 0, None) * np.clip(iy2 - iy1, 0, None)
+    area = (box[2] - box[0]) * (box[3] - box[1]) + (boxes[:, 2] - boxes[:, 0]) * (boxes[:, 3] - boxes[:, 1])
+    return inter / np.maximum(area - inter, 1e-12)
+
+
+class ImageRandomSampler(_Crop):
+    """SSD batch sampler (RandomSampler.scala): among the whole image and crops drawn by
+    samplers (scale in [0.3, 1], aspect ratio in [0.5, 2], up to 50 trials each) that reach
+    a minimum Jaccard overlap of {0.1, 0.3, 0.5, 0.7, 0.9} or any with a ground-truth box,
+    one is picked at random and cropped; follow with ImageRoiProject for the boxes."""
+
+    MIN_IOU = (None, 0.1, 0.3, 0.5, 0.7, 0.9, "max")
+
+    def __init__(self, max_trials=50, min_scale=0.3, max_scale=1.0, min_ar=0.5, max_ar=2.0):
+        self.max_trials, self.min_scale, self.max_scale = max_trials, min_scale, max_scale
+        self.min_ar, self.max_ar = min_ar, max_ar
+
+    def _sample_box(self):
+        scale = _RNG.uniform(self.min_scale, self.max_scale)
+        ar = _RNG.uniform(max(self.min_ar, scale ** 2), min(self.max_ar, 1.0 / scale ** 2))
+        bw, bh = scale * np.sqrt(ar), scale / np.sqrt(ar)
+        x1, y1 = _RNG.uniform(0, 1 - bw), _RNG.uniform(0, 1 - bh)
+        return np.array([x1, y1, x1 + bw, y1 + bh], np.float32)
+
+    def transform(self, f):
+        r = _roi(f)
+        gt = np.asarray(r["bboxes"], np.float32) if r is not None and len(r["bboxes"]) else None
+        cands = [np.array([0, 0, 1, 1], np.float32)]
+        for thr in self.MIN_IOU[1:]:
+            for _ in range(self.max_trials):
+                box = self._sample_box()
+                if gt is None:
+                    cands.append(box)
+                    break
+                ious = _iou(box, gt)
+                if (thr == "max" and ious.max() >= 1.0) or (thr != "max" and ious.max() >= thr):
+                    cands.append(box)
+                    break
+        box = cands[int(_RNG.integers(0, len(cands)))]
+        h, w = f["mat"].shape[:2]
+        return self._crop(f, box[0] * w, box[1] * h, box[2] * w, box[3] * h)
