@@ -1,11 +1,12 @@
 """File-system helpers (Zs/common/Utils.scala:35-278 FS helpers; Zs/utils/File.scala:24-112
 FileReader/FileWriter over Hadoop FS).
 
-Paths may be plain local paths, ``file://`` URIs or ``hdfs://`` URIs. Local
-paths go through the OS directly; ``hdfs://`` goes through the ``hdfs dfs`` CLI
-when one is on PATH (there is no JVM/Hadoop client in this framework), which
-covers the copy-in / copy-out pattern the reference uses for checkpoints and
-model files. Other schemes raise a clear error.
+Paths may be plain local paths, ``file://`` URIs, ``hdfs://`` URIs or ``s3://``
+(``s3a://``, ``s3n://``) URIs. Local paths go through the OS directly; ``hdfs://``
+goes through the ``hdfs dfs`` CLI when one is on PATH (there is no JVM/Hadoop client
+in this framework); ``s3://`` goes through the built-in SigV4 client
+(``zoo.utils.s3``). Together they cover the copy-in / copy-out pattern the reference
+uses for checkpoints and model files. Other schemes raise a clear error.
 """
 import os
 import shutil
@@ -43,9 +44,25 @@ def _remote_only(path):
         raise NotImplementedError("unsupported file system scheme %r in %s" % (scheme(path), path))
 
 
+def is_s3(path):
+    return scheme(path) in ("s3", "s3a", "s3n")
+
+
+def _s3():
+    from zoo.utils import s3
+    return s3.client(), s3.split_s3
+
+
 def exists(path):
     if is_local_path(path):
         return os.path.exists(local_path(path))
+    if is_s3(path):
+        c, split = _s3()
+        b, k = split(path)
+        if k and c.head(b, k) is not None:
+            return True
+        keys, pre = c.list(b, k.rstrip("/") + "/" if k else "", "/")
+        return bool(keys or pre)
     _remote_only(path)
     return _hdfs("-test", "-e", str(path), check=False).returncode == 0
 
@@ -53,6 +70,8 @@ def exists(path):
 def mkdirs(path):
     if is_local_path(path):
         os.makedirs(local_path(path), exist_ok=True)
+        return
+    if is_s3(path):   # object stores have no directories
         return
     _remote_only(path)
     _hdfs("-mkdir", "-p", str(path))
@@ -62,6 +81,14 @@ def list_files(path):
     if is_local_path(path):
         p = local_path(path)
         return sorted(os.path.join(p, f) for f in os.listdir(p)) if os.path.isdir(p) else [p]
+    if is_s3(path):
+        c, split = _s3()
+        b, k = split(path)
+        sch = scheme(path)
+        if k and c.head(b, k) is not None:
+            return [str(path)]
+        keys, pre = c.list(b, k.rstrip("/") + "/" if k else "", "/")
+        return sorted("%s://%s/%s" % (sch, b, x.rstrip("/")) for x in keys + pre)
     _remote_only(path)
     out = _hdfs("-ls", "-C", str(path)).stdout
     return sorted(line.strip() for line in out.splitlines() if line.strip())
@@ -75,6 +102,14 @@ def delete(path, recursive=True):
         elif os.path.exists(p):
             os.remove(p)
         return
+    if is_s3(path):
+        c, split = _s3()
+        b, k = split(path)
+        c.delete(b, k)
+        if recursive:
+            for key in c.list(b, k.rstrip("/") + "/")[0]:
+                c.delete(b, key)
+        return
     _remote_only(path)
     _hdfs("-rm", "-f", "-r" if recursive else "", str(path))
 
@@ -84,6 +119,12 @@ def get_remote_file_to_local(remote_path, local, over_write=False):
         raise FileExistsError(local)
     if is_local_path(remote_path):
         shutil.copyfile(local_path(remote_path), local)
+        return
+    if is_s3(remote_path):
+        c, split = _s3()
+        data = c.get(*split(remote_path))
+        with open(local, "wb") as f:
+            f.write(data)
         return
     _remote_only(remote_path)
     _hdfs("-get", "-f" if over_write else "", str(remote_path), local)
@@ -97,6 +138,14 @@ def put_local_file_to_remote(local, remote_path, over_write=False):
         d = os.path.dirname(os.path.abspath(dst))
         os.makedirs(d, exist_ok=True)
         shutil.copyfile(local, dst)
+        return
+    if is_s3(remote_path):
+        c, split = _s3()
+        b, k = split(remote_path)
+        if not over_write and c.head(b, k) is not None:
+            raise FileExistsError(str(remote_path))
+        with open(local, "rb") as f:
+            c.put(b, k, f.read())
         return
     _remote_only(remote_path)
     _hdfs("-put", "-f" if over_write else "", local, str(remote_path))
