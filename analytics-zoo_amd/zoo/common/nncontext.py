@@ -234,7 +234,31 @@ def init_spark_on_local(cores=2, conf=None, python_location=None, spark_log_leve
     return init_nncontext(conf)
 
 
-def init_spark_on_yarn(*args, **kwargs):
-    """YARN is not part of the MI355X deployment model; use torchrun / the zoo launcher."""
-    raise NotImplementedError("init_spark_on_yarn: launch one process per GPU with "
-                              "`python -m torch.distributed.run` and call init_nncontext() instead")
+def init_spark_on_yarn(hadoop_conf=None, conda_name=None, num_executors=2, executor_cores=4,
+                       executor_memory="2g", driver_memory="1g", driver_cores=4, extra_executor_memory_for_ray=None,
+                       extra_python_lib=None, penv_archive=None, additional_archive=None, hadoop_user_name="root",
+                       spark_yarn_archive=None, spark_log_level="WARN", redirect_spark_log=True, jars=None,
+                       conf=None, **kwargs):
+    """Reference launcher (Py/common/nncontext.py:43-170). There is no YARN/JVM tier on an
+    MI355X node: an application's executors are the ranks of a torch.distributed job (one
+    process per GPU). Inside a launched job (``WORLD_SIZE`` set by
+    ``zoo.common.launcher`` / torchrun) this joins it; otherwise it starts the local
+    single-process context. The requested executor shape is recorded on the context
+    (``ctx.executor_request``) so scripts can hand it to ``zoo.common.launcher.launch``
+    (``num_executors`` -> ranks, ``executor_cores`` -> OMP threads per rank)."""
+    if "WORLD_SIZE" not in os.environ:
+        log.warning("init_spark_on_yarn: no YARN here; running in-process. Start %d ranks with "
+                    "`python -m zoo.common.launcher --nproc-per-node %d <script>` for a distributed job",
+                    num_executors, num_executors)
+    os.environ.setdefault("OMP_NUM_THREADS", str(int(executor_cores)))
+    ctx = init_nncontext(conf)
+    ctx.executor_request = {"num_executors": int(num_executors), "executor_cores": int(executor_cores),
+                            "executor_memory": executor_memory, "driver_memory": driver_memory,
+                            "conda_name": conda_name, "hadoop_conf": hadoop_conf}
+    return ctx
+
+
+def init_spark_standalone(num_executors=1, executor_cores=2, conf=None, **kwargs):
+    """Standalone-cluster launcher of later reference versions: same mapping as
+    :func:`init_spark_on_yarn`."""
+    return init_spark_on_yarn(num_executors=num_executors, executor_cores=executor_cores, conf=conf)
