@@ -104,6 +104,45 @@ __global__ __launch_bounds__(256) void act_kernel(const T* __restrict__ x, const
   }
 }
 
+// 8 elements per thread with 16-byte loads/stores (n % 8 == 0, 16-byte aligned pointers)
+template <typename T>
+ZOO_DEV void ld8(const T* p, size_t i8, float* v) {
+  if constexpr (sizeof(T) == 4) {
+    const float4 a = reinterpret_cast<const float4*>(p)[2 * i8], b = reinterpret_cast<const float4*>(p)[2 * i8 + 1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+    unpack8(reinterpret_cast<const uint4*>(p)[i8], v);
+  }
+}
+template <typename T>
+ZOO_DEV void st8(T* p, size_t i8, const float* v) {
+  if constexpr (sizeof(T) == 4) {
+    reinterpret_cast<float4*>(p)[2 * i8] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(p)[2 * i8 + 1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    reinterpret_cast<uint4*>(p)[i8] = pack8(v);
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void act_kernel_v8(const T* __restrict__ x, const T* __restrict__ dy,
+                                                     T* __restrict__ out, size_t n8, int a, float alpha) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    float v[8];
+    ld8(x, i, v);
+    if (dy) {
+      float d[8];
+      ld8(dy, i, d);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = d[e] * act_d(v[e], a, alpha);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = act_f(v[e], a, alpha);
+    }
+    st8(out, i, v);
+  }
+}
+
 ZOO_DEV uint32_t pw_fmix(uint32_t h) {
   h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
   return h;
@@ -243,6 +282,18 @@ using namespace zoo;
 
 extern "C" hipError_t zoo_act(const void* x, const void* dy, void* out, size_t n, int f32, int a, float alpha,
                               hipStream_t st) {
+  const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
+                    reinterpret_cast<uintptr_t>(out)) & 15) == 0;
+  if (n % 8 == 0 && al) {
+    const size_t n8 = n / 8;
+    if (f32)
+      hipLaunchKernelGGL(act_kernel_v8<float>, dim3(pw_grid(n8)), dim3(256), 0, st, (const float*)x,
+                         (const float*)dy, (float*)out, n8, a, alpha);
+    else
+      hipLaunchKernelGGL(act_kernel_v8<bf16_t>, dim3(pw_grid(n8)), dim3(256), 0, st, (const bf16_t*)x,
+                         (const bf16_t*)dy, (bf16_t*)out, n8, a, alpha);
+    return hipGetLastError();
+  }
   if (f32)
     hipLaunchKernelGGL(act_kernel<float>, dim3(pw_grid(n)), dim3(256), 0, st, (const float*)x, (const float*)dy,
                        (float*)out, n, a, alpha);

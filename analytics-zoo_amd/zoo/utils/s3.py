@@ -66,6 +66,10 @@ class S3Error(IOError):
         self.status = status
 
 
+class S3ConfigError(RuntimeError):
+    pass
+
+
 class S3Client:
     def __init__(self, endpoint=None, region=None, access_key=None, secret_key=None, session_token=None,
                  timeout=60):
@@ -81,6 +85,9 @@ class S3Client:
         self.timeout = timeout
 
     def _request(self, method, bucket, key="", query=None, body=b"", extra_headers=None, what="request"):
+        if not self.access_key and not (os.environ.get("ZOO_S3_ENDPOINT") or os.environ.get("AWS_ENDPOINT_URL")):
+            raise S3ConfigError("s3:// paths need AWS_ACCESS_KEY_ID / AWS_SECRET_ACCESS_KEY (and ZOO_S3_ENDPOINT "
+                                "or AWS_ENDPOINT_URL for S3-compatible stores)")
         query = dict(query or {})
         uri = "/" + _uri_encode(bucket) + ("/" + _uri_encode(key) if key else "")
         payload_hash = hashlib.sha256(body).hexdigest()

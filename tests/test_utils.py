@@ -44,8 +44,16 @@ def test_remote_scheme_without_client_is_explicit(monkeypatch):
     monkeypatch.setenv("PATH", "")
     with pytest.raises(NotImplementedError):
         zfile.exists("hdfs://namenode:9000/x")
-    with pytest.raises(NotImplementedError):
+    monkeypatch.delenv("AWS_ACCESS_KEY_ID", raising=False)
+    monkeypatch.delenv("ZOO_S3_ENDPOINT", raising=False)
+    monkeypatch.delenv("AWS_ENDPOINT_URL", raising=False)
+    from zoo.utils import s3
+    s3.reset_client()
+    with pytest.raises(s3.S3ConfigError, match="AWS_ACCESS_KEY_ID"):   # s3 needs credentials, fails fast
         zfile.exists("s3://bucket/x")
+    s3.reset_client()
+    with pytest.raises(NotImplementedError):
+        zfile.exists("gs://bucket/x")
 
 
 def test_common_utils_save_load_and_carriers(tmp_path):
