@@ -61,6 +61,7 @@ ZOO_DEV bf16x8 w2_frag(const char* blk, int lo_off, int hi_off) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+template <bool PP>
 __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __restrict__ dY,
                                                             const bf16_t* __restrict__ X, float* __restrict__ dW,
                                                             float* __restrict__ part, W2Geom g,
@@ -163,6 +164,12 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
     }
   }
   __builtin_amdgcn_s_barrier();
+  // PP (ping-pong): the two wave rows run one barrier apart, so on every SIMD (one wave of
+  // each row) one wave issues its LDS reads / DMA while the other runs its MFMAs; every
+  // phase then has a second barrier after its MFMAs (cdna_hip_programming.md §5 256²
+  // template). Hazards shift by half a phase: reads still come >= 1 barrier after every
+  // wave's retiring wait, restaging stays >= 1.5 phases after the last read.
+  if (PP && wm == 1) __builtin_amdgcn_s_barrier();
 
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
@@ -206,8 +213,10 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
           for (int j = 0; j < 2; ++j)
             acc[qa][qb][i][j] = mfma16(fa[i][kb], qb ? fb1[j][kb] : fb0[j][kb], acc[qa][qb][i][j]);
       __builtin_amdgcn_s_setprio(0);
+      if (PP) __builtin_amdgcn_s_barrier();
     }
   }
+  if (PP && wm == 0) __builtin_amdgcn_s_barrier();
 
   // ---- epilogue ----
   // fragment (qa, qb, i, j) reg r <-> dW row n0 + wm*128 + qa*64 + i*16 + 4*(lane>>4) + r,
@@ -322,12 +331,23 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
   const size_t smem = 4 * 2 * W2_HALF;  // 2 buffers x (A, B) x 2 halves = 128 KiB
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
-                        (int)smem);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
-  hipLaunchKernelGGL(wgrad256_kernel, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                     (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
+  static const bool pp = [] {
+    // measured neutral on the BERT / ResNet shapes (tools/wgrad_bench.py A/B: -3..+3 %): opt-in
+    const char* e = getenv("ZOO_W256_PINGPONG");
+    return e ? atoi(e) != 0 : false;
+  }();
+  if (pp)
+    hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
+  else
+    hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
   if (g.splits > 1) {
     const size_t total = (size_t)tiles * 8 * 32 * 64;
     hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);
