@@ -218,6 +218,14 @@ class KerasNet(Layer):
         return self.predict(x)
 
     # ------------------------------------------------------------------ misc
+    def save_to_keras2(self, json_path=None, hdf5_path=None):
+        """KerasNet.saveToKeras2: Keras 2 definition json and/or full-model HDF5 file
+        (zoo.pipeline.api.keras.keras_import.save_keras2)."""
+        from zoo.pipeline.api.keras.keras_import import save_keras2
+        return save_keras2(self, json_path, hdf5_path)
+
+    saveToKeras2 = save_to_keras2
+
     def get_layer(self, name):
         for m in self.modules():
             if isinstance(m, Layer) and m.name == name:

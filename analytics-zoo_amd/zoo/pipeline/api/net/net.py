@@ -6,7 +6,7 @@
   Net.load_onnx(path)            ONNX ModelProto -> GraphNet
   Net.load_torch(path)           TorchScript -> TorchNet
   Net.load_tf(path, in, out)     TF frozen graph / SavedModel -> TFNet
-  Net.load_keras                 not available (no Keras runtime here)
+  Net.load_keras(json, hdf5)     Keras 1.2 / 2.x definition + HDF5 weights -> zoo Keras model
 """
 
 
@@ -45,5 +45,8 @@ class Net:
 
     @staticmethod
     def load_keras(json_path=None, hdf5_path=None, by_name=False):
-        raise NotImplementedError("Keras 1.2 json/hdf5 import needs h5py/keras; rebuild the model with "
-                                  "zoo.pipeline.api.keras layers or go through ONNX")
+        """Keras model definition (json, or the model_config of a full-model HDF5 file) and
+        HDF5 weights -> zoo Keras Sequential / Model (zoo.pipeline.api.keras.keras_import;
+        HDF5 read by the built-in codec, no h5py)."""
+        from zoo.pipeline.api.keras.keras_import import load_keras
+        return load_keras(json_path, hdf5_path, by_name)
