@@ -4,7 +4,7 @@
   Net.load_bigdl(path, weights)  BigDL protobuf ``.model`` -> GraphNet
   Net.load_caffe(def, model)     Caffe prototxt + caffemodel -> GraphNet
   Net.load_onnx(path)            ONNX ModelProto -> GraphNet
-  Net.load_torch(path)           TorchScript -> TorchNet
+  Net.load_torch(path)           TorchScript or Lua Torch7 .t7 -> TorchNet
   Net.load_tf(path, in, out)     TF frozen graph / SavedModel -> TFNet
   Net.load_keras(json, hdf5)     Keras 1.2 / 2.x definition + HDF5 weights -> zoo Keras model
 """
@@ -33,6 +33,14 @@ class Net:
 
     @staticmethod
     def load_torch(path, bigdl_type="float"):
+        """TorchScript archive -> TorchNet; a Lua Torch7 ``.t7`` nn model (Net.loadTorch,
+        BigDL TorchFile) -> torch module rebuilt from the decoded objects."""
+        with open(path, "rb") as f:
+            magic = f.read(4)
+        if magic[:2] != b"PK":   # not a zip archive: Torch7 binary serialisation
+            from zoo.pipeline.api.net.torch7 import load_torch7
+            from zoo.pipeline.api.net.torch_net import TorchNet
+            return TorchNet.from_pytorch(load_torch7(path))
         from zoo.pipeline.api.net.torch_net import TorchNet
         return TorchNet.load(path)
 
