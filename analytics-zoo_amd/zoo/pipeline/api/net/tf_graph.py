@@ -347,8 +347,46 @@ def _hw(lst, nhwc):
     return (lst[1], lst[2]) if nhwc else (lst[2], lst[3])
 
 
-def _conv2d(node, x, w, depthwise=False):
+def _conv2d_native(g, node, x, w):
+    """NHWC Conv2D on the implicit-GEMM MFMA kernel (bf16 compute, fp32 out); the HWIO filter
+    is packed once per weight version."""
+    from zoo import ops
+    kh, kw, cin, cout = w.shape
+    strides = node.attr.get("strides", [1, 1, 1, 1])
+    dil = node.attr.get("dilations", [1, 1, 1, 1])
+    sh, sw, dh, dw = strides[1], strides[2], dil[1], dil[2]
+    cin_p = cin if cin % 8 == 0 else (4 if cin <= 4 else ops.ceil8(cin))
+    k_p = ops.ceil8(cout)
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    packed = g._packed.get(key)
+    if packed is None:
+        w4 = torch.zeros(k_p, kh, kw, cin_p, device=x.device)
+        w4[:cout, :, :, :cin] = w.float().permute(3, 0, 1, 2)
+        packed = g._packed[key] = ops.pack_weight(w4)
+    xn = x
+    pad = node.s("padding", "VALID")
+    pt = pb_ = pl = pr = 0
+    if pad == "SAME":
+        pt, pb_ = _same_pad(x.shape[1], kh, sh, dh)
+        pl, pr = _same_pad(x.shape[2], kw, sw, dw)
+    elif pad == "EXPLICIT":
+        ep = node.attr.get("explicit_paddings", [0] * 8)[2:6]
+        pt, pb_, pl, pr = ep
+    sym = pt == pb_ and pl == pr
+    if not sym or cin_p != cin:
+        xn = F.pad(xn, (0, cin_p - cin, 0 if sym else pl, 0 if sym else pr, 0 if sym else pt, 0 if sym else pb_))
+    ph, pw = (pt, pl) if sym else (0, 0)
+    g.native_calls += 1
+    y = ops.conv2d_nhwc(xn.to(torch.bfloat16).contiguous(), packed, None, kernel=(kh, kw), stride=(sh, sw),
+                        pad=[ph, pw], dil=(dh, dw), out_f32=True)
+    return y[..., :cout]
+
+
+def _conv2d(node, x, w, depthwise=False, g=None):
     nhwc = _nhwc(node)
+    if (g is not None and g.native_bf16 and x.is_cuda and not depthwise and nhwc and w.dim() == 4
+            and x.shape[-1] == w.shape[2]):
+        return _conv2d_native(g, node, x, w)
     strides = node.attr.get("strides", [1, 1, 1, 1])
     dil = node.attr.get("dilations", [1, 1, 1, 1])
     sh, sw = _hw(strides, nhwc)
@@ -505,6 +543,11 @@ class TFGraph:
     def __init__(self, nodes, values):
         self.nodes = {n.name: n for n in nodes}
         self.values = values  # name -> torch tensor (Const / variables)
+        # native bf16 execution of Conv2D / MatMul on the GPU (MFMA kernels; opt-in because the
+        # graph's own dtype is fp32): TFNet.use_native_kernels(True) or ZOO_TF_NATIVE_BF16=1
+        self.native_bf16 = os.environ.get("ZOO_TF_NATIVE_BF16", "0") == "1"
+        self._packed = {}
+        self.native_calls = 0
 
     def needed(self, fetches, feeds=()):
         feed_nodes = {split_name(f)[0] for f in feeds}
@@ -621,6 +664,10 @@ def _matmul(g, node, a, b):
         a = a.transpose(-1, -2)
     if node.attr.get("transpose_b", False):
         b = b.transpose(-1, -2)
+    if g is not None and g.native_bf16 and a.is_cuda and a.dim() == 2 and b.dim() == 2 and a.is_floating_point():
+        from zoo import ops
+        g.native_calls += 1
+        return ops.linear(a.float(), b.t().float().contiguous()).float()
     return torch.matmul(a, b.to(a.dtype))
 
 
@@ -873,7 +920,7 @@ _OPS = {
     "BiasAddGrad": _bias_add_grad,
     "MatMul": _matmul, "BatchMatMul": _batch_matmul, "BatchMatMulV2": _batch_matmul,
     "BiasAdd": _bias_add, "BiasAddV1": _bias_add,
-    "Conv2D": lambda g, n, x, w: _conv2d(n, x, w),
+    "Conv2D": lambda g, n, x, w: _conv2d(n, x, w, g=g),
     "DepthwiseConv2dNative": lambda g, n, x, w: _conv2d(n, x, w, depthwise=True),
     "MaxPool": lambda g, n, x: _pool(n, x, "max"), "AvgPool": lambda g, n, x: _pool(n, x, "avg"),
     "FusedBatchNorm": _fused_bn, "FusedBatchNormV2": _fused_bn, "FusedBatchNormV3": _fused_bn, "LRN": _lrn,

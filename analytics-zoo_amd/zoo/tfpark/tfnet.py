@@ -109,6 +109,12 @@ class TFNet(nn.Module):
                 self._param_names[n.name] = pn
         self._graph = graph
 
+    def use_native_kernels(self, enable=True):
+        """Run the graph's Conv2D / MatMul on the native MFMA kernels in bf16 (fp32 in/out) on
+        the GPU; the default is exact fp32 execution with the PyTorch ops."""
+        self._graph.native_bf16 = bool(enable)
+        return self
+
     @staticmethod
     def _initial_value(graph, nodes, var):
         """A variable missing from the checkpoint takes the value of its
