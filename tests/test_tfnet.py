@@ -208,19 +208,6 @@ def test_export_tf_freezes_trained_variables(tmp_path):
         export_tf(object(), str(tmp_path / "bad"), [], [])
 
 
-@pytest.mark.gpu
-def test_tfnet_native_kernels_bf16(gpu):
-    """use_native_kernels(): the graph's MatMul runs on the native GEMM path in bf16."""
-    net = TFNet.from_saved_model(os.path.join(R, "saved-model-resource"), inputs=["flatten_input:0"],
-                                 outputs=["dense_2/Softmax:0"])
-    x = np.random.rand(8, 28, 28, 1).astype(np.float32)
-    ref = net.forward_numpy(x)
-    net = net.to(gpu).use_native_kernels(True)
-    out = net.forward_numpy(x)
-    assert net._graph.native_calls > 0
-    np.testing.assert_allclose(out, ref, atol=2e-2)
-
-
 def test_tf_conv2d_native_path_geometry_on_cpu_reference():
     """The SAME / VALID / strided Conv2D geometry the native path reproduces (CPU check of
     the padding arithmetic it shares with the reference path)."""
@@ -234,20 +221,3 @@ def test_tf_conv2d_native_path_geometry_on_cpu_reference():
         exp = (9 + st - 1) // st if pad == "SAME" else (9 - 3) // st + 1
         assert y.shape == (2, exp, exp, 5)
 
-
-@pytest.mark.gpu
-def test_tf_conv2d_native_matches_fp32(gpu):
-    import torch
-    from zoo.pipeline.api.net.tf_graph import Node, TFGraph, _conv2d
-    g = TFGraph([], {})
-    g.native_bf16 = True
-    torch.manual_seed(0)
-    x = torch.randn(2, 9, 9, 3)
-    w = torch.randn(3, 3, 3, 16) * 0.2
-    for pad, st in (("SAME", 1), ("SAME", 2), ("VALID", 2)):
-        n = Node("c", "Conv2D", [], [], {"strides": [1, st, st, 1], "padding": pad, "data_format": "NHWC"})
-        ref = _conv2d(n, x, w)
-        out = _conv2d(n, x.to(gpu), w.to(gpu), g=g).float().cpu()
-        assert out.shape == ref.shape
-        assert (out - ref).abs().max().item() < 5e-2 * ref.abs().max().item()
-    assert g.native_calls == 3
