@@ -263,8 +263,18 @@ __global__ __launch_bounds__(256) void wgrad256_fold_kernel(const float* __restr
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
   const f32x4* p = reinterpret_cast<const f32x4*>(part) + idx;
-  f32x4 s = p[0];
-  for (int sp = 1; sp < g.splits; ++sp) s += p[(size_t)sp * total];
+  // 4 independent partial sums keep 4 loads in flight (the splits are summed in a fixed
+  // order per lane, so the result stays deterministic)
+  f32x4 s = p[0], s1 = f32x4{0.f, 0.f, 0.f, 0.f}, s2 = s1, s3 = s1;
+  int sp = 1;
+  for (; sp + 3 < g.splits; sp += 4) {
+    s += p[(size_t)sp * total];
+    s1 += p[(size_t)(sp + 1) * total];
+    s2 += p[(size_t)(sp + 2) * total];
+    s3 += p[(size_t)(sp + 3) * total];
+  }
+  for (; sp < g.splits; ++sp) s += p[(size_t)sp * total];
+  s += (s1 + s2) + s3;
   const int tile = (int)(idx / per_tile);
   const int rem = (int)(idx - (size_t)tile * per_tile);
   const int w = rem >> 11, f = (rem >> 6) & 31, lane = rem & 63;

@@ -348,10 +348,12 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.Ktot = R * S * g.C;
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
-  // 1x1 stride-1 convs with >= 256 input and output channels are plain GEMMs: the 256x256-tile
-  // kernel (wgrad256.hip) is 1.3-1.6x the implicit-GEMM wgrad there (tools/wgrad_bench.py --resnet)
+  // 1x1 stride-1 convs with >= 128 input and output channels (and up to 2^18 pixels) are plain
+  // GEMMs where the 256x256-tile kernel (wgrad256.hip) beats the implicit-GEMM wgrad
+  // (tools/wgrad_bench.py --resnet: 1.1-1.6x; at 802816 pixels the 128-row tiles win)
   static const bool use256 = env_flag("ZOO_WGRAD256", true);
-  if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= 256 && g.C >= 256 &&
+  if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= 128 && g.C >= 128 &&
+      g.M <= (1 << 18) &&
       x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
     linear_wgrad(dy.view({(int64_t)g.M, g.K}), x.view({(int64_t)g.M, g.C}), dw);
     return;
