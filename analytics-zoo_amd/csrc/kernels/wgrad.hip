@@ -299,11 +299,19 @@ __global__ __launch_bounds__(256) void wgrad_fold1_kernel(const float* __restric
   if (i >= n4) return;
   const int s0 = blockIdx.y * kFoldGroup, s1 = min(splits, s0 + kFoldGroup);
   const float4* p = reinterpret_cast<const float4*>(part) + i;
-  float4 s = p[(size_t)s0 * n4];
-  for (int sp = s0 + 1; sp < s1; ++sp) {
+  // two interleaved partial sums keep loads in flight (fixed order: deterministic)
+  float4 s = p[(size_t)s0 * n4], t = make_float4(0.f, 0.f, 0.f, 0.f);
+  int sp = s0 + 1;
+  for (; sp + 1 < s1; sp += 2) {
+    const float4 v = p[(size_t)sp * n4], u = p[(size_t)(sp + 1) * n4];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+  }
+  if (sp < s1) {
     const float4 v = p[(size_t)sp * n4];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
+  s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
   reinterpret_cast<float4*>(lvl1)[(size_t)blockIdx.y * n4 + i] = s;
 }
 
@@ -314,11 +322,18 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const float* __restrict
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const int k = (int)(i / q), c4 = (int)(i - (size_t)k * q) * 4;
     const float4* p = reinterpret_cast<const float4*>(part) + i;
-    float4 s = p[0];
-    for (int sp = 1; sp < splits; ++sp) {
+    float4 s = p[0], t = make_float4(0.f, 0.f, 0.f, 0.f);
+    int sp = 1;
+    for (; sp + 1 < splits; sp += 2) {
+      const float4 v = p[(size_t)sp * n4], u = p[(size_t)(sp + 1) * n4];
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    if (sp < splits) {
       const float4 v = p[(size_t)sp * n4];
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
     }
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
     float* d = dW + (size_t)k * ldw + c4;
     d[0] += s.x; d[1] += s.y; d[2] += s.z; d[3] += s.w;
   }
