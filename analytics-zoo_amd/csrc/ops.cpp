@@ -271,6 +271,13 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   float* const stat_dst = sp ? sp : bs.sums;
   torch::Tensor part;
   const int tiles_m = (g.M + 127) / 128;  // IG_BM
+  // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
+  // the atomics go straight into the final 2K floats, no slot fold launch needed
+  static const int slot_min_tiles = [] {
+    const char* e = getenv("ZOO_STAT_SLOT_MIN_TILES");
+    return e ? atoi(e) : 512;
+  }();
+  if (g.stat_slots == zoo::kStatSlots && tiles_m <= slot_min_tiles) g.stat_slots = 0;
   if (stat_dst && stats_partial()) {
     part = torch::empty({(int64_t)tiles_m, 2 * (int64_t)K}, x.options().dtype(at::kFloat));
     g.stat_slots = zoo::kStatPartial;
