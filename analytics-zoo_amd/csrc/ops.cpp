@@ -26,6 +26,9 @@ hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, in
 hipError_t zoo_flip_weights_batched(const void*, int, int, hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
 int zoo_wgrad_plan(WgradGeom*);
+hipError_t zoo_bmm(const void*, const void*, void*, const long*, int, int, hipStream_t);
+hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t);
+hipError_t zoo_row_l2norm(const void*, const void*, const void*, void*, long, int, int, float, hipStream_t);
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
@@ -332,6 +335,73 @@ void flip_weights_batched(torch::Tensor table, int n, int nblocks) {
 }
 
 int flip_desc_ints() { return (int)(sizeof(zoo::FlipDesc) / sizeof(int)); }
+
+// C[b] = A[b] (M x K) * B[b]^T where B is given as [Bt, N, K]: any strides (views from
+// transpose / expand), at least one of each operand's two inner dims contiguous.
+torch::Tensor bmm_nt(torch::Tensor a, torch::Tensor b, bool out_bf16) {
+  TORCH_CHECK(a.is_cuda() && b.is_cuda(), "bmm: GPU tensors expected");
+  TORCH_CHECK(a.scalar_type() == at::kBFloat16 && b.scalar_type() == at::kBFloat16, "bmm: bf16 operands");
+  TORCH_CHECK(a.dim() == 3 && b.dim() == 3, "bmm: [B, M, K] x [B, N, K] expected");
+  TORCH_CHECK(a.size(0) == b.size(0) && a.size(2) == b.size(2), "bmm: batch / K mismatch");
+  const int64_t B = a.size(0), M = a.size(1), K = a.size(2), N = b.size(1);
+  TORCH_CHECK(B < 65536 && M < (1 << 30) && N < (1 << 30) && K < (1 << 30), "bmm: size out of range");
+  TORCH_CHECK((a.stride(2) == 1 || a.stride(1) == 1 || M == 1) && (b.stride(2) == 1 || b.stride(1) == 1 || N == 1),
+              "bmm: one inner dim of each operand must be contiguous");
+  auto c = torch::empty({B, M, N}, a.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat));
+  if (c.numel() == 0) return c;
+  if (K == 0) return c.zero_();
+  auto al16 = [](const torch::Tensor& t) {
+    const bool kc = t.stride(2) == 1;
+    const int64_t other = kc ? t.stride(1) : t.stride(2);
+    return reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0 && other % 8 == 0 && t.stride(0) % 8 == 0;
+  };
+  const int vec = al16(a) && al16(b) ? 1 : 0;
+  // a row-contiguous operand with stride(2) == 1 too (size-1 dims) counts as k-contiguous
+  const long geom[12] = {(long)B, (long)M, (long)N, (long)K, (long)a.stride(0), (long)a.stride(1),
+                         (long)a.stride(2), (long)b.stride(0), (long)b.stride(1), (long)b.stride(2),
+                         (long)c.stride(0), (long)c.stride(1)};
+  check_hip(zoo_bmm(a.data_ptr(), b.data_ptr(), c.data_ptr(), geom, out_bf16 ? 1 : 0, vec, cur_stream()), "bmm");
+  return c;
+}
+
+// reduce over the last (contiguous) dim: op 0 sum, 1 mean, 2 max, 3 min, 4 sum of squares
+torch::Tensor row_reduce(torch::Tensor x, int64_t op) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 1, "row_reduce: contiguous GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "row_reduce: fp32 or bf16");
+  TORCH_CHECK(op >= 0 && op <= 4, "row_reduce: op");
+  const int64_t cols = x.size(-1);
+  TORCH_CHECK(cols > 0 && cols < (1LL << 31), "row_reduce: last dim size");
+  auto sizes = x.sizes().vec();
+  sizes.pop_back();
+  auto out = torch::empty(sizes, x.options().dtype(at::kFloat));
+  const int64_t rows = x.numel() / cols;
+  if (rows == 0) return out;
+  check_hip(zoo_row_reduce(x.data_ptr(), out.data_ptr<float>(), rows, (int)cols, x.scalar_type() == at::kFloat,
+                           (int)op, cur_stream()), "row_reduce");
+  return out;
+}
+
+// L2-normalise rows of the last dim (dy/y given: the backward)
+torch::Tensor row_l2norm(torch::Tensor x, c10::optional<torch::Tensor> dy, c10::optional<torch::Tensor> y,
+                         double eps) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous() && x.dim() >= 1, "row_l2norm: contiguous GPU tensor");
+  TORCH_CHECK(x.scalar_type() == at::kFloat || x.scalar_type() == at::kBFloat16, "row_l2norm: fp32 or bf16");
+  const bool bwd = dy.has_value() && dy->defined();
+  if (bwd) {
+    TORCH_CHECK(y.has_value() && y->defined(), "row_l2norm backward needs y");
+    TORCH_CHECK(dy->sizes() == x.sizes() && y->sizes() == x.sizes() && dy->is_contiguous() && y->is_contiguous() &&
+                    dy->scalar_type() == x.scalar_type() && y->scalar_type() == x.scalar_type(),
+                "row_l2norm: dy / y must match x");
+  }
+  auto out = torch::empty_like(x);
+  const int64_t cols = x.size(-1);
+  const int64_t rows = cols ? x.numel() / cols : 0;
+  if (rows == 0) return out;
+  check_hip(zoo_row_l2norm(x.data_ptr(), bwd ? dy->data_ptr() : nullptr, bwd ? y->data_ptr() : nullptr,
+                           out.data_ptr(), rows, (int)cols, x.scalar_type() == at::kFloat, (float)eps, cur_stream()),
+            "row_l2norm");
+  return out;
+}
 
 void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw);
 
@@ -1743,6 +1813,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("linear_wgrad", &linear_wgrad);
+  m.def("bmm_nt", &bmm_nt);
+  m.def("row_reduce", &row_reduce);
+  m.def("row_l2norm", &row_l2norm);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("causal"),
         py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("nms_sorted", &nms_sorted);

@@ -53,8 +53,13 @@ def _apply(fn, *args):
     return fn(*args)
 
 
+def _reduce(op, axis, keep):
+    from zoo.ops.reduce import reduce   # native row reductions on the GPU (HK14)
+    return lambda t: reduce(t, axis, op, keep)
+
+
 def mean(x, axis=0, keepDims=False):  # noqa: N803 - reference name
-    return _apply(lambda t: t.mean(dim=axis, keepdim=keepDims), x)
+    return _apply(_reduce("mean", axis, keepDims), x)
 
 
 def abs(x):  # noqa: A001 - reference name
@@ -62,7 +67,7 @@ def abs(x):  # noqa: A001 - reference name
 
 
 def sum(x, axis=0, keepDims=False):  # noqa: A001,N803
-    return _apply(lambda t: t.sum(dim=axis, keepdim=keepDims), x)
+    return _apply(_reduce("sum", axis, keepDims), x)
 
 
 def clip(x, min, max):  # noqa: A002
@@ -129,7 +134,8 @@ def stack(inputs, axis=1):
 
 
 def l2_normalize(x, axis):
-    return _apply(lambda t: t / torch.sqrt(torch.clamp((t * t).sum(dim=axis, keepdim=True), min=EPS)), x)
+    from zoo.ops.reduce import l2_normalize as _l2   # native row kernel on the GPU (HK14)
+    return _apply(lambda t: _l2(t, axis, EPS), x)
 
 
 def mm(x, y, axes=None):
@@ -142,7 +148,8 @@ def mm(x, y, axes=None):
                 a = a.transpose(ax_a, a.dim() - 1)
             if ax_b != b.dim() - 2:
                 b = b.transpose(ax_b, b.dim() - 2)
-        return torch.matmul(a, b)
+        from zoo.ops.bmm import bmm   # native batched GEMM on the GPU (HK2)
+        return bmm(a, b)
     return _apply(f, x, y)
 
 
@@ -159,7 +166,8 @@ def batch_dot(x, y, axes=1, normalize=False):
             return (a * b).sum(dim=1, keepdim=True)
         a2 = a.transpose(axes[0], -1) if axes[0] != a.dim() - 1 else a
         b2 = b.transpose(axes[1], 1) if axes[1] != 1 else b
-        return torch.matmul(a2, b2)
+        from zoo.ops.bmm import bmm   # native batched GEMM on the GPU (HK2)
+        return bmm(a2, b2)
     return _apply(f, x, y)
 
 

@@ -186,7 +186,49 @@ class ConvLSTM2D(Layer):
             return (None, s[1], self.nb_filter, h, w)
         return (None, self.nb_filter, h, w)
 
+    def _packed(self, w):
+        """[4f, c, kh, kw] torch-layout weight -> the native kernels' packed [K8, ldb] weight
+        (differentiable: the conv's weight gradient flows back to the parameter)."""
+        K, C, R, S = w.shape
+        cp = C if C % 8 == 0 else (4 if C <= 4 else ops.ceil8(C))
+        w4 = F.pad(w.permute(0, 2, 3, 1), (0, cp - C, 0, 0, 0, 0, 0, ops.ceil8(K) - K))
+        return ops.pack_weight(w4), cp
+
+    def _call_native(self, x):
+        """GPU path: input and recurrent convolutions on the implicit-GEMM MFMA kernel in
+        NHWC (bf16), gate math on the same tensors."""
+        B, T, C, H, W = x.shape
+        f = self.nb_filter
+        K = 4 * f
+        R, S = self.k
+        pad = (R // 2, S // 2)
+        wx, cpx = self._packed(self.Wx)
+        wh, cph = self._packed(self.Wh)
+        bias = F.pad(self.b, (0, ops.ceil8(K) - K)).float()
+        xn = x.reshape(B * T, C, H, W).permute(0, 2, 3, 1)
+        if cpx != C:
+            xn = F.pad(xn, (0, cpx - C))
+        xs = ops.conv2d_nhwc(xn, wx, bias, kernel=(R, S), stride=self.subsample, pad=pad, out_f32=True)[..., :K]
+        Ho, Wo = xs.shape[1], xs.shape[2]
+        xs = xs.reshape(B, T, Ho, Wo, K)
+        h = xs.new_zeros(B, Ho, Wo, f)
+        c = h.clone()
+        outs = []
+        for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):
+            hp = F.pad(h, (0, cph - f)) if cph != f else h
+            g = xs[:, t] + ops.conv2d_nhwc(hp, wh, None, kernel=(R, S), stride=(1, 1), pad=pad, out_f32=True)[..., :K]
+            i = apply_activation(g[..., :f], self.inner_activation)
+            fg = apply_activation(g[..., f:2 * f], self.inner_activation)
+            cc = apply_activation(g[..., 2 * f:3 * f], self.activation)
+            o = apply_activation(g[..., 3 * f:], self.inner_activation)
+            c = fg * c + i * cc
+            h = o * apply_activation(c, self.activation)
+            outs.append(h.permute(0, 3, 1, 2))
+        return torch.stack(outs, 1) if self.return_sequences else outs[-1]
+
     def call(self, x):
+        if x.is_cuda and (self.k[0] % 2 == 1 and self.k[1] % 2 == 1):
+            return self._call_native(x)
         B, T = x.shape[:2]
         pad = (self.k[0] // 2, self.k[1] // 2)
         xs = F.conv2d(x.reshape(B * T, *x.shape[2:]), self.Wx.to(x.dtype), self.b.to(x.dtype), self.subsample, pad)
