@@ -486,9 +486,12 @@ class Merge(Layer):
         if m == "concat":
             return torch.cat(xs, dim=self.concat_axis)
         if m == "dot":
-            return (xs[0] * xs[1]).sum(dim=-1, keepdim=True)
+            from zoo.ops.reduce import reduce   # native row reduction on the GPU (HK14)
+            return reduce(xs[0] * xs[1], -1, "sum", keepdim=True)
         if m == "cos":
-            return torch.nn.functional.cosine_similarity(xs[0], xs[1], dim=-1).unsqueeze(-1)
+            from zoo.ops.reduce import l2_normalize, reduce
+            a, b = l2_normalize(xs[0], -1, 1e-16), l2_normalize(xs[1], -1, 1e-16)
+            return reduce(a * b, -1, "sum", keepdim=True)
         raise ValueError("Unsupported merge mode %s" % m)
 
 
