@@ -28,6 +28,8 @@ hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*,
 int zoo_wgrad_plan(WgradGeom*);
 hipError_t zoo_bmm(const void*, const void*, void*, const long*, int, int, hipStream_t);
 hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t);
+hipError_t zoo_ssd_match(const float*, const int*, const float*, int, int, int, float, float, float, int, int*,
+                         float*, unsigned long long*, float*, long long*, hipStream_t);
 hipError_t zoo_row_l2norm(const void*, const void*, const void*, void*, long, int, int, float, hipStream_t);
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
@@ -401,6 +403,34 @@ torch::Tensor row_l2norm(torch::Tensor x, c10::optional<torch::Tensor> dy, c10::
                            out.data_ptr(), rows, (int)cols, x.scalar_type() == at::kFloat, (float)eps, cur_stream()),
             "row_l2norm");
   return out;
+}
+
+// SSD matching: gt [B, G, 5] (label, x1, y1, x2, y2), count [B] int32, priors [P, 4]
+// centre-size -> (loc_t [B, P, 4] fp32, conf_t [B, P] int64)
+std::vector<torch::Tensor> ssd_match(torch::Tensor gt, torch::Tensor count, torch::Tensor priors, double overlap,
+                                     double v0, double v1, int64_t bg_label) {
+  req(gt, at::kFloat, "gt");
+  req(priors, at::kFloat, "priors");
+  TORCH_CHECK(count.is_cuda() && count.scalar_type() == at::kInt && count.is_contiguous(), "ssd_match: count int32");
+  TORCH_CHECK(gt.dim() == 3 && gt.size(2) == 5 && priors.dim() == 2 && priors.size(1) == 4,
+              "ssd_match: gt [B, G, 5], priors [P, 4]");
+  TORCH_CHECK(count.numel() == gt.size(0), "ssd_match: count per image");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(priors.data_ptr()) % 16 == 0, "ssd_match: aligned priors");
+  const int B = gt.size(0), G = gt.size(1), P = priors.size(0);
+  TORCH_CHECK(B < 65536 && G < (1 << 20) && P < (1 << 30), "ssd_match: sizes");
+  auto o = gt.options();
+  auto loc_t = torch::empty({B, P, 4}, o);
+  auto conf_t = torch::empty({B, P}, o.dtype(at::kLong));
+  if (B == 0 || P == 0) return {loc_t, conf_t};
+  auto best_gt = torch::empty({B, P}, o.dtype(at::kInt));
+  auto best_iou = torch::empty({B, P}, o);
+  auto gt_best = torch::empty({B, std::max(G, 1)}, o.dtype(at::kLong));
+  check_hip(zoo_ssd_match(gt.data_ptr<float>(), count.data_ptr<int>(), priors.data_ptr<float>(), B, G, P,
+                          (float)overlap, (float)v0, (float)v1, (int)bg_label, best_gt.data_ptr<int>(),
+                          best_iou.data_ptr<float>(), reinterpret_cast<unsigned long long*>(gt_best.data_ptr()),
+                          loc_t.data_ptr<float>(), reinterpret_cast<long long*>(conf_t.data_ptr()), cur_stream()),
+            "ssd_match");
+  return {loc_t, conf_t};
 }
 
 void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw);
@@ -1814,6 +1844,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("embedding_bwd", &embedding_bwd);
   m.def("linear_wgrad", &linear_wgrad);
   m.def("bmm_nt", &bmm_nt);
+  m.def("ssd_match", &ssd_match);
   m.def("row_reduce", &row_reduce);
   m.def("row_l2norm", &row_l2norm);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("causal"),

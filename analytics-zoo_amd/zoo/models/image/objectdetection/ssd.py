@@ -288,16 +288,32 @@ class MultiBoxLoss(nn.Module):
         labels[best_gt_iou < self.overlap] = self.bg
         return encode(gt_boxes[best_gt], priors, self.var), labels
 
+    def match_native(self, targets, priors):
+        """All images at once on the GPU (csrc/kernels/detect.hip ssd_match, HK21)."""
+        from zoo.ops._native import native
+        dev = priors.device
+        G = max([int(t.shape[0]) for t in targets] + [1])
+        gt = torch.zeros(len(targets), G, 5, device=dev)
+        for i, t in enumerate(targets):
+            if t.shape[0]:
+                gt[i, :t.shape[0]] = t.to(dev).float()
+        count = torch.tensor([int(t.shape[0]) for t in targets], dtype=torch.int32, device=dev)
+        return native().ssd_match(gt, count, priors.float().contiguous(), float(self.overlap), float(self.var[0]),
+                                  float(self.var[2]), int(self.bg))
+
     def forward(self, loc, conf, priors, targets):
         """targets: list of [G, 5] (label, x1, y1, x2, y2) per image."""
         B, P, _ = loc.shape
-        loc_t, conf_t = [], []
-        for t in targets:
-            t = t.to(loc.device)
-            l, c = self.match(t[:, 1:], t[:, 0], priors)
-            loc_t.append(l)
-            conf_t.append(c)
-        loc_t, conf_t = torch.stack(loc_t), torch.stack(conf_t)
+        if loc.is_cuda and self.var[0] == self.var[1] and self.var[2] == self.var[3]:
+            loc_t, conf_t = self.match_native(targets, priors.to(loc.device))
+        else:
+            loc_t, conf_t = [], []
+            for t in targets:
+                t = t.to(loc.device)
+                l, c = self.match(t[:, 1:], t[:, 0], priors)
+                loc_t.append(l)
+                conf_t.append(c)
+            loc_t, conf_t = torch.stack(loc_t), torch.stack(conf_t)
         pos = conf_t != self.bg
         n_pos = pos.sum().clamp(min=1).float()
         loss_l = F.smooth_l1_loss(loc[pos].float(), loc_t[pos], reduction="sum")

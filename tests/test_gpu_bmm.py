@@ -98,3 +98,28 @@ def test_native_l2_normalize_fwd_bwd():
         (gn,) = torch.autograd.grad(out, x, g)
         assert torch.allclose(gn, gr, atol=1e-4)
     assert torch.allclose(A.sum(x, axis=2), x.sum(2), atol=1e-4)
+
+
+@pytest.mark.gpu
+def test_ssd_native_matching_matches_reference():
+    """MultiBoxLoss matching on the native kernel vs the per-image torch matcher."""
+    from zoo.models.image.objectdetection.ssd import MultiBoxLoss, SSDConfig, prior_boxes
+    torch.manual_seed(6)
+    priors = prior_boxes(SSDConfig()).float()
+    crit = MultiBoxLoss(num_classes=21)
+    targets = []
+    for n in (3, 0, 7, 1):
+        xy = torch.rand(n, 2) * 0.7
+        wh = torch.rand(n, 2) * 0.3 + 0.02
+        lab = torch.randint(1, 21, (n, 1)).float()
+        targets.append(torch.cat([lab, xy, xy + wh], 1))
+    ref_l, ref_c = [], []
+    for t in targets:
+        l, c = crit.match(t[:, 1:], t[:, 0], priors)
+        ref_l.append(l)
+        ref_c.append(c)
+    ref_l, ref_c = torch.stack(ref_l), torch.stack(ref_c)
+    loc_t, conf_t = crit.match_native([t.cuda() for t in targets], priors.cuda())
+    assert torch.equal(conf_t.cpu(), ref_c)
+    pos = ref_c != 0
+    assert torch.allclose(loc_t.cpu()[pos], ref_l[pos], atol=1e-4)
