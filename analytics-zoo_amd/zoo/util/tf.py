@@ -119,3 +119,41 @@ def export_tf(sess, folder, inputs, outputs, generate_backward=False, allow_non_
 def strip_unused(net, input_names, output_names):
     """The sub-graph of ``net`` needed for ``output_names`` given ``input_names`` (node names)."""
     return net._graph.needed(output_names, input_names)  # noqa: SLF001
+
+
+def attr_value(v):
+    """Python value -> serialized AttrValue (int -> i, float -> f, bool -> b, str/bytes -> s,
+    ("type", dt) -> type, ("shape", dims) -> shape, np.ndarray -> tensor, list of ints -> list.i)."""
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "type":
+        return pb.enc_int(6, int(v[1]))
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "shape":
+        return pb.enc_bytes(7, b"".join(pb.enc_bytes(2, pb.enc_int(1, int(d) & 0xFFFFFFFFFFFFFFFF)) for d in v[1]))
+    if isinstance(v, bool):
+        return pb.enc_int(5, 1 if v else 0)
+    if isinstance(v, int):
+        return pb.enc_int(3, v & 0xFFFFFFFFFFFFFFFF)
+    if isinstance(v, float):
+        return pb.enc_float(4, v)
+    if isinstance(v, (str, bytes)):
+        return pb.enc_bytes(2, v.encode() if isinstance(v, str) else v)
+    if isinstance(v, np.ndarray):
+        return pb.enc_bytes(8, tensor_proto(v))
+    if isinstance(v, (list, tuple)):
+        return pb.enc_bytes(1, b"".join(pb.enc_int(3, int(x) & 0xFFFFFFFFFFFFFFFF) for x in v))
+    raise TypeError("attr_value: %r" % type(v))
+
+
+def node_def(name, op, inputs=(), **attrs):
+    """A serialized NodeDef (programmatic TF graph building, e.g. for tests and exports)."""
+    out = pb.enc_bytes(1, name.encode()) + pb.enc_bytes(2, op.encode())
+    for i in inputs:
+        out += pb.enc_bytes(3, i.encode())
+    for k, v in attrs.items():
+        out += _attr_entry(k, attr_value(v))
+    return out
+
+
+def graph_def(nodes):
+    """Serialized GraphDef from serialized NodeDefs."""
+    return b"".join(pb.enc_bytes(1, n) for n in nodes)
+

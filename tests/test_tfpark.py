@@ -60,7 +60,7 @@ def test_tfoptimizer_from_keras_and_dataframe():
     opt.set_gradient_clipping_by_l2_norm(10.0)
     opt.optimize(T.MaxEpoch(10))
     assert m.evaluate(x, y[:, 0])[0] < before
-    with pytest.raises(NotImplementedError):
+    with pytest.raises(TypeError, match="TFNet"):
         TFOptimizer.from_loss(None, None)
 
 
@@ -142,3 +142,73 @@ def test_tfdataset_string_bytes_and_rdd_sources():
     rd = TFDataset.from_rdd(FakeRDD(samples), batch_per_thread=8)
     x, y = next(iter(rd.get_prediction_data().data(train=False)))
     assert tuple(np.asarray(x).shape) == (8, 3) and list(np.asarray(y)) == [i % 2 for i in range(8)]
+
+
+def _linreg_graph(tmp_path, with_train_op=None):
+    """x [N, 3] -> pred = x @ w + b; loss = mean((pred - y)^2); variables with Assign initialisers."""
+    import numpy as np
+    from zoo.util.tf import graph_def, node_def
+    F32 = ("type", 1)
+    nodes = [
+        node_def("x", "Placeholder", dtype=F32, shape=("shape", [-1, 3])),
+        node_def("y", "Placeholder", dtype=F32, shape=("shape", [-1, 1])),
+        node_def("w", "VariableV2", dtype=F32, shape=("shape", [3, 1])),
+        node_def("w/init", "Const", dtype=F32, value=np.zeros((3, 1), np.float32)),
+        node_def("w/Assign", "Assign", ["w", "w/init"], T=F32),
+        node_def("b", "VariableV2", dtype=F32, shape=("shape", [1])),
+        node_def("b/init", "Const", dtype=F32, value=np.zeros((1,), np.float32)),
+        node_def("b/Assign", "Assign", ["b", "b/init"], T=F32),
+        node_def("mm", "MatMul", ["x", "w"], T=F32, transpose_a=False, transpose_b=False),
+        node_def("pred", "Add", ["mm", "b"], T=F32),
+        node_def("diff", "Sub", ["pred", "y"], T=F32),
+        node_def("sq", "Square", ["diff"], T=F32),
+        node_def("axes", "Const", dtype=("type", 3), value=np.array([0, 1], np.int32)),
+        node_def("loss", "Mean", ["sq", "axes"], T=F32, Tidx=("type", 3), keep_dims=False),
+    ]
+    if with_train_op:
+        nodes += [node_def("lr", "Const", dtype=F32, value=np.array(0.1, np.float32)),
+                  node_def("grad_w", "Identity", ["w"], T=F32),
+                  node_def("grad_b", "Identity", ["b"], T=F32),
+                  node_def("upd_w", "ApplyGradientDescent", ["w", "lr", "grad_w"], T=F32),
+                  node_def("upd_b", "ApplyGradientDescent", ["b", "lr", "grad_b"], T=F32),
+                  node_def("train", "NoOp", ["^upd_w", "^upd_b"])]
+    p = tmp_path / "graph.pb"
+    p.write_bytes(graph_def(nodes))
+    return str(p)
+
+
+def test_tfoptimizer_from_loss_trains_graph_variables(tmp_path):
+    """In-graph loss (TFOptimizer.from_loss): the graph's variables are trained through the
+    TF-graph executor + autograd + the native fused optimizer."""
+    import numpy as np
+    from zoo.common import triggers as T
+    from zoo.tfpark.tf_optimizer import TFOptimizer
+    from zoo.tfpark.tfnet import TFNet
+    r = np.random.RandomState(0)
+    x = r.randn(256, 3).astype(np.float32)
+    y = (x @ np.array([[1.5], [-2.0], [0.5]], np.float32) + 0.3).astype(np.float32)
+    net = TFNet(_linreg_graph(tmp_path), ["x:0", "y:0"], ["loss:0"], trainable=True)
+    batches = [(x[i:i + 32], y[i:i + 32]) for i in range(0, 256, 32)]
+    from zoo.pipeline.api.keras.optimizers import Adam
+    opt = TFOptimizer.from_loss(net, Adam(lr=0.05), dataset=batches)
+    opt.optimize(end_trigger=T.MaxEpoch(40))
+    assert opt.losses[-1] < 0.05 * opt.losses[0]
+    w = dict(net.named_parameters())
+    vals = sorted(float(v) for p in w.values() for v in p.detach().cpu().reshape(-1))
+    assert abs(vals[0] + 2.0) < 0.3 and abs(vals[-1] - 1.5) < 0.3
+
+
+def test_tfoptimizer_from_train_op_uses_graph_optimizer(tmp_path):
+    import numpy as np
+    from zoo.common import triggers as T
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.tfpark.tf_optimizer import TFOptimizer
+    from zoo.tfpark.tfnet import TFNet
+    r = np.random.RandomState(1)
+    x = r.randn(128, 3).astype(np.float32)
+    y = (x @ np.array([[1.0], [1.0], [1.0]], np.float32)).astype(np.float32)
+    net = TFNet(_linreg_graph(tmp_path, with_train_op=True), ["x:0", "y:0"], ["loss:0"], trainable=True)
+    opt = TFOptimizer.from_train_op("train", net, dataset=[(x[i:i + 32], y[i:i + 32]) for i in range(0, 128, 32)])
+    assert isinstance(opt.optim, SGD) and abs(opt.optim.current_lr() - 0.1) < 1e-7
+    opt.optimize(end_trigger=T.MaxEpoch(20))
+    assert opt.losses[-1] < 0.01 * opt.losses[0]
