@@ -15,8 +15,18 @@
 //    codec (zoo/utils/bigdl_proto.py) to walk nested messages without protoc.
 //  * NativeStore (serving.cpp) — the Cluster Serving queue: Redis-protocol
 //    streams/hashes with a TCP front end and GIL-free worker fast paths.
+//
+// Everything above the Python bindings is plain C++17: with -DZOO_RT_NO_PYTHON the file
+// compiles without pybind11 so tools/sanitize_runtime.py can build it into a standalone
+// ASan/UBSan/TSan self-test (csrc/runtime/selftest/rt_selftest.cpp).
+#ifndef ZOO_RT_NO_PYTHON
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
+namespace py = pybind11;
+#define ZOO_RT_NOGIL py::gil_scoped_release nogil_
+#else
+#define ZOO_RT_NOGIL (void)0
+#endif
 
 #include <atomic>
 #include <condition_variable>
@@ -30,8 +40,6 @@
 #include <thread>
 #include <unordered_map>
 #include <vector>
-
-namespace py = pybind11;
 
 namespace {
 
@@ -82,7 +90,7 @@ class Gatherer {
   }
 
   void wait(int64_t ticket) {
-    py::gil_scoped_release nogil;
+    ZOO_RT_NOGIL;
     std::unique_lock<std::mutex> g(mu_);
     done_cv_.wait(g, [&] { return pending_.find(ticket) == pending_.end(); });
   }
@@ -127,7 +135,7 @@ class Gatherer {
 
 // ------------------------------------------------------------------ CRC32C
 uint32_t crc_table[8][256];
-bool crc_init = false;
+std::once_flag crc_once;
 
 void init_crc() {
   const uint32_t poly = 0x82F63B78u;  // Castagnoli, reflected
@@ -138,11 +146,10 @@ void init_crc() {
   }
   for (uint32_t i = 0; i < 256; ++i)
     for (int t = 1; t < 8; ++t) crc_table[t][i] = (crc_table[t - 1][i] >> 8) ^ crc_table[0][crc_table[t - 1][i] & 0xff];
-  crc_init = true;
 }
 
 uint32_t crc32c_raw(const uint8_t* p, size_t n) {
-  if (!crc_init) init_crc();
+  std::call_once(crc_once, init_crc);  // writer threads may race to the first CRC
   uint32_t c = 0xFFFFFFFFu;
   while (n >= 8) {
     uint64_t v;
@@ -160,19 +167,8 @@ uint32_t crc32c_raw(const uint8_t* p, size_t n) {
 
 uint32_t mask_crc(uint32_t c) { return ((c >> 15) | (c << 17)) + 0xa282ead8u; }
 
-uint32_t crc32c(py::bytes b) {
-  std::string s = b;
-  return crc32c_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size());
-}
-
-uint32_t masked_crc32c(py::bytes b) {
-  std::string s = b;
-  return mask_crc(crc32c_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
-}
-
 // TFRecord: uint64 length | uint32 masked_crc(length) | data | uint32 masked_crc(data)
-py::bytes tfrecord_frame(py::bytes b) {
-  std::string s = b;
+std::string tfrecord_frame_raw(const std::string& s) {
   std::string out;
   out.resize(12 + s.size() + 4);
   uint64_t len = s.size();
@@ -182,16 +178,21 @@ py::bytes tfrecord_frame(py::bytes b) {
   std::memcpy(&out[12], s.data(), s.size());
   uint32_t dc = mask_crc(crc32c_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
   std::memcpy(&out[12 + s.size()], &dc, 4);
-  return py::bytes(out);
+  return out;
 }
 
 // ------------------------------------------------------------------ protobuf
-// Returns [(field_number, wire_type, value)] where value is an int for
-// varint/fixed and bytes for length-delimited fields.
-py::list pb_fields(py::bytes b) {
-  std::string s = b;
-  const uint8_t* p = reinterpret_cast<const uint8_t*>(s.data());
-  const uint8_t* end = p + s.size();
+// One wire-format field: varint/fixed values in `v`, length-delimited payloads as
+// [off, off + v) into the scanned buffer.
+struct PbField {
+  int field, wt;
+  uint64_t v;
+  size_t off;
+};
+
+void pb_scan(const uint8_t* base, size_t size, std::vector<PbField>* out) {
+  const uint8_t* p = base;
+  const uint8_t* end = base + size;
   auto varint = [&](uint64_t& v) {
     v = 0;
     int shift = 0;
@@ -204,42 +205,65 @@ py::list pb_fields(py::bytes b) {
     }
     throw std::runtime_error("pb: truncated varint");
   };
-  py::list out;
   while (p < end) {
     uint64_t key;
     varint(key);
-    const int field = (int)(key >> 3), wt = (int)(key & 7);
-    if (wt == 0) {
-      uint64_t v;
-      varint(v);
-      out.append(py::make_tuple(field, wt, py::int_(v)));
-    } else if (wt == 1) {
+    PbField f{(int)(key >> 3), (int)(key & 7), 0, 0};
+    if (f.wt == 0) {
+      varint(f.v);
+    } else if (f.wt == 1) {
       if (end - p < 8) throw std::runtime_error("pb: truncated fixed64");
-      uint64_t v;
-      std::memcpy(&v, p, 8);
+      std::memcpy(&f.v, p, 8);
       p += 8;
-      out.append(py::make_tuple(field, wt, py::int_(v)));
-    } else if (wt == 2) {
-      uint64_t n;
-      varint(n);
-      if ((uint64_t)(end - p) < n) throw std::runtime_error("pb: truncated bytes");
-      out.append(py::make_tuple(field, wt, py::bytes(reinterpret_cast<const char*>(p), n)));
-      p += n;
-    } else if (wt == 5) {
+    } else if (f.wt == 2) {
+      varint(f.v);
+      if ((uint64_t)(end - p) < f.v) throw std::runtime_error("pb: truncated bytes");
+      f.off = (size_t)(p - base);
+      p += f.v;
+    } else if (f.wt == 5) {
       if (end - p < 4) throw std::runtime_error("pb: truncated fixed32");
       uint32_t v;
       std::memcpy(&v, p, 4);
+      f.v = v;
       p += 4;
-      out.append(py::make_tuple(field, wt, py::int_(v)));
     } else {
-      throw std::runtime_error("pb: unsupported wire type " + std::to_string(wt));
+      throw std::runtime_error("pb: unsupported wire type " + std::to_string(f.wt));
     }
+    out->push_back(f);
+  }
+}
+
+#ifndef ZOO_RT_NO_PYTHON
+uint32_t crc32c(py::bytes b) {
+  std::string s = b;
+  return crc32c_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size());
+}
+
+uint32_t masked_crc32c(py::bytes b) {
+  std::string s = b;
+  return mask_crc(crc32c_raw(reinterpret_cast<const uint8_t*>(s.data()), s.size()));
+}
+
+py::bytes tfrecord_frame(py::bytes b) { return py::bytes(tfrecord_frame_raw(std::string(b))); }
+
+// Returns [(field_number, wire_type, value)] where value is an int for
+// varint/fixed and bytes for length-delimited fields.
+py::list pb_fields(py::bytes b) {
+  std::string s = b;
+  std::vector<PbField> fs;
+  pb_scan(reinterpret_cast<const uint8_t*>(s.data()), s.size(), &fs);
+  py::list out;
+  for (const auto& f : fs) {
+    if (f.wt == 2) out.append(py::make_tuple(f.field, f.wt, py::bytes(s.data() + f.off, (size_t)f.v)));
+    else out.append(py::make_tuple(f.field, f.wt, py::int_(f.v)));
   }
   return out;
 }
+#endif
 
 }  // namespace
 
+#ifndef ZOO_RT_NO_PYTHON
 void register_serving(py::module& m);  // serving.cpp
 
 PYBIND11_MODULE(_runtime, m) {
@@ -257,3 +281,4 @@ PYBIND11_MODULE(_runtime, m) {
   m.def("tfrecord_frame", &tfrecord_frame);
   m.def("pb_fields", &pb_fields);
 }
+#endif  // ZOO_RT_NO_PYTHON

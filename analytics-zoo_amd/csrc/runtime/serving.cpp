@@ -32,10 +32,12 @@
 #include <unordered_map>
 #include <vector>
 
+#ifndef ZOO_RT_NO_PYTHON  // the self-test build (tools/sanitize_runtime.py) has no Python
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
 namespace py = pybind11;
+#endif
 
 namespace zoo_serving {
 
@@ -68,6 +70,7 @@ void encode(const Reply& r, std::string& out) {
   }
 }
 
+#ifndef ZOO_RT_NO_PYTHON
 py::object to_py(const Reply& r) {
   switch (r.k) {
     case Reply::SIMPLE: return py::str(r.s);
@@ -83,6 +86,7 @@ py::object to_py(const Reply& r) {
   }
   return py::none();
 }
+#endif
 
 // ------------------------------------------------------------------ helpers
 std::string upper(std::string s) {
@@ -218,15 +222,15 @@ class Store {
     {
       std::unique_lock<std::mutex> lk(mu_);
       const auto deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(block_ms > 0 ? block_ms : 0);
+      bool last = false;
       while (true) {
+        // look the stream up again after every wait: a DEL / FLUSHALL / XGROUP DESTROY from
+        // another connection may have erased it while the lock was released
         auto it = streams_.find(key);
         if (it == streams_.end() || !it->second.groups.count(group)) throw std::runtime_error("NOGROUP No such key or consumer group");
         take(it->second, it->second.groups[group], consumer, count, &got);
-        if (!got.empty() || block_ms <= 0 || stop_) break;
-        if (cv_.wait_until(lk, deadline) == std::cv_status::timeout) {
-          take(it->second, it->second.groups[group], consumer, count, &got);
-          break;
-        }
+        if (last || !got.empty() || block_ms <= 0 || stop_) break;
+        last = cv_.wait_until(lk, deadline) == std::cv_status::timeout;
       }
     }
     for (auto& m : got) {
@@ -600,7 +604,11 @@ class Store {
 class Server {
  public:
   explicit Server(std::shared_ptr<Store> st) : store_(std::move(st)) {}
-  ~Server() { stop(); }
+  ~Server() {
+    stop();
+    std::lock_guard<std::mutex> g(cmu_);
+    if (stopper_.joinable()) stopper_.join();
+  }
 
   int start(const std::string& host, int port) {
     lfd_ = socket(AF_INET, SOCK_STREAM, 0);
@@ -624,7 +632,10 @@ class Server {
     return port_;
   }
 
+  // idempotent; a second caller blocks until the first one has joined every thread, so
+  // the Server can be destroyed as soon as any stop() returns
   void stop() {
+    std::lock_guard<std::mutex> sg(stop_mu_);
     if (!running_.exchange(false)) return;
     store_->shutdown();
     ::shutdown(lfd_, SHUT_RDWR);
@@ -706,7 +717,7 @@ class Server {
     std::string buf, out;
     std::vector<std::string> args;
     char tmp[1 << 16];
-    bool alive = true;
+    bool alive = true, shutdown_req = false;
     while (alive && running_) {
       const ssize_t r = recv(fd, tmp, sizeof(tmp), 0);
       if (r <= 0) break;
@@ -719,7 +730,7 @@ class Server {
           if (upper(args[0]) == "SHUTDOWN") {
             out += "+OK\r\n";
             alive = false;
-            std::thread([this] { stop(); }).detach();
+            shutdown_req = true;
             break;
           }
           encode(store_->exec(args), out);
@@ -739,6 +750,9 @@ class Server {
     {
       std::lock_guard<std::mutex> g(cmu_);
       conns_.erase(fd);
+      // SHUTDOWN: stop from a separate (joined) thread, after the +OK went out -- stop()
+      // joins this connection thread, so it cannot run here
+      if (shutdown_req && !stopper_.joinable()) stopper_ = std::thread([this] { stop(); });
     }
     close(fd);
   }
@@ -747,12 +761,14 @@ class Server {
   int lfd_ = -1, port_ = 0;
   std::atomic<bool> running_{false};
   std::thread acceptor_;
-  std::mutex cmu_;
+  std::mutex cmu_, stop_mu_;
   std::set<int> conns_;
   std::vector<std::thread> threads_;
+  std::thread stopper_;
 };
 
 // ------------------------------------------------------------------ python facade
+#ifndef ZOO_RT_NO_PYTHON
 class NativeStore {
  public:
   explicit NativeStore(size_t maxmem) : store_(std::make_shared<Store>(maxmem)) {}
@@ -808,8 +824,11 @@ class NativeStore {
   std::shared_ptr<Store> store_;
   std::unique_ptr<Server> server_;
 };
+#endif  // ZOO_RT_NO_PYTHON
 
 }  // namespace zoo_serving
+
+#ifndef ZOO_RT_NO_PYTHON
 
 void register_serving(py::module& m) {
   using zoo_serving::NativeStore;
@@ -827,3 +846,4 @@ void register_serving(py::module& m) {
     return py::bytes(out);
   });
 }
+#endif  // ZOO_RT_NO_PYTHON
