@@ -77,12 +77,41 @@ def run_models(a):
     bench_model("BERT-base seq128", imb, bert_in, [1, 8, 32, 128], a.iters)
 
 
-def _producer_proc(cfg, p, n, images, jpgs):
+def _producer_proc(cfg, p, n, images, jpgs, ready=None, go=None):
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
     from zoo.serving import InputQueue
     q = InputQueue(cfg)
+    if ready is not None:  # imports + connection done: the timed run starts when all are ready
+        ready.put(p)
+        go.wait()
     for i in range(p, images, n):
-        q.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+        _send(q, "im%d" % i, jpgs[i % len(jpgs)])
+
+
+def _send(q, uri, payload):
+    """JPEG bytes -> image record; a numpy array (BERT token ids) -> tensor record"""
+    if isinstance(payload, np.ndarray):
+        q.enqueue_tensor(uri, payload)
+    else:
+        q.enqueue_encoded(uri, payload)
+
+
+class _BertTokens(torch.nn.Module):
+    """Serving head for BERT-base: a [B, L] float tensor of token ids (the Cluster Serving
+    tensor record format) -> pooled [B, 768] output; segment 0, positions 0..L-1, full mask."""
+
+    def __init__(self, L=128):
+        super().__init__()
+        from zoo.pipeline.api.keras.layers import BERT
+        self.L = L
+        self.m = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512,
+                      intermediate_size=3072, output_all_block=False)
+
+    def forward(self, x):
+        tok = x.long()
+        b = tok.shape[0]
+        pos = torch.arange(self.L, device=tok.device).repeat(b, 1)
+        return self.m([tok, torch.zeros_like(tok), pos, torch.ones(b, self.L, device=tok.device)])[1]
 
 
 def run_e2e(a):
@@ -105,11 +134,16 @@ def run_e2e(a):
             cfg = os.path.join(d, "config.yaml")
             open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,224,224\n  filter: topN(5)\n"
                                  "params:\n  batch_size: %d\n" % (srv.port, a.batch))
-            s = ClusterServing(cfg, model=resnet50(), device="cuda")
+            bert = a.model == "bert"
+            if bert:  # token-id tensor records instead of JPEGs
+                jpgs = [rng.integers(0, 30522, 128).astype(np.float32) for _ in range(16)]
+            s = ClusterServing(cfg, model=_BertTokens() if bert else resnet50(), device="cuda")
+            model_name = "BERT-base seq128 bf16" if bert else "ResNet-50 bf16"
+            data_name = "synthetic token ids [128]" if bert else "synthetic 256x256 JPEG"
             inq, outq = InputQueue(cfg), OutputQueue(cfg)
             # warm-up (graph capture for the batch shape)
             for i in range(a.batch):
-                inq.enqueue_encoded("warm%d" % i, jpgs[i % len(jpgs)])
+                _send(inq, "warm%d" % i, jpgs[i % len(jpgs)])
             s.run(max_records=a.batch, idle_timeout=30)
             outq.dequeue()
             s.records = 0
@@ -117,25 +151,30 @@ def run_e2e(a):
 
             if a.drain:  # worker-only throughput: the queue is filled before the worker starts
                 for i in range(a.images):
-                    inq.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+                    _send(inq, "im%d" % i, jpgs[i % len(jpgs)])
                 s.records = 0
                 td = time.perf_counter()
                 s.run(max_records=a.images, idle_timeout=30)
                 el = time.perf_counter() - td
                 got = outq.dequeue()
-                print(json.dumps({"bench": "cluster-serving-drain", "model": "ResNet-50 bf16", "batch": a.batch,
-                                  "images": len(got), "throughput": round(len(got) / el, 1), "unit": "images/sec",
-                                  "n_gpus": 1, "data": "synthetic 256x256 JPEG"}), flush=True)
+                print(json.dumps({"bench": "cluster-serving-drain", "model": model_name, "batch": a.batch,
+                                  "images": len(got), "throughput": round(len(got) / el, 1), "unit": "records/sec",
+                                  "n_gpus": 1, "data": data_name}), flush=True)
                 return
 
             if a.client_procs:  # producers in separate processes (spawned: no GPU state in them)
                 import multiprocessing as mp
                 ctxmp = mp.get_context("spawn")
-                t0 = time.perf_counter()
-                procs = [ctxmp.Process(target=_producer_proc, args=(cfg, p, a.client_procs, a.images, jpgs))
+                ready, go = ctxmp.Queue(), ctxmp.Event()
+                procs = [ctxmp.Process(target=_producer_proc,
+                                       args=(cfg, p, a.client_procs, a.images, jpgs, ready, go))
                          for p in range(a.client_procs)]
                 for pr in procs:
                     pr.start()
+                for _ in procs:
+                    ready.get(timeout=240)
+                t0 = time.perf_counter()
+                go.set()
                 sent_q = None
                 ths = []
                 for i in range(a.images):
@@ -147,7 +186,7 @@ def run_e2e(a):
                 q = inq if p == 0 else InputQueue(cfg)   # one connection per producer thread
                 for i in range(p, a.images, a.producers):
                     sent["im%d" % i] = time.perf_counter()
-                    q.enqueue_encoded("im%d" % i, jpgs[i % len(jpgs)])
+                    _send(q, "im%d" % i, jpgs[i % len(jpgs)])
             if ths is None:
                 ths = [threading.Thread(target=producer, args=(p,)) for p in range(a.producers)]
                 t0 = time.perf_counter()
@@ -169,7 +208,8 @@ def run_e2e(a):
             el = time.perf_counter() - t0
             lat = [(done[k] - sent[k]) * 1e3 for k in done if k in sent]
             # the model alone at the same batch (same InferenceModel replica, input already on the GPU)
-            xm = torch.randn(a.batch, 3, 224, 224, device="cuda")
+            xm = (torch.randint(0, 30522, (a.batch, 128), device="cuda").float() if bert
+                  else torch.randn(a.batch, 3, 224, 224, device="cuda"))
             for _ in range(3):
                 s.im.predict(xm)
             tm = time.perf_counter()
@@ -177,14 +217,14 @@ def run_e2e(a):
                 s.im.predict(xm)
             model_tp = 20 * a.batch / (time.perf_counter() - tm)
             from zoo.serving.resp import NativeRespServer
-            print(json.dumps({"bench": "cluster-serving-e2e", "model": "ResNet-50 bf16", "batch": a.batch,
-                              "images": len(done), "throughput": round(len(done) / el, 1), "unit": "images/sec",
+            print(json.dumps({"bench": "cluster-serving-e2e", "model": model_name, "batch": a.batch,
+                              "images": len(done), "throughput": round(len(done) / el, 1), "unit": "records/sec",
                               "p50_ms": round(_pct(lat, 50), 2), "p99_ms": round(_pct(lat, 99), 2),
                               "model_only_throughput": round(model_tp, 1),
                               "e2e_over_model": round(len(done) / el / model_tp, 3),
                               "producers": ("%d processes" % a.client_procs) if a.client_procs else a.producers,
                               "queue": "native" if isinstance(srv, NativeRespServer) else "python",
-                              "n_gpus": 1, "data": "synthetic 256x256 JPEG"}), flush=True)
+                              "n_gpus": 1, "data": data_name}), flush=True)
     finally:
         srv.shutdown()
         srv.server_close()
@@ -199,6 +239,8 @@ def main():
     ap.add_argument("--producers", type=int, default=4)
     ap.add_argument("--client-procs", type=int, default=0, help="producers in N separate processes")
     ap.add_argument("--drain", action="store_true", help="prefill the queue, time the worker alone")
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"],
+                    help="e2e: ResNet-50 on JPEG records or BERT-base on token-id tensor records")
     a = ap.parse_args()
     run_models(a) if a.mode == "model" else run_e2e(a)
 

@@ -133,6 +133,37 @@ def top_n(t, n):
     return "[" + "".join("[%d,%s]" % (i, repr(float(flat[i]))) for i in idx) + "]"
 
 
+def _top_n_rows(a, n):
+    """top_n for every row of a [B, F] array at once: candidates by argpartition, ordered by
+    (value desc, index asc) -- the same order as top_n's stable sort; rows whose n-th value
+    is tied with values outside the candidates fall back to top_n."""
+    B, F = a.shape
+    if n >= F:
+        return [top_n(r, n) for r in a]
+    cand = np.sort(np.argpartition(-a, n - 1, axis=1)[:, :n], axis=1)
+    vals = np.take_along_axis(a, cand, axis=1)
+    order = np.argsort(-vals, axis=1, kind="stable")
+    idx = np.take_along_axis(cand, order, axis=1)
+    top = np.take_along_axis(vals, order, axis=1)
+    ties = (a >= top[:, -1:]).sum(axis=1) > n
+    out = []
+    for b in range(B):
+        if ties[b]:
+            out.append(top_n(a[b], n))
+        else:
+            out.append("[" + "".join("[%d,%s]" % (i, repr(v)) for i, v in zip(idx[b].tolist(), top[b].tolist())) + "]")
+    return out
+
+
+def post_process_batch(outs, flt="None"):
+    """post_process over a batch of model outputs; topN runs vectorised over the batch."""
+    if flt and flt.startswith("topN(") and flt.endswith(")") and isinstance(outs, np.ndarray) and outs.ndim >= 2:
+        n = int(flt[5:-1])
+        a = np.ascontiguousarray(outs.reshape(outs.shape[0], -1), dtype=np.float32)
+        return _top_n_rows(a, n)
+    return [post_process(r, flt) for r in outs]
+
+
 def post_process(t, flt="None"):
     if flt and flt != "None":
         if not flt.endswith(")") or len(flt.split("(")) != 2:
@@ -217,8 +248,8 @@ class ClusterServing:
         out = self.im.predict(batch)
         outs = out if isinstance(out, np.ndarray) else out[0]
         flt = self.cfg["filter"]
-        for uri, row in zip(uris, outs):
-            self.db.hset("result:" + uri, "value", post_process(row, flt))
+        for uri, val in zip(uris, post_process_batch(outs, flt)):
+            self.db.hset("result:" + uri, "value", val)
         self.db.xack(STREAM, GROUP, *ids)
         self.db.xdel(STREAM, *ids)
         self.records += len(ids)
@@ -367,7 +398,8 @@ class ClusterServing:
                 ids, uris, decoded = item
                 out = self.im.predict(self._to_batch(decoded))
                 outs = out if isinstance(out, np.ndarray) else out[0]
-                self.db.finish(STREAM, GROUP, ids, [("result:" + u, post_process(r, flt)) for u, r in zip(uris, outs)])
+                vals = post_process_batch(outs, flt)
+                self.db.finish(STREAM, GROUP, ids, [("result:" + u, v) for u, v in zip(uris, vals)])
                 self.records += len(ids)
                 if self.summary is not None:
                     dt = max(time.time() - self._t0, 1e-9)

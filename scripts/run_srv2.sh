@@ -1,0 +1,7 @@
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+T="timeout -k 10"
+$T 300 python analytics-zoo_amd/tools/serving_bench.py e2e --model bert --batch 128 --images 8192 --drain > gpurun_out/serving_bert_drain.log 2>&1 || exit 1
+$T 300 python analytics-zoo_amd/tools/serving_bench.py e2e --model bert --batch 128 --images 8192 --producers 4 > gpurun_out/serving_bert_e2e.log 2>&1 || exit 2
+$T 300 python analytics-zoo_amd/tools/serving_bench.py e2e --batch 128 --images 4096 --drain > gpurun_out/serving_rn_drain.log 2>&1 || exit 3

@@ -152,3 +152,21 @@ def test_native_local_client_fast_paths():
         assert lc.read_batch("image_stream", "serving", "w", 8, 10) == []
     finally:
         srv.shutdown()
+
+
+def test_post_process_batch_matches_per_row_top_n():
+    """the vectorised topN post-processing (worker hot path) is string-identical to the
+    per-row PostProcessing.topN, ties included"""
+    import numpy as np
+    from zoo.serving.server import post_process, post_process_batch
+    rng = np.random.default_rng(0)
+    for F in (3, 10, 768, 1000):
+        a = rng.standard_normal((32, F)).astype(np.float32)
+        a[3, :] = 0.5
+        a[4, :7] = 2.0
+        a[5] = np.round(a[5])
+        for n in (1, 5):
+            flt = "topN(%d)" % n
+            assert post_process_batch(a, flt) == [post_process(r, flt) for r in a]
+    b = rng.standard_normal((4, 6)).astype(np.float32)
+    assert post_process_batch(b, "None") == [post_process(r, "None") for r in b]
