@@ -207,7 +207,10 @@ class _LinearBlasFn(torch.autograd.Function):
     Weight gradients accumulate in fp32 into the engine's flat gradient buffer."""
 
     @staticmethod
-    def forward(ctx, x2, w, bias, act, need_grad):
+    def forward(ctx, x2, w, bias, act, need_grad, grad_add=None):
+        ctx.grad_add = grad_add
+        if grad_add is not None and need_grad:
+            grad_add.armed = True   # the residual consumer of x may now hand its gradient here
         wb = bf16_weight(w)
         bb = None if bias is None else _bf16_bias(bias)
         pre = None
@@ -254,7 +257,13 @@ class _LinearBlasFn(torch.autograd.Function):
             dy = dy * (y > 0).to(dy.dtype)
         elif ctx.act == "gelu":
             dy = torch.ops.aten.gelu_backward(dy, pre)
-        if ctx.needs_input_grad[0]:
+        ga = ctx.grad_add
+        if ga is not None and ga.grad is not None:
+            # residual gradient of x folded into the data-gradient GEMM (beta = 1)
+            g = ga.grad.reshape(dy.shape[0], -1).to(torch.bfloat16)
+            ga.grad, ga.armed = None, False
+            dx = torch.addmm(g, dy, bf16_weight(w)) if ctx.needs_input_grad[0] else g
+        elif ctx.needs_input_grad[0]:
             dx = torch.mm(dy, bf16_weight(w))
         if ctx.needs_input_grad[1]:
             gbuf = getattr(w, "_zoo_grad", None)
@@ -284,7 +293,7 @@ class _LinearBlasFn(torch.autograd.Function):
                 if hook is not None:
                     hook(bias)
                 db = None
-        return dx, dw, db, None, None
+        return dx, dw, db, None, None, None
 
 
 _ADDMM_DTYPE_OK = [True]
@@ -334,9 +343,11 @@ def _use_blas(x, Cin, K, act):
         act in (None, "linear", "relu", "gelu")
 
 
-def linear(x, w, bias=None, act=None):
+def linear(x, w, bias=None, act=None, grad_add=None):
     """y = act(x @ w^T + b). Uses the MFMA GEMM when features are 8-aligned and
-    the input is on the GPU; otherwise the plain library GEMM (hipBLASLt)."""
+    the input is on the GPU; otherwise the plain library GEMM (hipBLASLt).
+    ``grad_add``: a :class:`zoo.ops.nn.GradAdd` whose residual gradient the data-gradient
+    GEMM adds (only armed on the library-GEMM path; elsewhere autograd sums as usual)."""
     K, Cin = w.shape
     lead = x.shape[:-1]
     if x.is_cuda and (Cin % 8 or K % 8) and x.shape[-1] == Cin:
@@ -352,7 +363,7 @@ def linear(x, w, bias=None, act=None):
         xb = (xb if xb.dtype == torch.bfloat16 else xb.to(torch.bfloat16)).contiguous()
         need_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or
                                                   (bias is not None and bias.requires_grad))
-        y = _LinearBlasFn.apply(xb, w, bias, None if act == "linear" else act, need_grad)
+        y = _LinearBlasFn.apply(xb, w, bias, None if act == "linear" else act, need_grad, grad_add)
         return y.reshape(*lead, K).to(x.dtype)
     if x.is_cuda and Cin % 8 == 0 and K % 8 == 0 and w.shape[1] == Cin:
         x2 = x.reshape(-1, 1, 1, Cin)

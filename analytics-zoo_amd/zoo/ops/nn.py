@@ -55,30 +55,49 @@ def _drop_rng():
     return _DROP_RNG[0]
 
 
+class GradAdd:
+    """Residual-gradient handoff between the two consumers of a Transformer block input x:
+    the first consumer, a linear layer on the library GEMM (``linear(..., grad_add=h)``),
+    arms it in forward; the residual ``dropout_add(a, x, ..., grad_add=h)`` then parks its
+    x-gradient here in backward instead of returning it, and the linear's backward folds
+    it into its data-gradient GEMM (dx = dy W + g, beta = 1) -- no separate gradient-add
+    pass over x. Reference: the residual adds of TransformerLayer.scala:129-181."""
+    __slots__ = ("armed", "grad")
+
+    def __init__(self):
+        self.armed, self.grad = False, None
+
+
 class _DropoutAddFn(torch.autograd.Function):
     """out = x + dropout(a): one native pass; the keep-mask is a counter-based hash of a
     per-call seed, so backward regenerates it (no mask tensor is stored)."""
 
     @staticmethod
-    def forward(ctx, a, x, p):
+    def forward(ctx, a, x, p, handoff=None):
         seed = _drop_rng().getrandbits(62)   # host RNG: no device sync, no tensor op
         ctx.p, ctx.seed = p, seed
+        ctx.handoff = handoff if (handoff is not None and handoff.armed) else None
         return native().dropout_add(a, x, p, seed)
 
     @staticmethod
     def backward(ctx, g):
         g = g.contiguous()
-        return native().dropout_add(g, None, ctx.p, ctx.seed), g, None
+        da = native().dropout_add(g, None, ctx.p, ctx.seed)
+        if ctx.handoff is not None:
+            ctx.handoff.grad = g      # added by the armed linear's dgrad GEMM
+            return da, None, None, None
+        return da, g, None, None
 
 
-def dropout_add(a, x, p, training=True):
-    """``x + F.dropout(a, p, training)`` (Transformer residual branch)."""
+def dropout_add(a, x, p, training=True, grad_add=None):
+    """``x + F.dropout(a, p, training)`` (Transformer residual branch). ``grad_add``: a
+    :class:`GradAdd` armed by the linear layer that also consumes ``x``."""
     if not training or p <= 0:
         return x + a
     if a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and a.shape == x.shape and \
             a.numel() % 8 == 0 and a.numel() >= _DROP_FUSE_MIN and not torch.cuda.is_current_stream_capturing():
         # small tensors are launch/host-bound: the C++ dropout path has less per-call overhead
-        return _DropoutAddFn.apply(a.contiguous(), x.contiguous(), float(p))
+        return _DropoutAddFn.apply(a.contiguous(), x.contiguous(), float(p), grad_add)
     return x + F.dropout(a, p, True)
 
 
