@@ -136,28 +136,63 @@ ZOO_DEV RowSplit row_split(int cpr) {
   return r;
 }
 
+// training statistics of the BatchNorm applied to the residual input (downsample
+// shortcut): the residual operand is then the raw shortcut conv output and is normalised
+// with these in the same pass, so the shortcut's own apply pass and its output tensor go away
+struct BnSide {
+  const float* stats;  // null: the residual is added as is
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  float* save_mean;
+  float* save_invstd;
+};
+
+ZOO_DEV void bn_bookkeeping(const float* stats, float* running_mean, float* running_var, float* save_mean,
+                            float* save_invstd, int M, int C, float eps, float momentum) {
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mu = stats[c] * invM;
+    const float var = fmaxf(stats[C + c] * invM - mu * mu, 0.f);
+    save_mean[c] = mu;
+    save_invstd[c] = rsqrtf(var + eps);
+    if (running_mean) {
+      const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
+      running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
+    }
+  }
+}
+
+ZOO_DEV void bn_coeffs(const float* stats, const float* gamma, const float* beta, int chunk, int C, float invM,
+                       float eps, float* sc, float* sh) {
+  float s1[8], s2[8], g8[8], b8[8];
+  load8f(stats, chunk, s1);
+  load8f(stats + C, chunk, s2);
+  if (gamma) load8f(gamma, chunk, g8);
+  if (beta) load8f(beta, chunk, b8);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float mu = s1[e] * invM;
+    const float is = rsqrtf(fmaxf(s2[e] * invM - mu * mu, 0.f) + eps);
+    sc[e] = gamma ? g8[e] * is : is;
+    sh[e] = (beta ? b8[e] : 0.f) - mu * sc[e];
+  }
+}
+
 // forward apply (training): stats -> scale/shift per thread
 __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
     const bf16_t* __restrict__ X, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, const bf16_t* __restrict__ resid, bf16_t* __restrict__ Y,
     float* __restrict__ running_mean, float* __restrict__ running_var, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, int M, int C, float eps, float momentum, int relu, int training,
-    int rows_per_block) {
+    int rows_per_block, BnSide r2) {
   const float invM = 1.f / (float)M;
-  if (blockIdx.x == 0) {  // bookkeeping: saved statistics + running averages
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-      if (training) {
-        const float mu = stats[c] * invM;
-        const float var = fmaxf(stats[C + c] * invM - mu * mu, 0.f);
-        save_mean[c] = mu;
-        save_invstd[c] = rsqrtf(var + eps);
-        if (running_mean) {
-          const float unbiased = M > 1 ? var * (float)M / (float)(M - 1) : var;
-          running_mean[c] = (1.f - momentum) * running_mean[c] + momentum * mu;
-          running_var[c] = (1.f - momentum) * running_var[c] + momentum * unbiased;
-        }
-      }
-    }
+  if (blockIdx.x == 0 && training) {  // bookkeeping: saved statistics + running averages
+    bn_bookkeeping(stats, running_mean, running_var, save_mean, save_invstd, M, C, eps, momentum);
+    if (r2.stats)
+      bn_bookkeeping(r2.stats, r2.running_mean, r2.running_var, r2.save_mean, r2.save_invstd, M, C, eps, momentum);
   }
   const int cpr = C >> 3;
   const RowSplit rs = row_split(cpr);
@@ -193,6 +228,12 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
         sh[e] = (beta ? b8[e] : 0.f) - mu * sc[e];
       }
     }
+    float sc2[8], sh2[8];
+    if (r2.stats) {
+      bn_coeffs(r2.stats, r2.gamma, r2.beta, chunk, C, invM, eps, sc2, sh2);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) sh[e] += sh2[e];  // both shifts folded into one
+    }
     // 4 rows per step: four independent 16-byte loads (x 2 with a residual) in flight per thread
     for (int rb = r0; rb < r1; rb += rstride) {
       uint4 xv[4], rv[4];
@@ -214,8 +255,13 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
         if (resid) {
           float q[8];
           unpack8(rv[u], q);
+          if (r2.stats) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += q[e];
+            for (int e = 0; e < 8; ++e) v[e] += q[e] * sc2[e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += q[e];
+          }
         }
         if (relu) {
 #pragma unroll
@@ -513,15 +559,24 @@ static void apply_grid(int M, int C, int tile_units, int* blocks, int* rpb) {
   *blocks = M > 0 ? (M + *rpb - 1) / *rpb : 1;
 }
 
+// r2 (7 pointers, nullable): BatchNorm of the residual (stats, gamma, beta, running mean,
+// running var, save mean, save invstd); r2 == null or r2[0] == null: plain residual add
 extern "C" hipError_t zoo_bn_fwd_apply(const void* X, const float* stats, const float* gamma,
                                        const float* beta, const void* resid, void* Y, float* rmean,
                                        float* rvar, float* smean, float* sinv, int M, int C, float eps,
-                                       float momentum, int relu, int training, hipStream_t st) {
+                                       float momentum, int relu, int training, const void* const* r2,
+                                       hipStream_t st) {
   int rpb, blocks;
   apply_grid(M, C, 4, &blocks, &rpb);
+  BnSide side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (r2 && r2[0] && training) {
+    side.stats = (const float*)r2[0]; side.gamma = (const float*)r2[1]; side.beta = (const float*)r2[2];
+    side.running_mean = (float*)r2[3]; side.running_var = (float*)r2[4];
+    side.save_mean = (float*)r2[5]; side.save_invstd = (float*)r2[6];
+  }
   hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X,
                      stats, gamma, beta, (const bf16_t*)resid, (bf16_t*)Y, rmean, rvar, smean, sinv, M, C, eps,
-                     momentum, relu, training, rpb);
+                     momentum, relu, training, rpb, side);
   return hipGetLastError();
 }
 

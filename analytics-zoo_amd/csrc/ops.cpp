@@ -42,7 +42,7 @@ int zoo_act_bwd_reduce_parts(int, int);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
-                            float*, float*, int, int, float, float, int, int, hipStream_t);
+                            float*, float*, int, int, float, float, int, int, const void* const*, hipStream_t);
 hipError_t zoo_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*,
                             const float*, void*, void*, float*, float*, int, int, hipStream_t);
 hipError_t zoo_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -561,7 +561,7 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
                            c10::optional<torch::Tensor> beta, c10::optional<torch::Tensor> resid,
                            c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
                            torch::Tensor smean, torch::Tensor sinv, double eps, double momentum, bool relu,
-                           bool training) {
+                           bool training, std::vector<c10::optional<torch::Tensor>> resid_bn) {
   req(x, at::kBFloat16, "x");
   const int C = x.size(-1);
   const int64_t M = x.numel() / C;
@@ -585,11 +585,31 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
   check_al16(opt_ptr<float>(beta), "beta");
   check_al16(opt_ptr<float>(rmean), "running_mean");
   check_al16(opt_ptr<float>(rvar), "running_var");
+  // resid_bn: [stats, gamma, beta, running_mean, running_var, save_mean, save_invstd] of the
+  // BatchNorm applied to `resid` (the raw shortcut conv output) inside this pass; empty: none
+  const void* r2[7] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  if (!resid_bn.empty()) {
+    TORCH_CHECK(training && resid_bn.size() == 7, "bn: resid_bn needs 7 entries (training only)");
+    TORCH_CHECK(resid.has_value() && resid->defined(), "bn: resid_bn without resid");
+    const int64_t need[7] = {2 * (int64_t)C, C, C, C, C, C, C};
+    for (int i = 0; i < 7; ++i) {
+      auto& t = resid_bn[i];
+      if (!t.has_value() || !t->defined()) {
+        TORCH_CHECK(i == 1 || i == 2 || i == 3 || i == 4, "bn: resid_bn stats/save buffers are required");
+        continue;
+      }
+      req(*t, at::kFloat, "resid_bn");
+      TORCH_CHECK(t->is_contiguous() && t->numel() >= need[i], "bn: resid_bn buffer size");
+      check_al16(t->data_ptr<float>(), "resid_bn");
+      r2[i] = t->data_ptr();
+    }
+  }
   auto y = torch::empty_like(x);
   check_hip(zoo_bn_fwd_apply(x.data_ptr(), training ? stats.data_ptr<float>() : nullptr, opt_ptr<float>(gamma),
                              opt_ptr<float>(beta), opt_ptr<void>(resid), y.data_ptr(), opt_ptr<float>(rmean),
                              opt_ptr<float>(rvar), smean.data_ptr<float>(), sinv.data_ptr<float>(), (int)M, C,
-                             (float)eps, (float)momentum, relu, training, cur_stream()),
+                             (float)eps, (float)momentum, relu, training, resid_bn.empty() ? nullptr : r2,
+                             cur_stream()),
             "bn_fwd_apply");
   return y;
 }
@@ -1821,7 +1841,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("get_reduce_modes", []() { return std::make_tuple(g_stats_partial, g_wgrad_partial); });
   m.def("bn_reduce", &bn_reduce);
   m.def("stat_len", &stat_len);
-  m.def("bn_fwd_apply", &bn_fwd_apply);
+  m.def("bn_fwd_apply", &bn_fwd_apply, py::arg("x"), py::arg("stats"), py::arg("gamma"), py::arg("beta"),
+        py::arg("resid"), py::arg("rmean"), py::arg("rvar"), py::arg("smean"), py::arg("sinv"), py::arg("eps"),
+        py::arg("momentum"), py::arg("relu"), py::arg("training"),
+        py::arg("resid_bn") = std::vector<c10::optional<torch::Tensor>>());
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from zoo import ops
-from zoo.ops.bn import BNProducer, GradHandoff
+from zoo.ops.bn import BNProducer, GradHandoff, conv_stats
 
 
 class ConvBN(nn.Module):
@@ -37,16 +37,26 @@ class ConvBN(nn.Module):
         self.register_buffer("running_var", torch.ones(cout))
 
     def forward(self, x, resid=None, resid_handoff=None, grad_add=None, producer_in=None, producer_out=None,
-                dx_handoff=None):
+                dx_handoff=None, resid_bn=None):
         return ops.conv_bn_act(x, self.weight, self.gamma, self.beta, self.running_mean, self.running_var,
                                kernel=(self.k, self.k), stride=(self.stride, self.stride),
                                pad=(self.pad, self.pad), eps=self.eps, momentum=self.momentum, relu=self.relu,
                                resid=resid, training=self.training, resid_handoff=resid_handoff, grad_add=grad_add,
-                               producer_in=producer_in, producer_out=producer_out, dx_handoff=dx_handoff)
+                               producer_in=producer_in, producer_out=producer_out, dx_handoff=dx_handoff,
+                               resid_bn=resid_bn)
+
+    def forward_stats(self, x, grad_add=None):
+        """Training-mode projection shortcut: raw conv output + its BN (ShortcutBN), to be
+        applied inside the consuming unit's BN pass. Returns (raw, resid_bn argument)."""
+        y, holder = conv_stats(x, self.weight, self.running_mean, self.running_var, kernel=(self.k, self.k),
+                               stride=(self.stride, self.stride), pad=(self.pad, self.pad), grad_add=grad_add)
+        return y, (holder, self.gamma, self.beta)
 
 
 # cross-unit BN-backward fusion (BNProducer); the switch exists for A/B numerics tests
 FUSE_BN_BACKWARD = True
+# projection-shortcut BatchNorm applied inside the block's last BN pass (ShortcutBN)
+FUSE_SHORTCUT_BN = os.environ.get("ZOO_FUSE_SHORTCUT_BN", "1") != "0"
 # 7x7/2 stem computed as a 4x4/1 conv on a space-to-depth(2) input (GPU)
 S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
 
@@ -88,10 +98,14 @@ class Bottleneck(nn.Module):
         # x feeds both `down` and conv1: conv1 (created later, so its backward runs first) hands its dx
         # to down's dgrad epilogue, which adds it -- no separate gradient-add pass over x
         dh = GradHandoff()
-        sc = self.down(x, grad_add=dh)
+        if FUSE_SHORTCUT_BN and self.down.eps == self.conv3.eps and self.down.momentum == self.conv3.momentum:
+            # the shortcut's BatchNorm is applied inside conv3's BN pass (no shortcut apply pass)
+            sc, rbn = self.down.forward_stats(x, grad_add=dh)
+        else:
+            sc, rbn = self.down(x, grad_add=dh), None
         h = self.conv1(x, producer_out=p1, dx_handoff=dh)
         h = self.conv2(h, producer_in=p1, producer_out=p2)
-        return self.conv3(h, resid=sc, producer_in=p2, producer_out=p3), p3
+        return self.conv3(h, resid=sc, producer_in=p2, producer_out=p3, resid_bn=rbn), p3
 
 
 class BasicBlock(nn.Module):
@@ -113,9 +127,12 @@ class BasicBlock(nn.Module):
             h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
             return self.conv2(h, resid=x, resid_handoff=ho, producer_in=p1, producer_out=p2), p2
         dh = GradHandoff()
-        sc = self.down(x, grad_add=dh)
+        if FUSE_SHORTCUT_BN and self.down.eps == self.conv2.eps and self.down.momentum == self.conv2.momentum:
+            sc, rbn = self.down.forward_stats(x, grad_add=dh)
+        else:
+            sc, rbn = self.down(x, grad_add=dh), None
         h = self.conv1(x, producer_out=p1, dx_handoff=dh)
-        return self.conv2(h, resid=sc, producer_in=p1, producer_out=p2), p2
+        return self.conv2(h, resid=sc, producer_in=p1, producer_out=p2, resid_bn=rbn), p2
 
 
 class Dense(nn.Module):

@@ -24,8 +24,8 @@ from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
 
 # Per-channel statistics buffers are "slotted" ([2C final][STAT_SLOTS x 2C][counter]):
-# producers spread their atomics over the slots and the last block folds them
-# (csrc/kernels/common.h slotted_finalize). Must match zoo::kStatSlots.
+# producers spread their atomics over the slots and stats_finalize_kernel folds them
+# (csrc/kernels/bn.hip). Must match zoo::kStatSlots.
 STAT_SLOTS = 16
 
 
@@ -101,9 +101,10 @@ class _ConvBNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
                 relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None,
-                dx_out=None):
+                dx_out=None, resid_bn=None, gamma2=None, beta2=None):
         C_ = native()
         K = w.shape[0]
+        ctx.resid_bn = resid_bn if (resid_bn is not None and training) else None
         ctx.handoff_out, ctx.handoff_in, ctx.dx_out = handoff_out, handoff_in, dx_out
         ctx.producer_in = producer_in
         wb = bf16_weight(w)
@@ -114,9 +115,19 @@ class _ConvBNActFn(torch.autograd.Function):
             all_reduce_stats(stats[:2 * K], y.numel() // K)
         smean = torch.empty(K, device=x.device, dtype=torch.float32)
         sinv = torch.empty(K, device=x.device, dtype=torch.float32)
+        rb = ctx.resid_bn
+        side = []
+        if rb is not None:
+            # `resid` is the raw shortcut conv output: its BatchNorm runs inside this apply pass
+            rb.smean = torch.empty(K, device=x.device, dtype=torch.float32)
+            rb.sinv = torch.empty(K, device=x.device, dtype=torch.float32)
+            side = [rb.stats, gamma2.detach(), beta2.detach(), rb.running_mean, rb.running_var, rb.smean, rb.sinv]
+            ctx.gamma2, ctx.beta2 = gamma2, beta2
         z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
                             beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,
-                            training)
+                            training, side)
+        if rb is not None:
+            ctx.yres = resid        # shortcut conv output: its BN backward needs it
         ctx.save_for_backward(x, w, gamma, y, z if relu else None, smean, sinv)
         ctx.meta = (R, S, stride, pad, relu, resid is not None, x.shape)
         ctx.producer_out = producer_out
@@ -155,6 +166,9 @@ class _ConvBNActFn(torch.autograd.Function):
         if dresid is not None and ctx.handoff_out is not None:
             ctx.handoff_out.grad = dresid   # consumed by the block's first conv (fused add)
             dresid = None
+        dgam2 = dbet2 = None
+        if ctx.resid_bn is not None and dresid is not None:
+            dresid, dgam2, dbet2 = _shortcut_bn_bwd(ctx, dresid, K)
         dx = None
         if ctx.needs_input_grad[0]:
             add = None
@@ -181,7 +195,8 @@ class _ConvBNActFn(torch.autograd.Function):
         if own_b:
             _notify(ctx.beta_ref)
         return (dx, None if own_w else gw.to(w.dtype), None if own_g else dgam, None if own_b else dbet, dresid,
-                None, None, None, None, None, None, None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None, None, None, None, None, None,
+                None, dgam2, dbet2)
 
 
 class _ConvBNActFnB(_ConvBNActFn):
@@ -190,11 +205,108 @@ class _ConvBNActFnB(_ConvBNActFn):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad, eps, momentum,
                 relu, training, handoff_out=None, handoff_in=None, producer_in=None, producer_out=None,
-                dx_out=None):
+                dx_out=None, resid_bn=None, gamma2=None, beta2=None):
         ctx.beta_ref = beta
         return _ConvBNActFn.forward(ctx, x, w, gamma, beta, resid, running_mean, running_var, R, S, stride, pad,
                                     eps, momentum, relu, training, handoff_out, handoff_in, producer_in,
-                                    producer_out, dx_out)
+                                    producer_out, dx_out, resid_bn, gamma2, beta2)
+
+
+class ShortcutBN:
+    """The BatchNorm of a projection shortcut whose apply is fused into the block's last
+    unit: ``conv_stats`` fills ``stats`` (the shortcut conv's epilogue statistics), the last
+    unit's BN apply normalises the raw shortcut output with them in the same pass
+    (bn_fwd_apply resid_bn) and its backward runs this BatchNorm's backward, handing the
+    shortcut conv the gradient of its raw output. The shortcut's own apply pass and its
+    normalised output tensor are never materialised."""
+    __slots__ = ("stats", "running_mean", "running_var", "smean", "sinv", "sync", "m_local")
+
+    def __init__(self, running_mean, running_var):
+        self.running_mean, self.running_var = running_mean, running_var
+        self.stats = self.smean = self.sinv = None
+        self.sync, self.m_local = False, 0
+
+
+def _shortcut_bn_bwd(ctx, dres, K):
+    """BatchNorm backward of the fused shortcut: (sum dz, sum dz*xhat) over the raw
+    shortcut output, then dx = A dz + B x + D. Returns (d_raw, dgamma2, dbeta2)."""
+    C_ = native()
+    rb, yres = ctx.resid_bn, ctx.yres
+    gamma2, beta2 = ctx.gamma2, ctx.beta2
+    sums = workspace.zeros(stat_len(K), dres.device)
+    C_.bn_reduce(dres, None, yres, rb.smean, rb.sinv, sums, 1)
+    dgam, own_g = _grad_target(gamma2)
+    dbet, own_b = _grad_target(beta2)
+    dg, db = dgam, dbet
+    if rb.sync:
+        if dgam is not None:
+            dgam.add_(sums[K:2 * K])
+        if dbet is not None:
+            dbet.add_(sums[:K])
+        all_reduce_stats(sums[:2 * K], rb.m_local)
+        dg = db = None
+    outs = C_.bn_bwd_apply(dres, None, yres, rb.smean, rb.sinv, gamma2.detach(), sums, False, dg, db)
+    if own_g:
+        _notify(gamma2)
+    if own_b:
+        _notify(beta2)
+    ctx.yres = ctx.resid_bn = None
+    return outs[0], (None if own_g else dgam), (None if own_b else dbet)
+
+
+class _ConvStatsFn(torch.autograd.Function):
+    """Projection-shortcut conv with BatchNorm statistics only (its BN is applied by the
+    block's last unit, see ShortcutBN). Backward: dgrad (adding the gradient handed off by
+    the block's first conv, GradHandoff) + wgrad of the raw-output gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, R, S, stride, pad, holder, handoff_in):
+        K = w.shape[0]
+        stats = workspace.zeros(stat_len(K), x.device)
+        y = _kern.conv_fwd(x, bf16_weight(w), R, S, stride, pad, stats=stats)
+        holder.sync = sync_bn_active()
+        holder.m_local = y.numel() // K
+        if holder.sync:
+            all_reduce_stats(stats[:2 * K], holder.m_local)
+        holder.stats = stats
+        ctx.save_for_backward(x, w)
+        ctx.meta = (R, S, stride, pad, x.shape)
+        ctx.handoff_in = handoff_in
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        C_ = native()
+        x, w = ctx.saved_tensors
+        R, S, stride, pad, xshape = ctx.meta
+        dy = dy.contiguous()
+        if dy.dtype != torch.bfloat16:
+            dy = dy.to(torch.bfloat16)
+        K = w.shape[0]
+        dx = None
+        if ctx.needs_input_grad[0]:
+            add = None
+            if ctx.handoff_in is not None:
+                add = ctx.handoff_in.grad
+                ctx.handoff_in.grad = None
+                if add is None:
+                    raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
+            dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, xshape[3], xshape[1], xshape[2], stride, pad,
+                                  resid=add, resid_inplace=add is not None)
+        gw, own_w = _grad_target(w)
+        C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
+        if own_w:
+            _notify(w)
+        return dx, None if own_w else gw.to(w.dtype), None, None, None, None, None, None
+
+
+def conv_stats(x, w, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0), grad_add=None):
+    """Training-mode projection shortcut (GPU): (raw conv output, ShortcutBN) -- the BN is
+    applied by the consumer unit (``conv_bn_act(..., resid=raw, resid_bn=holder, ...)``)."""
+    holder = ShortcutBN(running_mean, running_var)
+    xb = (x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)).contiguous()
+    y = _ConvStatsFn.apply(xb, w, kernel[0], kernel[1], tuple(stride), tuple(pad), holder, grad_add)
+    return y, holder
 
 
 def bn_ref(y, gamma, beta, running_mean, running_var, eps, momentum, training):
@@ -249,7 +361,7 @@ def conv_bn_act_eval(x, w, gamma, beta, running_mean, running_var, kernel, strid
 
 def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0),
                 eps=1e-5, momentum=0.1, relu=True, resid=None, training=True, resid_handoff=None, grad_add=None,
-                producer_in=None, producer_out=None, dx_handoff=None):
+                producer_in=None, producer_out=None, dx_handoff=None, resid_bn=None):
     """z = relu?(BN(conv(x)) + resid) for NHWC input with a packed weight.
 
     ``resid_handoff``/``grad_add``: a shared :class:`GradHandoff` that routes the
@@ -261,7 +373,9 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
     to be filled for this unit's own output. ``dx_handoff``: this unit's input
     gradient is handed to the unit whose ``grad_add`` is the same GradHandoff
     (which must run its backward later) instead of being returned — two
-    consumers of one tensor then need no separate gradient-add pass."""
+    consumers of one tensor then need no separate gradient-add pass.
+    ``resid_bn``: ``(ShortcutBN, gamma2, beta2)`` -- ``resid`` is a raw shortcut conv output
+    (``conv_stats``) whose BatchNorm is applied in this unit's apply pass (GPU training)."""
     R, S = kernel
     if x.is_cuda and not training and not (torch.is_grad_enabled() and (x.requires_grad or w.requires_grad)):
         return conv_bn_act_eval(x, w, gamma, beta, running_mean, running_var, kernel, tuple(stride), tuple(pad),
@@ -271,9 +385,15 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
             x = x.to(torch.bfloat16)
         if resid is not None:
             resid = resid.to(torch.bfloat16).contiguous()
+        holder, g2, b2 = resid_bn if resid_bn is not None else (None, None, None)
+        if holder is not None and not training:
+            raise ValueError("conv_bn_act: resid_bn (fused shortcut BatchNorm) is a training-mode path")
         return _ConvBNActFnB.apply(x.contiguous(), w, gamma, beta, resid, running_mean, running_var, R, S,
                                    tuple(stride), tuple(pad), float(eps), float(momentum), bool(relu),
-                                   bool(training), resid_handoff, grad_add, producer_in, producer_out, dx_handoff)
+                                   bool(training), resid_handoff, grad_add, producer_in, producer_out, dx_handoff,
+                                   holder, g2, b2)
+    if resid_bn is not None:
+        raise ValueError("conv_bn_act: resid_bn (fused shortcut BatchNorm) needs the GPU path")
     y = conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1)))
     if training and sync_bn_active():
         z = sync_batch_norm(y.float(), gamma, beta, running_mean, running_var, eps, momentum)
