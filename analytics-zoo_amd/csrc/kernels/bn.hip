@@ -455,6 +455,194 @@ __global__ __launch_bounds__(256) void stats_part_lvl2_kernel(const float* __res
   out[c] += s;
 }
 
+// ---------------------------------------------------------------------------------------
+// Stem fusion: BatchNorm -> ReLU -> max-pool in one pass over the RAW conv output (ResNet
+// stem, reference SpatialBatchNormalization + ReLU + SpatialMaxPooling of
+// Zs/models/image/imageclassification ResNet). relu(sc*x + sh) is monotone in x (increasing
+// for sc >= 0, decreasing for sc < 0), so the pooled value is the affine image of the
+// window max (or min) of the raw x: the [N,H,W,C] BN output is never written. Per pooled
+// element the kernel keeps the raw winner (`best`, bf16 = exact) and its tap; a tap of
+// kClipped marks a pooled value the ReLU clipped (no gradient flows back through it).
+// Backward: (1) the BN reductions sum(dz), sum(dz*xhat) are taken in POOLED space (dz is
+// non-zero only at winning taps: xhat there is (best - mu) * invstd), (2) one pass over the
+// input gathers dz from the windows a pixel won and applies dx = A*dz + B*x + D. Together
+// they replace bn_fwd_apply + maxpool_fwd and maxpool_bwd + bn_reduce + bn_bwd_apply.
+// Row-per-block layout (power-of-two C/8 <= 256): each thread owns one fixed 8-channel
+// chunk (threadIdx & (C/8-1)), so its per-channel coefficients load once.
+constexpr uint8_t kClipped = 0xff;
+
+__global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
+    const bf16_t* __restrict__ X, const float* __restrict__ stats, const float* __restrict__ gamma,
+    const float* __restrict__ beta, bf16_t* __restrict__ Y, bf16_t* __restrict__ best_out,
+    uint8_t* __restrict__ arg, float* __restrict__ running_mean, float* __restrict__ running_var,
+    float* __restrict__ save_mean, float* __restrict__ save_invstd, int M, float eps, float momentum, int H, int W,
+    int C, int P, int Q, int R, int S, int sh_, int sw_, int ph, int pw, int lg) {
+  if (blockIdx.x == 0)
+    bn_bookkeeping(stats, running_mean, running_var, save_mean, save_invstd, M, C, eps, momentum);
+  const float invM = 1.f / (float)M;
+  const int mask = (C >> 3) - 1;
+  const int chunk = threadIdx.x & mask;
+  float sc[8], sh[8], sg[8];
+  bn_coeffs(stats, gamma, beta, chunk, C, invM, eps, sc, sh);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) sg[e] = sc[e] >= 0.f ? 1.f : -1.f;
+  const int row = blockIdx.x;  // n * P + p
+  const int n = row / P, p = row - n * P;
+  const int r_lo = max(0, ph - p * sh_), r_hi = min(R, H + ph - p * sh_);
+  const bf16_t* xn = X + (size_t)n * H * W * C + (ptrdiff_t)(p * sh_ - ph) * W * C;
+  const size_t ybase = (size_t)row * Q * C;
+  for (int j = threadIdx.x; j < (Q << lg); j += 256) {
+    const int q = j >> lg;
+    const int s_lo = max(0, pw - q * sw_), s_hi = min(S, W + pw - q * sw_);
+    float bt[8];  // best of sg * x
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { bt[e] = -INFINITY; bi[e] = 0; }
+    const bf16_t* xq = xn + (ptrdiff_t)(q * sw_ - pw) * C + chunk * 8;
+    for (int r = r_lo; r < r_hi; ++r) {
+      for (int s = s_lo; s < s_hi; ++s) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(xq + (r * W + s) * C), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float t = sg[e] * v[e];
+          if (t > bt[e]) { bt[e] = t; bi[e] = (uint8_t)(r * S + s); }
+        }
+      }
+    }
+    float b[8], o[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      b[e] = sg[e] * bt[e];
+      const float z = b[e] * sc[e] + sh[e];
+      o[e] = z > 0.f ? z : 0.f;
+      if (!(z > 0.f)) bi[e] = kClipped;
+    }
+    const size_t off = ybase + (size_t)j * 8;
+    *reinterpret_cast<uint4*>(Y + off) = pack8(o);
+    *reinterpret_cast<uint4*>(best_out + off) = pack8(b);
+    uint2 pk;
+    pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+    pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+    *reinterpret_cast<uint2*>(arg + off) = pk;
+  }
+}
+
+// sums[c] += sum dz, sums[C + c] += sum dz * xhat over the pooled elements (grid-strided rows)
+__global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_reduce_kernel(
+    const bf16_t* __restrict__ dY, const bf16_t* __restrict__ best, const uint8_t* __restrict__ arg,
+    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, float* __restrict__ sums, int rows,
+    int Q, int C, int lg) {
+  __shared__ float red[256][17];
+  const int mask = (C >> 3) - 1;
+  const int chunk = threadIdx.x & mask;
+  float mu[8], is[8], s1[8], s2[8];
+  load8f(save_mean, chunk, mu);
+  load8f(save_invstd, chunk, is);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const size_t base = (size_t)row * Q * C;
+    for (int j = threadIdx.x; j < (Q << lg); j += 256) {
+      const size_t off = base + (size_t)j * 8;
+      const uint2 ab = *reinterpret_cast<const uint2*>(arg + off);
+      float g[8], b[8];
+      unpack8(*reinterpret_cast<const uint4*>(dY + off), g);
+      unpack8(*reinterpret_cast<const uint4*>(best + off), b);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const uint32_t t = ((e < 4 ? ab.x : ab.y) >> (8 * (e & 3))) & 0xff;
+        const float d = t == kClipped ? 0.f : g[e];
+        s1[e] += d;
+        s2[e] += d * ((b[e] - mu[e]) * is[e]);
+      }
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { red[threadIdx.x][e] = s1[e]; red[threadIdx.x][8 + e] = s2[e]; }
+  __syncthreads();
+  const int lanes = 256 >> lg;  // threads sharing one chunk: tid = lane * (C/8) + chunk
+  for (int i = threadIdx.x; i < 2 * C; i += 256) {
+    const int which = i >= C, c = i - which * C, ch = c >> 3, e = c & 7;
+    float a = 0.f;
+    for (int l = 0; l < lanes; ++l) a += red[(l << lg) + ch][which * 8 + e];
+    atomicAdd(sums + i, a);
+  }
+}
+
+// dx = A*dz + B*x + D with dz gathered from the pooled windows this pixel won
+__global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_apply_kernel(
+    const bf16_t* __restrict__ dY, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ X,
+    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, const float* __restrict__ gamma,
+    const float* __restrict__ sums, bf16_t* __restrict__ dX, float* __restrict__ dgamma, float* __restrict__ dbeta,
+    int M, int H, int W, int C, int P, int Q, int R, int S, int sh_, int sw_, int ph, int pw, int lg) {
+  if (blockIdx.x == 0) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      if (dgamma) dgamma[c] += sums[C + c];
+      if (dbeta) dbeta[c] += sums[c];
+    }
+  }
+  const float invM = 1.f / (float)M;
+  const int mask = (C >> 3) - 1;
+  const int chunk = threadIdx.x & mask;
+  float ka[8], kb[8], kd[8];
+  {
+    float is8[8], mu8[8], g8[8], q1[8], q2[8];
+    load8f(save_invstd, chunk, is8);
+    load8f(save_mean, chunk, mu8);
+    load8f(sums, chunk, q1);
+    load8f(sums + C, chunk, q2);
+    if (gamma) load8f(gamma, chunk, g8);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float is = is8[e], mu = mu8[e];
+      const float a = (gamma ? g8[e] : 1.f) * is;
+      const float m1 = q1[e] * invM, m2 = q2[e] * invM;
+      ka[e] = a;
+      kb[e] = -a * is * m2;
+      kd[e] = a * (mu * is * m2 - m1);
+    }
+  }
+  const int row = blockIdx.x;  // n * H + h
+  const int n = row / H, h = row - n * H;
+  const int p_lo = max(0, (h + ph - R + sh_) / sh_);
+  const int p_hi = min(P - 1, (h + ph) / sh_);
+  const size_t nb = (size_t)n * P * Q * C + chunk * 8;
+  const size_t xbase = (size_t)row * W * C;
+  for (int j = threadIdx.x; j < (W << lg); j += 256) {
+    const int w = j >> lg;
+    const int q_lo = max(0, (w + pw - S + sw_) / sw_);
+    const int q_hi = min(Q - 1, (w + pw) / sw_);
+    float dz[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) dz[e] = 0.f;
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * sh_ - ph);
+      if (r < 0 || r >= R) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * sw_ - pw);
+        if (s < 0 || s >= S) continue;
+        const uint32_t tap = (uint32_t)(r * S + s);
+        const size_t o = nb + (size_t)(p * Q + q) * C;
+        const uint2 ab = *reinterpret_cast<const uint2*>(arg + o);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dY + o), g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (((ab.x >> (8 * e)) & 0xff) == tap) dz[e] += g[e];
+          if (((ab.y >> (8 * e)) & 0xff) == tap) dz[4 + e] += g[4 + e];
+        }
+      }
+    }
+    const size_t off = xbase + (size_t)j * 8;
+    float x[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(X + off), x);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = ka[e] * dz[e] + kb[e] * x[e] + kd[e];
+    *reinterpret_cast<uint4*>(dX + off) = pack8(o);
+  }
+}
+
 // contiguous row range per block: ~kApplyBlocks blocks, at least kMinRows rows per thread-row
 static int apply_rows_per_block(int M, int C) {
   static const int target = [] {
@@ -630,4 +818,39 @@ extern "C" int zoo_act_bwd_reduce(const void* dZ, const void* Z, void* dY, float
   }
 #undef ZOO_COLSUM
   return ch;
+}
+
+// fused stem BN -> ReLU -> max-pool (see bn_relu_maxpool_fwd_kernel); C/8 must be a power of
+// two <= 256, R*S < 255 (checked by the caller)
+static int pool_row_lg(int C) {
+  const int cpr = C >> 3;
+  int lg = 0;
+  while ((1 << lg) < cpr) ++lg;
+  return lg;
+}
+
+extern "C" hipError_t zoo_bn_relu_maxpool_fwd(const void* X, const float* stats, const float* gamma,
+                                              const float* beta, void* Y, void* best, void* arg, float* rmean,
+                                              float* rvar, float* smean, float* sinv, float eps, float momentum,
+                                              int N, int H, int W, int C, int P, int Q, int R, int S, int sh, int sw,
+                                              int ph, int pw, hipStream_t st) {
+  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(N * P), dim3(256), 0, st, (const bf16_t*)X, stats, gamma,
+                     beta, (bf16_t*)Y, (bf16_t*)best, (uint8_t*)arg, rmean, rvar, smean, sinv, N * H * W, eps,
+                     momentum, H, W, C, P, Q, R, S, sh, sw, ph, pw, pool_row_lg(C));
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_bn_relu_maxpool_bwd(const void* dY, const void* best, const void* arg, const void* X,
+                                              const float* smean, const float* sinv, const float* gamma,
+                                              float* sums, void* dX, float* dgamma, float* dbeta, int N, int H,
+                                              int W, int C, int P, int Q, int R, int S, int sh, int sw, int ph,
+                                              int pw, hipStream_t st) {
+  const int lg = pool_row_lg(C);
+  const int rows = N * P;
+  hipLaunchKernelGGL(bn_relu_maxpool_bwd_reduce_kernel, dim3(rows < 512 ? rows : 512), dim3(256), 0, st,
+                     (const bf16_t*)dY, (const bf16_t*)best, (const uint8_t*)arg, smean, sinv, sums, rows, Q, C, lg);
+  hipLaunchKernelGGL(bn_relu_maxpool_bwd_apply_kernel, dim3(N * H), dim3(256), 0, st, (const bf16_t*)dY,
+                     (const uint8_t*)arg, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, dgamma, dbeta,
+                     N * H * W, H, W, C, P, Q, R, S, sh, sw, ph, pw, lg);
+  return hipGetLastError();
 }

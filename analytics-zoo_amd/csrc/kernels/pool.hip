@@ -96,6 +96,100 @@ __global__ __launch_bounds__(256) void maxpool_bwd_kernel(const bf16_t* __restri
   }
 }
 
+// Row-per-block variants for a power-of-two C/8 (ResNet stem, every NHWC net with C % 64
+// == 0 ...): one block owns one (n, output row) [fwd] or (n, input row) [bwd], so the
+// row's window bounds are block-uniform (scalar) and the per-thread index split is a
+// shift/mask. The grid-stride kernels above spend ~6 integer divisions per element and
+// ran VALU-bound (stem bwd 236 us = 2.4 TB/s at b256).
+__global__ __launch_bounds__(256) void maxpool_fwd_row_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                              uint8_t* __restrict__ arg, int H, int W, int C, int P,
+                                                              int Q, int R, int S, int sh, int sw, int ph, int pw,
+                                                              int lg) {
+  const int row = blockIdx.x;  // n * P + p
+  const int n = row / P, p = row - n * P;
+  const int mask = (C >> 3) - 1;
+  const int r_lo = max(0, ph - p * sh), r_hi = min(R, H + ph - p * sh);
+  const bf16_t* xn = X + (size_t)n * H * W * C + (size_t)(p * sh - ph) * W * C;
+  const size_t ybase = (size_t)row * Q * C;
+  for (int j = threadIdx.x; j < (Q << lg); j += 256) {
+    const int q = j >> lg, chunk = j & mask;
+    const int s_lo = max(0, pw - q * sw), s_hi = min(S, W + pw - q * sw);
+    float best[8];
+    uint8_t bi[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { best[e] = -INFINITY; bi[e] = 0; }
+    const bf16_t* xq = xn + (q * sw - pw) * C + chunk * 8;
+    for (int r = r_lo; r < r_hi; ++r) {
+      for (int s = s_lo; s < s_hi; ++s) {
+        float v[8];
+        unpack8(*reinterpret_cast<const uint4*>(xq + (r * W + s) * C), v);
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (v[e] > best[e]) { best[e] = v[e]; bi[e] = (uint8_t)(r * S + s); }
+      }
+    }
+    const size_t o = ybase + (size_t)j * 8;
+    *reinterpret_cast<uint4*>(Y + o) = pack8(best);
+    if (arg) {
+      uint2 pk;
+      pk.x = bi[0] | (bi[1] << 8) | (bi[2] << 16) | ((uint32_t)bi[3] << 24);
+      pk.y = bi[4] | (bi[5] << 8) | (bi[6] << 16) | ((uint32_t)bi[7] << 24);
+      *reinterpret_cast<uint2*>(arg + o) = pk;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void maxpool_bwd_row_kernel(const bf16_t* __restrict__ dY,
+                                                              const uint8_t* __restrict__ arg,
+                                                              bf16_t* __restrict__ dX, int H, int W, int C, int P,
+                                                              int Q, int R, int S, int sh, int sw, int ph, int pw,
+                                                              int lg) {
+  const int row = blockIdx.x;  // n * H + h
+  const int n = row / H, h = row - n * H;
+  const int mask = (C >> 3) - 1;
+  // output rows p with p*sh - ph <= h <= p*sh - ph + R - 1 (block-uniform)
+  const int p_lo = max(0, (h + ph - R + sh) / sh);
+  const int p_hi = min(P - 1, (h + ph) / sh);
+  const size_t nb = (size_t)n * P * Q * C;
+  const size_t xbase = (size_t)row * W * C;
+  for (int j = threadIdx.x; j < (W << lg); j += 256) {
+    const int w = j >> lg, chunk = j & mask;
+    const int q_lo = max(0, (w + pw - S + sw) / sw);
+    const int q_hi = min(Q - 1, (w + pw) / sw);
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int p = p_lo; p <= p_hi; ++p) {
+      const int r = h - (p * sh - ph);
+      if (r < 0 || r >= R) continue;
+      for (int q = q_lo; q <= q_hi; ++q) {
+        const int s = w - (q * sw - pw);
+        if (s < 0 || s >= S) continue;
+        const uint32_t tap = (uint32_t)(r * S + s);
+        const size_t o = nb + (size_t)(p * Q + q) * C + chunk * 8;
+        const uint2 ab = *reinterpret_cast<const uint2*>(arg + o);
+        float g[8];
+        unpack8(*reinterpret_cast<const uint4*>(dY + o), g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (((ab.x >> (8 * e)) & 0xff) == tap) acc[e] += g[e];
+          if (((ab.y >> (8 * e)) & 0xff) == tap) acc[4 + e] += g[4 + e];
+        }
+      }
+    }
+    *reinterpret_cast<uint4*>(dX + xbase + (size_t)j * 8) = pack8(acc);
+  }
+}
+
+// log2 of C/8 when it is a power of two, else -1 (row kernels not applicable)
+static int row_lg(int C) {
+  const int cpr = C >> 3;
+  if (cpr <= 0 || (cpr & (cpr - 1))) return -1;
+  int lg = 0;
+  while ((1 << lg) < cpr) ++lg;
+  return lg;
+}
+
 // global average pool [N][HW][C] -> [N][C] (fp32 accumulate, bf16 or fp32 out)
 __global__ __launch_bounds__(256) void gap_fwd_kernel(const bf16_t* __restrict__ X, bf16_t* __restrict__ Y,
                                                       int N, int HW, int C) {
@@ -224,6 +318,12 @@ using namespace zoo;
 
 extern "C" hipError_t zoo_maxpool_fwd(const void* X, void* Y, void* arg, int N, int H, int W, int C, int P, int Q,
                                       int R, int S, int sh, int sw, int ph, int pw, hipStream_t st) {
+  const int lg = row_lg(C);
+  if (lg >= 0 && R * S <= 256) {
+    hipLaunchKernelGGL(maxpool_fwd_row_kernel, dim3(N * P), dim3(256), 0, st, (const bf16_t*)X, (bf16_t*)Y,
+                       (uint8_t*)arg, H, W, C, P, Q, R, S, sh, sw, ph, pw, lg);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(maxpool_fwd_kernel, dim3(pgrid((size_t)N * P * Q * (C / 8))), dim3(256), 0, st,
                      (const bf16_t*)X, (bf16_t*)Y, (uint8_t*)arg, N, H, W, C, P, Q, R, S, sh, sw, ph, pw);
   return hipGetLastError();
@@ -231,6 +331,12 @@ extern "C" hipError_t zoo_maxpool_fwd(const void* X, void* Y, void* arg, int N, 
 
 extern "C" hipError_t zoo_maxpool_bwd(const void* dY, const void* arg, void* dX, int N, int H, int W, int C, int P,
                                       int Q, int R, int S, int sh, int sw, int ph, int pw, hipStream_t st) {
+  const int lg = row_lg(C);
+  if (lg >= 0 && R * S <= 256) {
+    hipLaunchKernelGGL(maxpool_bwd_row_kernel, dim3(N * H), dim3(256), 0, st, (const bf16_t*)dY,
+                       (const uint8_t*)arg, (bf16_t*)dX, H, W, C, P, Q, R, S, sh, sw, ph, pw, lg);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(maxpool_bwd_kernel, dim3(pgrid((size_t)N * H * W * (C / 8))), dim3(256), 0, st,
                      (const bf16_t*)dY, (const uint8_t*)arg, (bf16_t*)dX, N, H, W, C, P, Q, R, S, sh, sw, ph, pw);
   return hipGetLastError();

@@ -47,6 +47,12 @@ hipError_t zoo_bn_bwd_apply(const void*, const void*, const void*, const float*,
                             const float*, void*, void*, float*, float*, int, int, hipStream_t);
 hipError_t zoo_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                            hipStream_t);
+hipError_t zoo_bn_relu_maxpool_fwd(const void*, const float*, const float*, const float*, void*, void*, void*, float*,
+                                   float*, float*, float*, float, float, int, int, int, int, int, int, int, int, int,
+                                   int, int, int, hipStream_t);
+hipError_t zoo_bn_relu_maxpool_bwd(const void*, const void*, const void*, const void*, const float*, const float*,
+                                   const float*, float*, void*, float*, float*, int, int, int, int, int, int, int, int,
+                                   int, int, int, int, hipStream_t);
 hipError_t zoo_maxpool_bwd(const void*, const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
                            hipStream_t);
 hipError_t zoo_gap_fwd(const void*, void*, int, int, int, hipStream_t);
@@ -684,6 +690,69 @@ torch::Tensor maxpool_bwd(torch::Tensor dy, torch::Tensor arg, int H, int W, int
   return dx;
 }
 
+
+// Fused BatchNorm(training stats) -> ReLU -> max-pool over a raw conv output x [N,H,W,C]
+// (ResNet stem). Returns {pooled, raw winner, tap}; see bn_relu_maxpool_fwd_kernel.
+static void check_stem_pool(const torch::Tensor& x, int R, int S, int ph, int pw) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "bn_relu_maxpool: NHWC with C%8==0");
+  const int cpr = x.size(3) / 8;
+  TORCH_CHECK((cpr & (cpr - 1)) == 0 && cpr <= 256, "bn_relu_maxpool: C/8 must be a power of two <= 256");
+  TORCH_CHECK(R * S < 255 && 2 * ph < R + 1 && 2 * pw < S + 1, "bn_relu_maxpool: window/padding");
+  TORCH_CHECK(x.numel() < (1LL << 31), "bn_relu_maxpool: tensor too large for 32-bit indexing");
+}
+
+std::vector<torch::Tensor> bn_relu_maxpool_fwd(torch::Tensor x, torch::Tensor stats, torch::Tensor gamma,
+                                               torch::Tensor beta, torch::Tensor rmean, torch::Tensor rvar,
+                                               torch::Tensor smean, torch::Tensor sinv, double eps, double momentum,
+                                               int R, int S, int sh, int sw, int ph, int pw) {
+  check_stem_pool(x, R, S, ph, pw);
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  for (auto* t : {&stats, &gamma, &beta, &rmean, &rvar, &smean, &sinv}) req(*t, at::kFloat, "bn vector");
+  TORCH_CHECK(stats.numel() >= 2 * C && gamma.numel() == C && beta.numel() == C && rmean.numel() == C &&
+                  rvar.numel() == C && smean.numel() == C && sinv.numel() == C, "bn_relu_maxpool: vector sizes");
+  const int P = pool_out(H, R, sh, ph, false), Q = pool_out(W, S, sw, pw, false);
+  TORCH_CHECK(P > 0 && Q > 0, "bn_relu_maxpool: empty output");
+  auto y = torch::empty({N, P, Q, C}, x.options());
+  auto best = torch::empty({N, P, Q, C}, x.options());
+  auto arg = torch::empty({N, P, Q, C}, x.options().dtype(at::kByte));
+  check_hip(zoo_bn_relu_maxpool_fwd(x.data_ptr(), stats.data_ptr<float>(), gamma.data_ptr<float>(),
+                                    beta.data_ptr<float>(), y.data_ptr(), best.data_ptr(), arg.data_ptr(),
+                                    rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(),
+                                    sinv.data_ptr<float>(), (float)eps, (float)momentum, N, H, W, C, P, Q, R, S, sh,
+                                    sw, ph, pw, cur_stream()),
+            "bn_relu_maxpool_fwd");
+  return {y, best, arg};
+}
+
+// backward of bn_relu_maxpool_fwd: sums (>= 2C fp32, zeroed by the caller) receive
+// (sum dz, sum dz*xhat); dgamma/dbeta (optional) += them; returns dx [N,H,W,C]
+torch::Tensor bn_relu_maxpool_bwd(torch::Tensor dy, torch::Tensor best, torch::Tensor arg, torch::Tensor x,
+                                  torch::Tensor smean, torch::Tensor sinv, torch::Tensor gamma, torch::Tensor sums,
+                                  c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta, int R,
+                                  int S, int sh, int sw, int ph, int pw) {
+  check_stem_pool(x, R, S, ph, pw);
+  req(dy, at::kBFloat16, "dy");
+  req(best, at::kBFloat16, "best");
+  req(arg, at::kByte, "arg");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  const int P = pool_out(H, R, sh, ph, false), Q = pool_out(W, S, sw, pw, false);
+  const std::vector<int64_t> pshape{N, P, Q, C};
+  TORCH_CHECK(dy.sizes() == pshape && best.sizes() == pshape && arg.sizes() == pshape,
+              "bn_relu_maxpool_bwd: pooled tensors must be [N,P,Q,C]");
+  for (auto* t : {&smean, &sinv, &gamma, &sums}) req(*t, at::kFloat, "bn vector");
+  TORCH_CHECK(smean.numel() == C && sinv.numel() == C && gamma.numel() == C && sums.numel() >= 2 * C,
+              "bn_relu_maxpool_bwd: vector sizes");
+  if (dgamma.has_value()) TORCH_CHECK(dgamma->numel() == C && dgamma->scalar_type() == at::kFloat, "dgamma");
+  if (dbeta.has_value()) TORCH_CHECK(dbeta->numel() == C && dbeta->scalar_type() == at::kFloat, "dbeta");
+  auto dx = torch::empty_like(x);
+  check_hip(zoo_bn_relu_maxpool_bwd(dy.data_ptr(), best.data_ptr(), arg.data_ptr(), x.data_ptr(),
+                                    smean.data_ptr<float>(), sinv.data_ptr<float>(), gamma.data_ptr<float>(),
+                                    sums.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dgamma),
+                                    opt_ptr<float>(dbeta), N, H, W, C, P, Q, R, S, sh, sw, ph, pw, cur_stream()),
+            "bn_relu_maxpool_bwd");
+  return dx;
+}
 
 std::vector<int64_t> pool_shape(int H, int W, int R, int S, int sh, int sw, int ph, int pw, bool ceil_mode) {
   return {pool_out(H, R, sh, ph, ceil_mode), pool_out(W, S, sw, pw, ceil_mode)};
@@ -1848,6 +1917,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);
+  m.def("bn_relu_maxpool_bwd", &bn_relu_maxpool_bwd);
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("softmax_xent", &softmax_xent);

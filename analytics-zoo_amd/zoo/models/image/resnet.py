@@ -17,7 +17,7 @@ import torch
 import torch.nn as nn
 
 from zoo import ops
-from zoo.ops.bn import BNProducer, GradHandoff, conv_stats
+from zoo.ops.bn import BNProducer, GradHandoff, bn_relu_maxpool, conv_stats, stem_pool_fusable
 
 
 class ConvBN(nn.Module):
@@ -57,6 +57,8 @@ class ConvBN(nn.Module):
 FUSE_BN_BACKWARD = True
 # projection-shortcut BatchNorm applied inside the block's last BN pass (ShortcutBN)
 FUSE_SHORTCUT_BN = os.environ.get("ZOO_FUSE_SHORTCUT_BN", "1") != "0"
+# ResNet stem BatchNorm + ReLU fused into the max-pool pass (bn_relu_maxpool)
+FUSE_STEM_POOL = os.environ.get("ZOO_FUSE_STEM_POOL", "1") != "0"
 # 7x7/2 stem computed as a 4x4/1 conv on a space-to-depth(2) input (GPU)
 S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
 
@@ -205,19 +207,37 @@ class ResNet(nn.Module):
         w8 = torch.nn.functional.pad(w7, (0, 0, 0, 1, 0, 1))                 # [K, 8, 8, 4]
         return w8.reshape(K, 4, 2, 4, 2, 4).permute(0, 1, 3, 2, 4, 5).reshape(K, 256).contiguous()
 
+    def _stem_bn(self, y, holder):
+        """Unfused fallback of the stem-pool fusion: BN+ReLU of the raw stem output (its
+        statistics were already taken by the conv and are recomputed by batch_norm_nhwc)."""
+        st = self.stem
+        holder.stats = None
+        return ops.batch_norm_nhwc(y, st.gamma, st.beta, st.running_mean, st.running_var, st.eps, st.momentum,
+                                   relu=True, training=True)
+
     def forward(self, x):
         if self._stem_s2d_ok(x):
             # stem as a 4x4 stride-1 conv on the space-to-depth(2) image: 16 input channels
             # take the vector implicit-GEMM path; the NCHW->NHWC pass becomes the s2d pass
             xs = ops.native().nchw_to_s2d(x.float().contiguous(), 3)
             st = self.stem
-            x = ops.conv_bn_act(xs, self._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
-                                kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
-                                relu=True, training=st.training)
+            if st.training and FUSE_STEM_POOL and torch.is_grad_enabled():
+                # stem BN + ReLU applied inside the max-pool pass (bn_relu_maxpool): the conv
+                # emits statistics only and the 112x112 BN output is never written
+                y, holder = conv_stats(xs, self._s2d_weight(), st.running_mean, st.running_var, kernel=(4, 4))
+                if stem_pool_fusable(y, (3, 3), (1, 1)):
+                    x = bn_relu_maxpool(y, holder, st.gamma, st.beta, st.eps, st.momentum)
+                else:
+                    x = ops.max_pool2d_nhwc(self._stem_bn(y, holder), (3, 3), (2, 2), (1, 1))
+            else:
+                x = ops.conv_bn_act(xs, self._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
+                                    kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
+                                    relu=True, training=st.training)
+                x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
         else:
             x = self.to_nhwc(x)
             x = self.stem(x)
-        x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+            x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
         if self.training and _fusing(x):
             prod = None
             for stage in self.stages:

@@ -465,3 +465,58 @@ def batch_norm_nhwc(y, gamma, beta, running_mean, running_var, eps=1e-5, momentu
     if relu:
         z = torch.relu(z)
     return z.to(y.dtype)
+
+
+class _BNReluMaxPoolFn(torch.autograd.Function):
+    """Training-mode BatchNorm -> ReLU -> max-pool over a RAW conv output whose statistics
+    the conv epilogue produced (``conv_stats``): one pass forward, two backward, and the
+    [N,H,W,C] BN output is never materialised (csrc/kernels/bn.hip, stem fusion)."""
+
+    @staticmethod
+    def forward(ctx, y, gamma, beta, holder, eps, momentum, R, S, sh, sw, ph, pw):
+        K = y.shape[-1]
+        smean = torch.empty(K, device=y.device, dtype=torch.float32)
+        sinv = torch.empty(K, device=y.device, dtype=torch.float32)
+        out, best, arg = native().bn_relu_maxpool_fwd(y, holder.stats, gamma.detach().float().contiguous(),
+                                                      beta.detach().float().contiguous(), holder.running_mean,
+                                                      holder.running_var, smean, sinv, eps, momentum,
+                                                      R, S, sh, sw, ph, pw)
+        holder.stats = None
+        ctx.save_for_backward(y, gamma, beta, best, arg, smean, sinv)
+        ctx.geom = (R, S, sh, sw, ph, pw)
+        ctx.mark_non_differentiable(best, arg)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        y, gamma, beta, best, arg, smean, sinv = ctx.saved_tensors
+        dout = dout.contiguous()
+        if dout.dtype != torch.bfloat16:
+            dout = dout.to(torch.bfloat16)
+        K = y.shape[-1]
+        sums = workspace.zeros(stat_len(K), dout.device)
+        dgam, own_g = _grad_target(gamma)
+        dbet, own_b = _grad_target(beta)
+        dx = native().bn_relu_maxpool_bwd(dout, best, arg, y, smean, sinv, gamma.detach().float().contiguous(),
+                                          sums, dgam, dbet, *ctx.geom)
+        if own_g:
+            _notify(gamma)
+        if own_b:
+            _notify(beta)
+        return (dx, None if own_g else dgam, None if own_b else dbet) + (None,) * 9
+
+
+def stem_pool_fusable(y, kernel, pad):
+    """Whether ``bn_relu_maxpool`` applies: GPU, power-of-two C/8 <= 256, no SyncBN, and not
+    the deterministic mode (its pooled-space reduction uses fp32 atomics)."""
+    from zoo.ops._native import deterministic
+    cpr = y.shape[-1] // 8
+    return (y.is_cuda and y.shape[-1] % 8 == 0 and 0 < cpr <= 256 and (cpr & (cpr - 1)) == 0
+            and kernel[0] * kernel[1] < 255 and not sync_bn_active() and not deterministic())
+
+
+def bn_relu_maxpool(y, holder, gamma, beta, eps=1e-5, momentum=0.1, kernel=(3, 3), stride=(2, 2), pad=(1, 1)):
+    """relu(BN(y)) -> max_pool for a raw conv output ``y`` with its ``conv_stats`` holder
+    (training, GPU). Equals ``max_pool2d_nhwc(batch_norm_nhwc(y, ..., relu=True), ...)``."""
+    return _BNReluMaxPoolFn.apply(y, gamma, beta, holder, float(eps), float(momentum), kernel[0], kernel[1],
+                                  stride[0], stride[1], pad[0], pad[1])

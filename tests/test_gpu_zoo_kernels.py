@@ -78,6 +78,27 @@ def test_max_pool_ceil_mode(gpu):
     assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
 
 
+@pytest.mark.parametrize("N,H,W,C,k,s,p,ceil", [(2, 112, 112, 64, 3, 2, 1, False),   # ResNet stem
+                                                 (3, 17, 13, 128, 2, 2, 0, False),
+                                                 (2, 15, 15, 8, 3, 2, 1, True),
+                                                 (1, 9, 20, 256, 3, 1, 1, False),
+                                                 (2, 11, 11, 48, 3, 2, 1, False)])    # C/8 = 6: grid-stride kernel
+def test_max_pool_row_kernels(gpu, N, H, W, C, k, s, p, ceil):
+    """Row-per-block max-pool kernels (power-of-two C/8) fwd + bwd vs fp32 torch."""
+    from zoo.ops.pool import max_pool2d_nhwc
+    x = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    yr = F.max_pool2d(xr, k, s, p, ceil_mode=ceil)
+    xg = x.detach().clone().requires_grad_(True)
+    y = max_pool2d_nhwc(xg, (k, k), (s, s), (p, p), ceil_mode=ceil)
+    assert y.shape == (N, yr.shape[2], yr.shape[3], C)
+    assert torch.equal(y.float(), yr.detach().permute(0, 2, 3, 1))  # max of bf16 values is exact
+    dy = torch.randn_like(y)
+    y.backward(dy)
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+
+
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("log", [False, True])
 @pytest.mark.parametrize("n", [10, 1000, 4099])
