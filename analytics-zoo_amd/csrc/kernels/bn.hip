@@ -471,12 +471,17 @@ __global__ __launch_bounds__(256) void stats_part_lvl2_kernel(const float* __res
 // chunk (threadIdx & (C/8-1)), so its per-channel coefficients load once.
 constexpr uint8_t kClipped = 0xff;
 
+// STEM: the ResNet geometry (3x3, stride 2, pad 1) as compile-time constants, so the
+// window bounds and divisions fold (the runtime arguments are then ignored)
+template <bool STEM>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
     const bf16_t* __restrict__ X, const float* __restrict__ stats, const float* __restrict__ gamma,
     const float* __restrict__ beta, bf16_t* __restrict__ Y, bf16_t* __restrict__ best_out,
     uint8_t* __restrict__ arg, float* __restrict__ running_mean, float* __restrict__ running_var,
     float* __restrict__ save_mean, float* __restrict__ save_invstd, int M, float eps, float momentum, int H, int W,
-    int C, int P, int Q, int R, int S, int sh_, int sw_, int ph, int pw, int lg) {
+    int C, int P, int Q, int R_, int S_, int sh_r, int sw_r, int ph_r, int pw_r, int lg) {
+  const int R = STEM ? 3 : R_, S = STEM ? 3 : S_, sh_ = STEM ? 2 : sh_r, sw_ = STEM ? 2 : sw_r;
+  const int ph = STEM ? 1 : ph_r, pw = STEM ? 1 : pw_r;
   if (blockIdx.x == 0)
     bn_bookkeeping(stats, running_mean, running_var, save_mean, save_invstd, M, C, eps, momentum);
   const float invM = 1.f / (float)M;
@@ -571,11 +576,14 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_reduce_kernel(
 }
 
 // dx = A*dz + B*x + D with dz gathered from the pooled windows this pixel won
+template <bool STEM>
 __global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_apply_kernel(
     const bf16_t* __restrict__ dY, const uint8_t* __restrict__ arg, const bf16_t* __restrict__ X,
     const float* __restrict__ save_mean, const float* __restrict__ save_invstd, const float* __restrict__ gamma,
     const float* __restrict__ sums, bf16_t* __restrict__ dX, float* __restrict__ dgamma, float* __restrict__ dbeta,
-    int M, int H, int W, int C, int P, int Q, int R, int S, int sh_, int sw_, int ph, int pw, int lg) {
+    int M, int H, int W, int C, int P, int Q, int R_, int S_, int sh_r, int sw_r, int ph_r, int pw_r, int lg) {
+  const int R = STEM ? 3 : R_, S = STEM ? 3 : S_, sh_ = STEM ? 2 : sh_r, sw_ = STEM ? 2 : sw_r;
+  const int ph = STEM ? 1 : ph_r, pw = STEM ? 1 : pw_r;
   if (blockIdx.x == 0) {
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       if (dgamma) dgamma[c] += sums[C + c];
@@ -834,9 +842,11 @@ extern "C" hipError_t zoo_bn_relu_maxpool_fwd(const void* X, const float* stats,
                                               float* rvar, float* smean, float* sinv, float eps, float momentum,
                                               int N, int H, int W, int C, int P, int Q, int R, int S, int sh, int sw,
                                               int ph, int pw, hipStream_t st) {
-  hipLaunchKernelGGL(bn_relu_maxpool_fwd_kernel, dim3(N * P), dim3(256), 0, st, (const bf16_t*)X, stats, gamma,
-                     beta, (bf16_t*)Y, (bf16_t*)best, (uint8_t*)arg, rmean, rvar, smean, sinv, N * H * W, eps,
-                     momentum, H, W, C, P, Q, R, S, sh, sw, ph, pw, pool_row_lg(C));
+  const bool stem = R == 3 && S == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1;
+  hipLaunchKernelGGL(stem ? bn_relu_maxpool_fwd_kernel<true> : bn_relu_maxpool_fwd_kernel<false>, dim3(N * P),
+                     dim3(256), 0, st, (const bf16_t*)X, stats, gamma, beta, (bf16_t*)Y, (bf16_t*)best,
+                     (uint8_t*)arg, rmean, rvar, smean, sinv, N * H * W, eps, momentum, H, W, C, P, Q, R, S, sh, sw,
+                     ph, pw, pool_row_lg(C));
   return hipGetLastError();
 }
 
@@ -849,7 +859,9 @@ extern "C" hipError_t zoo_bn_relu_maxpool_bwd(const void* dY, const void* best, 
   const int rows = N * P;
   hipLaunchKernelGGL(bn_relu_maxpool_bwd_reduce_kernel, dim3(rows < 512 ? rows : 512), dim3(256), 0, st,
                      (const bf16_t*)dY, (const bf16_t*)best, (const uint8_t*)arg, smean, sinv, sums, rows, Q, C, lg);
-  hipLaunchKernelGGL(bn_relu_maxpool_bwd_apply_kernel, dim3(N * H), dim3(256), 0, st, (const bf16_t*)dY,
+  const bool stem = R == 3 && S == 3 && sh == 2 && sw == 2 && ph == 1 && pw == 1;
+  hipLaunchKernelGGL(stem ? bn_relu_maxpool_bwd_apply_kernel<true> : bn_relu_maxpool_bwd_apply_kernel<false>,
+                     dim3(N * H), dim3(256), 0, st, (const bf16_t*)dY,
                      (const uint8_t*)arg, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, dgamma, dbeta,
                      N * H * W, H, W, C, P, Q, R, S, sh, sw, ph, pw, lg);
   return hipGetLastError();

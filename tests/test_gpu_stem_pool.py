@@ -13,8 +13,10 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
 
 
-@pytest.mark.parametrize("N,H,W,C", [(2, 112, 112, 64), (3, 15, 17, 128), (2, 9, 8, 16)])
-def test_bn_relu_maxpool_vs_fp32(gpu, N, H, W, C):
+@pytest.mark.parametrize("N,H,W,C,k,s,p", [(2, 112, 112, 64, 3, 2, 1), (3, 15, 17, 128, 3, 2, 1),
+                                           (2, 9, 8, 16, 3, 2, 1),      # compile-time stem geometry
+                                           (2, 10, 13, 32, 2, 2, 0), (2, 11, 9, 64, 3, 1, 1)])  # generic
+def test_bn_relu_maxpool_vs_fp32(gpu, N, H, W, C, k, s, p):
     from zoo.ops.bn import ShortcutBN, bn_relu_maxpool, stat_len
     torch.manual_seed(0)
     y = (torch.randn(N, H, W, C, device=gpu) * 2 + 0.5).bfloat16()
@@ -27,13 +29,13 @@ def test_bn_relu_maxpool_vs_fp32(gpu, N, H, W, C):
     st[:C], st[C:2 * C] = yf.sum(0), (yf * yf).sum(0)
     holder.stats = st
     yg = y.clone().requires_grad_(True)
-    out = bn_relu_maxpool(yg, holder, gamma, beta, 1e-5, 0.1)
+    out = bn_relu_maxpool(yg, holder, gamma, beta, 1e-5, 0.1, (k, k), (s, s), (p, p))
 
     yr = y.float().permute(0, 3, 1, 2).requires_grad_(True)
     gr, br = gamma.detach().clone().requires_grad_(True), beta.detach().clone().requires_grad_(True)
     rm2, rv2 = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
     zr = F.relu(F.batch_norm(yr, rm2, rv2, gr, br, training=True, momentum=0.1, eps=1e-5))
-    outr = F.max_pool2d(zr, 3, 2, 1)
+    outr = F.max_pool2d(zr, k, s, p)
     assert out.shape == (N, outr.shape[2], outr.shape[3], C)
     assert rel(out, outr.permute(0, 2, 3, 1)) < 1e-2
     assert rel(rm, rm2) < 1e-4 and rel(rv, rv2) < 1e-4
