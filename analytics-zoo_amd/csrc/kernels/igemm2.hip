@@ -1,0 +1,531 @@
+// Implicit-GEMM convolution / GEMM, second generation: large tiles, full-line LDS-DMA
+// staging, counted-vmcnt software pipeline (gfx950 / MI355X).
+//
+//   Y[m][n] = epilogue( sum_k A[m][k] * W[n][k] )      m = output pixel (n,p,q), n = Cout,
+//                                                      k = (r, s, c) filter tap x channel
+//
+// Scope: every conv / linear whose reduction runs over whole 64-channel slices (C % 64 == 0),
+// i.e. all ResNet-50 convs but the stem, transformer linears, and the parity-decomposed
+// dgrads built on them (zoo/ops/_kern.py conv_dgrad). Each 64-deep K-tile is then ONE filter
+// tap (r, s) and a contiguous 64-channel run, so the tap decode is wave-uniform scalar work
+// and every staged row is one full 128-byte line of the NHWC activation.
+//
+// Why a second kernel (profiles/PERF.md "Why the conv GEMMs stop at ~500 TF/s"): igemm.hip's
+// 128x64 tiles with 64x32 wave tiles need 0.75 LDS fragment reads per MFMA plus 24 KiB of
+// staging per 64 MFMAs, which makes the LDS array -- not the matrix cores -- the bound. Here:
+//   * wave tile 64x64 (or 128x64): 0.5 fragment reads per v_mfma_f32_16x16x32_bf16;
+//   * block tiles 128x128 / 256x128 / 256x64 / 256x256 chosen per shape on the host;
+//   * A and B staged with global_load_lds (16 B per lane, no VGPRs, no ds_write): one wave
+//     instruction moves 8 rows x 128 B -- whole cache lines, so the TA sees 8 lines per
+//     instruction instead of 16 half lines;
+//   * LDS image [row][128 B] with the 16-byte chunk XOR-swizzled by (row & 7). The DMA image
+//     is lane-linear, so the swizzle is applied through the per-lane SOURCE chunk (each row's
+//     8 lanes still fetch its whole line, permuted); fragment reads apply the same XOR. With the
+//     ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS every 16-lane group of a 16x16x32
+//     fragment read lands on 16 distinct 16-byte bank slots: conflict-free;
+//   * STAGES-deep LDS ring: tile kt+STAGES-1 is issued at the top of iteration kt; the end of
+//     the iteration waits with a counted `s_waitcnt vmcnt((STAGES-2) * DMA-per-tile)` and a raw
+//     s_barrier, so with STAGES=3 one tile stays in flight across every barrier and the main
+//     loop never drains the memory queue (cdna_hip_programming.md "Pipelining across barriers");
+//   * all LDS is one extern __shared__ array and the loop issues no VGPR-destination global
+//     load (the two .s traps of cdna_hip_programming.md §5 item 4).
+// Epilogue: per wave, 16-row slices of the fp32 accumulators go through a wave-private LDS
+// patch and leave as row-contiguous 16-byte stores, with the same fusions as igemm.hip:
+// EPI 1 = plain conv + BN statistics (the forward of every conv->BN unit), EPI 2 = backward
+// (residual-gradient add, producer ReLU mask, fused BN-backward sums, strided output remap),
+// EPI 0 = general (bias, activation, residual, fp32 output, statistics, remap).
+//
+// Reference parity: the MKL-DNN convolution / inner-product primitives behind BigDL
+// SpatialConvolution and Linear (Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110,
+// Dense.scala).
+#include <stdlib.h>
+
+#include "common.h"
+#include "geom.h"
+
+namespace zoo {
+
+typedef __attribute__((address_space(3))) void i2_lds_void;
+typedef __attribute__((address_space(1))) const void i2_gl_void;
+
+// zero page read by the DMA for rows beyond M / N and for padding taps
+__device__ __attribute__((aligned(64))) bf16_t i2_zero_page[32];
+
+template <int N>
+ZOO_DEV void i2_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int NWM, int NWN, int TM, int TN>
+struct I2Cfg {
+  static constexpr int NW = NWM * NWN, NT = NW * 64;
+  static constexpr int WTM = TM * 16, WTN = TN * 16;  // wave tile
+  static constexpr int BM = NWM * WTM, BN = NWN * WTN;  // block tile
+  static constexpr int A_PW = BM / (8 * NW), B_PW = BN / (8 * NW);  // DMA instructions per wave per K-tile
+  static constexpr int DPT = A_PW + B_PW;
+  static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int EPI_PITCH = WTN + 4;  // fp32 patch pitch (16-byte aligned rows)
+  static constexpr int EPI_BYTES = NW * 16 * EPI_PITCH * 4 + NWM * BN * 2 * 4;
+  static_assert(A_PW * 8 * NW == BM && B_PW * 8 * NW == BN, "tile rows must split into 8-row DMA groups");
+};
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1, int EPI>
+__global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
+    const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y, float* __restrict__ Yf,
+    const float* __restrict__ bias, const bf16_t* __restrict__ resid, float* __restrict__ stats, ConvGeom g, int act,
+    BwdStats bs) {
+  using Cfg = I2Cfg<NWM, NWN, TM, TN>;
+  constexpr int NW = Cfg::NW, WTM = Cfg::WTM, WTN = Cfg::WTN, BM = Cfg::BM, BN = Cfg::BN;
+  constexpr int A_PW = Cfg::A_PW, B_PW = Cfg::B_PW, DPT = Cfg::DPT, SB = Cfg::STAGE_BYTES;
+
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / NWN, wn = w - (w / NWN) * NWN;
+
+  const int ntn = (g.K + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int tm = bid / ntn, tn = bid - tm * ntn;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = g.Ktot >> 6;  // C % 64 == 0: one 64-deep K-tile per (tap, 64-channel slice)
+
+  // ---- staging assignment: lane -> row lr of each 8-row group, global 16-byte chunk gc ----
+  const int lr = lane >> 3;
+  const int gc = (lane & 7) ^ lr;  // XOR swizzle through the source (LDS image lane-linear)
+  const int PQ = g.P * g.Q;
+  int a_base[A_PW], a_ih[A_PW], a_iw[A_PW];
+#pragma unroll
+  for (int i = 0; i < A_PW; ++i) {
+    const int m = m0 + (i * NW + w) * 8 + lr;
+    const bool ok = m < g.M;
+    if constexpr (IS1x1) {
+      a_base[i] = ok ? m * g.C + gc * 8 : -1;
+      a_ih[i] = a_iw[i] = 0;
+    } else {
+      const int mm = ok ? m : 0;
+      const int n = mm / PQ, pq = mm - n * PQ;
+      const int p = pq / g.Q, q = pq - p * g.Q;
+      a_base[i] = n * g.H * g.W * g.C + gc * 8;
+      a_ih[i] = ok ? p * g.sh - g.ph : -(1 << 28);  // invalid rows never pass the bounds check
+      a_iw[i] = q * g.sw - g.pw;
+    }
+  }
+  const bf16_t* b_src[B_PW];
+#pragma unroll
+  for (int i = 0; i < B_PW; ++i) {
+    const int n = n0 + (i * NW + w) * 8 + lr;
+    b_src[i] = n < g.K ? Wm + (size_t)n * g.ldb + gc * 8 : nullptr;
+  }
+
+  // tap decode of the NEXT tile to stage (wave-uniform)
+  int st_r = 0, st_s = 0, st_c = 0, st_k = 0;
+  auto stage = [&](int buf) {
+    char* sa = smem + buf * SB + w * 1024;
+    char* sb = smem + buf * SB + BM * 128 + w * 1024;
+#pragma unroll
+    for (int i = 0; i < A_PW; ++i) {
+      const bf16_t* src;
+      if constexpr (IS1x1) {
+        src = a_base[i] >= 0 ? X + a_base[i] + st_k : i2_zero_page;
+      } else {
+        const int ih = a_ih[i] + st_r * g.dh, iw = a_iw[i] + st_s * g.dw;
+        const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        src = ok ? X + a_base[i] + (ih * g.W + iw) * g.C + st_c : i2_zero_page;
+      }
+      __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)(sa + i * NW * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const bf16_t* src = b_src[i] ? b_src[i] + st_k : i2_zero_page;
+      __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)(sb + i * NW * 1024), 16, 0, 0);
+    }
+    st_k += 64;
+    if constexpr (!IS1x1) {
+      st_c += 64;
+      if (st_c == g.C) {
+        st_c = 0;
+        if (++st_s == g.S) { st_s = 0; ++st_r; }
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // fragment reads: lane -> tile row (lane & 15), chunk kk*4 + (lane >> 4), XOR (row & 7)
+  const int rl = (lane & 15) * 128;
+  const int co0 = (((lane >> 4)) ^ (lane & 7)) << 4;
+  const int co1 = ((4 + (lane >> 4)) ^ (lane & 7)) << 4;
+  auto compute = [&](int buf) {
+    const char* ab = smem + buf * SB + (wm * WTM) * 128 + rl;
+    const char* bb = smem + buf * SB + (BM + wn * WTN) * 128 + rl;
+    // all fragment reads of the tile up front (the kk = 1 reads overlap the kk = 0 MFMAs)
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int co = kk ? co1 : co0;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[kk][j] = *reinterpret_cast<const bf16x8*>(bb + j * 2048 + co);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) af[kk][i] = *reinterpret_cast<const bf16x8*>(ab + i * 2048 + co);
+    }
+    // (no s_setprio: it made hipcc wait for all 16 reads before the first MFMA)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
+
+  };
+
+  // ---- main loop ----
+#pragma unroll
+  for (int s = 0; s < STAGES - 1; ++s)
+    if (s < nk) stage(s);
+  if (STAGES == 3 && nk > 1) i2_wait_vm<DPT>();
+  else i2_wait_vm<0>();
+  __builtin_amdgcn_s_barrier();
+  int cbuf = 0, sbuf = STAGES - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool issue = kt + STAGES - 1 < nk;
+    if (issue) stage(sbuf);
+    compute(cbuf);
+    // tile kt+1 must have landed (every wave's part) before any wave reads it; with STAGES = 3
+    // the tile issued above stays in flight across the barrier
+    if constexpr (STAGES == 3) {
+      if (issue) i2_wait_vm<DPT>();
+      else i2_wait_vm<0>();
+    } else {
+      i2_wait_vm<0>();
+    }
+    // every fragment read of this buffer has returned before any wave restages it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    cbuf = cbuf + 1 == STAGES ? 0 : cbuf + 1;
+    sbuf = sbuf + 1 == STAGES ? 0 : sbuf + 1;
+  }
+
+  // ---- epilogue ----
+  // every wave is past the last barrier: the operand ring is free. Wave-private fp32 patch of
+  // 16 rows x WTN columns; one 16-row accumulator slice at a time.
+  constexpr int PITCH = Cfg::EPI_PITCH;
+  constexpr int CPR = WTN / 8;            // 8-column chunks per patch row
+  constexpr int PPL = 16 * CPR / 64;      // pieces (row, chunk) per lane per slice
+  float* patch = reinterpret_cast<float*>(smem) + w * 16 * PITCH;
+  float* red = reinterpret_cast<float*>(smem) + NW * 16 * PITCH;  // [NWM][BN][2]
+  const int fr = lane & 15, fq = lane >> 4;
+  const int ch = lane % CPR;              // constant per lane: (lane + 64 h) % CPR
+  const int colt = wn * WTN + ch * 8;     // column inside the block tile
+  const int col0 = n0 + colt;
+  const bool col_ok = col0 < g.K;         // K % 8 == 0 (launcher)
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  float bsv[8], mu[8], iv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { bsv[e] = 0.f; mu[e] = 0.f; iv[e] = 0.f; }
+  if constexpr (EPI == 0) {
+    if (bias && col_ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) bsv[e] = bias[col0 + e];
+    }
+  }
+  if constexpr (EPI != 1) {
+    if (bs.sums && col_ok) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
+    }
+  }
+  // EPI 1: stats only; EPI 2: BN-backward sums only; EPI 0: either (stats win)
+  const bool want_stats = stats != nullptr || bs.sums != nullptr;
+
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) patch[(fq * 4 + r) * PITCH + j * 16 + fr] = acc[i][j][r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+    for (int h = 0; h < PPL; ++h) {
+      const int pidx = lane + 64 * h;
+      const int prow = pidx / CPR;
+      const int m = m0 + wm * WTM + i * 16 + prow;
+      const float4 lo = *reinterpret_cast<const float4*>(patch + prow * PITCH + ch * 8);
+      const float4 hi = *reinterpret_cast<const float4*>(patch + prow * PITCH + ch * 8 + 4);
+      if (m >= g.M || !col_ok) continue;
+      float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+      size_t off;
+      if (EPI != 1 && g.omap) {
+        const int n = m / PQ, pq = m - n * PQ;
+        const int p = pq / g.Q, q = pq - p * g.Q;
+        off = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
+      } else {
+        off = (size_t)m * g.K + col0;
+      }
+      if constexpr (EPI == 1) {
+        const uint4 pk = pack8(v);
+        *reinterpret_cast<uint4*>(Y + off) = pk;
+        if (want_stats) {
+          float q[8];
+          unpack8(pk, q);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
+        }
+      } else if constexpr (EPI == 2) {
+        if (resid) {
+          float rv[8];
+          unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += rv[e];
+        }
+        if (bs.z) {
+          float zz[8];
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+        }
+        const uint4 pk = pack8(v);
+        *reinterpret_cast<uint4*>(Y + off) = pk;
+        if (bs.sums) {
+          float q[8], yy[8];
+          unpack8(pk, q);
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += q[e];
+            s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+          }
+        }
+      } else {
+        if (resid) {
+          float rv[8];
+          unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += rv[e];
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e] + bsv[e], act);
+        if (bs.sums && bs.z) {
+          float zz[8];
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+        }
+        if (Yf) {
+          *reinterpret_cast<float4*>(Yf + off) = make_float4(v[0], v[1], v[2], v[3]);
+          *reinterpret_cast<float4*>(Yf + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
+        }
+        if (Y) {
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(Y + off) = pk;
+          float q[8];
+          unpack8(pk, q);
+          if (stats) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
+          } else if (bs.sums) {
+            float yy[8];
+            unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+
+  if (!want_stats) return;
+  // per-column sums: lanes sharing `ch` differ in bits >= log2(CPR); fold them, then the wave
+  // rows of the block through LDS, then one store / atomic per column per block
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  }
+  if (lane < CPR) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(wm * BN + colt + e) * 2 + 0] = s1[e];
+      red[(wm * BN + colt + e) * 2 + 1] = s2[e];
+    }
+  }
+  __syncthreads();
+  float* const sacc = stats ? stats : bs.sums;
+  for (int c = tid; c < BN; c += Cfg::NT) {
+    const int col = n0 + c;
+    if (col >= g.K) continue;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int r = 0; r < NWM; ++r) { a += red[(r * BN + c) * 2]; b += red[(r * BN + c) * 2 + 1]; }
+    if (g.stat_slots == kStatPartial) {
+      float* const dst = sacc + (size_t)tm * 2 * g.K;
+      dst[col] = a;
+      dst[g.K + col] = b;
+    } else {
+      float* const dst = g.stat_slots > 0 ? slot_ptr(sacc, 2 * g.K, g.stat_slots) : sacc;
+      atomicAdd(dst + col, a);
+      atomicAdd(dst + g.K + col, b);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+
+// tile configurations (NWM, NWN, TM, TN, STAGES): block = (NWM*TM*16) x (NWN*TN*16)
+enum I2Tile : int {
+  I2_AUTO = 0,
+  I2_128x128 = 1,   // 4 waves (2x2) of 64x64, 2-stage ring: 64 KiB LDS, 2 workgroups / CU
+  I2_256x128 = 2,   // 8 waves (4x2) of 64x64, 2-stage: 96 KiB, 1 / CU
+  I2_256x128_3 = 3, // 8 waves (4x2) of 64x64, 3-stage: 144 KiB, 1 / CU
+  I2_256x64 = 4,    // 4 waves (4x1) of 64x64, 2-stage: 80 KiB, 2 / CU
+  I2_256x256 = 5,   // 8 waves (2x4) of 128x64, 2-stage: 128 KiB, 1 / CU
+  I2_128x64 = 6,    // 4 waves (2x2) of 64x32, 3-stage: 72 KiB, 2 / CU
+  I2_128x128_3 = 7, // 4 waves (2x2) of 64x64, 3-stage: 96 KiB, 1 / CU
+};
+
+static int g_i2_mode = -1;  // -1: unset (read ZOO_IGEMM2), 0: off, 1: on
+static int g_i2_tile = -1;  // -1: unset (read ZOO_IGEMM2_TILE), 0 auto, else I2Tile
+
+static int i2_mode() {
+  if (g_i2_mode < 0) {
+    const char* e = getenv("ZOO_IGEMM2");
+    g_i2_mode = e ? atoi(e) : 1;
+  }
+  return g_i2_mode;
+}
+static int i2_tile_force() {
+  if (g_i2_tile < 0) {
+    const char* e = getenv("ZOO_IGEMM2_TILE");
+    g_i2_tile = e ? atoi(e) : 0;
+  }
+  return g_i2_tile;
+}
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1, int EPI>
+static hipError_t i2_launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                            const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
+                            hipStream_t st) {
+  using Cfg = I2Cfg<NWM, NWN, TM, TN>;
+  const int tiles = ((g.M + Cfg::BM - 1) / Cfg::BM) * ((g.K + Cfg::BN - 1) / Cfg::BN);
+  size_t smem = (size_t)STAGES * Cfg::STAGE_BYTES;
+  if (smem < (size_t)Cfg::EPI_BYTES) smem = Cfg::EPI_BYTES;
+  auto kfn = &igemm2_kernel<NWM, NWN, TM, TN, STAGES, IS1x1, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(tiles), dim3(Cfg::NT), smem, st, X, W, Y, Yf, bias, resid, stats, g, act, bs);
+  return hipGetLastError();
+}
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1>
+static hipError_t i2_epi(int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                         const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
+                         hipStream_t st) {
+  if (epi == 1) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (epi == 2) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 2>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 0>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+}
+
+template <bool IS1x1>
+static hipError_t i2_tile(int tile, int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf,
+                          const float* bias, const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                          const BwdStats& bs, hipStream_t st) {
+  switch (tile) {
+    case I2_128x128: return i2_epi<2, 2, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_256x128: return i2_epi<4, 2, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_256x128_3: return i2_epi<4, 2, 4, 4, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_256x64: return i2_epi<4, 1, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_256x256: return i2_epi<2, 4, 8, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_128x64: return i2_epi<2, 2, 4, 2, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    case I2_128x128_3: return i2_epi<2, 2, 4, 4, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+static int i2_bm(int tile) {
+  switch (tile) {
+    case I2_128x128: case I2_128x64: case I2_128x128_3: return 128;
+    default: return 256;
+  }
+}
+static int i2_bn(int tile) {
+  switch (tile) {
+    case I2_256x64: case I2_128x64: return 64;
+    case I2_256x256: return 256;
+    default: return 128;
+  }
+}
+
+// shape -> tile heuristic (tools/conv_sweep.py --igemm2-tiles picks it on the GPU)
+static int i2_choose(const ConvGeom& g) {
+  const int f = i2_tile_force();
+  if (f > 0) return f;
+  auto tiles = [&](int t) { return (long)((g.M + i2_bm(t) - 1) / i2_bm(t)) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
+  if (g.K <= 64) return tiles(I2_256x64) >= 512 ? I2_256x64 : I2_128x64;
+  if (g.K <= 128) return tiles(I2_256x128) >= 512 ? I2_256x128_3 : I2_128x128;
+  if (tiles(I2_256x256) >= 512 && g.K % 256 == 0) return I2_256x256;
+  if (tiles(I2_256x128) >= 512) return I2_256x128_3;
+  if (tiles(I2_128x128) >= 256) return I2_128x128;
+  return I2_128x64;
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+// eligibility: whole 64-channel K-tiles, plain (non-input-dilated) conv, 16-byte rows
+extern "C" int zoo_igemm2_eligible(const ConvGeom* g) {
+  if (i2_mode() == 0) return 0;
+  return g->C % 64 == 0 && g->lh == 1 && g->lw == 1 && g->K % 8 == 0 && g->ldb % 8 == 0 &&
+         g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot;
+}
+
+// m-tile height the dispatcher will use for this geometry (partial-statistics buffers are
+// [ceil(M / bm)][2K]); 0 = not taken by igemm2
+extern "C" int zoo_igemm2_bm(const ConvGeom* g) {
+  if (!zoo_igemm2_eligible(g)) return 0;
+  return i2_bm(i2_choose(*g));
+}
+
+extern "C" void zoo_igemm2_set(int mode, int tile) {
+  if (mode >= 0) g_i2_mode = mode;
+  if (tile >= 0) g_i2_tile = tile;
+}
+
+extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Yf, const float* bias,
+                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
+                                 hipStream_t st) {
+  if (!zoo_igemm2_eligible(g)) return hipErrorNotSupported;
+  BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
+                     g->H == g->P && g->W == g->Q;
+  int epi = 0;
+  if (Y && !Yf && !bias && !resid && act == 0 && !g->omap && !bs.sums) epi = 1;
+  else if (Y && !Yf && !bias && act == 0 && !stats) epi = 2;
+  const int tile = i2_choose(*g);
+  const bf16_t* x = (const bf16_t*)X;
+  const bf16_t* w = (const bf16_t*)W;
+  if (is1x1)
+    return i2_tile<true>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
+  return i2_tile<false>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
+}

@@ -19,6 +19,8 @@ using zoo::GemmGeom;
 extern "C" {
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
                      const zoo::BwdStats*, hipStream_t);
+int zoo_igemm2_bm(const ConvGeom*);
+void zoo_igemm2_set(int, int);
 hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, const void*, float*, const GemmGeom*,
                        int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -281,7 +283,9 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   // they are folded in order into the caller's buffer (its first 2K floats)
   float* const stat_dst = sp ? sp : bs.sums;
   torch::Tensor part;
-  const int tiles_m = (g.M + 127) / 128;  // IG_BM
+  // m-tile height of the kernel the dispatcher picks (igemm.hip: 128; igemm2.hip: 128 or 256)
+  const int bm = zoo_igemm2_bm(&g) > 0 ? zoo_igemm2_bm(&g) : 128;
+  const int tiles_m = (g.M + bm - 1) / bm;
   // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
   // the atomics go straight into the final 2K floats, no slot fold launch needed
   static const int slot_min_tiles = [] {
@@ -1901,6 +1905,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gelu") = false);
   m.def("softmax_rows_bwd", &softmax_rows_bwd);
   m.def("lrn", &lrn);
+  m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
+        "igemm2 A/B switch: mode 0 off / 1 on (-1 keep), tile 0 auto / I2Tile id (-1 keep)");
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });
   m.def("get_deterministic", []() { return g_deterministic; });
   m.def("set_reduce_modes", [](bool stats_part, bool wgrad_part) {

@@ -55,6 +55,20 @@ def weights_epoch():
     return _EPOCH[0]
 
 
+_STATS_EPOCH = [0]
+
+
+def bump_stats_epoch():
+    """Called whenever a native training-mode BatchNorm forward rewrites running statistics
+    through raw pointers (no ``_version`` bump): caches derived from running stats (the
+    eval-mode BN fold) key on this."""
+    _STATS_EPOCH[0] += 1
+
+
+def stats_epoch():
+    return _STATS_EPOCH[0]
+
+
 def register_flat(flat):
     """Give a FlatParams its own flip cache (it dies with the FlatParams, so cached
     pointers never outlive the buffer they point into)."""

@@ -61,3 +61,24 @@ def set_deterministic(on=True):
 def deterministic():
     m = _load()
     return bool(m.get_deterministic()) if m is not None else False
+
+
+def native_build_info():
+    """Provenance of the loaded native libraries: the manifest written by the build
+    (tools/build_native.py) plus ``source_hash_matches`` -- whether that build was made from
+    the csrc/ files present in this tree right now (content hashes, not mtimes)."""
+    import json
+    pkg = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = os.path.join(pkg, "_build_manifest.json")
+    info = {"manifest": None, "source_hash_matches": None, "loaded": available()}
+    if os.path.exists(path):
+        with open(path) as f:
+            info["manifest"] = json.load(f)
+        try:
+            from zoo.utils.build import tree_source_hash
+            cur = tree_source_hash()
+            info["tree_source_hash"] = cur
+            info["source_hash_matches"] = cur == info["manifest"].get("source_hash")
+        except (OSError, ImportError):
+            pass
+    return info

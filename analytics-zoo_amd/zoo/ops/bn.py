@@ -123,6 +123,8 @@ class _ConvBNActFn(torch.autograd.Function):
             rb.sinv = torch.empty(K, device=x.device, dtype=torch.float32)
             side = [rb.stats, gamma2.detach(), beta2.detach(), rb.running_mean, rb.running_var, rb.smean, rb.sinv]
             ctx.gamma2, ctx.beta2 = gamma2, beta2
+        if training:
+            _kern.bump_stats_epoch()
         z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
                             beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,
                             training, side)
@@ -333,7 +335,10 @@ def _folded(w, gamma, beta, running_mean, running_var, eps, cols=None):
     """Inference-time BatchNorm folding: W' = W * gamma/sqrt(var+eps) (per output row),
     b' = beta - mean * gamma/sqrt(var+eps). Cached on the weight parameter and rebuilt
     when any of the five tensors changes (in-place updates bump ``_version``)."""
-    key = tuple((t.data_ptr(), t._version) for t in (w, gamma, beta, running_mean, running_var)) + (float(eps),)
+    # the engine's fused optimizer writes weights, and the native BN kernels write running
+    # statistics, through raw pointers (no ``_version`` bump): the two epochs cover those writers
+    key = tuple((t.data_ptr(), t._version) for t in (w, gamma, beta, running_mean, running_var)) + (
+        float(eps), _kern.weights_epoch(), _kern.stats_epoch())
     c = getattr(w, "_zoo_bn_fold", None)
     if c is not None and c[0] == key:
         return c[1], c[2]
@@ -421,6 +426,8 @@ class _BNActFn(torch.autograd.Function):
                 all_reduce_stats(stats[:2 * K], y.numel() // K)
         smean = torch.empty(K, device=y.device, dtype=torch.float32)
         sinv = torch.empty(K, device=y.device, dtype=torch.float32)
+        if training:
+            _kern.bump_stats_epoch()
         z = C_.bn_fwd_apply(y, stats, gamma.detach(), beta.detach(), resid, running_mean, running_var, smean,
                             sinv, eps, momentum, relu, training)
         ctx.save_for_backward(y, gamma, beta, z if relu else None, smean, sinv)
@@ -477,6 +484,7 @@ class _BNReluMaxPoolFn(torch.autograd.Function):
         K = y.shape[-1]
         smean = torch.empty(K, device=y.device, dtype=torch.float32)
         sinv = torch.empty(K, device=y.device, dtype=torch.float32)
+        _kern.bump_stats_epoch()
         out, best, arg = native().bn_relu_maxpool_fwd(y, holder.stats, gamma.detach().float().contiguous(),
                                                       beta.detach().float().contiguous(), holder.running_mean,
                                                       holder.running_var, smean, sinv, eps, momentum,

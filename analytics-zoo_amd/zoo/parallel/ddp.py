@@ -42,6 +42,25 @@ docs/docs/wp-bigdl.md:140-160):
   result equals the dense all-reduce (the table must get gradient only through
   lookups: no dense regulariser on it).
 
+Ordering (every rank must issue the same collectives in the same order): the calibration
+step records the order in which buckets BECOME ready (the sequence number of each parameter's
+last contribution); later steps launch early in that order, and ``finish()`` launches whatever
+is left -- including all buckets of a zombie rank that failed part-way through backward -- in
+that same recorded order, so a zombie's collective sequence matches the healthy ranks'.
+
+Row-sparse sync is host-sync free and capturable: each rank scatters a per-row "touched"
+mask (uint8, V bytes), the masks are summed (one all-reduce), the union rows are compacted on
+the device into a fixed-capacity index buffer (capacity min(V, world * ids-per-step), agreed
+in the calibration step) and ONE fixed-size all-reduce moves just those rows. A rank without
+lookups contributes a zero mask, so every rank always issues the same collectives.
+
+ZeRO-1 weight all-gather: the updated shards go out as bf16 (half of BigDL's fp32 bytes are
+not needed for the bf16 compute copy); the 1-D parameters that layers read in fp32 (BatchNorm
+gamma/beta, biases) are reassembled exactly with one small fp32 all-reduce, and the fp32 view
+of every other parameter is the bf16 value on EVERY rank (identical across ranks; the exact
+fp32 masters live in the owners' shards and are gathered in full only for checkpoints,
+``sync_master``).
+
 All persistent comm buffers are allocated once (chunk = ceil(bucket/N) rounded
 to 64 elements). ``force_comm`` runs the whole bucket / comm-stream / event
 path on a world-size-1 process group (RCCL with one rank), so the overlapped
@@ -96,7 +115,7 @@ def record_lookup(table, idx):
 
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "params", "pending", "launched", "cb", "so", "pack", "recv", "gath",
-                 "works", "post", "sparse")
+                 "works", "post", "sparse", "gath16", "ev0", "ev1")
 
     def __init__(self, idx, lo, hi):
         self.idx, self.lo, self.hi = idx, lo, hi
@@ -109,6 +128,8 @@ class _Bucket:
         self.works = []
         self.post = None
         self.sparse = []     # [(param, lo, hi)] when every parameter of the bucket is row-sparse
+        self.gath16 = None   # ZeRO-1 bf16 weight all-gather target
+        self.ev0 = self.ev1 = None  # comm-stream events around the bucket's collectives (stats)
 
 
 class GradSync:
@@ -166,6 +187,19 @@ class GradSync:
         # contribution counting (calibration) -----------------------------------
         self._counts = {}
         self._expected = None
+        self._seq = 0
+        self._last_seq = {}
+        self.order = None          # bucket launch order learned in the calibration step
+        self.launch_log = []       # bucket indices in the order this step launched them
+        # row-sparse capacity (rows) per table, agreed in the calibration step
+        self._sparse_cap = {}
+        # ZeRO-1: flat ranges of the 1-D (fp32-read) parameters, gathered exactly in fp32
+        self._small_idx = None
+        self._small_buf = None
+        # comm statistics (bench.py at N > 1): exposed wait + per-bucket collective time
+        self.collect_stats = False
+        self.stats = {"steps": 0, "exposed_ms": 0.0, "bucket_ms": {}, "bucket_bytes": {}}
+        self._wait_ev = None
         self._install_hooks()
         self.reset()
 
@@ -202,12 +236,29 @@ class GradSync:
         if self.mode == "sharded":
             self.shard_grad = torch.zeros(self.shard_size, dtype=torch.float32, device=dev)
             self.shard_master = torch.zeros(self.shard_size, dtype=torch.float32, device=dev)
-            gath = torch.empty(sum(b.cb for b in self.buckets) * self.world, dtype=torch.float32, device=dev)
+            tot = sum(b.cb for b in self.buckets) * self.world
+            gath = torch.empty(tot, dtype=torch.float32, device=dev)      # checkpoint-time fp32 gather
+            gath16 = torch.empty(tot, dtype=torch.bfloat16, device=dev)   # per-step bf16 weight gather
+            self._shard16 = torch.empty(self.shard_size, dtype=torch.bfloat16, device=dev)
             off = 0
             for b in self.buckets:
                 n = b.cb * self.world
                 b.gath = gath[off:off + n]
+                b.gath16 = gath16[off:off + n]
                 off += n
+            # 1-D parameters (BN gamma/beta, biases: read in fp32 by the layers) travel exactly
+            idx = []
+            for p, (lo, hi) in zip(self.flat.params, self.flat.ranges()):
+                if p.dim() <= 1:
+                    idx.append(torch.arange(lo, hi, dtype=torch.long))
+            if idx and self.flat.bf16 is not None:
+                self._small_idx = torch.cat(idx).to(dev)
+                self._small_buf = torch.zeros(self._small_idx.numel(), dtype=torch.float32, device=dev)
+                own = torch.zeros(self.flat.numel, dtype=torch.bool)
+                for b in self.buckets:
+                    lo, hi = self._chunk(b)
+                    own[lo:hi] = True
+                self._small_own = own[self._small_idx.cpu()].to(dev)
             self.load_shard_from_master()
         self._bufs = True
 
@@ -262,6 +313,7 @@ class GradSync:
             b.launched = False
             b.works = []
             b.post = None
+        self.launch_log = []
 
     def _ready(self, p):
         if not self.comm:
@@ -270,6 +322,8 @@ class GradSync:
             pid = id(p)
             c = self._counts.get(pid, 0) + 1
             self._counts[pid] = c
+            self._seq += 1
+            self._last_seq[pid] = self._seq
             if not self.overlap or self._expected is None:
                 return
             b = self.param_bucket.get(pid)
@@ -294,12 +348,19 @@ class GradSync:
     def _launch(self, b):
         self._ensure_buffers()
         b.launched = True
+        self.launch_log.append(b.idx)
         if self.comm_stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.grad.device))
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if self.collect_stats:
+                    b.ev0 = torch.cuda.Event(enable_timing=True)
+                    b.ev1 = torch.cuda.Event(enable_timing=True)
+                    b.ev0.record(self.comm_stream)
                 self._issue(b)
+                if self.collect_stats:
+                    b.ev1.record(self.comm_stream)
         else:
             self._issue(b)
 
@@ -338,33 +399,59 @@ class GradSync:
         if out16 is not None:
             out16.copy_(s)
 
+    def _touched_ids(self, p):
+        touched = getattr(p, "_zoo_touched", None) or []
+        if getattr(p, "_zoo_touch_step", -1) != _TOUCH_STEP[0]:
+            touched = []
+        return touched
+
+    def _sparse_capacity(self, p, n_local):
+        """Rows the fixed-size union buffer holds: min(V, world * ids-per-step), agreed once
+        (calibration) with a MAX all-reduce of the per-rank id counts."""
+        key = id(p)
+        cap = self._sparse_cap.get(key)
+        if cap is None:
+            dev = self.flat.grad.device if self.backend != "gloo" else torch.device("cpu")
+            t = torch.tensor([n_local], dtype=torch.long, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            n_max = int(t.item())
+            cap = (min(p.shape[0], max(n_max, 1) * self.world), n_max)
+            self._sparse_cap[key] = cap
+        elif n_local > cap[1]:
+            raise RuntimeError("row-sparse table %s: %d lookups this step > the %d agreed in the calibration "
+                               "step (the union buffer could overflow)" % (tuple(p.shape), n_local, cap[1]))
+        return cap[0]
+
     def _row_sparse_allreduce(self, p, lo, hi):
-        """Sum table p's gradient over the ranks through the union of looked-up rows
-        (False: no lookup was recorded, the caller reduces the dense range)."""
-        touched = getattr(p, "_zoo_touched", None)
-        if not touched:
-            return False
+        """Sum table p's gradient over the ranks through the union of looked-up rows: a summed
+        uint8 touched mask, device-side compaction into a fixed-capacity row list, one fixed-size
+        all-reduce of those rows. No host synchronisation after the calibration step, and the
+        same collectives on every rank whatever it looked up (an idle rank sends a zero mask)."""
         V, D = p.shape
         g = self.flat.grad[lo:lo + V * D].view(V, D)
         dev = g.device
-        ids = torch.cat([t.to(dev).long() for t in touched])
-        u = torch.unique(ids[(ids >= 0) & (ids < V)])
-        cnt = torch.tensor([u.numel()], device=dev, dtype=torch.long)
-        cnts = [torch.empty_like(cnt) for _ in range(self.world)]
-        dist.all_gather(cnts, cnt, group=self.group)
-        m = int(max(int(c.item()) for c in cnts))
-        if m == 0:
-            return True
-        pad = torch.full((m,), V, device=dev, dtype=torch.long)
-        pad[:u.numel()] = u
-        allids = [torch.empty_like(pad) for _ in range(self.world)]
-        dist.all_gather(allids, pad, group=self.group)
-        union = torch.unique(torch.cat(allids))
-        union = union[union < V]
-        rows = g.index_select(0, union)
+        touched = self._touched_ids(p)
+        n_local = int(sum(t.numel() for t in touched))
+        cap = self._sparse_capacity(p, n_local)
+        mask = torch.zeros(V, dtype=torch.uint8 if self.backend != "gloo" else torch.int32, device=dev)
+        if touched:
+            ids = torch.cat([t.to(dev).long() for t in touched])
+            ids = ids[(ids >= 0) & (ids < V)] if not ids.is_cuda else ids.clamp(0, V - 1)
+            mask.index_fill_(0, ids, 1)
+        dist.all_reduce(mask, group=self.group)
+        on = mask > 0
+        pos = torch.cumsum(on.to(torch.int32), 0) - 1
+        slot = torch.where(on, pos.long(), torch.full_like(pos, cap, dtype=torch.long))
+        slot = slot.clamp(max=cap)
+        buf = torch.full((cap + 1,), V, dtype=torch.long, device=dev)
+        buf.scatter_(0, slot, torch.arange(V, device=dev))
+        rows_idx = buf[:cap]
+        first = rows_idx[:1].clamp(max=V - 1)
+        rows_idx = torch.where(rows_idx < V, rows_idx, first)   # padding slots repeat the first row
+        rows = g.index_select(0, rows_idx)
         dist.all_reduce(rows, group=self.group)
-        g.index_copy_(0, union, rows)
-        self.sparse_rows = getattr(self, "sparse_rows", 0) + int(union.numel())
+        g.index_copy_(0, rows_idx, rows)
+        self.sparse_rows = getattr(self, "sparse_rows", 0) + cap
         return True
 
     def _issue(self, b):
@@ -373,7 +460,9 @@ class GradSync:
         g = self.flat.grad[b.lo:b.hi]
         n = b.hi - b.lo
         if self.mode == "allreduce" and not self.compress:
-            if b.sparse and all(self._row_sparse_allreduce(p, lo, hi) for p, lo, hi in b.sparse):
+            if b.sparse:   # always the sparse protocol: identical collectives on every rank
+                for p, plo, phi in b.sparse:
+                    self._row_sparse_allreduce(p, plo, phi)
                 return
             dist.all_reduce(g, group=self.group)
             return
@@ -408,13 +497,76 @@ class GradSync:
         wait for every bucket's collectives."""
         if not self.comm:
             return
-        if self._expected is None:  # end of the calibration step
-            self._expected = dict(self._counts)
-        for b in self.buckets:
+        calib = self._expected is None
+        order = self.order if self.order is not None else range(len(self.buckets))
+        for i in order:
+            b = self.buckets[i]
             if not b.launched:
                 self._launch(b)
+        if calib:  # end of the calibration step: learn counts and the readiness order
+            self._expected = dict(self._counts)
+            self.order = self._readiness_order()
+        if self.comm_stream is not None:
+            cur = torch.cuda.current_stream(self.flat.grad.device)
+            if self.collect_stats:
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(cur)
+                cur.wait_stream(self.comm_stream)
+                e1.record(cur)
+                self._wait_ev = (e0, e1)
+            else:
+                cur.wait_stream(self.comm_stream)
+
+    def _readiness_order(self):
+        """Bucket launch order of every later step: buckets that launch early, by the sequence
+        number of their last gradient contribution; then the ones only finish() launches
+        (row-sparse, no contributions) by index -- exactly what a healthy rank does."""
+        early, late = [], []
+        for b in self.buckets:
+            seqs = [self._last_seq.get(pid, 0) for pid in b.params if self._expected.get(pid, 0) > 0]
+            if b.sparse or not seqs:
+                late.append(b.idx)
+            else:
+                early.append((max(seqs), b.idx))
+        return [i for _, i in sorted(early)] + late
+
+    def wait_comm(self):
+        """Make the current stream wait for everything issued on the comm stream (a zombie
+        rank calls this before zeroing gradients that in-flight collectives may still read)."""
         if self.comm_stream is not None:
             torch.cuda.current_stream(self.flat.grad.device).wait_stream(self.comm_stream)
+
+    def collect_comm_stats(self):
+        """Fold this step's events into ``self.stats`` (synchronises on the events)."""
+        if not self.collect_stats or self.comm_stream is None:
+            return
+        if self._wait_ev is not None:
+            e0, e1 = self._wait_ev
+            e1.synchronize()
+            self.stats["exposed_ms"] += e0.elapsed_time(e1)
+            self._wait_ev = None
+        for b in self.buckets:
+            if b.ev0 is not None and b.ev1 is not None:
+                b.ev1.synchronize()
+                self.stats["bucket_ms"][b.idx] = self.stats["bucket_ms"].get(b.idx, 0.0) + b.ev0.elapsed_time(b.ev1)
+                self.stats["bucket_bytes"][b.idx] = (b.hi - b.lo) * (2 if self.compress else 4)
+                b.ev0 = b.ev1 = None
+        self.stats["steps"] += 1
+
+    def comm_summary(self):
+        """exposed comm ms/step and per-bucket algorithm / bus bandwidth (GB/s)."""
+        st = self.stats
+        n = max(st["steps"], 1)
+        out = {"exposed_comm_ms_per_step": round(st["exposed_ms"] / n, 3), "buckets": []}
+        k = 2.0 * (self.world - 1) / self.world if self.world > 1 else 0.0
+        for i in sorted(st["bucket_ms"]):
+            ms = st["bucket_ms"][i] / n
+            by = st["bucket_bytes"].get(i, 0)
+            alg = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
+            out["buckets"].append({"bucket": i, "MB": round(by / 1e6, 2), "ms": round(ms, 3),
+                                   "algbw_GBs": round(alg, 1), "busbw_GBs": round(alg * k, 1)})
+        return out
 
     def step(self, optim, clip=None):
         """finish comm, (clip), run the optimizer."""
@@ -428,6 +580,8 @@ class GradSync:
             if clip is not None:
                 clip(flat.grad, gscale, self)
             optim.step(flat.master, flat.grad, flat.bf16, gscale)
+        if self.collect_stats:
+            self.collect_comm_stats()
         self.reset()
 
     def _sharded_step(self, optim, gscale, clip):
@@ -439,20 +593,54 @@ class GradSync:
                               self.shard_master, self.shard_grad, None, gscale)
         else:
             optim.step(self.shard_master, self.shard_grad, None, gscale)
-        # all-gather the updated fp32 master shards straight back into the full flat buffer
-        # (per bucket, on the comm stream), then ONE cast pass refreshes the bf16 compute copy.
-        # The fp32 masters are gathered (not only 16-bit weights) because layers read fp32
-        # parameters directly (BN gamma/beta, biases, embeddings): every rank must see the
-        # same values, bit for bit.
+        # all-gather the updated shards. The bf16 compute copy is gathered directly (2 bytes per
+        # parameter on the wire instead of BigDL's fp32 4); the 1-D fp32-read parameters get
+        # their exact fp32 values from one small all-reduce; every other fp32 master view
+        # becomes the (rank-identical) bf16 value. Without a bf16 compute copy (CPU) the fp32
+        # masters are gathered as before.
         stream = self.comm_stream
         if stream is not None:
             stream.wait_stream(torch.cuda.current_stream(flat.master.device))
             with torch.cuda.stream(stream):
-                self._gather_masters()
+                self._gather_weights()
             torch.cuda.current_stream(flat.master.device).wait_stream(stream)
         else:
+            self._gather_weights()
+        from zoo.ops._kern import bump_weights_epoch
+        bump_weights_epoch()
+
+    def _gather_weights(self):
+        flat = self.flat
+        if flat.bf16 is None or not flat.master.is_cuda:
+            # CPU (gloo) / no compute copy: the layers read the fp32 masters -> gather them exactly
             self._gather_masters()
-        flat.refresh_bf16()
+            flat.refresh_bf16()
+            return
+        self._shard16.copy_(self.shard_master)
+        for b in self.buckets:
+            self._gather(b.gath16, self._shard16[b.so:b.so + b.cb])
+            flat.bf16[b.lo:b.hi].copy_(b.gath16[:b.hi - b.lo])
+        flat.master.copy_(flat.bf16)
+        if self._small_idx is not None:
+            # exact fp32 for the 1-D parameters: owners contribute their values, others zero
+            mine = self._exact_master(self._small_idx)
+            self._small_buf.copy_(torch.where(self._small_own, mine, torch.zeros_like(mine)))
+            dist.all_reduce(self._small_buf, group=self.group)
+            flat.master.index_copy_(0, self._small_idx, self._small_buf)
+
+    def _exact_master(self, gidx):
+        """Exact fp32 values of global flat positions ``gidx`` that this rank owns (zeros
+        elsewhere) from the shard (positions map through the bucket chunks)."""
+        if not hasattr(self, "_g2s"):
+            g2s = torch.full((self.flat.numel,), -1, dtype=torch.long)
+            for b in self.buckets:
+                lo, hi = self._chunk(b)
+                if hi > lo:
+                    g2s[lo:hi] = torch.arange(b.so, b.so + hi - lo)
+            self._g2s_small = g2s[gidx.cpu()].to(gidx.device)
+            self._g2s = True
+        sidx = self._g2s_small
+        return torch.where(sidx >= 0, self.shard_master[sidx.clamp(min=0)], torch.zeros((), device=sidx.device))
 
     def _gather_masters(self):
         flat = self.flat
@@ -461,8 +649,18 @@ class GradSync:
             flat.master[b.lo:b.hi].copy_(b.gath[:b.hi - b.lo])
 
     def sync_master(self):
-        """Kept for API compatibility: the fp32 masters are gathered every step."""
-        return
+        """Exact fp32 masters on every rank (checkpoints): ZeRO-1 steps only gather the bf16
+        weights plus the exact 1-D parameters, so gather the full fp32 shards here."""
+        if self.mode != "sharded" or not self.comm or self.shard_master is None:
+            return
+        stream = self.comm_stream
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream(self.flat.master.device))
+            with torch.cuda.stream(stream):
+                self._gather_masters()
+            torch.cuda.current_stream(self.flat.master.device).wait_stream(stream)
+        else:
+            self._gather_masters()
 
     def all_reduce_scalars(self, values):
         """CC4/CC6: batch small metric/loss reductions into ONE all-reduce."""

@@ -25,6 +25,7 @@ Decoding builds plain Python objects only.
 import numpy as np
 
 from zoo.utils.protobuf import (as_float32, as_int32, as_str, enc_bytes, enc_float, enc_int, enc_packed_floats,
+                                enc_packed_doubles,
                                 enc_packed_ints, fields, group, packed_doubles, packed_floats, packed_varints,
                                 pb_fields_py)  # noqa: F401  (pb_fields_py re-exported for tensorboard)
 
@@ -39,7 +40,9 @@ class TensorRef:
         self.size, self.stride, self.offset, self.n = size, stride, offset, n
         self.storage_id, self.tensor_id, self.data = storage_id, tensor_id, data
 
-    def materialize(self, storages):
+    def materialize(self, storages, native=False):
+        """numpy array of the tensor: float32 by default; ``native`` keeps the storage dtype
+        (int32 / int64 / float64 storages round-trip exactly)."""
         data = self.data
         if data is None:
             data = storages.get(self.storage_id)
@@ -47,14 +50,15 @@ class TensorRef:
             data = storages.get(("tensor", self.tensor_id))
         if data is None:
             raise ValueError("BigDL tensor %s: storage %s not found" % (self.tensor_id, self.storage_id))
+        out_dt = data.dtype if native else np.float32
         if not self.size:
-            return np.asarray(data[self.offset - 1:self.offset], dtype=np.float32).reshape(())
+            return np.asarray(data[self.offset - 1:self.offset], dtype=out_dt).reshape(())
         off = max(self.offset - 1, 0)
         strides = self.stride or list(np.cumprod(([1] + self.size[::-1])[:-1])[::-1])
         itemsize = data.dtype.itemsize
         view = np.lib.stride_tricks.as_strided(data[off:], shape=tuple(self.size),
                                                strides=tuple(int(s) * itemsize for s in strides))
-        return np.array(view, dtype=np.float32)
+        return np.array(view, dtype=out_dt)
 
 
 def _storage(b):
@@ -65,9 +69,9 @@ def _storage(b):
     elif 3 in g:
         data = packed_doubles(g[3])
     elif 6 in g:
-        data = np.asarray(packed_varints(g[6]), dtype=np.float64)
+        data = np.asarray(packed_varints(g[6]), dtype=np.int32)
     elif 7 in g:
-        data = np.asarray(packed_varints(g[7]), dtype=np.float64)
+        data = np.asarray(packed_varints(g[7]), dtype=np.int64)
     else:
         data = None
     return sid, data

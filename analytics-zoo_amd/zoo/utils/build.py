@@ -13,5 +13,11 @@ def _mod():
     return m
 
 
-def build_native(force=False, jobs=8, verbose=False):
-    return _mod().build_all(force=force, jobs=jobs, verbose=verbose)
+def build_native(force=False, jobs=8, verbose=False, out_dir=None):
+    """Content-stamped build (rebuilds exactly the objects whose source / headers / command
+    changed); returns the provenance manifest."""
+    return _mod().build_all(force=force, jobs=jobs, verbose=verbose, out_dir=out_dir)
+
+
+def tree_source_hash():
+    return _mod().tree_source_hash()

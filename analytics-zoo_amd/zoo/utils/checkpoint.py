@@ -37,6 +37,26 @@ def save_object(obj, path, overwrite=True):
             os.remove(tmp)
 
 
+def save_bytes(data, path, overwrite=True):
+    """Atomic write of raw bytes (same path rules as :func:`save_object`)."""
+    if "://" in path and not path.startswith("file://"):
+        from zoo.common.utils import save_file
+        return save_file(lambda p: save_bytes(data, p, True), path)
+    path = _local(path)
+    if os.path.exists(path) and not overwrite:
+        raise FileExistsError(path)
+    d = os.path.dirname(os.path.abspath(path))
+    os.makedirs(d, exist_ok=True)
+    fd, tmp = tempfile.mkstemp(dir=d, prefix="zoo_tmp_", suffix=".part")
+    try:
+        with os.fdopen(fd, "wb") as f:
+            f.write(data)
+        os.replace(tmp, path)
+    finally:
+        if os.path.exists(tmp):
+            os.remove(tmp)
+
+
 def load_object(path):
     if "://" in path and not path.startswith("file://"):
         from zoo.common.utils import load_from_file

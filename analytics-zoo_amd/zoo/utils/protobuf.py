@@ -167,6 +167,10 @@ def enc_packed_floats(field, arr):
     return enc_bytes(field, np.asarray(arr, dtype="<f4").tobytes())
 
 
+def enc_packed_doubles(field, arr):
+    return enc_bytes(field, np.asarray(arr, dtype="<f8").tobytes())
+
+
 # ---- text format (prototxt) ---------------------------------------------------------
 _TOK = re.compile(r'\s*(?:(#[^\n]*)|("(?:[^"\\]|\\.)*"|\'(?:[^\'\\]|\\.)*\')|([{}:\[\],;<>])|([^\s{}:\[\],;<>"\']+))')
 

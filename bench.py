@@ -93,6 +93,47 @@ def build_ncf(ctx, batch):
     return eng, (x, y), "NCF", {"users": users, "items": items, "embed": 20, "hidden": [40, 20, 10]}
 
 
+def grad_sync_label(eng, a):
+    """What the gradient synchronisation actually did: "none" when no collective runs."""
+    if not eng.sync.comm:
+        return "none"
+    lab = "sharded(ZeRO-1,bf16-weight-gather)" if eng.sync.mode == "sharded" else "allreduce(bucketed,overlapped)"
+    return lab + ("+bf16-wire" if a.grad_compression else "")
+
+
+def comm_diagnostics(eng, x, y, world):
+    """Self-check fields for multi-GPU runs (measured AFTER the timed steps, so the event
+    timing does not perturb them): RCCL world size, cross-rank max |difference| of a checksum
+    of the fp32 master weights (0 = every rank holds the same model), exposed comm time per
+    step (the compute stream's wait on the comm stream) and per-bucket bus bandwidth."""
+    sync = eng.sync
+    if not sync.comm:
+        return {"rccl_world": 1}
+    sync.collect_stats = True
+    for _ in range(3):
+        eng.train_step(x, y)
+    torch.cuda.synchronize()
+    sync.collect_stats = False
+    summ = sync.comm_summary()
+    sync.sync_master()
+    m = eng.flat.master.double()
+    w = (torch.arange(m.numel(), device=m.device) % 1009 + 1).double()
+    cs = torch.stack([m.sum(), (m * w).sum()])
+    hi, lo = cs.clone(), cs.clone()
+    if world > 1:
+        dist.all_reduce(hi, op=dist.ReduceOp.MAX)
+        dist.all_reduce(lo, op=dist.ReduceOp.MIN)
+    b = summ["buckets"]
+    bus = [r["busbw_GBs"] for r in b if r["ms"] > 0]
+    return {"rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
+            "comm_backend": dist.get_backend() if dist.is_initialized() else None,
+            "master_checksum_maxdiff": float((hi - lo).abs().max().item()),
+            "exposed_comm_ms_per_step": summ["exposed_comm_ms_per_step"],
+            "comm_buckets": len(b), "comm_MB_per_step": round(sum(r["MB"] for r in b), 1),
+            "bucket_busbw_GBs": {"mean": round(sum(bus) / len(bus), 1) if bus else 0.0,
+                                 "max": max(bus) if bus else 0.0, "min": min(bus) if bus else 0.0}}
+
+
 def main():
     a = parse()
     from zoo.common.nncontext import init_nncontext
@@ -130,6 +171,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
     final_loss = float(loss.float().item())
+    diag = comm_diagnostics(eng, x, y, world)
     total = batch * world * a.steps
     value = total / elapsed
     if ctx.rank == 0:
@@ -140,12 +182,12 @@ def main():
             "dtype": "bf16", "data": "synthetic (random-init weights, random inputs/labels)",
             "config": dict({"model": model_name, "global_batch": batch * world, "per_gpu_batch": batch,
                             "seq_len": None, "parallelism": "dp%d" % world,
-                            "grad_sync": ("sharded(ZeRO-1)" if a.sharded else "allreduce(bucketed,overlapped)") +
-                            ("+bf16-wire" if a.grad_compression else "")},
+                            "grad_sync": grad_sync_label(eng, a)},
                            **extra),
             "first_loss": round(float(first_loss.float().item()), 4) if first_loss is not None else None,
             "final_loss": round(final_loss, 4),
         }
+        out.update(diag)
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

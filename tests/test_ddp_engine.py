@@ -300,3 +300,74 @@ def test_row_sparse_embedding_sync_matches_dense_allreduce():
     assert dense[0][1] == 0 and sparse[0][1] == 4        # four tables, one bucket each
     rows = sparse[0][2]
     assert 0 < rows < 3 * (2 * 501 + 2 * 301)            # only the looked-up union moved
+
+
+# ---------------------------------------------------------------------------
+# round 3: bucket launch order = calibrated readiness order, also for a zombie rank
+# ---------------------------------------------------------------------------
+class _OutOfOrder(nn.Module):
+    """Registration order a, b, c; forward uses b first, then a, then c -> backward produces
+    c, a, b: the flat layout (reverse registration: c, b, a) is NOT the readiness order."""
+
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = nn.Linear(8, 8)
+        self.b = nn.Linear(6, 8)
+        self.c = nn.Linear(8, 1)
+        self.fail = False
+
+    def forward(self, x):
+        h = torch.tanh(self.b(x))
+        h = torch.tanh(self.a(h))
+        if self.fail:   # fails in backward, after c's gradient is produced
+            h = _Boom.apply(h)
+        return self.c(h)
+
+
+class _Boom(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        raise RuntimeError("injected backward failure")
+
+
+def _order_worker(rank, world, port, q):
+    ctx = _init(rank, world, port)
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    m = _OutOfOrder()
+    eng = TrainingEngine(m, MeanSquaredError(), SGD(learningrate=0.05), ctx=ctx, bucket_mb=1e-6)
+    x, y = _toy(16)
+    x, y = torch.from_numpy(x), torch.from_numpy(y)
+    logs = []
+    fin = eng.sync.finish
+
+    def finish():
+        fin()
+        logs.append(list(eng.sync.launch_log))
+    eng.sync.finish = finish
+    for step in range(4):
+        m.fail = (rank == 1 and step == 2)
+        eng.train_step(x, y)
+    q.put((rank, (logs, list(eng.sync.order), [b.params for b in eng.sync.buckets],
+                  [id(p) for p in (m.c.weight, m.c.bias, m.a.weight, m.a.bias, m.b.weight, m.b.bias)],
+                  eng._local_failure is not None)))
+    ctx.stop()
+
+
+def test_bucket_order_follows_readiness_and_zombie_replays_it():
+    res = _run(_order_worker)
+    logs0, order0, bparams, pids, _ = res[0]
+    logs1, order1, _, _, zombie1 = res[1]
+    assert zombie1 and order0 == order1
+    # one parameter per bucket; readiness by layer = c, then a, then b (flat layout: c, b, a)
+    layer_of = {pid: "ccaabb"[i] for i, pid in enumerate(pids)}
+    assert [layer_of[bparams[i][0]] for i in order0] == list("ccaabb")
+    assert order0 != sorted(order0)
+    for s in range(1, 4):   # every later step (the zombie's step 2 included) launches in that order
+        assert logs0[s] == order0 and logs1[s] == order0

@@ -321,3 +321,89 @@ def test_phase_timing_and_debug_sync_are_inert_on_cpu():
     eng.debug_sync = True
     eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
     assert eng.phase_times() == {}
+
+
+# ----------------------------------------------------------------------------
+# round-3 checkpoint interop: restore-by-name, OptimMethod records, neval ordering
+# ----------------------------------------------------------------------------
+def test_checkpoint_roundtrip_with_unserialisable_layers(tmp_path):
+    """A model with a Lambda layer and a wrapped torch module (constructor arguments the
+    ``.model`` file cannot represent) reloads into the live model by layer name."""
+    from zoo.pipeline.api.autograd import Lambda
+    from zoo.pipeline.api.keras.layers import Dense, KerasLayerWrapper
+    from zoo.pipeline.api.keras.models import Sequential
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    torch.manual_seed(0)
+    m = Sequential()
+    m.add(Dense(8, activation="tanh", input_shape=(4,)))
+    m.add(Lambda(lambda t: t * 2.0))
+    m.add(KerasLayerWrapper(torch.nn.Linear(8, 3)))
+    m.add(Dense(1))
+    x, y = _toy(32)
+    eng = TrainingEngine(m, MeanSquaredError(), SGD(learningrate=0.05, momentum=0.9))
+    eng.set_checkpoint(str(tmp_path / "ck"), overwrite=False)
+    for _ in range(3):
+        eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
+    eng.save_checkpoint()
+    ref = {k: v.clone() for k, v in m.state_dict().items()}
+    mom = [b.clone() for b in eng.optim._buffers]
+    with torch.no_grad():
+        for p in m.parameters():
+            p.add_(1.0)
+    eng.optim.clear_history()
+    eng.load_checkpoint(eng.latest_checkpoint())
+    for k, v in m.state_dict().items():
+        assert torch.allclose(v.float(), ref[k].float()), k
+    assert all(torch.allclose(a, b) for a, b in zip(eng.optim._buffers, mom))
+
+
+def test_optim_method_record_is_bigdl_protobuf(tmp_path):
+    from zoo.utils.bigdl_model import is_bigdl_model_file, load_optim_method, save_optim_method
+    from zoo.utils import bigdl_proto as P
+    d = {"class": "SGD", "state": {"neval": 7, "epoch": 2, "Loss": 0.25, "tag": "x"},
+         "hyper": {"learningrate": 0.1, "momentum": 0.9, "nesterov": True},
+         "buffers": [torch.randn(13), torch.arange(5, dtype=torch.int64) * (1 << 40)]}
+    p = str(tmp_path / "optimMethod-SGD.7")
+    save_optim_method(d, p)
+    assert is_bigdl_model_file(p)
+    root, _ = P.load_bigdl_spec(p)
+    assert root.type == "com.intel.analytics.bigdl.optim.SGD"
+    assert root.attr["learningRate"] == pytest.approx(0.1) and root.attr["state.neval"] == 7
+    e = load_optim_method(p)
+    assert e["class"] == "SGD" and e["state"] == d["state"] and e["hyper"] == d["hyper"]
+    assert torch.equal(e["buffers"][0], d["buffers"][0])
+    assert e["buffers"][1].dtype == torch.int64 and torch.equal(e["buffers"][1], d["buffers"][1])
+
+
+def test_int64_buffers_roundtrip_exactly(tmp_path):
+    from zoo.utils.bigdl_model import load_bigdl_model, save_bigdl_model
+    net = torch.nn.BatchNorm1d(3)
+    net.num_batches_tracked.fill_((1 << 40) + 3)
+    p = str(tmp_path / "bn.model")
+    save_bigdl_model(net, p)
+    net2 = torch.nn.BatchNorm1d(3)
+    load_bigdl_model(p, model=net2)
+    assert int(net2.num_batches_tracked) == (1 << 40) + 3
+
+
+def test_latest_checkpoint_by_iteration_not_mtime(tmp_path):
+    import time
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(32)
+    eng = TrainingEngine(_mlp(), MeanSquaredError(), SGD(learningrate=0.05))
+    ck = tmp_path / "ck"
+    eng.set_checkpoint(str(ck), overwrite=False)
+    for _ in range(3):
+        eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
+        eng.save_checkpoint()
+    files = sorted(f for f in os.listdir(ck) if f.startswith("model."))
+    assert len(files) == 3
+    # a restored copy: the OLDEST snapshot gets the newest mtime
+    now = time.time()
+    for i, f in enumerate(sorted(files, key=lambda f: int(f.split(".")[1]))):
+        os.utime(ck / f, (now - 100 * i, now - 100 * i))
+    assert eng.latest_checkpoint().endswith("model.%d" % max(int(f.split(".")[1]) for f in files))

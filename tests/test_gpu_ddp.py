@@ -89,3 +89,43 @@ def test_forced_comm_bf16_wire_tracks_fp32(gpu, rccl_world1):
     for e in (e1, e2):  # bf16 gradient rounding: a small relative perturbation of the update
         d = (e0.flat.master - e.flat.master).norm() / e0.flat.master.norm()
         assert d.item() < 0.01
+
+
+def test_zombie_finish_replays_the_recorded_bucket_order(gpu, rccl_world1):
+    """Healthy steps launch buckets in the calibrated readiness order; a rank that failed
+    part-way through backward (some buckets launched, the rest not) finishes in that same
+    order, so its RCCL collective sequence matches the healthy ranks'."""
+    eng, _, _ = _train(rccl_world1, force=True, steps=3)
+    s = eng.sync
+    assert s.order is not None and sorted(s.order) == list(range(len(s.buckets)))
+    s.reset()
+    for i in s.order[:2]:           # the zombie got this far before failing
+        s._launch(s.buckets[i])
+    s.wait_comm()
+    eng.flat.grad.zero_()
+    s.finish()
+    assert s.launch_log == s.order
+    torch.cuda.synchronize()
+    s.reset()
+
+
+def test_comm_stats_fields(gpu, rccl_world1):
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    ctx = rccl_world1
+    old = ctx.config.force_comm
+    ctx.config.force_comm = True
+    try:
+        eng = TrainingEngine(_model(), softmax_cross_entropy, SGD(learningrate=0.05), ctx=ctx, bucket_mb=0.05)
+    finally:
+        ctx.config.force_comm = old
+    eng.sync.collect_stats = True
+    x = torch.randn(8, 3, 64, 64, device="cuda")
+    y = torch.randint(0, 16, (8,), device="cuda")
+    for _ in range(3):
+        eng.train_step(x, y)
+    summ = eng.sync.comm_summary()
+    assert summ["exposed_comm_ms_per_step"] >= 0.0
+    assert len(summ["buckets"]) == len(eng.sync.buckets)
+    assert all(b["ms"] >= 0 and b["MB"] > 0 for b in summ["buckets"])
