@@ -476,17 +476,18 @@ static int i2_bn(int tile) {
   }
 }
 
-// shape -> tile heuristic (tools/conv_sweep.py --igemm2-tiles picks it on the GPU)
+// shape -> tile (tools/igemm2_bench.py on ResNet-50 b256 + transformer GEMMs, round 3):
+//   * N >= 256: 256x256 (8 waves of 128x64) while the grid still fills >= ~0.6 of the chip
+//     (>= 160 tiles), else 128x128 (two 4-wave workgroups per CU);
+//   * N <= 128: igemm.hip's 128x{64,128} tiles are as fast or faster (its lean epilogues were
+//     tuned for exactly these memory-bound shapes) -> 0 = "not taken" unless forced.
 static int i2_choose(const ConvGeom& g) {
   const int f = i2_tile_force();
   if (f > 0) return f;
   auto tiles = [&](int t) { return (long)((g.M + i2_bm(t) - 1) / i2_bm(t)) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
-  if (g.K <= 64) return tiles(I2_256x64) >= 512 ? I2_256x64 : I2_128x64;
-  if (g.K <= 128) return tiles(I2_256x128) >= 512 ? I2_256x128_3 : I2_128x128;
-  if (tiles(I2_256x256) >= 512 && g.K % 256 == 0) return I2_256x256;
-  if (tiles(I2_256x128) >= 512) return I2_256x128_3;
-  if (tiles(I2_128x128) >= 256) return I2_128x128;
-  return I2_128x64;
+  if (g.K < 256) return 0;
+  if (tiles(I2_256x256) >= 160) return I2_256x256;
+  return I2_128x128;
 }
 
 }  // namespace zoo
@@ -497,7 +498,7 @@ using namespace zoo;
 extern "C" int zoo_igemm2_eligible(const ConvGeom* g) {
   if (i2_mode() == 0) return 0;
   return g->C % 64 == 0 && g->lh == 1 && g->lw == 1 && g->K % 8 == 0 && g->ldb % 8 == 0 &&
-         g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot;
+         g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot && i2_choose(*g) > 0;
 }
 
 // m-tile height the dispatcher will use for this geometry (partial-statistics buffers are

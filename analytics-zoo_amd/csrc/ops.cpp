@@ -21,6 +21,12 @@ hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, cons
                      const zoo::BwdStats*, hipStream_t);
 int zoo_igemm2_bm(const ConvGeom*);
 void zoo_igemm2_set(int, int);
+hipError_t zoo_wlrn(const void*, const void*, void*, float*, float*, int, int, int, int, int, float, float, int,
+                    hipStream_t);
+hipError_t zoo_resize_bilinear(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
+hipError_t zoo_upsample(const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+hipError_t zoo_lstm_gates(const float*, const float*, const float*, float*, float*, float*, const float*,
+                          const float*, float*, float*, int, int, int, int, int, hipStream_t);
 hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, const void*, float*, const GemmGeom*,
                        int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -934,6 +940,131 @@ torch::Tensor lrn(torch::Tensor x, c10::optional<torch::Tensor> dy, int size, do
                     (float)beta, (float)k, bwd, x.scalar_type() == at::kFloat, cur_stream()),
             "lrn");
   return out;
+}
+
+// ---- Keras layer kernels (keras_ops.hip) -------------------------------------------------
+static void req_act(const torch::Tensor& t, const char* what) {
+  TORCH_CHECK(t.is_cuda() && t.is_contiguous(), what, ": contiguous GPU tensor expected");
+  TORCH_CHECK(t.scalar_type() == at::kFloat || t.scalar_type() == at::kBFloat16, what, ": fp32 or bf16");
+}
+
+// WithinChannelLRN2D on NHWC: forward (dy absent) or backward (dx)
+torch::Tensor within_lrn(torch::Tensor x, c10::optional<torch::Tensor> dy, int size, double alpha, double beta) {
+  req_act(x, "within_lrn");
+  TORCH_CHECK(x.dim() == 4, "within_lrn: NHWC input");
+  TORCH_CHECK(size >= 1 && size <= 31, "within_lrn: window 1..31");
+  const bool bwd = dy.has_value() && dy->defined();
+  if (bwd) TORCH_CHECK(dy->sizes() == x.sizes() && dy->is_contiguous() && dy->scalar_type() == x.scalar_type(),
+                       "within_lrn: dy must match x");
+  auto out = torch::empty_like(x);
+  if (x.numel() == 0) return out;
+  TORCH_CHECK(x.numel() < (1LL << 40), "within_lrn: too large");
+  torch::Tensor q, sc;
+  if (bwd) {
+    q = torch::empty(x.sizes(), x.options().dtype(at::kFloat));
+    sc = torch::empty(x.sizes(), x.options().dtype(at::kFloat));
+  }
+  check_hip(zoo_wlrn(x.data_ptr(), bwd ? dy->data_ptr() : nullptr, out.data_ptr(), bwd ? q.data_ptr<float>() : nullptr,
+                     bwd ? sc.data_ptr<float>() : nullptr, x.size(0), x.size(1), x.size(2), x.size(3), size,
+                     (float)alpha, (float)beta, x.scalar_type() == at::kBFloat16, cur_stream()),
+            "within_lrn");
+  return out;
+}
+
+// ResizeBilinear (BigDL / TF-legacy sampling) on NHWC
+torch::Tensor resize_bilinear(torch::Tensor x, int OH, int OW, bool align) {
+  req_act(x, "resize_bilinear");
+  TORCH_CHECK(x.dim() == 4 && OH > 0 && OW > 0 && x.size(1) > 0 && x.size(2) > 0, "resize_bilinear: NHWC, sizes");
+  auto y = torch::empty({x.size(0), OH, OW, x.size(3)}, x.options());
+  if (y.numel() == 0) return y;
+  check_hip(zoo_resize_bilinear(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), OH, OW, align,
+                                0, x.scalar_type() == at::kBFloat16, cur_stream()),
+            "resize_bilinear");
+  return y;
+}
+
+torch::Tensor resize_bilinear_bwd(torch::Tensor dy, int H, int W, bool align) {
+  req_act(dy, "resize_bilinear_bwd");
+  TORCH_CHECK(dy.dim() == 4 && H > 0 && W > 0, "resize_bilinear_bwd: NHWC dy");
+  auto dx = torch::zeros({dy.size(0), H, W, dy.size(3)}, dy.options().dtype(at::kFloat));
+  if (dy.numel() == 0) return dx.to(dy.scalar_type());
+  check_hip(zoo_resize_bilinear(dy.data_ptr(), dx.data_ptr(), dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2),
+                                align, 1, dy.scalar_type() == at::kBFloat16, cur_stream()),
+            "resize_bilinear_bwd");
+  return dy.scalar_type() == at::kFloat ? dx : dx.to(dy.scalar_type());
+}
+
+// nearest upsampling of x [N, D, H, W, C] by (fd, fh, fw); backward sums the blocks
+torch::Tensor upsample_nd(torch::Tensor x, int fd, int fh, int fw, bool backward) {
+  req_act(x, "upsample");
+  TORCH_CHECK(x.dim() == 5 && fd >= 1 && fh >= 1 && fw >= 1, "upsample: [N, D, H, W, C] and factors >= 1");
+  torch::Tensor out;
+  int D = x.size(1), H = x.size(2), W = x.size(3);
+  if (!backward) {
+    out = torch::empty({x.size(0), (int64_t)D * fd, (int64_t)H * fh, (int64_t)W * fw, x.size(4)}, x.options());
+  } else {
+    TORCH_CHECK(D % fd == 0 && H % fh == 0 && W % fw == 0, "upsample backward: dy dims must divide by the factors");
+    D /= fd; H /= fh; W /= fw;
+    out = torch::empty({x.size(0), D, H, W, x.size(4)}, x.options());
+  }
+  if (out.numel() == 0) return out;
+  check_hip(zoo_upsample(x.data_ptr(), out.data_ptr(), x.size(0), D, H, W, x.size(4), fd, fh, fw, backward,
+                         x.scalar_type() == at::kBFloat16, cur_stream()),
+            "upsample");
+  return out;
+}
+
+// ConvLSTM gate step: g = gx + gh ([M, 4F] fp32) -> (h, c, acts)
+std::vector<torch::Tensor> lstm_gates_fwd(torch::Tensor gx, c10::optional<torch::Tensor> gh,
+                                          c10::optional<torch::Tensor> cprev, int64_t iact, int64_t act) {
+  req(gx, at::kFloat, "gx");
+  TORCH_CHECK(gx.dim() == 2 && gx.size(1) % 4 == 0, "lstm_gates: gx [M, 4F]");
+  const int64_t M = gx.size(0), F = gx.size(1) / 4;
+  if (gh.has_value() && gh->defined()) {
+    req(*gh, at::kFloat, "gh");
+    TORCH_CHECK(gh->sizes() == gx.sizes(), "lstm_gates: gh must match gx");
+  }
+  if (cprev.has_value() && cprev->defined()) {
+    req(*cprev, at::kFloat, "cprev");
+    TORCH_CHECK(cprev->numel() == M * F, "lstm_gates: c_prev [M, F]");
+  }
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "lstm_gates: activation code");
+  auto h = torch::empty({M, F}, gx.options());
+  auto c = torch::empty({M, F}, gx.options());
+  auto acts = torch::empty_like(gx);
+  if (M * F == 0) return {h, c, acts};
+  check_hip(zoo_lstm_gates(gx.data_ptr<float>(), gh.has_value() && gh->defined() ? gh->data_ptr<float>() : nullptr,
+                           cprev.has_value() && cprev->defined() ? cprev->data_ptr<float>() : nullptr,
+                           h.data_ptr<float>(), c.data_ptr<float>(), acts.data_ptr<float>(), nullptr, nullptr, nullptr,
+                           nullptr, (int)M, (int)F, (int)iact, (int)act, 0, cur_stream()),
+            "lstm_gates_fwd");
+  return {h, c, acts};
+}
+
+std::vector<torch::Tensor> lstm_gates_bwd(c10::optional<torch::Tensor> dh, c10::optional<torch::Tensor> dcn,
+                                          torch::Tensor acts, c10::optional<torch::Tensor> cprev, torch::Tensor c,
+                                          int64_t iact, int64_t act) {
+  req(acts, at::kFloat, "acts");
+  req(c, at::kFloat, "c");
+  const int64_t M = acts.size(0), F = acts.size(1) / 4;
+  TORCH_CHECK(c.numel() == M * F, "lstm_gates_bwd: c [M, F]");
+  auto opt = [&](const c10::optional<torch::Tensor>& t, const char* n) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    req(*t, at::kFloat, n);
+    TORCH_CHECK(t->numel() == M * F, "lstm_gates_bwd: ", n, " [M, F]");
+    return t->data_ptr<float>();
+  };
+  const float* pdh = opt(dh, "dh");
+  const float* pdc = opt(dcn, "dc");
+  const float* pcp = opt(cprev, "cprev");
+  auto dg = torch::empty_like(acts);
+  auto dcp = torch::empty_like(c);
+  if (M * F == 0) return {dg, dcp};
+  check_hip(zoo_lstm_gates(nullptr, nullptr, pcp, nullptr, c.data_ptr<float>(), acts.data_ptr<float>(), pdh, pdc,
+                           dg.data_ptr<float>(), dcp.data_ptr<float>(), (int)M, (int)F, (int)iact, (int)act, 1,
+                           cur_stream()),
+            "lstm_gates_bwd");
+  return {dg, dcp};
 }
 
 torch::Tensor gap_fwd(torch::Tensor x) {
@@ -1905,6 +2036,12 @@ PYBIND11_MODULE(_C, m) {
         py::arg("gelu") = false);
   m.def("softmax_rows_bwd", &softmax_rows_bwd);
   m.def("lrn", &lrn);
+  m.def("within_lrn", &within_lrn);
+  m.def("resize_bilinear", &resize_bilinear);
+  m.def("resize_bilinear_bwd", &resize_bilinear_bwd);
+  m.def("upsample_nd", &upsample_nd);
+  m.def("lstm_gates_fwd", &lstm_gates_fwd);
+  m.def("lstm_gates_bwd", &lstm_gates_bwd);
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
         "igemm2 A/B switch: mode 0 off / 1 on (-1 keep), tile 0 auto / I2Tile id (-1 keep)");
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });

@@ -9,5 +9,5 @@ from zoo.ops.conv import conv2d_nhwc, linear, pack_weight, unpack_weight, ceil8,
 from zoo.ops.bn import conv_bn_act, batch_norm_nhwc, GradHandoff, BNProducer
 from zoo.ops.pool import max_pool2d_nhwc, global_avg_pool_nhwc
 from zoo.ops.loss import softmax_cross_entropy
-from zoo.ops.nn import layer_norm, embedding, dropout_add
+from zoo.ops.nn import layer_norm, embedding, dropout_add, depthwise_conv2d_nhwc, lrn_channels_last
 from zoo.ops.attention import attention

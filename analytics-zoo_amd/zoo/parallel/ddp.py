@@ -564,7 +564,7 @@ class GradSync:
             ms = st["bucket_ms"][i] / n
             by = st["bucket_bytes"].get(i, 0)
             alg = by / (ms * 1e-3) / 1e9 if ms > 0 else 0.0
-            out["buckets"].append({"bucket": i, "MB": round(by / 1e6, 2), "ms": round(ms, 3),
+            out["buckets"].append({"bucket": i, "bytes": by, "MB": round(by / 1e6, 3), "ms": round(ms, 3),
                                    "algbw_GBs": round(alg, 1), "busbw_GBs": round(alg * k, 1)})
         return out
 

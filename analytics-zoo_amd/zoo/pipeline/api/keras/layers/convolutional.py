@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.ops import layers as ops_layers
 from zoo.pipeline.api.keras.base import Layer, apply_activation, check_activation, init_tensor, to_shape
 
 
@@ -314,6 +315,20 @@ class SeparableConvolution2D(Layer):
             (None, out[0], out[1], self.nb_filter)
 
     def call(self, x):
+        if x.is_cuda and self.kernel[0] * self.kernel[1] <= 9 and (self.cin * self.depth_multiplier) % 8 == 0:
+            # native: depthwise kernel (NHWC) -> pointwise 1x1 on the implicit-GEMM conv
+            xn = x.permute(0, 2, 3, 1) if self.dim_ordering == "th" else x
+            if self.border_mode == "same":
+                p = [_same_pads(xn.shape[1 + i], self.kernel[i], self.subsample[i]) for i in range(2)]
+                xn = F.pad(xn, (0, 0, p[1][0], p[1][1], p[0][0], p[0][1]))
+            if self.depth_multiplier > 1:
+                xn = xn.repeat_interleave(self.depth_multiplier, dim=-1)
+            R, S = self.kernel
+            taps = self.depthwise.reshape(self.cin * self.depth_multiplier, R * S).t()   # [R*S, C*m]
+            d = ops.depthwise_conv2d_nhwc(xn, taps, None, kernel=(R, S), stride=self.subsample)
+            y = ops.linear(d, self.pointwise, self.bias)
+            y = apply_activation(y, self.activation).to(x.dtype)
+            return y.permute(0, 3, 1, 2).contiguous() if self.dim_ordering == "th" else y
         xc = x if self.dim_ordering == "th" else x.permute(0, 3, 1, 2)
         pad = 0
         if self.border_mode == "same":
@@ -347,14 +362,23 @@ class Convolution3D(Layer):
         return (None, self.nb_filter, *out) if self.dim_ordering == "th" else (None, *out, self.nb_filter)
 
     def call(self, x):
-        xc = x if self.dim_ordering == "th" else x.permute(0, 4, 1, 2, 3)
+        from zoo.ops.layers import conv3d_ndhwc
+        xn = x if self.dim_ordering == "tf" else x.permute(0, 2, 3, 4, 1)        # NDHWC
         if self.border_mode == "same":
-            p = [_same_pads(xc.shape[2 + i], self.kernel[i], self.subsample[i]) for i in range(3)]
-            xc = F.pad(xc, (p[2][0], p[2][1], p[1][0], p[1][1], p[0][0], p[0][1]))
-        y = F.conv3d(xc, self.weight.to(xc.dtype), None if self.bias is None else self.bias.to(xc.dtype),
-                     stride=self.subsample)
-        y = apply_activation(y, self.activation)
-        return y if self.dim_ordering == "th" else y.permute(0, 2, 3, 4, 1)
+            p = [_same_pads(xn.shape[1 + i], self.kernel[i], self.subsample[i]) for i in range(3)]
+            xn = F.pad(xn, (0, 0, p[2][0], p[2][1], p[1][0], p[1][1], p[0][0], p[0][1]))
+        K, C = self.weight.shape[0], self.weight.shape[1]
+        if x.is_cuda and (C % 8 or K % 8):   # 16-byte channel granule of the MFMA conv: zero-pad
+            cp, kp = (-C) % 8, (-K) % 8
+            xn = F.pad(xn, (0, cp))
+            w5 = F.pad(self.weight.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
+            b = None if self.bias is None else F.pad(self.bias, (0, kp))
+            y = conv3d_ndhwc(xn.to(torch.bfloat16), w5, b, stride=self.subsample)[..., :K]
+        else:
+            y = conv3d_ndhwc(xn.to(torch.bfloat16) if x.is_cuda else xn, self.weight.permute(0, 2, 3, 4, 1),
+                             self.bias, stride=self.subsample)
+        y = apply_activation(y.to(x.dtype), self.activation)
+        return y if self.dim_ordering == "tf" else y.permute(0, 4, 1, 2, 3)
 
 
 Conv3D = Convolution3D
@@ -432,7 +456,7 @@ class UpSampling1D(Layer):
         return (None, None if s[1] is None else s[1] * self.length, s[2])
 
     def call(self, x):
-        return x.repeat_interleave(self.length, dim=1)
+        return ops_layers.upsample_nearest(x, (self.length,))
 
 
 class UpSampling2D(Layer):
@@ -446,8 +470,9 @@ class UpSampling2D(Layer):
         return (None, s[1] * self.size[0], s[2] * self.size[1], s[3])
 
     def call(self, x):
-        a = 2 if self.dim_ordering == "th" else 1
-        return x.repeat_interleave(self.size[0], dim=a).repeat_interleave(self.size[1], dim=a + 1)
+        if self.dim_ordering == "th":
+            return ops_layers.upsample_nearest(x.permute(0, 2, 3, 1), self.size).permute(0, 3, 1, 2)
+        return ops_layers.upsample_nearest(x, self.size)
 
 
 class UpSampling3D(Layer):
@@ -461,10 +486,9 @@ class UpSampling3D(Layer):
         return (None,) + tuple(d * k for d, k in zip(s[1:4], self.size)) + (s[4],)
 
     def call(self, x):
-        a = 2 if self.dim_ordering == "th" else 1
-        for i, k in enumerate(self.size):
-            x = x.repeat_interleave(k, dim=a + i)
-        return x
+        if self.dim_ordering == "th":
+            return ops_layers.upsample_nearest(x.permute(0, 2, 3, 4, 1), self.size).permute(0, 4, 1, 2, 3)
+        return ops_layers.upsample_nearest(x, self.size)
 
 
 class ZeroPadding1D(Layer):
@@ -574,6 +598,8 @@ class ResizeBilinear(Layer):
         return (None, s[1], self.oh, self.ow) if self.dim_ordering == "th" else (None, self.oh, self.ow, s[3])
 
     def call(self, x):
-        xc = x if self.dim_ordering == "th" else x.permute(0, 3, 1, 2)
-        y = F.interpolate(xc, size=(self.oh, self.ow), mode="bilinear", align_corners=self.align)
-        return y if self.dim_ordering == "th" else y.permute(0, 2, 3, 1)
+        # BigDL nn.ResizeBilinear sampling (TF legacy: src = dst * in/out, or (in-1)/(out-1)
+        # with align_corners); native NHWC kernel on the GPU
+        xn = x.permute(0, 2, 3, 1) if self.dim_ordering == "th" else x
+        y = ops_layers.resize_bilinear(xn.contiguous(), self.oh, self.ow, self.align)
+        return y.permute(0, 3, 1, 2) if self.dim_ordering == "th" else y

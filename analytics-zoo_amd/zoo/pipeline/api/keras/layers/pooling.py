@@ -114,12 +114,16 @@ class _Pool1D(Layer):
         return (None, _pool_out(s[1], self.pool_length, self.stride, self.border_mode), s[2])
 
     def call(self, x):
-        xc = x.transpose(1, 2)
+        from zoo.ops.layers import pool1d_nwc
+        pad = (0, 0)
         if self.border_mode == "same":
-            p = _same_pad(xc.shape[2], self.pool_length, self.stride)
-            xc = F.pad(xc, p, value=float("-inf") if self.kind == "max" else 0.0)
-        f = F.max_pool1d if self.kind == "max" else F.avg_pool1d
-        return f(xc, self.pool_length, self.stride).transpose(1, 2)
+            pad = tuple(_same_pad(x.shape[1], self.pool_length, self.stride))
+        if x.is_cuda and pad != (0, 0) and x.shape[-1] % 8 == 0:
+            # explicit edge padding (-inf for max, 0 for average as the reference does), then
+            # the native pool with no implicit padding
+            x = F.pad(x, (0, 0, pad[0], pad[1]), value=float("-inf") if self.kind == "max" else 0.0)
+            pad = (0, 0)
+        return pool1d_nwc(x, self.kind, self.pool_length, self.stride, pad).to(x.dtype)
 
 
 class MaxPooling1D(_Pool1D):
@@ -146,10 +150,12 @@ class _Pool3D(Layer):
         return (None, s[1]) + o if self.dim_ordering == "th" else (None,) + o + (s[4],)
 
     def call(self, x):
-        xc = x if self.dim_ordering == "th" else x.permute(0, 4, 1, 2, 3)
-        f = F.max_pool3d if self.kind == "max" else F.avg_pool3d
-        y = f(xc, self.pool_size, self.strides)
-        return y if self.dim_ordering == "th" else y.permute(0, 2, 3, 4, 1)
+        from zoo.ops.layers import pool3d_ndhwc
+        xn = x if self.dim_ordering == "tf" else x.permute(0, 2, 3, 4, 1)
+        if x.is_cuda:
+            xn = xn.contiguous()
+        y = pool3d_ndhwc(xn, self.kind, self.pool_size, self.strides).to(x.dtype)
+        return y if self.dim_ordering == "tf" else y.permute(0, 4, 1, 2, 3)
 
 
 class MaxPooling3D(_Pool3D):

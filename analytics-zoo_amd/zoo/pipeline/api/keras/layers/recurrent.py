@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.ops.layers import lstm_gates
 from zoo.ops import rnn as rnn_ops
 from zoo.pipeline.api.keras.base import Layer, apply_activation, init_tensor
 
@@ -210,24 +211,26 @@ class ConvLSTM2D(Layer):
             xn = F.pad(xn, (0, cpx - C))
         xs = ops.conv2d_nhwc(xn, wx, bias, kernel=(R, S), stride=self.subsample, pad=pad, out_f32=True)[..., :K]
         Ho, Wo = xs.shape[1], xs.shape[2]
-        xs = xs.reshape(B, T, Ho, Wo, K)
-        h = xs.new_zeros(B, Ho, Wo, f)
-        c = h.clone()
+        xs = xs.reshape(B, T, Ho * Wo, K)
+        M = B * Ho * Wo
+        h = c = None
         outs = []
         for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):
-            hp = F.pad(h, (0, cph - f)) if cph != f else h
-            g = xs[:, t] + ops.conv2d_nhwc(hp, wh, None, kernel=(R, S), stride=(1, 1), pad=pad, out_f32=True)[..., :K]
-            i = apply_activation(g[..., :f], self.inner_activation)
-            fg = apply_activation(g[..., f:2 * f], self.inner_activation)
-            cc = apply_activation(g[..., 2 * f:3 * f], self.activation)
-            o = apply_activation(g[..., 3 * f:], self.inner_activation)
-            c = fg * c + i * cc
-            h = o * apply_activation(c, self.activation)
-            outs.append(h.permute(0, 3, 1, 2))
+            gh = None
+            if h is not None:   # h_0 = 0: no recurrent conv on the first step
+                hn = h.reshape(B, Ho, Wo, f)
+                hp = F.pad(hn, (0, cph - f)) if cph != f else hn
+                gh = ops.conv2d_nhwc(hp, wh, None, kernel=(R, S), stride=(1, 1), pad=pad,
+                                     out_f32=True)[..., :K].reshape(M, K)
+            # gate activations, cell and hidden update in ONE native pass (keras_ops.hip)
+            h, c = lstm_gates(xs[:, t].reshape(M, K), gh, c, self.inner_activation, self.activation)
+            outs.append(h.reshape(B, Ho, Wo, f).permute(0, 3, 1, 2))
         return torch.stack(outs, 1) if self.return_sequences else outs[-1]
 
     def call(self, x):
-        if x.is_cuda and (self.k[0] % 2 == 1 and self.k[1] % 2 == 1):
+        from zoo.ops.layers import ACT_CODES
+        if x.is_cuda and (self.k[0] % 2 == 1 and self.k[1] % 2 == 1) and \
+                self.activation in ACT_CODES and self.inner_activation in ACT_CODES:
             return self._call_native(x)
         B, T = x.shape[:2]
         pad = (self.k[0] // 2, self.k[1] // 2)
@@ -270,7 +273,41 @@ class ConvLSTM3D(Layer):
             return (None, s[1], self.nb_filter) + tuple(s[3:])
         return (None, self.nb_filter) + tuple(s[3:])
 
+    def _call_native(self, x):
+        """GPU path (InternalConvLSTM3D.scala): the input convolution for all timesteps in one
+        3-D conv (implicit-GEMM launches), per step one recurrent 3-D conv and one fused
+        gate / cell / hidden pass."""
+        from zoo.ops.layers import conv3d_ndhwc
+        B, T, C = x.shape[:3]
+        sp = tuple(x.shape[3:])
+        f, k = self.nb_filter, self.k
+        K = 4 * f
+        p = k // 2
+        cp, fp, kp = (-C) % 8, (-f) % 8, (-K) % 8
+        xn = x.reshape(B * T, C, *sp).permute(0, 2, 3, 4, 1)
+        xn = F.pad(xn, (0, cp)).to(torch.bfloat16)
+        wx = F.pad(self.Wx.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
+        wh = F.pad(self.Wh.permute(0, 2, 3, 4, 1), (0, fp, 0, 0, 0, 0, 0, 0, 0, kp))
+        bias = F.pad(self.b, (0, kp))
+        xs = conv3d_ndhwc(xn, wx, bias, stride=(1, 1, 1), pad=(p, p, p)).float()[..., :K]
+        osp = tuple(xs.shape[1:4])
+        P = osp[0] * osp[1] * osp[2]
+        xs = xs.reshape(B, T, P, K)
+        M = B * P
+        h = c = None
+        outs = []
+        for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):
+            gh = None
+            if h is not None:
+                hn = F.pad(h.reshape(B, *osp, f), (0, fp)).to(torch.bfloat16)
+                gh = conv3d_ndhwc(hn, wh, None, stride=(1, 1, 1), pad=(p, p, p)).float()[..., :K].reshape(M, K)
+            h, c = lstm_gates(xs[:, t].reshape(M, K), gh, c, "sigmoid", "tanh")
+            outs.append(h.reshape(B, *osp, f).permute(0, 4, 1, 2, 3))
+        return torch.stack(outs, 1).to(x.dtype) if self.return_sequences else outs[-1].to(x.dtype)
+
     def call(self, x):
+        if x.is_cuda and self.k % 2 == 1:
+            return self._call_native(x)
         B, T = x.shape[:2]
         p = self.k // 2
         xs = F.conv3d(x.reshape(B * T, *x.shape[2:]), self.Wx.to(x.dtype), self.b.to(x.dtype), 1, p)

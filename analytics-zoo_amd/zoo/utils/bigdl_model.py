@@ -352,8 +352,14 @@ def _torch_spec(model):
 
 def model_to_bytes(model, extra_attr=None):
     from zoo.pipeline.api.keras.base import Layer
-    spec = _keras_spec(model) if isinstance(model, Layer) and hasattr(model, "_init_args") or \
-        type(model).__name__ in ("Sequential", "Model") and isinstance(model, Layer) else _torch_spec(model)
+    from zoo.utils import bigdl_graph
+    if bigdl_graph.is_resnet(model):
+        # a real BigDL nn graph (SpatialConvolution / SpatialBatchNormalization / CAddTable / ...),
+        # not an opaque TorchModel blob (zoo.utils.bigdl_graph)
+        spec = bigdl_graph.resnet_graph_spec(model)
+    else:
+        spec = _keras_spec(model) if isinstance(model, Layer) and hasattr(model, "_init_args") or \
+            type(model).__name__ in ("Sequential", "Model") and isinstance(model, Layer) else _torch_spec(model)
     if extra_attr:
         spec.setdefault("attr", {}).update(extra_attr)
     return _Writer().module(spec)
@@ -674,6 +680,10 @@ def load_bigdl_model(path, model=None):
             model.load_state_dict(loaded.state_dict())
             return model
         return loaded
+    if model is not None and root.type.endswith("StaticGraph") and "zoo_class" in root.attr:
+        from zoo.utils import bigdl_graph
+        if bigdl_graph.is_resnet(model):
+            return bigdl_graph.restore_resnet(model, root, st)
     if root.type == TORCH_MODEL:
         sd = {n: torch.from_numpy(tr.materialize(st, native=True)) for n, tr in zip(root.attr["zoo_param_names"], root.parameters)}
         if model is None:

@@ -128,4 +128,4 @@ def test_comm_stats_fields(gpu, rccl_world1):
     summ = eng.sync.comm_summary()
     assert summ["exposed_comm_ms_per_step"] >= 0.0
     assert len(summ["buckets"]) == len(eng.sync.buckets)
-    assert all(b["ms"] >= 0 and b["MB"] > 0 for b in summ["buckets"])
+    assert all(b["ms"] >= 0 and b["bytes"] > 0 for b in summ["buckets"])
