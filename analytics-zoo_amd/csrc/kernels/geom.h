@@ -49,6 +49,15 @@ struct FlipDesc {
   int K, R, S, C, ldw, r0, s0, Ra, Sb, sh, sw, ldt, blk0, nblk;
 };
 
+// Epilogue class of an implicit-GEMM call (igemm.hip / igemm2.hip and the host binding agree on
+// it): 1 = plain bf16 output (+ BN statistics), 2 = backward (residual-gradient add, ReLU mask,
+// fused BN-backward sums, remap), 0 = general (bias / activation / fp32 output / ...)
+inline int igemm_epi(bool y, bool yf, bool bias, bool resid, int act, bool omap, bool bsums, bool stats) {
+  if (y && !yf && !bias && !resid && act == 0 && !omap && !bsums) return 1;
+  if (y && !yf && !bias && act == 0 && !stats) return 2;
+  return 0;
+}
+
 // Plain GEMM geometry (gemm256.hip): Y[M, N] = A[M, K] . B[N, K]^T
 struct GemmGeom {
   int M, N, K;

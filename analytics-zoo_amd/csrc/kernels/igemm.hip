@@ -659,7 +659,7 @@ static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, floa
 
 using namespace zoo;
 
-extern "C" int zoo_igemm2_eligible(const ConvGeom* g);
+extern "C" int zoo_igemm2_eligible(const ConvGeom* g, int epi);
 extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                  const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                  hipStream_t st);
@@ -668,7 +668,8 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
   // whole-64-channel K-tiles: the large-tile second-generation kernel (igemm2.hip)
-  if (zoo_igemm2_eligible(g)) return zoo_igemm2(X, W, Y, Yf, bias, resid, stats, g, act, bsp, st);
+  if (zoo_igemm2_eligible(g, igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats)))
+    return zoo_igemm2(X, W, Y, Yf, bias, resid, stats, g, act, bsp, st);
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;

@@ -476,16 +476,19 @@ static int i2_bn(int tile) {
   }
 }
 
-// shape -> tile (tools/igemm2_bench.py on ResNet-50 b256 + transformer GEMMs, round 3):
-//   * N >= 256: 256x256 (8 waves of 128x64) while the grid still fills >= ~0.6 of the chip
-//     (>= 160 tiles), else 128x128 (two 4-wave workgroups per CU);
-//   * N <= 128: igemm.hip's 128x{64,128} tiles are as fast or faster (its lean epilogues were
-//     tuned for exactly these memory-bound shapes) -> 0 = "not taken" unless forced.
-static int i2_choose(const ConvGeom& g) {
+// shape + epilogue -> tile, or 0 = "leave it to igemm.hip" (tools/igemm2_bench.py on the
+// ResNet-50 b256 convs with the model's own epilogues, round 3, profiles/igemm2_r3.md):
+//   * N (output channels) < 256: igemm.hip's 128x{64,128} tiles are as fast or faster;
+//   * a short reduction (Ktot < 256 forward, < 1024 for the BN-backward epilogue) is bound by
+//     the epilogue, where igemm.hip's row-pointer epilogues win;
+//   * otherwise 256x256 (8 waves of 128x64) while >= 160 tiles fill the chip, else 128x128.
+static int i2_choose(const ConvGeom& g, int epi) {
   const int f = i2_tile_force();
   if (f > 0) return f;
   auto tiles = [&](int t) { return (long)((g.M + i2_bm(t) - 1) / i2_bm(t)) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
   if (g.K < 256) return 0;
+  if (epi == 2 && g.Ktot < 1024) return 0;
+  if (epi != 2 && g.Ktot < 256) return 0;
   if (tiles(I2_256x256) >= 160) return I2_256x256;
   return I2_128x128;
 }
@@ -494,18 +497,19 @@ static int i2_choose(const ConvGeom& g) {
 
 using namespace zoo;
 
-// eligibility: whole 64-channel K-tiles, plain (non-input-dilated) conv, 16-byte rows
-extern "C" int zoo_igemm2_eligible(const ConvGeom* g) {
+// eligibility: whole 64-channel K-tiles, plain (non-input-dilated) conv, 16-byte rows, and a
+// shape / epilogue where the large tiles win
+extern "C" int zoo_igemm2_eligible(const ConvGeom* g, int epi) {
   if (i2_mode() == 0) return 0;
   return g->C % 64 == 0 && g->lh == 1 && g->lw == 1 && g->K % 8 == 0 && g->ldb % 8 == 0 &&
-         g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot && i2_choose(*g) > 0;
+         g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot && i2_choose(*g, epi) > 0;
 }
 
-// m-tile height the dispatcher will use for this geometry (partial-statistics buffers are
-// [ceil(M / bm)][2K]); 0 = not taken by igemm2
-extern "C" int zoo_igemm2_bm(const ConvGeom* g) {
-  if (!zoo_igemm2_eligible(g)) return 0;
-  return i2_bm(i2_choose(*g));
+// m-tile height the dispatcher will use for this geometry and epilogue (partial-statistics
+// buffers are [ceil(M / bm)][2K]); 0 = not taken by igemm2
+extern "C" int zoo_igemm2_bm(const ConvGeom* g, int epi) {
+  if (!zoo_igemm2_eligible(g, epi)) return 0;
+  return i2_bm(i2_choose(*g, epi));
 }
 
 extern "C" void zoo_igemm2_set(int mode, int tile) {
@@ -516,14 +520,12 @@ extern "C" void zoo_igemm2_set(int mode, int tile) {
 extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                  const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                  hipStream_t st) {
-  if (!zoo_igemm2_eligible(g)) return hipErrorNotSupported;
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bs.sums, stats);
+  if (!zoo_igemm2_eligible(g, epi)) return hipErrorNotSupported;
   const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
                      g->H == g->P && g->W == g->Q;
-  int epi = 0;
-  if (Y && !Yf && !bias && !resid && act == 0 && !g->omap && !bs.sums) epi = 1;
-  else if (Y && !Yf && !bias && act == 0 && !stats) epi = 2;
-  const int tile = i2_choose(*g);
+  const int tile = i2_choose(*g, epi);
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
   if (is1x1)

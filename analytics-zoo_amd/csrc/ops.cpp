@@ -19,7 +19,7 @@ using zoo::GemmGeom;
 extern "C" {
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
                      const zoo::BwdStats*, hipStream_t);
-int zoo_igemm2_bm(const ConvGeom*);
+int zoo_igemm2_bm(const ConvGeom*, int);
 void zoo_igemm2_set(int, int);
 hipError_t zoo_wlrn(const void*, const void*, void*, float*, float*, int, int, int, int, int, float, float, int,
                     hipStream_t);
@@ -27,6 +27,8 @@ hipError_t zoo_resize_bilinear(const void*, void*, int, int, int, int, int, int,
 hipError_t zoo_upsample(const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_lstm_gates(const float*, const float*, const float*, float*, float*, float*, const float*,
                           const float*, float*, float*, int, int, int, int, int, hipStream_t);
+hipError_t zoo_roi_pool(const void*, const float*, void*, int*, const void*, float*, int, int, int, int, int, int,
+                        int, float, int, int, hipStream_t);
 hipError_t zoo_gemm256(const void*, const void*, void*, float*, const float*, const void*, float*, const GemmGeom*,
                        int, const zoo::BwdStats*, hipStream_t);
 hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -290,7 +292,9 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   float* const stat_dst = sp ? sp : bs.sums;
   torch::Tensor part;
   // m-tile height of the kernel the dispatcher picks (igemm.hip: 128; igemm2.hip: 128 or 256)
-  const int bm = zoo_igemm2_bm(&g) > 0 ? zoo_igemm2_bm(&g) : 128;
+  const int epi = zoo::igemm_epi(out_bf16, out_f32, bp != nullptr, rp != nullptr, act, g.omap != 0,
+                                 bs.sums != nullptr, sp != nullptr);
+  const int bm = zoo_igemm2_bm(&g, epi) > 0 ? zoo_igemm2_bm(&g, epi) : 128;
   const int tiles_m = (g.M + bm - 1) / bm;
   // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
   // the atomics go straight into the final 2K floats, no slot fold launch needed
@@ -1065,6 +1069,39 @@ std::vector<torch::Tensor> lstm_gates_bwd(c10::optional<torch::Tensor> dh, c10::
                            cur_stream()),
             "lstm_gates_bwd");
   return {dg, dcp};
+}
+
+// Max RoI pooling (Faster R-CNN): features NHWC, rois [R, 5] fp32 -> (out [R, PH, PW, C], argmax int32)
+std::vector<torch::Tensor> roi_pool_fwd(torch::Tensor f, torch::Tensor rois, int PH, int PW, double scale) {
+  req_act(f, "roi_pool");
+  req(rois, at::kFloat, "rois");
+  TORCH_CHECK(f.dim() == 4 && rois.dim() == 2 && rois.size(1) == 5, "roi_pool: f NHWC, rois [R, 5]");
+  TORCH_CHECK(PH > 0 && PW > 0 && f.size(0) > 0, "roi_pool: pooled size / batch");
+  const int R = rois.size(0), H = f.size(1), W = f.size(2), C = f.size(3);
+  auto out = torch::empty({R, PH, PW, C}, f.options());
+  auto arg = torch::empty({R, PH, PW, C}, f.options().dtype(at::kInt));
+  if (out.numel() == 0) return {out, arg};
+  TORCH_CHECK((int64_t)H * W < (1LL << 31) && out.numel() < (1LL << 40), "roi_pool: too large");
+  check_hip(zoo_roi_pool(f.data_ptr(), rois.data_ptr<float>(), out.data_ptr(), arg.data_ptr<int>(), nullptr, nullptr,
+                         f.size(0), R, H, W, C, PH, PW, (float)scale, 0, f.scalar_type() == at::kBFloat16,
+                         cur_stream()),
+            "roi_pool");
+  return {out, arg};
+}
+
+torch::Tensor roi_pool_bwd(torch::Tensor dy, torch::Tensor argmax, torch::Tensor rois, int B, int H, int W) {
+  req_act(dy, "roi_pool_bwd");
+  req(rois, at::kFloat, "rois");
+  TORCH_CHECK(argmax.is_cuda() && argmax.scalar_type() == at::kInt && argmax.sizes() == dy.sizes() &&
+                  argmax.is_contiguous(), "roi_pool_bwd: argmax int32 like dy");
+  TORCH_CHECK(dy.dim() == 4 && rois.size(0) == dy.size(0) && B > 0, "roi_pool_bwd: shapes");
+  auto df = torch::zeros({B, H, W, dy.size(3)}, dy.options().dtype(at::kFloat));
+  if (dy.numel() == 0) return df;
+  check_hip(zoo_roi_pool(nullptr, rois.data_ptr<float>(), nullptr, argmax.data_ptr<int>(), dy.data_ptr(),
+                         df.data_ptr<float>(), B, dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2), 1.f, 1,
+                         dy.scalar_type() == at::kBFloat16, cur_stream()),
+            "roi_pool_bwd");
+  return df;
 }
 
 torch::Tensor gap_fwd(torch::Tensor x) {
@@ -2037,6 +2074,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("softmax_rows_bwd", &softmax_rows_bwd);
   m.def("lrn", &lrn);
   m.def("within_lrn", &within_lrn);
+  m.def("roi_pool_fwd", &roi_pool_fwd);
+  m.def("roi_pool_bwd", &roi_pool_bwd);
   m.def("resize_bilinear", &resize_bilinear);
   m.def("resize_bilinear_bwd", &resize_bilinear_bwd);
   m.def("upsample_nd", &upsample_nd);

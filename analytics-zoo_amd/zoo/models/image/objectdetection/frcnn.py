@@ -3,10 +3,15 @@ configs: Zs/models/image/objectdetection/ObjectDetectionConfig.scala:38-46, 70-1
 post-processing Postprocessor.scala:30-75; BigDL Proposal / RoiPooling /
 DetectionOutputFrcnn layers behind them).
 
-The network runs NCHW on the device (convolutions on MIOpen through torch, the
-linear heads on the framework's linear op). Proposal generation and per-class
-detection output are vectorised on the device; only the greedy NMS loop runs on
-the host, as in SSD's DetectionOutput.
+On the GPU the whole network runs channels-last on the native kernels: backbone
+(VGG16 conv1-conv5 / PVANet) and RPN convolutions on the implicit-GEMM MFMA conv with the
+bias + ReLU epilogue, max pooling, PVANet's C.ReLU BatchNorm and hyper-feature resize on the
+NHWC kernels, RoI max pooling on its own kernel (csrc/kernels/roi.hip), the fc heads on the
+framework's linear op. The parameters stay in torch layout (nn.Conv2d / nn.Linear) so the
+reference's weights load unchanged; the packed bf16 conv weights are derived and cached per
+weight version. On the CPU the same modules run as the fp32 torch reference. Proposal
+generation and per-class detection output are vectorised on the device; only the greedy NMS
+loop runs on the host, as in SSD's DetectionOutput.
 
 Pre-processing follows ``preprocessFrcnn(resolution, scaleMultipleOf)``: aspect
 scale to ``resolution`` on the short side (600 for VGG16, 640 with multiples of
@@ -104,18 +109,73 @@ class Proposal(nn.Module):
 
 
 def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16):
-    """Max RoI pooling (BigDL RoiPooling): each RoI, in feature coordinates, is
-    divided into pooled x pooled bins and max-reduced."""
+    """Max RoI pooling (BigDL RoiPooling / Caffe ROIPooling) of NCHW features: each RoI is
+    rounded to feature coordinates and split into pooled x pooled fractional bins
+    [floor(i * h / P), ceil((i + 1) * h / P)), clipped to the map; an empty bin is 0.
+    fp32 reference of the native channels-last kernel (roi_pool_nhwc)."""
     out = features.new_zeros(rois.shape[0], features.shape[1], pooled, pooled)
     H, W = features.shape[2], features.shape[3]
-    r = torch.round(rois[:, 1:] * spatial_scale).long()
+    r = torch.round(rois[:, 1:] * spatial_scale).long().tolist()
+    bidx = rois[:, 0].long().clamp(0, features.shape[0] - 1).tolist()
     for i in range(rois.shape[0]):
-        b = int(rois[i, 0])
-        x1, y1 = int(r[i, 0].clamp(0, W - 1)), int(r[i, 1].clamp(0, H - 1))
-        x2, y2 = int(r[i, 2].clamp(x1, W - 1)), int(r[i, 3].clamp(y1, H - 1))
-        crop = features[b:b + 1, :, y1:y2 + 1, x1:x2 + 1]
-        out[i] = F.adaptive_max_pool2d(crop, pooled)[0]
+        x1, y1, x2, y2 = r[i]
+        rw, rh = max(x2 - x1 + 1, 1), max(y2 - y1 + 1, 1)
+        for ph in range(pooled):
+            hs = min(max(int(math.floor(ph * rh / pooled)) + y1, 0), H)
+            he = min(max(int(math.ceil((ph + 1) * rh / pooled)) + y1, 0), H)
+            for pw in range(pooled):
+                ws = min(max(int(math.floor(pw * rw / pooled)) + x1, 0), W)
+                we = min(max(int(math.ceil((pw + 1) * rw / pooled)) + x1, 0), W)
+                if hs < he and ws < we:
+                    out[i, :, ph, pw] = features[bidx[i], :, hs:he, ws:we].amax((1, 2))
     return out
+
+
+class _RoiPoolFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, f, rois, pooled, scale):
+        out, arg = ops.native().roi_pool_fwd(f, rois, pooled, pooled, scale)
+        ctx.save_for_backward(arg, rois)
+        ctx.fshape = f.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        arg, rois = ctx.saved_tensors
+        B, H, W, _ = ctx.fshape
+        df = ops.native().roi_pool_bwd(dy.contiguous(), arg, rois, B, H, W)
+        return df, None, None, None
+
+
+def roi_pool_nhwc(features, rois, pooled=7, spatial_scale=1.0 / 16):
+    """Native max RoI pooling of channels-last features -> [R, pooled, pooled, C]."""
+    return _RoiPoolFn.apply(features.contiguous(), rois.float().contiguous(), int(pooled), float(spatial_scale))
+
+
+def _packed_conv(conv, cin):
+    """nn.Conv2d [K, C, R, S] -> packed [ceil8(K), ldb] weight over ``cin`` (>= C, zero padded)
+    input channels plus the padded bias; cached on the module per weight version."""
+    key = (conv.weight._version, conv.weight.data_ptr(), cin,
+           None if conv.bias is None else (conv.bias._version, conv.bias.data_ptr()))
+    c = getattr(conv, "_zoo_packed", None)
+    if c is not None and c[0] == key and not torch.is_grad_enabled():
+        return c[1], c[2]
+    K, C, R, S = conv.weight.shape
+    w4 = F.pad(conv.weight.permute(0, 2, 3, 1), (0, cin - C, 0, 0, 0, 0, 0, ops.ceil8(K) - K))
+    wp = ops.pack_weight(w4)
+    b = None if conv.bias is None else F.pad(conv.bias, (0, ops.ceil8(K) - K))
+    if not torch.is_grad_enabled():
+        conv._zoo_packed = (key, wp, b)
+    return wp, b
+
+
+def _nconv(x, conv, act=None):
+    """NHWC conv on the implicit-GEMM kernel with the module's own stride / padding."""
+    C = x.shape[-1]
+    wp, b = _packed_conv(conv, C)
+    y = ops.conv2d_nhwc(x, wp, b, kernel=conv.kernel_size, stride=conv.stride, pad=conv.padding, act=act)
+    K = conv.out_channels
+    return y if y.shape[-1] == K else y[..., :K]
 
 
 class DetectionOutputFrcnn(nn.Module):
@@ -223,6 +283,64 @@ class _PVANetLite(nn.Module):
         return self.fuse(hyper)
 
 
+def _vgg_native(seq, x):
+    mods = list(seq)
+    i = 0
+    while i < len(mods):
+        m = mods[i]
+        if isinstance(m, nn.Conv2d):
+            relu = i + 1 < len(mods) and isinstance(mods[i + 1], nn.ReLU)
+            x = _nconv(x, m, "relu" if relu else None)
+            i += 2 if relu else 1
+            continue
+        if isinstance(m, nn.MaxPool2d):
+            x = ops.max_pool2d_nhwc(x, (m.kernel_size, m.kernel_size), (m.stride, m.stride), (m.padding, m.padding),
+                                    ceil_mode=m.ceil_mode)
+        i += 1
+    return x
+
+
+def _crelu_native(u, x):
+    y = _nconv(x, u.conv)
+    z = torch.cat([y, -y], -1)
+    bn = u.bn
+    return ops.batch_norm_nhwc(z.contiguous(), bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.eps,
+                               bn.momentum if bn.momentum is not None else 0.1, relu=True,
+                               training=bn.training)
+
+
+def _seq_native(seq, x):
+    """nn.Sequential of Conv2d / ReLU / MaxPool2d on NHWC (inception branches)."""
+    return _vgg_native(seq, x)
+
+
+def _inception_native(u, x):
+    ys = [_seq_native(u.b1, x), _seq_native(u.b3, x), _seq_native(u.b5, x), _seq_native(u.bp, x)]
+    y = torch.cat(ys, -1)
+    return y + (x if u.proj is None else _nconv(x, u.proj))
+
+
+def _pvanet_native(net, x):
+    from zoo.ops.layers import resize_bilinear
+    x = _crelu_native(net.stem[0], x)
+    x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+    for u in net.c2:
+        x = _crelu_native(u, x)
+    c3 = x
+    for u in net.c3:
+        c3 = _crelu_native(u, c3)
+    c4 = c3
+    for u in net.c4:
+        c4 = _inception_native(u, c4)
+    c5 = c4
+    for u in net.c5:
+        c5 = _inception_native(u, c5)
+    h, w = c4.shape[1], c4.shape[2]
+    p3 = ops.max_pool2d_nhwc(c3, (3, 3), (2, 2), (1, 1))[:, :h, :w]
+    hyper = torch.cat([p3, c4, resize_bilinear(c5.contiguous(), h, w)], -1)
+    return _nconv(hyper.contiguous(), net.fuse[0], "relu")
+
+
 class FasterRCNN(nn.Module):
     """backbone (stride 16) -> RPN -> Proposal -> RoI pooling -> fc heads.
     forward(x, im_info) -> (rois [R, 5], cls_prob [R, C], bbox_pred [R, 4C])."""
@@ -250,7 +368,34 @@ class FasterRCNN(nn.Module):
         self.cls_score = nn.Linear(fc, num_classes)
         self.bbox_pred = nn.Linear(fc, 4 * num_classes)
 
+    def features_nhwc(self, x):
+        """GPU backbone: NCHW fp32 image -> NHWC bf16 stride-16 features (native kernels)."""
+        xn = ops.native().nchw_to_nhwc(x.float().contiguous(), 4)        # 3 -> 4 channels, bf16
+        if isinstance(self.features, nn.Sequential):
+            return _vgg_native(self.features, xn)
+        return _pvanet_native(self.features, xn)
+
+    def _forward_native(self, x, im_info):
+        f = self.features_nhwc(x)
+        r = _nconv(f, self.rpn_conv, "relu")
+        s = _nconv(r, self.rpn_cls)                                       # [B, H, W, 2A]
+        B, H, W, twoA = s.shape
+        A = twoA // 2
+        from zoo.ops.nn import softmax
+        prob = softmax(s.float().reshape(B, H, W, 2, A), dim=3).reshape(B, H, W, twoA)
+        deltas = _nconv(r, self.rpn_bbox).float()
+        rois = self.proposal(prob.permute(0, 3, 1, 2), deltas.permute(0, 3, 1, 2), im_info)
+        pooled = roi_pool_nhwc(f, rois, self.pooled)                      # [R, P, P, C]
+        pooled = pooled.permute(0, 3, 1, 2).flatten(1)                    # the fc6 weight's (C, P, P) order
+        h = ops.linear(pooled, self.fc6.weight, self.fc6.bias, act="relu")
+        h = ops.linear(h, self.fc7.weight, self.fc7.bias, act="relu")
+        cls = softmax(ops.linear(h, self.cls_score.weight, self.cls_score.bias).float(), -1)
+        box = ops.linear(h, self.bbox_pred.weight, self.bbox_pred.bias).float()
+        return rois, cls, box
+
     def forward(self, x, im_info):
+        if x.is_cuda:
+            return self._forward_native(x, im_info)
         f = self.features(x)
         r = F.relu(self.rpn_conv(f))
         s = self.rpn_cls(r)

@@ -195,7 +195,9 @@ def conv2d_nhwc(x, w, bias=None, kernel=(1, 1), stride=(1, 1), pad=(0, 0), dil=(
     return y if out_f32 or x.dtype == torch.float32 else y.to(x.dtype)
 
 
-_BLAS_LINEAR = os.environ.get("ZOO_LINEAR_BLAS", "1") != "0"
+# hipBLASLt for transformer-size linears is an opt-in comparator since round 3 (ZOO_LINEAR_BLAS=1);
+# by default they run on the hand-written MFMA GEMMs (_LinearNativeFn)
+_BLAS_LINEAR = os.environ.get("ZOO_LINEAR_BLAS", "0") == "1"
 
 
 class _LinearBlasFn(torch.autograd.Function):
@@ -296,6 +298,87 @@ class _LinearBlasFn(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
+class _LinearNativeFn(torch.autograd.Function):
+    """Transformer-size linear on the hand-written MFMA kernels (igemm / igemm2, zoo._C):
+
+      forward   y = act(x W^T + b): GEMM with the bias (+ReLU) epilogue; GELU keeps its bf16
+                pre-activation and applies the native GELU pass (its backward needs it)
+      backward  one native pass computes the activation backward and the fp32 bias-gradient
+                column sums (straight into the engine's flat gradient); dX = dY W on the GEMM
+                with the residual gradient (GradAdd) added in its epilogue; W^T is the cached
+                1x1 "flipped" weight (refreshed in the batched flip launch after each update);
+                dW += dY^T X on the 256x256 LDS-DMA weight-gradient kernel into the flat grad.
+    Reference: TransformerLayer.scala:120-181 / BERT.scala Dense layers."""
+
+    @staticmethod
+    def forward(ctx, x2, w, bias, act, need_grad, grad_add=None):
+        ctx.grad_add = grad_add
+        if grad_add is not None and need_grad:
+            grad_add.armed = True
+        N, K = w.shape
+        wb = bf16_weight(w)
+        bf = None if bias is None else bias.detach().float().contiguous()
+        x4 = x2.view(x2.shape[0], 1, 1, K)
+        pre = None
+        if act == "gelu" and need_grad:
+            pre = _kern.conv_fwd(x4, wb, 1, 1, bias=bf).view(-1, N)
+            y = native().act_fwd_bwd(pre, None, 4, 0.0)
+        else:
+            y = _kern.conv_fwd(x4, wb, 1, 1, bias=bf, act=ACT_CODES[act]).view(-1, N)
+        ctx.save_for_backward(x2, w, y if act == "relu" else None, pre)
+        ctx.act, ctx.has_bias, ctx.bias_ref = act, bias is not None, bias
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, w, y, pre = ctx.saved_tensors
+        dy = dy.to(torch.bfloat16).contiguous()
+        N, K = w.shape
+        dx = dw = db = None
+        if (ctx.has_bias and ctx.needs_input_grad[2]) or ctx.act in ("relu", "gelu"):
+            bias = ctx.bias_ref
+            want_db = bool(ctx.has_bias and ctx.needs_input_grad[2])
+            bbuf = getattr(bias, "_zoo_grad", None) if (want_db and bias is not None) else None
+            z = y if ctx.act == "relu" else (pre if ctx.act == "gelu" else None)
+            outs = native().act_bwd_reduce(dy, z, want_db, bbuf, ctx.act == "gelu")
+            dy = outs[0]
+            if want_db:
+                if bbuf is not None:
+                    hook = getattr(bias, "_zoo_grad_ready", None)
+                    if hook is not None:
+                        hook(bias)
+                else:
+                    db = outs[1].to(bias.dtype)
+        ga = ctx.grad_add
+        resid = None
+        if ga is not None and ga.grad is not None:
+            resid = ga.grad.reshape(dy.shape[0], K).to(torch.bfloat16).contiguous()
+            ga.grad, ga.armed = None, False
+        if ctx.needs_input_grad[0]:
+            wt = _kern.flip_weights(bf16_weight(w), N, 1, 1, K)       # W^T [K, ceil8(N)]
+            dx = _kern.conv_fwd(dy.view(-1, 1, 1, N), wt, 1, 1,
+                                resid=None if resid is None else resid.view(-1, 1, 1, K)).view(-1, K)
+        elif resid is not None:
+            dx = resid
+        if ctx.needs_input_grad[1]:
+            gbuf = getattr(w, "_zoo_grad", None)
+            g2 = gbuf.view(N, K) if gbuf is not None else torch.zeros(N, K, device=dy.device, dtype=torch.float32)
+            native().linear_wgrad(dy, x2, g2)
+            if gbuf is not None:
+                hook = getattr(w, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(w)
+            else:
+                dw = g2.to(w.dtype)
+        return dx, dw, db, None, None, None
+
+
+def _use_native_linear(x, Cin, K, act):
+    M = x.numel() // max(Cin, 1)
+    return M >= 1024 and Cin >= 256 and K >= 256 and Cin % 8 == 0 and K % 8 == 0 and \
+        act in (None, "linear", "relu", "gelu")
+
+
 _ADDMM_DTYPE_OK = [True]
 _WGRAD256 = os.environ.get("ZOO_WGRAD256", "1") != "0"
 
@@ -364,6 +447,13 @@ def linear(x, w, bias=None, act=None, grad_add=None):
         need_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or
                                                   (bias is not None and bias.requires_grad))
         y = _LinearBlasFn.apply(xb, w, bias, None if act == "linear" else act, need_grad, grad_add)
+        return y.reshape(*lead, K).to(x.dtype)
+    if x.is_cuda and w.shape[1] == Cin and x.shape[-1] == Cin and _use_native_linear(x, Cin, K, act):
+        xb = x.reshape(-1, Cin)
+        xb = (xb if xb.dtype == torch.bfloat16 else xb.to(torch.bfloat16)).contiguous()
+        need_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or
+                                                  (bias is not None and bias.requires_grad))
+        y = _LinearNativeFn.apply(xb, w, bias, None if act == "linear" else act, need_grad, grad_add)
         return y.reshape(*lead, K).to(x.dtype)
     if x.is_cuda and Cin % 8 == 0 and K % 8 == 0 and w.shape[1] == Cin:
         x2 = x.reshape(-1, 1, 1, Cin)

@@ -28,10 +28,14 @@ def test_bbox_transform_zero_deltas_is_identity():
 
 def test_roi_pool_is_max_over_bins():
     f = torch.arange(2 * 3 * 8 * 8, dtype=torch.float32).reshape(2, 3, 8, 8)
-    rois = torch.tensor([[1.0, 0.0, 0.0, 63.0, 63.0]])  # whole map at scale 1/8
+    rois = torch.tensor([[1.0, 0.0, 0.0, 56.0, 56.0]])  # whole 8x8 map at scale 1/8 (round(56/8) = 7)
     out = roi_pool(f, rois, pooled=2, spatial_scale=1 / 8)
     exp = torch.nn.functional.adaptive_max_pool2d(f[1:2], 2)[0]
     torch.testing.assert_close(out[0], exp)
+    # BigDL / Caffe bins: roi 0..8 (9 wide, past the map) -> bin 0 = [0, 5), bin 1 = [4, 9) clipped to 8
+    out = roi_pool(f, torch.tensor([[0.0, 0.0, 0.0, 63.0, 63.0]]), pooled=2, spatial_scale=1 / 8)
+    torch.testing.assert_close(out[0, :, 0, 0], f[0, :, :5, :5].amax((1, 2)))
+    torch.testing.assert_close(out[0, :, 1, 1], f[0, :, 4:, 4:].amax((1, 2)))
 
 
 def test_proposal_and_detection_output():
@@ -94,6 +98,57 @@ def test_native_nms_matches_cpu(gpu, n):
     assert got.cpu().tolist() == ref.tolist()
     got5 = nms(b.to(gpu), s.to(gpu), 0.5, n, max_keep=5)
     assert got5.cpu().tolist() == ref[:5].tolist()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
+def test_native_roi_pool_matches_reference(gpu, dt):
+    from zoo.models.image.objectdetection.frcnn import roi_pool_nhwc
+    torch.manual_seed(0)
+    f = torch.randn(2, 16, 24, 40)
+    rois = torch.tensor([[0, 0, 0, 300, 200], [1, 40, 30, 120, 90], [1, -20, 5, 700, 400], [0, 64, 64, 64, 64],
+                         [1, 100.4, 20.6, 180.2, 150.9]], dtype=torch.float32)
+    ref = roi_pool(f.to(dt).float(), rois, pooled=7, spatial_scale=1 / 16)
+    fn = f.to(dt).permute(0, 2, 3, 1).contiguous().to(gpu).requires_grad_(True)
+    out = roi_pool_nhwc(fn, rois.to(gpu), 7, 1 / 16)
+    torch.testing.assert_close(out.float().permute(0, 3, 1, 2).cpu(), ref, rtol=0, atol=0)
+    # backward: gradient routed to each bin's argmax (summed where RoIs overlap)
+    fr = f.to(dt).float().clone().requires_grad_(True)
+    dy = torch.randn(5, 16, 7, 7)
+    roi_pool(fr, rois, pooled=7, spatial_scale=1 / 16).backward(dy)
+    out.backward(dy.permute(0, 2, 3, 1).to(gpu).to(out.dtype))
+    torch.testing.assert_close(fn.grad.float().permute(0, 3, 1, 2).cpu(), fr.grad, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backbone", ["vgg16", "pvanet"])
+def test_frcnn_native_backbone_and_heads(gpu, backbone):
+    """The GPU path (native NHWC convs, pools, C.ReLU BN, resize, RoI pool, fc heads) against
+    the fp32 torch reference of the same weights; no MIOpen / hipBLASLt kernel runs."""
+    from torch.profiler import ProfilerActivity, profile
+    from zoo.models.image.objectdetection.frcnn import FasterRCNN
+    torch.manual_seed(0)
+    m = FasterRCNN(num_classes=21, backbone=backbone, pre_nms_topn=600, post_nms_topn=50).eval()
+    for mod in m.modules():       # keep activations O(1) through the deep stack
+        if isinstance(mod, torch.nn.Conv2d):
+            torch.nn.init.normal_(mod.weight, 0, (2.0 / (mod.in_channels * mod.kernel_size[0] ** 2)) ** 0.5)
+    x = torch.randn(1, 3, 224, 320)
+    with torch.no_grad():
+        ref = m.features(x)
+        g = m.to(gpu)
+        with profile(activities=[ProfilerActivity.CUDA]) as prof:
+            f = g.features_nhwc(x.to(gpu))
+            rois, cls, box = g(x.to(gpu), torch.tensor([[224.0, 320.0, 1.0]], device=gpu))
+            torch.cuda.synchronize()
+    out = f.float().permute(0, 3, 1, 2).cpu()
+    assert out.shape == ref.shape
+    assert ((out - ref).norm() / ref.norm()).item() < 3e-2
+    assert rois.shape[1] == 5 and cls.shape == (rois.shape[0], 21) and box.shape == (rois.shape[0], 84)
+    assert torch.allclose(cls.sum(-1), torch.ones_like(cls.sum(-1)), atol=1e-3)
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    bad = sorted({n for n in names if any(b in n for b in ("MIOpen", "miopen", "naive_conv", "Cijk_"))})
+    assert not bad, bad[:5]
+    assert any("roi_pool" in n for n in names)
 
 
 @pytest.mark.gpu

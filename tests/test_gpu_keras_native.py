@@ -102,5 +102,6 @@ def test_keras_layer_native_fwd_bwd(gpu, name):
     bad = sorted({n for n in names if any(b in n for b in BANNED)})
     assert not bad, bad[:5]
     if name.startswith("BatchNormalization"):
-        assert torch.allclose(g.running_mean.cpu(), cpu.running_mean, atol=1e-4)
-        assert torch.allclose(g.running_var.cpu(), cpu.running_var, rtol=1e-3, atol=1e-4)
+        # batch statistics of the bf16 activations: agree to bf16 resolution
+        assert torch.allclose(g.running_mean.cpu(), cpu.running_mean, atol=2e-3)
+        assert torch.allclose(g.running_var.cpu(), cpu.running_var, rtol=1e-2, atol=2e-3)

@@ -622,20 +622,35 @@ def test_engine_hipgraph_matches_eager(gpu):
     assert rel(p1, p0) < 1e-3
 
 
+@pytest.mark.parametrize("path", ["native", "blas"])
 @pytest.mark.parametrize("act", [None, "relu", "gelu"])
-def test_linear_blas_path_fwd_bwd(gpu, act):
-    """Transformer-size linear layers (hipBLASLt bf16 path): forward and the three
-    gradients vs fp32 autograd on bf16-rounded operands."""
+def test_linear_transformer_path_fwd_bwd(gpu, act, path, monkeypatch):
+    """Transformer-size linear layers: the hand-written MFMA path (default since round 3) and
+    the opt-in hipBLASLt comparator -- forward, the three gradients and a residual gradient
+    folded into the data-gradient GEMM, vs fp32 autograd on bf16-rounded operands. The native
+    path must run no hipBLASLt (Cijk_*) kernel."""
+    from torch.profiler import ProfilerActivity, profile
+    from zoo.ops import conv as conv_mod
     from zoo.ops import linear
-    from zoo.ops.conv import _use_blas
+    from zoo.ops.nn import GradAdd
+    monkeypatch.setattr(conv_mod, "_BLAS_LINEAR", path == "blas")
     torch.manual_seed(0)
     x = _bf(torch.randn(2048, 256, device=gpu)).requires_grad_(True)
     w = _bf(torch.randn(512, 256, device=gpu) * 0.05).requires_grad_(True)
     b = torch.randn(512, device=gpu).requires_grad_(True)
-    assert _use_blas(x, 256, 512, act)
-    y = linear(x.bfloat16(), w, b, act=act).float()
-    dy = torch.randn_like(y)
-    y.backward(dy)
+    if path == "blas":
+        assert conv_mod._use_blas(x, 256, 512, act)
+    else:
+        assert conv_mod._use_native_linear(x, 256, 512, act) and not conv_mod._use_blas(x, 256, 512, act)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        y = linear(x.bfloat16(), w, b, act=act).float()
+        dy = torch.randn_like(y)
+        y.backward(dy)
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    if path == "native":
+        assert not [n for n in names if "Cijk_" in n], "hipBLASLt kernel on the native linear path"
+        assert any("igemm" in n for n in names) and any("wgrad256" in n for n in names)
     xr, wr, br = (t.detach().clone().requires_grad_(True) for t in (x, w, b))
     yr = xr @ wr.t() + br
     if act == "relu":  # the ReLU mask of the bf16 output (entries at ~0 may round either way)
@@ -645,6 +660,25 @@ def test_linear_blas_path_fwd_bwd(gpu, act):
     yr.backward(dy)
     assert rel(y, yr) < 2e-2
     assert rel(x.grad, xr.grad) < 3e-2 and rel(w.grad, wr.grad) < 3e-2 and rel(b.grad, br.grad) < 3e-2
+
+
+def test_linear_native_residual_gradient_in_dgrad_epilogue(gpu):
+    """GradAdd: the residual consumer's gradient of x is added inside the dX GEMM epilogue."""
+    from zoo.ops import linear
+    from zoo.ops.nn import GradAdd, dropout_add
+    torch.manual_seed(1)
+    x = _bf(torch.randn(16384, 256, device=gpu)).requires_grad_(True)
+    w = _bf(torch.randn(256, 256, device=gpu) * 0.05).requires_grad_(True)
+    ga = GradAdd()
+    h = linear(x.bfloat16(), w, None, grad_add=ga)
+    # out = dropout(h) + x with a vanishing drop rate: the fused dropout-add hands the residual
+    # gradient of x to the armed linear (4M elements: the fused path's size threshold)
+    out = dropout_add(h, x.bfloat16(), 1e-7, training=True, grad_add=ga)
+    dy = torch.randn_like(out.float())
+    out.float().backward(dy)
+    xr, wr = x.detach().clone().requires_grad_(True), w.detach().clone().requires_grad_(True)
+    (xr @ wr.t() + xr).backward(dy)
+    assert rel(x.grad, xr.grad) < 3e-2 and rel(w.grad, wr.grad) < 3e-2
 
 
 def test_engine_phase_timing_and_roctx_on_gpu(gpu):
