@@ -126,9 +126,12 @@ __global__ void wlrn_bwd2_kernel(const T* __restrict__ x, const T* __restrict__ 
 }
 
 // ---------------------------------------------------------------- bilinear resize (NHWC)
-// BigDL / TF-legacy sampling: src = dst * scale, scale = in/out or (in-1)/(out-1) (align_corners)
-ZOO_DEV void lerp_idx(int o, int in, float scale, int& lo, int& hi, float& f) {
-  const float s = o * scale;
+// BigDL / TF-legacy sampling: src = dst * scale, scale = in/out or (in-1)/(out-1) (align_corners);
+// half-pixel mode (off = 0.5 * scale - 0.5, PyTorch align_corners=False / Caffe bilinear
+// deconvolution upsampling): src = max((dst + 0.5) * scale - 0.5, 0)
+ZOO_DEV void lerp_idx(int o, int in, float scale, float off, int& lo, int& hi, float& f) {
+  float s = o * scale + off;
+  s = s < 0.f ? 0.f : s;
   lo = (int)floorf(s);
   lo = lo < in - 1 ? lo : in - 1;
   hi = lo + 1 < in ? lo + 1 : in - 1;
@@ -138,7 +141,7 @@ ZOO_DEV void lerp_idx(int o, int in, float scale, int& lo, int& hi, float& f) {
 
 template <typename T>
 __global__ void resize_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, int N, int H, int W, int C, int OH,
-                                  int OW, float sh, float sw) {
+                                  int OW, float sh, float sw, float oh_off, float ow_off) {
   const size_t n = (size_t)N * OH * OW * C;
   GRID_STRIDE(i, n) {
     const int c = (int)(i % C);
@@ -149,8 +152,8 @@ __global__ void resize_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, in
     const size_t b = t / OH;
     int h0, h1, w0, w1;
     float fh, fw;
-    lerp_idx(oh, H, sh, h0, h1, fh);
-    lerp_idx(ow, W, sw, w0, w1, fw);
+    lerp_idx(oh, H, sh, oh_off, h0, h1, fh);
+    lerp_idx(ow, W, sw, ow_off, w0, w1, fw);
     const size_t base = b * H;
     const float a = ld(x, ((base + h0) * W + w0) * C + c), bb = ld(x, ((base + h0) * W + w1) * C + c);
     const float cc = ld(x, ((base + h1) * W + w0) * C + c), d = ld(x, ((base + h1) * W + w1) * C + c);
@@ -161,7 +164,7 @@ __global__ void resize_fwd_kernel(const T* __restrict__ x, T* __restrict__ y, in
 
 template <typename T>
 __global__ void resize_bwd_kernel(const T* __restrict__ dy, float* __restrict__ dx, int N, int H, int W, int C,
-                                  int OH, int OW, float sh, float sw) {
+                                  int OH, int OW, float sh, float sw, float oh_off, float ow_off) {
   const size_t n = (size_t)N * OH * OW * C;
   GRID_STRIDE(i, n) {
     const int c = (int)(i % C);
@@ -172,8 +175,8 @@ __global__ void resize_bwd_kernel(const T* __restrict__ dy, float* __restrict__ 
     const size_t b = t / OH;
     int h0, h1, w0, w1;
     float fh, fw;
-    lerp_idx(oh, H, sh, h0, h1, fh);
-    lerp_idx(ow, W, sw, w0, w1, fw);
+    lerp_idx(oh, H, sh, oh_off, h0, h1, fh);
+    lerp_idx(ow, W, sw, ow_off, w0, w1, fw);
     const float g = ld(dy, i);
     const size_t base = b * H;
     atomicAdd(dx + ((base + h0) * W + w0) * C + c, g * (1.f - fh) * (1.f - fw));
@@ -338,24 +341,26 @@ extern "C" hipError_t zoo_wlrn(const void* x, const void* dy, void* out, float* 
 
 extern "C" hipError_t zoo_resize_bilinear(const void* in, void* out, int N, int H, int W, int C, int OH, int OW,
                                           int align, int backward, int bf16, hipStream_t st) {
-  const float sh = (align && OH > 1) ? (float)(H - 1) / (OH - 1) : (float)H / OH;
-  const float sw = (align && OW > 1) ? (float)(W - 1) / (OW - 1) : (float)W / OW;
+  // align: 0 TF-legacy (BigDL ResizeBilinear), 1 align_corners, 2 half-pixel centres
+  const float sh = (align == 1 && OH > 1) ? (float)(H - 1) / (OH - 1) : (float)H / OH;
+  const float sw = (align == 1 && OW > 1) ? (float)(W - 1) / (OW - 1) : (float)W / OW;
+  const float oh_off = align == 2 ? 0.5f * sh - 0.5f : 0.f, ow_off = align == 2 ? 0.5f * sw - 0.5f : 0.f;
   const size_t n = (size_t)N * OH * OW * C;
   const int g = grid_for(n);
   if (!backward) {
     if (bf16)
       hipLaunchKernelGGL(resize_fwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)in, (bf16_t*)out, N, H,
-                         W, C, OH, OW, sh, sw);
+                         W, C, OH, OW, sh, sw, oh_off, ow_off);
     else
       hipLaunchKernelGGL(resize_fwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)in, (float*)out, N, H, W,
-                         C, OH, OW, sh, sw);
+                         C, OH, OW, sh, sw, oh_off, ow_off);
   } else {  // in = dy [N, OH, OW, C], out = fp32 dx [N, H, W, C] (zeroed by the caller)
     if (bf16)
       hipLaunchKernelGGL(resize_bwd_kernel<bf16_t>, dim3(g), dim3(256), 0, st, (const bf16_t*)in, (float*)out, N, H,
-                         W, C, OH, OW, sh, sw);
+                         W, C, OH, OW, sh, sw, oh_off, ow_off);
     else
       hipLaunchKernelGGL(resize_bwd_kernel<float>, dim3(g), dim3(256), 0, st, (const float*)in, (float*)out, N, H, W,
-                         C, OH, OW, sh, sw);
+                         C, OH, OW, sh, sw, oh_off, ow_off);
   }
   return hipGetLastError();
 }

@@ -975,25 +975,25 @@ torch::Tensor within_lrn(torch::Tensor x, c10::optional<torch::Tensor> dy, int s
   return out;
 }
 
-// ResizeBilinear (BigDL / TF-legacy sampling) on NHWC
-torch::Tensor resize_bilinear(torch::Tensor x, int OH, int OW, bool align) {
+// bilinear resize on NHWC; align: 0 BigDL / TF-legacy, 1 align_corners, 2 half-pixel centres
+torch::Tensor resize_bilinear(torch::Tensor x, int OH, int OW, int64_t align) {
   req_act(x, "resize_bilinear");
   TORCH_CHECK(x.dim() == 4 && OH > 0 && OW > 0 && x.size(1) > 0 && x.size(2) > 0, "resize_bilinear: NHWC, sizes");
   auto y = torch::empty({x.size(0), OH, OW, x.size(3)}, x.options());
   if (y.numel() == 0) return y;
-  check_hip(zoo_resize_bilinear(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), OH, OW, align,
-                                0, x.scalar_type() == at::kBFloat16, cur_stream()),
+  check_hip(zoo_resize_bilinear(x.data_ptr(), y.data_ptr(), x.size(0), x.size(1), x.size(2), x.size(3), OH, OW,
+                                (int)align, 0, x.scalar_type() == at::kBFloat16, cur_stream()),
             "resize_bilinear");
   return y;
 }
 
-torch::Tensor resize_bilinear_bwd(torch::Tensor dy, int H, int W, bool align) {
+torch::Tensor resize_bilinear_bwd(torch::Tensor dy, int H, int W, int64_t align) {
   req_act(dy, "resize_bilinear_bwd");
   TORCH_CHECK(dy.dim() == 4 && H > 0 && W > 0, "resize_bilinear_bwd: NHWC dy");
   auto dx = torch::zeros({dy.size(0), H, W, dy.size(3)}, dy.options().dtype(at::kFloat));
   if (dy.numel() == 0) return dx.to(dy.scalar_type());
   check_hip(zoo_resize_bilinear(dy.data_ptr(), dx.data_ptr(), dy.size(0), H, W, dy.size(3), dy.size(1), dy.size(2),
-                                align, 1, dy.scalar_type() == at::kBFloat16, cur_stream()),
+                                (int)align, 1, dy.scalar_type() == at::kBFloat16, cur_stream()),
             "resize_bilinear_bwd");
   return dy.scalar_type() == at::kFloat ? dx : dx.to(dy.scalar_type());
 }

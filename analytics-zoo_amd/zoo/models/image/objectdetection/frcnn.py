@@ -115,17 +115,22 @@ def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16):
     fp32 reference of the native channels-last kernel (roi_pool_nhwc)."""
     out = features.new_zeros(rois.shape[0], features.shape[1], pooled, pooled)
     H, W = features.shape[2], features.shape[3]
-    r = torch.round(rois[:, 1:] * spatial_scale).long().tolist()
+    # C round() (half away from zero) of the fp32 scaled box, bin edges in fp32 arithmetic --
+    # exactly what Caffe's ROIPoolingLayer (and the native kernel) compute
+    v = (rois[:, 1:].float() * np.float32(spatial_scale)).cpu().numpy().astype(np.float32)
+    r = (np.sign(v) * np.floor(np.abs(v) + np.float32(0.5))).astype(np.int64).tolist()
     bidx = rois[:, 0].long().clamp(0, features.shape[0] - 1).tolist()
+    P = np.float32(pooled)
     for i in range(rois.shape[0]):
         x1, y1, x2, y2 = r[i]
         rw, rh = max(x2 - x1 + 1, 1), max(y2 - y1 + 1, 1)
+        bw, bh = np.float32(rw) / P, np.float32(rh) / P
         for ph in range(pooled):
-            hs = min(max(int(math.floor(ph * rh / pooled)) + y1, 0), H)
-            he = min(max(int(math.ceil((ph + 1) * rh / pooled)) + y1, 0), H)
+            hs = min(max(int(np.floor(np.float32(ph) * bh)) + y1, 0), H)
+            he = min(max(int(np.ceil(np.float32(ph + 1) * bh)) + y1, 0), H)
             for pw in range(pooled):
-                ws = min(max(int(math.floor(pw * rw / pooled)) + x1, 0), W)
-                we = min(max(int(math.ceil((pw + 1) * rw / pooled)) + x1, 0), W)
+                ws = min(max(int(np.floor(np.float32(pw) * bw)) + x1, 0), W)
+                we = min(max(int(np.ceil(np.float32(pw + 1) * bw)) + x1, 0), W)
                 if hs < he and ws < we:
                     out[i, :, ph, pw] = features[bidx[i], :, hs:he, ws:we].amax((1, 2))
     return out
@@ -337,7 +342,7 @@ def _pvanet_native(net, x):
         c5 = _inception_native(u, c5)
     h, w = c4.shape[1], c4.shape[2]
     p3 = ops.max_pool2d_nhwc(c3, (3, 3), (2, 2), (1, 1))[:, :h, :w]
-    hyper = torch.cat([p3, c4, resize_bilinear(c5.contiguous(), h, w)], -1)
+    hyper = torch.cat([p3, c4, resize_bilinear(c5.contiguous(), h, w, align=2)], -1)   # half-pixel
     return _nconv(hyper.contiguous(), net.fuse[0], "relu")
 
 

@@ -68,8 +68,11 @@ class _ResizeFn(torch.autograd.Function):
 
 
 def _lerp_table(o, i, align, device):
-    scale = (i - 1) / (o - 1) if (align and o > 1) else i / o
+    mode = int(align)
+    scale = (i - 1) / (o - 1) if (mode == 1 and o > 1) else i / o
     s = torch.arange(o, device=device, dtype=torch.float64) * scale
+    if mode == 2:
+        s = (s + 0.5 * scale - 0.5).clamp_min(0)
     lo = s.floor().clamp(max=i - 1).long()
     hi = (lo + 1).clamp(max=i - 1)
     f = (s - lo.double()).clamp(0, 1).float()
@@ -77,7 +80,8 @@ def _lerp_table(o, i, align, device):
 
 
 def resize_bilinear_ref(x, oh, ow, align=False):
-    """NHWC bilinear resize with BigDL / TF-legacy sampling (src = dst * scale)."""
+    """NHWC bilinear resize. ``align``: False / 0 BigDL / TF-legacy sampling (src = dst * scale),
+    True / 1 align_corners, 2 half-pixel centres (PyTorch align_corners=False)."""
     xf = x.float()
     h0, h1, fh = _lerp_table(oh, x.shape[1], align, x.device)
     w0, w1, fw = _lerp_table(ow, x.shape[2], align, x.device)
@@ -91,7 +95,7 @@ def resize_bilinear_ref(x, oh, ow, align=False):
 
 def resize_bilinear(x, oh, ow, align=False):
     if _gpu_ok(x) and x.dim() == 4:
-        return _ResizeFn.apply(x.contiguous(), int(oh), int(ow), bool(align))
+        return _ResizeFn.apply(x.contiguous(), int(oh), int(ow), int(align))
     return resize_bilinear_ref(x, oh, ow, align)
 
 

@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python -u -m pytest tests/test_frcnn.py tests/test_gpu_keras_native.py tests/test_gpu_kernels.py tests/test_gpu_igemm2.py -q --timeout 180 --timeout-method thread > gpurun_out/t_r3c.log 2>&1
+$T 900 python -u -m pytest tests/test_frcnn.py tests/test_gpu_keras_native.py tests/test_gpu_kernels.py tests/test_gpu_igemm2.py tests/test_gpu_native_nets.py -q --timeout 180 --timeout-method thread > gpurun_out/t_r3c.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" gpurun_out/t_r3c.log | tail -20
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 for i in 1 2; do

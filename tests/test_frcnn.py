@@ -171,3 +171,16 @@ def test_ssd_mobilenet_config_shapes():
     assert P == 19 * 19 * 4 + (100 + 25 + 9 + 4 + 1) * 6
     dets = d.detect_batch(np.random.rand(1, 3, 300, 300).astype(np.float32))
     assert dets[0].shape[1] == 6
+
+
+def test_half_pixel_resize_reference_matches_interpolate():
+    """resize mode 2 (PVANet hyper-feature upsampling on the GPU path) is PyTorch's
+    align_corners=False bilinear: the NHWC reference agrees with F.interpolate."""
+    import torch.nn.functional as F
+    from zoo.ops.layers import resize_bilinear_ref
+    torch.manual_seed(0)
+    x = torch.randn(2, 5, 7, 3)
+    for oh, ow in [(10, 14), (9, 4), (5, 7)]:
+        ref = F.interpolate(x.permute(0, 3, 1, 2), size=(oh, ow), mode="bilinear", align_corners=False)
+        out = resize_bilinear_ref(x, oh, ow, align=2).permute(0, 3, 1, 2)
+        torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)

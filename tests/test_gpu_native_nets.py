@@ -12,24 +12,83 @@ NETS = [("vgg-16", 224), ("alexnet", 227), ("squeezenet", 227), ("mobilenet", 22
         ("inception-v1", 224), ("inception-v3", 299), ("densenet-161", 224)]
 
 
+BANNED = ("miopen", "MIOpen", "mlo", "naive_conv", "gridwise_", "Cijk_")
+
+# per-group gradient agreement with the fp32 CPU reference of the same weights (cosine of the
+# concatenated group gradient). bf16 activations carry ~0.4 % relative noise per element; BN
+# gamma/beta gradients are batch reductions of products of two noisy terms and, in the deep
+# gamma=1 stacks (DenseNet-161, Inception-v3), sit where torch's own bf16 autocast also drifts
+# (profiles/resnet50_parity_r2.md) -> looser than the conv / fc weights.
+GROUP_COS = {"conv": 0.97, "fc": 0.98, "bn": 0.90, "dw": 0.97}
+
+
+def _group(name, p):
+    if name.endswith(("gamma", "beta")):
+        return "bn"
+    if "fc" in name or "classifier" in name:
+        return "fc"
+    if p.dim() == 2 and p.shape[0] <= 25 and "dw" in name:
+        return "dw"
+    return "conv"
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
+
+
 @pytest.mark.parametrize("name,hw", NETS)
-def test_backbone_trains_natively(gpu, name, hw):
+def test_backbone_matches_fp32_and_trains_natively(gpu, name, hw, monkeypatch):
+    """Forward logits and per-group parameter gradients of the native bf16 NHWC backbone vs the
+    same weights through the fp32 CPU reference path (plain F.conv2d / batch-norm / pooling),
+    training-mode BatchNorm, dropout disabled on both sides; the GPU trace holds zoo:: kernels
+    and no MIOpen / hipBLASLt kernel; then one engine step per net trains (finite loss)."""
+    import copy
+    from torch.profiler import ProfilerActivity, profile
     from zoo.common.nncontext import init_nncontext
+    from zoo.models.image import native_nets
     from zoo.models.image.imageclassification.nets import build
     from zoo.ops import softmax_cross_entropy
     from zoo.pipeline.api.keras.optimizers import SGD
     from zoo.pipeline.engine import TrainingEngine
     init_nncontext("nets-test")
+    monkeypatch.setattr(native_nets, "_dropout", lambda x, p, training: x)
     torch.manual_seed(0)
+    net = build(name, 16)
+    ref = copy.deepcopy(net).train()
+    g = copy.deepcopy(net).to(gpu).train()
+    x = torch.randn(2, 3, hw, hw)
+    y = torch.randint(0, 16, (2,))
+    out_r = ref(x)
+    F.cross_entropy(out_r.float(), y).backward()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        out_g = g(x.to(gpu))
+        softmax_cross_entropy(out_g, y.to(gpu)).backward()
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    assert any("zoo::" in n for n in names)
+    bad = sorted({n for n in names if any(b in n for b in BANNED)})
+    assert not bad, bad[:5]
+    rel = ((out_g.float().cpu() - out_r.float()).norm() / out_r.float().norm()).item()
+    assert rel < 0.05, ("logits", rel)
+    groups = {}
+    for (n, pr), (_, pg) in zip(ref.named_parameters(), g.named_parameters()):
+        if pr.grad is None or pr.grad.abs().max() == 0:
+            continue
+        k = _group(n, pr)
+        a, b = groups.setdefault(k, ([], []))
+        a.append(pg.grad.detach().float().cpu().flatten())
+        b.append(pr.grad.detach().float().flatten())
+    report = {k: round(_cos(torch.cat(a), torch.cat(b)), 4) for k, (a, b) in groups.items()}
+    print(name, "logits rel %.4f" % rel, report)
+    for k, c in report.items():
+        assert c >= GROUP_COS[k], (k, c, report)
+    # and the engine trains it (fused optimizer, flat buffers)
     eng = TrainingEngine(build(name, 16), softmax_cross_entropy, SGD(learningrate=0.01, momentum=0.9))
-    x = torch.randn(4, 3, hw, hw, device=gpu)
-    y = torch.randint(0, 16, (4,), device=gpu)
-    losses = [float(eng.train_step(x, y).item()) for _ in range(3)]
+    xg = torch.randn(4, 3, hw, hw, device=gpu)
+    yg = torch.randint(0, 16, (4,), device=gpu)
+    losses = [float(eng.train_step(xg, yg).item()) for _ in range(2)]
     assert all(l == l and 0 < l < 50 for l in losses), losses
-    eng.model.eval()
-    with torch.no_grad():
-        out = eng.model(x)
-    assert tuple(out.shape) == (4, 16)
 
 
 def test_mobilenet_v2_matches_fp32_reference(gpu):
