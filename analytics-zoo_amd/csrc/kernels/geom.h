@@ -55,6 +55,8 @@ struct FlipDesc {
 inline int igemm_epi(bool y, bool yf, bool bias, bool resid, int act, bool omap, bool bsums, bool stats) {
   if (y && !yf && !bias && !resid && act == 0 && !omap && !bsums) return 1;
   if (y && !yf && !bias && act == 0 && !stats) return 2;
+  // bf16 output with bias and / or ReLU / GELU only (transformer / MLP linears)
+  if (y && !yf && !resid && !omap && !bsums && !stats && (act == 0 || act == 1 || act == 2)) return 3;
   return 0;
 }
 

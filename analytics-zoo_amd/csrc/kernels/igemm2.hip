@@ -33,7 +33,8 @@
 // patch and leave as row-contiguous 16-byte stores, with the same fusions as igemm.hip:
 // EPI 1 = plain conv + BN statistics (the forward of every conv->BN unit), EPI 2 = backward
 // (residual-gradient add, producer ReLU mask, fused BN-backward sums, strided output remap),
-// EPI 0 = general (bias, activation, residual, fp32 output, statistics, remap).
+// EPI 0 = general (bias, activation, residual, fp32 output, statistics, remap);
+// EPI 3 = bf16 output + bias + none / ReLU / GELU (the transformer linears' forward).
 //
 // Reference parity: the MKL-DNN convolution / inner-product primitives behind BigDL
 // SpatialConvolution and Linear (Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110,
@@ -228,13 +229,13 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
   float bsv[8], mu[8], iv[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) { bsv[e] = 0.f; mu[e] = 0.f; iv[e] = 0.f; }
-  if constexpr (EPI == 0) {
+  if constexpr (EPI == 0 || EPI == 3) {
     if (bias && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) bsv[e] = bias[col0 + e];
     }
   }
-  if constexpr (EPI != 1) {
+  if constexpr (EPI == 0 || EPI == 2) {
     if (bs.sums && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
@@ -262,14 +263,26 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
       if (m >= g.M || !col_ok) continue;
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       size_t off;
-      if (EPI != 1 && g.omap) {
+      if (EPI != 1 && EPI != 3 && g.omap) {
         const int n = m / PQ, pq = m - n * PQ;
         const int p = pq / g.Q, q = pq - p * g.Q;
         off = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
       } else {
         off = (size_t)m * g.K + col0;
       }
-      if constexpr (EPI == 1) {
+      if constexpr (EPI == 3) {
+        // lean bias / activation epilogue: the activation branch is per 8-column piece
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += bsv[e];
+        if (act == ACT_RELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (act == ACT_GELU) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+        }
+        *reinterpret_cast<uint4*>(Y + off) = pack8(v);
+      } else if constexpr (EPI == 1) {
         const uint4 pk = pack8(v);
         *reinterpret_cast<uint4*>(Y + off) = pk;
         if (want_stats) {
@@ -347,7 +360,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   }
 
-  if (!want_stats) return;
+  if (EPI == 3 || !want_stats) return;
   // per-column sums: lanes sharing `ch` differ in bits >= log2(CPR); fold them, then the wave
   // rows of the block through LDS, then one store / atomic per column per block
 #pragma unroll
@@ -443,6 +456,7 @@ static hipError_t i2_epi(int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, f
                          hipStream_t st) {
   if (epi == 1) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   if (epi == 2) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 2>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (epi == 3) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 3>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 0>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
 }
 

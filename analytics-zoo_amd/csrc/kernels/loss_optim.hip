@@ -62,6 +62,42 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const T* __restrict__
   }
 }
 
+// NLL of probabilities (ClassNLLCriterion with log_prob_as_input = false, Zs ClassNLLCriterion /
+// keras SparseCategoricalCrossEntropy): loss_i = -log(clamp(p[i, y_i], eps, 1)); one thread per
+// row, wave-reduced sums. dp (optional, unscaled) = -1 / p at the label where eps <= p <= 1
+// (torch.clamp's pass-through band), 0 elsewhere -- the caller scales it by dloss / count.
+template <typename T>
+__global__ __launch_bounds__(256) void prob_nll_kernel(const T* __restrict__ probs, const int64_t* __restrict__ labels,
+                                                       float* __restrict__ loss_sum, float* __restrict__ count,
+                                                       float* __restrict__ dp, int B, int NC, float eps,
+                                                       int ignore_index, int per_row) {
+  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  float l = 0.f, c = 0.f;
+  if (row < B) {
+    const int64_t lab = labels[row];
+    const bool valid = lab != ignore_index && lab >= 0 && lab < NC;
+    const float p = valid ? ld(probs + (size_t)row * NC, (int)lab) : 1.f;
+    const float pc = fminf(fmaxf(p, eps), 1.f);
+    l = valid ? -__logf(pc) : 0.f;
+    c = valid ? 1.f : 0.f;
+    if (dp) {
+      const bool pass = valid && p >= eps && p <= 1.f;
+      for (int j = 0; j < NC; ++j) dp[(size_t)row * NC + j] = (pass && j == lab) ? -1.f / pc : 0.f;
+    }
+    if (per_row) {
+      loss_sum[row] = l;
+      count[row] = c;
+    }
+  }
+  if (per_row) return;
+  l = warp_sum(l);
+  c = warp_sum(c);
+  if ((threadIdx.x & 63) == 0 && c > 0.f) {
+    atomicAdd(loss_sum, l);
+    atomicAdd(count, c);
+  }
+}
+
 // ---------------- optimizers over flat buffers ----------------
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ pbf, size_t n,
@@ -259,6 +295,18 @@ extern "C" hipError_t zoo_softmax_xent(const void* logits, int is_f32, const int
   else
     hipLaunchKernelGGL(softmax_xent_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)logits, labels,
                        loss_sum, count, (bf16_t*)dlogits, B, NC, grad_scale, ignore_index, per_row);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_prob_nll(const void* probs, int is_f32, const int64_t* labels, float* loss_sum, float* count,
+                                   float* dp, int B, int NC, float eps, int ignore_index, int per_row, hipStream_t st) {
+  const int blocks = (B + 255) / 256;
+  if (is_f32)
+    hipLaunchKernelGGL(prob_nll_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)probs, labels, loss_sum,
+                       count, dp, B, NC, eps, ignore_index, per_row);
+  else
+    hipLaunchKernelGGL(prob_nll_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)probs, labels,
+                       loss_sum, count, dp, B, NC, eps, ignore_index, per_row);
   return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 
 #include "kernels/geom.h"
+#include "kernels/ncf.h"
 
 using zoo::ConvGeom;
 using zoo::WgradGeom;
@@ -17,6 +18,11 @@ using zoo::BwdStats;
 using zoo::GemmGeom;
 
 extern "C" {
+hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
+                        hipStream_t);
+int zoo_ncf_tier(int, int, int, int, int, int, int);
+int zoo_ncf_nwg(int, int, int, int, int, int, int);
+hipError_t zoo_ncf(const zoo::NcfArgs*, float* const*, int, hipStream_t);
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
                      const zoo::BwdStats*, hipStream_t);
 int zoo_igemm2_bm(const ConvGeom*, int);
@@ -1145,6 +1151,30 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
   return {loss};
 }
 
+// NLL of probabilities [B, NC] against int64 labels: {loss_sum, count} (+ unscaled dprobs)
+std::vector<torch::Tensor> prob_nll(torch::Tensor probs, torch::Tensor labels, bool want_grad, double eps,
+                                    int64_t ignore_index) {
+  TORCH_CHECK(probs.is_cuda() && probs.is_contiguous() && probs.dim() == 2, "prob_nll: 2-D GPU probabilities");
+  TORCH_CHECK(probs.scalar_type() == at::kFloat || probs.scalar_type() == at::kBFloat16, "prob_nll: dtype");
+  req(labels, at::kLong, "labels");
+  TORCH_CHECK(labels.numel() == probs.size(0) && probs.size(0) < (1LL << 31), "prob_nll: labels size");
+  const int B = probs.size(0), NC = probs.size(1);
+  const bool per_row = g_deterministic;
+  auto loss = per_row ? torch::empty({2, B}, probs.options().dtype(at::kFloat))
+                      : torch::zeros({2}, probs.options().dtype(at::kFloat));
+  torch::Tensor dp;
+  if (want_grad) dp = torch::empty({B, NC}, probs.options().dtype(at::kFloat));
+  if (B > 0)
+    check_hip(zoo_prob_nll(probs.data_ptr(), probs.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                           loss.data_ptr<float>(), loss.data_ptr<float>() + (per_row ? B : 1),
+                           want_grad ? dp.data_ptr<float>() : nullptr, B, NC, (float)eps, (int)ignore_index,
+                           per_row ? 1 : 0, cur_stream()),
+              "prob_nll");
+  if (per_row) loss = loss.sum(1);
+  if (want_grad) return {loss, dp};
+  return {loss};
+}
+
 void check_flat(const torch::Tensor& t, const char* n, int64_t numel) {
   req(t, at::kFloat, n);
   TORCH_CHECK(t.numel() == numel, n, " numel mismatch");
@@ -2041,6 +2071,101 @@ std::vector<torch::Tensor> rnn_bwd(c10::optional<torch::Tensor> dhseq, c10::opti
 
 }  // namespace
 
+
+// Fused NeuralCF forward / backward (kernels/ncf.hip).
+//   t    = [tu, ti, tmu, tmi, w1, b1, w2, b2, w3, b3, wo, bo]   (empty tensor = absent)
+//   dims = [eu, ei, em, h1, h2, h3, nc, id_off]
+// forward (dprobs absent): returns probs [B, nc] fp32. backward: gradients are ADDED into
+//   g = [gtu, gti, gtmu, gtmi, gw1, gb1, gw2, gb2, gw3, gb3, gwo, gbo] (fp32, empty = skip).
+static bool has(const torch::Tensor& t) { return t.defined() && t.numel() > 0; }
+
+static void ncf_req_w(const torch::Tensor& w, int64_t r, int64_t c, const char* what) {
+  req(w, at::kFloat, what);
+  TORCH_CHECK(w.numel() == r * c && (c == 1 || (w.dim() == 2 && w.size(0) == r && w.size(1) == c)), "ncf: ", what,
+              " shape");
+}
+
+int64_t ncf_tier(std::vector<int64_t> d) {
+  TORCH_CHECK(d.size() >= 7, "ncf_tier: dims");
+  return zoo_ncf_tier(d[0], d[1], d[2], d[3], d[4], d[5], d[6]);
+}
+
+torch::Tensor ncf_fused(torch::Tensor ids, std::vector<torch::Tensor> t, std::vector<int64_t> dims,
+                        c10::optional<torch::Tensor> dprobs, std::vector<torch::Tensor> g) {
+  TORCH_CHECK(t.size() == 12 && dims.size() == 8, "ncf: 12 tensors, 8 dims");
+  req(ids, at::kLong, "ncf ids");
+  TORCH_CHECK(ids.dim() == 2 && ids.size(1) == 2 && ids.size(0) > 0 && ids.size(0) < (1LL << 31), "ncf: ids [B, 2]");
+  const int eu = dims[0], ei = dims[1], em = dims[2], h1 = dims[3], h2 = dims[4], h3 = dims[5], nc = dims[6];
+  TORCH_CHECK(zoo_ncf_tier(eu, ei, em, h1, h2, h3, nc) >= 0, "ncf: unsupported widths");
+  const auto& tu = t[0];
+  const auto& ti = t[1];
+  TORCH_CHECK(tu.is_cuda() && (tu.scalar_type() == at::kBFloat16 || tu.scalar_type() == at::kFloat),
+              "ncf: tables fp32 / bf16 on the GPU");
+  const auto tdt = tu.scalar_type();
+  const int align = tdt == at::kFloat ? 16 : 8;
+  auto tab = [&](const torch::Tensor& x, int64_t rows, int e, const char* what) {
+    req(x, tdt, what);
+    TORCH_CHECK(x.dim() == 2 && x.size(1) == e && (rows < 0 || x.size(0) == rows) && x.size(0) < (1LL << 31),
+                "ncf: ", what, " shape");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % align == 0, "ncf: ", what, " alignment");
+  };
+  tab(tu, -1, eu, "user table");
+  tab(ti, -1, ei, "item table");
+  if (em > 0) {
+    tab(t[2], tu.size(0), em, "mf user table");
+    tab(t[3], ti.size(0), em, "mf item table");
+  }
+  ncf_req_w(t[4], h1, eu + ei, "w1");
+  ncf_req_w(t[6], h2, h1, "w2");
+  ncf_req_w(t[8], h3, h2, "w3");
+  ncf_req_w(t[10], nc, h3 + em, "wo");
+  const int hb[4] = {h1, h2, h3, nc};
+  for (int i = 0; i < 4; ++i)
+    if (has(t[5 + 2 * i])) ncf_req_w(t[5 + 2 * i], hb[i], 1, "bias");
+  zoo::NcfArgs a{};
+  a.ids = ids.data_ptr<int64_t>();
+  a.B = ids.size(0);
+  a.id_off = dims[7];
+  a.tu = tu.data_ptr();
+  a.ti = ti.data_ptr();
+  a.tmu = em > 0 ? t[2].data_ptr() : nullptr;
+  a.tmi = em > 0 ? t[3].data_ptr() : nullptr;
+  a.Vu = tu.size(0);
+  a.Vi = ti.size(0);
+  a.eu = eu; a.ei = ei; a.em = em; a.h1 = h1; a.h2 = h2; a.h3 = h3; a.nc = nc;
+  auto fp = [&](int i) -> const float* { return has(t[i]) ? t[i].data_ptr<float>() : nullptr; };
+  a.w1 = fp(4); a.b1 = fp(5); a.w2 = fp(6); a.b2 = fp(7); a.w3 = fp(8); a.b3 = fp(9); a.wo = fp(10); a.bo = fp(11);
+  a.nwg = zoo_ncf_nwg(eu, ei, em, h1, h2, h3, nc);
+  const int bf16 = tdt == at::kBFloat16;
+  if (!dprobs.has_value() || !dprobs->defined()) {
+    auto probs = torch::empty({a.B, nc}, ids.options().dtype(at::kFloat));
+    a.probs = probs.data_ptr<float>();
+    check_hip(zoo_ncf(&a, nullptr, bf16, cur_stream()), "ncf_fwd");
+    return probs;
+  }
+  req(*dprobs, at::kFloat, "ncf dprobs");
+  TORCH_CHECK(dprobs->dim() == 2 && dprobs->size(0) == a.B && dprobs->size(1) == nc, "ncf: dprobs [B, nc]");
+  a.dprobs = dprobs->data_ptr<float>();
+  TORCH_CHECK(g.size() == 12, "ncf: 12 gradient slots");
+  auto gp = [&](int i, int64_t n) -> float* {
+    if (!has(g[i])) return nullptr;
+    req(g[i], at::kFloat, "ncf grad");
+    TORCH_CHECK(g[i].numel() == n, "ncf: gradient ", i, " has ", g[i].numel(), " elements, expected ", n);
+    return g[i].data_ptr<float>();
+  };
+  a.gtu = gp(0, tu.numel());
+  a.gti = gp(1, ti.numel());
+  a.gtmu = em > 0 ? gp(2, t[2].numel()) : nullptr;
+  a.gtmi = em > 0 ? gp(3, t[3].numel()) : nullptr;
+  float* dst[8] = {gp(4, (int64_t)h1 * (eu + ei)), gp(5, h1), gp(6, (int64_t)h2 * h1), gp(7, h2),
+                   gp(8, (int64_t)h3 * h2), gp(9, h3), gp(10, (int64_t)nc * (h3 + em)), gp(11, nc)};
+  const int grid = (a.B + 255) / 256;
+  auto partial = torch::empty({grid, a.nwg}, ids.options().dtype(at::kFloat));
+  a.partial = partial.data_ptr<float>();
+  check_hip(zoo_ncf(&a, dst, bf16, cur_stream()), "ncf_bwd");
+  return partial;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "zoo native gfx950 (MI355X) kernel library";
   m.def("resize_normalize", &resize_normalize);
@@ -2076,6 +2201,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("within_lrn", &within_lrn);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);
+  m.def("ncf_fused", &ncf_fused);
+  m.def("prob_nll", &prob_nll);
+  m.def("ncf_tier", &ncf_tier);
   m.def("resize_bilinear", &resize_bilinear);
   m.def("resize_bilinear_bwd", &resize_bilinear_bwd);
   m.def("upsample_nd", &upsample_nd);

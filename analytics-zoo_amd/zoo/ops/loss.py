@@ -34,3 +34,30 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
     if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16):
         return _SoftmaxXentFn.apply(logits.contiguous(), labels.contiguous(), int(ignore_index))
     return F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
+
+
+class _ProbNllFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, probs, labels, eps, ignore_index, size_average):
+        outs = native().prob_nll(probs, labels, True, eps, ignore_index)
+        acc, dp = outs[0], outs[1]
+        count = acc[1].clamp_min(1.0) if size_average else torch.ones_like(acc[1])
+        ctx.save_for_backward(dp, count)
+        ctx.dtype = probs.dtype
+        return acc[0] / count
+
+    @staticmethod
+    def backward(ctx, g):
+        dp, count = ctx.saved_tensors
+        return (dp * (g / count)).to(ctx.dtype), None, None, None, None
+
+
+def prob_nll(probs, labels, eps=1e-7, ignore_index=-100, size_average=True):
+    """-mean(log(clamp(probs[i, label_i], eps, 1))) over non-ignored rows (ClassNLLCriterion on
+    probabilities): one native pass computes the loss and the (unscaled) gradient."""
+    labels = labels.long().reshape(-1)
+    if probs.is_cuda and probs.dim() == 2 and probs.dtype in (torch.float32, torch.bfloat16):
+        return _ProbNllFn.apply(probs.contiguous(), labels.contiguous(), float(eps), int(ignore_index),
+                                bool(size_average))
+    logp = torch.log(torch.clamp(probs.float(), eps, 1.0))
+    return F.nll_loss(logp, labels, ignore_index=ignore_index, reduction="mean" if size_average else "sum")

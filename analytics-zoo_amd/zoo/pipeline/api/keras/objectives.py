@@ -65,11 +65,14 @@ class ClassNLLCriterion(LossFunction):
         t = y_true.to(y_pred.device).long().reshape(-1)
         if not self.zero_based_label:
             t = t - 1
-        logp = y_pred.float() if self.log_prob_as_input else torch.log(torch.clamp(y_pred.float(), EPS, 1.0))
-        logp = logp.reshape(t.shape[0], -1)
         ignore = self.padding_value if self.padding_value >= 0 else -100
         if self.padding_value >= 0 and not self.zero_based_label:
             ignore = self.padding_value - 1
+        if not self.log_prob_as_input and self.weights is None and y_pred.is_cuda:
+            # one native pass: loss + gradient of -log(clamp(p[label])) (zoo.ops.loss.prob_nll)
+            return ops.prob_nll(y_pred.reshape(t.shape[0], -1), t, EPS, ignore, self.size_average)
+        logp = y_pred.float() if self.log_prob_as_input else torch.log(torch.clamp(y_pred.float(), EPS, 1.0))
+        logp = logp.reshape(t.shape[0], -1)
         w = None if self.weights is None else torch.as_tensor(self.weights, dtype=torch.float32, device=logp.device)
         return F.nll_loss(logp, t, weight=w, ignore_index=ignore, reduction="mean" if self.size_average else "sum")
 
