@@ -9,8 +9,9 @@
 //
 //   fwd   y[n,p,q,c]  = act(sum_rs x[n, p*sh-ph+r, q*sw-pw+s, c] * w[r,s,c] + b[c])
 //   dgrad dx[n,h,w,c] = sum over the taps that reach (h, w) (gather form: no atomics)
-//   wgrad dw[r,s,c]  += sum_pixels dy * x  (per-thread register partials, one wave
-//                        shuffle reduction, fp32 atomics per wave)
+//   wgrad dw[r,s,c]  += sum_pixels dy * x  (per-thread register partials, wave shuffle fold,
+//                        block fold in LDS, one deterministic partial row per block, then a
+//                        column-sum kernel -- no global atomics)
 //
 // Reference: BigDL SpatialSeparableConvolution / SpatialConvolution(nGroup) behind
 // Zs/pipeline/api/keras/layers/SeparableConvolution2D.scala and the MobileNet
@@ -91,11 +92,17 @@ __global__ __launch_bounds__(256) void dwconv_dgrad_kernel(const bf16_t* __restr
   }
 }
 
-// wgrad: thread layout [row lane][chunk] over output pixels; RS_MAX taps in registers
+// wgrad: thread layout [row lane][chunk] over output pixels; RS_MAX taps in registers. Each
+// block folds its waves' partial sums into an LDS [RS][C] accumulator and writes ONE
+// deterministic partial row (no global atomics); dwconv_wgrad_reduce_kernel adds the rows.
 template <int RS_MAX>
 __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ dY,
-                                                          float* __restrict__ dW, DwGeom g, int rows_per_block) {
+                                                          float* __restrict__ partial, DwGeom g, int rows_per_block) {
+  extern __shared__ __align__(16) float dw_red[];   // [RS][C]
   const int cpr = g.C >> 3;
+  const int RS = g.R * g.S;
+  for (int i = threadIdx.x; i < RS * g.C; i += 256) dw_red[i] = 0.f;
+  __syncthreads();
   // chunk lanes per wave row: cpr rounded up to a power of two (<= 64) so that the lanes
   // sharing a chunk are a power-of-two stride apart for the shuffle fold; surplus lanes
   // carry zeros
@@ -107,7 +114,6 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const bf16_t* __restr
   const int M = g.N * g.P * g.Q;
   const int r0 = blockIdx.x * rows_per_block;
   const int r1 = min(M, r0 + rows_per_block);
-  const int RS = g.R * g.S;
   const int nchunk_iter = (cpr + lanes - 1) / lanes;
   for (int it = 0; it < nchunk_iter; ++it) {
     const int chunk = ch0 + it * lanes;
@@ -136,7 +142,8 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const bf16_t* __restr
         for (int e = 0; e < 8; ++e) acc[t][e] += dv[e] * xv[e];
       }
     }
-    // fold the wave's pixel rows (lanes with the same chunk are `lanes` apart)
+    // fold the wave's pixel rows (lanes with the same chunk are `lanes` apart), then the
+    // block's waves in LDS (4 LDS atomics per value: the waves of the block)
 #pragma unroll
     for (int t = 0; t < RS_MAX; ++t) {
       if (t >= RS) break;
@@ -148,10 +155,30 @@ __global__ __launch_bounds__(256) void dwconv_wgrad_kernel(const bf16_t* __restr
       }
       if (my_row == 0 && cok) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) atomicAdd(dW + (size_t)t * g.C + chunk * 8 + e, acc[t][e]);
+        for (int e = 0; e < 8; ++e) atomicAdd(dw_red + t * g.C + chunk * 8 + e, acc[t][e]);
       }
     }
   }
+  __syncthreads();
+  float* dst = partial + (size_t)blockIdx.x * RS * g.C;
+  for (int i = threadIdx.x; i < RS * g.C; i += 256) dst[i] = dw_red[i];
+}
+
+// dW[i] += sum over the nb partial rows (16 columns x 16 row slices per block)
+__global__ __launch_bounds__(256) void dwconv_wgrad_reduce_kernel(const float* __restrict__ partial, int nb, int n,
+                                                                 float* __restrict__ dW) {
+  __shared__ float red[16][17];
+  const int cl = threadIdx.x & 15, part = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  float s = 0.f;
+  if (col < n)
+    for (int b = part; b < nb; b += 16) s += partial[(size_t)b * n + col];
+  red[part][cl] = s;
+  __syncthreads();
+  if (part != 0 || col >= n) return;
+#pragma unroll
+  for (int k = 1; k < 16; ++k) s += red[k][cl];
+  dW[col] += s;
 }
 
 static int dw_grid(size_t total) {
@@ -180,22 +207,42 @@ extern "C" hipError_t zoo_dwconv_dgrad(const void* dY, const void* W, void* dX, 
   return hipGetLastError();
 }
 
-// requires R*S <= 9 (the caller falls back otherwise)
-extern "C" hipError_t zoo_dwconv_wgrad(const void* X, const void* dY, float* dW, const int* gi, hipStream_t st) {
+// requires R*S <= 9 (the caller falls back otherwise). `partial` holds >= dwconv_wgrad_blocks()
+// rows of R*S*C floats.
+static int dw_wgrad_rpb(int M) {
+  // <= 256 blocks (bounded partial buffer), >= 64 pixels per block
+  int rpb = (M + 255) / 256;
+  return rpb < 64 ? 64 : rpb;
+}
+
+extern "C" int zoo_dwconv_wgrad_blocks(const int* gi) {
+  const int M = gi[0] * gi[4] * gi[5];
+  const int rpb = dw_wgrad_rpb(M);
+  return (M + rpb - 1) / rpb;
+}
+
+extern "C" hipError_t zoo_dwconv_wgrad(const void* X, const void* dY, float* dW, float* partial, const int* gi,
+                                       hipStream_t st) {
   DwGeom g{gi[0], gi[1], gi[2], gi[3], gi[4], gi[5], gi[6], gi[7], gi[8], gi[9], gi[10], gi[11]};
   const int M = g.N * g.P * g.Q;
-  // ~1024 blocks, >= 64 pixels per block
-  int rpb = (M + 1023) / 1024;
-  if (rpb < 64) rpb = 64;
+  const int rpb = dw_wgrad_rpb(M);
   const int blocks = (M + rpb - 1) / rpb;
-  if (g.R * g.S <= 1)
-    hipLaunchKernelGGL(dwconv_wgrad_kernel<1>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)dY,
-                       dW, g, rpb);
-  else if (g.R * g.S <= 4)
-    hipLaunchKernelGGL(dwconv_wgrad_kernel<4>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)dY,
-                       dW, g, rpb);
-  else
-    hipLaunchKernelGGL(dwconv_wgrad_kernel<9>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X, (const bf16_t*)dY,
-                       dW, g, rpb);
+  const int n = g.R * g.S * g.C;
+  const size_t lds = (size_t)n * 4;
+  if (lds > 160 * 1024) return hipErrorInvalidValue;
+#define ZOO_DW_WG(RSM)                                                                                        \
+  do {                                                                                                       \
+    auto k = &dwconv_wgrad_kernel<RSM>;                                                                      \
+    if (lds > 64 * 1024)                                                                                     \
+      hipFuncSetAttribute(reinterpret_cast<const void*>(k), hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(256), lds, st, (const bf16_t*)X, (const bf16_t*)dY, partial, g, rpb); \
+  } while (0)
+  if (g.R * g.S <= 1) ZOO_DW_WG(1);
+  else if (g.R * g.S <= 4) ZOO_DW_WG(4);
+  else ZOO_DW_WG(9);
+#undef ZOO_DW_WG
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((n + 15) / 16), dim3(256), 0, st, partial, blocks, n, dW);
   return hipGetLastError();
 }

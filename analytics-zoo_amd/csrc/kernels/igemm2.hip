@@ -491,7 +491,7 @@ static int i2_bn(int tile) {
 }
 
 // shape + epilogue -> tile, or 0 = "leave it to igemm.hip" (tools/igemm2_bench.py on the
-// ResNet-50 b256 convs with the model's own epilogues, round 3, profiles/igemm2_r3.md):
+// ResNet-50 b256 convs with the model's own epilogues, round 3, profiles/r3/igemm2_r3.md):
 //   * N (output channels) < 256: igemm.hip's 128x{64,128} tiles are as fast or faster;
 //   * a short reduction (Ktot < 256 forward, < 1024 for the BN-backward epilogue) is bound by
 //     the epilogue, where igemm.hip's row-pointer epilogues win;

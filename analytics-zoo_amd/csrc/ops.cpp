@@ -78,7 +78,8 @@ hipError_t zoo_avgpool_bwd(const void*, void*, int, int, int, int, int, int, int
                            hipStream_t);
 hipError_t zoo_dwconv_fwd(const void*, const void*, const float*, void*, const int*, int, hipStream_t);
 hipError_t zoo_dwconv_dgrad(const void*, const void*, void*, const int*, hipStream_t);
-hipError_t zoo_dwconv_wgrad(const void*, const void*, float*, const int*, hipStream_t);
+hipError_t zoo_dwconv_wgrad(const void*, const void*, float*, float*, const int*, hipStream_t);
+int zoo_dwconv_wgrad_blocks(const int*);
 hipError_t zoo_softmax_rows(const void*, void*, int, int, int, int, hipStream_t);
 hipError_t zoo_softmax_rows_bwd(const void*, const void*, void*, int, int, int, int, hipStream_t);
 hipError_t zoo_lrn(const void*, const void*, void*, size_t, int, int, float, float, float, int, int, hipStream_t);
@@ -858,8 +859,11 @@ void dwconv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, in
   const int P = dy.size(1), Q = dy.size(2);
   TORCH_CHECK(P == (x.size(1) + 2 * ph - R) / sh + 1 && Q == (x.size(2) + 2 * pw - S) / sw + 1,
               "dwconv_wgrad: geometry");
+  TORCH_CHECK((int64_t)R * S * C * 4 <= 160 * 1024, "dwconv_wgrad: R*S*C too large for the LDS fold");
   auto g = dw_geom(x, R, S, sh, sw, ph, pw, P, Q);
-  check_hip(zoo_dwconv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), g.data(), cur_stream()),
+  auto partial = torch::empty({(int64_t)zoo_dwconv_wgrad_blocks(g.data()) * R * S * C}, dw.options());
+  check_hip(zoo_dwconv_wgrad(x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), partial.data_ptr<float>(), g.data(),
+                             cur_stream()),
             "dwconv_wgrad");
 }
 

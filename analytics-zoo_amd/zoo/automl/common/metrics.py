@@ -77,19 +77,27 @@ def R2(y_true, y_pred, multioutput="raw_values"):  # noqa: N802
 METRICS = {"me": ME, "mae": MAE, "mse": MSE, "rmse": RMSE, "r2": R2, "smape": sMAPE, "mpe": MPE, "mape": MAPE,
            "mdape": MDAPE, "smdape": sMDAPE, "mspe": MSPE}
 MAXIMIZE = {"r2"}
+# Keras metric names accepted where a forecaster / pipeline was configured with them
+ALIASES = {"mean_squared_error": "mse", "mean_absolute_error": "mae", "root_mean_squared_error": "rmse",
+           "mean_absolute_percentage_error": "mape", "r_square": "r2"}
+
+
+def _name(metric):
+    m = metric.lower()
+    return ALIASES.get(m, m)
 
 
 class Evaluator:
     @staticmethod
     def evaluate(metric, y_true, y_pred, multioutput="raw_values"):
         Evaluator.check_metric(metric)
-        return METRICS[metric.lower()](y_true, y_pred, multioutput)
+        return METRICS[_name(metric)](y_true, y_pred, multioutput)
 
     @staticmethod
     def check_metric(metric):
-        if metric.lower() not in METRICS:
+        if _name(metric) not in METRICS:
             raise ValueError("metric %s not supported (%s)" % (metric, sorted(METRICS)))
 
     @staticmethod
     def higher_is_better(metric):
-        return metric.lower() in MAXIMIZE
+        return _name(metric) in MAXIMIZE

@@ -25,14 +25,21 @@ class Recipe:
 
 
 def _past(look_back):
-    if isinstance(look_back, (tuple, list)):
-        lo, hi = int(look_back[0]), int(look_back[1])
-        if lo < 2 or hi < lo:
-            raise ValueError("look_back (min, max) must satisfy 2 <= min <= max")
+    """past_seq_len search config from ``look_back``: an int >= 2, or an (min, max) int tuple
+    sampled uniformly (a min below 2 is raised to 2) -- recipe.py:117-152 semantics."""
+    if isinstance(look_back, tuple) and len(look_back) == 2 and all(isinstance(v, int) and not isinstance(v, bool)
+                                                                   for v in look_back):
+        lo, hi = look_back
+        if hi < 2:
+            raise ValueError("The max look back value should be at least 2")
+        lo = max(2, lo)
         return RandomSample(lambda spec: int(np.random.randint(lo, hi + 1)))
-    if int(look_back) < 2:
-        raise ValueError("look_back must be >= 2")
-    return int(look_back)
+    if isinstance(look_back, int) and not isinstance(look_back, bool):
+        if look_back < 2:
+            raise ValueError("look back value should not be smaller than 2. Current value is %s" % look_back)
+        return look_back
+    raise ValueError("look back is %r.\n look_back should be either a tuple with 2 int values: (min_len, max_len) "
+                     "or a single int" % (look_back,))
 
 
 class SmokeRecipe(Recipe):

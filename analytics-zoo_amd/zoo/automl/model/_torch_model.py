@@ -104,8 +104,9 @@ class TorchTSModel(BaseModel):
         os.makedirs(d, exist_ok=True)
         torch.save(self.state_dict(), model_path)
         cfg = dict(self.config, input_dim=self.input_dim, future_seq_len=self.future_seq_len)
-        with open(config_path, "w") as f:
-            json.dump({k: _jsonable(v) for k, v in cfg.items()}, f)
+        # merged into the bundle's shared config file (feature transformer state + trial config)
+        from zoo.automl.common.util import save_config
+        save_config(config_path, {k: _jsonable(v) for k, v in cfg.items()})
 
     def restore(self, model_path, **config):
         self.config.update(config)

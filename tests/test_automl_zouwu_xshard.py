@@ -36,12 +36,13 @@ def test_feature_transformer_rolling():
     from zoo.automl.feature.time_sequence import TimeSequenceFeatureTransformer
     df = _ts(50)
     ft = TimeSequenceFeatureTransformer(future_seq_len=2)
-    x, y = ft.fit_transform(df, past_seq_len=4, selected_features=["HOUR", "IS_WEEKEND"])
+    x, y = ft.fit_transform(df, past_seq_len=4, selected_features=["HOUR(datetime)", "IS_WEEKEND(datetime)"])
     assert x.shape == (45, 4, 3) and y.shape == (45, 2)
     # target column is first; y is the scaled target of the next 2 steps
     assert np.allclose(x[1, -1, 0], y[0, 0])
-    back = ft.post_processing(df, y, True)
+    truth, back = ft.post_processing(df, y, True)
     assert np.allclose(back[:, 0], df["value"].values[4:49], atol=1e-6)
+    assert np.allclose(truth, back, atol=1e-6)
 
 
 def test_search_expand_grid_random():
@@ -87,12 +88,11 @@ def test_zouwu_forecasters_and_autots(tmp_path):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((64, 6, 2)).astype(np.float32)
     y = x[:, -1, :1] * 0.5
-    f = LSTMForecaster(target_dim=1, feature_dim=2, lr=0.01)
+    f = LSTMForecaster(horizon=1, feature_dim=2, lr=0.01)
     before = f.evaluate(x, y)[0]
     f.fit(x, y, batch_size=16, epochs=20)
     assert f.evaluate(x, y)[0] < before
-    m = MTNetForecaster(target_dim=1, feature_dim=2, long_series_num=2, series_length=2, ar_window_size=2,
-                        cnn_height=2)
+    m = MTNetForecaster(horizon=1, feature_dim=2, lb_long_steps=2, lb_long_stepsize=2, ar_window=2, cnn_height=2)
     assert m.predict(m.preprocess_input(x)).shape == (64, 1)
     df = _ts(120)
     ppl = AutoTSTrainer(horizon=1).fit(df[:100], df[100:], recipe=SmokeRecipe())
