@@ -99,4 +99,12 @@ struct RnnArgs {
   int B, T, act, iact;
 };
 
+
+// JPEG batch geometry (image.hip jpeg_* kernels; host entropy decoder csrc/runtime/jpeg.cpp)
+struct JpegGeom {
+  int N, ncomp, w, h, hmax, vmax;
+  int hs[3], vs[3], bw[3], bh[3], boff[3];   // sampling, padded block grid, block offset per component
+  int total;                                 // blocks per image (all components)
+};
+
 }  // namespace zoo

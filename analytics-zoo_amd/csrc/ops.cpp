@@ -18,6 +18,9 @@ using zoo::BwdStats;
 using zoo::GemmGeom;
 
 extern "C" {
+hipError_t zoo_jpeg_idct(const int16_t*, const int32_t*, uint8_t*, const zoo::JpegGeom*, hipStream_t);
+hipError_t zoo_jpeg_color_resize(const uint8_t*, void*, const zoo::JpegGeom*, int, int, const float*, const float*,
+                                 int, int, hipStream_t);
 hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
                         hipStream_t);
 int zoo_ncf_tier(int, int, int, int, int, int, int);
@@ -1694,6 +1697,71 @@ torch::Tensor resize_normalize(torch::Tensor in, int64_t Ho, int64_t Wo, std::ve
 }
 
 
+
+// GPU half of the JPEG decoder: geometry g = [N, ncomp, w, h, hmax, vmax, hs0..2, vs0..2, bw0..2, bh0..2,
+// boff0..2, total] (zoo/feature/image/jpeg.py builds it from csrc/runtime/jpeg.cpp's batch output)
+static zoo::JpegGeom jpeg_geom(const std::vector<int64_t>& v) {
+  TORCH_CHECK(v.size() == 22, "jpeg geometry: 22 ints");
+  zoo::JpegGeom g;
+  g.N = v[0]; g.ncomp = v[1]; g.w = v[2]; g.h = v[3]; g.hmax = v[4]; g.vmax = v[5];
+  for (int c = 0; c < 3; ++c) {
+    g.hs[c] = v[6 + c]; g.vs[c] = v[9 + c]; g.bw[c] = v[12 + c]; g.bh[c] = v[15 + c]; g.boff[c] = v[18 + c];
+  }
+  g.total = v[21];
+  TORCH_CHECK(g.N > 0 && (g.ncomp == 1 || g.ncomp == 3) && g.w > 0 && g.h > 0 && g.hmax >= 1 && g.vmax >= 1,
+              "jpeg geometry: header");
+  long blocks = 0;
+  for (int c = 0; c < g.ncomp; ++c) {
+    TORCH_CHECK(g.hs[c] >= 1 && g.hs[c] <= g.hmax && g.vs[c] >= 1 && g.vs[c] <= g.vmax, "jpeg geometry: sampling");
+    TORCH_CHECK(g.boff[c] == blocks, "jpeg geometry: component offsets");
+    // the padded grid must cover the component (the kernels index it unchecked)
+    TORCH_CHECK((long)g.bw[c] * 8 >= ((long)g.w * g.hs[c] + g.hmax - 1) / g.hmax &&
+                    (long)g.bh[c] * 8 >= ((long)g.h * g.vs[c] + g.vmax - 1) / g.vmax,
+                "jpeg geometry: block grid smaller than the component");
+    blocks += (long)g.bw[c] * g.bh[c];
+  }
+  TORCH_CHECK(blocks == g.total, "jpeg geometry: total blocks");
+  return g;
+}
+
+torch::Tensor jpeg_idct(torch::Tensor coef, torch::Tensor qt, std::vector<int64_t> geom) {
+  const auto g = jpeg_geom(geom);
+  req(coef, at::kShort, "jpeg coef");
+  req(qt, at::kInt, "jpeg qt");
+  TORCH_CHECK(coef.dim() == 3 && coef.size(0) == g.N && coef.size(1) == g.total && coef.size(2) == 64,
+              "jpeg coef [N, total, 64]");
+  TORCH_CHECK(qt.dim() == 3 && qt.size(0) == g.N && qt.size(1) == g.ncomp && qt.size(2) == 64, "jpeg qt [N, ncomp, 64]");
+  auto planes = torch::empty({(int64_t)g.N, (int64_t)g.total * 64}, coef.options().dtype(at::kByte));
+  check_hip(zoo_jpeg_idct(coef.data_ptr<int16_t>(), qt.data_ptr<int32_t>(), planes.data_ptr<uint8_t>(), &g,
+                          cur_stream()),
+            "jpeg_idct");
+  return planes;
+}
+
+torch::Tensor jpeg_color_resize(torch::Tensor planes, std::vector<int64_t> geom, int64_t Ho, int64_t Wo,
+                                std::vector<double> mean, std::vector<double> stdv, bool swap_rb, int64_t layout) {
+  const auto g = jpeg_geom(geom);
+  req(planes, at::kByte, "jpeg planes");
+  TORCH_CHECK(planes.numel() == (int64_t)g.N * g.total * 64, "jpeg planes size");
+  TORCH_CHECK(layout >= 0 && layout <= 2, "layout 0 (NCHW f32), 1 (NHWC4 bf16) or 2 (RGB uint8)");
+  if (layout == 2) TORCH_CHECK(Ho == g.h && Wo == g.w, "layout 2 is the decoded image (no resize)");
+  TORCH_CHECK(Ho > 0 && Wo > 0, "bad output size");
+  float m[3] = {0.f, 0.f, 0.f}, sd[3] = {1.f, 1.f, 1.f};
+  for (size_t i = 0; i < 3 && i < mean.size(); ++i) m[i] = (float)mean[i];
+  for (size_t i = 0; i < 3 && i < stdv.size(); ++i) sd[i] = (float)stdv[i];
+  if (mean.size() == 1) m[1] = m[2] = m[0];
+  if (stdv.size() == 1) sd[1] = sd[2] = sd[0];
+  for (int i = 0; i < 3; ++i) TORCH_CHECK(sd[i] != 0.f, "std must be non-zero");
+  torch::Tensor out;
+  if (layout == 0) out = torch::empty({(int64_t)g.N, 3, Ho, Wo}, planes.options().dtype(at::kFloat));
+  else if (layout == 1) out = torch::empty({(int64_t)g.N, Ho, Wo, 4}, planes.options().dtype(at::kBFloat16));
+  else out = torch::empty({(int64_t)g.N, Ho, Wo, 3}, planes.options());
+  check_hip(zoo_jpeg_color_resize(planes.data_ptr<uint8_t>(), out.data_ptr(), &g, (int)Ho, (int)Wo, m, sd,
+                                  swap_rb ? 1 : 0, (int)layout, cur_stream()),
+            "jpeg_color_resize");
+  return out;
+}
+
 // Y[M, N] = epilogue(A[M, K] . B[N, K]^T) on the 256x256 LDS-DMA kernel (gemm256.hip).
 torch::Tensor gemm(torch::Tensor a, torch::Tensor b, c10::optional<torch::Tensor> bias,
                    c10::optional<torch::Tensor> resid, c10::optional<torch::Tensor> stats, int64_t act, bool out_f32,
@@ -2173,6 +2241,8 @@ torch::Tensor ncf_fused(torch::Tensor ids, std::vector<torch::Tensor> t, std::ve
 PYBIND11_MODULE(_C, m) {
   m.doc() = "zoo native gfx950 (MI355X) kernel library";
   m.def("resize_normalize", &resize_normalize);
+  m.def("jpeg_idct", &jpeg_idct);
+  m.def("jpeg_color_resize", &jpeg_color_resize);
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd);
   m.def("flip_weights", &flip_weights);

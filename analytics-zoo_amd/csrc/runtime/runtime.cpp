@@ -265,10 +265,12 @@ py::list pb_fields(py::bytes b) {
 
 #ifndef ZOO_RT_NO_PYTHON
 void register_serving(py::module& m);  // serving.cpp
+void register_jpeg(py::module& m);     // jpeg.cpp
 
 PYBIND11_MODULE(_runtime, m) {
   m.doc() = "zoo native host runtime (batch gather, TFRecord/CRC32C, protobuf wire scanner, serving queue)";
   register_serving(m);
+  register_jpeg(m);
   py::class_<Gatherer>(m, "Gatherer")
       .def(py::init<int>(), py::arg("nthreads") = 4)
       .def("gather", &Gatherer::gather)

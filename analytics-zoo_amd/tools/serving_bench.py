@@ -8,6 +8,10 @@ ResNet-50 + BERT-base, throughput + p50 latency").
   serving_bench.py e2e [--images N]    end-to-end Cluster Serving: JPEG images through the
                                        RESP (Redis-protocol) queue -> batching worker ->
                                        GPU resize/normalize -> ResNet-50 -> top-N results
+  serving_bench.py openloop            open-loop load: client processes send at FIXED offered
+                                       rates (independent of responses) for --duration s each;
+                                       per rate: achieved throughput, p50 / p99 service latency
+                                       (send -> result written), unfinished records
 
 Random-init weights, synthetic inputs. Prints one JSON line per measurement.
 """
@@ -230,9 +234,198 @@ def run_e2e(a):
         srv.server_close()
 
 
+def _openloop_client(cfg, rate, t_start, duration, prefix, payloads, out_q):
+    """Send at ``rate`` records/s from ``t_start`` (wall clock) for ``duration`` s, on a fixed
+    schedule regardless of responses; report [(uri, send_wall_time)]."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from zoo.serving import InputQueue
+    q = InputQueue(cfg)
+    sent = []
+    n = int(rate * duration)
+    while time.time() < t_start:
+        time.sleep(0.001)
+    for i in range(n):
+        due = t_start + i / rate
+        now = time.time()
+        if due > now:
+            time.sleep(due - now)
+        uri = "%s-%d" % (prefix, i)
+        ts = time.time()
+        _send(q, uri, payloads[i % len(payloads)])
+        sent.append((uri, ts))
+    out_q.put(sent)
+
+
+def run_openloop(a):
+    import multiprocessing as mp
+    import tempfile
+    from PIL import Image
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.resnet import resnet50
+    from zoo.serving import ClusterServing, InputQueue
+    from zoo.serving.resp import RespServer
+    init_nncontext("serving-openloop")
+    srv = RespServer("127.0.0.1", 0).start()
+    rng = np.random.default_rng(0)
+    jpgs = []
+    for _ in range(16):
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
+        jpgs.append(buf.getvalue())
+    done = {}
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            cfg = os.path.join(d, "config.yaml")
+            open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,224,224\n  filter: topN(5)\n"
+                                 "params:\n  batch_size: %d\n" % (srv.port, a.batch))
+            s = ClusterServing(cfg, model=resnet50(), device="cuda")
+
+            def hook(uris, t):
+                for u in uris:
+                    done[u] = t
+            s.finish_hook = hook
+            inq = InputQueue(cfg)
+            # warm-up: every bucket shape captured, then the worker keeps running
+            for i in range(4 * a.batch):
+                _send(inq, "warm%d" % i, jpgs[i % len(jpgs)])
+            worker = threading.Thread(target=s.run, kwargs={"idle_timeout": None}, daemon=True)
+            worker.start()
+            t = time.time()
+            while sum(1 for k in done if k.startswith("warm")) < 4 * a.batch and time.time() - t < 120:
+                time.sleep(0.01)
+            for bsz in (8, 16, 32, 64, 128, 256, 512):   # capture the remaining buckets
+                if bsz > a.batch:
+                    break
+                x = torch.zeros(bsz, 3, 224, 224, device="cuda")
+                s.im.predict(x)
+            # capacity: a pre-filled queue drained by the worker
+            n_cap = 20 * a.batch
+            t0 = time.time()
+            for i in range(n_cap):
+                _send(inq, "cap%d" % i, jpgs[i % len(jpgs)])
+            while sum(1 for k in done if k.startswith("cap")) < n_cap and time.time() - t0 < 120:
+                time.sleep(0.005)
+            cap_done = [done[k] for k in done if k.startswith("cap")]
+            capacity = len(cap_done) / max(1e-9, max(cap_done) - t0) if cap_done else 0.0
+            print(json.dumps({"bench": "cluster-serving-capacity", "batch": a.batch, "records": len(cap_done),
+                              "closed_loop_throughput": round(capacity, 1), "note": "includes enqueue from one "
+                              "client thread"}), flush=True)
+            rates = [float(r) for r in a.rates.split(",")] if a.rates else \
+                [round(f * capacity) for f in (0.1, 0.25, 0.5, 0.7, 0.85, 1.0, 1.2)]
+            ctx = mp.get_context("spawn")
+            for ri, rate in enumerate(rates):
+                if rate <= 0:
+                    continue
+                nproc = max(1, int(np.ceil(rate / a.client_rate)))
+                outq = ctx.Queue()
+                t_start = time.time() + 3.0
+                procs = [ctx.Process(target=_openloop_client,
+                                     args=(cfg, rate / nproc, t_start, a.duration, "r%dp%d" % (ri, p), jpgs, outq))
+                         for p in range(nproc)]
+                for p in procs:
+                    p.start()
+                sent = []
+                for _ in procs:
+                    sent += outq.get(timeout=a.duration + 240)
+                for p in procs:
+                    p.join()
+                grace = time.time() + 10.0
+                while time.time() < grace and any(u not in done for u, _ in sent[-200:]):
+                    time.sleep(0.01)
+                warm = t_start + 1.0
+                win = [(u, ts) for u, ts in sent if ts >= warm]
+                lat = [(done[u] - ts) * 1e3 for u, ts in win if u in done]
+                fin = [done[u] for u, _ in sent if u in done and warm <= done[u] <= t_start + a.duration]
+                achieved = len(fin) / max(1e-9, a.duration - 1.0)
+                offered = len(sent) / a.duration
+                print(json.dumps({"bench": "cluster-serving-openloop", "model": "ResNet-50 bf16",
+                                  "batch_cap": a.batch, "offered_rate": round(offered, 1),
+                                  "achieved_throughput": round(achieved, 1), "unit": "records/sec",
+                                  "p50_ms": round(_pct(lat, 50), 2) if lat else None,
+                                  "p99_ms": round(_pct(lat, 99), 2) if lat else None,
+                                  "unfinished": sum(1 for u, _ in sent if u not in done),
+                                  "client_procs": nproc, "duration_s": a.duration, "n_gpus": 1,
+                                  "decode": "gpu-jpeg" if os.environ.get("ZOO_SERVING_GPU_JPEG", "1") != "0"
+                                  else "cpu", "data": "synthetic 256x256 JPEG"}), flush=True)
+                time.sleep(1.0)
+            s.stop()
+    finally:
+        srv.shutdown()
+        srv.server_close()
+
+
+def run_dist(a):
+    """One serving worker per GPU, launched unchanged by torch.distributed.run on 1..8 GPUs:
+    every rank owns an in-process native queue, pre-fills it with --images JPEG records and
+    drains it through its own worker (C++ Huffman decode threads + GPU IDCT / resize + ResNet-50
+    + topN); ranks start together (barrier) and rank 0 prints the whole-node throughput."""
+    import tempfile
+    import torch.distributed as dist
+    from PIL import Image
+    from zoo.models.image.resnet import resnet50
+    from zoo.serving import ClusterServing, InputQueue
+    from zoo.serving.resp import RespServer
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("gloo")
+    # each rank gets its share of the node's CPU threads for the entropy decoder
+    os.environ.setdefault("ZOO_SERVING_JPEG_THREADS", str(max(2, (os.cpu_count() or 16) // max(1, world) // 2)))
+    from zoo.common.nncontext import init_nncontext
+    init_nncontext("serving-dist")
+    srv = RespServer("127.0.0.1", 0).start()
+    rng = np.random.default_rng(rank)
+    jpgs = []
+    for _ in range(16):
+        buf = io.BytesIO()
+        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
+        jpgs.append(buf.getvalue())
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            cfg = os.path.join(d, "config.yaml")
+            open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,224,224\n  filter: topN(5)\n"
+                                 "params:\n  batch_size: %d\n" % (srv.port, a.batch))
+            s = ClusterServing(cfg, model=resnet50(), device="cuda:%d" % local)
+            inq = InputQueue(cfg)
+            for i in range(2 * a.batch):
+                _send(inq, "warm%d" % i, jpgs[i % len(jpgs)])
+            s.run(max_records=2 * a.batch, idle_timeout=60)
+            s.records = 0
+            for i in range(a.images):
+                _send(inq, "im%d" % i, jpgs[i % len(jpgs)])
+            if world > 1:
+                dist.barrier()
+            t0 = time.perf_counter()
+            s.run(max_records=a.images, idle_timeout=60)
+            el = time.perf_counter() - t0
+            tp = torch.tensor([s.records / el, el], dtype=torch.float64)
+            if world > 1:
+                allv = [torch.zeros_like(tp) for _ in range(world)]
+                dist.all_gather(allv, tp)
+            else:
+                allv = [tp]
+            if rank == 0:
+                total = sum(float(v[0]) for v in allv)
+                print(json.dumps({"bench": "cluster-serving-dist-drain", "model": "ResNet-50 bf16", "batch": a.batch,
+                                  "images_per_gpu": a.images, "throughput": round(total, 1), "unit": "records/sec",
+                                  "per_gpu": [round(float(v[0]), 1) for v in allv], "n_gpus": world,
+                                  "decode": "gpu-jpeg" if os.environ.get("ZOO_SERVING_GPU_JPEG", "1") != "0"
+                                  else "cpu", "data": "synthetic 256x256 JPEG"}), flush=True)
+    finally:
+        srv.shutdown()
+        srv.server_close()
+        if world > 1:
+            dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["model", "e2e"])
+    ap.add_argument("mode", choices=["model", "e2e", "openloop", "dist"])
+    ap.add_argument("--rates", default="", help="openloop: comma-separated offered rates (default: fractions "
+                    "of the measured capacity)")
+    ap.add_argument("--duration", type=float, default=8.0, help="openloop: seconds per offered rate")
+    ap.add_argument("--client-rate", type=float, default=1500.0, help="openloop: records/s per client process")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--images", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=64)
@@ -242,7 +435,7 @@ def main():
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"],
                     help="e2e: ResNet-50 on JPEG records or BERT-base on token-id tensor records")
     a = ap.parse_args()
-    run_models(a) if a.mode == "model" else run_e2e(a)
+    {"model": run_models, "e2e": run_e2e, "openloop": run_openloop, "dist": run_dist}[a.mode](a)
 
 
 if __name__ == "__main__":

@@ -5,8 +5,10 @@ One worker process per GPU. Each worker:
   1. joins consumer group ``serving`` on stream ``image_stream`` (XREADGROUP),
   2. takes up to ``batch_size`` records (``uri`` + base64 ``image`` — an
      encoded image — or ``tensor``: base64 float32 bytes with a ``shape`` field),
-  3. decodes images on a CPU thread pool, then does resize + normalize +
-     layout on the GPU in ONE fused HIP kernel (csrc/kernels/image.hip),
+  3. decodes images: baseline JPEGs are Huffman-decoded on C++ threads (csrc/runtime/jpeg.cpp)
+     and the IDCT / chroma upsampling / YCbCr->RGB / resize / normalize run on the GPU
+     (csrc/kernels/image.hip); other images decode on the CPU and only resize + normalize +
+     layout run on the GPU,
   4. runs the model through InferenceModel (HIP stream + captured hipGraph
      per batch shape, bf16/fp32),
   5. post-processes (``topN(k)`` filter or the full nested-list string) and
@@ -178,6 +180,16 @@ def post_process(t, flt="None"):
     return tensor_to_ndarray_string(t)
 
 
+def _bucket(n, cap):
+    """Smallest power of two >= n (at least 8), capped at the configured batch size."""
+    if os.environ.get("ZOO_SERVING_BUCKETS", "1") == "0":
+        return n
+    b = 8
+    while b < n:
+        b <<= 1
+    return max(n, min(b, cap))
+
+
 class ClusterServing:
     def __init__(self, config, model=None, consumer=None, device=None):
         from zoo.pipeline.inference import InferenceModel
@@ -199,6 +211,7 @@ class ClusterServing:
         self._pinned, self._pin_idx = {}, {}
         self._dpool = None
         self.stop_flag = threading.Event()
+        self.finish_hook = None   # callable(uris, wall_time) after each batch's results are written
         self.records = 0
         self.summary = None
         if self.cfg.get("tensorboard"):
@@ -274,6 +287,9 @@ class ClusterServing:
         ids = [r[0] for r in recs]
         uris = [r[1] for r in recs]
         if self.im.device.type == "cuda" and all(r[2] == "image" for r in recs):
+            hit = self._jpeg_coeffs([r[3] for r in recs])
+            if hit is not None:   # GPU JPEG path: entropy-decoded here, IDCT onward on the GPU
+                return ids, uris, hit
             dp = self._decode_procs()
             buf = dp.decode([r[3] for r in recs]) if dp is not None else None
             out = ("rgb", buf) if buf is not None else self._decode_rgb_pinned(recs)
@@ -289,6 +305,37 @@ class ClusterServing:
                 return "tensor", np.frombuffer(payload, np.float32).reshape([int(x) for x in shape.split(",")])
             raise ValueError("record has neither image nor tensor")
         return ids, uris, list(self.pool.map(dec, recs))
+
+    def _jpeg_coeffs(self, payloads):
+        """Baseline JPEGs of one geometry: Huffman-decode the batch on C++ threads (no GIL)
+        straight into a pinned host ring slot -> ("jpeg", coefficient dict, pinned view); the
+        IDCT, chroma upsampling, colour conversion and resize run on the GPU (image.hip).
+        None -> the CPU decode paths (PNG, progressive JPEG, mixed sizes,
+        ZOO_SERVING_GPU_JPEG=0)."""
+        if os.environ.get("ZOO_SERVING_GPU_JPEG", "1") == "0":
+            return None
+        from zoo.feature.image import jpeg
+        nt = int(os.environ.get("ZOO_SERVING_JPEG_THREADS", str(min(16, os.cpu_count() or 8))))
+        ring = getattr(self, "_coef_ring", None)
+        slot = None
+        if ring is not None:
+            slot = ring[self._coef_idx % len(ring)]
+            self._coef_idx += 1
+        d = jpeg.batch_coeffs(payloads, nt, None if slot is None else slot.numpy())
+        if d is None and slot is not None:
+            d = jpeg.batch_coeffs(payloads, nt)      # unsupported stream, or the ring is too small
+            slot = None
+        if d is None:
+            return None
+        if slot is None:   # (re)size the ring for this batch geometry and copy this batch in
+            need = d["coef"].size
+            self._coef_ring = [torch.empty(need, dtype=torch.int16, pin_memory=True) for _ in range(4)]
+            self._coef_idx = 1
+            slot = self._coef_ring[0]
+            slot.numpy()[:need] = d["coef"].reshape(-1)
+            d["coef"] = slot.numpy()[:need].reshape(d["coef"].shape)
+        n = d["coef"].size
+        return ("jpeg", d, slot[:n].view(d["coef"].shape))
 
     def _decode_procs(self):
         """The multi-process decode pool (zoo/serving/decode_pool.py); ZOO_SERVING_DECODE_PROCS=0
@@ -331,6 +378,11 @@ class ClusterServing:
         return ("rgb", buf)
 
     def _to_batch(self, decoded):
+        if isinstance(decoded, tuple) and decoded[0] == "jpeg":
+            from zoo.feature.image import jpeg
+            c, h, w = self.cfg["image_shape"]
+            return jpeg.planes_to_input(decoded[1], (int(h), int(w)), self.cfg["mean"], self.cfg["std"],
+                                        not self.cfg["to_rgb"], 0, self.im.device, coef_host=decoded[2])
         if isinstance(decoded, tuple) and decoded[0] == "rgb":
             c, h, w = self.cfg["image_shape"]
             dev = self.im.device
@@ -396,10 +448,17 @@ class ClusterServing:
                 if isinstance(item, Exception):
                     raise item
                 ids, uris, decoded = item
-                out = self.im.predict(self._to_batch(decoded))
+                x = self._to_batch(decoded)
+                n = x.shape[0]
+                nb = _bucket(n, bs)
+                if nb > n:   # pad to a power-of-two bucket: hipGraphs for ~log2(batch) shapes only
+                    x = torch.cat([x, x.new_zeros((nb - n,) + tuple(x.shape[1:]))])
+                out = self.im.predict(x)
                 outs = out if isinstance(out, np.ndarray) else out[0]
-                vals = post_process_batch(outs, flt)
+                vals = post_process_batch(outs[:n], flt)
                 self.db.finish(STREAM, GROUP, ids, [("result:" + u, v) for u, v in zip(uris, vals)])
+                if self.finish_hook is not None:
+                    self.finish_hook(uris, time.time())
                 self.records += len(ids)
                 if self.summary is not None:
                     dt = max(time.time() - self._t0, 1e-9)
