@@ -394,10 +394,7 @@ __global__ __launch_bounds__(256) void act_colsum_kernel(const bf16_t* __restric
         unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
         if (ACT == 2) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            const float x = z[e];
-            a[e] *= 0.5f * (1.f + erff(x * 0.70710678118654752f)) + x * 0.39894228040143268f * __expf(-0.5f * x * x);
-          }
+          for (int e = 0; e < 8; ++e) a[e] *= gelu_grad_f(z[e]);
         } else {
 #pragma unroll
           for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;

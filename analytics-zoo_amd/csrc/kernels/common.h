@@ -101,10 +101,36 @@ ZOO_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
 // Activation codes shared with the Python side (zoo/ops/_codes.py).
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2, ACT_SIGMOID = 3, ACT_TANH = 4 };
 
+// GELU (erf form) on the fast path: erf by Abramowitz-Stegun 7.1.26 (|error| <= 1.5e-7, under
+// fp32 / bf16 output precision) with the hardware exp and reciprocal -- branch-free, ~15 VALU
+// ops where ocml's erff runs range-split polynomials (the GELU passes of a BERT step were
+// VALU-bound on it: profiles/bert_base_train_b128_r2.md act_kernel_v8 / act_colsum_kernel<2>).
+// The Gaussian factor exp(-x^2/2) is shared by the CDF and the density of the derivative.
+ZOO_DEV void gelu_parts(float x, float& cdf, float& dens) {
+  const float u = x * 0.70710678118654752f;
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, fabsf(u), 1.f));
+  const float e = __expf(-u * u);
+  const float p =
+      t * fmaf(t, fmaf(t, fmaf(t, fmaf(t, 1.061405429f, -1.453152027f), 1.421413741f), -0.284496736f), 0.254829592f);
+  const float q = 0.5f * p * e;            // 0.5 * erfc(|u|)
+  cdf = u < 0.f ? q : 1.f - q;
+  dens = 0.39894228040143268f * e;         // phi(x)
+}
+ZOO_DEV float gelu_f(float x) {
+  float c, d;
+  gelu_parts(x, c, d);
+  return x * c;
+}
+ZOO_DEV float gelu_grad_f(float x) {
+  float c, d;
+  gelu_parts(x, c, d);
+  return fmaf(x, d, c);
+}
+
 ZOO_DEV float apply_act(float x, int act) {
   switch (act) {
     case ACT_RELU: return x > 0.f ? x : 0.f;
-    case ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case ACT_GELU: return gelu_f(x);
     case ACT_SIGMOID: return 1.f / (1.f + __expf(-x));
     case ACT_TANH: return tanhf(x);
     default: return x;

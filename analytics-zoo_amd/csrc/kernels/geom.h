@@ -39,6 +39,10 @@ struct BwdStats {
   const float* mean;
   const float* inv;
   float* sums;        // [2*K]
+  // 1: z is a GELU pre-activation -- the output is scaled by GELU'(z) instead of masked, and
+  // `sums` collects its plain column sums (the producing linear's bias gradient); y / mean /
+  // inv are unused (the transformer FFN: GELU backward in the next linear's dgrad epilogue)
+  int zgelu;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

@@ -392,7 +392,7 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 
   if constexpr (EPI == 2) {
     float mu[8], iv[8];
-    if (bs.sums && col_ok) {
+    if (bs.sums && !bs.zgelu && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
     }
@@ -421,19 +421,30 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
       if (bs.z) {
         float zz[8];
         unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+        if (bs.zgelu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+        }
       }
       const uint4 pk = pack8(v);
       *reinterpret_cast<uint4*>(Y + off) = pk;
       if (bs.sums) {
-        float q[8], yy[8];
+        float q[8];
         unpack8(pk, q);
-        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+        if (bs.zgelu) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          s1[e] += q[e];
-          s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+          for (int e = 0; e < 8; ++e) s1[e] += q[e];
+        } else {
+          float yy[8];
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            s1[e] += q[e];
+            s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+          }
         }
       }
     }

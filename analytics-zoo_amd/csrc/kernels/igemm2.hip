@@ -236,7 +236,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
     }
   }
   if constexpr (EPI == 0 || EPI == 2) {
-    if (bs.sums && col_ok) {
+    if (bs.sums && !bs.zgelu && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
     }
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
         } else if (act == ACT_GELU) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = 0.5f * v[e] * (1.f + erff(v[e] * 0.70710678118654752f));
+          for (int e = 0; e < 8; ++e) v[e] = gelu_f(v[e]);
         }
         *reinterpret_cast<uint4*>(Y + off) = pack8(v);
       } else if constexpr (EPI == 1) {
@@ -301,19 +301,30 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
         if (bs.z) {
           float zz[8];
           unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+          if (bs.zgelu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+            for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+          }
         }
         const uint4 pk = pack8(v);
         *reinterpret_cast<uint4*>(Y + off) = pk;
         if (bs.sums) {
-          float q[8], yy[8];
+          float q[8];
           unpack8(pk, q);
-          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+          if (bs.zgelu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            s1[e] += q[e];
-            s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+            for (int e = 0; e < 8; ++e) s1[e] += q[e];
+          } else {
+            float yy[8];
+            unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+            }
           }
         }
       } else {

@@ -71,30 +71,63 @@ __global__ __launch_bounds__(256) void prob_nll_kernel(const T* __restrict__ pro
                                                        float* __restrict__ loss_sum, float* __restrict__ count,
                                                        float* __restrict__ dp, int B, int NC, float eps,
                                                        int ignore_index, int per_row) {
-  const int row = blockIdx.x * blockDim.x + threadIdx.x;
+  // grid-stride over rows; the scalar sums are reduced per block in LDS so a launch issues at
+  // most 2 * gridDim same-address atomics (one per wave serialised ~28 us at B = 65536)
   float l = 0.f, c = 0.f;
-  if (row < B) {
+  for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < B; row += gridDim.x * blockDim.x) {
     const int64_t lab = labels[row];
     const bool valid = lab != ignore_index && lab >= 0 && lab < NC;
     const float p = valid ? ld(probs + (size_t)row * NC, (int)lab) : 1.f;
     const float pc = fminf(fmaxf(p, eps), 1.f);
-    l = valid ? -__logf(pc) : 0.f;
-    c = valid ? 1.f : 0.f;
+    const float lr = valid ? -__logf(pc) : 0.f;
+    const float cr = valid ? 1.f : 0.f;
     if (dp) {
       const bool pass = valid && p >= eps && p <= 1.f;
       for (int j = 0; j < NC; ++j) dp[(size_t)row * NC + j] = (pass && j == lab) ? -1.f / pc : 0.f;
     }
     if (per_row) {
-      loss_sum[row] = l;
-      count[row] = c;
+      loss_sum[row] = lr;
+      count[row] = cr;
     }
+    l += lr;
+    c += cr;
   }
   if (per_row) return;
+  __shared__ float red[2][4];
   l = warp_sum(l);
   c = warp_sum(c);
-  if ((threadIdx.x & 63) == 0 && c > 0.f) {
-    atomicAdd(loss_sum, l);
-    atomicAdd(count, c);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = l;
+    red[1][w] = c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    l = red[0][0] + red[0][1] + red[0][2] + red[0][3];
+    c = red[1][0] + red[1][1] + red[1][2] + red[1][3];
+    if (c > 0.f) {
+      atomicAdd(loss_sum, l);
+      atomicAdd(count, c);
+    }
+  }
+}
+
+// d loss / d probs of the NLL above, already scaled by the upstream gradient and 1 / count
+// (both device scalars): the backward is this one pass, no separate scale kernels
+template <typename T>
+__global__ __launch_bounds__(256) void prob_nll_grad_kernel(const T* __restrict__ probs,
+                                                            const int64_t* __restrict__ labels,
+                                                            const float* __restrict__ g, const float* __restrict__ count,
+                                                            float* __restrict__ dp, int B, int NC, float eps,
+                                                            int ignore_index) {
+  const float s = g[0] / fmaxf(count[0], 1.f);
+  for (int row = blockIdx.x * blockDim.x + threadIdx.x; row < B; row += gridDim.x * blockDim.x) {
+    const int64_t lab = labels[row];
+    const bool valid = lab != ignore_index && lab >= 0 && lab < NC;
+    const float p = valid ? ld(probs + (size_t)row * NC, (int)lab) : 1.f;
+    const bool pass = valid && p >= eps && p <= 1.f;
+    const float d = pass ? -s / fminf(fmaxf(p, eps), 1.f) : 0.f;
+    for (int j = 0; j < NC; ++j) dp[(size_t)row * NC + j] = j == lab ? d : 0.f;
   }
 }
 
@@ -300,13 +333,27 @@ extern "C" hipError_t zoo_softmax_xent(const void* logits, int is_f32, const int
 
 extern "C" hipError_t zoo_prob_nll(const void* probs, int is_f32, const int64_t* labels, float* loss_sum, float* count,
                                    float* dp, int B, int NC, float eps, int ignore_index, int per_row, hipStream_t st) {
-  const int blocks = (B + 255) / 256;
+  const int rb = (B + 255) / 256;
+  const int blocks = per_row ? rb : (rb < 128 ? rb : 128);
   if (is_f32)
     hipLaunchKernelGGL(prob_nll_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)probs, labels, loss_sum,
                        count, dp, B, NC, eps, ignore_index, per_row);
   else
     hipLaunchKernelGGL(prob_nll_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)probs, labels,
                        loss_sum, count, dp, B, NC, eps, ignore_index, per_row);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_prob_nll_grad(const void* probs, int is_f32, const int64_t* labels, const float* g,
+                                        const float* count, float* dp, int B, int NC, float eps, int ignore_index,
+                                        hipStream_t st) {
+  const int blocks = (B + 255) / 256;
+  if (is_f32)
+    hipLaunchKernelGGL(prob_nll_grad_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)probs, labels, g,
+                       count, dp, B, NC, eps, ignore_index);
+  else
+    hipLaunchKernelGGL(prob_nll_grad_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)probs, labels, g,
+                       count, dp, B, NC, eps, ignore_index);
   return hipGetLastError();
 }
 

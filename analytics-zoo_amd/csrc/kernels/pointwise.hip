@@ -34,7 +34,7 @@ ZOO_DEV float act_f(float x, int a, float alpha) {
     case PW_RELU6: return fminf(fmaxf(x, 0.f), 6.f);
     case PW_ELU: return x > 0.f ? x : alpha * (__expf(x) - 1.f);
     case PW_SELU: return 1.0507009873554805f * (x > 0.f ? x : 1.6732632423543772f * (__expf(x) - 1.f));
-    case PW_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case PW_GELU: return gelu_f(x);
     case PW_GELU_TANH: {
       const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
       return 0.5f * x * (1.f + tanhf(u));
@@ -60,10 +60,7 @@ ZOO_DEV float act_d(float x, int a, float alpha) {
     case PW_RELU6: return (x > 0.f && x < 6.f) ? 1.f : 0.f;
     case PW_ELU: return x > 0.f ? 1.f : alpha * __expf(x);
     case PW_SELU: return 1.0507009873554805f * (x > 0.f ? 1.f : 1.6732632423543772f * __expf(x));
-    case PW_GELU: {
-      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-      return cdf + x * 0.3989422804014327f * __expf(-0.5f * x * x);
-    }
+    case PW_GELU: return gelu_grad_f(x);
     case PW_GELU_TANH: {
       const float u = 0.7978845608028654f * (x + 0.044715f * x * x * x);
       const float t = tanhf(u);

@@ -23,6 +23,8 @@ hipError_t zoo_jpeg_color_resize(const uint8_t*, void*, const zoo::JpegGeom*, in
                                  int, int, hipStream_t);
 hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
                         hipStream_t);
+hipError_t zoo_prob_nll_grad(const void*, int, const int64_t*, const float*, const float*, float*, int, int, float, int,
+                             hipStream_t);
 int zoo_ncf_tier(int, int, int, int, int, int, int);
 int zoo_ncf_nwg(int, int, int, int, int, int, int);
 hipError_t zoo_ncf(const zoo::NcfArgs*, float* const*, int, hipStream_t);
@@ -278,13 +280,25 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     TORCH_CHECK(bsums->numel() == 2 * K || bsums->numel() == stat_len(K),
                 "bn sums must be [2*K] (or the slotted stat_len(K))");
     g.stat_slots = bsums->numel() == 2 * K ? 0 : zoo::kStatSlots;
-    TORCH_CHECK(by.has_value() && bmean.has_value() && binv.has_value(), "fused bn-backward needs y/mean/inv");
-    req(*by, at::kBFloat16, "bn y");
-    req(*bmean, at::kFloat, "bn mean");
-    req(*binv, at::kFloat, "bn inv");
-    TORCH_CHECK(bmean->numel() == K && binv->numel() == K, "bn mean/inv must be [K]");
     const int64_t full = g.omap ? (int64_t)g.N * g.oH * g.oW * K : (int64_t)g.M * K;
-    TORCH_CHECK(by->numel() == full, "bn y must match the output");
+    const bool gelu = !(by.has_value() && by->defined());
+    if (gelu) {
+      // GELU-backward mode: bz = the GELU pre-activation of this GEMM's output, sums = column
+      // sums of the scaled output (bias gradient of the producing linear)
+      TORCH_CHECK(bz.has_value() && bz->defined(), "gelu-backward epilogue needs the pre-activation (bz)");
+      TORCH_CHECK(bp == nullptr && act == 0, "gelu-backward epilogue: no bias / activation");
+      bs.zgelu = 1;
+    } else {
+      TORCH_CHECK(bmean.has_value() && binv.has_value(), "fused bn-backward needs y/mean/inv");
+      req(*by, at::kBFloat16, "bn y");
+      req(*bmean, at::kFloat, "bn mean");
+      req(*binv, at::kFloat, "bn inv");
+      TORCH_CHECK(bmean->numel() == K && binv->numel() == K, "bn mean/inv must be [K]");
+      TORCH_CHECK(by->numel() == full, "bn y must match the output");
+      bs.y = by->data_ptr();
+      bs.mean = bmean->data_ptr<float>();
+      bs.inv = binv->data_ptr<float>();
+    }
     if (bz.has_value() && bz->defined()) {
       req(*bz, at::kBFloat16, "bn z");
       TORCH_CHECK(bz->numel() == full, "bn z must match the output");
@@ -292,9 +306,6 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     }
     TORCH_CHECK(!stats.has_value() || !stats->defined(), "stats and fused bn-backward are exclusive");
     TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
-    bs.y = by->data_ptr();
-    bs.mean = bmean->data_ptr<float>();
-    bs.inv = binv->data_ptr<float>();
     bs.sums = bsums->data_ptr<float>();
   }
   // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
@@ -1180,6 +1191,26 @@ std::vector<torch::Tensor> prob_nll(torch::Tensor probs, torch::Tensor labels, b
   if (per_row) loss = loss.sum(1);
   if (want_grad) return {loss, dp};
   return {loss};
+}
+
+// scaled gradient of prob_nll: dprobs = -g / (max(count, 1) * clamp(p[label])) at the label
+torch::Tensor prob_nll_grad(torch::Tensor probs, torch::Tensor labels, torch::Tensor g, torch::Tensor count,
+                            double eps, int64_t ignore_index) {
+  TORCH_CHECK(probs.is_cuda() && probs.is_contiguous() && probs.dim() == 2, "prob_nll_grad: 2-D GPU probabilities");
+  TORCH_CHECK(probs.scalar_type() == at::kFloat || probs.scalar_type() == at::kBFloat16, "prob_nll_grad: dtype");
+  req(labels, at::kLong, "labels");
+  req(g, at::kFloat, "g");
+  req(count, at::kFloat, "count");
+  TORCH_CHECK(g.numel() >= 1 && count.numel() >= 1, "prob_nll_grad: scalar g / count");
+  TORCH_CHECK(labels.numel() == probs.size(0) && probs.size(0) < (1LL << 31), "prob_nll_grad: labels size");
+  const int B = probs.size(0), NC = probs.size(1);
+  auto dp = torch::empty({B, NC}, probs.options().dtype(at::kFloat));
+  if (B > 0)
+    check_hip(zoo_prob_nll_grad(probs.data_ptr(), probs.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                                g.data_ptr<float>(), count.data_ptr<float>(), dp.data_ptr<float>(), B, NC, (float)eps,
+                                (int)ignore_index, cur_stream()),
+              "prob_nll_grad");
+  return dp;
 }
 
 void check_flat(const torch::Tensor& t, const char* n, int64_t numel) {
@@ -2277,6 +2308,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("roi_pool_bwd", &roi_pool_bwd);
   m.def("ncf_fused", &ncf_fused);
   m.def("prob_nll", &prob_nll);
+  m.def("prob_nll_grad", &prob_nll_grad);
   m.def("ncf_tier", &ncf_tier);
   m.def("resize_bilinear", &resize_bilinear);
   m.def("resize_bilinear_bwd", &resize_bilinear_bwd);

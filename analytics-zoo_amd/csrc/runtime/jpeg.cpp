@@ -19,6 +19,7 @@
 #include <atomic>
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <string>
 #include <thread>
 #include <vector>
@@ -89,6 +90,46 @@ static bool build_huff(Huff& t, const uint8_t* counts, const uint8_t* vals, int 
   }
   t.present = true;
   return k == nvals;
+}
+
+// Built tables keyed by their DHT bytes (class, counts, values). Encoders reuse a handful of
+// tables (the Annex K defaults, or one optimised set per image source), so a per-thread cache
+// turns the ~10 us rebuild of each 1024-entry lookup table per image into a memcmp.
+struct HuffCache {
+  struct Entry {
+    uint8_t key[1 + 16 + 256];
+    int klen;
+    Huff h;
+  };
+  std::vector<std::unique_ptr<Entry>> e;
+  size_t next = 0;
+
+  const Huff* get(int tc, const uint8_t* counts, const uint8_t* vals, int nv) {
+    const int klen = 1 + 16 + nv;
+    for (auto& x : e)
+      if (x->klen == klen && x->key[0] == (uint8_t)tc && !memcmp(x->key + 1, counts, 16) &&
+          !memcmp(x->key + 17, vals, nv))
+        return &x->h;
+    std::unique_ptr<Entry> n(new Entry());
+    n->klen = klen;
+    n->key[0] = (uint8_t)tc;
+    memcpy(n->key + 1, counts, 16);
+    memcpy(n->key + 17, vals, nv);
+    if (!build_huff(n->h, counts, vals, nv)) return nullptr;
+    if (e.size() < 32) {
+      e.push_back(std::move(n));
+      return &e.back()->h;
+    }
+    e[next] = std::move(n);            // round-robin replacement
+    const Huff* r = &e[next]->h;
+    next = (next + 1) % e.size();
+    return r;
+  }
+};
+
+static HuffCache& huff_cache() {
+  thread_local HuffCache c;
+  return c;
 }
 
 struct Bits {
@@ -212,7 +253,8 @@ struct Decoder {
   Info info;
   uint16_t qt[4][64];
   bool qpresent[4] = {false, false, false, false};
-  Huff dct[4], act[4];
+  const Huff* dct[4] = {nullptr, nullptr, nullptr, nullptr};   // thread-local cache entries
+  const Huff* act[4] = {nullptr, nullptr, nullptr, nullptr};
   std::vector<int16_t> coef[3];   // per component [bh][bw][64] (when no external destination)
   int16_t* dst[3] = {nullptr, nullptr, nullptr};   // external zeroed destination per component
 
@@ -293,7 +335,11 @@ struct Decoder {
             int nv = 0;
             for (int i = 0; i < 16; ++i) nv += counts[i];
             if (nv > 256 || o + 17 + nv > sl) return E_TABLE;
-            if (!build_huff(tc ? act[th] : dct[th], counts, seg + o + 17, nv)) return E_TABLE;
+            if (!header_only) {   // geometry probes need no tables
+              const Huff* h = huff_cache().get(tc ? 1 : 0, counts, seg + o + 17, nv);
+              if (!h) return E_TABLE;
+              (tc ? act[th] : dct[th]) = h;
+            }
             o += 17 + nv;
           }
           break;
@@ -316,7 +362,7 @@ struct Decoder {
             if (comps[i] < 0) return E_MARKER;
             td[i] = seg[2 + 2 * i] >> 4;
             ta[i] = seg[2 + 2 * i] & 3;
-            if (td[i] > 3 || !dct[td[i]].present || !act[ta[i]].present) return E_TABLE;
+            if (td[i] > 3 || !dct[td[i]] || !act[ta[i]]) return E_TABLE;
           }
           const uint8_t* q = p + len;
           const int rc = scan(q, end, ns, comps, td, ta, &q);
@@ -355,7 +401,7 @@ struct Decoder {
       for (int by = 0; by < nby; ++by)
         for (int bx = 0; bx < nbx; ++bx) {
           if (info.restart && todo == 0 && !restart()) return E_TRUNC;
-          if (!decode_block(b, dct[td[0]], act[ta[0]], pred[0], plane(c) + ((size_t)by * info.bw[c] + bx) * 64))
+          if (!decode_block(b, *dct[td[0]], *act[ta[0]], pred[0], plane(c) + ((size_t)by * info.bw[c] + bx) * 64))
             return E_HUFF;
           --todo;
         }
@@ -368,7 +414,7 @@ struct Decoder {
             for (int v = 0; v < info.vs[c]; ++v)
               for (int h = 0; h < info.hs[c]; ++h) {
                 const size_t by = (size_t)my * info.vs[c] + v, bx = (size_t)mx * info.hs[c] + h;
-                if (!decode_block(b, dct[td[i]], act[ta[i]], pred[i], plane(c) + (by * info.bw[c] + bx) * 64))
+                if (!decode_block(b, *dct[td[i]], *act[ta[i]], pred[i], plane(c) + (by * info.bw[c] + bx) * 64))
                   return E_HUFF;
               }
           }

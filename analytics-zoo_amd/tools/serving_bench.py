@@ -118,6 +118,42 @@ class _BertTokens(torch.nn.Module):
         return self.m([tok, torch.zeros_like(tok), pos, torch.ones(b, self.L, device=tok.device)])[1]
 
 
+def _jpegs(kind, seed, n=16):
+    """16 distinct 256x256 JPEGs. ``noise``: uniform random pixels (the entropy decoder's worst
+    case, ~60 KB each); ``natural``: photo-like content -- low-frequency colour fields, soft
+    blobs and edges plus sensor-level noise, quality 90 (~2 bits / pixel, the range of ImageNet
+    JPEGs)."""
+    from PIL import Image
+    rng = np.random.default_rng(seed)
+    out = []
+    yy, xx = np.mgrid[0:256, 0:256].astype(np.float32) / 256.0
+    for _ in range(n):
+        if kind == "noise":
+            img = rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)
+            q = 75
+        else:
+            img = np.zeros((256, 256, 3), np.float32)
+            for c in range(3):
+                for _ in range(4):
+                    fx, fy, ph = rng.uniform(0.5, 4.0), rng.uniform(0.5, 4.0), rng.uniform(0, 6.28)
+                    img[..., c] += rng.uniform(10, 40) * np.sin(6.28 * (fx * xx + fy * yy) + ph)
+                img[..., c] += rng.uniform(60, 190)
+            for _ in range(6):
+                cx, cy, r = rng.uniform(0, 1), rng.uniform(0, 1), rng.uniform(0.03, 0.2)
+                blob = np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * r * r))
+                img += blob[..., None] * rng.uniform(-80, 80, 3)
+            for _ in range(3):                                   # hard edges (object boundaries)
+                a_, b_, c_ = rng.uniform(-1, 1, 3)
+                img += ((a_ * xx + b_ * yy + c_) > 0)[..., None] * rng.uniform(-40, 40, 3)
+            img += rng.normal(0, 3.0, img.shape)
+            img = np.clip(img, 0, 255).astype(np.uint8)
+            q = 90
+        buf = io.BytesIO()
+        Image.fromarray(img).save(buf, format="JPEG", quality=q)
+        out.append(buf.getvalue())
+    return out
+
+
 def run_e2e(a):
     from PIL import Image
     from zoo.common.nncontext import init_nncontext
@@ -127,12 +163,7 @@ def run_e2e(a):
     import tempfile
     init_nncontext("serving-e2e")
     srv = RespServer("127.0.0.1", 0).start()
-    rng = np.random.default_rng(0)
-    jpgs = []
-    for _ in range(16):
-        buf = io.BytesIO()
-        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
-        jpgs.append(buf.getvalue())
+    jpgs = _jpegs(a.images_kind, 0)
     try:
         with tempfile.TemporaryDirectory() as d:
             cfg = os.path.join(d, "config.yaml")
@@ -266,12 +297,7 @@ def run_openloop(a):
     from zoo.serving.resp import RespServer
     init_nncontext("serving-openloop")
     srv = RespServer("127.0.0.1", 0).start()
-    rng = np.random.default_rng(0)
-    jpgs = []
-    for _ in range(16):
-        buf = io.BytesIO()
-        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
-        jpgs.append(buf.getvalue())
+    jpgs = _jpegs(a.images_kind, 0)
     done = {}
     try:
         with tempfile.TemporaryDirectory() as d:
@@ -346,7 +372,7 @@ def run_openloop(a):
                                   "unfinished": sum(1 for u, _ in sent if u not in done),
                                   "client_procs": nproc, "duration_s": a.duration, "n_gpus": 1,
                                   "decode": "gpu-jpeg" if os.environ.get("ZOO_SERVING_GPU_JPEG", "1") != "0"
-                                  else "cpu", "data": "synthetic 256x256 JPEG"}), flush=True)
+                                  else "cpu", "data": "synthetic 256x256 JPEG (%s)" % a.images_kind}), flush=True)
                 time.sleep(1.0)
             s.stop()
     finally:
@@ -375,12 +401,7 @@ def run_dist(a):
     from zoo.common.nncontext import init_nncontext
     init_nncontext("serving-dist")
     srv = RespServer("127.0.0.1", 0).start()
-    rng = np.random.default_rng(rank)
-    jpgs = []
-    for _ in range(16):
-        buf = io.BytesIO()
-        Image.fromarray(rng.integers(0, 255, (256, 256, 3), dtype=np.uint8)).save(buf, format="JPEG")
-        jpgs.append(buf.getvalue())
+    jpgs = _jpegs(a.images_kind, rank)
     try:
         with tempfile.TemporaryDirectory() as d:
             cfg = os.path.join(d, "config.yaml")
@@ -411,7 +432,7 @@ def run_dist(a):
                                   "images_per_gpu": a.images, "throughput": round(total, 1), "unit": "records/sec",
                                   "per_gpu": [round(float(v[0]), 1) for v in allv], "n_gpus": world,
                                   "decode": "gpu-jpeg" if os.environ.get("ZOO_SERVING_GPU_JPEG", "1") != "0"
-                                  else "cpu", "data": "synthetic 256x256 JPEG"}), flush=True)
+                                  else "cpu", "data": "synthetic 256x256 JPEG (%s)" % a.images_kind}), flush=True)
     finally:
         srv.shutdown()
         srv.server_close()
@@ -426,6 +447,8 @@ def main():
                     "of the measured capacity)")
     ap.add_argument("--duration", type=float, default=8.0, help="openloop: seconds per offered rate")
     ap.add_argument("--client-rate", type=float, default=1500.0, help="openloop: records/s per client process")
+    ap.add_argument("--images-kind", default="natural", choices=["natural", "noise"],
+                    help="synthetic JPEG content: photo-like (default) or uniform noise (decoder worst case)")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--images", type=int, default=2048)
     ap.add_argument("--batch", type=int, default=64)

@@ -163,9 +163,11 @@ def _dropout(x, p, training):
 
 
 class NativeNet(nn.Module):
-    """Base: NCHW fp32 input -> NHWC bf16 -> features -> classifier."""
+    """Base: NCHW fp32 input -> NHWC bf16 -> features -> classifier. ``trace_hw``: the input
+    size the BigDL graph encoder (zoo.utils.bigdl_graph.native_graph_spec) traces at."""
 
     in_channels = 3
+    trace_hw = 224
 
     def prepare(self, x):
         return to_nhwc(x, self.in_channels, _cin_pad(self.in_channels))
@@ -200,6 +202,8 @@ class VGG(NativeNet):
 
 
 class AlexNet(NativeNet):
+    trace_hw = 227
+
     def __init__(self, num_classes=1000):
         super().__init__()
         self.features = nn.Sequential(
@@ -229,6 +233,8 @@ class _Fire(nn.Module):
 
 class SqueezeNet(NativeNet):
     """SqueezeNet 1.1."""
+
+    trace_hw = 227
 
     def __init__(self, num_classes=1000):
         super().__init__()
@@ -377,6 +383,8 @@ class _IncA(nn.Module):
 
 class InceptionV3(NativeNet):
     """Inception-v3 (stem + A blocks + grid reductions; factorised 1x7/7x1 B stage)."""
+
+    trace_hw = 299
 
     def __init__(self, num_classes=1000):
         super().__init__()

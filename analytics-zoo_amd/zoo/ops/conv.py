@@ -311,7 +311,7 @@ class _LinearNativeFn(torch.autograd.Function):
     Reference: TransformerLayer.scala:120-181 / BERT.scala Dense layers."""
 
     @staticmethod
-    def forward(ctx, x2, w, bias, act, need_grad, grad_add=None):
+    def forward(ctx, x2, w, bias, act, need_grad, grad_add=None, gelu_link=None, gelu_src=None):
         ctx.grad_add = grad_add
         if grad_add is not None and need_grad:
             grad_add.armed = True
@@ -325,6 +325,13 @@ class _LinearNativeFn(torch.autograd.Function):
             y = native().act_fwd_bwd(pre, None, 4, 0.0)
         else:
             y = _kern.conv_fwd(x4, wb, 1, 1, bias=bf, act=ACT_CODES[act]).view(-1, N)
+        ctx.gelu_link = ctx.gelu_src = None
+        if gelu_link is not None and pre is not None:
+            gelu_link.pre, gelu_link.y, gelu_link.db, gelu_link.done = pre, y, None, False
+            ctx.gelu_link = gelu_link
+        if (gelu_src is not None and need_grad and gelu_src.pre is not None and gelu_src.y is not None and
+                gelu_src.y.data_ptr() == x2.data_ptr() and gelu_src.y.shape == x2.shape):
+            ctx.gelu_src = gelu_src            # x2 IS the GELU output of the linked linear
         ctx.save_for_backward(x2, w, y if act == "relu" else None, pre)
         ctx.act, ctx.has_bias, ctx.bias_ref = act, bias is not None, bias
         return y
@@ -335,7 +342,23 @@ class _LinearNativeFn(torch.autograd.Function):
         dy = dy.to(torch.bfloat16).contiguous()
         N, K = w.shape
         dx = dw = db = None
-        if (ctx.has_bias and ctx.needs_input_grad[2]) or ctx.act in ("relu", "gelu"):
+        link = ctx.gelu_link
+        if link is not None and link.done:
+            # the consuming linear already applied GELU' in its dgrad epilogue (dy = d pre)
+            # and summed the bias gradient there
+            if ctx.has_bias and ctx.needs_input_grad[2]:
+                bias = ctx.bias_ref
+                bbuf = getattr(bias, "_zoo_grad", None)
+                if bbuf is not None:
+                    bbuf.add_(link.db)
+                    hook = getattr(bias, "_zoo_grad_ready", None)
+                    if hook is not None:
+                        hook(bias)
+                else:
+                    db = link.db.to(bias.dtype)
+            link.pre = link.y = link.db = None
+            link.done = False
+        elif (ctx.has_bias and ctx.needs_input_grad[2]) or ctx.act in ("relu", "gelu"):
             bias = ctx.bias_ref
             want_db = bool(ctx.has_bias and ctx.needs_input_grad[2])
             bbuf = getattr(bias, "_zoo_grad", None) if (want_db and bias is not None) else None
@@ -354,7 +377,16 @@ class _LinearNativeFn(torch.autograd.Function):
         if ga is not None and ga.grad is not None:
             resid = ga.grad.reshape(dy.shape[0], K).to(torch.bfloat16).contiguous()
             ga.grad, ga.armed = None, False
-        if ctx.needs_input_grad[0]:
+        src = ctx.gelu_src
+        if ctx.needs_input_grad[0] and src is not None and src.pre is not None:
+            # dgrad epilogue: d pre = (dy W^T (+ resid)) * GELU'(pre), column sums -> b1's gradient
+            wt = _kern.flip_weights(bf16_weight(w), N, 1, 1, K)
+            sums = torch.zeros(2 * K, dtype=torch.float32, device=dy.device)
+            dx = _kern.conv_fwd(dy.view(-1, 1, 1, N), wt, 1, 1,
+                                resid=None if resid is None else resid.view(-1, 1, 1, K),
+                                bstats=(src.pre.view(-1, 1, 1, K), None, None, None, sums)).view(-1, K)
+            src.db, src.done = sums[:K], True
+        elif ctx.needs_input_grad[0]:
             wt = _kern.flip_weights(bf16_weight(w), N, 1, 1, K)       # W^T [K, ceil8(N)]
             dx = _kern.conv_fwd(dy.view(-1, 1, 1, N), wt, 1, 1,
                                 resid=None if resid is None else resid.view(-1, 1, 1, K)).view(-1, K)
@@ -370,7 +402,7 @@ class _LinearNativeFn(torch.autograd.Function):
                     hook(w)
             else:
                 dw = g2.to(w.dtype)
-        return dx, dw, db, None, None, None
+        return dx, dw, db, None, None, None, None, None
 
 
 def _use_native_linear(x, Cin, K, act):
@@ -380,6 +412,9 @@ def _use_native_linear(x, Cin, K, act):
 
 
 _ADDMM_DTYPE_OK = [True]
+# GELU backward in the consuming linear's dgrad epilogue (GeluLink); ZOO_GELU_DGRAD=0 restores the
+# separate activation-backward pass
+_GELU_DGRAD = os.environ.get("ZOO_GELU_DGRAD", "1") != "0"
 _WGRAD256 = os.environ.get("ZOO_WGRAD256", "1") != "0"
 
 
@@ -426,11 +461,13 @@ def _use_blas(x, Cin, K, act):
         act in (None, "linear", "relu", "gelu")
 
 
-def linear(x, w, bias=None, act=None, grad_add=None):
+def linear(x, w, bias=None, act=None, grad_add=None, gelu_link=None, gelu_src=None):
     """y = act(x @ w^T + b). Uses the MFMA GEMM when features are 8-aligned and
     the input is on the GPU; otherwise the plain library GEMM (hipBLASLt).
     ``grad_add``: a :class:`zoo.ops.nn.GradAdd` whose residual gradient the data-gradient
-    GEMM adds (only armed on the library-GEMM path; elsewhere autograd sums as usual)."""
+    GEMM adds (only armed on the library-GEMM path; elsewhere autograd sums as usual).
+    ``gelu_link`` / ``gelu_src``: a :class:`zoo.ops.nn.GeluLink` joining a GELU linear to the
+    linear that consumes its output (native path only; ignored elsewhere)."""
     K, Cin = w.shape
     lead = x.shape[:-1]
     if x.is_cuda and (Cin % 8 or K % 8) and x.shape[-1] == Cin:
@@ -453,7 +490,8 @@ def linear(x, w, bias=None, act=None, grad_add=None):
         xb = (xb if xb.dtype == torch.bfloat16 else xb.to(torch.bfloat16)).contiguous()
         need_grad = torch.is_grad_enabled() and (x.requires_grad or w.requires_grad or
                                                   (bias is not None and bias.requires_grad))
-        y = _LinearNativeFn.apply(xb, w, bias, None if act == "linear" else act, need_grad, grad_add)
+        y = _LinearNativeFn.apply(xb, w, bias, None if act == "linear" else act, need_grad, grad_add,
+                                  gelu_link if _GELU_DGRAD else None, gelu_src if _GELU_DGRAD else None)
         return y.reshape(*lead, K).to(x.dtype)
     if x.is_cuda and Cin % 8 == 0 and K % 8 == 0 and w.shape[1] == Cin:
         x2 = x.reshape(-1, 1, 1, Cin)

@@ -39,17 +39,17 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
 class _ProbNllFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, probs, labels, eps, ignore_index, size_average):
-        outs = native().prob_nll(probs, labels, True, eps, ignore_index)
-        acc, dp = outs[0], outs[1]
-        count = acc[1].clamp_min(1.0) if size_average else torch.ones_like(acc[1])
-        ctx.save_for_backward(dp, count)
-        ctx.dtype = probs.dtype
-        return acc[0] / count
+        acc = native().prob_nll(probs, labels, False, eps, ignore_index)[0]
+        count = acc[1:2] if size_average else torch.ones_like(acc[1:2])
+        ctx.save_for_backward(probs, labels, count)
+        ctx.eps, ctx.ignore = eps, ignore_index
+        return acc[0] / count.clamp_min(1.0)[0]
 
     @staticmethod
     def backward(ctx, g):
-        dp, count = ctx.saved_tensors
-        return (dp * (g / count)).to(ctx.dtype), None, None, None, None
+        probs, labels, count = ctx.saved_tensors
+        dp = native().prob_nll_grad(probs, labels, g.float().reshape(1).contiguous(), count, ctx.eps, ctx.ignore)
+        return dp.to(probs.dtype), None, None, None, None
 
 
 def prob_nll(probs, labels, eps=1e-7, ignore_index=-100, size_average=True):

@@ -94,13 +94,30 @@ def ncf_fused(ids, dims, tu, ti, tmu, tmi, w1, b1, w2, b2, w3, b3, wo, bo):
                         w3, b3, wo, bo)
 
 
-def ncf_reference(ids, tu, ti, tmu, tmi, w1, b1, w2, b2, w3, b3, wo, bo, id_off=0):
-    """Plain fp32 PyTorch NeuralCF forward (same math as the kernel; CPU / parity tests)."""
+class _Bf16Stage(torch.autograd.Function):
+    """Round to bf16 in the forward AND the backward: the kernel parks activations and staged
+    gradients as bf16 LDS rows (csrc/kernels/ncf.hip), this replays that rounding in fp32."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.bfloat16().float()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.bfloat16().float()
+
+
+def ncf_reference(ids, tu, ti, tmu, tmi, w1, b1, w2, b2, w3, b3, wo, bo, id_off=0, bf16_stage=False):
+    """Plain fp32 PyTorch NeuralCF forward (same math as the kernel; CPU / parity tests).
+    ``bf16_stage``: round at the points where the kernel stages through bf16 (gathered rows,
+    hidden activations and their pre-activation gradients) -- the
+    emulated-bf16 baseline the kernel's gradient noise is measured against."""
+    st = _Bf16Stage.apply if bf16_stage else (lambda t: t)
     u = ids[:, 0].long() - id_off
     i = ids[:, 1].long() - id_off
-    h = torch.cat([F.embedding(u, tu.float()), F.embedding(i, ti.float())], 1)
+    h = st(torch.cat([F.embedding(u, tu.float()), F.embedding(i, ti.float())], 1))
     for w, b in ((w1, b1), (w2, b2), (w3, b3)):
-        h = torch.relu(F.linear(h, w.float(), None if b is None else b.float()))
+        h = torch.relu(st(F.linear(h, w.float(), None if b is None else b.float())))
     if tmu is not None:
-        h = torch.cat([h, F.embedding(u, tmu.float()) * F.embedding(i, tmi.float())], 1)
+        h = torch.cat([h, st(F.embedding(u, tmu.float()) * F.embedding(i, tmi.float()))], 1)
     return torch.softmax(F.linear(h, wo.float(), None if bo is None else bo.float()), -1)

@@ -68,6 +68,21 @@ class GradAdd:
         self.armed, self.grad = False, None
 
 
+class GeluLink:
+    """GELU-backward handoff between the two linears of a Transformer FFN
+    (``m = linear(n, W1, b1, act="gelu", gelu_link=l); out = linear(m, W2, b2, gelu_src=l)``):
+    the first parks its bf16 pre-activation here in forward; the second's backward runs its
+    data-gradient GEMM with the GELU derivative applied in the epilogue (and the first's bias
+    gradient as the epilogue's column sums), so it returns d pre instead of d m and the first
+    skips its activation-backward pass. Valid because m has no other consumer in the block.
+    Reference: the FFN of TransformerLayer.scala:129-181."""
+    __slots__ = ("pre", "y", "db", "done")
+
+    def __init__(self):
+        self.pre = self.y = self.db = None
+        self.done = False
+
+
 class _DropoutAddFn(torch.autograd.Function):
     """out = x + dropout(a): one native pass; the keep-mask is a counter-based hash of a
     per-call seed, so backward regenerates it (no mask tensor is stored)."""

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from zoo import ops
 from zoo.ops.attention import attention_packed
-from zoo.ops.nn import GradAdd, dropout_add
+from zoo.ops.nn import GeluLink, GradAdd, dropout_add
 from zoo.pipeline.api.keras.base import Layer
 
 
@@ -75,10 +75,11 @@ class _Block(nn.Module):
         n = ops.layer_norm(dropout_add(a, x, self.hidden_drop, self.training, grad_add=h1), self.ln1_g, self.ln1_b,
                            self.ln_eps)
         act = "gelu" if self.gelu == "erf" else None
-        m = ops.linear(n, self.fc1_w, self.fc1_b, act=act, grad_add=h2)
+        gl = GeluLink() if act == "gelu" else None      # GELU backward in fc2's dgrad epilogue
+        m = ops.linear(n, self.fc1_w, self.fc1_b, act=act, grad_add=h2, gelu_link=gl)
         if self.gelu != "erf":  # GPT tanh approximation
             m = 0.5 * m * (1 + torch.tanh(math.sqrt(2 / math.pi) * (m + 0.044715 * m * m * m)))
-        m = ops.linear(m, self.fc2_w, self.fc2_b)
+        m = ops.linear(m, self.fc2_w, self.fc2_b, gelu_src=gl)
         return ops.layer_norm(dropout_add(m, n, self.hidden_drop, self.training, grad_add=h2), self.ln2_g,
                               self.ln2_b, self.ln_eps)
 

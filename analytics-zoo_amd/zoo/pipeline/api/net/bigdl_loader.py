@@ -31,7 +31,8 @@ def _conv(spec, st):
     sw, sh = a.get("strideW", 1), a.get("strideH", 1)
     pw, ph = a.get("padW", 0), a.get("padH", 0)
     same = pw == -1 or ph == -1
-    conv = nn.Conv2d(n_in, n_out, (kh, kw), (sh, sw), 0 if same else (ph, pw), groups=g,
+    dil = (int(a.get("dilationH", 1) or 1), int(a.get("dilationW", 1) or 1))
+    conv = nn.Conv2d(n_in, n_out, (kh, kw), (sh, sw), 0 if same else (ph, pw), dilation=dil, groups=g,
                      bias=spec.bias is not None and a.get("withBias", True) is not False)
     with torch.no_grad():
         conv.weight.copy_(_t(spec.weight, st).reshape(conv.weight.shape))
@@ -112,7 +113,7 @@ def convert(spec, st):
     a = spec.attr
     if t == "Linear":
         return _linear(spec, st), False
-    if t in ("SpatialConvolution", "SpatialShareConvolution"):
+    if t in ("SpatialConvolution", "SpatialShareConvolution", "SpatialDilatedConvolution"):
         return _conv(spec, st), False
     if t == "SpatialMaxPooling":
         return _pool(spec, "max"), False
@@ -133,6 +134,11 @@ def convert(spec, st):
               "SoftSign": F.softsign, "Abs": torch.abs, "Exp": torch.exp, "Log": torch.log, "Sqrt": torch.sqrt,
               "Square": torch.square, "HardTanh": lambda x: torch.clamp(x, -1, 1)}[t]
         return G.Fn(fn, t), False
+    if t == "Input":
+        return G.Fn(lambda x: x, t), False
+    if t == "Narrow":
+        d, off, ln = int(a.get("dimension", 1)), int(a.get("offset", 1)), int(a.get("length", 1))
+        return G.Fn(lambda x: x.narrow(d - 1, off - 1, ln if ln > 0 else x.shape[d - 1] - off + 2 + ln), t), False
     if t == "LeakyReLU":
         ns = float(a.get("negval", 0.01))
         return G.Fn(lambda x: F.leaky_relu(x, ns), t), False

@@ -357,6 +357,8 @@ def model_to_bytes(model, extra_attr=None):
         # a real BigDL nn graph (SpatialConvolution / SpatialBatchNormalization / CAddTable / ...),
         # not an opaque TorchModel blob (zoo.utils.bigdl_graph)
         spec = bigdl_graph.resnet_graph_spec(model)
+    elif bigdl_graph.is_native_net(model):
+        spec = bigdl_graph.native_graph_spec(model)
     else:
         spec = _keras_spec(model) if isinstance(model, Layer) and hasattr(model, "_init_args") or \
             type(model).__name__ in ("Sequential", "Model") and isinstance(model, Layer) else _torch_spec(model)
@@ -684,6 +686,8 @@ def load_bigdl_model(path, model=None):
         from zoo.utils import bigdl_graph
         if bigdl_graph.is_resnet(model):
             return bigdl_graph.restore_resnet(model, root, st)
+        if bigdl_graph.is_native_net(model):
+            return bigdl_graph.restore_native(model, root, st)
     if root.type == TORCH_MODEL:
         sd = {n: torch.from_numpy(tr.materialize(st, native=True)) for n, tr in zip(root.attr["zoo_param_names"], root.parameters)}
         if model is None:

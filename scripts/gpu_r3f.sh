@@ -3,7 +3,7 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T="timeout -k 10"
-$T 600 python -u -m pytest tests/test_ncf_fused.py tests/test_gpu_native_nets.py tests/test_gpu_zoo_kernels.py -v --timeout 300 --timeout-method thread > gpurun_out/t_r3f.log 2>&1
+$T 600 python -u -m pytest tests/test_ncf_fused.py tests/test_jpeg.py tests/test_gpu_native_nets.py tests/test_gpu_zoo_kernels.py -v --timeout 300 --timeout-method thread > gpurun_out/t_r3f.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|logits rel" gpurun_out/t_r3f.log | tail -24
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 $T 300 python -u bench.py --model ncf --batch 65536 --steps 50 --warmup 10 > gpurun_out/bench_ncf_f.log 2>&1 || exit 4

@@ -225,3 +225,92 @@ def test_resnet50_checkpoint_roundtrip_through_bigdl_graph(tmp_path):
         ref = m(x)
         assert torch.allclose(load_bigdl(p)(x), ref, rtol=1e-3, atol=1e-4)
         assert torch.allclose(m2(x), ref, rtol=1e-5, atol=1e-6)
+
+
+def _native_roundtrip(tmp_path, m, hw, classes):
+    """save as a BigDL StaticGraph -> (a) Net.load_bigdl rebuilds an NCHW fp32 torch graph with the
+    same forward, (b) load_bigdl_model restores every tensor into a fresh net by module path."""
+    import copy
+    import torch
+    from zoo.pipeline.api.net.bigdl_loader import load_bigdl
+    from zoo.utils.bigdl_model import load_bigdl_model, save_bigdl_model
+    from zoo.utils.bigdl_proto import load_bigdl_spec
+    with torch.no_grad():
+        for mod in m.modules():
+            if hasattr(mod, "running_mean"):
+                mod.running_mean.uniform_(-0.1, 0.1)
+                mod.running_var.uniform_(0.5, 1.5)
+                mod.beta.uniform_(-0.1, 0.1)
+    m.eval()
+    p = str(tmp_path / "model.1")
+    save_bigdl_model(m, p)
+    spec, _ = load_bigdl_spec(p)
+    kinds = {s.short_type for s in spec.submodules}
+    assert spec.short_type == "StaticGraph" and "TorchModel" not in kinds
+    x = torch.randn(2, 3, hw, hw)
+    fresh = copy.deepcopy(m)
+    with torch.no_grad():
+        for t in fresh.parameters():
+            t.normal_()
+        ref = m(x).float()
+        got = load_bigdl(p)(x).float()
+        assert got.shape == (2, classes)
+        assert ((got - ref).norm() / ref.norm()).item() < 1e-4
+        load_bigdl_model(p, model=fresh)
+        assert torch.equal(fresh(x).float(), ref)
+    return kinds
+
+
+@pytest.mark.parametrize("name,hw", [("mobilenet", 96), ("mobilenet-v2", 96), ("squeezenet", 99),
+                                     ("inception-v1", 96)])
+def test_native_backbones_as_bigdl_graphs(tmp_path, name, hw, monkeypatch):
+    import torch
+    from zoo.models.image.imageclassification.nets import build
+    torch.manual_seed(0)
+    m = build(name, 10)
+    m.trace_hw = hw
+    kinds = _native_roundtrip(tmp_path, m, hw, 10)
+    assert "SpatialConvolution" in kinds
+    if name.startswith("mobilenet"):        # depthwise = grouped SpatialConvolution
+        from zoo.utils.bigdl_proto import load_bigdl_spec
+        spec, _ = load_bigdl_spec(str(tmp_path / "model.1"))
+        assert any(s.short_type == "SpatialConvolution" and s.attr.get("nGroup", 1) > 1 for s in spec.submodules)
+    if name in ("squeezenet", "inception-v1"):
+        assert "JoinTable" in kinds
+
+
+def test_small_densenet_as_bigdl_graph(tmp_path):
+    import torch
+    from zoo.models.image.native_nets import DenseNet
+    torch.manual_seed(0)
+    m = DenseNet(num_classes=7, growth=8, blocks=(2, 2), init_features=16, bn_size=2)
+    m.trace_hw = 64
+    _native_roundtrip(tmp_path, m, 64, 7)
+
+
+def test_flatten_dense_glue_as_bigdl_graph(tmp_path):
+    """VGG/AlexNet-style head (NHWC flatten -> dropout -> Dense, ReLU glue) and an Inception-v3
+    style residual add: the Linear weight is permuted to BigDL's NCHW flatten order."""
+    import torch
+    from zoo.models.image import native_nets as nn_
+    from zoo.models.image.resnet import Dense
+
+    class Tiny(nn_.NativeNet):
+        trace_hw = 16
+
+        def __init__(self):
+            super().__init__()
+            self.c1 = nn_.CB(nn_._cin_pad(3), 12, 3, 1, 1)
+            self.c2 = nn_.CBR(12, 12, 3, 1, 1, relu=False)
+            self.pool = nn_.MaxPool(2, 2)
+            self.fc1, self.fc2 = Dense(12 * 8 * 8, 20), Dense(20, 5)
+
+        def forward(self, x):
+            h = self.c1(self.prepare(x))
+            h = torch.relu(h + self.c2(h))
+            h = self.pool(h).reshape(x.shape[0], -1)
+            h = torch.relu(self.fc1(nn_._dropout(h, 0.5, self.training)))
+            return self.fc2(h)
+    torch.manual_seed(0)
+    kinds = _native_roundtrip(tmp_path, Tiny(), 16, 5)
+    assert {"CAddTable", "View", "Dropout", "Linear"} <= kinds

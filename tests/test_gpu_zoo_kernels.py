@@ -15,7 +15,11 @@ def rel(a, b):
 
 
 @pytest.mark.parametrize("C,H,k,stride,pad", [(32, 14, 3, 1, 1), (96, 15, 3, 2, 1), (144, 8, 3, 1, 0),
-                                              (64, 9, 1, 1, 0), (40, 10, 2, 2, 0)])
+                                              (64, 9, 1, 1, 0), (40, 10, 2, 2, 0),
+                                              # sliding-window 3x3 wgrad: wide rows, 2-channel-chunk
+                                              # groups, 1024 / 960 channels on 7x7, odd sizes
+                                              (32, 112, 3, 1, 1), (8, 57, 3, 2, 1), (1024, 7, 3, 1, 1),
+                                              (960, 7, 3, 1, 1), (24, 113, 3, 2, 1)])
 def test_depthwise_conv_fwd_bwd(gpu, C, H, k, stride, pad):
     from zoo.ops.nn import depthwise_conv2d_nhwc
     N = 3
@@ -33,6 +37,21 @@ def test_depthwise_conv_fwd_bwd(gpu, C, H, k, stride, pad):
     yr.backward(dy.float().permute(0, 3, 1, 2))
     assert rel(xg.grad, xr.grad.permute(0, 2, 3, 1)) < 1e-2
     assert rel(w.grad, wr.grad.reshape(C, k * k).t()) < 1e-2
+
+
+def test_depthwise_wgrad_deterministic(gpu):
+    from zoo.ops.nn import depthwise_conv2d_nhwc
+    x = torch.randn(8, 56, 56, 128, device=gpu).bfloat16()
+    dy = torch.randn(8, 56, 56, 128, device=gpu).bfloat16()
+    grads = []
+    for _ in range(2):
+        w = torch.randn(9, 128, device=gpu).requires_grad_(True)
+        torch.manual_seed(0)
+        with torch.no_grad():
+            w.copy_(torch.randn(9, 128, device=gpu))
+        depthwise_conv2d_nhwc(x, w, kernel=(3, 3), stride=(1, 1), pad=(1, 1)).backward(dy)
+        grads.append(w.grad.clone())
+    assert torch.equal(grads[0], grads[1])
 
 
 def test_depthwise_conv_relu_bias(gpu):

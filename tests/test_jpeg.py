@@ -66,7 +66,9 @@ def test_gpu_decode_matches_reference(gpu, hw, kw):
     ref = jpeg.coeffs_to_rgb(d, 0).astype(int)
     got = out.cpu().numpy().astype(int)
     assert got.shape == (2, hw[0], hw[1], 3)
-    assert np.abs(got[0] - ref).max() <= 1 and (got[0] != ref).mean() < 0.01
+    # fp32 device math vs the fp64 twin: a chroma sample on a rounding boundary moves by 1 and
+    # the 1.772 / 1.402 YCbCr coefficients carry that to a 2 in R or B
+    assert np.abs(got[0] - ref).max() <= 2 and (got[0] != ref).mean() < 0.01
     assert torch.equal(out[0], out[1])
 
 

@@ -86,15 +86,23 @@ def test_fused_matches_fp32_reference(gpu, mf, B):
     lr.backward()
     rel = ((p.float().cpu() - pr).norm() / pr.norm()).item()
     assert rel < 1e-2, rel
-    gg, gr = _grads(g), _grads(cpu)
+    # the emulated-bf16 twin: same model, rounded where the kernel stages through bf16
+    emu = copy.deepcopy(m)
+    pe = ncf_reference(x, *_ref_args(emu), bf16_stage=True)
+    torch.nn.functional.nll_loss(torch.log(pe.clamp_min(1e-7)), y).backward()
+    gg, gr, ge = _grads(g), _grads(cpu), _grads(emu)
     for n, a in gr.items():
         if a is None:
             continue
         b = gg[n]
         assert b is not None, n
         e = ((b - a).norm() / a.norm().clamp_min(1e-12)).item()
-        # embedding rows get dZ back-propagated through three bf16-staged layers
-        assert e < (6e-2 if "embeddings" in n else 3e-2), (n, e)
+        e_emu = ((ge[n] - a).norm() / a.norm().clamp_min(1e-12)).item()
+        # per-record bf16 staging noise (ReLU mask flips, rounded dZ rows) adds up as sqrt(B)
+        # against a gradient that grows as B: at small batches the kernel is held to the
+        # emulated-bf16 error, not to a fixed bound
+        tol = 6e-2 if "embeddings" in n else 3e-2
+        assert e < max(tol, 2.0 * e_emu) and e < 0.2, (n, e, e_emu)
 
 
 @gpu_mark
