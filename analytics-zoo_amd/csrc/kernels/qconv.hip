@@ -17,12 +17,24 @@
 //     where colscale = s_in * s_w[c] / s_out, bias = folded-BN bias / s_out and
 //     rscale = s_resid / s_out (all precomputed on the host from calibration), so an int8
 //     output is round-to-nearest + saturate of v.
+//
+// FP8 (OCP e4m3fn) twin, same kernel body: the operands are e4m3 bytes (per-channel weight
+// scale = amax / 448, calibrated per-tensor activation scales), the 128-byte k-step feeds ONE
+// v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales) per fragment pair instead of two i8
+// MFMAs -- the K=128 scaled form is the one that runs at the fp8 peak (2x bf16, MI355X_MICROARCH
+// "FP8"); a lane's 32 operand bytes are the two consecutive 16-byte chunks 2(l>>4), 2(l>>4)+1 of
+// the row (A and B use the same k map, so the reduction pairs them correctly). fp32
+// accumulation; the epilogue converts with the hardware e4m3 conversion after clamping to
+// +-448 (e4m3fn has no infinity).
+#include <type_traits>
+
 #include "common.h"
 #include "geom.h"
 
 namespace zoo {
 
 typedef int qi32x4 __attribute__((ext_vector_type(4)));
+typedef int qi32x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void q_lds_void;
 typedef __attribute__((address_space(1))) const void q_gl_void;
 
@@ -36,7 +48,25 @@ ZOO_DEV int8_t q_sat(float v) {
   return (int8_t)(r > 127.f ? 127.f : (r < -127.f ? -127.f : r));
 }
 
-template <bool IS1x1, int BN>
+// 4 floats -> 4 OCP e4m3fn bytes (round to nearest even, clamped to the finite range)
+ZOO_DEV uint32_t f8_pack4(float a, float b, float c, float d) {
+  a = fminf(fmaxf(a, -448.f), 448.f);
+  b = fminf(fmaxf(b, -448.f), 448.f);
+  c = fminf(fmaxf(c, -448.f), 448.f);
+  d = fminf(fmaxf(d, -448.f), 448.f);
+  int w = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+  w = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, w, true);
+  return (uint32_t)w;
+}
+
+ZOO_DEV void f8_unpack4(uint32_t w, float* f) {
+  f[0] = __builtin_amdgcn_cvt_f32_fp8((int)w, 0);
+  f[1] = __builtin_amdgcn_cvt_f32_fp8((int)w, 1);
+  f[2] = __builtin_amdgcn_cvt_f32_fp8((int)w, 2);
+  f[3] = __builtin_amdgcn_cvt_f32_fp8((int)w, 3);
+}
+
+template <bool IS1x1, int BN, bool FP8>
 __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict__ X, const int8_t* __restrict__ Wm,
                                                       void* __restrict__ Y, const float* __restrict__ colscale,
                                                       const float* __restrict__ bias,
@@ -120,16 +150,41 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
     }
   };
 
-  qi32x4 acc[NI][NJ];
+  typedef typename std::conditional<FP8, f32x4, qi32x4>::type acc_t;
+  acc_t acc[NI][NJ];
 #pragma unroll
   for (int i = 0; i < NI; ++i)
 #pragma unroll
-    for (int j = 0; j < NJ; ++j) acc[i][j] = qi32x4{0, 0, 0, 0};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = acc_t{0, 0, 0, 0};
   const int fr = lane & 15, fq = lane >> 4;
 
   auto compute = [&](int buf) {
     const int8_t* a = As + buf * BM * BK;
     const int8_t* b = Bs + buf * BN * BK;
+    if constexpr (FP8) {
+      qi32x8 af[NI], bfg[NJ];
+      const int c0 = 2 * fq, c1 = 2 * fq + 1;
+#pragma unroll
+      for (int i = 0; i < NI; ++i) {
+        const int row = wm * 64 + i * 16 + fr;
+        const qi32x4 lo = *reinterpret_cast<const qi32x4*>(a + row * BK + ((c0 ^ qc_swz(row)) << 4));
+        const qi32x4 hi = *reinterpret_cast<const qi32x4*>(a + row * BK + ((c1 ^ qc_swz(row)) << 4));
+        af[i] = qi32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int row = wn * WN + j * 16 + fr;
+        const qi32x4 lo = *reinterpret_cast<const qi32x4*>(b + row * BK + ((c0 ^ qc_swz(row)) << 4));
+        const qi32x4 hi = *reinterpret_cast<const qi32x4*>(b + row * BK + ((c1 ^ qc_swz(row)) << 4));
+        bfg[j] = qi32x8{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      }
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af[i], bfg[j], acc[i][j], 0, 0, 0, 0, 0, 0);
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       const int chunk = kk * 4 + fq;
@@ -147,7 +202,9 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
 #pragma unroll
       for (int i = 0; i < NI; ++i)
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bfg[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (!FP8) acc[i][j] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[i], bfg[j], acc[i][j], 0, 0, 0);
+        }
     }
   };
 
@@ -191,10 +248,18 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
                   hi.x + bv[4], hi.y + bv[5], hi.z + bv[6], hi.w + bv[7]};
     if (resid) {
       const uint2 rq = *reinterpret_cast<const uint2*>(resid + off);
+      if constexpr (FP8) {
+        float r[8];
+        f8_unpack4(rq.x, r);
+        f8_unpack4(rq.y, r + 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        v[e] += (float)(int8_t)(rq.x >> (8 * e)) * rscale;
-        v[4 + e] += (float)(int8_t)(rq.y >> (8 * e)) * rscale;
+        for (int e = 0; e < 8; ++e) v[e] += r[e] * rscale;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[e] += (float)(int8_t)(rq.x >> (8 * e)) * rscale;
+          v[4 + e] += (float)(int8_t)(rq.y >> (8 * e)) * rscale;
+        }
       }
     }
     if (relu) {
@@ -203,6 +268,9 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
     }
     if (out_bf16) {
       *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Y) + off) = pack8(v);
+    } else if constexpr (FP8) {
+      *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(Y) + off) =
+          make_uint2(f8_pack4(v[0], v[1], v[2], v[3]), f8_pack4(v[4], v[5], v[6], v[7]));
     } else {
       uint2 pk;
       pk.x = (uint32_t)(uint8_t)q_sat(v[0]) | ((uint32_t)(uint8_t)q_sat(v[1]) << 8) |
@@ -231,7 +299,25 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const bf16_t* __restri
   }
 }
 
-// global average pool of an int8 NHWC tensor -> bf16 [N][C] (dequantised with `scale`)
+// bf16 -> e4m3 with one per-tensor inverse scale
+__global__ __launch_bounds__(256) void quantize_f8_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
+                                                          size_t n16, float inv_scale) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
+    float a[8], b[8];
+    unpack8(reinterpret_cast<const uint4*>(x)[2 * i], a);
+    unpack8(reinterpret_cast<const uint4*>(x)[2 * i + 1], b);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[e] *= inv_scale;
+      b[e] *= inv_scale;
+    }
+    reinterpret_cast<uint4*>(q)[i] = make_uint4(f8_pack4(a[0], a[1], a[2], a[3]), f8_pack4(a[4], a[5], a[6], a[7]),
+                                                f8_pack4(b[0], b[1], b[2], b[3]), f8_pack4(b[4], b[5], b[6], b[7]));
+  }
+}
+
+// global average pool of an int8 (FP8: e4m3) NHWC tensor -> bf16 [N][C] (dequantised with `scale`)
+template <bool FP8>
 __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ X, bf16_t* __restrict__ Y, int N,
                                                      int HW, int C, float scale) {
   const int cpr = C >> 3;
@@ -241,10 +327,18 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
     const int8_t* base = X + (size_t)n * HW * C + chunk * 8;
     for (int s = 0; s < HW; ++s) {
       const uint2 v = *reinterpret_cast<const uint2*>(base + (size_t)s * C);
+      if constexpr (FP8) {
+        float f[8];
+        f8_unpack4(v.x, f);
+        f8_unpack4(v.y, f + 4);
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        acc[e] += (float)(int8_t)(v.x >> (8 * e));
-        acc[4 + e] += (float)(int8_t)(v.y >> (8 * e));
+        for (int e = 0; e < 8; ++e) acc[e] += f[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          acc[e] += (float)(int8_t)(v.x >> (8 * e));
+          acc[4 + e] += (float)(int8_t)(v.y >> (8 * e));
+        }
       }
     }
     const float k = scale / (float)HW;
@@ -254,7 +348,7 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
   }
 }
 
-template <bool IS1x1, int BN>
+template <bool IS1x1, int BN, bool FP8>
 static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const float* cs, const float* bias,
                             const int8_t* resid, float rscale, const ConvGeom& g, int relu, int out_bf16,
                             hipStream_t st) {
@@ -265,11 +359,11 @@ static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const flo
   static bool attr = false;
   if (!attr) {
     const size_t mx = (size_t)2 * (QC_BM + BN) * QC_BK > epi_b ? (size_t)2 * (QC_BM + BN) * QC_BK : epi_b;
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&qconv_kernel<IS1x1, BN>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&qconv_kernel<IS1x1, BN, FP8>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)mx);
     attr = true;
   }
-  hipLaunchKernelGGL((qconv_kernel<IS1x1, BN>), dim3(tiles), dim3(QC_NT), smem, st, X, W, Y, cs, bias, resid, rscale,
+  hipLaunchKernelGGL((qconv_kernel<IS1x1, BN, FP8>), dim3(tiles), dim3(QC_NT), smem, st, X, W, Y, cs, bias, resid, rscale,
                      g, relu, out_bf16);
   return hipGetLastError();
 }
@@ -278,9 +372,9 @@ static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const flo
 
 using namespace zoo;
 
-// g: geometry in int8 elements (C, Ktot = R*S*C, ldb all multiples of 16)
+// g: geometry in int8 elements (C, Ktot = R*S*C, ldb all multiples of 16); fp8: e4m3 operands
 extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const float* colscale, const float* bias,
-                                const void* resid, float rscale, const ConvGeom* g, int relu, int out_bf16,
+                                const void* resid, float rscale, const ConvGeom* g, int relu, int out_bf16, int fp8,
                                 hipStream_t st) {
   const int8_t* x = (const int8_t*)X;
   const int8_t* w = (const int8_t*)W;
@@ -289,11 +383,17 @@ extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const flo
                      g->H == g->P && g->W == g->Q;
   const long tiles64 = (long)((g->M + QC_BM - 1) / QC_BM) * ((g->K + 63) / 64);
   const bool wide = g->K > 64 && tiles64 < 1536;   // few tiles: 128-wide n tiles fill the chip better
-  if (is1x1)
-    return wide ? launch_qc<true, 128>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)
-                : launch_qc<true, 64>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);
-  return wide ? launch_qc<false, 128>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)
-              : launch_qc<false, 64>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);
+#define ZOO_QC(F8)                                                                                                 \
+  do {                                                                                                             \
+    if (is1x1)                                                                                                     \
+      return wide ? launch_qc<true, 128, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)           \
+                  : launch_qc<true, 64, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);           \
+    return wide ? launch_qc<false, 128, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)            \
+                : launch_qc<false, 64, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);            \
+  } while (0)
+  if (fp8) ZOO_QC(true);
+  ZOO_QC(false);
+#undef ZOO_QC
 }
 
 extern "C" hipError_t zoo_quantize_i8(const void* x, void* q, size_t n, float inv_scale, hipStream_t st) {
@@ -305,9 +405,22 @@ extern "C" hipError_t zoo_quantize_i8(const void* x, void* q, size_t n, float in
   return hipGetLastError();
 }
 
-extern "C" hipError_t zoo_gap_i8(const void* x, void* y, int N, int HW, int C, float scale, hipStream_t st) {
+extern "C" hipError_t zoo_quantize_f8(const void* x, void* q, size_t n, float inv_scale, hipStream_t st) {
+  const size_t n16 = n / 16;
+  size_t blocks = (n16 + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(quantize_f8_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, st, (const bf16_t*)x, (int8_t*)q,
+                     n16, inv_scale);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_gap_i8(const void* x, void* y, int N, int HW, int C, float scale, int fp8, hipStream_t st) {
   int blocks = (N * (C / 8) + 255) / 256;
-  hipLaunchKernelGGL(gap_i8_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x, (bf16_t*)y, N,
-                     HW, C, scale);
+  if (fp8)
+    hipLaunchKernelGGL(gap_i8_kernel<true>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
+                       (bf16_t*)y, N, HW, C, scale);
+  else
+    hipLaunchKernelGGL(gap_i8_kernel<false>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
+                       (bf16_t*)y, N, HW, C, scale);
   return hipGetLastError();
 }

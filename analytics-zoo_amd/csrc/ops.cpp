@@ -132,9 +132,10 @@ hipError_t zoo_sparse_linear_fwd(const int64_t*, const int64_t*, const float*, c
 hipError_t zoo_sparse_linear_bwd(const int64_t*, const int64_t*, const float*, const float*, float*, float*, int64_t,
                                  int, int, int, hipStream_t);
 hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*, const void*, float, const ConvGeom*,
-                     int, int, hipStream_t);
+                     int, int, int, hipStream_t);
 hipError_t zoo_quantize_i8(const void*, void*, size_t, float, hipStream_t);
-hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, hipStream_t);
+hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, int, hipStream_t);
+hipError_t zoo_quantize_f8(const void*, void*, size_t, float, hipStream_t);
 hipError_t zoo_act(const void*, const void*, void*, size_t, int, int, float, hipStream_t);
 hipError_t zoo_dropout(const void*, void*, size_t, int, float, uint64_t, hipStream_t);
 hipError_t zoo_loss(const void*, const void*, void*, float*, size_t, int, int, float, float, hipStream_t);
@@ -1530,8 +1531,11 @@ torch::Tensor box_decode(torch::Tensor loc, torch::Tensor priors, double v0, dou
 torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw,
                     torch::Tensor colscale, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
                     double rscale, bool relu, bool out_bf16) {
-  req(x, at::kChar, "x");
-  req(w, at::kChar, "w");
+  // int8 or OCP fp8 e4m3 operands (the fp8 twin of the kernel); both operands the same format
+  const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
+  const auto qt = fp8 ? at::kFloat8_e4m3fn : at::kChar;
+  req(x, qt, "x");
+  req(w, qt, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "qconv: x NHWC 4-D, w 2-D [K, ldb]");
   const int C = x.size(3), K = w.size(0), ldb = w.size(1);
   TORCH_CHECK(C % 16 == 0, "qconv: input channels must be a multiple of 16, got ", C);
@@ -1553,13 +1557,13 @@ torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int 
   }
   const void* rp = nullptr;
   if (resid.has_value() && resid->defined()) {
-    req(*resid, at::kChar, "resid");
+    req(*resid, qt, "resid");
     TORCH_CHECK(resid->numel() == (int64_t)g.M * K, "qconv: resid must match the output");
     rp = resid->data_ptr();
   }
-  auto y = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(out_bf16 ? at::kBFloat16 : at::kChar));
+  auto y = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(out_bf16 ? at::kBFloat16 : qt));
   check_hip(zoo_qconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), colscale.data_ptr<float>(), bp, rp, (float)rscale,
-                      &g, relu, out_bf16, cur_stream()),
+                      &g, relu, out_bf16, fp8 ? 1 : 0, cur_stream()),
             "qconv");
   return y;
 }
@@ -1572,12 +1576,21 @@ torch::Tensor quantize_i8(torch::Tensor x, double inv_scale) {
   return q;
 }
 
+torch::Tensor quantize_f8(torch::Tensor x, double inv_scale) {
+  req(x, at::kBFloat16, "x");
+  TORCH_CHECK(x.numel() % 16 == 0, "quantize_f8: numel must be a multiple of 16");
+  auto q = torch::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
+  check_hip(zoo_quantize_f8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, cur_stream()), "quantize_f8");
+  return q;
+}
+
 torch::Tensor gap_i8(torch::Tensor x, double scale) {
-  req(x, at::kChar, "x");
+  const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
+  req(x, fp8 ? at::kFloat8_e4m3fn : at::kChar, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap_i8: NHWC with C % 8 == 0");
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
   auto y = torch::empty({N, C}, x.options().dtype(at::kBFloat16));
-  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, cur_stream()), "gap_i8");
+  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, fp8 ? 1 : 0, cur_stream()), "gap_i8");
   return y;
 }
 
@@ -2287,6 +2300,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("box_decode", &box_decode);
   m.def("quantize_i8", &quantize_i8);
   m.def("gap_i8", &gap_i8);
+  m.def("quantize_f8", &quantize_f8);
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("sparse_linear_fwd", &sparse_linear_fwd);

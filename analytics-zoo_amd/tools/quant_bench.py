@@ -1,6 +1,6 @@
-"""ResNet-50 inference throughput: bf16 (fused conv+BN kernels) vs static int8
-(zoo.ops.qresnet, implicit-GEMM int8 conv on the i8 matrix cores) vs the dynamic int8
-path of zoo.ops.quant (im2col + GEMM), plus the int8-vs-bf16 logit agreement.
+"""ResNet-50 inference throughput: bf16 (fused conv+BN kernels) vs static int8 and static OCP
+fp8 e4m3 (zoo.ops.qresnet, implicit-GEMM conv on the i8 / fp8 matrix cores) vs the dynamic int8
+path of zoo.ops.quant (im2col + GEMM), plus the quantized-vs-bf16 logit agreement.
 python tools/quant_bench.py [--batch 256] [--iters 20] [--no-dynamic]"""
 import argparse
 import json
@@ -13,7 +13,7 @@ import torch  # noqa: E402
 
 from zoo.models.image.resnet import resnet50  # noqa: E402
 from zoo.ops import quant as Q  # noqa: E402
-from zoo.ops.qresnet import Int8ResNet  # noqa: E402
+from zoo.ops.qresnet import Fp8ResNet, Int8ResNet  # noqa: E402
 
 
 def bench(m, x, iters):
@@ -50,6 +50,14 @@ def main():
     res = {"bench": "resnet50-inference", "batch": a.batch, "bf16_img_s": round(a.batch / tb, 1),
            "int8_static_img_s": round(a.batch / ts, 1), "int8_vs_bf16_logit_cos": round(cos, 4),
            "int8_vs_bf16_top1_agree": round(top1, 4), "speedup": round(tb / ts, 3)}
+    q8f = Fp8ResNet(m, calib)
+    tf = bench(q8f, x, a.iters)
+    with torch.no_grad():
+        outf = q8f(x).float()
+    res["fp8_static_img_s"] = round(a.batch / tf, 1)
+    res["fp8_vs_bf16_logit_cos"] = round(torch.nn.functional.cosine_similarity(outf.flatten(), ref.flatten(),
+                                                                               dim=0).item(), 4)
+    res["fp8_vs_bf16_top1_agree"] = round((outf.argmax(1) == ref.argmax(1)).float().mean().item(), 4)
     if not a.no_dynamic:
         Q.quantize(m)
         td = bench(m, x, a.iters)

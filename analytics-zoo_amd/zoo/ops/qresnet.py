@@ -13,6 +13,11 @@ calibrated int8 convolutions through MKL-DNN; this is the MI355X counterpart
 * the stem (3-channel input) and the classifier stay bf16; the last block's int8 output
   is average-pooled and dequantised by one kernel.
 
+``fmt="fp8"`` is the same network on OCP e4m3fn (per-channel weight scales amax / 448,
+calibrated per-tensor activation scales amax / 448) through the fp8 twin of the kernel: one
+``v_mfma_f32_16x16x128_f8f6f4`` per 128-byte k-step (the fp8 peak, 2x bf16), fp32 accumulation,
+hardware e4m3 conversion in the epilogue (``Fp8ResNet``).
+
 ``qconv_ref`` is the float64 CPU model of the kernel (same rounding) used as the oracle.
 """
 import torch
@@ -21,13 +26,29 @@ import torch.nn as nn
 from zoo.ops._native import native
 
 
-def _q_weight(unit):
-    """ConvBN (eval) -> (int8 [K, R*S*C], per-channel scale [K], folded bias [K])."""
+QMAX = {"int8": 127.0, "fp8": 448.0}
+F8 = torch.float8_e4m3fn
+
+
+def _fmt_of(t):
+    return "fp8" if t.dtype == F8 else "int8"
+
+
+def to_fp8(v):
+    """float -> e4m3fn with the kernel's clamp to the finite range (round to nearest even)."""
+    return v.float().clamp(-448.0, 448.0).to(F8)
+
+
+def _q_weight(unit, fmt="int8"):
+    """ConvBN (eval) -> (int8 / e4m3 [K, R*S*C], per-channel scale [K], folded bias [K])."""
     inv = torch.rsqrt(unit.running_var.float() + unit.eps)
     g = unit.gamma.detach().float() * inv
     w = unit.weight.detach().float()[:, :unit.k * unit.k * unit.cin] * g[:, None]
-    s = w.abs().amax(dim=1).clamp_min(1e-12) / 127.0
-    q = torch.round(w / s[:, None]).clamp_(-127, 127).to(torch.int8)
+    s = w.abs().amax(dim=1).clamp_min(1e-12) / QMAX[fmt]
+    if fmt == "fp8":
+        q = to_fp8(w / s[:, None])
+    else:
+        q = torch.round(w / s[:, None]).clamp_(-127, 127).to(torch.int8)
     b = unit.beta.detach().float() - unit.running_mean.float() * g
     return q.contiguous(), s, b
 
@@ -37,8 +58,9 @@ def _sat(v):
 
 
 def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
-    """float64 CPU model of qconv: xq int8 NHWC, wq int8 [K, R*S*C]."""
+    """float64 CPU model of qconv: xq int8 / e4m3 NHWC, wq [K, R*S*C] of the same format."""
     import torch.nn.functional as F
+    fmt = _fmt_of(xq)
     N, H, W, C = xq.shape
     K = wq.shape[0]
     w4 = wq[:, :R * S * C].double().reshape(K, R, S, C).permute(0, 3, 1, 2)
@@ -48,7 +70,9 @@ def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0,
         v = v + resid.double() * rscale
     if relu:
         v = v.clamp_min(0)
-    return v.to(torch.bfloat16) if out_bf16 else _sat(v).to(torch.int8)
+    if out_bf16:
+        return v.to(torch.bfloat16)
+    return to_fp8(v) if fmt == "fp8" else _sat(v).to(torch.int8)
 
 
 def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
@@ -58,17 +82,20 @@ def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, rel
     return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16)
 
 
-def quantize_act(x, scale):
+def quantize_act(x, scale, fmt="int8"):
     if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 16 == 0:
-        return native().quantize_i8(x.contiguous(), 1.0 / scale)
+        fn = native().quantize_f8 if fmt == "fp8" else native().quantize_i8
+        return fn(x.contiguous(), 1.0 / scale)
+    if fmt == "fp8":
+        return to_fp8(x.double() / scale)
     return _sat(x.double() / scale).to(torch.int8)
 
 
 class _QUnit:
-    """One conv unit: int8 weights and the epilogue constants for given in/out scales."""
+    """One conv unit: quantized weights and the epilogue constants for given in/out scales."""
 
-    def __init__(self, unit, device):
-        self.q, self.sw, self.b = (t.to(device) for t in _q_weight(unit))
+    def __init__(self, unit, device, fmt="int8"):
+        self.q, self.sw, self.b = (t.to(device) for t in _q_weight(unit, fmt))
         self.k, self.stride, self.pad, self.relu = unit.k, unit.stride, unit.pad, unit.relu
 
     def bind(self, s_in, s_out):
@@ -82,22 +109,30 @@ class _QUnit:
 
 
 class Int8ResNet(nn.Module):
-    """Calibrated static-int8 inference twin of a ``zoo.models.image.resnet.ResNet``."""
+    """Calibrated static-int8 (``fmt="fp8"``: e4m3) inference twin of a
+    ``zoo.models.image.resnet.ResNet``."""
 
-    def __init__(self, model, calib_x):
+    fmt = "int8"
+
+    def __init__(self, model, calib_x, fmt=None):
         super().__init__()
         from zoo.models.image import resnet as R
+        if fmt is not None:
+            self.fmt = fmt
+        if self.fmt not in QMAX:
+            raise ValueError("quantized format must be one of %s" % sorted(QMAX))
         model.eval()
         self.model = model
         dev = next(model.parameters()).device
+        f = self.fmt
         self.blocks = []
         for stage in model.stages:
             for blk in stage:
-                units = {"conv1": _QUnit(blk.conv1, dev), "conv2": _QUnit(blk.conv2, dev)}
+                units = {"conv1": _QUnit(blk.conv1, dev, f), "conv2": _QUnit(blk.conv2, dev, f)}
                 if isinstance(blk, R.Bottleneck):
-                    units["conv3"] = _QUnit(blk.conv3, dev)
+                    units["conv3"] = _QUnit(blk.conv3, dev, f)
                 if blk.down is not None:
-                    units["down"] = _QUnit(blk.down, dev)
+                    units["down"] = _QUnit(blk.down, dev, f)
                 self.blocks.append((blk, units))
         self.calibrate(calib_x)
 
@@ -118,7 +153,8 @@ class Int8ResNet(nn.Module):
     @torch.no_grad()
     def calibrate(self, x):
         """Per-tensor absmax of every int8 tensor of the network on ``x`` (run in bf16)."""
-        amax = lambda t: max(float(t.float().abs().max()), 1e-6) / 127.0  # noqa: E731
+        qmax = QMAX[self.fmt]
+        amax = lambda t: max(float(t.float().abs().max()), 1e-6) / qmax  # noqa: E731
         h = self._stem(x)
         self.s_in = amax(h)
         s_x = self.s_in
@@ -150,7 +186,7 @@ class Int8ResNet(nn.Module):
     @torch.no_grad()
     def forward(self, x):
         h = self._stem(x)
-        xq = quantize_act(h, self.s_in)
+        xq = quantize_act(h, self.s_in, self.fmt)
         for blk, u in self.blocks:
             s_x, s_sc, s_o = blk._q_scales
             sc = u["down"](xq) if "down" in u else xq
@@ -166,9 +202,16 @@ class Int8ResNet(nn.Module):
         return self.model.fc(feat)
 
 
-def quantize_resnet(model, calib_x):
-    """Static-int8 inference twin of ``model`` (a zoo ResNet), calibrated on ``calib_x``."""
-    return Int8ResNet(model, calib_x)
+class Fp8ResNet(Int8ResNet):
+    """Calibrated static OCP-fp8 (e4m3fn) inference twin of a zoo ResNet."""
+
+    fmt = "fp8"
 
 
-__all__ = ["Int8ResNet", "quantize_resnet", "qconv", "qconv_ref", "quantize_act"]
+def quantize_resnet(model, calib_x, fmt="int8"):
+    """Static-int8 (or ``fmt="fp8"``) inference twin of ``model`` (a zoo ResNet), calibrated on
+    ``calib_x``."""
+    return (Fp8ResNet if fmt == "fp8" else Int8ResNet)(model, calib_x)
+
+
+__all__ = ["Int8ResNet", "Fp8ResNet", "quantize_resnet", "qconv", "qconv_ref", "quantize_act", "to_fp8"]

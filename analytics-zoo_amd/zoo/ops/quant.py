@@ -158,17 +158,22 @@ def _quantizable_conv(m):
         isinstance(m.padding, tuple) and m.padding_mode == "zeros"
 
 
-def quantize(model, calib_data=None):
+def quantize(model, calib_data=None, dtype="int8"):
     """Convert supported layers of ``model`` to int8 in place; returns the model (eval mode).
     With ``calib_data`` (an input batch) a zoo ResNet is instead returned as its calibrated
-    static-int8 twin (zoo.ops.qresnet.Int8ResNet; the original model is left as is)."""
+    static twin (zoo.ops.qresnet.Int8ResNet; the original model is left as is); ``dtype="fp8"``
+    selects the OCP e4m3 twin (Fp8ResNet, fp8 matrix cores), which needs calibration data."""
     from zoo.models.image import resnet as R
     from zoo.pipeline.api.keras.layers.core import Dense as KDense
     model.eval()
+    if dtype not in ("int8", "fp8"):
+        raise ValueError("dtype must be 'int8' or 'fp8'")
+    if dtype == "fp8" and (calib_data is None or not isinstance(model, R.ResNet)):
+        raise ValueError("fp8 quantization is the calibrated static path: a zoo ResNet and calib_data")
     if calib_data is not None and isinstance(model, R.ResNet):
-        from zoo.ops.qresnet import Int8ResNet
+        from zoo.ops.qresnet import Fp8ResNet, Int8ResNet
         dev = next(model.parameters()).device
-        q = Int8ResNet(model, torch.as_tensor(calib_data).to(dev))
+        q = (Fp8ResNet if dtype == "fp8" else Int8ResNet)(model, torch.as_tensor(calib_data).to(dev))
         q._zoo_quantized = True
         return q
 

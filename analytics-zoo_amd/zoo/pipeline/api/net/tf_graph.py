@@ -157,6 +157,8 @@ def parse_attr(b):
         return parse_tensor(g[8][0][1])
     if 9 in g:
         return pb.as_str(g[9][0][1])
+    if 10 in g:   # func: NameAttrList (tf.data map / filter functions)
+        return {"func": pb.as_str(pb.group(g[10][0][1])[1][0][1])}
     return None
 
 

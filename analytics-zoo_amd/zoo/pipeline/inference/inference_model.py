@@ -132,14 +132,14 @@ class InferenceModel:
         self._t0 = None
 
     # ------------------------------------------------------------------ loading
-    def _install(self, model, quantize=False, calib_data=None):
+    def _install(self, model, quantize=False, calib_data=None, qdtype="int8"):
         model = model.to(self.device)
         if self.dtype is not None:
             model = model.to(self.dtype)
         model.eval()
         if quantize:  # blas=false in the reference loaders -> BigDL quantize() (int8)
             from zoo.ops.quant import quantize as _q
-            model = _q(model, calib_data)
+            model = _q(model, calib_data, dtype=qdtype)
         for p in model.parameters():
             p.requires_grad_(False)
         self.model = model
@@ -156,11 +156,12 @@ class InferenceModel:
             self._n_replicas += 1
         return r
 
-    def load_module(self, module, blas=True, calib_data=None):
+    def load_module(self, module, blas=True, calib_data=None, qdtype="int8"):
         """Serve an in-memory torch.nn.Module (the PyTorch loader, doLoadPyTorch).
         ``blas=False`` quantizes to int8 as the reference loaders do; with ``calib_data`` a
-        zoo ResNet gets the calibrated static-int8 kernels (zoo.ops.qresnet)."""
-        return self._install(module, quantize=not blas, calib_data=calib_data)
+        zoo ResNet gets the calibrated static-int8 kernels (zoo.ops.qresnet), or with
+        ``qdtype="fp8"`` the OCP-fp8 ones."""
+        return self._install(module, quantize=not blas, calib_data=calib_data, qdtype=qdtype)
 
     def load(self, model_path, weight_path=None, blas=True):
         """Zoo Keras/ZooModel file (doLoad, InferenceModel.scala:97-110)."""
@@ -177,12 +178,13 @@ class InferenceModel:
         from zoo.pipeline.api.net import Net
         return self._install(Net.load_caffe(model_path, weight_path), quantize=not blas)
 
-    def quantize(self, calib_data=None):
+    def quantize(self, calib_data=None, dtype="int8"):
         """Re-install the loaded model as its int8 version (InferenceModelFactory.scala:33,47);
-        ``calib_data`` selects the calibrated static-int8 path where the model supports it."""
+        ``calib_data`` selects the calibrated static path where the model supports it, and
+        ``dtype="fp8"`` its e4m3 variant on the fp8 matrix cores."""
         if self.model is None:
             raise RuntimeError("load a model first")
-        return self._install(self.model, quantize=True, calib_data=calib_data)
+        return self._install(self.model, quantize=True, calib_data=calib_data, qdtype=dtype)
 
     def load_onnx(self, model_path):
         from zoo.pipeline.api.onnx import load_onnx

@@ -83,11 +83,21 @@ class TFDataset:
     @staticmethod
     def from_tf_data_dataset(dataset, batch_size=-1, batch_per_thread=-1, hard_code_batch_size=False,
                              validation_dataset=None, sequential_order=False, shuffle=True):
-        """Py/tfpark/tf_dataset.py:TFDataDataset (T4 TFDataFeatureSet). Without TensorFlow the
-        dataset is any iterable of UNBATCHED elements -- ``x`` or ``(x, y)`` numpy-convertible
-        (a ``tf.data.Dataset`` exposing ``as_numpy_iterator`` works as is); it is materialised
-        once into host arrays and served by the native FeatureSet gather."""
+        """Py/tfpark/tf_dataset.py:TFDataDataset (T4 TFDataFeatureSet). ``dataset`` is a tf.data
+        pipeline as its serialized dataset graph -- GraphDef bytes, a path to one, or a
+        ``tf.data.Dataset`` (``_as_serialized_graph``) -- executed by zoo.tfpark.tf_data_graph
+        (a trailing batch is undone: the FeatureSet batches), or any iterable of UNBATCHED
+        elements ``x`` / ``(x, y)``. Elements are materialised once into host arrays and served
+        by the native FeatureSet gather."""
+        from zoo.tfpark.tf_data_graph import TFDataGraph, serialized_graph
         bs = TFDataset._bs(batch_size, batch_per_thread)
+
+        def from_graph(d):
+            gb = serialized_graph(d) if d is not None and not isinstance(d, (list, tuple)) else None
+            if gb is None:
+                return d
+            return [e[0] if len(e) == 1 else tuple(e) for e in TFDataGraph(gb).unbatched()]
+        dataset, validation_dataset = from_graph(dataset), from_graph(validation_dataset)
         train = _iterable_featureset(dataset, bs, shuffle and not sequential_order and batch_size > 0)
         val = _iterable_featureset(validation_dataset, bs, False) if validation_dataset is not None else None
         return TFDataset(train, val, batch_size, batch_per_thread)

@@ -31,7 +31,13 @@ def _name(t):
 
 
 def tensor_proto(arr):
-    """numpy array -> serialized TensorProto (dtype, shape, tensor_content)."""
+    """numpy array -> serialized TensorProto (dtype, shape, tensor_content; strings / bytes ->
+    DT_STRING string_val)."""
+    arr = np.asarray(arr)
+    if arr.dtype == object or arr.dtype.kind in ("S", "U"):
+        shape = b"".join(pb.enc_bytes(2, pb.enc_int(1, int(d))) for d in arr.shape)
+        vals = [v.encode() if isinstance(v, str) else bytes(v) for v in arr.reshape(-1).tolist()]
+        return pb.enc_int(1, 7) + pb.enc_bytes(2, shape) + b"".join(pb.enc_bytes(8, v) for v in vals)
     arr = np.ascontiguousarray(arr)
     dt = _TF_DT.get(arr.dtype)
     if dt is None:
@@ -47,8 +53,9 @@ def _attr_entry(key, attr_value):
 
 def const_node(name, arr):
     arr = np.asarray(arr)
+    dt = 7 if (arr.dtype == object or arr.dtype.kind in ("S", "U")) else _TF_DT[np.ascontiguousarray(arr).dtype]
     return (pb.enc_bytes(1, name.encode()) + pb.enc_bytes(2, b"Const") +
-            _attr_entry("dtype", pb.enc_int(6, _TF_DT[np.ascontiguousarray(arr).dtype])) +
+            _attr_entry("dtype", pb.enc_int(6, dt)) +
             _attr_entry("value", pb.enc_bytes(8, tensor_proto(arr))))
 
 
@@ -126,6 +133,16 @@ def attr_value(v):
     ("type", dt) -> type, ("shape", dims) -> shape, np.ndarray -> tensor, list of ints -> list.i)."""
     if isinstance(v, tuple) and len(v) == 2 and v[0] == "type":
         return pb.enc_int(6, int(v[1]))
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "func":          # NameAttrList
+        return pb.enc_bytes(10, pb.enc_bytes(1, v[1].encode()))
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "types":         # list(type)
+        return pb.enc_bytes(1, pb.enc_packed_ints(6, [int(t) for t in v[1]]))
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "shapes":        # list(shape)
+        return pb.enc_bytes(1, b"".join(
+            pb.enc_bytes(7, b"".join(pb.enc_bytes(2, pb.enc_int(1, int(d) & 0xFFFFFFFFFFFFFFFF)) for d in dims))
+            for dims in v[1]))
+    if isinstance(v, tuple) and len(v) == 2 and v[0] == "strings":       # list(string)
+        return pb.enc_bytes(1, b"".join(pb.enc_bytes(2, x.encode() if isinstance(x, str) else x) for x in v[1]))
     if isinstance(v, tuple) and len(v) == 2 and v[0] == "shape":
         return pb.enc_bytes(7, b"".join(pb.enc_bytes(2, pb.enc_int(1, int(d) & 0xFFFFFFFFFFFFFFFF)) for d in v[1]))
     if isinstance(v, bool):
@@ -153,7 +170,25 @@ def node_def(name, op, inputs=(), **attrs):
     return out
 
 
-def graph_def(nodes):
-    """Serialized GraphDef from serialized NodeDefs."""
-    return b"".join(pb.enc_bytes(1, n) for n in nodes)
+def graph_def(nodes, library=()):
+    """Serialized GraphDef from serialized NodeDefs (+ FunctionDefs for its function library)."""
+    out = b"".join(pb.enc_bytes(1, n) for n in nodes)
+    if library:
+        out += pb.enc_bytes(2, b"".join(pb.enc_bytes(1, f) for f in library))
+    return out
+
+
+def function_def(name, inputs, outputs, nodes, ret):
+    """Serialized FunctionDef: ``inputs`` / ``outputs`` lists of (arg name, TF dtype enum), body
+    ``nodes`` (NodeDefs whose inputs use the function naming ``arg`` / ``node:out_arg:i``) and
+    ``ret`` {output arg: "node:out_arg:i"} (a tf.data map / filter function)."""
+    sig = pb.enc_bytes(1, name.encode())
+    for n, dt in inputs:
+        sig += pb.enc_bytes(2, pb.enc_bytes(1, n.encode()) + pb.enc_int(3, int(dt)))
+    for n, dt in outputs:
+        sig += pb.enc_bytes(3, pb.enc_bytes(1, n.encode()) + pb.enc_int(3, int(dt)))
+    out = pb.enc_bytes(1, sig) + b"".join(pb.enc_bytes(3, n) for n in nodes)
+    for k, v in ret.items():
+        out += pb.enc_bytes(4, pb.enc_bytes(1, k.encode()) + pb.enc_bytes(2, v.encode()))
+    return out
 

@@ -65,3 +65,65 @@ def test_inference_model_static_int8_with_hipgraph(gpu):
     assert np.allclose(out, out2)
     cos = float((out * ref).sum() / (np.linalg.norm(out) * np.linalg.norm(ref)))
     assert cos > 0.95, cos
+
+
+# ---- OCP fp8 (e4m3fn) twin: v_mfma_f32_16x16x128_f8f6f4 ----
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [(2, 14, 64, 64, 1, 1, 0), (2, 14, 64, 128, 3, 1, 1),
+                                                  (3, 15, 32, 64, 3, 2, 1), (1, 7, 512, 2048, 1, 1, 0),
+                                                  (4, 28, 16, 72, 3, 1, 1)])
+@pytest.mark.parametrize("resid,relu,out_bf16", [(False, True, False), (True, True, False), (True, False, True)])
+def test_fp8conv_matches_float64_model(gpu, N, H, C, K, R, stride, pad, resid, relu, out_bf16):
+    from zoo.ops.qresnet import qconv, qconv_ref, to_fp8
+    g = torch.Generator().manual_seed(N * 1000 + C + K)
+    xq = to_fp8(torch.randn(N, H, H, C, generator=g) * 40)
+    wq = to_fp8(torch.randn(K, R * R * C, generator=g) * 40)
+    cs = (torch.rand(K, generator=g) * 2e-4 + 1e-5).float()
+    b = (torch.randn(K, generator=g) * 3).float()
+    P = (H + 2 * pad - R) // stride + 1
+    rq = to_fp8(torch.randn(N, P, P, K, generator=g) * 40) if resid else None
+    ref = qconv_ref(xq, wq, R, R, stride, pad, cs, b, rq, 0.37, relu, out_bf16)
+    out = qconv(xq.to(gpu), wq.to(gpu), R, R, stride, pad, cs.to(gpu), b.to(gpu),
+                None if rq is None else rq.to(gpu), 0.37, relu, out_bf16).cpu()
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    o, r = out.float(), ref.float()
+    if out_bf16:
+        assert torch.allclose(o, r, rtol=1e-2, atol=1e-2)
+    else:
+        # fp32 vs fp64 accumulation can move a value across an e4m3 rounding boundary (one ulp,
+        # 2^-3 relative) on rare ties
+        bad = (o - r).abs() > 0.13 * r.abs() + 1e-6
+        assert float(bad.float().mean()) < 1e-3 and float(((o != r).float()).mean()) < 2e-2
+
+
+def test_fp8_resnet_tracks_bf16_model(gpu):
+    from zoo.models.image.resnet import resnet50
+    from zoo.ops.qresnet import Fp8ResNet
+    torch.manual_seed(0)
+    m = resnet50(num_classes=100).to(gpu).eval()
+    x = torch.randn(16, 3, 224, 224, device=gpu)
+    with torch.no_grad():
+        ref = m(x).float()
+    q = Fp8ResNet(m, torch.randn(16, 3, 224, 224, device=gpu))
+    with torch.no_grad():
+        out = q(x).float()
+    assert out.shape == ref.shape and torch.isfinite(out).all()
+    cos = torch.nn.functional.cosine_similarity(out.flatten(), ref.flatten(), dim=0).item()
+    assert cos > 0.9, cos
+
+
+def test_inference_model_fp8(gpu):
+    import numpy as np
+    from zoo.models.image.resnet import resnet18
+    from zoo.ops.qresnet import Fp8ResNet
+    from zoo.pipeline.inference import InferenceModel
+    torch.manual_seed(1)
+    m = resnet18(num_classes=10).to(gpu).eval()
+    x = torch.randn(8, 3, 64, 64)
+    with torch.no_grad():
+        ref = m(x.to(gpu)).float().cpu().numpy()
+    im = InferenceModel(1, device=gpu).load_module(m, blas=False, calib_data=torch.randn(8, 3, 64, 64),
+                                                   qdtype="fp8")
+    assert isinstance(im.model, Fp8ResNet)
+    out = im.predict(x)
+    cos = float((out * ref).sum() / (np.linalg.norm(out) * np.linalg.norm(ref)))
+    assert cos > 0.9, cos
