@@ -1,12 +1,11 @@
-"""AutoML time-series models (Py/automl/model/*.py): BaseModel wrappers
-(VanillaLSTM, LSTMSeq2Seq, MTNetKeras, TimeSequenceModel) over the torch networks
-in ``_nets`` (VanillaLSTMNet, LSTMSeq2SeqNet, MTNetNet; ``build_model`` builds one
-from a trial config)."""
-from zoo.automl.model._nets import MODELS, LSTMSeq2SeqNet, MTNetNet, VanillaLSTMNet, build_model  # noqa: F401
+"""AutoML time-series models (Py/automl/model/*.py): VanillaLSTM, LSTMSeq2Seq (teacher-forced
+encoder-decoder), MTNetKeras (memory network with attention RNN encoders) and the
+TimeSequenceModel dispatcher, each a BaseModel over its torch network trained by the engine."""
+from zoo.automl.model._nets import MODELS, VanillaLSTMNet, build_model  # noqa: F401
 from zoo.automl.model.abstract import BaseModel  # noqa: F401
 from zoo.automl.model.VanillaLSTM import VanillaLSTM  # noqa: F401,E402
-from zoo.automl.model.Seq2Seq import LSTMSeq2Seq  # noqa: F401,E402
-from zoo.automl.model.MTNet_keras import MTNetKeras  # noqa: F401,E402
+from zoo.automl.model.Seq2Seq import LSTMSeq2Seq, LSTMSeq2SeqNet  # noqa: F401,E402
+from zoo.automl.model.MTNet_keras import MTNetKeras, MTNetNet  # noqa: F401,E402
 from zoo.automl.model.time_sequence import TimeSequenceModel  # noqa: F401,E402
 
 MTNet = MTNetNet  # network class under its short name

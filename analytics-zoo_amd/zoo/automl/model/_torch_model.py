@@ -29,6 +29,11 @@ class TorchTSModel(BaseModel):
     net_cls = None
     required = set()
     optional = set()
+    default_batch_size = 32
+
+    def _optimizer(self, cfg):
+        from zoo.pipeline.api.keras.optimizers import Adam
+        return Adam(lr=float(cfg.get("lr", 1e-3)))
 
     def __init__(self, check_optional_config=False, future_seq_len=1):
         self.check_optional_config = check_optional_config
@@ -54,7 +59,6 @@ class TorchTSModel(BaseModel):
 
     # -- BaseModel
     def fit_eval(self, x, y, validation_data=None, mc=False, verbose=0, **config):
-        from zoo.pipeline.api.keras.optimizers import Adam
         from zoo.pipeline.api.net import TorchNet
         self.config.update(config)
         cfg = self.config
@@ -65,8 +69,10 @@ class TorchTSModel(BaseModel):
             self._build(x.shape[-1], cfg)
         if self.net is None:
             self.net = TorchNet.from_pytorch(self.model, input_shape=x.shape[1:])
-            self.net.compile(optimizer=Adam(lr=float(cfg.get("lr", 1e-3))), loss=cfg.get("loss", "mse"))
-        self.net.fit(x, y, batch_size=int(cfg.get("batch_size", 32)), nb_epoch=int(cfg.get("epochs", 1)))
+            self.net.compile(optimizer=self._optimizer(cfg), loss=cfg.get("loss", "mse"))
+        # a batch larger than the data trains on all of it (Keras' partial last batch)
+        bs = max(1, min(int(cfg.get("batch_size", self.default_batch_size)), len(x)))
+        self.net.fit(x, y, batch_size=bs, nb_epoch=int(cfg.get("epochs", 1)))
         metric = cfg.get("metric", "mse")
         vx, vy = validation_data if validation_data is not None else (x, y)
         return float(self.evaluate(vx, vy, [metric])[0])

@@ -12,7 +12,8 @@ import logging
 import numpy as np
 import torch
 
-from zoo.automl.model._nets import MTNetNet, VanillaLSTMNet
+from zoo.automl.model._nets import VanillaLSTMNet
+from zoo.automl.model.MTNet_keras import MTNetNet
 
 log = logging.getLogger("zoo.zouwu")
 

@@ -178,14 +178,14 @@ def test_model_fit_eval_save_restore_uncertainty(kind, tmp_path):
         cfg.update(long_num=long_num, time_step=time_step, ar_window=2, cnn_height=2)
     if kind == "Seq2seq":
         cfg.update(latent_dim=16)
-    m = cls(future_seq_len=future)
+    m = cls(check_optional_config=False, future_seq_len=future)
     m.fit_eval(x, y, validation_data=(vx, vy), mc=True, **cfg)
     m.evaluate(vx, vy)
     pred = m.predict(tx)
     assert pred.shape == (tx.shape[0], y.shape[1])
     d = str(tmp_path / "m")
     save(d, model=m)
-    m2 = cls(future_seq_len=future)
+    m2 = cls(check_optional_config=False, future_seq_len=future)
     restore(d, model=m2, config=cfg)
     np.testing.assert_array_almost_equal(pred, m2.predict(tx), decimal=4)
     m2.fit_eval(x, y, epochs=1)

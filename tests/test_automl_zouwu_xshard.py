@@ -78,7 +78,9 @@ def test_mtnet_and_seq2seq_models_forward():
     from zoo.automl.model import LSTMSeq2SeqNet, MTNetNet
     x = torch.randn(4, 9, 3)
     assert MTNetNet(3, 2, time_step=3, long_num=2, ar_window=2)(x).shape == (4, 2)
-    assert LSTMSeq2SeqNet(3, 3, latent_dim=8)(x).shape == (4, 3)
+    net = LSTMSeq2SeqNet(3, 1, latent_dim=8, past_seq_len=9)
+    assert net.decode(x, 3).shape == (4, 3, 1)
+    assert net(torch.cat([x, torch.zeros(4, 3, 3)], 1)).shape == (4, 3, 1)     # teacher-forced graph
 
 
 def test_zouwu_forecasters_and_autots(tmp_path):
@@ -176,7 +178,7 @@ def test_automl_base_models_fit_eval_save_restore(tmp_path):
     assert np.allclose(m2.predict(x), m.predict(x), atol=1e-5)
     mean, std = m.predict_with_uncertainty(x[:8], n_iter=4)
     assert mean.shape == (8, 1) and std.shape == (8, 1)
-    with pytest.raises(ValueError, match="Missing required"):
+    with pytest.raises(ValueError, match="look-back"):     # defaults long_num 7, time_step 1 need 8 steps
         MTNetKeras().fit_eval(x, y, epochs=1)
     mt = MTNetKeras(future_seq_len=1)
     assert mt.fit_eval(x, y, long_num=2, time_step=2, epochs=1) >= 0
