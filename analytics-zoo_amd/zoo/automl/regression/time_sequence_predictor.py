@@ -8,9 +8,6 @@ import logging
 from zoo.automl.common.metrics import Evaluator
 from zoo.automl.config.recipe import SmokeRecipe
 from zoo.automl.feature.time_sequence import TimeSequenceFeatureTransformer
-from zoo.automl.model.time_sequence import TimeSequenceModel
-from zoo.automl.pipeline.time_sequence import TimeSequencePipeline
-from zoo.automl.search import SearchEngine
 
 log = logging.getLogger("zoo.automl")
 
@@ -34,31 +31,53 @@ class TimeSequencePredictor:
 
     def fit(self, input_df, validation_df=None, metric="mse", recipe=None, mc=False, resources_per_trial=None,
             distributed=False, hdfs_url=None, n_parallel=1):
+        """Search with ``recipe`` (the reference's _hp_search: RayTuneSearchEngine.compile / run,
+        stop criteria = recipe.runtime_params() minus num_samples), then load the best trial's
+        checkpoint (feature transformer + model + config) as the pipeline."""
+        from zoo.automl.pipeline.time_sequence import load_ts_pipeline
+        from zoo.automl.search.RayTuneSearchEngine import RayTuneSearchEngine
         Evaluator.check_metric(metric)
+        self._check_input(input_df, validation_df)
         recipe = recipe or SmokeRecipe()
-        feats = self._ft().get_feature_list(input_df)
-        val_df = validation_df if validation_df is not None else input_df
-
-        def trial(config):
-            config = dict(config, **self._identity_config())
-            ft = self._ft()
-            x, y = ft.fit_transform(input_df, **config)
-            vx, vy = ft.transform(val_df, is_train=True)
-            model = TimeSequenceModel(check_optional_config=False, future_seq_len=self.future_seq_len)
-            cfg = dict(config, epochs=int(config.get("epochs", 1)) * int(recipe.training_iteration))
-            model.fit_eval(x, y, validation_data=(vx, vy), mc=mc, **cfg)
-            ppl = TimeSequencePipeline(feature_transformers=ft, model=model, config=config, name=self.name)
-            return {metric: float(ppl.evaluate(val_df, [metric], "uniform_average")[0]), "pipeline": ppl}
-
-        engine = SearchEngine(n_parallel=n_parallel)
-        mode = "max" if Evaluator.higher_is_better(metric) else "min"
-        best_cfg, best = engine.run(trial, recipe.search_space(feats), recipe.num_samples, metric, mode,
-                                    search_alg=recipe.search_algorithm(),
-                                    search_alg_params=recipe.search_algorithm_params(),
-                                    fixed_params=recipe.fixed_params())
-        self.pipeline = best["pipeline"]
-        self.trials = engine.trials
+        feats = self._ft().get_feature_list(input_df[0] if isinstance(input_df, list) else input_df)
+        runtime_params = dict(recipe.runtime_params())
+        num_samples = runtime_params.pop("num_samples")
+        searcher = RayTuneSearchEngine(logs_dir=self.logs_dir, resources_per_trial=resources_per_trial,
+                                       name=self.name, n_parallel=n_parallel)
+        fixed = recipe.fixed_params()
+        if recipe.search_algorithm() == "BayesOpt":     # box space; constants ride in fixed_params
+            space = recipe.search_space(feats)
+            fixed = dict(fixed or {})
+        else:
+            space = dict(recipe.search_space(feats), **self._identity_config())
+        searcher.compile(input_df, search_space=space, num_samples=num_samples, stop=runtime_params,
+                         search_algorithm=recipe.search_algorithm(),
+                         search_algorithm_params=recipe.search_algorithm_params(),
+                         fixed_params=None if fixed is None else dict(fixed, **self._identity_config()),
+                         feature_transformers=self._ft(), future_seq_len=self.future_seq_len,
+                         validation_df=validation_df, mc=mc, metric=metric)
+        searcher.run()
+        best = searcher.get_best_trials(k=1)[0]
+        self.trials = searcher.trials
+        self.pipeline = load_ts_pipeline(best.model_path)
+        self.pipeline.name = self.name
         return self.pipeline
+
+    def _check_input(self, input_df, validation_df):
+        import pandas as pd
+
+        def cols(df):
+            need = [self.dt_col, self.target_col] + list(self.extra_features_col or [])
+            missing = set(need) - set(df.columns)
+            if missing:
+                raise ValueError("Missing Columns in the input data frame:" + ",".join(sorted(missing)))
+        for d in (input_df if isinstance(input_df, list) else [input_df]):
+            if not isinstance(d, pd.DataFrame):
+                raise ValueError("input_df should be a data frame or a list of data frames")
+            cols(d)
+        if validation_df is not None:
+            for d in (validation_df if isinstance(validation_df, list) else [validation_df]):
+                cols(d)
 
     def evaluate(self, input_df, metric=("mse",)):
         return self.pipeline.evaluate(input_df, list(metric))

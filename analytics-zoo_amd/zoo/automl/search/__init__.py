@@ -187,5 +187,5 @@ class SearchEngine(_AbstractSearchEngine):
         log.info("best trial %s -> %s", best[0], best[1])
         return best
 
-
-RayTuneSearchEngine = SearchEngine  # the reference's engine name
+# the reference's driver (compile / run / get_best_trials -> TrialOutput) lives in the submodule
+# of its name: zoo.automl.search.RayTuneSearchEngine.RayTuneSearchEngine

@@ -156,7 +156,10 @@ def test_time_sequence_predictor_with_bayes_recipe():
     tsp = TimeSequencePredictor(future_seq_len=1)
     ppl = tsp.fit(df, recipe=BayesRecipe(num_samples=3, look_back=(2, 4), epochs=1, training_iteration=1))
     assert len(tsp.trials) == 3
-    assert all(2 <= c["past_seq_len"] <= 4 and c["model"] == "LSTM" for c, _ in tsp.trials)
+    from zoo.automl.common.util import convert_bayes_configs
+    cfgs = [convert_bayes_configs(t.config) for t in tsp.trials]          # raw GP points + fixed params
+    assert all(2 <= c["past_seq_len"] <= 4 and c["model"] == "LSTM" for c in cfgs)
+    assert all(t.last_result["training_iteration"] == 1 for t in tsp.trials)     # stop criterion
     assert ppl.predict(df).shape[0] > 0
 
 
@@ -190,9 +193,10 @@ def test_automl_base_models_fit_eval_save_restore(tmp_path):
 
 
 def test_search_engine_abstract_contract():
-    from zoo.automl.search import GridSearch, RandomSample, RayTuneSearchEngine, SearchEngine
+    from zoo.automl.search import GridSearch, RandomSample, SearchEngine
+    from zoo.automl.search.RayTuneSearchEngine import RayTuneSearchEngine
     from zoo.automl.search.abstract import SearchEngine as Abstract
-    assert issubclass(SearchEngine, Abstract) and RayTuneSearchEngine is SearchEngine
+    assert issubclass(SearchEngine, Abstract) and issubclass(RayTuneSearchEngine, Abstract)
     eng = SearchEngine()
     space = {"a": GridSearch([1, 2, 3]), "b": RandomSample(lambda spec: spec["a"] * 10)}
     best_cfg, best = eng.run(lambda c: {"mse": abs(c["a"] - 2) + 0.0 * c["b"]}, space)
