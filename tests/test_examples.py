@@ -24,6 +24,11 @@ CASES = [
     ("serving/quick_start.py", ["--images", "4", "--batch", "2"]),
     ("attention/transformer.py", ["--n", "32", "--epochs", "1", "--seq-len", "8", "--hidden", "16"]),
     ("objectdetection/ssd_train_predict.py", ["--steps", "1", "--batch", "1"]),
+    ("imageclassification/predict.py", ["--images", "2", "--model", "squeezenet"]),
+    ("inception/inception.py", ["--batch", "2", "--iters", "2", "--classes", "10", "--image-size", "64"]),
+    ("quantization/quantized_inference.py", ["--depth", "18", "--batch", "2", "--image-size", "64"]),
+    ("streaming/streaming_text_classification.py", ["--lines", "12", "--micro-batch", "4", "--epochs", "2"]),
+    ("openvino/predict.py", ["--batch", "2"]),
 ]
 
 
