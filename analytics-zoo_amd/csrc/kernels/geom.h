@@ -64,6 +64,11 @@ inline int igemm_epi(bool y, bool yf, bool bias, bool resid, int act, bool omap,
   return 0;
 }
 
+// Tile-routing class of an epilogue (igemm2.hip i2_choose): the GELU-backward form of EPI 2
+// (BwdStats.zgelu) reads one tensor, not the BN-backward's two plus a reduction, and routes like
+// the plain epilogues; everywhere else the routing class is the epilogue itself.
+inline int igemm_route_epi(int epi, bool zgelu) { return (epi == 2 && zgelu) ? 4 : epi; }
+
 // Plain GEMM geometry (gemm256.hip): Y[M, N] = A[M, K] . B[N, K]^T
 struct GemmGeom {
   int M, N, K;

@@ -593,6 +593,51 @@ __global__ __launch_bounds__(256) void flip_weights_batched_kernel(const FlipDes
     else hi = mid - 1;
   }
   const FlipDesc d = descs[lo];
+  if (d.R == 1 && d.S == 1 && d.Ra == 1 && d.Sb == 1) {
+    // 1x1 filters (every transformer linear): a plain [K][C] -> [C][K] transpose through a
+    // 64x64 LDS tile, both global sides coalesced 4-byte pairs (the element loop below reads W
+    // with a stride of ldw per lane: 595 us per BERT-base step, profiles/r3/bert_base_train_b128_r3.md)
+    __shared__ bf16_t tl[64][66];
+    const int tk = (d.K + 63) >> 6, tc = (d.C + 63) >> 6;
+    const bf16_t* W = static_cast<const bf16_t*>(d.W);
+    bf16_t* Wt = static_cast<bf16_t*>(d.Wt);
+    const int tid = threadIdx.x, pr = tid >> 5, pc = (tid & 31) * 2;   // 8 rows x 32 pairs per pass
+    for (int t = b - d.blk0; t < tk * tc; t += d.nblk) {
+      const int k0 = (t / tc) * 64, c0 = (t % tc) * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = pr + 8 * i, k = k0 + r, c = c0 + pc;
+        bf16_t v0 = bf16_t(0), v1 = bf16_t(0);
+        if (k < d.K) {
+          const bf16_t* src = W + (size_t)k * d.ldw + c;
+          if (c + 1 < d.C) {
+            v0 = src[0];
+            v1 = src[1];
+          } else if (c < d.C) {
+            v0 = src[0];
+          }
+        }
+        tl[r][pc] = v0;
+        tl[r][pc + 1] = v1;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int r = pr + 8 * i, c = c0 + r, k = k0 + pc;
+        if (c < d.C) {
+          bf16_t* dst = Wt + (size_t)c * d.ldt + k;
+          if (k + 1 < d.K) {
+            dst[0] = tl[pc][r];
+            dst[1] = tl[pc + 1][r];
+          } else if (k < d.K) {
+            dst[0] = tl[pc][r];
+          }
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
   const int total = d.C * d.Ra * d.Sb * d.K;
   const int step = d.nblk * blockDim.x;
   for (int idx = (b - d.blk0) * blockDim.x + threadIdx.x; idx < total; idx += step) {
@@ -679,7 +724,8 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
   // whole-64-channel K-tiles: the large-tile second-generation kernel (igemm2.hip)
-  if (zoo_igemm2_eligible(g, igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats)))
+  if (zoo_igemm2_eligible(g, igemm_route_epi(igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats),
+                                             bsp && bsp->zgelu)))
     return zoo_igemm2(X, W, Y, Yf, bias, resid, stats, g, act, bsp, st);
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const bf16_t* x = (const bf16_t*)X;

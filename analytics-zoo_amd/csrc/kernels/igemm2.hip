@@ -505,7 +505,9 @@ static int i2_bn(int tile) {
 // ResNet-50 b256 convs with the model's own epilogues, round 3, profiles/r3/igemm2_r3.md):
 //   * N (output channels) < 256: igemm.hip's 128x{64,128} tiles are as fast or faster;
 //   * a short reduction (Ktot < 256 forward, < 1024 for the BN-backward epilogue) is bound by
-//     the epilogue, where igemm.hip's row-pointer epilogues win;
+//     the epilogue, where igemm.hip's row-pointer epilogues win (the GELU-backward form of EPI 2,
+//     routing class 4, follows the forward rule: igemm.hip took 162 us vs ~77 us for BERT's
+//     16384x3072x768 FFN dgrad, profiles/r3/bert_base_train_b128_r3.md);
 //   * otherwise 256x256 (8 waves of 128x64) while >= 160 tiles fill the chip, else 128x128.
 static int i2_choose(const ConvGeom& g, int epi) {
   const int f = i2_tile_force();
@@ -547,10 +549,11 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
                                  hipStream_t st) {
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bs.sums, stats);
-  if (!zoo_igemm2_eligible(g, epi)) return hipErrorNotSupported;
+  const int route = igemm_route_epi(epi, bs.zgelu != 0);
+  if (!zoo_igemm2_eligible(g, route)) return hipErrorNotSupported;
   const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 &&
                      g->H == g->P && g->W == g->Q;
-  const int tile = i2_choose(*g, epi);
+  const int tile = i2_choose(*g, route);
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
   if (is1x1)

@@ -316,7 +316,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   // m-tile height of the kernel the dispatcher picks (igemm.hip: 128; igemm2.hip: 128 or 256)
   const int epi = zoo::igemm_epi(out_bf16, out_f32, bp != nullptr, rp != nullptr, act, g.omap != 0,
                                  bs.sums != nullptr, sp != nullptr);
-  const int bm = zoo_igemm2_bm(&g, epi) > 0 ? zoo_igemm2_bm(&g, epi) : 128;
+  const int route = zoo::igemm_route_epi(epi, bs.zgelu != 0);
+  const int bm = zoo_igemm2_bm(&g, route) > 0 ? zoo_igemm2_bm(&g, route) : 128;
   const int tiles_m = (g.M + bm - 1) / bm;
   // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
   // the atomics go straight into the final 2K floats, no slot fold launch needed
