@@ -9,7 +9,10 @@ materialising a [batch, sum(wide_dims)] multi-hot matrix in HBM.
 Deep part: multi-hot indicator columns + per-column embeddings +
 continuous columns -> MLP. ``model_type`` in {wide, deep, wide_n_deep}.
 """
+import torch
+
 from zoo.models.recommendation.recommender import Recommender
+from zoo.pipeline.api.keras.base import Layer
 from zoo.pipeline.api.keras.engine.topology import Model, merge
 from zoo.pipeline.api.keras.layers import (Activation, CAdd, Dense, Embedding, Flatten, Input, Select,
                                            SparseEmbedding)
@@ -38,6 +41,15 @@ class ColumnFeatureInfo:
                     self.wide_base_cols, self.wide_base_dims, self.wide_cross_cols, self.wide_cross_dims,
                     self.indicator_cols, self.indicator_dims, self.embed_cols, self.embed_in_dims,
                     self.embed_out_dims, self.continuous_cols, self.label))
+
+
+class _DeepTowerInput(Layer):
+    """The concatenated deep-tower input in the MFMA kernels' compute dtype (bf16 on the GPU):
+    the Dense chain then runs bf16 in and out with no per-layer fp32 <-> bf16 conversions in
+    forward or backward (profiles/r3/wide_and_deep_b8192_r3.md); identity on the CPU."""
+
+    def call(self, x):
+        return x.to(torch.bfloat16) if x.is_cuda and x.is_floating_point() else x
 
 
 class WideAndDeep(Recommender):
@@ -86,6 +98,7 @@ class WideAndDeep(Recommender):
         if not parts:
             raise TypeError("Empty deep tensors")
         h = parts[0] if len(parts) == 1 else merge(parts, mode="concat")
+        h = _DeepTowerInput()(h)
         for u in self.hidden_layers:
             h = Dense(u, activation="relu")(h)
         return inputs, Dense(self.class_num, activation="relu")(h)

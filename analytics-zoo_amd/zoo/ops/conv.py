@@ -474,10 +474,10 @@ def linear(x, w, bias=None, act=None, grad_add=None, gelu_link=None, gelu_src=No
         # zero-pad features to the MFMA kernels' 8-element granule (keeps small
         # layers such as NCF's 30->10->5 off hipBLASLt's tall-skinny fp32 wgrad)
         pc, pk = (-Cin) % 8, (-K) % 8
-        xp = F.pad(x, (0, pc))
+        xp = F.pad(x, (0, pc)) if pc else x
         wp = F.pad(w, (0, pc, 0, pk))
-        bp = None if bias is None else F.pad(bias, (0, pk))
-        return linear(xp, wp, bp, act)[..., :K]
+        bp = None if bias is None or not pk else F.pad(bias, (0, pk))
+        return linear(xp, wp, bias if bp is None else bp, act)[..., :K]
     if x.is_cuda and w.shape[1] == Cin and x.shape[-1] == Cin and _use_blas(x, Cin, K, act):
         xb = x.reshape(-1, Cin)
         xb = (xb if xb.dtype == torch.bfloat16 else xb.to(torch.bfloat16)).contiguous()
