@@ -127,7 +127,207 @@ __global__ __launch_bounds__(256) void ssd_match_encode_kernel(
   conf_t[(size_t)b * P + p] = iou < overlap ? bg_label : (long long)r[0];
 }
 
+// ---- hard negative mining (MultiBoxLoss.scala: 3:1 negatives by confidence loss) ----------
+// One 1024-thread block per image. k = ceil(ratio * #positives) (<= P - 1) priors with the
+// largest loss among neg_ce (= ce, 0 on positives) are selected: the exact k-th largest value by
+// a 4-pass 8-bit MSB-first radix select over the loss bits (losses are >= 0, so their bit
+// patterns order like the values), then every prior above it plus the first (by prior index)
+// ones equal to it. Output: pos | neg as a byte mask. Replaces argsort(argsort()) ranking.
+constexpr int MINE_T = 1024;
+
+__global__ __launch_bounds__(MINE_T) void ssd_mine_kernel(const float* __restrict__ ce,
+                                                         const long long* __restrict__ conf_t, int P, int bg,
+                                                         float ratio, unsigned char* __restrict__ sel) {
+  __shared__ unsigned hist[256];
+  __shared__ unsigned s_prefix, s_mask;
+  __shared__ int s_npos, s_rem, s_base;
+  __shared__ int scan[MINE_T];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* c = ce + (size_t)b * P;
+  const long long* lab = conf_t + (size_t)b * P;
+  unsigned char* out = sel + (size_t)b * P;
+  if (tid == 0) { s_npos = 0; s_prefix = 0u; s_mask = 0u; }
+  __syncthreads();
+  int np = 0;
+  for (int p = tid; p < P; p += MINE_T) np += lab[p] != bg;
+  atomicAdd(&s_npos, np);
+  __syncthreads();
+  int k = (int)ceilf(ratio * (float)s_npos);
+  if (k > P - 1) k = P - 1;
+  if (k <= 0) {
+    for (int p = tid; p < P; p += MINE_T) out[p] = lab[p] != bg;
+    return;
+  }
+  if (tid == 0) s_rem = k;
+  for (int shift = 24; shift >= 0; shift -= 8) {
+    for (int i = tid; i < 256; i += MINE_T) hist[i] = 0u;
+    __syncthreads();
+    const unsigned pre = s_prefix, msk = s_mask;
+    for (int p = tid; p < P; p += MINE_T) {
+      const float v = lab[p] != bg ? 0.f : fmaxf(c[p], 0.f);
+      const unsigned u = __float_as_uint(v);
+      if ((u & msk) == pre) atomicAdd(&hist[(u >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int rem = s_rem, d = 255;
+      for (; d > 0; --d) {
+        if ((int)hist[d] >= rem) break;
+        rem -= (int)hist[d];
+      }
+      s_rem = rem;
+      s_prefix = pre | ((unsigned)d << shift);
+      s_mask = msk | (255u << shift);
+    }
+    __syncthreads();
+  }
+  const unsigned thr = s_prefix;
+  const int need_eq = s_rem;          // ties at the threshold still to take, lowest prior index first
+  if (tid == 0) s_base = 0;
+  __syncthreads();
+  for (int p0 = 0; p0 < P; p0 += MINE_T) {
+    const int p = p0 + tid;
+    bool pos = false, gt = false, eq = false;
+    if (p < P) {
+      pos = lab[p] != bg;
+      const unsigned u = __float_as_uint(pos ? 0.f : fmaxf(c[p], 0.f));
+      gt = u > thr;
+      eq = u == thr;
+    }
+    scan[tid] = eq ? 1 : 0;
+    __syncthreads();
+    for (int off = 1; off < MINE_T; off <<= 1) {       // inclusive Hillis-Steele scan
+      const int v = tid >= off ? scan[tid - off] : 0;
+      __syncthreads();
+      scan[tid] += v;
+      __syncthreads();
+    }
+    const int before = s_base + scan[tid] - (eq ? 1 : 0);
+    if (p < P) out[p] = (pos || gt || (eq && before < need_eq)) ? 1 : 0;
+    __syncthreads();
+    if (tid == MINE_T - 1) s_base += scan[tid];
+    __syncthreads();
+  }
+}
+
+// ---- SSD conv4_3 NormalizeScale: y = x / (||x||_2 + eps) * w over the channels (NHWC) ------
+// one wave per row, 8-channel bf16 chunks (C % 8 == 0); the backward folds dw per block into a
+// partial row (fixed-order column sums afterwards: deterministic)
+__global__ __launch_bounds__(256) void l2norm_scale_fwd_kernel(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                               bf16_t* __restrict__ y, float* __restrict__ rn, long R,
+                                                               int C, float eps) {
+  const int lane = threadIdx.x & 63;
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int cpr = C >> 3;
+  const bf16_t* xr = x + row * C;
+  float s = 0.f;
+  for (int ch = lane; ch < cpr; ch += 64) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + ch * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) s = fmaf(v[e], v[e], s);
+  }
+  s = warp_sum(s);
+  const float n = sqrtf(s) + eps;
+  const float inv = 1.f / n;
+  if (lane == 0) rn[row] = n;
+  for (int ch = lane; ch < cpr; ch += 64) {
+    float v[8];
+    unpack8(*reinterpret_cast<const uint4*>(xr + ch * 8), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = v[e] * inv * w[ch * 8 + e];
+    *reinterpret_cast<uint4*>(y + row * C + ch * 8) = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void l2norm_scale_bwd_kernel(const bf16_t* __restrict__ dy, const bf16_t* __restrict__ x,
+                                                               const float* __restrict__ w, const float* __restrict__ rn,
+                                                               bf16_t* __restrict__ dx, float* __restrict__ dwp, long R,
+                                                               int C, float eps, int rows_per_block) {
+  extern __shared__ float l2_dw[];          // [4 waves][C]
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int cpr = C >> 3;
+  for (int i = threadIdx.x; i < 4 * C; i += 256) l2_dw[i] = 0.f;
+  __syncthreads();
+  const long r0 = (long)blockIdx.x * rows_per_block;
+  const long r1 = r0 + rows_per_block < R ? r0 + rows_per_block : R;
+  for (long row = r0 + wv; row < r1; row += 4) {
+    const bf16_t* xr = x + row * C;
+    const bf16_t* dr = dy + row * C;
+    const float n = rn[row], inv = 1.f / n, sq = n - eps;
+    float dot = 0.f;
+    for (int ch = lane; ch < cpr; ch += 64) {
+      float xv[8], dv[8];
+      unpack8(*reinterpret_cast<const uint4*>(xr + ch * 8), xv);
+      unpack8(*reinterpret_cast<const uint4*>(dr + ch * 8), dv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        dot = fmaf(w[ch * 8 + e] * dv[e], xv[e], dot);
+        l2_dw[wv * C + ch * 8 + e] += dv[e] * xv[e] * inv;     // this wave's lanes own disjoint columns
+      }
+    }
+    dot = warp_sum(dot);
+    const float k = sq > 0.f ? dot / (n * n * sq) : 0.f;
+    for (int ch = lane; ch < cpr; ch += 64) {
+      float xv[8], dv[8], o[8];
+      unpack8(*reinterpret_cast<const uint4*>(xr + ch * 8), xv);
+      unpack8(*reinterpret_cast<const uint4*>(dr + ch * 8), dv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) o[e] = w[ch * 8 + e] * dv[e] * inv - xv[e] * k;
+      *reinterpret_cast<uint4*>(dx + row * C + ch * 8) = pack8(o);
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += 256)
+    dwp[(size_t)blockIdx.x * C + i] = ((l2_dw[i] + l2_dw[C + i]) + l2_dw[2 * C + i]) + l2_dw[3 * C + i];
+}
+
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restrict__ part, int nb, int n,
+                                                          float* __restrict__ out) {
+  const int col = blockIdx.x * 256 + threadIdx.x;
+  if (col >= n) return;
+  float s = 0.f;
+  for (int b = 0; b < nb; ++b) s += part[(size_t)b * n + col];
+  out[col] += s;
+}
+
 }  // namespace zoo
+
+extern "C" hipError_t zoo_ssd_mine(const float* ce, const long long* conf_t, int B, int P, int bg, float ratio,
+                                   unsigned char* sel, hipStream_t st) {
+  hipLaunchKernelGGL(zoo::ssd_mine_kernel, dim3(B), dim3(zoo::MINE_T), 0, st, ce, conf_t, P, bg, ratio, sel);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_l2norm_scale_fwd(const void* x, const float* w, void* y, float* rn, long R, int C, float eps,
+                                           hipStream_t st) {
+  const long blocks = (R + 3) / 4;
+  hipLaunchKernelGGL(zoo::l2norm_scale_fwd_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const zoo::bf16_t*)x, w,
+                     (zoo::bf16_t*)y, rn, R, C, eps);
+  return hipGetLastError();
+}
+
+extern "C" int zoo_l2norm_scale_bwd_blocks(long R) {
+  long rpb = (R + 511) / 512;
+  if (rpb < 16) rpb = 16;
+  return (int)((R + rpb - 1) / rpb);
+}
+
+// dw (fp32 [C]) += sum over rows; part: zoo_l2norm_scale_bwd_blocks(R) x C floats
+extern "C" hipError_t zoo_l2norm_scale_bwd(const void* dy, const void* x, const float* w, const float* rn, void* dx,
+                                           float* dw, float* part, long R, int C, float eps, hipStream_t st) {
+  const int nb = zoo_l2norm_scale_bwd_blocks(R);
+  const int rpb = (int)((R + nb - 1) / nb);
+  const size_t lds = (size_t)4 * C * sizeof(float);
+  if (lds > 64 * 1024) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(zoo::l2norm_scale_bwd_kernel, dim3(nb), dim3(256), lds, st, (const zoo::bf16_t*)dy,
+                     (const zoo::bf16_t*)x, w, rn, (zoo::bf16_t*)dx, part, R, C, eps, rpb);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(zoo::colsum_rows_kernel, dim3((C + 255) / 256), dim3(256), 0, st, part, nb, C, dw);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t zoo_ssd_match(const float* gt, const int* count, const float* priors, int B, int G, int P,
                                     float overlap, float v0, float v1, int bg_label, int* best_gt, float* best_iou,

@@ -52,6 +52,11 @@ hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t)
 hipError_t zoo_ssd_match(const float*, const int*, const float*, int, int, int, float, float, float, int, int*,
                          float*, unsigned long long*, float*, long long*, hipStream_t);
 hipError_t zoo_row_l2norm(const void*, const void*, const void*, void*, long, int, int, float, hipStream_t);
+hipError_t zoo_ssd_mine(const float*, const long long*, int, int, int, float, unsigned char*, hipStream_t);
+hipError_t zoo_l2norm_scale_fwd(const void*, const float*, void*, float*, long, int, float, hipStream_t);
+int zoo_l2norm_scale_bwd_blocks(long);
+hipError_t zoo_l2norm_scale_bwd(const void*, const void*, const float*, const float*, void*, float*, float*, long, int,
+                                float, hipStream_t);
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
@@ -446,6 +451,60 @@ torch::Tensor row_l2norm(torch::Tensor x, c10::optional<torch::Tensor> dy, c10::
                            out.data_ptr(), rows, (int)cols, x.scalar_type() == at::kFloat, (float)eps, cur_stream()),
             "row_l2norm");
   return out;
+}
+
+// SSD hard negative mining: ce [B, P] fp32 (per-prior confidence loss), conf_t [B, P] int64 ->
+// uint8 [B, P] mask of positives | the ceil(ratio * #pos) hardest negatives per image
+torch::Tensor ssd_mine(torch::Tensor ce, torch::Tensor conf_t, int64_t bg_label, double ratio) {
+  req(ce, at::kFloat, "ce");
+  TORCH_CHECK(conf_t.is_cuda() && conf_t.scalar_type() == at::kLong && conf_t.is_contiguous(), "ssd_mine: conf_t int64");
+  TORCH_CHECK(ce.dim() == 2 && conf_t.sizes() == ce.sizes(), "ssd_mine: ce / conf_t [B, P]");
+  const int64_t B = ce.size(0), P = ce.size(1);
+  TORCH_CHECK(B < (1 << 30) && P < (1 << 30), "ssd_mine: sizes");
+  auto sel = torch::empty({B, P}, ce.options().dtype(at::kByte));
+  if (B == 0 || P == 0) return sel;
+  check_hip(zoo_ssd_mine(ce.data_ptr<float>(), reinterpret_cast<const long long*>(conf_t.data_ptr()), (int)B, (int)P,
+                         (int)bg_label, (float)ratio, sel.data_ptr<uint8_t>(), cur_stream()),
+            "ssd_mine");
+  return sel;
+}
+
+// NormalizeScale over the last dim: y = x / (||x|| + eps) * w (bf16 x / y, fp32 w); returns (y, norm [R])
+std::vector<torch::Tensor> l2norm_scale_fwd(torch::Tensor x, torch::Tensor w, double eps) {
+  req(x, at::kBFloat16, "x");
+  req(w, at::kFloat, "w");
+  const int64_t C = x.size(-1);
+  TORCH_CHECK(C % 8 == 0 && w.numel() == C, "l2norm_scale: C % 8 == 0, w [C]");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0, "l2norm_scale: aligned x");
+  const int64_t R = x.numel() / C;
+  auto y = torch::empty_like(x);
+  auto rn = torch::empty({R}, x.options().dtype(at::kFloat));
+  if (R) check_hip(zoo_l2norm_scale_fwd(x.data_ptr(), w.data_ptr<float>(), y.data_ptr(), rn.data_ptr<float>(), R,
+                                        (int)C, (float)eps, cur_stream()),
+                   "l2norm_scale_fwd");
+  return {y, rn};
+}
+
+// backward: (dx bf16, dw fp32 [C])
+std::vector<torch::Tensor> l2norm_scale_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor w, torch::Tensor rn,
+                                            double eps) {
+  req(dy, at::kBFloat16, "dy");
+  req(x, at::kBFloat16, "x");
+  req(w, at::kFloat, "w");
+  req(rn, at::kFloat, "norm");
+  const int64_t C = x.size(-1), R = x.numel() / C;
+  TORCH_CHECK(dy.sizes() == x.sizes() && C % 8 == 0 && w.numel() == C && rn.numel() == R && C <= 4096,
+              "l2norm_scale_bwd: shapes");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(x.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(dy.data_ptr()) % 16 == 0,
+              "l2norm_scale_bwd: aligned");
+  auto dx = torch::empty_like(x);
+  auto dw = torch::zeros({C}, w.options());
+  if (R == 0) return {dx, dw};
+  auto part = torch::empty({(int64_t)zoo_l2norm_scale_bwd_blocks(R) * C}, w.options());
+  check_hip(zoo_l2norm_scale_bwd(dy.data_ptr(), x.data_ptr(), w.data_ptr<float>(), rn.data_ptr<float>(), dx.data_ptr(),
+                                 dw.data_ptr<float>(), part.data_ptr<float>(), R, (int)C, (float)eps, cur_stream()),
+            "l2norm_scale_bwd");
+  return {dx, dw};
 }
 
 // SSD matching: gt [B, G, 5] (label, x1, y1, x2, y2), count [B] int32, priors [P, 4]
@@ -2370,6 +2429,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear_wgrad", &linear_wgrad);
   m.def("bmm_nt", &bmm_nt);
   m.def("ssd_match", &ssd_match);
+  m.def("ssd_mine", &ssd_mine);
+  m.def("l2norm_scale_fwd", &l2norm_scale_fwd);
+  m.def("l2norm_scale_bwd", &l2norm_scale_bwd);
   m.def("row_reduce", &row_reduce);
   m.def("row_l2norm", &row_l2norm);
   m.def("attn_fwd", &attn_fwd, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"), py::arg("causal"),

@@ -119,9 +119,48 @@ class NormalizeScale(nn.Module):
         self.eps = eps
 
     def forward(self, x):
+        if x.is_cuda and x.dtype == torch.bfloat16 and x.shape[-1] % 8 == 0:
+            return _L2NormScaleFn.apply(x.contiguous(), self.weight, float(self.eps))
         xf = x.float()
         n = xf.pow(2).sum(-1, keepdim=True).sqrt() + self.eps
         return (xf / n * self.weight).to(x.dtype)
+
+
+class _L2NormScaleFn(torch.autograd.Function):
+    """One fused native pass each way (csrc/kernels/detect.hip l2norm_scale_*): the torch
+    composition re-read the [B, 38, 38, 512] map five times forward and eight backward."""
+
+    @staticmethod
+    def forward(ctx, x, w, eps):
+        from zoo.ops._native import native
+        y, n = native().l2norm_scale_fwd(x, w.float().contiguous(), eps)
+        ctx.save_for_backward(x, w, n)
+        ctx.eps = eps
+        return y
+
+    @staticmethod
+    def backward(ctx, g):
+        from zoo.ops._native import native
+        x, w, n = ctx.saved_tensors
+        dx, dw = native().l2norm_scale_bwd(g.contiguous().to(x.dtype), x, w.float().contiguous(), n, ctx.eps)
+        return dx, dw.to(w.dtype), None
+
+
+def mine_hard_negatives(ce, pos, ratio):
+    """pos | the ceil(ratio * #pos) (<= P - 1) highest-loss negatives of each row, ties taken in
+    prior order (MultiBoxLoss.scala hard negative mining). ce [B, P] per-prior loss."""
+    B, P = ce.shape
+    if ce.is_cuda:
+        from zoo.ops._native import native
+        conf = pos.long() if pos.dtype == torch.bool else pos
+        # the kernel takes labels; any label != bg (0 here) marks a positive
+        return native().ssd_mine(ce.detach().float().contiguous(), conf.contiguous(), 0, float(ratio)).bool()
+    neg_ce = ce.detach().float().masked_fill(pos, 0).clamp_min(0)
+    order = torch.sort(neg_ce, dim=1, descending=True, stable=True).indices
+    rank = torch.empty_like(order)
+    rank.scatter_(1, order, torch.arange(P, device=ce.device).expand(B, P))
+    k = torch.ceil(float(ratio) * pos.sum(1, keepdim=True).float()).clamp(max=P - 1)
+    return pos | (rank < k)
 
 
 def _vgg16_base():
@@ -316,14 +355,12 @@ class MultiBoxLoss(nn.Module):
             loc_t, conf_t = torch.stack(loc_t), torch.stack(conf_t)
         pos = conf_t != self.bg
         n_pos = pos.sum().clamp(min=1).float()
-        loss_l = F.smooth_l1_loss(loc[pos].float(), loc_t[pos], reduction="sum")
+        # masked sums instead of boolean indexing: no nonzero / gather / index_put round trips
+        sl1 = F.smooth_l1_loss(loc.float(), loc_t, reduction="none").sum(-1)
+        loss_l = torch.where(pos, sl1, 0.0).sum()     # where, not *: a degenerate box's inf stays out
         ce = F.cross_entropy(conf.reshape(-1, self.n).float(), conf_t.reshape(-1), reduction="none").reshape(B, P)
-        neg_ce = ce.clone().detach()
-        neg_ce[pos] = 0
-        rank = neg_ce.argsort(1, descending=True).argsort(1)
-        n_neg = (self.ratio * pos.sum(1, keepdim=True)).clamp(max=P - 1)
-        neg = rank < n_neg
-        loss_c = ce[pos | neg].sum()
+        sel = mine_hard_negatives(ce, pos, self.ratio)
+        loss_c = torch.where(sel, ce, 0.0).sum()
         return (loss_l + loss_c) / n_pos
 
 

@@ -123,3 +123,45 @@ def test_ssd_native_matching_matches_reference():
     assert torch.equal(conf_t.cpu(), ref_c)
     pos = ref_c != 0
     assert torch.allclose(loc_t.cpu()[pos], ref_l[pos], atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,frac", [(8732, 0.02), (8732, 0.4), (3000, 0.0), (1500, 0.9)])
+def test_ssd_native_mining_matches_stable_rank(P, frac):
+    """Hard negative mining kernel (radix select, detect.hip ssd_mine) vs the stable-sort rank on
+    the CPU: identical masks, including ties (quantised losses) and the P - 1 clamp."""
+    from zoo.models.image.objectdetection.ssd import mine_hard_negatives
+    torch.manual_seed(7)
+    B = 5
+    ce = torch.rand(B, P)
+    ce[1] = (ce[1] * 8).floor() / 8                 # heavy ties
+    ce[2, : P // 3] = 0.0
+    pos = torch.rand(B, P) < frac
+    pos[3] = False                                    # no positives: nothing mined
+    ref = mine_hard_negatives(ce, pos, 3.0)
+    out = mine_hard_negatives(ce.cuda(), pos.cuda(), 3.0).cpu()
+    assert torch.equal(out, ref)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 38, 38, 512), (3, 5, 7, 64), (2, 1, 1, 1024)])
+def test_normalize_scale_native_fwd_bwd(shape):
+    """SSD conv4_3 NormalizeScale on the fused kernels vs the fp32 torch composition."""
+    from zoo.models.image.objectdetection.ssd import NormalizeScale
+    torch.manual_seed(8)
+    m = NormalizeScale(shape[-1]).cuda()
+    with torch.no_grad():
+        m.weight.uniform_(5, 25)
+    x = torch.relu(torch.randn(*shape, device="cuda")).bfloat16()
+    xr = x.float().requires_grad_(True)
+    wr = m.weight.detach().clone().requires_grad_(True)
+    ref = xr / (xr.pow(2).sum(-1, keepdim=True).sqrt() + m.eps) * wr
+    xn = x.clone().requires_grad_(True)
+    out = m(xn)
+    assert out.dtype == torch.bfloat16
+    assert ((out.float() - ref).norm() / ref.norm()).item() < 1e-2
+    g = torch.randn_like(ref).bfloat16()
+    gx, gw = torch.autograd.grad(ref, (xr, wr), g.float())
+    nx, nw = torch.autograd.grad(out, (xn, m.weight), g)
+    assert ((nx.float() - gx).norm() / gx.norm()).item() < 2e-2
+    assert ((nw - gw).norm() / gw.norm()).item() < 1e-2

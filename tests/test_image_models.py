@@ -107,3 +107,25 @@ def test_mean_average_precision():
     half = [np.array([[1, 0.9, 0.1, 0.1, 0.4, 0.4]]), np.zeros((0, 6))]
     m = mean_average_precision(half, gts, 3, use_07=False)
     assert 0 < m < 1
+
+
+def test_hard_negative_mining_matches_rank_rule():
+    """mine_hard_negatives == the reference's rank < ratio * #pos rule (distinct losses) and
+    takes exactly ceil(ratio * #pos) negatives, clamped to P - 1."""
+    import torch
+    from zoo.models.image.objectdetection.ssd import mine_hard_negatives
+    torch.manual_seed(0)
+    B, P = 4, 200
+    ce = torch.rand(B, P)
+    pos = torch.rand(B, P) < 0.05
+    pos[3] = torch.rand(P) < 0.5                      # 3 * #pos > P - 1: clamped
+    sel = mine_hard_negatives(ce, pos, 3.0)
+    neg_ce = ce.clone()
+    neg_ce[pos] = 0
+    rank = neg_ce.argsort(1, descending=True).argsort(1)
+    ref = pos | (rank < (3.0 * pos.sum(1, keepdim=True)).clamp(max=P - 1))
+    assert torch.equal(sel, ref)
+    n_neg = (sel & ~pos).sum(1)
+    want = (3 * pos.sum(1)).clamp(max=P - 1)
+    assert torch.all(n_neg <= want)
+    assert torch.all(n_neg[:3] == want[:3])
