@@ -50,6 +50,14 @@ struct W2Geom {
   int m_per_split, splits, tiles_n, tiles_k;
 };
 
+// implicit-GEMM (im2col) form of the X operand for convolutions: X[m][k] with m = output
+// pixel (n, p, q) and k = (r * S + s) * C + c reads x[n][p*sh - ph + r*dh][q*sw - pw + s*dw][c]
+// of the NHWC input (zero outside). C % 8 == 0, so a lane's 16-byte chunk never straddles taps.
+struct W2Conv {
+  int H, W, C, P, Q, S;
+  int sh, sw, ph, pw, dh, dw;
+};
+
 // one fragment = two transposed 4-row reads of an 8-row block (rows 0-3 -> elements 0-3)
 ZOO_DEV bf16x8 w2_frag(const char* blk, int lo_off, int hi_off) {
   const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((w2_lds_i16x4*)(blk + lo_off));
@@ -61,11 +69,11 @@ ZOO_DEV bf16x8 w2_frag(const char* blk, int lo_off, int hi_off) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
-template <bool PP>
+template <bool PP, bool IMPL>
 __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __restrict__ dY,
                                                             const bf16_t* __restrict__ X, float* __restrict__ dW,
                                                             float* __restrict__ part, W2Geom g,
-                                                            const bf16_t* __restrict__ zpage) {
+                                                            const bf16_t* __restrict__ zpage, W2Conv cv) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -100,6 +108,35 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
     for (int h = 0; h < 2; ++h) b_col[h][j] = k0 + (idx >> 2) * 64 + h * 32 + ((lane >> 4) & 1) * 16 + c8;
   }
 
+  // IMPL: per (half, instruction) the lane's k chunk is one fixed tap (r, s) and channel c;
+  // its pixel (n, p, q) advances by 64 rows per staged m-step without integer division
+  int xoff_h[2][2], xoff_w[2][2], xc[2][2], pn[2][2], pp[2][2], pq[2][2];
+  int adv_n = 0, adv_p = 0, adv_q = 0;
+  if constexpr (IMPL) {
+    const int PQ = cv.P * cv.Q;
+    adv_n = W2_BM / PQ;
+    adv_p = (W2_BM % PQ) / cv.Q;
+    adv_q = (W2_BM % PQ) % cv.Q;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int k = b_col[h][j];
+        const int t = k / cv.C;
+        const int r = t / cv.S;
+        xc[h][j] = k - t * cv.C;
+        // a k beyond K gets an offset that fails the row bounds test
+        xoff_h[h][j] = k < g.K ? r * cv.dh - cv.ph : -(1 << 28);
+        xoff_w[h][j] = (t - r * cv.S) * cv.dw - cv.pw;
+        const int m = ms + b_row[j];
+        const int mm = m < g.M ? m : 0;
+        pn[h][j] = mm / PQ;
+        const int rem = mm - pn[h][j] * PQ;
+        pp[h][j] = rem / cv.Q;
+        pq[h][j] = rem - pp[h][j] * cv.Q;
+      }
+  }
+
   auto half_base = [&](int buf, int op, int h) -> char* {
     return smem + (((buf * 2 + op) * 2 + h) * W2_HALF);
   };
@@ -113,6 +150,14 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
       if (op == 0) {
         const int m = mrow0 + a_row, n = a_col[h][j];
         src = (m < me && n < g.N) ? dY + (size_t)m * g.ldy + n : zpage;
+      } else if constexpr (IMPL) {
+        const int m = mrow0 + b_row[j];
+        const int hi = pp[h][j] * cv.sh + xoff_h[h][j], wi = pq[h][j] * cv.sw + xoff_w[h][j];
+        const bool ok = m < me && (unsigned)hi < (unsigned)cv.H && (unsigned)wi < (unsigned)cv.W;
+        src = ok ? X + (((size_t)pn[h][j] * cv.H + hi) * cv.W + wi) * cv.C + xc[h][j] : zpage;
+        pq[h][j] += adv_q; pp[h][j] += adv_p; pn[h][j] += adv_n;
+        if (pq[h][j] >= cv.Q) { pq[h][j] -= cv.Q; ++pp[h][j]; }
+        if (pp[h][j] >= cv.P) { pp[h][j] -= cv.P; ++pn[h][j]; }
       } else {
         const int m = mrow0 + b_row[j], k = b_col[h][j];
         src = (m < me && k < g.K) ? X + (size_t)m * g.ldx + k : zpage;
@@ -341,23 +386,59 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
   const size_t smem = 4 * 2 * W2_HALF;  // 2 buffers x (A, B) x 2 halves = 128 KiB
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<true>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<true, false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false>),
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false, false>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false, true>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr = true;
   }
+  const W2Conv cv{};
   static const bool pp = [] {
     // measured neutral on the BERT / ResNet shapes (tools/wgrad_bench.py A/B: -3..+3 %): opt-in
     const char* e = getenv("ZOO_W256_PINGPONG");
     return e ? atoi(e) != 0 : false;
   }();
   if (pp)
-    hipLaunchKernelGGL(wgrad256_kernel<true>, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
+    hipLaunchKernelGGL((wgrad256_kernel<true, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
   else
-    hipLaunchKernelGGL(wgrad256_kernel<false>, dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page());
+    hipLaunchKernelGGL((wgrad256_kernel<false, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
+  if (g.splits > 1) {
+    const size_t total = (size_t)tiles * 8 * 32 * 64;
+    hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);
+  }
+  return hipGetLastError();
+}
+
+// convolution weight gradient on the same kernel, X staged as the implicit im2col matrix:
+// dW[Cout][(r*S + s)*C + c] (row stride ldw) += sum over output pixels; dY = [Nb*P*Q][Cout]
+// contiguous, x = NHWC [Nb][H][W][C] with C % 8 == 0. part: zoo_wgrad256_part_floats(M, Cout,
+// R*S*C) fp32 scratch.
+extern "C" hipError_t zoo_wgrad256_conv(const void* dY, const void* X, float* dW, float* part, int Nb, int H, int W,
+                                        int C, int Cout, int R, int S, int P, int Q, int sh, int sw, int ph, int pw,
+                                        int dh, int dw, int ldw, hipStream_t st) {
+  if (C % 8 || Cout % 8) return hipErrorInvalidValue;
+  W2Geom g;
+  g.M = Nb * P * Q; g.N = Cout; g.K = R * S * C;
+  g.ldy = Cout; g.ldx = 0; g.ldw = ldw;
+  g.tiles_n = (g.N + W2_T - 1) / W2_T;
+  g.tiles_k = (g.K + W2_T - 1) / W2_T;
+  g.splits = zoo_wgrad256_plan(g.M, g.N, g.K, &g.m_per_split);
+  if (g.splits > 1 && !part) return hipErrorInvalidValue;
+  const W2Conv cv{H, W, C, P, Q, S, sh, sw, ph, pw, dh, dw};
+  const int tiles = g.tiles_n * g.tiles_k;
+  const size_t smem = 4 * 2 * W2_HALF;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false, true>),
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL((wgrad256_kernel<false, true>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                     (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
   if (g.splits > 1) {
     const size_t total = (size_t)tiles * 8 * 32 * 64;
     hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);

@@ -59,6 +59,8 @@ hipError_t zoo_l2norm_scale_bwd(const void*, const void*, const float*, const fl
                                 float, hipStream_t);
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
+hipError_t zoo_wgrad256_conv(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, int,
+                             int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
 size_t zoo_stats_part_scratch(int, int);
 hipError_t zoo_stats_part_finalize(float*, const float*, float*, int, int, hipStream_t);
@@ -536,6 +538,7 @@ std::vector<torch::Tensor> ssd_match(torch::Tensor gt, torch::Tensor count, torc
 }
 
 void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw);
+static void check_al16(const void* p, const char* what);
 
 // dW (fp32, [K, ldw]) += wgrad(x, dy)
 void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int S, int sh, int sw, int ph, int pw,
@@ -565,6 +568,26 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
       g.M <= (1 << 18) &&
       x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
     linear_wgrad(dy.view({(int64_t)g.M, g.K}), x.view({(int64_t)g.M, g.C}), dw);
+    return;
+  }
+  // other convs with >= ZOO_WGRAD256_CONV_COUT output channels (3x3, strided 1x1): the same
+  // 256x256-tile kernel with the im2col X operand gathered by its LDS-DMA (tools/wgrad_bench.py
+  // --conv); narrower outputs waste most of its 256-row tile and stay on wgrad.hip
+  static const int conv256_cout = [] {
+    const char* e = getenv("ZOO_WGRAD256_CONV_COUT");
+    return e ? atoi(e) : 256;
+  }();
+  if (use256 && conv256_cout > 0 && g.K >= conv256_cout && g.C % 8 == 0 && x.is_contiguous() &&
+      dy.is_contiguous() && dw.stride(1) == 1 && (int64_t)g.M * g.K < (1LL << 31) &&
+      (int64_t)g.N * g.H * g.W * g.C < (1LL << 40)) {
+    check_al16(x.data_ptr(), "conv_wgrad x");
+    check_al16(dy.data_ptr(), "conv_wgrad dy");
+    const size_t pf = zoo_wgrad256_part_floats(g.M, g.K, g.Ktot);
+    torch::Tensor part;
+    if (pf) part = torch::empty({(int64_t)pf}, dw.options());
+    check_hip(zoo_wgrad256_conv(dy.data_ptr(), x.data_ptr(), dw.data_ptr<float>(), pf ? part.data_ptr<float>() : nullptr,
+                                g.N, g.H, g.W, g.C, g.K, R, S, g.P, g.Q, sh, sw, ph, pw, dh, dil_w, g.ldw, cur_stream()),
+              "wgrad256_conv");
     return;
   }
   g.m_per_split = 0;

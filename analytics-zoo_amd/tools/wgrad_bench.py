@@ -34,7 +34,12 @@ def main():
     ap.add_argument("--m", type=int, default=16384)
     ap.add_argument("--more", action="store_true", help="also square / ResNet 1x1 shapes")
     ap.add_argument("--resnet", action="store_true", help="ResNet-50 b256 1x1 stride-1 conv shapes (M, Cout, Cin)")
+    ap.add_argument("--conv", action="store_true",
+                    help="ResNet-50 b256 3x3 / strided conv weight gradients through conv_wgrad (the route is "
+                         "chosen by ZOO_WGRAD256_CONV_COUT: 0 = wgrad.hip, default 256 = implicit wgrad256)")
     a = ap.parse_args()
+    if a.conv:
+        return conv_main()
     dev = torch.device("cuda")
     M = a.m
     shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
@@ -77,6 +82,32 @@ def main():
             t = timeit(fn)
             res[name] = {"us": round(t * 1e6, 1), "tflops": round(flop / t / 1e12, 1), "rel_err": float("%.2e" % err)}
         print(json.dumps(res), flush=True)
+
+
+def conv_main():
+    dev = torch.device("cuda")
+    # (N, H, Cin, Cout, R, stride, pad, count in the network)
+    cases = [(256, 56, 64, 64, 3, 1, 1, 3), (256, 56, 128, 128, 3, 2, 1, 1), (256, 28, 128, 128, 3, 1, 1, 3),
+             (256, 28, 256, 256, 3, 2, 1, 1), (256, 14, 256, 256, 3, 1, 1, 5), (256, 14, 512, 512, 3, 2, 1, 1),
+             (256, 7, 512, 512, 3, 1, 1, 2), (256, 56, 256, 512, 1, 2, 0, 1), (256, 28, 512, 1024, 1, 2, 0, 1),
+             (256, 14, 1024, 2048, 1, 2, 0, 1)]
+    total = 0.0
+    for N, H, Cin, Cout, R, st, pad, cnt in cases:
+        x = torch.randn(N, H, H, Cin, device=dev).bfloat16()
+        P = (H + 2 * pad - R) // st + 1
+        dy = (torch.randn(N, P, P, Cout, device=dev) * 0.1).bfloat16()
+        g = torch.zeros(Cout, R * R * Cin, device=dev)
+
+        def fn():
+            C.conv_wgrad(x, dy, g, R, R, st, st, pad, pad, 1, 1)
+        t = timeit(fn)
+        flop = 2.0 * N * P * P * Cout * R * R * Cin
+        total += t * cnt
+        print(json.dumps({"N": N, "H": H, "Cin": Cin, "Cout": Cout, "R": R, "stride": st, "count": cnt,
+                          "us": round(t * 1e6, 1), "tflops": round(flop / t / 1e12, 1),
+                          "route_cout": os.environ.get("ZOO_WGRAD256_CONV_COUT", "256")}), flush=True)
+        del x, dy, g
+    print(json.dumps({"network_ms": round(total * 1e3, 3)}), flush=True)
 
 
 if __name__ == "__main__":

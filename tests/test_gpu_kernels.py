@@ -764,3 +764,38 @@ def test_batched_flip_cache_tracks_weight_updates(gpu):
     assert len(flat._flip_cache.entries) == len(specs)
     assert _kern._owner_cache(ps[0]._zoo_bf16) is flat._flip_cache
     assert _kern._owner_cache(ps[0]._zoo_bf16.clone()) is None
+
+
+WGRAD256_CONV_SHAPES = [
+    # N, H, W, Cin, Cout, R, stride, pad, dil -- Cout >= 256: the implicit-GEMM wgrad256 path
+    (4, 14, 14, 256, 256, 3, 1, 1, 1),
+    (8, 7, 7, 64, 512, 3, 1, 1, 1),        # P*Q = 49 < 64: the pixel walk wraps images per m-step
+    (3, 15, 15, 128, 264, 3, 2, 1, 1),     # Cout and R*S*Cin not multiples of the tile
+    (4, 14, 14, 256, 512, 1, 2, 0, 1),     # strided 1x1 (projection shortcut)
+    (2, 13, 11, 40, 256, 3, 1, 2, 2),      # dilated
+    (64, 28, 28, 64, 256, 3, 1, 1, 1),     # many splits + ordered fold
+]
+
+
+@pytest.mark.parametrize("shape", WGRAD256_CONV_SHAPES)
+def test_conv_wgrad_implicit_256(gpu, shape):
+    """conv_wgrad routed to wgrad256 with the im2col operand gathered by its LDS-DMA vs fp32
+    torch conv weight gradient ([Cout][(r, s, c)] layout, padded columns untouched)."""
+    from zoo.ops import native
+    C = native()
+    N, H, W, Cin, Cout, R, st, pad, dil = shape
+    torch.manual_seed(11)
+    x = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
+    xr = x.float().permute(0, 3, 1, 2)
+    wr = torch.zeros(Cout, Cin, R, R, device=gpu, requires_grad=True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad, dilation=dil)
+    P, Q = yr.shape[2], yr.shape[3]
+    dy = torch.randn(N, P, Q, Cout, device=gpu).bfloat16()
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    ktot = R * R * Cin
+    dw = torch.zeros(Cout, ktot + 8, device=gpu)
+    dw[:, :ktot] = 0.5                                   # accumulates into dW
+    C.conv_wgrad(x, dy, dw, R, R, st, st, pad, pad, dil, dil)
+    ref = wr.grad.permute(0, 2, 3, 1).reshape(Cout, -1) + 0.5
+    assert rel(dw[:, :ktot], ref) < 1e-3
+    assert dw[:, ktot:].abs().max().item() == 0.0
