@@ -108,12 +108,16 @@ class Proposal(nn.Module):
         return torch.cat(rois) if rois else torch.zeros(0, 5, device=dev)
 
 
-def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16):
+def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16, return_argmax=False):
     """Max RoI pooling (BigDL RoiPooling / Caffe ROIPooling) of NCHW features: each RoI is
     rounded to feature coordinates and split into pooled x pooled fractional bins
     [floor(i * h / P), ceil((i + 1) * h / P)), clipped to the map; an empty bin is 0.
-    fp32 reference of the native channels-last kernel (roi_pool_nhwc)."""
+    fp32 reference of the native channels-last kernel (roi_pool_nhwc). ``return_argmax``
+    also returns the Caffe argmax (flat h * W + w of the FIRST maximum in row-major order,
+    -1 for an empty bin) that routes the backward; autograd through ``amax`` would split the
+    gradient between tied maxima instead."""
     out = features.new_zeros(rois.shape[0], features.shape[1], pooled, pooled)
+    arg = torch.full(out.shape, -1, dtype=torch.long, device=features.device) if return_argmax else None
     H, W = features.shape[2], features.shape[3]
     # C round() (half away from zero) of the fp32 scaled box, bin edges in fp32 arithmetic --
     # exactly what Caffe's ROIPoolingLayer (and the native kernel) compute
@@ -132,8 +136,12 @@ def roi_pool(features, rois, pooled=7, spatial_scale=1.0 / 16):
                 ws = min(max(int(np.floor(np.float32(pw) * bw)) + x1, 0), W)
                 we = min(max(int(np.ceil(np.float32(pw + 1) * bw)) + x1, 0), W)
                 if hs < he and ws < we:
-                    out[i, :, ph, pw] = features[bidx[i], :, hs:he, ws:we].amax((1, 2))
-    return out
+                    win = features[bidx[i], :, hs:he, ws:we]
+                    out[i, :, ph, pw] = win.amax((1, 2))
+                    if arg is not None:
+                        a = win.detach().flatten(1).argmax(1)      # first maximum
+                        arg[i, :, ph, pw] = (hs + a // (we - ws)) * W + ws + a % (we - ws)
+    return (out, arg) if return_argmax else out
 
 
 class _RoiPoolFn(torch.autograd.Function):
