@@ -116,4 +116,17 @@ struct JpegGeom {
   int total;                                 // blocks per image (all components)
 };
 
+// deep_input segments (wnd.hip): dense column blocks and embedding lookups of one row
+constexpr int DI_MAX_SEG = 8;
+struct DeepSeg {
+  const float* src;   // dense: [B][ld] fp32; embedding: table [V][width] fp32
+  float* gsrc;        // embedding: fp32 table gradient (null: no gradient)
+  int col0, width, ld, id_col, V, emb;
+};
+
+struct DeepSegs {
+  DeepSeg s[DI_MAX_SEG];
+  int n;
+};
+
 }  // namespace zoo

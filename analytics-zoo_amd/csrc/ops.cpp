@@ -52,6 +52,10 @@ hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t)
 hipError_t zoo_ssd_match(const float*, const int*, const float*, int, int, int, float, float, float, int, int*,
                          float*, unsigned long long*, float*, long long*, hipStream_t);
 hipError_t zoo_row_l2norm(const void*, const void*, const void*, void*, long, int, int, float, hipStream_t);
+hipError_t zoo_deep_input(const float*, int, const zoo::DeepSegs*, void*, const void*, int, int, hipStream_t);
+int zoo_wnd_head_blocks(int);
+hipError_t zoo_wnd_head_fwd(const float*, const void*, int, const float*, float*, int, int, hipStream_t);
+hipError_t zoo_wnd_head_bwd(const float*, const float*, float*, void*, int, float*, float*, int, int, hipStream_t);
 hipError_t zoo_ssd_mine(const float*, const long long*, int, int, int, float, unsigned char*, hipStream_t);
 hipError_t zoo_l2norm_scale_fwd(const void*, const float*, void*, float*, long, int, float, hipStream_t);
 int zoo_l2norm_scale_bwd_blocks(long);
@@ -453,6 +457,132 @@ torch::Tensor row_l2norm(torch::Tensor x, c10::optional<torch::Tensor> dy, c10::
                            out.data_ptr(), rows, (int)cols, x.scalar_type() == at::kFloat, (float)eps, cur_stream()),
             "row_l2norm");
   return out;
+}
+
+// Wide&Deep deep-tower input row: segments k = dense fp32 [B, w] blocks (id_cols[k] < 0) or
+// embedding lookups of fp32 tables [V, D] at the float id in column id_cols[k] of ids [B, E]
+static zoo::DeepSegs deep_segs(const torch::Tensor& ids, const std::vector<torch::Tensor>& srcs,
+                               const std::vector<int64_t>& id_cols, const std::vector<torch::Tensor>* grads, int* W) {
+  TORCH_CHECK(srcs.size() == id_cols.size() && srcs.size() <= (size_t)zoo::DI_MAX_SEG && !srcs.empty(),
+              "deep_input: 1..8 segments, one id column entry each");
+  const int64_t B = ids.size(0);
+  zoo::DeepSegs sg{};
+  sg.n = (int)srcs.size();
+  int col = 0;
+  for (size_t k = 0; k < srcs.size(); ++k) {
+    const auto& t = srcs[k];
+    req(t, at::kFloat, "deep_input segment");
+    TORCH_CHECK(t.dim() == 2, "deep_input: 2-D segments");
+    zoo::DeepSeg& d = sg.s[k];
+    d.src = t.data_ptr<float>();
+    d.col0 = col;
+    d.width = (int)t.size(1);
+    d.emb = id_cols[k] >= 0;
+    d.gsrc = nullptr;
+    if (d.emb) {
+      TORCH_CHECK(id_cols[k] < ids.size(1), "deep_input: id column out of range");
+      d.id_col = (int)id_cols[k];
+      d.V = (int)t.size(0);
+      d.ld = d.width;
+      if (grads && (*grads)[k].defined() && (*grads)[k].numel()) {
+        const auto& g = (*grads)[k];
+        req(g, at::kFloat, "deep_input table gradient");
+        TORCH_CHECK(g.sizes() == t.sizes(), "deep_input: table gradient shape");
+        d.gsrc = g.data_ptr<float>();
+      }
+    } else {
+      TORCH_CHECK(t.size(0) == B, "deep_input: dense segment batch");
+      d.id_col = 0;
+      d.V = 0;
+      d.ld = (int)t.size(1);
+    }
+    col += d.width;
+  }
+  *W = col;
+  return sg;
+}
+
+torch::Tensor deep_input_fwd(torch::Tensor ids, std::vector<torch::Tensor> srcs, std::vector<int64_t> id_cols) {
+  req(ids, at::kFloat, "ids");
+  TORCH_CHECK(ids.dim() == 2 && ids.size(0) < (1 << 30), "deep_input: ids [B, E]");
+  int W = 0;
+  const zoo::DeepSegs sg = deep_segs(ids, srcs, id_cols, nullptr, &W);
+  auto out = torch::empty({ids.size(0), (int64_t)W}, ids.options().dtype(at::kBFloat16));
+  if (ids.size(0) && W)
+    check_hip(zoo_deep_input(ids.data_ptr<float>(), (int)ids.size(1), &sg, out.data_ptr(), nullptr, (int)ids.size(0), W,
+                             cur_stream()),
+              "deep_input_fwd");
+  return out;
+}
+
+void deep_input_bwd(torch::Tensor dout, torch::Tensor ids, std::vector<torch::Tensor> srcs, std::vector<int64_t> id_cols,
+                    std::vector<torch::Tensor> grads) {
+  req(ids, at::kFloat, "ids");
+  req(dout, at::kBFloat16, "dout");
+  TORCH_CHECK(grads.size() == srcs.size(), "deep_input_bwd: one gradient entry per segment");
+  int W = 0;
+  const zoo::DeepSegs sg = deep_segs(ids, srcs, id_cols, &grads, &W);
+  TORCH_CHECK(dout.dim() == 2 && dout.size(0) == ids.size(0) && dout.size(1) == W, "deep_input_bwd: dout [B, W]");
+  if (ids.size(0) && W)
+    check_hip(zoo_deep_input(ids.data_ptr<float>(), (int)ids.size(1), &sg, nullptr, dout.data_ptr(), (int)ids.size(0),
+                             W, cur_stream()),
+              "deep_input_bwd");
+}
+
+// Wide&Deep head: softmax(wide + bias + deep) (fp32 probabilities [B, C], C <= 32)
+torch::Tensor wnd_head_fwd(c10::optional<torch::Tensor> wide, c10::optional<torch::Tensor> deep,
+                           c10::optional<torch::Tensor> bias) {
+  const torch::Tensor* ref = wide.has_value() ? &*wide : (deep.has_value() ? &*deep : nullptr);
+  TORCH_CHECK(ref != nullptr, "wnd_head: wide or deep input required");
+  const int64_t B = ref->size(0), C = ref->size(1);
+  TORCH_CHECK(C >= 1 && C <= 32 && B < (1 << 30), "wnd_head: 1..32 classes");
+  if (wide.has_value()) {
+    req(*wide, at::kFloat, "wide");
+    TORCH_CHECK(wide->dim() == 2 && wide->size(0) == B && wide->size(1) == C, "wnd_head: wide [B, C]");
+  }
+  bool dbf = false;
+  if (deep.has_value()) {
+    TORCH_CHECK(deep->is_cuda() && deep->is_contiguous() && deep->dim() == 2 && deep->size(0) == B && deep->size(1) == C,
+                "wnd_head: deep [B, C] contiguous");
+    TORCH_CHECK(deep->scalar_type() == at::kFloat || deep->scalar_type() == at::kBFloat16, "wnd_head: deep fp32/bf16");
+    dbf = deep->scalar_type() == at::kBFloat16;
+  }
+  if (bias.has_value()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == C, "wnd_head: bias [C]");
+  }
+  auto prob = torch::empty({B, C}, ref->options().dtype(at::kFloat));
+  if (B)
+    check_hip(zoo_wnd_head_fwd(wide.has_value() ? wide->data_ptr<float>() : nullptr,
+                               deep.has_value() ? deep->data_ptr() : nullptr, dbf,
+                               bias.has_value() ? bias->data_ptr<float>() : nullptr, prob.data_ptr<float>(), (int)B,
+                               (int)C, cur_stream()),
+              "wnd_head_fwd");
+  return prob;
+}
+
+// backward: returns (dwide fp32 | empty, ddeep in deep_dtype | empty); gbias (fp32 [C]) += column sums
+std::vector<torch::Tensor> wnd_head_bwd(torch::Tensor prob, torch::Tensor g, bool need_wide, bool need_deep,
+                                        bool deep_bf16, c10::optional<torch::Tensor> gbias) {
+  req(prob, at::kFloat, "prob");
+  req(g, at::kFloat, "grad");
+  TORCH_CHECK(prob.dim() == 2 && g.sizes() == prob.sizes() && prob.size(1) <= 32, "wnd_head_bwd: [B, C <= 32]");
+  const int64_t B = prob.size(0), C = prob.size(1);
+  torch::Tensor dw, dd, part;
+  if (need_wide) dw = torch::empty_like(prob);
+  if (need_deep) dd = torch::empty({B, C}, prob.options().dtype(deep_bf16 ? at::kBFloat16 : at::kFloat));
+  if (gbias.has_value()) {
+    req(*gbias, at::kFloat, "gbias");
+    TORCH_CHECK(gbias->numel() == C, "wnd_head_bwd: gbias [C]");
+    part = torch::empty({(int64_t)zoo_wnd_head_blocks((int)B) * C}, prob.options());
+  }
+  if (B)
+    check_hip(zoo_wnd_head_bwd(prob.data_ptr<float>(), g.data_ptr<float>(), need_wide ? dw.data_ptr<float>() : nullptr,
+                               need_deep ? dd.data_ptr() : nullptr, deep_bf16,
+                               gbias.has_value() ? gbias->data_ptr<float>() : nullptr,
+                               gbias.has_value() ? part.data_ptr<float>() : nullptr, (int)B, (int)C, cur_stream()),
+              "wnd_head_bwd");
+  return {need_wide ? dw : torch::Tensor(), need_deep ? dd : torch::Tensor()};
 }
 
 // SSD hard negative mining: ce [B, P] fp32 (per-prior confidence loss), conf_t [B, P] int64 ->
@@ -2453,6 +2583,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("bmm_nt", &bmm_nt);
   m.def("ssd_match", &ssd_match);
   m.def("ssd_mine", &ssd_mine);
+  m.def("deep_input_fwd", &deep_input_fwd);
+  m.def("deep_input_bwd", &deep_input_bwd);
+  m.def("wnd_head_fwd", &wnd_head_fwd);
+  m.def("wnd_head_bwd", &wnd_head_bwd);
   m.def("l2norm_scale_fwd", &l2norm_scale_fwd);
   m.def("l2norm_scale_bwd", &l2norm_scale_bwd);
   m.def("row_reduce", &row_reduce);

@@ -12,10 +12,10 @@ continuous columns -> MLP. ``model_type`` in {wide, deep, wide_n_deep}.
 import torch
 
 from zoo.models.recommendation.recommender import Recommender
-from zoo.pipeline.api.keras.base import Layer
-from zoo.pipeline.api.keras.engine.topology import Model, merge
-from zoo.pipeline.api.keras.layers import (Activation, CAdd, Dense, Embedding, Flatten, Input, Select,
-                                           SparseEmbedding)
+from zoo.ops.wnd import deep_input, wnd_head
+from zoo.pipeline.api.keras.base import Layer, init_tensor
+from zoo.pipeline.api.keras.engine.topology import Model
+from zoo.pipeline.api.keras.layers import Dense, Input, SparseEmbedding
 
 
 class ColumnFeatureInfo:
@@ -43,13 +43,71 @@ class ColumnFeatureInfo:
                     self.embed_out_dims, self.continuous_cols, self.label))
 
 
-class _DeepTowerInput(Layer):
-    """The concatenated deep-tower input in the MFMA kernels' compute dtype (bf16 on the GPU):
-    the Dense chain then runs bf16 in and out with no per-layer fp32 <-> bf16 conversions in
-    forward or backward (profiles/r3/wide_and_deep_b8192_r3.md); identity on the CPU."""
+class DeepColumns(Layer):
+    """The deep tower's input row: [indicator multi-hot | embedding(id_0) | ... | continuous]
+    (WideAndDeep.scala:122-135: Select + LookupTable per embed column, JoinTable). One native
+    kernel gathers the embedding rows (float ids converted in the kernel) and writes the whole
+    row as the bf16 MFMA operand of the first Dense (zoo.ops.wnd.deep_input, csrc/kernels/wnd.hip);
+    the table gradients are scatter-added straight into the flat gradient. Input: the list of
+    present column groups in the order (indicator, embed ids, continuous)."""
 
-    def call(self, x):
-        return x.to(torch.bfloat16) if x.is_cuda and x.is_floating_point() else x
+    def __init__(self, indicator_dim=0, embed_in_dims=(), embed_out_dims=(), continuous_dim=0, init="normal",
+                 **kwargs):
+        super().__init__(**kwargs)
+        self.indicator_dim, self.continuous_dim = int(indicator_dim), int(continuous_dim)
+        self.embed_in_dims = [int(d) for d in embed_in_dims]
+        self.embed_out_dims = [int(d) for d in embed_out_dims]
+        self.init = init
+
+    def build(self, input_shape):
+        for i, (din, dout) in enumerate(zip(self.embed_in_dims, self.embed_out_dims)):
+            w = torch.empty(din + 1, dout)          # ids are 1-based: row 0 stays unused, as LookupTable
+            init_tensor(w, self.init)
+            self.register_parameter("embeddings_%d" % i, torch.nn.Parameter(w))
+
+    def compute_output_shape(self, input_shape):
+        return (None, self.indicator_dim + sum(self.embed_out_dims) + self.continuous_dim)
+
+    def call(self, xs):
+        xs = list(xs) if isinstance(xs, (list, tuple)) else [xs]
+        segs, ids = [], None
+        k = 0
+        if self.indicator_dim:
+            segs.append(("dense", xs[k]))
+            k += 1
+        if self.embed_in_dims:
+            ids = xs[k]
+            k += 1
+            for i in range(len(self.embed_in_dims)):
+                segs.append(("embed", getattr(self, "embeddings_%d" % i), i))
+        if self.continuous_dim:
+            segs.append(("dense", xs[k]))
+        if ids is None:
+            ids = xs[0].new_zeros(xs[0].shape[0], 1)
+        return deep_input(ids, segs)
+
+
+class WideDeepHead(Layer):
+    """softmax(wide + bias + deep): the wide tower's CAdd bias, the CAddTable merge and the final
+    SoftMax of WideAndDeep.scala:136-144 in one native pass each way (zoo.ops.wnd.wnd_head).
+    Input: [wide, deep], [wide] (with bias) or [deep] (no bias)."""
+
+    def __init__(self, class_num, wide=True, deep=True, **kwargs):
+        super().__init__(**kwargs)
+        self.class_num, self.has_wide, self.has_deep = int(class_num), bool(wide), bool(deep)
+
+    def build(self, input_shape):
+        if self.has_wide:
+            self.bias = torch.nn.Parameter(torch.zeros(self.class_num))
+
+    def compute_output_shape(self, input_shape):
+        return (None, self.class_num)
+
+    def call(self, xs):
+        xs = list(xs) if isinstance(xs, (list, tuple)) else [xs]
+        wide = xs[0] if self.has_wide else None
+        deep = xs[-1] if self.has_deep else None
+        return wnd_head(wide, deep, self.bias if self.has_wide else None)
 
 
 class WideAndDeep(Recommender):
@@ -75,30 +133,21 @@ class WideAndDeep(Recommender):
         n = len(ci.wide_base_cols) + len(ci.wide_cross_cols)
         dims = sum(ci.wide_base_dims) + sum(ci.wide_cross_dims)
         inp = Input(shape=(n,))
-        lin = SparseEmbedding(dims, self.class_num, combiner="sum", init="zero")(inp)
-        return inp, CAdd((self.class_num,))(lin)
+        return inp, SparseEmbedding(dims, self.class_num, combiner="sum", init="zero")(inp)
 
     def _deep(self):
         ci = self.column_info
-        inputs, parts = [], []
+        inputs = []
         if ci.indicator_dims:
-            ind = Input(shape=(sum(ci.indicator_dims),))
-            inputs.append(ind)
-            parts.append(ind)
+            inputs.append(Input(shape=(sum(ci.indicator_dims),)))
         if ci.embed_in_dims:
-            emb_in = Input(shape=(len(ci.embed_in_dims),))
-            inputs.append(emb_in)
-            for i, (din, dout) in enumerate(zip(ci.embed_in_dims, ci.embed_out_dims)):
-                sel = Flatten()(Select(1, i)(emb_in))
-                parts.append(Flatten()(Embedding(din + 1, dout, init="normal")(sel)))
+            inputs.append(Input(shape=(len(ci.embed_in_dims),)))
         if ci.continuous_cols:
-            cont = Input(shape=(len(ci.continuous_cols),))
-            inputs.append(cont)
-            parts.append(cont)
-        if not parts:
+            inputs.append(Input(shape=(len(ci.continuous_cols),)))
+        if not inputs:
             raise TypeError("Empty deep tensors")
-        h = parts[0] if len(parts) == 1 else merge(parts, mode="concat")
-        h = _DeepTowerInput()(h)
+        h = DeepColumns(sum(ci.indicator_dims), ci.embed_in_dims, ci.embed_out_dims, len(ci.continuous_cols))(
+            inputs if len(inputs) > 1 else inputs[0])
         for u in self.hidden_layers:
             h = Dense(u, activation="relu")(h)
         return inputs, Dense(self.class_num, activation="relu")(h)
@@ -106,10 +155,10 @@ class WideAndDeep(Recommender):
     def build_model(self):
         if self.model_type == "wide":
             inp, lin = self._wide()
-            return Model(inp, Activation("softmax")(lin))
+            return Model(inp, WideDeepHead(self.class_num, wide=True, deep=False)(lin))
         if self.model_type == "deep":
             ins, deep = self._deep()
-            return Model(ins if len(ins) > 1 else ins[0], Activation("softmax")(deep))
+            return Model(ins if len(ins) > 1 else ins[0], WideDeepHead(self.class_num, wide=False, deep=True)(deep))
         winp, wide = self._wide()
         ins, deep = self._deep()
-        return Model([winp] + ins, Activation("softmax")(merge([wide, deep], mode="sum")))
+        return Model([winp] + ins, WideDeepHead(self.class_num)([wide, deep]))

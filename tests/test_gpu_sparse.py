@@ -132,3 +132,46 @@ def test_sparse_keras_layers_and_wide_and_deep_train_on_gpu(gpu):
     eng = TrainingEngine(model, ClassNLLCriterion(log_prob_as_input=False, zero_based_label=False), Adam(lr=1e-2))
     losses = [float(eng.train_step(xs, y)) for _ in range(15)]
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.gpu
+def test_wnd_deep_input_and_head_match_torch(gpu):
+    """Wide&Deep fused kernels (csrc/kernels/wnd.hip) vs the fp32 torch composition: the deep
+    input row (indicator | two embedding lookups from float ids | continuous; out-of-range id
+    -> zeros) forward + table gradients, and softmax(wide + bias + deep) forward + all three
+    gradients (fp32 and bf16 deep tower)."""
+    from zoo.ops.wnd import deep_input, wnd_head
+    torch.manual_seed(9)
+    B = 1000
+    ind = (torch.rand(B, 23, device=gpu) > 0.8).float()
+    cont = torch.rand(B, 1, device=gpu)
+    t0 = torch.randn(301, 64, device=gpu, requires_grad=True)
+    t1 = torch.randn(57, 16, device=gpu, requires_grad=True)
+    ids = torch.stack([torch.randint(0, 301, (B,), device=gpu), torch.randint(0, 57, (B,), device=gpu)], 1).float()
+    ids[3, 1] = 57                                        # out of range -> zero row, no gradient
+    out = deep_input(ids, [("dense", ind), ("embed", t0, 0), ("embed", t1, 1), ("dense", cont)])
+    assert out.dtype == torch.bfloat16 and out.shape == (B, 23 + 64 + 16 + 1)
+    r0, r1 = t0.detach().clone().requires_grad_(True), t1.detach().clone().requires_grad_(True)
+    i1 = ids[:, 1].long()
+    e1 = r1[i1.clamp(max=56)] * (i1 < 57).float().unsqueeze(1)
+    ref = torch.cat([ind, r0[ids[:, 0].long()], e1, cont], 1)
+    assert rel(out.float(), ref) < 1e-2
+    g = torch.randn(B, ref.shape[1], device=gpu)
+    out.backward(g.bfloat16())
+    ref.backward(g.bfloat16().float())
+    assert rel(t0.grad, r0.grad) < 1e-4
+    assert rel(t1.grad, r1.grad) < 1e-4
+    for dd in (torch.float32, torch.bfloat16):
+        wide = torch.randn(B, 5, device=gpu, requires_grad=True)
+        deep = torch.randn(B, 5, device=gpu).to(dd).requires_grad_(True)
+        bias = torch.randn(5, device=gpu, requires_grad=True)
+        p = wnd_head(wide, deep, bias)
+        wr, dr, br = (t.detach().float().clone().requires_grad_(True) for t in (wide, deep, bias))
+        pr = torch.softmax(wr + br + dr, -1)
+        assert rel(p, pr) < 1e-5
+        gp = torch.randn(B, 5, device=gpu)
+        p.backward(gp)
+        pr.backward(gp)
+        assert rel(wide.grad, wr.grad) < 1e-4
+        assert rel(deep.grad.float(), dr.grad) < 1e-2
+        assert rel(bias.grad, br.grad) < 1e-4
