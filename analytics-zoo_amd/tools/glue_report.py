@@ -2,7 +2,7 @@
 """Which framework-level ops launch the non-native ("glue") GPU kernels of a training step:
 torch.profiler with CUDA activity over a few engine steps, aten ops ranked by the device time of
 the kernels they launch, with input shapes; zoo:: kernels (hand-written HIP) are reported as one
-line. Models: wnd (Wide&Deep ml-20m shape), ssd (SSD-300 VGG), ncf.
+line. Models: wnd (Wide&Deep ml-20m shape), ssd (SSD-300 VGG), ncf, resnet (bench.py ResNet-50 b256).
 
   python tools/glue_report.py --model wnd [--steps 3]
 """
@@ -50,12 +50,17 @@ def _engine(name):
             lab = torch.randint(1, 21, (3, 1), generator=g).float()
             gt.append(torch.cat([lab, xy, xy + wh], 1).to(ctx.device))
         return TrainingEngine(m, loss_fn, SGD(learningrate=1e-3, momentum=0.9)), x, gt
+    if name == "resnet":
+        sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+        import bench
+        eng, (x, y), _, _ = bench.build_resnet50(ctx, 256)
+        return eng, x, y
     raise ValueError(name)
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="wnd", choices=["wnd", "ssd", "ncf"])
+    ap.add_argument("--model", default="wnd", choices=["wnd", "ssd", "ncf", "resnet"])
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rows", type=int, default=30)
     a = ap.parse_args()
