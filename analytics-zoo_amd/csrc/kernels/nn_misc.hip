@@ -213,6 +213,143 @@ __global__ __launch_bounds__(256) void layernorm_bwd_reg_kernel(const T* __restr
   }
 }
 
+// bf16 LayerNorm backward, v2: 4-element (8-byte) chunks so D = 768 maps onto all 64 lanes
+// (3 chunks each; the 8-element layout left half the wave idle on its second chunk), two rows
+// per wave iteration with all of both rows' loads issued before the first reduction (twice the
+// bytes in flight per wave), and the dgamma / dbeta block partials stored plainly
+// (part[block][2][D]) for an ordered fold instead of ~10^6 contended global atomics.
+template <int NCH>
+__global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __restrict__ dY,
+                                                               const bf16_t* __restrict__ X,
+                                                               const float* __restrict__ g,
+                                                               const float* __restrict__ mean,
+                                                               const float* __restrict__ rstd, bf16_t* __restrict__ dX,
+                                                               float* __restrict__ part, int rows, int D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const float invD = 1.f / (float)D;
+  float gg[NCH][4], pg[NCH][4], pb[NCH][4];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { gg[k][e] = 1.f; pg[k][e] = 0.f; pb[k][e] = 0.f; }
+    if (g && c < D) {
+      const float4 g0 = *reinterpret_cast<const float4*>(g + c);
+      gg[k][0] = g0.x; gg[k][1] = g0.y; gg[k][2] = g0.z; gg[k][3] = g0.w;
+    }
+  }
+  const int pairs = (rows + 1) >> 1;
+  for (int pr = blockIdx.x * 4 + wid; pr < pairs; pr += gridDim.x * 4) {
+    const int r0 = pr * 2;
+    const bool has1 = r0 + 1 < rows;
+    uint2 xv[2][NCH], dv[2][NCH];
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int c = (k * 64 + lane) * 4;
+        const bool ok = c < D && (h == 0 || has1);
+        const size_t off = (size_t)(r0 + h) * D + c;
+        xv[h][k] = ok ? *reinterpret_cast<const uint2*>(X + off) : make_uint2(0u, 0u);
+        dv[h][k] = ok ? *reinterpret_cast<const uint2*>(dY + off) : make_uint2(0u, 0u);
+      }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h == 1 && !has1) break;
+      const int row = r0 + h;
+      const float mu = mean[row], rs = rstd[row];
+      float xh[NCH][4], gv[NCH][4];
+      float a = 0.f, bsum = 0.f;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int c = (k * 64 + lane) * 4;
+        xh[k][0] = bf2f((bf16_t)(xv[h][k].x & 0xFFFFu)); xh[k][1] = bf2f((bf16_t)(xv[h][k].x >> 16));
+        xh[k][2] = bf2f((bf16_t)(xv[h][k].y & 0xFFFFu)); xh[k][3] = bf2f((bf16_t)(xv[h][k].y >> 16));
+        gv[k][0] = bf2f((bf16_t)(dv[h][k].x & 0xFFFFu)); gv[k][1] = bf2f((bf16_t)(dv[h][k].x >> 16));
+        gv[k][2] = bf2f((bf16_t)(dv[h][k].y & 0xFFFFu)); gv[k][3] = bf2f((bf16_t)(dv[h][k].y >> 16));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          xh[k][e] = c < D ? (xh[k][e] - mu) * rs : 0.f;
+          const float gy = gv[k][e] * gg[k][e];
+          a = fmaf(gy, xh[k][e], a);
+          bsum += gy;
+          pg[k][e] = fmaf(gv[k][e], xh[k][e], pg[k][e]);
+          pb[k][e] += gv[k][e];
+        }
+      }
+      a = warp_sum(a) * invD;
+      bsum = warp_sum(bsum) * invD;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) {
+        const int c = (k * 64 + lane) * 4;
+        if (c >= D) continue;
+        float o[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = rs * (gv[k][e] * gg[k][e] - bsum - xh[k][e] * a);
+        *reinterpret_cast<uint2*>(dX + (size_t)row * D + c) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+      }
+    }
+  }
+  if (!part) return;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    const int c = (k * 64 + lane) * 4;
+    if (c >= D) continue;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      red[(wid * 2) * D + c + e] = pg[k][e];
+      red[(wid * 2 + 1) * D + c + e] = pb[k][e];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * D; i += blockDim.x) {
+    const int w2 = i >= D ? 1 : 0, col = i - w2 * D;
+    part[(size_t)blockIdx.x * 2 * D + i] =
+        ((red[(0 * 2 + w2) * D + col] + red[(1 * 2 + w2) * D + col]) + red[(2 * 2 + w2) * D + col]) +
+        red[(3 * 2 + w2) * D + col];
+  }
+}
+
+// Ordered two-level fold of the block partials: level 1 sums groups of 32 partial rows per
+// column (64 columns x one group per workgroup, 4 independent chains), level 2 adds the group
+// sums in order into dg / db. (A single pass with one thread per column was latency-bound:
+// ~150 us for 1024 partial rows.)
+constexpr int LN_FOLD_G = 32;
+
+__global__ __launch_bounds__(64) void layernorm_part_fold1_kernel(const float* __restrict__ part, int nb, int n2,
+                                                                  float* __restrict__ lvl) {
+  const int col = blockIdx.x * 64 + threadIdx.x;
+  if (col >= n2) return;
+  const int b0 = blockIdx.y * LN_FOLD_G, b1 = min(nb, b0 + LN_FOLD_G);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int b = b0;
+  for (; b + 3 < b1; b += 4) {
+    s0 += part[(size_t)b * n2 + col];
+    s1 += part[(size_t)(b + 1) * n2 + col];
+    s2 += part[(size_t)(b + 2) * n2 + col];
+    s3 += part[(size_t)(b + 3) * n2 + col];
+  }
+  for (; b < b1; ++b) s0 += part[(size_t)b * n2 + col];
+  lvl[(size_t)blockIdx.y * n2 + col] = (s0 + s1) + (s2 + s3);
+}
+
+// one wave per column: lane l reads group l's sum (ng <= 64), fixed-order shuffle tree
+__global__ __launch_bounds__(256) void layernorm_part_fold2_kernel(const float* __restrict__ lvl, int ng, int D,
+                                                                   float* __restrict__ dg, float* __restrict__ db) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= 2 * D) return;
+  const float s = warp_sum(lane < ng ? lvl[(size_t)lane * 2 * D + i] : 0.f);
+  if (lane != 0) return;
+  if (i < D) {
+    if (dg) dg[i] += s;
+  } else if (db) {
+    db[i - D] += s;
+  }
+}
+
 // ---------------------------------------------------------------- Dropout (+ residual add)
 // out = x + keep(i) * a * scale  (x optional). keep(i) is a counter-based hash of (seed, i),
 // so backward regenerates the mask instead of storing it: da = keep(i) * dout * scale.
@@ -429,9 +566,53 @@ extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, 
   return hipGetLastError();
 }
 
+static int ln_v2_nch(int D) {
+  static const bool on = [] {
+    const char* e = getenv("ZOO_LN_BWD_V2");
+    return e ? atoi(e) != 0 : true;
+  }();
+  if (!on || D % 4 || D > 64 * 4 * 4) return 0;
+  return (D + 255) / 256;                      // 4-element chunks per lane
+}
+
+static int ln_v2_blocks(int rows) {
+  int b = ((rows + 1) / 2 + 7) / 8;            // >= 2 row pairs per wave
+  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+// fp32 scratch floats the bf16 v2 backward needs for its dgamma / dbeta partials (0: none)
+extern "C" size_t zoo_layernorm_bwd_part_floats(int rows, int D, int f32) {
+  if (f32 || !ln_v2_nch(D)) return 0;
+  const int nb = ln_v2_blocks(rows);
+  return ((size_t)nb + (nb + LN_FOLD_G - 1) / LN_FOLD_G) * 2 * D;
+}
+
 extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
                                         const float* rstd, void* dX, float* dg, float* db, int rows, int D,
-                                        hipStream_t st) {
+                                        float* part, hipStream_t st) {
+  const int nch = f32 ? 0 : ln_v2_nch(D);
+  if (nch && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+    const int blocks = ln_v2_blocks(rows);
+    float* pp = (dg || db) ? part : nullptr;
+    if ((dg || db) && !part) return hipErrorInvalidValue;
+    const size_t lds = (size_t)8 * D * sizeof(float);
+#define ZOO_LNB2(N)                                                                                              \
+  hipLaunchKernelGGL((layernorm_bwd_v2_kernel<N>), dim3(blocks), dim3(256), lds, st, (const bf16_t*)dY,         \
+                     (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, pp, rows, D)
+    if (nch == 1) ZOO_LNB2(1);
+    else if (nch == 2) ZOO_LNB2(2);
+    else if (nch == 3) ZOO_LNB2(3);
+    else ZOO_LNB2(4);
+#undef ZOO_LNB2
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !pp) return e;
+    const int ng = (blocks + LN_FOLD_G - 1) / LN_FOLD_G;
+    float* lvl = pp + (size_t)blocks * 2 * D;
+    hipLaunchKernelGGL(layernorm_part_fold1_kernel, dim3((2 * D + 63) / 64, ng), dim3(64), 0, st, pp, blocks, 2 * D,
+                       lvl);
+    hipLaunchKernelGGL(layernorm_part_fold2_kernel, dim3((2 * D + 3) / 4), dim3(256), 0, st, lvl, ng, D, dg, db);
+    return hipGetLastError();
+  }
   const bool al = (reinterpret_cast<uintptr_t>(g) & 15) == 0 && (f32 ? D % 4 == 0 : D % 8 == 0);
   if (al && D <= 2048 && (f32 ? D % 8 == 0 : true)) {
     // ~512 blocks of 4 waves; each wave loops over rows, so the dgamma/dbeta partials are

@@ -120,7 +120,8 @@ hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
 hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
-                             float*, int, int, hipStream_t);
+                             float*, int, int, float*, hipStream_t);
+size_t zoo_layernorm_bwd_part_floats(int, int, int);
 hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, int, int64_t, hipStream_t);
 hipError_t zoo_resize_normalize(const void*, void*, int, int, int, int, int, int, const float*, const float*, int, int,
                                 hipStream_t);
@@ -1625,9 +1626,12 @@ torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<tor
   if (dg.has_value() && dg->defined()) { req(*dg, at::kFloat, "dgamma"); TORCH_CHECK(dg->numel() == D, "dg"); }
   if (db.has_value() && db->defined()) { req(*db, at::kFloat, "dbeta"); TORCH_CHECK(db->numel() == D, "db"); }
   auto dx = torch::empty_like(x);
+  torch::Tensor part;
+  const size_t pf = zoo_layernorm_bwd_part_floats((int)rows, D, f32);
+  if (pf && (opt_ptr<float>(dg) || opt_ptr<float>(db))) part = torch::empty({(int64_t)pf}, mean.options());
   check_hip(zoo_layernorm_bwd(dy.data_ptr(), x.data_ptr(), f32, opt_ptr<float>(g), mean.data_ptr<float>(),
                               rstd.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dg), opt_ptr<float>(db),
-                              (int)rows, D, cur_stream()),
+                              (int)rows, D, part.defined() ? part.data_ptr<float>() : nullptr, cur_stream()),
             "layernorm_bwd");
   return dx;
 }

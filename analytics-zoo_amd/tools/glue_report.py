@@ -2,7 +2,7 @@
 """Which framework-level ops launch the non-native ("glue") GPU kernels of a training step:
 torch.profiler with CUDA activity over a few engine steps, aten ops ranked by the device time of
 the kernels they launch, with input shapes; zoo:: kernels (hand-written HIP) are reported as one
-line. Models: wnd (Wide&Deep ml-20m shape), ssd (SSD-300 VGG), ncf, resnet (bench.py ResNet-50 b256).
+line. Models: wnd (Wide&Deep ml-20m shape), ssd (SSD-300 VGG), ncf, resnet (bench.py ResNet-50 b256), bert (BERT-base b128 s128).
 
   python tools/glue_report.py --model wnd [--steps 3]
 """
@@ -50,6 +50,20 @@ def _engine(name):
             lab = torch.randint(1, 21, (3, 1), generator=g).float()
             gt.append(torch.cat([lab, xy, xy + wh], 1).to(ctx.device))
         return TrainingEngine(m, loss_fn, SGD(learningrate=1e-3, momentum=0.9)), x, gt
+    if name == "bert":
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        from bert_train import _Classifier
+        from zoo.ops import softmax_cross_entropy
+        from zoo.pipeline.api.keras.layers import BERT
+        from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+        bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512,
+                    intermediate_size=3072, output_all_block=False)
+        B, L = 128, 128
+        dev = ctx.device
+        xs = [torch.randint(0, 30522, (B, L), device=dev), torch.zeros(B, L, dtype=torch.long, device=dev),
+              torch.arange(L, device=dev).repeat(B, 1), torch.ones(B, L, device=dev)]
+        y = torch.randint(0, 2, (B,), device=dev)
+        return TrainingEngine(_Classifier(bert), softmax_cross_entropy, AdamWeightDecay(lr=2e-5)), xs, y
     if name == "resnet":
         sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
         import bench
@@ -60,7 +74,7 @@ def _engine(name):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--model", default="wnd", choices=["wnd", "ssd", "ncf", "resnet"])
+    ap.add_argument("--model", default="wnd", choices=["wnd", "ssd", "ncf", "resnet", "bert"])
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--rows", type=int, default=30)
     a = ap.parse_args()

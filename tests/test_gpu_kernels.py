@@ -393,7 +393,7 @@ def test_resnet_learns_synthetic_task(gpu):
 
 
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("rows,D", [(37, 768), (4099, 768), (515, 1000), (300, 2048), (64, 100)])
+@pytest.mark.parametrize("rows,D", [(37, 768), (4099, 768), (16384, 768), (5, 256), (515, 1000), (300, 2048), (64, 100)])
 def test_layernorm_kernel(gpu, dt, rows, D):
     """register-resident (D % 8 == 0, D <= 2048) and generic paths, fwd + bwd"""
     from zoo.ops import layer_norm
