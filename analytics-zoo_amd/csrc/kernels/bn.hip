@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
     const float* __restrict__ beta, const bf16_t* __restrict__ resid, bf16_t* __restrict__ Y,
     float* __restrict__ running_mean, float* __restrict__ running_var, float* __restrict__ save_mean,
     float* __restrict__ save_invstd, int M, int C, float eps, float momentum, int relu, int training,
-    int rows_per_block, BnSide r2) {
+    int rows_per_block, BnSide r2, uint8_t* __restrict__ mask) {
   const float invM = 1.f / (float)M;
   if (blockIdx.x == 0 && training) {  // bookkeeping: saved statistics + running averages
     bn_bookkeeping(stats, running_mean, running_var, save_mean, save_invstd, M, C, eps, momentum);
@@ -263,6 +263,12 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
             for (int e = 0; e < 8; ++e) v[e] += q[e];
           }
         }
+        if (mask) {  // ReLU bit mask for the consumer's fused BN-backward (BwdStats.zmode 2)
+          unsigned b = 0;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b |= (v[e] > 0.f ? 1u : 0u) << e;
+          mask[((size_t)r * C >> 3) + chunk] = (uint8_t)b;
+        }
         if (relu) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = v[e] > 0.f ? v[e] : 0.f;
@@ -275,6 +281,8 @@ __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
 
 // backward apply: dx = A_c*dy + B_c*x + D_c with
 //   A = gamma*is, B = -A*is*mean(dy*xhat), D = A*(mu*is*mean(dy*xhat) - mean(dy))
+// U rows per thread per step (2 or 4): U x (dz, x[, z]) 16-byte loads in flight per thread
+template <int U>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
     const bf16_t* __restrict__ dZ, const bf16_t* __restrict__ Z, const bf16_t* __restrict__ X,
     const float* __restrict__ save_mean, const float* __restrict__ save_invstd,
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
   const int cpr = C >> 3;
   const RowSplit rs = row_split(cpr);
   if (rs.rsub >= rs.rstep) return;
-  const int tile = 2 * rs.rstep;
+  const int tile = U * rs.rstep;
   const bool inter = rows_per_block == 0;
   const int r0 = (inter ? blockIdx.x * tile : blockIdx.x * rows_per_block) + rs.rsub;
   const int r1 = inter ? M : min(M, blockIdx.x * rows_per_block + rows_per_block);
@@ -314,9 +322,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
       kd[e] = a * (mu * is * m2 - m1);
     }
     for (int rb = r0; rb < r1; rb += rstride) {
-      uint4 dv[2], xv[2], zv[2];
+      uint4 dv[U], xv[U], zv[U];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int r = rb + u * rs.rstep;
         const size_t off = (size_t)(r < r1 ? r : rb) * C + chunk * 8;
         dv[u] = *reinterpret_cast<const uint4*>(dZ + off);
@@ -324,7 +332,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(
         if (Z) zv[u] = *reinterpret_cast<const uint4*>(Z + off);
       }
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
+      for (int u = 0; u < U; ++u) {
         const int r = rb + u * rs.rstep;
         if (r >= r1) break;
         const size_t off = (size_t)r * C + chunk * 8;
@@ -758,7 +766,7 @@ extern "C" hipError_t zoo_bn_fwd_apply(const void* X, const float* stats, const 
                                        const float* beta, const void* resid, void* Y, float* rmean,
                                        float* rvar, float* smean, float* sinv, int M, int C, float eps,
                                        float momentum, int relu, int training, const void* const* r2,
-                                       hipStream_t st) {
+                                       void* mask, hipStream_t st) {
   int rpb, blocks;
   apply_grid(M, C, 4, &blocks, &rpb);
   BnSide side{nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -769,7 +777,7 @@ extern "C" hipError_t zoo_bn_fwd_apply(const void* X, const float* stats, const 
   }
   hipLaunchKernelGGL(bn_fwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X,
                      stats, gamma, beta, (const bf16_t*)resid, (bf16_t*)Y, rmean, rvar, smean, sinv, M, C, eps,
-                     momentum, relu, training, rpb, side);
+                     momentum, relu, training, rpb, side, (uint8_t*)mask);
   return hipGetLastError();
 }
 
@@ -777,11 +785,21 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                                        const float* sinv, const float* gamma, const float* sums, void* dX,
                                        void* dResid, float* dgamma, float* dbeta, int M, int C,
                                        hipStream_t st) {
+  // rows per step: 4 keeps 8-12 loads in flight per thread (ZOO_BN_BWD_ROWS=2: the round-2 form)
+  static const int rows = [] {
+    const char* e = getenv("ZOO_BN_BWD_ROWS");
+    return e && atoi(e) == 2 ? 2 : 4;
+  }();
   int rpb, blocks;
-  apply_grid(M, C, 2, &blocks, &rpb);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dZ,
-                     (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
-                     dgamma, dbeta, M, C, rpb);
+  apply_grid(M, C, rows, &blocks, &rpb);
+  if (rows == 2)
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<2>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dZ,
+                       (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
+                       dgamma, dbeta, M, C, rpb);
+  else
+    hipLaunchKernelGGL(bn_bwd_apply_kernel<4>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dZ,
+                       (const bf16_t*)Z, (const bf16_t*)X, smean, sinv, gamma, sums, (bf16_t*)dX, (bf16_t*)dResid,
+                       dgamma, dbeta, M, C, rpb);
   return hipGetLastError();
 }
 

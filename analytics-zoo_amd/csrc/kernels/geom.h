@@ -43,6 +43,16 @@ struct BwdStats {
   // `sums` collects its plain column sums (the producing linear's bias gradient); y / mean /
   // inv are unused (the transformer FFN: GELU backward in the next linear's dgrad epilogue)
   int zgelu;
+  // ReLU-mask source when zgelu == 0 (bnmask.h bnm_apply):
+  //   0: z is the bf16 ReLU output, keep where z > 0 (nullptr: no mask);
+  //   1: no z read -- the mask is recomputed from y (already read for the sums) with the
+  //      producer's affine: y * gamma * inv + (beta - mean * gamma * inv) > 0, the expression its
+  //      forward apply evaluated (units without a residual add);
+  //   2: z is a bit mask written by the forward apply, bit (c % 8) of byte (m * K + c) / 8
+  //      (units with a residual add, where y alone does not determine the sign)
+  int zmode;
+  const float* mgamma;  // zmode 1 (nullptr: gamma = 1 / beta = 0)
+  const float* mbeta;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

@@ -23,6 +23,7 @@
 
 #include "common.h"
 #include "geom.h"
+#include "bnmask.h"
 
 namespace zoo {
 
@@ -391,11 +392,13 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
 
   if constexpr (EPI == 2) {
-    float mu[8], iv[8];
-    if (bs.sums && !bs.zgelu && col_ok) {
+    float mu[8], iv[8], msc[8], msh[8];
+    const bool bnsum = bs.sums && !bs.zgelu;
+    if (bnsum && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
     }
+    bnm_coeffs(bs, col0, col_ok && !bs.zgelu, msc, msh);
     const int rend = min(BM, g.M - m0);
     for (int rr = rr0; col_ok && rr < rend; rr += RSTEP) {
       const int m = m0 + rr;
@@ -418,16 +421,15 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += rv[e];
       }
-      if (bs.z) {
+      float yy[8];
+      if (bnsum) unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+      if (bs.zgelu) {
         float zz[8];
         unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
-        if (bs.zgelu) {
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
-        } else {
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
-        }
+        for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
+      } else {
+        bnm_apply(bs, off, yy, msc, msh, v);
       }
       const uint4 pk = pack8(v);
       *reinterpret_cast<uint4*>(Y + off) = pk;
@@ -438,8 +440,6 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) s1[e] += q[e];
         } else {
-          float yy[8];
-          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
             s1[e] += q[e];
@@ -477,13 +477,12 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
       *reinterpret_cast<float4*>(Yf + off) = make_float4(v[0], v[1], v[2], v[3]);
       *reinterpret_cast<float4*>(Yf + off + 4) = make_float4(v[4], v[5], v[6], v[7]);
     }
+    float yy[8];
     if (bs.sums) {  // fused BN-backward: mask with the producer's ReLU, accumulate (dy, dy*xhat)
-      if (bs.z) {
-        float zz[8];
-        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
-      }
+      unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+      float msc[8], msh[8];
+      bnm_coeffs(bs, col0, true, msc, msh);
+      bnm_apply(bs, off, yy, msc, msh, v);
     }
     if (Y) {
       const uint4 pk = pack8(v);
@@ -494,9 +493,8 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
       } else if (bs.sums) {
-        float q[8], yy[8];
+        float q[8];
         unpack8(pk, q);
-        unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           s1[e] += q[e];

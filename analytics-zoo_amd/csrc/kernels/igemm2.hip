@@ -43,6 +43,7 @@
 
 #include "common.h"
 #include "geom.h"
+#include "bnmask.h"
 
 namespace zoo {
 
@@ -235,11 +236,13 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
       for (int e = 0; e < 8; ++e) bsv[e] = bias[col0 + e];
     }
   }
+  float msc[8], msh[8];
   if constexpr (EPI == 0 || EPI == 2) {
     if (bs.sums && !bs.zgelu && col_ok) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) { mu[e] = bs.mean[col0 + e]; iv[e] = bs.inv[col0 + e]; }
     }
+    bnm_coeffs(bs, col0, col_ok && bs.sums && !bs.zgelu, msc, msh);
   }
   // EPI 1: stats only; EPI 2: BN-backward sums only; EPI 0: either (stats win)
   const bool want_stats = stats != nullptr || bs.sums != nullptr;
@@ -298,16 +301,16 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rv[e];
         }
-        if (bs.z) {
+        float yy[8];
+        const bool bnsum = bs.sums && !bs.zgelu;
+        if (bnsum) unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+        if (bs.zgelu) {
           float zz[8];
           unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
-          if (bs.zgelu) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
-          } else {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
-          }
+          for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
+        } else {
+          bnm_apply(bs, off, yy, msc, msh, v);
         }
         const uint4 pk = pack8(v);
         *reinterpret_cast<uint4*>(Y + off) = pk;
@@ -318,8 +321,6 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) s1[e] += q[e];
           } else {
-            float yy[8];
-            unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               s1[e] += q[e];
@@ -336,11 +337,10 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
         }
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e] + bsv[e], act);
-        if (bs.sums && bs.z) {
-          float zz[8];
-          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+        float yy[8];
+        if (bs.sums) {
+          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+          bnm_apply(bs, off, yy, msc, msh, v);
         }
         if (Yf) {
           *reinterpret_cast<float4*>(Yf + off) = make_float4(v[0], v[1], v[2], v[3]);
@@ -355,8 +355,6 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
           } else if (bs.sums) {
-            float yy[8];
-            unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               s1[e] += q[e];

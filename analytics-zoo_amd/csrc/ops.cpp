@@ -74,7 +74,8 @@ int zoo_act_bwd_reduce_parts(int, int);
 hipError_t zoo_bn_reduce(const void*, const void*, const void*, const float*, const float*, float*, int, int, int, int,
                          hipStream_t);
 hipError_t zoo_bn_fwd_apply(const void*, const float*, const float*, const float*, const void*, void*, float*, float*,
-                            float*, float*, int, int, float, float, int, int, const void* const*, hipStream_t);
+                            float*, float*, int, int, float, float, int, int, const void* const*, void*,
+                            hipStream_t);
 hipError_t zoo_bn_bwd_apply(const void*, const void*, const void*, const float*, const float*, const float*,
                             const float*, void*, void*, float*, float*, int, int, hipStream_t);
 hipError_t zoo_maxpool_fwd(const void*, void*, void*, int, int, int, int, int, int, int, int, int, int, int, int,
@@ -235,7 +236,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        int out_w, c10::optional<torch::Tensor> out, std::vector<int64_t> omap,
                        c10::optional<torch::Tensor> bz, c10::optional<torch::Tensor> by,
                        c10::optional<torch::Tensor> bmean, c10::optional<torch::Tensor> binv,
-                       c10::optional<torch::Tensor> bsums) {
+                       c10::optional<torch::Tensor> bsums, c10::optional<torch::Tensor> bgamma,
+                       c10::optional<torch::Tensor> bbeta) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -312,10 +314,27 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
       bs.mean = bmean->data_ptr<float>();
       bs.inv = binv->data_ptr<float>();
     }
-    if (bz.has_value() && bz->defined()) {
+    if (bz.has_value() && bz->defined() && !gelu && bz->scalar_type() == at::kByte) {
+      // producer ReLU as a bit mask (bn_fwd_apply mask): 1 bit per output element
+      TORCH_CHECK(bz->is_cuda() && bz->is_contiguous() && bz->numel() * 8 == full,
+                  "bn z bit mask must be a contiguous uint8 [numel/8] tensor");
+      bs.z = bz->data_ptr();
+      bs.zmode = 2;
+    } else if (bz.has_value() && bz->defined()) {
       req(*bz, at::kBFloat16, "bn z");
       TORCH_CHECK(bz->numel() == full, "bn z must match the output");
       bs.z = bz->data_ptr();
+    } else if (!gelu && bgamma.has_value() && bgamma->defined()) {
+      // producer ReLU recomputed from y with its affine (no residual add in that unit)
+      req(*bgamma, at::kFloat, "bn gamma");
+      TORCH_CHECK(bgamma->numel() == K, "bn gamma must be [K]");
+      bs.mgamma = bgamma->data_ptr<float>();
+      if (bbeta.has_value() && bbeta->defined()) {
+        req(*bbeta, at::kFloat, "bn beta");
+        TORCH_CHECK(bbeta->numel() == K, "bn beta must be [K]");
+        bs.mbeta = bbeta->data_ptr<float>();
+      }
+      bs.zmode = 1;
     }
     TORCH_CHECK(!stats.has_value() || !stats->defined(), "stats and fused bn-backward are exclusive");
     TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
@@ -817,7 +836,8 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
                            c10::optional<torch::Tensor> beta, c10::optional<torch::Tensor> resid,
                            c10::optional<torch::Tensor> rmean, c10::optional<torch::Tensor> rvar,
                            torch::Tensor smean, torch::Tensor sinv, double eps, double momentum, bool relu,
-                           bool training, std::vector<c10::optional<torch::Tensor>> resid_bn) {
+                           bool training, std::vector<c10::optional<torch::Tensor>> resid_bn,
+                           c10::optional<torch::Tensor> mask) {
   req(x, at::kBFloat16, "x");
   const int C = x.size(-1);
   const int64_t M = x.numel() / C;
@@ -860,11 +880,18 @@ torch::Tensor bn_fwd_apply(torch::Tensor x, torch::Tensor stats, c10::optional<t
       r2[i] = t->data_ptr();
     }
   }
+  // mask: [M*C/8] uint8 ReLU bit mask of the pre-ReLU sign (BwdStats.zmode 2 consumers)
+  void* mp = nullptr;
+  if (mask.has_value() && mask->defined()) {
+    TORCH_CHECK(mask->is_cuda() && mask->scalar_type() == at::kByte && mask->is_contiguous() &&
+                    mask->numel() == M * C / 8, "bn: mask must be a contiguous uint8 [M*C/8] tensor");
+    mp = mask->data_ptr();
+  }
   auto y = torch::empty_like(x);
   check_hip(zoo_bn_fwd_apply(x.data_ptr(), training ? stats.data_ptr<float>() : nullptr, opt_ptr<float>(gamma),
                              opt_ptr<float>(beta), opt_ptr<void>(resid), y.data_ptr(), opt_ptr<float>(rmean),
                              opt_ptr<float>(rvar), smean.data_ptr<float>(), sinv.data_ptr<float>(), (int)M, C,
-                             (float)eps, (float)momentum, relu, training, resid_bn.empty() ? nullptr : r2,
+                             (float)eps, (float)momentum, relu, training, resid_bn.empty() ? nullptr : r2, mp,
                              cur_stream()),
             "bn_fwd_apply");
   return y;
@@ -2505,7 +2532,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("jpeg_idct", &jpeg_idct);
   m.def("jpeg_color_resize", &jpeg_color_resize);
   m.def("gemm", &gemm);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
+        py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none());
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
@@ -2560,7 +2588,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("bn_fwd_apply", &bn_fwd_apply, py::arg("x"), py::arg("stats"), py::arg("gamma"), py::arg("beta"),
         py::arg("resid"), py::arg("rmean"), py::arg("rvar"), py::arg("smean"), py::arg("sinv"), py::arg("eps"),
         py::arg("momentum"), py::arg("relu"), py::arg("training"),
-        py::arg("resid_bn") = std::vector<c10::optional<torch::Tensor>>());
+        py::arg("resid_bn") = std::vector<c10::optional<torch::Tensor>>(), py::arg("mask") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

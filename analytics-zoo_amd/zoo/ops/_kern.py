@@ -19,14 +19,18 @@ from zoo.ops._native import native
 
 def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
              act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None):
-    """``bstats = (z or None, y, mean, inv, sums)`` fuses the producing unit's
-    BN-backward reduction (and ReLU mask) into this conv's epilogue."""
-    bz = by = bm = bi = bsum = None
+    """``bstats = (z or None, y, mean, inv, sums[, gamma, beta])`` fuses the producing unit's
+    BN-backward reduction (and ReLU mask) into this conv's epilogue. The mask source: a bf16
+    ``z`` (ReLU output), a uint8 ``z`` (1-bit mask of the forward apply), or -- z None and
+    gamma given -- recomputed from ``y`` with the unit's affine (csrc/kernels/bnmask.h)."""
+    bz = by = bm = bi = bsum = bg = bb = None
     if bstats is not None:
-        bz, by, bm, bi, bsum = bstats
+        bz, by, bm, bi, bsum = bstats[:5]
+        if len(bstats) > 5:
+            bg, bb = bstats[5], bstats[6]
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
-                             list(omap) if omap else [], bz, by, bm, bi, bsum)
+                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb)
 
 
 # ---------------------------------------------------------------------------

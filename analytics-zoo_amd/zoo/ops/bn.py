@@ -28,6 +28,11 @@ from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_acti
 # (csrc/kernels/bn.hip). Must match zoo::kStatSlots.
 STAT_SLOTS = 16
 
+# How a consumer's fused BN-backward epilogue recovers this unit's ReLU mask (BwdStats.zmode,
+# csrc/kernels/bnmask.h): 1 = recompute it from y (no residual) or read a 1-bit mask written by
+# the forward apply (residual units); 0 = re-read the bf16 ReLU output z (A/B comparator).
+_BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
+
 
 def stat_len(c):
     return 2 * int(c) * (STAT_SLOTS + 1) + 4
@@ -67,20 +72,32 @@ class BNProducer:
     # producer -> z would be a reference cycle that keeps every step's
     # activations alive until the cyclic GC runs. The consumer passes its own
     # saved input (which is z) to bstats() instead.
-    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused")
+    # With ZOO_BN_MASK (default) the consumer never re-reads z for the mask: a unit without a
+    # residual hands over its affine (gamma, beta) and the epilogue recomputes the sign from the
+    # y it reads for the sums anyway; a residual unit hands over the 1-bit mask its forward
+    # apply wrote (``mask``). 2 bytes per element less epilogue traffic either way.
+    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused", "gamma", "beta", "mask")
 
     def __init__(self, relu, y, mean, inv):
         self.relu, self.y, self.mean, self.inv = relu, y, mean, inv
         self.sums = None
         self.fused = False
+        self.gamma = self.beta = self.mask = None
 
     def bstats(self, z):
         self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
         self.fused = True
-        return (z if self.relu else None, self.y, self.mean, self.inv, self.sums)
+        if not self.relu:
+            return (None, self.y, self.mean, self.inv, self.sums)
+        if self.mask is not None:
+            return (self.mask, self.y, self.mean, self.inv, self.sums)
+        if self.gamma is not None:
+            return (None, self.y, self.mean, self.inv, self.sums, self.gamma, self.beta)
+        return (z, self.y, self.mean, self.inv, self.sums)
 
     def release(self):
         self.y = self.mean = self.inv = self.sums = None
+        self.gamma = self.beta = self.mask = None
         self.fused = False
 
 
@@ -125,9 +142,17 @@ class _ConvBNActFn(torch.autograd.Function):
             ctx.gamma2, ctx.beta2 = gamma2, beta2
         if training:
             _kern.bump_stats_epoch()
+        mask = None
+        po = producer_out if (training and relu and _BN_MASK) else None
+        if po is not None and resid is not None:
+            mask = torch.empty(y.numel() // 8, device=x.device, dtype=torch.uint8)
         z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
                             beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,
-                            training, side)
+                            training, side, mask)
+        if po is not None:
+            po.mask = mask
+            if resid is None:
+                po.gamma, po.beta = gamma.detach(), beta.detach()
         if rb is not None:
             ctx.yres = resid        # shortcut conv output: its BN backward needs it
         ctx.save_for_backward(x, w, gamma, y, z if relu else None, smean, sinv)

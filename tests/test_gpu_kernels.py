@@ -300,6 +300,50 @@ def test_resnet_bn_backward_fusion_matches_unfused(gpu, block):
     assert F.cosine_similarity(u[0], f[0], dim=0).item() > 0.98
 
 
+@pytest.mark.parametrize("block", ["bottleneck", "basic"])
+def test_resnet_bn_mask_modes_match_z_reads(gpu, block):
+    """The fused BN-backward epilogue's ReLU mask recomputed from y (units without a residual)
+    or read from the forward apply's 1-bit mask (residual units) must equal the mask from
+    re-reading the bf16 ReLU output z. With the ordered (atomic-free) reductions the runs are
+    bit-reproducible, so the gradients must be IDENTICAL, and the mask buffers really used."""
+    import zoo.models.image.resnet as R
+    import zoo.ops.bn as B
+    from zoo.ops import softmax_cross_entropy, deterministic, set_deterministic
+    torch.manual_seed(0)
+    blk = R.Bottleneck if block == "bottleneck" else R.BasicBlock
+    m = R.ResNet(blk, [2, 2, 1, 1], num_classes=16, width=16).to(gpu)
+    x = torch.randn(8, 3, 96, 96, device=gpu)
+    y = torch.randint(0, 16, (8,), device=gpu)
+    grads = []
+    seen = {"mask": 0, "affine": 0}
+    orig = B.BNProducer.bstats
+
+    def spy(self, z):
+        out = orig(self, z)
+        if out[0] is not None and out[0].dtype == torch.uint8:
+            seen["mask"] += 1
+        if len(out) > 5:
+            seen["affine"] += 1
+        return out
+    prev = deterministic()
+    try:
+        set_deterministic(True)
+        B.BNProducer.bstats = spy
+        for mode in (False, False, True, True):
+            B._BN_MASK = mode
+            m.zero_grad(set_to_none=True)
+            softmax_cross_entropy(m(x), y).backward()
+            grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.parameters()]).double())
+    finally:
+        B._BN_MASK = True
+        B.BNProducer.bstats = orig
+        set_deterministic(prev)
+    assert seen["mask"] > 0 and seen["affine"] > 0, seen
+    assert torch.equal(grads[0], grads[1]) and torch.equal(grads[2], grads[3]), "not reproducible"
+    diff = (grads[0] - grads[2]).abs().max().item()
+    assert diff == 0.0, diff
+
+
 def test_resnet_s2d_stem_matches_7x7_stem(gpu):
     """The space-to-depth stem (4x4/1 conv on the s2d image) must equal the 7x7/2
     conv+BN+ReLU stem: output, input-free weight gradient and BN parameter grads."""
