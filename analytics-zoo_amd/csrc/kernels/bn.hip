@@ -785,10 +785,11 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                                        const float* sinv, const float* gamma, const float* sums, void* dX,
                                        void* dResid, float* dgamma, float* dbeta, int M, int C,
                                        hipStream_t st) {
-  // rows per step: 4 keeps 8-12 loads in flight per thread (ZOO_BN_BWD_ROWS=2: the round-2 form)
+  // rows per step (ZOO_BN_BWD_ROWS=4: 8-12 loads in flight per thread): 2 and 4 measure the
+  // same, 6-8.6 TB/s on the ResNet-50 shapes (tools/bn_bench.py, round 3)
   static const int rows = [] {
     const char* e = getenv("ZOO_BN_BWD_ROWS");
-    return e && atoi(e) == 2 ? 2 : 4;
+    return e && atoi(e) == 4 ? 4 : 2;
   }();
   int rpb, blocks;
   apply_grid(M, C, rows, &blocks, &rpb);
@@ -808,7 +809,13 @@ static void colsum_grid(int M, int C, int* ct, int* col_groups, int* chunks, int
   const int cpr = C >> 3;
   *ct = (cpr % 64 == 0 || cpr > 256) ? 64 : 32;
   *col_groups = (cpr + *ct - 1) / *ct;
-  int ch = 1024 / *col_groups;
+  // total blocks (ZOO_COLSUM_BLOCKS): every block ends in one fp32 atomic per column, so the
+  // block count is also the number of adders per output address
+  static const int target = [] {
+    const char* e = getenv("ZOO_COLSUM_BLOCKS");
+    return e && atoi(e) > 0 ? atoi(e) : 256;  // BERT b128: 17.37 -> 17.20 ms/step vs 1024
+  }();
+  int ch = target / *col_groups;
   const int max_ch = (M + 31) / 32;
   if (ch > max_ch) ch = max_ch;
   if (ch < 1) ch = 1;

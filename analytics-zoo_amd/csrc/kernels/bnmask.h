@@ -43,4 +43,22 @@ ZOO_DEV void bnm_apply(const BwdStats& bs, size_t off, const float* yy, const fl
   }
 }
 
+// bnm_apply with the mask operand already loaded (batched epilogues that issue every pass's
+// loads before the first store): mbits = the zmode-2 byte, zv = the zmode-0 z chunk
+ZOO_DEV void bnm_apply_pre(const BwdStats& bs, const float* yy, const float* sc, const float* sh, unsigned mbits,
+                           const uint4& zv, float* v) {
+  if (bs.zmode == 1) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = yy[e] * sc[e] + sh[e] > 0.f ? v[e] : 0.f;
+  } else if (bs.zmode == 2) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = (mbits >> e) & 1u ? v[e] : 0.f;
+  } else if (bs.z) {
+    float zz[8];
+    unpack8(zv, zz);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+  }
+}
+
 }  // namespace zoo

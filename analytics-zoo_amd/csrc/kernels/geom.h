@@ -53,6 +53,7 @@ struct BwdStats {
   int zmode;
   const float* mgamma;  // zmode 1 (nullptr: gamma = 1 / beta = 0)
   const float* mbeta;
+  int unbatched;        // 1: igemm.hip EPI 2 row loop without batched loads (A/B, ZOO_EPI2_BATCH=0)
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

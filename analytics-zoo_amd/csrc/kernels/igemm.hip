@@ -400,6 +400,66 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     }
     bnm_coeffs(bs, col0, col_ok && !bs.zgelu, msc, msh);
     const int rend = min(BM, g.M - m0);
+    // Full tiles: the global loads (residual gradient, producer y, mask) of PB passes are all
+    // issued before the first of their stores, so each wave keeps PB x 2-3 16-byte loads in
+    // flight instead of one pass's worth (the row loop is otherwise latency-bound: a stage-1
+    // conv1 dgrad moved ~1.4 GB at 3.9 TB/s). Each element is still read before it is written
+    // by the same lane, so an in-place residual (resid == Y) stays correct.
+    constexpr int NP = BM / RSTEP;
+    constexpr int PB = NP < 4 ? NP : 4;
+    if (rend == BM && col_ok && !bs.zgelu && !bs.unbatched) {
+#pragma unroll
+      for (int p0 = 0; p0 < NP; p0 += PB) {
+        size_t offs[PB];
+        uint4 rv[PB], yv[PB], zv[PB];
+        unsigned mb[PB];
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const int m = m0 + rr0 + (p0 + u) * RSTEP;
+          if (g.omap) {
+            const int n = m / PQ, pq = m - n * PQ;
+            const int p = pq / g.Q, q = pq - p * g.Q;
+            offs[u] = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
+          } else {
+            offs[u] = (size_t)m * g.K + col0;
+          }
+          rv[u] = yv[u] = zv[u] = uint4{0u, 0u, 0u, 0u};
+          mb[u] = 0u;
+          if (resid) rv[u] = *reinterpret_cast<const uint4*>(resid + offs[u]);
+          if (bnsum) yv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + offs[u]);
+          if (bs.zmode == 2) mb[u] = reinterpret_cast<const uint8_t*>(bs.z)[offs[u] >> 3];
+          else if (bs.zmode == 0 && bs.z)
+            zv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + offs[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < PB; ++u) {
+          const int rr = rr0 + (p0 + u) * RSTEP;
+          const float4 lo = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8);
+          const float4 hi = *reinterpret_cast<const float4*>(Cs + rr * EPI_LD + ch * 8 + 4);
+          float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+          if (resid) {
+            float r8[8];
+            unpack8(rv[u], r8);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += r8[e];
+          }
+          float yy[8];
+          unpack8(yv[u], yy);
+          bnm_apply_pre(bs, yy, msc, msh, mb[u], zv[u], v);
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(Y + offs[u]) = pk;
+          if (bnsum) {
+            float q[8];
+            unpack8(pk, q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+            }
+          }
+        }
+      }
+    } else
     for (int rr = rr0; col_ok && rr < rend; rr += RSTEP) {
       const int m = m0 + rr;
       float v[8];

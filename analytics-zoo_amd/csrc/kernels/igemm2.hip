@@ -247,8 +247,58 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
   // EPI 1: stats only; EPI 2: BN-backward sums only; EPI 0: either (stats win)
   const bool want_stats = stats != nullptr || bs.sums != nullptr;
 
+  // EPI 2: the global operands of 16-row slice i + 1 (residual gradient, producer y, ReLU
+  // mask / GELU pre-activation) are fetched while slice i is staged and stored, so their
+  // latency overlaps the LDS patch round trip instead of serialising every slice
+  // (ZOO_EPI2_BATCH=0: loads at the point of use)
+  // (tiles with 128 accumulator registers per lane -- 256x256 -- have no room for the
+  // prefetch registers: it spilled to scratch there, so they keep the loads at their use)
+  const bool pre2 = EPI == 2 && TM * TN <= 16 && !bs.unbatched;
+  uint4 nrv[PPL], nyv[PPL], nzv[PPL];
+  unsigned nmb[PPL];
+  auto slice_off = [&](int i, int h, bool& ok) -> size_t {
+    const int prow = (lane + 64 * h) / CPR;
+    const int m = m0 + wm * WTM + i * 16 + prow;
+    ok = m < g.M && col_ok;
+    if (!ok) return 0;
+    if (g.omap) {
+      const int n = m / PQ, pq = m - n * PQ;
+      const int p = pq / g.Q, q = pq - p * g.Q;
+      return ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
+    }
+    return (size_t)m * g.K + col0;
+  };
+  auto fetch2 = [&](int i) {
+#pragma unroll
+    for (int h = 0; h < PPL; ++h) {
+      bool ok;
+      const size_t off = slice_off(i, h, ok);
+      nrv[h] = nyv[h] = nzv[h] = uint4{0u, 0u, 0u, 0u};
+      nmb[h] = 0u;
+      if (!ok) continue;
+      if (resid) nrv[h] = *reinterpret_cast<const uint4*>(resid + off);
+      if (bs.sums && !bs.zgelu) nyv[h] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off);
+      if (bs.zgelu || (bs.zmode == 0 && bs.z))
+        nzv[h] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off);
+      else if (bs.zmode == 2)
+        nmb[h] = reinterpret_cast<const uint8_t*>(bs.z)[off >> 3];
+    }
+  };
+  if constexpr (EPI == 2) {
+    if (pre2) fetch2(0);
+  }
+
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
+    uint4 crv[PPL], cyv[PPL], czv[PPL];
+    unsigned cmb[PPL];
+    if constexpr (EPI == 2) {
+      if (pre2) {
+#pragma unroll
+        for (int h = 0; h < PPL; ++h) { crv[h] = nrv[h]; cyv[h] = nyv[h]; czv[h] = nzv[h]; cmb[h] = nmb[h]; }
+        if (i + 1 < TM) fetch2(i + 1);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
@@ -297,18 +347,21 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
       } else if constexpr (EPI == 2) {
         if (resid) {
           float rv[8];
-          unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+          unpack8(pre2 ? crv[h] : *reinterpret_cast<const uint4*>(resid + off), rv);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] += rv[e];
         }
         float yy[8];
         const bool bnsum = bs.sums && !bs.zgelu;
-        if (bnsum) unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
+        if (bnsum)
+          unpack8(pre2 ? cyv[h] : *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off), yy);
         if (bs.zgelu) {
           float zz[8];
-          unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+          unpack8(pre2 ? czv[h] : *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] *= gelu_grad_f(zz[e]);
+        } else if (pre2) {
+          bnm_apply_pre(bs, yy, msc, msh, cmb[h], czv[h], v);
         } else {
           bnm_apply(bs, off, yy, msc, msh, v);
         }

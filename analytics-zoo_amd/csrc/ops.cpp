@@ -340,6 +340,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
     bs.sums = bsums->data_ptr<float>();
   }
+  static const bool epi2_unbatched = !env_flag("ZOO_EPI2_BATCH", true);
+  bs.unbatched = epi2_unbatched ? 1 : 0;
   // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
   // they are folded in order into the caller's buffer (its first 2K floats)
   float* const stat_dst = sp ? sp : bs.sums;
