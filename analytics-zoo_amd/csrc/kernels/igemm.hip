@@ -241,6 +241,45 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     }
   };
 
+  // ---- EPI 2 operand prefetch (1x1 dgrads: a short K loop, often one tile) ----
+  // The backward epilogue's global operands (residual gradient, producer y, ReLU mask) do not
+  // depend on the GEMM: for 1x1 layers their first batch of loads is issued here, so it is in
+  // flight together with the operand DMA instead of after the MFMAs (ZOO_EPI2_BATCH=0: off).
+  constexpr int E2_CPR = BN / 8, E2_RSTEP = IG_NT / E2_CPR;
+  constexpr int E2_NP = BM / E2_RSTEP, E2_PB = E2_NP < 4 ? E2_NP : 4;
+  const int e2_ch = tid % E2_CPR, e2_rr0 = tid / E2_CPR, e2_col0 = n0 + e2_ch * 8;
+  const bool e2_fast = EPI == 2 && e2_col0 < g.K && g.M - m0 >= BM && !bs.zgelu && !bs.unbatched;
+  size_t e2_off[E2_PB];
+  uint4 e2_rv[E2_PB], e2_yv[E2_PB], e2_zv[E2_PB];
+  unsigned e2_mb[E2_PB];
+  auto e2_fetch = [&](int p0) {
+#pragma unroll
+    for (int u = 0; u < E2_PB; ++u) {
+      const int m = m0 + e2_rr0 + (p0 + u) * E2_RSTEP;
+      if (g.omap) {
+        const int n = m / PQ, pq = m - n * PQ;
+        const int p = pq / g.Q, q = pq - p * g.Q;
+        e2_off[u] = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + e2_col0;
+      } else {
+        e2_off[u] = (size_t)m * g.K + e2_col0;
+      }
+      e2_rv[u] = e2_yv[u] = e2_zv[u] = uint4{0u, 0u, 0u, 0u};
+      e2_mb[u] = 0u;
+      if (resid) e2_rv[u] = *reinterpret_cast<const uint4*>(resid + e2_off[u]);
+      if (bs.sums) e2_yv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + e2_off[u]);
+      if (bs.zmode == 2) e2_mb[u] = reinterpret_cast<const uint8_t*>(bs.z)[e2_off[u] >> 3];
+      else if (bs.zmode == 0 && bs.z)
+        e2_zv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + e2_off[u]);
+    }
+  };
+  // only for 1-2 K-tiles: across a longer K loop the held registers and the extra in-flight
+  // loads cost more than they hide (conv3 dgrad, Ktot 256: 161 -> 178 us; conv1, Ktot 64:
+  // 303 -> 275 us, profiles/r3/epilogue_batching_r3.md)
+  const bool e2_early = IS1x1 && e2_fast && g.ldb <= 2 * BK;
+  if constexpr (EPI == 2 && IS1x1) {
+    if (e2_early) e2_fetch(0);
+  }
+
   // ---- main loop: one barrier per K tile, loads of tile k+1 overlap MFMA on tile k ----
   if constexpr (DMA) {
     // tile k+1 streams into the other LDS buffer (free since the previous barrier)
@@ -405,32 +444,17 @@ __global__ __launch_bounds__(256, 2) void igemm_kernel(
     // flight instead of one pass's worth (the row loop is otherwise latency-bound: a stage-1
     // conv1 dgrad moved ~1.4 GB at 3.9 TB/s). Each element is still read before it is written
     // by the same lane, so an in-place residual (resid == Y) stays correct.
-    constexpr int NP = BM / RSTEP;
-    constexpr int PB = NP < 4 ? NP : 4;
-    if (rend == BM && col_ok && !bs.zgelu && !bs.unbatched) {
+    constexpr int NP = E2_NP, PB = E2_PB;
+    static_assert(E2_RSTEP == RSTEP, "EPI 2 prefetch geometry");
+    if (e2_fast) {
 #pragma unroll
       for (int p0 = 0; p0 < NP; p0 += PB) {
-        size_t offs[PB];
-        uint4 rv[PB], yv[PB], zv[PB];
-        unsigned mb[PB];
-#pragma unroll
-        for (int u = 0; u < PB; ++u) {
-          const int m = m0 + rr0 + (p0 + u) * RSTEP;
-          if (g.omap) {
-            const int n = m / PQ, pq = m - n * PQ;
-            const int p = pq / g.Q, q = pq - p * g.Q;
-            offs[u] = ((size_t)(n * g.oH + g.oh0 + g.osh * p) * g.oW + g.ow0 + g.osw * q) * g.K + col0;
-          } else {
-            offs[u] = (size_t)m * g.K + col0;
-          }
-          rv[u] = yv[u] = zv[u] = uint4{0u, 0u, 0u, 0u};
-          mb[u] = 0u;
-          if (resid) rv[u] = *reinterpret_cast<const uint4*>(resid + offs[u]);
-          if (bnsum) yv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + offs[u]);
-          if (bs.zmode == 2) mb[u] = reinterpret_cast<const uint8_t*>(bs.z)[offs[u] >> 3];
-          else if (bs.zmode == 0 && bs.z)
-            zv[u] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + offs[u]);
-        }
+        if (!(p0 == 0 && e2_early)) e2_fetch(p0);  // batch 0 may be in flight since the prologue
+        const size_t* offs = e2_off;
+        const uint4* rv = e2_rv;
+        const uint4* yv = e2_yv;
+        const uint4* zv = e2_zv;
+        const unsigned* mb = e2_mb;
 #pragma unroll
         for (int u = 0; u < PB; ++u) {
           const int rr = rr0 + (p0 + u) * RSTEP;

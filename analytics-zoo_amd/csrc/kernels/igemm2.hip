@@ -565,6 +565,15 @@ static int i2_choose(const ConvGeom& g, int epi) {
   if (f > 0) return f;
   auto tiles = [&](int t) { return (long)((g.M + i2_bm(t) - 1) / i2_bm(t)) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
   if (g.K < 256) return 0;
+  if (epi == 4) {
+    // GELU-backward dgrad (BERT FFN): ZOO_I2_GELU_TILE picks its tile (A/B of the 128x128
+    // tile, whose EPI 2 prefetches the next slice's pre-activation, against 256x256)
+    static const int gt = [] {
+      const char* e = getenv("ZOO_I2_GELU_TILE");
+      return e ? atoi(e) : 0;
+    }();
+    if (gt > 0 && g.Ktot >= 256) return gt;
+  }
   if (epi == 2 && g.Ktot < 1024) return 0;
   if (epi != 2 && g.Ktot < 256) return 0;
   if (tiles(I2_256x256) >= 160) return I2_256x256;
