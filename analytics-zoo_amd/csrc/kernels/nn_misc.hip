@@ -224,7 +224,8 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
                                                                const float* __restrict__ g,
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ rstd, bf16_t* __restrict__ dX,
-                                                               float* __restrict__ part, int rows, int D) {
+                                                               float* __restrict__ part, int rows, int D,
+                                                               const bf16_t* __restrict__ dY2) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
   for (int pr = blockIdx.x * 4 + wid; pr < pairs; pr += gridDim.x * 4) {
     const int r0 = pr * 2;
     const bool has1 = r0 + 1 < rows;
-    uint2 xv[2][NCH], dv[2][NCH];
+    uint2 xv[2][NCH], dv[2][NCH], d2[2][NCH];
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
@@ -254,6 +255,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
         const size_t off = (size_t)(r0 + h) * D + c;
         xv[h][k] = ok ? *reinterpret_cast<const uint2*>(X + off) : make_uint2(0u, 0u);
         dv[h][k] = ok ? *reinterpret_cast<const uint2*>(dY + off) : make_uint2(0u, 0u);
+        d2[h][k] = ok && dY2 ? *reinterpret_cast<const uint2*>(dY2 + off) : make_uint2(0u, 0u);
       }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -269,6 +271,10 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
         xh[k][2] = bf2f((bf16_t)(xv[h][k].y & 0xFFFFu)); xh[k][3] = bf2f((bf16_t)(xv[h][k].y >> 16));
         gv[k][0] = bf2f((bf16_t)(dv[h][k].x & 0xFFFFu)); gv[k][1] = bf2f((bf16_t)(dv[h][k].x >> 16));
         gv[k][2] = bf2f((bf16_t)(dv[h][k].y & 0xFFFFu)); gv[k][3] = bf2f((bf16_t)(dv[h][k].y >> 16));
+        if (dY2) {  // second output gradient (a residual consumer's, LayerNorm GradAdd), summed in fp32
+          gv[k][0] += bf2f((bf16_t)(d2[h][k].x & 0xFFFFu)); gv[k][1] += bf2f((bf16_t)(d2[h][k].x >> 16));
+          gv[k][2] += bf2f((bf16_t)(d2[h][k].y & 0xFFFFu)); gv[k][3] += bf2f((bf16_t)(d2[h][k].y >> 16));
+        }
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           xh[k][e] = c < D ? (xh[k][e] - mu) * rs : 0.f;
@@ -587,18 +593,22 @@ extern "C" size_t zoo_layernorm_bwd_part_floats(int rows, int D, int f32) {
   return ((size_t)nb + (nb + LN_FOLD_G - 1) / LN_FOLD_G) * 2 * D;
 }
 
+// dY2 (nullable): a second output gradient added to dY inside the bf16 v2 kernel; the other
+// paths return hipErrorNotSupported for it (the caller then adds it first)
 extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
                                         const float* rstd, void* dX, float* dg, float* db, int rows, int D,
-                                        float* part, hipStream_t st) {
+                                        float* part, const void* dY2, hipStream_t st) {
   const int nch = f32 ? 0 : ln_v2_nch(D);
-  if (nch && (reinterpret_cast<uintptr_t>(g) & 15) == 0) {
+  const bool v2 = nch && (reinterpret_cast<uintptr_t>(g) & 15) == 0;
+  if (dY2 && !v2) return hipErrorNotSupported;
+  if (v2) {
     const int blocks = ln_v2_blocks(rows);
     float* pp = (dg || db) ? part : nullptr;
     if ((dg || db) && !part) return hipErrorInvalidValue;
     const size_t lds = (size_t)8 * D * sizeof(float);
 #define ZOO_LNB2(N)                                                                                              \
   hipLaunchKernelGGL((layernorm_bwd_v2_kernel<N>), dim3(blocks), dim3(256), lds, st, (const bf16_t*)dY,         \
-                     (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, pp, rows, D)
+                     (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, pp, rows, D, (const bf16_t*)dY2)
     if (nch == 1) ZOO_LNB2(1);
     else if (nch == 2) ZOO_LNB2(2);
     else if (nch == 3) ZOO_LNB2(3);

@@ -121,7 +121,7 @@ hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
 hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
-                             float*, int, int, float*, hipStream_t);
+                             float*, int, int, float*, const void*, hipStream_t);
 size_t zoo_layernorm_bwd_part_floats(int, int, int);
 hipError_t zoo_embedding_fwd(const void*, int, const int64_t*, void*, int, int, int, int64_t, hipStream_t);
 hipError_t zoo_resize_normalize(const void*, void*, int, int, int, int, int, int, const float*, const float*, int, int,
@@ -1645,7 +1645,8 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, c10::optional<torch::T
 }
 
 torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> g, torch::Tensor mean,
-                            torch::Tensor rstd, c10::optional<torch::Tensor> dg, c10::optional<torch::Tensor> db) {
+                            torch::Tensor rstd, c10::optional<torch::Tensor> dg, c10::optional<torch::Tensor> db,
+                            c10::optional<torch::Tensor> dy2) {
   TORCH_CHECK(dy.is_cuda() && dy.is_contiguous() && x.is_contiguous(), "layernorm_bwd: contiguous GPU tensors");
   TORCH_CHECK(dy.scalar_type() == x.scalar_type() && dy.numel() == x.numel(), "layernorm_bwd: dy/x mismatch");
   const bool f32 = is_f32(x);
@@ -1658,10 +1659,25 @@ torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<tor
   torch::Tensor part;
   const size_t pf = zoo_layernorm_bwd_part_floats((int)rows, D, f32);
   if (pf && (opt_ptr<float>(dg) || opt_ptr<float>(db))) part = torch::empty({(int64_t)pf}, mean.options());
-  check_hip(zoo_layernorm_bwd(dy.data_ptr(), x.data_ptr(), f32, opt_ptr<float>(g), mean.data_ptr<float>(),
-                              rstd.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dg), opt_ptr<float>(db),
-                              (int)rows, D, part.defined() ? part.data_ptr<float>() : nullptr, cur_stream()),
-            "layernorm_bwd");
+  // dy2: a second gradient of the output (the residual consumer's, GradAdd), summed inside the
+  // kernel where it supports it, else added here first
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    TORCH_CHECK(dy2->is_cuda() && dy2->is_contiguous() && dy2->scalar_type() == dy.scalar_type() &&
+                    dy2->numel() == dy.numel(), "layernorm_bwd: dy2 must match dy");
+    d2 = dy2->data_ptr();
+  }
+  hipError_t e = zoo_layernorm_bwd(dy.data_ptr(), x.data_ptr(), f32, opt_ptr<float>(g), mean.data_ptr<float>(),
+                                   rstd.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dg), opt_ptr<float>(db),
+                                   (int)rows, D, part.defined() ? part.data_ptr<float>() : nullptr, d2, cur_stream());
+  if (e == hipErrorNotSupported && d2) {
+    (void)hipGetLastError();
+    auto dys = dy.add(*dy2);
+    e = zoo_layernorm_bwd(dys.data_ptr(), x.data_ptr(), f32, opt_ptr<float>(g), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), dx.data_ptr(), opt_ptr<float>(dg), opt_ptr<float>(db), (int)rows,
+                          D, part.defined() ? part.data_ptr<float>() : nullptr, nullptr, cur_stream());
+  }
+  check_hip(e, "layernorm_bwd");
   return dx;
 }
 
@@ -2610,7 +2626,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("sum_chunks_bf16", &sum_chunks_bf16);
   m.def("add_bf16", &add_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
-  m.def("layernorm_bwd", &layernorm_bwd);
+  m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("mean"),
+        py::arg("rstd"), py::arg("dg"), py::arg("db"), py::arg("dy2") = py::none());
   m.def("embedding_fwd", &embedding_fwd);
   m.def("embedding_bwd", &embedding_bwd);
   m.def("linear_wgrad", &linear_wgrad);

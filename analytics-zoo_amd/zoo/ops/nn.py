@@ -24,10 +24,13 @@ def _ready(p):
 
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, gamma, beta, eps):
+    def forward(ctx, x, gamma, beta, eps, grad_in=None):
         y, mean, rstd = native().layernorm_fwd(x, None if gamma is None else gamma.detach(),
                                                None if beta is None else beta.detach(), eps)
         ctx.save_for_backward(x, gamma, beta, mean, rstd)
+        ctx.grad_in = grad_in
+        if grad_in is not None:
+            grad_in.armed = True   # a residual consumer of y may park its gradient here
         return y
 
     @staticmethod
@@ -35,13 +38,19 @@ class _LayerNormFn(torch.autograd.Function):
         x, gamma, beta, mean, rstd = ctx.saved_tensors
         dg, own_g = _target(gamma) if gamma is not None else (None, False)
         db, own_b = _target(beta) if beta is not None else (None, False)
+        dy2 = None
+        h = ctx.grad_in
+        if h is not None:
+            dy2, h.grad = h.grad, None
+            if dy2 is not None:
+                dy2 = dy2.contiguous().to(x.dtype)
         dx = native().layernorm_bwd(dy.contiguous().to(x.dtype), x, None if gamma is None else gamma.detach(), mean,
-                                    rstd, dg, db)
+                                    rstd, dg, db, dy2)
         if own_g:
             _ready(gamma)
         if own_b:
             _ready(beta)
-        return dx, (None if own_g else dg), (None if own_b else db), None
+        return dx, (None if own_g else dg), (None if own_b else db), None, None
 
 
 _DROP_RNG = []
@@ -116,10 +125,13 @@ def dropout_add(a, x, p, training=True, grad_add=None):
     return x + F.dropout(a, p, True)
 
 
-def layer_norm(x, gamma=None, beta=None, eps=1e-5):
+def layer_norm(x, gamma=None, beta=None, eps=1e-5, grad_in=None):
+    """``grad_in``: a :class:`GradAdd` the consumers of the OUTPUT can park a gradient in
+    (``dropout_add(a, y, ..., grad_add=h)``, the Transformer residual): the backward kernel sums
+    it with the incoming gradient, so autograd runs no separate add over y."""
     D = x.shape[-1]
     if x.is_cuda and D % 8 == 0 and x.dtype in (torch.float32, torch.bfloat16):
-        return _LayerNormFn.apply(x.contiguous(), gamma, beta, float(eps))
+        return _LayerNormFn.apply(x.contiguous(), gamma, beta, float(eps), grad_in)
     if (gamma is not None and gamma.dtype != x.dtype) or (beta is not None and beta.dtype != x.dtype):
         # fp32 affine parameters with a low-precision input: normalise in fp32
         return F.layer_norm(x.float(), (D,), None if gamma is None else gamma.float(),

@@ -31,6 +31,9 @@ from zoo.pipeline.api.keras.base import Layer
 # BERT-base b128 (same-box A/B 17.13/17.15 ms off vs 17.24/17.15 on: hipBLASLt's beta=1
 # epilogue costs what the separate add did), so opt-in
 _RESID_GRAD_FUSE = os.environ.get("ZOO_RESID_GRAD_FUSE", "0") != "0"
+# residual gradient summed inside the producing LayerNorm's backward kernel instead (the
+# LayerNorm that made x / n is armed; the residual dropout_add parks its gradient there)
+_LN_GRAD_ADD = os.environ.get("ZOO_LN_GRAD_ADD", "1") != "0"
 
 
 def _normal(shape, std):
@@ -63,6 +66,12 @@ class _Block(nn.Module):
         # x and n each feed a linear and a residual add: the add's x-gradient is folded into
         # the linear's data-gradient GEMM (GradAdd) instead of a separate autograd sum
         h1, h2 = (GradAdd(), GradAdd()) if _RESID_GRAD_FUSE else (None, None)
+        # ... or into the backward of the LayerNorm that produced x (the previous block's output
+        # LayerNorm, which attached its holder to x) and n (this block's first LayerNorm)
+        lx = ln_n = ln_out = None
+        if h1 is None and _LN_GRAD_ADD and x.is_cuda and torch.is_grad_enabled():
+            lx = getattr(x, "_zoo_grad_in", None)
+            ln_n, ln_out = GradAdd(), GradAdd()
         qkv = ops.linear(x, self.qkv_w, self.qkv_b, grad_add=h1)     # [B, L, 3H]
         # strided fused kernels (attention-probability dropout in-kernel), no head copies
         a = attention_packed(qkv, nh, mask=mask, causal=causal, dropout_p=self.attn_drop, training=self.training)
@@ -72,16 +81,20 @@ class _Block(nn.Module):
                               training=self.training)
             a = a.transpose(1, 2).reshape(B, L, H)
         a = ops.linear(a, self.proj_w, self.proj_b)
-        n = ops.layer_norm(dropout_add(a, x, self.hidden_drop, self.training, grad_add=h1), self.ln1_g, self.ln1_b,
-                           self.ln_eps)
+        n = ops.layer_norm(dropout_add(a, x, self.hidden_drop, self.training, grad_add=h1 if h1 is not None else lx),
+                           self.ln1_g, self.ln1_b, self.ln_eps, grad_in=ln_n)
         act = "gelu" if self.gelu == "erf" else None
         gl = GeluLink() if act == "gelu" else None      # GELU backward in fc2's dgrad epilogue
         m = ops.linear(n, self.fc1_w, self.fc1_b, act=act, grad_add=h2, gelu_link=gl)
         if self.gelu != "erf":  # GPT tanh approximation
             m = 0.5 * m * (1 + torch.tanh(math.sqrt(2 / math.pi) * (m + 0.044715 * m * m * m)))
         m = ops.linear(m, self.fc2_w, self.fc2_b, gelu_src=gl)
-        return ops.layer_norm(dropout_add(m, n, self.hidden_drop, self.training, grad_add=h2), self.ln2_g,
-                              self.ln2_b, self.ln_eps)
+        out = ops.layer_norm(dropout_add(m, n, self.hidden_drop, self.training,
+                                         grad_add=h2 if h2 is not None else ln_n),
+                             self.ln2_g, self.ln2_b, self.ln_eps, grad_in=ln_out)
+        if ln_out is not None:
+            out._zoo_grad_in = ln_out   # the next block's residual parks its x-gradient here
+        return out
 
 
 class TransformerLayer(Layer):
