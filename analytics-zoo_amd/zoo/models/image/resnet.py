@@ -45,11 +45,12 @@ class ConvBN(nn.Module):
                                producer_in=producer_in, producer_out=producer_out, dx_handoff=dx_handoff,
                                resid_bn=resid_bn)
 
-    def forward_stats(self, x, grad_add=None):
+    def forward_stats(self, x, grad_add=None, dx_handoff=None):
         """Training-mode projection shortcut: raw conv output + its BN (ShortcutBN), to be
         applied inside the consuming unit's BN pass. Returns (raw, resid_bn argument)."""
         y, holder = conv_stats(x, self.weight, self.running_mean, self.running_var, kernel=(self.k, self.k),
-                               stride=(self.stride, self.stride), pad=(self.pad, self.pad), grad_add=grad_add)
+                               stride=(self.stride, self.stride), pad=(self.pad, self.pad), grad_add=grad_add,
+                               dx_handoff=dx_handoff)
         return y, (holder, self.gamma, self.beta)
 
 
@@ -61,6 +62,9 @@ FUSE_SHORTCUT_BN = os.environ.get("ZOO_FUSE_SHORTCUT_BN", "1") != "0"
 FUSE_STEM_POOL = os.environ.get("ZOO_FUSE_STEM_POOL", "1") != "0"
 # 7x7/2 stem computed as a 4x4/1 conv on a space-to-depth(2) input (GPU)
 S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
+# projection blocks: the shortcut's dgrad runs first and hands its dx to conv1's dgrad, which then
+# also fuses the previous block's BN-backward reduction (stage transitions)
+SHORTCUT_FIRST = os.environ.get("ZOO_SHORTCUT_FIRST", "1") != "0"
 
 
 def _bp():
@@ -97,15 +101,27 @@ class Bottleneck(nn.Module):
             h = self.conv1(x, grad_add=ho, producer_in=prod, producer_out=p1)
             h = self.conv2(h, producer_in=p1, producer_out=p2)
             return self.conv3(h, resid=x, resid_handoff=ho, producer_in=p2, producer_out=p3), p3
-        # x feeds both `down` and conv1: conv1 (created later, so its backward runs first) hands its dx
-        # to down's dgrad epilogue, which adds it -- no separate gradient-add pass over x
         dh = GradHandoff()
-        if FUSE_SHORTCUT_BN and self.down.eps == self.conv3.eps and self.down.momentum == self.conv3.momentum:
-            # the shortcut's BatchNorm is applied inside conv3's BN pass (no shortcut apply pass)
-            sc, rbn = self.down.forward_stats(x, grad_add=dh)
+        fuse_sc = FUSE_SHORTCUT_BN and self.down.eps == self.conv3.eps and self.down.momentum == self.conv3.momentum
+        if SHORTCUT_FIRST and self.conv1.stride == 1 and self.conv1.k == 1:
+            # x feeds both `down` and conv1. `down` is created after conv1, so its backward runs first
+            # and hands its (possibly strided, zero-filled) dx to conv1, whose stride-1 dgrad covers
+            # every position: its epilogue adds it AND fuses the previous block's BN-backward
+            # reduction (producer_in) -- no separate reduction pass over x at stage transitions
+            h = self.conv1(x, grad_add=dh, producer_in=prod, producer_out=p1)
+            if fuse_sc:
+                sc, rbn = self.down.forward_stats(x, dx_handoff=dh)
+            else:
+                sc, rbn = self.down(x, dx_handoff=dh), None
         else:
-            sc, rbn = self.down(x, grad_add=dh), None
-        h = self.conv1(x, producer_out=p1, dx_handoff=dh)
+            # conv1 (created later, so its backward runs first) hands its dx to down's dgrad
+            # epilogue, which adds it -- no separate gradient-add pass over x
+            if fuse_sc:
+                # the shortcut's BatchNorm is applied inside conv3's BN pass (no shortcut apply pass)
+                sc, rbn = self.down.forward_stats(x, grad_add=dh)
+            else:
+                sc, rbn = self.down(x, grad_add=dh), None
+            h = self.conv1(x, producer_out=p1, dx_handoff=dh)
         h = self.conv2(h, producer_in=p1, producer_out=p2)
         return self.conv3(h, resid=sc, producer_in=p2, producer_out=p3, resid_bn=rbn), p3
 

@@ -287,7 +287,7 @@ class _ConvStatsFn(torch.autograd.Function):
     the block's first conv, GradHandoff) + wgrad of the raw-output gradient."""
 
     @staticmethod
-    def forward(ctx, x, w, R, S, stride, pad, holder, handoff_in):
+    def forward(ctx, x, w, R, S, stride, pad, holder, handoff_in, dx_out=None):
         K = w.shape[0]
         stats = workspace.zeros(stat_len(K), x.device)
         y = _kern.conv_fwd(x, bf16_weight(w), R, S, stride, pad, stats=stats)
@@ -299,6 +299,7 @@ class _ConvStatsFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.meta = (R, S, stride, pad, x.shape)
         ctx.handoff_in = handoff_in
+        ctx.dx_out = dx_out
         return y
 
     @staticmethod
@@ -320,19 +321,25 @@ class _ConvStatsFn(torch.autograd.Function):
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
             dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, xshape[3], xshape[1], xshape[2], stride, pad,
                                   resid=add, resid_inplace=add is not None)
+            if ctx.dx_out is not None:
+                # the other consumer of x (the block's conv1) adds it in its dgrad epilogue
+                ctx.dx_out.grad = dx
+                dx = None
         gw, own_w = _grad_target(w)
         C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
         if own_w:
             _notify(w)
-        return dx, None if own_w else gw.to(w.dtype), None, None, None, None, None, None
+        return dx, None if own_w else gw.to(w.dtype), None, None, None, None, None, None, None
 
 
-def conv_stats(x, w, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0), grad_add=None):
+def conv_stats(x, w, running_mean, running_var, kernel=(1, 1), stride=(1, 1), pad=(0, 0), grad_add=None,
+               dx_handoff=None):
     """Training-mode projection shortcut (GPU): (raw conv output, ShortcutBN) -- the BN is
-    applied by the consumer unit (``conv_bn_act(..., resid=raw, resid_bn=holder, ...)``)."""
+    applied by the consumer unit (``conv_bn_act(..., resid=raw, resid_bn=holder, ...)``).
+    ``grad_add`` / ``dx_handoff``: see :func:`conv_bn_act`."""
     holder = ShortcutBN(running_mean, running_var)
     xb = (x if x.dtype == torch.bfloat16 else x.to(torch.bfloat16)).contiguous()
-    y = _ConvStatsFn.apply(xb, w, kernel[0], kernel[1], tuple(stride), tuple(pad), holder, grad_add)
+    y = _ConvStatsFn.apply(xb, w, kernel[0], kernel[1], tuple(stride), tuple(pad), holder, grad_add, dx_handoff)
     return y, holder
 
 

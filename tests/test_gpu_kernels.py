@@ -344,6 +344,33 @@ def test_resnet_bn_mask_modes_match_z_reads(gpu, block):
     assert diff == 0.0, diff
 
 
+def test_resnet_shortcut_first_matches(gpu):
+    """Projection blocks with the shortcut's dgrad first (its dx handed to conv1's dgrad, which
+    then also fuses the previous block's BN-backward reduction) vs the conv1-first order: the
+    same gradients up to bf16 rounding of the handed-off partial sum (deterministic reductions)."""
+    import zoo.models.image.resnet as R
+    from zoo.ops import softmax_cross_entropy, deterministic, set_deterministic
+    torch.manual_seed(0)
+    m = R.ResNet(R.Bottleneck, [2, 2, 2, 1], num_classes=16, width=16).to(gpu)
+    x = torch.randn(8, 3, 96, 96, device=gpu)
+    y = torch.randint(0, 16, (8,), device=gpu)
+    grads = []
+    prev = deterministic()
+    try:
+        set_deterministic(True)
+        for sf in (False, True):
+            R.SHORTCUT_FIRST = sf
+            m.zero_grad(set_to_none=True)
+            softmax_cross_entropy(m(x), y).backward()
+            grads.append(torch.cat([p.grad.detach().float().flatten() for p in m.parameters()]).double())
+    finally:
+        R.SHORTCUT_FIRST = True
+        set_deterministic(prev)
+    rel = ((grads[0] - grads[1]).norm() / grads[0].norm()).item()
+    assert rel < 2e-2, rel
+    assert F.cosine_similarity(grads[0], grads[1], dim=0).item() > 0.999
+
+
 def test_resnet_s2d_stem_matches_7x7_stem(gpu):
     """The space-to-depth stem (4x4/1 conv on the s2d image) must equal the 7x7/2
     conv+BN+ReLU stem: output, input-free weight gradient and BN parameter grads."""
