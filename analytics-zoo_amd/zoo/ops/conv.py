@@ -381,7 +381,9 @@ class _LinearNativeFn(torch.autograd.Function):
         if ctx.needs_input_grad[0] and src is not None and src.pre is not None:
             # dgrad epilogue: d pre = (dy W^T (+ resid)) * GELU'(pre), column sums -> b1's gradient
             wt = _kern.flip_weights(bf16_weight(w), N, 1, 1, K)
-            sums = torch.zeros(2 * K, dtype=torch.float32, device=dy.device)
+            # per-step arena (zeroed once per engine step) instead of a fill launch per layer
+            from zoo.ops import workspace
+            sums = workspace.zeros(2 * K, dy.device)
             dx = _kern.conv_fwd(dy.view(-1, 1, 1, N), wt, 1, 1,
                                 resid=None if resid is None else resid.view(-1, 1, 1, K),
                                 bstats=(src.pre.view(-1, 1, 1, K), None, None, None, sums)).view(-1, K)
