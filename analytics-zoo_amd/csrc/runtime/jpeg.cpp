@@ -63,6 +63,9 @@ static bool build_huff(Huff& t, const uint8_t* counts, const uint8_t* vals, int 
   for (int len = 1; len <= 16; ++len) {
     t.valptr[len] = k;
     t.mincode[len] = code;
+    // reject an over-subscribed code space BEFORE any lookup entry of this length is written:
+    // (code << shift) | f must stay inside the 1024-entry table, and every symbol must exist
+    if (code + counts[len - 1] > (1 << len) || k + counts[len - 1] > nvals) return false;
     for (int i = 0; i < counts[len - 1]; ++i) {
       if (len <= 10) {
         const int shift = 10 - len;
@@ -281,6 +284,9 @@ struct Decoder {
       const int sl = len - 2;
       switch (m) {
         case 0xC0: case 0xC1: {
+          // one frame per image: a second SOF (after a scan) would change the block grid the
+          // destination planes were sized for -- reject it before any scan writes
+          if (frame) return E_MARKER;
           if (sl < 6 || seg[0] != 8) return E_UNSUPPORTED;
           info.h = (seg[1] << 8) | seg[2];
           info.w = (seg[3] << 8) | seg[4];
@@ -351,6 +357,7 @@ struct Decoder {
         case 0xDA: {   // SOS + entropy-coded data
           if (!frame) return E_MARKER;
           if (header_only) return OK;
+          if (sl < 1) return E_TRUNC;
           const int ns = seg[0];
           if (ns < 1 || ns > info.ncomp || sl < 1 + 2 * ns + 3) return E_UNSUPPORTED;
           int comps[3], td[3], ta[3];

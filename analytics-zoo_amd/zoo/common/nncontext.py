@@ -30,12 +30,17 @@ log = logging.getLogger("zoo")
 class ZooConfig:
     # engine
     dtype: str = "bf16"
-    # gradient bucket size: the last bucket (the earliest layers) is launched only
-    # when backward ends and is exposed; 16 MB keeps that tail short while each
-    # message is still large enough for full xGMI ring bandwidth
-    bucket_mb: float = 16.0
+    # gradient bucket size (MB of fp32 gradient): xGMI is 7 point-to-point links per GPU, and a
+    # collective only reaches per-link bandwidth with multi-MB per-peer messages -- 32 MB (16 MB
+    # on a bf16 wire, 2 MB per peer at N=8) amortises RCCL's per-call latency while the last
+    # bucket (the earliest layers, exposed after backward) stays a short tail. Engines size
+    # buckets per model (bench.py: NCF = one bucket)
+    bucket_mb: float = 32.0
     overlap_comm: bool = True
-    grad_compression: str = ""          # ZOO_GRAD_COMPRESSION=bf16: 16-bit gradient transfer
+    # 16-bit gradient transfer, BigDL's default (docs/docs/wp-bigdl.md:140-160: gradients always
+    # travel as 16-bit chunks): "auto" = bf16 wire with fp32 accumulation whenever GPU
+    # collectives run (world > 1, or force_comm), fp32 on CPU/gloo; "" / "none" = fp32 wire
+    grad_compression: str = "auto"      # ZOO_GRAD_COMPRESSION
     sharded_optimizer: bool = False
     hip_graph: bool = False
     # failure handling (bigdl.failure.retryTimes / retryTimeInterval, Topology.scala:1181-1182)

@@ -43,6 +43,7 @@ def bf16_weight(w):
     (in-place updates bump ``_version``), so inference pays no per-call cast."""
     c = getattr(w, "_zoo_bf16", None)
     if c is not None:
+        w._zoo_bf16_read = True   # ZeRO-1 may gather this parameter as bf16 (parallel/ddp.py)
         return c
     if w.dtype == torch.bfloat16:
         return w.detach()

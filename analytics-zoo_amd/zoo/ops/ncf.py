@@ -37,6 +37,9 @@ def _table_src(tables):
     """bf16 engine copies of the four tables when every one has one, else the fp32 tables."""
     copies = [getattr(t, "_zoo_bf16", None) if t is not None else None for t in tables]
     if all(c is not None and c.dtype == torch.bfloat16 for c, t in zip(copies, tables) if t is not None):
+        for t in tables:
+            if t is not None:
+                t._zoo_bf16_read = True
         return [c if t is not None else None for c, t in zip(copies, tables)]
     return [t.detach() if t is not None else None for t in tables]
 

@@ -101,6 +101,8 @@ class _DropoutAddFn(torch.autograd.Function):
         seed = _drop_rng().getrandbits(62)   # host RNG: no device sync, no tensor op
         ctx.p, ctx.seed = p, seed
         ctx.handoff = handoff if (handoff is not None and handoff.armed) else None
+        if ctx.handoff is not None:
+            handoff.armed = False   # one parking consumer per arming; any other consumer returns its grad
         return native().dropout_add(a, x, p, seed)
 
     @staticmethod
@@ -108,7 +110,8 @@ class _DropoutAddFn(torch.autograd.Function):
         g = g.contiguous()
         da = native().dropout_add(g, None, ctx.p, ctx.seed)
         if ctx.handoff is not None:
-            ctx.handoff.grad = g      # added by the armed linear's dgrad GEMM
+            h = ctx.handoff           # added by the armed consumer's backward (dgrad GEMM / LayerNorm)
+            h.grad = g if h.grad is None else h.grad + g
             return da, None, None, None
         return da, g, None, None
 
@@ -147,6 +150,8 @@ class _EmbeddingFn(torch.autograd.Function):
             src = getattr(table, "_zoo_bf16", None)
             if src is None or src.dtype != compute_dtype:
                 src = table.detach().to(compute_dtype)
+            else:
+                table._zoo_bf16_read = True
         out = native().embedding_fwd(src.contiguous(), idx, pad)
         ctx.save_for_backward(idx)
         ctx.table = table

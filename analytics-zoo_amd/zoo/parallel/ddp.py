@@ -5,9 +5,11 @@ This replaces BigDL's Spark-BlockManager ``AllReduceParameter`` (SURVEY.md
 docs/docs/wp-bigdl.md:140-160):
 
 * Gradients live in ONE flat fp32 buffer (:class:`FlatParams`) laid out in
-  backward order and cut into contiguous buckets (``bucket_mb``, 16 MB by
+  backward order and cut into contiguous buckets (``bucket_mb``, 32 MB by
   default: big enough for full per-link bandwidth on xGMI, small enough that
   the last bucket -- launched when backward ends -- is a short exposed tail).
+* The wire format defaults to bf16 on the GPU (``compress="auto"``; BigDL ships
+  16-bit gradient chunks, wp-bigdl.md:140-160), fp32 on gloo/CPU.
 * A bucket is launched on a dedicated comm stream (waiting on an event of the
   compute stream) as soon as EVERY gradient contribution of its parameters has
   been enqueued. The number of contributions per parameter is learned in the
@@ -48,11 +50,14 @@ last contribution); later steps launch early in that order, and ``finish()`` lau
 is left -- including all buckets of a zombie rank that failed part-way through backward -- in
 that same recorded order, so a zombie's collective sequence matches the healthy ranks'.
 
-Row-sparse sync is host-sync free and capturable: each rank scatters a per-row "touched"
-mask (uint8, V bytes), the masks are summed (one all-reduce), the union rows are compacted on
-the device into a fixed-capacity index buffer (capacity min(V, world * ids-per-step), agreed
-in the calibration step) and ONE fixed-size all-reduce moves just those rows. A rank without
-lookups contributes a zero mask, so every rank always issues the same collectives.
+Row-sparse sync: each rank scatters a per-row "touched" mask (uint8, V bytes; int32 at >= 256
+ranks), the masks are summed (one all-reduce), the union rows are compacted on the device into a
+fixed-capacity index buffer (capacity min(V, world * ids-per-step), agreed in the calibration
+step) and ONE fixed-size all-reduce moves just those rows. A rank without lookups contributes a
+zero mask, so every rank always issues the same collectives. A rank that looks up more ids than
+agreed raises a flag carried in the same mask all-reduce; every rank reads the summed flag and
+falls back to the dense all-reduce together for that step. Tables whose capacity reaches V/2 are
+always reduced densely (the mask + rows would move more than the dense table).
 
 ZeRO-1 weight all-gather: the updated shards go out as bf16 (half of BigDL's fp32 bytes are
 not needed for the bf16 compute copy); the 1-D parameters that layers read in fp32 (BatchNorm
@@ -139,13 +144,15 @@ class GradSync:
         tensor parallelism it holds the ranks that share a tensor-parallel rank,
         so TP-sharded weights are only averaged over true replicas."""
         self.flat = flat
-        self.compress = compress if compress in ("bf16",) else None
         self.group = group
         initialized = dist.is_available() and dist.is_initialized()
         self.world = dist.get_world_size(group) if initialized else 1
         self.rank = dist.get_rank(group) if initialized else 0
         self.comm = initialized and (self.world > 1 or force_comm)
         self.backend = dist.get_backend(group) if initialized else None
+        if compress == "auto":   # BigDL's 16-bit gradient chunks on the GPU path, exact fp32 on gloo/CPU
+            compress = "bf16" if (self.comm and flat.grad.is_cuda) else None
+        self.compress = compress if compress in ("bf16",) else None
         self.mode = mode if self.comm else "allreduce"
         self.is_cuda = flat.grad.is_cuda
         self.overlap = bool(overlap) and self.comm and self.is_cuda
@@ -246,10 +253,13 @@ class GradSync:
                 b.gath = gath[off:off + n]
                 b.gath16 = gath16[off:off + n]
                 off += n
-            # 1-D parameters (BN gamma/beta, biases: read in fp32 by the layers) travel exactly
+            # parameters the layers read in fp32 travel exactly: every parameter that no native
+            # kernel read through its bf16 compute copy (``_zoo_bf16_read``, set by the conv / linear
+            # / embedding / NCF ops in the calibration forward) -- BN gamma/beta, biases, fp32
+            # embedding tables (compute_dtype=None), fp32 torch layers of the Keras/AutoML fallbacks
             idx = []
             for p, (lo, hi) in zip(self.flat.params, self.flat.ranges()):
-                if p.dim() <= 1:
+                if p.dim() <= 1 or not getattr(p, "_zoo_bf16_read", False):
                     idx.append(torch.arange(lo, hi, dtype=torch.long))
             if idx and self.flat.bf16 is not None:
                 self._small_idx = torch.cat(idx).to(dev)
@@ -406,8 +416,11 @@ class GradSync:
         return touched
 
     def _sparse_capacity(self, p, n_local):
-        """Rows the fixed-size union buffer holds: min(V, world * ids-per-step), agreed once
-        (calibration) with a MAX all-reduce of the per-rank id counts."""
+        """(rows the fixed-size union buffer holds, agreed ids-per-rank), agreed once (calibration)
+        with a MAX all-reduce of the per-rank id counts: capacity min(V, world * ids-per-step).
+        Capacity ``None`` = the union can cover half the table or more: the row-sparse protocol
+        (a V-sized mask all-reduce plus the rows) would move MORE than the dense all-reduce, so
+        the table is reduced densely (e.g. NCF ml-20m at b65536 x 8 ranks: capacity >= V)."""
         key = id(p)
         cap = self._sparse_cap.get(key)
         if cap is None:
@@ -415,12 +428,10 @@ class GradSync:
             t = torch.tensor([n_local], dtype=torch.long, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
             n_max = int(t.item())
-            cap = (min(p.shape[0], max(n_max, 1) * self.world), n_max)
+            rows = min(p.shape[0], max(n_max, 1) * self.world)
+            cap = (rows if 2 * rows < p.shape[0] else None, n_max)
             self._sparse_cap[key] = cap
-        elif n_local > cap[1]:
-            raise RuntimeError("row-sparse table %s: %d lookups this step > the %d agreed in the calibration "
-                               "step (the union buffer could overflow)" % (tuple(p.shape), n_local, cap[1]))
-        return cap[0]
+        return cap
 
     def _row_sparse_allreduce(self, p, lo, hi):
         """Sum table p's gradient over the ranks through the union of looked-up rows: a summed
@@ -432,13 +443,27 @@ class GradSync:
         dev = g.device
         touched = self._touched_ids(p)
         n_local = int(sum(t.numel() for t in touched))
-        cap = self._sparse_capacity(p, n_local)
-        mask = torch.zeros(V, dtype=torch.uint8 if self.backend != "gloo" else torch.int32, device=dev)
+        cap, n_max = self._sparse_capacity(p, n_local)
+        if cap is None:                       # dense wins (decided identically on every rank)
+            dist.all_reduce(g, group=self.group)
+            return False
+        # uint8 sums wrap at 256 ranks; gloo has no uint8 sum
+        mdt = torch.uint8 if (self.backend != "gloo" and self.world < 256) else torch.int32
+        mask = torch.zeros(V + 1, dtype=mdt, device=dev)
         if touched:
             ids = torch.cat([t.to(dev).long() for t in touched])
             ids = ids[(ids >= 0) & (ids < V)] if not ids.is_cuda else ids.clamp(0, V - 1)
-            mask.index_fill_(0, ids, 1)
+            mask[:V].index_fill_(0, ids, 1)
+        # slot V: this rank looked up more ids than agreed (variable-length ids, a larger batch than
+        # the calibration batch) -> the union could overflow the capacity. The flag travels in the
+        # mask all-reduce, so every rank sees the same sum and takes the same branch below.
+        if n_local > n_max:
+            mask[V] = 1
         dist.all_reduce(mask, group=self.group)
+        if bool(mask[V].item()):   # one small host read per step: the price of a collective decision
+            dist.all_reduce(g, group=self.group)  # every rank: dense fallback for this step
+            return False
+        mask = mask[:V]
         on = mask > 0
         pos = torch.cumsum(on.to(torch.int32), 0) - 1
         slot = torch.where(on, pos.long(), torch.full_like(pos, cap, dtype=torch.long))

@@ -5,9 +5,16 @@ the NCF records/sec metric (BASELINE.json).
 
   python bench.py --gpus N --steps K --warmup W [--batch 256] [--model resnet50|ncf]
 
-For N > 1 launch one rank per GPU:
+For N > 1 one rank runs per GPU. Either launch the ranks yourself:
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
       --master-port P bench.py --gpus N --steps K --warmup W
+or run ``python bench.py --gpus N`` directly: without WORLD_SIZE in the environment the
+process does not touch the GPU, starts ``torch.distributed.run`` with N ranks as a child
+process (never exec) and exits with its return code. A launched job whose world size is
+not ``--gpus`` exits non-zero instead of reporting a mislabeled number.
+
+Multi-GPU defaults are BigDL's: 16-bit (bf16) gradient wire with fp32 accumulation
+(``ZOO_GRAD_COMPRESSION=auto``), 32 MB buckets for ResNet-50, one bucket for NCF.
 
 Each step = synthetic batch -> NCHW->NHWC bf16 conversion -> forward ->
 softmax cross-entropy -> backward -> RCCL gradient all-reduce (bucketed,
@@ -19,14 +26,13 @@ barrier + device sync; the max elapsed time over ranks is reported.
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "analytics-zoo_amd"))
-
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
 
 BASELINE_METRIC = "images/sec (whole node) ResNet-50 bf16"
 BASELINE_VALUE = None  # BASELINE.json "published" is empty -> vs_baseline null
@@ -38,16 +44,26 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=256, help="per-GPU batch")
-    ap.add_argument("--model", default="resnet50", choices=["resnet50", "ncf"])
+    ap.add_argument("--model", default="resnet50", choices=["resnet50", "ncf", "mlp"],
+                    help="mlp: a small CPU-capable dry-run model for launcher/DP tests (not a benchmark)")
     ap.add_argument("--sharded", action="store_true", help="ZeRO-1 sharded optimizer (BigDL AllReduceParameter)")
     ap.add_argument("--force-comm", action="store_true",
                     help="run the bucketed RCCL path even at world size 1 (implied by --sharded)")
-    ap.add_argument("--grad-compression", default="", choices=["", "bf16"])
+    ap.add_argument("--grad-compression", default="auto", choices=["auto", "", "none", "bf16"],
+                    help="gradient wire: auto = bf16 whenever GPU collectives run (BigDL 16-bit transfer)")
+    ap.add_argument("--bucket-mb", type=float, default=0.0, help="0: per-model default (ResNet 32, NCF one bucket)")
     ap.add_argument("--profile-steps", type=int, default=0)
     return ap.parse_args()
 
 
+def _sync(dev):
+    import torch
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+
+
 def build_resnet50(ctx, batch):
+    import torch
     from zoo.models.image.resnet import resnet50
     from zoo.ops import softmax_cross_entropy
     from zoo.pipeline.api.keras.optimizers import SGD, EpochDecayWithWarmUp
@@ -62,7 +78,7 @@ def build_resnet50(ctx, batch):
     warm = 10
     optim = SGD(learningrate=0.01, momentum=0.9, weightdecay=1e-4, dampening=0.0, nesterov=True,
                 learningrate_schedule=EpochDecayWithWarmUp(warm, (0.1 - 0.01) / warm, lambda epoch: 0))
-    eng = TrainingEngine(model, softmax_cross_entropy, optim)
+    eng = TrainingEngine(model, softmax_cross_entropy, optim, bucket_mb=a_bucket(32.0))
     dev = ctx.device
     g = torch.Generator(device=dev)
     g.manual_seed(ctx.rank)
@@ -72,6 +88,7 @@ def build_resnet50(ctx, batch):
 
 
 def build_ncf(ctx, batch):
+    import torch
     from zoo.models.recommendation.neuralcf import NeuralCF
     from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
     from zoo.pipeline.api.keras.optimizers import Adam
@@ -82,7 +99,9 @@ def build_ncf(ctx, batch):
     model = NeuralCF(users, items, 5, user_embed=20, item_embed=20, hidden_layers=(40, 20, 10), include_mf=True,
                      mf_embed=20)
     # NCF's step is ~130 small kernels: capture forward+backward as one hipGraph
-    eng = TrainingEngine(model, SparseCategoricalCrossEntropy(), Adam(lr=1e-3), hip_graph=True)
+    # the whole gradient (26 MB fp32) in ONE bucket: NCF's backward is ~0.1 ms, too short to overlap
+    eng = TrainingEngine(model, SparseCategoricalCrossEntropy(), Adam(lr=1e-3), hip_graph=True,
+                         bucket_mb=a_bucket(1024.0))
     dev = ctx.device
     g = torch.Generator(device=dev)
     g.manual_seed(ctx.rank)
@@ -93,12 +112,38 @@ def build_ncf(ctx, batch):
     return eng, (x, y), "NCF", {"users": users, "items": items, "embed": 20, "hidden": [40, 20, 10]}
 
 
+def build_mlp(ctx, batch):
+    """Dry-run model (CPU/gloo capable): exercises launcher, ranks, DP sync and the JSON line."""
+    import torch
+    import torch.nn as nn
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    torch.manual_seed(1234)
+    model = nn.Sequential(nn.Linear(64, 256), nn.Tanh(), nn.Linear(256, 256), nn.Tanh(), nn.Linear(256, 1))
+    eng = TrainingEngine(model, MeanSquaredError(), SGD(learningrate=0.01, momentum=0.9),
+                         bucket_mb=a_bucket(0.25))
+    g = torch.Generator(device=ctx.device)
+    g.manual_seed(ctx.rank)
+    x = torch.randn(batch, 64, device=ctx.device, generator=g)
+    y = torch.randn(batch, 1, device=ctx.device, generator=g)
+    return eng, (x, y), "MLP-dry-run", {"note": "launcher/DP dry-run model, not a benchmark"}
+
+
+_BUCKET = [0.0]
+
+
+def a_bucket(default):
+    return _BUCKET[0] if _BUCKET[0] > 0 else default
+
+
 def grad_sync_label(eng, a):
     """What the gradient synchronisation actually did: "none" when no collective runs."""
     if not eng.sync.comm:
         return "none"
     lab = "sharded(ZeRO-1,bf16-weight-gather)" if eng.sync.mode == "sharded" else "allreduce(bucketed,overlapped)"
-    return lab + ("+bf16-wire" if a.grad_compression else "")
+    return lab + ("+bf16-wire" if eng.sync.compress else "+fp32-wire") + \
+        ",%d-buckets" % len(eng.sync.buckets)
 
 
 def comm_diagnostics(eng, x, y, world):
@@ -106,13 +151,15 @@ def comm_diagnostics(eng, x, y, world):
     timing does not perturb them): RCCL world size, cross-rank max |difference| of a checksum
     of the fp32 master weights (0 = every rank holds the same model), exposed comm time per
     step (the compute stream's wait on the comm stream) and per-bucket bus bandwidth."""
+    import torch
+    import torch.distributed as dist
     sync = eng.sync
     if not sync.comm:
         return {"rccl_world": 1}
     sync.collect_stats = True
     for _ in range(3):
         eng.train_step(x, y)
-    torch.cuda.synchronize()
+    _sync(x.device)
     sync.collect_stats = False
     summ = sync.comm_summary()
     sync.sync_master()
@@ -134,39 +181,79 @@ def comm_diagnostics(eng, x, y, world):
                                  "max": max(bus) if bus else 0.0, "min": min(bus) if bus else 0.0}}
 
 
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def self_launch(a):
+    """--gpus N > 1 without a launcher: start N ranks with torch.distributed.run as a CHILD
+    process. This process has not touched the GPU (no torch.cuda call, no HIP context) and
+    never execs; it waits and returns the child's exit code."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # dmabuf IPC for RCCL between the ranks
+    print("bench.py: launching %d ranks: %s" % (a.gpus, " ".join(cmd)), file=sys.stderr, flush=True)
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = parse()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(a)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != a.gpus:
+        print("bench.py: --gpus %d but the job has WORLD_SIZE=%d ranks; refusing to report a "
+              "mislabeled number" % (a.gpus, world_env), file=sys.stderr, flush=True)
+        return 2
+    _BUCKET[0] = a.bucket_mb
+    import torch
+    import torch.distributed as dist
     from zoo.common.nncontext import init_nncontext
+    comp = "" if a.grad_compression == "none" else a.grad_compression
     ctx = init_nncontext("bench", sharded_optimizer=a.sharded, force_comm=a.force_comm or a.sharded,
-                         grad_compression=a.grad_compression)
+                         grad_compression=comp)
     world = ctx.world_size
+    if world != a.gpus:
+        print("bench.py: --gpus %d but the process group has %d ranks" % (a.gpus, world), file=sys.stderr)
+        return 2
+    dev = ctx.device
     if a.model == "resnet50":
         batch = a.batch
         eng, (x, y), model_name, extra = build_resnet50(ctx, batch)
         metric, unit = BASELINE_METRIC, "images/sec"
-    else:
+    elif a.model == "ncf":
         batch = a.batch if a.batch != 256 else 65536
         eng, (x, y), model_name, extra = build_ncf(ctx, batch)
         metric, unit = "records/sec (whole node) NCF", "records/sec"
+    else:
+        batch = a.batch
+        eng, (x, y), model_name, extra = build_mlp(ctx, batch)
+        metric, unit = "samples/sec (dry-run MLP, not a benchmark)", "samples/sec"
 
     first_loss = None
     for _ in range(a.warmup):
         l0 = eng.train_step(x, y)
         if first_loss is None:
             first_loss = l0
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t0 = time.perf_counter()
     for _ in range(a.steps):
         loss = eng.train_step(x, y)
-    torch.cuda.synchronize()
+    _sync(dev)
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=ctx.device)
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
@@ -179,7 +266,8 @@ def main():
             "metric": metric, "value": round(value, 2), "unit": unit, "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16", "data": "synthetic (random-init weights, random inputs/labels)",
+            "dtype": "bf16" if dev.type == "cuda" else "fp32",
+            "data": "synthetic (random-init weights, random inputs/labels)",
             "config": dict({"model": model_name, "global_batch": batch * world, "per_gpu_batch": batch,
                             "seq_len": None, "parallelism": "dp%d" % world,
                             "grad_sync": grad_sync_label(eng, a)},
@@ -192,7 +280,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -371,3 +371,46 @@ def test_bucket_order_follows_readiness_and_zombie_replays_it():
     assert order0 != sorted(order0)
     for s in range(1, 4):   # every later step (the zombie's step 2 included) launches in that order
         assert logs0[s] == order0 and logs1[s] == order0
+
+
+# ---------------------------------------------------------------------------
+# round 4: row-sparse capacity decisions are collective
+# ---------------------------------------------------------------------------
+def _ncf_var_worker(rank, world, port, q, sparse, users):
+    ctx = _init(rank, world, port)
+    from zoo.models.recommendation.neuralcf import NeuralCF
+    from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
+    from zoo.pipeline.api.keras.optimizers import Adam
+    from zoo.pipeline.engine import TrainingEngine
+    torch.manual_seed(0)
+    m = NeuralCF(users, 300, 5, user_embed=8, item_embed=8, hidden_layers=(16, 8), mf_embed=8,
+                 row_sparse_sync=sparse)
+    eng = TrainingEngine(m, SparseCategoricalCrossEntropy(), Adam(lr=0.01), ctx=ctx, bucket_mb=0.001)
+    r = np.random.RandomState(100 + rank)
+    for step in range(3):
+        # rank 1 looks up MORE ids than in the calibration step at step 2 (variable batch)
+        n = 32 if not (rank == 1 and step == 2) else 96
+        x = np.stack([r.randint(1, 60, n), r.randint(1, 40, n)], 1).astype(np.float32)
+        y = r.randint(0, 5, n).astype(np.int64)
+        eng.train_step(torch.from_numpy(x), torch.from_numpy(y))
+    q.put((rank, (eng.flat.master.detach().numpy().copy(), getattr(eng.sync, "sparse_rows", 0))))
+    ctx.stop()
+
+
+def test_row_sparse_overflow_falls_back_together():
+    """One rank exceeding the agreed lookup count must not raise or hang: the flag travels in the
+    mask all-reduce and every rank reduces densely for that step -> equals the dense run."""
+    dense = _run(_ncf_var_worker, False, 500)
+    sparse = _run(_ncf_var_worker, True, 500)
+    for rk in (0, 1):
+        assert np.allclose(dense[rk][0], sparse[rk][0], atol=1e-6)
+    assert np.allclose(sparse[0][0], sparse[1][0], atol=1e-7)
+
+
+def test_row_sparse_picks_dense_when_union_covers_half_the_table():
+    """Capacity = world * ids-per-step >= V/2: the mask + rows protocol would move more than the
+    dense table, so the table is all-reduced densely (no mask all-reduce, no sparse rows)."""
+    sparse = _run(_ncf_var_worker, True, 100)    # 2 ranks x 32 ids >= 101/2 for the user tables
+    dense = _run(_ncf_var_worker, False, 100)
+    for rk in (0, 1):
+        assert np.allclose(dense[rk][0], sparse[rk][0], atol=1e-6)

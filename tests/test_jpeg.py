@@ -56,6 +56,39 @@ def test_unsupported_streams_fall_back():
     assert jpeg.batch_coeffs([_enc(_img(32, 32))[:200]]) is None
 
 
+def test_malformed_huffman_table_is_rejected():
+    """an over-subscribed DHT (255 codes of length 1) must be rejected before the
+    10-bit lookup table is filled (it used to write ~256 KB past it)."""
+    good = _enc(_img(32, 32))
+    counts = bytes([255] + [0] * 15)
+    vals = bytes(range(255))
+    seg = b"\xff\xc4" + (2 + 17 + len(vals)).to_bytes(2, "big") + b"\x00" + counts + vals
+    bad = good[:2] + seg + good[2:]
+    for _ in range(3):
+        assert jpeg.batch_coeffs([bad]) is None
+    # a code space over-subscribed only at a later length (2 codes of len 1 + 1 of len 2)
+    counts = bytes([2, 1] + [0] * 14)
+    seg = b"\xff\xc4" + (2 + 17 + 3).to_bytes(2, "big") + b"\x10" + counts + b"\x00\x01\x02"
+    assert jpeg.batch_coeffs([good[:2] + seg + good[2:]]) is None
+    assert jpeg.batch_coeffs([good]) is not None
+
+
+def test_second_frame_header_after_a_scan_is_rejected():
+    """a second SOF after the first scan (larger geometry) must not re-size the block
+    grid of a caller-provided destination: the decode fails before any scan writes."""
+    good = _enc(_img(16, 16))
+    big = _enc(_img(512, 512))
+    i_sof = big.index(b"\xff\xc0")
+    sof_len = int.from_bytes(big[i_sof + 2:i_sof + 4], "big")
+    sof = big[i_sof:i_sof + 2 + sof_len]
+    i_sos = big.index(b"\xff\xda")
+    tail = big[i_sos:]                               # the big image's scan + EOI
+    evil = good[:-2] + sof + tail
+    d = jpeg.batch_coeffs([good], nthreads=1)
+    out = np.zeros((1,) + d["coef"].shape[1:], np.int16)
+    assert jpeg.batch_coeffs([evil], nthreads=1, out=out) is None
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("hw,kw", CASES)
 def test_gpu_decode_matches_reference(gpu, hw, kw):
