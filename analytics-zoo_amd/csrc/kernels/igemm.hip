@@ -802,9 +802,19 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
                                  const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                  hipStream_t st);
 
+extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs);
+extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
+                             const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st);
+
 extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
+  {
+    // memory-bound 1x1 shapes: the persistent streaming kernel (pw.hip)
+    const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats);
+    const int route = igemm_route_epi(epi, bsp && bsp->zgelu);
+    if (zoo_pw_eligible(g, route, bsp)) return zoo_pw(X, W, Y, resid, stats, g, epi, bsp, st);
+  }
   // whole-64-channel K-tiles: the large-tile second-generation kernel (igemm2.hip)
   if (zoo_igemm2_eligible(g, igemm_route_epi(igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats),
                                              bsp && bsp->zgelu)))

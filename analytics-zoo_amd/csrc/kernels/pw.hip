@@ -1,0 +1,379 @@
+// Streaming pointwise (1x1, stride-1) convolution / GEMM for the memory-bound shapes of a
+// ResNet training step (gfx950 / MI355X).
+//
+//   Y[m][n] = epilogue( sum_k A[m][k] * B[n][k] )      A: NHWC activations [M][K] (K = Cin),
+//                                                       B: weights [N][ldb] (row n = output channel)
+//
+// Why a third GEMM kernel: the 1x1 convs whose output width is 64 / 128 channels (and the
+// 64 / 128-deep ones with 256 / 512 outputs) do 26 GFLOP at b256 but move 0.1 - 0.6 GB, so they
+// are bound by HBM, and the BN-fused epilogues are half of those bytes. The tiled kernels
+// (igemm.hip / igemm2.hip) run one output tile per workgroup: every tile pays its operand
+// latency, then its epilogue latency (the producer y loads of the fused BN backward), then
+// atomics on the same 2K statistics addresses from every one of 6272 tiles -- a stage-1
+// conv3 data gradient with the BN-backward epilogue took 283-316 us against ~110 us of bytes
+// (profiles/r3/resnet50_b256_step_timeline_final_r3.md #353/#370).
+//
+// Structure (no LDS operand ring, no barrier in the main loop):
+//   * persistent: every WAVE walks its own sequence of 16 / 32-pixel tiles; the grid is one
+//     occupancy-full wave of workgroups. Output channels are split across workgroups in groups of
+//     NP = 64 / 128 (N / NP = NSPLIT groups): workgroup b owns group g and LDS holds only that
+//     group's NP x K weights (<= 64 KiB), loaded ONCE in MFMA fragment order (1 KiB per 16-row x
+//     32-deep fragment, lane-linear: conflict-free ds_read_b128) as the MFMA A operand. The
+//     NSPLIT workgroups that share a pixel range sit on one XCD (blocks b, b+8, ... share an XCD
+//     under round-robin dispatch) and walk it in step, so the activations come from HBM once and
+//     from that XCD's L2 the other NSPLIT - 1 times;
+//   * the activations are the MFMA B operand and a 16x16x32 B fragment is exactly one 16-byte
+//     global load per lane (pixel lane & 15, k-chunk lane >> 4): the tile goes straight from
+//     HBM into VGPRs, and the NEXT tile's loads are issued before this tile's MFMAs (a 16 KiB
+//     register double buffer per wave, 8 waves per CU: ~128 KiB in flight per CU);
+//   * D = W . A^T puts one pixel on each lane and 4 consecutive output channels in its 4
+//     accumulator registers; a wave-private LDS patch turns them into row-contiguous 16-byte
+//     pieces for the epilogue (full-line NHWC loads / stores). Its global operands (producer y, residual gradient,
+//     ReLU mask) are issued at the top of the tile, BEFORE the next tile's prefetch, so the
+//     in-order vmcnt never makes the epilogue wait for the prefetch;
+//   * BatchNorm statistics / BN-backward sums: per-lane registers for the whole kernel (a lane's
+//     8-channel chunk is fixed), one shuffle reduction + LDS add at exit, one global atomic per
+//     channel per WORKGROUP.
+//
+// Epilogues: EPI 1 = bf16 output + BN statistics of the stored values (the forward of every
+// conv->BN unit); EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
+// and the producer's fused BN-backward sums (sum dy, sum dy * xhat).
+// Reference parity: MKL-DNN 1x1 convolution primitives behind BigDL SpatialConvolution
+// (Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110), SURVEY.md §2.16 HK3 / HK5.
+#include <stdlib.h>
+
+#include "common.h"
+#include "geom.h"
+
+namespace zoo {
+
+struct PwArgs {
+  int M;          // rows (pixels)
+  int N;          // output channels (row stride of Y / y / resid)
+  int ldb;        // weight row stride (elements)
+  int nsplit;     // channel groups of NP (N = nsplit * NP)
+  int stat_mode;  // 0: atomics into stats[0..2N), >0: slotted (slot_ptr), kStatPartial: [grid][2N] rows
+};
+
+constexpr int PW_NW = 8;  // waves per workgroup (2 per SIMD)
+
+// NP = output channels per workgroup (64 / 128), TPM = pixels per wave tile (16 / 32), KT = K / 32
+template <int NP, int TPM, int KT, int EPI>
+__global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
+                                                           bf16_t* __restrict__ Y, const bf16_t* __restrict__ resid,
+                                                           float* __restrict__ stats, PwArgs p, BwdStats bs) {
+  constexpr int K = KT * 32;
+  constexpr int MJ = TPM / 16, NI = NP / 16;
+  constexpr int NT = PW_NW * 64;
+  // epilogue geometry: row-contiguous pieces of 8 channels; CPR lanes cover one NP-channel row
+  constexpr int CPR = NP / 8, RPP = 64 / CPR, HP = 16 / RPP, PITCH = NP + 4;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* wfr = smem;                                                // NI * KT fragments of 1 KiB
+  float* ssum = reinterpret_cast<float*>(smem + NP * K * 2);       // [2][NP] statistics
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const int N = p.N;
+  float* patch = ssum + 2 * NP + w * 16 * PITCH;                   // wave-private fp32 16 x NP patch
+
+  // ---- workgroup -> (channel group, pixel group); XCD-local channel groups ----
+  const int b = blockIdx.x, G = gridDim.x;
+  const int xcd = b & 7, li = b >> 3;
+  const int g = li % p.nsplit;
+  const int mg = (li / p.nsplit) * 8 + xcd;          // pixel group (set of 8 wave streams)
+  const int MG = G / p.nsplit;                       // pixel groups (launcher: G % (8 * nsplit) == 0)
+  const int n0 = g * NP;
+
+  // ---- this group's weights -> LDS fragment image ----
+  for (int idx = tid; idx < NP * KT * 4; idx += NT) {
+    const int n = idx / (KT * 4), kc = idx - n * (KT * 4);
+    const int kb = kc >> 2, q = kc & 3;
+    const uint4 v = *reinterpret_cast<const uint4*>(B + (size_t)(n0 + n) * p.ldb + kc * 8);
+    *reinterpret_cast<uint4*>(wfr + (((n >> 4) * KT + kb) * 64 + (n & 15) + 16 * q) * 16) = v;
+  }
+  for (int c = tid; c < 2 * NP; c += NT) ssum[c] = 0.f;
+  __syncthreads();
+
+  const bool bnsum = EPI == 2 && bs.sums != nullptr && !bs.zgelu;
+  const bool want = EPI == 1 ? stats != nullptr : bnsum;
+  const int ch = lane % CPR, lr = lane / CPR;
+  const int c0 = n0 + ch * 8;                        // the lane's fixed 8-channel chunk
+  // per-lane BN constants of that chunk (EPI 2)
+  float cmu[8], civ[8], csc[8], csh[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { cmu[e] = civ[e] = csc[e] = csh[e] = 0.f; }
+  if (EPI == 2 && bnsum) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      cmu[e] = bs.mean[c0 + e];
+      civ[e] = bs.inv[c0 + e];
+      if (bs.zmode == 1) {
+        csc[e] = bs.mgamma ? bs.mgamma[c0 + e] * civ[e] : civ[e];
+        csh[e] = (bs.mbeta ? bs.mbeta[c0 + e] : 0.f) - cmu[e] * csc[e];
+      }
+    }
+  }
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+
+  const int ntiles = (p.M + TPM - 1) / TPM;
+  const int gw = mg * PW_NW + w, GW = MG * PW_NW;
+
+  // A fragments of tile t: lane -> pixel row t*TPM + 16 j + fr, k-chunk kb*32 + 8 fq
+  auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT]) {
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      int row = t * TPM + 16 * j + fr;
+      row = row < p.M ? row : p.M - 1;  // rows past M compute garbage that is never stored
+      const bf16_t* src = A + (size_t)row * K + 8 * fq;
+#pragma unroll
+      for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
+    }
+  };
+  auto wsync = [&]() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  };
+
+  auto process = [&](int t, bf16x8 (&cur)[MJ][KT], bf16x8 (&nxt)[MJ][KT]) {
+    // (1) epilogue operands of THIS tile first (in-order vmcnt: they must not queue behind the prefetch)
+    uint4 ey[MJ][HP], er[MJ][HP];
+    unsigned em[MJ][HP];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+#pragma unroll
+        for (int h = 0; h < HP; ++h) {
+          int m = t * TPM + 16 * j + lr + RPP * h;
+          m = m < p.M ? m : p.M - 1;
+          const size_t off = (size_t)m * N + c0;
+          ey[j][h] = bnsum ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off)
+                           : make_uint4(0u, 0u, 0u, 0u);
+          er[j][h] = resid ? *reinterpret_cast<const uint4*>(resid + off) : make_uint4(0u, 0u, 0u, 0u);
+          em[j][h] = bs.zmode == 2 ? (unsigned)reinterpret_cast<const uint8_t*>(bs.z)[off >> 3] : 0u;
+        }
+    }
+    // (2) prefetch the next tile of this wave
+    const int tn = t + GW;
+    if (tn < ntiles) load_tile(tn, nxt);
+
+    // (3) MFMAs: D[channel][pixel] = W . A^T; weight fragments double-buffered one k-block ahead,
+    //     the scheduling fence per k-block keeps hipcc from hoisting every ds_read of the tile
+    f32x4 acc[MJ][NI];
+#pragma unroll
+    for (int j = 0; j < MJ; ++j)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    bf16x8 wf[2][NI];
+    auto wload = [&](int kb, bf16x8 (&dst)[NI]) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) dst[i] = *reinterpret_cast<const bf16x8*>(wfr + ((i * KT + kb) * 64 + lane) * 16);
+    };
+    wload(0, wf[0]);
+#pragma unroll
+    for (int kb = 0; kb < KT; ++kb) {
+      if (kb + 1 < KT) wload(kb + 1, wf[(kb + 1) & 1]);
+#pragma unroll
+      for (int j = 0; j < MJ; ++j)
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[j][i] = mfma16(wf[kb & 1][i], cur[j][kb], acc[j][i]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    // (4) epilogue, one 16-pixel slice at a time through the wave's patch
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+#pragma unroll
+      for (int i = 0; i < NI; ++i) *reinterpret_cast<f32x4*>(patch + fr * PITCH + 16 * i + 4 * fq) = acc[j][i];
+      wsync();
+#pragma unroll
+      for (int h = 0; h < HP; ++h) {
+        const int row = lr + RPP * h;
+        const int m = t * TPM + 16 * j + row;
+        const bool ok = m < p.M;
+        const float4 lo = *reinterpret_cast<const float4*>(patch + row * PITCH + ch * 8);
+        const float4 hi = *reinterpret_cast<const float4*>(patch + row * PITCH + ch * 8 + 4);
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        float yy[8];
+        if constexpr (EPI == 2) {
+          if (resid) {
+            float rv[8];
+            unpack8(er[j][h], rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rv[e];
+          }
+          unpack8(ey[j][h], yy);
+          if (bs.zmode == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = yy[e] * csc[e] + csh[e] > 0.f ? v[e] : 0.f;
+          } else if (bs.zmode == 2) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (em[j][h] >> e) & 1u ? v[e] : 0.f;
+          }
+        }
+        const uint4 pk = pack8(v);
+        if (ok) *reinterpret_cast<uint4*>(Y + (size_t)m * N + c0) = pk;
+        if (want && ok) {
+          float q[8];
+          unpack8(pk, q);
+          if constexpr (EPI == 1) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * q[e];
+            }
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * (yy[e] - cmu[e]) * civ[e];
+            }
+          }
+        }
+      }
+      wsync();
+    }
+  };
+
+  bf16x8 fa[MJ][KT], fb[MJ][KT];
+  int t = gw;
+  if (t < ntiles) load_tile(t, fa);
+  for (; t < ntiles; t += 2 * GW) {
+    process(t, fa, fb);
+    if (t + GW < ntiles) process(t + GW, fb, fa);
+  }
+
+  if (!want) return;
+  // lanes sharing a channel chunk differ in the bits >= log2(CPR)
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+#pragma unroll
+    for (int o = CPR; o < 64; o <<= 1) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+    if (lane < CPR) {
+      atomicAdd(ssum + ch * 8 + e, s1[e]);
+      atomicAdd(ssum + NP + ch * 8 + e, s2[e]);
+    }
+  }
+  __syncthreads();
+  float* dst = EPI == 1 ? stats : bs.sums;
+  if (p.stat_mode > 0) dst = slot_ptr(dst, 2 * N, p.stat_mode);
+  for (int c = tid; c < NP; c += NT) {
+    atomicAdd(dst + n0 + c, ssum[c]);
+    atomicAdd(dst + N + n0 + c, ssum[NP + c]);
+  }
+}
+
+static int g_pw_mode = -1;  // -1 unset (ZOO_PW), 0 off, 1 on
+
+static int pw_mode() {
+  if (g_pw_mode < 0) {
+    const char* e = getenv("ZOO_PW");
+    g_pw_mode = e ? atoi(e) : 1;
+  }
+  return g_pw_mode;
+}
+
+static int pw_ncu() {
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  return ncu;
+}
+
+// group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave
+static size_t pw_smem(int NP, int K) { return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4; }
+
+template <int NP, int TPM, int KT, int EPI>
+static hipError_t pw_launch(const ConvGeom& g, const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* resid,
+                            float* stats, const BwdStats& bs, hipStream_t st) {
+  auto kfn = &pw_kernel<NP, TPM, KT, EPI>;
+  const size_t smem = pw_smem(NP, KT * 32);
+  static int per_cu = 0;
+  if (per_cu == 0) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, reinterpret_cast<const void*>(kfn), PW_NW * 64, smem) !=
+            hipSuccess || nb < 1)
+      nb = 1;
+    per_cu = nb;
+  }
+  const int nsplit = g.K / NP;
+  // pixel groups: one occupancy-full wave of workgroups, a multiple of 8 (XCD-local channel
+  // groups), capped by the work (8 wave streams per group)
+  int mgroups = pw_ncu() * per_cu / nsplit;
+  mgroups = mgroups / 8 * 8;
+  if (mgroups < 8) mgroups = 8;
+  const int need = ((g.M + TPM - 1) / TPM + PW_NW - 1) / PW_NW;
+  const int need8 = (need + 7) / 8 * 8;
+  if (mgroups > need8) mgroups = need8;
+  PwArgs a{g.M, g.K, g.ldb, nsplit, g.stat_slots};
+  hipLaunchKernelGGL(kfn, dim3(mgroups * nsplit), dim3(PW_NW * 64), smem, st, X, W, Y, resid, stats, a, bs);
+  return hipGetLastError();
+}
+
+// (NP, K) -> TPM: 32 while the double-buffered activation fragments plus the accumulators stay
+// within ~96 VGPRs, else 16 (no scratch spills at 2 waves / SIMD)
+template <int EPI>
+static hipError_t pw_dispatch(const ConvGeom& g, int NP, const bf16_t* X, const bf16_t* W, bf16_t* Y,
+                              const bf16_t* resid, float* stats, const BwdStats& bs, hipStream_t st) {
+  const int K = g.Ktot;
+#define PW_CASE(np, k, TPM) \
+  if (NP == np && K == k) return pw_launch<np, TPM, k / 32, EPI>(g, X, W, Y, resid, stats, bs, st);
+  PW_CASE(64, 64, 32)
+  PW_CASE(64, 128, 32)
+  PW_CASE(64, 256, 16)
+  PW_CASE(64, 512, 16)
+  PW_CASE(128, 64, EPI == 2 ? 16 : 32)
+  PW_CASE(128, 128, 16)
+  PW_CASE(128, 256, 16)
+#undef PW_CASE
+  return hipErrorNotSupported;
+}
+
+// channels per workgroup: 128 while its weights stay <= 64 KiB, else 64; 0 = not handled
+static int pw_np(int N, int K) {
+  if (K != 64 && K != 128 && K != 256 && K != 512) return 0;
+  if (N % 128 == 0 && K <= 256) return 128;
+  if (N % 64 == 0) return 64;
+  return 0;
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+extern "C" void zoo_pw_set(int mode) { g_pw_mode = mode; }
+
+// 1x1 / stride 1 / unpadded, whole rows (A row stride == Ktot), no output remap, forward with
+// BN statistics (EPI 1) or the backward epilogue (EPI 2, not the GELU form)
+extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs) {
+  if (pw_mode() <= 0) return 0;
+  if (route != 1 && route != 2) return 0;
+  // the backward epilogue handles the bit-mask (2) and recomputed (1) ReLU masks, or none
+  if (route == 2 && bs && bs->zmode == 0 && bs->z) return 0;
+  // deterministic / partial-buffer statistics: per-m-tile rows are the tiled kernels' contract
+  if (g->stat_slots == kStatPartial) return 0;
+  const bool is1x1 = g->R == 1 && g->S == 1 && g->sh == 1 && g->sw == 1 && g->ph == 0 && g->pw == 0 && g->lh == 1 &&
+                     g->lw == 1 && g->H == g->P && g->W == g->Q && g->omap == 0;
+  // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
+  // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
+  if (route == 1 && g->Ktot > 256) return 0;
+  return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
+}
+
+extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
+                             const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
+  BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const int NP = pw_np(g->K, g->Ktot);
+  if (epi == 1)
+    return pw_dispatch<1>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
+  return pw_dispatch<2>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr, bs,
+                        st);
+}

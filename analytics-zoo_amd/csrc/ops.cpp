@@ -32,6 +32,8 @@ hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, cons
                      const zoo::BwdStats*, hipStream_t);
 int zoo_igemm2_bm(const ConvGeom*, int);
 void zoo_igemm2_set(int, int);
+int zoo_pw_eligible(const ConvGeom*, int, const zoo::BwdStats*);
+void zoo_pw_set(int);
 hipError_t zoo_wlrn(const void*, const void*, void*, float*, float*, int, int, int, int, int, float, float, int,
                     hipStream_t);
 hipError_t zoo_resize_bilinear(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -359,6 +361,9 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     return e ? atoi(e) : 512;
   }();
   if (g.stat_slots == zoo::kStatSlots && tiles_m <= slot_min_tiles) g.stat_slots = 0;
+  // the persistent 1x1 kernel (pw.hip) adds each workgroup's sums once (~256 adders per address):
+  // straight into the final 2K floats, no slot fold
+  if (g.stat_slots > 0 && !stats_partial() && zoo_pw_eligible(&g, route, &bs)) g.stat_slots = 0;
   if (stat_dst && stats_partial()) {
     part = torch::empty({(int64_t)tiles_m, 2 * (int64_t)K}, x.options().dtype(at::kFloat));
     g.stat_slots = zoo::kStatPartial;
@@ -2592,6 +2597,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("upsample_nd", &upsample_nd);
   m.def("lstm_gates_fwd", &lstm_gates_fwd);
   m.def("lstm_gates_bwd", &lstm_gates_bwd);
+  m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
+        "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
         "igemm2 A/B switch: mode 0 off / 1 on (-1 keep), tile 0 auto / I2Tile id (-1 keep)");
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });
