@@ -99,24 +99,20 @@ class LSTMSeq2Seq(BaseModel):
 
     # ------------------------------------------------------------------ data
     def _get_decoder_inputs(self, x, y):
-        """Lagged target series for teacher forcing (decoder input one timestamp ahead of y)."""
-        decoder_input_data = np.zeros(y.shape, np.float32)
-        decoder_input_data[1:, ] = y[:-1, ]
-        decoder_input_data[0, 0] = x[-1, -1, :self.target_col_num]
-        decoder_input_data[0, 1:] = y[0, :-1]
-        return decoder_input_data
+        """Teacher-forcing decoder inputs: the target series shifted back by one sample (sample i
+        reads sample i-1's targets); sample 0 has no predecessor and reads its own targets one
+        step late, led by the last observed target of the final input window."""
+        tc = self.target_col_num
+        head = np.concatenate([x[-1:, -1:, :tc], y[:1, :-1]], axis=1)
+        return np.concatenate([head, y[:-1]], axis=0).astype(np.float32)
 
     def _get_len(self, x, y):
-        self.past_seq_len = x.shape[1]
-        self.feature_num = x.shape[2]
-        self.target_col_num = y.shape[2]
+        (_, self.past_seq_len, self.feature_num), self.target_col_num = x.shape, y.shape[2]
 
     @staticmethod
     def _expand_y(y):
         y = np.asarray(y, np.float32)
-        while y.ndim < 3:
-            y = np.expand_dims(y, axis=2)
-        return y
+        return y.reshape(y.shape + (1,) * max(0, 3 - y.ndim))
 
     def _pack(self, x, dec):
         n, f = len(x), max(self.feature_num, self.target_col_num)

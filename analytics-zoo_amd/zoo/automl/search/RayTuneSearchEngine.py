@@ -61,6 +61,35 @@ def _run_local_trial(args):
     return trial
 
 
+class _TrialTrainer:
+    """The per-trial train function (picklable, so spawned worker processes can run it):
+    fit the trial's feature transformer, then train the model up to ``max_iters`` epochs of
+    ``fit_eval``, reporting ``reward_metric`` (metric_op * mean metric) each epoch and keeping
+    the best epoch's (transformer, model, config) in ``best.ckpt`` of the trial directory."""
+    ckpt = "best.ckpt"
+    max_iters = 100
+
+    def __init__(self, input_df, feature_transformers, future_seq_len, validation_df, metric_op, mc):
+        self.input_df, self.ft = input_df, feature_transformers
+        self.future_seq_len, self.validation_df = future_seq_len, validation_df
+        self.metric_op, self.mc = metric_op, mc
+
+    def __call__(self, config, report):
+        ft = copy.deepcopy(self.ft)
+        model = TimeSequenceModel(check_optional_config=False, future_seq_len=self.future_seq_len)
+        config = dict(convert_bayes_configs(config))
+        x, y = ft.fit_transform(copy.deepcopy(self.input_df), **config)
+        val = None if self.validation_df is None else ft.transform(copy.deepcopy(self.validation_df))
+        best = None
+        for epoch in range(1, self.max_iters + 1):
+            metric = model.fit_eval(x, y, validation_data=val, mc=self.mc, **config)
+            reward = self.metric_op * float(np.mean(metric))
+            if best is None or reward > best:
+                best = reward
+                save_zip(self.ckpt, ft, model, config)
+            report(training_iteration=epoch, reward_metric=reward, checkpoint=self.ckpt)
+
+
 class RayTuneSearchEngine(SearchEngine):
     def __init__(self, logs_dir="", resources_per_trial=None, name="", remote_dir=None, n_parallel=1):
         super().__init__(n_parallel=n_parallel, logs_dir=logs_dir)
@@ -125,67 +154,64 @@ class RayTuneSearchEngine(SearchEngine):
         return [_run_local_trial(a) for a in args]
 
     def get_best_trials(self, k=1):
-        sorted_trials = RayTuneSearchEngine._get_sorted_trials(self.trials, metric="reward_metric")
-        return [self._make_trial_output(t) for t in sorted_trials[:k]]
+        ranked = self._get_sorted_trials(self.trials, metric="reward_metric")
+        return [self._make_trial_output(t) for t in ranked[:k]]
 
     def _make_trial_output(self, trial):
         return TrialOutput(config=trial.config, model_path=os.path.join(trial.logdir, trial.last_result["checkpoint"]))
 
+    # ---- trial ranking: higher reported metric is better (mse is reported negated) ----------
     @staticmethod
-    def _get_best_trial(trial_list, metric):
-        return max(trial_list, key=lambda trial: trial.last_result.get(metric, 0))
+    def _score(trial, metric):
+        return trial.last_result.get(metric, 0)
 
-    @staticmethod
-    def _get_sorted_trials(trial_list, metric):
-        return sorted(trial_list, key=lambda trial: trial.last_result.get(metric, 0), reverse=True)
+    @classmethod
+    def _get_sorted_trials(cls, trial_list, metric):
+        scored = [(cls._score(t, metric), n, t) for n, t in enumerate(trial_list)]
+        scored.sort(key=lambda e: (-e[0], e[1]))       # stable: ties keep submission order
+        return [t for _, _, t in scored]
 
-    @staticmethod
-    def _get_best_result(trial_list, metric):
-        return {metric: RayTuneSearchEngine._get_best_trial(trial_list, metric).last_result[metric]}
+    @classmethod
+    def _get_best_trial(cls, trial_list, metric):
+        ranked = cls._get_sorted_trials(trial_list, metric)
+        return ranked[0] if ranked else None
+
+    @classmethod
+    def _get_best_result(cls, trial_list, metric):
+        best = cls._get_best_trial(trial_list, metric)
+        return {metric: best.last_result[metric]}
 
     def test_run(self):
-        def mock_reporter(**kwargs):
-            assert "reward_metric" in kwargs, "Did not report proper metric"
-            assert "checkpoint" in kwargs, "Accidentally removed `checkpoint`?"
-            raise GoodError("This works.")
+        """Smoke-check the train function against a probe reporter: the first report must carry
+        the reward metric and the checkpoint name (what run() and get_best_trials() rely on).
+        Returns 1 when it does; raises otherwise."""
+        seen = {}
+
+        def probe(**report):
+            seen.update(report)
+            raise GoodError("train function reported")
+        probe_config = {"out_units": 1, "selected_features": ["MONTH(datetime)", "WEEKDAY(datetime)"]}
         try:
-            self.train_func({"out_units": 1, "selected_features": ["MONTH(datetime)", "WEEKDAY(datetime)"]},
-                            mock_reporter)
+            self.train_func(probe_config, probe)
         except GoodError:
+            missing = [k for k in ("reward_metric", "checkpoint") if k not in seen]
+            if missing:
+                raise AssertionError("train function report lacks %s" % ", ".join(missing))
             return 1
-        raise Exception("Didn't call reporter...")
+        raise RuntimeError("train function returned without reporting a result")
 
     @staticmethod
     def _is_validation_df_valid(validation_df):
-        df_not_empty = isinstance(validation_df, pd.DataFrame) and not validation_df.empty
-        df_list_not_empty = isinstance(validation_df, list) and validation_df and \
-            not all(d.empty for d in validation_df)
-        return validation_df is not None and bool(df_not_empty or df_list_not_empty)
+        """A usable validation set: a non-empty DataFrame, or a list holding at least one."""
+        frames = validation_df if isinstance(validation_df, list) else [validation_df]
+        return any(isinstance(f, pd.DataFrame) and not f.empty for f in frames)
 
     @staticmethod
     def _prepare_train_func(input_df, feature_transformers, future_seq_len, validation_df=None, metric_op=1,
                             mc=False, remote_dir=None):
-        is_val_df_valid = RayTuneSearchEngine._is_validation_df_valid(validation_df)
-
-        def train_func(config, tune_reporter):
-            trial_ft = copy.deepcopy(feature_transformers)
-            trial_model = TimeSequenceModel(check_optional_config=False, future_seq_len=future_seq_len)
-            trial_input_df = copy.deepcopy(input_df)
-            config = convert_bayes_configs(config).copy()
-            x_train, y_train = trial_ft.fit_transform(trial_input_df, **config)
-            validation_data = None
-            if is_val_df_valid:
-                validation_data = trial_ft.transform(copy.deepcopy(validation_df))
-            best_reward_m = -np.inf
-            for i in range(1, 101):
-                result = trial_model.fit_eval(x_train, y_train, validation_data=validation_data, mc=mc, **config)
-                reward_m = metric_op * float(np.mean(result))
-                ckpt_name = "best.ckpt"
-                if reward_m > best_reward_m:
-                    best_reward_m = reward_m
-                    save_zip(ckpt_name, trial_ft, trial_model, config)
-                tune_reporter(training_iteration=i, reward_metric=reward_m, checkpoint=ckpt_name)
-        return train_func
+        return _TrialTrainer(input_df, feature_transformers, future_seq_len,
+                             validation_df if RayTuneSearchEngine._is_validation_df_valid(validation_df) else None,
+                             metric_op, mc)
 
     def _prepare_tune_config(self, space):
         # GridSearch / RandomSample markers are expanded by the local engine as they are
