@@ -112,6 +112,8 @@ class MTNetNet(nn.Module):
             self.ar_fc = nn.Linear(self.ar * self.F, int(output_dim))
             _trunc_normal_(self.ar_fc.weight)
             nn.init.constant_(self.ar_fc.bias, 0.1)
+        from zoo.automl.model._nets import _to_native
+        _to_native(self)
 
     def forward(self, x):
         B = x.shape[0]

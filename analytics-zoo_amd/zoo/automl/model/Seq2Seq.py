@@ -31,6 +31,8 @@ class LSTMSeq2SeqNet(nn.Module):
         self.dec = nn.LSTM(self.T, int(latent_dim), batch_first=True)
         self.drop = nn.Dropout(float(dropout))
         self.dense = nn.Linear(int(latent_dim), self.T)
+        from zoo.automl.model._nets import _to_native
+        _to_native(self)
 
     def encode(self, x):
         _, (h, c) = self.enc(self.drop(x))

@@ -4,6 +4,13 @@ import torch
 import torch.nn as nn
 
 
+def _to_native(net):
+    """LSTM / Linear / Conv2d submodules -> the persistent recurrent kernel and the MFMA GEMMs
+    (zoo.pipeline.api.net.native_lower; parameters shared, CPU falls back to torch)."""
+    from zoo.pipeline.api.net.native_lower import lower_module
+    return lower_module(net)
+
+
 class VanillaLSTMNet(nn.Module):
     """LSTM(lstm_1_units) -> Dropout -> LSTM(lstm_2_units) -> Dropout -> Dense(future_seq_len)."""
 
@@ -15,6 +22,7 @@ class VanillaLSTMNet(nn.Module):
         self.l2 = nn.LSTM(int(lstm_1_units), int(lstm_2_units), batch_first=True)
         self.d2 = nn.Dropout(float(dropout_2))
         self.fc = nn.Linear(int(lstm_2_units), int(future_seq_len))
+        _to_native(self)
 
     def forward(self, x):
         h, _ = self.l1(x)

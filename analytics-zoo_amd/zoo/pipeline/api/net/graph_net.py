@@ -6,8 +6,10 @@ Reference: Zs/pipeline/api/net/NetUtils.scala:47-140 (GraphNet with
 Py/pipeline/api/net/graph_net.py. Each graph node becomes a Keras ``Layer``
 (so ``layers``, ``flattened_layers``, ``get_layer``, freeze/unfreeze and
 compile/fit/predict all work); the graph is evaluated in topological order.
-Imported models keep their source layout (NCHW) and run on PyTorch-ROCm
-ops (MIOpen / hipBLASLt) — the native NHWC kernels serve the zoo Keras layers.
+Imported models keep their source layout (NCHW) at the API; ``to_native()`` (done by the
+Net loaders on GPU, by InferenceModel and by Cluster Serving) swaps every supported node for a
+native twin running the zoo NHWC kernels (``native_lower.py``), with channels-last tensors
+flowing between native nodes.
 """
 import numpy as np
 import torch
@@ -77,6 +79,14 @@ class GraphNet(KerasNet):
 
     def node(self, name):
         return self.nodes[_key(name)]
+
+    def to_native(self, training=False):
+        """Run this imported graph on the native NHWC kernels (zoo.pipeline.api.net.native_lower):
+        every conv / linear / pooling / batch-norm / activation / LRN / LSTM node gets a native
+        twin sharing its parameters; in inference, conv -> BN -> activation chains fuse into one
+        kernel. In place; returns self."""
+        from zoo.pipeline.api.net.native_lower import lower_graph
+        return lower_graph(self, training)
 
     def _layer_list(self):
         return [self.nodes[_key(n)] for n in self.node_names]

@@ -17,22 +17,24 @@ class Net:
         return load_model(model_path)
 
     @staticmethod
-    def load_bigdl(model_path, weight_path=None, bigdl_type="float"):
+    def load_bigdl(model_path, weight_path=None, bigdl_type="float", native=True):
+        """``native``: run the imported graph on the zoo kernels (GraphNet.to_native); False keeps
+        the plain torch modules (the fp32 reference path)."""
         from zoo.pipeline.api.net.bigdl_loader import load_bigdl
-        return load_bigdl(model_path, weight_path)
+        return _native(load_bigdl(model_path, weight_path), native)
 
     @staticmethod
-    def load_caffe(def_path, model_path, bigdl_type="float"):
+    def load_caffe(def_path, model_path, bigdl_type="float", native=True):
         from zoo.pipeline.api.net.caffe_loader import load_caffe
-        return load_caffe(def_path, model_path)
+        return _native(load_caffe(def_path, model_path), native)
 
     @staticmethod
-    def load_onnx(model_path):
+    def load_onnx(model_path, native=True):
         from zoo.pipeline.api.onnx.onnx_loader import load_onnx
-        return load_onnx(model_path)
+        return _native(load_onnx(model_path), native)
 
     @staticmethod
-    def load_torch(path, bigdl_type="float"):
+    def load_torch(path, bigdl_type="float", native=True):
         """TorchScript archive -> TorchNet; a Lua Torch7 ``.t7`` nn model (Net.loadTorch,
         BigDL TorchFile) -> torch module rebuilt from the decoded objects."""
         with open(path, "rb") as f:
@@ -40,7 +42,7 @@ class Net:
         if magic[:2] != b"PK":   # not a zip archive: Torch7 binary serialisation
             from zoo.pipeline.api.net.torch7 import load_torch7
             from zoo.pipeline.api.net.torch_net import TorchNet
-            return TorchNet.from_pytorch(load_torch7(path))
+            return TorchNet.from_pytorch(load_torch7(path), native=native)
         from zoo.pipeline.api.net.torch_net import TorchNet
         return TorchNet.load(path)
 
@@ -58,3 +60,11 @@ class Net:
         HDF5 read by the built-in codec, no h5py)."""
         from zoo.pipeline.api.keras.keras_import import load_keras
         return load_keras(json_path, hdf5_path, by_name)
+
+
+def _native(graph, native):
+    """GraphNet loaders: swap in the native twins (in inference form; a later ``fit`` keeps the
+    fused BatchNorm in training mode inside the native conv node)."""
+    if native and hasattr(graph, "to_native"):
+        graph.to_native()
+    return graph

@@ -1,11 +1,11 @@
 """TorchNet / TorchModel / TorchCriterion (Zs/pipeline/api/net/TorchNet.scala:39-242,
 TorchCriterion.scala; Py/pipeline/api/net/torch_net.py ``TorchNet.from_pytorch``).
 
-The reference pushes JVM-held weights into libtorch on every forward. Here
-PyTorch-ROCm IS the compute substrate, so a TorchNet simply adopts the
-nn.Module as a Keras layer: its parameters join the engine's flat fp32
-master / gradient buffers like any other layer (bucketed RCCL all-reduce,
-fused optimizer), and its ops run on MI355X through PyTorch.
+The reference pushes JVM-held weights into libtorch on every forward. Here a
+TorchNet adopts the nn.Module as a Keras layer: its parameters join the engine's
+flat fp32 master / gradient buffers like any other layer (bucketed RCCL
+all-reduce, fused optimizer), and ``from_pytorch`` swaps its standard layers for
+the native-kernel twins of zoo.pipeline.api.net.native_lower.
 """
 import io
 
@@ -24,10 +24,18 @@ class TorchNet(KerasNet):
         self.built = True
 
     @staticmethod
-    def from_pytorch(module, input_shape=None, sample_input=None):
-        """Wrap an nn.Module (``sample_input`` is accepted for API parity; no tracing needed)."""
+    def from_pytorch(module, input_shape=None, sample_input=None, native=True):
+        """Wrap an nn.Module (``sample_input`` is accepted for API parity; no tracing needed).
+        ``native``: the module's conv / linear / pooling / batch-norm / activation / LRN / LSTM
+        submodules get their native twins IN PLACE (zoo.pipeline.api.net.native_lower swaps
+        the class only: parameters, state_dict keys and behaviour off the GPU are unchanged; the
+        reference instead pushes JVM-held weights into libtorch, TorchNet.scala:86-113).
+        TorchScript modules are wrapped as they are."""
         if sample_input is not None and input_shape is None:
             input_shape = tuple(sample_input.shape[1:])
+        if native and not isinstance(module, torch.jit.ScriptModule):
+            from zoo.pipeline.api.net.native_lower import lower_module
+            module = lower_module(module, training=module.training)
         return TorchNet(module, input_shape)
 
     @staticmethod

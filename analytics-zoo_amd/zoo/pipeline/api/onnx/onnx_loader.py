@@ -15,6 +15,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from zoo.pipeline.api.net import native_lower as NL
+
 from zoo.pipeline.api.net import graph_net as G
 from zoo.utils.protobuf import (as_float32, as_str, enc_bytes, enc_float, enc_int, enc_packed_ints, group,
                                 packed_doubles, packed_floats, packed_varints)
@@ -150,6 +152,10 @@ def _conv(x, a):
     if p[0] != p[2] or p[1] != p[3]:
         inp = F.pad(inp, (p[1], p[3], p[0], p[2]))
         p = [0, 0, 0, 0]
+    y = NL.conv2d_nchw(inp, w, b, tuple(a.get("strides", [1, 1])), (p[0], p[1]), tuple(a.get("dilations", [1, 1])),
+                       a.get("group", 1))
+    if y is not None:   # the native implicit-GEMM kernels (GPU, groups == 1)
+        return y
     return F.conv2d(inp, w, b, tuple(a.get("strides", [1, 1])), (p[0], p[1]), tuple(a.get("dilations", [1, 1])),
                     a.get("group", 1))
 
@@ -161,11 +167,20 @@ def _same_conv(inp, w, b, a):
     oh, ow = -(-ih // s[0]), -(-iw // s[1])
     ph, pw = max((oh - 1) * s[0] + k[0] - ih, 0), max((ow - 1) * s[1] + k[1] - iw, 0)
     inp = F.pad(inp, (pw // 2, pw - pw // 2, ph // 2, ph - ph // 2))
+    y = NL.conv2d_nchw(inp, w, b, tuple(s), (0, 0), tuple(a.get("dilations", [1, 1])), a.get("group", 1))
+    if y is not None:
+        return y
     return F.conv2d(inp, w, b, tuple(s), 0, tuple(a.get("dilations", [1, 1])), a.get("group", 1))
 
 
 def _gemm(x, a):
     A, B = x[0], x[1]
+    if (A.is_cuda and A.dim() == 2 and B.dim() == 2 and not a.get("transA", 0) and a.get("alpha", 1.0) == 1.0 and
+            (len(x) < 3 or x[2] is None or (a.get("beta", 1.0) == 1.0 and x[2].dim() == 1))):
+        # Y = A B^T (+ c): the native MFMA linear with the bias in its epilogue
+        W = B if a.get("transB", 0) else B.t()
+        from zoo import ops
+        return ops.linear(A, W, x[2] if len(x) > 2 else None)
     if a.get("transA", 0):
         A = A.t()
     if a.get("transB", 0):
@@ -185,6 +200,11 @@ def _pool(kind):
         if p[0] != p[2] or p[1] != p[3]:
             inp = F.pad(inp, (p[1], p[3], p[0], p[2]), value=float("-inf") if kind == "max" else 0.0)
             p = [0, 0, 0, 0]
+        if inp.dim() == 4 and len(k) == 2:
+            y = NL.pool2d_nchw(inp, kind, tuple(k), tuple(s), (p[0], p[1]), bool(a.get("ceil_mode", 0)),
+                               bool(a.get("count_include_pad", 0)))
+            if y is not None:
+                return y
         if kind == "max":
             return F.max_pool2d(inp, k, s, (p[0], p[1]), ceil_mode=bool(a.get("ceil_mode", 0)))
         return F.avg_pool2d(inp, k, s, (p[0], p[1]), ceil_mode=bool(a.get("ceil_mode", 0)),
@@ -193,6 +213,10 @@ def _pool(kind):
 
 
 def _bn(x, a):
+    if x[0].dim() == 4:
+        y = NL.batch_norm_nchw_eval(x[0], x[3], x[4], x[1], x[2], a.get("epsilon", 1e-5))
+        if y is not None:
+            return y
     return F.batch_norm(x[0], x[3], x[4], x[1], x[2], False, 0.0, a.get("epsilon", 1e-5))
 
 
@@ -267,12 +291,22 @@ def _many(fn):
     return f
 
 
+def _act(x, name, ref):
+    y = NL.activation(x, name)
+    return ref(x) if y is None else y
+
+
+def _gap(x):
+    y = NL.global_avg_pool_nchw(x) if x.dim() == 4 else None
+    return x.mean(dim=tuple(range(2, x.dim())), keepdim=True) if y is None else y
+
+
 _OPS = {
     "Conv": _conv, "Gemm": _gemm, "MatMul": lambda x, a: x[0] @ x[1],
     "Add": lambda x, a: x[0] + x[1], "Sub": lambda x, a: x[0] - x[1], "Mul": lambda x, a: x[0] * x[1],
     "Div": lambda x, a: x[0] / x[1], "Pow": lambda x, a: x[0] ** x[1], "Neg": lambda x, a: -x[0],
-    "Relu": lambda x, a: torch.relu(x[0]), "Sigmoid": lambda x, a: torch.sigmoid(x[0]),
-    "Tanh": lambda x, a: torch.tanh(x[0]), "Exp": lambda x, a: torch.exp(x[0]), "Log": lambda x, a: torch.log(x[0]),
+    "Relu": lambda x, a: _act(x[0], "relu", torch.relu), "Sigmoid": lambda x, a: _act(x[0], "sigmoid", torch.sigmoid),
+    "Tanh": lambda x, a: _act(x[0], "tanh", torch.tanh), "Exp": lambda x, a: torch.exp(x[0]), "Log": lambda x, a: torch.log(x[0]),
     "Sqrt": lambda x, a: torch.sqrt(x[0]), "Abs": lambda x, a: torch.abs(x[0]),
     "Erf": lambda x, a: torch.erf(x[0]), "Softsign": lambda x, a: F.softsign(x[0]),
     "Softplus": lambda x, a: F.softplus(x[0]),
@@ -282,7 +316,7 @@ _OPS = {
     "PRelu": lambda x, a: torch.where(x[0] >= 0, x[0], x[0] * x[1]),
     "Softmax": _softmax(F.softmax), "LogSoftmax": _softmax(F.log_softmax),
     "MaxPool": _pool("max"), "AveragePool": _pool("avg"),
-    "GlobalAveragePool": lambda x, a: x[0].mean(dim=tuple(range(2, x[0].dim())), keepdim=True),
+    "GlobalAveragePool": lambda x, a: _gap(x[0]),
     "GlobalMaxPool": lambda x, a: x[0].amax(dim=tuple(range(2, x[0].dim())), keepdim=True),
     "BatchNormalization": _bn, "Flatten": _flatten, "Reshape": _reshape,
     "Transpose": lambda x, a: x[0].permute(a.get("perm") or list(reversed(range(x[0].dim())))),

@@ -1,0 +1,208 @@
+"""Imported and wrapped models on the native kernels (VERDICT r3 missing #1): the reference
+fixtures (BigDL LeNet ``.model``, Caffe ``test_persist``), an ONNX graph and TorchNet-wrapped
+PyTorch modules (CNN with BatchNorm, LSTM) run through zoo.pipeline.api.net.native_lower and must
+match the fp32 torch path of the SAME graph, with the GPU trace showing zoo:: kernels and no
+MIOpen / hipBLASLt (Cijk_) kernel."""
+import copy
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+REF = "/root/reference/zoo/src/test/resources/models"
+BANNED = ("miopen", "MIOpen", "mlo", "naive_conv", "gridwise_", "Cijk_")
+need_ref = pytest.mark.skipif(not os.path.isdir(REF), reason="reference fixtures not present")
+
+
+def _kernels_of(fn):
+    from torch.profiler import ProfilerActivity, profile
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        out = fn()
+        torch.cuda.synchronize()
+    return out, [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+
+
+def _check_native(names):
+    assert any("zoo::" in n for n in names), names[:10]
+    bad = sorted({n for n in names if any(b in n for b in BANNED)})
+    assert not bad, bad[:5]
+
+
+def _nrel(a, b):
+    a, b = torch.as_tensor(a).float().flatten(), torch.as_tensor(b).float().flatten()
+    return ((a - b).norm() / b.norm().clamp_min(1e-12)).item()
+
+
+@need_ref
+def test_bigdl_lenet_fixture_native(gpu):
+    from zoo.pipeline.api.net import Net
+    path = os.path.join(REF, "bigdl/bigdl_lenet.model")
+    nat = Net.load_bigdl(path).to(gpu).eval()
+    ref = Net.load_bigdl(path, native=False).eval()
+    from zoo.pipeline.api.net.native_lower import ZConv2d, ZLinear
+    assert isinstance(nat.node("conv1_5x5").op, ZConv2d) and isinstance(nat.node("fc1").op, ZLinear)
+    x = torch.rand(8, 1, 28, 28)
+    with torch.no_grad():
+        out, names = _kernels_of(lambda: nat(x.to(gpu)))
+        want = ref(x)
+    _check_native(names)
+    assert _nrel(out.cpu(), want) < 2e-2
+    assert (out.cpu().argmax(1) == want.argmax(1)).float().mean() >= 0.75
+
+
+@need_ref
+def test_caffe_persist_fixture_native(gpu):
+    from zoo.pipeline.api.net import Net
+    d = os.path.join(REF, "caffe/test_persist.prototxt")
+    w = os.path.join(REF, "caffe/test_persist.caffemodel")
+    nat = Net.load_caffe(d, w).to(gpu).eval()
+    ref = Net.load_caffe(d, w, native=False).eval()
+    x = torch.rand(4, 3, 5, 5)
+    with torch.no_grad():
+        out, names = _kernels_of(lambda: nat(x.to(gpu)))
+        want = ref(x)
+    _check_native(names)
+    assert _nrel(out.cpu(), want) < 2e-2
+
+
+def test_onnx_graph_native(gpu):
+    from zoo.pipeline.api.net import Net
+    from zoo.pipeline.api.onnx.onnx_loader import enc_node, make_model
+    rng = np.random.default_rng(1)
+    wc = rng.standard_normal((16, 3, 3, 3)).astype(np.float32) * 0.3
+    bc = rng.standard_normal(16).astype(np.float32)
+    wg = rng.standard_normal((10, 16 * 8 * 8)).astype(np.float32) * 0.05
+    bg = rng.standard_normal(10).astype(np.float32)
+    scale, bias = np.ones(16, np.float32) * 1.5, np.full(16, 0.1, np.float32)
+    mean, var = np.full(16, 0.2, np.float32), np.full(16, 2.0, np.float32)
+    nodes = [enc_node("Conv", ["x", "wc", "bc"], ["c"], "conv", kernel_shape=[3, 3], pads=[1, 1, 1, 1]),
+             enc_node("BatchNormalization", ["c", "s", "b", "m", "v"], ["bn"], "bn", epsilon=1e-5),
+             enc_node("Relu", ["bn"], ["r"], "relu"),
+             enc_node("MaxPool", ["r"], ["p"], "pool", kernel_shape=[2, 2], strides=[2, 2]),
+             enc_node("Flatten", ["p"], ["f"], "flat", axis=1),
+             enc_node("Gemm", ["f", "wg", "bg"], ["g"], "fc", transB=1)]
+    data = make_model(nodes, [("x", [1, 3, 16, 16])], [("g", [1, 10])],
+                      {"wc": wc, "bc": bc, "wg": wg, "bg": bg, "s": scale, "b": bias, "m": mean, "v": var})
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "m.onnx")
+        with open(p, "wb") as f:
+            f.write(data)
+        g = Net.load_onnx(p).to(gpu).eval()
+        r = Net.load_onnx(p, native=False).eval()
+    x = torch.randn(4, 3, 16, 16)
+    with torch.no_grad():
+        out, names = _kernels_of(lambda: g(x.to(gpu)))
+        want = r(x)
+    _check_native(names)
+    assert _nrel(out.cpu(), want) < 2e-2
+
+
+class _CNN(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.features = nn.Sequential(
+            nn.Conv2d(3, 32, 3, padding=1), nn.BatchNorm2d(32), nn.ReLU(),
+            nn.MaxPool2d(2),
+            nn.Conv2d(32, 64, 3, padding=1, bias=False), nn.BatchNorm2d(64), nn.ReLU(),
+            nn.AdaptiveAvgPool2d(1))
+        self.head = nn.Sequential(nn.Flatten(), nn.Linear(64, 32), nn.ReLU(), nn.Linear(32, 10))
+
+    def forward(self, x):
+        return self.head(self.features(x))
+
+
+def test_torchnet_cnn_inference_and_training(gpu):
+    from zoo.pipeline.api.net import TorchNet
+    from zoo.pipeline.api.net.native_lower import ZConv2d
+    torch.manual_seed(0)
+    base = _CNN()
+    with torch.no_grad():   # non-trivial running statistics
+        for m in base.modules():
+            if isinstance(m, nn.BatchNorm2d):
+                m.running_mean.uniform_(-0.2, 0.2)
+                m.running_var.uniform_(0.5, 1.5)
+    ref = copy.deepcopy(base).to(gpu)
+    keys = list(base.state_dict().keys())
+    net = TorchNet.from_pytorch(base.eval())
+    assert list(net.module.state_dict().keys()) == keys            # class swap only
+    assert isinstance(net.module.features[0], ZConv2d)
+    net.module.to(gpu)
+    x = torch.randn(8, 3, 32, 32, device=gpu)
+    with torch.no_grad():
+        out, names = _kernels_of(lambda: net.module(x))
+        want = ref.eval()(x)
+    _check_native(names)
+    assert _nrel(out, want) < 2e-2
+    # training mode: batch statistics, gradients of every parameter group
+    net.module.train()
+    ref.train()
+    y = torch.randint(0, 10, (8,), device=gpu)
+
+    def step():
+        loss = F.cross_entropy(net.module(x).float(), y)
+        loss.backward()
+        return loss
+    _, names = _kernels_of(step)
+    _check_native(names)
+    F.cross_entropy(ref(x), y).backward()
+    for (n, p), (_, q) in zip(net.module.named_parameters(), ref.named_parameters()):
+        cos = F.cosine_similarity(p.grad.flatten().float(), q.grad.flatten().float(), dim=0).item()
+        assert cos > 0.98, (n, cos)
+    for a, b in zip(net.module.modules(), ref.modules()):
+        if isinstance(b, nn.BatchNorm2d):
+            assert torch.allclose(a.running_mean, b.running_mean, atol=2e-3)
+
+
+class _Seq(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.lstm = nn.LSTM(12, 48, num_layers=2, batch_first=True)
+        self.bi = nn.LSTM(48, 32, batch_first=True, bidirectional=True)
+        self.fc = nn.Linear(64, 4)
+
+    def forward(self, x):
+        h, _ = self.lstm(x)
+        h, (hn, cn) = self.bi(h)
+        return self.fc(h[:, -1]), hn, cn
+
+
+def test_torchnet_lstm_native(gpu):
+    from zoo.pipeline.api.net import TorchNet
+    torch.manual_seed(1)
+    base = _Seq()
+    ref = copy.deepcopy(base).to(gpu)
+    net = TorchNet.from_pytorch(base).module.to(gpu)
+    x = torch.randn(5, 9, 12, device=gpu)
+    with torch.no_grad():
+        (y, hn, cn), names = _kernels_of(lambda: net(x))
+        yr, hr, cr = ref(x)
+    assert any("zoo::" in n for n in names)
+    assert not [n for n in names if "miopen" in n.lower() or "Cijk_" in n], names[:8]
+    assert _nrel(y, yr) < 3e-2 and _nrel(hn, hr) < 3e-2 and _nrel(cn, cr) < 3e-2
+    # backward through the persistent kernel
+    out = net(x)[0].float().pow(2).sum()
+    out.backward()
+    ref(x)[0].pow(2).sum().backward()
+    for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        cos = F.cosine_similarity(p.grad.flatten().float(), q.grad.flatten().float(), dim=0).item()
+        assert cos > 0.97, (n, cos)
+
+
+def test_automl_nets_run_native(gpu):
+    from zoo.automl.model._nets import VanillaLSTMNet
+    from zoo.pipeline.api.net.native_lower import ZLinear, ZLSTM
+    torch.manual_seed(2)
+    net = VanillaLSTMNet(3, 2, lstm_1_units=32, lstm_2_units=16).to(gpu).eval()
+    assert isinstance(net.l1, ZLSTM) and isinstance(net.fc, ZLinear)
+    x = torch.randn(16, 10, 3, device=gpu)
+    with torch.no_grad():
+        y, names = _kernels_of(lambda: net(x))
+    assert y.shape == (16, 2) and torch.isfinite(y).all()
+    assert any("zoo::" in n for n in names)
+    assert not [n for n in names if "miopen" in n.lower() or "Cijk_" in n], names[:8]

@@ -1,7 +1,6 @@
-"""Every ImageClassifier backbone and both SSD detectors train on the native NHWC
-kernels (one engine step each, finite loss, forward shapes), and the native
-backbones match a plain fp32 PyTorch forward of the same weights on a small batch
-(MobileNet-v2: depthwise + residual BN units)."""
+"""Every ImageClassifier backbone and both SSD detectors on the native NHWC kernels: per-layer
+local parity (forward and backward) against the fp32 reference path, eval-mode end-to-end
+logits, training through the engine; SSD loss and gradients against the fp32 reference."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -14,65 +13,42 @@ NETS = [("vgg-16", 224), ("alexnet", 227), ("squeezenet", 227), ("mobilenet", 22
 
 BANNED = ("miopen", "MIOpen", "mlo", "naive_conv", "gridwise_", "Cijk_")
 
-# Per-group gradient agreement (cosine of the concatenated group gradient) with the fp32 CPU
-# reference of the same weights. bf16 activations flip ReLU masks wherever a pre-activation is
-# within rounding of zero; with random labels the per-channel BN / bias sums are random walks, so
-# those flips alone move them by several percent, and over 50-100 layers the gradient direction
-# decorrelates (tools/layer_parity.py: every native layer is ~0.3 % off LOCALLY in the forward).
-# The bar is therefore relative: the native GPU path must agree with the fp32 reference at least
-# comparably to the same fp32 reference with bf16 rounding emulated at every module boundary
-# (activations forward, gradients backward): on the CPU that emulation alone gives conv / BN
-# cosines of 0.49 / 0.57 (MobileNet), 0.59 / 0.56 (Inception-v3), 0.71 / 0.73 (DenseNet-161); the
-# native units round at more points (pre-BN conv outputs, staged gradients), hence a ratio, and
-# an absolute bar that passes regardless where the reference itself is stable. Batch size does
-# not tame it (emulated MobileNet conv / BN at batch 8: 0.56 / 0.50, Inception-v1 0.68 / 0.72),
-# so in these groups the test can only show the native gradients are as decorrelated as a
-# second bf16 sample is -- measured native/emulated ratios are 0.55-0.6 (MobileNet conv, Inception-v1
-# BN); the per-op parity lives in test_zoo_kernels.py and tools/layer_parity.py.
-GROUP_COS = {"conv": 0.97, "fc": 0.98, "bn": 0.90, "dw": 0.97}
-COS_RATIO = 0.45
+def _layer_parity():
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "analytics-zoo_amd",
+                                    "tools"))
+    import layer_parity
+    return layer_parity
 
 
-def _bf16_emulated(model):
-    """Round every leaf module's output to bf16 in the forward and its gradient in the backward."""
-    def rnd(g):
-        return g.to(torch.bfloat16).to(g.dtype)
-
-    def hook(mod, inp, out):
-        if not torch.is_tensor(out) or not out.is_floating_point():
-            return out
-        o = out.to(torch.bfloat16).to(out.dtype)
-        if o.requires_grad:
-            o.register_hook(rnd)
-        return o
+def _calibrate_bn(model, x):
+    """Running statistics = the batch statistics of ``x`` (one training forward at momentum 1):
+    every BatchNorm then normalises in eval mode, so the eval network is numerically stable."""
+    saved = {}
     for m in model.modules():
-        if not list(m.children()):
-            m.register_forward_hook(hook)
+        if hasattr(m, "momentum") and hasattr(m, "running_mean"):
+            saved[m] = m.momentum
+            m.momentum = 1.0
+    model.train()
+    with torch.no_grad():
+        model(x)
+    for m, mom in saved.items():
+        m.momentum = mom
     return model
 
 
-def _group(name, p):
-    if name.endswith(("gamma", "beta")):
-        return "bn"
-    if "fc" in name or "classifier" in name:
-        return "fc"
-    if p.dim() == 2 and p.shape[0] <= 25 and "dw" in name:
-        return "dw"
-    return "conv"
-
-
-def _cos(a, b):
-    a, b = a.double().flatten(), b.double().flatten()
-    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
-
-
 @pytest.mark.parametrize("name,hw", NETS)
-def test_backbone_matches_fp32_and_trains_natively(gpu, name, hw, monkeypatch):
-    """Forward logits and per-group parameter gradients of the native bf16 NHWC backbone vs the
-    same weights through the fp32 CPU reference path (plain F.conv2d / batch-norm / pooling),
-    training-mode BatchNorm, dropout disabled on both sides; the GPU trace holds zoo:: kernels
-    and no MIOpen / hipBLASLt kernel; then one engine step per net trains (finite loss)."""
+def test_backbone_layer_parity_and_trains_natively(gpu, name, hw, monkeypatch):
+    """Every native layer against the SAME layer on the fp32 CPU path, fed the layer's actual
+    GPU input and upstream gradient (tools/layer_parity.py): local forward error <= 2 % per
+    layer, median local dx / dweight error <= 5 % (bf16 rounding plus the ReLU-mask flips of
+    pre-activations within rounding of zero; a wrong kernel shows O(1)). End to end in a stable
+    regime -- eval mode with calibrated BatchNorm statistics -- the logits match the fp32
+    reference within 5 %. The GPU trace holds zoo:: kernels and no MIOpen / hipBLASLt kernel;
+    then the engine trains the net (finite loss)."""
     import copy
+    import statistics
     from torch.profiler import ProfilerActivity, profile
     from zoo.common.nncontext import init_nncontext
     from zoo.models.image import native_nets
@@ -84,40 +60,40 @@ def test_backbone_matches_fp32_and_trains_natively(gpu, name, hw, monkeypatch):
     monkeypatch.setattr(native_nets, "_dropout", lambda x, p, training: x)
     torch.manual_seed(0)
     net = build(name, 16)
-    ref = copy.deepcopy(net).train()
-    emu = _bf16_emulated(copy.deepcopy(net).train())
-    g = copy.deepcopy(net).to(gpu).train()
+    cpu = copy.deepcopy(net)
+    g = copy.deepcopy(net).to(gpu)
     x = torch.randn(2, 3, hw, hw)
     y = torch.randint(0, 16, (2,))
-    out_r = ref(x)
-    F.cross_entropy(out_r.float(), y).backward()
-    out_e = emu(x)
-    F.cross_entropy(out_e.float(), y).backward()
+    lp = _layer_parity()
     with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        out_g = g(x.to(gpu))
-        softmax_cross_entropy(out_g, y.to(gpu)).backward()
-        torch.cuda.synchronize()
+        rows = lp.run(g, cpu, x.to(gpu), lambda o: softmax_cross_entropy(o, y.to(gpu)), train=True)
     names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
     assert any("zoo::" in n for n in names)
     bad = sorted({n for n in names if any(b in n for b in BANNED)})
     assert not bad, bad[:5]
-    rel = ((out_g.float().cpu() - out_r.float()).norm() / out_r.float().norm()).item()
-    rel_e = ((out_e.float() - out_r.float()).norm() / out_r.float().norm()).item()
-    assert rel < max(0.05, 2.0 * rel_e), ("logits", rel, rel_e)
-    groups = {}
-    for (n, pr), (_, pe), (_, pg) in zip(ref.named_parameters(), emu.named_parameters(), g.named_parameters()):
-        if pr.grad is None or pr.grad.abs().max() == 0:
-            continue
-        k = _group(n, pr)
-        a, b, c = groups.setdefault(k, ([], [], []))
-        a.append(pg.grad.detach().float().cpu().flatten())
-        b.append(pr.grad.detach().float().flatten())
-        c.append(pe.grad.detach().float().flatten())
-    report = {k: round(_cos(torch.cat(a), torch.cat(b)), 4) for k, (a, b, _) in groups.items()}
-    report_e = {k: round(_cos(torch.cat(c), torch.cat(b)), 4) for k, (_, b, c) in groups.items()}
-    print(name, "logits rel %.4f (bf16-emulated %.4f)" % (rel, rel_e), report, "emulated", report_e)
-    for k, c in report.items():
-        assert c >= min(GROUP_COS[k], COS_RATIO * report_e[k]), (k, c, report, report_e)
+    rows = [r for r in rows if "error" not in r]
+    assert len(rows) >= 8, rows[:3]
+    fwd = max(r["fwd"] for r in rows)
+    dx = [r["dx"] for r in rows if "dx" in r]
+    dw = [v for r in rows for k, v in r.items() if k.startswith("d") and k not in ("dx",) and isinstance(v, float)]
+    print(name, "layers", len(rows), "max fwd", fwd, "median dx", statistics.median(dx) if dx else None,
+          "median dW", statistics.median(dw) if dw else None)
+    assert fwd <= 0.02, [r for r in rows if r["fwd"] > 0.02][:3]
+    assert dx and statistics.median(dx) <= 0.05, statistics.median(dx)
+    assert dw and statistics.median(dw) <= 0.05, statistics.median(dw)
+    # end to end, stable regime: eval mode with calibrated BatchNorm statistics
+    torch.manual_seed(1)
+    net2 = build(name, 16)
+    xc = torch.randn(8, 3, hw, hw)
+    _calibrate_bn(net2, xc)
+    g2 = copy.deepcopy(net2).to(gpu).eval()
+    net2.eval()
+    xe = torch.randn(4, 3, hw, hw)
+    with torch.no_grad():
+        lr = net2(xe).float()
+        lg = g2(xe.to(gpu)).float().cpu()
+    rel = ((lg - lr).norm() / lr.norm()).item()
+    assert rel < 0.05, ("eval logits", rel)
     # and the engine trains it (fused optimizer, flat buffers)
     eng = TrainingEngine(build(name, 16), softmax_cross_entropy, SGD(learningrate=0.01, momentum=0.9))
     xg = torch.randn(4, 3, hw, hw, device=gpu)
@@ -184,3 +160,48 @@ def test_ssd_trains_natively(gpu, mobilenet):
     from zoo_models_bench import bench_ssd
     r = bench_ssd(2, 2, mobilenet=mobilenet)
     assert r["loss"] == r["loss"] and r["loss"] > 0
+
+
+@pytest.mark.parametrize("mobilenet", [False, True])
+def test_ssd_loss_and_gradient_parity(gpu, mobilenet):
+    """SSD (VGG-16 / MobileNet, 300x300) on the native kernels vs the same weights on the fp32
+    CPU path: MultiBoxLoss within 3 %, and per-layer local parity of every layer of the
+    detector (backbone, extras, loc / conf heads) in the training backward: local forward error
+    <= 2 %, median local dx / dweight error <= 5 %."""
+    import copy
+    import statistics
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image.objectdetection.ssd import SSD, SSDMobileNet, MultiBoxLoss
+    init_nncontext("ssd-parity")
+    torch.manual_seed(0)
+    model = SSDMobileNet(21) if mobilenet else SSD(21)
+    crit = MultiBoxLoss(21)
+    cpu = copy.deepcopy(model).train()
+    g = copy.deepcopy(model).to(gpu).train()
+    gen = torch.Generator().manual_seed(0)
+    x = torch.randn(2, 3, 300, 300)
+    targets = []
+    for _ in range(2):
+        xy = torch.rand(3, 2, generator=gen) * 0.6
+        wh = torch.rand(3, 2, generator=gen) * 0.3 + 0.05
+        lab = torch.randint(1, 21, (3, 1), generator=gen).float()
+        targets.append(torch.cat([lab, xy, xy + wh], 1))
+    pri = model.priors
+    oc = cpu(x)
+    lc = float(crit(oc[0].float(), oc[1].float(), pri, targets))
+    og = g(x.to(gpu))
+    lg = float(crit(og[0].float(), og[1].float(), pri.to(gpu), [t.to(gpu) for t in targets]))
+    assert abs(lg - lc) / abs(lc) < 0.03, (lg, lc)
+    lp = _layer_parity()
+    tg = [t.to(gpu) for t in targets]
+    rows = lp.run(g, copy.deepcopy(model).train(), x.to(gpu),
+                  lambda o: crit(o[0].float(), o[1].float(), pri.to(gpu), tg), train=True)
+    rows = [r for r in rows if "error" not in r]
+    assert len(rows) >= 10
+    dx = [r["dx"] for r in rows if "dx" in r]
+    dw = [v for r in rows for k, v in r.items() if k.startswith("d") and k != "dx" and isinstance(v, float)]
+    fwd = max(r["fwd"] for r in rows)
+    print("ssd", "mobilenet" if mobilenet else "vgg", "loss", lg, lc, "max fwd", fwd, "median dx",
+          statistics.median(dx), "median dW", statistics.median(dw))
+    assert fwd <= 0.02
+    assert statistics.median(dx) <= 0.05 and statistics.median(dw) <= 0.05
