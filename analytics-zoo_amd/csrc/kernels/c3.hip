@@ -1,0 +1,491 @@
+// Persistent streaming 3x3 convolution for the 64-channel stride-1 layers of ResNet stage 1
+// (56x56x64 -> 64, forward and its data gradient) on gfx950.
+//
+//   Y[n][p][q][k] = epilogue( sum_{r,s,c} X[n][p+r-1][q+s-1][c] * W[k][r][s][c] ),  C = K = 64
+//
+// Why a separate kernel (profiles/r4/c3_r4.md): the implicit-GEMM kernels (igemm.hip, and
+// igemm2.hip's band tiles that already read all nine taps from one LDS patch) spent ~115 us on
+// a conv whose MFMA time is ~24 us and whose bytes take ~35 us: with the MFMAs, the B staging
+// and the output stores all switched off the band kernel still took 70 us. Each workgroup was a
+// serial latency chain -- patch DMA, nine barrier-separated K-tiles each waiting on an L2 weight
+// tile, epilogue -- and only two fit a CU. Here one workgroup per CU streams whole images:
+//   * the 9 x 64 x 64 weights live in VGPRs for the whole kernel (36 MFMA B fragments per
+//     lane, loaded once straight from global memory): no weight staging, no per-tap barrier;
+//   * input rows stream through an LDS ring of 2*TP + 2 rows (TP = 224 / W output rows per
+//     band): band b reads rows b*TP-1 .. b*TP+TP while rows (b+1)*TP+1 .. (b+1)*TP+TP of the
+//     next band land behind it (LDS-DMA, 16 B per lane), so each input line is fetched ONCE;
+//     the ring rows carry their zero padding columns permanently;
+//   * one barrier per band (224 output pixels x 64 channels, 252 MFMAs per wave);
+//   * the epilogue leaves through a wave-private LDS patch as row-contiguous 16-byte stores;
+//     BN statistics (forward) / BN-backward sums (dgrad) stay in registers across all bands
+//     and are added once per workgroup. The dgrad epilogue (residual-gradient add, producer
+//     ReLU mask in any BwdStats.zmode) prefetches the band's operands before its MFMAs.
+// LDS chunk swizzle: pixel row px holds 16-byte chunk c at position c ^ (px & 7) (ds_read_b128
+// fragment reads of 16 consecutive pixels then hit distinct bank slots), applied through the
+// per-lane DMA source as in igemm2.hip.
+//
+// Reference parity: the MKL-DNN convolution behind BigDL SpatialConvolution in the ResNet-50
+// bottleneck (Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110).
+#include <stdlib.h>
+
+#include "common.h"
+#include "geom.h"
+#include "bnmask.h"
+
+namespace zoo {
+
+typedef __attribute__((address_space(3))) void c3_lds_void;
+typedef __attribute__((address_space(1))) const void c3_gl_void;
+
+__device__ __attribute__((aligned(64))) bf16_t c3_zero_page[64];
+
+constexpr int C3_NT = 256;                 // 4 waves: 2 (m) x 2 (n), wave tile 112 x 32
+constexpr int C3_BM = 224, C3_TM = 7, C3_TN = 2;
+constexpr int C3_PITCH = 36;               // epilogue fp32 patch pitch (32 columns + 4)
+constexpr int C3_EPI_BYTES = 4 * 112 * C3_PITCH * 4 + 2 * 64 * 2 * 4 + 4 * 64 * 4;
+
+struct C3Geom {
+  int N, H, W;         // input = output spatial (stride 1, pad 1); C = K = 64
+  int TP, nbands;      // output rows per band (224 / W), bands per image
+  int RR, PW2;         // ring rows (2 TP + 2), pixels per ring row (W + 2)
+  int bpc, chunks, items;  // bands per work item, items per image, total items
+  int ldb;             // weight row stride (>= 576)
+  int partial;         // 1: statistics as one partial row per workgroup (ordered fold by the host)
+  unsigned long long* stamps;  // diagnostic build only: [grid][4 waves][5 segments] cycle sums
+};
+
+ZOO_DEV void c3_dma(const bf16_t* src, char* dst) {
+  __builtin_amdgcn_global_load_lds((c3_gl_void*)src, (c3_lds_void*)dst, 16, 0, 0);
+}
+
+// in-kernel cycle stamp (diagnostic instantiation only, cdna_hip_programming.md §7)
+#define C3_STAMP(var)                                                                  \
+  if constexpr (STAMP) {                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");       \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+  }
+
+template <int EPI, bool STAMP = false>
+__global__ __launch_bounds__(C3_NT, 1) void c3_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
+                                                      bf16_t* __restrict__ Y, const bf16_t* __restrict__ resid,
+                                                      float* __restrict__ stats, C3Geom g, BwdStats bs) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  char* const ring = smem;
+  const int ring_bytes = g.RR * g.PW2 * 128;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  float* const patch = reinterpret_cast<float*>(smem + ring_bytes) + w * 112 * C3_PITCH;
+  float* const red = reinterpret_cast<float*>(smem + ring_bytes) + 4 * 112 * C3_PITCH;  // [2][64][2]
+  // dgrad epilogue per-channel constants [mean | inv | mask scale | mask shift][64] (LDS, not
+  // VGPRs: the register file holds the weights, accumulators and the prefetched operands)
+  float* const coef = red + 2 * 64 * 2;
+  const int lr = lane >> 3;
+  const int W = g.W, H = g.H;
+  const int PQ = H * W;
+
+  // ---- padding columns of every ring row: zero once, the row DMA never touches them ----
+  for (int i = tid; i < g.RR * 16; i += C3_NT) {
+    const int row = i >> 4, side = (i >> 3) & 1, c = i & 7;
+    const int px = row * g.PW2 + (side ? g.PW2 - 1 : 0);
+    *reinterpret_cast<uint4*>(ring + px * 128 + c * 16) = make_uint4(0u, 0u, 0u, 0u);
+  }
+
+  // ---- weights: all nine taps' B fragments in registers ----
+  // fragment (tap t, kk, j): lane holds W[n = wn*32 + j*16 + (lane & 15)][t*64 + kk*32 + (lane>>4)*8 .. +7]
+  bf16x8 bw[9][2][C3_TN];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < C3_TN; ++j) {
+        const int n = wn * 32 + j * 16 + (lane & 15);
+        bw[t][kk][j] = *reinterpret_cast<const bf16x8*>(Wt + (size_t)n * g.ldb + t * 64 + kk * 32 + (lane >> 4) * 8);
+      }
+
+  // ring row loader: input rows h0 .. h0+nrows-1 of image img into slots (h + 1) mod RR, pixels
+  // 1..W; piece (row k, 8-pixel group c) goes to wave (k * W/8 + c) % 4
+  const int ppr = W >> 3;
+  auto load_rows = [&](int img, int h0, int nrows) {
+    const int np = nrows * ppr;
+    for (int q = w; q < np; q += 4) {  // q, k, c, h, slot: wave-uniform (scalar) values
+      const int k = q / ppr, c = q - k * ppr;
+      const int h = h0 + k;
+      int slot = (h + 1) % g.RR;
+      if (slot < 0) slot += g.RR;
+      const int px0 = slot * g.PW2 + 1 + c * 8;
+      // per lane only the pixel-in-piece and the swizzled chunk: scalar row base + 32-bit offset
+      const int gch = (lane & 7) ^ ((px0 + lr) & 7);
+      const bf16_t* src = c3_zero_page;
+      if ((unsigned)h < (unsigned)H) {
+        const bf16_t* rowbase = X + (((size_t)img * H + h) * W + c * 8) * 64;
+        src = rowbase + (lr * 64 + gch * 8);
+      }
+      c3_dma(src, ring + px0 * 128);
+    }
+  };
+
+  // per-lane output rows of its 7 row tiles (MFMA rows = lane & 15)
+  int a_pp[C3_TM], a_qq[C3_TM];
+#pragma unroll
+  for (int i = 0; i < C3_TM; ++i) {
+    const int t = wm * 112 + i * 16 + (lane & 15);
+    a_pp[i] = t / W;
+    a_qq[i] = t - a_pp[i] * W;
+  }
+  // epilogue piece of each slice: patch row er = lane >> 2, 8-column chunk ch = lane & 3
+  const int er = lane >> 2, ch = lane & 3;
+  const int col = wn * 32 + ch * 8;
+  int e_pp[C3_TM];
+#pragma unroll
+  for (int i = 0; i < C3_TM; ++i) e_pp[i] = (wm * 112 + i * 16 + er) / W;
+
+  float s1[8], s2[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  if constexpr (EPI == 2) {
+    if (tid < 64) {
+      float sc1[8], sh1[8];
+      const int c8 = tid & ~7;
+      bnm_coeffs(bs, c8, bs.sums != nullptr, sc1, sh1);
+      coef[tid] = bs.sums ? bs.mean[tid] : 0.f;
+      coef[64 + tid] = bs.sums ? bs.inv[tid] : 0.f;
+      coef[128 + tid] = sc1[tid & 7];
+      coef[192 + tid] = sh1[tid & 7];
+    }
+  }
+
+  const int fr = lane & 15, fq = lane >> 4;
+  const int co_hi = lane >> 4;
+  unsigned long long st_sum[5] = {0ull, 0ull, 0ull, 0ull, 0ull};
+
+  for (int item = blockIdx.x; item < g.items; item += gridDim.x) {
+    const int img = item / g.chunks;
+    const int b0 = (item - img * g.chunks) * g.bpc;
+    const int b1 = min(g.nbands, b0 + g.bpc);
+    load_rows(img, b0 * g.TP - 1, g.TP + 2);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int b = b0; b < b1; ++b) {
+      unsigned long long t0 = 0, t1 = 0, t2 = 0, t3 = 0, t4 = 0;
+      C3_STAMP(t0);
+      if (b + 1 < b1) load_rows(img, (b + 1) * g.TP + 1, g.TP);
+      const size_t mbase = (size_t)img * PQ + (size_t)b * g.TP * W;  // first output pixel of the band
+      // dgrad epilogue operands of this band, in flight during the MFMAs
+      // (the residual gradient and zmode 0's bf16 z are read at their use: neither is a ResNet
+      // form, and prefetching them too spilled registers)
+      uint4 py_v[C3_TM];
+      unsigned pm_v[C3_TM];
+      if constexpr (EPI == 2) {
+#pragma unroll
+        for (int i = 0; i < C3_TM; ++i) {
+          const bool ok = b * g.TP + e_pp[i] < H;
+          const size_t off = (mbase + wm * 112 + i * 16 + er) * 64 + col;
+          py_v[i] = make_uint4(0u, 0u, 0u, 0u);
+          pm_v[i] = 0u;
+          if (ok) {
+            if (bs.sums) py_v[i] = *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off);
+            if (bs.zmode == 2) pm_v[i] = reinterpret_cast<const uint8_t*>(bs.z)[off >> 3];
+          }
+        }
+      }
+
+      C3_STAMP(t1);
+      // ---- 9 taps x 2 k-halves x 7 x 2 MFMAs ----
+      f32x4 acc[C3_TM][C3_TN];
+#pragma unroll
+      for (int i = 0; i < C3_TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C3_TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      // per lane, once per band: the byte address of its k-half-0 fragment for every
+      // (filter row, filter column, row tile) -- 63 addresses; k-half 1 is the same address
+      // with chunk bit 2 flipped (byte bit 6), so a fragment read costs at most one VALU
+      int fad[3][3][C3_TM];
+      const int sbase = (b * g.TP) % g.RR;
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int i = 0; i < C3_TM; ++i) {
+          // input row p + r - 1 sits in slot (p + r) mod RR; sbase + pp + r < 2 RR
+          int slot = sbase + a_pp[i] + r;
+          slot = slot >= g.RR ? slot - g.RR : slot;
+          const int px = slot * g.PW2 + a_qq[i];
+#pragma unroll
+          for (int s = 0; s < 3; ++s) fad[r][s][i] = (px + s) * 128 + ((co_hi ^ ((px + s) & 7)) << 4);
+        }
+      // two-buffer tap pipeline: the 14 fragment reads of tap t+1 are interleaved with the 28
+      // MFMAs of tap t (one read per MFMA gap); tap t's reads are retired (lgkmcnt(0)) BEFORE
+      // tap t+1's are issued, so at most 14 LDS reads are ever outstanding: lgkmcnt is 4 bits,
+      // and with 28 pending hipcc can only wait for 0 (which exposed every other tap's reads)
+      bf16x8 afb[2][2][C3_TM];
+      auto read_tap = [&](int t, int buf) {
+        const int r = t / 3, s = t - r * 3;
+#pragma unroll
+        for (int i = 0; i < C3_TM; ++i) {
+          afb[buf][0][i] = *reinterpret_cast<const bf16x8*>(ring + fad[r][s][i]);
+          afb[buf][1][i] = *reinterpret_cast<const bf16x8*>(ring + (fad[r][s][i] ^ 64));
+        }
+      };
+      read_tap(0, 0);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
+        __builtin_amdgcn_sched_barrier(0);
+        // MFMA k of tap t, then (k >= 14) fragment read k-14 of tap t+1, pinned in that order:
+        // the reads start once the k-half-0 fragments are consumed, so no read lands in a
+        // register an in-flight MFMA still sources
+        const int r1 = (t + 1) / 3, s1 = (t + 1) - r1 * 3;
+#pragma unroll
+        for (int k = 0; k < 28; ++k) {
+          const int kk = k / 14, i = (k % 14) / 2, j = k % 2;
+          acc[i][j] = mfma16(afb[t & 1][kk][i], bw[t][kk][j], acc[i][j]);
+          if (t + 1 < 9 && k >= 14) {
+            const int ri = (k - 14) >> 1, rk = k & 1;
+            afb[(t + 1) & 1][rk][ri] = *reinterpret_cast<const bf16x8*>(ring + (fad[r1][s1][ri] ^ (rk << 6)));
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
+
+      C3_STAMP(t2);
+      // ---- epilogue: all 7 slices through the wave-private patch in one LDS round trip ----
+#pragma unroll
+      for (int i = 0; i < C3_TM; ++i)
+#pragma unroll
+        for (int j = 0; j < C3_TN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) patch[(i * 16 + fq * 4 + r) * C3_PITCH + j * 16 + fr] = acc[i][j][r];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      float4 elo[C3_TM], ehi[C3_TM];
+#pragma unroll
+      for (int i = 0; i < C3_TM; ++i) {
+        elo[i] = *reinterpret_cast<const float4*>(patch + (i * 16 + er) * C3_PITCH + ch * 8);
+        ehi[i] = *reinterpret_cast<const float4*>(patch + (i * 16 + er) * C3_PITCH + ch * 8 + 4);
+      }
+#pragma unroll
+      for (int i = 0; i < C3_TM; ++i) {
+        const float4 lo = elo[i], hi = ehi[i];
+        if (b * g.TP + e_pp[i] >= H) continue;
+        float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+        const size_t off = (mbase + wm * 112 + i * 16 + er) * 64 + col;
+        if constexpr (EPI == 1) {
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(Y + off) = pk;
+          if (stats) {
+            float q[8];
+            unpack8(pk, q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += q[e]; s2[e] += q[e] * q[e]; }
+          }
+        } else {
+          if (resid) {  // (no ResNet 3x3 dgrad has one: read at its use)
+            float rv[8];
+            unpack8(*reinterpret_cast<const uint4*>(resid + off), rv);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += rv[e];
+          }
+          float yy[8], mu[8], iv[8], msc[8], msh[8];
+          unpack8(py_v[i], yy);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            mu[e] = coef[col + e];
+            iv[e] = coef[64 + col + e];
+            msc[e] = coef[128 + col + e];
+            msh[e] = coef[192 + col + e];
+          }
+          if (bs.zmode == 0 && bs.z) {
+            float zz[8];
+            unpack8(*reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.z) + off), zz);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = zz[e] > 0.f ? v[e] : 0.f;
+          } else if (bs.zmode != 0) {
+            bnm_apply_pre(bs, yy, msc, msh, pm_v[i], make_uint4(0u, 0u, 0u, 0u), v);
+          }
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(Y + off) = pk;
+          if (bs.sums) {
+            float q[8];
+            unpack8(pk, q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += q[e];
+              s2[e] += q[e] * (yy[e] - mu[e]) * iv[e];
+            }
+          }
+        }
+      }
+      C3_STAMP(t3);
+      // the next band's rows have landed and every wave is done reading this band's slots
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      C3_STAMP(t4);
+      if constexpr (STAMP) {
+        st_sum[0] += t1 - t0; st_sum[1] += t2 - t1; st_sum[2] += t3 - t2; st_sum[3] += t4 - t3;
+        st_sum[4] += 1;
+      }
+    }
+  }
+
+  if constexpr (STAMP) {
+    if (lane == 0)
+      for (int k = 0; k < 5; ++k) g.stamps[((size_t)blockIdx.x * 4 + w) * 5 + k] = st_sum[k];
+  }
+  // ---- statistics: lanes sharing ch (bits 2..5), then the two wave rows, once per workgroup ----
+  float* const sacc = EPI == 1 ? stats : bs.sums;
+  if (!sacc) return;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+#pragma unroll
+    for (int o = 4; o < 64; o <<= 1) {
+      s1[e] += __shfl_xor(s1[e], o, 64);
+      s2[e] += __shfl_xor(s2[e], o, 64);
+    }
+  }
+  if (lane < 4) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      red[(wm * 64 + col + e) * 2 + 0] = s1[e];
+      red[(wm * 64 + col + e) * 2 + 1] = s2[e];
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const float a = red[tid * 2] + red[(64 + tid) * 2];
+    const float c = red[tid * 2 + 1] + red[(64 + tid) * 2 + 1];
+    if (g.partial) {
+      sacc[(size_t)blockIdx.x * 128 + tid] = a;
+      sacc[(size_t)blockIdx.x * 128 + 64 + tid] = c;
+    } else {
+      atomicAdd(sacc + tid, a);
+      atomicAdd(sacc + 64 + tid, c);
+    }
+  }
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+static int c3_mode() {
+  static const int m = [] {
+    const char* e = getenv("ZOO_C3");
+    return e ? atoi(e) : 1;
+  }();
+  return m;
+}
+static int g_c3_force = -1;  // -1: ZOO_C3, 0 off, 1 on (tests / A/B)
+static unsigned long long* g_c3_stamps = nullptr;
+static int g_c3_stamp_grid = 0;
+
+// diagnostic build (ZOO_C3_STAMPS): copy the last launch's [grid][4][5] stamp sums to host
+extern "C" int zoo_c3_stamps(unsigned long long* host, int cap) {
+  if (!g_c3_stamps) return 0;
+  const int n = g_c3_stamp_grid * 4 * 5 < cap ? g_c3_stamp_grid * 4 * 5 : cap;
+  hipDeviceSynchronize();
+  hipMemcpy(host, g_c3_stamps, (size_t)n * sizeof(unsigned long long), hipMemcpyDeviceToHost);
+  return n;
+}
+
+static int c3_ncu() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    if (n <= 0) n = 256;
+  }
+  return n;
+}
+
+static bool c3_geom(const ConvGeom& g, C3Geom& c) {
+  if (!(g.C == 64 && g.K == 64 && g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 &&
+        g.dh == 1 && g.dw == 1 && g.lh == 1 && g.lw == 1 && g.H == g.P && g.W == g.Q && !g.omap && g.Ktot == 576 &&
+        g.ldb >= 576 && g.ldb % 8 == 0))
+    return false;
+  if (g.W % 8 || C3_BM % g.W || C3_BM / g.W > g.H) return false;
+  c.N = g.N; c.H = g.H; c.W = g.W;
+  c.TP = C3_BM / g.W;
+  c.nbands = (g.H + c.TP - 1) / c.TP;
+  c.RR = 2 * c.TP + 2;
+  c.PW2 = g.W + 2;
+  if ((size_t)c.RR * c.PW2 * 128 + C3_EPI_BYTES > 160 * 1024) return false;
+  // work items: whole images when there are enough of them to fill the CUs, else images split
+  // into runs of bands (each run re-reads its first band's two halo rows)
+  const int ncu = c3_ncu();
+  int chunks = (ncu + g.N - 1) / g.N;
+  if (chunks > c.nbands) chunks = c.nbands;
+  if (chunks < 1) chunks = 1;
+  c.bpc = (c.nbands + chunks - 1) / chunks;
+  c.chunks = (c.nbands + c.bpc - 1) / c.bpc;
+  c.items = g.N * c.chunks;
+  c.ldb = g.ldb;
+  c.partial = 0;
+  c.stamps = nullptr;
+  return true;
+}
+
+// workgroups of zoo_c3 for this conv (rows of its partial-statistics buffer), 0 = not eligible
+extern "C" int zoo_c3_grid(const ConvGeom* g, int epi, const BwdStats* bs) {
+  const int on = g_c3_force >= 0 ? g_c3_force : c3_mode();
+  if (!on) return 0;
+  if (epi != 1 && epi != 2) return 0;
+  if (epi == 2 && bs && bs->zgelu) return 0;
+  C3Geom c;
+  if (!c3_geom(*g, c)) return 0;
+  return c.items < c3_ncu() ? c.items : c3_ncu();
+}
+
+extern "C" void zoo_c3_set(int on) { g_c3_force = on; }
+
+extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* resid, float* stats,
+                             const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
+  BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
+  const int grid = zoo_c3_grid(g, epi, &bs);
+  if (grid <= 0) return hipErrorNotSupported;
+  C3Geom c;
+  c3_geom(*g, c);
+  c.partial = g->stat_slots == kStatPartial ? 1 : 0;
+
+  if (g->stat_slots > 0) return hipErrorInvalidValue;  // direct atomics or partial rows only
+  const size_t smem = (size_t)c.RR * c.PW2 * 128 + C3_EPI_BYTES;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<1>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<2>), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        160 * 1024);
+    attr = true;
+  }
+  static const bool stamp = getenv("ZOO_C3_STAMPS") != nullptr;
+  if (stamp) {  // diagnostic build: per-segment cycle sums into a buffer read by zoo_c3_stamps
+    static bool sattr = false;
+    if (!sattr) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<1, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<2, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      sattr = true;
+    }
+    if (!g_c3_stamps) hipMalloc(&g_c3_stamps, 4096 * 4 * 5 * sizeof(unsigned long long));
+    g_c3_stamp_grid = grid;
+    c.stamps = g_c3_stamps;
+    if (epi == 1)
+      hipLaunchKernelGGL((c3_kernel<1, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
+                         (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+    else
+      hipLaunchKernelGGL((c3_kernel<2, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
+                         (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+    return hipGetLastError();
+  }
+  if (epi == 1)
+    hipLaunchKernelGGL(c3_kernel<1>, dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
+                       (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+  else
+    hipLaunchKernelGGL(c3_kernel<2>, dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
+                       (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+  return hipGetLastError();
+}

@@ -28,6 +28,9 @@ struct ConvGeom {
   // each workgroup STORES its column sums into row tm, and zoo_stats_part_finalize
   // folds the rows in a fixed order (deterministic, contention-free)
   int stat_slots;
+  // experiment bits (igemm2 band tiles, ZOO_I2_DBG; 0 in production): 1 = no MFMA, 2 = no
+  // epilogue stores, 4 = no B staging in the loop, 8 = no A fragment reads
+  int dbg;
 };
 
 // Fused BatchNorm-backward statistics in a dgrad epilogue: the conv computing

@@ -806,9 +806,18 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
 extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st);
 
+extern "C" int zoo_c3_grid(const ConvGeom* g, int epi, const BwdStats* bs);
+extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* resid, float* stats,
+                             const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st);
+
 extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
+  {
+    // stride-1 3x3 64 -> 64 channel convs (ResNet stage 1): the persistent streaming kernel (c3.hip)
+    const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats);
+    if (zoo_c3_grid(g, epi, bsp) > 0) return zoo_c3(X, W, Y, resid, stats, g, epi, bsp, st);
+  }
   {
     // memory-bound 1x1 shapes: the persistent streaming kernel (pw.hip)
     const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats);

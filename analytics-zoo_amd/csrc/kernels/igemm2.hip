@@ -68,17 +68,29 @@ struct I2Cfg {
   static constexpr int STAGE_BYTES = (BM + BN) * 128;
   static constexpr int EPI_PITCH = WTN + 4;  // fp32 patch pitch (16-byte aligned rows)
   static constexpr int EPI_BYTES = NW * 16 * EPI_PITCH * 4 + NWM * BN * 2 * 4;
-  static_assert(A_PW * 8 * NW == BM && B_PW * 8 * NW == BN, "tile rows must split into 8-row DMA groups");
+  static_assert(B_PW * 8 * NW == BN, "B tile rows must split into 8-row DMA groups");
 };
 
-template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1, int EPI>
-__global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
+// A-operand modes: I2_AM_IMPLICIT stages BM im2col rows per K-tile (any tap geometry);
+// I2_AM_1X1 the same rows of a 1x1 conv / GEMM; I2_AM_BAND (stride-1 3x3, pad 1) stages the
+// block's input rows ONCE per 64-channel slice -- a band of TP = BM / Q output rows of one
+// image needs (TP + 2) x (Q + 2) halo pixels -- and reads all nine taps' A fragments from that
+// LDS patch, so each activation line is fetched ~1.3x instead of 9x per conv (the small-channel
+// ResNet stage-1/2 3x3 convs, which the per-tap gather left L2/LDS-DMA bound at ~300 TF/s).
+// Slice s+1's patch streams into the second patch buffer during slice s's K-tiles.
+enum I2AMode : int { I2_AM_IMPLICIT = 0, I2_AM_1X1 = 1, I2_AM_BAND = 2 };
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, int AM, int EPI>
+__global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igemm2_kernel(
     const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wm, bf16_t* __restrict__ Y, float* __restrict__ Yf,
     const float* __restrict__ bias, const bf16_t* __restrict__ resid, float* __restrict__ stats, ConvGeom g, int act,
     BwdStats bs) {
   using Cfg = I2Cfg<NWM, NWN, TM, TN>;
   constexpr int NW = Cfg::NW, WTM = Cfg::WTM, WTN = Cfg::WTN, BM = Cfg::BM, BN = Cfg::BN;
   constexpr int A_PW = Cfg::A_PW, B_PW = Cfg::B_PW, DPT = Cfg::DPT, SB = Cfg::STAGE_BYTES;
+  constexpr bool IS1x1 = AM == I2_AM_1X1;
+  constexpr bool BAND = AM == I2_AM_BAND;
+  static_assert(BAND || A_PW * 8 * NW == BM, "A tile rows must split into 8-row DMA groups");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -88,16 +100,58 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
   const int ntn = (g.K + BN - 1) / BN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tm = bid / ntn, tn = bid - tm * ntn;
-  const int m0 = tm * BM, n0 = tn * BN;
+  const int PQ = g.P * g.Q;
+  // band mode: m-tile tm = (image, band of TP output rows); rows of the next image are not ours
+  const int TP = BAND ? BM / g.Q : 0;
+  const int nbands = BAND ? (g.P + TP - 1) / TP : 1;
+  const int b_img = BAND ? tm / nbands : 0;
+  const int b_p0 = BAND ? (tm - b_img * nbands) * TP : 0;
+  const int m0 = BAND ? b_img * PQ + b_p0 * g.Q : tm * BM, n0 = tn * BN;
+  const int mlim = BAND ? min(g.M, b_img * PQ + PQ) : g.M;
   const int nk = g.Ktot >> 6;  // C % 64 == 0: one 64-deep K-tile per (tap, 64-channel slice)
 
   // ---- staging assignment: lane -> row lr of each 8-row group, global 16-byte chunk gc ----
   const int lr = lane >> 3;
   const int gc = (lane & 7) ^ lr;  // XOR swizzle through the source (LDS image lane-linear)
-  const int PQ = g.P * g.Q;
+
+  // band geometry: patch row pr = pi * PW2 + pj holds input pixel (b_p0 - 1 + pi, pj - 1);
+  // a slice buffer is PROWS (multiple of 8) rows x 128 B; then the B ring, then a 1 KiB junk
+  // slot per wave for DMA pieces past the patch end (keeps every wave's vmcnt count uniform)
+  const int PW2 = g.Q + 2;
+  const int prow_n = BAND ? (TP + 2) * PW2 : 0;
+  const int npiece = (prow_n + 7) >> 3;
+  const int nslice = g.C >> 6;
+  const int pbytes = npiece * 1024;
+  const int bring = BAND ? (nslice > 1 ? 2 : 1) * pbytes : 0;  // B ring offset
+  char* const junk = smem + bring + STAGES * BN * 128 + w * 1024;
+  auto stage_piece = [&](int j, int cs, int buf) {
+    const bf16_t* src = i2_zero_page;
+    char* dst = junk;
+    if (j < npiece) {
+      const int pr = j * 8 + lr;
+      const int pi = pr / PW2, pj = pr - pi * PW2;
+      const int ih = b_p0 - 1 + pi, iw = pj - 1;
+      if (pr < prow_n && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+        src = X + (((size_t)b_img * g.H + ih) * g.W + iw) * g.C + cs * 64 + gc * 8;
+      dst = smem + buf * pbytes + j * 1024;
+    }
+    __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)dst, 16, 0, 0);
+  };
+  // per lane: patch row of its pixel's window origin for each of its TM row tiles
+  int a_pb[BAND ? TM : 1];
+  if constexpr (BAND) {
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int t = wm * WTM + i * 16 + (lane & 15);  // < BM = TP * Q
+      const int pp = t / g.Q;
+      a_pb[i] = pp * PW2 + (t - pp * g.Q);
+    }
+  }
+
   int a_base[A_PW], a_ih[A_PW], a_iw[A_PW];
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
+    if constexpr (BAND) break;
     const int m = m0 + (i * NW + w) * 8 + lr;
     const bool ok = m < g.M;
     if constexpr (IS1x1) {
@@ -121,6 +175,19 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
 
   // tap decode of the NEXT tile to stage (wave-uniform)
   int st_r = 0, st_s = 0, st_c = 0, st_k = 0;
+  // band mode: K-tiles run slice-major (all nine taps of 64-channel slice 0, then slice 1, ...)
+  // so one patch slice serves nine consecutive tiles; weights are [K][tap][C]
+  int sb_tap = 0, sb_cs = 0;
+  auto stage_b = [&](int buf) {
+    char* sb = smem + bring + buf * (BN * 128) + w * 1024;
+    const int koff = sb_tap * g.C + sb_cs * 64;
+#pragma unroll
+    for (int i = 0; i < B_PW; ++i) {
+      const bf16_t* src = b_src[i] ? b_src[i] + koff : i2_zero_page;
+      __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)(sb + i * NW * 1024), 16, 0, 0);
+    }
+    if (++sb_tap == 9) { sb_tap = 0; ++sb_cs; }
+  };
   auto stage = [&](int buf) {
     char* sa = smem + buf * SB + w * 1024;
     char* sb = smem + buf * SB + BM * 128 + w * 1024;
@@ -183,16 +250,85 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
 
   };
+  // band mode: A fragments from the patch slice `pbuf` at tap offset toff (patch rows); the
+  // chunk XOR uses the patch row actually addressed (rows are stored swizzled by their own index)
+  auto compute_band = [&](int buf, int pbuf, int toff) {
+    const char* pa = smem + pbuf * pbytes;
+    const char* bb = smem + bring + buf * (BN * 128) + (wn * WTN) * 128 + rl;
+    bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int co = kk ? co1 : co0;
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bfr[kk][j] = *reinterpret_cast<const bf16x8*>(bb + j * 2048 + co);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int pr = a_pb[i] + toff;
+        af[kk][i] = *reinterpret_cast<const bf16x8*>(pa + pr * 128 + (((kk * 4 + (lane >> 4)) ^ (pr & 7)) << 4));
+      }
+    }
+    // every fragment read is issued before the first MFMA (counted lgkmcnt waits then retire
+    // them in order); left alone, hipcc recycles 3-4 fragment registers and drains the LDS
+    // queue (lgkmcnt(0)) every 2-4 MFMAs, exposing the LDS latency ~7x per K-tile
+    __builtin_amdgcn_sched_barrier(0);
+    if (g.dbg & 1) return;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16(af[kk][i], bfr[kk][j], acc[i][j]);
+  };
 
   // ---- main loop ----
+  if constexpr (BAND) {
+    // prologue: patch slice 0 (all waves, junk-padded to a uniform count), then B tiles
+    const int rounds0 = (npiece + NW - 1) / NW;
+    for (int r = 0; r < rounds0; ++r) stage_piece(r * NW + w, 0, 0);
+#pragma unroll
+    for (int s = 0; s < STAGES - 1; ++s)
+      if (s < nk) stage_b(s);
+    if (STAGES == 3 && nk > 1) i2_wait_vm<B_PW>();
+    else i2_wait_vm<0>();
+    __builtin_amdgcn_s_barrier();
+    int cbuf = 0, sbuf = STAGES - 1;
+    int cs = 0, tap = 0, toff = 0, tr = 0, tsc = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool issue = kt + STAGES - 1 < nk && !(g.dbg & 4);
+      if (issue) stage_b(sbuf);
+      // slice cs+1 streams in during taps 0..7 of slice cs (one piece per wave per tap; the
+      // wait at the end of tap 8 sees the last of them land before slice cs+1 is read)
+      const bool piece = cs + 1 < nslice && tap < 8 && tap * NW < npiece;
+      if (piece) stage_piece(tap * NW + w, cs + 1, (cs + 1) & 1);
+      if (!(g.dbg & 8)) compute_band(cbuf, cs & 1, toff);
+      if constexpr (STAGES == 3) {
+        if (issue) {
+          if (piece) i2_wait_vm<B_PW + 1>(); else i2_wait_vm<B_PW>();
+        } else {
+          if (piece) i2_wait_vm<1>(); else i2_wait_vm<0>();
+        }
+      } else {
+        i2_wait_vm<0>();
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      cbuf = cbuf + 1 == STAGES ? 0 : cbuf + 1;
+      sbuf = sbuf + 1 == STAGES ? 0 : sbuf + 1;
+      if (++tap == 9) { tap = 0; ++cs; tr = 0; tsc = 0; toff = 0; }
+      else if (++tsc == 3) { tsc = 0; ++tr; toff = tr * PW2; }
+      else ++toff;
+    }
+  }
+  int cbuf = 0, sbuf = STAGES - 1;
+  if constexpr (!BAND) {
 #pragma unroll
   for (int s = 0; s < STAGES - 1; ++s)
     if (s < nk) stage(s);
   if (STAGES == 3 && nk > 1) i2_wait_vm<DPT>();
   else i2_wait_vm<0>();
   __builtin_amdgcn_s_barrier();
-  int cbuf = 0, sbuf = STAGES - 1;
-  for (int kt = 0; kt < nk; ++kt) {
+  }
+  for (int kt = 0; kt < (BAND ? 0 : nk); ++kt) {
     const bool issue = kt + STAGES - 1 < nk;
     if (issue) stage(sbuf);
     compute(cbuf);
@@ -259,7 +395,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
   auto slice_off = [&](int i, int h, bool& ok) -> size_t {
     const int prow = (lane + 64 * h) / CPR;
     const int m = m0 + wm * WTM + i * 16 + prow;
-    ok = m < g.M && col_ok;
+    ok = m < mlim && col_ok;
     if (!ok) return 0;
     if (g.omap) {
       const int n = m / PQ, pq = m - n * PQ;
@@ -313,7 +449,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
       const int m = m0 + wm * WTM + i * 16 + prow;
       const float4 lo = *reinterpret_cast<const float4*>(patch + prow * PITCH + ch * 8);
       const float4 hi = *reinterpret_cast<const float4*>(patch + prow * PITCH + ch * 8 + 4);
-      if (m >= g.M || !col_ok) continue;
+      if (m >= mlim || !col_ok) continue;
       float v[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
       size_t off;
       if (EPI != 1 && EPI != 3 && g.omap) {
@@ -337,7 +473,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, 2) void igemm2_kernel(
         *reinterpret_cast<uint4*>(Y + off) = pack8(v);
       } else if constexpr (EPI == 1) {
         const uint4 pk = pack8(v);
-        *reinterpret_cast<uint4*>(Y + off) = pk;
+        if (!(BAND && (g.dbg & 2))) *reinterpret_cast<uint4*>(Y + off) = pk;
         if (want_stats) {
           float q[8];
           unpack8(pk, q);
@@ -474,10 +610,17 @@ enum I2Tile : int {
   I2_256x256 = 5,   // 8 waves (2x4) of 128x64, 2-stage: 128 KiB, 1 / CU
   I2_128x64 = 6,    // 4 waves (2x2) of 64x32, 3-stage: 72 KiB, 2 / CU
   I2_128x128_3 = 7, // 4 waves (2x2) of 64x64, 3-stage: 96 KiB, 1 / CU
+  // band mode (I2_AM_BAND, 224 = 4 x 56 or 8 x 28 output pixels; LDS = patch slice(s) + B ring)
+  I2_B224x64 = 8,   // 4 waves (2x2) of 112x32, 3-stage: 45 KiB patch + 24 KiB ring, 2 / CU
+  I2_B224x128 = 9,  // 8 waves (2x4) of 112x32, 3-stage: 2 x 38 KiB patches + 48 KiB ring, 1 / CU
+  I2_B224x128w = 10,// 4 waves (2x2) of 112x64, 3-stage (A/B of the wider wave tile)
 };
+
+static bool i2_is_band(int tile) { return tile >= I2_B224x64; }
 
 static int g_i2_mode = -1;  // -1: unset (read ZOO_IGEMM2), 0: off, 1: on
 static int g_i2_tile = -1;  // -1: unset (read ZOO_IGEMM2_TILE), 0 auto, else I2Tile
+static int g_i2_band = -1;  // -1: unset (read ZOO_I2_BAND), 0: off, 1: on
 
 static int i2_mode() {
   if (g_i2_mode < 0) {
@@ -493,67 +636,145 @@ static int i2_tile_force() {
   }
   return g_i2_tile;
 }
-
-template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1, int EPI>
-static hipError_t i2_launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
-                            const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
-                            hipStream_t st) {
-  using Cfg = I2Cfg<NWM, NWN, TM, TN>;
-  const int tiles = ((g.M + Cfg::BM - 1) / Cfg::BM) * ((g.K + Cfg::BN - 1) / Cfg::BN);
-  size_t smem = (size_t)STAGES * Cfg::STAGE_BYTES;
-  if (smem < (size_t)Cfg::EPI_BYTES) smem = Cfg::EPI_BYTES;
-  auto kfn = &igemm2_kernel<NWM, NWN, TM, TN, STAGES, IS1x1, EPI>;
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-    attr_set = true;
+static int i2_band_mode() {
+  if (g_i2_band < 0) {
+    const char* e = getenv("ZOO_I2_BAND");
+    g_i2_band = e ? atoi(e) : 1;
   }
-  hipLaunchKernelGGL(kfn, dim3(tiles), dim3(Cfg::NT), smem, st, X, W, Y, Yf, bias, resid, stats, g, act, bs);
-  return hipGetLastError();
-}
-
-template <int NWM, int NWN, int TM, int TN, int STAGES, bool IS1x1>
-static hipError_t i2_epi(int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
-                         const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
-                         hipStream_t st) {
-  if (epi == 1) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  if (epi == 2) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 2>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  if (epi == 3) return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 3>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-  return i2_launch<NWM, NWN, TM, TN, STAGES, IS1x1, 0>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-}
-
-template <bool IS1x1>
-static hipError_t i2_tile(int tile, int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf,
-                          const float* bias, const bf16_t* resid, float* stats, const ConvGeom& g, int act,
-                          const BwdStats& bs, hipStream_t st) {
-  switch (tile) {
-    case I2_128x128: return i2_epi<2, 2, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_256x128: return i2_epi<4, 2, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_256x128_3: return i2_epi<4, 2, 4, 4, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_256x64: return i2_epi<4, 1, 4, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_256x256: return i2_epi<2, 4, 8, 4, 2, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_128x64: return i2_epi<2, 2, 4, 2, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    case I2_128x128_3: return i2_epi<2, 2, 4, 4, 3, IS1x1>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
-    default: return hipErrorInvalidValue;
-  }
+  return g_i2_band;
 }
 
 static int i2_bm(int tile) {
   switch (tile) {
     case I2_128x128: case I2_128x64: case I2_128x128_3: return 128;
+    case I2_B224x64: case I2_B224x128: case I2_B224x128w: return 224;
     default: return 256;
   }
 }
 static int i2_bn(int tile) {
   switch (tile) {
-    case I2_256x64: case I2_128x64: return 64;
+    case I2_256x64: case I2_128x64: case I2_B224x64: return 64;
     case I2_256x256: return 256;
     default: return 128;
   }
 }
+static int i2_nw(int tile) {
+  switch (tile) {
+    case I2_256x128: case I2_256x128_3: case I2_256x256: case I2_B224x128: return 8;
+    default: return 4;
+  }
+}
+
+// band geometry of a tile on this conv: rows per band, bands per image, LDS patch slice bytes
+struct I2Band {
+  int tp, nbands, pbytes;
+};
+static I2Band i2_band_geom(const ConvGeom& g, int bm) {
+  I2Band b;
+  b.tp = bm / g.Q;
+  b.nbands = (g.P + b.tp - 1) / b.tp;
+  b.pbytes = (((b.tp + 2) * (g.Q + 2) + 7) / 8) * 1024;
+  return b;
+}
+
+// m-tiles of a tile on this conv (band tiles: images x bands)
+static long i2_tiles_m(const ConvGeom& g, int tile) {
+  if (i2_is_band(tile)) return (long)g.N * i2_band_geom(g, i2_bm(tile)).nbands;
+  return (g.M + i2_bm(tile) - 1) / i2_bm(tile);
+}
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, int AM, int EPI>
+static hipError_t i2_launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                            const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
+                            hipStream_t st) {
+  using Cfg = I2Cfg<NWM, NWN, TM, TN>;
+  const int ntn = (g.K + Cfg::BN - 1) / Cfg::BN;
+  long tiles;
+  size_t smem;
+  if constexpr (AM == I2_AM_BAND) {
+    const I2Band b = i2_band_geom(g, Cfg::BM);
+    tiles = (long)g.N * b.nbands * ntn;
+    smem = (size_t)(g.C > 64 ? 2 : 1) * b.pbytes + (size_t)STAGES * Cfg::BN * 128 + (size_t)Cfg::NW * 1024;
+  } else {
+    tiles = (long)((g.M + Cfg::BM - 1) / Cfg::BM) * ntn;
+    smem = (size_t)STAGES * Cfg::STAGE_BYTES;
+  }
+  if (smem < (size_t)Cfg::EPI_BYTES) smem = Cfg::EPI_BYTES;
+  if (smem > 160 * 1024) return hipErrorInvalidValue;
+  auto kfn = &igemm2_kernel<NWM, NWN, TM, TN, STAGES, AM, EPI>;
+  static bool attr_set = false;
+  if (!attr_set) {
+    // band smem depends on the conv's width: allow the whole LDS once
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        AM == I2_AM_BAND ? 160 * 1024 : (int)smem);
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3((unsigned)tiles), dim3(Cfg::NT), smem, st, X, W, Y, Yf, bias, resid, stats, g, act, bs);
+  return hipGetLastError();
+}
+
+template <int NWM, int NWN, int TM, int TN, int STAGES, int AM>
+static hipError_t i2_epi(int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
+                         const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
+                         hipStream_t st) {
+  if (epi == 1) return i2_launch<NWM, NWN, TM, TN, STAGES, AM, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if (epi == 2) return i2_launch<NWM, NWN, TM, TN, STAGES, AM, 2>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  if constexpr (AM != I2_AM_BAND) {
+    if (epi == 3) return i2_launch<NWM, NWN, TM, TN, STAGES, AM, 3>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+  }
+  return i2_launch<NWM, NWN, TM, TN, STAGES, AM, 0>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+}
+
+template <int AM>
+static hipError_t i2_tile(int tile, int epi, const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf,
+                          const float* bias, const bf16_t* resid, float* stats, const ConvGeom& g, int act,
+                          const BwdStats& bs, hipStream_t st) {
+  if constexpr (AM == I2_AM_BAND) {
+    switch (tile) {
+      case I2_B224x64: return i2_epi<2, 2, 7, 2, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_B224x128: return i2_epi<2, 4, 7, 2, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_B224x128w: return i2_epi<2, 2, 7, 4, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    switch (tile) {
+      case I2_128x128: return i2_epi<2, 2, 4, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_256x128: return i2_epi<4, 2, 4, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_256x128_3: return i2_epi<4, 2, 4, 4, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_256x64: return i2_epi<4, 1, 4, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_256x256: return i2_epi<2, 4, 8, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_128x64: return i2_epi<2, 2, 4, 2, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_128x128_3: return i2_epi<2, 2, 4, 4, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      default: return hipErrorInvalidValue;
+    }
+  }
+}
+
+// band tile for a stride-1 3x3 conv (pad 1, no dilation, same-size output), or 0: the output
+// width must divide the 224-pixel tile into whole rows with bands no taller than the image
+// (Q = 56 -> 4 rows, Q = 28 -> 8 rows), the LDS patch + ring must fit, and each of the 8 DMA
+// rounds of a slice must cover its patch (npiece <= 8 * waves)
+static int i2_band_choose(const ConvGeom& g, int epi) {
+  if (!i2_band_mode()) return 0;
+  if (!(g.R == 3 && g.S == 3 && g.sh == 1 && g.sw == 1 && g.ph == 1 && g.pw == 1 && g.dh == 1 && g.dw == 1 &&
+        g.lh == 1 && g.lw == 1 && g.H == g.P && g.W == g.Q && !g.omap && g.C % 64 == 0 && g.Q > 0))
+    return 0;
+  if (epi == 3 || epi == 4) return 0;
+  if (224 % g.Q != 0 || 224 / g.Q > g.P) return 0;
+  static const int forced = [] {
+    const char* e = getenv("ZOO_I2_BAND_TILE");
+    return e ? atoi(e) : 0;
+  }();
+  const int t = forced >= I2_B224x64 ? forced : (g.K <= 64 ? I2_B224x64 : I2_B224x128);
+  const I2Band b = i2_band_geom(g, 224);
+  const size_t smem = (size_t)(g.C > 64 ? 2 : 1) * b.pbytes + 3 * (size_t)i2_bn(t) * 128 + (size_t)i2_nw(t) * 1024;
+  if (smem > 160 * 1024 || (g.C > 64 && b.pbytes / 1024 > 8 * i2_nw(t))) return 0;
+  return t;
+}
 
 // shape + epilogue -> tile, or 0 = "leave it to igemm.hip" (tools/igemm2_bench.py on the
 // ResNet-50 b256 convs with the model's own epilogues, round 3, profiles/r3/igemm2_r3.md):
+//   * stride-1 3x3 convs over 56- or 28-wide maps: the band tiles (patch reuse of the 9 taps);
 //   * N (output channels) < 256: igemm.hip's 128x{64,128} tiles are as fast or faster;
 //   * a short reduction (Ktot < 256 forward, < 1024 for the BN-backward epilogue) is bound by
 //     the epilogue, where igemm.hip's row-pointer epilogues win (the GELU-backward form of EPI 2,
@@ -561,9 +782,11 @@ static int i2_bn(int tile) {
 //     16384x3072x768 FFN dgrad, profiles/r3/bert_base_train_b128_r3.md);
 //   * otherwise 256x256 (8 waves of 128x64) while >= 160 tiles fill the chip, else 128x128.
 static int i2_choose(const ConvGeom& g, int epi) {
+  const int bt = i2_band_choose(g, epi);
+  if (bt > 0) return bt;
   const int f = i2_tile_force();
-  if (f > 0) return f;
-  auto tiles = [&](int t) { return (long)((g.M + i2_bm(t) - 1) / i2_bm(t)) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
+  if (f > 0 && !i2_is_band(f)) return f;
+  auto tiles = [&](int t) { return i2_tiles_m(g, t) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
   if (g.K < 256) return 0;
   if (epi == 4) {
     // GELU-backward dgrad (BERT FFN): ZOO_I2_GELU_TILE picks its tile (A/B of the 128x128
@@ -592,16 +815,26 @@ extern "C" int zoo_igemm2_eligible(const ConvGeom* g, int epi) {
          g->Ktot == g->R * g->S * g->C && g->ldb >= g->Ktot && i2_choose(*g, epi) > 0;
 }
 
-// m-tile height the dispatcher will use for this geometry and epilogue (partial-statistics
-// buffers are [ceil(M / bm)][2K]); 0 = not taken by igemm2
+// m-tile height the dispatcher will use for this geometry and epilogue; 0 = not taken by igemm2
 extern "C" int zoo_igemm2_bm(const ConvGeom* g, int epi) {
   if (!zoo_igemm2_eligible(g, epi)) return 0;
   return i2_bm(i2_choose(*g, epi));
 }
 
+// number of m-tiles (rows of a partial-statistics buffer [tiles_m][2K]); 0 = not taken by igemm2
+extern "C" int zoo_igemm2_tiles_m(const ConvGeom* g, int epi) {
+  if (!zoo_igemm2_eligible(g, epi)) return 0;
+  return (int)i2_tiles_m(*g, i2_choose(*g, epi));
+}
+
 extern "C" void zoo_igemm2_set(int mode, int tile) {
   if (mode >= 0) g_i2_mode = mode;
   if (tile >= 0) g_i2_tile = tile;
+}
+
+// band tiles on / off (-1: leave)
+extern "C" void zoo_igemm2_band_set(int on) {
+  if (on >= 0) g_i2_band = on;
 }
 
 extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Yf, const float* bias,
@@ -616,7 +849,17 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
   const int tile = i2_choose(*g, route);
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
+  if (i2_is_band(tile)) {
+    static const int dbg = [] {
+      const char* e = getenv("ZOO_I2_DBG");
+      return e ? atoi(e) : 0;
+    }();
+    ConvGeom gb = *g;
+    gb.dbg = dbg;
+    return i2_tile<I2_AM_BAND>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, gb, act, bs, st);
+  }
   if (is1x1)
-    return i2_tile<true>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
-  return i2_tile<false>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
+    return i2_tile<I2_AM_1X1>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
+  return i2_tile<I2_AM_IMPLICIT>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs,
+                                 st);
 }

@@ -31,6 +31,11 @@ hipError_t zoo_ncf(const zoo::NcfArgs*, float* const*, int, hipStream_t);
 hipError_t zoo_igemm(const void*, const void*, void*, float*, const float*, const void*, float*, const ConvGeom*, int,
                      const zoo::BwdStats*, hipStream_t);
 int zoo_igemm2_bm(const ConvGeom*, int);
+int zoo_igemm2_tiles_m(const ConvGeom*, int);
+void zoo_igemm2_band_set(int);
+int zoo_c3_grid(const ConvGeom*, int, const zoo::BwdStats*);
+void zoo_c3_set(int);
+int zoo_c3_stamps(unsigned long long*, int);
 void zoo_igemm2_set(int, int);
 int zoo_pw_eligible(const ConvGeom*, int, const zoo::BwdStats*);
 void zoo_pw_set(int);
@@ -352,8 +357,10 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   const int epi = zoo::igemm_epi(out_bf16, out_f32, bp != nullptr, rp != nullptr, act, g.omap != 0,
                                  bs.sums != nullptr, sp != nullptr);
   const int route = zoo::igemm_route_epi(epi, bs.zgelu != 0);
-  const int bm = zoo_igemm2_bm(&g, route) > 0 ? zoo_igemm2_bm(&g, route) : 128;
-  const int tiles_m = (g.M + bm - 1) / bm;
+  // persistent 3x3 kernel (c3.hip): one statistics row per workgroup
+  const int c3_grid = zoo_c3_grid(&g, epi, &bs);
+  const int i2_tm = c3_grid > 0 ? 0 : zoo_igemm2_tiles_m(&g, route);
+  const int tiles_m = c3_grid > 0 ? c3_grid : i2_tm > 0 ? i2_tm : (g.M + 127) / 128;
   // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
   // the atomics go straight into the final 2K floats, no slot fold launch needed
   static const int slot_min_tiles = [] {
@@ -363,7 +370,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   if (g.stat_slots == zoo::kStatSlots && tiles_m <= slot_min_tiles) g.stat_slots = 0;
   // the persistent 1x1 kernel (pw.hip) adds each workgroup's sums once (~256 adders per address):
   // straight into the final 2K floats, no slot fold
-  if (g.stat_slots > 0 && !stats_partial() && zoo_pw_eligible(&g, route, &bs)) g.stat_slots = 0;
+  if (g.stat_slots > 0 && !stats_partial() && (zoo_pw_eligible(&g, route, &bs) || c3_grid > 0)) g.stat_slots = 0;
   if (stat_dst && stats_partial()) {
     part = torch::empty({(int64_t)tiles_m, 2 * (int64_t)K}, x.options().dtype(at::kFloat));
     g.stat_slots = zoo::kStatPartial;
@@ -2601,6 +2608,23 @@ PYBIND11_MODULE(_C, m) {
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
         "igemm2 A/B switch: mode 0 off / 1 on (-1 keep), tile 0 auto / I2Tile id (-1 keep)");
+  m.def("c3_grid_for", [](int N, int H, int W) {
+          ConvGeom g{};
+          g.N = N; g.H = H; g.W = W; g.C = 64; g.K = 64; g.R = 3; g.S = 3; g.sh = 1; g.sw = 1; g.ph = 1; g.pw = 1;
+          g.dh = 1; g.dw = 1; g.lh = 1; g.lw = 1; g.P = H; g.Q = W; g.M = N * H * W; g.Ktot = 576; g.ldb = 576;
+          return zoo_c3_grid(&g, 1, nullptr);
+        }, "workgroups the persistent 3x3 kernel would use for an N x H x W x 64 forward (0: not eligible)");
+  m.def("c3_stamps", []() {
+          std::vector<unsigned long long> v(4096 * 4 * 5);
+          const int n = zoo_c3_stamps(v.data(), (int)v.size());
+          v.resize(n > 0 ? n : 0);
+          return v;
+        }, "diagnostic build (ZOO_C3_STAMPS=1): per-workgroup, per-wave cycle sums of the band segments "
+           "(row prefetch, MFMA taps, epilogue, wait+barrier, band count) of the last c3 launch");
+  m.def("c3_set", [](int on) { zoo_c3_set(on); },
+        "persistent 3x3 64-channel conv kernel (c3.hip): 1 on, 0 off, -1 back to ZOO_C3");
+  m.def("igemm2_band_set", [](int on) { zoo_igemm2_band_set(on); },
+        "igemm2 band tiles (stride-1 3x3 convs from an LDS halo patch): 1 on, 0 off, -1 keep");
   m.def("set_deterministic", [](bool on) { g_deterministic = on; });
   m.def("get_deterministic", []() { return g_deterministic; });
   m.def("set_reduce_modes", [](bool stats_part, bool wgrad_part) {

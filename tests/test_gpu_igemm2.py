@@ -139,3 +139,88 @@ def test_igemm2_linear_shapes(C2, gpu):
         y = _kern.conv_fwd(x, w, 1, 1, bias=b, act=2)
         ref = F.gelu(x.float().view(M, K) @ w.float().t() + b)
         assert rel(y.view(M, Nn), ref) < 1e-2, tile
+
+
+# ---- band tiles (stride-1 3x3 convs read from an LDS halo patch, igemm2.hip I2_AM_BAND) ----
+BAND_SHAPES = [
+    # N, H, W, Cin, Cout: 56-wide (4-row bands) and 28-wide (8-row bands, last band partial at
+    # H = 28 / 20), one and two 64-channel slices, Cout below / above / not a multiple of the tile
+    (2, 56, 56, 64, 64),
+    (3, 28, 28, 128, 128),
+    (2, 28, 28, 64, 128),
+    (2, 20, 28, 128, 72),
+    (1, 28, 28, 128, 256),
+    (2, 56, 56, 64, 200),
+]
+
+
+@pytest.fixture
+def Cband(gpu):
+    from zoo.ops import native
+    C = native()
+    yield C
+    C.igemm2_band_set(1)
+    C.igemm2_set(1, 0)
+
+
+@pytest.mark.parametrize("shape", BAND_SHAPES)
+def test_igemm2_band_fwd_stats(Cband, gpu, shape):
+    N, H, W, Cin, Cout = shape
+    torch.manual_seed(0)
+    x = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
+    w4 = (torch.randn(Cout, 3, 3, Cin, device=gpu) / math.sqrt(9 * Cin)).bfloat16()
+    w2 = w4.reshape(Cout, -1).contiguous()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w4.float().permute(0, 3, 1, 2), padding=1).permute(0, 2, 3, 1)
+    Cband.igemm2_band_set(1)
+    stats = torch.zeros(2 * Cout, device=gpu)
+    y = Cband.conv_fwd(x, w2, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, None, None, stats, 0, False, True, 0, 0, None, [],
+                       None, None, None, None, None)
+    assert rel(y, ref) < 1e-2
+    yf = y.float()
+    assert rel(stats, torch.cat([yf.sum((0, 1, 2)), (yf * yf).sum((0, 1, 2))])) < 1e-3
+    # same conv with the band tiles off (per-tap gather): agrees to bf16 rounding
+    Cband.igemm2_band_set(0)
+    y0 = Cband.conv_fwd(x, w2, 3, 3, 1, 1, 1, 1, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0, None, [],
+                        None, None, None, None, None)
+    assert rel(y, y0) < 1e-2
+
+
+@pytest.mark.parametrize("shape", [(2, 56, 56, 64, 64), (2, 28, 28, 128, 128), (2, 20, 28, 128, 64)])
+@pytest.mark.parametrize("zmode", ["z", "affine", "bits"])
+def test_igemm2_band_dgrad_fused_bn_backward(Cband, gpu, shape, zmode):
+    """Stride-1 3x3 dX through the band tiles with the BN-backward epilogue (residual-gradient
+    add, producer ReLU mask from z / from y and the producer affine / from a bit mask)."""
+    from zoo.ops import _kern
+    N, H, W, Cin, Cout = shape
+    torch.manual_seed(1)
+    y_pre = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
+    mean = y_pre.float().mean((0, 1, 2))
+    inv = torch.rsqrt(y_pre.float().var((0, 1, 2), unbiased=False) + 1e-5)
+    gamma = torch.rand(Cin, device=gpu) + 0.5
+    beta = torch.randn(Cin, device=gpu) * 0.1
+    pre = (y_pre.float() - mean) * inv * gamma + beta
+    z = torch.relu(pre).bfloat16()
+    w4 = (torch.randn(Cout, 3, 3, Cin, device=gpu) / math.sqrt(9 * Cin)).bfloat16()
+    w2 = w4.reshape(Cout, -1).contiguous()
+    dy = torch.randn(N, H, W, Cout, device=gpu).bfloat16()
+    resid = torch.randn(N, H, W, Cin, device=gpu).bfloat16() if zmode != "affine" else None
+    zr = z.float().permute(0, 3, 1, 2).requires_grad_(True)
+    F.conv2d(zr, w4.float().permute(0, 3, 1, 2), padding=1).backward(dy.float().permute(0, 3, 1, 2))
+    dz = zr.grad.permute(0, 2, 3, 1) + (resid.float() if resid is not None else 0.0)
+    keep = (pre > 0) if zmode == "affine" else (z.float() > 0)
+    ref = dz * keep
+    sums = torch.zeros(2 * Cin, device=gpu)
+    if zmode == "z":
+        bst = (z, y_pre, mean.contiguous(), inv.contiguous(), sums)
+    elif zmode == "affine":
+        bst = (None, y_pre, mean.contiguous(), inv.contiguous(), sums, gamma, beta)
+    else:
+        bits = (z.view(-1, 8) > 0).to(torch.uint8)
+        packed = (bits << torch.arange(8, device=gpu, dtype=torch.uint8)).sum(1).to(torch.uint8)
+        bst = (packed.contiguous(), y_pre, mean.contiguous(), inv.contiguous(), sums)
+    Cband.igemm2_band_set(1)
+    out = _kern.conv_dgrad(dy, w2, Cout, 3, 3, Cin, H, W, (1, 1), (1, 1), resid=resid, bstats=bst)
+    assert rel(out, ref) < 1e-2
+    q = out.float()
+    xhat = (y_pre.float() - mean) * inv
+    assert rel(sums, torch.cat([q.sum((0, 1, 2)), (q * xhat).sum((0, 1, 2))])) < 2e-3
