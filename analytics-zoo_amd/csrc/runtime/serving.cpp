@@ -19,6 +19,7 @@
 #include <sys/socket.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
@@ -252,10 +253,31 @@ class Store {
     return out;
   }
 
+  // latency tracking for the load generator: finish() stamps every result key it writes
+  void track(bool on) {
+    std::lock_guard<std::mutex> g(mu_);
+    track_ = on;
+    done_.clear();
+  }
+  // completion stamps (steady-clock ns, -1 = not finished) of `keys`, under one lock
+  void done_times(const std::vector<std::string>& keys, std::vector<long long>* out) {
+    std::lock_guard<std::mutex> g(mu_);
+    out->resize(keys.size());
+    for (size_t i = 0; i < keys.size(); ++i) {
+      auto it = done_.find(keys[i]);
+      (*out)[i] = it == done_.end() ? -1 : it->second;
+    }
+  }
+
   // fast path: HSET key field value for every result, then XACK + XDEL the ids
   void finish(const std::string& key, const std::string& group, const std::vector<std::string>& ids,
               const std::vector<std::pair<std::string, std::string>>& results, const std::string& field) {
     std::lock_guard<std::mutex> g(mu_);
+    if (track_) {
+      const long long now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now().time_since_epoch()).count();
+      for (auto& r : results) done_[r.first] = now;
+    }
     for (auto& r : results) {
       if (streams_.count(r.first)) continue;
       auto& h = hashes_[r.first];
@@ -598,6 +620,8 @@ class Store {
   std::unordered_map<std::string, Hash> hashes_;
   size_t used_ = 0, maxmem_;
   bool stop_ = false;
+  bool track_ = false;
+  std::unordered_map<std::string, long long> done_;  // result key -> finish stamp (ns)
 };
 
 // ------------------------------------------------------------------ TCP front end
@@ -767,6 +791,170 @@ class Server {
   std::thread stopper_;
 };
 
+// ------------------------------------------------------------------ load generator
+// Open-loop client for Cluster Serving measurements (BASELINE config 5): `threads` C++ threads
+// send records on a fixed schedule (record i is due at t0 + i / rate, whatever the responses)
+// for `duration` seconds, either straight into the in-process store (XADD through exec, the
+// path a co-located producer takes) or over TCP/RESP to the server's port (the network path of
+// the reference client, Py/serving/client.py:25-150). Completion is the store's finish() stamp
+// of the record's result key; latency = stamp - send time, both on this process's steady clock.
+// Replaces Python client processes, which saturated at ~6-8k records/s on the box's CPUs.
+struct LoadGenStats {
+  long long sent = 0, measured = 0, completed = 0, unfinished = 0;
+  double offered = 0, achieved = 0, p50 = 0, p90 = 0, p99 = 0, mean = 0, max = 0;
+};
+
+static long long lg_now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+      .count();
+}
+
+static void lg_resp_cmd(const std::vector<const std::string*>& parts, std::string& out) {
+  out += '*';
+  out += std::to_string(parts.size());
+  out += "\r\n";
+  for (auto* p : parts) {
+    out += '$';
+    out += std::to_string(p->size());
+    out += "\r\n";
+    out += *p;
+    out += "\r\n";
+  }
+}
+
+// read exactly one RESP reply line-group for an XADD (a bulk string or an error line)
+static bool lg_read_reply(int fd, std::string& buf) {
+  while (true) {
+    const size_t nl = buf.find("\r\n");
+    if (nl != std::string::npos) {
+      if (buf[0] == '$') {
+        const long len = std::strtol(buf.c_str() + 1, nullptr, 10);
+        const size_t need = nl + 2 + (len > 0 ? (size_t)len + 2 : 0);
+        if (buf.size() >= need) {
+          buf.erase(0, need);
+          return true;
+        }
+      } else {
+        buf.erase(0, nl + 2);
+        return true;
+      }
+    }
+    char tmp[4096];
+    const ssize_t r = ::recv(fd, tmp, sizeof(tmp), 0);
+    if (r <= 0) return false;
+    buf.append(tmp, (size_t)r);
+  }
+}
+
+LoadGenStats run_loadgen(const std::shared_ptr<Store>& st, const std::string& stream, const std::string& kind,
+                         const std::vector<std::string>& payloads, const std::string& shape, double rate,
+                         double duration, int threads, const std::string& prefix, double warm, double grace,
+                         int tcp_port) {
+  LoadGenStats S;
+  const long long n = (long long)(rate * duration);
+  if (n <= 0 || payloads.empty()) return S;
+  if (threads < 1) threads = 1;
+  std::vector<long long> sent_ns((size_t)n, -1);
+  std::vector<std::string> keys((size_t)n);
+  for (long long i = 0; i < n; ++i) keys[(size_t)i] = "result:" + prefix + "-" + std::to_string(i);
+  const std::string xadd = "XADD", star = "*", f_uri = "uri", f_shape = "shape";
+  const long long t0 = lg_now_ns() + 20000000LL;  // 20 ms for the threads to start
+  const double step_ns = 1e9 / rate;
+  std::atomic<long long> errors{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t) {
+    th.emplace_back([&, t] {
+      int fd = -1;
+      std::string rbuf, wbuf;
+      if (tcp_port > 0) {
+        fd = ::socket(AF_INET, SOCK_STREAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_port = htons((uint16_t)tcp_port);
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        int one = 1;
+        ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+        if (::connect(fd, (sockaddr*)&a, sizeof(a)) != 0) {
+          ::close(fd);
+          errors += 1;
+          return;
+        }
+      }
+      for (long long i = t; i < n; i += threads) {
+        const long long due = t0 + (long long)(i * step_ns);
+        std::this_thread::sleep_until(std::chrono::steady_clock::time_point(std::chrono::nanoseconds(due)));
+        const std::string uri = prefix + "-" + std::to_string(i);
+        const std::string& pl = payloads[(size_t)(i % (long long)payloads.size())];
+        sent_ns[(size_t)i] = lg_now_ns();
+        if (fd >= 0) {
+          wbuf.clear();
+          std::vector<const std::string*> parts{&xadd, &stream, &star, &f_uri, &uri, &kind, &pl};
+          if (!shape.empty()) { parts.push_back(&f_shape); parts.push_back(&shape); }
+          lg_resp_cmd(parts, wbuf);
+          size_t off = 0;
+          while (off < wbuf.size()) {
+            const ssize_t w = ::send(fd, wbuf.data() + off, wbuf.size() - off, MSG_NOSIGNAL);
+            if (w <= 0) break;
+            off += (size_t)w;
+          }
+          if (off < wbuf.size() || !lg_read_reply(fd, rbuf)) {
+            errors += 1;
+            break;
+          }
+        } else {
+          std::vector<std::string> cmd{xadd, stream, star, f_uri, uri, kind, pl};
+          if (!shape.empty()) { cmd.push_back(f_shape); cmd.push_back(shape); }
+          const Reply r = st->exec(cmd);
+          if (r.k == Reply::ERR) errors += 1;
+        }
+      }
+      if (fd >= 0) ::close(fd);
+    });
+  }
+  for (auto& x : th) x.join();
+  // wait for the tail (or the grace period)
+  std::vector<long long> done;
+  const long long deadline = lg_now_ns() + (long long)(grace * 1e9);
+  while (true) {
+    st->done_times(keys, &done);
+    long long left = 0;
+    for (long long i = 0; i < n; ++i)
+      if (sent_ns[(size_t)i] >= 0 && done[(size_t)i] < 0) ++left;
+    if (left == 0 || lg_now_ns() > deadline) break;
+    std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  }
+  const long long w0 = t0 + (long long)(warm * 1e9), w1 = t0 + (long long)(duration * 1e9);
+  std::vector<double> lat;
+  long long fin_in_window = 0;
+  for (long long i = 0; i < n; ++i) {
+    const long long s0 = sent_ns[(size_t)i], d = done[(size_t)i];
+    if (s0 < 0) continue;
+    ++S.sent;
+    if (d < 0) ++S.unfinished;
+    if (d >= w0 && d <= w1) ++fin_in_window;
+    if (s0 >= w0 && s0 <= w1) {
+      ++S.measured;
+      if (d >= 0) lat.push_back((d - s0) * 1e-6);
+    }
+  }
+  S.completed = (long long)lat.size();
+  S.offered = S.sent / duration;
+  S.achieved = fin_in_window / std::max(1e-9, duration - warm);
+  if (!lat.empty()) {
+    std::sort(lat.begin(), lat.end());
+    auto pct = [&](double q) { return lat[std::min(lat.size() - 1, (size_t)(q / 100.0 * (lat.size() - 1) + 0.5))]; };
+    S.p50 = pct(50);
+    S.p90 = pct(90);
+    S.p99 = pct(99);
+    S.max = lat.back();
+    double sum = 0;
+    for (double v : lat) sum += v;
+    S.mean = sum / lat.size();
+  }
+  if (errors.load() > 0) S.unfinished += errors.load();
+  return S;
+}
+
 // ------------------------------------------------------------------ python facade
 #ifndef ZOO_RT_NO_PYTHON
 class NativeStore {
@@ -820,6 +1008,26 @@ class NativeStore {
     store_->finish(key, group, ids, results, field);
   }
 
+  void track(bool on) { store_->track(on); }
+
+  // open-loop load generator (run_loadgen); blocks without the GIL, returns the measurement
+  py::dict loadgen(const std::string& stream, const std::string& kind, const std::vector<std::string>& payloads,
+                   const std::string& shape, double rate, double duration, int threads, const std::string& prefix,
+                   double warm, double grace, bool tcp) {
+    LoadGenStats S;
+    const int port = tcp && server_ && server_->running() ? server_->port() : 0;
+    if (tcp && port == 0) throw std::runtime_error("loadgen over TCP needs a running server (serve())");
+    {
+      py::gil_scoped_release nogil;
+      S = run_loadgen(store_, stream, kind, payloads, shape, rate, duration, threads, prefix, warm, grace, port);
+    }
+    py::dict d;
+    d["sent"] = S.sent; d["measured"] = S.measured; d["completed"] = S.completed; d["unfinished"] = S.unfinished;
+    d["offered_rate"] = S.offered; d["achieved_throughput"] = S.achieved;
+    d["p50_ms"] = S.p50; d["p90_ms"] = S.p90; d["p99_ms"] = S.p99; d["mean_ms"] = S.mean; d["max_ms"] = S.max;
+    return d;
+  }
+
  private:
   std::shared_ptr<Store> store_;
   std::unique_ptr<Server> server_;
@@ -839,7 +1047,13 @@ void register_serving(py::module& m) {
       .def("stop", &NativeStore::stop)
       .def("running", &NativeStore::running)
       .def("read_batch", &NativeStore::read_batch)
-      .def("finish", &NativeStore::finish);
+      .def("finish", &NativeStore::finish)
+      .def("track", &NativeStore::track, "stamp every result key finish() writes (load-generator latency)")
+      .def("loadgen", &NativeStore::loadgen, py::arg("stream"), py::arg("kind"), py::arg("payloads"),
+           py::arg("shape") = "", py::arg("rate") = 1000.0, py::arg("duration") = 5.0, py::arg("threads") = 4,
+           py::arg("prefix") = "lg", py::arg("warm") = 1.0, py::arg("grace") = 10.0, py::arg("tcp") = false,
+           "open-loop C++ load generator: records on a fixed schedule (in-process XADD or RESP over TCP), "
+           "latency from the store's finish stamps; returns offered/achieved rates and p50/p90/p99");
   m.def("b64decode", [](const std::string& s) {
     std::string out;
     if (!zoo_serving::b64decode(s, &out)) throw std::runtime_error("invalid base64");

@@ -12,6 +12,12 @@ ResNet-50 + BERT-base, throughput + p50 latency").
                                        rates (independent of responses) for --duration s each;
                                        per rate: achieved throughput, p50 / p99 service latency
                                        (send -> result written), unfinished records
+  serving_bench.py suite               BASELINE config 5 in one command: ResNet-50 (JPEG records)
+                                       and BERT-base (token-id tensor records), one serving worker
+                                       per GPU (run it unchanged under torch.distributed.run
+                                       --nproc-per-node N), the C++ open-loop load generator of
+                                       csrc/runtime/serving.cpp at fractions of the measured
+                                       capacity; rank 0 prints whole-node JSON per offered load
 
 Random-init weights, synthetic inputs. Prints one JSON line per measurement.
 """
@@ -440,9 +446,158 @@ def run_dist(a):
             dist.destroy_process_group()
 
 
+def _suite_model(name, a, rank, world, local, gather):
+    """One model through the suite on this rank: capacity (drain), model-only, open-loop loads."""
+    import base64
+    import tempfile
+    from zoo.models.image.resnet import resnet50
+    from zoo.serving import ClusterServing, InputQueue
+    from zoo.serving.resp import RespServer
+    bert = name == "bert"
+    srv = RespServer("127.0.0.1", 0).start()
+    out = []
+    try:
+        with tempfile.TemporaryDirectory() as d:
+            cfg = os.path.join(d, "config.yaml")
+            shape = "3,224,224" if not bert else "128"
+            open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: %s\n  filter: topN(5)\n"
+                                 "params:\n  batch_size: %d\n" % (srv.port, shape, a.batch))
+            model = _BertTokens() if bert else resnet50()
+            s = ClusterServing(cfg, model=model, device="cuda:%d" % local)
+            inq = InputQueue(cfg)
+            if bert:
+                rng = np.random.default_rng(rank)
+                toks = [rng.integers(0, 30522, (128,)).astype(np.float32) for _ in range(16)]
+                raw = toks
+                payloads = [base64.b64encode(t.tobytes()).decode() for t in toks]
+                kind, pshape = "tensor", "128"
+            else:
+                raw = _jpegs(a.images_kind, rank)
+                payloads = [base64.b64encode(j).decode() for j in raw]
+                kind, pshape = "image", ""
+            # warm-up: every batch bucket captured
+            for i in range(4 * a.batch):
+                _send(inq, "warm%d" % i, raw[i % len(raw)])
+            s.run(max_records=4 * a.batch, idle_timeout=120)
+            for bsz in (8, 16, 32, 64, 128, 256, 512):
+                if bsz > a.batch:
+                    break
+                x = (torch.randint(0, 30522, (bsz, 128), device="cuda:%d" % local).float() if bert
+                     else torch.zeros(bsz, 3, 224, 224, device="cuda:%d" % local))
+                s.im.predict(x)
+            # capacity: a pre-filled queue drained by the worker (the worker alone)
+            n_cap = a.images
+            for i in range(n_cap):
+                _send(inq, "cap%d" % i, raw[i % len(raw)])
+            s.records = 0
+            gather(None)
+            t0 = time.perf_counter()
+            s.run(max_records=n_cap, idle_timeout=60)
+            cap = s.records / (time.perf_counter() - t0)
+            # model alone at the serving batch (same InferenceModel replica, input on the GPU)
+            xm = (torch.randint(0, 30522, (a.batch, 128), device="cuda:%d" % local).float() if bert
+                  else torch.randn(a.batch, 3, 224, 224, device="cuda:%d" % local))
+            for _ in range(3):
+                s.im.predict(xm)
+            torch.cuda.synchronize()
+            tm = time.perf_counter()
+            for _ in range(10):
+                s.im.predict(xm)
+            torch.cuda.synchronize()
+            model_tp = 10 * a.batch / (time.perf_counter() - tm)
+            caps = gather([cap, model_tp])
+            node_cap = sum(c[0] for c in caps)
+            node_model = sum(c[1] for c in caps)
+            model_name = "BERT-base seq128 bf16" if bert else "ResNet-50 bf16"
+            if rank == 0:
+                print(json.dumps({"bench": "cluster-serving-capacity", "model": model_name, "batch_cap": a.batch,
+                                  "n_gpus": world, "drain_throughput": round(node_cap, 1),
+                                  "model_only_throughput": round(node_model, 1),
+                                  "drain_over_model": round(node_cap / max(node_model, 1e-9), 3),
+                                  "unit": "records/sec"}), flush=True)
+            # open loop: the C++ load generator on this rank's store, the worker in a thread
+            srv.store.track(True)
+            worker = threading.Thread(target=s.run, kwargs={"idle_timeout": None}, daemon=True)
+            worker.start()
+            fracs = [float(f) for f in a.fractions.split(",")]
+            for fi, f in enumerate(fracs):
+                rate = f * cap
+                gather(None)
+                st = srv.store.loadgen("image_stream", kind, payloads, pshape, rate, a.duration, a.lg_threads,
+                                       "r%d-%d-%s" % (rank, fi, name), 1.0, 15.0, bool(a.tcp))
+                allst = gather([st["offered_rate"], st["achieved_throughput"], st["p50_ms"], st["p99_ms"],
+                                st["unfinished"], st["p90_ms"]])
+                if rank == 0:
+                    rec = {"bench": "cluster-serving-suite", "model": model_name, "n_gpus": world,
+                           "load_fraction_of_capacity": f,
+                           "offered_rate": round(sum(v[0] for v in allst), 1),
+                           "achieved_throughput": round(sum(v[1] for v in allst), 1), "unit": "records/sec",
+                           "p50_ms": round(max(v[2] for v in allst), 2), "p90_ms": round(max(v[5] for v in allst), 2),
+                           "p99_ms": round(max(v[3] for v in allst), 2),
+                           "unfinished": int(sum(v[4] for v in allst)),
+                           "achieved_over_model": round(sum(v[1] for v in allst) / max(node_model, 1e-9), 3),
+                           "latency_note": "send -> result written; worst rank's percentile",
+                           "client": "C++ open-loop generator, %d threads per GPU, %s" % (
+                               a.lg_threads, "RESP over TCP" if a.tcp else "in-process XADD"),
+                           "batch_cap": a.batch, "duration_s": a.duration,
+                           "data": ("synthetic token ids [128]" if bert else
+                                    "synthetic 256x256 JPEG (%s)" % a.images_kind)}
+                    out.append(rec)
+                    print(json.dumps(rec), flush=True)
+                time.sleep(0.5)
+            s.stop()
+            worker.join(timeout=30)
+    finally:
+        srv.shutdown()
+        srv.server_close()
+    return out
+
+
+def run_suite(a):
+    """ResNet-50 and BERT-base serving, one worker per GPU (torch.distributed.run ranks)."""
+    import torch.distributed as dist
+    rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("gloo")
+    os.environ.setdefault("ZOO_SERVING_JPEG_THREADS", str(max(2, min(16, (os.cpu_count() or 16) // max(1, world) // 2))))
+    from zoo.common.nncontext import init_nncontext
+    init_nncontext("serving-suite")
+
+    def gather(vals):
+        """barrier (vals None) or all-gather of a small float list"""
+        if world == 1:
+            return [vals] if vals is not None else None
+        if vals is None:
+            dist.barrier()
+            return None
+        t = torch.tensor([float(v) for v in vals], dtype=torch.float64)
+        allv = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allv, t)
+        return [v.tolist() for v in allv]
+
+    results = []
+    try:
+        for name in a.models.split(","):
+            results += _suite_model(name, a, rank, world, local, gather)
+    finally:
+        if world > 1:
+            dist.destroy_process_group()
+    if rank == 0 and a.out:
+        with open(a.out, "w") as f:
+            json.dump(results, f, indent=1)
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("mode", choices=["model", "e2e", "openloop", "dist"])
+    ap.add_argument("mode", choices=["model", "e2e", "openloop", "dist", "suite"])
+    ap.add_argument("--models", default="resnet50,bert", help="suite: models to serve")
+    ap.add_argument("--fractions", default="0.25,0.5,0.7,0.85,1.0,1.2",
+                    help="suite: offered loads as fractions of the measured drain capacity")
+    ap.add_argument("--lg-threads", type=int, default=4, help="suite: C++ load-generator threads per GPU")
+    ap.add_argument("--tcp", action="store_true", help="suite: load generator over RESP/TCP (else in-process)")
+    ap.add_argument("--out", default="", help="suite: also write the records to this JSON file")
     ap.add_argument("--rates", default="", help="openloop: comma-separated offered rates (default: fractions "
                     "of the measured capacity)")
     ap.add_argument("--duration", type=float, default=8.0, help="openloop: seconds per offered rate")
@@ -458,7 +613,7 @@ def main():
     ap.add_argument("--model", default="resnet50", choices=["resnet50", "bert"],
                     help="e2e: ResNet-50 on JPEG records or BERT-base on token-id tensor records")
     a = ap.parse_args()
-    {"model": run_models, "e2e": run_e2e, "openloop": run_openloop, "dist": run_dist}[a.mode](a)
+    {"model": run_models, "e2e": run_e2e, "openloop": run_openloop, "dist": run_dist, "suite": run_suite}[a.mode](a)
 
 
 if __name__ == "__main__":

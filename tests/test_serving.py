@@ -170,3 +170,44 @@ def test_post_process_batch_matches_per_row_top_n():
             assert post_process_batch(a, flt) == [post_process(r, flt) for r in a]
     b = rng.standard_normal((4, 6)).astype(np.float32)
     assert post_process_batch(b, "None") == [post_process(r, "None") for r in b]
+
+
+@pytest.mark.parametrize("tcp", [False, True])
+def test_native_open_loop_load_generator(tcp):
+    """The C++ open-loop generator (csrc/runtime/serving.cpp run_loadgen) against a store with a
+    consumer that answers in batches: every record sent on schedule, latencies from the store's
+    finish stamps, achieved ~= offered below capacity; over TCP it goes through the RESP server."""
+    import base64
+    import threading
+    import time
+    from zoo import _runtime
+    st = _runtime.NativeStore(1 << 28)
+    st.serve("127.0.0.1", 0)
+    try:
+        st.execute([b"XGROUP", b"CREATE", b"image_stream", b"serving", b"0", b"MKSTREAM"])
+        st.track(True)
+        stop = threading.Event()
+
+        def consumer():
+            while not stop.is_set():
+                recs = st.read_batch("image_stream", "serving", "c0", 32, 10)
+                if recs:
+                    time.sleep(0.001)
+                    st.finish("image_stream", "serving", [r[0].decode() for r in recs],
+                              [("result:" + r[1], "ok") for r in recs], "value")
+
+        th = threading.Thread(target=consumer, daemon=True)
+        th.start()
+        payloads = [base64.b64encode(bytes([i]) * 500).decode() for i in range(4)]
+        d = st.loadgen("image_stream", "image", payloads, "", 2000.0, 1.5, 3, "t", 0.5, 5.0, tcp)
+        stop.set()
+        th.join(5)
+        assert d["sent"] == 3000 and d["unfinished"] == 0
+        assert d["measured"] == d["completed"] > 1500
+        assert abs(d["offered_rate"] - 2000.0) < 1.0
+        assert 1700 < d["achieved_throughput"] < 2300
+        assert 0 < d["p50_ms"] <= d["p90_ms"] <= d["p99_ms"] <= d["max_ms"] < 1000
+        # the records carry the uri / payload a worker decodes
+        assert st.execute([b"EXISTS", b"result:t-0"]) == 1
+    finally:
+        st.stop()
