@@ -303,6 +303,72 @@ __global__ void lstm_gates_bwd_kernel(const float* __restrict__ dh, const float*
   }
 }
 
+// Whole-sequence ConvLSTM step kernels (zoo/pipeline/api/keras/layers/recurrent.py
+// _ConvLSTMSeqFn): the forward also writes h_t as bf16 into the padded NHWC conv-input
+// history slot the next step's recurrent conv reads (row stride ldh, pad channels untouched =
+// 0), so a step is one recurrent conv + this kernel with no Python glue in between.
+__global__ void lstm_step_fwd_kernel(const float* __restrict__ gx, const float* __restrict__ gh,
+                                     const float* __restrict__ cprev, float* __restrict__ h, float* __restrict__ c,
+                                     float* __restrict__ acts, bf16_t* __restrict__ hb, int ldh, int M, int F,
+                                     int ldgh, int iact, int act) {
+  const size_t n = (size_t)M * F;
+  GRID_STRIDE(idx, n) {
+    const size_t m = idx / F;
+    const int j = (int)(idx % F);
+    const size_t r = m * 4 * F;
+    float g[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) g[q] = gx[r + q * F + j] + (gh ? gh[m * ldgh + q * F + j] : 0.f);
+    const float ig = lstm_act(g[0], iact), fg = lstm_act(g[1], iact);
+    const float cg = lstm_act(g[2], act), og = lstm_act(g[3], iact);
+    const float cp = cprev ? cprev[idx] : 0.f;
+    const float cn = fg * cp + ig * cg;
+    const float hn = og * lstm_act(cn, act);
+    c[idx] = cn;
+    h[idx] = hn;
+    hb[m * ldh + j] = f2bf(hn);
+    acts[r + j] = ig;
+    acts[r + F + j] = fg;
+    acts[r + 2 * F + j] = cg;
+    acts[r + 3 * F + j] = og;
+  }
+}
+
+// backward of one step: dh = dout (fp32 [M, F], may be null) + dhr (bf16 recurrent gradient,
+// row stride lddh, may be null); writes dg fp32 [M, 4F] (the input conv's gradient slot), dgb
+// bf16 [M, lddg] (the recurrent dgrad / wgrad operand) and dc_prev
+__global__ void lstm_step_bwd_kernel(const float* __restrict__ dout, const bf16_t* __restrict__ dhr, int lddh,
+                                     const float* __restrict__ dcn, const float* __restrict__ acts,
+                                     const float* __restrict__ cprev, const float* __restrict__ c,
+                                     float* __restrict__ dg, bf16_t* __restrict__ dgb, int lddg,
+                                     float* __restrict__ dcp, int M, int F, int iact, int act) {
+  const size_t n = (size_t)M * F;
+  GRID_STRIDE(idx, n) {
+    const size_t m = idx / F;
+    const int j = (int)(idx % F);
+    const size_t r = m * 4 * F;
+    const float ig = acts[r + j], fg = acts[r + F + j], cg = acts[r + 2 * F + j], og = acts[r + 3 * F + j];
+    const float tc = lstm_act(c[idx], act);
+    const float gh = (dout ? dout[idx] : 0.f) + (dhr ? bf2f(dhr[m * lddh + j]) : 0.f);
+    const float dc = gh * og * lstm_dact(tc, act) + (dcn ? dcn[idx] : 0.f);
+    const float cp = cprev ? cprev[idx] : 0.f;
+    const float d0 = dc * cg * lstm_dact(ig, iact), d1 = dc * cp * lstm_dact(fg, iact);
+    const float d2 = dc * ig * lstm_dact(cg, act), d3 = gh * tc * lstm_dact(og, iact);
+    dg[r + j] = d0;
+    dg[r + F + j] = d1;
+    dg[r + 2 * F + j] = d2;
+    dg[r + 3 * F + j] = d3;
+    if (dgb) {
+      bf16_t* o = dgb + m * lddg;
+      o[j] = f2bf(d0);
+      o[F + j] = f2bf(d1);
+      o[2 * F + j] = f2bf(d2);
+      o[3 * F + j] = f2bf(d3);
+    }
+    if (dcp) dcp[idx] = dc * fg;
+  }
+}
+
 static int grid_for(size_t n) {
   size_t b = (n + 255) / 256;
   return (int)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -396,5 +462,19 @@ extern "C" hipError_t zoo_lstm_gates(const float* gx, const float* gh, const flo
   else
     hipLaunchKernelGGL(lstm_gates_bwd_kernel, dim3(g), dim3(256), 0, st, dh, dcn, acts, cprev, c, dg, dcp, M, F, iact,
                        act);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_lstm_step(const float* gx, const float* gh, int ldgh, const float* cprev, float* h,
+                                    float* c, float* acts, void* hb, int ldh, const float* dout, const void* dhr,
+                                    int lddh, const float* dcn, float* dg, void* dgb, int lddg, float* dcp, int M,
+                                    int F, int iact, int act, int backward, hipStream_t st) {
+  const int g = grid_for((size_t)M * F);
+  if (!backward)
+    hipLaunchKernelGGL(lstm_step_fwd_kernel, dim3(g), dim3(256), 0, st, gx, gh, cprev, h, c, acts, (bf16_t*)hb, ldh,
+                       M, F, ldgh, iact, act);
+  else
+    hipLaunchKernelGGL(lstm_step_bwd_kernel, dim3(g), dim3(256), 0, st, dout, (const bf16_t*)dhr, lddh, dcn, acts,
+                       cprev, c, dg, (bf16_t*)dgb, lddg, dcp, M, F, iact, act);
   return hipGetLastError();
 }

@@ -92,7 +92,7 @@ __global__ __launch_bounds__(256) void prob_nll_kernel(const T* __restrict__ pro
     l += lr;
     c += cr;
   }
-  if (per_row) return;
+  if (per_row == 1) return;
   __shared__ float red[2][4];
   l = warp_sum(l);
   c = warp_sum(c);
@@ -105,10 +105,31 @@ __global__ __launch_bounds__(256) void prob_nll_kernel(const T* __restrict__ pro
   if (threadIdx.x == 0) {
     l = red[0][0] + red[0][1] + red[0][2] + red[0][3];
     c = red[1][0] + red[1][1] + red[1][2] + red[1][3];
-    if (c > 0.f) {
+    if (per_row == 2) {  // block partials, folded in order by prob_nll_finalize_kernel
+      loss_sum[blockIdx.x] = l;
+      count[blockIdx.x] = c;
+    } else if (c > 0.f) {
       atomicAdd(loss_sum, l);
       atomicAdd(count, c);
     }
+  }
+}
+
+// out[0] = sum(part loss) / max(sum(part count), 1) (or the plain sum), out[1] = count: the
+// loss scalar straight from the block partials (no zero-fill of accumulators, no clamp / div
+// launches; ordered, so deterministic)
+__global__ __launch_bounds__(64) void prob_nll_finalize_kernel(const float* __restrict__ part, int nb,
+                                                               float* __restrict__ out, int size_average) {
+  float l = 0.f, c = 0.f;
+  for (int b = threadIdx.x; b < nb; b += 64) {
+    l += part[b];
+    c += part[nb + b];
+  }
+  l = warp_sum(l);
+  c = warp_sum(c);
+  if (threadIdx.x == 0) {
+    out[0] = size_average ? l / fmaxf(c, 1.f) : l;
+    out[1] = c;
   }
 }
 
@@ -341,6 +362,22 @@ extern "C" hipError_t zoo_prob_nll(const void* probs, int is_f32, const int64_t*
   else
     hipLaunchKernelGGL(prob_nll_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)probs, labels,
                        loss_sum, count, dp, B, NC, eps, ignore_index, per_row);
+  return hipGetLastError();
+}
+
+// loss scalar + count of the probability NLL in two native launches: [out 2], part: 2 * 128 floats
+extern "C" hipError_t zoo_prob_nll_mean(const void* probs, int is_f32, const int64_t* labels, float* part,
+                                        float* out, int B, int NC, float eps, int ignore_index, int size_average,
+                                        hipStream_t st) {
+  const int rb = (B + 255) / 256;
+  const int blocks = rb < 128 ? (rb > 0 ? rb : 1) : 128;
+  if (is_f32)
+    hipLaunchKernelGGL(prob_nll_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)probs, labels, part,
+                       part + blocks, (float*)nullptr, B, NC, eps, ignore_index, 2);
+  else
+    hipLaunchKernelGGL(prob_nll_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)probs, labels, part,
+                       part + blocks, (float*)nullptr, B, NC, eps, ignore_index, 2);
+  hipLaunchKernelGGL(prob_nll_finalize_kernel, dim3(1), dim3(64), 0, st, part, blocks, out, size_average);
   return hipGetLastError();
 }
 

@@ -23,6 +23,7 @@ hipError_t zoo_jpeg_color_resize(const uint8_t*, void*, const zoo::JpegGeom*, in
                                  int, int, hipStream_t);
 hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
                         hipStream_t);
+hipError_t zoo_prob_nll_mean(const void*, int, const int64_t*, float*, float*, int, int, float, int, int, hipStream_t);
 hipError_t zoo_prob_nll_grad(const void*, int, const int64_t*, const float*, const float*, float*, int, int, float, int,
                              hipStream_t);
 int zoo_ncf_tier(int, int, int, int, int, int, int);
@@ -43,6 +44,9 @@ hipError_t zoo_wlrn(const void*, const void*, void*, float*, float*, int, int, i
                     hipStream_t);
 hipError_t zoo_resize_bilinear(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_upsample(const void*, void*, int, int, int, int, int, int, int, int, int, int, hipStream_t);
+hipError_t zoo_lstm_step(const float*, const float*, int, const float*, float*, float*, float*, void*, int,
+                         const float*, const void*, int, const float*, float*, void*, int, float*, int, int, int, int,
+                         int, hipStream_t);
 hipError_t zoo_lstm_gates(const float*, const float*, const float*, float*, float*, float*, const float*,
                           const float*, float*, float*, int, int, int, int, int, hipStream_t);
 hipError_t zoo_roi_pool(const void*, const float*, void*, int*, const void*, float*, int, int, int, int, int, int,
@@ -1351,6 +1355,71 @@ std::vector<torch::Tensor> lstm_gates_bwd(c10::optional<torch::Tensor> dh, c10::
   return {dg, dcp};
 }
 
+// Whole-sequence ConvLSTM step (keras_ops.hip lstm_step_*): every output is a caller-owned slot
+// of the sequence buffers; gh / hb / dhr / dgb are NHWC rows with their own (padded) strides.
+void lstm_step_fwd(torch::Tensor gx, c10::optional<torch::Tensor> gh, c10::optional<torch::Tensor> cprev,
+                   torch::Tensor h, torch::Tensor c, torch::Tensor acts, torch::Tensor hb, int64_t iact, int64_t act) {
+  req(gx, at::kFloat, "gx");
+  TORCH_CHECK(gx.dim() == 2 && gx.size(1) % 4 == 0, "lstm_step: gx [M, 4F]");
+  const int64_t M = gx.size(0), F = gx.size(1) / 4;
+  req(h, at::kFloat, "h"); req(c, at::kFloat, "c"); req(acts, at::kFloat, "acts"); req(hb, at::kBFloat16, "hb");
+  TORCH_CHECK(h.numel() == M * F && c.numel() == M * F && acts.numel() == M * 4 * F, "lstm_step: output sizes");
+  TORCH_CHECK(hb.numel() % M == 0 && hb.numel() / M >= F, "lstm_step: hb [M, >=F]");
+  const float* ghp = nullptr;
+  int64_t ldgh = 4 * F;
+  if (gh.has_value() && gh->defined()) {
+    req(*gh, at::kFloat, "gh");
+    TORCH_CHECK(gh->numel() % M == 0 && gh->numel() / M >= 4 * F, "lstm_step: gh [M, >=4F]");
+    ghp = gh->data_ptr<float>();
+    ldgh = gh->numel() / M;
+  }
+  const float* cp = nullptr;
+  if (cprev.has_value() && cprev->defined()) {
+    req(*cprev, at::kFloat, "cprev");
+    TORCH_CHECK(cprev->numel() == M * F, "lstm_step: c_prev [M, F]");
+    cp = cprev->data_ptr<float>();
+  }
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "lstm_step: activation code");
+  if (M * F == 0) return;
+  check_hip(zoo_lstm_step(gx.data_ptr<float>(), ghp, (int)ldgh, cp, h.data_ptr<float>(), c.data_ptr<float>(),
+                          acts.data_ptr<float>(), hb.data_ptr(), (int)(hb.numel() / M), nullptr, nullptr, 0, nullptr,
+                          nullptr, nullptr, 0, nullptr, (int)M, (int)F, (int)iact, (int)act, 0, cur_stream()),
+            "lstm_step_fwd");
+}
+
+void lstm_step_bwd(c10::optional<torch::Tensor> dout, c10::optional<torch::Tensor> dhr, c10::optional<torch::Tensor> dcn,
+                   torch::Tensor acts, c10::optional<torch::Tensor> cprev, torch::Tensor c, torch::Tensor dg,
+                   torch::Tensor dgb, torch::Tensor dcp, int64_t iact, int64_t act) {
+  req(acts, at::kFloat, "acts"); req(c, at::kFloat, "c"); req(dg, at::kFloat, "dg"); req(dcp, at::kFloat, "dcp");
+  req(dgb, at::kBFloat16, "dgb");
+  const int64_t M = acts.size(0), F = acts.size(1) / 4;
+  TORCH_CHECK(acts.dim() == 2 && c.numel() == M * F && dg.numel() == M * 4 * F && dcp.numel() == M * F,
+              "lstm_step_bwd: sizes");
+  TORCH_CHECK(dgb.numel() % M == 0 && dgb.numel() / M >= 4 * F, "lstm_step_bwd: dgb [M, >=4F]");
+  auto opt = [&](const c10::optional<torch::Tensor>& t, const char* n) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    req(*t, at::kFloat, n);
+    TORCH_CHECK(t->numel() == M * F, "lstm_step_bwd: ", n, " [M, F]");
+    return t->data_ptr<float>();
+  };
+  const float* pd = opt(dout, "dout");
+  const float* pdc = opt(dcn, "dc");
+  const float* pcp = opt(cprev, "cprev");
+  const void* pr = nullptr;
+  int64_t lddh = 0;
+  if (dhr.has_value() && dhr->defined()) {
+    req(*dhr, at::kBFloat16, "dhr");
+    TORCH_CHECK(dhr->numel() % M == 0 && dhr->numel() / M >= F, "lstm_step_bwd: dhr [M, >=F]");
+    pr = dhr->data_ptr();
+    lddh = dhr->numel() / M;
+  }
+  if (M * F == 0) return;
+  check_hip(zoo_lstm_step(nullptr, nullptr, 0, pcp, nullptr, c.data_ptr<float>(), acts.data_ptr<float>(), nullptr, 0,
+                          pd, pr, (int)lddh, pdc, dg.data_ptr<float>(), dgb.data_ptr(), (int)(dgb.numel() / M),
+                          dcp.data_ptr<float>(), (int)M, (int)F, (int)iact, (int)act, 1, cur_stream()),
+            "lstm_step_bwd");
+}
+
 // Max RoI pooling (Faster R-CNN): features NHWC, rois [R, 5] fp32 -> (out [R, PH, PW, C], argmax int32)
 std::vector<torch::Tensor> roi_pool_fwd(torch::Tensor f, torch::Tensor rois, int PH, int PW, double scale) {
   req_act(f, "roi_pool");
@@ -1447,6 +1516,24 @@ std::vector<torch::Tensor> prob_nll(torch::Tensor probs, torch::Tensor labels, b
   if (per_row) loss = loss.sum(1);
   if (want_grad) return {loss, dp};
   return {loss};
+}
+
+// [loss, count] of prob_nll in two native launches (block partials + an ordered fold): the loss
+// is already the mean (size_average) or the sum, so the caller launches nothing else
+torch::Tensor prob_nll_mean(torch::Tensor probs, torch::Tensor labels, double eps, int64_t ignore_index,
+                            bool size_average) {
+  TORCH_CHECK(probs.is_cuda() && probs.is_contiguous() && probs.dim() == 2, "prob_nll_mean: 2-D GPU probabilities");
+  TORCH_CHECK(probs.scalar_type() == at::kFloat || probs.scalar_type() == at::kBFloat16, "prob_nll_mean: dtype");
+  req(labels, at::kLong, "labels");
+  TORCH_CHECK(labels.numel() == probs.size(0) && probs.size(0) < (1LL << 31), "prob_nll_mean: labels size");
+  const int B = probs.size(0), NC = probs.size(1);
+  auto part = torch::empty({256}, probs.options().dtype(at::kFloat));
+  auto out = torch::empty({2}, probs.options().dtype(at::kFloat));
+  check_hip(zoo_prob_nll_mean(probs.data_ptr(), probs.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                              part.data_ptr<float>(), out.data_ptr<float>(), B, NC, (float)eps, (int)ignore_index,
+                              size_average ? 1 : 0, cur_stream()),
+            "prob_nll_mean");
+  return out;
 }
 
 // scaled gradient of prob_nll: dprobs = -g / (max(count, 1) * clamp(p[label])) at the label
@@ -2604,6 +2691,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("upsample_nd", &upsample_nd);
   m.def("lstm_gates_fwd", &lstm_gates_fwd);
   m.def("lstm_gates_bwd", &lstm_gates_bwd);
+  m.def("lstm_step_fwd", &lstm_step_fwd);
+  m.def("lstm_step_bwd", &lstm_step_bwd);
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
@@ -2646,6 +2735,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("softmax_xent", &softmax_xent);
+  m.def("prob_nll_mean", &prob_nll_mean);
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("adaptive", &adaptive);

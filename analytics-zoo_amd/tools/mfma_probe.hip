@@ -36,8 +36,9 @@ __global__ __launch_bounds__(256, 1) void probe(const bf16x8* __restrict__ src, 
     for (int e = 0; e < 16; ++e) acc32[i][e] = 0.f;
   unsigned long long t0, t1;
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
-  for (int st = 0; st < steps; ++st) {
-    const int cur = st & 1;
+  // two steps per iteration so the A double buffer is indexed with constants (a runtime
+  // index into a register array would put it in scratch memory)
+  auto body = [&](const int cur, const int st) {
     if constexpr (V == 2) {
 #pragma unroll
       for (int i = 0; i < 7; ++i)
@@ -56,6 +57,10 @@ __global__ __launch_bounds__(256, 1) void probe(const bf16x8* __restrict__ src, 
         __builtin_amdgcn_sched_barrier(0);
       }
     }
+  };
+  for (int st = 0; st < steps; st += 2) {
+    body(0, st);
+    body(1, st + 1);
   }
   asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");
   float s = 0.f;

@@ -39,15 +39,18 @@ def softmax_cross_entropy(logits, labels, ignore_index=-100):
 class _ProbNllFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, probs, labels, eps, ignore_index, size_average):
-        acc = native().prob_nll(probs, labels, False, eps, ignore_index)[0]
-        count = acc[1:2] if size_average else torch.ones_like(acc[1:2])
-        ctx.save_for_backward(probs, labels, count)
-        ctx.eps, ctx.ignore = eps, ignore_index
-        return acc[0] / count.clamp_min(1.0)[0]
+        # [loss, count] from the native pass + its ordered fold (no accumulator fill, no clamp /
+        # div launches); the backward scales by 1 / max(count, 1) itself
+        out = native().prob_nll_mean(probs, labels, eps, ignore_index, size_average)
+        ctx.save_for_backward(probs, labels, out[1:2])
+        ctx.eps, ctx.ignore, ctx.avg = eps, ignore_index, size_average
+        return out[0]
 
     @staticmethod
     def backward(ctx, g):
         probs, labels, count = ctx.saved_tensors
+        if not ctx.avg:
+            count = torch.ones_like(count)
         dp = native().prob_nll_grad(probs, labels, g.float().reshape(1).contiguous(), count, ctx.eps, ctx.ignore)
         return dp.to(probs.dtype), None, None, None, None
 

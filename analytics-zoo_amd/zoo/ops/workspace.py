@@ -17,8 +17,8 @@ def begin_step(device):
     need = _state["need"]
     if buf is None or buf.device != torch.device(device) or buf.numel() < need:
         _state["buf"] = torch.zeros(max(need, 1 << 16), dtype=torch.float32, device=device)
-    else:
-        buf.zero_()
+    elif _state["off"] > 0:
+        buf[:_state["off"]].zero_()   # only what the last step handed out is dirty (none: no launch)
     _state["off"] = 0
     _state["active"] = True
 

@@ -10,6 +10,8 @@ per-step path below (one [batch, hidden] x [hidden, gates*hidden] GEMM per step
 plus the gate math) is the CPU reference and the fallback for wider layers.
 Gate order follows Keras 1: LSTM (i, f, c, o), GRU (z, r, h).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -161,6 +163,84 @@ class GRU(_RNNBase):
         return (z * h + (1 - z) * hh,)
 
 
+# whole-sequence ConvLSTM2D path (_ConvLSTMSeqFn); ZOO_CONVLSTM_SEQ=0 keeps the per-step
+# autograd loop (A/B and fallback)
+_CONVLSTM_SEQ = os.environ.get("ZOO_CONVLSTM_SEQ", "1") != "0"
+
+
+class _ConvLSTMSeqFn(torch.autograd.Function):
+    """Whole ConvLSTM2D sequence on the native kernels with no per-step Python tensor glue:
+    per step ONE recurrent implicit-GEMM conv (fp32 gate pre-activations) and ONE fused step
+    kernel (gates, cell, hidden; h_t also written as bf16 into the padded NHWC history slot the
+    next step's conv reads). Backward through time per step: one fused step-backward kernel
+    (gate gradients fp32 for the input conv + bf16 for the recurrent convs, dc_prev), one
+    recurrent dgrad (weights flipped once per sequence) and one wgrad accumulating dWh in fp32.
+    Reference: InternalConvLSTM2D.scala (Zs/pipeline/api/keras/layers)."""
+
+    @staticmethod
+    def forward(ctx, gxs, wh, B, Ho, Wo, f, cph, R, S, iact, act, return_sequences):
+        C_ = ops.native()
+        from zoo.ops import _kern
+        from zoo.ops.conv import bf16_weight
+        T, M, K = gxs.shape
+        dev = gxs.device
+        pad = (R // 2, S // 2)
+        whb = bf16_weight(wh)
+        hist = torch.zeros(T + 1, B, Ho, Wo, cph, dtype=torch.bfloat16, device=dev)
+        hseq = torch.empty(T, M, f, dtype=torch.float32, device=dev)
+        cseq = torch.empty_like(hseq)
+        acts = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        for s in range(T):
+            gh = None
+            if s > 0:
+                gh = _kern.conv_fwd(hist[s], whb, R, S, (1, 1), pad, out_f32=True, out_bf16=False)
+            C_.lstm_step_fwd(gxs[s], gh, cseq[s - 1] if s > 0 else None, hseq[s], cseq[s], acts[s], hist[s + 1],
+                             iact, act)
+        ctx.save_for_backward(wh, hist, cseq, acts)
+        ctx.geo = (B, Ho, Wo, f, cph, R, S, iact, act, return_sequences)
+        return hseq if return_sequences else hseq[T - 1].clone()
+
+    @staticmethod
+    def backward(ctx, dout):
+        C_ = ops.native()
+        from zoo.ops import _kern
+        from zoo.ops.conv import bf16_weight
+        wh, hist, cseq, acts = ctx.saved_tensors
+        B, Ho, Wo, f, cph, R, S, iact, act, rseq = ctx.geo
+        T, M, K = acts.shape
+        dev = acts.device
+        pad = (R // 2, S // 2)
+        K8 = wh.shape[0]
+        whb = bf16_weight(wh)
+        whf = _kern.flip_weights(whb, K8, R, S, cph)          # once per sequence
+        dgxs = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        dgb = torch.zeros(B, Ho, Wo, K8, dtype=torch.bfloat16, device=dev)
+        dc = torch.empty(M, f, dtype=torch.float32, device=dev)
+        dc_next = None
+        dhr = None
+        gbuf = getattr(wh, "_zoo_grad", None)
+        dwh = gbuf if (gbuf is not None and ctx.needs_input_grad[1]) else \
+            torch.zeros(wh.shape, dtype=torch.float32, device=dev)
+        dout = dout.contiguous().float()
+        for s in range(T - 1, -1, -1):
+            d = dout[s] if rseq else (dout if s == T - 1 else None)
+            C_.lstm_step_bwd(d, dhr, dc_next, acts[s], cseq[s - 1] if s > 0 else None, cseq[s], dgxs[s], dgb, dc,
+                             iact, act)
+            dc_next = dc.clone() if s > 0 else None
+            if s > 0:
+                if ctx.needs_input_grad[1]:
+                    C_.conv_wgrad(hist[s], dgb, dwh, R, S, 1, 1, pad[0], pad[1], 1, 1)
+                dhr = _kern.conv_fwd(dgb, whf, R, S, (1, 1), (R - 1 - pad[0], S - 1 - pad[1]))
+        if gbuf is not None and ctx.needs_input_grad[1]:
+            hook = getattr(wh, "_zoo_grad_ready", None)
+            if hook is not None:
+                hook(wh)
+            dw = None
+        else:
+            dw = dwh.to(wh.dtype) if ctx.needs_input_grad[1] else None
+        return dgxs, dw, None, None, None, None, None, None, None, None, None, None
+
+
 class ConvLSTM2D(Layer):
     """Convolutional LSTM over (batch, time, channels, rows, cols) ('th')."""
 
@@ -211,6 +291,19 @@ class ConvLSTM2D(Layer):
             xn = F.pad(xn, (0, cpx - C))
         xs = ops.conv2d_nhwc(xn, wx, bias, kernel=(R, S), stride=self.subsample, pad=pad, out_f32=True)[..., :K]
         Ho, Wo = xs.shape[1], xs.shape[2]
+        from zoo.ops.layers import ACT_CODES
+        if _CONVLSTM_SEQ and K % 8 == 0 and ops.ceil8(K) == wh.shape[0]:
+            # whole-sequence path: time-major gate inputs in processing order, one autograd node
+            M = B * Ho * Wo
+            gxs = xs.reshape(B, T, Ho * Wo, K).permute(1, 0, 2, 3).reshape(T, M, K)
+            if self.go_backwards:
+                gxs = gxs.flip(0)
+            hs = _ConvLSTMSeqFn.apply(gxs.contiguous(), wh, B, Ho, Wo, f, cph, R, S,
+                                      ACT_CODES[self.inner_activation], ACT_CODES[self.activation],
+                                      bool(self.return_sequences))
+            if self.return_sequences:
+                return hs.reshape(T, B, Ho, Wo, f).permute(1, 0, 4, 2, 3)
+            return hs.reshape(B, Ho, Wo, f).permute(0, 3, 1, 2)
         xs = xs.reshape(B, T, Ho * Wo, K)
         M = B * Ho * Wo
         h = c = None

@@ -1,0 +1,15 @@
+#!/bin/bash
+# MFMA probe (fixed), ConvLSTM sequence path tests + bench, NCF loss tests + bench + profile
+cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/misc
+timeout -k 5 60 ./analytics-zoo_amd/tools/mfma_probe > gpurun_out/misc/probe2.log 2>&1; cat gpurun_out/misc/probe2.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_convlstm_seq.py tests/test_gpu_keras_native.py tests/test_ncf_fused.py -x -q -k "convlstm or ConvLSTM or prob_nll or ncf" --timeout 120 --timeout-method thread > gpurun_out/misc/b_tests.log 2>&1
+echo "tests rc=$?"; tail -4 gpurun_out/misc/b_tests.log
+timeout -k 10 200 python -u analytics-zoo_amd/tools/convlstm_bench.py > gpurun_out/misc/convlstm_bench.log 2>&1
+echo "convlstm bench rc=$?"; tail -2 gpurun_out/misc/convlstm_bench.log
+timeout -k 10 200 python -u bench.py --model ncf --batch 65536 --steps 50 --warmup 10 > gpurun_out/misc/bench_ncf.log 2>&1
+echo "ncf bench rc=$?"; tail -1 gpurun_out/misc/bench_ncf.log
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_ncf -o ncf -- python3 bench.py --model ncf --batch 65536 --steps 32 --warmup 10 > gpurun_out/misc/prof_ncf.log 2>&1 || exit 9
+DB=$(find /tmp/prof_ncf -name "*.db" | head -1)
+python3 analytics-zoo_amd/tools/prof_summary.py $DB 42 "NCF ml-20m shape b65536 (bench.py --model ncf under rocprofv3), round 4" > gpurun_out/misc/ncf_prof.md 2>&1
+head -24 gpurun_out/misc/ncf_prof.md

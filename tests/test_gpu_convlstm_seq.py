@@ -1,0 +1,41 @@
+"""Whole-sequence ConvLSTM2D (recurrent.py _ConvLSTMSeqFn: recurrent conv + fused step kernel
+per step, fused BPTT) against the fp32 PyTorch reference of the same layer (F.conv2d, the
+layer's own CPU path): output, input gradient and both weight gradients, with and without
+return_sequences / go_backwards. Reference: InternalConvLSTM2D.scala."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
+
+
+@pytest.mark.parametrize("rseq,back", [(True, False), (False, False), (True, True)])
+def test_convlstm2d_sequence_path_matches_fp32(gpu, rseq, back):
+    from zoo.pipeline.api.keras.layers import recurrent as R
+    torch.manual_seed(0)
+    T, B, C, H, W, f = 6, 2, 8, 10, 12, 16
+    layer = R.ConvLSTM2D(f, 3, 3, return_sequences=rseq, go_backwards=back, input_shape=(T, C, H, W))
+    layer._ensure_built((None, T, C, H, W))
+    ref = copy.deepcopy(layer)
+    x = torch.randn(B, T, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    (yr * g).sum().backward()
+    layer = layer.to(gpu)
+    assert R._CONVLSTM_SEQ
+    xg = x.to(gpu).requires_grad_(True)
+    y = layer(xg)
+    assert y.shape == yr.shape
+    (y.float() * g.to(gpu)).sum().backward()
+    assert rel(y, yr) < 3e-2
+    assert rel(xg.grad, xr.grad) < 5e-2
+    assert rel(layer.Wh.grad, ref.Wh.grad) < 5e-2
+    assert rel(layer.Wx.grad, ref.Wx.grad) < 5e-2
+    assert rel(layer.b.grad, ref.b.grad) < 5e-2
