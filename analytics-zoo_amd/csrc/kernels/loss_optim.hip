@@ -153,12 +153,15 @@ __global__ __launch_bounds__(256) void prob_nll_grad_kernel(const T* __restrict_
 }
 
 // ---------------- optimizers over flat buffers ----------------
-__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const float* __restrict__ g,
+// zero_g: the gradient slot is cleared after it is read (the engine's next step then needs no
+// fill launch over the flat gradient buffer)
+__global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ pbf, size_t n,
                                                   float lr, float momentum, float dampening, float wd,
-                                                  int nesterov, float gscale, int first_step) {
+                                                  int nesterov, float gscale, int first_step, int zero_g) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
+    if (zero_g) g[i] = 0.f;
     float pi = p[i];
     if (wd != 0.f) gi += wd * pi;
     if (momentum != 0.f) {
@@ -172,13 +175,14 @@ __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, const f
   }
 }
 
-__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ g,
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pbf, size_t n, float lr, float b1,
                                                    float b2, float eps, float wd, float bc1, float bc2,
-                                                   float gscale, int decoupled) {
+                                                   float gscale, int decoupled, int zero_g) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
+    if (zero_g) g[i] = 0.f;
     float pi = p[i];
     if (wd != 0.f && !decoupled) gi += wd * pi;
     const float mi = b1 * m[i] + (1.f - b1) * gi;
@@ -196,13 +200,14 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, const 
 
 // generic "RMSprop / Adagrad / Adadelta / Adamax" family in one kernel
 // kind: 0 rmsprop, 1 adagrad, 2 adadelta, 3 adamax
-__global__ __launch_bounds__(256) void adaptive_kernel(float* __restrict__ p, const float* __restrict__ g,
+__global__ __launch_bounds__(256) void adaptive_kernel(float* __restrict__ p, float* __restrict__ g,
                                                        float* __restrict__ s1, float* __restrict__ s2,
                                                        bf16_t* __restrict__ pbf, size_t n, int kind, float lr,
                                                        float rho, float rho2, float eps, float wd, float bc1,
-                                                       float gscale) {
+                                                       float gscale, int zero_g) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
+    if (zero_g) g[i] = 0.f;
     float pi = p[i];
     if (wd != 0.f) gi += wd * pi;
     float upd;
@@ -394,27 +399,31 @@ extern "C" hipError_t zoo_prob_nll_grad(const void* probs, int is_f32, const int
   return hipGetLastError();
 }
 
+// zero_g (optimizer-side gradient clear, ops.cpp optim_zero_grad): g is cleared after it is read
+static int g_zero_g = 0;
+extern "C" void zoo_optim_zero_grad(int on) { g_zero_g = on ? 1 : 0; }
+
 extern "C" hipError_t zoo_sgd(float* p, const float* g, float* mom, void* pbf, size_t n, float lr, float momentum,
                               float dampening, float wd, int nesterov, float gscale, int first_step,
                               hipStream_t st) {
-  hipLaunchKernelGGL(sgd_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, mom, (bf16_t*)pbf, n, lr, momentum,
-                     dampening, wd, nesterov, gscale, first_step);
+  hipLaunchKernelGGL(sgd_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), mom, (bf16_t*)pbf, n, lr,
+                     momentum, dampening, wd, nesterov, gscale, first_step, g_zero_g);
   return hipGetLastError();
 }
 
 extern "C" hipError_t zoo_adam(float* p, const float* g, float* m, float* v, void* pbf, size_t n, float lr, float b1,
                                float b2, float eps, float wd, float bc1, float bc2, float gscale, int decoupled,
                                hipStream_t st) {
-  hipLaunchKernelGGL(adam_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, m, v, (bf16_t*)pbf, n, lr, b1, b2, eps, wd,
-                     bc1, bc2, gscale, decoupled);
+  hipLaunchKernelGGL(adam_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), m, v, (bf16_t*)pbf, n,
+                     lr, b1, b2, eps, wd, bc1, bc2, gscale, decoupled, g_zero_g);
   return hipGetLastError();
 }
 
 extern "C" hipError_t zoo_adaptive(float* p, const float* g, float* s1, float* s2, void* pbf, size_t n, int kind,
                                    float lr, float rho, float rho2, float eps, float wd, float bc1, float gscale,
                                    hipStream_t st) {
-  hipLaunchKernelGGL(adaptive_kernel, dim3(egrid(n)), dim3(256), 0, st, p, g, s1, s2, (bf16_t*)pbf, n, kind, lr, rho,
-                     rho2, eps, wd, bc1, gscale);
+  hipLaunchKernelGGL(adaptive_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), s1, s2, (bf16_t*)pbf,
+                     n, kind, lr, rho, rho2, eps, wd, bc1, gscale, g_zero_g);
   return hipGetLastError();
 }
 

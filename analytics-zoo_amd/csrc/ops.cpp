@@ -23,6 +23,7 @@ hipError_t zoo_jpeg_color_resize(const uint8_t*, void*, const zoo::JpegGeom*, in
                                  int, int, hipStream_t);
 hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
                         hipStream_t);
+void zoo_optim_zero_grad(int);
 hipError_t zoo_prob_nll_mean(const void*, int, const int64_t*, float*, float*, int, int, float, int, int, hipStream_t);
 hipError_t zoo_prob_nll_grad(const void*, int, const int64_t*, const float*, const float*, float*, int, int, float, int,
                              hipStream_t);
@@ -2736,6 +2737,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_bwd", &gap_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("prob_nll_mean", &prob_nll_mean);
+  m.def("optim_zero_grad", [](bool on) { zoo_optim_zero_grad(on ? 1 : 0); },
+        "sgd / adam / adaptive clear each gradient element after reading it (engine: no per-step grad fill)");
   m.def("sgd", &sgd);
   m.def("adam", &adam);
   m.def("adaptive", &adaptive);

@@ -604,7 +604,11 @@ class GradSync:
             self.finish()
             if clip is not None:
                 clip(flat.grad, gscale, self)
-            optim.step(flat.master, flat.grad, flat.bf16, gscale)
+            if getattr(optim, "_native_zero_grad", False) and flat.grad.is_cuda:
+                # the optimizer kernel clears each gradient slot after reading it
+                flat.grad_clean = bool(optim.step(flat.master, flat.grad, flat.bf16, gscale, zero_grad=True))
+            else:
+                optim.step(flat.master, flat.grad, flat.bf16, gscale)
         if self.collect_stats:
             self.collect_comm_stats()
         self.reset()

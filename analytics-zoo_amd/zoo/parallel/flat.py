@@ -47,6 +47,9 @@ class FlatParams:
         self.numel = max(off, ALIGN)
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=dev)
         self.grad = torch.zeros(self.numel, dtype=torch.float32, device=dev)
+        # True while every gradient slot is known to be 0 (fresh, or cleared by the optimizer
+        # kernel that consumed it): the engine then skips its per-step fill of the buffer
+        self.grad_clean = True
         self.bf16 = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev) if bf16_copy else None
         for p, o in zip(self.params, self.offsets):
             n = p.numel()

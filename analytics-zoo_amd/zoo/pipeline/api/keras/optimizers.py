@@ -223,12 +223,25 @@ class OptimMethod:
             self._key = key
         return self._buffers
 
-    def step(self, master, grad, bf16=None, gscale=1.0):
-        """Update ``master`` (fp32 flat tensor or shard) in place from ``grad``."""
+    # optimizers whose native step clears the gradient after reading it when asked (zero_grad)
+    _native_zero_grad = False
+
+    def step(self, master, grad, bf16=None, gscale=1.0, zero_grad=False):
+        """Update ``master`` (fp32 flat tensor or shard) in place from ``grad``. With
+        ``zero_grad`` the native kernels also clear ``grad`` (returns True when they did)."""
         bufs = self._ensure_buffers(master.numel(), master.device)
         lr = self.current_lr()
+        cleared = False
         if master.is_cuda:
-            self._step_native(master, grad, bf16, bufs, lr, float(gscale))
+            if zero_grad and self._native_zero_grad:
+                native().optim_zero_grad(True)
+                try:
+                    self._step_native(master, grad, bf16, bufs, lr, float(gscale))
+                finally:
+                    native().optim_zero_grad(False)
+                cleared = True
+            else:
+                self._step_native(master, grad, bf16, bufs, lr, float(gscale))
         else:
             with torch.no_grad():
                 self._step_torch(master, grad * gscale, bufs, lr)
@@ -239,6 +252,7 @@ class OptimMethod:
             bump_weights_epoch()   # cached dgrad filter flips are stale now
         self.state["neval"] += 1
         self.state["evalCounter"] += 1
+        return cleared
 
     def optimize(self, flat, gscale=1.0):
         self.step(flat.master, flat.grad, flat.bf16, gscale)
@@ -289,6 +303,8 @@ class OptimMethod:
 class SGD(OptimMethod):
     """BigDL SGD: x -= lr * (momentum buffer of (g + wd*x)), with dampening / nesterov."""
 
+    _native_zero_grad = True
+
     n_states = 1
 
     def __init__(self, learningrate=1e-3, learningrate_decay=0.0, weightdecay=0.0, momentum=0.0, dampening=None,
@@ -329,6 +345,8 @@ class SGD(OptimMethod):
 class Adam(OptimMethod):
     """Zoo Adam (bias corrected, Adam.scala:59-106)."""
 
+    _native_zero_grad = True
+
     n_states = 2
 
     def __init__(self, lr=1e-3, beta_1=0.9, beta_2=0.999, epsilon=1e-8, decay=0.0, schedule=None,
@@ -359,6 +377,8 @@ class Adam(OptimMethod):
 
 class AdamWeightDecay(OptimMethod):
     """BERT-style Adam with decoupled weight decay and warmup (AdamWeightDecay.scala:75-124)."""
+
+    _native_zero_grad = True
 
     n_states = 2
 
@@ -409,6 +429,7 @@ class AdamWeightDecay(OptimMethod):
 
 
 class _Adaptive(OptimMethod):
+    _native_zero_grad = True
     kind = 0
 
     def _native_args(self):

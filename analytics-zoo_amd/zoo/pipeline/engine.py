@@ -3,7 +3,8 @@ InternalDistriOptimizer + BigDL DistriOptimizer, SURVEY.md §2.4 E1-E3, E5;
 call stack §3.2).
 
 One process per GPU. Per iteration:
-  1. ``flat.grad`` zeroed (one memset over the flat fp32 gradient buffer)
+  1. ``flat.grad`` zeroed (one memset over the flat fp32 gradient buffer -- or none: the native
+     optimizer kernels clear each gradient slot after reading it, FlatParams.grad_clean)
   2. forward on the native kernels (bf16 activations, bf16 weight copies)
   3. loss (+ fused loss gradient) and backward; conv/BN backward kernels
      accumulate straight into the flat gradient buffer and each finished
@@ -239,6 +240,7 @@ class TrainingEngine:
             # buckets launched before the failure may still be read by in-flight collectives
             self.sync.wait_comm()
             self.flat.grad.zero_()
+            self.flat.grad_clean = False
             loss = torch.zeros((), device=self.device)
         with ph.range("comm_optim"):
             try:
@@ -260,7 +262,9 @@ class TrainingEngine:
         return self.phases.resolve()
 
     def _fwd_bwd(self, inputs, target):
-        self.flat.grad.zero_()
+        if not getattr(self.flat, "grad_clean", False):
+            self.flat.grad.zero_()
+        self.flat.grad_clean = False
         workspace.begin_step(self.device)
         try:
             out = self.forward_fn(self.model, inputs)
@@ -292,6 +296,9 @@ class TrainingEngine:
                 torch.cuda.synchronize(self.device)
                 return self._fwd_bwd(inputs, target)
         graph, sx, sy, sloss = g
+        if not getattr(self.flat, "grad_clean", False):
+            self.flat.grad.zero_()      # the captured step may rely on the optimizer's clearing
+        self.flat.grad_clean = False
         for s_, t in zip(sx, xs):
             s_.copy_(t, non_blocking=True)
         sy.copy_(target, non_blocking=True)

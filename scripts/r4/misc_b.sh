@@ -13,3 +13,7 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_ncf -o ncf -- py
 DB=$(find /tmp/prof_ncf -name "*.db" | head -1)
 python3 analytics-zoo_amd/tools/prof_summary.py $DB 42 "NCF ml-20m shape b65536 (bench.py --model ncf under rocprofv3), round 4" > gpurun_out/misc/ncf_prof.md 2>&1
 head -24 gpurun_out/misc/ncf_prof.md
+for i in 1 2; do
+  timeout -k 10 200 python -u bench.py --steps 20 --warmup 5 > gpurun_out/misc/bench_rn_$i.log 2>&1 || exit 10
+  echo "resnet run=$i $(grep -o '"value": [0-9.]*' gpurun_out/misc/bench_rn_$i.log) $(grep -o '"final_loss": [0-9.]*' gpurun_out/misc/bench_rn_$i.log)"
+done
