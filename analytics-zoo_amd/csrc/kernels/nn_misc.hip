@@ -32,6 +32,26 @@ ZOO_DEV void st8<float>(float* p, const float* f) {
   *reinterpret_cast<float4*>(p + 4) = make_float4(f[4], f[5], f[6], f[7]);
 }
 
+// Dropout keep-mask: a counter-based hash of (seed, element index), so backward regenerates the
+// mask instead of storing it (da = keep * dout * scale). i8 = index of the element's 8-element
+// chunk in the flat tensor, e = element within the chunk. Shared by dropout_add_kernel and the
+// fused residual-dropout LayerNorm forward, which must draw identical masks.
+ZOO_DEV uint32_t drop_fmix(uint32_t h) {
+  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
+  return h;
+}
+ZOO_DEV uint32_t drop_base(size_t i8, uint32_t s1) { return drop_fmix((uint32_t)(i8 >> 29) ^ s1); }
+ZOO_DEV bool drop_keep(size_t i8, int e, uint32_t s0, uint32_t base, uint32_t thresh) {
+  return drop_fmix(((uint32_t)(i8 << 3) + e) * 0x9E3779B1u ^ s0 ^ base) >= thresh;
+}
+
+struct DropArgs {
+  const bf16_t* A;  // dropout branch (nullptr: plain LayerNorm)
+  bf16_t* S;        // residual sum out = X + keep * A * scale (the LayerNorm input saved for backward)
+  uint32_t thresh, s0, s1;
+  float scale;
+};
+
 // ---------------------------------------------------------------- LayerNorm
 template <typename T>
 __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const T* __restrict__ X, const float* __restrict__ g,
@@ -68,23 +88,41 @@ __global__ __launch_bounds__(256) void layernorm_fwd_kernel(const T* __restrict_
 // Row-resident variant for D <= NCH*512: one wave per row keeps its NCH x 8
 // values in registers between the statistics and the normalise pass (the row
 // is read once), and gamma/beta are read with 16-byte vector loads.
-template <typename T, int NCH>
+//
+// DROP (bf16 only): the Transformer residual LayerNorm(x + dropout(a)) in one pass -- the sum is
+// formed in registers, rounded to bf16 and stored (S, the tensor LayerNorm backward reads) and
+// normalised from the rounded values, so no separate dropout_add pass writes S and reads it back.
+template <typename T, int NCH, bool DROP = false>
 __global__ __launch_bounds__(256) void layernorm_fwd_reg_kernel(const T* __restrict__ X, const float* __restrict__ g,
                                                                 const float* __restrict__ b, T* __restrict__ Y,
                                                                 float* __restrict__ mean_out,
                                                                 float* __restrict__ rstd_out, int rows, int D,
-                                                                float eps) {
+                                                                float eps, DropArgs dr) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const T* x = X + (size_t)row * D;
   float v[NCH][8];
   float s = 0.f, ss = 0.f;
+  uint32_t dbase = 0;
+  if constexpr (DROP) dbase = drop_base(((size_t)row * D) >> 3, dr.s1);
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     const int c = (k * 64 + lane) * 8;
     if (c < D) {
       ld8(x + c, v[k]);
+      if constexpr (DROP) {
+        float a[8];
+        ld8(dr.A + (size_t)row * D + c, a);
+        const size_t i8 = ((size_t)row * D + c) >> 3;
+        // the hash base depends on i8 >> 29 only: recompute it for chunks past a 2^29 boundary
+        const uint32_t bs = (i8 >> 29) == ((((size_t)row * D) >> 3) >> 29) ? dbase : drop_base(i8, dr.s1);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[k][e] += drop_keep(i8, e, dr.s0, bs, dr.thresh) ? a[e] * dr.scale : 0.f;
+        const uint4 pk = pack8(v[k]);
+        *reinterpret_cast<uint4*>(dr.S + (size_t)row * D + c) = pk;
+        unpack8(pk, v[k]);
+      }
     } else {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[k][e] = 0.f;
@@ -357,12 +395,7 @@ __global__ __launch_bounds__(256) void layernorm_part_fold2_kernel(const float* 
 }
 
 // ---------------------------------------------------------------- Dropout (+ residual add)
-// out = x + keep(i) * a * scale  (x optional). keep(i) is a counter-based hash of (seed, i),
-// so backward regenerates the mask instead of storing it: da = keep(i) * dout * scale.
-ZOO_DEV uint32_t drop_fmix(uint32_t h) {
-  h ^= h >> 16; h *= 0x85EBCA6Bu; h ^= h >> 13; h *= 0xC2B2AE35u; h ^= h >> 16;
-  return h;
-}
+// out = x + keep(i) * a * scale  (x optional); see drop_keep above.
 
 __global__ __launch_bounds__(256) void dropout_add_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ X,
                                                           bf16_t* __restrict__ Out, size_t n8, uint32_t thresh,
@@ -371,11 +404,10 @@ __global__ __launch_bounds__(256) void dropout_add_kernel(const bf16_t* __restri
     float a[8], o[8];
     unpack8(reinterpret_cast<const uint4*>(A)[i], a);
     if (X) unpack8(reinterpret_cast<const uint4*>(X)[i], o);
-    const uint32_t base = drop_fmix((uint32_t)(i >> 29) ^ s1);
+    const uint32_t base = drop_base(i, s1);
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      const uint32_t h = drop_fmix(((uint32_t)(i << 3) + e) * 0x9E3779B1u ^ s0 ^ base);
-      const float v = h >= thresh ? a[e] * scale : 0.f;
+      const float v = drop_keep(i, e, s0, base, thresh) ? a[e] * scale : 0.f;
       o[e] = X ? o[e] + v : v;
     }
     reinterpret_cast<uint4*>(Out)[i] = pack8(o);
@@ -549,7 +581,7 @@ extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, 
   const bool al = ((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(b)) & 15) == 0;
 #define ZOO_LN_REG(T, NCH)                                                                                   \
   hipLaunchKernelGGL((layernorm_fwd_reg_kernel<T, NCH>), dim3(blocks), dim3(256), 0, st, (const T*)X, g, b, \
-                     (T*)Y, mean, rstd, rows, D, eps)
+                     (T*)Y, mean, rstd, rows, D, eps, DropArgs{})
   if (al && D <= 2048) {
     if (f32) {
       if (D <= 512) ZOO_LN_REG(float, 1);
@@ -569,6 +601,33 @@ extern "C" hipError_t zoo_layernorm_fwd(const void* X, int f32, const float* g, 
   else
     hipLaunchKernelGGL(layernorm_fwd_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)X, g, b,
                        (bf16_t*)Y, mean, rstd, rows, D, eps);
+  return hipGetLastError();
+}
+
+// Y = LayerNorm(S), S = X + dropout(A) (stored): the fused Transformer residual LayerNorm. bf16,
+// D % 8 == 0, D <= 2048, 16-byte aligned gamma / beta. Draws the mask zoo_dropout_add draws for
+// the same (n, p, seed), so its backward is zoo_dropout_add(dS, nullptr, ...).
+extern "C" hipError_t zoo_dropout_add_layernorm_fwd(const void* A, const void* X, const float* g, const float* b,
+                                                    void* S, void* Y, float* mean, float* rstd, int rows, int D,
+                                                    float eps, float p, uint64_t seed, hipStream_t st) {
+  if (D % 8 || D > 2048 || (((reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(b)) & 15) != 0))
+    return hipErrorInvalidValue;
+  const double t = (double)p * 4294967296.0;
+  DropArgs dr;
+  dr.A = (const bf16_t*)A;
+  dr.S = (bf16_t*)S;
+  dr.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  dr.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  dr.s0 = (uint32_t)seed;
+  dr.s1 = (uint32_t)(seed >> 32);
+  const int blocks = (rows + 3) / 4;
+#define ZOO_LN_DROP(NCH)                                                                                    \
+  hipLaunchKernelGGL((layernorm_fwd_reg_kernel<bf16_t, NCH, true>), dim3(blocks), dim3(256), 0, st,        \
+                     (const bf16_t*)X, g, b, (bf16_t*)Y, mean, rstd, rows, D, eps, dr)
+  if (D <= 512) ZOO_LN_DROP(1);
+  else if (D <= 1024) ZOO_LN_DROP(2);
+  else ZOO_LN_DROP(4);
+#undef ZOO_LN_DROP
   return hipGetLastError();
 }
 

@@ -268,6 +268,8 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
   //                                   col k0 + wn*64 + qb*32 + j*16 + (lane&15)
   if (part) {
     // fragment order: [split][tile][wave][qa][qb][i][j][lane] float4
+    // fragments wholly outside dW (tile overhang: N or K not a multiple of 256) are neither
+    // stored nor read by the fold -- half the partial traffic on 128-channel shapes
     f32x4* dst = reinterpret_cast<f32x4*>(part) + ((size_t)(split * tiles + tile) * 8 + w) * 32 * 64 + lane;
 #pragma unroll
     for (int qa = 0; qa < 2; ++qa)
@@ -276,7 +278,10 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
 #pragma unroll
         for (int i = 0; i < 4; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) dst[(((qa * 2 + qb) * 4 + i) * 2 + j) * 64] = acc[qa][qb][i][j];
+          for (int j = 0; j < 2; ++j) {
+            const bool live = k0 + wn * 64 + qb * 32 + j * 16 < g.K && n0 + wm * 128 + qa * 64 + i * 16 < g.N;
+            if (live) dst[(((qa * 2 + qb) * 4 + i) * 2 + j) * 64] = acc[qa][qb][i][j];
+          }
   } else {
     const int fr = lane & 15, fq = lane >> 4;
 #pragma unroll
@@ -307,6 +312,15 @@ __global__ __launch_bounds__(256) void wgrad256_fold_kernel(const float* __restr
   const size_t total = per_tile * tiles;
   const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (idx >= total) return;
+  const int tile = (int)(idx / per_tile);
+  const int rem = (int)(idx - (size_t)tile * per_tile);
+  const int w = rem >> 11, f = (rem >> 6) & 31, lane = rem & 63;
+  const int j = f & 1, i = (f >> 1) & 3, qb = (f >> 3) & 1, qa = f >> 4;
+  const int wm = w >> 2, wn = w & 3;
+  const int n0 = (tile / g.tiles_k) * W2_T, k0 = (tile % g.tiles_k) * W2_T;
+  const int col = k0 + wn * 64 + qb * 32 + j * 16 + (lane & 15);
+  const int row = n0 + wm * 128 + qa * 64 + i * 16 + (lane >> 4) * 4;
+  if (col >= g.K || row >= g.N) return;  // slot never written (see the partial store)
   const f32x4* p = reinterpret_cast<const f32x4*>(part) + idx;
   // 4 independent partial sums keep 4 loads in flight (the splits are summed in a fixed
   // order per lane, so the result stays deterministic)
@@ -320,15 +334,6 @@ __global__ __launch_bounds__(256) void wgrad256_fold_kernel(const float* __restr
   }
   for (; sp < g.splits; ++sp) s += p[(size_t)sp * total];
   s += (s1 + s2) + s3;
-  const int tile = (int)(idx / per_tile);
-  const int rem = (int)(idx - (size_t)tile * per_tile);
-  const int w = rem >> 11, f = (rem >> 6) & 31, lane = rem & 63;
-  const int j = f & 1, i = (f >> 1) & 3, qb = (f >> 3) & 1, qa = f >> 4;
-  const int wm = w >> 2, wn = w & 3;
-  const int n0 = (tile / g.tiles_k) * W2_T, k0 = (tile % g.tiles_k) * W2_T;
-  const int col = k0 + wn * 64 + qb * 32 + j * 16 + (lane & 15);
-  const int row = n0 + wm * 128 + qa * 64 + i * 16 + (lane >> 4) * 4;
-  if (col >= g.K) return;
 #pragma unroll
   for (int r = 0; r < 4; ++r)
     if (row + r < g.N) dW[(size_t)(row + r) * g.ldw + col] += s[r];

@@ -132,6 +132,8 @@ hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, h
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
+hipError_t zoo_dropout_add_layernorm_fwd(const void*, const void*, const float*, const float*, void*, void*, float*,
+                                         float*, int, int, float, float, uint64_t, hipStream_t);
 hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
                              float*, int, int, float*, const void*, hipStream_t);
 size_t zoo_layernorm_bwd_part_floats(int, int, int);
@@ -1744,6 +1746,29 @@ std::vector<torch::Tensor> layernorm_fwd(torch::Tensor x, c10::optional<torch::T
   return {y, mean, rstd};
 }
 
+// y = LayerNorm(s), s = x + dropout(a, p, seed) (the Transformer residual): {y, s, mean, rstd}
+std::vector<torch::Tensor> dropout_add_layernorm_fwd(torch::Tensor a, torch::Tensor x, torch::Tensor g, torch::Tensor b,
+                                                     double eps, double p, int64_t seed) {
+  req(a, at::kBFloat16, "a");
+  req(x, at::kBFloat16, "x");
+  req(g, at::kFloat, "gamma");
+  req(b, at::kFloat, "beta");
+  TORCH_CHECK(a.is_contiguous() && x.is_contiguous() && a.sizes() == x.sizes(), "dropout_add_layernorm: contiguous same-shape a / x");
+  const int D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && D <= 2048 && g.numel() == D && b.numel() == D, "dropout_add_layernorm: D % 8 == 0, D <= 2048");
+  TORCH_CHECK(rows < (1LL << 31), "dropout_add_layernorm: too many rows");
+  auto y = torch::empty_like(x);
+  auto s = torch::empty_like(x);
+  auto mean = torch::empty({rows}, x.options().dtype(at::kFloat));
+  auto rstd = torch::empty({rows}, x.options().dtype(at::kFloat));
+  check_hip(zoo_dropout_add_layernorm_fwd(a.data_ptr(), x.data_ptr(), g.data_ptr<float>(), b.data_ptr<float>(),
+                                          s.data_ptr(), y.data_ptr(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                                          (int)rows, D, (float)eps, (float)p, (uint64_t)seed, cur_stream()),
+            "dropout_add_layernorm_fwd");
+  return {y, s, mean, rstd};
+}
+
 torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<torch::Tensor> g, torch::Tensor mean,
                             torch::Tensor rstd, c10::optional<torch::Tensor> dg, c10::optional<torch::Tensor> db,
                             c10::optional<torch::Tensor> dy2) {
@@ -2750,6 +2775,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("sum_chunks_bf16", &sum_chunks_bf16);
   m.def("add_bf16", &add_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
+  m.def("dropout_add_layernorm_fwd", &dropout_add_layernorm_fwd);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("mean"),
         py::arg("rstd"), py::arg("dg"), py::arg("db"), py::arg("dy2") = py::none());
   m.def("embedding_fwd", &embedding_fwd);

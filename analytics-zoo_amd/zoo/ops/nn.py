@@ -128,6 +128,65 @@ def dropout_add(a, x, p, training=True, grad_add=None):
     return x + F.dropout(a, p, True)
 
 
+class _DropAddLNFn(torch.autograd.Function):
+    """y = LayerNorm(x + dropout(a)) in one native pass (the Transformer residual LayerNorm):
+    the residual sum s is formed in registers, stored once for the backward and normalised
+    without being read back. Backward: the LayerNorm backward gives ds; the regenerated mask
+    gives da = keep * ds / (1 - p); ds is x's gradient (or parked in an armed GradAdd)."""
+
+    @staticmethod
+    def forward(ctx, a, x, gamma, beta, eps, p, handoff=None, grad_in=None):
+        seed = _drop_rng().getrandbits(62)
+        y, s, mean, rstd = native().dropout_add_layernorm_fwd(a, x, gamma.detach(), beta.detach(), eps, p, seed)
+        ctx.save_for_backward(s, gamma, beta, mean, rstd)
+        ctx.p, ctx.seed = p, seed
+        ctx.handoff = handoff if (handoff is not None and handoff.armed) else None
+        if ctx.handoff is not None:
+            handoff.armed = False   # one parking consumer per arming, as _DropoutAddFn
+        ctx.grad_in = grad_in
+        if grad_in is not None:
+            grad_in.armed = True
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        s, gamma, beta, mean, rstd = ctx.saved_tensors
+        dg, own_g = _target(gamma)
+        db, own_b = _target(beta)
+        dy2 = None
+        h = ctx.grad_in
+        if h is not None:
+            dy2, h.grad = h.grad, None
+            if dy2 is not None:
+                dy2 = dy2.contiguous().to(s.dtype)
+        ds = native().layernorm_bwd(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd, dg, db, dy2)
+        if own_g:
+            _ready(gamma)
+        if own_b:
+            _ready(beta)
+        da = native().dropout_add(ds, None, ctx.p, ctx.seed)
+        dx = ds
+        if ctx.handoff is not None:
+            hh = ctx.handoff
+            hh.grad = ds if hh.grad is None else hh.grad + ds
+            dx = None
+        return da, dx, (None if own_g else dg), (None if own_b else db), None, None, None, None
+
+
+def dropout_add_layer_norm(a, x, p, training, gamma, beta, eps=1e-5, grad_add=None, grad_in=None):
+    """``layer_norm(dropout_add(a, x, p, training, grad_add), gamma, beta, eps, grad_in)`` -- the
+    Transformer residual LayerNorm -- as one native pass when it can be (bf16 GPU tensors, fp32
+    affine, D % 8 == 0, D <= 2048, dropout live, not under stream capture: the mask seed is drawn
+    on the host per call); otherwise the two ops. Reference: TransformerLayer.scala:129-181."""
+    D = x.shape[-1]
+    if training and p > 0 and a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and \
+            a.shape == x.shape and D % 8 == 0 and D <= 2048 and a.numel() >= _DROP_FUSE_MIN and \
+            gamma is not None and beta is not None and gamma.dtype == torch.float32 and \
+            beta.dtype == torch.float32 and not torch.cuda.is_current_stream_capturing():
+        return _DropAddLNFn.apply(a.contiguous(), x.contiguous(), gamma, beta, float(eps), float(p), grad_add, grad_in)
+    return layer_norm(dropout_add(a, x, p, training, grad_add=grad_add), gamma, beta, eps, grad_in=grad_in)
+
+
 def layer_norm(x, gamma=None, beta=None, eps=1e-5, grad_in=None):
     """``grad_in``: a :class:`GradAdd` the consumers of the OUTPUT can park a gradient in
     (``dropout_add(a, y, ..., grad_add=h)``, the Transformer residual): the backward kernel sums

@@ -23,7 +23,7 @@ import torch.nn.functional as F
 
 from zoo import ops
 from zoo.ops.attention import attention_packed
-from zoo.ops.nn import GeluLink, GradAdd, dropout_add
+from zoo.ops.nn import GeluLink, GradAdd, dropout_add, dropout_add_layer_norm
 from zoo.pipeline.api.keras.base import Layer
 
 
@@ -34,6 +34,15 @@ _RESID_GRAD_FUSE = os.environ.get("ZOO_RESID_GRAD_FUSE", "0") != "0"
 # residual gradient summed inside the producing LayerNorm's backward kernel instead (the
 # LayerNorm that made x / n is armed; the residual dropout_add parks its gradient there)
 _LN_GRAD_ADD = os.environ.get("ZOO_LN_GRAD_ADD", "1") != "0"
+# residual dropout-add fused into the LayerNorm forward (one pass: the sum is stored for the
+# backward but never read back), ops.nn.dropout_add_layer_norm
+_DROP_LN_FUSE = os.environ.get("ZOO_DROP_LN_FUSE", "1") != "0"
+
+
+def _res_ln(a, x, p, training, gamma, beta, eps, grad_add, grad_in):
+    if _DROP_LN_FUSE:
+        return dropout_add_layer_norm(a, x, p, training, gamma, beta, eps, grad_add=grad_add, grad_in=grad_in)
+    return ops.layer_norm(dropout_add(a, x, p, training, grad_add=grad_add), gamma, beta, eps, grad_in=grad_in)
 
 
 def _normal(shape, std):
@@ -81,17 +90,16 @@ class _Block(nn.Module):
                               training=self.training)
             a = a.transpose(1, 2).reshape(B, L, H)
         a = ops.linear(a, self.proj_w, self.proj_b)
-        n = ops.layer_norm(dropout_add(a, x, self.hidden_drop, self.training, grad_add=h1 if h1 is not None else lx),
-                           self.ln1_g, self.ln1_b, self.ln_eps, grad_in=ln_n)
+        n = _res_ln(a, x, self.hidden_drop, self.training, self.ln1_g, self.ln1_b, self.ln_eps,
+                    h1 if h1 is not None else lx, ln_n)
         act = "gelu" if self.gelu == "erf" else None
         gl = GeluLink() if act == "gelu" else None      # GELU backward in fc2's dgrad epilogue
         m = ops.linear(n, self.fc1_w, self.fc1_b, act=act, grad_add=h2, gelu_link=gl)
         if self.gelu != "erf":  # GPT tanh approximation
             m = 0.5 * m * (1 + torch.tanh(math.sqrt(2 / math.pi) * (m + 0.044715 * m * m * m)))
         m = ops.linear(m, self.fc2_w, self.fc2_b, gelu_src=gl)
-        out = ops.layer_norm(dropout_add(m, n, self.hidden_drop, self.training,
-                                         grad_add=h2 if h2 is not None else ln_n),
-                             self.ln2_g, self.ln2_b, self.ln_eps, grad_in=ln_out)
+        out = _res_ln(m, n, self.hidden_drop, self.training, self.ln2_g, self.ln2_b, self.ln_eps,
+                      h2 if h2 is not None else ln_n, ln_out)
         if ln_out is not None:
             out._zoo_grad_in = ln_out   # the next block's residual parks its x-gradient here
         return out
