@@ -66,7 +66,7 @@ ZOO_DEV void c3_dma(const bf16_t* src, char* dst) {
     __builtin_amdgcn_sched_barrier(0);                                                 \
   }
 
-template <int EPI, bool STAMP = false>
+template <int EPI, bool STAMP = false, bool LATE = false>
 __global__ __launch_bounds__(C3_NT, 1) void c3_kernel(const bf16_t* __restrict__ X, const bf16_t* __restrict__ Wt,
                                                       bf16_t* __restrict__ Y, const bf16_t* __restrict__ resid,
                                                       float* __restrict__ stats, C3Geom g, BwdStats bs) {
@@ -215,10 +215,12 @@ __global__ __launch_bounds__(C3_NT, 1) void c3_kernel(const bf16_t* __restrict__
 #pragma unroll
           for (int s = 0; s < 3; ++s) fad[r][s][i] = (px + s) * 128 + ((co_hi ^ ((px + s) & 7)) << 4);
         }
-      // two-buffer tap pipeline: the 14 fragment reads of tap t+1 are interleaved with the 28
-      // MFMAs of tap t (one read per MFMA gap); tap t's reads are retired (lgkmcnt(0)) BEFORE
+      // two-buffer tap pipeline: the 14 fragment reads of tap t+1 are interleaved with the first
+      // 14 MFMAs of tap t (one read per MFMA gap), so they have landed long before tap t+1's
+      // lgkmcnt(0) (reads in the LAST 14 gaps left the final read's latency exposed at every tap
+      // boundary: ZOO_C3_LATE=1 keeps that schedule for A/B). Tap t's reads are retired BEFORE
       // tap t+1's are issued, so at most 14 LDS reads are ever outstanding: lgkmcnt is 4 bits,
-      // and with 28 pending hipcc can only wait for 0 (which exposed every other tap's reads)
+      // and with 28 pending hipcc can only wait for 0
       bf16x8 afb[2][2][C3_TM];
       auto read_tap = [&](int t, int buf) {
         const int r = t / 3, s = t - r * 3;
@@ -233,17 +235,25 @@ __global__ __launch_bounds__(C3_NT, 1) void c3_kernel(const bf16_t* __restrict__
       for (int t = 0; t < 9; ++t) {
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0), vmcnt / expcnt untouched
         __builtin_amdgcn_sched_barrier(0);
-        // MFMA k of tap t, then (k >= 14) fragment read k-14 of tap t+1, pinned in that order:
-        // the reads start once the k-half-0 fragments are consumed, so no read lands in a
-        // register an in-flight MFMA still sources
+        // MFMA k of tap t, then fragment read q of tap t+1, pinned in that order. Early
+        // schedule (default): q = k for k < 14, k-half 0 first -- buffer (t+1)&1 last fed tap
+        // t-1, whose k-half-0 fragments were consumed >= 14 MFMAs and k-half-1 fragment ri
+        // >= 20 - ri MFMAs before the read overwrites it. Late schedule: q = k - 14 for k >= 14.
         const int r1 = (t + 1) / 3, s1 = (t + 1) - r1 * 3;
 #pragma unroll
         for (int k = 0; k < 28; ++k) {
           const int kk = k / 14, i = (k % 14) / 2, j = k % 2;
           acc[i][j] = mfma16(afb[t & 1][kk][i], bw[t][kk][j], acc[i][j]);
-          if (t + 1 < 9 && k >= 14) {
-            const int ri = (k - 14) >> 1, rk = k & 1;
-            afb[(t + 1) & 1][rk][ri] = *reinterpret_cast<const bf16x8*>(ring + (fad[r1][s1][ri] ^ (rk << 6)));
+          if constexpr (LATE) {
+            if (t + 1 < 9 && k >= 14) {
+              const int ri = (k - 14) >> 1, rk = k & 1;
+              afb[(t + 1) & 1][rk][ri] = *reinterpret_cast<const bf16x8*>(ring + (fad[r1][s1][ri] ^ (rk << 6)));
+            }
+          } else {
+            if (t + 1 < 9 && k < 14) {
+              const int ri = k % 7, rk = k / 7;
+              afb[(t + 1) & 1][rk][ri] = *reinterpret_cast<const bf16x8*>(ring + (fad[r1][s1][ri] ^ (rk << 6)));
+            }
           }
           __builtin_amdgcn_sched_barrier(0);
         }
@@ -479,6 +489,27 @@ extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* 
     else
       hipLaunchKernelGGL((c3_kernel<2, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
                          (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+    return hipGetLastError();
+  }
+  static const bool late = [] {
+    const char* e = getenv("ZOO_C3_LATE");
+    return e && atoi(e) != 0;
+  }();
+  if (late) {  // the previous read schedule (fragment reads in the last 14 MFMA gaps), for A/B
+    static bool lattr = false;
+    if (!lattr) {
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<1, false, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<2, false, true>),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      lattr = true;
+    }
+    if (epi == 1)
+      hipLaunchKernelGGL((c3_kernel<1, false, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X,
+                         (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
+    else
+      hipLaunchKernelGGL((c3_kernel<2, false, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X,
+                         (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
     return hipGetLastError();
   }
   if (epi == 1)

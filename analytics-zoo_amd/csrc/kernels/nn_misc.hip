@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
                                                                const float* __restrict__ mean,
                                                                const float* __restrict__ rstd, bf16_t* __restrict__ dX,
                                                                float* __restrict__ part, int rows, int D,
-                                                               const bf16_t* __restrict__ dY2) {
+                                                               const bf16_t* __restrict__ dY2, DropArgs dr) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -332,7 +332,21 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
         float o[4];
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = rs * (gv[k][e] * gg[k][e] - bsum - xh[k][e] * a);
-        *reinterpret_cast<uint2*>(dX + (size_t)row * D + c) = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        const uint2 pk = make_uint2(pack2bf(o[0], o[1]), pack2bf(o[2], o[3]));
+        *reinterpret_cast<uint2*>(dX + (size_t)row * D + c) = pk;
+        if (dr.S) {
+          // the residual-dropout branch's gradient from the same rounded values: dA = keep * dX * scale
+          // (dr.S carries dA here; the mask of zoo_dropout_add for this (p, seed))
+          const size_t E = (size_t)row * D + c;  // 4-aligned: one 8-element hash chunk
+          const size_t i8 = E >> 3;
+          const uint32_t bs = drop_base(i8, dr.s1);
+          const float q[4] = {bf2f((bf16_t)(pk.x & 0xFFFFu)), bf2f((bf16_t)(pk.x >> 16)), bf2f((bf16_t)(pk.y & 0xFFFFu)),
+                              bf2f((bf16_t)(pk.y >> 16))};
+          float d[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) d[e] = drop_keep(i8, (int)(E & 7) + e, dr.s0, bs, dr.thresh) ? q[e] * dr.scale : 0.f;
+          *reinterpret_cast<uint2*>(dr.S + E) = make_uint2(pack2bf(d[0], d[1]), pack2bf(d[2], d[3]));
+        }
       }
     }
   }
@@ -654,12 +668,12 @@ extern "C" size_t zoo_layernorm_bwd_part_floats(int rows, int D, int f32) {
 
 // dY2 (nullable): a second output gradient added to dY inside the bf16 v2 kernel; the other
 // paths return hipErrorNotSupported for it (the caller then adds it first)
-extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
-                                        const float* rstd, void* dX, float* dg, float* db, int rows, int D,
-                                        float* part, const void* dY2, hipStream_t st) {
+static hipError_t ln_bwd_impl(const void* dY, const void* X, int f32, const float* g, const float* mean,
+                              const float* rstd, void* dX, float* dg, float* db, int rows, int D, float* part,
+                              const void* dY2, const DropArgs& dr, hipStream_t st) {
   const int nch = f32 ? 0 : ln_v2_nch(D);
   const bool v2 = nch && (reinterpret_cast<uintptr_t>(g) & 15) == 0;
-  if (dY2 && !v2) return hipErrorNotSupported;
+  if ((dY2 || dr.S) && !v2) return hipErrorNotSupported;
   if (v2) {
     const int blocks = ln_v2_blocks(rows);
     float* pp = (dg || db) ? part : nullptr;
@@ -667,7 +681,7 @@ extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, 
     const size_t lds = (size_t)8 * D * sizeof(float);
 #define ZOO_LNB2(N)                                                                                              \
   hipLaunchKernelGGL((layernorm_bwd_v2_kernel<N>), dim3(blocks), dim3(256), lds, st, (const bf16_t*)dY,         \
-                     (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, pp, rows, D, (const bf16_t*)dY2)
+                     (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, pp, rows, D, (const bf16_t*)dY2, dr)
     if (nch == 1) ZOO_LNB2(1);
     else if (nch == 2) ZOO_LNB2(2);
     else if (nch == 3) ZOO_LNB2(3);
@@ -715,6 +729,30 @@ extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, 
     hipLaunchKernelGGL(layernorm_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), smem, st, (const bf16_t*)dY,
                        (const bf16_t*)X, g, mean, rstd, (bf16_t*)dX, dg, db, rows, D, rpb);
   return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_layernorm_bwd(const void* dY, const void* X, int f32, const float* g, const float* mean,
+                                        const float* rstd, void* dX, float* dg, float* db, int rows, int D,
+                                        float* part, const void* dY2, hipStream_t st) {
+  return ln_bwd_impl(dY, X, f32, g, mean, rstd, dX, dg, db, rows, D, part, dY2, DropArgs{}, st);
+}
+
+// backward of zoo_dropout_add_layernorm_fwd: dX (= the residual input's gradient) and, from the
+// same rounded values, dA = keep * dX / (1 - p) for the dropout branch -- no second pass over dX.
+// bf16 v2 kernel only (hipErrorNotSupported otherwise: the caller runs zoo_dropout_add on dX).
+extern "C" hipError_t zoo_layernorm_bwd_drop(const void* dY, const void* X, const float* g, const float* mean,
+                                             const float* rstd, void* dX, void* dA, float* dg, float* db, int rows,
+                                             int D, float* part, const void* dY2, float p, uint64_t seed,
+                                             hipStream_t st) {
+  const double t = (double)p * 4294967296.0;
+  DropArgs dr;
+  dr.A = nullptr;
+  dr.S = (bf16_t*)dA;
+  dr.thresh = t >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)t;
+  dr.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
+  dr.s0 = (uint32_t)seed;
+  dr.s1 = (uint32_t)(seed >> 32);
+  return ln_bwd_impl(dY, X, 0, g, mean, rstd, dX, dg, db, rows, D, part, dY2, dr, st);
 }
 
 extern "C" hipError_t zoo_embedding_fwd(const void* table, int f32, const int64_t* idx, void* out, int n, int D, int V,

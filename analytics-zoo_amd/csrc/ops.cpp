@@ -132,6 +132,8 @@ hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, h
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
+hipError_t zoo_layernorm_bwd_drop(const void*, const void*, const float*, const float*, const float*, void*, void*,
+                                  float*, float*, int, int, float*, const void*, float, uint64_t, hipStream_t);
 hipError_t zoo_dropout_add_layernorm_fwd(const void*, const void*, const float*, const float*, void*, void*, float*,
                                          float*, int, int, float, float, uint64_t, hipStream_t);
 hipError_t zoo_layernorm_bwd(const void*, const void*, int, const float*, const float*, const float*, void*, float*,
@@ -1806,6 +1808,46 @@ torch::Tensor layernorm_bwd(torch::Tensor dy, torch::Tensor x, c10::optional<tor
   return dx;
 }
 
+// backward of dropout_add_layernorm_fwd: {dx, da} (da = keep * dx / (1 - p), the dropout
+// branch's gradient, written by the same kernel where the bf16 v2 backward applies)
+std::vector<torch::Tensor> layernorm_bwd_drop(torch::Tensor dy, torch::Tensor x, torch::Tensor g, torch::Tensor mean,
+                                              torch::Tensor rstd, c10::optional<torch::Tensor> dg,
+                                              c10::optional<torch::Tensor> db, c10::optional<torch::Tensor> dy2,
+                                              double p, int64_t seed) {
+  req(dy, at::kBFloat16, "dy");
+  req(x, at::kBFloat16, "x");
+  req(g, at::kFloat, "gamma");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.numel() == x.numel(), "layernorm_bwd_drop: dy / x");
+  const int D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && mean.numel() == rows && rstd.numel() == rows && g.numel() == D, "layernorm_bwd_drop: shapes");
+  if (dg.has_value() && dg->defined()) { req(*dg, at::kFloat, "dgamma"); TORCH_CHECK(dg->numel() == D, "dg"); }
+  if (db.has_value() && db->defined()) { req(*db, at::kFloat, "dbeta"); TORCH_CHECK(db->numel() == D, "db"); }
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    TORCH_CHECK(dy2->is_contiguous() && dy2->scalar_type() == at::kBFloat16 && dy2->numel() == dy.numel(),
+                "layernorm_bwd_drop: dy2 must match dy");
+    d2 = dy2->data_ptr();
+  }
+  auto dx = torch::empty_like(x);
+  auto da = torch::empty_like(x);
+  torch::Tensor part;
+  const size_t pf = zoo_layernorm_bwd_part_floats((int)rows, D, 0);
+  if (pf && (opt_ptr<float>(dg) || opt_ptr<float>(db))) part = torch::empty({(int64_t)pf}, mean.options());
+  hipError_t e = zoo_layernorm_bwd_drop(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), mean.data_ptr<float>(),
+                                        rstd.data_ptr<float>(), dx.data_ptr(), da.data_ptr(), opt_ptr<float>(dg),
+                                        opt_ptr<float>(db), (int)rows, D, part.defined() ? part.data_ptr<float>() : nullptr,
+                                        d2, (float)p, (uint64_t)seed, cur_stream());
+  if (e == hipErrorNotSupported) {
+    (void)hipGetLastError();
+    dx = layernorm_bwd(dy, x, g, mean, rstd, dg, db, dy2);
+    da = dropout_add(dx, c10::nullopt, p, seed);
+    return {dx, da};
+  }
+  check_hip(e, "layernorm_bwd_drop");
+  return {dx, da};
+}
+
 torch::Tensor embedding_fwd(torch::Tensor table, torch::Tensor idx, int64_t pad) {
   TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.dim() == 2, "embedding: 2-D GPU table");
   req(idx, at::kLong, "indices");
@@ -2776,6 +2818,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("add_bf16", &add_bf16);
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("dropout_add_layernorm_fwd", &dropout_add_layernorm_fwd);
+  m.def("layernorm_bwd_drop", &layernorm_bwd_drop);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("mean"),
         py::arg("rstd"), py::arg("dg"), py::arg("db"), py::arg("dy2") = py::none());
   m.def("embedding_fwd", &embedding_fwd);

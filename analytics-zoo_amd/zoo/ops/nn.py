@@ -131,8 +131,8 @@ def dropout_add(a, x, p, training=True, grad_add=None):
 class _DropAddLNFn(torch.autograd.Function):
     """y = LayerNorm(x + dropout(a)) in one native pass (the Transformer residual LayerNorm):
     the residual sum s is formed in registers, stored once for the backward and normalised
-    without being read back. Backward: the LayerNorm backward gives ds; the regenerated mask
-    gives da = keep * ds / (1 - p); ds is x's gradient (or parked in an armed GradAdd)."""
+    without being read back. Backward: one LayerNorm-backward kernel writes ds and, with the
+    regenerated mask, da = keep * ds / (1 - p); ds is x's gradient (or parked in an armed GradAdd)."""
 
     @staticmethod
     def forward(ctx, a, x, gamma, beta, eps, p, handoff=None, grad_in=None):
@@ -159,12 +159,13 @@ class _DropAddLNFn(torch.autograd.Function):
             dy2, h.grad = h.grad, None
             if dy2 is not None:
                 dy2 = dy2.contiguous().to(s.dtype)
-        ds = native().layernorm_bwd(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd, dg, db, dy2)
+        # one kernel writes ds and the dropout branch's da = keep * ds / (1 - p)
+        ds, da = native().layernorm_bwd_drop(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd, dg, db, dy2,
+                                             ctx.p, ctx.seed)
         if own_g:
             _ready(gamma)
         if own_b:
             _ready(beta)
-        da = native().dropout_add(ds, None, ctx.p, ctx.seed)
         dx = ds
         if ctx.handoff is not None:
             hh = ctx.handoff

@@ -14,3 +14,11 @@ for l in open('gpurun_out/misc/wg_bert_$wg.log'):
         r=json.loads(l); print('  bert', r['M'], r['N'], r['K'], r['zoo_wgrad256']['us'], 'us')
 "
 done
+# BERT-base b128: fused residual LayerNorm on / off (same box)
+for f in 1 0 1; do
+  ZOO_DROP_LN_FUSE=$f timeout -k 10 240 python -u analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 30 > gpurun_out/misc/bert_dln$f.log 2>&1 || exit 5
+  echo "DROP_LN_FUSE=$f $(tail -1 gpurun_out/misc/bert_dln$f.log)"
+done
+# int8 / fp8 inference: throughput + top-1 agreement with bf16
+timeout -k 10 400 python -u analytics-zoo_amd/tools/quant_bench.py --batch 256 --iters 20 > gpurun_out/misc/quant.log 2>&1 || exit 6
+tail -6 gpurun_out/misc/quant.log
