@@ -85,7 +85,7 @@ __global__ __launch_bounds__(256) void prob_nll_kernel(const T* __restrict__ pro
       const bool pass = valid && p >= eps && p <= 1.f;
       for (int j = 0; j < NC; ++j) dp[(size_t)row * NC + j] = (pass && j == lab) ? -1.f / pc : 0.f;
     }
-    if (per_row) {
+    if (per_row == 1) {  // (per_row 2: loss_sum / count are the [gridDim] block partials)
       loss_sum[row] = lr;
       count[row] = cr;
     }
