@@ -737,8 +737,16 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   // GEMMs where the 256x256-tile kernel (wgrad256.hip) beats the implicit-GEMM wgrad
   // (tools/wgrad_bench.py --resnet: 1.1-1.6x; at 802816 pixels the 128-row tiles win)
   static const bool use256 = env_flag("ZOO_WGRAD256", true);
-  if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= 128 && g.C >= 128 &&
-      g.M <= (1 << 18) &&
+  static const long long m_max = [] {
+    const char* e = getenv("ZOO_WGRAD256_MMAX");
+    return e ? atoll(e) : (1LL << 18);
+  }();
+  static const int c_min = [] {
+    const char* e = getenv("ZOO_WGRAD256_CMIN");
+    return e ? atoi(e) : 128;
+  }();
+  if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= c_min && g.C >= c_min &&
+      g.M <= m_max &&
       x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
     linear_wgrad(dy.view({(int64_t)g.M, g.K}), x.view({(int64_t)g.M, g.C}), dw);
     return;

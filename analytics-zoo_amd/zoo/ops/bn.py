@@ -19,7 +19,7 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
-from zoo.ops import _kern, workspace
+from zoo.ops import _kern, workspace, wstream
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
 
@@ -214,9 +214,10 @@ class _ConvBNActFn(torch.autograd.Function):
                 ctx.dx_out.grad = dx
                 dx = None
         gw, own_w = _grad_target(w)
-        C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
-        if own_w:
-            _notify(w)
+        with wstream.wgrad(dy.device, x, dy, on=own_w):
+            C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
+            if own_w:
+                _notify(w)
         if own_g:
             _notify(gamma)
         if own_b:
@@ -326,9 +327,10 @@ class _ConvStatsFn(torch.autograd.Function):
                 ctx.dx_out.grad = dx
                 dx = None
         gw, own_w = _grad_target(w)
-        C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
-        if own_w:
-            _notify(w)
+        with wstream.wgrad(dy.device, x, dy, on=own_w):
+            C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
+            if own_w:
+                _notify(w)
         return dx, None if own_w else gw.to(w.dtype), None, None, None, None, None, None, None
 
 

@@ -23,7 +23,7 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
-from zoo.ops import _kern
+from zoo.ops import _kern, wstream
 
 ACT_CODES = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
 
@@ -398,12 +398,14 @@ class _LinearNativeFn(torch.autograd.Function):
         if ctx.needs_input_grad[1]:
             gbuf = getattr(w, "_zoo_grad", None)
             g2 = gbuf.view(N, K) if gbuf is not None else torch.zeros(N, K, device=dy.device, dtype=torch.float32)
-            native().linear_wgrad(dy, x2, g2)
-            if gbuf is not None:
-                hook = getattr(w, "_zoo_grad_ready", None)
-                if hook is not None:
-                    hook(w)
-            else:
+            # engine-owned gradient: on the weight-gradient side stream (zoo.ops.wstream)
+            with wstream.wgrad(dy.device, dy, x2, on=gbuf is not None):
+                native().linear_wgrad(dy, x2, g2)
+                if gbuf is not None:
+                    hook = getattr(w, "_zoo_grad_ready", None)
+                    if hook is not None:
+                        hook(w)
+            if gbuf is None:
                 dw = g2.to(w.dtype)
         return dx, dw, db, None, None, None, None, None
 

@@ -81,6 +81,7 @@ import torch
 import torch.distributed as dist
 
 from zoo.parallel.flat import FlatParams
+from zoo.ops import wstream
 
 CHUNK_ALIGN = 64
 # step counter for the row-sparse id records (bumped by GradSync.reset): an embedding lookup
@@ -362,8 +363,11 @@ class GradSync:
         if self.comm_stream is not None:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(self.flat.grad.device))
+            side = wstream.pending(self.flat.grad.device)
             with torch.cuda.stream(self.comm_stream):
                 self.comm_stream.wait_event(ev)
+                if side is not None:   # weight gradients still running on the side stream
+                    self.comm_stream.wait_stream(side)
                 if self.collect_stats:
                     b.ev0 = torch.cuda.Event(enable_timing=True)
                     b.ev1 = torch.cuda.Event(enable_timing=True)

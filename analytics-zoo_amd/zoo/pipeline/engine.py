@@ -32,7 +32,7 @@ import torch
 from zoo.common.triggers import EveryEpoch, MaxEpoch, Trigger
 from zoo.parallel.ddp import GradSync
 from zoo.parallel.flat import FlatParams
-from zoo.ops import workspace
+from zoo.ops import workspace, wstream
 
 log = logging.getLogger("zoo.engine")
 
@@ -269,7 +269,10 @@ class TrainingEngine:
         try:
             out = self.forward_fn(self.model, inputs)
             loss = self.criterion(out, target)
-            loss.backward()
+            # weight gradients overlap the data-gradient chain on a side stream, joined back
+            # before anything reads the gradients (zoo.ops.wstream)
+            with wstream.enabled(self.device):
+                loss.backward()
         finally:
             workspace.end_step()
         return loss.detach()
