@@ -319,16 +319,81 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
       else ++toff;
     }
   }
-  int cbuf = 0, sbuf = STAGES - 1;
-  if constexpr (!BAND) {
+  // Software-pipelined 2-stage loop (default for the 2-stage tiles; ConvGeom.dbg bit 16 = the
+  // plain loop below, ZOO_I2_PIPE=0): the fragment reads of k-half 1 of tile kt run in the MFMA
+  // gaps of k-half 0, and the reads of k-half 0 of tile kt+1 in the gaps of k-half 1 -- the
+  // barrier sits between the two halves, so no wave ever waits on an LDS read with its MFMA
+  // pipe empty (the plain loop issues all 2 x (TM + TN) reads, more than the 4-bit lgkmcnt can
+  // track, then its MFMAs: two exposed LDS latencies per K-tile, on every wave at once).
+  //   tile kt+2 is staged right after barrier kt into the buffer tile kt vacated (every wave's
+  //   reads of it retired by lgkmcnt(0) before that barrier) and must land by barrier kt+1.
+  if constexpr (!BAND && STAGES == 2) {
+    if (!(g.dbg & 16)) {
+      const char* abase = smem + (wm * WTM) * 128 + rl;
+      const char* bbase = smem + (BM + wn * WTN) * 128 + rl;
+      // A fragments of rows 0..TM-2 single-buffered and replaced in place (row i's next fragment
+      // is read one MFMA after row i's last use); the last row and the B fragments double-
+      // buffered, so every read of the other half issues in an MFMA gap of this one: 28 fewer
+      // VGPRs than two full fragment sets, which the 128-accumulator 256x256 tile cannot spare
+      bf16x8 pa[TM - 1], pl[2], pb[2][TN];
+      auto rda = [&](int buf, int kk, int i) {
+        const bf16x8 v = *reinterpret_cast<const bf16x8*>(abase + buf * SB + i * 2048 + (kk ? co1 : co0));
+        if (i == TM - 1) pl[kk] = v; else pa[i] = v;
+      };
+      auto rdb = [&](int buf, int kk, int j) {
+        pb[kk][j] = *reinterpret_cast<const bf16x8*>(bbase + buf * SB + j * 2048 + (kk ? co1 : co0));
+      };
+      // the TM x TN MFMAs of k-half kk (row-major); when rdo, the other half's fragments from
+      // buffer rbuf are read in its gaps: B j after MFMA j, the last A row after MFMA TN, A row
+      // i < TM-1 after MFMA (i+1)*TN (hipcc's counted lgkmcnt waits order every use)
+      auto half = [&](int kk, bool rdo, int rbuf, int rkk) {
 #pragma unroll
-  for (int s = 0; s < STAGES - 1; ++s)
-    if (s < nk) stage(s);
-  if (STAGES == 3 && nk > 1) i2_wait_vm<DPT>();
-  else i2_wait_vm<0>();
-  __builtin_amdgcn_s_barrier();
+        for (int q = 0; q < TM * TN; ++q) {
+          const int i = q / TN, j = q - (q / TN) * TN;
+          acc[i][j] = mfma16(i == TM - 1 ? pl[kk] : pa[i < TM - 1 ? i : 0], pb[kk][j], acc[i][j]);
+          if (rdo) {
+            if (q < TN) rdb(rbuf, rkk, q);
+            if (q == TN) rda(rbuf, rkk, TM - 1);
+            if (q >= TN && q % TN == 0) rda(rbuf, rkk, q / TN - 1);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      };
+      stage(0);
+      if (nk > 1) stage(1);
+      if (nk > 1) i2_wait_vm<DPT>(); else i2_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+#pragma unroll
+      for (int j = 0; j < TN; ++j) rdb(0, 0, j);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) rda(0, 0, i);
+      for (int kt = 0; kt < nk; ++kt) {
+        const int buf = kt & 1;
+        half(0, true, buf, 1);
+        // tile kt+1 (the only DMA in flight) has landed and no wave still reads tile kt
+        i2_wait_vm<0>();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        if (kt + 2 < nk) stage(buf);
+        half(1, kt + 1 < nk, buf ^ 1, 0);
+      }
+      // every wave's ring reads retired before the last barrier and the final half issues none:
+      // the epilogue may reuse the ring without another barrier
+    }
   }
-  for (int kt = 0; kt < (BAND ? 0 : nk); ++kt) {
+  int cbuf = 0, sbuf = STAGES - 1;
+  const bool plain = !BAND && !(STAGES == 2 && !(g.dbg & 16));
+  if constexpr (!BAND) {
+    if (plain) {
+#pragma unroll
+      for (int s = 0; s < STAGES - 1; ++s)
+        if (s < nk) stage(s);
+      if (STAGES == 3 && nk > 1) i2_wait_vm<DPT>();
+      else i2_wait_vm<0>();
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  for (int kt = 0; kt < (plain ? nk : 0); ++kt) {
     const bool issue = kt + STAGES - 1 < nk;
     if (issue) stage(sbuf);
     compute(cbuf);
@@ -858,8 +923,14 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
     gb.dbg = dbg;
     return i2_tile<I2_AM_BAND>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, gb, act, bs, st);
   }
+  static const int pipe = [] {
+    const char* e = getenv("ZOO_I2_PIPE");
+    return e ? atoi(e) : 1;
+  }();
+  ConvGeom gp = *g;
+  gp.dbg = pipe ? 0 : 16;  // bit 16: the plain (unpipelined) 2-stage loop
   if (is1x1)
-    return i2_tile<I2_AM_1X1>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs, st);
-  return i2_tile<I2_AM_IMPLICIT>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, *g, act, bs,
+    return i2_tile<I2_AM_1X1>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, gp, act, bs, st);
+  return i2_tile<I2_AM_IMPLICIT>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, gp, act, bs,
                                  st);
 }
