@@ -28,6 +28,10 @@ _enabled = set()  # device indices inside an engine backward
 _used = set()     # device indices with side work not yet joined
 
 
+def on():
+    return _ON
+
+
 def _stream(idx):
     s = _side.get(idx)
     if s is None:
@@ -73,6 +77,16 @@ def wgrad(dev, *reads, on=True):
         if t is not None and t.is_cuda:
             t.record_stream(s)
     _used.add(idx)
+
+
+def side_for(dev):
+    """The side stream of ``dev`` (created on first use)."""
+    return _stream(dev.index if dev.index is not None else torch.cuda.current_device())
+
+
+def mark_used(dev):
+    """Work was issued on the side stream outside ``wgrad`` (the in-backward optimizer)."""
+    _used.add(dev.index if dev.index is not None else torch.cuda.current_device())
 
 
 def pending(dev):

@@ -208,6 +208,12 @@ class GradSync:
         self.collect_stats = False
         self.stats = {"steps": 0, "exposed_ms": 0.0, "bucket_ms": {}, "bucket_bytes": {}}
         self._wait_ev = None
+        # in-backward optimizer (world 1, see enable_ibo): each bucket's update is issued on the
+        # weight-gradient side stream as soon as its last gradient contribution is in
+        self.ibo_optim = None
+        self.ibo_steps = 0
+        self._ibo_done = set()
+        self._ibo_cleared = True
         self._install_hooks()
         self.reset()
 
@@ -313,8 +319,20 @@ class GradSync:
             if hasattr(p, "register_post_accumulate_grad_hook"):
                 p._zoo_sync_hook = p.register_post_accumulate_grad_hook(self._ready)
 
+    def enable_ibo(self, optim):
+        """In-backward optimizer for a single-rank job: the update of bucket b runs on the
+        weight-gradient side stream (zoo.ops.wstream) once every parameter of b has received
+        the gradient contributions counted in the calibration step, overlapping the backward of
+        the remaining layers (a layer's weights are never read again in a backward after their
+        last gradient contribution). ``optim`` must support element ranges (supports_ranges)."""
+        if self.comm or not self.is_cuda:
+            return False
+        self.ibo_optim = optim
+        return True
+
     def reset(self):
         self._counts = {}
+        self._ibo_done = set()
         _TOUCH_STEP[0] += 1
         for b in self.buckets:
             if self._expected is None or b.sparse:
@@ -328,6 +346,8 @@ class GradSync:
 
     def _ready(self, p):
         if not self.comm:
+            if self.ibo_optim is not None:
+                self._ibo_ready(p)
             return
         with self._lock:
             pid = id(p)
@@ -521,6 +541,59 @@ class GradSync:
         if self.shard_master is not None:
             self.load_shard_from_master()
 
+    def _ibo_ready(self, p):
+        pid = id(p)
+        c = self._counts.get(pid, 0) + 1
+        self._counts[pid] = c
+        if self._expected is None:
+            return   # calibration step: counting only
+        b = self.param_bucket.get(pid)
+        if b is None or b.pending <= 0:
+            return
+        exp = self._expected.get(pid, 0)
+        if c > exp:
+            if b.launched:
+                raise RuntimeError(
+                    "GradSync: parameter %s got %d gradient contributions this step but %d in the calibration "
+                    "step, after its in-backward update ran; dynamic graphs need ZOO_OPTIM_IN_BWD=0"
+                    % (tuple(p.shape), c, exp))
+            b.pending = -1   # more contributions than calibrated: this bucket waits for step()
+            return
+        if c == exp:
+            b.pending -= 1
+            if b.pending == 0:
+                self._ibo_launch(b)
+
+    def _ibo_launch(self, b):
+        from zoo.ops import wstream
+        flat, dev = self.flat, self.flat.grad.device
+        side = wstream.side_for(dev) if wstream.active(dev) else None
+        if side is None:
+            return   # outside the engine's backward scope: step() updates it
+        side.wait_stream(torch.cuda.current_stream(dev))   # BN / bias gradients written on the compute stream
+        with torch.cuda.stream(side):
+            cl = self.ibo_optim.step_range(flat.master, flat.grad, flat.bf16, 1.0, b.lo, b.hi, zero_grad=True)
+        self._ibo_cleared = self._ibo_cleared and bool(cl)
+        wstream.mark_used(dev)
+        b.launched = True
+        self._ibo_done.add(b.idx)
+
+    def _ibo_step(self):
+        """End of an in-backward-optimizer step: update the buckets not launched during the
+        backward (calibration step, extra contributions, no gradient), then bump the counters."""
+        flat = self.flat
+        if self._expected is None:
+            self._expected = dict(self._counts)
+        cleared = True
+        for b in self.buckets:
+            if b.idx not in self._ibo_done:
+                cleared &= bool(self.ibo_optim.step_range(flat.master, flat.grad, flat.bf16, 1.0, b.lo, b.hi,
+                                                          zero_grad=True))
+        flat.grad_clean = cleared and self._ibo_cleared
+        self._ibo_cleared = True
+        self.ibo_optim.finish_step(flat.bf16 is not None)
+        self.ibo_steps += 1
+
     def finish(self):
         """Called after backward: launch what is left, make the compute stream
         wait for every bucket's collectives."""
@@ -601,6 +674,10 @@ class GradSync:
         """finish comm, (clip), run the optimizer."""
         flat = self.flat
         gscale = 1.0 / self.world
+        if self.ibo_optim is not None and optim is self.ibo_optim and clip is None:
+            self._ibo_step()
+            self.reset()
+            return
         if self.mode == "sharded" and self.comm:
             self.finish()
             self._sharded_step(optim, gscale, clip)

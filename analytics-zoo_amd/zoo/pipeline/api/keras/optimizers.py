@@ -229,30 +229,48 @@ class OptimMethod:
     def step(self, master, grad, bf16=None, gscale=1.0, zero_grad=False):
         """Update ``master`` (fp32 flat tensor or shard) in place from ``grad``. With
         ``zero_grad`` the native kernels also clear ``grad`` (returns True when they did)."""
+        cleared = self.step_range(master, grad, bf16, gscale, 0, master.numel(), zero_grad)
+        self.finish_step(bf16 is not None)
+        return cleared
+
+    # in-backward updates (zoo.parallel.ddp.GradSync, world 1): the step as a sequence of
+    # element ranges issued while the backward still runs, then one counter bump
+    def supports_ranges(self):
+        """Elementwise native update: any sub-range of the flat buffers can be stepped alone."""
+        return bool(self._native_zero_grad) and getattr(self, "parts", None) is None
+
+    def step_range(self, master, grad, bf16, gscale, lo, hi, zero_grad=False):
+        """The update of elements [lo, hi) of this step (no counter bump: ``finish_step``)."""
         bufs = self._ensure_buffers(master.numel(), master.device)
         lr = self.current_lr()
         cleared = False
+        full = lo == 0 and hi == master.numel()
+        m, g = (master, grad) if full else (master[lo:hi], grad[lo:hi])
+        b16 = bf16 if (bf16 is None or full) else bf16[lo:hi]
+        bs = bufs if full else [t[lo:hi] for t in bufs]
         if master.is_cuda:
             if zero_grad and self._native_zero_grad:
                 native().optim_zero_grad(True)
                 try:
-                    self._step_native(master, grad, bf16, bufs, lr, float(gscale))
+                    self._step_native(m, g, b16, bs, lr, float(gscale))
                 finally:
                     native().optim_zero_grad(False)
                 cleared = True
             else:
-                self._step_native(master, grad, bf16, bufs, lr, float(gscale))
+                self._step_native(m, g, b16, bs, lr, float(gscale))
         else:
             with torch.no_grad():
-                self._step_torch(master, grad * gscale, bufs, lr)
-                if bf16 is not None:
-                    bf16.copy_(master)
-        if bf16 is not None:
+                self._step_torch(m, g * gscale, bs, lr)
+                if b16 is not None:
+                    b16.copy_(m)
+        return cleared
+
+    def finish_step(self, had_bf16=True):
+        if had_bf16:
             from zoo.ops._kern import bump_weights_epoch
             bump_weights_epoch()   # cached dgrad filter flips are stale now
         self.state["neval"] += 1
         self.state["evalCounter"] += 1
-        return cleared
 
     def optimize(self, flat, gscale=1.0):
         self.step(flat.master, flat.grad, flat.bf16, gscale)

@@ -198,6 +198,13 @@ class TrainingEngine:
         self.hip_graph = (cfg.hip_graph if hip_graph is None else bool(hip_graph)) and self.device.type == "cuda"
         self._graphs = {}
         self._graph_warm = {}
+        # single-rank jobs: each bucket's optimizer update runs on the weight-gradient side
+        # stream as soon as its gradients are final, overlapping the rest of the backward
+        # (GradSync.enable_ibo). Not under hipGraph capture (the update would be baked into the
+        # graph with this step's learning rate), not with gradient clipping (a global norm).
+        self.ibo = bool(os.environ.get("ZOO_OPTIM_IN_BWD", "1") != "0" and clip is None and not self.hip_graph and
+                        wstream.on() and getattr(optim_method, "supports_ranges", lambda: False)() and
+                        self.sync.enable_ibo(optim_method))
 
     # ------------------------------------------------------------------
     def _maybe_inject_fault(self):
@@ -217,6 +224,10 @@ class TrainingEngine:
         ranks learn of the failure together and reload the latest checkpoint.
         A failing collective raises :class:`CommFailure` (restart by the launcher)."""
         multi = self.sync.comm and self.sync.world > 1
+        if self.sync.ibo_optim is not None and (self.sync.ibo_optim is not self.optim or self.clip is not None or
+                                                self.hip_graph):
+            self.sync.ibo_optim = None   # optimizer / clipping / graph mode changed: plain end-of-step update
+            self.ibo = False
         self.model.train()
         ph = self.phases
         loss = None
