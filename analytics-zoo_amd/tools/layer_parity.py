@@ -46,12 +46,15 @@ def run(gmodel, cmodel, x, loss_fn, train=True):
     hooks = []
     order = []
     for name, mod in _leaves(gmodel):
-        def fwd(mod, inp, out, name=name):
+        def fwd(mod, inp, kw, out, name=name):
             if name not in rec:
                 order.append(name)
-                rec[name] = {"in": [t.detach().clone() for t in _tensors(inp)], "kw": None,
+                # keyword tensors too (e.g. a fused residual, ``unit(x, resid=r)``): the CPU twin
+                # must see the same inputs or a fused add reads as an O(1) forward error
+                kwt = {k: v.detach().clone() for k, v in (kw or {}).items() if torch.is_tensor(v)}
+                rec[name] = {"in": [t.detach().clone() for t in _tensors(inp)], "kw": kwt,
                              "out": [t.detach().clone() for t in _tensors(out)]}
-        hooks.append(mod.register_forward_hook(fwd))
+        hooks.append(mod.register_forward_hook(fwd, with_kwargs=True))
 
         def bwd(mod, gin, gout, name=name):
             if name in rec and "gout" not in rec[name]:
@@ -74,8 +77,9 @@ def run(gmodel, cmodel, x, loss_fn, train=True):
         xs = [t.float().cpu().requires_grad_(t.is_floating_point()) for t in r["in"]]
         for p in cm.parameters():
             p.grad = None
+        kws = {k: v.float().cpu() for k, v in (r["kw"] or {}).items()}
         try:
-            y = cm(*xs)
+            y = cm(*xs, **kws)
         except Exception as e:  # noqa: BLE001
             rows.append({"layer": name, "type": type(cm).__name__, "error": str(e)[:200]})
             continue

@@ -33,7 +33,7 @@ def main():
     ap.add_argument("--batch", type=int, default=256)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-dynamic", action="store_true")
-    ap.add_argument("--train-steps", type=int, default=80)
+    ap.add_argument("--train-steps", type=int, default=300)
     a = ap.parse_args()
     torch.manual_seed(0)
     m = resnet50().cuda().eval()
@@ -60,13 +60,13 @@ def main():
                                                                                dim=0).item(), 4)
     res["fp8_vs_bf16_top1_agree"] = round((outf.argmax(1) == ref.argmax(1)).float().mean().item(), 4)
     # agreement on a model with real decision margins: ResNet-50 fitted to the synthetic task of
-    # zoo.utils.synthetic at 224x224 (the random-init numbers above are kept for continuity; a
+    # zoo.utils.synthetic at 128x128 (as tests/test_gpu_qconv.py) (the random-init numbers above are kept for continuity; a
     # random net's top-1 flips on noise)
     from zoo.utils.synthetic import agreement, class_templates, sample, train_briefly
     torch.manual_seed(0)
     mt = resnet50(num_classes=16).cuda()
-    T = class_templates(16, 224, device="cuda")
-    res["trained_task_acc"] = round(train_briefly(mt, T, steps=a.train_steps, batch=32), 4)
+    T = class_templates(16, 128, device="cuda")
+    res["trained_task_acc"] = round(train_briefly(mt, T, steps=a.train_steps), 4)
     cal, _ = sample(T, 64, seed=11)
     xt, _ = sample(T, 256, seed=12)
     with torch.no_grad():

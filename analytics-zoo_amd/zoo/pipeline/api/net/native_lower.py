@@ -421,7 +421,9 @@ def _fuse(conv, bn=None, act_mod=None):
     """conv [-> eval BatchNorm] [-> activation] as ONE native conv: the conv carries the BN and the
     activation, the absorbed modules pass their input through."""
     to_twin(conv)
-    conv._zoo_bn = bn
+    # a plain attribute, not a registered submodule: the BN stays where it is in the module tree
+    # and the state dict keeps its original keys (the lowering is a class swap only)
+    object.__setattr__(conv, "_zoo_bn", bn)
     conv._zoo_cache = None
     if bn is not None:
         to_twin(bn)

@@ -36,9 +36,11 @@ def sample(templates, n, seed=1, noise=0.5):
     return x.to(templates.device), y.to(templates.device)
 
 
-def train_briefly(model, templates, steps=60, batch=32, lr=0.05, seed=2):
+def train_briefly(model, templates, steps=300, batch=32, lr=0.01, seed=2):
     """Fit ``model`` (a zoo image classifier, NCHW input) to the synthetic task with the
-    framework's own training engine; returns the accuracy on a fresh batch."""
+    framework's own training engine; returns the accuracy on a fresh batch. (ResNet-50 from
+    scratch, batch 32 at 128x128: 300 steps at lr 0.01 reach 1.0; 80 steps at lr 0.05 diverge
+    early and stay near chance -- scripts/r4/dbg_fail.sh sweep.)"""
     from zoo.ops import softmax_cross_entropy
     from zoo.pipeline.api.keras.optimizers import SGD
     from zoo.pipeline.engine import TrainingEngine

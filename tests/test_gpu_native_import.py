@@ -190,6 +190,11 @@ def test_torchnet_lstm_native(gpu):
     out.backward()
     ref(x)[0].pow(2).sum().backward()
     for (n, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        if q.grad.norm() < 1e-8:
+            # e.g. the reverse direction's recurrent weights: only h[:, -1] (the reverse pass's FIRST
+            # step, from h0 = 0) reaches the loss, so their true gradient is exactly zero
+            assert p.grad.abs().max() < 1e-6, (n, p.grad.abs().max())
+            continue
         cos = F.cosine_similarity(p.grad.flatten().float(), q.grad.flatten().float(), dim=0).item()
         assert cos > 0.97, (n, cos)
 

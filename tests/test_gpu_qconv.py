@@ -40,7 +40,7 @@ def trained_resnet50(gpu):
     torch.manual_seed(0)
     m = resnet50(num_classes=16).to(gpu)
     T = class_templates(16, 128, device=gpu)
-    acc = train_briefly(m, T, steps=80, batch=32)
+    acc = train_briefly(m, T)
     assert acc > 0.9, acc
     return m, T
 

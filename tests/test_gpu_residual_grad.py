@@ -56,14 +56,15 @@ def test_stacked_blocks_with_layernorm_grad_add(gpu, monkeypatch):
                               sa._Block(256, 4, 1024, 0.1, 0.1, 0.02)).to(gpu).train()
     x = torch.randn(8, 128, 256, device=gpu).to(torch.bfloat16)
     parked = []
-    ln_fn = importlib.import_module("zoo.ops.nn")._LayerNormFn
-    orig = ln_fn.backward
-
-    def spy(ctx, dy):
-        if ctx.grad_in is not None and ctx.grad_in.grad is not None:
-            parked.append(1)
-        return orig(ctx, dy)
-    monkeypatch.setattr(ln_fn, "backward", staticmethod(spy))
+    nnm = importlib.import_module("zoo.ops.nn")
+    # the residual LayerNorms run as the fused dropout-add LayerNorm (ZOO_DROP_LN_FUSE) or as
+    # plain LayerNorms: count a parked gradient in either backward
+    for fn in (nnm._LayerNormFn, nnm._DropAddLNFn):
+        def spy(ctx, dy, orig=fn.backward):
+            if ctx.grad_in is not None and ctx.grad_in.grad is not None:
+                parked.append(1)
+            return orig(ctx, dy)
+        monkeypatch.setattr(fn, "backward", staticmethod(spy))
     gx0, g0 = _grads(blk, x, False, monkeypatch)
     assert not parked
     gx1, g1 = _grads(blk, x, True, monkeypatch)
