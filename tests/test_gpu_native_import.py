@@ -152,6 +152,11 @@ def test_torchnet_cnn_inference_and_training(gpu):
     _check_native(names)
     F.cross_entropy(ref(x), y).backward()
     for (n, p), (_, q) in zip(net.module.named_parameters(), ref.named_parameters()):
+        if q.grad.abs().max() < 1e-5:
+            # a conv bias feeding a training-mode BatchNorm: the batch mean removes it, so its
+            # true gradient is zero (the fp32 reference holds rounding noise; cosine is meaningless)
+            assert p.grad.abs().max() < 1e-3, (n, p.grad.abs().max())
+            continue
         cos = F.cosine_similarity(p.grad.flatten().float(), q.grad.flatten().float(), dim=0).item()
         assert cos > 0.98, (n, cos)
     for a, b in zip(net.module.modules(), ref.modules()):
