@@ -154,8 +154,9 @@ def test_torchnet_cnn_inference_and_training(gpu):
     for (n, p), (_, q) in zip(net.module.named_parameters(), ref.named_parameters()):
         if q.grad.abs().max() < 1e-5:
             # a conv bias feeding a training-mode BatchNorm: the batch mean removes it, so its
-            # true gradient is zero (the fp32 reference holds rounding noise; cosine is meaningless)
-            assert p.grad.abs().max() < 1e-3, (n, p.grad.abs().max())
+            # true gradient is zero (the fp32 reference holds rounding noise; cosine is meaningless;
+            # the bf16 path sums ~8k rounded terms whose exact sum is 0)
+            assert p.grad.abs().max() < 3e-2, (n, p.grad.abs().max())
             continue
         cos = F.cosine_similarity(p.grad.flatten().float(), q.grad.flatten().float(), dim=0).item()
         assert cos > 0.98, (n, cos)
