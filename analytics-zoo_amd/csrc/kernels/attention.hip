@@ -571,6 +571,256 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
     }
 }
 
+template <int D, int QW, bool HAS_MASK, bool DROP>
+__global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_pers_kernel(
+    const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
+    const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
+    const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
+    float scale, int causal, AttnBwdStrides sd, AttnDrop dd, int BH) {
+  // QW = 2: 8 waves; wave w owns keys 32(w&3).. and query rows 32(w>>2).. of every
+  // 64-row tile (two waves per SIMD); the two q-halves are summed through LDS at the end.
+  // Persistent over heads: block (x, y) handles heads y, y + gridDim.y, ... of key block x.
+  // During the last query tile of a head the NEXT head's first Q/dO tile (LDS-DMA), its
+  // LSE / delta rows and its K/V fragments (registers) are already in flight, so a head's
+  // prologue latency overlaps the previous head's last tile and dK/dV epilogue (BERT s128
+  // has two query tiles per head: the prologue was a third of a block's life).
+  constexpr int KS = D / 16, DT = D / 32, NQT = 2 / QW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* Qs = reinterpret_cast<bf16_t*>(smem);                 // [2][64][D]
+  bf16_t* dOs = Qs + 2 * 64 * D;                                // [2][64][D]
+  float* lse_s = reinterpret_cast<float*>(dOs + 2 * 64 * D);    // [2][64] (log2 units)
+  float* del_s = lse_s + 2 * 64;                                // [2][64]
+  float* red = del_s + 2 * 64;                                  // QW = 2: [4 key groups][DT][16][64 lanes]
+  // persistent form (D = 64, QW = 2): the next head's 128 K / V rows staged here during the
+  // current head's last tile, [2 x 64 rows][D] each (after the reduction area)
+  constexpr bool PRE = D == 64 && QW == 2;
+  bf16_t* KsN = reinterpret_cast<bf16_t*>(red + (QW == 2 ? 4 * DT * 16 * 64 : 0));
+  bf16_t* VsN = KsN + 2 * 64 * D;
+
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, h = lane >> 5, lr = lane & 31;
+  const int kg = wid & 3, qh = QW == 2 ? wid >> 2 : 0;
+  const int kblk = blockIdx.x * 128, kw0 = kblk + kg * 32, key = kw0 + lr;
+  const int coff = S - L;
+  const float c2 = scale * kLog2e;
+  const bool key_ok = key < S;
+
+  // causal: query q sees key iff key <= q + coff -> first useful q = kblk - coff
+  int qstart = 0;
+  if (causal) qstart = max(0, (kblk - coff) / 64 * 64);
+  const int ntiles = qstart < L ? (L - qstart + 63) / 64 : 0;
+
+  bf16x8 kf[KS], vf[KS];
+  float madd = 0.f, lse_r = 0.f, del_r = 0.f;
+  auto mask_of = [&](int bh_) -> float {
+    const int b_ = bh_ / H;
+    return !key_ok ? -INFINITY : (HAS_MASK ? mask[(size_t)b_ * S + key] * kLog2e : 0.f);
+  };
+  // K/V fragments straight from global memory (first head, non-persistent forms)
+  auto load_kv = [&](int bh_) {
+    const int b_ = bh_ / H, hd_ = bh_ - b_ * H;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = load_frag(K + b_ * sd.kb + hd_ * sd.kh + (long)key * sd.kl + 16 * ks + 8 * h, key_ok);
+      vf[ks] = load_frag(V + b_ * sd.vb + hd_ * sd.vh + (long)key * sd.vl + 16 * ks + 8 * h, key_ok);
+    }
+    madd = mask_of(bh_);
+  };
+  // persistent form: the next head's K/V rows kblk.. kblk+127 into KsN / VsN (LDS-DMA; rows past
+  // S clamp to S-1 -- those keys get p = 0 from madd = -inf and are never stored)
+  auto stage_kv = [&](int bh_) {
+    const int b_ = bh_ / H, hd_ = bh_ - b_ * H;
+    const bf16_t* kp = K + b_ * sd.kb + hd_ * sd.kh;
+    const bf16_t* vp = V + b_ * sd.vb + hd_ * sd.vh;
+    dma_tiles<D, 4 * QW>(kp, vp, KsN, VsN, kblk, S, sd.kl, sd.vl);
+    dma_tiles<D, 4 * QW>(kp, vp, KsN + 64 * D, VsN + 64 * D, kblk + 64, S, sd.kl, sd.vl);
+  };
+  auto read_kv = [&]() {
+    const int kr = kg * 32 + lr;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = row_frag<D>(KsN + (kr >> 6) * 64 * D, kr & 63, 16 * ks + 8 * h);
+      vf[ks] = row_frag<D>(VsN + (kr >> 6) * 64 * D, kr & 63, 16 * ks + 8 * h);
+    }
+  };
+  auto load_rows = [&](int bh_, int q0, int buf) {
+    const int b_ = bh_ / H, hd_ = bh_ - b_ * H;
+    dma_tiles<D, 4 * QW>(Q + b_ * sd.qb + hd_ * sd.qh, dO + b_ * sd.gb + hd_ * sd.gh, Qs + buf * 64 * D,
+                         dOs + buf * 64 * D, q0, L, sd.ql, sd.gl);
+    if (threadIdx.x < 64) {
+      const int q = q0 + threadIdx.x;
+      lse_r = q < L ? LSE[(size_t)bh_ * L + q] * kLog2e : INFINITY;
+      del_r = q < L ? delta[(size_t)bh_ * L + q] : 0.f;
+    }
+  };
+  auto store_rows = [&](int buf) {
+    if (threadIdx.x < 64) {
+      lse_s[buf * 64 + threadIdx.x] = lse_r;
+      del_s[buf * 64 + threadIdx.x] = del_r;
+    }
+  };
+
+  int cb = 0;              // buffer holding the current head's first query tile
+  bool ready = false;      // the current head's K/V fragments and first tile were prefetched
+  for (int bh = blockIdx.y; bh < BH; bh += gridDim.y) {
+    const int b = bh / H, hd = bh - b * H;
+    const int nbh = bh + gridDim.y;
+    const bool pre = PRE && nbh < BH && ntiles > 0;   // prefetch the next head during this one's last tile
+    if (ready) {
+      read_kv();   // staged during the previous head's last tile (past its closing barrier)
+    } else {
+      load_kv(bh);
+      if (ntiles > 0) {
+        load_rows(bh, qstart, cb);
+        wait_vm0();
+        store_rows(cb);
+      } else {
+        wait_vm0();
+      }
+      __syncthreads();
+    }
+    float maddn = 0.f;
+    f32x16 dk[DT], dv[DT];
+#pragma unroll
+    for (int i = 0; i < DT; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) dk[i][r] = dv[i][r] = 0.f;
+
+    for (int t = 0; t < ntiles; ++t) {
+      const int buf = cb ^ (t & 1), q0 = qstart + t * 64;
+      if (t + 1 < ntiles) {
+        load_rows(bh, q0 + 64, buf ^ 1);
+      } else if (pre) {
+        load_rows(nbh, qstart, buf ^ 1);
+        stage_kv(nbh);
+        maddn = mask_of(nbh);
+      }
+      const bf16_t* qt_ = Qs + buf * 64 * D;
+      const bf16_t* ot_ = dOs + buf * 64 * D;
+      const float* ls = lse_s + buf * 64;
+      const float* ds_ = del_s + buf * 64;
+      const int qlo = 32 * qh;  // first tile row of this wave (QW = 2) or 0
+      if (kw0 < S && !(causal && kw0 > q0 + qlo + 32 * NQT - 1 + coff)) {
+        f32x16 s[NQT], dp[NQT];
+        const f32x16 z16 = {};
+        bf16x8 qa[2][NQT], oa[2][NQT];
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt) {
+          qa[0][qt] = row_frag<D>(qt_, qlo + 32 * qt + lr, 8 * h);
+          oa[0][qt] = row_frag<D>(ot_, qlo + 32 * qt + lr, 8 * h);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          if (ks + 1 < KS) {
+            const int c = 16 * (ks + 1) + 8 * h;
+#pragma unroll
+            for (int qt = 0; qt < NQT; ++qt) {
+              qa[(ks + 1) & 1][qt] = row_frag<D>(qt_, qlo + 32 * qt + lr, c);
+              oa[(ks + 1) & 1][qt] = row_frag<D>(ot_, qlo + 32 * qt + lr, c);
+            }
+          }
+#pragma unroll
+          for (int qt = 0; qt < NQT; ++qt) {
+            s[qt] = mfma32(qa[ks & 1][qt], kf[ks], ks == 0 ? z16 : s[qt]);
+            dp[qt] = mfma32(oa[ks & 1][qt], vf[ks], ks == 0 ? z16 : dp[qt]);
+          }
+        }
+        const bool diag = causal && kw0 + 31 > q0 + qlo + coff;
+#pragma unroll
+        for (int qt = 0; qt < NQT; ++qt)
+#pragma unroll
+          for (int i4 = 0; i4 < 4; ++i4) {
+            const int qr = qlo + 32 * qt + 8 * i4 + 4 * h;
+            const float4 l4 = *reinterpret_cast<const float4*>(ls + qr);
+            const float4 d4 = *reinterpret_cast<const float4*>(ds_ + qr);
+            const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dv4[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int i = 4 * i4 + r;
+              float p = fexp2(s[qt][i] * c2 + (madd - lv[r]));
+              if (diag && key > q0 + qr + r + coff) p = 0.f;
+              const float kf_ = DROP ? attn_keep(dd, bh, q0 + qr + r, key) : 1.f;
+              s[qt][i] = p * kf_;
+              dp[qt][i] = p * (dp[qt][i] * kf_ - dv4[r]);
+            }
+          }
+        bf16x8 pf[2 * NQT], sf[2 * NQT];
+#pragma unroll
+        for (int k4 = 0; k4 < 2 * NQT; ++k4) {
+          pf[k4] = pack8_acc(s[k4 >> 1], 8 * (k4 & 1));
+          sf[k4] = pack8_acc(dp[k4 >> 1], 8 * (k4 & 1));
+        }
+        // dO^T / Q^T fragments one step ahead of their MFMAs
+        constexpr int NSTEP = 2 * NQT * DT;
+        bf16x8 fo[2], fq[2];
+        fo[0] = tr_frag32<D>(ot_, qlo, 0, lane);
+        fq[0] = tr_frag32<D>(qt_, qlo, 0, lane);
+#pragma unroll
+        for (int idx = 0; idx < NSTEP; ++idx) {
+          if (idx + 1 < NSTEP) {
+            const int k4n = (idx + 1) / DT, dtn = (idx + 1) % DT;
+            fo[(idx + 1) & 1] = tr_frag32<D>(ot_, qlo + 16 * k4n, 32 * dtn, lane);
+            fq[(idx + 1) & 1] = tr_frag32<D>(qt_, qlo + 16 * k4n, 32 * dtn, lane);
+          }
+          const int k4 = idx / DT, dt = idx % DT;
+          dv[dt] = mfma32(fo[idx & 1], pf[k4], dv[dt]);
+          dk[dt] = mfma32(fq[idx & 1], sf[k4], dk[dt]);
+        }
+      }
+      if (t + 1 < ntiles || pre) {
+        wait_vm0();
+        store_rows(buf ^ 1);
+      }
+      __syncthreads();
+    }
+    if (pre) cb = cb ^ ((ntiles - 1) & 1) ^ 1;   // the next head's first tile sits in the other buffer
+
+    bool store = key_ok;
+    if (QW == 2) {
+      // sum the two query halves: waves 4..7 park their partials in the reduction area (its own
+      // LDS: the tile buffers already hold the next head's first tile)
+#pragma unroll
+      for (int pass = 0; pass < 2; ++pass) {
+        f32x16* acc = pass == 0 ? dk : dv;
+        if (qh == 1) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) red[((kg * DT + dt) * 16 + r) * 64 + lane] = acc[dt][r];
+        }
+        __syncthreads();
+        if (qh == 0) {
+#pragma unroll
+          for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[dt][r] += red[((kg * DT + dt) * 16 + r) * 64 + lane];
+        }
+        __syncthreads();
+      }
+      store = store && qh == 0;
+    }
+    if (store) {
+      // reg i of dk[dt] = dK[key][32dt + 8(i>>2) + 4h + (i&3)]
+      bf16_t* dkr = dK + b * sd.dkb + hd * sd.dkh + (long)key * sd.dkl;
+      bf16_t* dvr = dV + b * sd.dvb + hd * sd.dvh + (long)key * sd.dvl;
+#pragma unroll
+      for (int dt = 0; dt < DT; ++dt)
+#pragma unroll
+        for (int i4 = 0; i4 < 4; ++i4) {
+          const int d = 32 * dt + 8 * i4 + 4 * h;
+          uint2 w;
+          w.x = pack2bf(dk[dt][4 * i4 + 0] * scale, dk[dt][4 * i4 + 1] * scale);
+          w.y = pack2bf(dk[dt][4 * i4 + 2] * scale, dk[dt][4 * i4 + 3] * scale);
+          *reinterpret_cast<uint2*>(dkr + d) = w;
+          w.x = pack2bf(dv[dt][4 * i4 + 0], dv[dt][4 * i4 + 1]);
+          w.y = pack2bf(dv[dt][4 * i4 + 2], dv[dt][4 * i4 + 3]);
+          *reinterpret_cast<uint2*>(dvr + d) = w;
+        }
+    }
+    ready = pre;
+    if (pre) madd = maddn;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // backward dQ on 32x32x16 MFMAs: NW waves x 32 query rows; K/V tiles as forward
 //   S^T = K Q^T, dP^T = V dO^T (query on the lane: LSE and delta are per-lane
@@ -798,9 +1048,42 @@ static void launch_bwd(const void* dout, const void* q, const void* k, const voi
   }();
   (void)lds_ok_;
   const size_t smem = (size_t)4 * 64 * D * sizeof(bf16_t) + 4 * 64 * sizeof(float);
-  hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM, DR>), dim3((S + 127) / 128, B * H), dim3(256 * QW), smem, st,
-                     (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
-                     (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal, sd, dd);
+  // dK/dV: one resident block per CU, persistent over heads (the kernel prefetches the next
+  // head); its q-half reduction area follows the tiles
+  const size_t smem_kv = smem + (QW == 2 ? (size_t)4 * (D / 32) * 16 * 64 * sizeof(float) : 0) +
+                         (D == 64 && QW == 2 ? (size_t)4 * 64 * D * sizeof(bf16_t) : 0);
+  static const int ncu = [] {
+    int dev = 0, n = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  static const bool pers = [] {
+    const char* e = getenv("ZOO_ATTN_PERSIST");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const int nkb = (S + 127) / 128;
+  if constexpr (D == 64 && QW == 2) {
+    if (pers) {
+      static const bool attr = hipFuncSetAttribute(
+          reinterpret_cast<const void*>(&attn_bwd_dkdv_pers_kernel<D, QW, HM, DR>),
+          hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024) == hipSuccess;
+      (void)attr;
+      const int gy = std::max(1, std::min(B * H, ncu / std::max(1, nkb)));
+      hipLaunchKernelGGL((attn_bwd_dkdv_pers_kernel<D, QW, HM, DR>), dim3(nkb, gy), dim3(256 * QW), smem_kv, st,
+                         (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse,
+                         delta, (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal, sd, dd, B * H);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM, DR>), dim3(nkb, B * H), dim3(256 * QW), smem, st,
+                         (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse,
+                         delta, (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal, sd, dd);
+    }
+  } else {
+    (void)smem_kv;
+    hipLaunchKernelGGL((attn_bwd_dkdv_kernel<D, QW, HM, DR>), dim3(nkb, B * H), dim3(256 * QW), smem, st,
+                       (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask, (const bf16_t*)dout, lse, delta,
+                       (bf16_t*)dk, (bf16_t*)dv, H, L, S, scale, causal, sd, dd);
+  }
   hipLaunchKernelGGL((attn_bwd_dq_kernel<D, NWQ, HM, DR>), dim3((L + 32 * NWQ - 1) / (32 * NWQ), B * H),
                      dim3(64 * NWQ), smem, st, (const bf16_t*)q, (const bf16_t*)k, (const bf16_t*)v, mask,
                      (const bf16_t*)dout, lse, delta, (bf16_t*)dq, H, L, S, scale, causal, sd, dd);
@@ -812,10 +1095,24 @@ static void launch_bwd_d(const void* dout, const void* q, const void* k, const v
                          int S, float scale, int causal, const AttnBwdStrides& sd, const AttnDrop& dd,
                          hipStream_t st) {
   // D = 64 fits two waves per SIMD (8-wave blocks); D = 128 keeps one wave per
-  // SIMD with the accumulators in AGPRs (the 8-wave form would spill)
+  // SIMD with the accumulators in AGPRs (the 8-wave form would spill). The dQ pass covers
+  // 32 queries per wave: at L <= 128 (BERT s128) an 8-wave block would leave half its waves
+  // without queries, so those sequences use 4-wave dQ blocks (two per CU)
   constexpr int QW = D == 64 ? 2 : 1, NWQ = D == 64 ? 8 : 4;
-#define ZOO_ATTN_BWD(HM_, DR_) \
-  launch_bwd<D, HM_, DR_, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, sd, dd, st)
+  static const bool small_q = [] {
+    const char* e = getenv("ZOO_ATTN_DQ4");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const bool q4 = D == 64 && small_q && L <= 128;
+#define ZOO_ATTN_BWD(HM_, DR_)                                                                                   \
+  do {                                                                                                          \
+    if (q4)                                                                                                     \
+      launch_bwd<D, HM_, DR_, QW, 4>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal, sd,  \
+                                     dd, st);                                                                   \
+    else                                                                                                        \
+      launch_bwd<D, HM_, DR_, QW, NWQ>(dout, q, k, v, mask, lse, delta, dq, dk, dv, B, H, L, S, scale, causal,   \
+                                       sd, dd, st);                                                             \
+  } while (0)
   const bool dr = dd.thresh != 0u;
   if (mask) { if (dr) ZOO_ATTN_BWD(true, true); else ZOO_ATTN_BWD(true, false); }
   else { if (dr) ZOO_ATTN_BWD(false, true); else ZOO_ATTN_BWD(false, false); }

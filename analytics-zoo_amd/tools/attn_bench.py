@@ -37,8 +37,25 @@ def timeit(fn, iters):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--bert", action="store_true",
+                    help="BERT-base training shape (B 128, H 12, L 128, D 64, key mask) with / without "
+                         "probability dropout and at half / quarter batch: is the pass latency- or work-bound?")
     a = ap.parse_args()
     C = native()
+    if a.bert:
+        for B in (128, 64, 32):
+            for p in (0.0, 0.1):
+                q, k, v = (torch.randn(B, 12, 128, 64, device="cuda", dtype=torch.bfloat16) for _ in range(3))
+                mask = torch.zeros(B, 128, device="cuda")
+                mask[:, 100:] = -10000.0
+                o, lse = C.attn_fwd(q, k, v, mask, False, p, 7)
+                do = torch.randn_like(o)
+                tf = timeit(lambda: C.attn_fwd(q, k, v, mask, False, p, 7), a.iters)
+                tb = timeit(lambda: C.attn_bwd(do, q, k, v, mask, o, lse, False, p, 7), a.iters)
+                fl = 4.0 * B * 12 * 128 * 128 * 64
+                print("BERT B%d pdrop %.1f  fwd %.1f us %.0f TF | bwd %.1f us %.0f TF" %
+                      (B, p, tf * 1e3, fl / tf / 1e9, tb * 1e3, 2.5 * fl / tb / 1e9), flush=True)
+        return
     for B, H, L, D, causal in SHAPES:
         q, k, v = (torch.randn(B, H, L, D, device="cuda", dtype=torch.bfloat16) for _ in range(3))
         o, lse = C.attn_fwd(q, k, v, None, causal)
