@@ -668,6 +668,24 @@ extern "C" size_t zoo_layernorm_bwd_part_floats(int rows, int D, int f32) {
 
 // dY2 (nullable): a second output gradient added to dY inside the bf16 v2 kernel; the other
 // paths return hipErrorNotSupported for it (the caller then adds it first)
+// deferred dgamma / dbeta fold (zoo_layernorm_defer_fold(1)): the v2 backward leaves its block
+// partials in `part` and the caller folds them later with zoo_layernorm_fold -- on the
+// weight-gradient side stream, off the data-gradient chain
+static int g_ln_defer_fold = 0;
+extern "C" void zoo_layernorm_defer_fold(int on) { g_ln_defer_fold = on ? 1 : 0; }
+extern "C" int zoo_layernorm_bwd_v2_blocks(int rows, int D, int f32) {
+  return (f32 || !ln_v2_nch(D)) ? 0 : ln_v2_blocks(rows);
+}
+extern "C" hipError_t zoo_layernorm_fold(float* part, int rows, int D, float* dg, float* db, hipStream_t st) {
+  const int blocks = ln_v2_blocks(rows);
+  const int ng = (blocks + LN_FOLD_G - 1) / LN_FOLD_G;
+  float* lvl = part + (size_t)blocks * 2 * D;
+  hipLaunchKernelGGL(layernorm_part_fold1_kernel, dim3((2 * D + 63) / 64, ng), dim3(64), 0, st, part, blocks, 2 * D,
+                     lvl);
+  hipLaunchKernelGGL(layernorm_part_fold2_kernel, dim3((2 * D + 3) / 4), dim3(256), 0, st, lvl, ng, D, dg, db);
+  return hipGetLastError();
+}
+
 static hipError_t ln_bwd_impl(const void* dY, const void* X, int f32, const float* g, const float* mean,
                               const float* rstd, void* dX, float* dg, float* db, int rows, int D, float* part,
                               const void* dY2, const DropArgs& dr, hipStream_t st) {
@@ -688,7 +706,7 @@ static hipError_t ln_bwd_impl(const void* dY, const void* X, int f32, const floa
     else ZOO_LNB2(4);
 #undef ZOO_LNB2
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !pp) return e;
+    if (e != hipSuccess || !pp || g_ln_defer_fold) return e;   // deferred: zoo_layernorm_fold
     const int ng = (blocks + LN_FOLD_G - 1) / LN_FOLD_G;
     float* lvl = pp + (size_t)blocks * 2 * D;
     hipLaunchKernelGGL(layernorm_part_fold1_kernel, dim3((2 * D + 63) / 64, ng), dim3(64), 0, st, pp, blocks, 2 * D,

@@ -132,6 +132,9 @@ hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, h
 hipError_t zoo_add_bf16(const void*, const void*, void*, size_t, hipStream_t);
 hipError_t zoo_layernorm_fwd(const void*, int, const float*, const float*, void*, float*, float*, int, int, float,
                              hipStream_t);
+void zoo_layernorm_defer_fold(int);
+int zoo_layernorm_bwd_v2_blocks(int, int, int);
+hipError_t zoo_layernorm_fold(float*, int, int, float*, float*, hipStream_t);
 hipError_t zoo_layernorm_bwd_drop(const void*, const void*, const float*, const float*, const float*, void*, void*,
                                   float*, float*, int, int, float*, const void*, float, uint64_t, hipStream_t);
 hipError_t zoo_dropout_add_layernorm_fwd(const void*, const void*, const float*, const float*, void*, void*, float*,
@@ -1856,6 +1859,58 @@ std::vector<torch::Tensor> layernorm_bwd_drop(torch::Tensor dy, torch::Tensor x,
   return {dx, da};
 }
 
+// LayerNorm backward with the dgamma / dbeta fold left to the caller (layernorm_fold, typically
+// on the weight-gradient side stream): {dx, da (dropout branch, or empty), part}. bf16 v2 path
+// only (raises otherwise: the caller uses layernorm_bwd / layernorm_bwd_drop).
+std::vector<torch::Tensor> layernorm_bwd_split(torch::Tensor dy, torch::Tensor x, torch::Tensor g, torch::Tensor mean,
+                                               torch::Tensor rstd, c10::optional<torch::Tensor> dy2, double p,
+                                               int64_t seed, bool drop) {
+  req(dy, at::kBFloat16, "dy");
+  req(x, at::kBFloat16, "x");
+  req(g, at::kFloat, "gamma");
+  TORCH_CHECK(dy.is_contiguous() && x.is_contiguous() && dy.numel() == x.numel(), "layernorm_bwd_split: dy / x");
+  const int D = x.size(-1);
+  const int64_t rows = x.numel() / D;
+  TORCH_CHECK(D % 8 == 0 && mean.numel() == rows && rstd.numel() == rows && g.numel() == D, "layernorm_bwd_split: shapes");
+  TORCH_CHECK(zoo_layernorm_bwd_v2_blocks((int)rows, D, 0) > 0 && (reinterpret_cast<uintptr_t>(g.data_ptr()) & 15) == 0,
+              "layernorm_bwd_split: needs the bf16 v2 backward");
+  const void* d2 = nullptr;
+  if (dy2.has_value() && dy2->defined()) {
+    TORCH_CHECK(dy2->is_contiguous() && dy2->scalar_type() == at::kBFloat16 && dy2->numel() == dy.numel(),
+                "layernorm_bwd_split: dy2 must match dy");
+    d2 = dy2->data_ptr();
+  }
+  auto dx = torch::empty_like(x);
+  torch::Tensor da = drop ? torch::empty_like(x) : torch::empty({0}, x.options());
+  auto part = torch::empty({(int64_t)zoo_layernorm_bwd_part_floats((int)rows, D, 0)}, mean.options());
+  // dg / db pointers only switch the partial output on; nothing is folded into them here
+  float* dummy = part.data_ptr<float>();
+  zoo_layernorm_defer_fold(1);
+  hipError_t e;
+  if (drop)
+    e = zoo_layernorm_bwd_drop(dy.data_ptr(), x.data_ptr(), g.data_ptr<float>(), mean.data_ptr<float>(),
+                               rstd.data_ptr<float>(), dx.data_ptr(), da.data_ptr(), dummy, dummy, (int)rows, D,
+                               part.data_ptr<float>(), d2, (float)p, (uint64_t)seed, cur_stream());
+  else
+    e = zoo_layernorm_bwd(dy.data_ptr(), x.data_ptr(), 0, g.data_ptr<float>(), mean.data_ptr<float>(),
+                          rstd.data_ptr<float>(), dx.data_ptr(), dummy, dummy, (int)rows, D, part.data_ptr<float>(), d2,
+                          cur_stream());
+  zoo_layernorm_defer_fold(0);
+  check_hip(e, "layernorm_bwd_split");
+  return {dx, da, part};
+}
+
+void layernorm_fold(torch::Tensor part, int64_t rows, int64_t D, c10::optional<torch::Tensor> dg,
+                    c10::optional<torch::Tensor> db) {
+  req(part, at::kFloat, "part");
+  if (dg.has_value() && dg->defined()) { req(*dg, at::kFloat, "dgamma"); TORCH_CHECK(dg->numel() == D, "dg"); }
+  if (db.has_value() && db->defined()) { req(*db, at::kFloat, "dbeta"); TORCH_CHECK(db->numel() == D, "db"); }
+  TORCH_CHECK((size_t)part.numel() >= zoo_layernorm_bwd_part_floats((int)rows, (int)D, 0), "layernorm_fold: part size");
+  check_hip(zoo_layernorm_fold(part.data_ptr<float>(), (int)rows, (int)D, opt_ptr<float>(dg), opt_ptr<float>(db),
+                               cur_stream()),
+            "layernorm_fold");
+}
+
 torch::Tensor embedding_fwd(torch::Tensor table, torch::Tensor idx, int64_t pad) {
   TORCH_CHECK(table.is_cuda() && table.is_contiguous() && table.dim() == 2, "embedding: 2-D GPU table");
   req(idx, at::kLong, "indices");
@@ -2827,6 +2882,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("layernorm_fwd", &layernorm_fwd);
   m.def("dropout_add_layernorm_fwd", &dropout_add_layernorm_fwd);
   m.def("layernorm_bwd_drop", &layernorm_bwd_drop);
+  m.def("layernorm_bwd_split", &layernorm_bwd_split);
+  m.def("layernorm_fold", &layernorm_fold);
   m.def("layernorm_bwd", &layernorm_bwd, py::arg("dy"), py::arg("x"), py::arg("g"), py::arg("mean"),
         py::arg("rstd"), py::arg("dg"), py::arg("db"), py::arg("dy2") = py::none());
   m.def("embedding_fwd", &embedding_fwd);

@@ -46,12 +46,18 @@ def main():
         eng.train_step(xs, y)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(a.iters):
+        h0 = time.perf_counter()
         loss = eng.train_step(xs, y)
+        host += time.perf_counter() - h0
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    # host_ms_per_step: time the Python / launch side spends issuing a step (no device sync inside
+    # the loop): close to ms_per_step means the step is host-bound, well below means device-bound
     print('{"bench": "bert-base-finetune-train", "batch": %d, "seq": %d, "ms_per_step": %.3f, "seq_per_s": %.1f, '
-          '"tokens_per_s": %.0f, "loss": %.4f}' % (B, L, dt * 1e3, B / dt, B * L / dt, float(loss)))
+          '"tokens_per_s": %.0f, "loss": %.4f, "host_ms_per_step": %.3f}' % (B, L, dt * 1e3, B / dt, B * L / dt,
+                                                                         float(loss), host / a.iters * 1e3))
 
 
 if __name__ == "__main__":

@@ -364,15 +364,17 @@ class _LinearNativeFn(torch.autograd.Function):
             want_db = bool(ctx.has_bias and ctx.needs_input_grad[2])
             bbuf = getattr(bias, "_zoo_grad", None) if (want_db and bias is not None) else None
             z = y if ctx.act == "relu" else (pre if ctx.act == "gelu" else None)
-            outs = native().act_bwd_reduce(dy, z, want_db, bbuf, ctx.act == "gelu")
-            dy = outs[0]
-            if want_db:
-                if bbuf is not None:
+            # no activation: the pass only sums dy's columns into the engine-owned bias gradient,
+            # nothing on the data-gradient path waits for it -> weight-gradient side stream
+            with wstream.wgrad(dy.device, dy, on=z is None and bbuf is not None):
+                outs = native().act_bwd_reduce(dy, z, want_db, bbuf, ctx.act == "gelu")
+                if want_db and bbuf is not None:
                     hook = getattr(bias, "_zoo_grad_ready", None)
                     if hook is not None:
                         hook(bias)
-                else:
-                    db = outs[1].to(bias.dtype)
+            dy = outs[0]
+            if want_db and bbuf is None:
+                db = outs[1].to(bias.dtype)
         ga = ctx.grad_add
         resid = None
         if ga is not None and ga.grad is not None:

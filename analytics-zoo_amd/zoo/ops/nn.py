@@ -22,6 +22,27 @@ def _ready(p):
         h(p)
 
 
+def _split_fold_ok(x, gamma, own_g, own_b):
+    """LayerNorm backward can leave its dgamma / dbeta fold to the weight-gradient side stream:
+    engine-owned gradients inside the engine's backward, bf16 rows on the v2 kernel."""
+    from zoo.ops import wstream
+    D = x.shape[-1]
+    return (own_g and own_b and x.is_cuda and x.dtype == torch.bfloat16 and D % 4 == 0 and D <= 1024 and
+            gamma.data_ptr() % 16 == 0 and _LN_V2 and wstream.active(x.device))
+
+
+_LN_V2 = __import__("os").environ.get("ZOO_LN_BWD_V2", "1") != "0"
+
+
+def _fold_on_side(part, x, dg, db, gamma, beta):
+    from zoo.ops import wstream
+    D = x.shape[-1]
+    with wstream.wgrad(x.device, part):
+        native().layernorm_fold(part, x.numel() // D, D, dg, db)
+        _ready(gamma)
+        _ready(beta)
+
+
 class _LayerNormFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, eps, grad_in=None):
@@ -44,6 +65,11 @@ class _LayerNormFn(torch.autograd.Function):
             dy2, h.grad = h.grad, None
             if dy2 is not None:
                 dy2 = dy2.contiguous().to(x.dtype)
+        if gamma is not None and beta is not None and _split_fold_ok(x, gamma, own_g, own_b):
+            dx, _, part = native().layernorm_bwd_split(dy.contiguous().to(x.dtype), x, gamma.detach(), mean, rstd,
+                                                       dy2, 0.0, 0, False)
+            _fold_on_side(part, x, dg, db, gamma, beta)
+            return dx, None, None, None, None
         dx = native().layernorm_bwd(dy.contiguous().to(x.dtype), x, None if gamma is None else gamma.detach(), mean,
                                     rstd, dg, db, dy2)
         if own_g:
@@ -159,13 +185,19 @@ class _DropAddLNFn(torch.autograd.Function):
             dy2, h.grad = h.grad, None
             if dy2 is not None:
                 dy2 = dy2.contiguous().to(s.dtype)
-        # one kernel writes ds and the dropout branch's da = keep * ds / (1 - p)
-        ds, da = native().layernorm_bwd_drop(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd, dg, db, dy2,
-                                             ctx.p, ctx.seed)
-        if own_g:
-            _ready(gamma)
-        if own_b:
-            _ready(beta)
+        # one kernel writes ds and the dropout branch's da = keep * ds / (1 - p); the dgamma / dbeta
+        # fold goes to the weight-gradient side stream when the engine owns those gradients
+        if _split_fold_ok(s, gamma, own_g, own_b):
+            ds, da, part = native().layernorm_bwd_split(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd,
+                                                        dy2, ctx.p, ctx.seed, True)
+            _fold_on_side(part, s, dg, db, gamma, beta)
+        else:
+            ds, da = native().layernorm_bwd_drop(dy.contiguous().to(s.dtype), s, gamma.detach(), mean, rstd, dg, db,
+                                                 dy2, ctx.p, ctx.seed)
+            if own_g:
+                _ready(gamma)
+            if own_b:
+                _ready(beta)
         dx = ds
         if ctx.handoff is not None:
             hh = ctx.handoff
