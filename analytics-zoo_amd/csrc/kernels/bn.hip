@@ -509,14 +509,41 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_fwd_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) { bt[e] = -INFINITY; bi[e] = 0; }
     const bf16_t* xq = xn + (ptrdiff_t)(q * sw_ - pw) * C + chunk * 8;
-    for (int r = r_lo; r < r_hi; ++r) {
-      for (int s = s_lo; s < s_hi; ++s) {
-        float v[8];
-        unpack8(*reinterpret_cast<const uint4*>(xq + (r * W + s) * C), v);
+    if constexpr (STEM) {
+      // 3x3 window fully unrolled: all nine 16-byte loads in flight at once (the runtime-bounded
+      // loop below issued them one dependent iteration at a time); taps outside the image are
+      // predicated off, never loaded
+      uint4 raw[9];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const float t = sg[e] * v[e];
-          if (t > bt[e]) { bt[e] = t; bi[e] = (uint8_t)(r * S + s); }
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          const bool ok = r >= r_lo && r < r_hi && s >= s_lo && s < s_hi;
+          raw[r * 3 + s] = ok ? *reinterpret_cast<const uint4*>(xq + (r * W + s) * C) : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+          if (!(r >= r_lo && r < r_hi && s >= s_lo && s < s_hi)) continue;
+          float v[8];
+          unpack8(raw[r * 3 + s], v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = sg[e] * v[e];
+            if (t > bt[e]) { bt[e] = t; bi[e] = (uint8_t)(r * 3 + s); }
+          }
+        }
+    } else {
+      for (int r = r_lo; r < r_hi; ++r) {
+        for (int s = s_lo; s < s_hi; ++s) {
+          float v[8];
+          unpack8(*reinterpret_cast<const uint4*>(xq + (r * W + s) * C), v);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float t = sg[e] * v[e];
+            if (t > bt[e]) { bt[e] = t; bi[e] = (uint8_t)(r * S + s); }
+          }
         }
       }
     }
@@ -629,27 +656,60 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_apply_kernel(
     float dz[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) dz[e] = 0.f;
-    for (int p = p_lo; p <= p_hi; ++p) {
-      const int r = h - (p * sh_ - ph);
-      if (r < 0 || r >= R) continue;
-      for (int q = q_lo; q <= q_hi; ++q) {
-        const int s = w - (q * sw_ - pw);
-        if (s < 0 || s >= S) continue;
-        const uint32_t tap = (uint32_t)(r * S + s);
-        const size_t o = nb + (size_t)(p * Q + q) * C;
-        const uint2 ab = *reinterpret_cast<const uint2*>(arg + o);
-        float g[8];
-        unpack8(*reinterpret_cast<const uint4*>(dY + o), g);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (((ab.x >> (8 * e)) & 0xff) == tap) dz[e] += g[e];
-          if (((ab.y >> (8 * e)) & 0xff) == tap) dz[4 + e] += g[4 + e];
-        }
-      }
-    }
     const size_t off = xbase + (size_t)j * 8;
     float x[8], o[8];
-    unpack8(*reinterpret_cast<const uint4*>(X + off), x);
+    if constexpr (STEM) {
+      // stride 2, 3x3: a pixel lies in at most 2 x 2 windows (p_lo .. p_lo + 1, q_lo .. q_lo + 1);
+      // all their dY / arg loads and the pixel's own x load are issued before any use
+      uint4 gv[4];
+      uint2 av[4];
+      bool okv[4];
+      uint32_t tapv[4];
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          const int p = p_lo + a, q = q_lo + c, k = a * 2 + c;
+          const int r = h - (p * 2 - 1), s = w - (q * 2 - 1);
+          okv[k] = p <= p_hi && q <= q_hi && r >= 0 && r < 3 && s >= 0 && s < 3;
+          tapv[k] = (uint32_t)(r * 3 + s);
+          const size_t ofs = nb + (size_t)(p * Q + q) * C;
+          av[k] = okv[k] ? *reinterpret_cast<const uint2*>(arg + ofs) : make_uint2(0xffffffffu, 0xffffffffu);
+          gv[k] = okv[k] ? *reinterpret_cast<const uint4*>(dY + ofs) : make_uint4(0u, 0u, 0u, 0u);
+        }
+      unpack8(*reinterpret_cast<const uint4*>(X + off), x);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        if (!okv[k]) continue;
+        float g[8];
+        unpack8(gv[k], g);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (((av[k].x >> (8 * e)) & 0xff) == tapv[k]) dz[e] += g[e];
+          if (((av[k].y >> (8 * e)) & 0xff) == tapv[k]) dz[4 + e] += g[4 + e];
+        }
+      }
+    } else {
+      for (int p = p_lo; p <= p_hi; ++p) {
+        const int r = h - (p * sh_ - ph);
+        if (r < 0 || r >= R) continue;
+        for (int q = q_lo; q <= q_hi; ++q) {
+          const int s = w - (q * sw_ - pw);
+          if (s < 0 || s >= S) continue;
+          const uint32_t tap = (uint32_t)(r * S + s);
+          const size_t o2 = nb + (size_t)(p * Q + q) * C;
+          const uint2 ab = *reinterpret_cast<const uint2*>(arg + o2);
+          float g[8];
+          unpack8(*reinterpret_cast<const uint4*>(dY + o2), g);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if (((ab.x >> (8 * e)) & 0xff) == tap) dz[e] += g[e];
+            if (((ab.y >> (8 * e)) & 0xff) == tap) dz[4 + e] += g[4 + e];
+          }
+        }
+      }
+      unpack8(*reinterpret_cast<const uint4*>(X + off), x);
+    }
 #pragma unroll
     for (int e = 0; e < 8; ++e) o[e] = ka[e] * dz[e] + kb[e] * x[e] + kd[e];
     *reinterpret_cast<uint4*>(dX + off) = pack8(o);

@@ -246,8 +246,11 @@ def main():
         dist.barrier()
     _sync(dev)
     t0 = time.perf_counter()
+    host = 0.0
     for _ in range(a.steps):
+        h0 = time.perf_counter()
         loss = eng.train_step(x, y)
+        host += time.perf_counter() - h0
     _sync(dev)
     if world > 1:
         dist.barrier()
@@ -274,6 +277,9 @@ def main():
                            **extra),
             "first_loss": round(float(first_loss.float().item()), 4) if first_loss is not None else None,
             "final_loss": round(final_loss, 4),
+            # issue time of a step on the host (no device sync inside the timed loop): near
+            # ms_per_step means host-bound, well below means device-bound
+            "host_ms_per_step": round(host / a.steps * 1e3, 3),
         }
         out.update(diag)
         print(json.dumps(out), flush=True)
