@@ -354,12 +354,21 @@ static const bf16_t* w2_zero_page() {
 
 // split plan: ~one workgroup per CU (256), >= 4 m-steps per split. Returns the number of
 // splits and fills m_per_split; the caller provides part (splits * tiles * 256 KiB) when > 1.
+// target override (> 0) for the calls made while it is set: conv weight gradients use fewer,
+// longer splits (ZOO_WGRAD256_CONV_WG, default 128). With the weight-gradient side stream they
+// run beside the memory-bound BatchNorm passes, where half the split-K partial traffic beat the
+// extra parallelism: ResNet-50 b256 12,149-12,179 -> 12,278-12,314 img/s; BERT's linear weight
+// gradients, beside compute-bound GEMMs, stay at 256 (15.73 vs 16.06 ms at 128).
+static int g_w256_target = 0;
+extern "C" void zoo_wgrad256_target(int t) { g_w256_target = t; }
+
 extern "C" int zoo_wgrad256_plan(int M, int N, int K, int* m_per_split) {
   const int tiles = ((N + W2_T - 1) / W2_T) * ((K + W2_T - 1) / W2_T);
-  static const int target = [] {
+  static const int target_default = [] {
     const char* e = getenv("ZOO_WGRAD256_WG");
     return e ? atoi(e) : 256;
   }();
+  const int target = g_w256_target > 0 ? g_w256_target : target_default;
   int splits = (target + tiles / 2) / tiles;
   const int max_splits = (M + 4 * W2_BM - 1) / (4 * W2_BM);
   if (splits > max_splits) splits = max_splits;

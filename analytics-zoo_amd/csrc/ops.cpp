@@ -75,6 +75,7 @@ hipError_t zoo_l2norm_scale_bwd(const void*, const void*, const float*, const fl
                                 float, hipStream_t);
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
+void zoo_wgrad256_target(int);
 hipError_t zoo_wgrad256_conv(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, int,
                              int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
@@ -732,6 +733,16 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   TORCH_CHECK(g.K % 8 == 0, "conv_wgrad: K must be a multiple of 8");
   const int P = (g.H + 2 * ph - dh * (R - 1) - 1) / sh + 1, Q = (g.W + 2 * pw - dil_w * (S - 1) - 1) / sw + 1;
   TORCH_CHECK(P == g.P && Q == g.Q, "conv_wgrad: dy spatial shape does not match the geometry");
+  // conv weight gradients: the wgrad256 split target of conv calls (zoo_wgrad256_target), for the
+  // duration of this call
+  static const int conv_wg = [] {
+    const char* e = getenv("ZOO_WGRAD256_CONV_WG");
+    return e ? atoi(e) : 128;
+  }();
+  struct TargetGuard {
+    explicit TargetGuard(int t) { zoo_wgrad256_target(t); }
+    ~TargetGuard() { zoo_wgrad256_target(0); }
+  } tguard(conv_wg);
   g.M = g.N * g.P * g.Q;
   g.Ktot = R * S * g.C;
   g.ldw = dw.size(-1);
