@@ -63,9 +63,14 @@ struct I2Cfg {
   static constexpr int NW = NWM * NWN, NT = NW * 64;
   static constexpr int WTM = TM * 16, WTN = TN * 16;  // wave tile
   static constexpr int BM = NWM * WTM, BN = NWN * WTN;  // block tile
-  static constexpr int A_PW = BM / (8 * NW), B_PW = BN / (8 * NW);  // DMA instructions per wave per K-tile
+  // DMA instructions per wave per K-tile. A tile whose rows do not split evenly over the waves
+  // (BM = 224 with 8 waves: 28 pieces) gives every wave the same count and sends the pieces past
+  // BM -- zero-page reads -- to a per-wave junk slot, so every wave's vmcnt count stays uniform
+  static constexpr int A_PW = (BM + 8 * NW - 1) / (8 * NW), B_PW = BN / (8 * NW);
+  static constexpr bool A_RAG = A_PW * 8 * NW != BM;
   static constexpr int DPT = A_PW + B_PW;
   static constexpr int STAGE_BYTES = (BM + BN) * 128;
+  static constexpr int JUNK_BYTES = A_RAG ? NW * 1024 : 0;
   static constexpr int EPI_PITCH = WTN + 4;  // fp32 patch pitch (16-byte aligned rows)
   static constexpr int EPI_BYTES = NW * 16 * EPI_PITCH * 4 + NWM * BN * 2 * 4;
   static_assert(B_PW * 8 * NW == BN, "B tile rows must split into 8-row DMA groups");
@@ -90,7 +95,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
   constexpr int A_PW = Cfg::A_PW, B_PW = Cfg::B_PW, DPT = Cfg::DPT, SB = Cfg::STAGE_BYTES;
   constexpr bool IS1x1 = AM == I2_AM_1X1;
   constexpr bool BAND = AM == I2_AM_BAND;
-  static_assert(BAND || A_PW * 8 * NW == BM, "A tile rows must split into 8-row DMA groups");
+  static_assert(BAND || A_PW * 8 * NW >= BM, "A tile rows must be covered by the 8-row DMA groups");
+  static_assert(BAND || BM % 8 == 0, "A tile rows must split into 8-row DMA groups");
 
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -152,8 +158,9 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
 #pragma unroll
   for (int i = 0; i < A_PW; ++i) {
     if constexpr (BAND) break;
-    const int m = m0 + (i * NW + w) * 8 + lr;
-    const bool ok = m < g.M;
+    const int prow = (i * NW + w) * 8;   // first tile row of this DMA piece (>= BM: junk piece)
+    const int m = m0 + prow + lr;
+    const bool ok = prow < BM && m < g.M;
     if constexpr (IS1x1) {
       a_base[i] = ok ? m * g.C + gc * 8 : -1;
       a_ih[i] = a_iw[i] = 0;
@@ -191,8 +198,10 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
   auto stage = [&](int buf) {
     char* sa = smem + buf * SB + w * 1024;
     char* sb = smem + buf * SB + BM * 128 + w * 1024;
+    char* const ajunk = smem + STAGES * SB + w * 1024;
 #pragma unroll
     for (int i = 0; i < A_PW; ++i) {
+      char* adst = (Cfg::A_RAG && (i * NW + w) * 8 >= BM) ? ajunk : sa + i * NW * 1024;
       const bf16_t* src;
       if constexpr (IS1x1) {
         src = a_base[i] >= 0 ? X + a_base[i] + st_k : i2_zero_page;
@@ -201,7 +210,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
         const bool ok = (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
         src = ok ? X + a_base[i] + (ih * g.W + iw) * g.C + st_c : i2_zero_page;
       }
-      __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)(sa + i * NW * 1024), 16, 0, 0);
+      __builtin_amdgcn_global_load_lds((i2_gl_void*)src, (i2_lds_void*)adst, 16, 0, 0);
     }
 #pragma unroll
     for (int i = 0; i < B_PW; ++i) {
@@ -679,9 +688,10 @@ enum I2Tile : int {
   I2_B224x64 = 8,   // 4 waves (2x2) of 112x32, 3-stage: 45 KiB patch + 24 KiB ring, 2 / CU
   I2_B224x128 = 9,  // 8 waves (2x4) of 112x32, 3-stage: 2 x 38 KiB patches + 48 KiB ring, 1 / CU
   I2_B224x128w = 10,// 4 waves (2x2) of 112x64, 3-stage (A/B of the wider wave tile)
+  I2_224x256 = 11,  // 8 waves (2x4) of 112x64, 2-stage: 120 KiB + junk slots, 1 / CU (wave quantization)
 };
 
-static bool i2_is_band(int tile) { return tile >= I2_B224x64; }
+static bool i2_is_band(int tile) { return tile >= I2_B224x64 && tile <= I2_B224x128w; }
 
 static int g_i2_mode = -1;  // -1: unset (read ZOO_IGEMM2), 0: off, 1: on
 static int g_i2_tile = -1;  // -1: unset (read ZOO_IGEMM2_TILE), 0 auto, else I2Tile
@@ -712,20 +722,20 @@ static int i2_band_mode() {
 static int i2_bm(int tile) {
   switch (tile) {
     case I2_128x128: case I2_128x64: case I2_128x128_3: return 128;
-    case I2_B224x64: case I2_B224x128: case I2_B224x128w: return 224;
+    case I2_B224x64: case I2_B224x128: case I2_B224x128w: case I2_224x256: return 224;
     default: return 256;
   }
 }
 static int i2_bn(int tile) {
   switch (tile) {
     case I2_256x64: case I2_128x64: case I2_B224x64: return 64;
-    case I2_256x256: return 256;
+    case I2_256x256: case I2_224x256: return 256;
     default: return 128;
   }
 }
 static int i2_nw(int tile) {
   switch (tile) {
-    case I2_256x128: case I2_256x128_3: case I2_256x256: case I2_B224x128: return 8;
+    case I2_256x128: case I2_256x128_3: case I2_256x256: case I2_B224x128: case I2_224x256: return 8;
     default: return 4;
   }
 }
@@ -762,7 +772,7 @@ static hipError_t i2_launch(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* 
     smem = (size_t)(g.C > 64 ? 2 : 1) * b.pbytes + (size_t)STAGES * Cfg::BN * 128 + (size_t)Cfg::NW * 1024;
   } else {
     tiles = (long)((g.M + Cfg::BM - 1) / Cfg::BM) * ntn;
-    smem = (size_t)STAGES * Cfg::STAGE_BYTES;
+    smem = (size_t)STAGES * Cfg::STAGE_BYTES + Cfg::JUNK_BYTES;
   }
   if (smem < (size_t)Cfg::EPI_BYTES) smem = Cfg::EPI_BYTES;
   if (smem > 160 * 1024) return hipErrorInvalidValue;
@@ -810,6 +820,7 @@ static hipError_t i2_tile(int tile, int epi, const bf16_t* X, const bf16_t* W, b
       case I2_256x256: return i2_epi<2, 4, 8, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       case I2_128x64: return i2_epi<2, 2, 4, 2, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       case I2_128x128_3: return i2_epi<2, 2, 4, 4, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_224x256: return i2_epi<2, 4, 7, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       default: return hipErrorInvalidValue;
     }
   }
@@ -864,7 +875,30 @@ static int i2_choose(const ConvGeom& g, int epi) {
   }
   if (epi == 2 && g.Ktot < 1024) return 0;
   if (epi != 2 && g.Ktot < 256) return 0;
-  if (tiles(I2_256x256) >= 160) return I2_256x256;
+  if (tiles(I2_256x256) >= 160) {
+    // wave quantization: one 256x256 workgroup per CU, so a grid of t tiles takes ceil(t / CUs)
+    // rounds. 224-row tiles cost 7/8 of a 256-row round: take them when they finish in fewer
+    // round-equivalents (BERT / ResNet stage 3-4: 196 tiles of 256 rows fill 77 % of the CUs,
+    // 224 tiles of 224 rows 88 %). ZOO_I2_Q224=0: always 256x256.
+    static const bool q224 = [] {
+      const char* e = getenv("ZOO_I2_Q224");
+      return e ? atoi(e) != 0 : false;
+    }();
+    if (q224 && epi != 4) {
+      static int ncu = 0;
+      if (!ncu) {
+        int dev = 0;
+        hipGetDevice(&dev);
+        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (ncu <= 0) ncu = 256;
+      }
+      const long t256 = tiles(I2_256x256), t224 = tiles(I2_224x256);
+      const double c256 = (double)((t256 + ncu - 1) / ncu);
+      const double c224 = (double)((t224 + ncu - 1) / ncu) * (224.0 / 256.0);
+      if (c224 < 0.97 * c256) return I2_224x256;
+    }
+    return I2_256x256;
+  }
   return I2_128x128;
 }
 
