@@ -2,7 +2,7 @@
 # igemm2 224x256 wave-quantization tile: numerics, conv / linear A/B, end to end
 cd /tmp && export TMPDIR=/tmp && cd "${GRAFT_REPO_ROOT:-/root/repo}"
 O=gpurun_out/q224; mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_igemm2.py -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
+ZOO_I2_TEST_224=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_igemm2.py -q --timeout 120 --timeout-method thread > $O/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -2 $O/tests.log; [ $rc -eq 0 ] || exit 2
 for q in 1 0; do
   ZOO_I2_Q224=$q timeout -k 10 200 python -u analytics-zoo_amd/tools/conv_sweep.py --ops fwd,dgrad > $O/sweep_q$q.log 2>&1 || exit 3
