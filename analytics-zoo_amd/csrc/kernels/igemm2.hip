@@ -879,10 +879,11 @@ static int i2_choose(const ConvGeom& g, int epi) {
     // wave quantization: one 256x256 workgroup per CU, so a grid of t tiles takes ceil(t / CUs)
     // rounds. 224-row tiles cost 7/8 of a 256-row round: take them when they finish in fewer
     // round-equivalents (BERT / ResNet stage 3-4: 196 tiles of 256 rows fill 77 % of the CUs,
-    // 224 tiles of 224 rows 88 %). ZOO_I2_Q224=0: always 256x256.
+    // 224 tiles of 224 rows 88 %; BERT linears 16384x{2304,768}x768 and x768x3072 -5..-7 %, ResNet-50
+    // fwd/dgrad conv sweep -1..-2 %, profiles/r4/ab/q224_*). ZOO_I2_Q224=0: always 256x256.
     static const bool q224 = [] {
       const char* e = getenv("ZOO_I2_Q224");
-      return e ? atoi(e) != 0 : false;
+      return e ? atoi(e) != 0 : true;
     }();
     if (q224 && epi != 4) {
       static int ncu = 0;
