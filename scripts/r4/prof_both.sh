@@ -10,5 +10,5 @@ head -14 $O/rn_summary.md
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/pb_bert -o bert -- python3 analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 10 > $O/bert.log 2>&1 || exit 3
 DB=$(find /tmp/pb_bert -name "*.db" | head -1)
 python3 analytics-zoo_amd/tools/prof_summary.py $DB 13 "BERT-base fine-tune b128 s128 (bert_train.py under rocprofv3), round 4" > $O/bert_summary.md 2>&1
-python3 analytics-zoo_amd/tools/prof_step.py $DB > $O/bert_step.md 2>&1
+python3 analytics-zoo_amd/tools/prof_step.py $DB "softmax_xent_kernel" > $O/bert_step.md 2>&1
 head -30 $O/bert_summary.md
