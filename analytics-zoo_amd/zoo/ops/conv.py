@@ -351,10 +351,12 @@ class _LinearNativeFn(torch.autograd.Function):
                 bias = ctx.bias_ref
                 bbuf = getattr(bias, "_zoo_grad", None)
                 if bbuf is not None:
-                    bbuf.add_(link.db)
-                    hook = getattr(bias, "_zoo_grad_ready", None)
-                    if hook is not None:
-                        hook(bias)
+                    # a bias-gradient add nothing on the data-gradient path waits for: side stream
+                    with wstream.wgrad(dy.device, link.db, on=True):
+                        bbuf.add_(link.db)
+                        hook = getattr(bias, "_zoo_grad_ready", None)
+                        if hook is not None:
+                            hook(bias)
                 else:
                     db = link.db.to(bias.dtype)
             link.pre = link.y = link.db = None
