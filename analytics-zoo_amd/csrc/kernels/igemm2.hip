@@ -713,8 +713,10 @@ static int i2_tile_force() {
 }
 static int i2_band_mode() {
   if (g_i2_band < 0) {
+    // off by default since the two-stream backward: ResNet-50 b256 12,273 / 12,267 img/s off vs
+    // 12,239 / 12,205 on, same box (scripts/r4/knobs.sh); the band tiles stay available (=1)
     const char* e = getenv("ZOO_I2_BAND");
-    g_i2_band = e ? atoi(e) : 1;
+    g_i2_band = e ? atoi(e) : 0;
   }
   return g_i2_band;
 }
