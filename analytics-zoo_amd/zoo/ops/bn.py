@@ -22,6 +22,7 @@ from zoo.ops._native import native
 from zoo.ops import _kern, workspace, wstream
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
+from zoo.parallel.flat import grad_slot
 
 # Per-channel statistics buffers are "slotted" ([2C final][STAT_SLOTS x 2C][counter]):
 # producers spread their atomics over the slots and stats_finalize_kernel folds them
@@ -45,7 +46,7 @@ def _notify(p):
 
 
 def _grad_target(p):
-    g = getattr(p, "_zoo_grad", None)
+    g = grad_slot(p)
     if g is not None:
         return g, True
     return torch.zeros(p.shape, dtype=torch.float32, device=p.device), False

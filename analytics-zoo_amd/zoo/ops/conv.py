@@ -24,6 +24,7 @@ import torch.nn.functional as F
 
 from zoo.ops._native import native
 from zoo.ops import _kern, wstream
+from zoo.parallel.flat import grad_slot
 
 ACT_CODES = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
 
@@ -128,7 +129,7 @@ class _Conv2dFn(torch.autograd.Function):
             # ReLU mask + bias-gradient column sums in one native pass
             # the bias gradient goes straight into the engine's flat gradient buffer when there is one
             bref = getattr(ctx, "bias_ref", None)
-            into = getattr(bref, "_zoo_grad", None) if (want_db and bref is not None) else None
+            into = grad_slot(bref) if (want_db and bref is not None) else None
             into = into if (into is not None and into.is_contiguous() and into.numel() == K) else None
             outs = C_.act_bwd_reduce(dy.to(torch.bfloat16).contiguous(), y if act == "relu" else None, want_db, into)
             dy = outs[0]
@@ -156,7 +157,7 @@ class _Conv2dFn(torch.autograd.Function):
             dx = _kern.conv_dgrad(dyb, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, dil,
                                   resid=getattr(ctx, "grad_add", None))
         if ctx.needs_input_grad[1]:
-            gbuf = getattr(w, "_zoo_grad", None)
+            gbuf = grad_slot(w)
             target = gbuf if gbuf is not None else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
             C_.conv_wgrad(x, dyb, target, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
             if gbuf is None:
@@ -245,7 +246,7 @@ class _LinearBlasFn(torch.autograd.Function):
             # straight into the flat gradient when the engine owns one (csrc/kernels/bn.hip
             # act_bwd_reduce_kernel)
             bias = ctx.bias_ref
-            bbuf = getattr(bias, "_zoo_grad", None) if bias is not None else None
+            bbuf = grad_slot(bias) if bias is not None else None
             z = y if ctx.act == "relu" else (pre if ctx.act == "gelu" else None)
             outs = native().act_bwd_reduce(dy, z, True, bbuf, ctx.act == "gelu")
             dy = outs[0]
@@ -269,7 +270,7 @@ class _LinearBlasFn(torch.autograd.Function):
         elif ctx.needs_input_grad[0]:
             dx = torch.mm(dy, bf16_weight(w))
         if ctx.needs_input_grad[1]:
-            gbuf = getattr(w, "_zoo_grad", None)
+            gbuf = grad_slot(w)
             if gbuf is not None:
                 # accumulate straight into the flat fp32 gradient (bf16 in, fp32 out)
                 g2 = gbuf.view(dy.shape[1], x2.shape[1])
@@ -289,7 +290,7 @@ class _LinearBlasFn(torch.autograd.Function):
         if ctx.has_bias and ctx.needs_input_grad[2] and not bias_done:
             bias = ctx.bias_ref
             db = torch.sum(dy, 0, dtype=torch.float32)   # fp32 accumulation, no fp32 copy of dy
-            bbuf = getattr(bias, "_zoo_grad", None) if bias is not None else None
+            bbuf = grad_slot(bias) if bias is not None else None
             if bbuf is not None:
                 bbuf.add_(db)
                 hook = getattr(bias, "_zoo_grad_ready", None)
@@ -349,7 +350,7 @@ class _LinearNativeFn(torch.autograd.Function):
             # and summed the bias gradient there
             if ctx.has_bias and ctx.needs_input_grad[2]:
                 bias = ctx.bias_ref
-                bbuf = getattr(bias, "_zoo_grad", None)
+                bbuf = grad_slot(bias)
                 if bbuf is not None:
                     # a bias-gradient add nothing on the data-gradient path waits for: side stream
                     with wstream.wgrad(dy.device, link.db, on=True):
@@ -364,7 +365,7 @@ class _LinearNativeFn(torch.autograd.Function):
         elif (ctx.has_bias and ctx.needs_input_grad[2]) or ctx.act in ("relu", "gelu"):
             bias = ctx.bias_ref
             want_db = bool(ctx.has_bias and ctx.needs_input_grad[2])
-            bbuf = getattr(bias, "_zoo_grad", None) if (want_db and bias is not None) else None
+            bbuf = grad_slot(bias) if (want_db and bias is not None) else None
             z = y if ctx.act == "relu" else (pre if ctx.act == "gelu" else None)
             # no activation: the pass only sums dy's columns into the engine-owned bias gradient,
             # nothing on the data-gradient path waits for it -> weight-gradient side stream
@@ -400,7 +401,7 @@ class _LinearNativeFn(torch.autograd.Function):
         elif resid is not None:
             dx = resid
         if ctx.needs_input_grad[1]:
-            gbuf = getattr(w, "_zoo_grad", None)
+            gbuf = grad_slot(w)
             g2 = gbuf.view(N, K) if gbuf is not None else torch.zeros(N, K, device=dy.device, dtype=torch.float32)
             # engine-owned gradient: on the weight-gradient side stream (zoo.ops.wstream)
             with wstream.wgrad(dy.device, dy, x2, on=gbuf is not None):

@@ -10,6 +10,7 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
+from zoo.parallel.flat import grad_slot
 
 
 def _t(p):
@@ -21,7 +22,7 @@ def _empty(dev):
 
 
 def _grad_target(p):
-    g = getattr(p, "_zoo_grad", None)
+    g = grad_slot(p)
     if g is not None:
         return g, True
     return torch.zeros(p.shape, dtype=torch.float32, device=p.device), False

@@ -7,10 +7,11 @@ import torch
 import torch.nn.functional as F
 
 from zoo.ops._native import native
+from zoo.parallel.flat import grad_slot
 
 
 def _target(p, shape=None):
-    g = getattr(p, "_zoo_grad", None)
+    g = grad_slot(p)
     if g is not None:
         return g, True
     return torch.zeros(shape if shape is not None else p.shape, dtype=torch.float32, device=p.device), False

@@ -20,12 +20,13 @@ which doubles as the numerics oracle of ``tests/test_gpu_zoo_kernels.py``.
 import torch
 
 from zoo.ops._native import native
+from zoo.parallel.flat import grad_slot
 
 _MODES = {"sum": 0, "mean": 1, "sqrtn": 2}
 
 
 def _target(p):
-    g = getattr(p, "_zoo_grad", None)
+    g = grad_slot(p)
     if g is not None:
         return g, True
     return torch.zeros(p.shape, dtype=torch.float32, device=p.device), False

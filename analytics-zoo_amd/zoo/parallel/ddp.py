@@ -17,7 +17,10 @@ docs/docs/wp-bigdl.md:140-160):
   twice (shared Keras layers, siamese KNRM/TextMatcher, tied embeddings)
   triggers its bucket only after its second contribution. A later step that
   adds MORE contributions than calibrated raises instead of reducing a partial
-  gradient.
+  gradient (collectives cannot be recalled). The single-rank in-backward
+  optimizer (``enable_ibo``) never raises: it calibrates over two steps, updates
+  in-backward only buckets whose counts agreed in both, and moves a bucket that
+  later breaks its count to the end-of-step update for the rest of the run.
 * ``mode="allreduce"``: every rank ends with the summed gradient.
   - fp32: one ``all_reduce`` per bucket.
   - ``compress="bf16"``: the bucket is packed to bf16 into a persistent buffer
@@ -50,7 +53,8 @@ last contribution); later steps launch early in that order, and ``finish()`` lau
 is left -- including all buckets of a zombie rank that failed part-way through backward -- in
 that same recorded order, so a zombie's collective sequence matches the healthy ranks'.
 
-Row-sparse sync: each rank scatters a per-row "touched" mask (uint8, V bytes; int32 at >= 256
+Row-sparse sync (fp32 wire only -- ``compress="bf16"``, the GPU default, reduces every bucket
+densely): each rank scatters a per-row "touched" mask (uint8, V bytes; int32 at >= 256
 ranks), the masks are summed (one all-reduce), the union rows are compacted on the device into a
 fixed-capacity index buffer (capacity min(V, world * ids-per-step), agreed in the calibration
 step) and ONE fixed-size all-reduce moves just those rows. A rank without lookups contributes a
@@ -75,6 +79,7 @@ Gradient averaging (1/N) is folded into the optimizer kernel's ``gscale``.
 On CPU (gloo) the same code runs synchronously; that is what the
 multi-process CPU tests exercise.
 """
+import logging
 import threading
 
 import torch
@@ -84,6 +89,7 @@ from zoo.parallel.flat import FlatParams
 from zoo.ops import wstream
 
 CHUNK_ALIGN = 64
+log = logging.getLogger("zoo")
 # step counter for the row-sparse id records (bumped by GradSync.reset): an embedding lookup
 # in a new step starts a new record list; a hipGraph replay runs no Python forward, so the
 # captured id tensors (rewritten by every replay) stay recorded
@@ -121,7 +127,7 @@ def record_lookup(table, idx):
 
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "params", "pending", "launched", "cb", "so", "pack", "recv", "gath",
-                 "works", "post", "sparse", "gath16", "ev0", "ev1")
+                 "works", "post", "sparse", "gath16", "ev0", "ev1", "ibo_off")
 
     def __init__(self, idx, lo, hi):
         self.idx, self.lo, self.hi = idx, lo, hi
@@ -136,6 +142,7 @@ class _Bucket:
         self.sparse = []     # [(param, lo, hi)] when every parameter of the bucket is row-sparse
         self.gath16 = None   # ZeRO-1 bf16 weight all-gather target
         self.ev0 = self.ev1 = None  # comm-stream events around the bucket's collectives (stats)
+        self.ibo_off = False        # in-backward update switched off (counts not stable)
 
 
 class GradSync:
@@ -214,6 +221,12 @@ class GradSync:
         self.ibo_steps = 0
         self._ibo_done = set()
         self._ibo_cleared = True
+        self._ibo_calib1 = None     # contribution counts of the first calibration step
+        self._ibo_hooks = []
+        # set by the TrainingEngine: gradients written while no engine step runs (a user's own
+        # loss.backward(), another driver) invalidate FlatParams.grad_clean and are not counted
+        self.engine_managed = False
+        self.in_step = False
         self._install_hooks()
         self.reset()
 
@@ -328,15 +341,40 @@ class GradSync:
         if self.comm or not self.is_cuda:
             return False
         self.ibo_optim = optim
+        for h in self._ibo_hooks:
+            h.remove()
+        self._ibo_hooks = []
+        for p in self.flat.params:
+            # native ops announce a gradient write before they enqueue it (flat.grad_slot);
+            # autograd-accumulated parameters through a tensor hook, which runs BEFORE the
+            # accumulation kernel is issued
+            p._zoo_grad_pre = self._ibo_pre
+            self._ibo_hooks.append(p.register_hook(lambda g, p=p: self._ibo_pre(p)))
         return True
+
+    def _ibo_pre(self, p):
+        """A gradient write into p's slot is about to be enqueued on the current stream. If
+        p's bucket was already updated in-backward this step, that write must not overlap the
+        side-stream update that reads and clears the slot: order it after the update."""
+        if self.ibo_optim is None or not self.in_step:
+            return
+        b = self.param_bucket.get(id(p))
+        if b is not None and b.launched:
+            dev = self.flat.grad.device
+            cur = torch.cuda.current_stream(dev)
+            side = wstream.side_for(dev)
+            if cur != side:
+                cur.wait_stream(side)
 
     def reset(self):
         self._counts = {}
         self._ibo_done = set()
         _TOUCH_STEP[0] += 1
         for b in self.buckets:
-            if self._expected is None or b.sparse:
-                b.pending = -1  # calibration step / row-sparse bucket: launched by finish()
+            if self._expected is None or b.sparse or b.ibo_off:
+                # calibration step / row-sparse bucket / in-backward update switched off for the
+                # bucket: launched (updated) by finish() / step()
+                b.pending = -1
             else:
                 b.pending = sum(1 for pid in b.params if self._expected.get(pid, 0) > 0)
             b.launched = False
@@ -345,6 +383,10 @@ class GradSync:
         self.launch_log = []
 
     def _ready(self, p):
+        if self.engine_managed and not self.in_step:
+            # a gradient written outside an engine step: the slots are no longer known clear
+            self.flat.grad_clean = False
+            return
         if not self.comm:
             if self.ibo_optim is not None:
                 self._ibo_ready(p)
@@ -460,8 +502,10 @@ class GradSync:
     def _row_sparse_allreduce(self, p, lo, hi):
         """Sum table p's gradient over the ranks through the union of looked-up rows: a summed
         uint8 touched mask, device-side compaction into a fixed-capacity row list, one fixed-size
-        all-reduce of those rows. No host synchronisation after the calibration step, and the
-        same collectives on every rank whatever it looked up (an idle rank sends a zero mask)."""
+        all-reduce of those rows. One small host read per step (the summed overflow flag, which
+        picks the dense fallback identically on every rank), and the same collectives on every
+        rank whatever it looked up (an idle rank sends a zero mask). Runs on the fp32 wire only:
+        with the bf16 wire (``compress``, the GPU default) the bucket takes the dense path."""
         V, D = p.shape
         g = self.flat.grad[lo:lo + V * D].view(V, D)
         dev = g.device
@@ -546,23 +590,40 @@ class GradSync:
         c = self._counts.get(pid, 0) + 1
         self._counts[pid] = c
         if self._expected is None:
-            return   # calibration step: counting only
+            return   # calibration steps: counting only
         b = self.param_bucket.get(pid)
-        if b is None or b.pending <= 0:
+        if b is None:
             return
         exp = self._expected.get(pid, 0)
         if c > exp:
-            if b.launched:
-                raise RuntimeError(
-                    "GradSync: parameter %s got %d gradient contributions this step but %d in the calibration "
-                    "step, after its in-backward update ran; dynamic graphs need ZOO_OPTIM_IN_BWD=0"
-                    % (tuple(p.shape), c, exp))
-            b.pending = -1   # more contributions than calibrated: this bucket waits for step()
+            # checked before the pending test: a launched bucket has pending 0
+            if not b.ibo_off:
+                self._ibo_disable(b, p, c, exp)
+            return
+        if b.pending <= 0:
             return
         if c == exp:
             b.pending -= 1
             if b.pending == 0:
                 self._ibo_launch(b)
+
+    def _ibo_disable(self, b, p, c, exp):
+        """p got more gradient contributions than calibrated: bucket b is updated at the end of
+        every later step. Not yet updated this step -> the end-of-step update sees the whole
+        gradient. Already updated -> the late contribution was ordered behind the update
+        (_ibo_pre) and lands in a cleared slot; it is dropped (the engine clears the buffer
+        before the next step) instead of being applied twice or leaking into the next step."""
+        b.ibo_off = True
+        if b.launched:
+            self._ibo_cleared = False
+            log.warning("in-backward optimizer: parameter %s got %d gradient contributions, %d calibrated, "
+                        "after its bucket was updated; this step's late contribution is dropped and the "
+                        "bucket is updated at the end of each step from now on (ZOO_OPTIM_IN_BWD=0 turns "
+                        "the in-backward update off)", tuple(p.shape), c, exp)
+        else:
+            b.pending = -1
+            log.warning("in-backward optimizer: parameter %s got %d gradient contributions, %d calibrated; "
+                        "its bucket is updated at the end of each step from now on", tuple(p.shape), c, exp)
 
     def _ibo_launch(self, b):
         from zoo.ops import wstream
@@ -583,7 +644,15 @@ class GradSync:
         backward (calibration step, extra contributions, no gradient), then bump the counters."""
         flat = self.flat
         if self._expected is None:
-            self._expected = dict(self._counts)
+            # two calibration steps: a bucket whose parameters' contribution counts differ
+            # between them (a layer used a variable number of times) is never updated in-backward
+            if self._ibo_calib1 is None:
+                self._ibo_calib1 = dict(self._counts)
+            else:
+                self._expected = dict(self._counts)
+                for b in self.buckets:
+                    if any(self._ibo_calib1.get(pid, 0) != self._expected.get(pid, 0) for pid in b.params):
+                        b.ibo_off = True
         cleared = True
         for b in self.buckets:
             if b.idx not in self._ibo_done:

@@ -22,6 +22,19 @@ import torch
 ALIGN = 64
 
 
+def grad_slot(p):
+    """The flat gradient view of ``p`` that native backward kernels write into (None when no
+    engine owns p's gradient). Native ops call this right before they enqueue such a write, so
+    a ``_zoo_grad_pre`` hook (the in-backward optimizer, GradSync._ibo_pre) can order the write
+    after an update of the same slot that is already in flight on another stream."""
+    g = getattr(p, "_zoo_grad", None)
+    if g is not None:
+        pre = getattr(p, "_zoo_grad_pre", None)
+        if pre is not None:
+            pre(p)
+    return g
+
+
 def _align(n, a=ALIGN):
     return (n + a - 1) // a * a
 
@@ -97,7 +110,7 @@ class FlatParams:
         """Give parameters private storage again (undo the flat re-homing)."""
         for p in self.params:
             p.data = p.data.clone()
-            for a in ("_zoo_grad", "_zoo_bf16"):
+            for a in ("_zoo_grad", "_zoo_bf16", "_zoo_grad_pre"):
                 if hasattr(p, a):
                     delattr(p, a)
             p.grad = None

@@ -20,6 +20,7 @@ from zoo import ops
 from zoo.ops.layers import lstm_gates
 from zoo.ops import rnn as rnn_ops
 from zoo.pipeline.api.keras.base import Layer, apply_activation, init_tensor
+from zoo.parallel.flat import grad_slot
 
 
 class _RNNBase(Layer):
@@ -218,7 +219,7 @@ class _ConvLSTMSeqFn(torch.autograd.Function):
         dc = torch.empty(M, f, dtype=torch.float32, device=dev)
         dc_next = None
         dhr = None
-        gbuf = getattr(wh, "_zoo_grad", None)
+        gbuf = grad_slot(wh)
         dwh = gbuf if (gbuf is not None and ctx.needs_input_grad[1]) else \
             torch.zeros(wh.shape, dtype=torch.float32, device=dev)
         dout = dout.contiguous().float()

@@ -31,12 +31,14 @@ the ONNX importer mapping nodes onto Zoo Keras layers
 mirrors ``zoo/pipeline/inference/openvino.py``'s native IR executor.
 """
 import copy
+import weakref
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from zoo import ops
+from zoo.ops import _kern
 from zoo.ops import pointwise as P
 from zoo.ops import pool as PO
 from zoo.pipeline.api.net import graph_net as G
@@ -119,10 +121,14 @@ class ZConv2d(_Twin, nn.Conv2d):
                                                  (self.bias is not None and self.bias.requires_grad))
         key = None
         if not need_grad:
+            # the engine's fused optimizer (weights) and the native BN forward (running statistics)
+            # write through raw pointers without bumping ``_version``: their epochs are in the key
             key = (self.weight._version, self.weight.data_ptr(), None if self.bias is None else self.bias._version,
                    training_bn, None if bn is None else (bn.running_mean._version, bn.running_var._version,
                                                          None if bn.weight is None else bn.weight._version,
-                                                         bn.running_mean.data_ptr()))
+                                                         None if bn.bias is None else bn.bias._version,
+                                                         bn.running_mean.data_ptr()),
+                   _kern.weights_epoch(), _kern.stats_epoch())
             if self._zoo_cache is not None and self._zoo_cache[0] == key:
                 return self._zoo_cache[1], self._zoo_cache[2]
         w = self.weight.float()
@@ -529,10 +535,12 @@ def _packed_cached(w, b):
     """Packed native weight / padded bias of an NCHW conv weight (ONNX initialisers: cached by
     tensor identity and version, recomputed only after an update)."""
     key = (id(w), None if b is None else id(b))
-    ver = (w._version, w.data_ptr(), None if b is None else b._version)
+    ver = (w._version, w.data_ptr(), None if b is None else b._version, _kern.weights_epoch())
     hit = _PACK_CACHE.get(key)
     need_grad = torch.is_grad_enabled() and (w.requires_grad or (b is not None and b.requires_grad))
-    if hit is not None and hit[0] == ver and not need_grad:
+    # ids are reused after garbage collection: the entry also holds weak references to its tensors
+    if hit is not None and hit[0] == ver and not need_grad and hit[3]() is w and \
+            (b is None or (hit[4] is not None and hit[4]() is b)):
         return hit[1], hit[2]
     K, C, R, S = w.shape
     cp, kp = _cin_pad(C), ops.ceil8(K)
@@ -542,7 +550,8 @@ def _packed_cached(w, b):
         w2 = F.pad(w2, (0, ld - R * S * cp))
     bb = F.pad(b.float() if b is not None else torch.zeros(K, device=w.device), (0, kp - K))
     if not need_grad:
-        _PACK_CACHE[key] = (ver, w2.detach().contiguous(), bb.detach().contiguous())
+        _PACK_CACHE[key] = (ver, w2.detach().contiguous(), bb.detach().contiguous(), weakref.ref(w),
+                            None if b is None else weakref.ref(b))
         if len(_PACK_CACHE) > 4096:
             _PACK_CACHE.clear()
     return w2, bb

@@ -178,6 +178,8 @@ class TrainingEngine:
                              else "allreduce", overlap=cfg.overlap_comm, compress=cfg.grad_compression or None,
                              force_comm=cfg.force_comm)
         self.sync.broadcast_parameters()
+        # gradient writes outside train_step (a user's own backward) mark the flat gradient dirty
+        self.sync.engine_managed = True
         self._local_failure = None
         self.clip = clip
         self.forward_fn = model_forward or (lambda m, x: m(x))
@@ -277,6 +279,7 @@ class TrainingEngine:
             self.flat.grad.zero_()
         self.flat.grad_clean = False
         workspace.begin_step(self.device)
+        self.sync.in_step = True
         try:
             out = self.forward_fn(self.model, inputs)
             loss = self.criterion(out, target)
@@ -285,6 +288,7 @@ class TrainingEngine:
             with wstream.enabled(self.device):
                 loss.backward()
         finally:
+            self.sync.in_step = False
             workspace.end_step()
         return loss.detach()
 
@@ -572,6 +576,7 @@ class TrainingEngine:
                 self.optim._buffers = bufs
                 self.optim._key = (bufs[0].numel(), str(self.device))
         self.flat.refresh_bf16()
+        self.flat.grad_clean = False
         self.state.update(_json.loads(meta.get("engine_state", "{}")))
         self.optim.state.update(_json.loads(meta.get("optim_state", "{}")))
         self.sync.reset()
@@ -629,4 +634,5 @@ class TrainingEngine:
             self.optim.load_state_dict(load_opt(opath))
             self.optim.to(self.device)
         self.sync.broadcast_parameters()
+        self.flat.grad_clean = False
         self.sync.reset()

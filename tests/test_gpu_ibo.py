@@ -84,3 +84,68 @@ def test_ibo_bert_adamw_matches_end_of_step_update(gpu, monkeypatch):
         # (the embedding / attention backward keep fp32 atomics even in deterministic mode)
         assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (l0, l1)
     assert ((w1 - w0).norm() / w0.norm()).item() < 1e-4
+
+
+class _SharedLoop(torch.nn.Module):
+    """One native Dense layer applied ``uses[t]`` times in step t: every application's backward
+    writes its weight gradient straight into the flat slot and counts as one contribution."""
+
+    def __init__(self, uses):
+        super().__init__()
+        from zoo.ops import linear
+        self._linear = linear
+        self.w_in = torch.nn.Parameter(torch.randn(64, 32) * 0.1)
+        self.w_mid = torch.nn.Parameter(torch.randn(64, 64) * 0.1)
+        self.w_sh = torch.nn.Parameter(torch.randn(64, 64) * 0.1)
+        self.b_sh = torch.nn.Parameter(torch.zeros(64))
+        self.w_out = torch.nn.Parameter(torch.randn(8, 64) * 0.1)
+        self.uses, self.t = list(uses), 0
+
+    def forward(self, x):
+        h = self._linear(x, self.w_in, None, act="relu")
+        h = self._linear(h, self.w_mid, None, act="relu")
+        k = self.uses[self.t % len(self.uses)]
+        self.t += 1
+        for _ in range(k):
+            h = self._linear(h, self.w_sh, self.b_sh, act="relu")
+        return self._linear(h, self.w_out, None).float()
+
+
+def _shared_run(uses, ibo, monkeypatch, gpu, steps):
+    from zoo.common.nncontext import init_nncontext
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD
+    init_nncontext("ibo-shared")
+    torch.manual_seed(3)
+    m = _SharedLoop(uses)
+    x = torch.randn(256, 32, device=gpu)
+    y = torch.randint(0, 8, (256,), device=gpu)
+    return _train(m, softmax_cross_entropy, SGD(learningrate=0.05, momentum=0.9), x, y, steps, ibo, monkeypatch,
+                  bucket_mb=0.001), m
+
+
+def test_ibo_variable_shared_layer_matches_end_of_step(gpu, monkeypatch):
+    """Counts that differ between the two calibration steps keep the shared layer's bucket on
+    the end-of-step update: the run equals ZOO_OPTIM_IN_BWD=0."""
+    uses = [1, 2, 1, 3, 2, 2, 1, 3]
+    (l0, w0), _ = _shared_run(uses, False, monkeypatch, gpu, 8)
+    (l1, w1), _ = _shared_run(uses, True, monkeypatch, gpu, 8)
+    for a, b in zip(l0, l1):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (l0, l1)
+    assert ((w1 - w0).norm() / w0.norm()).item() < 1e-6
+
+
+def test_ibo_late_contribution_degrades_without_raising(gpu, monkeypatch, caplog):
+    """A count that grows AFTER calibration (2, 2, then 3 uses): the step completes, a warning
+    is logged, the bucket moves to the end-of-step update for good, and the steps before the
+    surprise match the end-of-step run exactly."""
+    import logging
+    uses = [2, 2, 2, 3, 2, 2]
+    (l0, w0), _ = _shared_run(uses, False, monkeypatch, gpu, 6)
+    with caplog.at_level(logging.WARNING, logger="zoo"):
+        (l1, w1), _ = _shared_run(uses, True, monkeypatch, gpu, 6)
+    assert any("in-backward optimizer" in r.getMessage() for r in caplog.records)
+    for a, b in zip(l0[:4], l1[:4]):
+        assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (l0, l1)
+    assert all(abs(v) < 1e3 for v in l1) and torch.isfinite(w1).all()
+    assert ((w1 - w0).norm() / w0.norm()).item() < 0.05

@@ -165,6 +165,39 @@ def test_torchnet_cnn_inference_and_training(gpu):
             assert torch.allclose(a.running_mean, b.running_mean, atol=2e-3)
 
 
+def test_torchnet_eval_after_engine_training_sees_new_weights(gpu):
+    """the packed / BN-folded weight cache of a lowered conv must notice the engine's
+    raw-pointer writes (fused optimizer -> weights, native BN forward -> running statistics):
+    eval, train through the TrainingEngine, eval again == a fresh fp32 copy of the trained model."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.api.net import TorchNet
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext("lowered-cache")
+    torch.manual_seed(2)
+    net = TorchNet.from_pytorch(_CNN().eval())
+    net.module.to(gpu)
+    x = torch.randn(16, 3, 32, 32, device=gpu)
+    y = torch.randint(0, 10, (16,), device=gpu)
+    net.module.eval()
+    with torch.no_grad():
+        out0 = net.module(x).float()                 # fills the packed-weight caches
+    eng = TrainingEngine(net.module, lambda o, t: F.cross_entropy(o.float(), t), SGD(learningrate=0.1), hip_graph=False)
+    for _ in range(3):
+        eng.train_step(x, y)
+    torch.cuda.synchronize()
+    net.module.eval()
+    with torch.no_grad():
+        out1 = net.module(x).float()
+    fresh = _CNN()
+    fresh.load_state_dict({k: v.detach().float().cpu() for k, v in net.module.state_dict().items()})
+    fresh = fresh.to(gpu).eval()
+    with torch.no_grad():
+        want = fresh(x).float()
+    assert _nrel(out0, want) > 5e-2          # training moved the model
+    assert _nrel(out1, want) < 2e-2
+
+
 class _Seq(nn.Module):
     def __init__(self):
         super().__init__()
