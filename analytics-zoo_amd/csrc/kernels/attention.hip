@@ -136,6 +136,7 @@ struct AttnDrop {
   uint32_t thresh;  // 0: no dropout
   float scale;      // 1 / (1 - p)
   uint32_t s0, s1;
+  const uint32_t* off;  // per-step device seed offset (g_seed_off) or null
 };
 
 ZOO_DEV uint32_t attn_fmix(uint32_t h) {
@@ -177,6 +178,7 @@ __global__ __launch_bounds__(NW * 64, 8 / NW) void attn_fwd_kernel(
     const bf16_t* __restrict__ Q, const bf16_t* __restrict__ K, const bf16_t* __restrict__ V,
     const float* __restrict__ mask, bf16_t* __restrict__ O, float* __restrict__ LSE, int H, int L, int S,
     float scale, int causal, AttnStrides sd, AttnDrop dd) {
+  if (dd.thresh && dd.off) dd.s0 ^= *dd.off;
   constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);  // [2][64][D]
@@ -386,6 +388,7 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_kernel(
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
     float scale, int causal, AttnBwdStrides sd, AttnDrop dd) {
+  if (dd.thresh && dd.off) dd.s0 ^= *dd.off;
   // QW = 2: 8 waves; wave w owns keys 32(w&3).. and query rows 32(w>>2).. of every
   // 64-row tile (two waves per SIMD); the two q-halves are summed through LDS at the end
   constexpr int KS = D / 16, DT = D / 32, NQT = 2 / QW;
@@ -577,6 +580,7 @@ __global__ __launch_bounds__(256 * QW, 1) void attn_bwd_dkdv_pers_kernel(
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dK, bf16_t* __restrict__ dV, int H, int L, int S,
     float scale, int causal, AttnBwdStrides sd, AttnDrop dd, int BH) {
+  if (dd.thresh && dd.off) dd.s0 ^= *dd.off;
   // QW = 2: 8 waves; wave w owns keys 32(w&3).. and query rows 32(w>>2).. of every
   // 64-row tile (two waves per SIMD); the two q-halves are summed through LDS at the end.
   // Persistent over heads: block (x, y) handles heads y, y + gridDim.y, ... of key block x.
@@ -832,6 +836,7 @@ __global__ __launch_bounds__(NW * 64, 1) void attn_bwd_dq_kernel(
     const float* __restrict__ mask, const bf16_t* __restrict__ dO, const float* __restrict__ LSE,
     const float* __restrict__ delta, bf16_t* __restrict__ dQ, int H, int L, int S, float scale, int causal,
     AttnBwdStrides sd, AttnDrop dd) {
+  if (dd.thresh && dd.off) dd.s0 ^= *dd.off;
   constexpr int NTH = NW * 64, KS = D / 16, DT = D / 32;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   bf16_t* Ks = reinterpret_cast<bf16_t*>(smem);
@@ -1010,6 +1015,7 @@ static AttnDrop make_drop(float p, uint64_t seed) {
   d.scale = p >= 1.f ? 0.f : 1.f / (1.f - p);
   d.s0 = (uint32_t)seed;
   d.s1 = (uint32_t)(seed >> 32);
+  d.off = g_seed_off;
   return d;
 }
 

@@ -137,4 +137,9 @@ ZOO_DEV float apply_act(float x, int act) {
   }
 }
 
+// per-step dropout seed offset (device uint32, set by zoo_set_seed_offset in pointwise.hip): every
+// dropout kernel xors it into its host seed, so a hipGraph-captured step that replays baked host
+// seeds still draws a fresh mask each step (the host stages a new offset before every replay)
+extern const uint32_t* g_seed_off;
+
 }  // namespace zoo

@@ -103,7 +103,9 @@ struct WgradGeom {
 
 // Recurrent cells (rnn.hip). Activation codes shared with zoo/ops/rnn.py.
 enum RnnAct : int { RA_LINEAR = 0, RA_TANH = 1, RA_SIGMOID = 2, RA_HSIG = 3, RA_RELU = 4 };
-enum RnnCell : int { CELL_RNN = 0, CELL_LSTM = 1, CELL_GRU = 2 };
+// CELL_GRU: Keras / BigDL GRU (candidate over (r*h) . U_h); CELL_GRU_RA: the "reset-after" GRU of
+// torch.nn.GRU / GRUCell (candidate tanh(xn + r * (U_n h + b_hn)))
+enum RnnCell : int { CELL_RNN = 0, CELL_LSTM = 1, CELL_GRU = 2, CELL_GRU_RA = 3 };
 
 struct RnnArgs {
   const float* xw;     // [B, T, G*H] input projections (bias included)
@@ -119,6 +121,8 @@ struct RnnArgs {
   float* dgates;       // [B, T, G*H] (backward)
   float* dh0;          // [B, H] or null (backward)
   float* dc0;          // [B, H] or null (backward, LSTM)
+  const float* bhn;    // [H] candidate recurrent bias b_hn (GRU_RA) or null
+  float* dgn;          // [B, T, H] d(U_n h + b_hn) (backward, GRU_RA)
   int B, T, act, iact;
 };
 

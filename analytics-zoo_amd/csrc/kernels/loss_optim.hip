@@ -158,7 +158,12 @@ __global__ __launch_bounds__(256) void prob_nll_grad_kernel(const T* __restrict_
 __global__ __launch_bounds__(256) void sgd_kernel(float* __restrict__ p, float* __restrict__ g,
                                                   float* __restrict__ mom, bf16_t* __restrict__ pbf, size_t n,
                                                   float lr, float momentum, float dampening, float wd,
-                                                  int nesterov, float gscale, int first_step, int zero_g) {
+                                                  int nesterov, float gscale, int first_step, int zero_g,
+                                                  const float* __restrict__ hp) {
+  if (hp) {  // per-step values from device memory (hipGraph replays of a captured update)
+    lr = hp[0];
+    first_step = hp[3] != 0.f;
+  }
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
     if (zero_g) g[i] = 0.f;
@@ -179,7 +184,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ m, float* __restrict__ v,
                                                    bf16_t* __restrict__ pbf, size_t n, float lr, float b1,
                                                    float b2, float eps, float wd, float bc1, float bc2,
-                                                   float gscale, int decoupled, int zero_g) {
+                                                   float gscale, int decoupled, int zero_g,
+                                                   const float* __restrict__ hp) {
+  if (hp) {
+    lr = hp[0];
+    bc1 = hp[1];
+    bc2 = hp[2];
+  }
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
     if (zero_g) g[i] = 0.f;
@@ -204,7 +215,11 @@ __global__ __launch_bounds__(256) void adaptive_kernel(float* __restrict__ p, fl
                                                        float* __restrict__ s1, float* __restrict__ s2,
                                                        bf16_t* __restrict__ pbf, size_t n, int kind, float lr,
                                                        float rho, float rho2, float eps, float wd, float bc1,
-                                                       float gscale, int zero_g) {
+                                                       float gscale, int zero_g, const float* __restrict__ hp) {
+  if (hp) {
+    lr = hp[0];
+    bc1 = hp[1];
+  }
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     float gi = g[i] * gscale;
     if (zero_g) g[i] = 0.f;
@@ -402,12 +417,17 @@ extern "C" hipError_t zoo_prob_nll_grad(const void* probs, int is_f32, const int
 // zero_g (optimizer-side gradient clear, ops.cpp optim_zero_grad): g is cleared after it is read
 static int g_zero_g = 0;
 extern "C" void zoo_optim_zero_grad(int on) { g_zero_g = on ? 1 : 0; }
+// device hyper-parameters (ops.cpp optim_device_hparams): while set, the optimizer kernels read
+// lr / bias corrections / the first-step flag from this fp32 [4] buffer instead of their scalar
+// arguments -- a captured update then follows the schedule on every replay
+static const float* g_hp = nullptr;
+extern "C" void zoo_optim_device_hparams(const float* hp) { g_hp = hp; }
 
 extern "C" hipError_t zoo_sgd(float* p, const float* g, float* mom, void* pbf, size_t n, float lr, float momentum,
                               float dampening, float wd, int nesterov, float gscale, int first_step,
                               hipStream_t st) {
   hipLaunchKernelGGL(sgd_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), mom, (bf16_t*)pbf, n, lr,
-                     momentum, dampening, wd, nesterov, gscale, first_step, g_zero_g);
+                     momentum, dampening, wd, nesterov, gscale, first_step, g_zero_g, g_hp);
   return hipGetLastError();
 }
 
@@ -415,7 +435,7 @@ extern "C" hipError_t zoo_adam(float* p, const float* g, float* m, float* v, voi
                                float b2, float eps, float wd, float bc1, float bc2, float gscale, int decoupled,
                                hipStream_t st) {
   hipLaunchKernelGGL(adam_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), m, v, (bf16_t*)pbf, n,
-                     lr, b1, b2, eps, wd, bc1, bc2, gscale, decoupled, g_zero_g);
+                     lr, b1, b2, eps, wd, bc1, bc2, gscale, decoupled, g_zero_g, g_hp);
   return hipGetLastError();
 }
 
@@ -423,7 +443,7 @@ extern "C" hipError_t zoo_adaptive(float* p, const float* g, float* s1, float* s
                                    float lr, float rho, float rho2, float eps, float wd, float bc1, float gscale,
                                    hipStream_t st) {
   hipLaunchKernelGGL(adaptive_kernel, dim3(egrid(n)), dim3(256), 0, st, p, const_cast<float*>(g), s1, s2, (bf16_t*)pbf,
-                     n, kind, lr, rho, rho2, eps, wd, bc1, gscale, g_zero_g);
+                     n, kind, lr, rho, rho2, eps, wd, bc1, gscale, g_zero_g, g_hp);
   return hipGetLastError();
 }
 

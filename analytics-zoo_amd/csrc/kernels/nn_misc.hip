@@ -50,6 +50,7 @@ struct DropArgs {
   bf16_t* S;        // residual sum out = X + keep * A * scale (the LayerNorm input saved for backward)
   uint32_t thresh, s0, s1;
   float scale;
+  const uint32_t* off;  // per-step device seed offset (g_seed_off) or null
 };
 
 // ---------------------------------------------------------------- LayerNorm
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(256) void layernorm_fwd_reg_kernel(const T* __restr
                                                                 float* __restrict__ mean_out,
                                                                 float* __restrict__ rstd_out, int rows, int D,
                                                                 float eps, DropArgs dr) {
+  if (dr.A && dr.off) dr.s0 ^= *dr.off;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -264,6 +266,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
                                                                const float* __restrict__ rstd, bf16_t* __restrict__ dX,
                                                                float* __restrict__ part, int rows, int D,
                                                                const bf16_t* __restrict__ dY2, DropArgs dr) {
+  if (dr.A && dr.off) dr.s0 ^= *dr.off;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -413,7 +416,9 @@ __global__ __launch_bounds__(256) void layernorm_part_fold2_kernel(const float* 
 
 __global__ __launch_bounds__(256) void dropout_add_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ X,
                                                           bf16_t* __restrict__ Out, size_t n8, uint32_t thresh,
-                                                          float scale, uint32_t s0, uint32_t s1) {
+                                                          float scale, uint32_t s0, uint32_t s1,
+                                                          const uint32_t* __restrict__ soff) {
+  if (soff) s0 ^= *soff;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     float a[8], o[8];
     unpack8(reinterpret_cast<const uint4*>(A)[i], a);
@@ -634,6 +639,7 @@ extern "C" hipError_t zoo_dropout_add_layernorm_fwd(const void* A, const void* X
   dr.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   dr.s0 = (uint32_t)seed;
   dr.s1 = (uint32_t)(seed >> 32);
+  dr.off = g_seed_off;
   const int blocks = (rows + 3) / 4;
 #define ZOO_LN_DROP(NCH)                                                                                    \
   hipLaunchKernelGGL((layernorm_fwd_reg_kernel<bf16_t, NCH, true>), dim3(blocks), dim3(256), 0, st,        \
@@ -770,6 +776,7 @@ extern "C" hipError_t zoo_layernorm_bwd_drop(const void* dY, const void* X, cons
   dr.scale = p < 1.f ? 1.f / (1.f - p) : 0.f;
   dr.s0 = (uint32_t)seed;
   dr.s1 = (uint32_t)(seed >> 32);
+  dr.off = g_seed_off;
   return ln_bwd_impl(dY, X, 0, g, mean, rstd, dX, dg, db, rows, D, part, dY2, dr, st);
 }
 
@@ -823,6 +830,7 @@ extern "C" hipError_t zoo_dropout_add(const void* A, const void* X, void* Out, s
   if (blocks > 4096) blocks = 4096;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL(dropout_add_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)A,
-                     (const bf16_t*)X, (bf16_t*)Out, n8, thresh, scale, (uint32_t)seed, (uint32_t)(seed >> 32));
+                     (const bf16_t*)X, (bf16_t*)Out, n8, thresh, scale, (uint32_t)seed, (uint32_t)(seed >> 32),
+                     g_seed_off);
   return hipGetLastError();
 }

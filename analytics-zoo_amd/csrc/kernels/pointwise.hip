@@ -148,7 +148,9 @@ ZOO_DEV uint32_t pw_fmix(uint32_t h) {
 // out = keep(i) ? x * scale : 0 with keep(i) a counter hash of (seed, i)
 template <typename T>
 __global__ __launch_bounds__(256) void dropout_kernel(const T* __restrict__ x, T* __restrict__ out, size_t n,
-                                                      uint32_t thresh, float scale, uint32_t s0, uint32_t s1) {
+                                                      uint32_t thresh, float scale, uint32_t s0, uint32_t s1,
+                                                      const uint32_t* __restrict__ soff) {
+  if (soff) s0 ^= *soff;
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
     const uint32_t base = pw_fmix((uint32_t)(i >> 32) ^ s1);
     const uint32_t h = pw_fmix((uint32_t)i * 0x9E3779B1u ^ s0 ^ base);
@@ -277,6 +279,9 @@ static int pw_grid(size_t n) {
 
 using namespace zoo;
 
+const uint32_t* zoo::g_seed_off = nullptr;
+extern "C" void zoo_set_seed_offset(const uint32_t* p) { zoo::g_seed_off = p; }
+
 extern "C" hipError_t zoo_act(const void* x, const void* dy, void* out, size_t n, int f32, int a, float alpha,
                               hipStream_t st) {
   const bool al = ((reinterpret_cast<uintptr_t>(x) | reinterpret_cast<uintptr_t>(dy) |
@@ -307,10 +312,10 @@ extern "C" hipError_t zoo_dropout(const void* x, void* out, size_t n, int f32, f
   const uint32_t s0 = (uint32_t)seed, s1 = (uint32_t)(seed >> 32);
   if (f32)
     hipLaunchKernelGGL(dropout_kernel<float>, dim3(pw_grid(n)), dim3(256), 0, st, (const float*)x, (float*)out, n,
-                       thresh, scale, s0, s1);
+                       thresh, scale, s0, s1, g_seed_off);
   else
     hipLaunchKernelGGL(dropout_kernel<bf16_t>, dim3(pw_grid(n)), dim3(256), 0, st, (const bf16_t*)x,
-                       (bf16_t*)out, n, thresh, scale, s0, s1);
+                       (bf16_t*)out, n, thresh, scale, s0, s1, g_seed_off);
   return hipGetLastError();
 }
 

@@ -29,7 +29,7 @@
 //   u     [G*H, H] bf16 recurrent weight, gate-major rows (Keras order
 //                       LSTM i,f,c,o; GRU z,r,h)   -- U^T [H, G*H] for backward
 //   hseq  [B, T, H]     outputs, in processing order
-//   cseq  [B, T, H]     LSTM cell states (saved for backward)
+//   cseq  [B, T, H]     LSTM cell states / GRU_RA candidate recurrent pre-activations (saved)
 //   gates [B, T, G*H]   activated gates (saved for backward)
 //   dgate [B, T, G*H]   d(pre-activation) = d(xw)
 #include "common.h"
@@ -60,7 +60,7 @@ ZOO_DEV float ractd(float y, int a) {
 
 template <int CELL, int H>
 struct RnnCfg {
-  static constexpr int G = CELL == CELL_LSTM ? 4 : (CELL == CELL_GRU ? 3 : 1);
+  static constexpr int G = CELL == CELL_LSTM ? 4 : ((CELL == CELL_GRU || CELL == CELL_GRU_RA) ? 3 : 1);
   static constexpr int GH = G * H;
   static constexpr int NBLK = H / 16;             // 16-wide hidden column blocks
   static constexpr int NB = (NBLK + 7) / 8;       // blocks per wave (<= 8 waves)
@@ -176,6 +176,21 @@ __global__ __launch_bounds__((RnnCfg<CELL, H>::NW * 64)) void rnn_fwd_kernel(Rnn
             gp[0] = gi; gp[H] = gf; gp[2 * H] = gc; gp[3 * H] = go;
           }
           if (ok && a.cseq != nullptr) a.cseq[bt * H + j] = c;
+        } else if constexpr (CELL == CELL_GRU_RA) {
+          // reset-after GRU: one GEMM for z, r and the candidate's U_n h; the candidate's
+          // recurrent pre-activation an = U_n h + b_hn is saved (cseq) for the backward
+          const float gz = ract(xv[0][i] + acc[0][i], a.iact);
+          const float gr = ract(xv[1][i] + acc[1][i], a.iact);
+          const float an = acc[2][i] + (a.bhn != nullptr ? a.bhn[j] : 0.f);
+          const float gn = ract(xv[2][i] + gr * an, a.act);
+          const float hn = gz * hreg[nb][i] + (1.f - gz) * gn;
+          hreg[nb][i] = hn;
+          hs[cur ^ 1][row * LDH + j] = f2bf(hn);
+          if (ok && a.gates != nullptr) {
+            float* gp = a.gates + bt * GH + j;
+            gp[0] = gz; gp[H] = gr; gp[2 * H] = gn;
+          }
+          if (ok && a.cseq != nullptr) a.cseq[bt * H + j] = an;
         } else {  // GRU phase 1: z, r; stage r*h_{t-1} for the candidate GEMM
           const float gz = ract(xv[0][i] + acc[0][i], a.iact);
           const float gr = ract(xv[1][i] + acc[1][i], a.iact);
@@ -337,6 +352,27 @@ __global__ __launch_bounds__((RnnCfg<CELL, H>::NW * 64)) void rnn_bwd_kernel(Rnn
           }
 #pragma unroll
           for (int g = 0; g < 4; ++g) ds[cur][row * LDA + g * H + j] = f2bf(dgv[g]);
+        } else if constexpr (CELL == CELL_GRU_RA) {
+          // h = z h_p + (1 - z) n,  n = act(xn + r an),  an = U_n h_p + b_hn
+          const float* gp = a.gates + bt * GH + j;
+          const float z = gp[0], r = gp[H], n = gp[2 * H];
+          const float an = a.cseq[bt * H + j];
+          float hp = 0.f;
+          if (t > 0) hp = a.hseq[(bt - 1) * H + j];
+          else if (a.h0 != nullptr && ok) hp = a.h0[(size_t)b * H + j];
+          const float dn = ok ? dh * (1.f - z) * ractd(n, a.act) : 0.f;
+          const float dz = ok ? dh * (hp - n) * ractd(z, a.iact) : 0.f;
+          const float dr = ok ? dn * an * ractd(r, a.iact) : 0.f;
+          const float dan = dn * r;
+          dhd[nb][i] = ok ? dh * z : 0.f;
+          if (ok) {
+            float* dp = a.dgates + bt * GH + j;
+            dp[0] = dz; dp[H] = dr; dp[2 * H] = dn;
+            a.dgn[bt * H + j] = dan;
+          }
+          ds[cur][row * LDA + j] = f2bf(dz);
+          ds[cur][row * LDA + H + j] = f2bf(dr);
+          ds[cur][row * LDA + 2 * H + j] = f2bf(dan);
         } else {  // GRU phase 1: dz and the candidate's pre-activation gradient
           const float* gp = a.gates + bt * GH + j;
           const float z = gp[0], hh = gp[2 * H];
@@ -407,7 +443,7 @@ __global__ __launch_bounds__((RnnCfg<CELL, H>::NW * 64)) void rnn_bwd_kernel(Rnn
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         float v = acc[i];
-        if constexpr (GRU) v += dhd[nb][i];
+        if constexpr (GRU || CELL == CELL_GRU_RA) v += dhd[nb][i];
         dhrec[nb][i] = v;
       }
     }
@@ -455,6 +491,7 @@ extern "C" hipError_t zoo_rnn(const zoo::RnnArgs* a, int cell, int H, int bwd, h
     case zoo::CELL_RNN: return zoo::dispatch_h<zoo::CELL_RNN>(*a, H, bwd != 0, st);
     case zoo::CELL_LSTM: return zoo::dispatch_h<zoo::CELL_LSTM>(*a, H, bwd != 0, st);
     case zoo::CELL_GRU: return zoo::dispatch_h<zoo::CELL_GRU>(*a, H, bwd != 0, st);
+    case zoo::CELL_GRU_RA: return zoo::dispatch_h<zoo::CELL_GRU_RA>(*a, H, bwd != 0, st);
     default: return hipErrorInvalidValue;
   }
 }

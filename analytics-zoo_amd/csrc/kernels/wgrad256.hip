@@ -25,7 +25,11 @@
 //     workgroups so ~one wave of 256 workgroups fills the chip; each split stores its
 //     fp32 tile in MFMA-fragment order (1 KiB fully coalesced per wave store) and an
 //     ordered fold kernel sums the splits into dW (deterministic, no atomics). A single
-//     split accumulates straight into dW.
+//     split accumulates straight into dW. When the live part of the split tiles is small
+//     (<= ZOO_WGRAD256_ATOMIC_MB of added bytes, default 32 MB: the 64/128-channel ResNet
+//     shapes) and the deterministic mode is off, the splits add their tiles into dW with fp32
+//     atomics instead: no partial buffer, no fold launch (the r4 folds moved up to 64 MB per
+//     call through HBM beside the data-gradient chain).
 //
 // Reference parity: the weight-gradient half of BigDL Linear / SpatialConvolution
 // accGradParameters, as wgrad.hip.
@@ -48,6 +52,7 @@ struct W2Geom {
   int M, N, K;        // reduction rows, dY columns (dW rows), X columns (dW cols)
   int ldy, ldx, ldw;  // leading dims (elements); ldy, ldx % 8 == 0
   int m_per_split, splits, tiles_n, tiles_k;
+  int atomic;         // splits > 1 without partials: every split adds its tile into dW with fp32 atomics
 };
 
 // implicit-GEMM (im2col) form of the X operand for convolutions: X[m][k] with m = output
@@ -295,9 +300,17 @@ __global__ __launch_bounds__(W2_NT, 1) void wgrad256_kernel(const bf16_t* __rest
             const int col = k0 + wn * 64 + qb * 32 + j * 16 + fr;
             const int row = n0 + wm * 128 + qa * 64 + i * 16 + fq * 4;
             if (col < g.K) {
+              if (g.atomic) {
+                // no-return global_atomic_add_f32 (-munsafe-fp-atomics), executed at the memory
+                // side: one 16-lane x 4-row wave instruction per accumulator register
 #pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (row + r < g.N) dW[(size_t)(row + r) * g.ldw + col] += acc[qa][qb][i][j][r];
+                for (int r = 0; r < 4; ++r)
+                  if (row + r < g.N) atomicAdd(dW + (size_t)(row + r) * g.ldw + col, acc[qa][qb][i][j][r]);
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (row + r < g.N) dW[(size_t)(row + r) * g.ldw + col] += acc[qa][qb][i][j][r];
+              }
             }
           }
   }
@@ -380,10 +393,25 @@ extern "C" int zoo_wgrad256_plan(int M, int N, int K, int* m_per_split) {
   return splits;
 }
 
+// split-K by fp32 atomics (no partials) for this plan? Never in the deterministic mode (set
+// by the host through zoo_wgrad256_set_atomic(0)); the added bytes are splits x the live
+// (N x K) part of the output.
+static int g_w256_atomic = 1;
+extern "C" void zoo_wgrad256_set_atomic(int on) { g_w256_atomic = on; }
+
+static bool w2_atomic(int splits, int N, int K) {
+  static const double mb_max = [] {
+    const char* e = getenv("ZOO_WGRAD256_ATOMIC_MB");
+    return e ? atof(e) : 32.0;
+  }();
+  return g_w256_atomic && splits > 1 && (double)splits * N * K * 4 / 1e6 <= mb_max;
+}
+
 extern "C" size_t zoo_wgrad256_part_floats(int M, int N, int K) {
   int mps = 0;
   const int splits = zoo_wgrad256_plan(M, N, K, &mps);
   const size_t tiles = (size_t)((N + W2_T - 1) / W2_T) * ((K + W2_T - 1) / W2_T);
+  if (w2_atomic(splits, N, K)) return 0;
   return splits > 1 ? (size_t)splits * tiles * W2_T * W2_T : 0;
 }
 
@@ -395,7 +423,9 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
   g.tiles_n = (N + W2_T - 1) / W2_T;
   g.tiles_k = (K + W2_T - 1) / W2_T;
   g.splits = zoo_wgrad256_plan(M, N, K, &g.m_per_split);
-  if (g.splits > 1 && !part) return hipErrorInvalidValue;
+  g.atomic = w2_atomic(g.splits, N, K) ? 1 : 0;
+  if (g.splits > 1 && !g.atomic && !part) return hipErrorInvalidValue;
+  if (g.atomic || g.splits <= 1) part = nullptr;
   const int tiles = g.tiles_n * g.tiles_k;
   const size_t smem = 4 * 2 * W2_HALF;  // 2 buffers x (A, B) x 2 halves = 128 KiB
   static bool attr = false;
@@ -416,11 +446,11 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
   }();
   if (pp)
     hipLaunchKernelGGL((wgrad256_kernel<true, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
+                       (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
   else
     hipLaunchKernelGGL((wgrad256_kernel<false, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
-  if (g.splits > 1) {
+                       (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
+  if (g.splits > 1 && !g.atomic) {
     const size_t total = (size_t)tiles * 8 * 32 * 64;
     hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);
   }
@@ -441,7 +471,9 @@ extern "C" hipError_t zoo_wgrad256_conv(const void* dY, const void* X, float* dW
   g.tiles_n = (g.N + W2_T - 1) / W2_T;
   g.tiles_k = (g.K + W2_T - 1) / W2_T;
   g.splits = zoo_wgrad256_plan(g.M, g.N, g.K, &g.m_per_split);
-  if (g.splits > 1 && !part) return hipErrorInvalidValue;
+  g.atomic = w2_atomic(g.splits, g.N, g.K) ? 1 : 0;
+  if (g.splits > 1 && !g.atomic && !part) return hipErrorInvalidValue;
+  if (g.atomic || g.splits <= 1) part = nullptr;
   const W2Conv cv{H, W, C, P, Q, S, sh, sw, ph, pw, dh, dw};
   const int tiles = g.tiles_n * g.tiles_k;
   const size_t smem = 4 * 2 * W2_HALF;
@@ -452,8 +484,8 @@ extern "C" hipError_t zoo_wgrad256_conv(const void* dY, const void* X, float* dW
     attr = true;
   }
   hipLaunchKernelGGL((wgrad256_kernel<false, true>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                     (const bf16_t*)X, dW, g.splits > 1 ? part : nullptr, g, w2_zero_page(), cv);
-  if (g.splits > 1) {
+                     (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
+  if (g.splits > 1 && !g.atomic) {
     const size_t total = (size_t)tiles * 8 * 32 * 64;
     hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);
   }

@@ -24,6 +24,8 @@ hipError_t zoo_jpeg_color_resize(const uint8_t*, void*, const zoo::JpegGeom*, in
 hipError_t zoo_prob_nll(const void*, int, const int64_t*, float*, float*, float*, int, int, float, int, int,
                         hipStream_t);
 void zoo_optim_zero_grad(int);
+void zoo_optim_device_hparams(const float*);
+void zoo_set_seed_offset(const uint32_t*);
 hipError_t zoo_prob_nll_mean(const void*, int, const int64_t*, float*, float*, int, int, float, int, int, hipStream_t);
 hipError_t zoo_prob_nll_grad(const void*, int, const int64_t*, const float*, const float*, float*, int, int, float, int,
                              hipStream_t);
@@ -76,6 +78,7 @@ hipError_t zoo_l2norm_scale_bwd(const void*, const void*, const float*, const fl
 hipError_t zoo_wgrad256(const void*, const void*, float*, float*, int, int, int, int, int, int, hipStream_t);
 size_t zoo_wgrad256_part_floats(int, int, int);
 void zoo_wgrad256_target(int);
+void zoo_wgrad256_set_atomic(int);
 hipError_t zoo_wgrad256_conv(const void*, const void*, float*, float*, int, int, int, int, int, int, int, int, int, int,
                              int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_stats_finalize(float*, int, int, hipStream_t);
@@ -777,6 +780,7 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
       (int64_t)g.N * g.H * g.W * g.C < (1LL << 40)) {
     check_al16(x.data_ptr(), "conv_wgrad x");
     check_al16(dy.data_ptr(), "conv_wgrad dy");
+    zoo_wgrad256_set_atomic(wgrad_partial() ? 0 : 1);   // atomics split-K unless deterministic
     const size_t pf = zoo_wgrad256_part_floats(g.M, g.K, g.Ktot);
     torch::Tensor part;
     if (pf) part = torch::empty({(int64_t)pf}, dw.options());
@@ -828,6 +832,7 @@ void linear_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor dw) {
   TORCH_CHECK(M < (1LL << 31) && N < (1 << 30) && K < (1 << 30) && M * dy.stride(0) < (1LL << 40),
               "linear_wgrad: size out of range");
   if (M == 0 || N == 0 || K == 0) return;
+  zoo_wgrad256_set_atomic(wgrad_partial() ? 0 : 1);     // atomics split-K unless deterministic
   const size_t pf = zoo_wgrad256_part_floats((int)M, (int)N, (int)K);
   torch::Tensor part;
   if (pf) part = torch::empty({(int64_t)pf}, dw.options());
@@ -2584,8 +2589,8 @@ torch::Tensor qgemm(torch::Tensor a, torch::Tensor w, torch::Tensor amax, torch:
 
 // ---- persistent recurrent cells (rnn.hip): cell 0 SimpleRNN, 1 LSTM, 2 GRU ----
 int rnn_gates(int64_t cell) {
-  TORCH_CHECK(cell >= 0 && cell <= 2, "rnn: cell must be 0 (SimpleRNN), 1 (LSTM) or 2 (GRU)");
-  return cell == 1 ? 4 : (cell == 2 ? 3 : 1);
+  TORCH_CHECK(cell >= 0 && cell <= 3, "rnn: cell must be 0 (SimpleRNN), 1 (LSTM), 2 (GRU) or 3 (GRU reset-after)");
+  return cell == 1 ? 4 : (cell >= 2 ? 3 : 1);
 }
 
 void rnn_check_state(const c10::optional<torch::Tensor>& s, int64_t B, int64_t H, const char* name) {
@@ -2602,7 +2607,7 @@ void rnn_check_acts(int64_t act, int64_t iact) {
 // xw [B, T, G*H] fp32 (bias included), u [G*H, H] bf16 -> {hseq [B,T,H], cT [B,H] (LSTM), cseq, gates}
 std::vector<torch::Tensor> rnn_fwd(torch::Tensor xw, torch::Tensor u, c10::optional<torch::Tensor> h0,
                                    c10::optional<torch::Tensor> c0, int64_t cell, int64_t act, int64_t iact,
-                                   bool save) {
+                                   bool save, c10::optional<torch::Tensor> bhn) {
   req(xw, at::kFloat, "xw");
   req(u, at::kBFloat16, "u");
   const int G = rnn_gates(cell);
@@ -2618,7 +2623,11 @@ std::vector<torch::Tensor> rnn_fwd(torch::Tensor xw, torch::Tensor u, c10::optio
   auto hseq = torch::empty({B, T, H}, f32);
   torch::Tensor cT, cseq, gates;
   if (cell == 1) cT = torch::empty({B, H}, f32);
-  if (save && cell == 1) cseq = torch::empty({B, T, H}, f32);
+  if (save && (cell == 1 || cell == 3)) cseq = torch::empty({B, T, H}, f32);
+  if (bhn.has_value() && bhn->defined()) {
+    req(*bhn, at::kFloat, "bhn");
+    TORCH_CHECK(cell == 3 && bhn->numel() == H, "rnn_fwd: bhn is the [H] candidate bias of the GRU_RA cell");
+  }
   if (save && cell != 0) gates = torch::empty({B, T, G * H}, f32);
   zoo::RnnArgs a{};
   a.xw = xw.data_ptr<float>();
@@ -2629,6 +2638,7 @@ std::vector<torch::Tensor> rnn_fwd(torch::Tensor xw, torch::Tensor u, c10::optio
   a.cseq = cseq.defined() ? cseq.data_ptr<float>() : nullptr;
   a.gates = gates.defined() ? gates.data_ptr<float>() : nullptr;
   a.cT = cT.defined() ? cT.data_ptr<float>() : nullptr;
+  a.bhn = opt_ptr<float>(bhn);
   a.B = (int)B; a.T = (int)T; a.act = (int)act; a.iact = (int)iact;
   check_hip(zoo_rnn(&a, (int)cell, (int)H, 0, cur_stream()), "rnn_fwd");
   return {hseq, cT, cseq, gates};
@@ -2655,8 +2665,8 @@ std::vector<torch::Tensor> rnn_bwd(c10::optional<torch::Tensor> dhseq, c10::opti
   rnn_check_state(dcT, B, H, "dcT");
   rnn_check_state(h0, B, H, "h0");
   rnn_check_state(c0, B, H, "c0");
-  if (cell == 1) {
-    TORCH_CHECK(cseq.has_value() && cseq->defined(), "rnn_bwd: LSTM needs the saved cell states");
+  if (cell == 1 || cell == 3) {
+    TORCH_CHECK(cseq.has_value() && cseq->defined(), "rnn_bwd: LSTM / GRU_RA need the saved cseq");
     req(*cseq, at::kFloat, "cseq");
     TORCH_CHECK(cseq->sizes() == hseq.sizes(), "rnn_bwd: cseq shape");
   }
@@ -2669,8 +2679,9 @@ std::vector<torch::Tensor> rnn_bwd(c10::optional<torch::Tensor> dhseq, c10::opti
   auto f32 = hseq.options();
   auto dgates = torch::empty({B, T, G * H}, f32);
   auto dh0 = torch::empty({B, H}, f32);
-  torch::Tensor dc0;
+  torch::Tensor dc0, dgn;
   if (cell == 1) dc0 = torch::empty({B, H}, f32);
+  if (cell == 3) dgn = torch::empty({B, T, H}, f32);
   zoo::RnnArgs a{};
   a.u = ut.data_ptr();
   a.h0 = opt_ptr<float>(h0);
@@ -2683,9 +2694,10 @@ std::vector<torch::Tensor> rnn_bwd(c10::optional<torch::Tensor> dhseq, c10::opti
   a.dgates = dgates.data_ptr<float>();
   a.dh0 = dh0.data_ptr<float>();
   a.dc0 = dc0.defined() ? dc0.data_ptr<float>() : nullptr;
+  a.dgn = dgn.defined() ? dgn.data_ptr<float>() : nullptr;
   a.B = (int)B; a.T = (int)T; a.act = (int)act; a.iact = (int)iact;
   check_hip(zoo_rnn(&a, (int)cell, (int)H, 1, cur_stream()), "rnn_bwd");
-  return {dgates, dh0, dc0};
+  return {dgates, dh0, dc0, dgn};
 }
 
 }  // namespace
@@ -2878,6 +2890,26 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_bwd", &gap_bwd);
   m.def("softmax_xent", &softmax_xent);
   m.def("prob_nll_mean", &prob_nll_mean);
+  m.def("optim_device_hparams", [](c10::optional<torch::Tensor> hp) {
+          if (hp.has_value() && hp->defined()) {
+            req(*hp, at::kFloat, "hp");
+            TORCH_CHECK(hp->is_cuda() && hp->numel() >= 4 && hp->is_contiguous(), "optim_device_hparams: fp32 [4] GPU");
+            zoo_optim_device_hparams(hp->data_ptr<float>());
+          } else {
+            zoo_optim_device_hparams(nullptr);
+          }
+        },
+        "optimizer kernels read (lr, bc1, bc2, first_step) from this device buffer while set (None: off)");
+  m.def("set_dropout_seed_offset", [](c10::optional<torch::Tensor> off) {
+          if (off.has_value() && off->defined()) {
+            TORCH_CHECK(off->is_cuda() && off->scalar_type() == at::kInt && off->numel() >= 1,
+                        "set_dropout_seed_offset: int32 GPU tensor");
+            zoo_set_seed_offset(reinterpret_cast<const uint32_t*>(off->data_ptr<int>()));
+          } else {
+            zoo_set_seed_offset(nullptr);
+          }
+        },
+        "every dropout kernel xors this device word into its seed (hipGraph replays: fresh masks per step)");
   m.def("optim_zero_grad", [](bool on) { zoo_optim_zero_grad(on ? 1 : 0); },
         "sgd / adam / adaptive clear each gradient element after reading it (engine: no per-step grad fill)");
   m.def("sgd", &sgd);
@@ -2924,6 +2956,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd, py::arg("dout"), py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"),
         py::arg("o"), py::arg("lse"), py::arg("causal"), py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("attn_bwd_strided", &attn_bwd_strided);
-  m.def("rnn_fwd", &rnn_fwd);
+  m.def("rnn_fwd", &rnn_fwd, py::arg("xw"), py::arg("u"), py::arg("h0"), py::arg("c0"), py::arg("cell"),
+        py::arg("act"), py::arg("iact"), py::arg("save"), py::arg("bhn") = py::none());
   m.def("rnn_bwd", &rnn_bwd);
 }

@@ -32,6 +32,12 @@ def _trunc_normal_(t, std=0.1):
     return t
 
 
+def _mm(a, w, b=None):
+    """a @ w (+ b) with w [in, out] on the native MFMA GEMM (zoo.ops.linear)."""
+    from zoo import ops
+    return ops.linear(a, w.t().contiguous(), b)
+
+
 class AttentionRNN(nn.Module):
     """Stacked GRU cells (relu activation, input dropout) driven through the reference's
     AttentionRNNWrapper step: additive attention of the last cell state over the whole input
@@ -52,7 +58,12 @@ class AttentionRNN(nn.Module):
 
     @staticmethod
     def _relu_gru(cell, x, h):
-        # GRUCell with relu instead of tanh for the candidate (Keras GRUCell(activation="relu"))
+        # GRUCell with relu instead of tanh for the candidate (Keras GRUCell(activation="relu")):
+        # on the GPU one native input GEMM + one recurrent-kernel step (reset-after GRU cell)
+        from zoo.pipeline.api.net.native_lower import gru_cell_native
+        y = gru_cell_native(x, h, cell.weight_ih, cell.weight_hh, cell.bias_ih, cell.bias_hh, act="relu")
+        if y is not None:
+            return y.to(x.dtype)
         gi = nn.functional.linear(x, cell.weight_ih, cell.bias_ih)
         gh = nn.functional.linear(h, cell.weight_hh, cell.bias_hh)
         ir, iz, in_ = gi.chunk(3, 1)
@@ -65,12 +76,13 @@ class AttentionRNN(nn.Module):
     def forward(self, X):                                     # X [B, T, d] -> [B, hid[-1]]
         B, T, _ = X.shape
         hs = [X.new_zeros(B, c.hidden_size) for c in self.cells]
-        xw = X @ self.W1 + self.b2                               # [B, T, d]
+        mm = _mm if X.is_cuda else (lambda a, w, b=None: a @ w if b is None else a @ w + b)
+        xw = mm(X, self.W1, self.b2)                             # [B, T, d]
         for t in range(T):
-            score = (xw + (hs[-1] @ self.W2)[:, None]) @ self.V      # [B, T, 1]
+            score = mm(xw + mm(hs[-1], self.W2)[:, None], self.V)     # [B, T, 1]
             att = torch.softmax(score, dim=1)
             xa = (att * X).sum(1)
-            inp = torch.cat([X[:, t], xa], 1) @ self.W3 + self.b3
+            inp = mm(torch.cat([X[:, t], xa], 1), self.W3, self.b3)
             for i, cell in enumerate(self.cells):
                 hs[i] = self._relu_gru(cell, self.drop(inp), hs[i])
                 inp = hs[i]
@@ -122,7 +134,7 @@ class MTNetNet(nn.Module):
         mem = self.memory(long_x)                              # [B, n, H]
         ctx = self.context(long_x)
         q = self.query(short_x[:, None])                       # [B, 1, H]
-        prob = torch.softmax(mem @ q.transpose(1, 2), dim=1)   # [B, n, 1] attention over the blocks
+        prob = torch.softmax((mem * q).sum(-1, keepdim=True), dim=1)   # [B, n, 1] attention over the blocks
         pred_x = torch.cat([ctx * prob, q], 1).reshape(B, -1)
         y = self.out(pred_x)
         if self.ar_fc is not None:

@@ -12,6 +12,8 @@ convolution data-gradient driver.
 """
 import math
 
+import os
+
 import torch
 
 from zoo.ops._native import native
@@ -152,12 +154,36 @@ def flip_weights(w, K, R, S, C, r0=0, s0=0, Ra=None, Sb=None, sh=1, sw=1):
     return native().flip_weights(w, K, R, S, C, r0, s0, Ra, Sb, sh, sw)
 
 
+# fault injection for the parity tests (tests/test_gpu_native_nets.py): ZOO_FAULT_DGRAD="k:s" scales
+# the k-th conv data gradient of the process (0-based, counted from reset_fault_counter) by s --
+# proof that a per-layer parity bound catches a 5 % error in ONE layer's backward
+_DGRAD_CALLS = [0]
+
+
+def reset_fault_counter():
+    _DGRAD_CALLS[0] = 0
+
+
+def _fault(dx):
+    spec = os.environ.get("ZOO_FAULT_DGRAD")
+    if spec:
+        k, s = spec.split(":")
+        if _DGRAD_CALLS[0] == int(k) and dx is not None:
+            dx.mul_(float(s))
+        _DGRAD_CALLS[0] += 1
+    return dx
+
+
 def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None,
                resid_inplace=False):
     """dX [N,H,W,C] of y = conv(x, w) given dY [N,P,Q,K] and the bf16 packed weight.
     ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer).
     ``resid_inplace``: ``resid`` is a temporary the caller gives away; strided dgrads
     with tap-less parity classes accumulate into it instead of a copy of it."""
+    return _fault(_conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace))
+
+
+def _conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace):
     sh, sw = stride
     if (sh, sw) == (1, 1) or dil != (1, 1):
         wt = flip_weights(wb, K, R, S, C)

@@ -226,6 +226,27 @@ class OptimMethod:
     # optimizers whose native step clears the gradient after reading it when asked (zero_grad)
     _native_zero_grad = False
 
+    # -- device hyper-parameters (hipGraph-captured updates) --------------------
+    # A captured optimizer kernel would replay the learning rate / bias corrections of the
+    # capture step. With ``enable_device_hparams`` the native kernels read them from a device
+    # [lr, bc1, bc2, first_step] buffer that ``stage_device_hparams`` refreshes (one async
+    # host->device copy on the current stream) before each step, captured or eager.
+    _dev_hp = None
+
+    def _hparams(self):
+        """[lr, bc1, bc2, first_step] of the upcoming step (the kernels' per-step scalars)."""
+        return [self.current_lr(), 1.0, 1.0, 0.0]
+
+    def enable_device_hparams(self, device):
+        from zoo.ops.devscalar import DeviceStager
+        self._hp_stager = DeviceStager(4, torch.float32, device)
+        self._dev_hp = self._hp_stager.dev
+        self.stage_device_hparams()
+
+    def stage_device_hparams(self):
+        if self._dev_hp is not None:
+            self._hp_stager.stage(self._hparams())
+
     def step(self, master, grad, bf16=None, gscale=1.0, zero_grad=False):
         """Update ``master`` (fp32 flat tensor or shard) in place from ``grad``. With
         ``zero_grad`` the native kernels also clear ``grad`` (returns True when they did)."""
@@ -249,15 +270,22 @@ class OptimMethod:
         b16 = bf16 if (bf16 is None or full) else bf16[lo:hi]
         bs = bufs if full else [t[lo:hi] for t in bufs]
         if master.is_cuda:
-            if zero_grad and self._native_zero_grad:
-                native().optim_zero_grad(True)
-                try:
+            hp = self._dev_hp if (self._dev_hp is not None and self._dev_hp.device == master.device) else None
+            if hp is not None:
+                native().optim_device_hparams(hp)
+            try:
+                if zero_grad and self._native_zero_grad:
+                    native().optim_zero_grad(True)
+                    try:
+                        self._step_native(m, g, b16, bs, lr, float(gscale))
+                    finally:
+                        native().optim_zero_grad(False)
+                    cleared = True
+                else:
                     self._step_native(m, g, b16, bs, lr, float(gscale))
-                finally:
-                    native().optim_zero_grad(False)
-                cleared = True
-            else:
-                self._step_native(m, g, b16, bs, lr, float(gscale))
+            finally:
+                if hp is not None:
+                    native().optim_device_hparams(None)
         else:
             with torch.no_grad():
                 self._step_torch(m, g * gscale, bs, lr)
@@ -341,6 +369,9 @@ class SGD(OptimMethod):
                  learningrate_decay=self.learning_rate_decay)
         return h
 
+    def _hparams(self):
+        return [self.current_lr(), 1.0, 1.0, 1.0 if self.state["evalCounter"] == 0 else 0.0]
+
     def _step_native(self, master, grad, bf16, bufs, lr, gscale):
         first = self.state["evalCounter"] == 0
         native().sgd(master, grad, bufs[0] if self.momentum else None, bf16, lr, self.momentum, self.dampening,
@@ -379,6 +410,10 @@ class Adam(OptimMethod):
     def _bc(self):
         t = self.state["neval"]
         return 1 - self.beta_1 ** t, 1 - self.beta_2 ** t
+
+    def _hparams(self):
+        bc1, bc2 = self._bc()
+        return [self.current_lr(), bc1, bc2, 0.0]
 
     def _step_native(self, master, grad, bf16, bufs, lr, gscale):
         bc1, bc2 = self._bc()
@@ -452,6 +487,9 @@ class _Adaptive(OptimMethod):
 
     def _native_args(self):
         raise NotImplementedError
+
+    def _hparams(self):
+        return [self.current_lr(), self._native_args()[3], 1.0, 0.0]
 
     def _step_native(self, master, grad, bf16, bufs, lr, gscale):
         rho, rho2, eps, bc1 = self._native_args()

@@ -14,8 +14,12 @@ tensors), only ``forward`` computes on the zoo kernels:
 * max / average / global pooling -> the NHWC pooling kernels;
 * ``BatchNorm2d`` alone -> the native NHWC batch norm (training and inference);
 * ReLU / Tanh / Sigmoid / ELU / ... -> the native activation kernel; LRN -> the native LRN;
-* ``nn.LSTM`` (single direction or bidirectional, any layer count) -> the persistent recurrent
-  kernel (``ops.rnn.recurrent``).
+* ``nn.LSTM`` / ``nn.GRU`` (single direction or bidirectional, any layer count) and
+  ``nn.GRUCell`` -> the persistent recurrent kernel (``ops.rnn.recurrent``; torch's reset-after
+  GRU is its CELL_GRU_RA cell);
+* grouped / depthwise ``nn.Conv2d`` (Caffe ``group``, MobileNet) -> per-group implicit GEMMs /
+  the depthwise kernel; ``nn.ConvTranspose2d`` (Caffe ``Deconvolution``) -> the conv
+  data-gradient kernels.
 
 Layout: a native module takes NCHW and returns NCHW whose memory is channels-last (a
 ``permute`` view of the NHWC kernel output), so the next native module's NCHW -> NHWC permute is
@@ -103,19 +107,59 @@ class _Twin:
 
 
 class ZConv2d(_Twin, nn.Conv2d):
-    """nn.Conv2d (groups = 1, zero padding) [+ folded eval BatchNorm2d] [+ fused activation] on
-    the native implicit-GEMM kernels (igemm / igemm2 / pw)."""
+    """nn.Conv2d (zero padding) [+ folded eval BatchNorm2d] [+ fused activation] on the native
+    kernels: dense convs on the implicit-GEMM kernels (igemm / igemm2 / pw); depthwise convs
+    (groups = in_channels, any channel multiplier, <= 3x3 taps) on the depthwise kernel
+    (dwconv.hip); other grouped convs (Caffe ``group``, e.g. AlexNet's group 2) as one
+    implicit-GEMM conv per group over that group's channel slice."""
     _zoo_bn = None
     _zoo_act = None
     _zoo_cache = None
 
+    def _group_mode(self):
+        g, C, K = self.groups, self.in_channels, self.out_channels
+        if g == 1:
+            return "dense"
+        R, S = self.kernel_size
+        if g == C and K % C == 0 and R * S <= 9 and tuple(self.dilation) == (1, 1):
+            return "depthwise"
+        if C % g == 0 and K % g == 0:
+            return "grouped"
+        return None
+
     def _native_supported(self, x):
-        return (_native_ok(x) and self.groups == 1 and self.padding_mode == "zeros" and
-                isinstance(self.padding, tuple) and len(self.kernel_size) == 2)
+        return (_native_ok(x) and self.padding_mode == "zeros" and isinstance(self.padding, tuple) and
+                len(self.kernel_size) == 2 and self._group_mode() is not None)
+
+    def _folded_wb(self, training_bn):
+        """(fp32 weight [K, C/groups, R, S], bias [K]) with an eval BatchNorm folded in."""
+        bn = self._zoo_bn
+        w = self.weight.float()
+        K = w.shape[0]
+        b = self.bias.float() if self.bias is not None else torch.zeros(K, device=w.device)
+        if bn is not None and not training_bn:
+            s = torch.rsqrt(bn.running_var.float() + bn.eps)
+            if bn.weight is not None:
+                s = s * bn.weight.float()
+            b = (b - bn.running_mean.float()) * s + (bn.bias.float() if bn.bias is not None else 0.0)
+            w = w * s[:, None, None, None]
+        return w, b
+
+    @staticmethod
+    def _pack(w, b):
+        """[K, C, R, S] fp32 -> (packed [Kp, ceil8(R*S*Cp)], bias [Kp]) in the implicit-GEMM layout."""
+        K, C, R, S = w.shape
+        cp, kp = _cin_pad(C), ops.ceil8(K)
+        w2 = F.pad(w.permute(0, 2, 3, 1), (0, cp - C, 0, 0, 0, 0, 0, kp - K)).reshape(kp, R * S * cp)
+        ld = ops.ceil8(R * S * cp)
+        if ld != R * S * cp:
+            w2 = F.pad(w2, (0, ld - R * S * cp))
+        return w2, F.pad(b, (0, kp - K))
 
     def _packed(self, training_bn):
-        """(packed weight [Kp, ceil8(R*S*Cp)], bias [Kp]) with an eval BatchNorm folded in; cached by
-        parameter versions when no gradient is needed."""
+        """Native operands for this conv's group mode, cached by parameter versions when no
+        gradient is needed: dense -> (packed weight, bias); grouped -> a list of those per group;
+        depthwise -> (tap-major weight [R*S, Kp], bias [Kp])."""
         bn = self._zoo_bn
         need_grad = torch.is_grad_enabled() and (self.weight.requires_grad or
                                                  (self.bias is not None and self.bias.requires_grad))
@@ -130,26 +174,24 @@ class ZConv2d(_Twin, nn.Conv2d):
                                                          bn.running_mean.data_ptr()),
                    _kern.weights_epoch(), _kern.stats_epoch())
             if self._zoo_cache is not None and self._zoo_cache[0] == key:
-                return self._zoo_cache[1], self._zoo_cache[2]
-        w = self.weight.float()
-        K, C, R, S = w.shape
-        b = self.bias.float() if self.bias is not None else torch.zeros(K, device=w.device)
-        if bn is not None and not training_bn:
-            s = torch.rsqrt(bn.running_var.float() + bn.eps)
-            if bn.weight is not None:
-                s = s * bn.weight.float()
-            b = (b - bn.running_mean.float()) * s + (bn.bias.float() if bn.bias is not None else 0.0)
-            w = w * s[:, None, None, None]
-        cp, kp = _cin_pad(C), ops.ceil8(K)
-        w2 = F.pad(w.permute(0, 2, 3, 1), (0, cp - C, 0, 0, 0, 0, 0, kp - K)).reshape(kp, R * S * cp)
-        ld = ops.ceil8(R * S * cp)
-        if ld != R * S * cp:
-            w2 = F.pad(w2, (0, ld - R * S * cp))
-        b = F.pad(b, (0, kp - K))
+                return self._zoo_cache[1]
+        w, b = self._folded_wb(training_bn)
+        mode = self._group_mode()
+        K, Cg, R, S = w.shape
+        if mode == "dense":
+            out = self._pack(w, b)
+        elif mode == "grouped":
+            g = self.groups
+            Kg = K // g
+            out = [self._pack(w[i * Kg:(i + 1) * Kg], b[i * Kg:(i + 1) * Kg]) for i in range(g)]
+        else:   # depthwise: output channel o reads input channel o // multiplier
+            kp = ops.ceil8(K)
+            out = (F.pad(w.reshape(K, R * S).t(), (0, kp - K)), F.pad(b, (0, kp - K)))
         if key is not None:
-            w2, b = w2.detach().contiguous(), b.detach().contiguous()
-            self._zoo_cache = (key, w2, b)
-        return w2, b
+            out = [(a.detach().contiguous(), c.detach().contiguous()) for a, c in out] if mode == "grouped" else \
+                (out[0].detach().contiguous(), out[1].detach().contiguous())
+            self._zoo_cache = (key, out)
+        return out
 
     def forward(self, x):
         bn, act = self._zoo_bn, self._zoo_act
@@ -161,15 +203,74 @@ class ZConv2d(_Twin, nn.Conv2d):
             return P.act_ref(y, act) if act else y
         training_bn = bn is not None and bn.training
         K, C = self.out_channels, self.in_channels
-        w2, b = self._packed(training_bn)
+        mode = self._group_mode()
         fused = act if (act in _FUSABLE and not training_bn) else None
-        y = ops.conv2d_nhwc(to_nhwc(x, _cin_pad(C)), w2, b, kernel=tuple(self.kernel_size), stride=tuple(self.stride),
-                            pad=tuple(self.padding), dil=tuple(self.dilation), act=fused)
+        geo = dict(kernel=tuple(self.kernel_size), stride=tuple(self.stride), pad=tuple(self.padding))
+        if mode == "dense":
+            w2, b = self._packed(training_bn)
+            y = ops.conv2d_nhwc(to_nhwc(x, _cin_pad(C)), w2, b, dil=tuple(self.dilation), act=fused, **geo)
+        elif mode == "grouped":
+            g = self.groups
+            Cg, Kg = C // g, K // g
+            xn = to_nhwc(x)
+            outs = []
+            for i, (w2, b) in enumerate(self._packed(training_bn)):
+                xg = xn[..., i * Cg:(i + 1) * Cg]
+                if _cin_pad(Cg) != Cg:
+                    xg = F.pad(xg, (0, _cin_pad(Cg) - Cg))
+                yg = ops.conv2d_nhwc(xg.contiguous(), w2, b, dil=tuple(self.dilation), act=fused, **geo)
+                outs.append(yg[..., :Kg])
+            y = torch.cat(outs, -1)
+        else:
+            from zoo.ops.nn import depthwise_conv2d_nhwc
+            wdw, b = self._packed(training_bn)
+            xn = to_nhwc(x)
+            if K != C:
+                xn = xn.repeat_interleave(K // C, dim=3)
+            if ops.ceil8(K) != K:
+                xn = F.pad(xn, (0, ops.ceil8(K) - K))
+            dfuse = fused if fused == "relu" else None
+            y = depthwise_conv2d_nhwc(xn, wdw, b, act=dfuse, **geo)
+            if fused is not None and dfuse is None:
+                y = P.activation(y, fused)
         if training_bn:
             y = _bn_nhwc(y, bn, K)
         if act and fused is None:
             y = P.activation(y, act)
         return from_nhwc(y, K, x.dtype)
+
+
+class ZConvTranspose2d(_Twin, nn.ConvTranspose2d):
+    """nn.ConvTranspose2d (Caffe ``Deconvolution``, groups 1, no dilation) on the conv data-gradient
+    kernels: the transposed conv IS the dgrad of the conv whose weight it holds
+    (ops.conv.conv_transpose2d_nhwc); backward is a forward conv plus a weight gradient."""
+
+    def _native_supported(self, x):
+        return (_native_ok(x) and self.groups == 1 and tuple(self.dilation) == (1, 1) and
+                self.padding_mode == "zeros" and len(self.kernel_size) == 2)
+
+    def forward(self, x, output_size=None):
+        if not self._native_supported(x):
+            return nn.ConvTranspose2d.forward(self, x, output_size)
+        from zoo.ops.conv import conv_transpose2d_nhwc
+        R, S = self.kernel_size
+        sh, sw = self.stride
+        ph, pw = self.padding
+        opad = self._output_padding(x, output_size, list(self.stride), list(self.padding), list(self.kernel_size),
+                                    2, list(self.dilation))
+        H, W = x.shape[-2:]
+        oh = (H - 1) * sh - 2 * ph + R + opad[0]
+        ow = (W - 1) * sw - 2 * pw + S + opad[1]
+        Cin, Cout = self.in_channels, self.out_channels
+        cp, kp = ops.ceil8(Cin), ops.ceil8(Cout)
+        wd = F.pad(self.weight.float(), (0, 0, 0, 0, 0, kp - Cout, 0, cp - Cin))     # [cp, kp, R, S]
+        wf = wd.permute(0, 2, 3, 1).reshape(cp, R * S * kp)
+        if ops.ceil8(R * S * kp) != R * S * kp:
+            wf = F.pad(wf, (0, ops.ceil8(R * S * kp) - R * S * kp))
+        y = conv_transpose2d_nhwc(to_nhwc(x, cp), wf, (R, S), (sh, sw), (ph, pw), (oh, ow), kp)[..., :Cout]
+        if self.bias is not None:
+            y = y + self.bias.to(y.dtype)
+        return from_nhwc(y, Cout, x.dtype)
 
 
 def _bn_nhwc(y, bn, C):
@@ -396,12 +497,91 @@ class ZLSTM(_Twin, nn.LSTM):
         return out.to(x.dtype), (hn.to(x.dtype), cn.to(x.dtype))
 
 
+def _zrn(t, H):
+    """torch GRU gate blocks (r, z, n) -> the kernel's order (z, r, n)."""
+    return torch.cat([t[H:2 * H], t[:H], t[2 * H:]], 0)
+
+
+def _gru_operands(W, U, b_ih, b_hh, H):
+    """(W [3H, D], U [3H, H], xw bias [3H], b_hn [H]) of a torch GRU layer / cell in the
+    reset-after kernel's gate order: the input projection carries b_ih (+ b_hh for z and r); the
+    candidate's recurrent bias b_hn is applied inside the reset gate (rnn.hip CELL_GRU_RA)."""
+    Wz, Uz = _zrn(W, H), _zrn(U, H)
+    if b_ih is None:
+        return Wz, Uz, torch.zeros(3 * H, device=W.device), None
+    b = _zrn(b_ih, H) + torch.cat([b_hh[H:2 * H], b_hh[:H], torch.zeros(H, device=W.device, dtype=b_hh.dtype)])
+    return Wz, Uz, b, b_hh[2 * H:]
+
+
+def gru_cell_native(x, h, W, U, b_ih, b_hh, act="tanh"):
+    """One torch.nn.GRUCell step (reset-after; candidate activation ``act``) on the native
+    kernels: the input projection on the MFMA GEMM, the recurrent GEMM + gate math in one
+    persistent-kernel launch (T = 1). None when the shape is unsupported."""
+    from zoo.ops import rnn as R
+    H = U.shape[1]
+    if not (torch.is_tensor(x) and x.is_cuda and x.dim() == 2 and R.padded_hidden(H) is not None):
+        return None
+    Wz, Uz, b, bhn = _gru_operands(W, U, b_ih, b_hh, H)
+    _, hT, _ = R.recurrent(x.float().unsqueeze(1), Wz, b, Uz, "gru_ra", act, "sigmoid",
+                           None if h is None else h.float(), bhn=bhn)
+    return hT
+
+
+class ZGRU(_Twin, nn.GRU):
+    """nn.GRU (any layer count, bidirectional) on the persistent recurrent kernel's reset-after GRU
+    cell (rnn.hip CELL_GRU_RA): one input GEMM + one launch per layer and direction for the whole
+    sequence, forward and backward. nn.GRU's signature and outputs ``(output, h_n)``."""
+
+    def _native_supported(self, x):
+        from zoo.ops import rnn as R
+        return (torch.is_tensor(x) and x.is_cuda and x.dim() == 3 and
+                R.padded_hidden(self.hidden_size) is not None and (self.dropout == 0 or not self.training))
+
+    def forward(self, x, hx=None):
+        if not self._native_supported(x):
+            return nn.GRU.forward(self, x, hx)
+        from zoo.ops import rnn as R
+        xs = x if self.batch_first else x.transpose(0, 1)
+        D = 2 if self.bidirectional else 1
+        H = self.hidden_size
+        hs = []
+        inp = xs.float()
+        for layer in range(self.num_layers):
+            outs = []
+            for d in range(D):
+                sfx = "_l%d%s" % (layer, "_reverse" if d else "")
+                W, U = getattr(self, "weight_ih" + sfx), getattr(self, "weight_hh" + sfx)
+                bi = getattr(self, "bias_ih" + sfx) if self.bias else None
+                bh = getattr(self, "bias_hh" + sfx) if self.bias else None
+                Wz, Uz, b, bhn = _gru_operands(W, U, bi, bh, H)
+                i = layer * D + d
+                hseq, hT, _ = R.recurrent(inp, Wz, b, Uz, "gru_ra", "tanh", "sigmoid",
+                                          None if hx is None else hx[i].float(), go_backwards=bool(d), bhn=bhn)
+                outs.append((hseq.flip(1) if d else hseq).float())
+                hs.append(hT.float())
+            inp = outs[0] if D == 1 else torch.cat(outs, -1)
+        out = inp if self.batch_first else inp.transpose(0, 1)
+        return out.to(x.dtype), torch.stack(hs, 0).to(x.dtype)
+
+
+class ZGRUCell(_Twin, nn.GRUCell):
+    """nn.GRUCell on the native GEMM + one recurrent-kernel step (``gru_cell_native``)."""
+
+    def forward(self, x, hx=None):
+        if torch.is_tensor(x) and x.dim() == 2:
+            y = gru_cell_native(x, hx, self.weight_ih, self.weight_hh, self.bias_ih, self.bias_hh)
+            if y is not None:
+                return y.to(x.dtype)
+        return nn.GRUCell.forward(self, x, hx)
+
+
 # exact torch class -> twin class (subclasses of the torch classes are left alone: they may
 # override forward)
-_TWINS = {nn.Conv2d: ZConv2d, nn.Linear: ZLinear, nn.BatchNorm2d: ZBatchNorm2d, nn.MaxPool2d: ZMaxPool2d,
+_TWINS = {nn.Conv2d: ZConv2d, nn.ConvTranspose2d: ZConvTranspose2d, nn.Linear: ZLinear, nn.BatchNorm2d: ZBatchNorm2d, nn.MaxPool2d: ZMaxPool2d,
           nn.AvgPool2d: ZAvgPool2d, nn.AdaptiveAvgPool2d: ZAdaptiveAvgPool2d, nn.LocalResponseNorm: ZLocalResponseNorm,
           nn.ReLU: ZReLU, nn.Tanh: ZTanh, nn.Sigmoid: ZSigmoid, nn.ELU: ZELU, nn.LeakyReLU: ZLeakyReLU,
-          nn.ReLU6: ZReLU6, nn.GELU: ZGELU, nn.Softplus: ZSoftplus, nn.LSTM: ZLSTM,
+          nn.ReLU6: ZReLU6, nn.GELU: ZGELU, nn.Softplus: ZSoftplus, nn.LSTM: ZLSTM, nn.GRU: ZGRU,
+          nn.GRUCell: ZGRUCell,
           G.Pool2d: ZPool2d, G.LRN: ZLRN}
 
 
@@ -441,7 +621,7 @@ def _fuse(conv, bn=None, act_mod=None):
 
 
 def _fusable_conv(m):
-    return type(m) is nn.Conv2d and m.groups == 1
+    return type(m) is nn.Conv2d
 
 
 def _lower_sequence(mods, training):

@@ -25,6 +25,7 @@ import glob
 import logging
 import math
 import os
+import random
 import time
 
 import torch
@@ -202,11 +203,22 @@ class TrainingEngine:
         self._graph_warm = {}
         # single-rank jobs: each bucket's optimizer update runs on the weight-gradient side
         # stream as soon as its gradients are final, overlapping the rest of the backward
-        # (GradSync.enable_ibo). Not under hipGraph capture (the update would be baked into the
-        # graph with this step's learning rate), not with gradient clipping (a global norm).
-        self.ibo = bool(os.environ.get("ZOO_OPTIM_IN_BWD", "1") != "0" and clip is None and not self.hip_graph and
+        # (GradSync.enable_ibo). Not with gradient clipping (a global norm). Under hipGraph
+        # capture the updates are captured too: the optimizer kernels then read the learning rate
+        # and bias corrections from a device buffer staged before every replay
+        # (OptimMethod.enable_device_hparams), so the graph follows the schedule.
+        self.ibo = bool(os.environ.get("ZOO_OPTIM_IN_BWD", "1") != "0" and clip is None and
                         wstream.on() and getattr(optim_method, "supports_ranges", lambda: False)() and
                         self.sync.enable_ibo(optim_method))
+        if self.ibo and self.hip_graph and hasattr(optim_method, "enable_device_hparams"):
+            optim_method.enable_device_hparams(self.device)
+        # dropout under hipGraph: a device seed offset, restaged every step, is xored into the
+        # seeds the captured kernels replay (fresh masks per step)
+        self._seed_stager = None
+        if self.hip_graph:
+            from zoo.ops.devscalar import dropout_seed_stager
+            self._seed_stager = dropout_seed_stager(self.device)
+            self._seed_rng = random.Random(torch.initial_seed() + 977)
 
     # ------------------------------------------------------------------
     def _maybe_inject_fault(self):
@@ -227,9 +239,13 @@ class TrainingEngine:
         A failing collective raises :class:`CommFailure` (restart by the launcher)."""
         multi = self.sync.comm and self.sync.world > 1
         if self.sync.ibo_optim is not None and (self.sync.ibo_optim is not self.optim or self.clip is not None or
-                                                self.hip_graph):
+                                                (self.hip_graph and getattr(self.optim, "_dev_hp", None) is None)):
             self.sync.ibo_optim = None   # optimizer / clipping / graph mode changed: plain end-of-step update
             self.ibo = False
+        if getattr(self.optim, "_dev_hp", None) is not None:
+            self.optim.stage_device_hparams()
+        if self._seed_stager is not None:
+            self._seed_stager.stage([self._seed_rng.getrandbits(31)])   # this step's lr / bias corrections for the kernels
         self.model.train()
         ph = self.phases
         loss = None
@@ -313,7 +329,7 @@ class TrainingEngine:
                 self.hip_graph = False
                 torch.cuda.synchronize(self.device)
                 return self._fwd_bwd(inputs, target)
-        graph, sx, sy, sloss = g
+        graph, sx, sy, sloss, ibo_done = g
         if not getattr(self.flat, "grad_clean", False):
             self.flat.grad.zero_()      # the captured step may rely on the optimizer's clearing
         self.flat.grad_clean = False
@@ -321,6 +337,8 @@ class TrainingEngine:
             s_.copy_(t, non_blocking=True)
         sy.copy_(target, non_blocking=True)
         graph.replay()
+        # the buckets whose in-backward update is part of the graph: step() updates the rest
+        self.sync._ibo_done = set(ibo_done)
         return sloss.clone()
 
     def _capture(self, key, xs, target, as_list):
@@ -335,8 +353,9 @@ class TrainingEngine:
                 sloss = self._fwd_bwd(sx if as_list else sx[0], sy)
         finally:
             self.sync.overlap = overlap
+        ibo_done = set(self.sync._ibo_done)   # in-backward updates captured into the graph
         self.sync.reset()
-        g = (graph, sx, sy, sloss)
+        g = (graph, sx, sy, sloss, ibo_done)
         self._graphs[key] = g
         log.info("captured forward+backward as a hipGraph for inputs %s", key)
         return g

@@ -13,8 +13,10 @@ import torch
     (64, 256, 256),         # single split: direct accumulate
     (200, 8, 16),           # tiny
     (70000, 64, 256),       # long reduction (ResNet 1x1 shape class)
+    (200704, 512, 128),     # ResNet stage-2 1x1: atomic split-K (half-live tiles)
 ])
-def test_linear_wgrad_matches_fp64(M, N, K):
+@pytest.mark.parametrize("det", [False, True])   # True: partials + ordered fold; False: atomics where small
+def test_linear_wgrad_matches_fp64(M, N, K, det):
     from zoo.ops._native import native
     dev = torch.device("cuda")
     torch.manual_seed(M + N + K)
@@ -22,7 +24,11 @@ def test_linear_wgrad_matches_fp64(M, N, K):
     x = torch.randn(M, K, device=dev).bfloat16()
     init = torch.randn(N, K, device=dev)
     dw = init.clone()
-    native().linear_wgrad(dy, x, dw)
+    native().set_deterministic(det)
+    try:
+        native().linear_wgrad(dy, x, dw)
+    finally:
+        native().set_deterministic(False)
     ref = init.double() + dy.double().t() @ x.double()
     err = ((dw.double() - ref).norm() / ref.norm()).item()
     assert err < 1e-5, err
