@@ -325,6 +325,34 @@ __global__ __launch_bounds__(256) void nchw_to_s2d_kernel(const float* __restric
   }
 }
 
+// uint8 NHWC images (the input pipeline's wire format: 1/4 of the fp32 NCHW bytes over PCIe) ->
+// normalised, zero-padded space-to-depth(2) NHWC bf16 in one pass: Y[n][i][j][(dy*2+dx)*4 + c] =
+// X[n][2i+dy-pad][2j+dx-pad][c] * scale[c] + shift[c] (0 outside the image and for c >= C).
+__global__ __launch_bounds__(256) void nhwc_u8_to_s2d_kernel(const uint8_t* __restrict__ X, bf16_t* __restrict__ Y,
+                                                             int N, int C, int H, int W, int pad, int Hs, int Ws,
+                                                             float4 scale, float4 shift) {
+  const size_t total = (size_t)N * Hs * Ws * 2;
+  const float sc[4] = {scale.x, scale.y, scale.z, scale.w}, sh[4] = {shift.x, shift.y, shift.z, shift.w};
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+    const int dy = (int)(i & 1);
+    size_t t = i >> 1;
+    const int j = (int)(t % Ws); t /= Ws;
+    const int ii = (int)(t % Hs);
+    const int n = (int)(t / Hs);
+    const int h = 2 * ii + dy - pad;
+    float v[8];
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int w = 2 * j + dx - pad;
+      const bool ok = (unsigned)h < (unsigned)H && (unsigned)w < (unsigned)W;
+      const uint8_t* px = X + (((size_t)n * H + (ok ? h : 0)) * W + (ok ? w : 0)) * C;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) v[dx * 4 + c] = (ok && c < C) ? (float)px[c] * sc[c] + sh[c] : 0.f;
+    }
+    *reinterpret_cast<uint4*>(Y + ((((size_t)n * Hs + ii) * Ws + j) * 16) + dy * 8) = pack8(v);
+  }
+}
+
 __global__ __launch_bounds__(256) void bf16_to_f32_accum_kernel(const bf16_t* __restrict__ x, float* __restrict__ y,
                                                                  size_t n, int accumulate) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -468,6 +496,14 @@ extern "C" hipError_t zoo_nchw_to_s2d(const float* X, void* Y, int N, int C, int
                                        hipStream_t st) {
   hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(egrid((size_t)N * Hs * Ws * 2)), dim3(256), 0, st, X, (bf16_t*)Y, N, C,
                      H, W, 4, pad, Hs, Ws);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_nhwc_u8_to_s2d(const void* X, void* Y, int N, int C, int H, int W, int pad, int Hs, int Ws,
+                                          const float* scale, const float* shift, hipStream_t st) {
+  const float4 sc{scale[0], scale[1], scale[2], scale[3]}, sf{shift[0], shift[1], shift[2], shift[3]};
+  hipLaunchKernelGGL(nhwc_u8_to_s2d_kernel, dim3(egrid((size_t)N * Hs * Ws * 2)), dim3(256), 0, st,
+                     (const uint8_t*)X, (bf16_t*)Y, N, C, H, W, pad, Hs, Ws, sc, sf);
   return hipGetLastError();
 }
 

@@ -70,8 +70,9 @@ template <bool IS1x1, int BN, bool FP8>
 __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict__ X, const int8_t* __restrict__ Wm,
                                                       void* __restrict__ Y, const float* __restrict__ colscale,
                                                       const float* __restrict__ bias,
-                                                      const int8_t* __restrict__ resid, float rscale, ConvGeom g,
-                                                      int relu, int out_bf16) {
+                                                      const int8_t* __restrict__ resid, float rscale,
+                                                      const float* __restrict__ rvec, ConvGeom g, int relu,
+                                                      int out_bf16) {
   constexpr int BM = QC_BM, BK = QC_BK;
   constexpr int WN = BN / 2, NJ = WN / 16, NI = 4;
   constexpr int B_ROWS_PER_THREAD = BN / 32;
@@ -236,9 +237,12 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
   const int ch = tid % CPR, rr0 = tid / CPR;
   const int col0 = n0 + ch * 8;
   if (col0 >= g.K) return;
-  float bv[8];
+  float bv[8], rv[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bv[e] = bias ? bias[col0 + e] : 0.f;
+  for (int e = 0; e < 8; ++e) {
+    bv[e] = bias ? bias[col0 + e] : 0.f;
+    rv[e] = rvec ? rvec[col0 + e] : rscale;   // per-channel activation scales: s_resid[c] / s_out[c]
+  }
   const int rend = min(BM, g.M - m0);
   for (int rr = rr0; rr < rend; rr += RSTEP) {
     const size_t off = (size_t)(m0 + rr) * g.K + col0;
@@ -253,12 +257,12 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
         f8_unpack4(rq.x, r);
         f8_unpack4(rq.y, r + 4);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += r[e] * rscale;
+        for (int e = 0; e < 8; ++e) v[e] += r[e] * rv[e];
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] += (float)(int8_t)(rq.x >> (8 * e)) * rscale;
-          v[4 + e] += (float)(int8_t)(rq.y >> (8 * e)) * rscale;
+          v[e] += (float)(int8_t)(rq.x >> (8 * e)) * rv[e];
+          v[4 + e] += (float)(int8_t)(rq.y >> (8 * e)) * rv[4 + e];
         }
       }
     }
@@ -283,17 +287,21 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
 }
 
 // bf16 -> int8 with one per-tensor inverse scale (16 elements per thread, 16-byte stores)
+// inv_vec (optional, C % 16 == 0): one inverse scale per channel of the NHWC tensor (last dim C)
 __global__ __launch_bounds__(256) void quantize_i8_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
-                                                          size_t n16, float inv_scale) {
+                                                          size_t n16, float inv_scale, const float* __restrict__ inv_vec,
+                                                          int C) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
     float a[8], b[8];
     unpack8(reinterpret_cast<const uint4*>(x)[2 * i], a);
     unpack8(reinterpret_cast<const uint4*>(x)[2 * i + 1], b);
+    const int c0 = inv_vec ? (int)((i * 16) % (size_t)C) : 0;
     uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      w[e >> 2] |= (uint32_t)(uint8_t)q_sat(a[e] * inv_scale) << (8 * (e & 3));
-      w[2 + (e >> 2)] |= (uint32_t)(uint8_t)q_sat(b[e] * inv_scale) << (8 * (e & 3));
+      const float sa = inv_vec ? inv_vec[c0 + e] : inv_scale, sb = inv_vec ? inv_vec[c0 + 8 + e] : inv_scale;
+      w[e >> 2] |= (uint32_t)(uint8_t)q_sat(a[e] * sa) << (8 * (e & 3));
+      w[2 + (e >> 2)] |= (uint32_t)(uint8_t)q_sat(b[e] * sb) << (8 * (e & 3));
     }
     reinterpret_cast<uint4*>(q)[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -301,15 +309,17 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const bf16_t* __restri
 
 // bf16 -> e4m3 with one per-tensor inverse scale
 __global__ __launch_bounds__(256) void quantize_f8_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
-                                                          size_t n16, float inv_scale) {
+                                                          size_t n16, float inv_scale, const float* __restrict__ inv_vec,
+                                                          int C) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
     float a[8], b[8];
     unpack8(reinterpret_cast<const uint4*>(x)[2 * i], a);
     unpack8(reinterpret_cast<const uint4*>(x)[2 * i + 1], b);
+    const int c0 = inv_vec ? (int)((i * 16) % (size_t)C) : 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      a[e] *= inv_scale;
-      b[e] *= inv_scale;
+      a[e] *= inv_vec ? inv_vec[c0 + e] : inv_scale;
+      b[e] *= inv_vec ? inv_vec[c0 + 8 + e] : inv_scale;
     }
     reinterpret_cast<uint4*>(q)[i] = make_uint4(f8_pack4(a[0], a[1], a[2], a[3]), f8_pack4(a[4], a[5], a[6], a[7]),
                                                 f8_pack4(b[0], b[1], b[2], b[3]), f8_pack4(b[4], b[5], b[6], b[7]));
@@ -319,7 +329,7 @@ __global__ __launch_bounds__(256) void quantize_f8_kernel(const bf16_t* __restri
 // global average pool of an int8 (FP8: e4m3) NHWC tensor -> bf16 [N][C] (dequantised with `scale`)
 template <bool FP8>
 __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ X, bf16_t* __restrict__ Y, int N,
-                                                     int HW, int C, float scale) {
+                                                     int HW, int C, float scale, const float* __restrict__ svec) {
   const int cpr = C >> 3;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N * cpr; i += gridDim.x * blockDim.x) {
     const int chunk = i % cpr, n = i / cpr;
@@ -341,17 +351,16 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
         }
       }
     }
-    const float k = scale / (float)HW;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= k;
+    for (int e = 0; e < 8; ++e) acc[e] *= (svec ? svec[chunk * 8 + e] : scale) / (float)HW;
     *reinterpret_cast<uint4*>(Y + (size_t)n * C + chunk * 8) = pack8(acc);
   }
 }
 
 template <bool IS1x1, int BN, bool FP8>
 static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const float* cs, const float* bias,
-                            const int8_t* resid, float rscale, const ConvGeom& g, int relu, int out_bf16,
-                            hipStream_t st) {
+                            const int8_t* resid, float rscale, const float* rvec, const ConvGeom& g, int relu,
+                            int out_bf16, hipStream_t st) {
   const int tiles = ((g.M + QC_BM - 1) / QC_BM) * ((g.K + BN - 1) / BN);
   const size_t main_b = (size_t)(g.ldb > QC_BK ? 2 : 1) * (QC_BM + BN) * QC_BK;
   const size_t epi_b = (size_t)QC_BM * (BN + 4) * sizeof(float);
@@ -364,7 +373,7 @@ static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const flo
     attr = true;
   }
   hipLaunchKernelGGL((qconv_kernel<IS1x1, BN, FP8>), dim3(tiles), dim3(QC_NT), smem, st, X, W, Y, cs, bias, resid, rscale,
-                     g, relu, out_bf16);
+                     rvec, g, relu, out_bf16);
   return hipGetLastError();
 }
 
@@ -374,8 +383,8 @@ using namespace zoo;
 
 // g: geometry in int8 elements (C, Ktot = R*S*C, ldb all multiples of 16); fp8: e4m3 operands
 extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const float* colscale, const float* bias,
-                                const void* resid, float rscale, const ConvGeom* g, int relu, int out_bf16, int fp8,
-                                hipStream_t st) {
+                                const void* resid, float rscale, const float* rvec, const ConvGeom* g, int relu,
+                                int out_bf16, int fp8, hipStream_t st) {
   const int8_t* x = (const int8_t*)X;
   const int8_t* w = (const int8_t*)W;
   const int8_t* r = (const int8_t*)resid;
@@ -386,41 +395,44 @@ extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const flo
 #define ZOO_QC(F8)                                                                                                 \
   do {                                                                                                             \
     if (is1x1)                                                                                                     \
-      return wide ? launch_qc<true, 128, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)           \
-                  : launch_qc<true, 64, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);           \
-    return wide ? launch_qc<false, 128, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st)            \
-                : launch_qc<false, 64, F8>(x, w, Y, colscale, bias, r, rscale, *g, relu, out_bf16, st);            \
+      return wide ? launch_qc<true, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st)           \
+                  : launch_qc<true, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st);           \
+    return wide ? launch_qc<false, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st)            \
+                : launch_qc<false, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st);            \
   } while (0)
   if (fp8) ZOO_QC(true);
   ZOO_QC(false);
 #undef ZOO_QC
 }
 
-extern "C" hipError_t zoo_quantize_i8(const void* x, void* q, size_t n, float inv_scale, hipStream_t st) {
+extern "C" hipError_t zoo_quantize_i8(const void* x, void* q, size_t n, float inv_scale, const float* inv_vec, int C,
+                                       hipStream_t st) {
   const size_t n16 = n / 16;
   size_t blocks = (n16 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(quantize_i8_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, st, (const bf16_t*)x, (int8_t*)q,
-                     n16, inv_scale);
+                     n16, inv_scale, inv_vec, C);
   return hipGetLastError();
 }
 
-extern "C" hipError_t zoo_quantize_f8(const void* x, void* q, size_t n, float inv_scale, hipStream_t st) {
+extern "C" hipError_t zoo_quantize_f8(const void* x, void* q, size_t n, float inv_scale, const float* inv_vec, int C,
+                                       hipStream_t st) {
   const size_t n16 = n / 16;
   size_t blocks = (n16 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(quantize_f8_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, st, (const bf16_t*)x, (int8_t*)q,
-                     n16, inv_scale);
+                     n16, inv_scale, inv_vec, C);
   return hipGetLastError();
 }
 
-extern "C" hipError_t zoo_gap_i8(const void* x, void* y, int N, int HW, int C, float scale, int fp8, hipStream_t st) {
+extern "C" hipError_t zoo_gap_i8(const void* x, void* y, int N, int HW, int C, float scale, const float* svec, int fp8,
+                                  hipStream_t st) {
   int blocks = (N * (C / 8) + 255) / 256;
   if (fp8)
     hipLaunchKernelGGL(gap_i8_kernel<true>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
-                       (bf16_t*)y, N, HW, C, scale);
+                       (bf16_t*)y, N, HW, C, scale, svec);
   else
     hipLaunchKernelGGL(gap_i8_kernel<false>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
-                       (bf16_t*)y, N, HW, C, scale);
+                       (bf16_t*)y, N, HW, C, scale, svec);
   return hipGetLastError();
 }

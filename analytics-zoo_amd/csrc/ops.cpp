@@ -130,6 +130,8 @@ hipError_t zoo_clip(float*, size_t, float, float, const float*, float, hipStream
 hipError_t zoo_nchw_to_nhwc(const float*, void*, int, int, int, int, int, hipStream_t);
 hipError_t zoo_dropout_add(const void*, const void*, void*, size_t, float, uint64_t, hipStream_t);
 hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
+hipError_t zoo_nhwc_u8_to_s2d(const void*, void*, int, int, int, int, int, int, int, const float*, const float*,
+                              hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
 hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, hipStream_t);
@@ -167,11 +169,11 @@ hipError_t zoo_sparse_linear_fwd(const int64_t*, const int64_t*, const float*, c
                                  int, int, int64_t, hipStream_t);
 hipError_t zoo_sparse_linear_bwd(const int64_t*, const int64_t*, const float*, const float*, float*, float*, int64_t,
                                  int, int, int, hipStream_t);
-hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*, const void*, float, const ConvGeom*,
-                     int, int, int, hipStream_t);
-hipError_t zoo_quantize_i8(const void*, void*, size_t, float, hipStream_t);
-hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, int, hipStream_t);
-hipError_t zoo_quantize_f8(const void*, void*, size_t, float, hipStream_t);
+hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*, const void*, float, const float*,
+                     const ConvGeom*, int, int, int, hipStream_t);
+hipError_t zoo_quantize_i8(const void*, void*, size_t, float, const float*, int, hipStream_t);
+hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, const float*, int, hipStream_t);
+hipError_t zoo_quantize_f8(const void*, void*, size_t, float, const float*, int, hipStream_t);
 hipError_t zoo_act(const void*, const void*, void*, size_t, int, int, float, hipStream_t);
 hipError_t zoo_dropout(const void*, void*, size_t, int, float, uint64_t, hipStream_t);
 hipError_t zoo_loss(const void*, const void*, void*, float*, size_t, int, int, float, float, hipStream_t);
@@ -1692,6 +1694,22 @@ torch::Tensor nchw_to_s2d(torch::Tensor x, int pad) {
   return y;
 }
 
+// uint8 NHWC images -> normalised s2d(2) NHWC bf16 (x * scale[c] + shift[c]), the stem's input
+torch::Tensor nhwc_u8_to_s2d(torch::Tensor x, int pad, std::vector<double> scale, std::vector<double> shift) {
+  TORCH_CHECK(x.is_cuda() && x.scalar_type() == at::kByte && x.is_contiguous(), "nhwc_u8_to_s2d: contiguous uint8 GPU");
+  TORCH_CHECK(x.dim() == 4 && x.size(3) <= 4, "nhwc_u8_to_s2d: [N, H, W, C<=4] input");
+  const int N = x.size(0), H = x.size(1), W = x.size(2), C = x.size(3);
+  TORCH_CHECK((int)scale.size() >= C && (int)shift.size() >= C, "nhwc_u8_to_s2d: one scale / shift per channel");
+  float sc[4] = {0.f, 0.f, 0.f, 0.f}, sh[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < C; ++c) { sc[c] = (float)scale[c]; sh[c] = (float)shift[c]; }
+  const int Hs = (H + 2 * pad + 1) / 2, Ws = (W + 2 * pad + 1) / 2;
+  auto y = torch::empty({N, Hs, Ws, 16}, x.options().dtype(at::kBFloat16));
+  if (y.numel() == 0) return y;
+  check_hip(zoo_nhwc_u8_to_s2d(x.data_ptr(), y.data_ptr(), N, C, H, W, pad, Hs, Ws, sc, sh, cur_stream()),
+            "nhwc_u8_to_s2d");
+  return y;
+}
+
 torch::Tensor nchw_to_nhwc(torch::Tensor x, int cpad) {
   req(x, at::kFloat, "x");
   TORCH_CHECK(x.dim() == 4, "nchw_to_nhwc: 4-D input");
@@ -2038,7 +2056,7 @@ torch::Tensor box_decode(torch::Tensor loc, torch::Tensor priors, double v0, dou
 // (saturating round) or bf16 (out_bf16).
 torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw,
                     torch::Tensor colscale, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
-                    double rscale, bool relu, bool out_bf16) {
+                    double rscale, bool relu, bool out_bf16, c10::optional<torch::Tensor> rvec) {
   // int8 or OCP fp8 e4m3 operands (the fp8 twin of the kernel); both operands the same format
   const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
   const auto qt = fp8 ? at::kFloat8_e4m3fn : at::kChar;
@@ -2069,36 +2087,60 @@ torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int 
     TORCH_CHECK(resid->numel() == (int64_t)g.M * K, "qconv: resid must match the output");
     rp = resid->data_ptr();
   }
+  const float* rv = nullptr;   // per-channel residual scale s_resid[c] / s_out[c] (overrides rscale)
+  if (rvec.has_value() && rvec->defined()) {
+    req(*rvec, at::kFloat, "rvec");
+    TORCH_CHECK(rvec->numel() == K, "qconv: rvec must be [K]");
+    rv = rvec->data_ptr<float>();
+  }
   auto y = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(out_bf16 ? at::kBFloat16 : qt));
-  check_hip(zoo_qconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), colscale.data_ptr<float>(), bp, rp, (float)rscale,
+  check_hip(zoo_qconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), colscale.data_ptr<float>(), bp, rp, (float)rscale, rv,
                       &g, relu, out_bf16, fp8 ? 1 : 0, cur_stream()),
             "qconv");
   return y;
 }
 
-torch::Tensor quantize_i8(torch::Tensor x, double inv_scale) {
+// inv_vec (optional): one inverse scale per channel of the NHWC tensor (C = last dim, C % 16 == 0)
+static const float* chan_vec(const c10::optional<torch::Tensor>& v, const torch::Tensor& x, const char* what) {
+  if (!v.has_value() || !v->defined()) return nullptr;
+  req(*v, at::kFloat, what);
+  TORCH_CHECK(v->numel() == x.size(-1) && x.size(-1) % 16 == 0, what, ": one value per channel, C % 16 == 0");
+  return v->data_ptr<float>();
+}
+
+torch::Tensor quantize_i8(torch::Tensor x, double inv_scale, c10::optional<torch::Tensor> inv_vec) {
   req(x, at::kBFloat16, "x");
   TORCH_CHECK(x.numel() % 16 == 0, "quantize_i8: numel must be a multiple of 16");
+  const float* iv = chan_vec(inv_vec, x, "quantize_i8 inv_vec");
   auto q = torch::empty(x.sizes(), x.options().dtype(at::kChar));
-  check_hip(zoo_quantize_i8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, cur_stream()), "quantize_i8");
+  check_hip(zoo_quantize_i8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, iv, (int)x.size(-1), cur_stream()),
+            "quantize_i8");
   return q;
 }
 
-torch::Tensor quantize_f8(torch::Tensor x, double inv_scale) {
+torch::Tensor quantize_f8(torch::Tensor x, double inv_scale, c10::optional<torch::Tensor> inv_vec) {
   req(x, at::kBFloat16, "x");
   TORCH_CHECK(x.numel() % 16 == 0, "quantize_f8: numel must be a multiple of 16");
+  const float* iv = chan_vec(inv_vec, x, "quantize_f8 inv_vec");
   auto q = torch::empty(x.sizes(), x.options().dtype(at::kFloat8_e4m3fn));
-  check_hip(zoo_quantize_f8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, cur_stream()), "quantize_f8");
+  check_hip(zoo_quantize_f8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, iv, (int)x.size(-1), cur_stream()),
+            "quantize_f8");
   return q;
 }
 
-torch::Tensor gap_i8(torch::Tensor x, double scale) {
+torch::Tensor gap_i8(torch::Tensor x, double scale, c10::optional<torch::Tensor> svec) {
   const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
   req(x, fp8 ? at::kFloat8_e4m3fn : at::kChar, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap_i8: NHWC with C % 8 == 0");
   const int N = x.size(0), HW = x.size(1) * x.size(2), C = x.size(3);
+  const float* sv = nullptr;
+  if (svec.has_value() && svec->defined()) {
+    req(*svec, at::kFloat, "svec");
+    TORCH_CHECK(svec->numel() == C, "gap_i8: svec must be [C]");
+    sv = svec->data_ptr<float>();
+  }
   auto y = torch::empty({N, C}, x.options().dtype(at::kBFloat16));
-  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, fp8 ? 1 : 0, cur_stream()), "gap_i8");
+  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, sv, fp8 ? 1 : 0, cur_stream()), "gap_i8");
   return y;
 }
 
@@ -2808,15 +2850,17 @@ PYBIND11_MODULE(_C, m) {
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
-  m.def("qconv", &qconv);
+  m.def("qconv", &qconv, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"),
+        py::arg("ph"), py::arg("pw"), py::arg("colscale"), py::arg("bias"), py::arg("resid"), py::arg("rscale"),
+        py::arg("relu"), py::arg("out_bf16"), py::arg("rvec") = py::none());
   m.def("act_fwd_bwd", &act_fwd_bwd);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("loss_fwd", &loss_fwd);
   m.def("auc_hist", &auc_hist);
   m.def("box_decode", &box_decode);
-  m.def("quantize_i8", &quantize_i8);
-  m.def("gap_i8", &gap_i8);
-  m.def("quantize_f8", &quantize_f8);
+  m.def("quantize_i8", &quantize_i8, py::arg("x"), py::arg("inv_scale"), py::arg("inv_vec") = py::none());
+  m.def("gap_i8", &gap_i8, py::arg("x"), py::arg("scale"), py::arg("svec") = py::none());
+  m.def("quantize_f8", &quantize_f8, py::arg("x"), py::arg("inv_scale"), py::arg("inv_vec") = py::none());
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);
   m.def("sparse_linear_fwd", &sparse_linear_fwd);
@@ -2947,6 +2991,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("pdrop") = 0.0, py::arg("seed") = 0);
   m.def("nms_sorted", &nms_sorted);
   m.def("nchw_to_s2d", &nchw_to_s2d);
+  m.def("nhwc_u8_to_s2d", &nhwc_u8_to_s2d);
   m.def("dropout_add", &dropout_add, py::arg("a"), py::arg("x") = py::none(), py::arg("p"), py::arg("seed"));
   m.def("attn_fwd_strided", &attn_fwd_strided, py::arg("q"), py::arg("k"), py::arg("v"), py::arg("mask"),
         py::arg("causal"), py::arg("out_blhd"), py::arg("pdrop") = 0.0, py::arg("seed") = 0);

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--seq", type=int, default=128)
+    ap.add_argument("--graph", action="store_true",
+                    help="capture forward + backward + in-backward optimizer as one hipGraph per step")
     a = ap.parse_args()
     from zoo.common.nncontext import init_nncontext
     from zoo.pipeline.api.keras.layers import BERT
@@ -37,7 +39,7 @@ def main():
     dev = torch.device("cuda")
     bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512, intermediate_size=3072,
                 output_all_block=False)
-    eng = TrainingEngine(_Classifier(bert), softmax_cross_entropy, AdamWeightDecay(lr=2e-5))
+    eng = TrainingEngine(_Classifier(bert), softmax_cross_entropy, AdamWeightDecay(lr=2e-5), hip_graph=a.graph)
     B, L = a.batch, a.seq
     xs = [torch.randint(0, 30522, (B, L), device=dev), torch.zeros(B, L, dtype=torch.long, device=dev),
           torch.arange(L, device=dev).repeat(B, 1), torch.ones(B, L, device=dev)]
@@ -53,11 +55,22 @@ def main():
         host += time.perf_counter() - h0
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.iters
+    replay_ms = None
+    if eng._graphs:
+        # host cost of the bare hipGraph launch (no staging, no optimizer tail)
+        g = next(iter(eng._graphs.values()))[0]
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        for _ in range(5):
+            g.replay()
+        replay_ms = (time.perf_counter() - h0) / 5 * 1e3
+        torch.cuda.synchronize()
     # host_ms_per_step: time the Python / launch side spends issuing a step (no device sync inside
     # the loop): close to ms_per_step means the step is host-bound, well below means device-bound
     print('{"bench": "bert-base-finetune-train", "batch": %d, "seq": %d, "ms_per_step": %.3f, "seq_per_s": %.1f, '
-          '"tokens_per_s": %.0f, "loss": %.4f, "host_ms_per_step": %.3f}' % (B, L, dt * 1e3, B / dt, B * L / dt,
-                                                                         float(loss), host / a.iters * 1e3))
+          '"tokens_per_s": %.0f, "loss": %.4f, "host_ms_per_step": %.3f, "hip_graph": %s, "graphs": %d, "graph_replay_host_ms": %s}'
+          % (B, L, dt * 1e3, B / dt, B * L / dt, float(loss), host / a.iters * 1e3, "true" if eng.hip_graph else "false",
+             len(eng._graphs), "null" if replay_ms is None else "%.3f" % replay_ms))
 
 
 if __name__ == "__main__":

@@ -38,9 +38,29 @@ def _tensors(xs):
     return [x for x in (xs if isinstance(xs, (list, tuple)) else [xs]) if torch.is_tensor(x)]
 
 
-def run(gmodel, cmodel, x, loss_fn, train=True):
+def _round_weights_bf16(cmodel):
+    """The CPU twin computes with the bf16 values the GPU kernels read for matrix weights (dim >= 2:
+    packed conv / dense / depthwise weights); BatchNorm affine and biases stay fp32 as on the GPU.
+    Without it the per-weight bf16 rounding alone moves pre-activations across ReLU's zero in
+    ~0.1 % of the elements, a ~3-4 % L2 difference in dx that would mask real kernel errors."""
+    with torch.no_grad():
+        for p in cmodel.parameters():
+            if p.dim() >= 2:
+                p.copy_(p.to(torch.bfloat16).float())
+
+
+def affine_rel(row):
+    """BatchNorm affine gradients relative to the norm of the stacked [dgamma; dbeta] reference:
+    dgamma is a cancelling sum (sum dy * xhat: exactly zero at gamma=1, beta=0 for a unit whose
+    consumer normalises again, e.g. conv-BN-ReLU -> depthwise-BN), so its own norm is no scale."""
+    return row.get("daffine")
+
+
+def run(gmodel, cmodel, x, loss_fn, train=True, round_bf16=True):
     gmodel.train(train)
     cmodel.train(train)
+    if round_bf16:
+        _round_weights_bf16(cmodel)
     cmods = dict(_leaves(cmodel))
     rec = {}
     hooks = []
@@ -69,6 +89,17 @@ def run(gmodel, cmodel, x, loss_fn, train=True):
         h.remove()
     gparams = {n: p for n, p in gmodel.named_parameters()}
     rows = []
+    from zoo.ops.conv import REF_BF16_STORAGE
+    saved = REF_BF16_STORAGE[0]
+    REF_BF16_STORAGE[0] = bool(round_bf16)
+    try:
+        _compare(order, rec, cmods, gparams, rows, train)
+    finally:
+        REF_BF16_STORAGE[0] = saved
+    return rows
+
+
+def _compare(order, rec, cmods, gparams, rows, train):
     for name in order:
         r = rec[name]
         cm = cmods.get(name)
@@ -97,8 +128,14 @@ def run(gmodel, cmodel, x, loss_fn, train=True):
                     gp = gparams.get(name + "." + pn)
                     if p.grad is not None and gp is not None and gp.grad is not None and p.grad.abs().max() > 0:
                         row["d" + pn] = round(_rel(gp.grad, p.grad), 5)
+                # BatchNorm affine pair, normalised by the pair's reference norm (affine_rel)
+                pair = [(name + "." + a, getattr(cm, a, None)) for a in ("gamma", "beta")]
+                if all(isinstance(q, torch.Tensor) and q.grad is not None and gparams.get(n) is not None and
+                       gparams[n].grad is not None for n, q in pair):
+                    ref = torch.cat([q.grad.flatten() for _, q in pair])
+                    got = torch.cat([gparams[n].grad.detach().float().cpu().flatten() for n, _ in pair])
+                    row["daffine"] = round(_rel(got, ref), 5)
         rows.append(row)
-    return rows
 
 
 def main():

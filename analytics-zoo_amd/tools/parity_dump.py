@@ -2,7 +2,7 @@
 """Dump the per-layer local parity rows (tools/layer_parity.py) of every ImageClassifier backbone
 and both SSD detectors, training backward included, as JSON: the data behind the per-layer
 bounds of tests/test_gpu_native_nets.py.
-  python tools/parity_dump.py <out_dir>"""
+  python tools/parity_dump.py <out_dir> [name,name,...]"""
 import copy
 import json
 import os
@@ -20,7 +20,9 @@ NETS = [("vgg-16", 224), ("alexnet", 227), ("squeezenet", 227), ("mobilenet", 22
 
 def main():
     out = sys.argv[1]
+    only = set(sys.argv[2].split(",")) if len(sys.argv) > 2 else None
     os.makedirs(out, exist_ok=True)
+    from zoo.ops import _kern
     from zoo.common.nncontext import init_nncontext
     from zoo.models.image import native_nets
     from zoo.models.image.imageclassification.nets import build
@@ -29,6 +31,9 @@ def main():
     native_nets._dropout = lambda x, p, training: x
     dev = torch.device("cuda")
     for name, hw in NETS:
+        if only and name not in only:
+            continue
+        _kern.reset_fault_counter()
         torch.manual_seed(0)
         net = build(name, 16)
         x = torch.randn(2, 3, hw, hw)
@@ -39,6 +44,9 @@ def main():
         print(name, len(rows), flush=True)
     from zoo.models.image.objectdetection.ssd import SSD, SSDMobileNet, MultiBoxLoss
     for mob in (False, True):
+        if only and ("ssd-mobilenet" if mob else "ssd-vgg") not in only:
+            continue
+        _kern.reset_fault_counter()
         torch.manual_seed(0)
         model = SSDMobileNet(21) if mob else SSD(21)
         crit = MultiBoxLoss(21)

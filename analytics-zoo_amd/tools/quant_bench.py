@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--no-dynamic", action="store_true")
     ap.add_argument("--train-steps", type=int, default=300)
+    ap.add_argument("--task-hw", type=int, default=224, help="image size of the synthetic trained task")
+    ap.add_argument("--under-steps", type=int, default=80,
+                    help="steps of the under-trained model (lr 0.05: diverges early, near-chance accuracy)")
     a = ap.parse_args()
     torch.manual_seed(0)
     m = resnet50().cuda().eval()
@@ -59,22 +62,28 @@ def main():
     res["fp8_vs_bf16_logit_cos"] = round(torch.nn.functional.cosine_similarity(outf.flatten(), ref.flatten(),
                                                                                dim=0).item(), 4)
     res["fp8_vs_bf16_top1_agree"] = round((outf.argmax(1) == ref.argmax(1)).float().mean().item(), 4)
-    # agreement on a model with real decision margins: ResNet-50 fitted to the synthetic task of
-    # zoo.utils.synthetic at 128x128 (as tests/test_gpu_qconv.py) (the random-init numbers above are kept for continuity; a
-    # random net's top-1 flips on noise)
+    # agreement on models with real decision margins: ResNet-50 fitted to the synthetic task of
+    # zoo.utils.synthetic at --task-hw (the random-init numbers above are kept for continuity; a
+    # random net's top-1 flips on noise). Two models: "trained" (--train-steps at lr 0.01, fits the
+    # task) and "under" (--under-steps at lr 0.05: diverges early and keeps near-chance accuracy --
+    # the r4 model whose BatchNorm statistics broke per-tensor int8). Activation scales per channel
+    # (default) and, for comparison, per tensor.
     from zoo.utils.synthetic import agreement, class_templates, sample, train_briefly
-    torch.manual_seed(0)
-    mt = resnet50(num_classes=16).cuda()
-    T = class_templates(16, 128, device="cuda")
-    res["trained_task_acc"] = round(train_briefly(mt, T, steps=a.train_steps), 4)
+    T = class_templates(16, a.task_hw, device="cuda")
     cal, _ = sample(T, 64, seed=11)
     xt, _ = sample(T, 256, seed=12)
-    with torch.no_grad():
-        rt = mt(xt).float()
-        for fmt, cls in (("int8", Int8ResNet), ("fp8", Fp8ResNet)):
-            top1_t, cos_t = agreement(cls(mt, cal)(xt).float(), rt)
-            res["%s_vs_bf16_top1_agree_trained" % fmt] = round(top1_t, 4)
-            res["%s_vs_bf16_rowcos_trained" % fmt] = round(cos_t, 4)
+    for tag, steps, lr in (("trained", a.train_steps, 0.01), ("under", a.under_steps, 0.05)):
+        torch.manual_seed(0)
+        mt = resnet50(num_classes=16).cuda()
+        res["%s_task_acc" % tag] = round(train_briefly(mt, T, steps=steps, lr=lr), 4)
+        with torch.no_grad():
+            rt = mt(xt).float()
+            for fmt, cls in (("int8", Int8ResNet), ("fp8", Fp8ResNet)):
+                for sc in ("channel", "tensor"):
+                    top1_t, cos_t = agreement(cls(mt, cal, act_scales=sc)(xt).float(), rt)
+                    k = "%s_%s_%s" % (fmt, sc, tag)
+                    res[k + "_top1_agree"] = round(top1_t, 4)
+                    res[k + "_rowcos"] = round(cos_t, 4)
     if not a.no_dynamic:
         Q.quantize(m)
         td = bench(m, x, a.iters)

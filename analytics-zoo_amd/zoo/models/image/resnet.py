@@ -197,6 +197,9 @@ class ResNet(nn.Module):
         self.stages = nn.Sequential(*stages)
         self.fc = Dense(cin, num_classes)
         self.num_classes = num_classes
+        # uint8 NHWC image batches (the input pipeline's wire format) are normalised on the device,
+        # fused into the stem's space-to-depth pass: x / 255 - mean) / std per channel (ImageNet)
+        self.input_mean, self.input_std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
 
     def to_nhwc(self, x):
         """NCHW fp32 images -> NHWC bf16 with channels zero-padded for 16-byte loads."""
@@ -231,29 +234,52 @@ class ResNet(nn.Module):
         return ops.batch_norm_nhwc(y, st.gamma, st.beta, st.running_mean, st.running_var, st.eps, st.momentum,
                                    relu=True, training=True)
 
+    def _u8_scale_shift(self, c):
+        mean = list(self.input_mean) + [0.0] * (c - len(self.input_mean))
+        std = list(self.input_std) + [1.0] * (c - len(self.input_std))
+        return [1.0 / (255.0 * s) for s in std[:c]], [-m / s for m, s in zip(mean[:c], std[:c])]
+
+    def _from_u8(self, x):
+        """uint8 NHWC [N, H, W, C] -> normalised fp32 NCHW (reference / non-fused path)."""
+        sc, sh = self._u8_scale_shift(x.shape[-1])
+        y = x.float() * torch.tensor(sc, device=x.device) + torch.tensor(sh, device=x.device)
+        return y.permute(0, 3, 1, 2).contiguous()
+
     def forward(self, x):
+        if x.dtype == torch.uint8 and x.dim() == 4 and x.shape[-1] == self.in_channels:
+            if self._stem_s2d_ok(x.permute(0, 3, 1, 2)):
+                # normalisation fused into the space-to-depth pass (no fp32 NCHW copy on the device)
+                sc, sh = self._u8_scale_shift(self.in_channels)
+                xs = ops.native().nhwc_u8_to_s2d(x.contiguous(), 3, sc, sh)
+                return self._forward_s2d(xs)
+            x = self._from_u8(x)
         if self._stem_s2d_ok(x):
             # stem as a 4x4 stride-1 conv on the space-to-depth(2) image: 16 input channels
             # take the vector implicit-GEMM path; the NCHW->NHWC pass becomes the s2d pass
-            xs = ops.native().nchw_to_s2d(x.float().contiguous(), 3)
-            st = self.stem
-            if st.training and FUSE_STEM_POOL and torch.is_grad_enabled():
-                # stem BN + ReLU applied inside the max-pool pass (bn_relu_maxpool): the conv
-                # emits statistics only and the 112x112 BN output is never written
-                y, holder = conv_stats(xs, self._s2d_weight(), st.running_mean, st.running_var, kernel=(4, 4))
-                if stem_pool_fusable(y, (3, 3), (1, 1)):
-                    x = bn_relu_maxpool(y, holder, st.gamma, st.beta, st.eps, st.momentum)
-                else:
-                    x = ops.max_pool2d_nhwc(self._stem_bn(y, holder), (3, 3), (2, 2), (1, 1))
+            return self._forward_s2d(ops.native().nchw_to_s2d(x.float().contiguous(), 3))
+        x = self.to_nhwc(x)
+        x = self.stem(x)
+        x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+        return self._forward_stages(x)
+
+    def _forward_s2d(self, xs):
+        st = self.stem
+        if st.training and FUSE_STEM_POOL and torch.is_grad_enabled():
+            # stem BN + ReLU applied inside the max-pool pass (bn_relu_maxpool): the conv
+            # emits statistics only and the 112x112 BN output is never written
+            y, holder = conv_stats(xs, self._s2d_weight(), st.running_mean, st.running_var, kernel=(4, 4))
+            if stem_pool_fusable(y, (3, 3), (1, 1)):
+                x = bn_relu_maxpool(y, holder, st.gamma, st.beta, st.eps, st.momentum)
             else:
-                x = ops.conv_bn_act(xs, self._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
-                                    kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
-                                    relu=True, training=st.training)
-                x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+                x = ops.max_pool2d_nhwc(self._stem_bn(y, holder), (3, 3), (2, 2), (1, 1))
         else:
-            x = self.to_nhwc(x)
-            x = self.stem(x)
+            x = ops.conv_bn_act(xs, self._s2d_weight(), st.gamma, st.beta, st.running_mean, st.running_var,
+                                kernel=(4, 4), stride=(1, 1), pad=(0, 0), eps=st.eps, momentum=st.momentum,
+                                relu=True, training=st.training)
             x = ops.max_pool2d_nhwc(x, (3, 3), (2, 2), (1, 1))
+        return self._forward_stages(x)
+
+    def _forward_stages(self, x):
         if self.training and _fusing(x):
             prod = None
             for stage in self.stages:

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from zoo.ops._native import native
 from zoo.ops import _kern, workspace, wstream
-from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref
+from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref, ref_storage
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
 from zoo.parallel.flat import grad_slot
 
@@ -434,7 +434,7 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
                                    holder, g2, b2)
     if resid_bn is not None:
         raise ValueError("conv_bn_act: resid_bn (fused shortcut BatchNorm) needs the GPU path")
-    y = conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1)))
+    y = ref_storage(conv2d_ref(x, w, (R, S, x.shape[3], tuple(stride), tuple(pad), (1, 1))))
     if training and sync_bn_active():
         z = sync_batch_norm(y.float(), gamma, beta, running_mean, running_var, eps, momentum)
     else:

@@ -34,10 +34,20 @@ class DeviceStager:
 _SEED = {}
 
 
+def _key(device):
+    d = torch.device(device)
+    return d.index if d.index is not None else torch.cuda.current_device()
+
+
+def seed_offset_live(device):
+    """Whether the dropout kernels of ``device`` read a per-step device seed offset."""
+    return _key(device) in _SEED
+
+
 def dropout_seed_stager(device):
     """The process-wide dropout seed offset of ``device`` (created and registered with the
     kernels on first use; never freed, since every later dropout launch reads it)."""
-    key = str(torch.device(device))
+    key = _key(device)
     st = _SEED.get(key)
     if st is None:
         from zoo.ops._native import native

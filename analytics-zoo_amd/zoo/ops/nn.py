@@ -339,6 +339,9 @@ def depthwise_conv2d_nhwc(x, w, bias=None, kernel=(3, 3), stride=(1, 1), pad=(0,
         return _DwConvFn.apply(x.to(torch.bfloat16).contiguous(), w, bias, R, S, tuple(stride), tuple(pad), act)
     wt = w.float().t().reshape(C, 1, R, S)
     y = F.conv2d(x.permute(0, 3, 1, 2).float(), wt, None if bias is None else bias.float(), stride, pad, groups=C)
+    if act in (None, "linear"):
+        from zoo.ops.conv import ref_storage
+        y = ref_storage(y)     # stored in bf16 on the GPU before the BatchNorm that follows
     if act == "relu":
         y = torch.relu(y)
     elif act not in (None, "linear"):

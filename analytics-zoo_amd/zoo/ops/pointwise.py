@@ -77,9 +77,16 @@ class _DropoutFn(torch.autograd.Function):
 def dropout(x, p, training=True):
     if not training or p <= 0:
         return x
-    if _native_ok(x) and not torch.cuda.is_current_stream_capturing():
+    # under hipGraph capture the host seed is baked into the graph: native only when the engine
+    # registered the per-step device seed offset the kernel xors in (zoo.ops.devscalar)
+    if _native_ok(x) and (not torch.cuda.is_current_stream_capturing() or _seed_offset_live(x.device)):
         return _DropoutFn.apply(x.contiguous(), float(p))
     return F.dropout(x, p, True)
+
+
+def _seed_offset_live(dev):
+    from zoo.ops.devscalar import seed_offset_live
+    return seed_offset_live(dev)
 
 
 LOSS_CODES = {"mse": 0, "mae": 1, "smooth_l1": 2, "bce": 3, "bce_logits": 4, "hinge": 5, "squared_hinge": 6,

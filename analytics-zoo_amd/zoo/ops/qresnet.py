@@ -5,8 +5,14 @@ calibrated int8 convolutions through MKL-DNN; this is the MI355X counterpart
 (SURVEY.md §2.16 HK23):
 
 * weights: BatchNorm folded in, symmetric int8 with one scale per output channel;
-* activations: int8 NHWC between layers with one calibrated per-tensor scale each
-  (absmax over a calibration batch run through the bf16 model, / 127);
+* activations: int8 NHWC between layers with one calibrated scale PER CHANNEL (absmax over a
+  calibration batch run through the bf16 model, / 127). A per-tensor scale lets one outlier
+  channel -- e.g. a BatchNorm with a near-zero running variance in a briefly trained model,
+  whose folded bias is huge -- crush every other channel to a few int8 levels (r4: logit
+  cosine -0.33 against bf16 on such a model). The input scales are folded into the next conv's
+  weights before their per-output-channel quantization (w'[n, (r,s,c)] = w[n, (r,s,c)] * s_in[c]),
+  the output scales go into the epilogue's per-channel colscale / bias, and the residual add
+  takes a per-channel rscale vector -- the kernels' math is unchanged;
 * every conv unit is ONE kernel: int8 x int8 on ``v_mfma_i32_16x16x64_i8`` (2x the bf16
   MFMA rate, half the bytes), epilogue ``acc * s_in*s_w[c]/s_out + b[c]/s_out
   (+ resid * s_r/s_out) -> ReLU -> saturating int8``;
@@ -39,25 +45,38 @@ def to_fp8(v):
     return v.float().clamp(-448.0, 448.0).to(F8)
 
 
-def _q_weight(unit, fmt="int8"):
-    """ConvBN (eval) -> (int8 / e4m3 [K, R*S*C], per-channel scale [K], folded bias [K])."""
+def _fold_weight(unit):
+    """ConvBN (eval) -> (BN-folded fp32 weight [K, R*S*C], folded bias [K])."""
     inv = torch.rsqrt(unit.running_var.float() + unit.eps)
     g = unit.gamma.detach().float() * inv
     w = unit.weight.detach().float()[:, :unit.k * unit.k * unit.cin] * g[:, None]
+    b = unit.beta.detach().float() - unit.running_mean.float() * g
+    return w, b
+
+
+def _quant_rows(w, fmt="int8"):
+    """fp32 [K, R*S*C] -> (int8 / e4m3 rows, per-row scale [K])."""
     s = w.abs().amax(dim=1).clamp_min(1e-12) / QMAX[fmt]
     if fmt == "fp8":
         q = to_fp8(w / s[:, None])
     else:
         q = torch.round(w / s[:, None]).clamp_(-127, 127).to(torch.int8)
-    b = unit.beta.detach().float() - unit.running_mean.float() * g
-    return q.contiguous(), s, b
+    return q.contiguous(), s
+
+
+def _q_weight(unit, fmt="int8"):
+    """ConvBN (eval) -> (int8 / e4m3 [K, R*S*C], per-channel scale [K], folded bias [K])."""
+    w, b = _fold_weight(unit)
+    q, s = _quant_rows(w, fmt)
+    return q, s, b
 
 
 def _sat(v):
     return torch.clamp(torch.round(v), -127, 127)
 
 
-def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
+def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False,
+              rvec=None):
     """float64 CPU model of qconv: xq int8 / e4m3 NHWC, wq [K, R*S*C] of the same format."""
     import torch.nn.functional as F
     fmt = _fmt_of(xq)
@@ -67,7 +86,7 @@ def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0,
     acc = F.conv2d(xq.double().permute(0, 3, 1, 2), w4, stride=stride, padding=pad).permute(0, 2, 3, 1)
     v = acc * colscale.double() + (bias.double() if bias is not None else 0.0)
     if resid is not None:
-        v = v + resid.double() * rscale
+        v = v + resid.double() * (rvec.double() if rvec is not None else rscale)
     if relu:
         v = v.clamp_min(0)
     if out_bf16:
@@ -75,37 +94,60 @@ def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0,
     return to_fp8(v) if fmt == "fp8" else _sat(v).to(torch.int8)
 
 
-def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False):
+def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False, rvec=None):
+    """``rvec`` (optional [K]): per-channel residual scale, overrides ``rscale``."""
     if xq.is_cuda:
         return native().qconv(xq, wq, R, S, stride, stride, pad, pad, colscale, bias, resid, float(rscale),
-                              bool(relu), bool(out_bf16))
-    return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16)
+                              bool(relu), bool(out_bf16), rvec)
+    return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16, rvec)
 
 
 def quantize_act(x, scale, fmt="int8"):
-    if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 16 == 0:
+    """bf16 NHWC -> int8 / e4m3 with ``scale`` a float (per tensor) or a [C] tensor (per channel)."""
+    vec = torch.is_tensor(scale)
+    if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 16 == 0 and (not vec or x.shape[-1] % 16 == 0):
         fn = native().quantize_f8 if fmt == "fp8" else native().quantize_i8
+        if vec:
+            return fn(x.contiguous(), 1.0, (1.0 / scale).float().contiguous())
         return fn(x.contiguous(), 1.0 / scale)
+    s = scale.double().to(x.device) if vec else scale
     if fmt == "fp8":
-        return to_fp8(x.double() / scale)
-    return _sat(x.double() / scale).to(torch.int8)
+        return to_fp8(x.double() / s)
+    return _sat(x.double() / s).to(torch.int8)
 
 
 class _QUnit:
-    """One conv unit: quantized weights and the epilogue constants for given in/out scales."""
+    """One conv unit: quantized weights and the epilogue constants for given in/out scales
+    (floats: per tensor; [C] tensors: per channel)."""
 
     def __init__(self, unit, device, fmt="int8"):
-        self.q, self.sw, self.b = (t.to(device) for t in _q_weight(unit, fmt))
+        self.w, self.b = (t.to(device) for t in _fold_weight(unit))
+        self.fmt, self.cin = fmt, unit.cin
         self.k, self.stride, self.pad, self.relu = unit.k, unit.stride, unit.pad, unit.relu
 
     def bind(self, s_in, s_out):
         self.s_in, self.s_out = s_in, s_out
-        self.colscale = (self.sw * (s_in / s_out)).float().contiguous()
+        if torch.is_tensor(s_in):
+            # input scales folded into the weight columns (column (r, s, c) -> s_in[c]) before the
+            # per-output-channel weight quantization: acc * sw[n] is then the real-valued output
+            self.q, sw = _quant_rows(self.w * s_in.float().repeat(self.k * self.k)[None, :], self.fmt)
+            self.colscale = (sw / s_out).float().contiguous()
+        else:
+            self.q, sw = _quant_rows(self.w, self.fmt)
+            self.colscale = (sw * (s_in / s_out)).float().contiguous()
         self.bias = (self.b / s_out).float().contiguous()
 
     def __call__(self, xq, resid=None, s_resid=None):
+        rvec = None
+        rscale = 0.0
+        if resid is not None:
+            r = s_resid / self.s_out
+            if torch.is_tensor(r):
+                rvec = r.float().contiguous()
+            else:
+                rscale = r
         return qconv(xq, self.q, self.k, self.k, self.stride, self.pad, self.colscale, self.bias, resid,
-                     0.0 if resid is None else s_resid / self.s_out, self.relu)
+                     rscale, self.relu, rvec=rvec)
 
 
 class Int8ResNet(nn.Module):
@@ -113,14 +155,20 @@ class Int8ResNet(nn.Module):
     ``zoo.models.image.resnet.ResNet``."""
 
     fmt = "int8"
+    act_scales = "channel"
 
-    def __init__(self, model, calib_x, fmt=None):
+    def __init__(self, model, calib_x, fmt=None, act_scales=None):
+        """``act_scales``: "channel" (one activation scale per channel) or "tensor" (one per tensor)."""
         super().__init__()
         from zoo.models.image import resnet as R
         if fmt is not None:
             self.fmt = fmt
+        if act_scales is not None:
+            self.act_scales = act_scales
         if self.fmt not in QMAX:
             raise ValueError("quantized format must be one of %s" % sorted(QMAX))
+        if self.act_scales not in ("channel", "tensor"):
+            raise ValueError("act_scales must be 'channel' or 'tensor'")
         model.eval()
         self.model = model
         dev = next(model.parameters()).device
@@ -154,7 +202,12 @@ class Int8ResNet(nn.Module):
     def calibrate(self, x):
         """Per-tensor absmax of every int8 tensor of the network on ``x`` (run in bf16)."""
         qmax = QMAX[self.fmt]
-        amax = lambda t: max(float(t.float().abs().max()), 1e-6) / qmax  # noqa: E731
+        if self.act_scales == "channel":
+            def amax(t):
+                return t.float().abs().amax(dim=tuple(range(t.dim() - 1))).clamp_min(1e-6) / qmax
+        else:
+            def amax(t):
+                return max(float(t.float().abs().max()), 1e-6) / qmax
         h = self._stem(x)
         self.s_in = amax(h)
         s_x = self.s_in
@@ -195,10 +248,13 @@ class Int8ResNet(nn.Module):
                 xq = u["conv3"](u["conv2"](h1), resid=sc, s_resid=s_sc)
             else:
                 xq = u["conv2"](h1, resid=sc, s_resid=s_sc)
+        vec = torch.is_tensor(self.s_out)
         if xq.is_cuda:
-            feat = native().gap_i8(xq.contiguous(), self.s_out)
+            feat = native().gap_i8(xq.contiguous(), 1.0, self.s_out.float().contiguous()) if vec else \
+                native().gap_i8(xq.contiguous(), self.s_out)
         else:
-            feat = (xq.double() * self.s_out).mean((1, 2)).to(torch.bfloat16)
+            s = self.s_out.double().to(xq.device) if vec else self.s_out
+            feat = (xq.double() * s).mean((1, 2)).to(torch.bfloat16)
         return self.model.fc(feat)
 
 
@@ -208,10 +264,10 @@ class Fp8ResNet(Int8ResNet):
     fmt = "fp8"
 
 
-def quantize_resnet(model, calib_x, fmt="int8"):
+def quantize_resnet(model, calib_x, fmt="int8", act_scales="channel"):
     """Static-int8 (or ``fmt="fp8"``) inference twin of ``model`` (a zoo ResNet), calibrated on
-    ``calib_x``."""
-    return (Fp8ResNet if fmt == "fp8" else Int8ResNet)(model, calib_x)
+    ``calib_x`` with per-channel (default) or per-tensor activation scales."""
+    return (Fp8ResNet if fmt == "fp8" else Int8ResNet)(model, calib_x, act_scales=act_scales)
 
 
 __all__ = ["Int8ResNet", "Fp8ResNet", "quantize_resnet", "qconv", "qconv_ref", "quantize_act", "to_fp8"]

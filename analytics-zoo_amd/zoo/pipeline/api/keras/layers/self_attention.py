@@ -24,6 +24,7 @@ import torch.nn.functional as F
 from zoo import ops
 from zoo.ops.attention import attention_packed
 from zoo.ops.nn import GeluLink, GradAdd, dropout_add, dropout_add_layer_norm
+from zoo.ops.pointwise import dropout as ops_dropout
 from zoo.pipeline.api.keras.base import Layer
 
 
@@ -147,7 +148,7 @@ class TransformerLayer(Layer):
         e = ops.embedding(tok, self.tok) + ops.embedding(pos, self.tok)
         if e.is_cuda:
             e = e.to(torch.bfloat16)
-        return F.dropout(e, self.embedding_drop, self.training)
+        return ops_dropout(e, self.embedding_drop, self.training)
 
     def call(self, xs):
         x = self._embed(xs)
@@ -200,8 +201,8 @@ class BERT(Layer):
         e = ops.embedding(tok, self.word) + ops.embedding(typ, self.token_type) + ops.embedding(pos, self.position)
         if e.is_cuda:  # bf16 activations end to end on the GPU (LayerNorm / attention / GEMMs all take bf16)
             e = e.to(torch.bfloat16)
-        x = F.dropout(ops.layer_norm(e, self.emb_ln_g, self.emb_ln_b, self.layer_norm_eps), self.hidden_drop,
-                      self.training)
+        x = ops_dropout(ops.layer_norm(e, self.emb_ln_g, self.emb_ln_b, self.layer_norm_eps), self.hidden_drop,
+                        self.training)
         mask = None
         if amask is not None:
             mask = (1.0 - amask.float()) * -10000.0  # [B, L] additive key mask (BERT.scala:94-105)

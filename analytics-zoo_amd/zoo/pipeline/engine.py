@@ -151,6 +151,16 @@ def _checkpoint_iteration(path):
     return -1
 
 
+def _tensors(b):
+    if isinstance(b, torch.Tensor):
+        return [b] if b.is_cuda else []
+    if isinstance(b, (list, tuple)):
+        return [t for v in b for t in _tensors(v)]
+    if isinstance(b, dict):
+        return [t for v in b.values() for t in _tensors(v)]
+    return []
+
+
 def _move(batch, device, non_blocking=True):
     if isinstance(batch, torch.Tensor):
         return batch.to(device, non_blocking=non_blocking)
@@ -405,6 +415,45 @@ class TrainingEngine:
             return data.data(train=True, epoch=self.state["epoch"])
         return iter(data)
 
+    def _device_batches(self, it):
+        """(x, y) on the device, one batch ahead: host batch i+1's copy is issued on a dedicated
+        copy stream BEFORE step i is issued, so the DMA overlaps step i's kernels; the compute
+        stream waits on the copy's event only when it reaches the batch (FeatureSet /
+        SampleToMiniBatch prefetch, NNEstimator.scala:382-470 -- here over PCIe from pinned host
+        batches). ``ZOO_COPY_STREAM=0``: copies on the compute stream right before the step."""
+        dev = self.device
+        if dev.type != "cuda" or os.environ.get("ZOO_COPY_STREAM", "1") == "0":
+            for batch in it:
+                yield _move(batch[0], dev), _move(batch[1], dev)
+            return
+        if getattr(self, "_copy_stream", None) is None:
+            self._copy_stream = torch.cuda.Stream(dev)
+        cs = self._copy_stream
+
+        def issue(batch):
+            with torch.cuda.stream(cs):
+                x, y = _move(batch[0], dev), _move(batch[1], dev)
+                ev = torch.cuda.Event()
+                ev.record(cs)
+            return x, y, ev
+
+        def handoff(item):
+            x, y, ev = item
+            cur = torch.cuda.current_stream(dev)
+            cur.wait_event(ev)
+            for t in _tensors(x) + _tensors(y):
+                t.record_stream(cur)   # allocated on the copy stream, consumed on the compute stream
+            return x, y
+
+        ahead = None
+        for batch in it:
+            nxt = issue(batch)
+            if ahead is not None:
+                yield handoff(ahead)
+            ahead = nxt
+        if ahead is not None:
+            yield handoff(ahead)
+
     def _fit_loop(self, data, end_trigger, validation, val_methods, val_trigger, log_every, callbacks):
         state = self.state
         while not end_trigger(state):
@@ -412,10 +461,7 @@ class TrainingEngine:
             recs = 0
             t_last = time.time()
             n_since = 0
-            for batch in self._iter_epoch(data):
-                x, y = batch[0], batch[1]
-                x = _move(x, self.device)
-                y = _move(y, self.device)
+            for x, y in self._device_batches(self._iter_epoch(data)):
                 loss = self.train_step(x, y)
                 bs = (x[0] if isinstance(x, (list, tuple)) else x).shape[0] * self.sync.world
                 recs += bs

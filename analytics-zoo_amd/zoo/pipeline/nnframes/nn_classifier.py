@@ -250,7 +250,9 @@ class NNEstimator(_Params):
             val = self._featureset(vdf, vbs, False)
             val_methods = to_metrics(vm, crit)
         end = self.endWhen or T.MaxEpoch(self.maxEpoch)
-        eng.fit(data, end_trigger=end, validation=val, val_methods=val_methods, val_trigger=val_trigger)
+        # per-iteration callbacks (engine, state): monitoring hooks, e.g. bench.py --input featureset
+        eng.fit(data, end_trigger=end, validation=val, val_methods=val_methods, val_trigger=val_trigger,
+                callbacks=getattr(self, "_train_callbacks", ()))
         self.engine = eng
         return self._create_model()
 

@@ -53,6 +53,10 @@ def parse():
                     help="gradient wire: auto = bf16 whenever GPU collectives run (BigDL 16-bit transfer)")
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="0: per-model default (ResNet 32, NCF one bucket)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--input", default="device", choices=["device", "featureset"],
+                    help="featureset: ResNet-50 trained through NNEstimator.fit on a synthetic DataFrame of uint8 "
+                         "NHWC images (FeatureSet -> pinned batches -> copy stream -> on-device normalisation), "
+                         "BASELINE config 2; device: one device-resident fp32 batch")
     return ap.parse_args()
 
 
@@ -135,6 +139,54 @@ _BUCKET = [0.0]
 
 def a_bucket(default):
     return _BUCKET[0] if _BUCKET[0] > 0 else default
+
+
+def run_featureset(a, ctx, world):
+    """ResNet-50 through NNEstimator.fit (NNEstimator.scala:382-470): a pandas DataFrame of uint8
+    224x224x3 images -> FeatureSet (native gather into pinned batches) -> the engine's copy
+    stream (one batch ahead) -> uint8 normalisation fused into the stem. Times EXACTLY the K
+    iterations after W warm-up iterations (device sync + barrier at both ends, from a per-
+    iteration callback); returns (elapsed seconds, first loss, final loss, engine)."""
+    import numpy as np
+    import pandas as pd
+    import torch
+    import torch.distributed as dist
+    from zoo.common.triggers import MaxIteration
+    from zoo.feature.common import Lambda
+    from zoo.models.image.resnet import resnet50
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD, EpochDecayWithWarmUp
+    from zoo.pipeline.nnframes.nn_classifier import NNEstimator
+    torch.manual_seed(1234)
+    model = resnet50(num_classes=1000, zero_init_residual=True)
+    warm = 10
+    optim = SGD(learningrate=0.01, momentum=0.9, weightdecay=1e-4, dampening=0.0, nesterov=True,
+                learningrate_schedule=EpochDecayWithWarmUp(warm, (0.1 - 0.01) / warm, lambda epoch: 0))
+    n = a.batch * world * (a.warmup + a.steps)       # one epoch covers the whole run: no epoch edge
+    rng = np.random.default_rng(4321)
+    imgs = rng.integers(0, 256, size=(n, 224, 224, 3), dtype=np.uint8)
+    labels = rng.integers(0, 1000, size=n)
+    df = pd.DataFrame({"features": list(imgs), "label": labels})
+    est = NNEstimator(model, softmax_cross_entropy, Lambda(lambda v: v), Lambda(lambda v: np.int64(v)))
+    est.setBatchSize(a.batch * world).setOptimMethod(optim).setEndWhen(MaxIteration(a.warmup + a.steps))
+    dev = ctx.device
+    mark = {}
+
+    def timer(eng, state):
+        it = state["neval"] - 1
+        if it == 1:
+            mark["first"] = eng._pending_loss[-1][1]
+        if it in (a.warmup, a.warmup + a.steps):
+            _sync(dev)
+            if world > 1:
+                dist.barrier()
+            _sync(dev)
+            mark[it] = time.perf_counter()
+            mark["last"] = eng._pending_loss[-1][1] if eng._pending_loss else None
+    est._train_callbacks = (timer,)
+    est.fit(df)
+    elapsed = mark[a.warmup + a.steps] - mark[a.warmup]
+    return elapsed, mark.get("first"), mark.get("last"), est.engine
 
 
 def grad_sync_label(eng, a):
@@ -223,6 +275,17 @@ def main():
         print("bench.py: --gpus %d but the process group has %d ranks" % (a.gpus, world), file=sys.stderr)
         return 2
     dev = ctx.device
+    if a.input == "featureset":
+        if a.model != "resnet50":
+            print("bench.py: --input featureset is the ResNet-50 NNEstimator config", file=sys.stderr)
+            return 2
+        elapsed, first_loss, loss, eng = run_featureset(a, ctx, world)
+        return report(a, ctx, world, dev, eng, None, None, elapsed, first_loss, loss, 0.0, a.batch,
+                      BASELINE_METRIC, "images/sec", "ResNet-50",
+                      {"image_size": 224, "optimizer": "SGD(nesterov, momentum=0.9, wd=1e-4, warmup 0.01->0.1/10 it)",
+                       "input": "featureset"},
+                      "synthetic uint8 NHWC images in a pandas DataFrame -> NNEstimator.fit (FeatureSet, "
+                      "pinned batches, copy stream); random-init weights")
     if a.model == "resnet50":
         batch = a.batch
         eng, (x, y), model_name, extra = build_resnet50(ctx, batch)
@@ -256,12 +319,21 @@ def main():
         dist.barrier()
     _sync(dev)
     elapsed = time.perf_counter() - t0
+    return report(a, ctx, world, dev, eng, x, y, elapsed, first_loss, loss, host, batch, metric, unit, model_name,
+                  extra, "synthetic (random-init weights, random inputs/labels)")
+
+
+def report(a, ctx, world, dev, eng, x, y, elapsed, first_loss, loss, host, batch, metric, unit, model_name, extra,
+           data):
+    """Max elapsed over ranks -> rank 0 prints the one JSON line."""
+    import torch
+    import torch.distributed as dist
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    final_loss = float(loss.float().item())
-    diag = comm_diagnostics(eng, x, y, world)
+    final_loss = float(loss.float().item()) if loss is not None else None
+    diag = comm_diagnostics(eng, x, y, world) if x is not None else {"rccl_world": world}
     total = batch * world * a.steps
     value = total / elapsed
     if ctx.rank == 0:
@@ -270,17 +342,18 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16" if dev.type == "cuda" else "fp32",
-            "data": "synthetic (random-init weights, random inputs/labels)",
+            "data": data,
             "config": dict({"model": model_name, "global_batch": batch * world, "per_gpu_batch": batch,
                             "seq_len": None, "parallelism": "dp%d" % world,
                             "grad_sync": grad_sync_label(eng, a)},
                            **extra),
             "first_loss": round(float(first_loss.float().item()), 4) if first_loss is not None else None,
-            "final_loss": round(final_loss, 4),
+            "final_loss": round(final_loss, 4) if final_loss is not None else None,
+        }
+        if x is not None:
             # issue time of a step on the host (no device sync inside the timed loop): near
             # ms_per_step means host-bound, well below means device-bound
-            "host_ms_per_step": round(host / a.steps * 1e3, 3),
-        }
+            out["host_ms_per_step"] = round(host / a.steps * 1e3, 3)
         out.update(diag)
         print(json.dumps(out), flush=True)
     if world > 1:

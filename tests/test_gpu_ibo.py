@@ -149,3 +149,78 @@ def test_ibo_late_contribution_degrades_without_raising(gpu, monkeypatch, caplog
         assert abs(a - b) < 1e-5 * max(1.0, abs(b)), (l0, l1)
     assert all(abs(v) < 1e3 for v in l1) and torch.isfinite(w1).all()
     assert ((w1 - w0).norm() / w0.norm()).item() < 0.05
+
+
+def _bert_cls(gpu, drop):
+    import torch.nn as nn
+    from zoo.pipeline.api.keras.layers import BERT
+
+    class Cls(nn.Module):
+        def __init__(self):
+            super().__init__()
+            self.bert = BERT(vocab=500, hidden_size=256, n_block=2, n_head=4, max_position_len=64,
+                             intermediate_size=1024, hidden_drop=drop, attn_drop=drop, output_all_block=False)
+            self.fc = nn.Linear(256, 3)
+
+        def forward(self, xs):
+            return self.fc(self.bert(xs)[1].float())
+    B, L = 32, 64
+    xs = [torch.randint(0, 500, (B, L), device=gpu), torch.zeros(B, L, dtype=torch.long, device=gpu),
+          torch.arange(L, device=gpu).repeat(B, 1), torch.ones(B, L, device=gpu)]
+    y = torch.randint(0, 3, (B,), device=gpu)
+    return Cls(), xs, y
+
+
+def test_graph_captured_ibo_matches_eager(gpu, monkeypatch):
+    """BERT training with the forward, backward AND the in-backward AdamW updates captured in one
+    hipGraph (learning rate / bias corrections read from device memory, staged before every
+    replay) follows the eager end-of-step run within the bars of the eager IBO test."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.ops import native, softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext("ibo-graph")
+    torch.manual_seed(1)
+    m, xs, y = _bert_cls(gpu, 0.0)
+    runs = {}
+    for graph in (False, True):
+        monkeypatch.setenv("ZOO_OPTIM_IN_BWD", "1" if graph else "0")
+        # total / warmup: the learning rate changes every step, so a baked-in rate would show
+        eng = TrainingEngine(copy.deepcopy(m), softmax_cross_entropy,
+                             AdamWeightDecay(lr=1e-4, warmup_portion=0.3, total=10), bucket_mb=0.5, hip_graph=graph)
+        assert eng.ibo == graph
+        native().set_deterministic(True)
+        try:
+            losses = [float(eng.train_step(xs, y).float().item()) for _ in range(7)]
+            torch.cuda.synchronize()
+        finally:
+            native().set_deterministic(False)
+        if graph:
+            assert len(eng._graphs) == 1 and eng.sync.ibo_steps == 7
+            assert len(next(iter(eng._graphs.values()))[4]) > 0     # in-backward updates inside the graph
+        runs[graph] = (losses, eng.flat.master.detach().clone())
+    (l0, w0), (l1, w1) = runs[False], runs[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) < 1e-3 * max(1.0, abs(b)), (l0, l1)
+    assert ((w1 - w0).norm() / w0.norm()).item() < 1e-4
+
+
+def test_graph_replay_draws_fresh_dropout_masks(gpu):
+    """Dropout inside a captured step: the seeds baked into the graph are xored with a device
+    offset restaged every step, so replays of the SAME batch with frozen weights (lr 0) give
+    different losses; with the offset held fixed they repeat exactly."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.ops import softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext("graph-dropout")
+    torch.manual_seed(2)
+    m, xs, y = _bert_cls(gpu, 0.1)
+    eng = TrainingEngine(m, softmax_cross_entropy, AdamWeightDecay(lr=0.0, weight_decay=0.0), hip_graph=True)
+    losses = [float(eng.train_step(xs, y).float().item()) for _ in range(6)]
+    assert len(eng._graphs) == 1
+    replayed = losses[2:]
+    assert len(set(round(v, 6) for v in replayed)) == len(replayed), losses
+    eng._seed_rng.getrandbits = lambda k: 12345     # a frozen offset: identical masks on every replay
+    frozen = [float(eng.train_step(xs, y).float().item()) for _ in range(3)]
+    assert max(frozen) - min(frozen) < 1e-6, frozen

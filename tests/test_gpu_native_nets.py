@@ -22,6 +22,42 @@ def _layer_parity():
     return layer_parity
 
 
+# Per-layer bounds (tools/layer_parity.py: the CPU twin computes with the bf16 weights the kernels
+# read and rounds a conv output the GPU stores in bf16 before its BatchNorm, so a healthy layer
+# differs only by accumulation order and output rounding). EVERY layer must meet them -- the
+# reference KerasBaseSpec (zoo/src/test/scala/com/intel/analytics/zoo/pipeline/api/keras/layers/
+# KerasBaseSpec.scala:45-90) checks every output and gradient, not a median. BatchNorm affine
+# gradients are checked as the stacked [dgamma; dbeta] pair (dgamma alone is a cancelling sum).
+# Measured r5 (profiles/r5/layer_parity_r5.md): every layer of the 8 backbones and both SSDs at
+# <= 0.2 % forward, <= 0.33 % dx, <= 0.26 % weight gradients, <= 0.23 % BN affine; one conv's dgrad
+# scaled by 1.05 shows 5.0 % in that layer alone
+FWD_MAX = 0.01
+DX_MAX = 0.01
+DW_MAX = 0.01
+AFFINE_MAX = 0.01
+# (net, layer, metric) -> why the bound does not apply
+EXEMPT = {}
+
+
+def _violations(net, rows):
+    bad = []
+    for r in rows:
+        checks = [("fwd", r["fwd"], FWD_MAX)]
+        for k, v in r.items():
+            if not isinstance(v, float) or not k.startswith("d"):
+                continue
+            if k == "dx":
+                checks.append((k, v, DX_MAX))
+            elif k == "daffine":
+                checks.append((k, v, AFFINE_MAX))
+            elif k not in ("dgamma", "dbeta"):
+                checks.append((k, v, DW_MAX))
+        for k, v, bound in checks:
+            if v > bound and (net, r["layer"], k) not in EXEMPT:
+                bad.append((r["layer"], k, v))
+    return bad
+
+
 def _calibrate_bn(model, x):
     """Running statistics = the batch statistics of ``x`` (one training forward at momentum 1):
     every BatchNorm then normalises in eval mode, so the eval network is numerically stable."""
@@ -40,15 +76,14 @@ def _calibrate_bn(model, x):
 
 @pytest.mark.parametrize("name,hw", NETS)
 def test_backbone_layer_parity_and_trains_natively(gpu, name, hw, monkeypatch):
-    """Every native layer against the SAME layer on the fp32 CPU path, fed the layer's actual
-    GPU input and upstream gradient (tools/layer_parity.py): local forward error <= 2 % per
-    layer, median local dx / dweight error <= 5 % (bf16 rounding plus the ReLU-mask flips of
-    pre-activations within rounding of zero; a wrong kernel shows O(1)). End to end in a stable
-    regime -- eval mode with calibrated BatchNorm statistics -- the logits match the fp32
-    reference within 5 %. The GPU trace holds zoo:: kernels and no MIOpen / hipBLASLt kernel;
+    """Every native layer against the SAME layer on the CPU path, fed the layer's actual GPU
+    input and upstream gradient (tools/layer_parity.py): forward, dx, every weight gradient and
+    the BatchNorm affine pair of EVERY layer within the per-layer bounds above (a wrong kernel
+    shows O(1); the fault-injection test below shows a 5 % error in one layer fails). End to end
+    in a stable regime -- eval mode with calibrated BatchNorm statistics -- the logits match the
+    fp32 reference within 5 %. The GPU trace holds zoo:: kernels and no MIOpen / hipBLASLt kernel;
     then the engine trains the net (finite loss)."""
     import copy
-    import statistics
     from torch.profiler import ProfilerActivity, profile
     from zoo.common.nncontext import init_nncontext
     from zoo.models.image import native_nets
@@ -73,14 +108,11 @@ def test_backbone_layer_parity_and_trains_natively(gpu, name, hw, monkeypatch):
     assert not bad, bad[:5]
     rows = [r for r in rows if "error" not in r]
     assert len(rows) >= 8, rows[:3]
-    fwd = max(r["fwd"] for r in rows)
-    dx = [r["dx"] for r in rows if "dx" in r]
-    dw = [v for r in rows for k, v in r.items() if k.startswith("d") and k not in ("dx",) and isinstance(v, float)]
-    print(name, "layers", len(rows), "max fwd", fwd, "median dx", statistics.median(dx) if dx else None,
-          "median dW", statistics.median(dw) if dw else None)
-    assert fwd <= 0.02, [r for r in rows if r["fwd"] > 0.02][:3]
-    assert dx and statistics.median(dx) <= 0.05, statistics.median(dx)
-    assert dw and statistics.median(dw) <= 0.05, statistics.median(dw)
+    assert any("dx" in r for r in rows)
+    bad = _violations(name, rows)
+    print(name, "layers", len(rows), "max fwd", max(r["fwd"] for r in rows),
+          "max dx", max(r.get("dx", 0.0) for r in rows), "violations", bad[:5])
+    assert not bad, bad[:8]
     # end to end, stable regime: eval mode with calibrated BatchNorm statistics
     torch.manual_seed(1)
     net2 = build(name, 16)
@@ -165,11 +197,10 @@ def test_ssd_trains_natively(gpu, mobilenet):
 @pytest.mark.parametrize("mobilenet", [False, True])
 def test_ssd_loss_and_gradient_parity(gpu, mobilenet):
     """SSD (VGG-16 / MobileNet, 300x300) on the native kernels vs the same weights on the fp32
-    CPU path: MultiBoxLoss within 3 %, and per-layer local parity of every layer of the
-    detector (backbone, extras, loc / conf heads) in the training backward: local forward error
-    <= 2 %, median local dx / dweight error <= 5 %."""
+    CPU path: MultiBoxLoss within 3 %, and per-layer local parity of EVERY layer of the
+    detector (backbone, extras, loc / conf heads) in the training backward within the per-layer
+    bounds above."""
     import copy
-    import statistics
     from zoo.common.nncontext import init_nncontext
     from zoo.models.image.objectdetection.ssd import SSD, SSDMobileNet, MultiBoxLoss
     init_nncontext("ssd-parity")
@@ -198,10 +229,32 @@ def test_ssd_loss_and_gradient_parity(gpu, mobilenet):
                   lambda o: crit(o[0].float(), o[1].float(), pri.to(gpu), tg), train=True)
     rows = [r for r in rows if "error" not in r]
     assert len(rows) >= 10
-    dx = [r["dx"] for r in rows if "dx" in r]
-    dw = [v for r in rows for k, v in r.items() if k.startswith("d") and k != "dx" and isinstance(v, float)]
-    fwd = max(r["fwd"] for r in rows)
-    print("ssd", "mobilenet" if mobilenet else "vgg", "loss", lg, lc, "max fwd", fwd, "median dx",
-          statistics.median(dx), "median dW", statistics.median(dw))
-    assert fwd <= 0.02
-    assert statistics.median(dx) <= 0.05 and statistics.median(dw) <= 0.05
+    nm = "ssd-mobilenet" if mobilenet else "ssd-vgg"
+    bad = _violations(nm, rows)
+    print(nm, "loss", lg, lc, "max fwd", max(r["fwd"] for r in rows), "violations", bad[:5])
+    assert not bad, bad[:8]
+
+
+@pytest.mark.parametrize("name,hw", [("vgg-16", 224), ("mobilenet", 224)])
+def test_layer_parity_catches_a_5pct_dgrad_fault(gpu, name, hw, monkeypatch):
+    """ZOO_FAULT_DGRAD scales ONE conv's data gradient by 1.05 (zoo/ops/_kern.py): the per-layer
+    check must flag exactly that kind of error (the median bar of r4 could not)."""
+    import copy
+    from zoo.common.nncontext import init_nncontext
+    from zoo.models.image import native_nets
+    from zoo.models.image.imageclassification.nets import build
+    from zoo.ops import _kern, softmax_cross_entropy
+    init_nncontext("nets-fault")
+    monkeypatch.setattr(native_nets, "_dropout", lambda x, p, training: x)
+    torch.manual_seed(0)
+    net = build(name, 16)
+    x = torch.randn(2, 3, hw, hw)
+    y = torch.randint(0, 16, (2,))
+    lp = _layer_parity()
+    monkeypatch.setenv("ZOO_FAULT_DGRAD", "3:1.05")
+    _kern.reset_fault_counter()
+    rows = lp.run(copy.deepcopy(net).to(gpu), copy.deepcopy(net), x.to(gpu),
+                  lambda o: softmax_cross_entropy(o, y.to(gpu)), train=True)
+    monkeypatch.delenv("ZOO_FAULT_DGRAD")
+    bad = _violations(name, [r for r in rows if "error" not in r])
+    assert bad and all(k == "dx" for _, k, _ in bad), bad
