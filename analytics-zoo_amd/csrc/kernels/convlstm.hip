@@ -1,0 +1,175 @@
+// One launch per ConvLSTM2D / ConvLSTM3D time step (gfx950): the recurrent convolution as an MFMA implicit
+// GEMM with the LSTM cell in its epilogue.
+//
+// Gate-interleaved layout: the gate weights (and the input convolution's output, the gate
+// gradients and the saved activations) are ordered column 4j + g = gate g (i, f, cand, o) of
+// hidden channel j. A 16x16x32 MFMA accumulator gives each lane one pixel and 4 CONSECUTIVE rows,
+// so with D = W . X^T (rows = gate columns, columns = pixels) a lane holds all four gate
+// pre-activations of one (pixel, channel): the cell update needs no data exchange, no LDS and
+// no second pass over gate tensors.
+//
+// Forward, step t:   g = gx_t + conv(h_{t-1}, Wh)  ->  i, f, cand, o;  c_t = f c_{t-1} + i cand;
+//                    h_t = o act(c_t)  (h_t also stored bf16 in the padded NHWC history slot that
+//                    step t + 1's conv reads). Step 0 (h_{-1} = 0) skips the GEMM.
+// Backward, step t:  dh_t = dout_t + conv(dgb_{t+1}, flip(Wh)) (the recurrent data gradient, rows =
+//                    hidden channels) and the step's cell backward in the same epilogue: gate
+//                    gradients fp32 (the input conv's gradient) + bf16 (dgb_t, the operand of the
+//                    next dgrad and of ONE batched weight-gradient conv over all steps), dc_{t-1}.
+//
+// One wave per workgroup, 16 pixels per wave, all gate rows per wave (NI = rows / 16 <= 16), the
+// reduction R*S*Cx walked 32 deep with the activation fragment gathered straight from global
+// (zero outside the image). Sized for the latency-bound recurrent step (M = B*H*W of a few
+// thousand pixels, 4F <= 256 gate rows): enough waves to cover every CU, no barrier.
+// ConvLSTM3D is the same kernel with a depth axis (D slices, Q depth taps).
+// Reference: InternalConvLSTM2D.scala / InternalConvLSTM3D.scala (Zs/pipeline/api/keras/layers),
+// SURVEY.md §2.16 HK11.
+#include "common.h"
+#include "lstm.h"
+
+namespace zoo {
+
+struct CLArgs {
+  const bf16_t* X;   // conv input [B][D][H][W][Cx] (null: no GEMM -- the step's recurrent term is 0)
+  const bf16_t* Wt;  // weights [Nr][ldw], row n = output row, k = ((q * R + r) * S + s) * Cx + channel
+  int B, D, H, Wd, Cx, Q, R, S, ldw, Nr, M, F, iact, act;   // ConvLSTM2D: D = Q = 1
+  // forward
+  const float* gx;      // [M][F][4] input-conv gate pre-activations (bias included)
+  const float* cprev;   // [M][F] or null
+  float* h;             // [M][F]
+  float* c;             // [M][F]
+  float* acts;          // [M][F][4] activated gates (saved for backward)
+  bf16_t* hb;           // [M][ldh] next history slot
+  int ldh;
+  // backward
+  const float* dout;    // [M][F] or null
+  const float* cc;      // c_t [M][F]
+  float* dc;            // in: dc_{t+1} contribution (null when dc_in is false), out: dc_{t-1}
+  int dc_in;
+  float* dg;            // [M][F][4]
+  bf16_t* dgb;          // [M][ldg] bf16 gate gradients
+  int ldg;
+};
+
+template <int NI>
+ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane) {
+#pragma unroll
+  for (int i = 0; i < NI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (!a.X) return;
+  const bool mok = m < a.M;
+  const int mm = mok ? m : 0;
+  const int x = mm % a.Wd, y = (mm / a.Wd) % a.H, z = (mm / (a.Wd * a.H)) % a.D, b = mm / (a.Wd * a.H * a.D);
+  const int KD = a.Q * a.R * a.S * a.Cx;
+  const int pq = a.Q / 2, ph = a.R / 2, pw = a.S / 2;
+  const int kq = 8 * (lane >> 4), nr = lane & 15;
+  bf16x8 zero;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) zero[e] = (__bf16)0.f;
+  for (int k0 = 0; k0 < KD; k0 += 32) {
+    const int k = k0 + kq;
+    bf16x8 bv = zero;
+    if (mok && k < KD) {
+      const int tap = k / a.Cx, ch = k - tap * a.Cx;
+      const int q = tap / (a.R * a.S), rs = tap - q * (a.R * a.S);
+      const int r = rs / a.S, s = rs - r * a.S;
+      const int zz = z + q - pq, yy = y + r - ph, xx = x + s - pw;
+      if (zz >= 0 && zz < a.D && yy >= 0 && yy < a.H && xx >= 0 && xx < a.Wd)
+        bv = *reinterpret_cast<const bf16x8*>(a.X + ((((size_t)b * a.D + zz) * a.H + yy) * a.Wd + xx) * a.Cx + ch);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int n = 16 * i + nr;
+      bf16x8 wv = zero;
+      if (n < a.Nr && k < KD) wv = *reinterpret_cast<const bf16x8*>(a.Wt + (size_t)n * a.ldw + k);
+      acc[i] = mfma16(wv, bv, acc[i]);
+    }
+  }
+}
+
+template <int NI>
+__global__ __launch_bounds__(64) void convlstm_fwd_kernel(CLArgs a) {
+  const int lane = threadIdx.x;
+  const int m = blockIdx.x * 16 + (lane & 15);
+  f32x4 acc[NI];
+  cl_gemm<NI>(a, m, acc, lane);
+  if (m >= a.M) return;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int j = 4 * i + (lane >> 4);   // rows 16 i + 4 (lane >> 4) + q = gate q of channel j
+    if (j >= a.F) continue;
+    const size_t e = (size_t)m * a.F + j;
+    const float4 g4 = *reinterpret_cast<const float4*>(a.gx + 4 * e);
+    const float ig = lstm_act(acc[i][0] + g4.x, a.iact), fg = lstm_act(acc[i][1] + g4.y, a.iact);
+    const float cg = lstm_act(acc[i][2] + g4.z, a.act), og = lstm_act(acc[i][3] + g4.w, a.iact);
+    const float cp = a.cprev ? a.cprev[e] : 0.f;
+    const float cn = fg * cp + ig * cg;
+    const float hn = og * lstm_act(cn, a.act);
+    a.c[e] = cn;
+    a.h[e] = hn;
+    a.hb[(size_t)m * a.ldh + j] = f2bf(hn);
+    *reinterpret_cast<float4*>(a.acts + 4 * e) = make_float4(ig, fg, cg, og);
+  }
+}
+
+template <int NI>
+__global__ __launch_bounds__(64) void convlstm_bwd_kernel(CLArgs a) {
+  const int lane = threadIdx.x;
+  const int m = blockIdx.x * 16 + (lane & 15);
+  f32x4 acc[NI];
+  cl_gemm<NI>(a, m, acc, lane);
+  if (m >= a.M) return;
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = 16 * i + 4 * (lane >> 4) + q;   // row = hidden channel of the data gradient
+      if (j >= a.F) continue;
+      const size_t e = (size_t)m * a.F + j;
+      const float4 g4 = *reinterpret_cast<const float4*>(a.acts + 4 * e);
+      const float ig = g4.x, fg = g4.y, cg = g4.z, og = g4.w;
+      const float tc = lstm_act(a.cc[e], a.act);
+      const float dh = acc[i][q] + (a.dout ? a.dout[e] : 0.f);
+      const float dcv = dh * og * lstm_dact(tc, a.act) + (a.dc_in ? a.dc[e] : 0.f);
+      const float cp = a.cprev ? a.cprev[e] : 0.f;
+      const float d0 = dcv * cg * lstm_dact(ig, a.iact), d1 = dcv * cp * lstm_dact(fg, a.iact);
+      const float d2 = dcv * ig * lstm_dact(cg, a.act), d3 = dh * tc * lstm_dact(og, a.iact);
+      *reinterpret_cast<float4*>(a.dg + 4 * e) = make_float4(d0, d1, d2, d3);
+      *reinterpret_cast<uint2*>(a.dgb + (size_t)m * a.ldg + 4 * j) =
+          make_uint2((uint32_t)f2bf(d0) | ((uint32_t)f2bf(d1) << 16), (uint32_t)f2bf(d2) | ((uint32_t)f2bf(d3) << 16));
+      a.dc[e] = dcv * fg;   // same lane read dc_{t+1}[e] above: in place
+    }
+  }
+}
+
+template <int NI>
+static hipError_t cl_launch(const CLArgs& a, int bwd, hipStream_t st) {
+  const dim3 grid((a.M + 15) / 16);
+  if (bwd)
+    hipLaunchKernelGGL(convlstm_bwd_kernel<NI>, grid, dim3(64), 0, st, a);
+  else
+    hipLaunchKernelGGL(convlstm_fwd_kernel<NI>, grid, dim3(64), 0, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace zoo
+
+using namespace zoo;
+
+// rows: forward 4F (gate rows), backward the hidden channels of the data gradient (>= F)
+extern "C" hipError_t zoo_convlstm_step(const void* X, const void* Wt, int B, int D, int H, int W, int Cx, int Q,
+                                        int R, int S, int ldw, int Nr, int F, int iact, int act, const float* gx,
+                                        const float* cprev, float* h, float* c, float* acts, void* hb, int ldh,
+                                        const float* dout, const float* cc, float* dc, int dc_in, float* dg,
+                                        void* dgb, int ldg, int bwd, hipStream_t st) {
+  CLArgs a{(const bf16_t*)X, (const bf16_t*)Wt, B, D, H, W, Cx, Q, R, S, ldw, Nr, B * D * H * W, F, iact, act,
+           gx, cprev, h, c, acts, (bf16_t*)hb, ldh, dout, cc, dc, dc_in, dg, (bf16_t*)dgb, ldg};
+  if (a.M <= 0) return hipSuccess;
+  const int ni = (Nr + 15) / 16;
+  switch (ni) {
+#define CL_CASE(n) \
+  case n: return cl_launch<n>(a, bwd, st);
+    CL_CASE(1) CL_CASE(2) CL_CASE(3) CL_CASE(4) CL_CASE(5) CL_CASE(6) CL_CASE(7) CL_CASE(8)
+    CL_CASE(9) CL_CASE(10) CL_CASE(11) CL_CASE(12) CL_CASE(13) CL_CASE(14) CL_CASE(15) CL_CASE(16)
+#undef CL_CASE
+    default: return hipErrorInvalidValue;
+  }
+}

@@ -57,6 +57,13 @@ struct BwdStats {
   const float* mgamma;  // zmode 1 (nullptr: gamma = 1 / beta = 0)
   const float* mbeta;
   int unbatched;        // 1: igemm.hip EPI 2 row loop without batched loads (A/B, ZOO_EPI2_BATCH=0)
+  // BatchNorm-backward PROLOGUE (pw.hip EPI 2, bnfold.hip): the GEMM's A operand X is the
+  // ReLU-masked gradient g of a conv -> BN unit; the kernel forms that unit's BN backward
+  // dy = coef[k] g + coef[Kx + k] pro_y + coef[2 Kx + k] in registers (Kx = X channels) and, if
+  // pro_dy is set, writes dy there for the weight gradient. nullptr: X is the operand itself.
+  const void* pro_y;
+  const float* pro_coef;
+  void* pro_dy;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

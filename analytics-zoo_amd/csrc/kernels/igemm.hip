@@ -813,6 +813,12 @@ extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* 
 extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
+  if (bsp && bsp->pro_y) {
+    // the BN-backward prologue exists only in pw.hip (the caller materialises dy otherwise)
+    const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp->sums, stats);
+    if (zoo_pw_eligible(g, igemm_route_epi(epi, bsp->zgelu), bsp)) return zoo_pw(X, W, Y, resid, stats, g, epi, bsp, st);
+    return hipErrorInvalidValue;
+  }
   {
     // stride-1 3x3 64 -> 64 channel convs (ResNet stage 1): the persistent streaming kernel (c3.hip)
     const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats);

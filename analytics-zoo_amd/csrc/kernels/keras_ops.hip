@@ -15,6 +15,7 @@
 // ConvLSTM2D,ConvLSTM3D}.scala and InternalConvLSTM3D.scala:40-218 (SURVEY.md §2.2 K3, §2.16
 // HK11/HK15/HK17).
 #include "common.h"
+#include "lstm.h"
 
 namespace zoo {
 
@@ -230,27 +231,6 @@ __global__ void upsample_bwd_kernel(const T* __restrict__ dy, T* __restrict__ dx
 }
 
 // ---------------------------------------------------------------- ConvLSTM gates
-// activation codes (zoo/ops/layers.py): 0 linear, 1 tanh, 2 sigmoid, 3 hard_sigmoid, 4 relu
-ZOO_DEV float lstm_act(float x, int a) {
-  switch (a) {
-    case 1: return tanhf(x);
-    case 2: return 1.f / (1.f + __expf(-x));
-    case 3: { const float v = 0.2f * x + 0.5f; return v < 0.f ? 0.f : (v > 1.f ? 1.f : v); }
-    case 4: return x > 0.f ? x : 0.f;
-    default: return x;
-  }
-}
-// derivative from the activation's OUTPUT
-ZOO_DEV float lstm_dact(float y, int a) {
-  switch (a) {
-    case 1: return 1.f - y * y;
-    case 2: return y * (1.f - y);
-    case 3: return (y > 0.f && y < 1.f) ? 0.2f : 0.f;
-    case 4: return y > 0.f ? 1.f : 0.f;
-    default: return 1.f;
-  }
-}
-
 // g = gx + gh ([M, 4F]: i | f | candidate | o); c = f * c_prev + i * act(cand); h = o * act(c)
 __global__ void lstm_gates_fwd_kernel(const float* __restrict__ gx, const float* __restrict__ gh,
                                       const float* __restrict__ cprev, float* __restrict__ h, float* __restrict__ c,

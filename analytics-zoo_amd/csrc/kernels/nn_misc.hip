@@ -266,7 +266,7 @@ __global__ __launch_bounds__(256) void layernorm_bwd_v2_kernel(const bf16_t* __r
                                                                const float* __restrict__ rstd, bf16_t* __restrict__ dX,
                                                                float* __restrict__ part, int rows, int D,
                                                                const bf16_t* __restrict__ dY2, DropArgs dr) {
-  if (dr.A && dr.off) dr.s0 ^= *dr.off;
+  if (dr.S && dr.off) dr.s0 ^= *dr.off;  // backward: dr.S (dA) marks the dropout branch
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* red = reinterpret_cast<float*>(smem);  // [4 waves][2][D]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;

@@ -38,6 +38,11 @@
 // Epilogues: EPI 1 = bf16 output + BN statistics of the stored values (the forward of every
 // conv->BN unit); EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
 // and the producer's fused BN-backward sums (sum dy, sum dy * xhat).
+// Prologue (PRO, EPI 2, K <= 256): the activation operand is the unit's OWN BN backward,
+// dy = A g + B y + Cc, formed in the operand registers from the masked gradient g and the unit's
+// pre-BN output y as they arrive (per-channel A | B | Cc in LDS); channel group 0 also writes dy
+// for the weight gradient (bnfold.hip: the separate BN-backward apply pass and the re-read of dy
+// are gone).
 // Reference parity: MKL-DNN 1x1 convolution primitives behind BigDL SpatialConvolution
 // (Zs/pipeline/api/keras/layers/Convolution2D.scala:86-110), SURVEY.md §2.16 HK3 / HK5.
 #include <stdlib.h>
@@ -58,7 +63,7 @@ struct PwArgs {
 constexpr int PW_NW = 8;  // waves per workgroup (2 per SIMD)
 
 // NP = output channels per workgroup (64 / 128), TPM = pixels per wave tile (16 / 32), KT = K / 32
-template <int NP, int TPM, int KT, int EPI>
+template <int NP, int TPM, int KT, int EPI, bool PRO>
 __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restrict__ A, const bf16_t* __restrict__ B,
                                                            bf16_t* __restrict__ Y, const bf16_t* __restrict__ resid,
                                                            float* __restrict__ stats, PwArgs p, BwdStats bs) {
@@ -75,6 +80,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   const int fr = lane & 15, fq = lane >> 4;
   const int N = p.N;
   float* patch = ssum + 2 * NP + w * 16 * PITCH;                   // wave-private fp32 16 x NP patch
+  float* pco = ssum + 2 * NP + PW_NW * 16 * PITCH;                 // PRO: A | B | Cc, [3][K]
 
   // ---- workgroup -> (channel group, pixel group); XCD-local channel groups ----
   const int b = blockIdx.x, G = gridDim.x;
@@ -92,6 +98,8 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     *reinterpret_cast<uint4*>(wfr + (((n >> 4) * KT + kb) * 64 + (n & 15) + 16 * q) * 16) = v;
   }
   for (int c = tid; c < 2 * NP; c += NT) ssum[c] = 0.f;
+  if constexpr (PRO)
+    for (int c = tid; c < 3 * K; c += NT) pco[c] = bs.pro_coef[c];
   __syncthreads();
 
   const bool bnsum = EPI == 2 && bs.sums != nullptr && !bs.zgelu;
@@ -121,7 +129,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   const int gw = mg * PW_NW + w, GW = MG * PW_NW;
 
   // A fragments of tile t: lane -> pixel row t*TPM + 16 j + fr, k-chunk kb*32 + 8 fq
-  auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT]) {
+  // (PRO: the unit's pre-BN output y at the same positions into yf)
+  constexpr int YJ = PRO ? MJ : 1, YK = PRO ? KT : 1;
+  auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT], bf16x8 (&yf)[YJ][YK]) {
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
       int row = t * TPM + 16 * j + fr;
@@ -129,6 +139,48 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
       const bf16_t* src = A + (size_t)row * K + 8 * fq;
 #pragma unroll
       for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
+      if constexpr (PRO) {
+        const bf16_t* ys = reinterpret_cast<const bf16_t*>(bs.pro_y) + (size_t)row * K + 8 * fq;
+#pragma unroll
+        for (int kb = 0; kb < KT; ++kb) yf[j][kb] = *reinterpret_cast<const bf16x8*>(ys + kb * 32);
+      }
+    }
+  };
+  // PRO: dy = A g + B y + Cc in place of g (and, channel group 0, stored for the weight gradient)
+  auto prologue = [&](int t, bf16x8 (&af)[MJ][KT], const bf16x8 (&yf)[YJ][YK]) {
+    if constexpr (PRO) {
+      // the coefficient reads are loop-invariant: hoisted out of the tile loop they would pin
+      // 24 * KT registers for the whole kernel. The empty clobber keeps them per chunk.
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int j = 0; j < MJ; ++j) {
+        const int row = t * TPM + 16 * j + fr;
+        const bool st = g == 0 && bs.pro_dy != nullptr && row < p.M;
+#pragma unroll
+        for (int kb = 0; kb < KT; ++kb) {
+          const int k0 = kb * 32 + 8 * fq;
+          const uint4 gu = __builtin_bit_cast(uint4, af[j][kb]), yu = __builtin_bit_cast(uint4, yf[j][kb]);
+          const uint32_t gw4[4] = {gu.x, gu.y, gu.z, gu.w}, yw4[4] = {yu.x, yu.y, yu.z, yu.w};
+          uint32_t ow[4];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {   // 4 channels at a time: 12 coefficient registers live
+            const float4 a4 = *reinterpret_cast<const float4*>(pco + k0 + 4 * h);
+            const float4 b4 = *reinterpret_cast<const float4*>(pco + K + k0 + 4 * h);
+            const float4 c4 = *reinterpret_cast<const float4*>(pco + 2 * K + k0 + 4 * h);
+            const uint32_t g0 = gw4[2 * h], g1 = gw4[2 * h + 1], y0 = yw4[2 * h], y1 = yw4[2 * h + 1];
+            const float o0 = a4.x * __uint_as_float(g0 << 16) + b4.x * __uint_as_float(y0 << 16) + c4.x;
+            const float o1 = a4.y * __uint_as_float(g0 & 0xffff0000u) + b4.y * __uint_as_float(y0 & 0xffff0000u) + c4.y;
+            const float o2 = a4.z * __uint_as_float(g1 << 16) + b4.z * __uint_as_float(y1 << 16) + c4.z;
+            const float o3 = a4.w * __uint_as_float(g1 & 0xffff0000u) + b4.w * __uint_as_float(y1 & 0xffff0000u) + c4.w;
+            ow[2 * h] = pack2bf(o0, o1);
+            ow[2 * h + 1] = pack2bf(o2, o3);
+          }
+          const uint4 pk = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+          af[j][kb] = __builtin_bit_cast(bf16x8, pk);
+          if (st) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(bs.pro_dy) + (size_t)row * K + k0) = pk;
+          __builtin_amdgcn_sched_barrier(0);   // one chunk's coefficients live at a time
+        }
+      }
     }
   };
   auto wsync = [&]() {
@@ -137,7 +189,8 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  auto process = [&](int t, bf16x8 (&cur)[MJ][KT], bf16x8 (&nxt)[MJ][KT]) {
+  auto process = [&](int t, bf16x8 (&cur)[MJ][KT], bf16x8 (&nxt)[MJ][KT], bf16x8 (&ycur)[YJ][YK],
+                     bf16x8 (&ynxt)[YJ][YK]) {
     // (1) epilogue operands of THIS tile first (in-order vmcnt: they must not queue behind the prefetch)
     uint4 ey[MJ][HP], er[MJ][HP];
     unsigned em[MJ][HP];
@@ -156,8 +209,11 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
         }
     }
     // (2) prefetch the next tile of this wave
+    // PRO: this tile's dy first (its g / y registers die before the next tile's are in flight)
+    prologue(t, cur, ycur);
+    if constexpr (PRO) __builtin_amdgcn_sched_barrier(0);
     const int tn = t + GW;
-    if (tn < ntiles) load_tile(tn, nxt);
+    if (tn < ntiles) load_tile(tn, nxt, ynxt);
 
     // (3) MFMAs: D[channel][pixel] = W . A^T; weight fragments double-buffered one k-block ahead,
     //     the scheduling fence per k-block keeps hipcc from hoisting every ds_read of the tile
@@ -237,11 +293,12 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   };
 
   bf16x8 fa[MJ][KT], fb[MJ][KT];
+  bf16x8 ya[YJ][YK], yb[YJ][YK];
   int t = gw;
-  if (t < ntiles) load_tile(t, fa);
+  if (t < ntiles) load_tile(t, fa, ya);
   for (; t < ntiles; t += 2 * GW) {
-    process(t, fa, fb);
-    if (t + GW < ntiles) process(t + GW, fb, fa);
+    process(t, fa, fb, ya, yb);
+    if (t + GW < ntiles) process(t + GW, fb, fa, yb, ya);
   }
 
   if (!want) return;
@@ -287,14 +344,16 @@ static int pw_ncu() {
   return ncu;
 }
 
-// group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave
-static size_t pw_smem(int NP, int K) { return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4; }
+// group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave (+ PRO: [3][K] coefficients)
+static size_t pw_smem(int NP, int K, bool pro) {
+  return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4 + (pro ? (size_t)3 * K * 4 : 0);
+}
 
-template <int NP, int TPM, int KT, int EPI>
+template <int NP, int TPM, int KT, int EPI, bool PRO>
 static hipError_t pw_launch(const ConvGeom& g, const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* resid,
                             float* stats, const BwdStats& bs, hipStream_t st) {
-  auto kfn = &pw_kernel<NP, TPM, KT, EPI>;
-  const size_t smem = pw_smem(NP, KT * 32);
+  auto kfn = &pw_kernel<NP, TPM, KT, EPI, PRO>;
+  const size_t smem = pw_smem(NP, KT * 32, PRO);
   static int per_cu = 0;
   if (per_cu == 0) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -320,12 +379,15 @@ static hipError_t pw_launch(const ConvGeom& g, const bf16_t* X, const bf16_t* W,
 
 // (NP, K) -> TPM: 32 while the double-buffered activation fragments plus the accumulators stay
 // within ~96 VGPRs, else 16 (no scratch spills at 2 waves / SIMD)
-template <int EPI>
+template <int EPI, bool PRO>
 static hipError_t pw_dispatch(const ConvGeom& g, int NP, const bf16_t* X, const bf16_t* W, bf16_t* Y,
                               const bf16_t* resid, float* stats, const BwdStats& bs, hipStream_t st) {
   const int K = g.Ktot;
-#define PW_CASE(np, k, TPM) \
-  if (NP == np && K == k) return pw_launch<np, TPM, k / 32, EPI>(g, X, W, Y, resid, stats, bs, st);
+  if (PRO && K > 256) return hipErrorNotSupported;   // operand + y fragments: K <= 256 in registers
+#define PW_CASE(np, k, TPM)                                                                    \
+  if constexpr (!PRO || (k) <= 256) {                                                          \
+    if (NP == np && K == k) return pw_launch<np, TPM, k / 32, EPI, PRO>(g, X, W, Y, resid, stats, bs, st); \
+  }
   PW_CASE(64, 64, 32)
   PW_CASE(64, 128, 32)
   PW_CASE(64, 256, 16)
@@ -365,6 +427,8 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
   // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
   if (route == 1 && g->Ktot > 256) return 0;
+  // the BN-backward prologue keeps operand and y fragments of a K <= 256 tile in registers
+  if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
 }
 
@@ -373,7 +437,10 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   const int NP = pw_np(g->K, g->Ktot);
   if (epi == 1)
-    return pw_dispatch<1>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
-  return pw_dispatch<2>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr, bs,
-                        st);
+    return pw_dispatch<1, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
+  if (bs.pro_y)
+    return pw_dispatch<2, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr,
+                                bs, st);
+  return pw_dispatch<2, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr,
+                               bs, st);
 }

@@ -132,6 +132,12 @@ hipError_t zoo_dropout_add(const void*, const void*, void*, size_t, float, uint6
 hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_nhwc_u8_to_s2d(const void*, void*, int, int, int, int, int, int, int, const float*, const float*,
                               hipStream_t);
+hipError_t zoo_bnfold_coef(int, const float*, const float*, const float*, const float*, long long, float*, float*,
+                           float*, hipStream_t);
+hipError_t zoo_bnpro_apply(const void*, const void*, const float*, void*, size_t, int, hipStream_t);
+hipError_t zoo_convlstm_step(const void*, const void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
+                             const float*, const float*, float*, float*, float*, void*, int, const float*,
+                             const float*, float*, int, float*, void*, int, int, hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
 hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, hipStream_t);
@@ -254,6 +260,8 @@ ConvGeom make_geom(const torch::Tensor& x, int K, int R, int S, int sh, int sw, 
   return g;
 }
 
+static void check_al16(const void* p, const char* what);
+
 // x: [N,H,W,C] bf16; w: [K, ldb] bf16 (logical [K][R][S][C] rows, zero padded to ldb)
 torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
                        int lh, int lw, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
@@ -262,7 +270,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bz, c10::optional<torch::Tensor> by,
                        c10::optional<torch::Tensor> bmean, c10::optional<torch::Tensor> binv,
                        c10::optional<torch::Tensor> bsums, c10::optional<torch::Tensor> bgamma,
-                       c10::optional<torch::Tensor> bbeta) {
+                       c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
+                       c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -367,6 +376,26 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   }
   static const bool epi2_unbatched = !env_flag("ZOO_EPI2_BATCH", true);
   bs.unbatched = epi2_unbatched ? 1 : 0;
+  // BN-backward prologue: x is a unit's masked output gradient g; the GEMM operand is that unit's
+  // BN backward dy = A g + B pro_y + Cc (pw.hip forms it in registers and writes pro_dy); kernels
+  // without the prologue get dy materialised first (into pro_dy when given)
+  torch::Tensor xin = x;
+  if (pro_y.has_value() && pro_y->defined()) {
+    req(*pro_y, at::kBFloat16, "pro_y");
+    TORCH_CHECK(pro_coef.has_value() && pro_coef->defined(), "conv_fwd: the BN-backward prologue needs pro_coef");
+    req(*pro_coef, at::kFloat, "pro_coef");
+    TORCH_CHECK(pro_y->numel() == x.numel() && pro_coef->numel() == 3 * (int64_t)C,
+                "conv_fwd: pro_y must match x, pro_coef must be [3 * C]");
+    if (pro_dy.has_value() && pro_dy->defined()) {
+      req(*pro_dy, at::kBFloat16, "pro_dy");
+      TORCH_CHECK(pro_dy->numel() == x.numel(), "conv_fwd: pro_dy must match x");
+      check_al16(pro_dy->data_ptr(), "pro_dy");
+    }
+    check_al16(pro_y->data_ptr(), "pro_y");
+    bs.pro_y = pro_y->data_ptr();
+    bs.pro_coef = pro_coef->data_ptr<float>();
+    bs.pro_dy = opt_ptr<void>(pro_dy);
+  }
   // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
   // they are folded in order into the caller's buffer (its first 2K floats)
   float* const stat_dst = sp ? sp : bs.sums;
@@ -395,6 +424,19 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     if (sp) sp = part.data_ptr<float>();
     else bs.sums = part.data_ptr<float>();
   }
+  // the prologue runs only in pw.hip; any other kernel (including pw with the deterministic
+  // partial statistics decided above) gets dy materialised first
+  if (bs.pro_y) {
+    if (!zoo_pw_eligible(&g, route, &bs)) {
+      xin = (pro_dy.has_value() && pro_dy->defined()) ? *pro_dy : torch::empty_like(x);
+      check_hip(zoo_bnpro_apply(x.data_ptr(), pro_y->data_ptr(), bs.pro_coef, xin.data_ptr(), x.numel(), C,
+                                cur_stream()),
+                "bnpro_apply");
+      bs.pro_y = nullptr;
+      bs.pro_coef = nullptr;
+      bs.pro_dy = nullptr;
+    }
+  }
   torch::Tensor y, yf;
   if (out.has_value() && out->defined()) {
     TORCH_CHECK(out_bf16 && !out_f32, "conv_fwd: explicit output must be bf16");
@@ -406,7 +448,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     if (out_bf16) y = torch::empty({g.N, g.P, g.Q, K}, x.options());
   }
   if (out_f32) yf = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(at::kFloat));
-  check_hip(zoo_igemm(x.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
+  check_hip(zoo_igemm(xin.data_ptr(), w.data_ptr(), out_bf16 ? y.data_ptr() : nullptr,
                       out_f32 ? yf.data_ptr<float>() : nullptr, bp, rp, sp, &g, act, &bs, cur_stream()),
             "igemm");
   if (g.stat_slots == zoo::kStatPartial) fold_partials(stat_dst, part, 2 * K, tiles_m);
@@ -1454,6 +1496,148 @@ void lstm_step_bwd(c10::optional<torch::Tensor> dout, c10::optional<torch::Tenso
             "lstm_step_bwd");
 }
 
+// One ConvLSTM2D step per launch (kernels/convlstm.hip), gate-interleaved layout (column 4j + g).
+// x: the step's conv input [B][D][H][W][Cx] bf16 (ConvLSTM2D: [B][H][W][Cx], D = Q = 1; None: no
+// recurrent term); wt: packed weights [rows][>= Q*R*S*Cx] -- forward the 4F gate rows, backward the
+// flipped weight (rows = hidden channels).
+static void convlstm_geom(const c10::optional<torch::Tensor>& x, const torch::Tensor& wt, int B, int D, int H, int W,
+                          int Q, int R, int S, int rows_min, int* Cx) {
+  req(wt, at::kBFloat16, "wt");
+  TORCH_CHECK(wt.dim() == 2 && wt.size(0) >= rows_min && wt.size(0) <= 256 && wt.size(1) % 8 == 0,
+              "convlstm: packed weight [rows <= 256][ldw % 8 == 0]");
+  TORCH_CHECK(Q % 2 == 1 && R % 2 == 1 && S % 2 == 1 && D >= 1, "convlstm: odd (same-padded) kernels");
+  *Cx = 0;
+  if (x.has_value() && x->defined()) {
+    req(*x, at::kBFloat16, "x");
+    const int64_t C = x->size(-1);
+    TORCH_CHECK(C % 8 == 0 && x->size(0) == B && x->numel() == (int64_t)B * D * H * W * C,
+                "convlstm: x [B, (D,) H, W, Cx % 8 == 0]");
+    *Cx = C;
+    TORCH_CHECK(wt.size(1) >= (int64_t)Q * R * S * *Cx, "convlstm: weight row shorter than Q*R*S*Cx");
+    check_al16(x->data_ptr(), "convlstm x");
+    check_al16(wt.data_ptr(), "convlstm wt");
+  }
+}
+
+void convlstm_fwd_step(c10::optional<torch::Tensor> x, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W,
+                       int64_t Q, int64_t R, int64_t S, torch::Tensor gx, c10::optional<torch::Tensor> cprev, torch::Tensor h,
+                       torch::Tensor c, torch::Tensor acts, torch::Tensor hb, int64_t iact, int64_t act) {
+  const int64_t M = B * D * H * W;
+  req(gx, at::kFloat, "gx"); req(h, at::kFloat, "h"); req(c, at::kFloat, "c"); req(acts, at::kFloat, "acts");
+  req(hb, at::kBFloat16, "hb");
+  TORCH_CHECK(M > 0 && gx.numel() % (4 * M) == 0, "convlstm_fwd: gx [M, F, 4]");
+  const int64_t F = gx.numel() / (4 * M);
+  TORCH_CHECK(h.numel() == M * F && c.numel() == M * F && acts.numel() == 4 * M * F, "convlstm_fwd: outputs");
+  TORCH_CHECK(hb.numel() % M == 0 && hb.numel() / M >= F, "convlstm_fwd: hb [M, >= F]");
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "convlstm: activation code");
+  int Cx;
+  convlstm_geom(x, wt, B, D, H, W, Q, R, S, 4 * F, &Cx);
+  const float* cp = nullptr;
+  if (cprev.has_value() && cprev->defined()) {
+    req(*cprev, at::kFloat, "cprev");
+    TORCH_CHECK(cprev->numel() == M * F, "convlstm_fwd: c_prev [M, F]");
+    cp = cprev->data_ptr<float>();
+  }
+  check_hip(zoo_convlstm_step(opt_ptr<void>(x), wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1), 4 * F, F, iact, act,
+                              gx.data_ptr<float>(), cp, h.data_ptr<float>(), c.data_ptr<float>(),
+                              acts.data_ptr<float>(), hb.data_ptr(), hb.numel() / M, nullptr, nullptr, nullptr, 0,
+                              nullptr, nullptr, 0, 0, cur_stream()),
+            "convlstm_fwd_step");
+}
+
+void convlstm_bwd_step(c10::optional<torch::Tensor> x, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W,
+                       int64_t Q, int64_t R, int64_t S, c10::optional<torch::Tensor> dout, torch::Tensor acts,
+                       c10::optional<torch::Tensor> cprev, torch::Tensor cc, torch::Tensor dc, bool dc_in,
+                       torch::Tensor dg, torch::Tensor dgb, int64_t iact, int64_t act) {
+  const int64_t M = B * D * H * W;
+  req(acts, at::kFloat, "acts"); req(cc, at::kFloat, "c"); req(dc, at::kFloat, "dc"); req(dg, at::kFloat, "dg");
+  req(dgb, at::kBFloat16, "dgb");
+  TORCH_CHECK(M > 0 && acts.numel() % (4 * M) == 0, "convlstm_bwd: acts [M, F, 4]");
+  const int64_t F = acts.numel() / (4 * M);
+  TORCH_CHECK(cc.numel() == M * F && dc.numel() == M * F && dg.numel() == 4 * M * F, "convlstm_bwd: sizes");
+  TORCH_CHECK(dgb.numel() % M == 0 && dgb.numel() / M >= 4 * F && (dgb.numel() / M) % 4 == 0,
+              "convlstm_bwd: dgb [M, >= 4F, % 4]");
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "convlstm: activation code");
+  int Cx;
+  convlstm_geom(x, wt, B, D, H, W, Q, R, S, F, &Cx);
+  auto opt = [&](const c10::optional<torch::Tensor>& t, const char* n) -> const float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    req(*t, at::kFloat, n);
+    TORCH_CHECK(t->numel() == M * F, "convlstm_bwd: ", n, " [M, F]");
+    return t->data_ptr<float>();
+  };
+  check_hip(zoo_convlstm_step(opt_ptr<void>(x), wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1), wt.size(0), F, iact,
+                              act, nullptr, opt(cprev, "cprev"), nullptr, nullptr, acts.data_ptr<float>(), nullptr, 0,
+                              opt(dout, "dout"), cc.data_ptr<float>(), dc.data_ptr<float>(), dc_in ? 1 : 0,
+                              dg.data_ptr<float>(), dgb.data_ptr(), dgb.numel() / M, 1, cur_stream()),
+            "convlstm_bwd_step");
+}
+
+// Whole ConvLSTM sequences: the step loop in C++ (T launches each way, no per-step Python view /
+// binding overhead -- at T = 32 that overhead, not the kernels, bounded the step). Sequence buffers
+// are time-major: gxs / acts / dgxs [T][M][F][4], hist [T+1][M][cph] (slot 0 zero), hseq / cseq
+// [T][M][F], dgb [T][M][K8]; dout [T][M][F] (rseq) or [M][F] (last step only).
+void convlstm_fwd_seq(torch::Tensor gxs, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W, int64_t Q,
+                      int64_t R, int64_t S, torch::Tensor hist, torch::Tensor hseq, torch::Tensor cseq,
+                      torch::Tensor acts, int64_t iact, int64_t act) {
+  req(gxs, at::kFloat, "gxs"); req(hist, at::kBFloat16, "hist"); req(hseq, at::kFloat, "hseq");
+  req(cseq, at::kFloat, "cseq"); req(acts, at::kFloat, "acts");
+  const int64_t M = B * D * H * W, T = gxs.size(0);
+  TORCH_CHECK(T > 0 && M > 0 && gxs.numel() % (4 * M * T) == 0, "convlstm_fwd_seq: gxs [T, M, F, 4]");
+  const int64_t F = gxs.numel() / (4 * M * T);
+  TORCH_CHECK(hseq.numel() == T * M * F && cseq.numel() == T * M * F && acts.numel() == 4 * T * M * F,
+              "convlstm_fwd_seq: hseq / cseq / acts sizes");
+  TORCH_CHECK(hist.size(0) == T + 1 && hist.numel() % ((T + 1) * M) == 0, "convlstm_fwd_seq: hist [T + 1, M, cph]");
+  const int64_t cph = hist.numel() / ((T + 1) * M);
+  TORCH_CHECK(cph % 8 == 0 && cph >= F, "convlstm_fwd_seq: hist channels");
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "convlstm: activation code");
+  auto x0 = hist[0].view({B, D * H, W, cph});
+  int Cx;
+  convlstm_geom(c10::optional<torch::Tensor>(x0), wt, B, D, H, W, Q, R, S, 4 * F, &Cx);
+  const uint16_t* hp = reinterpret_cast<const uint16_t*>(hist.data_ptr());
+  float* cs = cseq.data_ptr<float>();
+  for (int64_t s = 0; s < T; ++s) {
+    check_hip(zoo_convlstm_step(s > 0 ? hp + s * M * cph : nullptr, wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1),
+                                4 * F, F, iact, act, gxs.data_ptr<float>() + s * M * 4 * F,
+                                s > 0 ? cs + (s - 1) * M * F : nullptr, hseq.data_ptr<float>() + s * M * F,
+                                cs + s * M * F, acts.data_ptr<float>() + s * M * 4 * F,
+                                const_cast<uint16_t*>(hp) + (s + 1) * M * cph, cph, nullptr, nullptr, nullptr, 0,
+                                nullptr, nullptr, 0, 0, cur_stream()),
+              "convlstm_fwd_seq");
+  }
+}
+
+void convlstm_bwd_seq(torch::Tensor dout, bool rseq, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W,
+                      int64_t Q, int64_t R, int64_t S, torch::Tensor acts, torch::Tensor cseq, torch::Tensor dc,
+                      torch::Tensor dgxs, torch::Tensor dgb, int64_t iact, int64_t act) {
+  req(dout, at::kFloat, "dout"); req(acts, at::kFloat, "acts"); req(cseq, at::kFloat, "cseq");
+  req(dc, at::kFloat, "dc"); req(dgxs, at::kFloat, "dgxs"); req(dgb, at::kBFloat16, "dgb");
+  const int64_t M = B * D * H * W, T = acts.size(0);
+  TORCH_CHECK(T > 0 && M > 0 && acts.numel() % (4 * M * T) == 0, "convlstm_bwd_seq: acts [T, M, F, 4]");
+  const int64_t F = acts.numel() / (4 * M * T);
+  TORCH_CHECK(cseq.numel() == T * M * F && dc.numel() == M * F && dgxs.numel() == 4 * T * M * F,
+              "convlstm_bwd_seq: sizes");
+  TORCH_CHECK(dout.numel() == (rseq ? T : 1) * M * F, "convlstm_bwd_seq: dout [T, M, F] or [M, F]");
+  TORCH_CHECK(dgb.size(0) == T && dgb.numel() % (T * M) == 0, "convlstm_bwd_seq: dgb [T, M, K8]");
+  const int64_t K8 = dgb.numel() / (T * M);
+  TORCH_CHECK(K8 % 8 == 0 && K8 >= 4 * F, "convlstm_bwd_seq: dgb channels");
+  TORCH_CHECK(iact >= 0 && iact <= 4 && act >= 0 && act <= 4, "convlstm: activation code");
+  auto x0 = dgb[0].view({B, D * H, W, K8});
+  int Cx;
+  convlstm_geom(c10::optional<torch::Tensor>(x0), wt, B, D, H, W, Q, R, S, F, &Cx);
+  uint16_t* gb = reinterpret_cast<uint16_t*>(dgb.data_ptr());
+  const float* cs = cseq.data_ptr<float>();
+  for (int64_t s = T - 1; s >= 0; --s) {
+    const float* d = rseq ? dout.data_ptr<float>() + s * M * F : (s == T - 1 ? dout.data_ptr<float>() : nullptr);
+    check_hip(zoo_convlstm_step(s < T - 1 ? gb + (s + 1) * M * K8 : nullptr, wt.data_ptr(), B, D, H, W, Cx, Q, R, S,
+                                wt.size(1), wt.size(0), F, iact, act, nullptr, s > 0 ? cs + (s - 1) * M * F : nullptr,
+                                nullptr, nullptr, acts.data_ptr<float>() + s * M * 4 * F, nullptr, 0, d,
+                                cs + s * M * F, dc.data_ptr<float>(), s < T - 1 ? 1 : 0,
+                                dgxs.data_ptr<float>() + s * M * 4 * F, gb + s * M * K8, K8, 1, cur_stream()),
+              "convlstm_bwd_seq");
+  }
+}
+
 // Max RoI pooling (Faster R-CNN): features NHWC, rois [R, 5] fp32 -> (out [R, PH, PW, C], argmax int32)
 std::vector<torch::Tensor> roi_pool_fwd(torch::Tensor f, torch::Tensor rois, int PH, int PW, double scale) {
   req_act(f, "roi_pool");
@@ -1708,6 +1892,45 @@ torch::Tensor nhwc_u8_to_s2d(torch::Tensor x, int pad, std::vector<double> scale
   check_hip(zoo_nhwc_u8_to_s2d(x.data_ptr(), y.data_ptr(), N, C, H, W, pad, Hs, Ws, sc, sh, cur_stream()),
             "nhwc_u8_to_s2d");
   return y;
+}
+
+// BatchNorm-backward prologue (kernels/bnfold.hip, pw.hip PRO). Coefficients of a unit's BN
+// backward dy = A g + B y + Cc from its final sums [0, 2K) (sum g, sum g * xhat) over M rows:
+// returns coef [3K] = A | B | Cc; dgamma += S2, dbeta += S1 when given.
+torch::Tensor bnfold_coef(torch::Tensor gamma, torch::Tensor mean, torch::Tensor inv, torch::Tensor sums, int64_t M,
+                          c10::optional<torch::Tensor> dgamma, c10::optional<torch::Tensor> dbeta) {
+  req(gamma, at::kFloat, "gamma");
+  req(mean, at::kFloat, "mean");
+  req(inv, at::kFloat, "inv");
+  req(sums, at::kFloat, "sums");
+  const int64_t K = gamma.numel();
+  TORCH_CHECK(K > 0 && mean.numel() == K && inv.numel() == K && sums.numel() >= 2 * K && M > 0,
+              "bnfold_coef: per-channel vectors of length K, sums >= 2K");
+  for (auto* t : {&dgamma, &dbeta})
+    if (t->has_value()) {
+      req(**t, at::kFloat, "dgamma/dbeta");
+      TORCH_CHECK((*t)->numel() == K, "bnfold_coef: dgamma / dbeta length");
+    }
+  auto coef = torch::empty({3 * K}, gamma.options());
+  check_hip(zoo_bnfold_coef((int)K, gamma.data_ptr<float>(), mean.data_ptr<float>(), inv.data_ptr<float>(),
+                            sums.data_ptr<float>(), (long long)M, coef.data_ptr<float>(), opt_ptr<float>(dgamma),
+                            opt_ptr<float>(dbeta), cur_stream()),
+            "bnfold_coef");
+  return coef;
+}
+
+// dy = A g + B y + Cc materialised ([..., K] bf16, K % 8 == 0)
+void bnpro_apply(torch::Tensor g, torch::Tensor y, torch::Tensor coef, torch::Tensor out) {
+  req(g, at::kBFloat16, "g");
+  req(y, at::kBFloat16, "y");
+  req(coef, at::kFloat, "coef");
+  req(out, at::kBFloat16, "out");
+  const int64_t K = g.size(-1);
+  TORCH_CHECK(K % 8 == 0 && y.numel() == g.numel() && out.numel() == g.numel() && coef.numel() == 3 * K,
+              "bnpro_apply: g / y / out [..., K % 8 == 0], coef [3K]");
+  check_hip(zoo_bnpro_apply(g.data_ptr(), y.data_ptr(), coef.data_ptr<float>(), out.data_ptr(), g.numel(), (int)K,
+                            cur_stream()),
+            "bnpro_apply");
 }
 
 torch::Tensor nchw_to_nhwc(torch::Tensor x, int cpad) {
@@ -2846,7 +3069,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("jpeg_color_resize", &jpeg_color_resize);
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
-        py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none());
+        py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
+        py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none());
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
@@ -2891,6 +3115,10 @@ PYBIND11_MODULE(_C, m) {
   m.def("lstm_gates_bwd", &lstm_gates_bwd);
   m.def("lstm_step_fwd", &lstm_step_fwd);
   m.def("lstm_step_bwd", &lstm_step_bwd);
+  m.def("convlstm_fwd_step", &convlstm_fwd_step);
+  m.def("convlstm_bwd_step", &convlstm_bwd_step);
+  m.def("convlstm_fwd_seq", &convlstm_fwd_seq);
+  m.def("convlstm_bwd_seq", &convlstm_bwd_seq);
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
@@ -2926,6 +3154,8 @@ PYBIND11_MODULE(_C, m) {
         py::arg("momentum"), py::arg("relu"), py::arg("training"),
         py::arg("resid_bn") = std::vector<c10::optional<torch::Tensor>>(), py::arg("mask") = py::none());
   m.def("bn_bwd_apply", &bn_bwd_apply);
+  m.def("bnfold_coef", &bnfold_coef);
+  m.def("bnpro_apply", &bnpro_apply);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_relu_maxpool_fwd", &bn_relu_maxpool_fwd);

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""ConvLSTM2D forward+backward time: the whole-sequence native path (_ConvLSTMSeqFn: one
-recurrent conv + one fused step kernel per step forward, three launches per step backward)
-against the per-step autograd loop it replaced, and their numerical agreement.
+"""ConvLSTM2D forward+backward time: the one-launch-per-step path (_ConvLSTMFusedFn,
+convlstm.hip), the whole-sequence path (_ConvLSTMSeqFn: recurrent conv + step kernel forward,
+three launches per step backward) and the per-step autograd loop, and their agreement.
 
   python tools/convlstm_bench.py [--T 32] [--batch 8] [--hw 32] [--cin 16] [--filters 32]"""
 import argparse
@@ -32,8 +32,10 @@ def main():
     res = {"bench": "convlstm2d-fwd-bwd", "T": a.T, "batch": a.batch, "hw": a.hw, "cin": a.cin,
            "filters": a.filters}
     outs = {}
-    for mode in (0, 1):
-        R._CONVLSTM_SEQ = bool(mode)
+    names = {0: "loop", 1: "seq", 2: "fused"}
+    for mode in (0, 1, 2):
+        R._CONVLSTM_SEQ = mode > 0
+        R._CONVLSTM_FUSED = mode == 2
 
         def step():
             x.grad = None
@@ -50,12 +52,15 @@ def main():
             y = step()
         torch.cuda.synchronize()
         ms = (time.perf_counter() - t0) / a.iters * 1e3
-        res["ms_%s" % ("seq" if mode else "loop")] = round(ms, 3)
+        res["ms_%s" % names[mode]] = round(ms, 3)
         outs[mode] = (y.detach().float(), x.grad.detach().clone(), layer.Wh.grad.detach().clone())
-    res["speedup"] = round(res["ms_loop"] / res["ms_seq"], 2)
-    for k, n in enumerate(("y", "dx", "dWh")):
-        a0, a1 = outs[0][k], outs[1][k]
-        res["rel_%s" % n] = round(float((a0 - a1).abs().max() / a0.abs().max().clamp_min(1e-12)), 5)
+    res["speedup_seq"] = round(res["ms_loop"] / res["ms_seq"], 2)
+    res["speedup"] = round(res["ms_loop"] / res["ms_fused"], 2)
+    for mode in (1, 2):
+        for k, n in enumerate(("y", "dx", "dWh")):
+            a0, a1 = outs[0][k], outs[mode][k]
+            res["rel_%s_%s" % (names[mode], n)] = round(float((a0 - a1).abs().max() /
+                                                              a0.abs().max().clamp_min(1e-12)), 5)
     print(json.dumps(res), flush=True)
 
 

@@ -20,19 +20,23 @@ from zoo.ops._native import native
 
 
 def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
-             act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None):
+             act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None, pro=None):
     """``bstats = (z or None, y, mean, inv, sums[, gamma, beta])`` fuses the producing unit's
     BN-backward reduction (and ReLU mask) into this conv's epilogue. The mask source: a bf16
     ``z`` (ReLU output), a uint8 ``z`` (1-bit mask of the forward apply), or -- z None and
-    gamma given -- recomputed from ``y`` with the unit's affine (csrc/kernels/bnmask.h)."""
+    gamma given -- recomputed from ``y`` with the unit's affine (csrc/kernels/bnmask.h).
+    ``pro = (y, coef, dy_out or None)``: ``x`` is a unit's masked output gradient g and the GEMM
+    runs on that unit's BN backward dy = A g + B y + Cc instead (the BN-backward prologue,
+    csrc/kernels/bnfold.hip); dy is written to ``dy_out``."""
     bz = by = bm = bi = bsum = bg = bb = None
     if bstats is not None:
         bz, by, bm, bi, bsum = bstats[:5]
         if len(bstats) > 5:
             bg, bb = bstats[5], bstats[6]
+    py, pc, pd = pro if pro is not None else (None, None, None)
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
-                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb)
+                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd)
 
 
 # ---------------------------------------------------------------------------
@@ -175,20 +179,24 @@ def _fault(dx):
 
 
 def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None,
-               resid_inplace=False):
+               resid_inplace=False, pro=None):
     """dX [N,H,W,C] of y = conv(x, w) given dY [N,P,Q,K] and the bf16 packed weight.
     ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer).
     ``resid_inplace``: ``resid`` is a temporary the caller gives away; strided dgrads
-    with tap-less parity classes accumulate into it instead of a copy of it."""
-    return _fault(_conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace))
+    with tap-less parity classes accumulate into it instead of a copy of it.
+    ``pro``: the BN-backward prologue of :func:`conv_fwd` (stride-1 dgrads; ``dy`` is then the
+    masked gradient g of this conv's own BN unit)."""
+    return _fault(_conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro))
 
 
-def _conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace):
+def _conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro=None):
     sh, sw = stride
+    if pro is not None and not ((sh, sw) == (1, 1) or dil != (1, 1)):
+        raise ValueError("conv_dgrad: the BN-backward prologue needs a stride-1 dgrad")
     if (sh, sw) == (1, 1) or dil != (1, 1):
         wt = flip_weights(wb, K, R, S, C)
         return conv_fwd(dy, wt, R, S, (1, 1), (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1]), dil, stride,
-                        resid=resid, out_hw=(H, W), bstats=bstats)
+                        resid=resid, out_hw=(H, W), bstats=bstats, pro=pro)
     N = dy.shape[0]
     classes = []
     for a in range(sh):

@@ -20,7 +20,7 @@ import torch.nn.functional as F
 
 from zoo.ops._native import native
 from zoo.ops import _kern, workspace, wstream
-from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref, ref_storage
+from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref, ref_relu, ref_storage
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
 from zoo.parallel.flat import grad_slot
 
@@ -33,6 +33,21 @@ STAT_SLOTS = 16
 # csrc/kernels/bnmask.h): 1 = recompute it from y (no residual) or read a 1-bit mask written by
 # the forward apply (residual units); 0 = re-read the bf16 ReLU output z (A/B comparator).
 _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
+
+
+# BatchNorm backward of a 1x1 / stride-1 conv -> BN unit as a PROLOGUE of its own dgrad
+# (csrc/kernels/bnfold.hip, pw.hip PRO): when the consumer already produced the masked gradient g
+# and its sums, dy = A g + B y + Cc is formed in the dgrad kernel's operand registers from g and
+# the unit's y, and written once for the weight gradient -- no separate BN-backward pass and no
+# re-read of dy (6 instead of 8 bytes per element). Shapes the prologue kernel does not take get
+# dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B comparator).
+_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
+
+
+def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
+    return (_BN_FOLD[0] and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
+            and not getattr(ctx, "sync", False) and K % 8 == 0 and gamma.dtype == torch.float32
+            and gamma.is_contiguous())
 
 
 def stat_len(c):
@@ -176,12 +191,19 @@ class _ConvBNActFn(torch.autograd.Function):
         dgam, own_g = _grad_target(gamma)
         dbet, own_b = _grad_target(ctx.beta_ref) if hasattr(ctx, "beta_ref") else (None, False)
         po = ctx.producer_out
+        fold = None
         if po is not None and po.fused:
             # dz arrived already ReLU-masked with its (dy, dy*xhat) sums from the consumer's epilogue
             sums = po.sums
-            dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
-            outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dg, db)
-            dy = outs[0]
+            if _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
+                # the BN backward runs as the dgrad's prologue (see _BN_FOLD); dy is its by-product
+                coef = C_.bnfold_coef(gamma.detach(), smean, sinv, sums, y.numel() // K, dgam, dbet)
+                dy = torch.empty_like(dz)
+                fold = (y, coef, dy)
+            else:
+                dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
+                outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dg, db)
+                dy = outs[0]
             dresid = dz if has_resid else None
             po.release()
         else:
@@ -208,12 +230,15 @@ class _ConvBNActFn(torch.autograd.Function):
             pin = ctx.producer_in
             bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
             # a handed-off gradient is a temporary owned by this unit now: accumulate into it in place
-            dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, Cin, xshape[1], xshape[2], stride, pad, resid=add,
-                                  bstats=bst, resid_inplace=add is not None)
+            dx = _kern.conv_dgrad(dz if fold is not None else dy, bf16_weight(w), K, R, S, Cin, xshape[1],
+                                  xshape[2], stride, pad, resid=add, bstats=bst, resid_inplace=add is not None,
+                                  pro=fold)
             if ctx.dx_out is not None:
                 # another consumer of x adds this gradient in its own dgrad epilogue
                 ctx.dx_out.grad = dx
                 dx = None
+        elif fold is not None:
+            C_.bnpro_apply(dz, fold[0], fold[1], dy)   # no data gradient: dy for the wgrad alone
         gw, own_w = _grad_target(w)
         with wstream.wgrad(dy.device, x, dy, on=own_w):
             C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
@@ -442,7 +467,7 @@ def conv_bn_act(x, w, gamma, beta, running_mean, running_var, kernel=(1, 1), str
     if resid is not None:
         z = z + resid.float()
     if relu:
-        z = torch.relu(z)
+        z = ref_relu(z)
     return z.to(x.dtype) if x.dtype != torch.float32 else z
 
 
@@ -505,7 +530,7 @@ def batch_norm_nhwc(y, gamma, beta, running_mean, running_var, eps=1e-5, momentu
     if resid is not None:
         z = z + resid.float()
     if relu:
-        z = torch.relu(z)
+        z = ref_relu(z)
     return z.to(y.dtype)
 
 

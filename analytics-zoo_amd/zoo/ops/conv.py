@@ -103,6 +103,22 @@ def ref_storage(y):
     return y.to(torch.bfloat16).float() if REF_BF16_STORAGE[0] else y
 
 
+# Parity harness switch for the BACKWARD comparison: [keep-mask, uses]. A pre-activation that lands
+# within rounding of zero is a tie -- either ReLU decision is correct -- but a tie decided
+# differently by the GPU and the CPU twin moves that element's whole gradient. With a mask set,
+# the CPU paths' ReLU keeps exactly the elements the GPU forward kept (the forward itself is
+# compared without it) and counts its uses, so the harness can check it hit one ReLU.
+REF_RELU_MASK = [None, 0]
+
+
+def ref_relu(z):
+    m = REF_RELU_MASK[0]
+    if m is not None and m.shape == z.shape:
+        REF_RELU_MASK[1] += 1
+        return z * m.to(z.dtype)
+    return torch.relu(z)
+
+
 def conv2d_ref(x, w2, geom, bias=None):
     """fp32 PyTorch reference: x NHWC, packed weight -> NHWC."""
     R, S, C, stride, pad, dil = geom

@@ -119,6 +119,18 @@ class GeluLink:
         self.done = False
 
 
+def _native_drop(a):
+    """The fused native dropout kernels draw their masks from a host seed per call. Eager: for
+    tensors of at least _DROP_FUSE_MIN elements. Under hipGraph capture the host seed would be
+    baked into the graph, so only once the engine registered the per-step device seed offset the
+    kernels xor in (zoo.ops.devscalar) -- then always, so every mask of the captured step follows
+    that offset (torch's own dropout would advance its generator per replay instead)."""
+    if torch.cuda.is_current_stream_capturing():
+        from zoo.ops.devscalar import seed_offset_live
+        return seed_offset_live(a.device)
+    return a.numel() >= _DROP_FUSE_MIN
+
+
 class _DropoutAddFn(torch.autograd.Function):
     """out = x + dropout(a): one native pass; the keep-mask is a counter-based hash of a
     per-call seed, so backward regenerates it (no mask tensor is stored)."""
@@ -149,8 +161,8 @@ def dropout_add(a, x, p, training=True, grad_add=None):
     if not training or p <= 0:
         return x + a
     if a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and a.shape == x.shape and \
-            a.numel() % 8 == 0 and a.numel() >= _DROP_FUSE_MIN and not torch.cuda.is_current_stream_capturing():
-        # small tensors are launch/host-bound: the C++ dropout path has less per-call overhead
+            a.numel() % 8 == 0 and _native_drop(a):
+        # small eager tensors are launch/host-bound: the C++ dropout path has less per-call overhead
         return _DropoutAddFn.apply(a.contiguous(), x.contiguous(), float(p), grad_add)
     return x + F.dropout(a, p, True)
 
@@ -210,13 +222,13 @@ class _DropAddLNFn(torch.autograd.Function):
 def dropout_add_layer_norm(a, x, p, training, gamma, beta, eps=1e-5, grad_add=None, grad_in=None):
     """``layer_norm(dropout_add(a, x, p, training, grad_add), gamma, beta, eps, grad_in)`` -- the
     Transformer residual LayerNorm -- as one native pass when it can be (bf16 GPU tensors, fp32
-    affine, D % 8 == 0, D <= 2048, dropout live, not under stream capture: the mask seed is drawn
-    on the host per call); otherwise the two ops. Reference: TransformerLayer.scala:129-181."""
+    affine, D % 8 == 0, D <= 2048, dropout live, ``_native_drop``: the mask seed is drawn on the
+    host per call); otherwise the two ops. Reference: TransformerLayer.scala:129-181."""
     D = x.shape[-1]
     if training and p > 0 and a.is_cuda and a.dtype == torch.bfloat16 and x.dtype == torch.bfloat16 and \
             a.shape == x.shape and D % 8 == 0 and D <= 2048 and a.numel() >= _DROP_FUSE_MIN and \
             gamma is not None and beta is not None and gamma.dtype == torch.float32 and \
-            beta.dtype == torch.float32 and not torch.cuda.is_current_stream_capturing():
+            beta.dtype == torch.float32 and _native_drop(a):
         return _DropAddLNFn.apply(a.contiguous(), x.contiguous(), gamma, beta, float(eps), float(p), grad_add, grad_in)
     return layer_norm(dropout_add(a, x, p, training, grad_add=grad_add), gamma, beta, eps, grad_in=grad_in)
 

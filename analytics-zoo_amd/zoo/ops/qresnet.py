@@ -156,10 +156,15 @@ class Int8ResNet(nn.Module):
 
     fmt = "int8"
     act_scales = "channel"
+    act_clip = 0.0
 
-    def __init__(self, model, calib_x, fmt=None, act_scales=None):
-        """``act_scales``: "channel" (one activation scale per channel) or "tensor" (one per tensor)."""
+    def __init__(self, model, calib_x, fmt=None, act_scales=None, act_clip=None):
+        """``act_scales``: "channel" (one activation scale per channel) or "tensor" (one per tensor).
+        ``act_clip``: fraction of each channel's calibration values allowed to saturate (0: absmax;
+        e.g. 1e-4 keeps a few spatial outliers from stretching the channel's int8 grid)."""
         super().__init__()
+        if act_clip is not None:
+            self.act_clip = float(act_clip)
         from zoo.models.image import resnet as R
         if fmt is not None:
             self.fmt = fmt
@@ -202,9 +207,16 @@ class Int8ResNet(nn.Module):
     def calibrate(self, x):
         """Per-tensor absmax of every int8 tensor of the network on ``x`` (run in bf16)."""
         qmax = QMAX[self.fmt]
+        clip = self.act_clip
         if self.act_scales == "channel":
             def amax(t):
-                return t.float().abs().amax(dim=tuple(range(t.dim() - 1))).clamp_min(1e-6) / qmax
+                a = t.float().abs().reshape(-1, t.shape[-1])
+                if clip > 0:
+                    k = max(1, int(a.shape[0] * clip))     # the k-th largest value per channel
+                    a = a.topk(k, dim=0).values[-1]
+                else:
+                    a = a.amax(dim=0)
+                return a.clamp_min(1e-6) / qmax
         else:
             def amax(t):
                 return max(float(t.float().abs().max()), 1e-6) / qmax

@@ -167,6 +167,73 @@ class GRU(_RNNBase):
 # whole-sequence ConvLSTM2D path (_ConvLSTMSeqFn); ZOO_CONVLSTM_SEQ=0 keeps the per-step
 # autograd loop (A/B and fallback)
 _CONVLSTM_SEQ = os.environ.get("ZOO_CONVLSTM_SEQ", "1") != "0"
+# one launch per step (_ConvLSTMFusedFn, csrc/kernels/convlstm.hip) for up to 64 filters;
+# ZOO_CONVLSTM_FUSED=0 keeps the conv + step-kernel sequence path (A/B)
+_CONVLSTM_FUSED = os.environ.get("ZOO_CONVLSTM_FUSED", "1") != "0"
+
+
+def _gate_perm(f, device):
+    """Row order of the gate-interleaved layout: row 4j + g takes torch row g*f + j (gate g of
+    hidden channel j), so one MFMA accumulator lane holds all four gates of a channel."""
+    return (torch.arange(4, device=device)[None, :] * f + torch.arange(f, device=device)[:, None]).reshape(-1)
+
+
+class _ConvLSTMFusedFn(torch.autograd.Function):
+    """Whole ConvLSTM2D sequence, ONE launch per step each way, issued by a C++ loop
+    (convlstm_fwd_seq / convlstm_bwd_seq; csrc/kernels/convlstm.hip): the
+    recurrent conv is an MFMA implicit GEMM whose epilogue runs the LSTM cell (forward) or the
+    cell backward on the recurrent data gradient (backward). Gate tensors are gate-interleaved
+    ([M][F][4], weights permuted by _gate_perm). The recurrent weight gradient is ONE conv_wgrad
+    over all steps at the end (the per-step bf16 gate gradients are kept, [T][B,H,W,K8]).
+    Reference: InternalConvLSTM2D.scala (Zs/pipeline/api/keras/layers)."""
+
+    @staticmethod
+    def forward(ctx, gxs, wh, B, Ho, Wo, f, cph, R, S, iact, act, return_sequences):
+        C_ = ops.native()
+        from zoo.ops.conv import bf16_weight
+        T, M, K = gxs.shape
+        dev = gxs.device
+        whb = bf16_weight(wh)
+        hist = torch.zeros(T + 1, B, Ho, Wo, cph, dtype=torch.bfloat16, device=dev)
+        hseq = torch.empty(T, M, f, dtype=torch.float32, device=dev)
+        cseq = torch.empty_like(hseq)
+        acts = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        C_.convlstm_fwd_seq(gxs, whb, B, 1, Ho, Wo, 1, R, S, hist, hseq, cseq, acts, iact, act)
+        ctx.save_for_backward(wh, hist, cseq, acts)
+        ctx.geo = (B, Ho, Wo, f, cph, R, S, iact, act, return_sequences)
+        return hseq if return_sequences else hseq[T - 1].clone()
+
+    @staticmethod
+    def backward(ctx, dout):
+        C_ = ops.native()
+        from zoo.ops import _kern
+        from zoo.ops.conv import bf16_weight
+        wh, hist, cseq, acts = ctx.saved_tensors
+        B, Ho, Wo, f, cph, R, S, iact, act, rseq = ctx.geo
+        T, M, K = acts.shape
+        dev = acts.device
+        K8 = wh.shape[0]
+        whf = _kern.flip_weights(bf16_weight(wh), K8, R, S, cph)
+        dgxs = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        dgb = torch.zeros(T, B, Ho, Wo, K8, dtype=torch.bfloat16, device=dev)
+        dc = torch.empty(M, f, dtype=torch.float32, device=dev)
+        dout = dout.contiguous().float()
+        C_.convlstm_bwd_seq(dout, bool(rseq), whf, B, 1, Ho, Wo, 1, R, S, acts, cseq, dc, dgxs, dgb, iact, act)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            gbuf = grad_slot(wh)
+            dwh = gbuf if gbuf is not None else torch.zeros(wh.shape, dtype=torch.float32, device=dev)
+            if T > 1:
+                # every step's recurrent weight gradient in one conv: (T-1)*B images
+                C_.conv_wgrad(hist[1:T].reshape((T - 1) * B, Ho, Wo, cph), dgb[1:T].reshape((T - 1) * B, Ho, Wo, K8),
+                              dwh, R, S, 1, 1, R // 2, S // 2, 1, 1)
+            if gbuf is not None:
+                hook = getattr(wh, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(wh)
+            else:
+                dw = dwh.to(wh.dtype)
+        return dgxs, dw, None, None, None, None, None, None, None, None, None, None
 
 
 class _ConvLSTMSeqFn(torch.autograd.Function):
@@ -284,9 +351,14 @@ class ConvLSTM2D(Layer):
         K = 4 * f
         R, S = self.k
         pad = (R // 2, S // 2)
-        wx, cpx = self._packed(self.Wx)
-        wh, cph = self._packed(self.Wh)
-        bias = F.pad(self.b, (0, ops.ceil8(K) - K)).float()
+        fused = _CONVLSTM_SEQ and _CONVLSTM_FUSED and f <= 64 and K % 8 == 0
+        Wx, Wh, b = self.Wx, self.Wh, self.b
+        if fused:   # gate-interleaved rows (the permutation's gradient flows back to the parameters)
+            perm = _gate_perm(f, x.device)
+            Wx, Wh, b = Wx[perm], Wh[perm], b[perm]
+        wx, cpx = self._packed(Wx)
+        wh, cph = self._packed(Wh)
+        bias = F.pad(b, (0, ops.ceil8(K) - K)).float()
         xn = x.reshape(B * T, C, H, W).permute(0, 2, 3, 1)
         if cpx != C:
             xn = F.pad(xn, (0, cpx - C))
@@ -299,7 +371,8 @@ class ConvLSTM2D(Layer):
             gxs = xs.reshape(B, T, Ho * Wo, K).permute(1, 0, 2, 3).reshape(T, M, K)
             if self.go_backwards:
                 gxs = gxs.flip(0)
-            hs = _ConvLSTMSeqFn.apply(gxs.contiguous(), wh, B, Ho, Wo, f, cph, R, S,
+            fn = _ConvLSTMFusedFn if fused else _ConvLSTMSeqFn
+            hs = fn.apply(gxs.contiguous(), wh, B, Ho, Wo, f, cph, R, S,
                                       ACT_CODES[self.inner_activation], ACT_CODES[self.activation],
                                       bool(self.return_sequences))
             if self.return_sequences:
@@ -346,6 +419,63 @@ class ConvLSTM2D(Layer):
         return torch.stack(outs, 1) if self.return_sequences else h
 
 
+class _ConvLSTM3DFusedFn(torch.autograd.Function):
+    """Whole ConvLSTM3D sequence, one launch per step each way: the convlstm.hip step kernels
+    with a depth axis (no per-step pad / permute / conv3d glue). ``whp``: the recurrent weight
+    [4f, f, k, k, k] in gate-interleaved row order; packed (and flipped for the backward) here
+    once per call. Recurrent weight gradient: one conv_wgrad per depth tap over all steps.
+    Reference: InternalConvLSTM3D.scala (Zs/pipeline/api/keras/layers)."""
+
+    @staticmethod
+    def forward(ctx, gxs, whp, B, D, H, W, f, k, return_sequences):
+        C_ = ops.native()
+        T, M, K = gxs.shape
+        dev = gxs.device
+        cph, K8 = ops.ceil8(f), ops.ceil8(K)
+        w5 = F.pad(whp.detach().permute(0, 2, 3, 4, 1), (0, cph - f, 0, 0, 0, 0, 0, 0, 0, K8 - K))
+        wpk = ops.pack_weight(w5.reshape(K8, k, k * k, cph)).to(torch.bfloat16)   # [K8][k^3 * cph]
+        hist = torch.zeros(T + 1, B, D, H, W, cph, dtype=torch.bfloat16, device=dev)
+        hseq = torch.empty(T, M, f, dtype=torch.float32, device=dev)
+        cseq = torch.empty_like(hseq)
+        acts = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        C_.convlstm_fwd_seq(gxs, wpk, B, D, H, W, k, k, k, hist, hseq, cseq, acts, 2, 1)
+        ctx.save_for_backward(whp, hist, cseq, acts)
+        ctx.geo = (B, D, H, W, f, k, return_sequences)
+        return hseq if return_sequences else hseq[T - 1].clone()
+
+    @staticmethod
+    def backward(ctx, dout):
+        C_ = ops.native()
+        whp, hist, cseq, acts = ctx.saved_tensors
+        B, D, H, W, f, k, rseq = ctx.geo
+        T, M, K = acts.shape
+        dev = acts.device
+        cph, K8 = ops.ceil8(f), ops.ceil8(K)
+        # flipped weight for the recurrent data gradient: [cph][k^3 * K8], taps reversed
+        w5 = F.pad(whp.detach().permute(0, 2, 3, 4, 1), (0, cph - f, 0, 0, 0, 0, 0, 0, 0, K8 - K))
+        wfl = w5.flip(1, 2, 3).permute(4, 1, 2, 3, 0).reshape(cph, k, k * k, K8)
+        wfl = ops.pack_weight(wfl).to(torch.bfloat16)
+        dgxs = torch.empty(T, M, K, dtype=torch.float32, device=dev)
+        dgb = torch.zeros(T, B, D, H, W, K8, dtype=torch.bfloat16, device=dev)
+        dc = torch.empty(M, f, dtype=torch.float32, device=dev)
+        dout = dout.contiguous().float()
+        C_.convlstm_bwd_seq(dout, bool(rseq), wfl, B, D, H, W, k, k, k, acts, cseq, dc, dgxs, dgb, 2, 1)
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dw5 = torch.zeros(K8, k, k, k, cph, dtype=torch.float32, device=dev)
+            if T > 1:
+                p = k // 2
+                hp = F.pad(hist[1:T], (0, 0, 0, 0, 0, 0, p, p))          # depth-padded inputs of steps 1..T-1
+                gy = dgb[1:T].reshape((T - 1) * B * D, H, W, K8)
+                for kd in range(k):
+                    xk = hp[:, :, kd:kd + D].reshape((T - 1) * B * D, H, W, cph)
+                    part = torch.zeros(K8, k * k * cph, dtype=torch.float32, device=dev)
+                    C_.conv_wgrad(xk.contiguous(), gy, part, k, k, 1, 1, p, p, 1, 1)
+                    dw5[:, kd] = part.view(K8, k, k, cph)
+            dw = dw5[:K, ..., :f].permute(0, 4, 1, 2, 3).to(whp.dtype)
+        return dgxs, dw, None, None, None, None, None, None, None
+
+
 class ConvLSTM3D(Layer):
     """Convolutional LSTM over (batch, time, channels, d1, d2, d3)."""
 
@@ -369,8 +499,9 @@ class ConvLSTM3D(Layer):
 
     def _call_native(self, x):
         """GPU path (InternalConvLSTM3D.scala): the input convolution for all timesteps in one
-        3-D conv (implicit-GEMM launches), per step one recurrent 3-D conv and one fused
-        gate / cell / hidden pass."""
+        3-D conv (implicit-GEMM launches), then the whole sequence on the one-launch-per-step
+        kernels (_ConvLSTM3DFusedFn); beyond 64 filters (or with ZOO_CONVLSTM_FUSED=0) per step one
+        recurrent 3-D conv and one fused gate / cell / hidden pass."""
         from zoo.ops.layers import conv3d_ndhwc
         B, T, C = x.shape[:3]
         sp = tuple(x.shape[3:])
@@ -380,14 +511,30 @@ class ConvLSTM3D(Layer):
         cp, fp, kp = (-C) % 8, (-f) % 8, (-K) % 8
         xn = x.reshape(B * T, C, *sp).permute(0, 2, 3, 4, 1)
         xn = F.pad(xn, (0, cp)).to(torch.bfloat16)
-        wx = F.pad(self.Wx.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
-        wh = F.pad(self.Wh.permute(0, 2, 3, 4, 1), (0, fp, 0, 0, 0, 0, 0, 0, 0, kp))
-        bias = F.pad(self.b, (0, kp))
+        # gate-interleaved one-launch-per-step path (convlstm.hip) up to 64 filters
+        il = _CONVLSTM_SEQ and _CONVLSTM_FUSED and f <= 64 and K % 8 == 0
+        Wx, Whp, b = self.Wx, self.Wh, self.b
+        if il:
+            perm = _gate_perm(f, x.device)
+            Wx, Whp, b = Wx[perm], Whp[perm], b[perm]
+        wx = F.pad(Wx.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
+        wh = F.pad(Whp.permute(0, 2, 3, 4, 1), (0, fp, 0, 0, 0, 0, 0, 0, 0, kp))
+        bias = F.pad(b, (0, kp))
         xs = conv3d_ndhwc(xn, wx, bias, stride=(1, 1, 1), pad=(p, p, p)).float()[..., :K]
         osp = tuple(xs.shape[1:4])
         P = osp[0] * osp[1] * osp[2]
-        xs = xs.reshape(B, T, P, K)
         M = B * P
+        if il:
+            # whole sequence, one launch per step: time-major gate inputs in processing order
+            gxs = xs.reshape(B, T, P, K).permute(1, 0, 2, 3).reshape(T, M, K)
+            if self.go_backwards:
+                gxs = gxs.flip(0)
+            hs = _ConvLSTM3DFusedFn.apply(gxs.contiguous(), Whp, B, osp[0], osp[1], osp[2], f, k,
+                                          bool(self.return_sequences))
+            if self.return_sequences:
+                return hs.reshape(T, B, *osp, f).permute(1, 0, 5, 2, 3, 4).to(x.dtype)
+            return hs.reshape(B, *osp, f).permute(0, 4, 1, 2, 3).to(x.dtype)
+        xs = xs.reshape(B, T, P, K)
         h = c = None
         outs = []
         for t in (range(T - 1, -1, -1) if self.go_backwards else range(T)):

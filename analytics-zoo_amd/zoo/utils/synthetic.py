@@ -56,6 +56,27 @@ def train_briefly(model, templates, steps=300, batch=32, lr=0.01, seed=2):
     return acc
 
 
+def input_sensitivity(ref):
+    """Spread of a model's logits ACROSS inputs (mean over classes of the per-class std over the
+    batch) relative to their mean magnitude: ~0 for a collapsed model that ignores its input, on
+    which any agreement number is vacuous."""
+    ref = ref.float()
+    return (ref.std(0).mean() / ref.abs().mean().clamp_min(1e-12)).item()
+
+
+def margin_agreement(out, ref, rel_margin=0.1):
+    """Top-1 agreement over the samples whose reference top-1 / top-2 logit margin is at least
+    ``rel_margin`` of that row's logit std (a near-tie flips on any rounding); returns
+    (agreement, fraction of samples kept)."""
+    out, ref = out.float(), ref.float()
+    top2 = ref.topk(2, dim=1).values
+    keep = (top2[:, 0] - top2[:, 1]) >= rel_margin * ref.std(1)
+    if not bool(keep.any()):
+        return float("nan"), 0.0
+    agree = (out.argmax(1) == ref.argmax(1))[keep].float().mean().item()
+    return agree, keep.float().mean().item()
+
+
 def agreement(out, ref):
     """(top-1 agreement, mean per-sample cosine of mean-centred logits) of two logit batches."""
     out, ref = out.float(), ref.float()

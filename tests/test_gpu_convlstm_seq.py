@@ -15,9 +15,17 @@ def rel(a, b):
     return float((a - b).abs().max() / b.abs().max().clamp_min(1e-12))
 
 
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("rseq,back", [(True, False), (False, False), (True, True)])
-def test_convlstm2d_sequence_path_matches_fp32(gpu, rseq, back):
+def test_convlstm2d_sequence_path_matches_fp32(gpu, rseq, back, fused, monkeypatch):
+    """fused: one launch per step (_ConvLSTMFusedFn, convlstm.hip, gate-interleaved weights);
+    otherwise the recurrent conv + step kernel sequence (_ConvLSTMSeqFn)."""
     from zoo.pipeline.api.keras.layers import recurrent as R
+    monkeypatch.setattr(R, "_CONVLSTM_FUSED", fused)
+    used = []
+    orig_f, orig_s = R._ConvLSTMFusedFn.apply, R._ConvLSTMSeqFn.apply
+    monkeypatch.setattr(R._ConvLSTMFusedFn, "apply", lambda *a: (used.append("fused"), orig_f(*a))[1])
+    monkeypatch.setattr(R._ConvLSTMSeqFn, "apply", lambda *a: (used.append("seq"), orig_s(*a))[1])
     torch.manual_seed(0)
     T, B, C, H, W, f = 6, 2, 8, 10, 12, 16
     layer = R.ConvLSTM2D(f, 3, 3, return_sequences=rseq, go_backwards=back, input_shape=(T, C, H, W))
@@ -39,3 +47,29 @@ def test_convlstm2d_sequence_path_matches_fp32(gpu, rseq, back):
     assert rel(layer.Wh.grad, ref.Wh.grad) < 5e-2
     assert rel(layer.Wx.grad, ref.Wx.grad) < 5e-2
     assert rel(layer.b.grad, ref.b.grad) < 5e-2
+    assert used == ["fused" if fused else "seq"], used
+
+
+def test_convlstm2d_fused_odd_filters_and_wide_channels(gpu, monkeypatch):
+    """The fused step at F = 6 (24 gate rows: a partial MFMA row block; 8-channel padded history)
+    with a 5x3 kernel, against the fp32 reference."""
+    from zoo.pipeline.api.keras.layers import recurrent as R
+    monkeypatch.setattr(R, "_CONVLSTM_FUSED", True)
+    torch.manual_seed(1)
+    T, B, C, H, W, f = 4, 3, 5, 7, 9, 6
+    layer = R.ConvLSTM2D(f, 5, 3, return_sequences=True, input_shape=(T, C, H, W))
+    layer._ensure_built((None, T, C, H, W))
+    ref = copy.deepcopy(layer)
+    x = torch.randn(B, T, C, H, W)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(xr)
+    g = torch.randn_like(yr)
+    (yr * g).sum().backward()
+    layer = layer.to(gpu)
+    xg = x.to(gpu).requires_grad_(True)
+    y = layer(xg)
+    (y.float() * g.to(gpu)).sum().backward()
+    assert rel(y, yr) < 3e-2
+    assert rel(xg.grad, xr.grad) < 5e-2
+    assert rel(layer.Wh.grad, ref.Wh.grad) < 5e-2
+    assert rel(layer.Wx.grad, ref.Wx.grad) < 5e-2

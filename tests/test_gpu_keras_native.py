@@ -55,13 +55,15 @@ def _cases():
                        (2, 4, 6, 10, 10)),
         "ConvLSTM3D": (lambda: L.ConvLSTM3D(8, 3, return_sequences=True, input_shape=(3, 4, 5, 6, 6)),
                        (2, 3, 4, 5, 6, 6)),
+        "ConvLSTM3D_back": (lambda: L.ConvLSTM3D(6, 3, go_backwards=True, input_shape=(4, 3, 4, 5, 5)),
+                            (3, 4, 3, 4, 5, 5)),
     }
 
 
 CASES = ["SeparableConvolution2D", "SeparableConvolution2D_dm2", "Convolution3D", "Convolution3D_odd",
          "MaxPooling3D", "AveragePooling3D", "MaxPooling1D", "AveragePooling1D", "LRN2D", "WithinChannelLRN2D",
          "ResizeBilinear", "ResizeBilinear_align", "UpSampling1D", "UpSampling2D", "UpSampling3D",
-         "BatchNormalization_c6", "ConvLSTM2D", "ConvLSTM3D"]
+         "BatchNormalization_c6", "ConvLSTM2D", "ConvLSTM3D", "ConvLSTM3D_back"]
 
 
 @pytest.mark.parametrize("name", CASES)
