@@ -40,8 +40,8 @@ _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
 # and its sums, dy = A g + B y + Cc is formed in the dgrad kernel's operand registers from g and
 # the unit's y, and written once for the weight gradient -- no separate BN-backward pass and no
 # re-read of dy (6 instead of 8 bytes per element). Shapes the prologue kernel does not take get
-# dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B comparator).
-_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
+# dy materialised inside conv_fwd. Off by default until its same-box A/B wins (ZOO_BN_FOLD=1: on).
+_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "0") != "0"]
 
 
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
