@@ -8,9 +8,9 @@
 // (the BN backward, bn.hip bn_bwd_apply) as the A operand of its dgrad GEMM and as the dY
 // operand of its wgrad. Materialising dy costs a pass that reads g and y and writes dy, and the
 // dgrad then reads dy again: 8 bytes per element. With the prologue the 1x1 streaming kernel
-// (pw.hip, PRO) reads g and y straight into its operand registers, forms dy there with the
-// coefficients below, feeds the MFMAs and writes dy once for the weight gradient: 6 bytes per
-// element and one launch (plus its tail) less per unit.
+// (pw.hip, PRO; 64-channel units) reads g and y straight into its operand registers, forms dy
+// there with the coefficients below, feeds the MFMAs and writes dy once for the weight gradient:
+// 6 bytes per element and one launch (plus its tail) less per unit.
 //
 // bnfold_coef_kernel:  (A | B | Cc) [3K], dgamma += S2, dbeta += S1
 // bnpro_apply_kernel:  dy = A o g + B o y + Cc materialised (shapes the prologue kernel does not
@@ -43,10 +43,39 @@ __global__ __launch_bounds__(256) void bnfold_coef_kernel(int K, const float* __
   if (dbeta) dbeta[k] += sums[k];
 }
 
-// 8 channels per thread; K % 8 == 0
+// grid-stride over 8-channel chunks of rows; each thread keeps one fixed chunk's coefficients
+// (blockDim.x threads cover the row in chunks: K / 8 <= 256 chunks per row here)
 __global__ __launch_bounds__(256) void bnpro_apply_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                                           const float* __restrict__ coef, bf16_t* __restrict__ dy,
-                                                          size_t n8, int K) {
+                                                          long long rows, int K) {
+  const int cpr = K / 8;                        // chunks per row
+  const int rpb = blockDim.x / cpr;             // rows per block step (launcher: cpr <= 256, divides 256)
+  const int ch = threadIdx.x % cpr, r0 = threadIdx.x / cpr;
+  if (r0 >= rpb) return;
+  const int k0 = ch * 8;
+  float ca[8], cb[8], cc[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    ca[e] = coef[k0 + e];
+    cb[e] = coef[K + k0 + e];
+    cc[e] = coef[2 * K + k0 + e];
+  }
+  for (long long r = (long long)blockIdx.x * rpb + r0; r < rows; r += (long long)gridDim.x * rpb) {
+    const size_t off = (size_t)r * K + k0;
+    float gv[8], yv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(g + off), gv);
+    unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = ca[e] * gv[e] + cb[e] * yv[e] + cc[e];
+    *reinterpret_cast<uint4*>(dy + off) = pack8(o);
+  }
+}
+
+// any K % 8 == 0: grid-stride over 8-channel chunks (coefficients re-read per chunk)
+__global__ __launch_bounds__(256) void bnpro_apply_any_kernel(const bf16_t* __restrict__ g,
+                                                              const bf16_t* __restrict__ y,
+                                                              const float* __restrict__ coef,
+                                                              bf16_t* __restrict__ dy, size_t n8, int K) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const int k0 = (int)((i * 8) % K);
     float gv[8], yv[8], o[8];
@@ -72,11 +101,21 @@ extern "C" hipError_t zoo_bnfold_coef(int K, const float* gamma, const float* me
 
 extern "C" hipError_t zoo_bnpro_apply(const void* g, const void* y, const float* coef, void* dy, size_t n, int K,
                                       hipStream_t st) {
-  const size_t n8 = n / 8;
-  size_t blocks = (n8 + 255) / 256;
-  if (blocks > 8192) blocks = 8192;
-  if (blocks == 0) return hipSuccess;
+  if (K % 8) return hipErrorInvalidValue;
+  const long long rows = (long long)(n / K);
+  if (rows == 0) return hipSuccess;
+  if (K / 8 > 256 || 256 % (K / 8)) {   // not K = 8 * 2^j <= 2048: the generic chunk loop
+    const size_t n8 = n / 8;
+    size_t b = (n8 + 255) / 256;
+    if (b > 4096) b = 4096;
+    hipLaunchKernelGGL(bnpro_apply_any_kernel, dim3((unsigned)b), dim3(256), 0, st, (const bf16_t*)g,
+                       (const bf16_t*)y, coef, (bf16_t*)dy, n8, K);
+    return hipGetLastError();
+  }
+  const int rpb = 256 / (K / 8);
+  long long blocks = (rows + rpb - 1) / rpb;
+  if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(bnpro_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)g,
-                     (const bf16_t*)y, coef, (bf16_t*)dy, n8, K);
+                     (const bf16_t*)y, coef, (bf16_t*)dy, rows, K);
   return hipGetLastError();
 }

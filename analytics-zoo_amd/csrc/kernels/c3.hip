@@ -408,7 +408,8 @@ static int c3_ncu() {
     hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     if (n <= 0) n = 256;
   }
-  return n;
+  const int free_cus = n - g_reserved_cus;
+  return free_cus >= 8 ? free_cus : 8;
 }
 
 static bool c3_geom(const ConvGeom& g, C3Geom& c) {

@@ -141,5 +141,8 @@ ZOO_DEV float apply_act(float x, int act) {
 // dropout kernel xors it into its host seed, so a hipGraph-captured step that replays baked host
 // seeds still draws a fresh mask each step (the host stages a new offset before every replay)
 extern const uint32_t* g_seed_off;
+// CUs reserved for the weight-gradient side stream while it runs on a CU-masked stream
+// (zoo_set_reserved_cus, pw.hip): persistent kernels size their grids to the remaining CUs
+extern int g_reserved_cus;
 
 }  // namespace zoo

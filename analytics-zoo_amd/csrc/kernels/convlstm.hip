@@ -16,10 +16,12 @@
 //                    gradients fp32 (the input conv's gradient) + bf16 (dgb_t, the operand of the
 //                    next dgrad and of ONE batched weight-gradient conv over all steps), dc_{t-1}.
 //
-// One wave per workgroup, 16 pixels per wave, all gate rows per wave (NI = rows / 16 <= 16), the
-// reduction R*S*Cx walked 32 deep with the activation fragment gathered straight from global
-// (zero outside the image). Sized for the latency-bound recurrent step (M = B*H*W of a few
-// thousand pixels, 4F <= 256 gate rows): enough waves to cover every CU, no barrier.
+// Four waves per workgroup, 16 pixels per wave, all gate rows per wave (NI = rows / 16 <= 16).
+// The workgroup stages the step's weights in LDS once (rows padded by 16 B: conflict-free 16-byte
+// reads; from L2 when they exceed 128 KiB); the reduction Q*R*S*Cx is walked 32 deep with the
+// activation fragments gathered straight from global (zero outside the image) CL_PF chunks ahead.
+// Sized for the latency-bound recurrent step (M = B*D*H*W of a few thousand pixels, 4F <= 256
+// gate rows).
 // ConvLSTM3D is the same kernel with a depth axis (D slices, Q depth taps).
 // Reference: InternalConvLSTM2D.scala / InternalConvLSTM3D.scala (Zs/pipeline/api/keras/layers),
 // SURVEY.md §2.16 HK11.
@@ -50,47 +52,88 @@ struct CLArgs {
   int ldg;
 };
 
-template <int NI>
-ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane) {
+constexpr int CL_WAVES = 4;   // 4 waves x 16 pixels per workgroup
+constexpr int CL_PF = 4;      // activation chunks in flight per wave
+
+ZOO_DEV int cl_kdp(int KD) { return (KD + 31) / 32 * 32 + 8; }   // LDS row pitch (+16 B: conflict-free)
+
+// acc[i] (rows 16 i .. 16 i + 15, this lane's pixel m) = W[rows] . X_patch(m)
+// LDSW: the workgroup's weights staged once in LDS (rows padded to cl_kdp); else read from L2
+template <int NI, bool LDSW>
+ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane, const bf16_t* wl) {
 #pragma unroll
   for (int i = 0; i < NI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (!a.X) return;
   const bool mok = m < a.M;
   const int mm = mok ? m : 0;
   const int x = mm % a.Wd, y = (mm / a.Wd) % a.H, z = (mm / (a.Wd * a.H)) % a.D, b = mm / (a.Wd * a.H * a.D);
-  const int KD = a.Q * a.R * a.S * a.Cx;
+  const int KD = a.Q * a.R * a.S * a.Cx, KC = (KD + 31) / 32, kdp = cl_kdp(KD);
   const int pq = a.Q / 2, ph = a.R / 2, pw = a.S / 2;
   const int kq = 8 * (lane >> 4), nr = lane & 15;
-  bf16x8 zero;
+  const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
+  const bf16_t* X = a.X;
+  const int Cx = a.Cx, RS = a.R * a.S, S = a.S, D = a.D, H = a.H, Wd = a.Wd;
+  auto load_act = [=](int c) -> uint4 {
+    const int k = c * 32 + kq;
+    if (!mok || c >= KC || k >= KD) return z4;
+    const int tap = k / Cx, ch = k - tap * Cx;
+    const int q = tap / RS, rs = tap - q * RS;
+    const int r = rs / S, s = rs - r * S;
+    const int zz = z + q - pq, yy = y + r - ph, xx = x + s - pw;
+    if (zz < 0 || zz >= D || yy < 0 || yy >= H || xx < 0 || xx >= Wd) return z4;
+    return *reinterpret_cast<const uint4*>(X + ((((size_t)b * D + zz) * H + yy) * Wd + xx) * Cx + ch);
+  };
+  uint4 pre[CL_PF];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) zero[e] = (__bf16)0.f;
-  for (int k0 = 0; k0 < KD; k0 += 32) {
-    const int k = k0 + kq;
-    bf16x8 bv = zero;
-    if (mok && k < KD) {
-      const int tap = k / a.Cx, ch = k - tap * a.Cx;
-      const int q = tap / (a.R * a.S), rs = tap - q * (a.R * a.S);
-      const int r = rs / a.S, s = rs - r * a.S;
-      const int zz = z + q - pq, yy = y + r - ph, xx = x + s - pw;
-      if (zz >= 0 && zz < a.D && yy >= 0 && yy < a.H && xx >= 0 && xx < a.Wd)
-        bv = *reinterpret_cast<const bf16x8*>(a.X + ((((size_t)b * a.D + zz) * a.H + yy) * a.Wd + xx) * a.Cx + ch);
-    }
+  for (int u = 0; u < CL_PF; ++u) pre[u] = load_act(u);
+  for (int c0 = 0; c0 < KC; c0 += CL_PF) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) {
-      const int n = 16 * i + nr;
-      bf16x8 wv = zero;
-      if (n < a.Nr && k < KD) wv = *reinterpret_cast<const bf16x8*>(a.Wt + (size_t)n * a.ldw + k);
-      acc[i] = mfma16(wv, bv, acc[i]);
+    for (int u = 0; u < CL_PF; ++u) {
+      const int c = c0 + u;
+      if (c < KC) {
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, pre[u]);
+        pre[u] = load_act(c + CL_PF);
+        const int k = c * 32 + kq;
+#pragma unroll
+        for (int i = 0; i < NI; ++i) {
+          const int n = 16 * i + nr;
+          uint4 wv = z4;
+          if (LDSW) {
+            wv = *reinterpret_cast<const uint4*>(wl + (size_t)n * kdp + k);   // zero padded rows / k
+          } else if (n < a.Nr && k < KD) {
+            wv = *reinterpret_cast<const uint4*>(a.Wt + (size_t)n * a.ldw + k);
+          }
+          acc[i] = mfma16(__builtin_bit_cast(bf16x8, wv), bv, acc[i]);
+        }
+      }
     }
   }
 }
 
+// stage rows [0, 16 NI) of the weights (zero beyond Nr / KD) into LDS, pitch cl_kdp(KD)
 template <int NI>
-__global__ __launch_bounds__(64) void convlstm_fwd_kernel(CLArgs a) {
-  const int lane = threadIdx.x;
-  const int m = blockIdx.x * 16 + (lane & 15);
+ZOO_DEV void cl_stage(const CLArgs& a, bf16_t* wl) {
+  if (!a.X) return;
+  const int KD = a.Q * a.R * a.S * a.Cx, kdp = cl_kdp(KD);
+  const int per_row = kdp / 8;
+  for (int e = threadIdx.x; e < 16 * NI * per_row; e += blockDim.x) {
+    const int n = e / per_row, k = (e - n * per_row) * 8;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (n < a.Nr && k < KD) v = *reinterpret_cast<const uint4*>(a.Wt + (size_t)n * a.ldw + k);
+    *reinterpret_cast<uint4*>(wl + (size_t)n * kdp + k) = v;
+  }
+  __syncthreads();
+}
+
+template <int NI, bool LDSW>
+__global__ __launch_bounds__(64 * CL_WAVES) void convlstm_fwd_kernel(CLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char cl_smem[];
+  bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
+  if (LDSW) cl_stage<NI>(a, wl);
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
   f32x4 acc[NI];
-  cl_gemm<NI>(a, m, acc, lane);
+  cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
   if (m >= a.M) return;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -110,12 +153,15 @@ __global__ __launch_bounds__(64) void convlstm_fwd_kernel(CLArgs a) {
   }
 }
 
-template <int NI>
-__global__ __launch_bounds__(64) void convlstm_bwd_kernel(CLArgs a) {
-  const int lane = threadIdx.x;
-  const int m = blockIdx.x * 16 + (lane & 15);
+template <int NI, bool LDSW>
+__global__ __launch_bounds__(64 * CL_WAVES) void convlstm_bwd_kernel(CLArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char cl_smem[];
+  bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
+  if (LDSW) cl_stage<NI>(a, wl);
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
   f32x4 acc[NI];
-  cl_gemm<NI>(a, m, acc, lane);
+  cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
   if (m >= a.M) return;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
@@ -140,14 +186,24 @@ __global__ __launch_bounds__(64) void convlstm_bwd_kernel(CLArgs a) {
   }
 }
 
+// weights in LDS while they fit 128 KiB per workgroup (one workgroup per CU at these grids); else from L2
+constexpr size_t CL_LDS_MAX = 128 * 1024;
+
+template <int NI, bool LDSW>
+static hipError_t cl_launch2(const CLArgs& a, int bwd, size_t smem, hipStream_t st) {
+  const dim3 grid((a.M + 16 * CL_WAVES - 1) / (16 * CL_WAVES));
+  auto kf = bwd ? &convlstm_bwd_kernel<NI, LDSW> : &convlstm_fwd_kernel<NI, LDSW>;
+  if (LDSW) hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kf, grid, dim3(64 * CL_WAVES), LDSW ? smem : 0, st, a);
+  return hipGetLastError();
+}
+
 template <int NI>
 static hipError_t cl_launch(const CLArgs& a, int bwd, hipStream_t st) {
-  const dim3 grid((a.M + 15) / 16);
-  if (bwd)
-    hipLaunchKernelGGL(convlstm_bwd_kernel<NI>, grid, dim3(64), 0, st, a);
-  else
-    hipLaunchKernelGGL(convlstm_fwd_kernel<NI>, grid, dim3(64), 0, st, a);
-  return hipGetLastError();
+  const int KD = a.Q * a.R * a.S * a.Cx;
+  const size_t smem = (size_t)16 * NI * ((KD + 31) / 32 * 32 + 8) * 2;
+  if (a.X && smem <= CL_LDS_MAX) return cl_launch2<NI, true>(a, bwd, smem, st);
+  return cl_launch2<NI, false>(a, bwd, 0, st);
 }
 
 }  // namespace zoo

@@ -38,7 +38,7 @@
 // Epilogues: EPI 1 = bf16 output + BN statistics of the stored values (the forward of every
 // conv->BN unit); EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
 // and the producer's fused BN-backward sums (sum dy, sum dy * xhat).
-// Prologue (PRO, EPI 2, K <= 256): the activation operand is the unit's OWN BN backward,
+// Prologue (PRO, EPI 2, K = 64): the activation operand is the unit's OWN BN backward,
 // dy = A g + B y + Cc, formed in the operand registers from the masked gradient g and the unit's
 // pre-BN output y as they arrive (per-channel A | B | Cc in LDS); channel group 0 also writes dy
 // for the weight gradient (bnfold.hip: the separate BN-backward apply pass and the re-read of dy
@@ -131,6 +131,8 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   // A fragments of tile t: lane -> pixel row t*TPM + 16 j + fr, k-chunk kb*32 + 8 fq
   // (PRO: the unit's pre-BN output y at the same positions into yf)
   constexpr int YJ = PRO ? MJ : 1, YK = PRO ? KT : 1;
+  const bf16_t* const pro_y = reinterpret_cast<const bf16_t*>(bs.pro_y);
+  bf16_t* const pro_dy = reinterpret_cast<bf16_t*>(bs.pro_dy);
   auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT], bf16x8 (&yf)[YJ][YK]) {
 #pragma unroll
     for (int j = 0; j < MJ; ++j) {
@@ -140,7 +142,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
 #pragma unroll
       for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
       if constexpr (PRO) {
-        const bf16_t* ys = reinterpret_cast<const bf16_t*>(bs.pro_y) + (size_t)row * K + 8 * fq;
+        const bf16_t* ys = pro_y + (size_t)row * K + 8 * fq;
 #pragma unroll
         for (int kb = 0; kb < KT; ++kb) yf[j][kb] = *reinterpret_cast<const bf16x8*>(ys + kb * 32);
       }
@@ -155,7 +157,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
 #pragma unroll
       for (int j = 0; j < MJ; ++j) {
         const int row = t * TPM + 16 * j + fr;
-        const bool st = g == 0 && bs.pro_dy != nullptr && row < p.M;
+        const bool st = g == 0 && pro_dy != nullptr && row < p.M;
 #pragma unroll
         for (int kb = 0; kb < KT; ++kb) {
           const int k0 = kb * 32 + 8 * fq;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
           }
           const uint4 pk = make_uint4(ow[0], ow[1], ow[2], ow[3]);
           af[j][kb] = __builtin_bit_cast(bf16x8, pk);
-          if (st) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(bs.pro_dy) + (size_t)row * K + k0) = pk;
+          if (st) *reinterpret_cast<uint4*>(pro_dy + (size_t)row * K + k0) = pk;
           __builtin_amdgcn_sched_barrier(0);   // one chunk's coefficients live at a time
         }
       }
@@ -341,7 +343,8 @@ static int pw_ncu() {
     hipGetDevice(&dev);
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
-  return ncu;
+  const int free_cus = ncu - g_reserved_cus;
+  return free_cus >= 8 ? free_cus : 8;
 }
 
 // group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave (+ PRO: [3][K] coefficients)
@@ -383,9 +386,12 @@ template <int EPI, bool PRO>
 static hipError_t pw_dispatch(const ConvGeom& g, int NP, const bf16_t* X, const bf16_t* W, bf16_t* Y,
                               const bf16_t* resid, float* stats, const BwdStats& bs, hipStream_t st) {
   const int K = g.Ktot;
-  if (PRO && K > 256) return hipErrorNotSupported;   // operand + y fragments: K <= 256 in registers
+  // operand + y fragments of a double-buffered tile in registers: spill-free only at K = 64
+  // (K = 128 / 256 spilled 32-308 bytes per lane and ran 1.1-3.3x slower than apply + plain
+  // dgrad, profiles/r5/ab_bn_prologue_r5.md)
+  if (PRO && K > 64) return hipErrorNotSupported;
 #define PW_CASE(np, k, TPM)                                                                    \
-  if constexpr (!PRO || (k) <= 256) {                                                          \
+  if constexpr (!PRO || (k) <= 64) {                                                           \
     if (NP == np && K == k) return pw_launch<np, TPM, k / 32, EPI, PRO>(g, X, W, Y, resid, stats, bs, st); \
   }
   PW_CASE(64, 64, 32)
@@ -413,6 +419,9 @@ using namespace zoo;
 
 extern "C" void zoo_pw_set(int mode) { g_pw_mode = mode; }
 
+int zoo::g_reserved_cus = 0;
+extern "C" void zoo_set_reserved_cus(int n) { zoo::g_reserved_cus = n > 0 ? n : 0; }
+
 // 1x1 / stride 1 / unpadded, whole rows (A row stride == Ktot), no output remap, forward with
 // BN statistics (EPI 1) or the backward epilogue (EPI 2, not the GELU form)
 extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs) {
@@ -427,8 +436,8 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
   // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
   if (route == 1 && g->Ktot > 256) return 0;
-  // the BN-backward prologue keeps operand and y fragments of a K <= 256 tile in registers
-  if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
+  // the BN-backward prologue keeps operand and y fragments of a K = 64 tile in registers
+  if (bs && bs->pro_y && (route != 2 || g->Ktot > 64)) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
 }
 

@@ -43,6 +43,7 @@ int zoo_c3_stamps(unsigned long long*, int);
 void zoo_igemm2_set(int, int);
 int zoo_pw_eligible(const ConvGeom*, int, const zoo::BwdStats*);
 void zoo_pw_set(int);
+void zoo_set_reserved_cus(int);
 hipError_t zoo_wlrn(const void*, const void*, void*, float*, float*, int, int, int, int, int, float, float, int,
                     hipStream_t);
 hipError_t zoo_resize_bilinear(const void*, void*, int, int, int, int, int, int, int, int, int, hipStream_t);
@@ -1638,6 +1639,25 @@ void convlstm_bwd_seq(torch::Tensor dout, bool rseq, torch::Tensor wt, int64_t B
   }
 }
 
+// A stream restricted to `ncu` CUs spread evenly over the device (hipExtStreamCreateWithCUMask):
+// the weight-gradient side stream, so its kernels never take CU slots a persistent compute-stream
+// kernel is sized for (those size their grids to the remaining CUs, set_reserved_cus). Returns
+// the hipStream_t as an integer (torch.cuda.ExternalStream); the stream lives for the process.
+int64_t cu_mask_stream(int64_t ncu_side) {
+  int dev = 0, n = 0;
+  check_hip(hipGetDevice(&dev), "hipGetDevice");
+  check_hip(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev), "cu count");
+  TORCH_CHECK(ncu_side > 0 && ncu_side < n, "cu_mask_stream: 0 < ncu < ", n);
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int64_t i = 0; i < ncu_side; ++i) {
+    const int cu = (int)(i * n / ncu_side);
+    mask[cu / 32] |= 1u << (cu % 32);
+  }
+  hipStream_t s = nullptr;
+  check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()), "hipExtStreamCreateWithCUMask");
+  return reinterpret_cast<int64_t>(s);
+}
+
 // Max RoI pooling (Faster R-CNN): features NHWC, rois [R, 5] fp32 -> (out [R, PH, PW, C], argmax int32)
 std::vector<torch::Tensor> roi_pool_fwd(torch::Tensor f, torch::Tensor rois, int PH, int PW, double scale) {
   req_act(f, "roi_pool");
@@ -3118,6 +3138,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("convlstm_fwd_step", &convlstm_fwd_step);
   m.def("convlstm_bwd_step", &convlstm_bwd_step);
   m.def("convlstm_fwd_seq", &convlstm_fwd_seq);
+  m.def("cu_mask_stream", &cu_mask_stream);
+  m.def("set_reserved_cus", [](int64_t n) { zoo_set_reserved_cus((int)n); });
   m.def("convlstm_bwd_seq", &convlstm_bwd_seq);
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");

@@ -18,7 +18,7 @@ Zs/pipeline/api/keras/layers/BatchNormalization.scala:85-110).
 import torch
 import torch.nn.functional as F
 
-from zoo.ops._native import native
+from zoo.ops._native import native, deterministic as _deterministic
 from zoo.ops import _kern, workspace, wstream
 from zoo.ops.conv import bf16_weight, ceil8, conv2d_ref, ref_relu, ref_storage
 from zoo.parallel.sync_bn import all_reduce_stats, sync_batch_norm, sync_bn_active
@@ -40,14 +40,16 @@ _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
 # and its sums, dy = A g + B y + Cc is formed in the dgrad kernel's operand registers from g and
 # the unit's y, and written once for the weight gradient -- no separate BN-backward pass and no
 # re-read of dy (6 instead of 8 bytes per element). Shapes the prologue kernel does not take get
-# dy materialised inside conv_fwd. Off by default until its same-box A/B wins (ZOO_BN_FOLD=1: on).
-_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "0") != "0"]
+# dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B: profiles/r5/ab_bn_prologue_r5.md).
+_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
 
 
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
+    # K = 64: the only width whose prologue tile stays spill-free in registers (pw.hip PRO); wider
+    # units and the deterministic mode (partial statistics: no pw) keep bn_bwd_apply
     return (_BN_FOLD[0] and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
-            and not getattr(ctx, "sync", False) and K % 8 == 0 and gamma.dtype == torch.float32
-            and gamma.is_contiguous())
+            and not getattr(ctx, "sync", False) and K == 64 and Cin % 64 == 0
+            and gamma.dtype == torch.float32 and gamma.is_contiguous() and not _deterministic())
 
 
 def stat_len(c):

@@ -40,11 +40,11 @@ def test_bnfold_coef_and_apply_match_fp32_formulas(gpu):
     torch.testing.assert_close(out.float(), ref, rtol=1e-2, atol=1e-2)
 
 
-@pytest.mark.parametrize("M,K,N,det", [(4096, 256, 64, False), (3000, 64, 256, False), (2048, 128, 512, False),
-                                       (1024, 256, 1024, False), (512, 512, 128, False), (4096, 256, 64, True)])
+@pytest.mark.parametrize("M,K,N,det", [(4096, 64, 64, False), (3000, 64, 256, False), (4096, 256, 64, False),
+                                       (2048, 128, 512, False), (512, 72, 128, False), (3000, 64, 256, True)])
 def test_dgrad_prologue_matches_materialised_dy(gpu, M, K, N, det):
-    """A 1x1 dgrad with the BN-backward prologue (pw.hip PRO where it applies; K = 512 and the
-    deterministic mode's partial statistics take the materialising fallback) against the same
+    """A 1x1 dgrad with the BN-backward prologue (pw.hip PRO at K = 64; wider K, an odd width and
+    the deterministic mode's partial statistics take the materialising fallback) against the same
     dgrad of dy materialised in fp32: the output, the written dy, with a residual operand and the
     producer's fused BN-backward epilogue."""
     from zoo.ops import _kern, deterministic, set_deterministic
@@ -87,15 +87,16 @@ def _prologue_case(gpu, M, K, N):
 
 
 def test_bnfold_matches_unfolded_backward(gpu):
-    """Deterministic reductions: a bottleneck ResNet's gradients with the 1x1 units' BN backward
-    as the dgrad prologue vs materialised -- every weight and BN affine pair within 2 %, the
-    whole gradient within 0.5 %, and the prologue really taken."""
+    """A bottleneck ResNet (64-channel first stage: the prologue's units) with the 1x1 units' BN
+    backward as the dgrad prologue vs materialised: the gradient difference is held to the
+    run-to-run distance of the fp32-atomic reductions (as the BN-backward fusion test), overall
+    and per weight / BN affine pair (+3 %), and the prologue really taken."""
     import zoo.models.image.resnet as R
     import zoo.ops.bn as B
-    from zoo.ops import softmax_cross_entropy, deterministic, set_deterministic
+    from zoo.ops import softmax_cross_entropy
     torch.manual_seed(0)
-    m = R.ResNet(R.Bottleneck, [2, 2, 1, 1], num_classes=16, width=16).to(gpu)
-    x = torch.randn(8, 3, 96, 96, device=gpu)
+    m = R.ResNet(R.Bottleneck, [2, 1, 1, 1], num_classes=16, width=64).to(gpu)
+    x = torch.randn(8, 3, 64, 64, device=gpu)
     y = torch.randint(0, 16, (8,), device=gpu)
     taken = [0]
     orig = B._fold_ok
@@ -104,40 +105,40 @@ def test_bnfold_matches_unfolded_backward(gpu):
         ok = orig(*a)
         taken[0] += int(ok)
         return ok
-    prev = deterministic()
+    prev_fold = B._BN_FOLD[0]
     grads = []
     try:
-        set_deterministic(True)
         B._fold_ok = spy
-        for mode in (False, True, True):
+        for mode in (False, False, True, True):
             B._BN_FOLD[0] = mode
             m.zero_grad(set_to_none=True)
             softmax_cross_entropy(m(x), y).backward()
             grads.append({n: p.grad.detach().double().clone() for n, p in m.named_parameters()})
     finally:
-        B._BN_FOLD[0] = True
+        B._BN_FOLD[0] = prev_fold
         B._fold_ok = orig
-        set_deterministic(prev)
-    # conv1 of every block and conv3 of every block but the last (whose consumer, the pooling
-    # head, fuses nothing), both runs
-    assert taken[0] >= 2 * 11, taken
-    ref, fo, fo2 = grads
-    assert all(torch.equal(fo[n], fo2[n]) for n in fo), "folded backward not reproducible"
+    # the first stage's two conv1 units (64 channels), both prologue runs
+    assert taken[0] >= 2 * 2, taken
+
+    def flat(gd):
+        return torch.cat([v.flatten() for v in gd.values()])
+
+    def dist(a, b):
+        return ((a - b).norm() / b.norm()).item()
+    u0, u1, f0, f1 = (flat(g) for g in grads)
+    noise = max(dist(u0, u1), dist(f0, f1))
+    err = (dist(f0, u0) + dist(f1, u1)) / 2
+    assert err < 2.0 * noise + 0.005, (err, noise)
     # weights per tensor; BatchNorm affine gradients as each module's stacked [dgamma; dbeta] pair
-    # (the stem's dbeta is a sum over every stem position that nearly cancels: its own norm is no scale)
     groups = {}
-    for n in ref:
-        key = n.rsplit(".", 1)[0] + ".affine" if ref[n].dim() == 1 else n
+    for n in grads[0]:
+        key = n.rsplit(".", 1)[0] + ".affine" if grads[0][n].dim() == 1 else n
         groups.setdefault(key, []).append(n)
     bad = {}
-    num = den = 0.0
     for key, names in groups.items():
-        a = torch.cat([fo[n].flatten() for n in names])
-        b = torch.cat([ref[n].flatten() for n in names])
-        d, r = (a - b).norm().item(), b.norm().item()
-        num += d * d
-        den += r * r
-        if d > 0.02 * r + 1e-6:
-            bad[key] = d / max(r, 1e-12)
+        u0g, u1g, f0g, f1g = (torch.cat([g[n].flatten() for n in names]) for g in grads)
+        gnoise = max(dist(u0g, u1g), dist(f0g, f1g))
+        gerr = dist(f0g, u0g)
+        if gerr > 2.0 * gnoise + 0.03:
+            bad[key] = (gerr, gnoise)
     assert not bad, bad
-    assert (num / den) ** 0.5 < 0.005, (num / den) ** 0.5
