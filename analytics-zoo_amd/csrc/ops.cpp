@@ -3082,7 +3082,10 @@ torch::Tensor ncf_fused(torch::Tensor ids, std::vector<torch::Tensor> t, std::ve
   return partial;
 }
 
+void register_comm(py::module& m);   // comm.cpp
+
 PYBIND11_MODULE(_C, m) {
+  register_comm(m);
   m.doc() = "zoo native gfx950 (MI355X) kernel library";
   m.def("resize_normalize", &resize_normalize);
   m.def("jpeg_idct", &jpeg_idct);

@@ -51,7 +51,7 @@ def _sha(paths, extra=""):
 
 def source_files():
     """Every file a native build reads from the tree."""
-    pats = ["kernels/*.hip", "kernels/*.h", "ops.cpp", "runtime/*.cpp", "runtime/*.h"]
+    pats = ["kernels/*.hip", "kernels/*.h", "ops.cpp", "comm.cpp", "runtime/*.cpp", "runtime/*.h"]
     out = []
     for pat in pats:
         out += glob.glob(os.path.join(CSRC, pat))
@@ -131,11 +131,20 @@ def build_kernels(force=False, jobs=8, verbose=True, build_dir=None, pkg_dir=Non
     stamps.append(bstamp)
     if force or _stale(bobj, bstamp):
         todo.append((bobj, bstamp, bcmd))
+    # C++ comm layer (RCCL driven directly; the symbols resolve to torch's own librccl)
+    csrc = os.path.join(CSRC, "comm.cpp")
+    cobj = os.path.join(build_dir, "comm.cpp.o")
+    ccmd = bcmd[:-3] + ["-c", csrc, "-o", cobj]
+    cstamp = _sha([csrc], " ".join(ccmd[:-3]))
+    objs.append(cobj)
+    stamps.append(cstamp)
+    if force or _stale(cobj, cstamp):
+        todo.append((cobj, cstamp, ccmd))
     _compile_all(jobs, todo)
     out = os.path.join(pkg_dir, "_C" + _ext_suffix())
     link = [HIPCC, "--offload-arch=" + ARCH, "-shared", "-fPIC", "-o", out] + objs + \
         ["-L" + os.path.join(tdir, "lib"), "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
-         "-ltorch_python", "-Wl,-rpath," + os.path.join(tdir, "lib")]
+         "-ltorch_python", "-lrccl", "-Wl,-rpath," + os.path.join(tdir, "lib")]
     lstamp = hashlib.sha256(("".join(stamps) + " ".join(link[5:6])).encode()).hexdigest()
     if force or todo or _stale(out, lstamp):
         _run(link)

@@ -50,6 +50,12 @@ class ZooConfig:
     fault_inject_rank: int = -1          # ZOO_FAULT_INJECT_RANK: only this rank raises (-1: every rank)
     auto_resume: bool = False            # ZOO_AUTO_RESUME: fit() resumes from the latest checkpoint (launcher restarts)
     force_comm: bool = False             # ZOO_FORCE_COMM: run the collective path on a world-size-1 process group
+    # gradient-bucket collectives: "torch" = torch.distributed ProcessGroup calls; "native" = the
+    # C++ comm layer (csrc/comm.cpp: RCCL communicator of our own on GradSync's comm stream)
+    comm: str = "torch"                  # ZOO_COMM
+    # RCCL channels (CTAs) of the native communicator; 0 = RCCL's own choice. The 8 MI355X of a
+    # node are fully connected by 7 xGMI links each: one ring per link needs >= 7 channels
+    rccl_channels: int = 0               # ZOO_RCCL_CHANNELS
     # data
     num_workers: int = 4
     pin_memory: bool = True
@@ -70,7 +76,7 @@ class ZooConfig:
         "failure_retry_times": "ZOO_FAILURE_RETRY_TIMES", "failure_retry_interval_s": "ZOO_FAILURE_RETRY_INTERVAL",
         "fault_inject_step": "ZOO_FAULT_INJECT_STEP", "num_workers": "ZOO_NUM_WORKERS",
         "fault_inject_rank": "ZOO_FAULT_INJECT_RANK", "auto_resume": "ZOO_AUTO_RESUME",
-        "force_comm": "ZOO_FORCE_COMM",
+        "force_comm": "ZOO_FORCE_COMM", "comm": "ZOO_COMM", "rccl_channels": "ZOO_RCCL_CHANNELS",
         "pin_memory": "ZOO_PIN_MEMORY", "log_every": "ZOO_LOG_EVERY", "roctx": "ZOO_ROCTX", "seed": "ZOO_SEED",
         "phase_timing": "ZOO_PHASE_TIMING", "debug_sync": "ZOO_DEBUG_SYNC", "deterministic": "ZOO_DETERMINISTIC",
         "backend": "ZOO_DIST_BACKEND", "timeout_s": "ZOO_DIST_TIMEOUT",

@@ -147,7 +147,7 @@ class _Bucket:
 
 class GradSync:
     def __init__(self, flat: FlatParams, group=None, bucket_mb=16.0, mode="allreduce", overlap=True,
-                 compress=None, force_comm=False):
+                 compress=None, force_comm=False, comm="torch", rccl_channels=0):
         """``group``: the data-parallel process group (default: the world). With
         tensor parallelism it holds the ranks that share a tensor-parallel rank,
         so TP-sharded weights are only averaged over true replicas."""
@@ -165,6 +165,14 @@ class GradSync:
         self.is_cuda = flat.grad.is_cuda
         self.overlap = bool(overlap) and self.comm and self.is_cuda
         self.comm_stream = torch.cuda.Stream(device=flat.grad.device) if (self.is_cuda and self.comm) else None
+        # bucket collectives through the C++ comm layer (zoo/parallel/comm.py) instead of the
+        # ProcessGroup: same stream, same order, no per-call work objects
+        self.ncomm = None
+        if comm == "native" and self.comm and self.is_cuda:
+            from zoo.parallel.comm import NativeComm, native_comm_ok
+            if native_comm_ok(group):
+                with torch.cuda.device(flat.grad.device):
+                    self.ncomm = NativeComm(group, rccl_channels)
         self._lock = threading.Lock()
         self.src = dist.get_global_rank(group, 0) if (initialized and group is not None) else 0
         # -- buckets over contiguous parameter ranges ---------------------------
@@ -441,6 +449,9 @@ class GradSync:
             self._issue(b)
 
     def _a2a(self, out, inp):
+        if self.ncomm is not None:
+            self.ncomm.all_to_all(out, inp)
+            return
         if self.backend == "gloo":  # gloo has no all-to-all: gather every pack, keep our chunk of each
             parts = [torch.empty_like(inp) for _ in range(self.world)]
             dist.all_gather(parts, inp, group=self.group)
@@ -451,6 +462,9 @@ class GradSync:
         dist.all_to_all_single(out, inp, group=self.group)
 
     def _gather(self, out, mine):
+        if self.ncomm is not None:
+            self.ncomm.all_gather(out, mine)
+            return
         if self.backend == "gloo":
             parts = list(out.chunk(self.world))
             dist.all_gather(parts, mine, group=self.group)
@@ -458,6 +472,9 @@ class GradSync:
         dist.all_gather_into_tensor(out, mine, group=self.group)
 
     def _rs_fp32(self, out, inp):
+        if self.ncomm is not None:
+            self.ncomm.reduce_scatter(out, inp)
+            return
         if self.backend == "gloo":
             dist.all_reduce(inp, group=self.group)
             out.copy_(inp[self.rank * out.numel():(self.rank + 1) * out.numel()])
@@ -557,7 +574,10 @@ class GradSync:
                 for p, plo, phi in b.sparse:
                     self._row_sparse_allreduce(p, plo, phi)
                 return
-            dist.all_reduce(g, group=self.group)
+            if self.ncomm is not None:
+                self.ncomm.all_reduce(g)
+            else:
+                dist.all_reduce(g, group=self.group)
             return
         lo, hi = self._chunk(b)
         if self.compress:

@@ -187,7 +187,7 @@ class TrainingEngine:
         self.sync = GradSync(self.flat, group=self.dp_group, bucket_mb=bucket_mb or cfg.bucket_mb,
                              mode="sharded" if (cfg.sharded_optimizer if sharded is None else sharded)
                              else "allreduce", overlap=cfg.overlap_comm, compress=cfg.grad_compression or None,
-                             force_comm=cfg.force_comm)
+                             force_comm=cfg.force_comm, comm=cfg.comm, rccl_channels=cfg.rccl_channels)
         self.sync.broadcast_parameters()
         # gradient writes outside train_step (a user's own backward) mark the flat gradient dirty
         self.sync.engine_managed = True

@@ -18,3 +18,5 @@ for i in 1 2; do
   ZOO_SIDE_CUS=16 $T 200 python -u bench.py > gpurun_out/r5/b13_cu16_$i.log 2>&1 || exit 13
 done
 for f in gpurun_out/r5/b13_cu*_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f) $(grep -o '"final_loss": [0-9.]*' $f)"; done
+$T 600 python -u analytics-zoo_amd/tools/quant_bench.py --no-dynamic > gpurun_out/r5/b13_quant.log 2>&1 || exit 7
+tail -1 gpurun_out/r5/b13_quant.log | head -c 3000
