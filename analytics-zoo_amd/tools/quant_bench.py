@@ -35,6 +35,8 @@ def main():
     ap.add_argument("--no-dynamic", action="store_true")
     ap.add_argument("--train-steps", type=int, default=300)
     ap.add_argument("--task-hw", type=int, default=224, help="image size of the synthetic trained task")
+    ap.add_argument("--max-block-err", type=float, default=0.05,
+                    help="mixed precision: blocks whose calibrated int8 error exceeds this stay bf16")
     ap.add_argument("--under-steps", type=int, default=40,
                     help="steps of the under-trained model (lr 0.01: partly fitted)")
     a = ap.parse_args()
@@ -91,10 +93,18 @@ def main():
             rt = mt(xt).float()
             res["%s_input_sensitivity" % tag] = round(input_sensitivity(rt), 5)
             for fmt, cls in (("int8", Int8ResNet), ("fp8", Fp8ResNet)):
-                for sc, clip in (("channel", 0.0), ("channel", 1e-4), ("tensor", 0.0)):
-                    qo = cls(mt, cal, act_scales=sc, act_clip=clip)(xt).float()
+                for sc, clip, mix in (("channel", 0.0, None), ("channel", 1e-4, None), ("tensor", 0.0, None),
+                                      ("channel", 0.0, a.max_block_err)):
+                    qm = cls(mt, cal, act_scales=sc, act_clip=clip, max_block_err=mix)
+                    qo = qm(xt).float()
                     top1_t, cos_t = agreement(qo, rt)
-                    k = "%s_%s%s_%s" % (fmt, sc, "_clip%g" % clip if clip else "", tag)
+                    k = "%s_%s%s%s_%s" % (fmt, sc, "_clip%g" % clip if clip else "", "_mixed" if mix else "", tag)
+                    if mix is None and sc == "channel" and not clip:
+                        res["%s_%s_block_err" % (fmt, tag)] = [round(e, 4) for e in qm.block_err]
+                    if mix:
+                        res[k + "_bf16_blocks"] = sorted(qm.bf16_blocks)
+                        if fmt == "int8":
+                            res[k + "_img_s"] = round(a.batch / bench(qm, x, a.iters), 1)
                     res[k + "_top1_agree"] = round(top1_t, 4)
                     res[k + "_rowcos"] = round(cos_t, 4)
                     mt1, kept = margin_agreement(qo, rt)

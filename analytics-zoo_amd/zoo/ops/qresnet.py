@@ -116,6 +116,11 @@ def quantize_act(x, scale, fmt="int8"):
     return _sat(x.double() / s).to(torch.int8)
 
 
+def _dequant(xq, s):
+    """int8 / e4m3 NHWC -> fp32 with a per-tensor float or per-channel [C] scale."""
+    return xq.float() * (s.float().to(xq.device) if torch.is_tensor(s) else s)
+
+
 class _QUnit:
     """One conv unit: quantized weights and the epilogue constants for given in/out scales
     (floats: per tensor; [C] tensors: per channel)."""
@@ -158,11 +163,18 @@ class Int8ResNet(nn.Module):
     act_scales = "channel"
     act_clip = 0.0
 
-    def __init__(self, model, calib_x, fmt=None, act_scales=None, act_clip=None):
+    def __init__(self, model, calib_x, fmt=None, act_scales=None, act_clip=None, bf16_blocks=(), max_block_err=None):
         """``act_scales``: "channel" (one activation scale per channel) or "tensor" (one per tensor).
         ``act_clip``: fraction of each channel's calibration values allowed to saturate (0: absmax;
-        e.g. 1e-4 keeps a few spatial outliers from stretching the channel's int8 grid)."""
+        e.g. 1e-4 keeps a few spatial outliers from stretching the channel's int8 grid).
+        Mixed precision (TensorRT-style per-layer fallback): ``bf16_blocks`` -- indices of residual
+        blocks that stay on the bf16 kernels; ``max_block_err`` -- additionally keep in bf16 every
+        block whose calibrated local error (relative L2 of its quantized output against bf16, fed
+        the same input; ``block_err``) exceeds this. Activations are dequantised / requantised at
+        the boundaries."""
         super().__init__()
+        self.bf16_blocks = set(int(i) for i in bf16_blocks)
+        self.max_block_err = max_block_err
         if act_clip is not None:
             self.act_clip = float(act_clip)
         from zoo.models.image import resnet as R
@@ -223,6 +235,7 @@ class Int8ResNet(nn.Module):
         h = self._stem(x)
         self.s_in = amax(h)
         s_x = self.s_in
+        self.block_err = []
         for blk, u in self.blocks:
             sc = blk.down(h) if blk.down is not None else h
             s_sc = amax(sc) if blk.down is not None else s_x
@@ -244,22 +257,40 @@ class Int8ResNet(nn.Module):
             if "down" in u:
                 u["down"].bind(s_x, s_sc)
             blk._q_scales = (s_x, s_sc, s_o)
+            # the block's own quantization error: its quantized run on the bf16 input vs bf16
+            oq = _dequant(self._run_block(u, quantize_act(h, s_x, self.fmt), s_sc), s_o)
+            of = out.float()
+            self.block_err.append(float((oq - of).norm() / of.norm().clamp_min(1e-12)))
             h, s_x = out, s_o
         self.s_out = s_x
+        if self.max_block_err is not None:
+            self.bf16_blocks |= {i for i, e in enumerate(self.block_err) if e > self.max_block_err}
         return self
+
+    def _run_block(self, u, xq, s_sc):
+        sc = u["down"](xq) if "down" in u else xq
+        h1 = u["conv1"](xq)
+        if "conv3" in u:
+            return u["conv3"](u["conv2"](h1), resid=sc, s_resid=s_sc)
+        return u["conv2"](h1, resid=sc, s_resid=s_sc)
 
     @torch.no_grad()
     def forward(self, x):
         h = self._stem(x)
-        xq = quantize_act(h, self.s_in, self.fmt)
-        for blk, u in self.blocks:
+        xq = None                     # quantized activation (None: h is the bf16 one)
+        for i, (blk, u) in enumerate(self.blocks):
             s_x, s_sc, s_o = blk._q_scales
-            sc = u["down"](xq) if "down" in u else xq
-            h1 = u["conv1"](xq)
-            if "conv3" in u:
-                xq = u["conv3"](u["conv2"](h1), resid=sc, s_resid=s_sc)
-            else:
-                xq = u["conv2"](h1, resid=sc, s_resid=s_sc)
+            if i in self.bf16_blocks:
+                if xq is not None:
+                    h, xq = _dequant(xq, s_x).to(torch.bfloat16), None
+                h = blk(h)
+                continue
+            if xq is None:
+                xq = quantize_act(h, s_x, self.fmt)
+            xq = self._run_block(u, xq, s_sc)
+        if xq is None:                # the last block ran in bf16
+            from zoo import ops
+            return self.model.fc(ops.global_avg_pool_nhwc(h))
         vec = torch.is_tensor(self.s_out)
         if xq.is_cuda:
             feat = native().gap_i8(xq.contiguous(), 1.0, self.s_out.float().contiguous()) if vec else \

@@ -359,18 +359,25 @@ class ConvLSTM2D(Layer):
         wx, cpx = self._packed(Wx)
         wh, cph = self._packed(Wh)
         bias = F.pad(b, (0, ops.ceil8(K) - K)).float()
-        xn = x.reshape(B * T, C, H, W).permute(0, 2, 3, 1)
+        seq = _CONVLSTM_SEQ and K % 8 == 0 and ops.ceil8(K) == wh.shape[0]
+        if seq:
+            # time-major in processing order already at the (small) input: the input conv then
+            # writes the [T, M, K] gate inputs the sequence kernels read, no gate-tensor permute
+            xt = x.transpose(0, 1)
+            if self.go_backwards:
+                xt = xt.flip(0)
+            xn = xt.reshape(T * B, C, H, W).permute(0, 2, 3, 1)
+        else:
+            xn = x.reshape(B * T, C, H, W).permute(0, 2, 3, 1)
         if cpx != C:
             xn = F.pad(xn, (0, cpx - C))
         xs = ops.conv2d_nhwc(xn, wx, bias, kernel=(R, S), stride=self.subsample, pad=pad, out_f32=True)[..., :K]
         Ho, Wo = xs.shape[1], xs.shape[2]
         from zoo.ops.layers import ACT_CODES
-        if _CONVLSTM_SEQ and K % 8 == 0 and ops.ceil8(K) == wh.shape[0]:
+        if seq:
             # whole-sequence path: time-major gate inputs in processing order, one autograd node
             M = B * Ho * Wo
-            gxs = xs.reshape(B, T, Ho * Wo, K).permute(1, 0, 2, 3).reshape(T, M, K)
-            if self.go_backwards:
-                gxs = gxs.flip(0)
+            gxs = xs.reshape(T, M, K)
             fn = _ConvLSTMFusedFn if fused else _ConvLSTMSeqFn
             hs = fn.apply(gxs.contiguous(), wh, B, Ho, Wo, f, cph, R, S,
                                       ACT_CODES[self.inner_activation], ACT_CODES[self.activation],
@@ -509,10 +516,16 @@ class ConvLSTM3D(Layer):
         K = 4 * f
         p = k // 2
         cp, fp, kp = (-C) % 8, (-f) % 8, (-K) % 8
-        xn = x.reshape(B * T, C, *sp).permute(0, 2, 3, 4, 1)
-        xn = F.pad(xn, (0, cp)).to(torch.bfloat16)
         # gate-interleaved one-launch-per-step path (convlstm.hip) up to 64 filters
         il = _CONVLSTM_SEQ and _CONVLSTM_FUSED and f <= 64 and K % 8 == 0
+        if il:   # time-major in processing order at the input (see ConvLSTM2D)
+            xt = x.transpose(0, 1)
+            if self.go_backwards:
+                xt = xt.flip(0)
+            xn = xt.reshape(T * B, C, *sp).permute(0, 2, 3, 4, 1)
+        else:
+            xn = x.reshape(B * T, C, *sp).permute(0, 2, 3, 4, 1)
+        xn = F.pad(xn, (0, cp)).to(torch.bfloat16)
         Wx, Whp, b = self.Wx, self.Wh, self.b
         if il:
             perm = _gate_perm(f, x.device)
@@ -526,9 +539,7 @@ class ConvLSTM3D(Layer):
         M = B * P
         if il:
             # whole sequence, one launch per step: time-major gate inputs in processing order
-            gxs = xs.reshape(B, T, P, K).permute(1, 0, 2, 3).reshape(T, M, K)
-            if self.go_backwards:
-                gxs = gxs.flip(0)
+            gxs = xs.reshape(T, M, K)
             hs = _ConvLSTM3DFusedFn.apply(gxs.contiguous(), Whp, B, osp[0], osp[1], osp[2], f, k,
                                           bool(self.return_sequences))
             if self.return_sequences:

@@ -67,6 +67,30 @@ def test_int8_resnet_tracks_bf16_model(gpu, trained_resnet50):
     assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
 
 
+def test_int8_mixed_precision_blocks(gpu, trained_resnet50):
+    """Per-block bf16 fallback: the calibrated per-block error is reported for every residual
+    block, chosen blocks run on the bf16 kernels between dequantise / requantise boundaries, and
+    with every block in bf16 the twin reproduces the bf16 model (only the stem / classifier path
+    is shared)."""
+    from zoo.ops.qresnet import Int8ResNet
+    from zoo.utils.synthetic import agreement, sample
+    m, T = trained_resnet50
+    calib, _ = sample(T, 64, seed=11)
+    x, _ = sample(T, 128, seed=12)
+    with torch.no_grad():
+        ref = m(x).float()
+    q = Int8ResNet(m, calib, bf16_blocks=(0, 7, 15))
+    assert len(q.block_err) == 16 and all(0 < e < 0.5 for e in q.block_err), q.block_err
+    with torch.no_grad():
+        top1, cos = agreement(q(x).float(), ref)
+    assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
+    qa = Int8ResNet(m, calib, max_block_err=0.0)          # every block above 0 -> all bf16
+    assert qa.bf16_blocks == set(range(16))
+    with torch.no_grad():
+        out = qa(x).float()
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+
+
 def test_inference_model_static_int8_with_hipgraph(gpu):
     """InferenceModel.load_module(blas=False, calib_data=...) serves the calibrated int8
     twin through the hipGraph replica path; predictions track the bf16 model."""
