@@ -53,7 +53,7 @@ struct CLArgs {
 };
 
 constexpr int CL_WAVES = 4;   // 4 waves x 16 pixels per workgroup
-constexpr int CL_PF = 4;      // activation chunks in flight per wave
+constexpr int CL_PF = 8;      // activation chunks in flight per wave
 
 ZOO_DEV int cl_kdp(int KD) { return (KD + 31) / 32 * 32 + 8; }   // LDS row pitch (+16 B: conflict-free)
 
@@ -115,12 +115,27 @@ template <int NI>
 ZOO_DEV void cl_stage(const CLArgs& a, bf16_t* wl) {
   if (!a.X) return;
   const int KD = a.Q * a.R * a.S * a.Cx, kdp = cl_kdp(KD);
-  const int per_row = kdp / 8;
-  for (int e = threadIdx.x; e < 16 * NI * per_row; e += blockDim.x) {
-    const int n = e / per_row, k = (e - n * per_row) * 8;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (n < a.Nr && k < KD) v = *reinterpret_cast<const uint4*>(a.Wt + (size_t)n * a.ldw + k);
-    *reinterpret_cast<uint4*>(wl + (size_t)n * kdp + k) = v;
+  const int per_row = kdp / 8, total = 16 * NI * per_row;
+  // batches of 8 independent 16-byte loads in flight per thread before their LDS stores (a
+  // load-store-load loop would pay one L2 round trip per element: ~20 us for 73 KB)
+  constexpr int BATCH = 8;
+  const bf16_t* Wt = a.Wt;
+  const int ldw = a.ldw, Nr = a.Nr;
+  for (int e0 = threadIdx.x; e0 < total; e0 += BATCH * blockDim.x) {
+    uint4 v[BATCH];
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int e = e0 + u * blockDim.x;
+      const int n = e / per_row, k = (e - n * per_row) * 8;
+      v[u] = e < total && n < Nr && k < KD ? *reinterpret_cast<const uint4*>(Wt + (size_t)n * ldw + k)
+                                           : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < BATCH; ++u) {
+      const int e = e0 + u * blockDim.x;
+      const int n = e / per_row, k = (e - n * per_row) * 8;
+      if (e < total) *reinterpret_cast<uint4*>(wl + (size_t)n * kdp + k) = v[u];
+    }
   }
   __syncthreads();
 }

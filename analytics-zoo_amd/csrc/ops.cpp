@@ -795,13 +795,16 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.Ktot = R * S * g.C;
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
-  // 1x1 stride-1 convs with >= 128 input and output channels (and up to 2^18 pixels) are plain
+  // 1x1 stride-1 convs with >= 128 input and output channels (and up to 2^20 pixels) are plain
   // GEMMs where the 256x256-tile kernel (wgrad256.hip) beats the implicit-GEMM wgrad
-  // (tools/wgrad_bench.py --resnet: 1.1-1.6x; at 802816 pixels the 128-row tiles win)
+  // (tools/wgrad_bench.py --resnet: 1.1-1.6x). At 802816 pixels (the stage-1 1x1 convs) the
+  // 128-row tiles win in isolation, but inside the training step -- on the side stream beside
+  // the data-gradient chain -- the 256-wide kernel wins: +0.3-0.45 % images/s over five same-box
+  // pairs (profiles/r5/ab_wgrad256_mmax_r5.log), so the limit is 2^20 since round 5
   static const bool use256 = env_flag("ZOO_WGRAD256", true);
   static const long long m_max = [] {
     const char* e = getenv("ZOO_WGRAD256_MMAX");
-    return e ? atoll(e) : (1LL << 18);
+    return e ? atoll(e) : (1LL << 20);
   }();
   static const int c_min = [] {
     const char* e = getenv("ZOO_WGRAD256_CMIN");

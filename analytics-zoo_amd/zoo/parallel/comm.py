@@ -44,8 +44,8 @@ class NativeComm:
     def broadcast(self, t, root=0):
         self._m.comm_broadcast(self.h, t, root)
 
-    def group(self):
-        """``with comm.group():`` fuses the enclosed collectives into one RCCL launch group."""
+    def fused(self):
+        """``with comm.fused():`` fuses the enclosed collectives into one RCCL launch group."""
         return _Group(self._m)
 
     def close(self):

@@ -21,3 +21,19 @@ tail -3 gpurun_out/r5/b14_qtests.log
 [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 $T 600 python -u analytics-zoo_amd/tools/quant_bench.py --no-dynamic > gpurun_out/r5/b14_quant.log 2>&1 || exit 7
 tail -1 gpurun_out/r5/b14_quant.log | head -c 4000
+$T 200 python -u analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 20 > gpurun_out/r5/b15_bert_eager.log 2>&1 || exit 3
+tail -1 gpurun_out/r5/b15_bert_eager.log
+$T 200 python -u analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 20 --graph > gpurun_out/r5/b15_bert_graph.log 2>&1 || exit 4
+tail -1 gpurun_out/r5/b15_bert_graph.log
+for q in 2 4 8; do
+  DEBUG_HIP_FORCE_GRAPH_QUEUES=$q $T 200 python -u analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 20 --graph > gpurun_out/r5/b15_bert_graph_q$q.log 2>&1 || exit 5
+  echo "queues $q: $(tail -1 gpurun_out/r5/b15_bert_graph_q$q.log)"
+done
+DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 $T 200 python -u analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 20 --graph > gpurun_out/r5/b15_bert_graph_nopkt.log 2>&1 || exit 6
+echo "no packet capture: $(tail -1 gpurun_out/r5/b15_bert_graph_nopkt.log)"
+for i in 1 2; do
+  $T 200 python -u bench.py > gpurun_out/r5/b14_def_$i.log 2>&1 || exit 20
+  ZOO_WGRAD256_MMAX=1048576 $T 200 python -u bench.py > gpurun_out/r5/b14_mmax_$i.log 2>&1 || exit 21
+  ZOO_WGRAD256_MMAX=1048576 ZOO_WGRAD256_CMIN=64 $T 200 python -u bench.py > gpurun_out/r5/b14_cmin_$i.log 2>&1 || exit 22
+done
+for f in gpurun_out/r5/b14_{def,mmax,cmin}_*.log; do echo "$f $(grep -o '"value": [0-9.]*' $f)"; done

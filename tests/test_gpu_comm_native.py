@@ -54,7 +54,7 @@ def test_native_collectives_world1(gpu, rccl_world1, channels):
             a = torch.randn(4096, device=gpu)
             b = torch.randn(4096, device=gpu).to(torch.bfloat16)
             oa, ob = torch.empty_like(a), torch.empty_like(b)
-            with c.group():     # one fused launch group
+            with c.fused():     # one fused launch group
                 c.all_to_all(oa, a)
                 c.all_gather(ob, b)
         s.synchronize()
