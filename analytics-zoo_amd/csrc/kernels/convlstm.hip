@@ -53,9 +53,11 @@ struct CLArgs {
 };
 
 constexpr int CL_WAVES = 4;   // 4 waves x 16 pixels per workgroup
-constexpr int CL_PF = 8;      // activation chunks in flight per wave
+constexpr int CL_PF = 4;      // activation chunks in flight per wave
 
-ZOO_DEV int cl_kdp(int KD) { return (KD + 31) / 32 * 32 + 8; }   // LDS row pitch (+16 B: conflict-free)
+// reduction chunks of 32, padded to whole prefetch groups (the padding is zero in LDS and never loaded)
+ZOO_DEV int cl_kcp(int KD) { return ((KD + 31) / 32 + CL_PF - 1) / CL_PF * CL_PF; }
+ZOO_DEV int cl_kdp(int KD) { return cl_kcp(KD) * 32 + 8; }   // LDS row pitch (+16 B: conflict-free)
 
 // acc[i] (rows 16 i .. 16 i + 15, this lane's pixel m) = W[rows] . X_patch(m)
 // LDSW: the workgroup's weights staged once in LDS (rows padded to cl_kdp); else read from L2
@@ -73,38 +75,52 @@ ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane, const b
   const uint4 z4 = make_uint4(0u, 0u, 0u, 0u);
   const bf16_t* X = a.X;
   const int Cx = a.Cx, RS = a.R * a.S, S = a.S, D = a.D, H = a.H, Wd = a.Wd;
+  // branch-free: every lane loads from an in-bounds address (clamped) and zeroes the value when
+  // the tap is outside the image / reduction -- a predicated load in a divergent branch made the
+  // compiler wait for ALL outstanding loads (vmcnt(0)) before each chunk, serialising the prefetch
   auto load_act = [=](int c) -> uint4 {
-    const int k = c * 32 + kq;
-    if (!mok || c >= KC || k >= KD) return z4;
+    int k = c * 32 + kq;
+    const bool kin = mok && c < KC && k < KD;
+    k = kin ? k : 0;
     const int tap = k / Cx, ch = k - tap * Cx;
     const int q = tap / RS, rs = tap - q * RS;
     const int r = rs / S, s = rs - r * S;
     const int zz = z + q - pq, yy = y + r - ph, xx = x + s - pw;
-    if (zz < 0 || zz >= D || yy < 0 || yy >= H || xx < 0 || xx >= Wd) return z4;
-    return *reinterpret_cast<const uint4*>(X + ((((size_t)b * D + zz) * H + yy) * Wd + xx) * Cx + ch);
+    const bool ok = kin && zz >= 0 && zz < D && yy >= 0 && yy < H && xx >= 0 && xx < Wd;
+    const int zc = ok ? zz : z, yc = ok ? yy : y, xc = ok ? xx : x;
+    const uint4 v = *reinterpret_cast<const uint4*>(X + ((((size_t)b * D + zc) * H + yc) * Wd + xc) * Cx + ch);
+    return ok ? v : z4;
   };
   uint4 pre[CL_PF];
 #pragma unroll
   for (int u = 0; u < CL_PF; ++u) pre[u] = load_act(u);
-  for (int c0 = 0; c0 < KC; c0 += CL_PF) {
+  // whole prefetch groups (chunks past KC read zeros): a straight-line body, so the in-order
+  // vmcnt waits only for the chunk being consumed
+  const int KCp = cl_kcp(KD);
+  for (int c0 = 0; c0 < KCp; c0 += CL_PF) {
 #pragma unroll
     for (int u = 0; u < CL_PF; ++u) {
       const int c = c0 + u;
-      if (c < KC) {
+      {
         const bf16x8 bv = __builtin_bit_cast(bf16x8, pre[u]);
-        pre[u] = load_act(c + CL_PF);
         const int k = c * 32 + kq;
+        uint4 wv[NI];   // every row block's weight fragment first (one LDS wait), then the MFMAs
 #pragma unroll
         for (int i = 0; i < NI; ++i) {
           const int n = 16 * i + nr;
-          uint4 wv = z4;
           if (LDSW) {
-            wv = *reinterpret_cast<const uint4*>(wl + (size_t)n * kdp + k);   // zero padded rows / k
-          } else if (n < a.Nr && k < KD) {
-            wv = *reinterpret_cast<const uint4*>(a.Wt + (size_t)n * a.ldw + k);
+            wv[i] = *reinterpret_cast<const uint4*>(wl + (size_t)n * kdp + k);   // zero padded rows / k
+          } else {
+            const bool ok = n < a.Nr && k < KD;
+            const uint4 t = *reinterpret_cast<const uint4*>(a.Wt + (size_t)(ok ? n : 0) * a.ldw + (ok ? k : 0));
+            wv[i] = ok ? t : z4;
           }
-          acc[i] = mfma16(__builtin_bit_cast(bf16x8, wv), bv, acc[i]);
         }
+        __builtin_amdgcn_sched_barrier(0);   // keep the fragment reads batched ahead of the MFMAs
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[i] = mfma16(__builtin_bit_cast(bf16x8, wv[i]), bv, acc[i]);
+        // refill this slot after its use: the in-order vmcnt then waits only for this chunk's load
+        pre[u] = load_act(c + CL_PF);
       }
     }
   }
@@ -140,26 +156,40 @@ ZOO_DEV void cl_stage(const CLArgs& a, bf16_t* wl) {
   __syncthreads();
 }
 
+// The epilogue operands do not depend on the GEMM: they are loaded BEFORE it (every lane, clamped
+// addresses, no branch) so their latency hides behind the reduction; loading them between the
+// stores of the epilogue made each channel wait for its own round trip (the stores may alias the
+// loads): 11 us of a 23 us step.
 template <int NI, bool LDSW>
 __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_fwd_kernel(CLArgs a) {
   extern __shared__ __attribute__((aligned(16))) char cl_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
-  if (LDSW) cl_stage<NI>(a, wl);
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
+  const int mc = m < a.M ? m : a.M - 1, F = a.F;
+  const float* __restrict__ gx = a.gx;
+  const float* __restrict__ cprev = a.cprev;
+  float4 g4[NI];
+  float cp[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int j = 4 * i + (lane >> 4);   // rows 16 i + 4 (lane >> 4) + q = gate q of channel j
+    const size_t e = (size_t)mc * F + (j < F ? j : F - 1);
+    g4[i] = *reinterpret_cast<const float4*>(gx + 4 * e);
+    cp[i] = cprev ? cprev[e] : 0.f;
+  }
+  if (LDSW) cl_stage<NI>(a, wl);
   f32x4 acc[NI];
   cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
   if (m >= a.M) return;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
-    const int j = 4 * i + (lane >> 4);   // rows 16 i + 4 (lane >> 4) + q = gate q of channel j
-    if (j >= a.F) continue;
-    const size_t e = (size_t)m * a.F + j;
-    const float4 g4 = *reinterpret_cast<const float4*>(a.gx + 4 * e);
-    const float ig = lstm_act(acc[i][0] + g4.x, a.iact), fg = lstm_act(acc[i][1] + g4.y, a.iact);
-    const float cg = lstm_act(acc[i][2] + g4.z, a.act), og = lstm_act(acc[i][3] + g4.w, a.iact);
-    const float cp = a.cprev ? a.cprev[e] : 0.f;
-    const float cn = fg * cp + ig * cg;
+    const int j = 4 * i + (lane >> 4);
+    if (j >= F) continue;
+    const size_t e = (size_t)m * F + j;
+    const float ig = lstm_act(acc[i][0] + g4[i].x, a.iact), fg = lstm_act(acc[i][1] + g4[i].y, a.iact);
+    const float cg = lstm_act(acc[i][2] + g4[i].z, a.act), og = lstm_act(acc[i][3] + g4[i].w, a.iact);
+    const float cn = fg * cp[i] + ig * cg;
     const float hn = og * lstm_act(cn, a.act);
     a.c[e] = cn;
     a.h[e] = hn;
@@ -168,35 +198,64 @@ __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_fwd_kernel(CLArgs a) {
   }
 }
 
+// backward: operands of every (row block, channel) up front while NI <= 4 (the data-gradient rows
+// are the hidden channels: <= 64); wider row counts load them per row block
 template <int NI, bool LDSW>
 __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_bwd_kernel(CLArgs a) {
   extern __shared__ __attribute__((aligned(16))) char cl_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
-  if (LDSW) cl_stage<NI>(a, wl);
+  constexpr bool PRE = NI <= 4;
+  constexpr int NP = PRE ? NI : 1;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
+  const int mc = m < a.M ? m : a.M - 1, F = a.F;
+  const float* __restrict__ acts = a.acts;
+  const float* __restrict__ cc = a.cc;
+  const float* __restrict__ dout = a.dout;
+  const float* __restrict__ cprev = a.cprev;
+  const float* __restrict__ dcin = a.dc_in ? a.dc : nullptr;
+  float4 av[NP][4];
+  float cv[NP][4], ov[NP][4], dv[NP][4], pv[NP][4];
+  auto load_ops = [&](int i, int slot) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int j = 16 * i + 4 * (lane >> 4) + q;   // row = hidden channel of the data gradient
+      const size_t e = (size_t)mc * F + (j < F ? j : F - 1);
+      av[slot][q] = *reinterpret_cast<const float4*>(acts + 4 * e);
+      cv[slot][q] = cc[e];
+      ov[slot][q] = dout ? dout[e] : 0.f;
+      dv[slot][q] = dcin ? dcin[e] : 0.f;
+      pv[slot][q] = cprev ? cprev[e] : 0.f;
+    }
+  };
+  if constexpr (PRE) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) load_ops(i, i);
+  }
+  if (LDSW) cl_stage<NI>(a, wl);
   f32x4 acc[NI];
   cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
   if (m >= a.M) return;
 #pragma unroll
   for (int i = 0; i < NI; ++i) {
+    const int slot = PRE ? i : 0;
+    if constexpr (!PRE) load_ops(i, 0);
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int j = 16 * i + 4 * (lane >> 4) + q;   // row = hidden channel of the data gradient
-      if (j >= a.F) continue;
-      const size_t e = (size_t)m * a.F + j;
-      const float4 g4 = *reinterpret_cast<const float4*>(a.acts + 4 * e);
-      const float ig = g4.x, fg = g4.y, cg = g4.z, og = g4.w;
-      const float tc = lstm_act(a.cc[e], a.act);
-      const float dh = acc[i][q] + (a.dout ? a.dout[e] : 0.f);
-      const float dcv = dh * og * lstm_dact(tc, a.act) + (a.dc_in ? a.dc[e] : 0.f);
-      const float cp = a.cprev ? a.cprev[e] : 0.f;
+      const int j = 16 * i + 4 * (lane >> 4) + q;
+      if (j >= F) continue;
+      const size_t e = (size_t)m * F + j;
+      const float ig = av[slot][q].x, fg = av[slot][q].y, cg = av[slot][q].z, og = av[slot][q].w;
+      const float tc = lstm_act(cv[slot][q], a.act);
+      const float dh = acc[i][q] + ov[slot][q];
+      const float dcv = dh * og * lstm_dact(tc, a.act) + dv[slot][q];
+      const float cp = pv[slot][q];
       const float d0 = dcv * cg * lstm_dact(ig, a.iact), d1 = dcv * cp * lstm_dact(fg, a.iact);
       const float d2 = dcv * ig * lstm_dact(cg, a.act), d3 = dh * tc * lstm_dact(og, a.iact);
       *reinterpret_cast<float4*>(a.dg + 4 * e) = make_float4(d0, d1, d2, d3);
       *reinterpret_cast<uint2*>(a.dgb + (size_t)m * a.ldg + 4 * j) =
           make_uint2((uint32_t)f2bf(d0) | ((uint32_t)f2bf(d1) << 16), (uint32_t)f2bf(d2) | ((uint32_t)f2bf(d3) << 16));
-      a.dc[e] = dcv * fg;   // same lane read dc_{t+1}[e] above: in place
+      a.dc[e] = dcv * fg;   // this lane read dc_{t+1}[e] before: in place
     }
   }
 }
@@ -208,7 +267,11 @@ template <int NI, bool LDSW>
 static hipError_t cl_launch2(const CLArgs& a, int bwd, size_t smem, hipStream_t st) {
   const dim3 grid((a.M + 16 * CL_WAVES - 1) / (16 * CL_WAVES));
   auto kf = bwd ? &convlstm_bwd_kernel<NI, LDSW> : &convlstm_fwd_kernel<NI, LDSW>;
-  if (LDSW) hipFuncSetAttribute(reinterpret_cast<const void*>(kf), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  if (LDSW) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kf),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(kf, grid, dim3(64 * CL_WAVES), LDSW ? smem : 0, st, a);
   return hipGetLastError();
 }
@@ -216,7 +279,7 @@ static hipError_t cl_launch2(const CLArgs& a, int bwd, size_t smem, hipStream_t 
 template <int NI>
 static hipError_t cl_launch(const CLArgs& a, int bwd, hipStream_t st) {
   const int KD = a.Q * a.R * a.S * a.Cx;
-  const size_t smem = (size_t)16 * NI * ((KD + 31) / 32 * 32 + 8) * 2;
+  const size_t smem = (size_t)16 * NI * ((((KD + 31) / 32 + CL_PF - 1) / CL_PF * CL_PF) * 32 + 8) * 2;
   if (a.X && smem <= CL_LDS_MAX) return cl_launch2<NI, true>(a, bwd, smem, st);
   return cl_launch2<NI, false>(a, bwd, 0, st);
 }

@@ -865,7 +865,13 @@ static int i2_choose(const ConvGeom& g, int epi) {
   const int f = i2_tile_force();
   if (f > 0 && !i2_is_band(f)) return f;
   auto tiles = [&](int t) { return i2_tiles_m(g, t) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
-  if (g.K < 256) return 0;
+  // narrowest output the large-tile kernel takes (ZOO_I2_KMIN; the 128x128 tile serves 128-wide
+  // outputs such as the ResNet stage-2 3x3 convs when set to 128)
+  static const int kmin = [] {
+    const char* e = getenv("ZOO_I2_KMIN");
+    return e ? atoi(e) : 256;
+  }();
+  if (g.K < kmin) return 0;
   if (epi == 4) {
     // GELU-backward dgrad (BERT FFN): ZOO_I2_GELU_TILE picks its tile (A/B of the 128x128
     // tile, whose EPI 2 prefetches the next slice's pre-activation, against 256x256)
