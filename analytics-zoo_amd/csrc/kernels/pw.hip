@@ -38,7 +38,7 @@
 // Epilogues: EPI 1 = bf16 output + BN statistics of the stored values (the forward of every
 // conv->BN unit); EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
 // and the producer's fused BN-backward sums (sum dy, sum dy * xhat).
-// Prologue (PRO, EPI 2, K = 64): the activation operand is the unit's OWN BN backward,
+// Prologue (PRO, EPI 2, K = 64 / 128): the activation operand is the unit's OWN BN backward,
 // dy = A g + B y + Cc, formed in the operand registers from the masked gradient g and the unit's
 // pre-BN output y as they arrive (per-channel A | B | Cc in LDS); channel group 0 also writes dy
 // for the weight gradient (bnfold.hip: the separate BN-backward apply pass and the re-read of dy
@@ -386,10 +386,14 @@ template <int EPI, bool PRO>
 static hipError_t pw_dispatch(const ConvGeom& g, int NP, const bf16_t* X, const bf16_t* W, bf16_t* Y,
                               const bf16_t* resid, float* stats, const BwdStats& bs, hipStream_t st) {
   const int K = g.Ktot;
-  // operand + y fragments of a double-buffered tile in registers: spill-free only at K = 64
-  // (K = 128 / 256 spilled 32-308 bytes per lane and ran 1.1-3.3x slower than apply + plain
-  // dgrad, profiles/r5/ab_bn_prologue_r5.md)
-  if (PRO && K > 64) return hipErrorNotSupported;
+  // operand + y fragments of a double-buffered tile in registers: spill-free at K = 64, and at
+  // K = 128 with 64-channel groups and 16-pixel tiles (198 VGPRs); K = 256 spills 108-308 bytes
+  // per lane and ran 1.1-3.3x slower than apply + plain dgrad (profiles/r5/ab_bn_prologue_r5.md)
+  if (PRO && K > 128) return hipErrorNotSupported;
+  if constexpr (PRO) {
+    if (K == 128) return NP == 64 ? pw_launch<64, 16, 4, EPI, PRO>(g, X, W, Y, resid, stats, bs, st)
+                                  : hipErrorNotSupported;
+  }
 #define PW_CASE(np, k, TPM)                                                                    \
   if constexpr (!PRO || (k) <= 64) {                                                           \
     if (NP == np && K == k) return pw_launch<np, TPM, k / 32, EPI, PRO>(g, X, W, Y, resid, stats, bs, st); \
@@ -436,15 +440,16 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
   // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
   if (route == 1 && g->Ktot > 256) return 0;
-  // the BN-backward prologue keeps operand and y fragments of a K = 64 tile in registers
-  if (bs && bs->pro_y && (route != 2 || g->Ktot > 64)) return 0;
+  // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
+  if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
 }
 
 extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
-  const int NP = pw_np(g->K, g->Ktot);
+  // the prologue at K = 128 runs 64-channel groups (register budget, see pw_dispatch)
+  const int NP = (bs.pro_y && g->Ktot == 128 && g->K % 64 == 0) ? 64 : pw_np(g->K, g->Ktot);
   if (epi == 1)
     return pw_dispatch<1, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (bs.pro_y)

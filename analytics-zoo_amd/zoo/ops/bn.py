@@ -42,13 +42,15 @@ _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
 # re-read of dy (6 instead of 8 bytes per element). Shapes the prologue kernel does not take get
 # dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B: profiles/r5/ab_bn_prologue_r5.md).
 _BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
+# unit widths taken by the prologue (ZOO_BN_FOLD_K="64,128")
+_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
 
 
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
-    # K = 64: the only width whose prologue tile stays spill-free in registers (pw.hip PRO); wider
+    # K = 64 / 128: the widths whose prologue tile stays spill-free in registers (pw.hip PRO); wider
     # units and the deterministic mode (partial statistics: no pw) keep bn_bwd_apply
     return (_BN_FOLD[0] and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
-            and not getattr(ctx, "sync", False) and K == 64 and Cin % 64 == 0
+            and not getattr(ctx, "sync", False) and K in _PRO_K and Cin % 64 == 0
             and gamma.dtype == torch.float32 and gamma.is_contiguous() and not _deterministic())
 
 
