@@ -803,6 +803,9 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
                                  hipStream_t st);
 
 extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs);
+extern "C" int zoo_pw_stem_eligible(const ConvGeom* g, int route);
+extern "C" hipError_t zoo_pw_stem(const void* X, const void* W, void* Y, float* stats, const ConvGeom* g,
+                                  hipStream_t st);
 extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st);
 
@@ -829,6 +832,12 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
     const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats);
     const int route = igemm_route_epi(epi, bsp && bsp->zgelu);
     if (zoo_pw_eligible(g, route, bsp)) return zoo_pw(X, W, Y, resid, stats, g, epi, bsp, st);
+    // the space-to-depth ResNet stem (4x4, 16 -> 64) on the same persistent kernel with a gathered operand
+    static const bool stem_on = [] {
+      const char* e = getenv("ZOO_PW_STEM");
+      return e ? atoi(e) != 0 : true;
+    }();
+    if (stem_on && !(bsp && bsp->sums) && zoo_pw_stem_eligible(g, route)) return zoo_pw_stem(X, W, Y, stats, g, st);
   }
   // whole-64-channel K-tiles: the large-tile second-generation kernel (igemm2.hip)
   if (zoo_igemm2_eligible(g, igemm_route_epi(igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp && bsp->sums, stats),

@@ -36,7 +36,10 @@
 //     channel per WORKGROUP.
 //
 // Epilogues: EPI 1 = bf16 output + BN statistics of the stored values (the forward of every
-// conv->BN unit); EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
+// conv->BN unit); EPI 3 = EPI 1 for the ResNet stem as a 4x4 conv on the space-to-depth image
+// (16 channels, 256-deep reduction): the activation fragments are gathered from the 4x4 window
+// (two taps x 16 channels per 32-deep k-block: 64 contiguous bytes per pixel) instead of read as
+// a row; EPI 2 = backward: residual-gradient add, producer ReLU mask (bnmask.h zmodes)
 // and the producer's fused BN-backward sums (sum dy, sum dy * xhat).
 // Prologue (PRO, EPI 2, K = 64 / 128): the activation operand is the unit's OWN BN backward,
 // dy = A g + B y + Cc, formed in the operand registers from the masked gradient g and the unit's
@@ -58,6 +61,7 @@ struct PwArgs {
   int ldb;        // weight row stride (elements)
   int nsplit;     // channel groups of NP (N = nsplit * NP)
   int stat_mode;  // 0: atomics into stats[0..2N), >0: slotted (slot_ptr), kStatPartial: [grid][2N] rows
+  int gH, gW, gP, gQ;   // EPI 3 (stem gather): input / output spatial size
 };
 
 constexpr int PW_NW = 8;  // waves per workgroup (2 per SIMD)
@@ -103,7 +107,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   __syncthreads();
 
   const bool bnsum = EPI == 2 && bs.sums != nullptr && !bs.zgelu;
-  const bool want = EPI == 1 ? stats != nullptr : bnsum;
+  const bool want = EPI != 2 ? stats != nullptr : bnsum;
   const int ch = lane % CPR, lr = lane / CPR;
   const int c0 = n0 + ch * 8;                        // the lane's fixed 8-channel chunk
   // per-lane BN constants of that chunk (EPI 2)
@@ -138,9 +142,21 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     for (int j = 0; j < MJ; ++j) {
       int row = t * TPM + 16 * j + fr;
       row = row < p.M ? row : p.M - 1;  // rows past M compute garbage that is never stored
-      const bf16_t* src = A + (size_t)row * K + 8 * fq;
+      if constexpr (EPI == 3) {
+        // stem gather: k = (r * 4 + s) * 16 + c; k-block kb holds taps 2 kb, 2 kb + 1
+        const int PQ = p.gP * p.gQ;
+        const int n = row / PQ, rem = row - n * PQ, y = rem / p.gQ, x = rem - y * p.gQ;
+        const bf16_t* base = A + (((size_t)n * p.gH + y) * p.gW + x) * 16 + 8 * (fq & 1);
 #pragma unroll
-      for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
+        for (int kb = 0; kb < KT; ++kb) {
+          const int tap = 2 * kb + (fq >> 1), r = tap >> 2, s = tap & 3;
+          af[j][kb] = *reinterpret_cast<const bf16x8*>(base + ((size_t)r * p.gW + s) * 16);
+        }
+      } else {
+        const bf16_t* src = A + (size_t)row * K + 8 * fq;
+#pragma unroll
+        for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
+      }
       if constexpr (PRO) {
         const bf16_t* ys = pro_y + (size_t)row * K + 8 * fq;
 #pragma unroll
@@ -275,7 +291,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
         if (want && ok) {
           float q[8];
           unpack8(pk, q);
-          if constexpr (EPI == 1) {
+          if constexpr (EPI != 2) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
               s1[e] += q[e];
@@ -318,7 +334,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     }
   }
   __syncthreads();
-  float* dst = EPI == 1 ? stats : bs.sums;
+  float* dst = EPI != 2 ? stats : bs.sums;
   if (p.stat_mode > 0) dst = slot_ptr(dst, 2 * N, p.stat_mode);
   for (int c = tid; c < NP; c += NT) {
     atomicAdd(dst + n0 + c, ssum[c]);
@@ -375,7 +391,7 @@ static hipError_t pw_launch(const ConvGeom& g, const bf16_t* X, const bf16_t* W,
   const int need = ((g.M + TPM - 1) / TPM + PW_NW - 1) / PW_NW;
   const int need8 = (need + 7) / 8 * 8;
   if (mgroups > need8) mgroups = need8;
-  PwArgs a{g.M, g.K, g.ldb, nsplit, g.stat_slots};
+  PwArgs a{g.M, g.K, g.ldb, nsplit, g.stat_slots, g.H, g.W, g.P, g.Q};
   hipLaunchKernelGGL(kfn, dim3(mgroups * nsplit), dim3(PW_NW * 64), smem, st, X, W, Y, resid, stats, a, bs);
   return hipGetLastError();
 }
@@ -443,6 +459,22 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
+}
+
+// the ResNet stem in space-to-depth form (4x4 stride-1 unpadded conv, 16 -> 64 channels) with BN
+// statistics (EPI 3)
+extern "C" int zoo_pw_stem_eligible(const ConvGeom* g, int route) {
+  if (pw_mode() <= 0 || route != 1) return 0;
+  if (g->stat_slots == kStatPartial) return 0;
+  return g->R == 4 && g->S == 4 && g->C == 16 && g->K == 64 && g->sh == 1 && g->sw == 1 && g->ph == 0 &&
+         g->pw == 0 && g->lh == 1 && g->lw == 1 && g->dh == 1 && g->dw == 1 && g->omap == 0 && g->Ktot == 256 &&
+         g->ldb >= 256 && g->ldb % 8 == 0 && g->P == g->H - 3 && g->Q == g->W - 3 && g->M > 0;
+}
+
+extern "C" hipError_t zoo_pw_stem(const void* X, const void* W, void* Y, float* stats, const ConvGeom* g,
+                                  hipStream_t st) {
+  BwdStats bs{nullptr, nullptr, nullptr, nullptr, nullptr};
+  return pw_launch<64, 16, 8, 3, false>(*g, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
 }
 
 extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* resid, float* stats,
