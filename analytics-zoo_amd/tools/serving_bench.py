@@ -446,6 +446,29 @@ def run_dist(a):
             dist.destroy_process_group()
 
 
+class _GcWatch:
+    """Python GC pauses (gc.callbacks) -- a collector pass on the serving thread stalls every
+    batch behind it, which shows in the latency tail."""
+
+    def __init__(self):
+        import gc
+        self.t0, self.pauses = None, []
+        gc.callbacks.append(self._cb)
+
+    def _cb(self, phase, info):
+        if phase == "start":
+            self.t0 = time.perf_counter()
+        elif self.t0 is not None:
+            self.pauses.append((info.get("generation", -1), (time.perf_counter() - self.t0) * 1e3))
+            self.t0 = None
+
+    def take(self):
+        p, self.pauses = self.pauses, []
+        return {"n": len(p), "gen2": sum(1 for g, _ in p if g == 2),
+                "max_ms": round(max((d for _, d in p), default=0.0), 2),
+                "total_ms": round(sum(d for _, d in p), 1)}
+
+
 def _suite_model(name, a, rank, world, local, gather):
     """One model through the suite on this rank: capacity (drain), model-only, open-loop loads."""
     import base64
@@ -490,10 +513,14 @@ def _suite_model(name, a, rank, world, local, gather):
             for i in range(n_cap):
                 _send(inq, "cap%d" % i, raw[i % len(raw)])
             s.records = 0
+            for k in s.stage_time:
+                s.stage_time[k] = 0 if k == "batches" else 0.0
             gather(None)
             t0 = time.perf_counter()
             s.run(max_records=n_cap, idle_timeout=60)
             cap = s.records / (time.perf_counter() - t0)
+            nbat = max(1, s.stage_time["batches"])
+            stages = {k: round(v * 1e3 / nbat, 3) for k, v in s.stage_time.items() if k != "batches"}
             # model alone at the serving batch (same InferenceModel replica, input on the GPU)
             xm = (torch.randint(0, 30522, (a.batch, 128), device="cuda:%d" % local).float() if bert
                   else torch.randn(a.batch, 3, 224, 224, device="cuda:%d" % local))
@@ -514,15 +541,19 @@ def _suite_model(name, a, rank, world, local, gather):
                                   "n_gpus": world, "drain_throughput": round(node_cap, 1),
                                   "model_only_throughput": round(node_model, 1),
                                   "drain_over_model": round(node_cap / max(node_model, 1e-9), 3),
+                                  "rank0_host_ms_per_batch": stages, "batches": nbat,
+                                  "overlap": os.environ.get("ZOO_SERVING_ASYNC", "1") != "0",
                                   "unit": "records/sec"}), flush=True)
             # open loop: the C++ load generator on this rank's store, the worker in a thread
             srv.store.track(True)
             worker = threading.Thread(target=s.run, kwargs={"idle_timeout": None}, daemon=True)
             worker.start()
             fracs = [float(f) for f in a.fractions.split(",")]
+            gcw = _GcWatch()
             for fi, f in enumerate(fracs):
                 rate = f * cap
                 gather(None)
+                gcw.take()
                 st = srv.store.loadgen("image_stream", kind, payloads, pshape, rate, a.duration, a.lg_threads,
                                        "r%d-%d-%s" % (rank, fi, name), 1.0, 15.0, bool(a.tcp))
                 allst = gather([st["offered_rate"], st["achieved_throughput"], st["p50_ms"], st["p99_ms"],
@@ -536,6 +567,7 @@ def _suite_model(name, a, rank, world, local, gather):
                            "p99_ms": round(max(v[3] for v in allst), 2),
                            "unfinished": int(sum(v[4] for v in allst)),
                            "achieved_over_model": round(sum(v[1] for v in allst) / max(node_model, 1e-9), 3),
+                           "rank0_gc": gcw.take(),
                            "latency_note": "send -> result written; worst rank's percentile",
                            "client": "C++ open-loop generator, %d threads per GPU, %s" % (
                                a.lg_threads, "RESP over TCP" if a.tcp else "in-process XADD"),

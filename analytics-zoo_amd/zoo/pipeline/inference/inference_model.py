@@ -47,6 +47,9 @@ class _Replica:
         # so their static buffers must never alias
         self.pool = torch.cuda.graph_pool_handle() if dev.type == "cuda" else None
         self.graphs = {}
+        self.host_rings, self.host_idx, self.slot_events = {}, {}, {}
+
+    RING = 3
 
     def _forward(self, xs):
         m = self.owner.model
@@ -106,6 +109,74 @@ class _Replica:
                 res = out.float().cpu()
         self.stream.synchronize()
         return res
+
+    @torch.no_grad()
+    def run_async(self, xs, multi):
+        """Enqueue the forward on this replica's stream and copy the outputs into a pinned host
+        ring slot; the caller overlaps its host work (post-processing the previous batch,
+        preparing the next) with the GPU and collects the result later (_Pending.result)."""
+        dev = self.owner.device
+        if dev.type != "cuda":
+            out = self._forward([t.to(dev) for t in xs])
+            outs = list(out) if isinstance(out, (list, tuple)) else [out]
+            return _Pending(None, [o.float() for o in outs], multi, xs[0].shape[0])
+        cur = torch.cuda.current_stream(dev)
+        self.stream.wait_stream(cur)
+        for t in xs:   # the caller may free / reuse its inputs right away: keep them alive on our stream
+            if t.is_cuda:
+                t.record_stream(self.stream)
+        with torch.cuda.stream(self.stream):
+            g = None
+            if self.owner.use_graph:
+                try:
+                    g = self._graph_for(xs)
+                except RuntimeError as e:
+                    log.warning("hipGraph capture failed (%s); serving this model without graphs", e)
+                    self.owner.use_graph = False
+                    self.graphs.clear()
+            if g is not None:
+                graph, sin, sout = g
+                for s, t in zip(sin, xs):
+                    s.copy_(t, non_blocking=True)
+                graph.replay()
+                out = sout
+            else:
+                out = self._forward([t.to(dev, non_blocking=True) for t in xs])
+            outs = list(out) if isinstance(out, (list, tuple)) else [out]
+            key = tuple((tuple(o.shape), o.dtype) for o in outs)
+            ring = self.host_rings.get(key)
+            if ring is None:
+                ring = self.host_rings[key] = [[torch.empty(o.shape, dtype=torch.float32, pin_memory=True)
+                                                for o in outs] for _ in range(self.RING)]
+                self.host_idx[key] = 0
+            i = self.host_idx[key]
+            self.host_idx[key] = i + 1
+            slot = ring[i % self.RING]
+            ev = self.slot_events.get((key, i % self.RING))
+            if ev is not None:   # the slot's previous result must have been consumed (at most RING in flight)
+                ev.synchronize()
+            for h, o in zip(slot, outs):
+                h.copy_(o if o.dtype == torch.float32 else o.float(), non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+            self.slot_events[(key, i % self.RING)] = ev
+        return _Pending(ev, slot, multi, xs[0].shape[0])
+
+
+class _Pending:
+    """An enqueued prediction: result() waits for its D2H copy and returns the host output."""
+
+    def __init__(self, event, host, multi, n):
+        self.event, self.host, self.multi, self.n = event, host, multi, n
+
+    def done(self):
+        return self.event is None or self.event.query()
+
+    def result(self):
+        if self.event is not None:
+            self.event.synchronize()
+        h = [t[:self.n].numpy().copy() for t in self.host]   # the pinned slot is reused RING batches later
+        return h if self.multi else h[0]
 
 
 class InferenceModel:
@@ -244,6 +315,19 @@ class InferenceModel:
         if isinstance(outs[0], list):
             return [torch.cat([o[i] for o in outs]).numpy() for i in range(len(outs[0]))]
         return torch.cat(outs).numpy()
+
+    def predict_async(self, inputs):
+        """Enqueue one batch (no max_batch split) and return a handle: ``.result()`` -> ndarray
+        (or list). Host work done between the two calls overlaps the model on the GPU; up to
+        _Replica.RING results of one replica may be outstanding."""
+        xs, multi = _as_tensors(inputs)
+        r = self._take()
+        try:
+            p = r.run_async(xs, multi)
+        finally:
+            self._give(r)
+        self._account(xs[0].shape[0])
+        return p
 
     def do_predict(self, inputs):
         return self.predict(inputs)

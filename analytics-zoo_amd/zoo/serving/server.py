@@ -213,6 +213,10 @@ class ClusterServing:
         self.stop_flag = threading.Event()
         self.finish_hook = None   # callable(uris, wall_time) after each batch's results are written
         self.records = 0
+        # host seconds per serving stage of the pipelined loop (main thread; the reader's
+        # read + entropy decode under "read_decode")
+        self.stage_time = {"wait_input": 0.0, "preprocess_enqueue": 0.0, "wait_gpu": 0.0, "post_finish": 0.0,
+                           "read_decode": 0.0, "batches": 0}
         self.summary = None
         if self.cfg.get("tensorboard"):
             from zoo.tensorboard import FileWriter
@@ -319,8 +323,12 @@ class ClusterServing:
         ring = getattr(self, "_coef_ring", None)
         slot = None
         if ring is not None:
-            slot = ring[self._coef_idx % len(ring)]
+            k = self._coef_idx % len(ring)
+            slot = ring[k]
             self._coef_idx += 1
+            ev = self._coef_events.pop(k, None)
+            if ev is not None:   # the slot's previous upload must have left the host buffer
+                ev.synchronize()
         d = jpeg.batch_coeffs(payloads, nt, None if slot is None else slot.numpy())
         if d is None and slot is not None:
             d = jpeg.batch_coeffs(payloads, nt)      # unsupported stream, or the ring is too small
@@ -330,12 +338,13 @@ class ClusterServing:
         if slot is None:   # (re)size the ring for this batch geometry and copy this batch in
             need = d["coef"].size
             self._coef_ring = [torch.empty(need, dtype=torch.int16, pin_memory=True) for _ in range(4)]
+            self._coef_events = {}
             self._coef_idx = 1
             slot = self._coef_ring[0]
             slot.numpy()[:need] = d["coef"].reshape(-1)
             d["coef"] = slot.numpy()[:need].reshape(d["coef"].shape)
         n = d["coef"].size
-        return ("jpeg", d, slot[:n].view(d["coef"].shape))
+        return ("jpeg", d, slot[:n].view(d["coef"].shape), (self._coef_idx - 1) % len(self._coef_ring))
 
     def _decode_procs(self):
         """The multi-process decode pool (zoo/serving/decode_pool.py); ZOO_SERVING_DECODE_PROCS=0
@@ -381,8 +390,13 @@ class ClusterServing:
         if isinstance(decoded, tuple) and decoded[0] == "jpeg":
             from zoo.feature.image import jpeg
             c, h, w = self.cfg["image_shape"]
-            return jpeg.planes_to_input(decoded[1], (int(h), int(w)), self.cfg["mean"], self.cfg["std"],
-                                        not self.cfg["to_rgb"], 0, self.im.device, coef_host=decoded[2])
+            x = jpeg.planes_to_input(decoded[1], (int(h), int(w)), self.cfg["mean"], self.cfg["std"],
+                                     not self.cfg["to_rgb"], 0, self.im.device, coef_host=decoded[2])
+            if self.im.device.type == "cuda":
+                ev = torch.cuda.Event()
+                ev.record(torch.cuda.current_stream(self.im.device))
+                self._coef_events[decoded[3]] = ev
+            return x
         if isinstance(decoded, tuple) and decoded[0] == "rgb":
             c, h, w = self.cfg["image_shape"]
             dev = self.im.device
@@ -410,7 +424,9 @@ class ClusterServing:
         (hipGraph replica) + post-processing on the previous batch and hands every
         result and the XACK/XDEL of the batch to the store in one call."""
         import queue
-        q = queue.Queue(maxsize=2)
+        # decoded batches waiting for the GPU: the reader takes what the stream holds as soon as
+        # a slot frees, so a deeper queue means smaller batches that each wait longer
+        q = queue.Queue(maxsize=max(1, int(os.environ.get("ZOO_SERVING_QDEPTH", "1"))))
         done = threading.Event()
         bs = self.cfg["batch_size"]
 
@@ -426,7 +442,9 @@ class ClusterServing:
                             break
                         continue
                     last = time.time()
+                    t0 = time.perf_counter()
                     item = self._decode_native(recs)
+                    self.stage_time["read_decode"] += time.perf_counter() - t0
                     while not done.is_set():
                         try:
                             q.put(item, timeout=0.1)
@@ -440,32 +458,69 @@ class ClusterServing:
         th = threading.Thread(target=reader, daemon=True)
         th.start()
         flt = self.cfg["filter"]
+        # one batch of look-ahead: batch i+1 is preprocessed and enqueued on the GPU before batch
+        # i's results are post-processed and written, so the host work hides behind the model
+        overlap = os.environ.get("ZOO_SERVING_ASYNC", "1") != "0"
+        prof = self.stage_time
+        pending = None
+
+        def complete(p):
+            h, ids, uris, n = p
+            t0 = time.perf_counter()
+            out = h.result() if overlap else h
+            t1 = time.perf_counter()
+            outs = out if isinstance(out, np.ndarray) else out[0]
+            vals = post_process_batch(outs[:n], flt)
+            self.db.finish(STREAM, GROUP, ids, [("result:" + u, v) for u, v in zip(uris, vals)])
+            prof["wait_gpu"] += t1 - t0
+            prof["post_finish"] += time.perf_counter() - t1
+            prof["batches"] += 1
+            if self.finish_hook is not None:
+                self.finish_hook(uris, time.time())
+            self.records += len(ids)
+            if self.summary is not None:
+                dt = max(time.time() - self._t0, 1e-9)
+                self.summary.add_scalar("Serving Throughput", self.records / dt, self.records)
+                self.summary.add_scalar("Total Records Number", self.records, self.records)
+
         try:
             while True:
-                item = q.get()
+                t0 = time.perf_counter()
+                try:
+                    item = q.get_nowait()
+                except queue.Empty:
+                    if pending is not None:   # nothing queued: answer the in-flight batch now
+                        complete(pending)
+                        pending = None
+                        if max_records is not None and self.records >= max_records:
+                            break
+                    t0 = time.perf_counter()
+                    item = q.get()
+                prof["wait_input"] += time.perf_counter() - t0
                 if item is None:
                     break
                 if isinstance(item, Exception):
                     raise item
                 ids, uris, decoded = item
+                t0 = time.perf_counter()
                 x = self._to_batch(decoded)
                 n = x.shape[0]
                 nb = _bucket(n, bs)
                 if nb > n:   # pad to a power-of-two bucket: hipGraphs for ~log2(batch) shapes only
                     x = torch.cat([x, x.new_zeros((nb - n,) + tuple(x.shape[1:]))])
-                out = self.im.predict(x)
-                outs = out if isinstance(out, np.ndarray) else out[0]
-                vals = post_process_batch(outs[:n], flt)
-                self.db.finish(STREAM, GROUP, ids, [("result:" + u, v) for u, v in zip(uris, vals)])
-                if self.finish_hook is not None:
-                    self.finish_hook(uris, time.time())
-                self.records += len(ids)
-                if self.summary is not None:
-                    dt = max(time.time() - self._t0, 1e-9)
-                    self.summary.add_scalar("Serving Throughput", self.records / dt, self.records)
-                    self.summary.add_scalar("Total Records Number", self.records, self.records)
+                h = self.im.predict_async(x) if overlap else self.im.predict(x)
+                prof["preprocess_enqueue"] += time.perf_counter() - t0
+                if pending is not None:
+                    complete(pending)
+                pending = (h, ids, uris, n)
+                if not overlap:
+                    complete(pending)
+                    pending = None
                 if max_records is not None and self.records >= max_records:
                     break
+            if pending is not None:
+                complete(pending)
+                pending = None
         finally:
             done.set()
             th.join(timeout=5)
@@ -474,6 +529,12 @@ class ClusterServing:
     def run(self, running_flag=None, max_records=None, idle_timeout=None):
         """Serve until ``running_flag`` (a file path) disappears, ``max_records``
         are served, or nothing arrives for ``idle_timeout`` seconds."""
+        if os.environ.get("ZOO_SERVING_GC_FREEZE", "0") != "0":
+            # the model, graphs and buffers are long-lived: move them out of the collector's
+            # view so a full collection does not walk them in the middle of a batch
+            import gc
+            gc.collect()
+            gc.freeze()
         if hasattr(self.db, "read_batch") and os.environ.get("ZOO_SERVING_PIPELINE", "1") != "0":
             return self._run_pipelined(running_flag, max_records, idle_timeout)
         last = time.time()

@@ -597,6 +597,62 @@ def test_inference_model_hipgraph_replicas(gpu):
     assert im.predict(x[:2].numpy()).shape == (2, 10)
 
 
+def test_inference_model_predict_async(gpu):
+    """predict_async: several batches in flight on one replica (pinned output ring), inputs
+    freed by the caller right after the call, results equal to the synchronous predict."""
+    from zoo.models.image.resnet import resnet18
+    from zoo.pipeline.inference import InferenceModel
+    torch.manual_seed(0)
+    m = resnet18(num_classes=10).to(gpu).eval()
+    im = InferenceModel(1, device=gpu).load_module(m)
+    xs = [torch.randn(8, 3, 64, 64, device=gpu) for _ in range(6)]
+    refs = [im.predict(x) for x in xs]
+    for k in (1, 2, 3):   # up to RING outstanding
+        hs = []
+        for i, x in enumerate(xs):
+            hs.append(im.predict_async(x.clone()))   # the clone is dropped at once: record_stream keeps it
+            if len(hs) == k:
+                h = hs.pop(0)
+                j = i - k + 1
+                assert np.array_equal(h.result(), refs[j]), (k, j)
+        for j, h in zip(range(len(xs) - len(hs), len(xs)), hs):
+            assert np.array_equal(h.result(), refs[j]), (k, j)
+
+
+def test_serving_lookahead_matches_sync(gpu):
+    """The pipelined worker with one batch of GPU look-ahead (ZOO_SERVING_ASYNC=1) writes the
+    same results as the synchronous loop, including a short last batch."""
+    import os
+    import tempfile
+    from zoo.serving import ClusterServing, InputQueue, OutputQueue
+    from zoo.serving.resp import RespServer
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Conv2d(3, 4, 3), torch.nn.Flatten(), torch.nn.LazyLinear(6))
+    model(torch.zeros(1, 3, 16, 16))
+    rng = np.random.default_rng(1)
+    imgs = [rng.integers(0, 255, (20, 24, 3)).astype(np.uint8) for _ in range(37)]
+    got = {}
+    for mode in ("0", "1"):
+        os.environ["ZOO_SERVING_ASYNC"] = mode
+        srv = RespServer("127.0.0.1", 0).start()
+        try:
+            with tempfile.TemporaryDirectory() as d:
+                cfg = d + "/config.yaml"
+                open(cfg, "w").write("data:\n  src: 127.0.0.1:%d\n  image_shape: 3,16,16\n  filter: topN(3)\n"
+                                     "params:\n  batch_size: 8\n" % srv.port)
+                s = ClusterServing(cfg, model=model, device=gpu)
+                inq, outq = InputQueue(cfg), OutputQueue(cfg)
+                for i, im in enumerate(imgs):
+                    inq.enqueue_image("im%d" % i, im)
+                assert s.run(max_records=len(imgs), idle_timeout=10) == len(imgs)
+                got[mode] = outq.dequeue()
+        finally:
+            srv.shutdown()
+            srv.server_close()
+    os.environ.pop("ZOO_SERVING_ASYNC", None)
+    assert len(got["1"]) == len(imgs) and got["0"] == got["1"]
+
+
 def test_serving_worker_on_gpu(gpu):
     from zoo.serving import ClusterServing, InputQueue, OutputQueue
     from zoo.serving.resp import RespServer
