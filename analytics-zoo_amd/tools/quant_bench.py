@@ -93,7 +93,8 @@ def main():
             rt = mt(xt).float()
             res["%s_input_sensitivity" % tag] = round(input_sensitivity(rt), 5)
             for fmt, cls in (("int8", Int8ResNet), ("fp8", Fp8ResNet)):
-                for sc, clip, mix in (("channel", 0.0, None), ("channel", 1e-4, None), ("tensor", 0.0, None),
+                for sc, clip, mix in (("channel", 0.0, None), ("channel", 1e-4, None), ("mse", 0.0, None),
+                                      ("tensor", 0.0, None),
                                       ("channel", 0.0, a.max_block_err)):
                     qm = cls(mt, cal, act_scales=sc, act_clip=clip, max_block_err=mix)
                     qo = qm(xt).float()

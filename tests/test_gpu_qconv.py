@@ -45,7 +45,7 @@ def trained_resnet50(gpu):
     return m, T
 
 
-def _quant_agreement(trained, fmt):
+def _quant_agreement(trained, fmt, act_scales=None):
     from zoo.ops.qresnet import Fp8ResNet, Int8ResNet
     from zoo.utils.synthetic import agreement, sample
     m, T = trained
@@ -53,7 +53,7 @@ def _quant_agreement(trained, fmt):
     x, _ = sample(T, 128, seed=12)
     with torch.no_grad():
         ref = m(x).float()
-    q = (Fp8ResNet if fmt == "fp8" else Int8ResNet)(m, calib)
+    q = (Fp8ResNet if fmt == "fp8" else Int8ResNet)(m, calib, act_scales=act_scales)
     with torch.no_grad():
         out = q(x).float()
     assert out.shape == ref.shape and torch.isfinite(out).all()
@@ -64,6 +64,13 @@ def test_int8_resnet_tracks_bf16_model(gpu, trained_resnet50):
     """Per-sample agreement with the bf16 model: top-1 and the cosine of each sample's
     mean-centred logits (not a flattened cosine, which the shared logit offset dominates)."""
     top1, cos = _quant_agreement(trained_resnet50, "int8")
+    assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
+
+
+def test_int8_mse_scales_track_bf16_model(gpu, trained_resnet50):
+    """MSE-searched per-channel activation clipping: scales never exceed the channel absmax, and
+    the twin tracks the bf16 model as well as the absmax-calibrated one."""
+    top1, cos = _quant_agreement(trained_resnet50, "int8", act_scales="mse")
     assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
 
 
