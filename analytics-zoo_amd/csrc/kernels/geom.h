@@ -64,6 +64,10 @@ struct BwdStats {
   const void* pro_y;
   const float* pro_coef;
   void* pro_dy;
+  // 1: `resid` is a half-resolution [N, H/2, W/2, K] gradient added at the even (h, w) output
+  // positions only -- the compact data gradient of a 1x1 stride-2 projection shortcut, which
+  // then never gets its zero-interleaved full-size tensor (pw.hip EPI 2 only)
+  int resid_half;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

@@ -222,7 +222,18 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
           const size_t off = (size_t)m * N + c0;
           ey[j][h] = bnsum ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off)
                            : make_uint4(0u, 0u, 0u, 0u);
-          er[j][h] = resid ? *reinterpret_cast<const uint4*>(resid + off) : make_uint4(0u, 0u, 0u, 0u);
+          if (resid && bs.resid_half) {
+            // half-resolution residual: even (h, w) only; the address stays in bounds for odd
+            // positions (H, W even) and the value is dropped there, so the load is unconditional
+            const int hw = p.gH * p.gW;
+            const int n = m / hw, r = m - n * hw;
+            const int yy = r / p.gW, xx = r - yy * p.gW;
+            const size_t roff = ((size_t)(n * (p.gH >> 1) + (yy >> 1)) * (p.gW >> 1) + (xx >> 1)) * N + c0;
+            const uint4 rv = *reinterpret_cast<const uint4*>(resid + roff);
+            er[j][h] = ((yy | xx) & 1) ? make_uint4(0u, 0u, 0u, 0u) : rv;
+          } else {
+            er[j][h] = resid ? *reinterpret_cast<const uint4*>(resid + off) : make_uint4(0u, 0u, 0u, 0u);
+          }
           em[j][h] = bs.zmode == 2 ? (unsigned)reinterpret_cast<const uint8_t*>(bs.z)[off >> 3] : 0u;
         }
     }
@@ -458,6 +469,8 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   if (route == 1 && g->Ktot > 256) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
+  // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
+  if (bs && bs->resid_half && (route != 2 || (g->H & 1) || (g->W & 1))) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
 }
 

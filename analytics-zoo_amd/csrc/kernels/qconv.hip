@@ -40,6 +40,21 @@ typedef __attribute__((address_space(1))) const void q_gl_void;
 
 constexpr int QC_BM = 128, QC_BK = 128 /* bytes = int8 elements */, QC_NT = 256;
 __device__ __attribute__((aligned(16))) int8_t qc_zero_page[16];
+// the real zero of an offset-coded (unsigned) activation: padding taps of a QF_IN_U8 input
+__device__ __attribute__((aligned(16))) int8_t qc_u8zero_page[16] = {-128, -128, -128, -128, -128, -128, -128, -128,
+                                                                    -128, -128, -128, -128, -128, -128, -128, -128};
+
+// Unsigned (offset-coded) int8 activations: a non-negative tensor (post-ReLU) is stored as
+// q = clamp(round(x / s), 0, 255) - 128, x = (q + 128) s -- the full 8-bit grid instead of the
+// 7 bits a symmetric code leaves a ReLU output. The i8 MFMA sums q * w; the missing
+// 128 * sum_k w[n][k] is a per-output-channel constant the host folds into the bias (padding
+// taps read -128, the real zero, so the constant holds at the borders too).
+constexpr int QF_IN_U8 = 1, QF_OUT_U8 = 2, QF_RES_U8 = 4;
+
+ZOO_DEV int8_t q_sat_u8(float v) {
+  const float r = rintf(v);
+  return (int8_t)((r > 255.f ? 255.f : (r < 0.f ? 0.f : r)) - 128.f);
+}
 
 ZOO_DEV int qc_swz(int row) { return (row >> 1) & 7; }
 
@@ -72,7 +87,7 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
                                                       const float* __restrict__ bias,
                                                       const int8_t* __restrict__ resid, float rscale,
                                                       const float* __restrict__ rvec, ConvGeom g, int relu,
-                                                      int out_bf16) {
+                                                      int out_bf16, int qflags) {
   constexpr int BM = QC_BM, BK = QC_BK;
   constexpr int WN = BN / 2, NJ = WN / 16, NI = 4;
   constexpr int B_ROWS_PER_THREAD = BN / 32;
@@ -118,6 +133,7 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
     while (kc >= g.C) { kc -= g.C; if (++ks == g.S) { ks = 0; ++kr; } }
   }
   const int nk = (g.ldb + BK - 1) / BK;
+  const int8_t* a_pad = (!FP8 && (qflags & QF_IN_U8)) ? qc_u8zero_page : qc_zero_page;
 
   auto dma16 = [&](const int8_t* src, int8_t* dst) {
     __builtin_amdgcn_global_load_lds((q_gl_void*)src, (q_lds_void*)dst, 16, 0, 0);
@@ -129,14 +145,14 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
     if constexpr (IS1x1) {
       const bool kok = k < g.Ktot;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dma16(a_ok[i] && kok ? X + a_base[i] + k : qc_zero_page, adst + (32 * i) * BK);
+      for (int i = 0; i < 4; ++i) dma16(a_ok[i] && kok ? X + a_base[i] + k : a_pad, adst + (32 * i) * BK);
     } else {
       const bool kok = kr < g.R;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int ih = a_ih[i] + kr * g.dh, iw = a_iw[i] + ks * g.dw;
         const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        dma16(ok ? X + a_base[i] + (ih * g.W + iw) * g.C + kc : qc_zero_page, adst + (32 * i) * BK);
+        dma16(ok ? X + a_base[i] + (ih * g.W + iw) * g.C + kc : a_pad, adst + (32 * i) * BK);
       }
     }
     const bool kokb = k < g.ldb;
@@ -259,10 +275,11 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += r[e] * rv[e];
       } else {
+        const float ro = (qflags & QF_RES_U8) ? 128.f : 0.f;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[e] += (float)(int8_t)(rq.x >> (8 * e)) * rv[e];
-          v[4 + e] += (float)(int8_t)(rq.y >> (8 * e)) * rv[4 + e];
+          v[e] += ((float)(int8_t)(rq.x >> (8 * e)) + ro) * rv[e];
+          v[4 + e] += ((float)(int8_t)(rq.y >> (8 * e)) + ro) * rv[4 + e];
         }
       }
     }
@@ -275,6 +292,13 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
     } else if constexpr (FP8) {
       *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(Y) + off) =
           make_uint2(f8_pack4(v[0], v[1], v[2], v[3]), f8_pack4(v[4], v[5], v[6], v[7]));
+    } else if (qflags & QF_OUT_U8) {
+      uint2 pk;
+      pk.x = (uint32_t)(uint8_t)q_sat_u8(v[0]) | ((uint32_t)(uint8_t)q_sat_u8(v[1]) << 8) |
+             ((uint32_t)(uint8_t)q_sat_u8(v[2]) << 16) | ((uint32_t)(uint8_t)q_sat_u8(v[3]) << 24);
+      pk.y = (uint32_t)(uint8_t)q_sat_u8(v[4]) | ((uint32_t)(uint8_t)q_sat_u8(v[5]) << 8) |
+             ((uint32_t)(uint8_t)q_sat_u8(v[6]) << 16) | ((uint32_t)(uint8_t)q_sat_u8(v[7]) << 24);
+      *reinterpret_cast<uint2*>(reinterpret_cast<int8_t*>(Y) + off) = pk;
     } else {
       uint2 pk;
       pk.x = (uint32_t)(uint8_t)q_sat(v[0]) | ((uint32_t)(uint8_t)q_sat(v[1]) << 8) |
@@ -290,7 +314,7 @@ __global__ __launch_bounds__(256, 2) void qconv_kernel(const int8_t* __restrict_
 // inv_vec (optional, C % 16 == 0): one inverse scale per channel of the NHWC tensor (last dim C)
 __global__ __launch_bounds__(256) void quantize_i8_kernel(const bf16_t* __restrict__ x, int8_t* __restrict__ q,
                                                           size_t n16, float inv_scale, const float* __restrict__ inv_vec,
-                                                          int C) {
+                                                          int C, int u8) {
   for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x) {
     float a[8], b[8];
     unpack8(reinterpret_cast<const uint4*>(x)[2 * i], a);
@@ -300,8 +324,10 @@ __global__ __launch_bounds__(256) void quantize_i8_kernel(const bf16_t* __restri
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float sa = inv_vec ? inv_vec[c0 + e] : inv_scale, sb = inv_vec ? inv_vec[c0 + 8 + e] : inv_scale;
-      w[e >> 2] |= (uint32_t)(uint8_t)q_sat(a[e] * sa) << (8 * (e & 3));
-      w[2 + (e >> 2)] |= (uint32_t)(uint8_t)q_sat(b[e] * sb) << (8 * (e & 3));
+      const int8_t qa = u8 ? q_sat_u8(a[e] * sa) : q_sat(a[e] * sa);
+      const int8_t qb = u8 ? q_sat_u8(b[e] * sb) : q_sat(b[e] * sb);
+      w[e >> 2] |= (uint32_t)(uint8_t)qa << (8 * (e & 3));
+      w[2 + (e >> 2)] |= (uint32_t)(uint8_t)qb << (8 * (e & 3));
     }
     reinterpret_cast<uint4*>(q)[i] = make_uint4(w[0], w[1], w[2], w[3]);
   }
@@ -329,7 +355,8 @@ __global__ __launch_bounds__(256) void quantize_f8_kernel(const bf16_t* __restri
 // global average pool of an int8 (FP8: e4m3) NHWC tensor -> bf16 [N][C] (dequantised with `scale`)
 template <bool FP8>
 __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ X, bf16_t* __restrict__ Y, int N,
-                                                     int HW, int C, float scale, const float* __restrict__ svec) {
+                                                     int HW, int C, float scale, const float* __restrict__ svec,
+                                                     int u8) {
   const int cpr = C >> 3;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < N * cpr; i += gridDim.x * blockDim.x) {
     const int chunk = i % cpr, n = i / cpr;
@@ -351,8 +378,9 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
         }
       }
     }
+    const float zo = (!FP8 && u8) ? 128.f : 0.f;   // offset-coded input: mean(q) + 128
 #pragma unroll
-    for (int e = 0; e < 8; ++e) acc[e] *= (svec ? svec[chunk * 8 + e] : scale) / (float)HW;
+    for (int e = 0; e < 8; ++e) acc[e] = (acc[e] / (float)HW + zo) * (svec ? svec[chunk * 8 + e] : scale);
     *reinterpret_cast<uint4*>(Y + (size_t)n * C + chunk * 8) = pack8(acc);
   }
 }
@@ -360,7 +388,7 @@ __global__ __launch_bounds__(256) void gap_i8_kernel(const int8_t* __restrict__ 
 template <bool IS1x1, int BN, bool FP8>
 static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const float* cs, const float* bias,
                             const int8_t* resid, float rscale, const float* rvec, const ConvGeom& g, int relu,
-                            int out_bf16, hipStream_t st) {
+                            int out_bf16, int qflags, hipStream_t st) {
   const int tiles = ((g.M + QC_BM - 1) / QC_BM) * ((g.K + BN - 1) / BN);
   const size_t main_b = (size_t)(g.ldb > QC_BK ? 2 : 1) * (QC_BM + BN) * QC_BK;
   const size_t epi_b = (size_t)QC_BM * (BN + 4) * sizeof(float);
@@ -373,7 +401,7 @@ static hipError_t launch_qc(const int8_t* X, const int8_t* W, void* Y, const flo
     attr = true;
   }
   hipLaunchKernelGGL((qconv_kernel<IS1x1, BN, FP8>), dim3(tiles), dim3(QC_NT), smem, st, X, W, Y, cs, bias, resid, rscale,
-                     rvec, g, relu, out_bf16);
+                     rvec, g, relu, out_bf16, qflags);
   return hipGetLastError();
 }
 
@@ -384,7 +412,7 @@ using namespace zoo;
 // g: geometry in int8 elements (C, Ktot = R*S*C, ldb all multiples of 16); fp8: e4m3 operands
 extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const float* colscale, const float* bias,
                                 const void* resid, float rscale, const float* rvec, const ConvGeom* g, int relu,
-                                int out_bf16, int fp8, hipStream_t st) {
+                                int out_bf16, int fp8, int qflags, hipStream_t st) {
   const int8_t* x = (const int8_t*)X;
   const int8_t* w = (const int8_t*)W;
   const int8_t* r = (const int8_t*)resid;
@@ -395,10 +423,10 @@ extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const flo
 #define ZOO_QC(F8)                                                                                                 \
   do {                                                                                                             \
     if (is1x1)                                                                                                     \
-      return wide ? launch_qc<true, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st)           \
-                  : launch_qc<true, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st);           \
-    return wide ? launch_qc<false, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st)            \
-                : launch_qc<false, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, st);            \
+      return wide ? launch_qc<true, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, qflags, st)           \
+                  : launch_qc<true, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, qflags, st);           \
+    return wide ? launch_qc<false, 128, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, qflags, st)            \
+                : launch_qc<false, 64, F8>(x, w, Y, colscale, bias, r, rscale, rvec, *g, relu, out_bf16, qflags, st);            \
   } while (0)
   if (fp8) ZOO_QC(true);
   ZOO_QC(false);
@@ -406,12 +434,12 @@ extern "C" hipError_t zoo_qconv(const void* X, const void* W, void* Y, const flo
 }
 
 extern "C" hipError_t zoo_quantize_i8(const void* x, void* q, size_t n, float inv_scale, const float* inv_vec, int C,
-                                       hipStream_t st) {
+                                       int u8, hipStream_t st) {
   const size_t n16 = n / 16;
   size_t blocks = (n16 + 255) / 256;
   if (blocks > 8192) blocks = 8192;
   hipLaunchKernelGGL(quantize_i8_kernel, dim3(blocks ? blocks : 1), dim3(256), 0, st, (const bf16_t*)x, (int8_t*)q,
-                     n16, inv_scale, inv_vec, C);
+                     n16, inv_scale, inv_vec, C, u8);
   return hipGetLastError();
 }
 
@@ -426,13 +454,13 @@ extern "C" hipError_t zoo_quantize_f8(const void* x, void* q, size_t n, float in
 }
 
 extern "C" hipError_t zoo_gap_i8(const void* x, void* y, int N, int HW, int C, float scale, const float* svec, int fp8,
-                                  hipStream_t st) {
+                                  int u8, hipStream_t st) {
   int blocks = (N * (C / 8) + 255) / 256;
   if (fp8)
     hipLaunchKernelGGL(gap_i8_kernel<true>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
-                       (bf16_t*)y, N, HW, C, scale, svec);
+                       (bf16_t*)y, N, HW, C, scale, svec, u8);
   else
     hipLaunchKernelGGL(gap_i8_kernel<false>, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const int8_t*)x,
-                       (bf16_t*)y, N, HW, C, scale, svec);
+                       (bf16_t*)y, N, HW, C, scale, svec, u8);
   return hipGetLastError();
 }

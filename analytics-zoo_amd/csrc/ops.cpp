@@ -177,9 +177,9 @@ hipError_t zoo_sparse_linear_fwd(const int64_t*, const int64_t*, const float*, c
 hipError_t zoo_sparse_linear_bwd(const int64_t*, const int64_t*, const float*, const float*, float*, float*, int64_t,
                                  int, int, int, hipStream_t);
 hipError_t zoo_qconv(const void*, const void*, void*, const float*, const float*, const void*, float, const float*,
-                     const ConvGeom*, int, int, int, hipStream_t);
-hipError_t zoo_quantize_i8(const void*, void*, size_t, float, const float*, int, hipStream_t);
-hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, const float*, int, hipStream_t);
+                     const ConvGeom*, int, int, int, int, hipStream_t);
+hipError_t zoo_quantize_i8(const void*, void*, size_t, float, const float*, int, int, hipStream_t);
+hipError_t zoo_gap_i8(const void*, void*, int, int, int, float, const float*, int, int, hipStream_t);
 hipError_t zoo_quantize_f8(const void*, void*, size_t, float, const float*, int, hipStream_t);
 hipError_t zoo_act(const void*, const void*, void*, size_t, int, int, float, hipStream_t);
 hipError_t zoo_dropout(const void*, void*, size_t, int, float, uint64_t, hipStream_t);
@@ -272,7 +272,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bmean, c10::optional<torch::Tensor> binv,
                        c10::optional<torch::Tensor> bsums, c10::optional<torch::Tensor> bgamma,
                        c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
-                       c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy) {
+                       c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy,
+                       bool resid_half) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -309,11 +310,20 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     bp = bias->data_ptr<float>();
   }
   const void* rp = nullptr;
+  torch::Tensor resid_full;   // fallback of a half-resolution residual (kernels other than pw.hip)
   if (resid.has_value() && resid->defined()) {
     req(*resid, at::kBFloat16, "resid");
-    TORCH_CHECK(resid->numel() == (g.omap ? (int64_t)g.N * g.oH * g.oW * K : (int64_t)g.M * K),
-                "resid size mismatch");
+    if (resid_half) {
+      TORCH_CHECK(!g.omap && g.P % 2 == 0 && g.Q % 2 == 0 &&
+                      resid->numel() == (int64_t)g.N * (g.P / 2) * (g.Q / 2) * K,
+                  "conv_fwd: a half-resolution residual must be [N, P/2, Q/2, K] with P, Q even and no omap");
+    } else {
+      TORCH_CHECK(resid->numel() == (g.omap ? (int64_t)g.N * g.oH * g.oW * K : (int64_t)g.M * K),
+                  "resid size mismatch");
+    }
     rp = resid->data_ptr();
+  } else {
+    TORCH_CHECK(!resid_half, "conv_fwd: resid_half without a residual");
   }
   float* sp = nullptr;
   if (stats.has_value() && stats->defined()) {
@@ -325,6 +335,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     sp = stats->data_ptr<float>();
   }
   BwdStats bs{nullptr, nullptr, nullptr, nullptr, nullptr};
+  bs.resid_half = resid_half ? 1 : 0;
   if (bsums.has_value() && bsums->defined()) {
     req(*bsums, at::kFloat, "bn sums");
     TORCH_CHECK(bsums->numel() == 2 * K || bsums->numel() == stat_len(K),
@@ -437,6 +448,14 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
       bs.pro_coef = nullptr;
       bs.pro_dy = nullptr;
     }
+  }
+  if (bs.resid_half && !zoo_pw_eligible(&g, route, &bs)) {
+    // only pw.hip reads the half-resolution residual: zero-interleave it to full size
+    resid_full = torch::zeros({g.N, g.P, g.Q, K}, x.options());
+    resid_full.view({g.N, g.P / 2, 2, g.Q / 2, 2, K}).select(4, 0).select(2, 0).copy_(
+        resid->view({g.N, g.P / 2, g.Q / 2, K}));
+    rp = resid_full.data_ptr();
+    bs.resid_half = 0;
   }
   torch::Tensor y, yf;
   if (out.has_value() && out->defined()) {
@@ -2302,7 +2321,7 @@ torch::Tensor box_decode(torch::Tensor loc, torch::Tensor priors, double v0, dou
 // (saturating round) or bf16 (out_bf16).
 torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw,
                     torch::Tensor colscale, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
-                    double rscale, bool relu, bool out_bf16, c10::optional<torch::Tensor> rvec) {
+                    double rscale, bool relu, bool out_bf16, c10::optional<torch::Tensor> rvec, int64_t qflags) {
   // int8 or OCP fp8 e4m3 operands (the fp8 twin of the kernel); both operands the same format
   const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
   const auto qt = fp8 ? at::kFloat8_e4m3fn : at::kChar;
@@ -2339,9 +2358,12 @@ torch::Tensor qconv(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int 
     TORCH_CHECK(rvec->numel() == K, "qconv: rvec must be [K]");
     rv = rvec->data_ptr<float>();
   }
+  // qflags (int8 only): 1 input, 2 output, 4 residual offset-coded unsigned (qconv.hip QF_*)
+  TORCH_CHECK(qflags >= 0 && qflags < 8 && (!fp8 || qflags == 0), "qconv: qflags are int8-only bits 0..2");
+  TORCH_CHECK(!(qflags & 2) || (relu && !out_bf16), "qconv: an unsigned int8 output needs relu and an int8 output");
   auto y = torch::empty({g.N, g.P, g.Q, K}, x.options().dtype(out_bf16 ? at::kBFloat16 : qt));
   check_hip(zoo_qconv(x.data_ptr(), w.data_ptr(), y.data_ptr(), colscale.data_ptr<float>(), bp, rp, (float)rscale, rv,
-                      &g, relu, out_bf16, fp8 ? 1 : 0, cur_stream()),
+                      &g, relu, out_bf16, fp8 ? 1 : 0, (int)qflags, cur_stream()),
             "qconv");
   return y;
 }
@@ -2354,12 +2376,13 @@ static const float* chan_vec(const c10::optional<torch::Tensor>& v, const torch:
   return v->data_ptr<float>();
 }
 
-torch::Tensor quantize_i8(torch::Tensor x, double inv_scale, c10::optional<torch::Tensor> inv_vec) {
+torch::Tensor quantize_i8(torch::Tensor x, double inv_scale, c10::optional<torch::Tensor> inv_vec, bool u8) {
   req(x, at::kBFloat16, "x");
   TORCH_CHECK(x.numel() % 16 == 0, "quantize_i8: numel must be a multiple of 16");
   const float* iv = chan_vec(inv_vec, x, "quantize_i8 inv_vec");
   auto q = torch::empty(x.sizes(), x.options().dtype(at::kChar));
-  check_hip(zoo_quantize_i8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, iv, (int)x.size(-1), cur_stream()),
+  check_hip(zoo_quantize_i8(x.data_ptr(), q.data_ptr(), x.numel(), (float)inv_scale, iv, (int)x.size(-1), u8 ? 1 : 0,
+                            cur_stream()),
             "quantize_i8");
   return q;
 }
@@ -2374,7 +2397,7 @@ torch::Tensor quantize_f8(torch::Tensor x, double inv_scale, c10::optional<torch
   return q;
 }
 
-torch::Tensor gap_i8(torch::Tensor x, double scale, c10::optional<torch::Tensor> svec) {
+torch::Tensor gap_i8(torch::Tensor x, double scale, c10::optional<torch::Tensor> svec, bool u8) {
   const bool fp8 = x.scalar_type() == at::kFloat8_e4m3fn;
   req(x, fp8 ? at::kFloat8_e4m3fn : at::kChar, "x");
   TORCH_CHECK(x.dim() == 4 && x.size(3) % 8 == 0, "gap_i8: NHWC with C % 8 == 0");
@@ -2386,7 +2409,9 @@ torch::Tensor gap_i8(torch::Tensor x, double scale, c10::optional<torch::Tensor>
     sv = svec->data_ptr<float>();
   }
   auto y = torch::empty({N, C}, x.options().dtype(at::kBFloat16));
-  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, sv, fp8 ? 1 : 0, cur_stream()), "gap_i8");
+  TORCH_CHECK(!(fp8 && u8), "gap_i8: the unsigned code is int8-only");
+  check_hip(zoo_gap_i8(x.data_ptr(), y.data_ptr(), N, HW, C, (float)scale, sv, fp8 ? 1 : 0, u8 ? 1 : 0, cur_stream()),
+            "gap_i8");
   return y;
 }
 
@@ -3096,20 +3121,21 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
         py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
-        py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none());
+        py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false);
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);
   m.def("qconv", &qconv, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"),
         py::arg("ph"), py::arg("pw"), py::arg("colscale"), py::arg("bias"), py::arg("resid"), py::arg("rscale"),
-        py::arg("relu"), py::arg("out_bf16"), py::arg("rvec") = py::none());
+        py::arg("relu"), py::arg("out_bf16"), py::arg("rvec") = py::none(), py::arg("qflags") = 0);
   m.def("act_fwd_bwd", &act_fwd_bwd);
   m.def("dropout_fwd", &dropout_fwd);
   m.def("loss_fwd", &loss_fwd);
   m.def("auc_hist", &auc_hist);
   m.def("box_decode", &box_decode);
-  m.def("quantize_i8", &quantize_i8, py::arg("x"), py::arg("inv_scale"), py::arg("inv_vec") = py::none());
-  m.def("gap_i8", &gap_i8, py::arg("x"), py::arg("scale"), py::arg("svec") = py::none());
+  m.def("quantize_i8", &quantize_i8, py::arg("x"), py::arg("inv_scale"), py::arg("inv_vec") = py::none(),
+        py::arg("u8") = false);
+  m.def("gap_i8", &gap_i8, py::arg("x"), py::arg("scale"), py::arg("svec") = py::none(), py::arg("u8") = false);
   m.def("quantize_f8", &quantize_f8, py::arg("x"), py::arg("inv_scale"), py::arg("inv_vec") = py::none());
   m.def("embedding_bag_fwd", &embedding_bag_fwd);
   m.def("embedding_bag_bwd", &embedding_bag_bwd);

@@ -93,14 +93,19 @@ def main():
             rt = mt(xt).float()
             res["%s_input_sensitivity" % tag] = round(input_sensitivity(rt), 5)
             for fmt, cls in (("int8", Int8ResNet), ("fp8", Fp8ResNet)):
-                for sc, clip, mix in (("channel", 0.0, None), ("channel", 1e-4, None), ("mse", 0.0, None),
-                                      ("tensor", 0.0, None),
-                                      ("channel", 0.0, a.max_block_err)):
-                    qm = cls(mt, cal, act_scales=sc, act_clip=clip, max_block_err=mix)
+                # int8 activations in the unsigned offset code (default) and, "_s8", the signed one
+                for sc, clip, mix, u8 in (("channel", 0.0, None, True), ("channel", 0.0, None, False),
+                                          ("channel", 1e-4, None, True), ("mse", 0.0, None, True),
+                                          ("tensor", 0.0, None, True), ("tensor", 0.0, None, False),
+                                          ("channel", 0.0, a.max_block_err, True)):
+                    if fmt == "fp8" and not u8:
+                        continue
+                    qm = cls(mt, cal, act_scales=sc, act_clip=clip, max_block_err=mix, act_u8=u8)
                     qo = qm(xt).float()
                     top1_t, cos_t = agreement(qo, rt)
-                    k = "%s_%s%s%s_%s" % (fmt, sc, "_clip%g" % clip if clip else "", "_mixed" if mix else "", tag)
-                    if mix is None and sc == "channel" and not clip:
+                    k = "%s_%s%s%s%s_%s" % (fmt, sc, "_clip%g" % clip if clip else "", "_mixed" if mix else "",
+                                            "" if u8 else "_s8", tag)
+                    if mix is None and sc == "channel" and not clip and u8:
                         res["%s_%s_block_err" % (fmt, tag)] = [round(e, 4) for e in qm.block_err]
                     if mix:
                         res[k + "_bf16_blocks"] = sorted(qm.bf16_blocks)

@@ -20,14 +20,17 @@ from zoo.ops._native import native
 
 
 def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
-             act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None, pro=None):
+             act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None, pro=None,
+             resid_half=False):
     """``bstats = (z or None, y, mean, inv, sums[, gamma, beta])`` fuses the producing unit's
     BN-backward reduction (and ReLU mask) into this conv's epilogue. The mask source: a bf16
     ``z`` (ReLU output), a uint8 ``z`` (1-bit mask of the forward apply), or -- z None and
     gamma given -- recomputed from ``y`` with the unit's affine (csrc/kernels/bnmask.h).
     ``pro = (y, coef, dy_out or None)``: ``x`` is a unit's masked output gradient g and the GEMM
     runs on that unit's BN backward dy = A g + B y + Cc instead (the BN-backward prologue,
-    csrc/kernels/bnfold.hip); dy is written to ``dy_out``."""
+    csrc/kernels/bnfold.hip); dy is written to ``dy_out``.
+    ``resid_half``: ``resid`` is [N, P/2, Q/2, K], added at the even output positions only (the
+    compact data gradient of a 1x1 stride-2 shortcut, :func:`conv_dgrad_s2_compact`)."""
     bz = by = bm = bi = bsum = bg = bb = None
     if bstats is not None:
         bz, by, bm, bi, bsum = bstats[:5]
@@ -36,7 +39,7 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
     py, pc, pd = pro if pro is not None else (None, None, None)
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
-                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd)
+                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd, bool(resid_half))
 
 
 # ---------------------------------------------------------------------------
@@ -178,25 +181,36 @@ def _fault(dx):
     return dx
 
 
+def conv_dgrad_s2_compact(dy, wb, K, C):
+    """Data gradient of a 1x1 stride-2 unpadded conv in compact form: [N, P, Q, C], the values at
+    the even input positions (every other position of the full gradient is zero). Its consumer
+    adds it with ``resid_half`` instead of a zero-filled full-size tensor being written."""
+    return _fault(conv_fwd(dy, flip_weights(wb, K, 1, 1, C), 1, 1))
+
+
 def conv_dgrad(dy, wb, K, R, S, C, H, W, stride=(1, 1), pad=(0, 0), dil=(1, 1), resid=None, bstats=None,
-               resid_inplace=False, pro=None):
+               resid_inplace=False, pro=None, resid_half=False):
     """dX [N,H,W,C] of y = conv(x, w) given dY [N,P,Q,K] and the bf16 packed weight.
     ``bstats``: see :func:`conv_fwd` (the result is then the masked dy of the producer).
     ``resid_inplace``: ``resid`` is a temporary the caller gives away; strided dgrads
     with tap-less parity classes accumulate into it instead of a copy of it.
     ``pro``: the BN-backward prologue of :func:`conv_fwd` (stride-1 dgrads; ``dy`` is then the
     masked gradient g of this conv's own BN unit)."""
-    return _fault(_conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro))
+    return _fault(_conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro,
+                              resid_half))
 
 
-def _conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro=None):
+def _conv_dgrad(dy, wb, K, R, S, C, H, W, stride, pad, dil, resid, bstats, resid_inplace, pro=None,
+                resid_half=False):
     sh, sw = stride
+    if resid_half and not ((sh, sw) == (1, 1) and dil == (1, 1)):
+        raise ValueError("conv_dgrad: a half-resolution residual needs a stride-1 dgrad")
     if pro is not None and not ((sh, sw) == (1, 1) or dil != (1, 1)):
         raise ValueError("conv_dgrad: the BN-backward prologue needs a stride-1 dgrad")
     if (sh, sw) == (1, 1) or dil != (1, 1):
         wt = flip_weights(wb, K, R, S, C)
         return conv_fwd(dy, wt, R, S, (1, 1), (dil[0] * (R - 1) - pad[0], dil[1] * (S - 1) - pad[1]), dil, stride,
-                        resid=resid, out_hw=(H, W), bstats=bstats, pro=pro)
+                        resid=resid, out_hw=(H, W), bstats=bstats, pro=pro, resid_half=resid_half)
     N = dy.shape[0]
     classes = []
     for a in range(sh):

@@ -43,6 +43,9 @@ _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
 # dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B: profiles/r5/ab_bn_prologue_r5.md).
 _BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
 # unit widths taken by the prologue (ZOO_BN_FOLD_K="64,128")
+# the 1x1 stride-2 shortcut hands its data gradient to the block's conv1 in compact form
+# (GradHandoff.half), added at the even positions by conv1's dgrad epilogue (pw.hip resid_half)
+_HALF_RESID = __import__("os").environ.get("ZOO_HALF_RESID", "1") != "0"
 _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
 
 
@@ -76,10 +79,11 @@ class GradHandoff:
     block's FIRST conv, whose dgrad epilogue adds it (identity shortcut: both
     consume the block input). Replaces autograd's separate add kernel."""
 
-    __slots__ = ("grad",)
+    __slots__ = ("grad", "half")
 
     def __init__(self):
         self.grad = None
+        self.half = False   # grad is the compact [N, H/2, W/2, C] gradient of a stride-2 1x1 shortcut
 
 
 class BNProducer:
@@ -225,18 +229,22 @@ class _ConvBNActFn(torch.autograd.Function):
             dresid, dgam2, dbet2 = _shortcut_bn_bwd(ctx, dresid, K)
         dx = None
         if ctx.needs_input_grad[0]:
-            add = None
+            add, half = None, False
             if ctx.handoff_in is not None:
-                add = ctx.handoff_in.grad
-                ctx.handoff_in.grad = None
+                add, half = ctx.handoff_in.grad, ctx.handoff_in.half
+                ctx.handoff_in.grad, ctx.handoff_in.half = None, False
                 if add is None:
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
+            if half and tuple(stride) != (1, 1):   # only a stride-1 dgrad epilogue reads the compact form
+                full = torch.zeros(xshape[0], xshape[1], xshape[2], Cin, dtype=add.dtype, device=add.device)
+                full[:, ::2, ::2] = add
+                add, half = full, False
             pin = ctx.producer_in
             bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
             # a handed-off gradient is a temporary owned by this unit now: accumulate into it in place
             dx = _kern.conv_dgrad(dz if fold is not None else dy, bf16_weight(w), K, R, S, Cin, xshape[1],
                                   xshape[2], stride, pad, resid=add, bstats=bst, resid_inplace=add is not None,
-                                  pro=fold)
+                                  pro=fold, resid_half=half)
             if ctx.dx_out is not None:
                 # another consumer of x adds this gradient in its own dgrad epilogue
                 ctx.dx_out.grad = dx
@@ -350,9 +358,17 @@ class _ConvStatsFn(torch.autograd.Function):
                 ctx.handoff_in.grad = None
                 if add is None:
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
-            dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, xshape[3], xshape[1], xshape[2], stride, pad,
-                                  resid=add, resid_inplace=add is not None)
-            if ctx.dx_out is not None:
+            if (_HALF_RESID and add is None and ctx.dx_out is not None and (R, S) == (1, 1) and stride == (2, 2)
+                    and pad == (0, 0) and xshape[1] % 2 == 0 and xshape[2] % 2 == 0):
+                # 1x1 stride 2: the gradient is zero at every odd position -- hand the block's conv1
+                # the compact [N, H/2, W/2, C] values, its dgrad epilogue adds them at the even ones
+                ctx.dx_out.grad = _kern.conv_dgrad_s2_compact(dy, bf16_weight(w), K, xshape[3])
+                ctx.dx_out.half = True
+                dx = None
+            else:
+                dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, xshape[3], xshape[1], xshape[2], stride, pad,
+                                      resid=add, resid_inplace=add is not None)
+            if dx is not None and ctx.dx_out is not None:
                 # the other consumer of x (the block's conv1) adds it in its dgrad epilogue
                 ctx.dx_out.grad = dx
                 dx = None

@@ -75,50 +75,74 @@ def _sat(v):
     return torch.clamp(torch.round(v), -127, 127)
 
 
+def _sat_u8(v):
+    """unsigned (offset-coded) int8: round, clamp to [0, 255], store minus 128 (qconv.hip QF_*)"""
+    return torch.clamp(torch.round(v), 0, 255) - 128
+
+
+QF_IN_U8, QF_OUT_U8, QF_RES_U8 = 1, 2, 4
+
+
 def qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False,
-              rvec=None):
-    """float64 CPU model of qconv: xq int8 / e4m3 NHWC, wq [K, R*S*C] of the same format."""
+              rvec=None, qflags=0):
+    """float64 CPU model of qconv: xq int8 / e4m3 NHWC, wq [K, R*S*C] of the same format.
+    ``qflags``: which of input / output / residual use the unsigned offset code."""
     import torch.nn.functional as F
     fmt = _fmt_of(xq)
     N, H, W, C = xq.shape
     K = wq.shape[0]
     w4 = wq[:, :R * S * C].double().reshape(K, R, S, C).permute(0, 3, 1, 2)
-    acc = F.conv2d(xq.double().permute(0, 3, 1, 2), w4, stride=stride, padding=pad).permute(0, 2, 3, 1)
+    xd = xq.double()
+    if qflags & QF_IN_U8:   # the kernel pads with the code of 0 (-128) and the host folds 128 * sum(w)
+        xd = F.pad(xd.permute(0, 3, 1, 2), (pad, pad, pad, pad), value=-128.0)
+        acc = F.conv2d(xd, w4, stride=stride).permute(0, 2, 3, 1)
+    else:
+        acc = F.conv2d(xd.permute(0, 3, 1, 2), w4, stride=stride, padding=pad).permute(0, 2, 3, 1)
     v = acc * colscale.double() + (bias.double() if bias is not None else 0.0)
     if resid is not None:
-        v = v + resid.double() * (rvec.double() if rvec is not None else rscale)
+        r = resid.double() + (128.0 if qflags & QF_RES_U8 else 0.0)
+        v = v + r * (rvec.double() if rvec is not None else rscale)
     if relu:
         v = v.clamp_min(0)
     if out_bf16:
         return v.to(torch.bfloat16)
-    return to_fp8(v) if fmt == "fp8" else _sat(v).to(torch.int8)
+    if fmt == "fp8":
+        return to_fp8(v)
+    return (_sat_u8(v) if qflags & QF_OUT_U8 else _sat(v)).to(torch.int8)
 
 
-def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False, rvec=None):
+def qconv(xq, wq, R, S, stride, pad, colscale, bias, resid=None, rscale=0.0, relu=False, out_bf16=False, rvec=None,
+          qflags=0):
     """``rvec`` (optional [K]): per-channel residual scale, overrides ``rscale``."""
     if xq.is_cuda:
         return native().qconv(xq, wq, R, S, stride, stride, pad, pad, colscale, bias, resid, float(rscale),
-                              bool(relu), bool(out_bf16), rvec)
-    return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16, rvec)
+                              bool(relu), bool(out_bf16), rvec, int(qflags))
+    return qconv_ref(xq, wq, R, S, stride, pad, colscale, bias, resid, rscale, relu, out_bf16, rvec, qflags)
 
 
-def quantize_act(x, scale, fmt="int8"):
-    """bf16 NHWC -> int8 / e4m3 with ``scale`` a float (per tensor) or a [C] tensor (per channel)."""
+def quantize_act(x, scale, fmt="int8", u8=False):
+    """bf16 NHWC -> int8 / e4m3 with ``scale`` a float (per tensor) or a [C] tensor (per channel);
+    ``u8``: the unsigned offset code of a non-negative tensor (int8 only)."""
     vec = torch.is_tensor(scale)
     if x.is_cuda and x.dtype == torch.bfloat16 and x.numel() % 16 == 0 and (not vec or x.shape[-1] % 16 == 0):
-        fn = native().quantize_f8 if fmt == "fp8" else native().quantize_i8
+        if fmt == "fp8":
+            fn = native().quantize_f8
+        else:
+            def fn(t, inv, iv=None):
+                return native().quantize_i8(t, inv, iv, bool(u8))
         if vec:
             return fn(x.contiguous(), 1.0, (1.0 / scale).float().contiguous())
         return fn(x.contiguous(), 1.0 / scale)
     s = scale.double().to(x.device) if vec else scale
     if fmt == "fp8":
         return to_fp8(x.double() / s)
-    return _sat(x.double() / s).to(torch.int8)
+    return (_sat_u8 if u8 else _sat)(x.double() / s).to(torch.int8)
 
 
-def _dequant(xq, s):
+def _dequant(xq, s, u8=False):
     """int8 / e4m3 NHWC -> fp32 with a per-tensor float or per-channel [C] scale."""
-    return xq.float() * (s.float().to(xq.device) if torch.is_tensor(s) else s)
+    v = xq.float() + 128.0 if u8 else xq.float()
+    return v * (s.float().to(xq.device) if torch.is_tensor(s) else s)
 
 
 class _QUnit:
@@ -129,6 +153,7 @@ class _QUnit:
         self.w, self.b = (t.to(device) for t in _fold_weight(unit))
         self.fmt, self.cin = fmt, unit.cin
         self.k, self.stride, self.pad, self.relu = unit.k, unit.stride, unit.pad, unit.relu
+        self.qflags = 0     # QF_* bits: input / output / residual in the unsigned offset code
 
     def bind(self, s_in, s_out):
         self.s_in, self.s_out = s_in, s_out
@@ -141,6 +166,8 @@ class _QUnit:
             self.q, sw = _quant_rows(self.w, self.fmt)
             self.colscale = (sw * (s_in / s_out)).float().contiguous()
         self.bias = (self.b / s_out).float().contiguous()
+        if self.qflags & QF_IN_U8:   # x = (q + 128) s: the MFMA sums q * w, the 128 * sum(w) term is constant
+            self.bias = (self.bias + self.colscale * 128.0 * self.q.float().sum(1)).contiguous()
 
     def __call__(self, xq, resid=None, s_resid=None):
         rvec = None
@@ -151,8 +178,9 @@ class _QUnit:
                 rvec = r.float().contiguous()
             else:
                 rscale = r
+        qf = self.qflags if resid is not None else self.qflags & ~QF_RES_U8
         return qconv(xq, self.q, self.k, self.k, self.stride, self.pad, self.colscale, self.bias, resid,
-                     rscale, self.relu, rvec=rvec)
+                     rscale, self.relu, rvec=rvec, qflags=qf)
 
 
 class Int8ResNet(nn.Module):
@@ -163,7 +191,10 @@ class Int8ResNet(nn.Module):
     act_scales = "channel"
     act_clip = 0.0
 
-    def __init__(self, model, calib_x, fmt=None, act_scales=None, act_clip=None, bf16_blocks=(), max_block_err=None):
+    act_u8 = True
+
+    def __init__(self, model, calib_x, fmt=None, act_scales=None, act_clip=None, bf16_blocks=(), max_block_err=None,
+                 act_u8=None):
         """``act_scales``: "channel" (one activation scale per channel), "mse" (per channel, the
         clipping range minimising the calibration batch's squared quantization error) or "tensor"
         (one per tensor).
@@ -173,8 +204,13 @@ class Int8ResNet(nn.Module):
         blocks that stay on the bf16 kernels; ``max_block_err`` -- additionally keep in bf16 every
         block whose calibrated local error (relative L2 of its quantized output against bf16, fed
         the same input; ``block_err``) exceeds this. Activations are dequantised / requantised at
-        the boundaries."""
+        the boundaries.
+        ``act_u8`` (int8 only, default on): the non-negative activations (block inputs / outputs and
+        the ReLU outputs inside a block) use the unsigned offset code -- 255 levels over [0, amax]
+        instead of 127 -- and only the projection shortcut's output stays signed."""
         super().__init__()
+        if act_u8 is not None:
+            self.act_u8 = bool(act_u8)
         self.bf16_blocks = set(int(i) for i in bf16_blocks)
         self.max_block_err = max_block_err
         if act_clip is not None:
@@ -201,6 +237,20 @@ class Int8ResNet(nn.Module):
                 if blk.down is not None:
                     units["down"] = _QUnit(blk.down, dev, f)
                 self.blocks.append((blk, units))
+        self.u8 = self.act_u8 and self.fmt == "int8"
+        if self.u8:
+            for _, u in self.blocks:
+                # conv1 / conv2 / conv3 read and write unsigned tensors; the projection reads the
+                # unsigned block input and writes a signed (BN-only) shortcut; conv3's residual is
+                # the unsigned block input unless a projection produced it
+                for k in ("conv1", "conv2", "conv3"):
+                    if k in u:
+                        u[k].qflags = QF_IN_U8 | QF_OUT_U8
+                last = u["conv3"] if "conv3" in u else u["conv2"]
+                if "down" in u:
+                    u["down"].qflags = QF_IN_U8
+                else:
+                    last.qflags |= QF_RES_U8
         self.calibrate(calib_x)
 
     @torch.no_grad()
@@ -220,10 +270,10 @@ class Int8ResNet(nn.Module):
     @torch.no_grad()
     def calibrate(self, x):
         """Per-tensor absmax of every int8 tensor of the network on ``x`` (run in bf16)."""
-        qmax = QMAX[self.fmt]
+        qmax0 = QMAX[self.fmt]
         clip = self.act_clip
         if self.act_scales == "channel":
-            def amax(t):
+            def amax(t, qmax=qmax0):
                 a = t.float().abs().reshape(-1, t.shape[-1])
                 if clip > 0:
                     k = max(1, int(a.shape[0] * clip))     # the k-th largest value per channel
@@ -235,7 +285,7 @@ class Int8ResNet(nn.Module):
             # per channel, the clipping range (a fraction of the absmax) that minimises the
             # calibration batch's squared quantization error: a heavy-tailed channel trades a few
             # saturated outliers for a finer grid under the bulk of its values
-            def amax(t):
+            def amax(t, qmax=qmax0):
                 a = t.float().reshape(-1, t.shape[-1])
                 m = a.abs().amax(dim=0).clamp_min(1e-6)
                 best, best_err = m.clone(), None
@@ -244,7 +294,7 @@ class Int8ResNet(nn.Module):
                     if self.fmt == "fp8":
                         dq = to_fp8((a / sc).clamp(-qmax, qmax)).float() * sc
                     else:
-                        dq = (a / sc).round().clamp(-qmax, qmax) * sc
+                        dq = (a / sc).round().clamp(-qmax if qmax < 200 else 0, qmax) * sc
                     err = (dq - a).square().sum(dim=0)
                     if best_err is None:
                         best_err = err
@@ -254,24 +304,25 @@ class Int8ResNet(nn.Module):
                     best_err = torch.where(win, err, best_err)
                 return best / qmax
         else:
-            def amax(t):
+            def amax(t, qmax=qmax0):
                 return max(float(t.float().abs().max()), 1e-6) / qmax
+        qu = 255.0 if self.u8 else qmax0      # range of a non-negative (unsigned-coded) tensor
         h = self._stem(x)
-        self.s_in = amax(h)
+        self.s_in = amax(h, qu)
         s_x = self.s_in
         self.block_err = []
         for blk, u in self.blocks:
             sc = blk.down(h) if blk.down is not None else h
             s_sc = amax(sc) if blk.down is not None else s_x
             h1 = blk.conv1(h)
-            s1 = amax(h1)
+            s1 = amax(h1, qu)
             if "conv3" in u:
                 h2 = blk.conv2(h1)
-                s2 = amax(h2)
+                s2 = amax(h2, qu)
                 out = blk.conv3(h2, resid=sc)
             else:
                 out = blk.conv2(h1, resid=sc)
-            s_o = amax(out)
+            s_o = amax(out, qu)
             u["conv1"].bind(s_x, s1)
             if "conv3" in u:
                 u["conv2"].bind(s1, s2)
@@ -282,7 +333,7 @@ class Int8ResNet(nn.Module):
                 u["down"].bind(s_x, s_sc)
             blk._q_scales = (s_x, s_sc, s_o)
             # the block's own quantization error: its quantized run on the bf16 input vs bf16
-            oq = _dequant(self._run_block(u, quantize_act(h, s_x, self.fmt), s_sc), s_o)
+            oq = _dequant(self._run_block(u, quantize_act(h, s_x, self.fmt, self.u8), s_sc), s_o, self.u8)
             of = out.float()
             self.block_err.append(float((oq - of).norm() / of.norm().clamp_min(1e-12)))
             h, s_x = out, s_o
@@ -306,22 +357,22 @@ class Int8ResNet(nn.Module):
             s_x, s_sc, s_o = blk._q_scales
             if i in self.bf16_blocks:
                 if xq is not None:
-                    h, xq = _dequant(xq, s_x).to(torch.bfloat16), None
+                    h, xq = _dequant(xq, s_x, self.u8).to(torch.bfloat16), None
                 h = blk(h)
                 continue
             if xq is None:
-                xq = quantize_act(h, s_x, self.fmt)
+                xq = quantize_act(h, s_x, self.fmt, self.u8)
             xq = self._run_block(u, xq, s_sc)
         if xq is None:                # the last block ran in bf16
             from zoo import ops
             return self.model.fc(ops.global_avg_pool_nhwc(h))
         vec = torch.is_tensor(self.s_out)
         if xq.is_cuda:
-            feat = native().gap_i8(xq.contiguous(), 1.0, self.s_out.float().contiguous()) if vec else \
-                native().gap_i8(xq.contiguous(), self.s_out)
+            feat = native().gap_i8(xq.contiguous(), 1.0, self.s_out.float().contiguous(), self.u8) if vec else \
+                native().gap_i8(xq.contiguous(), self.s_out, None, self.u8)
         else:
             s = self.s_out.double().to(xq.device) if vec else self.s_out
-            feat = (xq.double() * s).mean((1, 2)).to(torch.bfloat16)
+            feat = ((xq.double() + (128.0 if self.u8 else 0.0)) * s).mean((1, 2)).to(torch.bfloat16)
         return self.model.fc(feat)
 
 

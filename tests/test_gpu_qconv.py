@@ -30,6 +30,49 @@ def test_qconv_matches_float64_model(gpu, N, H, C, K, R, stride, pad, resid, rel
         assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-3   # fp32 vs fp64 rounding ties
 
 
+@pytest.mark.parametrize("N,H,C,K,R,stride,pad", [(2, 14, 64, 128, 3, 1, 1), (3, 15, 32, 64, 3, 2, 1),
+                                                  (2, 14, 64, 64, 1, 1, 0), (2, 16, 128, 256, 1, 2, 0)])
+@pytest.mark.parametrize("qflags,resid,relu,out_bf16", [(7, True, True, False), (3, False, True, False),
+                                                        (1, False, True, True), (5, True, False, True),
+                                                        (1, True, False, False)])
+def test_qconv_unsigned_code_matches_float64_model(gpu, N, H, C, K, R, stride, pad, qflags, resid, relu, out_bf16):
+    """Offset-coded unsigned int8 operands (QF_IN_U8 input incl. its padding taps, QF_OUT_U8
+    output, QF_RES_U8 residual) against the float64 model."""
+    from zoo.ops.qresnet import qconv, qconv_ref
+    g = torch.Generator().manual_seed(N * 1000 + C + K + qflags)
+    xq = torch.randint(-128, 128, (N, H, H, C), generator=g, dtype=torch.int8)
+    wq = torch.randint(-127, 128, (K, R * R * C), generator=g, dtype=torch.int8)
+    cs = (torch.rand(K, generator=g) * 2e-4 + 1e-5).float()
+    b = (torch.randn(K, generator=g) * 3).float()
+    P = (H + 2 * pad - R) // stride + 1
+    rq = torch.randint(-128, 128, (N, P, P, K), generator=g, dtype=torch.int8) if resid else None
+    ref = qconv_ref(xq, wq, R, R, stride, pad, cs, b, rq, 0.37, relu, out_bf16, qflags=qflags)
+    out = qconv(xq.to(gpu), wq.to(gpu), R, R, stride, pad, cs.to(gpu), b.to(gpu),
+                None if rq is None else rq.to(gpu), 0.37, relu, out_bf16, qflags=qflags).cpu()
+    assert out.shape == ref.shape and out.dtype == ref.dtype
+    if out_bf16:
+        assert torch.allclose(out.float(), ref.float(), rtol=1e-2, atol=1e-2)
+    else:
+        d = (out.int() - ref.int()).abs()
+        assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-3
+
+
+def test_unsigned_quantize_and_gap(gpu):
+    from zoo import ops
+    from zoo.ops.qresnet import _dequant, quantize_act
+    torch.manual_seed(3)
+    x = (torch.rand(2, 5, 7, 32, device=gpu) * 3).bfloat16()
+    s = (x.float().reshape(-1, 32).amax(0) / 255).clamp_min(1e-6)
+    q = quantize_act(x, s, "int8", u8=True)
+    qc = quantize_act(x.cpu(), s.cpu(), "int8", u8=True)
+    d = (q.cpu().int() - qc.int()).abs()      # fp32 x * (1/s) on the GPU vs float64 x / s: rounding ties
+    assert int(d.max()) <= 1 and float((d > 0).float().mean()) < 1e-2
+    assert int(q.min()) >= -128 and ((_dequant(q, s, True) - x.float()).abs() <= s / 2 + 1e-3).all()
+    feat = ops.native().gap_i8(q, 1.0, s.float().contiguous(), True)
+    ref = _dequant(q, s, True).mean((1, 2))
+    assert torch.allclose(feat.float(), ref, rtol=1e-2, atol=1e-3)
+
+
 @pytest.fixture(scope="module")
 def trained_resnet50(gpu):
     """ResNet-50 fitted to a learnable synthetic task (zoo.utils.synthetic): quantization is judged
@@ -64,6 +107,19 @@ def test_int8_resnet_tracks_bf16_model(gpu, trained_resnet50):
     """Per-sample agreement with the bf16 model: top-1 and the cosine of each sample's
     mean-centred logits (not a flattened cosine, which the shared logit offset dominates)."""
     top1, cos = _quant_agreement(trained_resnet50, "int8")
+    assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
+
+
+def test_int8_signed_code_tracks_bf16_model(gpu, trained_resnet50):
+    """The symmetric (signed) activation code, act_u8=False, still tracks the model."""
+    from zoo.ops.qresnet import Int8ResNet
+    from zoo.utils.synthetic import agreement, sample
+    m, T = trained_resnet50
+    calib, _ = sample(T, 64, seed=11)
+    x, _ = sample(T, 128, seed=12)
+    with torch.no_grad():
+        ref = m(x).float()
+        top1, cos = agreement(Int8ResNet(m, calib, act_u8=False)(x).float(), ref)
     assert top1 >= 0.9 and cos >= 0.9, (top1, cos)
 
 

@@ -40,3 +40,28 @@ def test_fp8_needs_calibrated_resnet():
     from zoo.ops.quant import quantize
     with pytest.raises(ValueError):
         quantize(torch.nn.Sequential(torch.nn.Linear(4, 4)), dtype="fp8")
+
+
+def test_unsigned_int8_code_reference_matches_float_conv():
+    """Offset-coded unsigned activations (qresnet QF_IN_U8): q = round(x / s) - 128, padding taps
+    at the code of 0, and the 128 * sum(w) term folded into the bias reproduce the float conv of the
+    dequantised input (CPU float64 model of qconv.hip)."""
+    import torch.nn.functional as F
+    from zoo.ops.qresnet import QF_IN_U8, QF_OUT_U8, _dequant, _sat_u8, qconv_ref
+    torch.manual_seed(4)
+    x = torch.rand(2, 9, 9, 16) * 5
+    s = 5.0 / 255
+    xq = _sat_u8(x.double() / s).to(torch.int8)
+    wq = torch.randint(-127, 128, (8, 3 * 3 * 16), dtype=torch.int8)
+    cs = torch.full((8,), 1e-3)
+    b = torch.randn(8)
+    bias = b + cs * 128.0 * wq.float().sum(1)
+    out = qconv_ref(xq, wq, 3, 3, 1, 1, cs, bias, out_bf16=True, qflags=QF_IN_U8).double()
+    xd = _dequant(xq, s, True).double() / s
+    w4 = wq.double().reshape(8, 3, 3, 16).permute(0, 3, 1, 2)
+    ref = F.conv2d(xd.permute(0, 3, 1, 2), w4, padding=1).permute(0, 2, 3, 1) * cs.double() + b.double()
+    assert ((out - ref).norm() / ref.norm()).item() < 1e-2
+    # unsigned output: the code of relu(v), 255 levels
+    o8 = qconv_ref(xq, wq, 3, 3, 1, 1, cs, bias, relu=True, qflags=QF_IN_U8 | QF_OUT_U8)
+    assert o8.dtype == torch.int8
+    assert torch.equal(o8, (torch.clamp(torch.round(ref.clamp_min(0)), 0, 255) - 128).to(torch.int8))
