@@ -466,7 +466,11 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
                      g->lw == 1 && g->H == g->P && g->W == g->Q && g->omap == 0;
   // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
   // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
-  if (route == 1 && g->Ktot > 256) return 0;
+  static const int fwd_kmax = [] {
+    const char* e = getenv("ZOO_PW_FWD_KMAX");
+    return e ? atoi(e) : 256;
+  }();
+  if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W

@@ -356,10 +356,13 @@ extern "C" int zoo_wgrad_plan(WgradGeom* gp) {
   WgradGeom& g = *gp;
   const int bm = wgrad_bm(g);
   const int tiles = ((g.K + bm - 1) / bm) * ((g.Ktot + WG_BN - 1) / WG_BN);
-  // split the pixel reduction so that ~kTarget workgroups are in flight, >= kMinPix pixels each
+  // split the pixel reduction so that ~target workgroups are in flight, >= min_pix pixels each.
+  // 512 (one occupancy-full wave of 2 per CU) rather than 1024: the side-stream weight gradients
+  // then hold fewer CUs at a time next to the compute stream and write half the partials
+  // (ResNet-50 b256 +0.7 %, profiles/r5/ab_wgrad_wg_r5.log)
   static const int target = [] {
     const char* e = getenv("ZOO_WGRAD_WG");
-    return e ? atoi(e) : 1024;
+    return e ? atoi(e) : 512;
   }();
   static const int min_pix = [] {
     const char* e = getenv("ZOO_WGRAD_MINPIX");
@@ -386,10 +389,10 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
   if (splits <= 1) part = nullptr;
   const size_t smem = (size_t)2 * WG_BK * (bm + WG_BN) * sizeof(bf16_t);
   static const bool dma = [] {
-    // measured slower than register staging for the weight gradient (conv_sweep wgrad
-    // 7.34 vs 6.99 ms/step, bench 8912 vs 9045 img/s): opt-in until re-tuned
+    // LDS-DMA staging: slower in round 2 (bench 8912 vs 9045 img/s with register staging), ahead
+    // by 0.1-0.4 % in five round-5 pairs on the side stream (profiles/r5/ab_wgrad_wg_r5.log)
     const char* e = getenv("ZOO_WGRAD_DMA");
-    return e ? atoi(e) != 0 : false;
+    return e ? atoi(e) != 0 : true;
   }();
   if (g.C == 4) {
     if (bm == 64)
