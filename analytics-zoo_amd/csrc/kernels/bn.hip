@@ -181,6 +181,27 @@ ZOO_DEV void bn_coeffs(const float* stats, const float* gamma, const float* beta
   }
 }
 
+// Consumer-side forward apply (conv_fwd pro_fwd): the saved statistics, running averages and the
+// per-channel affine coef = [scale | 0 | shift] ([3][C]) of a conv -> BN -> ReLU unit whose
+// apply pass is done by its 1x1 consumer's operand prologue (pw.hip) instead
+__global__ __launch_bounds__(256) void bn_fwd_coef_kernel(const float* __restrict__ stats,
+                                                          const float* __restrict__ gamma,
+                                                          const float* __restrict__ beta, float* running_mean,
+                                                          float* running_var, float* save_mean, float* save_invstd,
+                                                          float* __restrict__ coef, int M, int C, float eps,
+                                                          float momentum) {
+  bn_bookkeeping(stats, running_mean, running_var, save_mean, save_invstd, M, C, eps, momentum);
+  const float invM = 1.f / (float)M;
+  for (int c = threadIdx.x; c < C; c += blockDim.x) {
+    const float mu = stats[c] * invM;
+    const float is = rsqrtf(fmaxf(stats[C + c] * invM - mu * mu, 0.f) + eps);
+    const float sc = gamma ? gamma[c] * is : is;
+    coef[c] = sc;
+    coef[C + c] = 0.f;
+    coef[2 * C + c] = (beta ? beta[c] : 0.f) - mu * sc;
+  }
+}
+
 // forward apply (training): stats -> scale/shift per thread
 __global__ __launch_bounds__(256) void bn_fwd_apply_kernel(
     const bf16_t* __restrict__ X, const float* __restrict__ stats, const float* __restrict__ gamma,
@@ -737,6 +758,14 @@ static int apply_rows_per_block(int M, int C) {
 }  // namespace zoo
 
 using namespace zoo;
+
+extern "C" hipError_t zoo_bn_fwd_coef(const float* stats, const float* gamma, const float* beta, float* rmean,
+                                      float* rvar, float* smean, float* sinv, float* coef, int M, int C, float eps,
+                                      float momentum, hipStream_t st) {
+  hipLaunchKernelGGL(bn_fwd_coef_kernel, dim3(1), dim3(256), 0, st, stats, gamma, beta, rmean, rvar, smean, sinv, coef,
+                     M, C, eps, momentum);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t zoo_stats_finalize(float* buf, int n2, int nslot, hipStream_t st) {
   hipLaunchKernelGGL(stats_finalize_kernel, dim3((n2 + 63) / 64), dim3(256), 0, st, buf, n2, nslot);

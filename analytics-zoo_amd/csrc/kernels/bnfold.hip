@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void bnfold_coef_kernel(int K, const float* __
 // (blockDim.x threads cover the row in chunks: K / 8 <= 256 chunks per row here)
 __global__ __launch_bounds__(256) void bnpro_apply_kernel(const bf16_t* __restrict__ g, const bf16_t* __restrict__ y,
                                                           const float* __restrict__ coef, bf16_t* __restrict__ dy,
-                                                          long long rows, int K) {
+                                                          long long rows, int K, int relu) {
   const int cpr = K / 8;                        // chunks per row
   const int rpb = blockDim.x / cpr;             // rows per block step (launcher: cpr <= 256, divides 256)
   const int ch = threadIdx.x % cpr, r0 = threadIdx.x / cpr;
@@ -66,7 +66,10 @@ __global__ __launch_bounds__(256) void bnpro_apply_kernel(const bf16_t* __restri
     unpack8(*reinterpret_cast<const uint4*>(g + off), gv);
     unpack8(*reinterpret_cast<const uint4*>(y + off), yv);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = ca[e] * gv[e] + cb[e] * yv[e] + cc[e];
+    for (int e = 0; e < 8; ++e) {
+      o[e] = ca[e] * gv[e] + cb[e] * yv[e] + cc[e];
+      if (relu) o[e] = fmaxf(o[e], 0.f);
+    }
     *reinterpret_cast<uint4*>(dy + off) = pack8(o);
   }
 }
@@ -75,14 +78,17 @@ __global__ __launch_bounds__(256) void bnpro_apply_kernel(const bf16_t* __restri
 __global__ __launch_bounds__(256) void bnpro_apply_any_kernel(const bf16_t* __restrict__ g,
                                                               const bf16_t* __restrict__ y,
                                                               const float* __restrict__ coef,
-                                                              bf16_t* __restrict__ dy, size_t n8, int K) {
+                                                              bf16_t* __restrict__ dy, size_t n8, int K, int relu) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
     const int k0 = (int)((i * 8) % K);
     float gv[8], yv[8], o[8];
     unpack8(*reinterpret_cast<const uint4*>(g + i * 8), gv);
     unpack8(*reinterpret_cast<const uint4*>(y + i * 8), yv);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = coef[k0 + e] * gv[e] + coef[K + k0 + e] * yv[e] + coef[2 * K + k0 + e];
+    for (int e = 0; e < 8; ++e) {
+      o[e] = coef[k0 + e] * gv[e] + coef[K + k0 + e] * yv[e] + coef[2 * K + k0 + e];
+      if (relu) o[e] = fmaxf(o[e], 0.f);
+    }
     *reinterpret_cast<uint4*>(dy + i * 8) = pack8(o);
   }
 }
@@ -99,8 +105,9 @@ extern "C" hipError_t zoo_bnfold_coef(int K, const float* gamma, const float* me
   return hipGetLastError();
 }
 
+// relu: max(., 0) of the result (the forward consumer-side apply's fallback, conv_fwd pro_fwd)
 extern "C" hipError_t zoo_bnpro_apply(const void* g, const void* y, const float* coef, void* dy, size_t n, int K,
-                                      hipStream_t st) {
+                                      int relu, hipStream_t st) {
   if (K % 8) return hipErrorInvalidValue;
   const long long rows = (long long)(n / K);
   if (rows == 0) return hipSuccess;
@@ -109,13 +116,13 @@ extern "C" hipError_t zoo_bnpro_apply(const void* g, const void* y, const float*
     size_t b = (n8 + 255) / 256;
     if (b > 4096) b = 4096;
     hipLaunchKernelGGL(bnpro_apply_any_kernel, dim3((unsigned)b), dim3(256), 0, st, (const bf16_t*)g,
-                       (const bf16_t*)y, coef, (bf16_t*)dy, n8, K);
+                       (const bf16_t*)y, coef, (bf16_t*)dy, n8, K, relu);
     return hipGetLastError();
   }
   const int rpb = 256 / (K / 8);
   long long blocks = (rows + rpb - 1) / rpb;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(bnpro_apply_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (const bf16_t*)g,
-                     (const bf16_t*)y, coef, (bf16_t*)dy, rows, K);
+                     (const bf16_t*)y, coef, (bf16_t*)dy, rows, K, relu);
   return hipGetLastError();
 }

@@ -68,6 +68,10 @@ struct BwdStats {
   // positions only -- the compact data gradient of a 1x1 stride-2 projection shortcut, which
   // then never gets its zero-interleaved full-size tensor (pw.hip EPI 2 only)
   int resid_half;
+  // 1: forward consumer-side BN apply (pw.hip EPI 1 prologue): X is a conv -> BN -> ReLU unit's
+  // pre-BN output y; the GEMM runs on relu(coef[k] y + coef[2 Kx + k]) (pro_coef [3][Kx], the
+  // middle row unused), written to pro_dy by channel group 0 -- that unit's output z
+  int pro_fwd;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

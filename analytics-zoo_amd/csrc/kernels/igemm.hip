@@ -816,7 +816,7 @@ extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* 
 extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf, const float* bias,
                                 const void* resid, float* stats, const ConvGeom* g, int act, const BwdStats* bsp,
                                 hipStream_t st) {
-  if (bsp && (bsp->pro_y || bsp->resid_half)) {
+  if (bsp && (bsp->pro_y || bsp->resid_half || bsp->pro_fwd)) {
     // the BN-backward prologue and the half-resolution residual exist only in pw.hip (the caller
     // materialises dy / the full-size residual otherwise)
     const int epi = igemm_epi(Y, Yf, bias, resid, act, g->omap, bsp->sums, stats);

@@ -134,7 +134,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
 
   // A fragments of tile t: lane -> pixel row t*TPM + 16 j + fr, k-chunk kb*32 + 8 fq
   // (PRO: the unit's pre-BN output y at the same positions into yf)
-  constexpr int YJ = PRO ? MJ : 1, YK = PRO ? KT : 1;
+  // PRO with EPI 1: the forward consumer-side BN apply -- one operand (X = y), no y fragments
+  constexpr bool PRO_Y = PRO && EPI == 2;
+  constexpr int YJ = PRO_Y ? MJ : 1, YK = PRO_Y ? KT : 1;
   const bf16_t* const pro_y = reinterpret_cast<const bf16_t*>(bs.pro_y);
   bf16_t* const pro_dy = reinterpret_cast<bf16_t*>(bs.pro_dy);
   auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT], bf16x8 (&yf)[YJ][YK]) {
@@ -157,16 +159,50 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
 #pragma unroll
         for (int kb = 0; kb < KT; ++kb) af[j][kb] = *reinterpret_cast<const bf16x8*>(src + kb * 32);
       }
-      if constexpr (PRO) {
+      if constexpr (PRO_Y) {
         const bf16_t* ys = pro_y + (size_t)row * K + 8 * fq;
 #pragma unroll
         for (int kb = 0; kb < KT; ++kb) yf[j][kb] = *reinterpret_cast<const bf16x8*>(ys + kb * 32);
       }
     }
   };
+  // PRO, EPI 1: z = relu(A y + Cc) in place of y (and, channel group 0, stored: the unit's output)
+  auto prologue_fwd = [&](int t, bf16x8 (&af)[MJ][KT]) {
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int row = t * TPM + 16 * j + fr;
+      const bool st = g == 0 && pro_dy != nullptr && row < p.M;
+#pragma unroll
+      for (int kb = 0; kb < KT; ++kb) {
+        const int k0 = kb * 32 + 8 * fq;
+        const uint4 xu = __builtin_bit_cast(uint4, af[j][kb]);
+        const uint32_t xw4[4] = {xu.x, xu.y, xu.z, xu.w};
+        uint32_t ow[4];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 a4 = *reinterpret_cast<const float4*>(pco + k0 + 4 * h);
+          const float4 c4 = *reinterpret_cast<const float4*>(pco + 2 * K + k0 + 4 * h);
+          const uint32_t x0 = xw4[2 * h], x1 = xw4[2 * h + 1];
+          const float o0 = fmaxf(a4.x * __uint_as_float(x0 << 16) + c4.x, 0.f);
+          const float o1 = fmaxf(a4.y * __uint_as_float(x0 & 0xffff0000u) + c4.y, 0.f);
+          const float o2 = fmaxf(a4.z * __uint_as_float(x1 << 16) + c4.z, 0.f);
+          const float o3 = fmaxf(a4.w * __uint_as_float(x1 & 0xffff0000u) + c4.w, 0.f);
+          ow[2 * h] = pack2bf(o0, o1);
+          ow[2 * h + 1] = pack2bf(o2, o3);
+        }
+        const uint4 pk = make_uint4(ow[0], ow[1], ow[2], ow[3]);
+        af[j][kb] = __builtin_bit_cast(bf16x8, pk);
+        if (st) *reinterpret_cast<uint4*>(pro_dy + (size_t)row * K + k0) = pk;
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   // PRO: dy = A g + B y + Cc in place of g (and, channel group 0, stored for the weight gradient)
   auto prologue = [&](int t, bf16x8 (&af)[MJ][KT], const bf16x8 (&yf)[YJ][YK]) {
-    if constexpr (PRO) {
+    if constexpr (PRO && EPI == 1) {
+      prologue_fwd(t, af);
+    } else if constexpr (PRO) {
       // the coefficient reads are loop-invariant: hoisted out of the tile loop they would pin
       // 24 * KT registers for the whole kernel. The empty clobber keeps them per chunk.
       asm volatile("" ::: "memory");
@@ -473,6 +509,8 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
+  // the forward consumer-side apply: plain forward epilogue, K <= 128 (register budget as above)
+  if (bs && bs->pro_fwd && (route != 1 || g->Ktot > 128 || bs->pro_y)) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
   if (bs && bs->resid_half && (route != 2 || (g->H & 1) || (g->W & 1))) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
@@ -498,7 +536,9 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   // the prologue at K = 128 runs 64-channel groups (register budget, see pw_dispatch)
-  const int NP = (bs.pro_y && g->Ktot == 128 && g->K % 64 == 0) ? 64 : pw_np(g->K, g->Ktot);
+  const int NP = ((bs.pro_y || bs.pro_fwd) && g->Ktot == 128 && g->K % 64 == 0) ? 64 : pw_np(g->K, g->Ktot);
+  if (epi == 1 && bs.pro_fwd)
+    return pw_dispatch<1, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (epi == 1)
     return pw_dispatch<1, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (bs.pro_y)

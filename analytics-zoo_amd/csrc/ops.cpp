@@ -135,7 +135,9 @@ hipError_t zoo_nhwc_u8_to_s2d(const void*, void*, int, int, int, int, int, int, 
                               hipStream_t);
 hipError_t zoo_bnfold_coef(int, const float*, const float*, const float*, const float*, long long, float*, float*,
                            float*, hipStream_t);
-hipError_t zoo_bnpro_apply(const void*, const void*, const float*, void*, size_t, int, hipStream_t);
+hipError_t zoo_bnpro_apply(const void*, const void*, const float*, void*, size_t, int, int, hipStream_t);
+hipError_t zoo_bn_fwd_coef(const float*, const float*, const float*, float*, float*, float*, float*, float*, int, int,
+                           float, float, hipStream_t);
 hipError_t zoo_convlstm_step(const void*, const void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
                              const float*, const float*, float*, float*, float*, void*, int, const float*,
                              const float*, float*, int, float*, void*, int, int, hipStream_t);
@@ -273,7 +275,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bsums, c10::optional<torch::Tensor> bgamma,
                        c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
                        c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy,
-                       bool resid_half) {
+                       bool resid_half, bool pro_fwd) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -408,6 +410,21 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     bs.pro_coef = pro_coef->data_ptr<float>();
     bs.pro_dy = opt_ptr<void>(pro_dy);
   }
+  // forward consumer-side BN apply: x is a conv -> BN -> ReLU unit's pre-BN output y; the GEMM runs
+  // on z = relu(coef[c] y + coef[2C + c]), which pw.hip forms in registers and writes to pro_dy
+  if (pro_fwd) {
+    TORCH_CHECK(!(pro_y.has_value() && pro_y->defined()), "conv_fwd: pro_fwd and pro_y are exclusive");
+    TORCH_CHECK(pro_coef.has_value() && pro_coef->defined() && pro_dy.has_value() && pro_dy->defined(),
+                "conv_fwd: pro_fwd needs pro_coef and pro_dy");
+    req(*pro_coef, at::kFloat, "pro_coef");
+    req(*pro_dy, at::kBFloat16, "pro_dy");
+    TORCH_CHECK(pro_coef->numel() == 3 * (int64_t)C && pro_dy->numel() == x.numel(),
+                "conv_fwd: pro_coef must be [3 * C], pro_dy must match x");
+    check_al16(pro_dy->data_ptr(), "pro_dy");
+    bs.pro_fwd = 1;
+    bs.pro_coef = pro_coef->data_ptr<float>();
+    bs.pro_dy = pro_dy->data_ptr();
+  }
   // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
   // they are folded in order into the caller's buffer (its first 2K floats)
   float* const stat_dst = sp ? sp : bs.sums;
@@ -441,13 +458,23 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   if (bs.pro_y) {
     if (!zoo_pw_eligible(&g, route, &bs)) {
       xin = (pro_dy.has_value() && pro_dy->defined()) ? *pro_dy : torch::empty_like(x);
-      check_hip(zoo_bnpro_apply(x.data_ptr(), pro_y->data_ptr(), bs.pro_coef, xin.data_ptr(), x.numel(), C,
+      check_hip(zoo_bnpro_apply(x.data_ptr(), pro_y->data_ptr(), bs.pro_coef, xin.data_ptr(), x.numel(), C, 0,
                                 cur_stream()),
                 "bnpro_apply");
       bs.pro_y = nullptr;
       bs.pro_coef = nullptr;
       bs.pro_dy = nullptr;
     }
+  }
+  if (bs.pro_fwd && !zoo_pw_eligible(&g, route, &bs)) {
+    // no prologue outside pw.hip: materialise z = relu(A y + Cc) into pro_dy and convolve that
+    check_hip(zoo_bnpro_apply(x.data_ptr(), x.data_ptr(), bs.pro_coef, pro_dy->data_ptr(), x.numel(), C, 1,
+                              cur_stream()),
+              "bnpro_apply relu");
+    xin = *pro_dy;
+    bs.pro_fwd = 0;
+    bs.pro_coef = nullptr;
+    bs.pro_dy = nullptr;
   }
   if (bs.resid_half && !zoo_pw_eligible(&g, route, &bs)) {
     // only pw.hip reads the half-resolution residual: zero-interleave it to full size
@@ -1970,7 +1997,7 @@ void bnpro_apply(torch::Tensor g, torch::Tensor y, torch::Tensor coef, torch::Te
   const int64_t K = g.size(-1);
   TORCH_CHECK(K % 8 == 0 && y.numel() == g.numel() && out.numel() == g.numel() && coef.numel() == 3 * K,
               "bnpro_apply: g / y / out [..., K % 8 == 0], coef [3K]");
-  check_hip(zoo_bnpro_apply(g.data_ptr(), y.data_ptr(), coef.data_ptr<float>(), out.data_ptr(), g.numel(), (int)K,
+  check_hip(zoo_bnpro_apply(g.data_ptr(), y.data_ptr(), coef.data_ptr<float>(), out.data_ptr(), g.numel(), (int)K, 0,
                             cur_stream()),
             "bnpro_apply");
 }
@@ -3121,7 +3148,24 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm", &gemm);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
         py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
-        py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false);
+        py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false,
+        py::arg("pro_fwd") = false);
+  m.def("bn_fwd_coef", [](torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean,
+                          torch::Tensor rvar, torch::Tensor smean, torch::Tensor sinv, int64_t M, double eps,
+                          double momentum) {
+    const int C = gamma.numel();
+    for (auto* t : {&stats, &gamma, &beta, &rmean, &rvar, &smean, &sinv}) req(*t, at::kFloat, "bn_fwd_coef vector");
+    TORCH_CHECK(stats.numel() >= 2 * C && beta.numel() == C && rmean.numel() == C && rvar.numel() == C &&
+                    smean.numel() == C && sinv.numel() == C && M > 0 && M < (1LL << 31),
+                "bn_fwd_coef: sizes");
+    auto coef = torch::empty({3 * (int64_t)C}, gamma.options());
+    check_hip(zoo_bn_fwd_coef(stats.data_ptr<float>(), gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                              rmean.data_ptr<float>(), rvar.data_ptr<float>(), smean.data_ptr<float>(),
+                              sinv.data_ptr<float>(), coef.data_ptr<float>(), (int)M, C, (float)eps, (float)momentum,
+                              cur_stream()),
+              "bn_fwd_coef");
+    return coef;
+  }, "statistics -> saved mean / invstd, running averages and the [scale | 0 | shift] forward affine");
   m.def("flip_weights", &flip_weights);
   m.def("flip_weights_batched", &flip_weights_batched);
   m.def("flip_desc_ints", &flip_desc_ints);

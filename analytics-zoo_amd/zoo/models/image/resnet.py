@@ -65,6 +65,10 @@ S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
 # projection blocks: the shortcut's dgrad runs first and hands its dx to conv1's dgrad, which then
 # also fuses the previous block's BN-backward reduction (stage transitions)
 SHORTCUT_FIRST = os.environ.get("ZOO_SHORTCUT_FIRST", "1") != "0"
+# bottlenecks: conv2's BN + ReLU applied by conv3 (1x1) in its operand prologue, conv2's apply pass
+# skipped (BNProducer.fwd_pro, pw.hip forward prologue). Off: -0.3 % with the 64- and 128-wide
+# units, +-0 with the 64-wide ones alone (profiles/r5/ab_fwd_consumer_apply_r5.md)
+FWD_PRO = os.environ.get("ZOO_FWD_PRO", "0") != "0"
 
 
 def _bp():
@@ -94,6 +98,8 @@ class Bottleneck(nn.Module):
             sc = self.down(x) if self.down is not None else x
             return self.conv3(self.conv2(self.conv1(x)), resid=sc)
         p1, p2, p3 = _bp(), _bp(), _bp()
+        if p2 is not None and FWD_PRO and self.conv3.k == 1 and self.conv3.stride == 1:
+            p2.fwd_pro = True
         if self.down is None:
             # identity shortcut: conv3's residual gradient is added in conv1's dgrad epilogue, which makes
             # conv1 the sole consumer of x -> it also fuses the previous block's BN-backward reduction

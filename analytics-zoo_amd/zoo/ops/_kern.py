@@ -21,7 +21,7 @@ from zoo.ops._native import native
 
 def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
              act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None, pro=None,
-             resid_half=False):
+             resid_half=False, pro_fwd=None):
     """``bstats = (z or None, y, mean, inv, sums[, gamma, beta])`` fuses the producing unit's
     BN-backward reduction (and ReLU mask) into this conv's epilogue. The mask source: a bf16
     ``z`` (ReLU output), a uint8 ``z`` (1-bit mask of the forward apply), or -- z None and
@@ -30,16 +30,22 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
     runs on that unit's BN backward dy = A g + B y + Cc instead (the BN-backward prologue,
     csrc/kernels/bnfold.hip); dy is written to ``dy_out``.
     ``resid_half``: ``resid`` is [N, P/2, Q/2, K], added at the even output positions only (the
-    compact data gradient of a 1x1 stride-2 shortcut, :func:`conv_dgrad_s2_compact`)."""
+    compact data gradient of a 1x1 stride-2 shortcut, :func:`conv_dgrad_s2_compact`).
+    ``pro_fwd = (coef, z_out)``: ``x`` is a conv -> BN -> ReLU unit's pre-BN output y and the GEMM
+    runs on that unit's z = relu(coef[c] y + coef[2C + c]), which is also written to ``z_out`` (the
+    forward consumer-side apply; ``coef`` from ``bn_fwd_coef``)."""
     bz = by = bm = bi = bsum = bg = bb = None
     if bstats is not None:
         bz, by, bm, bi, bsum = bstats[:5]
         if len(bstats) > 5:
             bg, bb = bstats[5], bstats[6]
     py, pc, pd = pro if pro is not None else (None, None, None)
+    if pro_fwd is not None:
+        pc, pd = pro_fwd
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
-                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd, bool(resid_half))
+                             list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd, bool(resid_half),
+                             pro_fwd is not None)
 
 
 # ---------------------------------------------------------------------------

@@ -46,6 +46,8 @@ _BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
 # the 1x1 stride-2 shortcut hands its data gradient to the block's conv1 in compact form
 # (GradHandoff.half), added at the even positions by conv1's dgrad epilogue (pw.hip resid_half)
 _HALF_RESID = __import__("os").environ.get("ZOO_HALF_RESID", "1") != "0"
+# forward consumer-side BN apply for units of these widths (pw.hip prologue: K <= 128)
+_FWD_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_FWD_PRO_K", "64,128").split(",") if v)
 _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
 
 
@@ -100,13 +102,19 @@ class BNProducer:
     # residual hands over its affine (gamma, beta) and the epilogue recomputes the sign from the
     # y it reads for the sums anyway; a residual unit hands over the 1-bit mask its forward
     # apply wrote (``mask``). 2 bytes per element less epilogue traffic either way.
-    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused", "gamma", "beta", "mask")
+    # Forward consumer-side apply (``fwd_pro``, set by the model when the single consumer is a 1x1
+    # stride-1 conv): the unit skips its apply pass and leaves ``pending = (y, coef, z)`` -- z an
+    # unwritten tensor -- and the consumer's conv forms z = relu(A y + Cc) in its operand prologue
+    # (pw.hip), writing z as it goes. 2 bytes per element of the z re-read saved, and a launch.
+    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused", "gamma", "beta", "mask", "fwd_pro", "pending")
 
     def __init__(self, relu, y, mean, inv):
         self.relu, self.y, self.mean, self.inv = relu, y, mean, inv
         self.sums = None
         self.fused = False
         self.gamma = self.beta = self.mask = None
+        self.fwd_pro = False
+        self.pending = None
 
     def bstats(self, z):
         self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
@@ -150,7 +158,13 @@ class _ConvBNActFn(torch.autograd.Function):
         ctx.producer_in = producer_in
         wb = bf16_weight(w)
         stats = workspace.zeros(stat_len(K), x.device) if training else None
-        y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
+        pend = producer_in.pending if producer_in is not None else None
+        if pend is not None:
+            # this conv applies the producer's BN + ReLU in its operand prologue and writes x (= z)
+            producer_in.pending = None
+            y = _kern.conv_fwd(pend[0], wb, R, S, stride, pad, stats=stats, pro_fwd=(pend[1], x))
+        else:
+            y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
         ctx.sync = bool(training) and sync_bn_active()
         if ctx.sync:  # SyncBN (P5): global statistics over the data-parallel group
             all_reduce_stats(stats[:2 * K], y.numel() // K)
@@ -170,9 +184,17 @@ class _ConvBNActFn(torch.autograd.Function):
         po = producer_out if (training and relu and _BN_MASK) else None
         if po is not None and resid is not None:
             mask = torch.empty(y.numel() // 8, device=x.device, dtype=torch.uint8)
-        z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
-                            beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,
-                            training, side, mask)
+        if (po is not None and po.fwd_pro and resid is None and rb is None and not ctx.sync and K in _FWD_PRO_K
+                and gamma.dtype == torch.float32 and beta.dtype == torch.float32):
+            # consumer-side apply: statistics bookkeeping + affine here, z formed by the consumer
+            coef = C_.bn_fwd_coef(stats, gamma.detach().contiguous(), beta.detach().contiguous(), running_mean,
+                                  running_var, smean, sinv, y.numel() // K, eps, momentum)
+            z = torch.empty_like(y)
+            po.pending = (y, coef)
+        else:
+            z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
+                                beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,
+                                training, side, mask)
         if po is not None:
             po.mask = mask
             if resid is None:
