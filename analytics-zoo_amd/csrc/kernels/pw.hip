@@ -357,13 +357,17 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     }
   };
 
+  // the operand fragments are double-buffered (the next tile's load is in flight during this
+  // tile's MFMAs); the prologue's y fragments are not: process() consumes them in the prologue
+  // BEFORE it issues the next tile's loads into the same registers (KT * 4 VGPRs saved, which
+  // is what lets the prologue run at K = 256)
   bf16x8 fa[MJ][KT], fb[MJ][KT];
-  bf16x8 ya[YJ][YK], yb[YJ][YK];
+  bf16x8 ya[YJ][YK];
   int t = gw;
   if (t < ntiles) load_tile(t, fa, ya);
   for (; t < ntiles; t += 2 * GW) {
-    process(t, fa, fb, ya, yb);
-    if (t + GW < ntiles) process(t + GW, fb, fa, yb, ya);
+    process(t, fa, fb, ya, ya);
+    if (t + GW < ntiles) process(t + GW, fb, fa, ya, ya);
   }
 
   if (!want) return;
@@ -452,9 +456,11 @@ static hipError_t pw_dispatch(const ConvGeom& g, int NP, const bf16_t* X, const 
   // operand + y fragments of a double-buffered tile in registers: spill-free at K = 64, and at
   // K = 128 with 64-channel groups and 16-pixel tiles (198 VGPRs); K = 256 spills 108-308 bytes
   // per lane and ran 1.1-3.3x slower than apply + plain dgrad (profiles/r5/ab_bn_prologue_r5.md)
-  if (PRO && K > 128) return hipErrorNotSupported;
+  if (PRO && K > 256) return hipErrorNotSupported;
   if constexpr (PRO) {
     if (K == 128) return NP == 64 ? pw_launch<64, 16, 4, EPI, PRO>(g, X, W, Y, resid, stats, bs, st)
+                                  : pw_launch<128, 16, 4, EPI, PRO>(g, X, W, Y, resid, stats, bs, st);
+    if (K == 256) return NP == 64 ? pw_launch<64, 16, 8, EPI, PRO>(g, X, W, Y, resid, stats, bs, st)
                                   : hipErrorNotSupported;
   }
 #define PW_CASE(np, k, TPM)                                                                    \
@@ -508,7 +514,7 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   }();
   if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
-  if (bs && bs->pro_y && (route != 2 || g->Ktot > 128)) return 0;
+  if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
   // the forward consumer-side apply: plain forward epilogue, K <= 128 (register budget as above)
   if (bs && bs->pro_fwd && (route != 1 || g->Ktot > 128 || bs->pro_y)) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
@@ -536,7 +542,14 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   // the prologue at K = 128 runs 64-channel groups (register budget, see pw_dispatch)
-  const int NP = ((bs.pro_y || bs.pro_fwd) && g->Ktot == 128 && g->K % 64 == 0) ? 64 : pw_np(g->K, g->Ktot);
+  // prologue: 64-channel groups at K = 256 (256 VGPRs); at K = 128 64 unless ZOO_PRO_NP128
+  static const bool np128 = [] {
+    const char* e = getenv("ZOO_PRO_NP128");
+    return e && atoi(e) != 0;
+  }();
+  const bool pro = bs.pro_y || bs.pro_fwd;
+  const int NP = (pro && ((g->Ktot == 128 && !np128) || g->Ktot == 256) && g->K % 64 == 0) ? 64
+                                                                                              : pw_np(g->K, g->Ktot);
   if (epi == 1 && bs.pro_fwd)
     return pw_dispatch<1, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (epi == 1)

@@ -41,10 +41,11 @@ def test_bnfold_coef_and_apply_match_fp32_formulas(gpu):
 
 
 @pytest.mark.parametrize("M,K,N,det", [(4096, 64, 64, False), (3000, 64, 256, False), (4096, 256, 64, False),
-                                       (2048, 128, 512, False), (512, 72, 128, False), (3000, 64, 256, True)])
+                                       (2048, 128, 512, False), (512, 72, 128, False), (3000, 64, 256, True),
+                                       (5000, 256, 256, False), (3000, 128, 128, False), (2000, 512, 64, False)])
 def test_dgrad_prologue_matches_materialised_dy(gpu, M, K, N, det):
-    """A 1x1 dgrad with the BN-backward prologue (pw.hip PRO at K = 64; wider K, an odd width and
-    the deterministic mode's partial statistics take the materialising fallback) against the same
+    """A 1x1 dgrad with the BN-backward prologue (pw.hip PRO at K = 64 / 128 / 256; K = 512, an odd
+    width and the deterministic mode's partial statistics take the materialising fallback) against the same
     dgrad of dy materialised in fp32: the output, the written dy, with a residual operand and the
     producer's fused BN-backward epilogue."""
     from zoo.ops import _kern, deterministic, set_deterministic
