@@ -529,6 +529,12 @@ class ClusterServing:
     def run(self, running_flag=None, max_records=None, idle_timeout=None):
         """Serve until ``running_flag`` (a file path) disappears, ``max_records``
         are served, or nothing arrives for ``idle_timeout`` seconds."""
+        sw = float(os.environ.get("ZOO_SERVING_SWITCH_MS", "0"))
+        if sw > 0:
+            # the reader and the main loop hand the GIL back and forth around every native call;
+            # Python's 5 ms switch interval can hold a waiting thread for that long
+            import sys
+            sys.setswitchinterval(sw / 1000.0)
         if os.environ.get("ZOO_SERVING_GC_FREEZE", "0") != "0":
             # the model, graphs and buffers are long-lived: move them out of the collector's
             # view so a full collection does not walk them in the middle of a batch
