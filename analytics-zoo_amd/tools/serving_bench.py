@@ -508,6 +508,10 @@ def _suite_model(name, a, rank, world, local, gather):
                 x = (torch.randint(0, 30522, (bsz, 128), device="cuda:%d" % local).float() if bert
                      else torch.zeros(bsz, 3, 224, 224, device="cuda:%d" % local))
                 s.im.predict(x)
+                # the look-ahead path's pinned output ring is per output shape: allocate it now, not
+                # in the first open-loop batch of that size (a pinned allocation stalls for ms)
+                for _ in range(3):
+                    s.im.predict_async(x).result()
             # capacity: a pre-filled queue drained by the worker (the worker alone)
             n_cap = a.images
             for i in range(n_cap):
