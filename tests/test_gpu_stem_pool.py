@@ -15,7 +15,7 @@ def rel(a, b):
 
 @pytest.mark.parametrize("N,H,W,C,k,s,p", [(2, 112, 112, 64, 3, 2, 1), (3, 15, 17, 128, 3, 2, 1),
                                            (2, 9, 8, 16, 3, 2, 1),      # compile-time stem geometry
-                                           (2, 10, 12, 16, 3, 2, 1), (1, 8, 6, 256, 3, 2, 1),   # 2x2-quad backward
+                                           (2, 10, 12, 16, 3, 2, 1), (1, 8, 6, 256, 3, 2, 1), (1, 8, 8, 256, 3, 2, 1),   # fwd2 pairs
                                            (2, 10, 13, 32, 2, 2, 0), (2, 11, 9, 64, 3, 1, 1)])  # generic
 def test_bn_relu_maxpool_vs_fp32(gpu, N, H, W, C, k, s, p):
     from zoo.ops.bn import ShortcutBN, bn_relu_maxpool, stat_len
