@@ -217,7 +217,11 @@ class TrainingEngine:
         # capture the updates are captured too: the optimizer kernels then read the learning rate
         # and bias corrections from a device buffer staged before every replay
         # (OptimMethod.enable_device_hparams), so the graph follows the schedule.
-        self.ibo = bool(os.environ.get("ZOO_OPTIM_IN_BWD", "1") != "0" and clip is None and
+        # Captured steps keep the optimizer at the end of the step unless ZOO_OPTIM_IN_BWD_GRAPH=1:
+        # NCF (one small bucket, the step launch-bound) replays 0.234 ms/step with the updates
+        # inside the graph against 0.228 without (profiles/r5/bench_ncf_r5.log)
+        ibo_graph_ok = not self.hip_graph or os.environ.get("ZOO_OPTIM_IN_BWD_GRAPH", "0") != "0"
+        self.ibo = bool(os.environ.get("ZOO_OPTIM_IN_BWD", "1") != "0" and clip is None and ibo_graph_ok and
                         wstream.on() and getattr(optim_method, "supports_ranges", lambda: False)() and
                         self.sync.enable_ibo(optim_method))
         if self.ibo and self.hip_graph and hasattr(optim_method, "enable_device_hparams"):

@@ -185,6 +185,7 @@ def test_graph_captured_ibo_matches_eager(gpu, monkeypatch):
     runs = {}
     for graph in (False, True):
         monkeypatch.setenv("ZOO_OPTIM_IN_BWD", "1" if graph else "0")
+        monkeypatch.setenv("ZOO_OPTIM_IN_BWD_GRAPH", "1")
         # total / warmup: the learning rate changes every step, so a baked-in rate would show
         eng = TrainingEngine(copy.deepcopy(m), softmax_cross_entropy,
                              AdamWeightDecay(lr=1e-4, warmup_portion=0.3, total=10), bucket_mb=0.5, hip_graph=graph)
