@@ -39,9 +39,23 @@ def _key(device):
     return d.index if d.index is not None else torch.cuda.current_device()
 
 
+_USED = set()   # devices whose captured graphs contain dropout kernels that read the offset
+
+
 def seed_offset_live(device):
-    """Whether the dropout kernels of ``device`` read a per-step device seed offset."""
-    return _key(device) in _SEED
+    """Whether the dropout kernels of ``device`` read a per-step device seed offset. Called by the
+    dropout paths while a graph is being captured; a True answer there also records that the
+    graph needs the offset restaged before its replays (``seed_offset_used``)."""
+    k = _key(device)
+    live = k in _SEED
+    if live and torch.cuda.is_current_stream_capturing():
+        _USED.add(k)
+    return live
+
+
+def seed_offset_used(device):
+    """Whether any graph captured on ``device`` reads the dropout seed offset."""
+    return _key(device) in _USED
 
 
 def dropout_seed_stager(device):
