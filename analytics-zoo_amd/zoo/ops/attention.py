@@ -18,6 +18,19 @@ from zoo.ops._native import available, native
 from zoo.ops.pointwise import _seed
 
 
+def _dropout_seed(device, pdrop):
+    """A per-call dropout seed. Under hipGraph capture the kernels XOR in the device seed
+    offset (attention.hip), so the capture must record that the graph reads it: the engine
+    restages the offset before a replay only when some captured kernel does
+    (devscalar.seed_offset_used)."""
+    if pdrop <= 0:
+        return 0
+    if torch.cuda.is_current_stream_capturing():
+        from zoo.ops.devscalar import seed_offset_live
+        seed_offset_live(device)
+    return _seed()
+
+
 def _reference(q, k, v, mask, causal, dropout_p, training):
     scale = 1.0 / math.sqrt(q.shape[-1])
     w = torch.matmul(q, k.transpose(-1, -2)) * scale
@@ -36,7 +49,7 @@ def _reference(q, k, v, mask, causal, dropout_p, training):
 class _FlashAttnFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, q, k, v, mask, causal, pdrop):
-        seed = _seed() if pdrop > 0 else 0
+        seed = _dropout_seed(q.device, pdrop)
         o, lse = native().attn_fwd(q, k, v, mask, causal, pdrop, seed)
         ctx.save_for_backward(q, k, v, mask, o, lse)
         ctx.causal, ctx.pdrop, ctx.seed = causal, pdrop, seed
@@ -71,7 +84,7 @@ class _FlashAttnPackedFn(torch.autograd.Function):
     def forward(ctx, qkv, mask, causal, pdrop, n_head):
         B, L, three_h = qkv.shape
         hd = three_h // (3 * n_head)
-        seed = _seed() if pdrop > 0 else 0
+        seed = _dropout_seed(qkv.device, pdrop)
         v5 = qkv.view(B, L, 3, n_head, hd).permute(2, 0, 3, 1, 4)   # [3, B, H, L, hd] strided views
         o, lse = native().attn_fwd_strided(v5[0], v5[1], v5[2], mask, causal, True, pdrop, seed)
         ctx.save_for_backward(qkv, mask, o, lse)
@@ -112,7 +125,7 @@ def attention_packed(qkv, n_head, mask=None, causal=False, dropout_p=0.0, traini
         return _FlashAttnPackedFn.apply(qkv, m, bool(causal), pdrop, n_head)
     v5 = qkv.view(B, L, 3, n_head, hd).permute(2, 0, 3, 1, 4)   # [3, B, H, L, hd] strided views
     o, _ = native().attn_fwd_strided(v5[0], v5[1], v5[2], m, bool(causal), True, pdrop,
-                                     _seed() if pdrop > 0 else 0)
+                                     _dropout_seed(qkv.device, pdrop))
     return o.view(B, L, n_head * hd)
 
 

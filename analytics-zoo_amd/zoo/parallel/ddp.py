@@ -127,7 +127,7 @@ def record_lookup(table, idx):
 
 class _Bucket:
     __slots__ = ("idx", "lo", "hi", "params", "pending", "launched", "cb", "so", "pack", "recv", "gath",
-                 "works", "post", "sparse", "gath16", "ev0", "ev1", "ibo_off")
+                 "works", "post", "sparse", "gath16", "ev0", "ev1", "ibo_off", "carry", "carry_late")
 
     def __init__(self, idx, lo, hi):
         self.idx, self.lo, self.hi = idx, lo, hi
@@ -141,6 +141,8 @@ class _Bucket:
         self.post = None
         self.sparse = []     # [(param, lo, hi)] when every parameter of the bucket is row-sparse
         self.gath16 = None   # ZeRO-1 bf16 weight all-gather target
+        self.carry = None    # in-backward optimizer: a late gradient contribution for the next update
+        self.carry_late = False
         self.ev0 = self.ev1 = None  # comm-stream events around the bucket's collectives (stats)
         self.ibo_off = False        # in-backward update switched off (counts not stable)
 
@@ -631,15 +633,17 @@ class GradSync:
         """p got more gradient contributions than calibrated: bucket b is updated at the end of
         every later step. Not yet updated this step -> the end-of-step update sees the whole
         gradient. Already updated -> the late contribution was ordered behind the update
-        (_ibo_pre) and lands in a cleared slot; it is dropped (the engine clears the buffer
-        before the next step) instead of being applied twice or leaking into the next step."""
+        (_ibo_pre) and lands in the cleared slot; the end of the step saves it (``b.carry``) and
+        the bucket's next update adds it in: nothing is lost or applied twice, the late part of
+        this one step arrives one update later."""
         b.ibo_off = True
         if b.launched:
             self._ibo_cleared = False
+            b.carry_late = True
             log.warning("in-backward optimizer: parameter %s got %d gradient contributions, %d calibrated, "
-                        "after its bucket was updated; this step's late contribution is dropped and the "
-                        "bucket is updated at the end of each step from now on (ZOO_OPTIM_IN_BWD=0 turns "
-                        "the in-backward update off)", tuple(p.shape), c, exp)
+                        "after its bucket was updated; this step's late contribution is applied with the "
+                        "next update and the bucket is updated at the end of each step from now on "
+                        "(ZOO_OPTIM_IN_BWD=0 turns the in-backward update off)", tuple(p.shape), c, exp)
         else:
             b.pending = -1
             log.warning("in-backward optimizer: parameter %s got %d gradient contributions, %d calibrated; "
@@ -676,8 +680,17 @@ class GradSync:
         cleared = True
         for b in self.buckets:
             if b.idx not in self._ibo_done:
+                carry = getattr(b, "carry", None)
+                if carry is not None:   # a late contribution of the previous step (_ibo_disable)
+                    flat.grad[b.lo:b.hi].add_(carry)
+                    b.carry = None
                 cleared &= bool(self.ibo_optim.step_range(flat.master, flat.grad, flat.bf16, 1.0, b.lo, b.hi,
                                                           zero_grad=True))
+            elif getattr(b, "carry_late", False):
+                # updated in-backward before the late contribution arrived: the slot holds only
+                # that contribution; keep it for this bucket's next (end-of-step) update
+                b.carry = flat.grad[b.lo:b.hi].clone()
+                b.carry_late = False
         flat.grad_clean = cleared and self._ibo_cleared
         self._ibo_cleared = True
         self.ibo_optim.finish_step(flat.bf16 is not None)

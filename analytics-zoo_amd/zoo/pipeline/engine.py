@@ -257,6 +257,12 @@ class TrainingEngine:
                                                 (self.hip_graph and getattr(self.optim, "_dev_hp", None) is None)):
             self.sync.ibo_optim = None   # optimizer / clipping / graph mode changed: plain end-of-step update
             self.ibo = False
+            # graphs captured with the in-backward updates inside would keep replaying them
+            # (unclipped, and doubled by the end-of-step update): recapture without
+            if any(g[4] for g in self._graphs.values()):
+                torch.cuda.synchronize(self.device)
+                self._graphs.clear()
+                self._graph_warm.clear()
         if getattr(self.optim, "_dev_hp", None) is not None:
             self.optim.stage_device_hparams()
         if self._seed_stager is not None and (not self._graphs or seed_offset_used(self.device)):

@@ -19,6 +19,7 @@ import logging
 import queue
 import threading
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -48,6 +49,7 @@ class _Replica:
         self.pool = torch.cuda.graph_pool_handle() if dev.type == "cuda" else None
         self.graphs = {}
         self.host_rings, self.host_idx, self.slot_events = {}, {}, {}
+        self.slot_owner = {}   # (key, slot) -> weakref of the _Pending whose result lives in the slot
 
     RING = 3
 
@@ -151,16 +153,26 @@ class _Replica:
                 self.host_idx[key] = 0
             i = self.host_idx[key]
             self.host_idx[key] = i + 1
-            slot = ring[i % self.RING]
-            ev = self.slot_events.get((key, i % self.RING))
-            if ev is not None:   # the slot's previous result must have been consumed (at most RING in flight)
-                ev.synchronize()
+            si = i % self.RING
+            prev = self.slot_owner.get((key, si))
+            prev = prev() if prev is not None else None
+            if prev is not None and not prev.consumed:
+                # more than RING handles outstanding: the slot's last result has not been read yet,
+                # so this batch gets fresh pinned buffers (the unread handle keeps the old ones)
+                ring[si] = [torch.empty(o.shape, dtype=torch.float32, pin_memory=True) for o in outs]
+            else:
+                ev = self.slot_events.get((key, si))
+                if ev is not None:   # the slot's previous D2H copy must be complete before it is rewritten
+                    ev.synchronize()
+            slot = ring[si]
             for h, o in zip(slot, outs):
                 h.copy_(o if o.dtype == torch.float32 else o.float(), non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
-            self.slot_events[(key, i % self.RING)] = ev
-        return _Pending(ev, slot, multi, xs[0].shape[0])
+            self.slot_events[(key, si)] = ev
+        pend = _Pending(ev, slot, multi, xs[0].shape[0])
+        self.slot_owner[(key, si)] = weakref.ref(pend)
+        return pend
 
 
 class _Pending:
@@ -168,6 +180,7 @@ class _Pending:
 
     def __init__(self, event, host, multi, n):
         self.event, self.host, self.multi, self.n = event, host, multi, n
+        self.consumed = False
 
     def done(self):
         return self.event is None or self.event.query()
@@ -176,6 +189,7 @@ class _Pending:
         if self.event is not None:
             self.event.synchronize()
         h = [t[:self.n].numpy().copy() for t in self.host]   # the pinned slot is reused RING batches later
+        self.consumed = True
         return h if self.multi else h[0]
 
 

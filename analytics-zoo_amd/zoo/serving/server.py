@@ -326,6 +326,11 @@ class ClusterServing:
             k = self._coef_idx % len(ring)
             slot = ring[k]
             self._coef_idx += 1
+            ev = self._coef_events.get(k)
+            if isinstance(ev, threading.Event):
+                # the slot's previous batch is still queued for the GPU: wait until _to_batch has
+                # enqueued its upload (never happens with a ring of qdepth + 3 slots)
+                ev.wait()
             ev = self._coef_events.pop(k, None)
             if ev is not None:   # the slot's previous upload must have left the host buffer
                 ev.synchronize()
@@ -337,14 +342,23 @@ class ClusterServing:
             return None
         if slot is None:   # (re)size the ring for this batch geometry and copy this batch in
             need = d["coef"].size
-            self._coef_ring = [torch.empty(need, dtype=torch.int16, pin_memory=True) for _ in range(4)]
+            self._coef_ring = [torch.empty(need, dtype=torch.int16, pin_memory=True)
+                               for _ in range(self._ring_slots())]
             self._coef_events = {}
             self._coef_idx = 1
             slot = self._coef_ring[0]
             slot.numpy()[:need] = d["coef"].reshape(-1)
             d["coef"] = slot.numpy()[:need].reshape(d["coef"].shape)
         n = d["coef"].size
-        return ("jpeg", d, slot[:n].view(d["coef"].shape), (self._coef_idx - 1) % len(self._coef_ring))
+        k = (self._coef_idx - 1) % len(self._coef_ring)
+        self._coef_events[k] = threading.Event()     # queued: set once its upload is enqueued
+        return ("jpeg", d, slot[:n].view(d["coef"].shape), k)
+
+    @staticmethod
+    def _ring_slots():
+        """Pinned host slots per ring: the reader runs up to ZOO_SERVING_QDEPTH queued batches plus
+        the one it decodes plus the one the GPU side holds ahead of the oldest upload still in flight."""
+        return max(4, int(os.environ.get("ZOO_SERVING_QDEPTH", "1")) + 3)
 
     def _decode_procs(self):
         """The multi-process decode pool (zoo/serving/decode_pool.py); ZOO_SERVING_DECODE_PROCS=0
@@ -375,9 +389,9 @@ class ClusterServing:
         ring = self._pinned.get(key)
         if ring is None:
             ring = self._pinned[key] = [torch.empty(len(ims), h, w, 3, dtype=torch.uint8, pin_memory=True)
-                                        for _ in range(4)]
+                                        for _ in range(self._ring_slots())]
             self._pin_idx[key] = 0
-        buf = ring[self._pin_idx[key] % 4]
+        buf = ring[self._pin_idx[key] % len(ring)]
         self._pin_idx[key] += 1
         arr = buf.numpy()
 
@@ -395,7 +409,12 @@ class ClusterServing:
             if self.im.device.type == "cuda":
                 ev = torch.cuda.Event()
                 ev.record(torch.cuda.current_stream(self.im.device))
-                self._coef_events[decoded[3]] = ev
+            else:
+                ev = None
+            queued = self._coef_events.get(decoded[3])
+            self._coef_events[decoded[3]] = ev
+            if isinstance(queued, threading.Event):
+                queued.set()
             return x
         if isinstance(decoded, tuple) and decoded[0] == "rgb":
             c, h, w = self.cfg["image_shape"]

@@ -137,8 +137,9 @@ def test_ibo_variable_shared_layer_matches_end_of_step(gpu, monkeypatch):
 
 def test_ibo_late_contribution_degrades_without_raising(gpu, monkeypatch, caplog):
     """A count that grows AFTER calibration (2, 2, then 3 uses): the step completes, a warning
-    is logged, the bucket moves to the end-of-step update for good, and the steps before the
-    surprise match the end-of-step run exactly."""
+    is logged, the bucket moves to the end-of-step update for good, the late contribution is
+    applied with the next update (not dropped), and the steps before the surprise match the
+    end-of-step run exactly."""
     import logging
     uses = [2, 2, 2, 3, 2, 2]
     (l0, w0), _ = _shared_run(uses, False, monkeypatch, gpu, 6)
@@ -151,7 +152,7 @@ def test_ibo_late_contribution_degrades_without_raising(gpu, monkeypatch, caplog
     assert ((w1 - w0).norm() / w0.norm()).item() < 0.05
 
 
-def _bert_cls(gpu, drop):
+def _bert_cls(gpu, drop, attn_drop=None):
     import torch.nn as nn
     from zoo.pipeline.api.keras.layers import BERT
 
@@ -159,7 +160,8 @@ def _bert_cls(gpu, drop):
         def __init__(self):
             super().__init__()
             self.bert = BERT(vocab=500, hidden_size=256, n_block=2, n_head=4, max_position_len=64,
-                             intermediate_size=1024, hidden_drop=drop, attn_drop=drop, output_all_block=False)
+                             intermediate_size=1024, hidden_drop=drop,
+                             attn_drop=drop if attn_drop is None else attn_drop, output_all_block=False)
             self.fc = nn.Linear(256, 3)
 
         def forward(self, xs):
@@ -225,3 +227,48 @@ def test_graph_replay_draws_fresh_dropout_masks(gpu):
     eng._seed_rng.getrandbits = lambda k: 12345     # a frozen offset: identical masks on every replay
     frozen = [float(eng.train_step(xs, y).float().item()) for _ in range(3)]
     assert max(frozen) - min(frozen) < 1e-6, frozen
+
+
+def test_graph_replay_attention_only_dropout_is_fresh(gpu):
+    """Attention-probability dropout alone (hidden dropout 0): the fused attention kernels read
+    the device seed offset, so the capture must mark it used and every replay draws new masks."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.ops import softmax_cross_entropy
+    from zoo.ops.devscalar import seed_offset_used
+    from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+    from zoo.pipeline.engine import TrainingEngine
+    init_nncontext("graph-attn-dropout")
+    torch.manual_seed(4)
+    m, xs, y = _bert_cls(gpu, 0.0, attn_drop=0.2)
+    eng = TrainingEngine(m, softmax_cross_entropy, AdamWeightDecay(lr=0.0, weight_decay=0.0), hip_graph=True)
+    losses = [float(eng.train_step(xs, y).float().item()) for _ in range(6)]
+    assert len(eng._graphs) == 1 and seed_offset_used(eng.device)
+    replayed = losses[2:]
+    assert len(set(round(v, 6) for v in replayed)) == len(replayed), losses
+
+
+def test_clipping_after_capture_recaptures_without_inbwd_updates(gpu, monkeypatch):
+    """A step captured WITH the in-backward updates must not be replayed once clipping is set
+    (the captured updates are unclipped and step() would update the buckets a second time):
+    the engine drops the graphs and recaptures a step without the updates."""
+    from zoo.common.nncontext import init_nncontext
+    from zoo.ops import softmax_cross_entropy
+    from zoo.parallel.ddp import global_norm_clip
+    from zoo.pipeline.api.keras.optimizers import AdamWeightDecay
+    from zoo.pipeline.engine import TrainingEngine
+    monkeypatch.setenv("ZOO_OPTIM_IN_BWD", "1")
+    monkeypatch.setenv("ZOO_OPTIM_IN_BWD_GRAPH", "1")
+    init_nncontext("ibo-graph-clip")
+    torch.manual_seed(5)
+    m, xs, y = _bert_cls(gpu, 0.0)
+    eng = TrainingEngine(m, softmax_cross_entropy, AdamWeightDecay(lr=1e-4), bucket_mb=0.5, hip_graph=True)
+    assert eng.ibo
+    for _ in range(4):
+        eng.train_step(xs, y)
+    assert len(eng._graphs) == 1 and len(next(iter(eng._graphs.values()))[4]) > 0
+    eng.clip = global_norm_clip(1.0)
+    eng.train_step(xs, y)
+    assert not eng.ibo and not eng._graphs
+    losses = [float(eng.train_step(xs, y).float().item()) for _ in range(4)]
+    assert len(eng._graphs) == 1 and len(next(iter(eng._graphs.values()))[4]) == 0
+    assert all(v == v and abs(v) < 1e3 for v in losses)

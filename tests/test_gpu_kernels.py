@@ -607,7 +607,7 @@ def test_inference_model_predict_async(gpu):
     im = InferenceModel(1, device=gpu).load_module(m)
     xs = [torch.randn(8, 3, 64, 64, device=gpu) for _ in range(6)]
     refs = [im.predict(x) for x in xs]
-    for k in (1, 2, 3):   # up to RING outstanding
+    for k in (1, 2, 3, 5):   # up to RING outstanding, and beyond (fresh pinned buffers, no aliasing)
         hs = []
         for i, x in enumerate(xs):
             hs.append(im.predict_async(x.clone()))   # the clone is dropped at once: record_stream keeps it
