@@ -13,7 +13,7 @@ import torch
 from zoo.utils import bigdl_proto as P
 from zoo.utils.bigdl_model import load_bigdl_model, save_bigdl_model
 
-FIX = "/root/reference/zoo/src/test/resources/models/zoo_keras"
+FIX = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "reference_models", "zoo_keras")
 needs_fixtures = pytest.mark.skipif(not os.path.isdir(FIX), reason="reference fixtures not present")
 
 

@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 from zoo.common.nncontext import init_nncontext
 
-REF = "/root/reference/zoo/src/test/resources/models"
+REF = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "reference_models")  # vendored
 PYREF = "/root/reference/pyzoo/test/zoo/resources"
 need_ref = pytest.mark.skipif(not os.path.exists(REF), reason="reference fixtures not present")
 
