@@ -42,6 +42,9 @@ class MemoryType:
 class DataStrategy:
     PARTITIONED = "PARTITIONED"
     REPLICATED = "REPLICATED"
+    # the arrays ARE this rank's partition (a Spark DataFrame partition living on its executor):
+    # no further sharding; every rank must hold the same number of samples (checked)
+    LOCAL = "LOCAL"
 
 
 def _world():
@@ -152,6 +155,9 @@ class ArrayFeatureSet(FeatureSet):
         if self.strategy == DataStrategy.REPLICATED:
             self.world, self.rank = 1, 0
         self.local_bs = max(1, self.batch_size // self.world)
+        self.presharded = self.strategy == DataStrategy.LOCAL
+        if self.presharded and self.world > 1:
+            self._check_equal_partitions()
         self._slices = 1
         self._dev_arrays = None
         self._pinned = None
@@ -172,19 +178,29 @@ class ArrayFeatureSet(FeatureSet):
             a = a.astype(np.float32)
         return np.ascontiguousarray(a)
 
+    def _check_equal_partitions(self):
+        """The synchronous collectives need every rank to run the same number of iterations."""
+        import torch.distributed as dist
+        dev = _device() if dist.get_backend() == "nccl" else torch.device("cpu")
+        t = torch.tensor([self.n, -self.n], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        hi, lo = int(t[0]), -int(t[1])
+        if hi != lo:
+            raise ValueError("DataStrategy.LOCAL needs equal partitions: ranks hold %d..%d samples" % (lo, hi))
+
     def size(self):
-        return self.n
+        return self.n * (self.world if self.presharded else 1)
 
     def num_of_slice(self):
         return self._slices
 
     def _order(self, train, epoch):
         if train and self.shuffle_:
-            rng = np.random.default_rng(1234 + (epoch or 0))
+            rng = np.random.default_rng(1234 + (epoch or 0) + (7919 * self.rank if self.presharded else 0))
             perm = rng.permutation(self.n)
         else:
             perm = np.arange(self.n)
-        if self.world > 1:
+        if self.world > 1 and not self.presharded:
             per = self.n // self.world if (train or self.drop_last) else int(math.ceil(self.n / self.world))
             shard = perm[self.rank::self.world][:per]
             return shard

@@ -105,6 +105,7 @@ class NNEstimator(_Params):
         self.checkpoint_config = None
         self._clip = None
         self.engine = None
+        self.localPartition = False
 
     # -- setters mirroring nn_classifier.py:224-437 --------------------------
     def setSamplePreprocessing(self, val):  # noqa: N802
@@ -146,6 +147,16 @@ class NNEstimator(_Params):
 
     def getDataCacheLevel(self):  # noqa: N802
         return self.dataCacheLevel[0]
+
+    def setLocalPartition(self, val=True):  # noqa: N802
+        """With one process per GPU: the DataFrame given to fit() is THIS rank's partition (as a
+        Spark DataFrame partition lives on its executor), not the whole dataset every rank
+        shards. All ranks must pass partitions of equal size; the batch size stays global."""
+        self.localPartition = bool(val)
+        return self
+
+    def isLocalPartition(self):  # noqa: N802
+        return self.localPartition
 
     def setLearningRate(self, val):  # noqa: N802
         self.learningRate = float(val)
@@ -219,7 +230,10 @@ class NNEstimator(_Params):
               "DEVICE": MemoryType.DEVICE}.get(level)
         if level == "DISK_AND_DRAM":
             mt = MemoryType.DISK_AND_DRAM(nslice)
-        return FeatureSet.from_ndarrays(feats, labels, batch_size, shuffle=shuffle, memory_type=mt)
+        from zoo.feature.common import DataStrategy
+        strategy = DataStrategy.LOCAL if self.localPartition else DataStrategy.PARTITIONED
+        return FeatureSet.from_ndarrays(feats, labels, batch_size, shuffle=shuffle, memory_type=mt,
+                                        data_strategy=strategy)
 
     def _label_for_criterion(self, y):
         return y

@@ -53,11 +53,15 @@ def parse():
                     help="gradient wire: auto = bf16 whenever GPU collectives run (BigDL 16-bit transfer)")
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="0: per-model default (ResNet 32, NCF one bucket)")
     ap.add_argument("--profile-steps", type=int, default=0)
-    ap.add_argument("--input", default="device", choices=["device", "featureset"],
+    ap.add_argument("--input", default="auto", choices=["auto", "device", "featureset"],
                     help="featureset: ResNet-50 trained through NNEstimator.fit on a synthetic DataFrame of uint8 "
                          "NHWC images (FeatureSet -> pinned batches -> copy stream -> on-device normalisation), "
-                         "BASELINE config 2; device: one device-resident fp32 batch")
-    return ap.parse_args()
+                         "BASELINE config 2; device: one device-resident fp32 batch reused every step; "
+                         "auto (default): featureset for ResNet-50, device for the other models")
+    a = ap.parse_args()
+    if a.input == "auto":
+        a.input = "featureset" if a.model == "resnet50" else "device"
+    return a
 
 
 def _sync(dev):
@@ -162,27 +166,32 @@ def run_featureset(a, ctx, world):
     warm = 10
     optim = SGD(learningrate=0.01, momentum=0.9, weightdecay=1e-4, dampening=0.0, nesterov=True,
                 learningrate_schedule=EpochDecayWithWarmUp(warm, (0.1 - 0.01) / warm, lambda epoch: 0))
-    n = a.batch * world * (a.warmup + a.steps)       # one epoch covers the whole run: no epoch edge
-    rng = np.random.default_rng(4321)
+    # each rank builds only ITS partition of the DataFrame (a Spark partition on its executor):
+    # one epoch covers the whole run, so no epoch edge falls inside the timed steps
+    n = a.batch * (a.warmup + a.steps)
+    rng = np.random.default_rng(4321 + 7 * ctx.rank)
     imgs = rng.integers(0, 256, size=(n, 224, 224, 3), dtype=np.uint8)
     labels = rng.integers(0, 1000, size=n)
     df = pd.DataFrame({"features": list(imgs), "label": labels})
     est = NNEstimator(model, softmax_cross_entropy, Lambda(lambda v: v), Lambda(lambda v: np.int64(v)))
     est.setBatchSize(a.batch * world).setOptimMethod(optim).setEndWhen(MaxIteration(a.warmup + a.steps))
+    est.setLocalPartition(True)
     dev = ctx.device
     mark = {}
 
     def timer(eng, state):
         it = state["neval"] - 1
+        # this iteration's device loss (a log_every flush has already moved it to the host)
+        cur = eng._pending_loss[-1][1] if eng._pending_loss else torch.tensor(state["Loss"])
         if it == 1:
-            mark["first"] = eng._pending_loss[-1][1]
+            mark["first"] = cur
         if it in (a.warmup, a.warmup + a.steps):
             _sync(dev)
             if world > 1:
                 dist.barrier()
             _sync(dev)
             mark[it] = time.perf_counter()
-            mark["last"] = eng._pending_loss[-1][1] if eng._pending_loss else None
+            mark["last"] = cur
     est._train_callbacks = (timer,)
     est.fit(df)
     elapsed = mark[a.warmup + a.steps] - mark[a.warmup]

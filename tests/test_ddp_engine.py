@@ -414,3 +414,82 @@ def test_row_sparse_picks_dense_when_union_covers_half_the_table():
     dense = _run(_ncf_var_worker, False, 100)
     for rk in (0, 1):
         assert np.allclose(dense[rk][0], sparse[rk][0], atol=1e-6)
+
+
+# ---------------------------------------------------------------------------
+# 4 ranks through the engine's bucketed all-reduce and ZeRO-1 paths
+# ---------------------------------------------------------------------------
+def _dp4_worker(rank, world, port, q, sharded, compress):
+    ctx = _init(rank, world, port, ZOO_GRAD_COMPRESSION=compress)
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(96)
+    per = 16 // world
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9), ctx=ctx,
+                         sharded=sharded, bucket_mb=0.0003)
+    nb = len(eng.sync.buckets)
+    for step in range(5):
+        sl = slice(step * 16 + rank * per, step * 16 + rank * per + per)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    eng.sync.sync_master()
+    q.put((rank, (eng.flat.master.detach().numpy().copy(), nb, eng.sync.world)))
+    ctx.stop()
+
+
+@pytest.mark.parametrize("sharded,compress", [(False, ""), (False, "bf16"), (True, ""), (True, "bf16")])
+def test_four_ranks_bucketed_and_zero1_match_single_process(sharded, compress):
+    res = _run(_dp4_worker, sharded, compress, world=4)
+    ws = [torch.from_numpy(res[r][0]) for r in range(4)]
+    assert all(res[r][1] > 1 and res[r][2] == 4 for r in range(4)), "expected several buckets over 4 ranks"
+    for w in ws[1:]:
+        assert torch.allclose(ws[0], w, atol=1e-6), "ranks diverged"
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.engine import TrainingEngine
+    x, y = _toy(96)
+    eng = TrainingEngine(_mlp(seed=0), MeanSquaredError(), SGD(learningrate=0.1, momentum=0.9))
+    for step in range(5):
+        sl = slice(step * 16, step * 16 + 16)
+        eng.train_step(torch.from_numpy(x[sl]), torch.from_numpy(y[sl]))
+    tol = 2e-2 * eng.flat.master.abs().max() if compress else 1e-5
+    assert (ws[0] - eng.flat.master).abs().max() < tol
+
+
+# ---------------------------------------------------------------------------
+# NNEstimator on per-rank DataFrame partitions (bench.py --input featureset)
+# ---------------------------------------------------------------------------
+def _local_part_worker(rank, world, port, q, n_local):
+    ctx = _init(rank, world, port)
+    import pandas as pd
+    from zoo.common import triggers as T
+    from zoo.pipeline.api.keras.objectives import MeanSquaredError
+    from zoo.pipeline.api.keras.optimizers import SGD
+    from zoo.pipeline.nnframes.nn_classifier import NNEstimator
+    x, y = _toy(64)
+    xs, ys = x[rank::world][:n_local[rank]], y[rank::world][:n_local[rank]]
+    df = pd.DataFrame({"features": list(xs), "label": list(ys)})
+    est = NNEstimator(_mlp(seed=0), MeanSquaredError(), [6], [1]).setBatchSize(8).setLocalPartition(True)
+    est.setOptimMethod(SGD(learningrate=0.1)).setEndWhen(T.MaxEpoch(3))
+    try:
+        est.fit(df)
+    except ValueError as e:
+        q.put((rank, ("error", str(e))))
+        ctx.stop()
+        return
+    eng = est.engine
+    q.put((rank, ("ok", eng.flat.master.detach().numpy().copy(), eng.state["neval"] - 1)))
+    ctx.stop()
+
+
+def test_nnestimator_local_partitions_train_in_lockstep():
+    res = _run(_local_part_worker, (32, 32))
+    (s0, m0, it0), (s1, m1, it1) = res[0], res[1]
+    assert s0 == s1 == "ok"
+    assert it0 == it1 == 3 * 32 // 4      # per-rank batch = 8 / 2 ranks, 3 epochs of 32 local rows
+    np.testing.assert_allclose(m0, m1, rtol=0, atol=1e-6)
+
+
+def test_nnestimator_local_partitions_must_be_equal():
+    res = _run(_local_part_worker, (32, 24))
+    assert res[0][0] == res[1][0] == "error" and "equal partitions" in res[0][1]
