@@ -65,12 +65,24 @@ def main():
             g.replay()
         replay_ms = (time.perf_counter() - h0) / 5 * 1e3
         torch.cuda.synchronize()
-    # host_ms_per_step: time the Python / launch side spends issuing a step (no device sync inside
-    # the loop): close to ms_per_step means the step is host-bound, well below means device-bound
+    # issue_ms_per_step: the host time of one step issued onto an IDLE device (synchronised
+    # before each probe step), i.e. pure issue cost with no blocking on a full queue or a ring slot.
+    # ms_per_step well above it means the step is device-bound; close to it means host-bound.
+    issue = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        h0 = time.perf_counter()
+        eng.train_step(xs, y)
+        issue.append(time.perf_counter() - h0)
+    torch.cuda.synchronize()
+    issue_ms = sorted(issue)[len(issue) // 2] * 1e3
+    # host_ms_per_step: time the Python / launch side spends in train_step inside the pipelined loop
+    # (issue time PLUS any time blocked on the device); kept for comparison with earlier logs
     print('{"bench": "bert-base-finetune-train", "batch": %d, "seq": %d, "ms_per_step": %.3f, "seq_per_s": %.1f, '
-          '"tokens_per_s": %.0f, "loss": %.4f, "host_ms_per_step": %.3f, "hip_graph": %s, "graphs": %d, "graph_replay_host_ms": %s}'
+          '"tokens_per_s": %.0f, "loss": %.4f, "host_ms_per_step": %.3f, "hip_graph": %s, "graphs": %d, "graph_replay_host_ms": %s, '
+          '"issue_ms_per_step": %.3f}'
           % (B, L, dt * 1e3, B / dt, B * L / dt, float(loss), host / a.iters * 1e3, "true" if eng.hip_graph else "false",
-             len(eng._graphs), "null" if replay_ms is None else "%.3f" % replay_ms))
+             len(eng._graphs), "null" if replay_ms is None else "%.3f" % replay_ms, issue_ms))
 
 
 if __name__ == "__main__":
