@@ -339,6 +339,179 @@ __global__ __launch_bounds__(256) void wgrad_fold_kernel(const float* __restrict
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Band weight gradient: the 64-output-channel stride-1 convs of ResNet stage 1 (3x3 64->64, the
+// 1x1 64->64 / 256->64) and the space-to-depth stem (4x4, 16 -> 64 channels).
+//
+// wgrad_kernel above tiles dW into 64 x 128 column blocks and gathers the im2col operand per
+// tile, so a 3x3 conv's activation lines are fetched 9x (once per tap) and its dY tile once per
+// column block; at these shapes (M = 0.8 - 3.2 M pixels, dW only 64 x 256..576) that made the
+// stage-1 3x3 weight gradients 234-511 us and the stem's 408 us -- the last kernel of the step
+// (profiles/r5/resnet50_b256_critical_path_final_r5.md rows 330-360).
+// Here a workgroup owns ALL of dW (64 x R*S*C fp32 in the accumulators of its 8 waves) and walks
+// bands of TP output rows of one image: the band's dY rows [TP*Q][64] and the input halo
+// [(TP+R-1) x (Q+S-1)][C] are staged into LDS once (each activation line is read ~(TP+R-1)/TP
+// times, each dY line once), and every tap's B fragments are transposed reads
+// (ds_read_b64_tr_b16) of the shifted halo rows -- a lane addresses its own row, so the tap shift
+// is only an address offset. The next band's global loads are issued into registers before this
+// band's MFMAs (register double buffer; LDS single-buffered). Each workgroup writes its dW
+// partial once; wgrad_fold*_kernel sum the partials in a fixed order (deterministic).
+// Waves: 2 halves of the 64 output channels x 4 groups of the 16-column blocks of dW.
+template <int C>
+ZOO_DEV int wb_xoff(int row, int col) {   // element offset of (halo row, channel) in LDS
+  if constexpr (C == 16) {
+    // 32-byte rows; 128 bytes of padding per 8 rows put rows h and h+8 of a transposed read
+    // half-wave on different bank halves
+    return row * 16 + (row >> 3) * 64 + col;
+  } else if constexpr (C == 64) {
+    return row * 64 + ((((col >> 4) ^ wg_f64(row)) & 3) << 4) + (col & 15);
+  } else {
+    return row * C + ((((col >> 4) ^ wg_f(row)) & (C / 16 - 1)) << 4) + (col & 15);
+  }
+}
+template <int C>
+constexpr int wb_xelems(int rows) {
+  return C == 16 ? rows * 16 + ((rows + 7) >> 3) * 64 : rows * C;
+}
+
+template <int R, int S, int C, int TP, int Q>
+struct WbCfg {
+  static constexpr int NT = 512;
+  static constexpr int HC = Q + S - 1, HR = TP + R - 1, HROWS = HR * HC;
+  static constexpr int NPX = (TP * Q + 31) / 32 * 32;       // band pixels, padded to 32-pixel K-steps
+  static constexpr int DY_PIECES = NPX * 8;                 // 16-byte pieces of the dY band
+  static constexpr int X_PIECES = HROWS * (C / 8);
+  static constexpr int PPT = (DY_PIECES + X_PIECES + NT - 1) / NT;
+  static constexpr int NCB = R * S * C / 16, NCBW = NCB / 4;
+  static constexpr int DY_ELEMS = NPX * 64, X_ELEMS = wb_xelems<C>(HROWS);
+  static constexpr size_t SMEM = (size_t)(DY_ELEMS + X_ELEMS) * 2;
+  static_assert(NCB % 4 == 0, "dW columns must split into 4 groups of 16-column blocks");
+  static_assert(C == 16 || C % 64 == 0, "C = 16 or a multiple of 64");
+  static_assert(SMEM <= 160 * 1024, "band does not fit in LDS");
+};
+
+template <int R, int S, int C, int TP, int Q>
+__global__ __launch_bounds__(512, 1) void wgrad_band_kernel(const bf16_t* __restrict__ X,
+                                                             const bf16_t* __restrict__ dY,
+                                                             float* __restrict__ part, WgradGeom g) {
+  using Cfg = WbCfg<R, S, C, TP, Q>;
+  constexpr int NT = Cfg::NT, HC = Cfg::HC, HROWS = Cfg::HROWS, NPX = Cfg::NPX, PPT = Cfg::PPT;
+  constexpr int DYP = Cfg::DY_PIECES, TOTAL = Cfg::DY_PIECES + Cfg::X_PIECES, NCBW = Cfg::NCBW;
+  constexpr int KTOT = R * S * C;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  bf16_t* dyl = reinterpret_cast<bf16_t*>(smem);
+  bf16_t* xl = dyl + Cfg::DY_ELEMS;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bands_per_img = (g.P + TP - 1) / TP;
+  const int nbands = g.N * bands_per_img;
+
+  uint4 st[PPT];
+  // piece -> (global source or zero) for band b
+  auto gload = [&](int b) {
+    const int n = b / bands_per_img, p0 = (b - n * bands_per_img) * TP;
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int pid = tid + i * NT;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (pid < DYP) {
+        const int row = pid >> 3, j = pid & 7;
+        const int pr = row / Q, pc = row - pr * Q;
+        if (row < TP * Q && p0 + pr < g.P)
+          v = *reinterpret_cast<const uint4*>(dY + ((size_t)(n * g.P + p0 + pr) * Q + pc) * 64 + 8 * j);
+      } else if (pid < TOTAL) {
+        const int q = pid - DYP;
+        const int row = q / (C / 8), j = q - row * (C / 8);
+        const int hr = row / HC, hc = row - hr * HC;
+        const int ih = p0 - g.ph + hr, iw = hc - g.pw;
+        if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+          v = *reinterpret_cast<const uint4*>(X + ((size_t)(n * g.H + ih) * g.W + iw) * C + 8 * j);
+      }
+      st[i] = v;
+    }
+  };
+  auto lstore = [&]() {
+#pragma unroll
+    for (int i = 0; i < PPT; ++i) {
+      const int pid = tid + i * NT;
+      if (pid < DYP) {
+        const int row = pid >> 3, j = pid & 7;
+        *reinterpret_cast<uint4*>(dyl + wg_off64(row, 8 * j)) = st[i];
+      } else if (pid < TOTAL) {
+        const int q = pid - DYP;
+        const int row = q / (C / 8), j = q - row * (C / 8);
+        *reinterpret_cast<uint4*>(xl + wb_xoff<C>(row, 8 * j)) = st[i];
+      }
+    }
+  };
+
+  f32x4 acc[2][NCBW];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < NCBW; ++c) acc[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int kb0 = 2 * (w & 1), cb0 = (w >> 1) * NCBW;
+  const int gq = lane >> 4, li = lane & 15, tq = li >> 2, tp = li & 3;
+  typedef __attribute__((address_space(3))) i16x4 lds_i16x4;
+  typedef short i16x8 __attribute__((ext_vector_type(8)));
+  auto tr = [&](const bf16_t* base, int o0, int o1) -> bf16x8 {
+    const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + o0));
+    const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_i16x4*)(base + o1));
+    i16x8 v;
+    v[0] = lo[0]; v[1] = lo[1]; v[2] = lo[2]; v[3] = lo[3];
+    v[4] = hi[0]; v[5] = hi[1]; v[6] = hi[2]; v[7] = hi[3];
+    return __builtin_bit_cast(bf16x8, v);
+  };
+  auto compute = [&]() {
+#pragma unroll 1
+    for (int ks = 0; ks < NPX / 32; ++ks) {
+      // this lane's two pixel rows of the K-step (transposed-read rows q and q + 4 of group gq)
+      const int i0 = ks * 32 + gq * 8 + tq, i1 = i0 + 4;
+      int pr0 = i0 / Q, pr1 = i1 / Q;
+      int h0 = pr0 * HC + (i0 - pr0 * Q), h1 = pr1 * HC + (i1 - pr1 * Q);
+      // padding pixels of the last K-step: their dY rows are zero, any halo row will do
+      h0 = i0 < TP * Q ? h0 : 0;
+      h1 = i1 < TP * Q ? h1 : 0;
+      bf16x8 af[2];
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int col = (kb0 + a) * 16 + 4 * tp;
+        af[a] = tr(dyl, wg_off64(i0, col), wg_off64(i1, col));
+      }
+#pragma unroll
+      for (int c = 0; c < NCBW; ++c) {
+        const int colg = (cb0 + c) * 16;                 // dW column block: tap (r, s), channels cc..cc+15
+        const int tap = colg / C, cc = colg - tap * C;
+        const int r = tap / S, s = tap - r * S;
+        const int sh = r * HC + s;
+        const bf16x8 bfr = tr(xl, wb_xoff<C>(h0 + sh, cc + 4 * tp), wb_xoff<C>(h1 + sh, cc + 4 * tp));
+        acc[0][c] = mfma16(af[0], bfr, acc[0][c]);
+        acc[1][c] = mfma16(af[1], bfr, acc[1][c]);
+      }
+    }
+  };
+
+  int band = blockIdx.x;
+  if (band < nbands) gload(band);
+  for (; band < nbands; band += gridDim.x) {
+    __syncthreads();              // the previous band's fragment reads are done
+    lstore();
+    __syncthreads();
+    if (band + (int)gridDim.x < nbands) gload(band + gridDim.x);   // in flight during the MFMAs
+    compute();
+  }
+  // this workgroup's partial: row = output channel kb*16 + 4*(lane>>4) + e, col = block*16 + (lane&15)
+  float* dst = part + (size_t)blockIdx.x * 64 * KTOT;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int c = 0; c < NCBW; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        dst[(size_t)((kb0 + a) * 16 + gq * 4 + e) * KTOT + (cb0 + c) * 16 + li] = acc[a][c][e];
+}
+
 }  // namespace zoo
 
 using namespace zoo;
@@ -427,4 +600,72 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
     hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, src, dW, g.K, g.Ktot, g.ldw, n);
   }
   return hipGetLastError();
+}
+
+// band weight gradient (wgrad_band_kernel): stride-1, K = 64 output channels, one of the shapes
+// instantiated below. Returns the number of partial rows it needs (0 = not handled); with
+// part != null it also runs the kernel and the ordered fold into dW.
+template <int R, int S, int C, int TP, int Q>
+static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, float* part, hipStream_t st) {
+  using Cfg = WbCfg<R, S, C, TP, Q>;
+  auto kfn = &wgrad_band_kernel<R, S, C, TP, Q>;
+  static bool attr = false;
+  if (!attr) {
+    hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                        (int)Cfg::SMEM);
+    attr = true;
+  }
+  static int ncu = 0;
+  if (ncu == 0) {
+    int dev = 0;
+    hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
+  }
+  const int nbands = g.N * ((g.P + TP - 1) / TP);
+  static const int target = [] {
+    const char* e = getenv("ZOO_WGRAD_BAND_WG");
+    return e ? atoi(e) : 0;
+  }();
+  int G = target > 0 ? target : ncu;
+  if (G > nbands) G = nbands;
+  if (!part) return G + (G > kFoldGroup ? (G + kFoldGroup - 1) / kFoldGroup : 0);
+  hipLaunchKernelGGL(kfn, dim3(G), dim3(Cfg::NT), Cfg::SMEM, st, (const bf16_t*)X, (const bf16_t*)dY, part, g);
+  const int Ktot = R * S * C;
+  const size_t n4 = (size_t)64 * (Ktot / 4);
+  const int blocks = (int)((n4 + 255) / 256 < 4096 ? (n4 + 255) / 256 : 4096);
+  const float* src = part;
+  int n = G;
+  if (G > kFoldGroup) {
+    const int groups = (G + kFoldGroup - 1) / kFoldGroup;
+    float* lvl1 = part + (size_t)G * 64 * Ktot;
+    hipLaunchKernelGGL(wgrad_fold1_kernel, dim3((unsigned)((n4 + 255) / 256), groups), dim3(256), 0, st, part, lvl1,
+                       n4, G);
+    src = lvl1;
+    n = groups;
+  }
+  hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, src, dW, 64, Ktot, g.ldw, n);
+  return G;
+}
+
+// 0: not a band shape; else the number of [64][Ktot] fp32 partial rows the call needs (part ==
+// null), or runs it (part != null)
+extern "C" int zoo_wgrad_band(const WgradGeom* gp, const void* X, const void* dY, float* dW, float* part,
+                              hipStream_t st) {
+  static const bool on = [] {
+    const char* e = getenv("ZOO_WGRAD_BAND");
+    return e ? atoi(e) != 0 : true;
+  }();
+  const WgradGeom& g = *gp;
+  if (!on || g.K != 64 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1 || g.P != g.H + 2 * g.ph - g.R + 1 ||
+      g.Q != g.W + 2 * g.pw - g.S + 1)
+    return 0;
+  if (g.R == 4 && g.S == 4 && g.C == 16 && g.ph == 0 && g.pw == 0 && g.Q == 112)
+    return wb_run<4, 4, 16, 4, 112>(g, X, dY, dW, part, st);
+  if (g.R == 3 && g.S == 3 && g.C == 64 && g.ph == 1 && g.pw == 1 && g.Q == 56)
+    return wb_run<3, 3, 64, 4, 56>(g, X, dY, dW, part, st);
+  if (g.R == 1 && g.S == 1 && g.C == 64 && g.ph == 0 && g.pw == 0 && g.Q == 56)
+    return wb_run<1, 1, 64, 4, 56>(g, X, dY, dW, part, st);
+  if (g.R == 1 && g.S == 1 && g.C == 256 && g.ph == 0 && g.pw == 0 && g.Q == 56)
+    return wb_run<1, 1, 256, 4, 56>(g, X, dY, dW, part, st);
+  return 0;
 }

@@ -62,6 +62,7 @@ hipError_t zoo_flip_weights(const void*, void*, int, int, int, int, int, int, in
 hipError_t zoo_flip_weights_batched(const void*, int, int, hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
 int zoo_wgrad_plan(WgradGeom*);
+int zoo_wgrad_band(const WgradGeom*, const void*, const void*, float*, float*, hipStream_t);
 hipError_t zoo_bmm(const void*, const void*, void*, const long*, int, int, hipStream_t);
 hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t);
 hipError_t zoo_ssd_match(const float*, const int*, const float*, int, int, int, float, float, float, int, int*,
@@ -882,6 +883,20 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
                                 g.N, g.H, g.W, g.C, g.K, R, S, g.P, g.Q, sh, sw, ph, pw, dh, dil_w, g.ldw, cur_stream()),
               "wgrad256_conv");
     return;
+  }
+  // the 64-output-channel stride-1 shapes of ResNet stage 1 and the space-to-depth stem: one
+  // workgroup per CU owns all of dW and walks bands of output rows staged once in LDS
+  // (wgrad.hip wgrad_band_kernel); deterministic ordered fold of the per-workgroup partials
+  if (x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
+    const int rows = zoo_wgrad_band(&g, nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (rows > 0) {
+      check_al16(x.data_ptr(), "conv_wgrad x");
+      check_al16(dy.data_ptr(), "conv_wgrad dy");
+      auto part = torch::empty({(int64_t)rows, (int64_t)g.K * g.Ktot}, dw.options());
+      zoo_wgrad_band(&g, x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), part.data_ptr<float>(), cur_stream());
+      check_hip(hipGetLastError(), "wgrad_band");
+      return;
+    }
   }
   g.m_per_split = 0;
   // split-K reduction: fp32 atomics into dW, or per-split partials + an ordered fold. Atomics

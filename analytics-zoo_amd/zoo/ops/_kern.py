@@ -118,6 +118,26 @@ class _FlipCache:
         self.table = None     # device int32 [n, desc_ints]
         self.table_n = 0
         self.nblocks = 0
+        self.pending = None   # event of a prefetched re-flip on the side stream (prefetch)
+
+    def prefetch(self, side):
+        """Re-flip every cached filter now, on ``side``, if the weights changed since the last
+        flip: issued at the start of a training step, the batched flip overlaps the forward
+        instead of sitting on the data-gradient chain in front of the first dgrad."""
+        ep = _EPOCH[0]
+        if not self.entries or all(e[2] == ep for e in self.entries.values()):
+            return
+        if self.table is None or self.table_n != len(self.entries):
+            self._build_table()
+        dev = self.table.device
+        side.wait_stream(torch.cuda.current_stream(dev))   # the last update of the weights
+        with torch.cuda.stream(side):
+            native().flip_weights_batched(self.table, self.table_n, self.nblocks)
+            ev = torch.cuda.Event()
+            ev.record(side)
+        for e in self.entries.values():
+            e[2] = ep
+        self.pending = ev
 
     def _build_table(self):
         import numpy as np
@@ -142,6 +162,9 @@ class _FlipCache:
         self.nblocks = blk
 
     def get(self, w, K, R, S, C, r0, s0, Ra, Sb, sh, sw):
+        if self.pending is not None:   # a prefetched flip writes the cached filters: order after it
+            torch.cuda.current_stream(w.device).wait_event(self.pending)
+            self.pending = None
         key = (w.data_ptr(), K, R, S, C, r0, s0, Ra, Sb, sh, sw)
         ep = _EPOCH[0]
         ent = self.entries.get(key)
@@ -157,6 +180,25 @@ class _FlipCache:
         self.entries[key] = [w, wt, ep]
         self.table = None
         return wt
+
+
+_PREFETCH = __import__("os").environ.get("ZOO_FLIP_PREFETCH", "1") != "0"
+
+
+def prefetch_flips(device):
+    """Start of a training step: re-flip the cached dgrad filters of every FlatParams on the
+    weight-gradient side stream (see _FlipCache.prefetch). No-op under capture."""
+    if not (_CACHE_ON and _PREFETCH and _FLATS) or device.type != "cuda" or torch.cuda.is_current_stream_capturing():
+        return
+    from zoo.ops import wstream
+    if not wstream.on():
+        return
+    side = wstream.side_for(device)
+    for ref in list(_FLATS.values()):
+        f = ref()
+        cache = getattr(f, "_flip_cache", None) if f is not None else None
+        if cache is not None and cache.entries and f.bf16.device == device:
+            cache.prefetch(side)
 
 
 def flip_weights(w, K, R, S, C, r0=0, s0=0, Ra=None, Sb=None, sh=1, sw=1):

@@ -49,13 +49,16 @@ _HALF_RESID = __import__("os").environ.get("ZOO_HALF_RESID", "1") != "0"
 # forward consumer-side BN apply for units of these widths (pw.hip prologue: K <= 128)
 _FWD_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_FWD_PRO_K", "64,128").split(",") if v)
 _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
+# wider units take the prologue only when their dgrad writes at most this many channels: one
+# channel group in pw.hip, so the prologue (and its y / g reads) runs once, not Cin / 64 times
+_PRO_NMAX = int(__import__("os").environ.get("ZOO_BN_FOLD_NMAX", "64"))
 
 
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
     # K = 64 / 128: the widths whose prologue tile stays spill-free in registers (pw.hip PRO); wider
     # units and the deterministic mode (partial statistics: no pw) keep bn_bwd_apply
     return (_BN_FOLD[0] and R == 1 and S == 1 and tuple(stride) == (1, 1) and tuple(pad) == (0, 0)
-            and not getattr(ctx, "sync", False) and K in _PRO_K and Cin % 64 == 0
+            and not getattr(ctx, "sync", False) and K in _PRO_K and Cin % 64 == 0 and (K <= 64 or Cin <= _PRO_NMAX)
             and gamma.dtype == torch.float32 and gamma.is_contiguous() and not _deterministic())
 
 

@@ -33,7 +33,7 @@ import torch
 from zoo.common.triggers import EveryEpoch, MaxEpoch, Trigger
 from zoo.parallel.ddp import GradSync
 from zoo.parallel.flat import FlatParams
-from zoo.ops import workspace, wstream
+from zoo.ops import _kern, workspace, wstream
 from zoo.ops.devscalar import seed_offset_used
 
 log = logging.getLogger("zoo.engine")
@@ -320,6 +320,7 @@ class TrainingEngine:
         workspace.begin_step(self.device)
         self.sync.in_step = True
         try:
+            _kern.prefetch_flips(self.device)   # the dgrad filters of the updated weights, beside the forward
             out = self.forward_fn(self.model, inputs)
             loss = self.criterion(out, target)
             # weight gradients overlap the data-gradient chain on a side stream, joined back

@@ -1,0 +1,21 @@
+#!/bin/bash
+# r6 A/B 1: band weight gradient (ZOO_WGRAD_BAND), flip prefetch (ZOO_FLIP_PREFETCH), BN-backward
+# prologue on the 256-wide stage-1 units (ZOO_BN_FOLD_K=64,256); numerics first
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/r6
+export TMPDIR=/tmp
+T="timeout -k 10"
+$T 600 python -u -m pytest tests/test_gpu_kernels.py -k "wgrad" tests/test_gpu_resnet50_parity.py tests/test_gpu_bnfold.py \
+  -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r6/ab1_tests.log 2>&1
+rc=$?; tail -3 gpurun_out/r6/ab1_tests.log; [ $rc -eq 0 ] || exit $rc
+run() {  # tag, env...
+  local tag=$1; shift
+  env "$@" $T 300 python -u bench.py --input device > gpurun_out/r6/ab1_$tag.log 2>&1 || exit 21
+  python3 -c "import json,sys; d=json.loads(open('gpurun_out/r6/ab1_$tag.log').read().strip().splitlines()[-1]); print('$tag', d['value'], d['ms_per_step'], d['first_loss'], d['final_loss'])"
+}
+for i in 1 2; do
+  run base$i ZOO_WGRAD_BAND=0 ZOO_FLIP_PREFETCH=0
+  run band$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=0
+  run bandflip$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=1
+  run bandflipfold$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=1 ZOO_BN_FOLD_K=64,256
+done
