@@ -104,6 +104,18 @@ struct GemmGeom {
   int lda, ldb, ldy;   // leading dims (elements), all % 8 == 0
 };
 
+// Grouped convolution (gconv.hip): one launch per direction, group = grid y.
+struct GConvArgs {
+  int N, H, W, C;        // input NHWC; C = groups * Cg is also the pixel stride of X / dX
+  int K;                 // output channels = groups * Kg, the pixel stride of Y / dY
+  int groups, Cg, Kg;
+  int R, S, P, Q;
+  int sh, sw, ph, pw, dh, dw;
+  int ldb;               // packed weight row stride (>= R*S*Cg, % 8 == 0), K rows
+  int act;               // forward activation (Act)
+  int mper;              // wgrad: output pixels per split (multiple of 32)
+};
+
 // Weight-gradient geometry (wgrad.hip).
 struct WgradGeom {
   int N, H, W, C;      // input activation (NHWC)

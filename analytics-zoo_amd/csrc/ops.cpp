@@ -14,6 +14,7 @@
 
 using zoo::ConvGeom;
 using zoo::WgradGeom;
+using zoo::GConvArgs;
 using zoo::BwdStats;
 using zoo::GemmGeom;
 
@@ -63,6 +64,7 @@ hipError_t zoo_flip_weights_batched(const void*, int, int, hipStream_t);
 hipError_t zoo_wgrad(const void*, const void*, float*, float*, const WgradGeom*, hipStream_t);
 int zoo_wgrad_plan(WgradGeom*);
 int zoo_wgrad_band(const WgradGeom*, const void*, const void*, float*, float*, hipStream_t);
+hipError_t zoo_gconv(int, const void*, const void*, const void*, void*, const float*, const GConvArgs*, hipStream_t);
 hipError_t zoo_bmm(const void*, const void*, void*, const long*, int, int, hipStream_t);
 hipError_t zoo_row_reduce(const void*, float*, long, int, int, int, hipStream_t);
 hipError_t zoo_ssd_match(const float*, const int*, const float*, int, int, int, float, float, float, int, int*,
@@ -1221,6 +1223,75 @@ torch::Tensor avgpool_bwd(torch::Tensor dy, int H, int W, int R, int S, int sh, 
                             cur_stream()),
             "avgpool_bwd");
   return dx;
+}
+
+// grouped conv (gconv.hip): x [N,H,W,C] bf16 NHWC, w [K, ldb] bf16 packed per output channel over
+// its group's (r, s, c) with C / groups channels, group g = output rows [g K/g, (g+1) K/g)
+static GConvArgs gconv_args(int N, int H, int W, int C, int K, int groups, int R, int S, int sh, int sw, int ph,
+                            int pw, int dh, int dw, int ldb, int act) {
+  TORCH_CHECK(groups >= 1 && C % groups == 0 && K % groups == 0, "grouped conv: channels must split into groups");
+  TORCH_CHECK(R >= 1 && S >= 1 && sh >= 1 && sw >= 1 && ph >= 0 && pw >= 0 && dh >= 1 && dw >= 1,
+              "grouped conv: bad geometry");
+  GConvArgs a{};
+  a.N = N; a.H = H; a.W = W; a.C = C; a.K = K; a.groups = groups; a.Cg = C / groups; a.Kg = K / groups;
+  a.R = R; a.S = S; a.sh = sh; a.sw = sw; a.ph = ph; a.pw = pw; a.dh = dh; a.dw = dw;
+  a.P = (H + 2 * ph - dh * (R - 1) - 1) / sh + 1;
+  a.Q = (W + 2 * pw - dw * (S - 1) - 1) / sw + 1;
+  TORCH_CHECK(a.P > 0 && a.Q > 0, "grouped conv: empty output");
+  TORCH_CHECK(ldb >= R * S * a.Cg && ldb % 8 == 0, "grouped conv: weight rows must be >= R*S*C/groups, %8 == 0");
+  a.ldb = ldb; a.act = act;
+  return a;
+}
+
+torch::Tensor gconv_fwd(torch::Tensor x, torch::Tensor w, c10::optional<torch::Tensor> bias, int groups, int R,
+                        int S, int sh, int sw, int ph, int pw, int dh, int dil_w, int act) {
+  req(x, at::kBFloat16, "x");
+  req(w, at::kBFloat16, "w");
+  TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "gconv_fwd: x NHWC, w [K, ldb]");
+  const int K = w.size(0);
+  auto a = gconv_args(x.size(0), x.size(1), x.size(2), x.size(3), K, groups, R, S, sh, sw, ph, pw, dh, dil_w,
+                      w.size(1), act);
+  const float* bp = nullptr;
+  if (bias.has_value() && bias->defined()) {
+    req(*bias, at::kFloat, "bias");
+    TORCH_CHECK(bias->numel() == K, "gconv_fwd: bias size");
+    bp = bias->data_ptr<float>();
+  }
+  if (a.Cg % 8 == 0) check_al16(x.data_ptr(), "gconv_fwd x");
+  check_al16(w.data_ptr(), "gconv_fwd w");
+  auto y = torch::empty({x.size(0), a.P, a.Q, K}, x.options());
+  check_hip(zoo_gconv(0, x.data_ptr(), w.data_ptr(), nullptr, y.data_ptr(), bp, &a, cur_stream()), "gconv_fwd");
+  return y;
+}
+
+torch::Tensor gconv_dgrad(torch::Tensor dy, torch::Tensor w, int groups, int H, int W, int C, int R, int S, int sh,
+                          int sw, int ph, int pw, int dh, int dil_w) {
+  req(dy, at::kBFloat16, "dy");
+  req(w, at::kBFloat16, "w");
+  const int K = w.size(0);
+  auto a = gconv_args(dy.size(0), H, W, C, K, groups, R, S, sh, sw, ph, pw, dh, dil_w, w.size(1), 0);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(1) == a.P && dy.size(2) == a.Q && dy.size(3) == K, "gconv_dgrad: dy shape");
+  if (a.Kg % 8 == 0) check_al16(dy.data_ptr(), "gconv_dgrad dy");
+  auto dx = torch::empty({dy.size(0), H, W, C}, dy.options());
+  check_hip(zoo_gconv(1, nullptr, w.data_ptr(), dy.data_ptr(), dx.data_ptr(), nullptr, &a, cur_stream()),
+            "gconv_dgrad");
+  return dx;
+}
+
+// dw (fp32 [K, ldb]) += grouped weight gradient
+void gconv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int groups, int R, int S, int sh, int sw,
+                 int ph, int pw, int dh, int dil_w) {
+  req(x, at::kBFloat16, "x");
+  req(dy, at::kBFloat16, "dy");
+  req(dw, at::kFloat, "dw");
+  TORCH_CHECK(dw.dim() == 2, "gconv_wgrad: dw [K, ldb]");
+  const int K = dw.size(0);
+  auto a = gconv_args(x.size(0), x.size(1), x.size(2), x.size(3), K, groups, R, S, sh, sw, ph, pw, dh, dil_w,
+                      dw.size(1), 0);
+  TORCH_CHECK(dy.dim() == 4 && dy.size(0) == x.size(0) && dy.size(1) == a.P && dy.size(2) == a.Q && dy.size(3) == K,
+              "gconv_wgrad: dy shape");
+  check_hip(zoo_gconv(2, x.data_ptr(), nullptr, dy.data_ptr(), dw.data_ptr(), nullptr, &a, cur_stream()),
+            "gconv_wgrad");
 }
 
 // depthwise conv: x [N,H,W,C] bf16, w [R*S, C] bf16 (tap-major)
@@ -3204,6 +3275,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("pool_shape", &pool_shape);
+  m.def("gconv_fwd", &gconv_fwd);
+  m.def("gconv_dgrad", &gconv_dgrad);
+  m.def("gconv_wgrad", &gconv_wgrad);
   m.def("dwconv_fwd", &dwconv_fwd);
   m.def("dwconv_dgrad", &dwconv_dgrad);
   m.def("dwconv_wgrad", &dwconv_wgrad);

@@ -224,6 +224,72 @@ def conv2d_nhwc(x, w, bias=None, kernel=(1, 1), stride=(1, 1), pad=(0, 0), dil=(
     return y if out_f32 or x.dtype == torch.float32 else y.to(x.dtype)
 
 
+class _GroupedConv2dFn(torch.autograd.Function):
+    """y = act(grouped_conv(x, w) + b): every direction is ONE native launch with the group index
+    in the grid (csrc/kernels/gconv.hip), no per-group slices / pads / concatenation."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, groups, R, S, stride, pad, dil, act):
+        wb = bf16_weight(w)
+        y = native().gconv_fwd(x, wb, None if bias is None else bias.detach().float().contiguous(), groups, R, S,
+                               stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ACT_CODES[act])
+        ctx.save_for_backward(x, w, y if act not in (None, "linear") else None)
+        ctx.geom = (groups, R, S, stride, pad, dil, act, bias is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, y = ctx.saved_tensors
+        groups, R, S, stride, pad, dil, act, has_bias = ctx.geom
+        dy = dy.float()
+        if act == "relu":
+            dy = dy * (y > 0).float()
+        elif act == "sigmoid":
+            yf = y.float()
+            dy = dy * yf * (1 - yf)
+        elif act == "tanh":
+            yf = y.float()
+            dy = dy * (1 - yf * yf)
+        elif act not in (None, "linear"):
+            raise NotImplementedError("backward through fused %s epilogue" % act)
+        dyb = dy.to(torch.bfloat16).contiguous()
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = native().gconv_dgrad(dyb, bf16_weight(w), groups, x.shape[1], x.shape[2], x.shape[3], R, S,
+                                      stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
+        if ctx.needs_input_grad[1]:
+            gbuf = grad_slot(w)
+            target = gbuf if gbuf is not None else torch.zeros(w.shape, dtype=torch.float32, device=w.device)
+            native().gconv_wgrad(x, dyb, target, groups, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1])
+            if gbuf is None:
+                dw = target.to(w.dtype)
+            else:
+                hook = getattr(w, "_zoo_grad_ready", None)
+                if hook is not None:
+                    hook(w)
+        if has_bias and ctx.needs_input_grad[2]:
+            db = dy.reshape(-1, dy.shape[-1]).sum(0)
+        return dx, dw, db, None, None, None, None, None, None, None
+
+
+def grouped_conv2d_nhwc(x, w, bias=None, groups=1, kernel=(1, 1), stride=(1, 1), pad=(0, 0), dil=(1, 1), act=None):
+    """Grouped NHWC conv. x: [N, H, W, C] (C = groups * Cg, unpadded); w: packed [K, ldb] where
+    row k holds output channel k's filter over its group's (r, s, c), c < Cg (ldb >= R*S*Cg, % 8)."""
+    R, S = kernel
+    if x.is_cuda:
+        if x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        return _GroupedConv2dFn.apply(x.contiguous(), w, bias, int(groups), R, S, tuple(stride), tuple(pad),
+                                      tuple(dil), act)
+    K = w.shape[0]
+    Cg = x.shape[3] // groups
+    w4 = w[:, :R * S * Cg].float().reshape(K, R, S, Cg).permute(0, 3, 1, 2)
+    y = F.conv2d(x.float().permute(0, 3, 1, 2), w4, bias=None if bias is None else bias.float(), stride=stride,
+                 padding=pad, dilation=dil, groups=groups).permute(0, 2, 3, 1)
+    y = _ref_act(y, act)
+    return y if x.dtype == torch.float32 else y.to(x.dtype)
+
+
 # hipBLASLt for transformer-size linears is an opt-in comparator since round 3 (ZOO_LINEAR_BLAS=1);
 # by default they run on the hand-written MFMA GEMMs (_LinearNativeFn)
 _BLAS_LINEAR = os.environ.get("ZOO_LINEAR_BLAS", "0") == "1"

@@ -110,8 +110,8 @@ class ZConv2d(_Twin, nn.Conv2d):
     """nn.Conv2d (zero padding) [+ folded eval BatchNorm2d] [+ fused activation] on the native
     kernels: dense convs on the implicit-GEMM kernels (igemm / igemm2 / pw); depthwise convs
     (groups = in_channels, any channel multiplier, <= 3x3 taps) on the depthwise kernel
-    (dwconv.hip); other grouped convs (Caffe ``group``, e.g. AlexNet's group 2) as one
-    implicit-GEMM conv per group over that group's channel slice."""
+    (dwconv.hip); other grouped convs (Caffe ``group``, e.g. AlexNet's group 2; ResNeXt) as ONE
+    grouped implicit-GEMM launch per direction with the group index in the grid (gconv.hip)."""
     _zoo_bn = None
     _zoo_act = None
     _zoo_cache = None
@@ -158,7 +158,7 @@ class ZConv2d(_Twin, nn.Conv2d):
 
     def _packed(self, training_bn):
         """Native operands for this conv's group mode, cached by parameter versions when no
-        gradient is needed: dense -> (packed weight, bias); grouped -> a list of those per group;
+        gradient is needed: dense -> (packed weight, bias); grouped -> (weight [K, ceil8(R*S*C/g)], bias);
         depthwise -> (tap-major weight [R*S, Kp], bias [Kp])."""
         bn = self._zoo_bn
         need_grad = torch.is_grad_enabled() and (self.weight.requires_grad or
@@ -181,15 +181,15 @@ class ZConv2d(_Twin, nn.Conv2d):
         if mode == "dense":
             out = self._pack(w, b)
         elif mode == "grouped":
-            g = self.groups
-            Kg = K // g
-            out = [self._pack(w[i * Kg:(i + 1) * Kg], b[i * Kg:(i + 1) * Kg]) for i in range(g)]
+            # [K, ceil8(R*S*Cg)]: each output channel's filter over its own group's channels
+            w2 = w.permute(0, 2, 3, 1).reshape(K, R * S * Cg)
+            ld = ops.ceil8(R * S * Cg)
+            out = (F.pad(w2, (0, ld - R * S * Cg)) if ld != R * S * Cg else w2, b)
         else:   # depthwise: output channel o reads input channel o // multiplier
             kp = ops.ceil8(K)
             out = (F.pad(w.reshape(K, R * S).t(), (0, kp - K)), F.pad(b, (0, kp - K)))
         if key is not None:
-            out = [(a.detach().contiguous(), c.detach().contiguous()) for a, c in out] if mode == "grouped" else \
-                (out[0].detach().contiguous(), out[1].detach().contiguous())
+            out = (out[0].detach().contiguous(), out[1].detach().contiguous())
             self._zoo_cache = (key, out)
         return out
 
@@ -210,17 +210,11 @@ class ZConv2d(_Twin, nn.Conv2d):
             w2, b = self._packed(training_bn)
             y = ops.conv2d_nhwc(to_nhwc(x, _cin_pad(C)), w2, b, dil=tuple(self.dilation), act=fused, **geo)
         elif mode == "grouped":
-            g = self.groups
-            Cg, Kg = C // g, K // g
-            xn = to_nhwc(x)
-            outs = []
-            for i, (w2, b) in enumerate(self._packed(training_bn)):
-                xg = xn[..., i * Cg:(i + 1) * Cg]
-                if _cin_pad(Cg) != Cg:
-                    xg = F.pad(xg, (0, _cin_pad(Cg) - Cg))
-                yg = ops.conv2d_nhwc(xg.contiguous(), w2, b, dil=tuple(self.dilation), act=fused, **geo)
-                outs.append(yg[..., :Kg])
-            y = torch.cat(outs, -1)
+            # one launch per direction, group index in the grid (csrc/kernels/gconv.hip)
+            from zoo.ops.conv import grouped_conv2d_nhwc
+            w2, b = self._packed(training_bn)
+            y = grouped_conv2d_nhwc(to_nhwc(x), w2, b, groups=self.groups, dil=tuple(self.dilation), act=fused,
+                                    **geo)
         else:
             from zoo.ops.nn import depthwise_conv2d_nhwc
             wdw, b = self._packed(training_bn)

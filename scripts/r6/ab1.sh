@@ -1,11 +1,12 @@
 #!/bin/bash
 # r6 A/B 1: band weight gradient (ZOO_WGRAD_BAND), flip prefetch (ZOO_FLIP_PREFETCH), BN-backward
-# prologue on the 256-wide stage-1 units (ZOO_BN_FOLD_K=64,256); numerics first
+# prologue on the 256-wide stage-1 units (ZOO_BN_FOLD_K=64,256); grouped conv tests; ResNet and
+# BERT step traces
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r6
 export TMPDIR=/tmp
 T="timeout -k 10"
-$T 600 python -u -m pytest tests/test_gpu_kernels.py -k "wgrad" tests/test_gpu_resnet50_parity.py tests/test_gpu_bnfold.py \
+$T 600 python -u -m pytest tests/test_gpu_native_import.py tests/test_gpu_kernels.py -k "wgrad or group" \
   -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r6/ab1_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r6/ab1_tests.log; [ $rc -eq 0 ] || exit $rc
 run() {  # tag, env...
@@ -18,4 +19,17 @@ for i in 1 2; do
   run band$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=0
   run bandflip$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=1
   run bandflipfold$i ZOO_WGRAD_BAND=1 ZOO_FLIP_PREFETCH=1 ZOO_BN_FOLD_K=64,256
+done
+rm -rf /tmp/prof_rn
+$T 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_rn -o rn -- python3 bench.py --input device --steps 8 --warmup 3 > gpurun_out/r6/prof_rn_ab1.log 2>&1 || exit 8
+DB=$(find /tmp/prof_rn -name "*.db" | head -1)
+python3 analytics-zoo_amd/tools/prof_step.py $DB --critical > gpurun_out/r6/prof_rn_ab1_step.md 2>&1
+tail -40 gpurun_out/r6/prof_rn_ab1_step.md
+for mode in eager graph; do
+  flag=""; [ $mode = graph ] && flag="--graph"
+  rm -rf /tmp/prof_bert_$mode
+  $T 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_bert_$mode -o bert -- python3 analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 6 $flag > gpurun_out/r6/prof_bert_$mode.log 2>&1 || exit 31
+  DB=$(find /tmp/prof_bert_$mode -name "*.db" | head -1)
+  python3 analytics-zoo_amd/tools/prof_step.py $DB softmax_xent 3 --critical > gpurun_out/r6/prof_bert_${mode}_step.md 2>&1
+  tail -30 gpurun_out/r6/prof_bert_${mode}_step.md
 done
