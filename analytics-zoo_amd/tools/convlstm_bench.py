@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""ConvLSTM2D forward+backward time: the one-launch-per-step path (_ConvLSTMFusedFn,
-convlstm.hip), the whole-sequence path (_ConvLSTMSeqFn: recurrent conv + step kernel forward,
-three launches per step backward) and the per-step autograd loop, and their agreement.
+"""ConvLSTM2D / ConvLSTM3D forward+backward time: the one-launch-per-step path (_ConvLSTMFusedFn /
+_ConvLSTM3DFusedFn, convlstm.hip), the 2-D whole-sequence path (_ConvLSTMSeqFn: recurrent conv +
+step kernel forward, three launches per step backward) and the per-step loop (one recurrent conv +
+one gate pass per step), and their agreement.
 
-  python tools/convlstm_bench.py [--T 32] [--batch 8] [--hw 32] [--cin 16] [--filters 32]"""
+  python tools/convlstm_bench.py [--dims 2|3] [--T 32] [--batch 8] [--hw 32] [--cin 16] [--filters 32]"""
 import argparse
 import json
 import os
@@ -22,18 +23,24 @@ def main():
     ap.add_argument("--cin", type=int, default=16)
     ap.add_argument("--filters", type=int, default=32)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--dims", type=int, default=2, choices=[2, 3])
     a = ap.parse_args()
     from zoo.pipeline.api.keras.layers import recurrent as R
     torch.manual_seed(0)
-    layer = R.ConvLSTM2D(a.filters, 3, 3, return_sequences=True, input_shape=(a.T, a.cin, a.hw, a.hw))
-    layer._ensure_built((None, a.T, a.cin, a.hw, a.hw))
+    sp = (a.hw,) * a.dims
+    if a.dims == 2:
+        layer = R.ConvLSTM2D(a.filters, 3, 3, return_sequences=True, input_shape=(a.T, a.cin) + sp)
+    else:
+        layer = R.ConvLSTM3D(a.filters, 3, return_sequences=True, input_shape=(a.T, a.cin) + sp)
+    layer._ensure_built((None, a.T, a.cin) + sp)
     layer = layer.cuda()
-    x = torch.randn(a.batch, a.T, a.cin, a.hw, a.hw, device="cuda", requires_grad=True)
-    res = {"bench": "convlstm2d-fwd-bwd", "T": a.T, "batch": a.batch, "hw": a.hw, "cin": a.cin,
+    x = torch.randn((a.batch, a.T, a.cin) + sp, device="cuda", requires_grad=True)
+    res = {"bench": "convlstm%dd-fwd-bwd" % a.dims, "T": a.T, "batch": a.batch, "hw": a.hw, "cin": a.cin,
            "filters": a.filters}
     outs = {}
     names = {0: "loop", 1: "seq", 2: "fused"}
-    for mode in (0, 1, 2):
+    # ConvLSTM3D has no separate whole-sequence mode: SEQ without FUSED is its per-step loop
+    for mode in ((0, 1, 2) if a.dims == 2 else (0, 2)):
         R._CONVLSTM_SEQ = mode > 0
         R._CONVLSTM_FUSED = mode == 2
 
@@ -54,9 +61,10 @@ def main():
         ms = (time.perf_counter() - t0) / a.iters * 1e3
         res["ms_%s" % names[mode]] = round(ms, 3)
         outs[mode] = (y.detach().float(), x.grad.detach().clone(), layer.Wh.grad.detach().clone())
-    res["speedup_seq"] = round(res["ms_loop"] / res["ms_seq"], 2)
+    if "ms_seq" in res:
+        res["speedup_seq"] = round(res["ms_loop"] / res["ms_seq"], 2)
     res["speedup"] = round(res["ms_loop"] / res["ms_fused"], 2)
-    for mode in (1, 2):
+    for mode in [m for m in (1, 2) if m in outs]:
         for k, n in enumerate(("y", "dx", "dWh")):
             a0, a1 = outs[0][k], outs[mode][k]
             res["rel_%s_%s" % (names[mode], n)] = round(float((a0 - a1).abs().max() /

@@ -26,10 +26,12 @@ DB=$(find /tmp/prof_rn -name "*.db" | head -1)
 python3 analytics-zoo_amd/tools/prof_step.py $DB --critical > gpurun_out/r6/prof_rn_ab1_step.md 2>&1
 tail -40 gpurun_out/r6/prof_rn_ab1_step.md
 for mode in eager graph; do
-  flag=""; [ $mode = graph ] && flag="--graph"
+  # loss kernel as the boundary: one per step; 3 warm-up + 10 timed + 5 idle-device probe steps
+  # (+ 5 bare replays with --graph): the period picked lies inside the pipelined timed loop
+  flag=""; back=8; [ $mode = graph ] && flag="--graph" && back=13
   rm -rf /tmp/prof_bert_$mode
-  $T 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_bert_$mode -o bert -- python3 analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 6 $flag > gpurun_out/r6/prof_bert_$mode.log 2>&1 || exit 31
+  $T 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_bert_$mode -o bert -- python3 analytics-zoo_amd/tools/bert_train.py --batch 128 --iters 10 $flag > gpurun_out/r6/prof_bert_$mode.log 2>&1 || exit 31
   DB=$(find /tmp/prof_bert_$mode -name "*.db" | head -1)
-  python3 analytics-zoo_amd/tools/prof_step.py $DB softmax_xent 3 --critical > gpurun_out/r6/prof_bert_${mode}_step.md 2>&1
+  python3 analytics-zoo_amd/tools/prof_step.py $DB softmax_xent $back --critical > gpurun_out/r6/prof_bert_${mode}_step.md 2>&1
   tail -30 gpurun_out/r6/prof_bert_${mode}_step.md
 done

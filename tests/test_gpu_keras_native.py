@@ -103,6 +103,14 @@ def test_keras_layer_native_fwd_bwd(gpu, name):
     assert any("zoo::" in n for n in names), names[:10]
     bad = sorted({n for n in names if any(b in n for b in BANNED)})
     assert not bad, bad[:5]
+    if name.startswith("ConvLSTM"):
+        # the whole-sequence path ran: one step kernel per timestep each way (convlstm.hip), no
+        # per-step recurrent conv + gate passes
+        T = shape[1]
+        fwd = sum("convlstm_fwd_kernel" in n for n in names)
+        bwd = sum("convlstm_bwd_kernel" in n for n in names)
+        assert T - 1 <= fwd <= T and T - 1 <= bwd <= T, (name, fwd, bwd, T)
+        assert not any("lstm_gates" in n for n in names), name
     if name.startswith("BatchNormalization"):
         # batch statistics of the bf16 activations: agree to bf16 resolution
         assert torch.allclose(g.running_mean.cpu(), cpu.running_mean, atol=2e-3)
