@@ -371,7 +371,7 @@ def test_mtnet_runs_native(gpu):
 _ALEX_GROUP_PROTO = """name: "alexgrp"
 input: "data"
 input_dim: 2
-input_dim: 3
+input_dim: 8
 input_dim: 39
 input_dim: 39
 layer { name: "conv1" type: "Convolution" bottom: "data" top: "conv1" convolution_param { num_output: 48 kernel_size: 5 stride: 2 } }
@@ -400,7 +400,7 @@ def test_caffe_alexnet_group_single_launch(gpu, tmp_path):
     for n in ("conv2", "conv3", "conv4"):
         assert nat.node(n).op._group_mode() == "grouped", n
     nat = nat.to(gpu)
-    x = torch.randn(2, 3, 39, 39)
+    x = torch.randn(2, 8, 39, 39)
     with torch.no_grad():
         out, names = _kernels_of(lambda: nat(x.to(gpu)))
         want = ref(x)
