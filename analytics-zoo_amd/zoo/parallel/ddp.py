@@ -53,8 +53,7 @@ last contribution); later steps launch early in that order, and ``finish()`` lau
 is left -- including all buckets of a zombie rank that failed part-way through backward -- in
 that same recorded order, so a zombie's collective sequence matches the healthy ranks'.
 
-Row-sparse sync (fp32 wire only -- ``compress="bf16"``, the GPU default, reduces every bucket
-densely): each rank scatters a per-row "touched" mask (uint8, V bytes; int32 at >= 256
+Row-sparse sync (fp32 wire, or the 16-bit wire of the dense buckets for the union rows): each rank scatters a per-row "touched" mask (uint8, V bytes; int32 at >= 256
 ranks), the masks are summed (one all-reduce), the union rows are compacted on the device into a
 fixed-capacity index buffer (capacity min(V, world * ids-per-step), agreed in the calibration
 step) and ONE fixed-size all-reduce moves just those rows. A rank without lookups contributes a
@@ -518,6 +517,23 @@ class GradSync:
             self._sparse_cap[key] = cap
         return cap
 
+    def _rows16_allreduce(self, rows):
+        """Sum a [cap, D] fp32 row block over the ranks on the 16-bit wire: the dense buckets'
+        protocol (bf16 pack, all-to-all, fp32 sum of this rank's chunk, all-gather of the bf16
+        sums), so the row-sparse path moves half the bytes of its fp32 form."""
+        n = rows.numel()
+        cb = (n + self.world - 1) // self.world
+        cb = (cb + CHUNK_ALIGN - 1) // CHUNK_ALIGN * CHUNK_ALIGN
+        pack = torch.zeros(cb * self.world, dtype=torch.bfloat16, device=rows.device)
+        pack[:n].copy_(rows.reshape(-1))
+        recv = torch.empty_like(pack)
+        self._a2a(recv, pack)
+        mine = torch.empty(cb, dtype=torch.bfloat16, device=rows.device)
+        self._sum_chunks(recv, out16=mine)
+        gath = torch.empty_like(pack)
+        self._gather(gath, mine)
+        return gath[:n].view_as(rows).float()
+
     def _row_sparse_allreduce(self, p, lo, hi):
         """Sum table p's gradient over the ranks through the union of looked-up rows: a summed
         uint8 touched mask, device-side compaction into a fixed-capacity row list, one fixed-size
@@ -561,7 +577,10 @@ class GradSync:
         first = rows_idx[:1].clamp(max=V - 1)
         rows_idx = torch.where(rows_idx < V, rows_idx, first)   # padding slots repeat the first row
         rows = g.index_select(0, rows_idx)
-        dist.all_reduce(rows, group=self.group)
+        if self.compress:
+            rows = self._rows16_allreduce(rows)
+        else:
+            dist.all_reduce(rows, group=self.group)
         g.index_copy_(0, rows_idx, rows)
         self.sparse_rows = getattr(self, "sparse_rows", 0) + cap
         return True
@@ -571,11 +590,12 @@ class GradSync:
         after a collective that consumes its result waits on the device only."""
         g = self.flat.grad[b.lo:b.hi]
         n = b.hi - b.lo
+        if self.mode == "allreduce" and b.sparse:
+            # always the sparse protocol (fp32 or 16-bit wire): identical collectives on every rank
+            for p, plo, phi in b.sparse:
+                self._row_sparse_allreduce(p, plo, phi)
+            return
         if self.mode == "allreduce" and not self.compress:
-            if b.sparse:   # always the sparse protocol: identical collectives on every rank
-                for p, plo, phi in b.sparse:
-                    self._row_sparse_allreduce(p, plo, phi)
-                return
             if self.ncomm is not None:
                 self.ncomm.all_reduce(g)
             else:

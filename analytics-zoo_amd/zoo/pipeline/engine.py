@@ -227,6 +227,23 @@ class TrainingEngine:
                         self.sync.enable_ibo(optim_method))
         if self.ibo and self.hip_graph and hasattr(optim_method, "enable_device_hparams"):
             optim_method.enable_device_hparams(self.device)
+        # hipGraph with collectives over the native comm layer (ZooConfig.comm = "native"): the WHOLE
+        # data-parallel step -- forward, backward, the bucket collectives (RCCL on the comm stream,
+        # captured with the graph) and the optimizer update (device-scalar lr / bias corrections) --
+        # is ONE replay (BigDL's per-iteration AllReduceParameter sync in
+        # Topology.scala:1128-1206). The row-sparse protocol reads a host flag per step, so models
+        # with row-sparse tables keep the eager path; ZOO_GRAPH_FULL_STEP=0 keeps comm + update eager.
+        s_ = self.sync
+        self.full_graph = bool(
+            self.hip_graph and s_.comm and s_.ncomm is not None and not self.ibo and clip is None
+            and s_.mode == "allreduce" and getattr(optim_method, "supports_ranges", lambda: False)()
+            and hasattr(optim_method, "enable_device_hparams")
+            and not any(b.sparse for b in s_.buckets)
+            and os.environ.get("ZOO_GRAPH_FULL_STEP", "1") != "0")
+        self._full_optim = optim_method if self.full_graph else None
+        self._replayed_full = False
+        if self.full_graph:
+            optim_method.enable_device_hparams(self.device)
         # dropout under hipGraph: a device seed offset, restaged every step, is xored into the
         # seeds the captured kernels replay (fresh masks per step)
         self._seed_stager = None
@@ -263,6 +280,13 @@ class TrainingEngine:
                 torch.cuda.synchronize(self.device)
                 self._graphs.clear()
                 self._graph_warm.clear()
+        if self.full_graph and (self.clip is not None or self.optim is not self._full_optim):
+            # clipping / a new optimizer: the captured update no longer applies -- recapture the
+            # step without it (comm + update eager after the replay)
+            self.full_graph = False
+            torch.cuda.synchronize(self.device)
+            self._graphs.clear()
+            self._graph_warm.clear()
         if getattr(self.optim, "_dev_hp", None) is not None:
             self.optim.stage_device_hparams()
         if self._seed_stager is not None and (not self._graphs or seed_offset_used(self.device)):
@@ -295,6 +319,13 @@ class TrainingEngine:
             self.flat.grad_clean = False
             loss = torch.zeros((), device=self.device)
         with ph.range("comm_optim"):
+            if self._replayed_full:
+                # collectives and update ran inside the replay: host-side bookkeeping only
+                self._replayed_full = False
+                self.optim.finish_step(self.flat.bf16 is not None)
+                self.sync.reset()
+                self.state["neval"] += 1
+                return loss
             try:
                 self.sync.step(self.optim, self.clip)
             except Exception as e:  # noqa: BLE001
@@ -353,7 +384,7 @@ class TrainingEngine:
                 self.hip_graph = False
                 torch.cuda.synchronize(self.device)
                 return self._fwd_bwd(inputs, target)
-        graph, sx, sy, sloss, ibo_done = g
+        graph, sx, sy, sloss, ibo_done, full = g
         if not getattr(self.flat, "grad_clean", False):
             self.flat.grad.zero_()      # the captured step may rely on the optimizer's clearing
         self.flat.grad_clean = False
@@ -361,6 +392,9 @@ class TrainingEngine:
             s_.copy_(t, non_blocking=True)
         sy.copy_(target, non_blocking=True)
         graph.replay()
+        if full:   # the captured update cleared every gradient slot
+            self.flat.grad_clean = True
+            self._replayed_full = True
         # the buckets whose in-backward update is part of the graph: step() updates the rest
         self.sync._ibo_done = set(ibo_done)
         return sloss.clone()
@@ -372,16 +406,25 @@ class TrainingEngine:
         self.sync.overlap = False  # no collectives inside the capture: finish() launches them after replay
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()
+        full = self.full_graph
         try:
             with torch.cuda.graph(graph):
                 sloss = self._fwd_bwd(sx if as_list else sx[0], sy)
+                if full:
+                    # the bucket collectives (native comm, comm stream forked from the capture
+                    # stream) and the update, which reads its hyper-parameters from device memory
+                    flat = self.flat
+                    self.sync.finish()
+                    self.optim.step_range(flat.master, flat.grad, flat.bf16, 1.0 / self.sync.world, 0,
+                                          flat.master.numel(), zero_grad=True)
         finally:
             self.sync.overlap = overlap
         ibo_done = set(self.sync._ibo_done)   # in-backward updates captured into the graph
         self.sync.reset()
-        g = (graph, sx, sy, sloss, ibo_done)
+        g = (graph, sx, sy, sloss, ibo_done, full)
         self._graphs[key] = g
-        log.info("captured forward+backward as a hipGraph for inputs %s", key)
+        log.info("captured %s as a hipGraph for inputs %s",
+                 "forward+backward+collectives+update" if full else "forward+backward", key)
         return g
 
     # ------------------------------------------------------------------

@@ -271,8 +271,8 @@ def test_tensor_parallel_mlp_trains_through_engine():
 # ---------------------------------------------------------------------------
 # row-sparse embedding-gradient sync (NCF at DP): equals the dense all-reduce
 # ---------------------------------------------------------------------------
-def _ncf_worker(rank, world, port, q, sparse):
-    ctx = _init(rank, world, port)
+def _ncf_worker(rank, world, port, q, sparse, compress=""):
+    ctx = _init(rank, world, port, ZOO_GRAD_COMPRESSION=compress)
     from zoo.models.recommendation.neuralcf import NeuralCF
     from zoo.pipeline.api.keras.objectives import SparseCategoricalCrossEntropy
     from zoo.pipeline.api.keras.optimizers import Adam
@@ -291,9 +291,12 @@ def _ncf_worker(rank, world, port, q, sparse):
     ctx.stop()
 
 
-def test_row_sparse_embedding_sync_matches_dense_allreduce():
-    dense = _run(_ncf_worker, False)
-    sparse = _run(_ncf_worker, True)
+@pytest.mark.parametrize("compress", ["", "bf16"])
+def test_row_sparse_embedding_sync_matches_dense_allreduce(compress):
+    """fp32 wire, and the 16-bit wire (union rows packed to bf16, fp32 chunk sums, bf16 gather)
+    against the dense bucket protocol on the same wire."""
+    dense = _run(_ncf_worker, False, compress)
+    sparse = _run(_ncf_worker, True, compress)
     for rk in (0, 1):
         assert np.allclose(dense[rk][0], sparse[rk][0], atol=1e-6), "row-sparse sync differs from dense"
     assert np.allclose(sparse[0][0], sparse[1][0], atol=1e-7), "ranks diverged"

@@ -103,3 +103,45 @@ def test_engine_over_native_comm_matches_local_bitwise(gpu, rccl_world1, sharded
     assert e1.sync.ncomm is not None and len(e1.sync.buckets) > 2
     assert l0 == l1
     assert torch.equal(e0.flat.master, e1.flat.master)
+
+
+def test_full_step_graph_over_native_comm_matches_eager_bitwise(gpu, rccl_world1):
+    """with comm="native" and hip_graph the WHOLE data-parallel step -- forward,
+    backward, the bucket collectives (RCCL, captured on the comm stream) and the optimizer
+    update (device-scalar lr) -- is one graph replay, and in deterministic mode it reproduces the
+    eager step over the same communicator bit for bit, with an lr schedule that changes every step."""
+    from zoo.models.image.resnet import Bottleneck, ResNet
+    from zoo.ops import deterministic, set_deterministic, softmax_cross_entropy
+    from zoo.pipeline.api.keras.optimizers import SGD, Poly
+    from zoo.pipeline.engine import TrainingEngine
+    ctx = rccl_world1
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1)
+    x = torch.randn(8, 3, 64, 64, device="cuda", generator=g)
+    y = torch.randint(0, 16, (8,), device="cuda", generator=g)
+
+    def run(graph):
+        old = (ctx.config.force_comm, ctx.config.comm, ctx.config.grad_compression)
+        ctx.config.force_comm, ctx.config.comm, ctx.config.grad_compression = True, "native", "bf16"
+        try:
+            torch.manual_seed(3)
+            eng = TrainingEngine(ResNet(Bottleneck, [1, 1, 1, 1], num_classes=16, width=16), softmax_cross_entropy,
+                                 SGD(learningrate=0.05, momentum=0.9, learningrate_schedule=Poly(0.5, 20)),
+                                 ctx=ctx, bucket_mb=0.05, hip_graph=graph)
+        finally:
+            ctx.config.force_comm, ctx.config.comm, ctx.config.grad_compression = old
+        losses = [eng.train_step(x, y).float().item() for _ in range(7)]
+        torch.cuda.synchronize()
+        return eng, losses
+    prev = deterministic()
+    set_deterministic(True)
+    try:
+        e0, l0 = run(False)
+        e1, l1 = run(True)
+    finally:
+        set_deterministic(prev)
+    assert e1.full_graph and e1.sync.ncomm is not None and len(e1.sync.buckets) > 2
+    assert len(e1._graphs) == 1 and next(iter(e1._graphs.values()))[5]   # collectives + update captured
+    assert e1.optim.state["neval"] == e0.optim.state["neval"] == 8
+    assert l0 == l1, (l0, l1)
+    assert torch.equal(e0.flat.master, e1.flat.master)
