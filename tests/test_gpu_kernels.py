@@ -971,3 +971,44 @@ def test_conv_wgrad_band(gpu, shape):
     dw2[:, :ktot] = 0.5
     C.conv_wgrad(x, dy, dw2, R, R, 1, 1, pad, pad, 1, 1)
     assert torch.equal(dw, dw2)
+
+
+GCONV_SHAPES = [
+    # N, H, W, C, K, groups, R, stride, pad
+    (2, 13, 13, 48, 64, 2, 5, 1, 2),     # AlexNet conv2-like
+    (2, 13, 13, 64, 64, 2, 3, 2, 1),     # strided grouped
+    (2, 7, 7, 64, 32, 16, 3, 1, 1),      # ResNeXt-like: 4-channel groups, 2 outputs per group
+    (3, 9, 11, 24, 72, 3, 1, 1, 0),      # 1x1 grouped, K per group 24
+]
+
+
+@pytest.mark.parametrize("shape", GCONV_SHAPES)
+def test_grouped_conv_kernels_vs_fp32(gpu, shape):
+    """gconv.hip forward / data gradient / weight gradient against fp32 torch grouped conv on the
+    same bf16-rounded operands (dW accumulates into a padded [K, ldb] buffer)."""
+    from zoo.ops import native
+    C_ = native()
+    N, H, W, C, K, g, R, st, pad = shape
+    Cg = C // g
+    torch.manual_seed(21)
+    x = torch.randn(N, H, W, C, device=gpu).bfloat16()
+    w4 = (torch.randn(K, Cg, R, R, device=gpu) / math.sqrt(R * R * Cg)).bfloat16()
+    ld = (R * R * Cg + 7) // 8 * 8
+    wp = torch.zeros(K, ld, device=gpu, dtype=torch.bfloat16)
+    wp[:, :R * R * Cg] = w4.permute(0, 2, 3, 1).reshape(K, -1)
+    b = torch.randn(K, device=gpu)
+    xr = x.float().permute(0, 3, 1, 2).requires_grad_(True)
+    wr = w4.float().requires_grad_(True)
+    yr = F.conv2d(xr, wr, stride=st, padding=pad, groups=g)
+    y = C_.gconv_fwd(x, wp, b, g, R, R, st, st, pad, pad, 1, 1, 0)
+    ref = yr.detach().permute(0, 2, 3, 1) + b
+    assert y.shape == ref.shape
+    assert rel(y, ref) < 1e-2
+    dy = torch.randn(y.shape, device=gpu).bfloat16()
+    yr.backward(dy.float().permute(0, 3, 1, 2))
+    dx = C_.gconv_dgrad(dy, wp, g, H, W, C, R, R, st, st, pad, pad, 1, 1)
+    assert rel(dx, xr.grad.permute(0, 2, 3, 1)) < 1e-2
+    dw = torch.zeros(K, ld, device=gpu)
+    C_.gconv_wgrad(x, dy, dw, g, R, R, st, st, pad, pad, 1, 1)
+    assert rel(dw[:, :R * R * Cg], wr.grad.permute(0, 2, 3, 1).reshape(K, -1)) < 1e-3
+    assert dw[:, R * R * Cg:].abs().max().item() == 0.0
