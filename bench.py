@@ -53,6 +53,9 @@ def parse():
                     help="gradient wire: auto = bf16 whenever GPU collectives run (BigDL 16-bit transfer)")
     ap.add_argument("--bucket-mb", type=float, default=0.0, help="0: per-model default (ResNet 32, NCF one bucket)")
     ap.add_argument("--profile-steps", type=int, default=0)
+    ap.add_argument("--comm", default="auto", choices=["auto", "torch", "native"],
+                    help="bucket collectives through the torch ProcessGroup or the C++ RCCL layer; auto: native for "
+                         "NCF (its captured step then holds the collectives and the update: one replay per step)")
     ap.add_argument("--input", default="auto", choices=["auto", "device", "featureset"],
                     help="featureset: ResNet-50 trained through NNEstimator.fit on a synthetic DataFrame of uint8 "
                          "NHWC images (FeatureSet -> pinned batches -> copy stream -> on-device normalisation), "
@@ -204,7 +207,8 @@ def grad_sync_label(eng, a):
         return "none"
     lab = "sharded(ZeRO-1,bf16-weight-gather)" if eng.sync.mode == "sharded" else "allreduce(bucketed,overlapped)"
     return lab + ("+bf16-wire" if eng.sync.compress else "+fp32-wire") + \
-        ",%d-buckets" % len(eng.sync.buckets)
+        ",%d-buckets" % len(eng.sync.buckets) + (",native-comm" if eng.sync.ncomm is not None else "") + \
+        (",whole-step-hipgraph" if getattr(eng, "full_graph", False) else "")
 
 
 def comm_diagnostics(eng, x, y, world):
@@ -277,8 +281,9 @@ def main():
     import torch.distributed as dist
     from zoo.common.nncontext import init_nncontext
     comp = "" if a.grad_compression == "none" else a.grad_compression
+    comm = a.comm if a.comm != "auto" else ("native" if a.model == "ncf" else "torch")
     ctx = init_nncontext("bench", sharded_optimizer=a.sharded, force_comm=a.force_comm or a.sharded,
-                         grad_compression=comp)
+                         grad_compression=comp, comm=comm)
     world = ctx.world_size
     if world != a.gpus:
         print("bench.py: --gpus %d but the process group has %d ranks" % (a.gpus, world), file=sys.stderr)
