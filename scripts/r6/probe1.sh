@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out/r6
 export TMPDIR=/tmp
 T="timeout -k 10"
-$T 300 python -u -m pytest tests/test_gpu_kernels.py -k "gconv" -q --timeout 120 --timeout-method thread \
+$T 300 python -u -m pytest tests/test_gpu_kernels.py -k "grouped_conv_kernels" -q --timeout 120 --timeout-method thread \
   -p no:cacheprovider > gpurun_out/r6/probe1_gconv.log 2>&1
 rc=$?; tail -3 gpurun_out/r6/probe1_gconv.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
 # stop at the first crash (segfault / abort / timeout): nothing more runs on the GPU after it
