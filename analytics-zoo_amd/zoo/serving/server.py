@@ -215,6 +215,8 @@ class ClusterServing:
         self.records = 0
         # host seconds per serving stage of the pipelined loop (main thread; the reader's
         # read + entropy decode under "read_decode")
+        # set to a list (or deque) to collect per-batch stage stamps of the pipelined loop
+        self.batch_trace = None
         self.stage_time = {"wait_input": 0.0, "preprocess_enqueue": 0.0, "wait_gpu": 0.0, "post_finish": 0.0,
                            "read_decode": 0.0, "batches": 0}
         self.summary = None
@@ -463,10 +465,11 @@ class ClusterServing:
                     last = time.time()
                     t0 = time.perf_counter()
                     item = self._decode_native(recs)
-                    self.stage_time["read_decode"] += time.perf_counter() - t0
+                    t1 = time.perf_counter()
+                    self.stage_time["read_decode"] += t1 - t0
                     while not done.is_set():
                         try:
-                            q.put(item, timeout=0.1)
+                            q.put((item, (t0, t1)), timeout=0.1)
                             break
                         except queue.Full:
                             continue
@@ -484,15 +487,26 @@ class ClusterServing:
         pending = None
 
         def complete(p):
-            h, ids, uris, n = p
+            h, ids, uris, n, st = p
             t0 = time.perf_counter()
             out = h.result() if overlap else h
             t1 = time.perf_counter()
             outs = out if isinstance(out, np.ndarray) else out[0]
             vals = post_process_batch(outs[:n], flt)
+            t2 = time.perf_counter()
             self.db.finish(STREAM, GROUP, ids, [("result:" + u, v) for u, v in zip(uris, vals)])
+            t3 = time.perf_counter()
             prof["wait_gpu"] += t1 - t0
-            prof["post_finish"] += time.perf_counter() - t1
+            prof["post_finish"] += t3 - t1
+            if self.batch_trace is not None:
+                # per-batch stage stamps (ms): read+decode, queued for the GPU side, H2D +
+                # preprocess, model enqueue, held behind the previous batch, D2H wait, top-N, write
+                r0, r1, d0, d1, d2 = st
+                self.batch_trace.append({"n": n, "total": (t3 - r0) * 1e3, "decode": (r1 - r0) * 1e3,
+                                         "queued": (d0 - r1) * 1e3, "h2d_pre": (d1 - d0) * 1e3,
+                                         "enqueue": (d2 - d1) * 1e3, "lookahead": (t0 - d2) * 1e3,
+                                         "wait_gpu": (t1 - t0) * 1e3, "post": (t2 - t1) * 1e3,
+                                         "write": (t3 - t2) * 1e3})
             prof["batches"] += 1
             if self.finish_hook is not None:
                 self.finish_hook(uris, time.time())
@@ -520,18 +534,20 @@ class ClusterServing:
                     break
                 if isinstance(item, Exception):
                     raise item
-                ids, uris, decoded = item
+                (ids, uris, decoded), (r0, r1) = item
                 t0 = time.perf_counter()
                 x = self._to_batch(decoded)
                 n = x.shape[0]
                 nb = _bucket(n, bs)
                 if nb > n:   # pad to a power-of-two bucket: hipGraphs for ~log2(batch) shapes only
                     x = torch.cat([x, x.new_zeros((nb - n,) + tuple(x.shape[1:]))])
+                t1 = time.perf_counter()
                 h = self.im.predict_async(x) if overlap else self.im.predict(x)
-                prof["preprocess_enqueue"] += time.perf_counter() - t0
+                t2 = time.perf_counter()
+                prof["preprocess_enqueue"] += t2 - t0
                 if pending is not None:
                     complete(pending)
-                pending = (h, ids, uris, n)
+                pending = (h, ids, uris, n, (r0, r1, t0, t1, t2))
                 if not overlap:
                     complete(pending)
                     pending = None
