@@ -77,6 +77,18 @@ void req_dev(const torch::Tensor& t, const char* what) {
 
 hipStream_t cur() { return c10::hip::getCurrentHIPStream().stream(); }
 
+// A one-rank communicator's collectives are identities: a device copy on the current stream (or
+// nothing, in place) instead of an RCCL launch. Keeps world-1 runs (force_comm, tests) free of
+// RCCL's single-rank paths, which a hipGraph capture of an all-to-all left hanging at communicator
+// teardown (profiles/r6/rccl_capture_probe_all_to_all_r6.log).
+bool local_copy(const ZComm* c, void* dst, const void* src, size_t bytes) {
+  if (c->world != 1) return false;
+  if (dst != src && bytes > 0)
+    TORCH_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, cur()) == hipSuccess,
+                "zoo comm: local copy failed");
+  return true;
+}
+
 }  // namespace
 
 py::bytes comm_unique_id() {
@@ -131,6 +143,7 @@ std::vector<int64_t> comm_info(int64_t h) {
 void comm_all_reduce(int64_t h, torch::Tensor t, const std::string& op) {
   ZComm* c = get(h);
   req_dev(t, "all_reduce tensor");
+  if (local_copy(c, t.data_ptr(), t.data_ptr(), 0)) return;
   check_nccl(ncclAllReduce(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), op_of(op), c->comm, cur()),
              "ncclAllReduce");
 }
@@ -142,6 +155,7 @@ void comm_reduce_scatter(int64_t h, torch::Tensor out, torch::Tensor inp, const 
   req_dev(inp, "reduce_scatter input");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && inp.numel() == out.numel() * c->world,
               "reduce_scatter: input must hold world x out elements of the same dtype");
+  if (local_copy(c, out.data_ptr(), inp.data_ptr(), out.nbytes())) return;
   check_nccl(ncclReduceScatter(inp.data_ptr(), out.data_ptr(), out.numel(), dtype_of(out), op_of(op), c->comm, cur()),
              "ncclReduceScatter");
 }
@@ -153,6 +167,7 @@ void comm_all_gather(int64_t h, torch::Tensor out, torch::Tensor inp) {
   req_dev(inp, "all_gather input");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() * c->world,
               "all_gather: out must hold world x input elements of the same dtype");
+  if (local_copy(c, out.data_ptr(), inp.data_ptr(), out.nbytes())) return;
   check_nccl(ncclAllGather(inp.data_ptr(), out.data_ptr(), inp.numel(), dtype_of(inp), c->comm, cur()),
              "ncclAllGather");
 }
@@ -164,6 +179,7 @@ void comm_all_to_all(int64_t h, torch::Tensor out, torch::Tensor inp) {
   req_dev(inp, "all_to_all input");
   TORCH_CHECK(out.scalar_type() == inp.scalar_type() && out.numel() == inp.numel() && inp.numel() % c->world == 0,
               "all_to_all: equal-size tensors of the same dtype, divisible by the world size");
+  if (local_copy(c, out.data_ptr(), inp.data_ptr(), out.nbytes())) return;
   check_nccl(ncclAllToAll(inp.data_ptr(), out.data_ptr(), inp.numel() / c->world, dtype_of(inp), c->comm, cur()),
              "ncclAllToAll");
 }
@@ -172,6 +188,7 @@ void comm_broadcast(int64_t h, torch::Tensor t, int64_t root) {
   ZComm* c = get(h);
   req_dev(t, "broadcast tensor");
   TORCH_CHECK(root >= 0 && root < c->world, "broadcast: root");
+  if (local_copy(c, t.data_ptr(), t.data_ptr(), 0)) return;
   check_nccl(ncclBroadcast(t.data_ptr(), t.data_ptr(), t.numel(), dtype_of(t), (int)root, c->comm, cur()),
              "ncclBroadcast");
 }

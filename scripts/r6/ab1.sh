@@ -7,7 +7,7 @@ mkdir -p gpurun_out/r6
 export TMPDIR=/tmp
 T="timeout -k 10"
 $T 600 python -u -m pytest tests/test_gpu_native_import.py tests/test_gpu_kernels.py tests/test_gpu_comm_native.py \
-  -k "wgrad or group" -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  -k "wgrad or group or grouped_conv" -q --timeout 200 --timeout-method thread -p no:cacheprovider \
   > gpurun_out/r6/ab1_tests.log 2>&1
 rc=$?; tail -3 gpurun_out/r6/ab1_tests.log
 # test failures (1) do not stop the A/B; a crash, fault or timeout does
@@ -38,3 +38,7 @@ for mode in eager graph; do
   python3 analytics-zoo_amd/tools/prof_step.py $DB softmax_xent $back --critical > gpurun_out/r6/prof_bert_${mode}_step.md 2>&1
   tail -30 gpurun_out/r6/prof_bert_${mode}_step.md
 done
+# last: the whole-step hipGraph over the native comm layer (a crash here ends the call)
+$T 300 python -u -m pytest tests/test_gpu_comm_native.py -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+  > gpurun_out/r6/ab1_fullstep.log 2>&1
+echo "fullstep rc=$?"; tail -3 gpurun_out/r6/ab1_fullstep.log

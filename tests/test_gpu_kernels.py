@@ -1011,4 +1011,5 @@ def test_grouped_conv_kernels_vs_fp32(gpu, shape):
     dw = torch.zeros(K, ld, device=gpu)
     C_.gconv_wgrad(x, dy, dw, g, R, R, st, st, pad, pad, 1, 1)
     assert rel(dw[:, :R * R * Cg], wr.grad.permute(0, 2, 3, 1).reshape(K, -1)) < 1e-3
-    assert dw[:, R * R * Cg:].abs().max().item() == 0.0
+    if ld > R * R * Cg:
+        assert dw[:, R * R * Cg:].abs().max().item() == 0.0
