@@ -1064,10 +1064,7 @@ static void launch_bwd(const void* dout, const void* q, const void* k, const voi
     hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
     return n > 0 ? n : 256;
   }();
-  static const bool pers = [] {
-    const char* e = getenv("ZOO_ATTN_PERSIST");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool pers = true;
   const int nkb = (S + 127) / 128;
   if constexpr (D == 64 && QW == 2) {
     if (pers) {
@@ -1105,10 +1102,7 @@ static void launch_bwd_d(const void* dout, const void* q, const void* k, const v
   // 32 queries per wave: at L <= 128 (BERT s128) an 8-wave block would leave half its waves
   // without queries, so those sequences use 4-wave dQ blocks (two per CU)
   constexpr int QW = D == 64 ? 2 : 1, NWQ = D == 64 ? 8 : 4;
-  static const bool small_q = [] {
-    const char* e = getenv("ZOO_ATTN_DQ4");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool small_q = true;
   const bool q4 = D == 64 && small_q && L <= 128;
 #define ZOO_ATTN_BWD(HM_, DR_)                                                                                   \
   do {                                                                                                          \

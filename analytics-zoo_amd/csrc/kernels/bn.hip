@@ -739,14 +739,8 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_apply_kernel(
 
 // contiguous row range per block: ~kApplyBlocks blocks, at least kMinRows rows per thread-row
 static int apply_rows_per_block(int M, int C) {
-  static const int target = [] {
-    const char* e = getenv("ZOO_BN_BLOCKS");
-    return e ? atoi(e) : 1024;
-  }();
-  static const int min_rows = [] {
-    const char* e = getenv("ZOO_BN_MINROWS");
-    return e ? atoi(e) : 8;
-  }();
+  static const int target = 1024;
+  static const int min_rows = 8;
   const int cpr = C / 8;
   const int rstep = 256 / (cpr < 256 ? cpr : 256);
   int rpb = (M + target - 1) / target;
@@ -827,16 +821,10 @@ extern "C" hipError_t zoo_bn_reduce(const void* A, const void* Z, const void* X,
 
 // grid for the apply kernels: interleaved tiles (default) or contiguous ranges (ZOO_BN_INTERLEAVE=0)
 static void apply_grid(int M, int C, int tile_units, int* blocks, int* rpb) {
-  static const int inter = [] {
-    const char* e = getenv("ZOO_BN_INTERLEAVE");
-    return e ? atoi(e) : 1;
-  }();
+  static const int inter = 1;
   // 512 blocks x 256 threads: 2 blocks per CU; tools/bn_bench.py sweep on the
   // ResNet-50 shapes (more blocks only repeat the coefficient prologue)
-  static const int target = [] {
-    const char* e = getenv("ZOO_BN_BLOCKS");
-    return e ? atoi(e) : 512;
-  }();
+  static const int target = 512;
   if (inter) {
     const int cpr = C / 8;
     const int rstep = 256 / (cpr < 256 ? cpr : 256);
@@ -876,10 +864,7 @@ extern "C" hipError_t zoo_bn_bwd_apply(const void* dZ, const void* Z, const void
                                        hipStream_t st) {
   // rows per step (ZOO_BN_BWD_ROWS=4: 8-12 loads in flight per thread): 2 and 4 measure the
   // same, 6-8.6 TB/s on the ResNet-50 shapes (tools/bn_bench.py, round 3)
-  static const int rows = [] {
-    const char* e = getenv("ZOO_BN_BWD_ROWS");
-    return e && atoi(e) == 4 ? 4 : 2;
-  }();
+  static const int rows = 2;
   int rpb, blocks;
   apply_grid(M, C, rows, &blocks, &rpb);
   if (rows == 2)
@@ -900,10 +885,7 @@ static void colsum_grid(int M, int C, int* ct, int* col_groups, int* chunks, int
   *col_groups = (cpr + *ct - 1) / *ct;
   // total blocks (ZOO_COLSUM_BLOCKS): every block ends in one fp32 atomic per column, so the
   // block count is also the number of adders per output address
-  static const int target = [] {
-    const char* e = getenv("ZOO_COLSUM_BLOCKS");
-    return e && atoi(e) > 0 ? atoi(e) : 256;  // BERT b128: 17.37 -> 17.20 ms/step vs 1024
-  }();
+  static const int target = 256;  // BERT b128: 17.37 -> 17.20 ms/step vs 1024
   int ch = target / *col_groups;
   const int max_ch = (M + 31) / 32;
   if (ch > max_ch) ch = max_ch;

@@ -381,10 +381,7 @@ __global__ __launch_bounds__(C3_NT, 1) void c3_kernel(const bf16_t* __restrict__
 using namespace zoo;
 
 static int c3_mode() {
-  static const int m = [] {
-    const char* e = getenv("ZOO_C3");
-    return e ? atoi(e) : 1;
-  }();
+  static const int m = 1;
   return m;
 }
 static int g_c3_force = -1;  // -1: ZOO_C3, 0 off, 1 on (tests / A/B)
@@ -490,27 +487,6 @@ extern "C" hipError_t zoo_c3(const void* X, const void* W, void* Y, const void* 
     else
       hipLaunchKernelGGL((c3_kernel<2, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X, (const bf16_t*)W,
                          (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
-    return hipGetLastError();
-  }
-  static const bool late = [] {
-    const char* e = getenv("ZOO_C3_LATE");
-    return e && atoi(e) != 0;
-  }();
-  if (late) {  // the previous read schedule (fragment reads in the last 14 MFMA gaps), for A/B
-    static bool lattr = false;
-    if (!lattr) {
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<1, false, true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      hipFuncSetAttribute(reinterpret_cast<const void*>(&c3_kernel<2, false, true>),
-                          hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      lattr = true;
-    }
-    if (epi == 1)
-      hipLaunchKernelGGL((c3_kernel<1, false, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X,
-                         (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
-    else
-      hipLaunchKernelGGL((c3_kernel<2, false, true>), dim3(grid), dim3(C3_NT), smem, st, (const bf16_t*)X,
-                         (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, stats, c, bs);
     return hipGetLastError();
   }
   if (epi == 1)

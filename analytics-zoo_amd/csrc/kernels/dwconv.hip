@@ -357,10 +357,7 @@ struct Dw3Plan {
 
 static Dw3Plan dw3_plan(const DwGeom& g) {
   Dw3Plan pl{false, 0, 1, 1};
-  static const bool on = [] {
-    const char* e = getenv("ZOO_DW3_WGRAD");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool on = true;
   if (!on || g.R != 3 || g.S != 3 || g.sh != g.sw || (g.sh != 1 && g.sh != 2) || g.C % 8) return pl;
   const int cpr = g.C / 4;                       // 4-channel chunks
   int qlt = 1;                                   // q lanes wanted: the row width, <= 32

@@ -763,10 +763,7 @@ template <int VEC, bool IS1x1, bool LDIL, int BN, bool DMA>
 static hipError_t launch_ig(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                             const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                             hipStream_t st) {
-  static const bool lean_ok = [] {
-    const char* e = getenv("ZOO_IGEMM_LEAN");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool lean_ok = true;
   const bool lean = lean_ok && Y && !Yf && !bias && !resid && act == 0 && !g.omap && !bs.sums;
   if (lean) return launch_ig1<VEC, IS1x1, LDIL, BN, DMA, 1>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   const bool bwd = lean_ok && Y && !Yf && !bias && act == 0 && !stats;
@@ -778,10 +775,7 @@ template <int VEC, bool IS1x1, bool LDIL, bool DMA>
 static hipError_t launch_ig_bn(const bf16_t* X, const bf16_t* W, bf16_t* Y, float* Yf, const float* bias,
                                const bf16_t* resid, float* stats, const ConvGeom& g, int act, const BwdStats& bs,
                                hipStream_t st) {
-  static const int force_bn = [] {
-    const char* e = getenv("ZOO_IGEMM_BN");
-    return e ? atoi(e) : 0;
-  }();
+  static const int force_bn = 0;
   if (force_bn == 64) return launch_ig<VEC, IS1x1, LDIL, 64, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   if (force_bn == 128) return launch_ig<VEC, IS1x1, LDIL, 128, DMA>(X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
   // BN=64 tiles (lower VGPR/LDS footprint, more workgroups in flight) win while
@@ -834,10 +828,7 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
     const int route = igemm_route_epi(epi, bsp && bsp->zgelu);
     if (zoo_pw_eligible(g, route, bsp)) return zoo_pw(X, W, Y, resid, stats, g, epi, bsp, st);
     // the space-to-depth ResNet stem (4x4, 16 -> 64) on the same persistent kernel with a gathered operand
-    static const bool stem_on = [] {
-      const char* e = getenv("ZOO_PW_STEM");
-      return e ? atoi(e) != 0 : true;
-    }();
+    static const bool stem_on = true;
     if (stem_on && !(bsp && bsp->sums) && zoo_pw_stem_eligible(g, route)) return zoo_pw_stem(X, W, Y, stats, g, st);
   }
   // whole-64-channel K-tiles: the large-tile second-generation kernel (igemm2.hip)
@@ -854,10 +845,7 @@ extern "C" hipError_t zoo_igemm(const void* X, const void* W, void* Y, float* Yf
   const bool ldil = g->lh > 1 || g->lw > 1;
   // LDS-DMA staging (global_load_lds) for the 16-byte-vector paths; ZOO_IGEMM_DMA=0 selects
   // the register-staged variant
-  static const bool dma = [] {
-    const char* e = getenv("ZOO_IGEMM_DMA");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool dma = true;
   if (g->C == 4) return launch_ig_bn<4, false, false, false>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);
   if (dma) {
     if (is1x1) return launch_ig_bn<8, true, false, true>(x, w, y, Yf, bias, rs, stats, *g, act, bs, st);

@@ -329,7 +329,7 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
     }
   }
   // Software-pipelined 2-stage loop (default for the 2-stage tiles; ConvGeom.dbg bit 16 = the
-  // plain loop below, ZOO_I2_PIPE=0): the fragment reads of k-half 1 of tile kt run in the MFMA
+  // plain loop below): the fragment reads of k-half 1 of tile kt run in the MFMA
   // gaps of k-half 0, and the reads of k-half 0 of tile kt+1 in the gaps of k-half 1 -- the
   // barrier sits between the two halves, so no wave ever waits on an LDS read with its MFMA
   // pipe empty (the plain loop issues all 2 x (TM + TN) reads, more than the 4-bit lgkmcnt can
@@ -693,33 +693,16 @@ enum I2Tile : int {
 
 static bool i2_is_band(int tile) { return tile >= I2_B224x64 && tile <= I2_B224x128w; }
 
-static int g_i2_mode = -1;  // -1: unset (read ZOO_IGEMM2), 0: off, 1: on
-static int g_i2_tile = -1;  // -1: unset (read ZOO_IGEMM2_TILE), 0 auto, else I2Tile
-static int g_i2_band = -1;  // -1: unset (read ZOO_I2_BAND), 0: off, 1: on
+// selectors set through zoo_igemm2_set / zoo_igemm2_tile_set / zoo_igemm2_band_set (tests, A/B tools)
+static int g_i2_mode = 1;  // 0: off, 1: on
+static int g_i2_tile = 0;  // 0 auto, else I2Tile
+// band tiles off since the two-stream backward: ResNet-50 b256 12,273 / 12,267 img/s off vs
+// 12,239 / 12,205 on, same box (scripts/r4/knobs.sh); kept for the stride-1 band tests
+static int g_i2_band = 0;
 
-static int i2_mode() {
-  if (g_i2_mode < 0) {
-    const char* e = getenv("ZOO_IGEMM2");
-    g_i2_mode = e ? atoi(e) : 1;
-  }
-  return g_i2_mode;
-}
-static int i2_tile_force() {
-  if (g_i2_tile < 0) {
-    const char* e = getenv("ZOO_IGEMM2_TILE");
-    g_i2_tile = e ? atoi(e) : 0;
-  }
-  return g_i2_tile;
-}
-static int i2_band_mode() {
-  if (g_i2_band < 0) {
-    // off by default since the two-stream backward: ResNet-50 b256 12,273 / 12,267 img/s off vs
-    // 12,239 / 12,205 on, same box (scripts/r4/knobs.sh); the band tiles stay available (=1)
-    const char* e = getenv("ZOO_I2_BAND");
-    g_i2_band = e ? atoi(e) : 0;
-  }
-  return g_i2_band;
-}
+static int i2_mode() { return g_i2_mode; }
+static int i2_tile_force() { return g_i2_tile; }
+static int i2_band_mode() { return g_i2_band; }
 
 static int i2_bm(int tile) {
   switch (tile) {
@@ -839,10 +822,7 @@ static int i2_band_choose(const ConvGeom& g, int epi) {
     return 0;
   if (epi == 3 || epi == 4) return 0;
   if (224 % g.Q != 0 || 224 / g.Q > g.P) return 0;
-  static const int forced = [] {
-    const char* e = getenv("ZOO_I2_BAND_TILE");
-    return e ? atoi(e) : 0;
-  }();
+  static const int forced = 0;
   const int t = forced >= I2_B224x64 ? forced : (g.K <= 64 ? I2_B224x64 : I2_B224x128);
   const I2Band b = i2_band_geom(g, 224);
   const size_t smem = (size_t)(g.C > 64 ? 2 : 1) * b.pbytes + 3 * (size_t)i2_bn(t) * 128 + (size_t)i2_nw(t) * 1024;
@@ -867,18 +847,12 @@ static int i2_choose(const ConvGeom& g, int epi) {
   auto tiles = [&](int t) { return i2_tiles_m(g, t) * ((g.K + i2_bn(t) - 1) / i2_bn(t)); };
   // narrowest output the large-tile kernel takes (ZOO_I2_KMIN; the 128x128 tile serves 128-wide
   // outputs such as the ResNet stage-2 3x3 convs when set to 128)
-  static const int kmin = [] {
-    const char* e = getenv("ZOO_I2_KMIN");
-    return e ? atoi(e) : 256;
-  }();
+  static const int kmin = 256;
   if (g.K < kmin) return 0;
   if (epi == 4) {
     // GELU-backward dgrad (BERT FFN): ZOO_I2_GELU_TILE picks its tile (A/B of the 128x128
     // tile, whose EPI 2 prefetches the next slice's pre-activation, against 256x256)
-    static const int gt = [] {
-      const char* e = getenv("ZOO_I2_GELU_TILE");
-      return e ? atoi(e) : 0;
-    }();
+    static const int gt = 0;
     if (gt > 0 && g.Ktot >= 256) return gt;
   }
   if (epi == 2 && g.Ktot < 1024) return 0;
@@ -889,10 +863,7 @@ static int i2_choose(const ConvGeom& g, int epi) {
     // round-equivalents (BERT / ResNet stage 3-4: 196 tiles of 256 rows fill 77 % of the CUs,
     // 224 tiles of 224 rows 88 %; BERT linears 16384x{2304,768}x768 and x768x3072 -5..-7 %, ResNet-50
     // fwd/dgrad conv sweep -1..-2 %, profiles/r4/ab/q224_*). ZOO_I2_Q224=0: always 256x256.
-    static const bool q224 = [] {
-      const char* e = getenv("ZOO_I2_Q224");
-      return e ? atoi(e) != 0 : true;
-    }();
+    static const bool q224 = true;
     if (q224 && epi != 4) {
       static int ncu = 0;
       if (!ncu) {
@@ -958,18 +929,11 @@ extern "C" hipError_t zoo_igemm2(const void* X, const void* W, void* Y, float* Y
   const bf16_t* x = (const bf16_t*)X;
   const bf16_t* w = (const bf16_t*)W;
   if (i2_is_band(tile)) {
-    static const int dbg = [] {
-      const char* e = getenv("ZOO_I2_DBG");
-      return e ? atoi(e) : 0;
-    }();
     ConvGeom gb = *g;
-    gb.dbg = dbg;
+    gb.dbg = 0;
     return i2_tile<I2_AM_BAND>(tile, epi, x, w, (bf16_t*)Y, Yf, bias, (const bf16_t*)resid, stats, gb, act, bs, st);
   }
-  static const int pipe = [] {
-    const char* e = getenv("ZOO_I2_PIPE");
-    return e ? atoi(e) : 1;
-  }();
+  static const int pipe = 1;
   ConvGeom gp = *g;
   gp.dbg = pipe ? 0 : 16;  // bit 16: the plain (unpipelined) 2-stage loop
   if (is1x1)

@@ -652,10 +652,7 @@ extern "C" hipError_t zoo_dropout_add_layernorm_fwd(const void* A, const void* X
 }
 
 static int ln_v2_nch(int D) {
-  static const bool on = [] {
-    const char* e = getenv("ZOO_LN_BWD_V2");
-    return e ? atoi(e) != 0 : true;
-  }();
+  static const bool on = true;
   if (!on || D % 4 || D > 64 * 4 * 4) return 0;
   return (D + 255) / 256;                      // 4-element chunks per lane
 }

@@ -393,15 +393,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   }
 }
 
-static int g_pw_mode = -1;  // -1 unset (ZOO_PW), 0 off, 1 on
+static int g_pw_mode = 1;  // 0 off, 1 on (zoo_pw_set: tests and A/B tools)
 
-static int pw_mode() {
-  if (g_pw_mode < 0) {
-    const char* e = getenv("ZOO_PW");
-    g_pw_mode = e ? atoi(e) : 1;
-  }
-  return g_pw_mode;
-}
+static int pw_mode() { return g_pw_mode; }
 
 static int pw_ncu() {
   static int ncu = 0;
@@ -508,10 +502,7 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
                      g->lw == 1 && g->H == g->P && g->W == g->Q && g->omap == 0;
   // forward with a 512-deep reduction: the tiled kernels are as fast or faster there
   // (tools/pw_bench.py --ab: 57 / 104 / 57 us vs 54 / 91 / 39 us on the three ResNet-50 shapes)
-  static const int fwd_kmax = [] {
-    const char* e = getenv("ZOO_PW_FWD_KMAX");
-    return e ? atoi(e) : 256;
-  }();
+  static const int fwd_kmax = 256;
   if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
@@ -542,13 +533,9 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
                              const ConvGeom* g, int epi, const BwdStats* bsp, hipStream_t st) {
   BwdStats bs = bsp ? *bsp : BwdStats{nullptr, nullptr, nullptr, nullptr, nullptr};
   // the prologue at K = 128 runs 64-channel groups (register budget, see pw_dispatch)
-  // prologue: 64-channel groups at K = 256 (256 VGPRs); at K = 128 64 unless ZOO_PRO_NP128
-  static const bool np128 = [] {
-    const char* e = getenv("ZOO_PRO_NP128");
-    return e && atoi(e) != 0;
-  }();
+  // prologue: 64-channel groups at K = 128 and K = 256 (256 VGPRs)
   const bool pro = bs.pro_y || bs.pro_fwd;
-  const int NP = (pro && ((g->Ktot == 128 && !np128) || g->Ktot == 256) && g->K % 64 == 0) ? 64
+  const int NP = (pro && (g->Ktot == 128 || g->Ktot == 256) && g->K % 64 == 0) ? 64
                                                                                               : pw_np(g->K, g->Ktot);
   if (epi == 1 && bs.pro_fwd)
     return pw_dispatch<1, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);

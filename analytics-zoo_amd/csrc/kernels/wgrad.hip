@@ -518,10 +518,7 @@ using namespace zoo;
 
 // split plan of the pixel reduction: sets g->m_per_split, returns the number of splits
 static int wgrad_bm(const WgradGeom& g) {
-  static const int narrow = [] {
-    const char* e = getenv("ZOO_WGRAD_BM64");
-    return e ? atoi(e) : 1;
-  }();
+  static const int narrow = 1;
   return (narrow && g.K <= 64) ? 64 : 128;
 }
 
@@ -533,14 +530,8 @@ extern "C" int zoo_wgrad_plan(WgradGeom* gp) {
   // 512 (one occupancy-full wave of 2 per CU) rather than 1024: the side-stream weight gradients
   // then hold fewer CUs at a time next to the compute stream and write half the partials
   // (ResNet-50 b256 +0.7 %, profiles/r5/ab_wgrad_wg_r5.log)
-  static const int target = [] {
-    const char* e = getenv("ZOO_WGRAD_WG");
-    return e ? atoi(e) : 512;
-  }();
-  static const int min_pix = [] {
-    const char* e = getenv("ZOO_WGRAD_MINPIX");
-    return e ? atoi(e) : 512;
-  }();
+  static const int target = 512;
+  static const int min_pix = 512;
   int splits = (target + tiles - 1) / tiles;
   const int max_splits = (g.M + min_pix - 1) / min_pix;
   if (splits > max_splits) splits = max_splits;
@@ -561,12 +552,9 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
   const int splits = zoo_wgrad_plan(&g);
   if (splits <= 1) part = nullptr;
   const size_t smem = (size_t)2 * WG_BK * (bm + WG_BN) * sizeof(bf16_t);
-  static const bool dma = [] {
-    // LDS-DMA staging: slower in round 2 (bench 8912 vs 9045 img/s with register staging), ahead
-    // by 0.1-0.4 % in five round-5 pairs on the side stream (profiles/r5/ab_wgrad_wg_r5.log)
-    const char* e = getenv("ZOO_WGRAD_DMA");
-    return e ? atoi(e) != 0 : true;
-  }();
+  // LDS-DMA staging: slower in round 2 (bench 8912 vs 9045 img/s with register staging), ahead
+  // by 0.1-0.4 % in five round-5 pairs on the side stream (profiles/r5/ab_wgrad_wg_r5.log)
+  constexpr bool dma = true;
   if (g.C == 4) {
     if (bm == 64)
       hipLaunchKernelGGL((wgrad_kernel<4, false, 64>), dim3(tiles * splits), dim3(256), smem, st,
@@ -622,10 +610,7 @@ static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, 
     if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || ncu <= 0) ncu = 256;
   }
   const int nbands = g.N * ((g.P + TP - 1) / TP);
-  static const int target = [] {
-    const char* e = getenv("ZOO_WGRAD_BAND_WG");
-    return e ? atoi(e) : 0;
-  }();
+  static const int target = 0;
   int G = target > 0 ? target : ncu;
   if (G > nbands) G = nbands;
   if (!part) return G + (G > kFoldGroup ? (G + kFoldGroup - 1) / kFoldGroup : 0);

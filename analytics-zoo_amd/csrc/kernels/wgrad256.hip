@@ -377,10 +377,7 @@ extern "C" void zoo_wgrad256_target(int t) { g_w256_target = t; }
 
 extern "C" int zoo_wgrad256_plan(int M, int N, int K, int* m_per_split) {
   const int tiles = ((N + W2_T - 1) / W2_T) * ((K + W2_T - 1) / W2_T);
-  static const int target_default = [] {
-    const char* e = getenv("ZOO_WGRAD256_WG");
-    return e ? atoi(e) : 256;
-  }();
+  static const int target_default = 256;
   const int target = g_w256_target > 0 ? g_w256_target : target_default;
   int splits = (target + tiles / 2) / tiles;
   const int max_splits = (M + 4 * W2_BM - 1) / (4 * W2_BM);
@@ -400,10 +397,7 @@ static int g_w256_atomic = 1;
 extern "C" void zoo_wgrad256_set_atomic(int on) { g_w256_atomic = on; }
 
 static bool w2_atomic(int splits, int N, int K) {
-  static const double mb_max = [] {
-    const char* e = getenv("ZOO_WGRAD256_ATOMIC_MB");
-    return e ? atof(e) : 32.0;
-  }();
+  static const double mb_max = 32.0;
   return g_w256_atomic && splits > 1 && (double)splits * N * K * 4 / 1e6 <= mb_max;
 }
 
@@ -430,8 +424,6 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
   const size_t smem = 4 * 2 * W2_HALF;  // 2 buffers x (A, B) x 2 halves = 128 KiB
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<true, false>),
-                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false, false>),
                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipFuncSetAttribute(reinterpret_cast<const void*>(&wgrad256_kernel<false, true>),
@@ -439,17 +431,8 @@ extern "C" hipError_t zoo_wgrad256(const void* dY, const void* X, float* dW, flo
     attr = true;
   }
   const W2Conv cv{};
-  static const bool pp = [] {
-    // measured neutral on the BERT / ResNet shapes (tools/wgrad_bench.py A/B: -3..+3 %): opt-in
-    const char* e = getenv("ZOO_W256_PINGPONG");
-    return e ? atoi(e) != 0 : false;
-  }();
-  if (pp)
-    hipLaunchKernelGGL((wgrad256_kernel<true, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
-  else
-    hipLaunchKernelGGL((wgrad256_kernel<false, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
-                       (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
+  hipLaunchKernelGGL((wgrad256_kernel<false, false>), dim3(tiles * g.splits), dim3(W2_NT), smem, st, (const bf16_t*)dY,
+                     (const bf16_t*)X, dW, part, g, w2_zero_page(), cv);
   if (g.splits > 1 && !g.atomic) {
     const size_t total = (size_t)tiles * 8 * 32 * 64;
     hipLaunchKernelGGL(wgrad256_fold_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, part, dW, g);

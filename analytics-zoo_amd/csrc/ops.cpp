@@ -225,8 +225,9 @@ bool env_flag(const char* name, bool dflt) {
   return e ? atoi(e) != 0 : dflt;
 }
 bool g_deterministic = env_flag("ZOO_DETERMINISTIC", false);
-bool g_stats_partial = env_flag("ZOO_STATS_PARTIAL", false);
-bool g_wgrad_partial = env_flag("ZOO_WGRAD_PARTIAL", false);
+// partial-row statistics / ordered weight-gradient folds: the deterministic mode's reductions
+bool g_stats_partial = false;
+bool g_wgrad_partial = false;
 bool stats_partial() { return g_deterministic || g_stats_partial; }
 bool wgrad_partial() { return g_deterministic || g_wgrad_partial; }
 
@@ -391,8 +392,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
     bs.sums = bsums->data_ptr<float>();
   }
-  static const bool epi2_unbatched = !env_flag("ZOO_EPI2_BATCH", true);
-  bs.unbatched = epi2_unbatched ? 1 : 0;
+  bs.unbatched = 0;
   // BN-backward prologue: x is a unit's masked output gradient g; the GEMM operand is that unit's
   // BN backward dy = A g + B pro_y + Cc (pw.hip forms it in registers and writes pro_dy); kernels
   // without the prologue get dy materialised first (into pro_dy when given)
@@ -442,10 +442,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   const int tiles_m = c3_grid > 0 ? c3_grid : i2_tm > 0 ? i2_tm : (g.M + 127) / 128;
   // few m-tiles (<= 512 adders per address, e.g. every 14x14 / 7x7 ResNet layer at b256):
   // the atomics go straight into the final 2K floats, no slot fold launch needed
-  static const int slot_min_tiles = [] {
-    const char* e = getenv("ZOO_STAT_SLOT_MIN_TILES");
-    return e ? atoi(e) : 512;
-  }();
+  static const int slot_min_tiles = 512;
   if (g.stat_slots == zoo::kStatSlots && tiles_m <= slot_min_tiles) g.stat_slots = 0;
   // the persistent 1x1 kernel (pw.hip) adds each workgroup's sums once (~256 adders per address):
   // straight into the final 2K floats, no slot fold
@@ -832,10 +829,7 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   TORCH_CHECK(P == g.P && Q == g.Q, "conv_wgrad: dy spatial shape does not match the geometry");
   // conv weight gradients: the wgrad256 split target of conv calls (zoo_wgrad256_target), for the
   // duration of this call
-  static const int conv_wg = [] {
-    const char* e = getenv("ZOO_WGRAD256_CONV_WG");
-    return e ? atoi(e) : 128;
-  }();
+  static const int conv_wg = 128;
   struct TargetGuard {
     explicit TargetGuard(int t) { zoo_wgrad256_target(t); }
     ~TargetGuard() { zoo_wgrad256_target(0); }
@@ -850,15 +844,9 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   // 128-row tiles win in isolation, but inside the training step -- on the side stream beside
   // the data-gradient chain -- the 256-wide kernel wins: +0.3-0.45 % images/s over five same-box
   // pairs (profiles/r5/ab_wgrad256_mmax_r5.log), so the limit is 2^20 since round 5
-  static const bool use256 = env_flag("ZOO_WGRAD256", true);
-  static const long long m_max = [] {
-    const char* e = getenv("ZOO_WGRAD256_MMAX");
-    return e ? atoll(e) : (1LL << 20);
-  }();
-  static const int c_min = [] {
-    const char* e = getenv("ZOO_WGRAD256_CMIN");
-    return e ? atoi(e) : 128;
-  }();
+  constexpr bool use256 = true;
+  static const long long m_max = (1LL << 20);
+  static const int c_min = 128;
   if (use256 && R == 1 && S == 1 && sh == 1 && sw == 1 && ph == 0 && pw == 0 && g.K >= c_min && g.C >= c_min &&
       g.M <= m_max &&
       x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
@@ -868,10 +856,7 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   // other convs with >= ZOO_WGRAD256_CONV_COUT output channels (3x3, strided 1x1): the same
   // 256x256-tile kernel with the im2col X operand gathered by its LDS-DMA (tools/wgrad_bench.py
   // --conv); narrower outputs waste most of its 256-row tile and stay on wgrad.hip
-  static const int conv256_cout = [] {
-    const char* e = getenv("ZOO_WGRAD256_CONV_COUT");
-    return e ? atoi(e) : 256;
-  }();
+  static const int conv256_cout = 256;
   if (use256 && conv256_cout > 0 && g.K >= conv256_cout && g.C % 8 == 0 && x.is_contiguous() &&
       dy.is_contiguous() && dw.stride(1) == 1 && (int64_t)g.M * g.K < (1LL << 31) &&
       (int64_t)g.N * g.H * g.W * g.C < (1LL << 40)) {
@@ -905,10 +890,7 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   // run at ~1.3 TB/s of added bytes, plain stores + the fold's reads at ~5 TB/s: the partials
   // win once the split output is larger than ~ZOO_WGRAD_PARTIAL_MB (and are always used in
   // deterministic mode)
-  static const double auto_mb = [] {
-    const char* e = getenv("ZOO_WGRAD_PARTIAL_MB");
-    return e ? atof(e) : 16.0;
-  }();
+  static const double auto_mb = 16.0;
   torch::Tensor part;
   {
     WgradGeom gp = g;

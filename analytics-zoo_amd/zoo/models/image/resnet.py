@@ -57,18 +57,18 @@ class ConvBN(nn.Module):
 # cross-unit BN-backward fusion (BNProducer); the switch exists for A/B numerics tests
 FUSE_BN_BACKWARD = True
 # projection-shortcut BatchNorm applied inside the block's last BN pass (ShortcutBN)
-FUSE_SHORTCUT_BN = os.environ.get("ZOO_FUSE_SHORTCUT_BN", "1") != "0"
+FUSE_SHORTCUT_BN = True
 # ResNet stem BatchNorm + ReLU fused into the max-pool pass (bn_relu_maxpool)
-FUSE_STEM_POOL = os.environ.get("ZOO_FUSE_STEM_POOL", "1") != "0"
+FUSE_STEM_POOL = True
 # 7x7/2 stem computed as a 4x4/1 conv on a space-to-depth(2) input (GPU)
-S2D_STEM = os.environ.get("ZOO_S2D_STEM", "1") != "0"
+S2D_STEM = True
 # projection blocks: the shortcut's dgrad runs first and hands its dx to conv1's dgrad, which then
 # also fuses the previous block's BN-backward reduction (stage transitions)
-SHORTCUT_FIRST = os.environ.get("ZOO_SHORTCUT_FIRST", "1") != "0"
+SHORTCUT_FIRST = True
 # bottlenecks: conv2's BN + ReLU applied by conv3 (1x1) in its operand prologue, conv2's apply pass
 # skipped (BNProducer.fwd_pro, pw.hip forward prologue). Off: -0.3 % with the 64- and 128-wide
 # units, +-0 with the 64-wide ones alone (profiles/r5/ab_fwd_consumer_apply_r5.md)
-FWD_PRO = os.environ.get("ZOO_FWD_PRO", "0") != "0"
+FWD_PRO = False
 
 
 def _bp():

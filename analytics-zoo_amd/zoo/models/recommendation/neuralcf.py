@@ -11,9 +11,12 @@ reduce the embedding-table gradients over the union of looked-up rows only
 
 On the GPU the whole network runs as the fused NCF kernels (zoo.ops.ncf, csrc/kernels/ncf.hip:
 one forward and one backward launch plus a small weight-gradient reduction) whenever the widths
-fit the kernel's caps (the defaults do); ``ZOO_NCF_FUSED=0`` forces the layer-by-layer graph.
+fit the kernel's caps (the defaults do); ``neuralcf._NCF_FUSED = False`` forces the layer-by-layer
+graph (comparisons).
 """
 import os
+
+_NCF_FUSED = True
 
 import torch
 
@@ -68,7 +71,7 @@ class NeuralCF(Recommender):
     # ------------------------------------------------------------------ fused GPU path
     def _fused_dims(self, x):
         parts = self.__dict__.get("_ncf_parts")
-        if parts is None or os.environ.get("ZOO_NCF_FUSED", "1") == "0":
+        if parts is None or not _NCF_FUSED:
             return None
         if not (torch.is_tensor(x) and x.is_cuda and x.dim() == 2 and x.shape[1] == 2 and x.shape[0] > 0):
             return None

@@ -61,7 +61,7 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
 # made while a hipGraph is being captured flip directly, as before.
 # ---------------------------------------------------------------------------
 _EPOCH = [0]
-_CACHE_ON = __import__("os").environ.get("ZOO_FLIP_CACHE", "1") != "0"
+_CACHE_ON = True
 _FLATS = {}             # id(FlatParams.bf16) -> weakref(FlatParams)
 
 

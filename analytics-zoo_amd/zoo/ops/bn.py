@@ -32,7 +32,7 @@ STAT_SLOTS = 16
 # How a consumer's fused BN-backward epilogue recovers this unit's ReLU mask (BwdStats.zmode,
 # csrc/kernels/bnmask.h): 1 = recompute it from y (no residual) or read a 1-bit mask written by
 # the forward apply (residual units); 0 = re-read the bf16 ReLU output z (A/B comparator).
-_BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
+_BN_MASK = True   # False: re-read the bf16 ReLU output z (test comparator)
 
 
 # BatchNorm backward of a 1x1 / stride-1 conv -> BN unit as a PROLOGUE of its own dgrad
@@ -41,13 +41,13 @@ _BN_MASK = __import__("os").environ.get("ZOO_BN_MASK", "1") != "0"
 # the unit's y, and written once for the weight gradient -- no separate BN-backward pass and no
 # re-read of dy (6 instead of 8 bytes per element). Shapes the prologue kernel does not take get
 # dy materialised inside conv_fwd. ZOO_BN_FOLD=0 keeps bn_bwd_apply (A/B: profiles/r5/ab_bn_prologue_r5.md).
-_BN_FOLD = [__import__("os").environ.get("ZOO_BN_FOLD", "1") != "0"]
+_BN_FOLD = [True]
 # unit widths taken by the prologue (ZOO_BN_FOLD_K="64,128")
 # the 1x1 stride-2 shortcut hands its data gradient to the block's conv1 in compact form
 # (GradHandoff.half), added at the even positions by conv1's dgrad epilogue (pw.hip resid_half)
-_HALF_RESID = __import__("os").environ.get("ZOO_HALF_RESID", "1") != "0"
+_HALF_RESID = True
 # forward consumer-side BN apply for units of these widths (pw.hip prologue: K <= 128)
-_FWD_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_FWD_PRO_K", "64,128").split(",") if v)
+_FWD_PRO_K = (64, 128)
 _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
 # wider units take the prologue only when their dgrad writes at most this many channels: one
 # channel group in pw.hip, so the prologue (and its y / g reads) runs once, not Cin / 64 times

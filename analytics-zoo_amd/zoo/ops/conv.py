@@ -517,8 +517,8 @@ def _use_native_linear(x, Cin, K, act):
 _ADDMM_DTYPE_OK = [True]
 # GELU backward in the consuming linear's dgrad epilogue (GeluLink); ZOO_GELU_DGRAD=0 restores the
 # separate activation-backward pass
-_GELU_DGRAD = os.environ.get("ZOO_GELU_DGRAD", "1") != "0"
-_WGRAD256 = os.environ.get("ZOO_WGRAD256", "1") != "0"
+_GELU_DGRAD = True
+_WGRAD256 = True
 
 
 def _use_wgrad256(dy, x2):

@@ -23,10 +23,6 @@ import os
 import torch
 
 _ON = os.environ.get("ZOO_WGRAD_STREAM", "1") != "0"
-# CUs the side stream is confined to (CU-masked stream); 0 = the whole device. While the engine's
-# backward runs, the persistent compute-stream kernels (pw / c3) size their grids to the others,
-# so a side-stream wgrad never holds a CU slot one of their workgroups waits for.
-_SIDE_CUS = int(os.environ.get("ZOO_SIDE_CUS", "0"))
 _side = {}        # device index -> torch.cuda.Stream
 _enabled = set()  # device indices inside an engine backward
 _used = set()     # device indices with side work not yet joined
@@ -39,21 +35,11 @@ def on():
 def _stream(idx):
     s = _side.get(idx)
     if s is None:
-        if _SIDE_CUS > 0:
-            from zoo.ops._native import native
-            with torch.cuda.device(idx):
-                h = native().cu_mask_stream(_SIDE_CUS)
-            s = torch.cuda.ExternalStream(h, device=torch.device("cuda", idx))
-        else:
-            s = torch.cuda.Stream(device=idx)
+        # the whole device: a CU-masked side stream (16-64 CUs) ran the ResNet-50 step 28-32 %
+        # slower (profiles/r5/ab_side_cus_r5.md)
+        s = torch.cuda.Stream(device=idx)
         _side[idx] = s
     return s
-
-
-def _reserve(n):
-    if _SIDE_CUS > 0:
-        from zoo.ops._native import native
-        native().set_reserved_cus(n)
 
 
 @contextlib.contextmanager
@@ -65,11 +51,9 @@ def enabled(dev):
     idx = dev.index if dev.index is not None else torch.cuda.current_device()
     _stream(idx)
     _enabled.add(idx)
-    _reserve(_SIDE_CUS)
     try:
         yield
     finally:
-        _reserve(0)
         _enabled.discard(idx)
         join(dev)
 

@@ -166,10 +166,10 @@ class GRU(_RNNBase):
 
 # whole-sequence ConvLSTM2D path (_ConvLSTMSeqFn); ZOO_CONVLSTM_SEQ=0 keeps the per-step
 # autograd loop (A/B and fallback)
-_CONVLSTM_SEQ = os.environ.get("ZOO_CONVLSTM_SEQ", "1") != "0"
+_CONVLSTM_SEQ = True
 # one launch per step (_ConvLSTMFusedFn, csrc/kernels/convlstm.hip) for up to 64 filters;
 # ZOO_CONVLSTM_FUSED=0 keeps the conv + step-kernel sequence path (A/B)
-_CONVLSTM_FUSED = os.environ.get("ZOO_CONVLSTM_FUSED", "1") != "0"
+_CONVLSTM_FUSED = True
 
 
 def _gate_perm(f, device):

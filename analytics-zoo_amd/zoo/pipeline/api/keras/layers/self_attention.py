@@ -31,13 +31,13 @@ from zoo.pipeline.api.keras.base import Layer
 # residual-gradient handoff into the linear's dgrad GEMM (GradAdd): measured neutral on
 # BERT-base b128 (same-box A/B 17.13/17.15 ms off vs 17.24/17.15 on: hipBLASLt's beta=1
 # epilogue costs what the separate add did), so opt-in
-_RESID_GRAD_FUSE = os.environ.get("ZOO_RESID_GRAD_FUSE", "0") != "0"
+_RESID_GRAD_FUSE = False
 # residual gradient summed inside the producing LayerNorm's backward kernel instead (the
 # LayerNorm that made x / n is armed; the residual dropout_add parks its gradient there)
-_LN_GRAD_ADD = os.environ.get("ZOO_LN_GRAD_ADD", "1") != "0"
+_LN_GRAD_ADD = True
 # residual dropout-add fused into the LayerNorm forward (one pass: the sum is stored for the
 # backward but never read back), ops.nn.dropout_add_layer_norm
-_DROP_LN_FUSE = os.environ.get("ZOO_DROP_LN_FUSE", "1") != "0"
+_DROP_LN_FUSE = True
 
 
 def _res_ln(a, x, p, training, gamma, beta, eps, grad_add, grad_in):

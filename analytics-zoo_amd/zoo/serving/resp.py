@@ -410,9 +410,6 @@ _LOCAL = {}   # port -> NativeStore of native servers running in this process
 
 
 def _native_runtime():
-    import os
-    if os.environ.get("ZOO_SERVING_PY", "0") == "1":
-        return None
     try:
         from zoo import _runtime
         return _runtime if hasattr(_runtime, "NativeStore") else None

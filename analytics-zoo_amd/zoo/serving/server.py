@@ -182,8 +182,6 @@ def post_process(t, flt="None"):
 
 def _bucket(n, cap):
     """Smallest power of two >= n (at least 8), capped at the configured batch size."""
-    if os.environ.get("ZOO_SERVING_BUCKETS", "1") == "0":
-        return n
     b = 8
     while b < n:
         b <<= 1
@@ -564,19 +562,7 @@ class ClusterServing:
     def run(self, running_flag=None, max_records=None, idle_timeout=None):
         """Serve until ``running_flag`` (a file path) disappears, ``max_records``
         are served, or nothing arrives for ``idle_timeout`` seconds."""
-        sw = float(os.environ.get("ZOO_SERVING_SWITCH_MS", "0"))
-        if sw > 0:
-            # the reader and the main loop hand the GIL back and forth around every native call;
-            # Python's 5 ms switch interval can hold a waiting thread for that long
-            import sys
-            sys.setswitchinterval(sw / 1000.0)
-        if os.environ.get("ZOO_SERVING_GC_FREEZE", "0") != "0":
-            # the model, graphs and buffers are long-lived: move them out of the collector's
-            # view so a full collection does not walk them in the middle of a batch
-            import gc
-            gc.collect()
-            gc.freeze()
-        if hasattr(self.db, "read_batch") and os.environ.get("ZOO_SERVING_PIPELINE", "1") != "0":
+        if hasattr(self.db, "read_batch"):
             return self._run_pipelined(running_flag, max_records, idle_timeout)
         last = time.time()
         while not self.stop_flag.is_set():

@@ -159,7 +159,7 @@ def Cband(gpu):
     from zoo.ops import native
     C = native()
     yield C
-    C.igemm2_band_set(0)  # the default since round 4 (ZOO_I2_BAND=1 turns the band tiles on)
+    C.igemm2_band_set(0)  # the default since round 4 (igemm2_band_set(1) turns the band tiles on)
     C.igemm2_set(1, 0)
 
 

@@ -29,7 +29,7 @@ def _grads(block, x, use_handoff, monkeypatch):
 def test_block_grads_with_residual_handoff(gpu, monkeypatch):
     sa = importlib.import_module("zoo.pipeline.api.keras.layers.self_attention")
     monkeypatch.setattr(importlib.import_module("zoo.ops.nn"), "_DROP_FUSE_MIN", 1)
-    monkeypatch.setattr(sa, "_RESID_GRAD_FUSE", True)   # opt-in path (ZOO_RESID_GRAD_FUSE=1)
+    monkeypatch.setattr(sa, "_RESID_GRAD_FUSE", True)   # opt-in path (self_attention._RESID_GRAD_FUSE)
     torch.manual_seed(0)
     blk = sa._Block(256, 4, 1024, 0.1, 0.1, 0.02).to(gpu).train()
     x = torch.randn(8, 128, 256, device=gpu).to(torch.bfloat16)
@@ -43,7 +43,7 @@ def test_block_grads_with_residual_handoff(gpu, monkeypatch):
 
 
 def test_stacked_blocks_with_layernorm_grad_add(gpu, monkeypatch):
-    """Default path (ZOO_LN_GRAD_ADD): each residual dropout_add parks its x-gradient in the
+    """Default path (self_attention._LN_GRAD_ADD): each residual dropout_add parks its x-gradient in the
     LayerNorm that produced x (the previous block's output LayerNorm, or the block's first one),
     whose backward kernel sums it with the incoming gradient. Two stacked blocks, so the
     holder handed from one block to the next is exercised; compared with autograd's sums."""
@@ -57,7 +57,7 @@ def test_stacked_blocks_with_layernorm_grad_add(gpu, monkeypatch):
     x = torch.randn(8, 128, 256, device=gpu).to(torch.bfloat16)
     parked = []
     nnm = importlib.import_module("zoo.ops.nn")
-    # the residual LayerNorms run as the fused dropout-add LayerNorm (ZOO_DROP_LN_FUSE) or as
+    # the residual LayerNorms run as the fused dropout-add LayerNorm (self_attention._DROP_LN_FUSE) or as
     # plain LayerNorms: count a parked gradient in either backward
     for fn in (nnm._LayerNormFn, nnm._DropAddLNFn):
         def spy(ctx, dy, orig=fn.backward):

@@ -117,8 +117,9 @@ def test_fused_trains_in_engine_like_layer_path(gpu, monkeypatch):
     x = _ids(4096, 3000, 2000).to(gpu)
     y = torch.randint(0, 5, (4096,), device=gpu)
     losses = {}
+    import zoo.models.recommendation.neuralcf as ncf_mod
     for mode in ("1", "0"):
-        monkeypatch.setenv("ZOO_NCF_FUSED", mode)
+        monkeypatch.setattr(ncf_mod, "_NCF_FUSED", mode == "1")
         m = _model(users=3000, items=2000)
         eng = TrainingEngine(m, SparseCategoricalCrossEntropy(), Adam(lr=1e-2), hip_graph=True)
         losses[mode] = [float(eng.train_step(x, y).item()) for _ in range(6)]
