@@ -48,7 +48,9 @@ _BN_FOLD = [True]
 _HALF_RESID = True
 # forward consumer-side BN apply for units of these widths (pw.hip prologue: K <= 128)
 _FWD_PRO_K = (64, 128)
-_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64").split(",") if v)
+# 256: the stage-1 conv3 units (one 64-channel group): 12,804 / 12,822 -> 13,031 / 13,015 images/s with
+# the band weight gradient (profiles/r6/ab1_r6.md)
+_PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64,256").split(",") if v)
 # wider units take the prologue only when their dgrad writes at most this many channels: one
 # channel group in pw.hip, so the prologue (and its y / g reads) runs once, not Cin / 64 times
 _PRO_NMAX = int(__import__("os").environ.get("ZOO_BN_FOLD_NMAX", "64"))
