@@ -72,6 +72,13 @@ struct BwdStats {
   // pre-BN output y; the GEMM runs on relu(coef[k] y + coef[2 Kx + k]) (pro_coef [3][Kx], the
   // middle row unused), written to pro_dy by channel group 0 -- that unit's output z
   int pro_fwd;
+  // forward prologue of a RESIDUAL unit (pw.hip EPI 4, a ResNet block output consumed by the next
+  // block's 1x1 conv1): z = relu(A y + Cc + R) with R = pro_res, or R = rA pro_res + rC when
+  // pro_rcoef ([3][Kx], a projection shortcut's BatchNorm) is set; channel group 0 also writes
+  // the 1-bit ReLU mask of z to pro_mask (BwdStats.zmode 2 layout) for the unit's BN backward
+  const void* pro_res;
+  const float* pro_rcoef;
+  void* pro_mask;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

@@ -84,7 +84,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   const int fr = lane & 15, fq = lane >> 4;
   const int N = p.N;
   float* patch = ssum + 2 * NP + w * 16 * PITCH;                   // wave-private fp32 16 x NP patch
-  float* pco = ssum + 2 * NP + PW_NW * 16 * PITCH;                 // PRO: A | B | Cc, [3][K]
+  float* pco = ssum + 2 * NP + PW_NW * 16 * PITCH;                 // PRO: A | B | Cc, [3][K] (+ EPI 4: rA | - | rC)
 
   // ---- workgroup -> (channel group, pixel group); XCD-local channel groups ----
   const int b = blockIdx.x, G = gridDim.x;
@@ -104,6 +104,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   for (int c = tid; c < 2 * NP; c += NT) ssum[c] = 0.f;
   if constexpr (PRO)
     for (int c = tid; c < 3 * K; c += NT) pco[c] = bs.pro_coef[c];
+  if constexpr (PRO && EPI == 4)
+    if (bs.pro_rcoef)
+      for (int c = tid; c < 3 * K; c += NT) pco[3 * K + c] = bs.pro_rcoef[c];
   __syncthreads();
 
   const bool bnsum = EPI == 2 && bs.sums != nullptr && !bs.zgelu;
@@ -136,7 +139,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   // (PRO: the unit's pre-BN output y at the same positions into yf)
   // PRO with EPI 1: the forward consumer-side BN apply -- one operand (X = y), no y fragments
   constexpr bool PRO_Y = PRO && EPI == 2;
-  constexpr int YJ = PRO_Y ? MJ : 1, YK = PRO_Y ? KT : 1;
+  // EPI 4: the forward prologue of a residual unit reads the residual at the operand positions
+  constexpr bool PRO_R = PRO && EPI == 4;
+  constexpr int YJ = (PRO_Y || PRO_R) ? MJ : 1, YK = (PRO_Y || PRO_R) ? KT : 1;
   const bf16_t* const pro_y = reinterpret_cast<const bf16_t*>(bs.pro_y);
   bf16_t* const pro_dy = reinterpret_cast<bf16_t*>(bs.pro_dy);
   auto load_tile = [&](int t, bf16x8 (&af)[MJ][KT], bf16x8 (&yf)[YJ][YK]) {
@@ -163,6 +168,11 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
         const bf16_t* ys = pro_y + (size_t)row * K + 8 * fq;
 #pragma unroll
         for (int kb = 0; kb < KT; ++kb) yf[j][kb] = *reinterpret_cast<const bf16x8*>(ys + kb * 32);
+      }
+      if constexpr (PRO_R) {
+        const bf16_t* rs = reinterpret_cast<const bf16_t*>(bs.pro_res) + (size_t)row * K + 8 * fq;
+#pragma unroll
+        for (int kb = 0; kb < KT; ++kb) yf[j][kb] = *reinterpret_cast<const bf16x8*>(rs + kb * 32);
       }
     }
   };
@@ -198,10 +208,64 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
       }
     }
   };
+  // PRO, EPI 4: z = relu(A y + Cc + R), R the residual (or rA r + rC with a shortcut BatchNorm); channel
+  // group 0 stores z (the block output, the next residual) and its 1-bit ReLU mask
+  auto prologue_fwd_res = [&](int t, bf16x8 (&af)[MJ][KT], const bf16x8 (&rf)[YJ][YK]) {
+    asm volatile("" ::: "memory");
+    const bool raff = bs.pro_rcoef != nullptr;
+    uint8_t* const pmask = reinterpret_cast<uint8_t*>(bs.pro_mask);
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) {
+      const int row = t * TPM + 16 * j + fr;
+      const bool st = g == 0 && pro_dy != nullptr && row < p.M;
+#pragma unroll
+      for (int kb = 0; kb < KT; ++kb) {
+        const int k0 = kb * 32 + 8 * fq;
+        float yv[8], rv[8];
+        unpack8(__builtin_bit_cast(uint4, af[j][kb]), yv);
+        unpack8(__builtin_bit_cast(uint4, rf[j][kb]), rv);
+        float o[8];
+        unsigned bits = 0;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const float4 a4 = *reinterpret_cast<const float4*>(pco + k0 + 4 * h);
+          const float4 c4 = *reinterpret_cast<const float4*>(pco + 2 * K + k0 + 4 * h);
+          float r4[4] = {rv[4 * h], rv[4 * h + 1], rv[4 * h + 2], rv[4 * h + 3]};
+          if (raff) {
+            const float4 ra = *reinterpret_cast<const float4*>(pco + 3 * K + k0 + 4 * h);
+            const float4 rc = *reinterpret_cast<const float4*>(pco + 5 * K + k0 + 4 * h);
+            r4[0] = r4[0] * ra.x + rc.x;
+            r4[1] = r4[1] * ra.y + rc.y;
+            r4[2] = r4[2] * ra.z + rc.z;
+            r4[3] = r4[3] * ra.w + rc.w;
+          }
+          const float v0 = a4.x * yv[4 * h] + c4.x + r4[0], v1 = a4.y * yv[4 * h + 1] + c4.y + r4[1];
+          const float v2 = a4.z * yv[4 * h + 2] + c4.z + r4[2], v3 = a4.w * yv[4 * h + 3] + c4.w + r4[3];
+          bits |= (v0 > 0.f ? 1u : 0u) << (4 * h);
+          bits |= (v1 > 0.f ? 1u : 0u) << (4 * h + 1);
+          bits |= (v2 > 0.f ? 1u : 0u) << (4 * h + 2);
+          bits |= (v3 > 0.f ? 1u : 0u) << (4 * h + 3);
+          o[4 * h] = fmaxf(v0, 0.f);
+          o[4 * h + 1] = fmaxf(v1, 0.f);
+          o[4 * h + 2] = fmaxf(v2, 0.f);
+          o[4 * h + 3] = fmaxf(v3, 0.f);
+        }
+        const uint4 pk = pack8(o);
+        af[j][kb] = __builtin_bit_cast(bf16x8, pk);
+        if (st) {
+          *reinterpret_cast<uint4*>(pro_dy + (size_t)row * K + k0) = pk;
+          if (pmask) pmask[((size_t)row * K + k0) >> 3] = (uint8_t)bits;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
   // PRO: dy = A g + B y + Cc in place of g (and, channel group 0, stored for the weight gradient)
   auto prologue = [&](int t, bf16x8 (&af)[MJ][KT], const bf16x8 (&yf)[YJ][YK]) {
     if constexpr (PRO && EPI == 1) {
       prologue_fwd(t, af);
+    } else if constexpr (PRO_R) {
+      prologue_fwd_res(t, af, yf);
     } else if constexpr (PRO) {
       // the coefficient reads are loop-invariant: hoisted out of the tile loop they would pin
       // 24 * KT registers for the whole kernel. The empty clobber keeps them per chunk.
@@ -408,16 +472,18 @@ static int pw_ncu() {
   return free_cus >= 8 ? free_cus : 8;
 }
 
-// group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave (+ PRO: [3][K] coefficients)
-static size_t pw_smem(int NP, int K, bool pro) {
-  return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4 + (pro ? (size_t)3 * K * 4 : 0);
+// group weights + [2][NP] sums + one fp32 16 x (NP + 4) patch per wave (+ PRO: [3][K] coefficients,
+// [6][K] with a residual's affine in EPI 4)
+static size_t pw_smem(int NP, int K, bool pro, bool res = false) {
+  return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4 +
+         (pro ? (size_t)(res ? 6 : 3) * K * 4 : 0);
 }
 
 template <int NP, int TPM, int KT, int EPI, bool PRO>
 static hipError_t pw_launch(const ConvGeom& g, const bf16_t* X, const bf16_t* W, bf16_t* Y, const bf16_t* resid,
                             float* stats, const BwdStats& bs, hipStream_t st) {
   auto kfn = &pw_kernel<NP, TPM, KT, EPI, PRO>;
-  const size_t smem = pw_smem(NP, KT * 32, PRO);
+  const size_t smem = pw_smem(NP, KT * 32, PRO, EPI == 4);
   static int per_cu = 0;
   if (per_cu == 0) {
     hipFuncSetAttribute(reinterpret_cast<const void*>(kfn), hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -506,8 +572,10 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
   if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
-  // the forward consumer-side apply: plain forward epilogue, K <= 128 (register budget as above)
-  if (bs && bs->pro_fwd && (route != 1 || g->Ktot > 128 || bs->pro_y)) return 0;
+  // the forward consumer-side apply: plain forward epilogue, K <= 128 (register budget as above);
+  // with a residual operand (EPI 4) up to K = 256 in 64-channel groups
+  if (bs && bs->pro_fwd && (route != 1 || g->Ktot > (bs->pro_res ? 256 : 128) || bs->pro_y)) return 0;
+  if (bs && bs->pro_res && (g->K % 64 != 0 || g->Ktot % 64 != 0)) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
   if (bs && bs->resid_half && (route != 2 || (g->H & 1) || (g->W & 1))) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;
@@ -537,6 +605,8 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
   const bool pro = bs.pro_y || bs.pro_fwd;
   const int NP = (pro && (g->Ktot == 128 || g->Ktot == 256) && g->K % 64 == 0) ? 64
                                                                                               : pw_np(g->K, g->Ktot);
+  if (epi == 1 && bs.pro_fwd && bs.pro_res)
+    return pw_dispatch<4, true>(*g, 64, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (epi == 1 && bs.pro_fwd)
     return pw_dispatch<1, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (epi == 1)

@@ -279,7 +279,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bsums, c10::optional<torch::Tensor> bgamma,
                        c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
                        c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy,
-                       bool resid_half, bool pro_fwd) {
+                       bool resid_half, bool pro_fwd, c10::optional<torch::Tensor> pro_rcoef,
+                       c10::optional<torch::Tensor> pro_mask) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -397,6 +398,12 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   // BN backward dy = A g + B pro_y + Cc (pw.hip forms it in registers and writes pro_dy); kernels
   // without the prologue get dy materialised first (into pro_dy when given)
   torch::Tensor xin = x;
+  // forward prologue of a residual unit: pro_y is its residual operand (pw.hip EPI 4), not a BN input
+  c10::optional<torch::Tensor> pro_res;
+  if (pro_fwd && pro_y.has_value() && pro_y->defined()) {
+    pro_res = pro_y;
+    pro_y = c10::nullopt;
+  }
   if (pro_y.has_value() && pro_y->defined()) {
     req(*pro_y, at::kBFloat16, "pro_y");
     TORCH_CHECK(pro_coef.has_value() && pro_coef->defined(), "conv_fwd: the BN-backward prologue needs pro_coef");
@@ -427,6 +434,22 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     bs.pro_fwd = 1;
     bs.pro_coef = pro_coef->data_ptr<float>();
     bs.pro_dy = pro_dy->data_ptr();
+    if (pro_res.has_value()) {
+      req(*pro_res, at::kBFloat16, "pro_res");
+      TORCH_CHECK(pro_res->numel() == x.numel(), "conv_fwd: the prologue residual must match x");
+      check_al16(pro_res->data_ptr(), "pro_res");
+      bs.pro_res = pro_res->data_ptr();
+      if (pro_rcoef.has_value() && pro_rcoef->defined()) {
+        req(*pro_rcoef, at::kFloat, "pro_rcoef");
+        TORCH_CHECK(pro_rcoef->numel() == 3 * (int64_t)C, "conv_fwd: pro_rcoef must be [3 * C]");
+        bs.pro_rcoef = pro_rcoef->data_ptr<float>();
+      }
+      if (pro_mask.has_value() && pro_mask->defined()) {
+        TORCH_CHECK(pro_mask->scalar_type() == at::kByte && pro_mask->numel() * 8 == x.numel(),
+                    "conv_fwd: pro_mask must be uint8 [x.numel() / 8]");
+        bs.pro_mask = pro_mask->data_ptr();
+      }
+    }
   }
   // partial-buffer statistics: the kernel stores per-m-tile column sums into `part`, then
   // they are folded in order into the caller's buffer (its first 2K floats)
@@ -466,6 +489,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
       bs.pro_dy = nullptr;
     }
   }
+  TORCH_CHECK(!(bs.pro_res && !zoo_pw_eligible(&g, route, &bs)),
+              "conv_fwd: the residual forward prologue runs on pw.hip only (1x1 stride-1, K <= 256)");
   if (bs.pro_fwd && !zoo_pw_eligible(&g, route, &bs)) {
     // no prologue outside pw.hip: materialise z = relu(A y + Cc) into pro_dy and convolve that
     check_hip(zoo_bnpro_apply(x.data_ptr(), x.data_ptr(), bs.pro_coef, pro_dy->data_ptr(), x.numel(), C, 1,
@@ -3217,7 +3242,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
         py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
         py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false,
-        py::arg("pro_fwd") = false);
+        py::arg("pro_fwd") = false, py::arg("pro_rcoef") = py::none(), py::arg("pro_mask") = py::none());
   m.def("bn_fwd_coef", [](torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean,
                           torch::Tensor rvar, torch::Tensor smean, torch::Tensor sinv, int64_t M, double eps,
                           double momentum) {

@@ -69,6 +69,10 @@ SHORTCUT_FIRST = True
 # skipped (BNProducer.fwd_pro, pw.hip forward prologue). Off: -0.3 % with the 64- and 128-wide
 # units, +-0 with the 64-wide ones alone (profiles/r5/ab_fwd_consumer_apply_r5.md)
 FWD_PRO = False
+# block outputs: the block's last BN + residual + ReLU applied by the NEXT block's 1x1 conv1 in its
+# operand prologue (which writes the block output and its ReLU mask); the block's apply pass over
+# the full-width tensor is skipped (zoo.ops.bn _FWD_PRO_RES_K: the 256-wide stage-1 outputs)
+FWD_PRO_RES = True
 
 
 def _bp():
@@ -91,8 +95,14 @@ class Bottleneck(nn.Module):
         self.conv3 = ConvBN(width, cout, 1, relu=True, zero_gamma=zero_init_residual)
         self.down = ConvBN(cin, cout, 1, stride=stride, relu=False) if (stride != 1 or cin != cout) else None
 
-    def forward(self, x, prod=None):
-        """``prod``: BNProducer of ``x`` (the previous block's last unit). Returns
+    def consumes_block_output_1x1(self):
+        """The block's input feeds only its own 1x1 stride-1 conv1 (identity shortcut): the previous
+        block's output apply can move into conv1's prologue."""
+        return self.down is None and self.conv1.k == 1 and self.conv1.stride == 1
+
+    def forward(self, x, prod=None, out_pro=False):
+        """``prod``: BNProducer of ``x`` (the previous block's last unit). ``out_pro``: the next
+        block's conv1 applies this block's output BN + residual + ReLU. Returns
         (out, BNProducer of out) when fusing, else out."""
         if not (self.training and _fusing(x)):
             sc = self.down(x) if self.down is not None else x
@@ -100,6 +110,8 @@ class Bottleneck(nn.Module):
         p1, p2, p3 = _bp(), _bp(), _bp()
         if p2 is not None and FWD_PRO and self.conv3.k == 1 and self.conv3.stride == 1:
             p2.fwd_pro = True
+        if p3 is not None and out_pro:
+            p3.fwd_pro = True
         if self.down is None:
             # identity shortcut: conv3's residual gradient is added in conv1's dgrad epilogue, which makes
             # conv1 the sole consumer of x -> it also fuses the previous block's BN-backward reduction
@@ -288,8 +300,13 @@ class ResNet(nn.Module):
     def _forward_stages(self, x):
         if self.training and _fusing(x):
             prod = None
-            for stage in self.stages:
-                for blk in stage:
+            blocks = [blk for stage in self.stages for blk in stage]
+            for i, blk in enumerate(blocks):
+                nxt = blocks[i + 1] if i + 1 < len(blocks) else None
+                if FWD_PRO_RES and isinstance(blk, Bottleneck) and isinstance(nxt, Bottleneck) and \
+                        nxt.consumes_block_output_1x1():
+                    x, prod = blk(x, prod, out_pro=True)
+                else:
                     x, prod = blk(x, prod)
         else:
             x = self.stages(x)

@@ -33,19 +33,24 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
     compact data gradient of a 1x1 stride-2 shortcut, :func:`conv_dgrad_s2_compact`).
     ``pro_fwd = (coef, z_out)``: ``x`` is a conv -> BN -> ReLU unit's pre-BN output y and the GEMM
     runs on that unit's z = relu(coef[c] y + coef[2C + c]), which is also written to ``z_out`` (the
-    forward consumer-side apply; ``coef`` from ``bn_fwd_coef``)."""
+    forward consumer-side apply; ``coef`` from ``bn_fwd_coef``). ``pro_fwd = (coef, z_out, resid, rcoef,
+    mask)``: the unit has a residual -- z = relu(A y + Cc + R), R = resid or rA resid + rC (rcoef, a
+    projection shortcut's BatchNorm) -- and its 1-bit ReLU mask goes to ``mask`` (pw.hip EPI 4)."""
     bz = by = bm = bi = bsum = bg = bb = None
     if bstats is not None:
         bz, by, bm, bi, bsum = bstats[:5]
         if len(bstats) > 5:
             bg, bb = bstats[5], bstats[6]
     py, pc, pd = pro if pro is not None else (None, None, None)
+    prc = pmask = None
     if pro_fwd is not None:
-        pc, pd = pro_fwd
+        pc, pd = pro_fwd[0], pro_fwd[1]
+        if len(pro_fwd) > 2:
+            py, prc, pmask = pro_fwd[2], pro_fwd[3], pro_fwd[4]
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
                              list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd, bool(resid_half),
-                             pro_fwd is not None)
+                             pro_fwd is not None, prc, pmask)
 
 
 # ---------------------------------------------------------------------------

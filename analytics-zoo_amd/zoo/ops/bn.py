@@ -48,6 +48,9 @@ _BN_FOLD = [True]
 _HALF_RESID = True
 # forward consumer-side BN apply for units of these widths (pw.hip prologue: K <= 128)
 _FWD_PRO_K = (64, 128)
+# ... and for RESIDUAL units (a ResNet block output consumed by the next block's 1x1 conv1, pw.hip EPI 4:
+# the block's BN + residual + ReLU apply pass is gone, conv1 writes the block output and its mask)
+_FWD_PRO_RES_K = (256,)
 # 256: the stage-1 conv3 units (one 64-channel group): 12,804 / 12,822 -> 13,031 / 13,015 images/s with
 # the band weight gradient (profiles/r6/ab1_r6.md)
 _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64,256").split(",") if v)
@@ -165,9 +168,10 @@ class _ConvBNActFn(torch.autograd.Function):
         stats = workspace.zeros(stat_len(K), x.device) if training else None
         pend = producer_in.pending if producer_in is not None else None
         if pend is not None:
-            # this conv applies the producer's BN + ReLU in its operand prologue and writes x (= z)
+            # this conv applies the producer's BN (+ residual) + ReLU in its operand prologue and
+            # writes x (= z, and the producer's ReLU mask for a residual unit)
             producer_in.pending = None
-            y = _kern.conv_fwd(pend[0], wb, R, S, stride, pad, stats=stats, pro_fwd=(pend[1], x))
+            y = _kern.conv_fwd(pend[0], wb, R, S, stride, pad, stats=stats, pro_fwd=(pend[1], x) + tuple(pend[2:]))
         else:
             y = _kern.conv_fwd(x, wb, R, S, stride, pad, stats=stats)
         ctx.sync = bool(training) and sync_bn_active()
@@ -196,6 +200,21 @@ class _ConvBNActFn(torch.autograd.Function):
                                   running_var, smean, sinv, y.numel() // K, eps, momentum)
             z = torch.empty_like(y)
             po.pending = (y, coef)
+        elif (po is not None and po.fwd_pro and mask is not None and not ctx.sync and K in _FWD_PRO_RES_K
+              and not _deterministic() and resid.dtype == torch.bfloat16 and resid.is_contiguous()
+              and resid.shape == y.shape and gamma.dtype == torch.float32 and beta.dtype == torch.float32
+              and (rb is None or (gamma2.dtype == torch.float32 and beta2.dtype == torch.float32))):
+            # residual unit, consumer-side: the next block's conv1 forms z = relu(A y + Cc + R) and the
+            # mask; here only the statistics bookkeeping (both BatchNorms) and the affine coefficients
+            M_ = y.numel() // K
+            coef = C_.bn_fwd_coef(stats, gamma.detach().contiguous(), beta.detach().contiguous(), running_mean,
+                                  running_var, smean, sinv, M_, eps, momentum)
+            rcoef = None
+            if rb is not None:
+                rcoef = C_.bn_fwd_coef(rb.stats, gamma2.detach().contiguous(), beta2.detach().contiguous(),
+                                       rb.running_mean, rb.running_var, rb.smean, rb.sinv, M_, eps, momentum)
+            z = torch.empty_like(y)
+            po.pending = (y, coef, resid, rcoef, mask)
         else:
             z = C_.bn_fwd_apply(y, stats if training else torch.empty(0, device=x.device), gamma.detach(),
                                 beta.detach(), resid, running_mean, running_var, smean, sinv, eps, momentum, relu,

@@ -82,3 +82,81 @@ def test_resnet50_fwd_pro_matches_apply(gpu):
     assert diff <= 3 * noise + 1e-3, (diff, noise)
     # running statistics updated the same way
     assert max(rel(b, a) for a, b in zip(bufs[0], bufs[2]) if a.norm() > 0) < 1e-2
+
+
+@pytest.mark.parametrize("shortcut_bn", [False, True])
+def test_conv_fwd_pro_residual(gpu, shortcut_bn):
+    """Residual unit, consumer side (pw.hip EPI 4): the 1x1 conv forms the block output
+    z = relu(A y + C + R), R the identity residual or a projection shortcut's BatchNorm of its raw
+    output, writes z and the 1-bit ReLU mask, and convolves z -- against fp32 PyTorch."""
+    from zoo.ops import _kern, native
+    from zoo.ops.bn import stat_len
+    N, H, W, C, K = 2, 12, 12, 256, 64
+    torch.manual_seed(7 + shortcut_bn)
+
+    def bn_coef(t, gamma, beta):
+        tf = t.float().reshape(-1, C)
+        stats = torch.zeros(max(stat_len(C), 2 * C), device=gpu)
+        stats[:C], stats[C:2 * C] = tf.sum(0), (tf * tf).sum(0)
+        rm, rv = torch.zeros(C, device=gpu), torch.ones(C, device=gpu)
+        sm, si = torch.empty(C, device=gpu), torch.empty(C, device=gpu)
+        coef = native().bn_fwd_coef(stats, gamma, beta, rm, rv, sm, si, tf.shape[0], 1e-5, 0.1)
+        mu, var = tf.mean(0), tf.var(0, unbiased=False)
+        return coef, (tf - mu) * (var + 1e-5).rsqrt() * gamma + beta
+    y = (torch.randn(N, H, W, C, device=gpu) * 1.5 + 0.3).bfloat16()
+    r = (torch.randn(N, H, W, C, device=gpu) * 0.8).bfloat16()
+    coef, yn = bn_coef(y, torch.randn(C, device=gpu) * 0.7, torch.randn(C, device=gpu) * 0.2)
+    if shortcut_bn:
+        rcoef, rn = bn_coef(r, torch.randn(C, device=gpu) * 0.5, torch.randn(C, device=gpu) * 0.1)
+    else:
+        rcoef, rn = None, r.float().reshape(-1, C)
+    pre = (yn + rn).reshape(N, H, W, C)
+    zref = F.relu(pre)
+    w = (torch.randn(K, C, device=gpu) * 0.05).bfloat16()
+    z = torch.empty_like(y)
+    mask = torch.empty(y.numel() // 8, dtype=torch.uint8, device=gpu)
+    st = torch.zeros(stat_len(K), device=gpu)
+    out = _kern.conv_fwd(y, w, 1, 1, stats=st, pro_fwd=(coef, z, r, rcoef, mask))
+    assert rel(z, zref) < 1e-2
+    bits = ((mask.view(-1, 1).int() >> torch.arange(8, device=gpu)) & 1).reshape(pre.shape)
+    agree = (bits.bool() == (pre > 0)).float().mean().item()
+    assert agree > 0.999, agree        # only exact-zero ties may differ
+    ref = (zref.reshape(-1, C) @ w.float().t()).reshape(N, H, W, K)
+    assert rel(out, ref) < 1e-2
+
+
+def test_resnet50_block_output_prologue_matches_apply(gpu):
+    """ResNet-50 training step with the stage-1 block outputs formed by the next block's conv1
+    prologue (FWD_PRO_RES) vs the separate BN + residual + ReLU apply pass: the bar is the
+    run-to-run spread of the apply path itself (atomic statistics)."""
+    import zoo.models.image.resnet as R
+    from zoo.ops import softmax_cross_entropy
+    torch.manual_seed(1)
+    m = R.resnet50(num_classes=100, zero_init_residual=False).to(gpu).train()
+    x = torch.randn(16, 3, 96, 96, device=gpu)
+    t = torch.randint(0, 100, (16,), device=gpu)
+    sd = {k: v.clone() for k, v in m.state_dict().items()}
+    grads, losses, bufs = [], [], []
+    prev = R.FWD_PRO_RES
+    try:
+        for on in (False, False, True):
+            R.FWD_PRO_RES = on
+            m.load_state_dict(sd)
+            m.zero_grad(set_to_none=True)
+            loss = softmax_cross_entropy(m(x), t)
+            loss.backward()
+            losses.append(float(loss))
+            grads.append([p.grad.detach().float().clone() for p in m.parameters()])
+            bufs.append([b.detach().float().clone() for b in m.buffers() if b.dtype.is_floating_point])
+    finally:
+        R.FWD_PRO_RES = prev
+
+    def worst(a, b):
+        return min(F.cosine_similarity(u.flatten(), v.flatten(), dim=0).item()
+                   for u, v in zip(a, b) if u.norm() > 0 and v.norm() > 0)
+    noise = 1.0 - worst(grads[0], grads[1])
+    diff = 1.0 - worst(grads[0], grads[2])
+    print("loss %s, gradient 1-cos: run-to-run %.2e, prologue vs apply %.2e" % (losses, noise, diff))
+    assert abs(losses[2] - losses[0]) <= 2 * abs(losses[1] - losses[0]) + 1e-3 * abs(losses[0])
+    assert diff <= 3 * noise + 1e-3, (diff, noise)
+    assert max(rel(b, a) for a, b in zip(bufs[0], bufs[2]) if a.norm() > 0) < 1e-2
