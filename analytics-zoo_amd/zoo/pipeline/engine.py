@@ -404,6 +404,7 @@ class TrainingEngine:
         sy = target.detach().clone()
         overlap = self.sync.overlap
         self.sync.overlap = False  # no collectives inside the capture: finish() launches them after replay
+        _kern.begin_capture()
         torch.cuda.synchronize(self.device)
         graph = torch.cuda.CUDAGraph()
         full = self.full_graph
