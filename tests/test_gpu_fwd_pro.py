@@ -159,4 +159,9 @@ def test_resnet50_block_output_prologue_matches_apply(gpu):
     print("loss %s, gradient 1-cos: run-to-run %.2e, prologue vs apply %.2e" % (losses, noise, diff))
     assert abs(losses[2] - losses[0]) <= 2 * abs(losses[1] - losses[0]) + 1e-3 * abs(losses[0])
     assert diff <= 3 * noise + 1e-3, (diff, noise)
-    assert max(rel(b, a) for a, b in zip(bufs[0], bufs[2]) if a.norm() > 0) < 1e-2
+    # running statistics: an untrained ResNet-50 amplifies the atomic-order noise of the statistics
+    # through 50 BatchNorms, so the bar is again the apply path's own run-to-run spread
+    bnoise = max(rel(b, a) for a, b in zip(bufs[0], bufs[1]) if a.norm() > 0)
+    bdiff = max(rel(b, a) for a, b in zip(bufs[0], bufs[2]) if a.norm() > 0)
+    print("running-statistics rel: run-to-run %.2e, prologue vs apply %.2e" % (bnoise, bdiff))
+    assert bdiff <= 3 * bnoise + 1e-3, (bdiff, bnoise)
