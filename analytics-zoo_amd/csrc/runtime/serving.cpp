@@ -195,6 +195,47 @@ struct Stream {
 
 typedef std::unordered_map<std::string, std::string> Hash;
 
+// Key space split over 64 hash tables. One std::unordered_map holding every result key rehashes
+// all of it when it doubles: at a few 100k keys that is a 20-100 ms stop of the whole store under
+// its lock (every XADD, read and finish waits), which was the latency tail of the open-loop
+// serving bench (profiles/r6/serving.md). With 64 shards each doubling moves 1/64 of the keys.
+template <class V>
+class ShardedMap {
+ public:
+  static constexpr int kShards = 64;
+  ShardedMap() {
+    for (auto& s : s_) s.reserve(1024);
+  }
+  V* find(const std::string& k) {
+    auto& s = shard(k);
+    auto it = s.find(k);
+    return it == s.end() ? nullptr : &it->second;
+  }
+  V& operator[](const std::string& k) { return shard(k)[k]; }
+  size_t count(const std::string& k) const { return shard(k).count(k); }
+  size_t erase(const std::string& k) { return shard(k).erase(k); }
+  size_t size() const {
+    size_t n = 0;
+    for (auto& s : s_) n += s.size();
+    return n;
+  }
+  void clear() {
+    for (auto& s : s_) s.clear();
+  }
+  template <class F>
+  void for_each(F&& f) const {
+    for (auto& s : s_)
+      for (auto& kv : s) f(kv.first, kv.second);
+  }
+
+ private:
+  std::unordered_map<std::string, V>& shard(const std::string& k) { return s_[pick(k)]; }
+  const std::unordered_map<std::string, V>& shard(const std::string& k) const { return s_[pick(k)]; }
+  // the top bits pick the shard; the table inside buckets by the value modulo its size
+  static size_t pick(const std::string& k) { return (std::hash<std::string>()(k) >> 58) & (kShards - 1); }
+  std::unordered_map<std::string, V> s_[kShards];
+};
+
 struct Record {
   std::string sid, uri, kind, payload, shape;
 };
@@ -259,13 +300,17 @@ class Store {
     track_ = on;
     done_.clear();
   }
-  // completion stamps (steady-clock ns, -1 = not finished) of `keys`, under one lock
-  void done_times(const std::vector<std::string>& keys, std::vector<long long>* out) {
-    std::lock_guard<std::mutex> g(mu_);
-    out->resize(keys.size());
-    for (size_t i = 0; i < keys.size(); ++i) {
-      auto it = done_.find(keys[i]);
-      (*out)[i] = it == done_.end() ? -1 : it->second;
+  // completion stamps (steady-clock ns, -1 = not finished) of keys[idx[j]] -> (*out)[idx[j]]; the
+  // lock is taken per 256 keys so a poll over 100k keys never holds the serving worker's finish()
+  void done_times(const std::vector<std::string>& keys, const std::vector<size_t>& idx,
+                  std::vector<long long>* out) {
+    out->resize(keys.size(), -1);
+    for (size_t j0 = 0; j0 < idx.size(); j0 += 256) {
+      std::lock_guard<std::mutex> g(mu_);
+      for (size_t j = j0; j < std::min(idx.size(), j0 + 256); ++j) {
+        const long long* d = done_.find(keys[idx[j]]);
+        (*out)[idx[j]] = d == nullptr ? -1 : *d;
+      }
     }
   }
 
@@ -511,16 +556,16 @@ class Store {
       return cmd == "HMSET" ? Reply::simple("OK") : Reply::num(added);
     }
     if (cmd == "HGET") {
-      auto it = hashes_.find(a.at(1));
-      if (it == hashes_.end()) return Reply::nil();
-      auto f = it->second.find(a.at(2));
-      return f == it->second.end() ? Reply::nil() : Reply::bulk(f->second);
+      const Hash* h = hashes_.find(a.at(1));
+      if (h == nullptr) return Reply::nil();
+      auto f = h->find(a.at(2));
+      return f == h->end() ? Reply::nil() : Reply::bulk(f->second);
     }
     if (cmd == "HGETALL") {
       Reply r = Reply::arr();
-      auto it = hashes_.find(a.at(1));
-      if (it == hashes_.end()) return r;
-      for (auto& kv : it->second) {
+      const Hash* h = hashes_.find(a.at(1));
+      if (h == nullptr) return r;
+      for (auto& kv : *h) {
         r.a.push_back(Reply::bulk(kv.first));
         r.a.push_back(Reply::bulk(kv.second));
       }
@@ -531,8 +576,9 @@ class Store {
       const std::string& pat = a.at(1);
       for (auto& kv : streams_)
         if (glob(pat.c_str(), kv.first.c_str())) r.a.push_back(Reply::bulk(kv.first));
-      for (auto& kv : hashes_)
-        if (glob(pat.c_str(), kv.first.c_str())) r.a.push_back(Reply::bulk(kv.first));
+      hashes_.for_each([&](const std::string& k, const Hash&) {
+        if (glob(pat.c_str(), k.c_str())) r.a.push_back(Reply::bulk(k));
+      });
       return r;
     }
     if (cmd == "EXISTS") {
@@ -543,10 +589,10 @@ class Store {
     if (cmd == "DEL") {
       long long c = 0;
       for (size_t i = 1; i < n; ++i) {
-        auto h = hashes_.find(a[i]);
-        if (h != hashes_.end()) {
-          for (auto& kv : h->second) used_ -= kv.first.size() + kv.second.size();
-          hashes_.erase(h);
+        const Hash* h = hashes_.find(a[i]);
+        if (h != nullptr) {
+          for (auto& kv : *h) used_ -= kv.first.size() + kv.second.size();
+          hashes_.erase(a[i]);
           ++c;
           continue;
         }
@@ -617,11 +663,11 @@ class Store {
   std::mutex mu_;
   std::condition_variable cv_;
   std::unordered_map<std::string, Stream> streams_;
-  std::unordered_map<std::string, Hash> hashes_;
+  ShardedMap<Hash> hashes_;
   size_t used_ = 0, maxmem_;
   bool stop_ = false;
   bool track_ = false;
-  std::unordered_map<std::string, long long> done_;  // result key -> finish stamp (ns)
+  ShardedMap<long long> done_;  // result key -> finish stamp (ns)
 };
 
 // ------------------------------------------------------------------ TCP front end
@@ -913,14 +959,18 @@ LoadGenStats run_loadgen(const std::shared_ptr<Store>& st, const std::string& st
   }
   for (auto& x : th) x.join();
   // wait for the tail (or the grace period)
-  std::vector<long long> done;
+  std::vector<long long> done((size_t)n, -1);
+  std::vector<size_t> left;
+  for (long long i = 0; i < n; ++i)
+    if (sent_ns[(size_t)i] >= 0) left.push_back((size_t)i);
   const long long deadline = lg_now_ns() + (long long)(grace * 1e9);
   while (true) {
-    st->done_times(keys, &done);
-    long long left = 0;
-    for (long long i = 0; i < n; ++i)
-      if (sent_ns[(size_t)i] >= 0 && done[(size_t)i] < 0) ++left;
-    if (left == 0 || lg_now_ns() > deadline) break;
+    st->done_times(keys, left, &done);   // only the keys still open
+    size_t k = 0;
+    for (size_t i : left)
+      if (done[i] < 0) left[k++] = i;
+    left.resize(k);
+    if (left.empty() || lg_now_ns() > deadline) break;
     std::this_thread::sleep_for(std::chrono::milliseconds(5));
   }
   const long long w0 = t0 + (long long)(warm * 1e9), w1 = t0 + (long long)(duration * 1e9);

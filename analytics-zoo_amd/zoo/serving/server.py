@@ -18,6 +18,7 @@ Throughput / record counts go to TensorBoard ("Serving Throughput",
 "Total Records Number", InferenceSummary.scala).
 """
 import base64
+import gc
 import io
 import logging
 import os
@@ -562,6 +563,12 @@ class ClusterServing:
     def run(self, running_flag=None, max_records=None, idle_timeout=None):
         """Serve until ``running_flag`` (a file path) disappears, ``max_records``
         are served, or nothing arrives for ``idle_timeout`` seconds."""
+        # the model, its graphs, buffers and the imported libraries are long-lived: moved out of
+        # the collector's view, a full collection walks only what serving allocates. Without it a
+        # gen-2 pass over the whole heap stalled the BERT worker 42-55 ms once per 6 s at 0.85
+        # load (rank0_gc in profiles/r6/serving_suite_*_r6.log, the p99 of that load)
+        gc.collect()
+        gc.freeze()
         if hasattr(self.db, "read_batch"):
             return self._run_pipelined(running_flag, max_records, idle_timeout)
         last = time.time()

@@ -211,3 +211,28 @@ def test_native_open_loop_load_generator(tcp):
         assert st.execute([b"EXISTS", b"result:t-0"]) == 1
     finally:
         st.stop()
+
+
+def test_native_store_growth_has_no_stop_the_world_rehash():
+    """Result keys spread over 64 hash tables (csrc/runtime/serving.cpp ShardedMap): writing 300k
+    results never stalls one finish() call for a whole-table rehash (the r6 serving tail, a 20-40
+    ms stop every time the single table doubled); the keyspace commands see every shard."""
+    import time
+    from zoo import _runtime
+    st = _runtime.NativeStore(1 << 30)
+    st.track(True)
+    worst, n, b = 0.0, 4688 * 64, 64
+    for i in range(0, n, b):
+        res = [("result:g-%d" % j, "v") for j in range(i, i + b)]
+        t = time.perf_counter()
+        st.finish("image_stream", "serving", [], res, "value")
+        worst = max(worst, time.perf_counter() - t)
+    assert st.execute([b"DBSIZE"]) == n
+    assert worst < 0.012, worst   # the single-table store: 88-99 ms worst call here
+    keys = st.execute([b"KEYS", b"result:g-29999?"])
+    assert sorted(keys) == sorted(("result:g-29999%d" % d).encode() for d in range(10))
+    assert st.execute([b"DEL", b"result:g-0", b"result:g-1", b"nope"]) == 2
+    assert st.execute([b"EXISTS", b"result:g-0", b"result:g-2"]) == 1
+    assert st.execute([b"HGET", b"result:g-2", b"value"]) == b"v"
+    st.execute([b"FLUSHALL"])
+    assert st.execute([b"DBSIZE"]) == 0
