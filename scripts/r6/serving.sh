@@ -6,7 +6,7 @@ mkdir -p gpurun_out/r6
 export TMPDIR=/tmp
 T="timeout -k 10"
 for i in 1 2 3; do
-  $T 600 python -u analytics-zoo_amd/tools/serving_bench.py suite --duration 6 --images 4096 \
+  $T 600 python -u analytics-zoo_amd/tools/serving_bench.py suite --duration 6 --images 16384 \
     --fractions 0.5,0.7,0.85,1.0,1.2 --out gpurun_out/r6/serving_suite_$i.json > gpurun_out/r6/serving_suite_$i.log 2>&1 || exit 12
   grep -h '"bench"' gpurun_out/r6/serving_suite_$i.log | python3 -c "
 import json,sys
