@@ -463,7 +463,8 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
   // (ZOO_EPI2_BATCH=0: loads at the point of use)
   // (tiles with 128 accumulator registers per lane -- 256x256 -- have no room for the
   // prefetch registers: it spilled to scratch there, so they keep the loads at their use)
-  const bool pre2 = EPI == 2 && TM * TN <= 16 && !bs.unbatched;
+  // (the 12-wave 256x192 tile runs 3 waves per SIMD: 168 VGPRs, where the prefetch spilled too)
+  const bool pre2 = EPI == 2 && TM * TN <= 16 && NW <= 8 && !bs.unbatched;
   uint4 nrv[PPL], nyv[PPL], nzv[PPL];
   unsigned nmb[PPL];
   auto slice_off = [&](int i, int h, bool& ok) -> size_t {
@@ -689,6 +690,8 @@ enum I2Tile : int {
   I2_B224x128 = 9,  // 8 waves (2x4) of 112x32, 3-stage: 2 x 38 KiB patches + 48 KiB ring, 1 / CU
   I2_B224x128w = 10,// 4 waves (2x2) of 112x64, 3-stage (A/B of the wider wave tile)
   I2_224x256 = 11,  // 8 waves (2x4) of 112x64, 2-stage: 120 KiB + junk slots, 1 / CU (wave quantization)
+  I2_256x192 = 12,  // 12 waves (4x3) of 64x64, 2-stage: 112 KiB + junk slots, 1 / CU: a 768-wide output
+                    // is 4 column tiles, so 16384 rows make 256 tiles -- one full round on 256 CUs
 };
 
 static bool i2_is_band(int tile) { return tile >= I2_B224x64 && tile <= I2_B224x128w; }
@@ -715,12 +718,14 @@ static int i2_bn(int tile) {
   switch (tile) {
     case I2_256x64: case I2_128x64: case I2_B224x64: return 64;
     case I2_256x256: case I2_224x256: return 256;
+    case I2_256x192: return 192;
     default: return 128;
   }
 }
 static int i2_nw(int tile) {
   switch (tile) {
     case I2_256x128: case I2_256x128_3: case I2_256x256: case I2_B224x128: case I2_224x256: return 8;
+    case I2_256x192: return 12;
     default: return 4;
   }
 }
@@ -806,6 +811,7 @@ static hipError_t i2_tile(int tile, int epi, const bf16_t* X, const bf16_t* W, b
       case I2_128x64: return i2_epi<2, 2, 4, 2, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       case I2_128x128_3: return i2_epi<2, 2, 4, 4, 3, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       case I2_224x256: return i2_epi<2, 4, 7, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
+      case I2_256x192: return i2_epi<4, 3, 4, 4, 2, AM>(epi, X, W, Y, Yf, bias, resid, stats, g, act, bs, st);
       default: return hipErrorInvalidValue;
     }
   }

@@ -590,11 +590,31 @@ extern "C" hipError_t zoo_wgrad(const void* X, const void* dY, float* dW, float*
   return hipGetLastError();
 }
 
+// final fold of a TRANSPOSED band partial: the 1x1 64 -> 256 convs run the band kernel with the
+// operands swapped (64-channel X in the dY role, 256-channel dY in the X role), so the partials are
+// dW^T [64][Ktot]; this sums the n partial rows in order and adds element (c, k) into dW[k][c]
+__global__ __launch_bounds__(256) void wgrad_fold_t_kernel(const float* __restrict__ part, float* __restrict__ dW,
+                                                          int Ktot, int ldw, int splits) {
+  const int n = 64 * Ktot;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int c = i / Ktot, k = i - c * Ktot;
+    float s = part[i], t = 0.f;
+    int sp = 1;
+    for (; sp + 1 < splits; sp += 2) {
+      s += part[(size_t)sp * n + i];
+      t += part[(size_t)(sp + 1) * n + i];
+    }
+    if (sp < splits) s += part[(size_t)sp * n + i];
+    dW[(size_t)k * ldw + c] += s + t;
+  }
+}
+
 // band weight gradient (wgrad_band_kernel): stride-1, K = 64 output channels, one of the shapes
 // instantiated below. Returns the number of partial rows it needs (0 = not handled); with
 // part != null it also runs the kernel and the ordered fold into dW.
 template <int R, int S, int C, int TP, int Q>
-static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, float* part, hipStream_t st) {
+static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, float* part, hipStream_t st,
+                  bool transposed = false) {
   using Cfg = WbCfg<R, S, C, TP, Q>;
   auto kfn = &wgrad_band_kernel<R, S, C, TP, Q>;
   static bool attr = false;
@@ -628,7 +648,10 @@ static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, 
     src = lvl1;
     n = groups;
   }
-  hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, src, dW, 64, Ktot, g.ldw, n);
+  if (transposed)
+    hipLaunchKernelGGL(wgrad_fold_t_kernel, dim3((64 * Ktot + 255) / 256), dim3(256), 0, st, src, dW, Ktot, g.ldw, n);
+  else
+    hipLaunchKernelGGL(wgrad_fold_kernel, dim3(blocks), dim3(256), 0, st, src, dW, 64, Ktot, g.ldw, n);
   return G;
 }
 
@@ -636,14 +659,27 @@ static int wb_run(const WgradGeom& g, const void* X, const void* dY, float* dW, 
 // null), or runs it (part != null)
 extern "C" int zoo_wgrad_band(const WgradGeom* gp, const void* X, const void* dY, float* dW, float* part,
                               hipStream_t st) {
-  static const bool on = [] {
+  // 1: every band shape; 2: only the 64-output-channel ones (A/B of the transposed 64 -> 256 case)
+  static const int on = [] {
     const char* e = getenv("ZOO_WGRAD_BAND");
-    return e ? atoi(e) != 0 : true;
+    return e ? atoi(e) : 1;
   }();
   const WgradGeom& g = *gp;
-  if (!on || g.K != 64 || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1 || g.P != g.H + 2 * g.ph - g.R + 1 ||
+  if (!on || g.sh != 1 || g.sw != 1 || g.dh != 1 || g.dw != 1 || g.P != g.H + 2 * g.ph - g.R + 1 ||
       g.Q != g.W + 2 * g.pw - g.S + 1)
     return 0;
+  if (on == 1 && g.K == 256 && g.R == 1 && g.S == 1 && g.C == 64 && g.ph == 0 && g.pw == 0 && g.Q == 56) {
+    // 1x1 64 -> 256 (stage-1 conv3 and projection shortcut): dW^T = X^T dY is the 256-channel
+    // band shape with the operands swapped; the fold writes it back transposed. wgrad256's
+    // im2col kernel took 180-580 us per call there on the side stream, the last work of the step
+    // (profiles/r6/ab4_prof_rn_step_r6.md rows 320-368)
+    WgradGeom t = g;
+    t.C = 256;
+    t.K = 64;
+    t.Ktot = 256;
+    return wb_run<1, 1, 256, 4, 56>(t, dY, X, dW, part, st, true);
+  }
+  if (g.K != 64) return 0;
   if (g.R == 4 && g.S == 4 && g.C == 16 && g.ph == 0 && g.pw == 0 && g.Q == 112)
     return wb_run<4, 4, 16, 4, 112>(g, X, dY, dW, part, st);
   if (g.R == 3 && g.S == 3 && g.C == 64 && g.ph == 1 && g.pw == 1 && g.Q == 56)

@@ -863,6 +863,21 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
   g.Ktot = R * S * g.C;
   g.ldw = dw.size(-1);
   TORCH_CHECK(dw.dim() == 2 && dw.size(0) == g.K && g.ldw >= g.Ktot, "conv_wgrad: dw must be [K, >=R*S*C]");
+  // the 64-output-channel stride-1 shapes of ResNet stage 1, the space-to-depth stem and (operands
+  // swapped) the 1x1 64 -> 256 convs of stage 1: one workgroup per CU owns all of dW and walks
+  // bands of output rows staged once in LDS
+  // (wgrad.hip wgrad_band_kernel); deterministic ordered fold of the per-workgroup partials
+  if (x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
+    const int rows = zoo_wgrad_band(&g, nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (rows > 0) {
+      check_al16(x.data_ptr(), "conv_wgrad x");
+      check_al16(dy.data_ptr(), "conv_wgrad dy");
+      auto part = torch::empty({(int64_t)rows, (int64_t)g.K * g.Ktot}, dw.options());
+      zoo_wgrad_band(&g, x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), part.data_ptr<float>(), cur_stream());
+      check_hip(hipGetLastError(), "wgrad_band");
+      return;
+    }
+  }
   // 1x1 stride-1 convs with >= 128 input and output channels (and up to 2^20 pixels) are plain
   // GEMMs where the 256x256-tile kernel (wgrad256.hip) beats the implicit-GEMM wgrad
   // (tools/wgrad_bench.py --resnet: 1.1-1.6x). At 802816 pixels (the stage-1 1x1 convs) the
@@ -895,20 +910,6 @@ void conv_wgrad(torch::Tensor x, torch::Tensor dy, torch::Tensor dw, int R, int 
                                 g.N, g.H, g.W, g.C, g.K, R, S, g.P, g.Q, sh, sw, ph, pw, dh, dil_w, g.ldw, cur_stream()),
               "wgrad256_conv");
     return;
-  }
-  // the 64-output-channel stride-1 shapes of ResNet stage 1 and the space-to-depth stem: one
-  // workgroup per CU owns all of dW and walks bands of output rows staged once in LDS
-  // (wgrad.hip wgrad_band_kernel); deterministic ordered fold of the per-workgroup partials
-  if (x.is_contiguous() && dy.is_contiguous() && dw.stride(1) == 1) {
-    const int rows = zoo_wgrad_band(&g, nullptr, nullptr, nullptr, nullptr, nullptr);
-    if (rows > 0) {
-      check_al16(x.data_ptr(), "conv_wgrad x");
-      check_al16(dy.data_ptr(), "conv_wgrad dy");
-      auto part = torch::empty({(int64_t)rows, (int64_t)g.K * g.Ktot}, dw.options());
-      zoo_wgrad_band(&g, x.data_ptr(), dy.data_ptr(), dw.data_ptr<float>(), part.data_ptr<float>(), cur_stream());
-      check_hip(hipGetLastError(), "wgrad_band");
-      return;
-    }
   }
   g.m_per_split = 0;
   // split-K reduction: fp32 atomics into dW, or per-split partials + an ordered fold. Atomics

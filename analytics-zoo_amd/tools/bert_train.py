@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--seq", type=int, default=128)
     ap.add_argument("--graph", action="store_true",
                     help="capture forward + backward + in-backward optimizer as one hipGraph per step")
+    ap.add_argument("--i2-tile", type=int, default=0,
+                    help="force one igemm2 tile for every linear (igemm2.hip I2Tile; 0 = per-shape choice)")
     a = ap.parse_args()
     from zoo.common.nncontext import init_nncontext
     from zoo.pipeline.api.keras.layers import BERT
@@ -36,6 +38,9 @@ def main():
     from zoo.pipeline.engine import TrainingEngine
     from zoo.ops import softmax_cross_entropy
     init_nncontext("bert-train")
+    if a.i2_tile:
+        from zoo.ops import native
+        native().igemm2_set(-1, a.i2_tile)
     dev = torch.device("cuda")
     bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512, intermediate_size=3072,
                 output_all_block=False)

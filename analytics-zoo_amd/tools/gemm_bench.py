@@ -38,12 +38,34 @@ def main():
     ap.add_argument("--shapes", default=None, help="comma-separated indices into SHAPES")
     ap.add_argument("--zoo-only", action="store_true")
     ap.add_argument("--bert", action="store_true", help="BERT-base b128 x L128 linear-layer shapes")
+    ap.add_argument("--tiles", default=None,
+                    help="comma-separated igemm2 tiles to force (0 = auto; igemm2.hip I2Tile): per-tile time "
+                         "and error of the plain 1x1-conv GEMM")
     a = ap.parse_args()
     shapes = SHAPES if a.shapes is None else [SHAPES[int(i)] for i in a.shapes.split(",")]
     if a.bert:  # (M, N, K) of QKV, attention output, FFN1, FFN2 at 16384 tokens
         shapes = [(16384, 2304, 768), (16384, 768, 768), (16384, 3072, 768), (16384, 768, 3072),
                   (4096, 2304, 768), (4096, 768, 3072)]
     dev = torch.device("cuda:0")
+    if a.tiles:
+        for M, N, K in shapes:
+            x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+            w = (torch.rand(N, K, device=dev) * 2 - 1).bfloat16()
+            x4 = x.view(1, M, 1, K)
+            ref = x.float() @ w.float().t()
+            rec = {"M": M, "N": N, "K": K}
+            for t in [int(v) for v in a.tiles.split(",")]:
+                C.igemm2_set(-1, t)
+                fn = lambda: C.conv_fwd(x4, w, 1, 1, 1, 1, 0, 0, 1, 1, 1, 1, None, None, None, 0, False, True, 0, 0,
+                                        None, [], None, None, None, None, None)
+                y = fn().view(M, N).float()
+                rec["t%d_err" % t] = round(float((y - ref).abs().max() / ref.abs().max()), 5)
+                tt = timeit(fn, 50)
+                rec["t%d_us" % t] = round(tt * 1e6, 1)
+                rec["t%d_TF" % t] = round(2.0 * M * N * K / tt / 1e12, 1)
+            C.igemm2_set(-1, 0)
+            print(json.dumps(rec), flush=True)
+        return
     rows = []
     for M, N, K in shapes:
         x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()

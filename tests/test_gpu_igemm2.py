@@ -18,7 +18,7 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-TILES = [1, 2, 3, 4, 5, 6, 7, 11]   # 11: 224x256 (ragged A staging through junk slots)
+TILES = [1, 2, 3, 4, 5, 6, 7, 11, 12]   # 11: 224x256 (ragged A staging through junk slots); 12: 12-wave 256x192
 
 
 def rel(a, b):

@@ -929,12 +929,14 @@ def test_conv_wgrad_implicit_256(gpu, shape):
 
 
 WGRAD_BAND_SHAPES = [
-    # N, H, W, Cin, R, pad -- Cout 64, stride 1: the band weight gradient (wgrad.hip wgrad_band_kernel)
-    (2, 56, 56, 64, 3, 1),       # ResNet stage-1 3x3 (grid smaller than the CU count)
-    (32, 56, 56, 64, 3, 1),      # several bands per workgroup + the two-level ordered fold
-    (3, 56, 56, 64, 1, 0),       # stage-1 block-1 conv1
-    (2, 56, 56, 256, 1, 0),      # stage-1 conv1 of blocks 2-3
-    (2, 115, 115, 16, 4, 0),     # space-to-depth stem (4x4 on 16 channels)
+    # N, H, W, Cin, R, pad, Cout -- stride 1: the band weight gradient (wgrad.hip wgrad_band_kernel)
+    (2, 56, 56, 64, 3, 1, 64),       # ResNet stage-1 3x3 (grid smaller than the CU count)
+    (32, 56, 56, 64, 3, 1, 64),      # several bands per workgroup + the two-level ordered fold
+    (3, 56, 56, 64, 1, 0, 64),       # stage-1 block-1 conv1
+    (2, 56, 56, 256, 1, 0, 64),      # stage-1 conv1 of blocks 2-3
+    (2, 115, 115, 16, 4, 0, 64),     # space-to-depth stem (4x4 on 16 channels)
+    (3, 56, 56, 64, 1, 0, 256),      # stage-1 conv3 / shortcut 64 -> 256: operands swapped, transposed fold
+    (32, 56, 56, 64, 1, 0, 256),     # the same with the two-level fold
 ]
 
 
@@ -945,8 +947,7 @@ def test_conv_wgrad_band(gpu, shape):
     from torch.profiler import ProfilerActivity, profile
     from zoo.ops import native
     C = native()
-    N, H, W, Cin, R, pad = shape
-    Cout = 64
+    N, H, W, Cin, R, pad, Cout = shape
     torch.manual_seed(12)
     x = torch.randn(N, H, W, Cin, device=gpu).bfloat16()
     xr = x.float().permute(0, 3, 1, 2)
