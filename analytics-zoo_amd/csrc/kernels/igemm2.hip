@@ -702,6 +702,9 @@ static int g_i2_tile = 0;  // 0 auto, else I2Tile
 // band tiles off since the two-stream backward: ResNet-50 b256 12,273 / 12,267 img/s off vs
 // 12,239 / 12,205 on, same box (scripts/r4/knobs.sh); kept for the stride-1 band tests
 static int g_i2_band = 0;
+// 256x192 tiles for outputs that are a multiple of 192 wide: 0 off, 1 forward-type epilogues,
+// 2 also the backward epilogues (BN / GELU backward)
+static int g_i2_w192 = 1;
 
 static int i2_mode() { return g_i2_mode; }
 static int i2_tile_force() { return g_i2_tile; }
@@ -869,21 +872,28 @@ static int i2_choose(const ConvGeom& g, int epi) {
     // round-equivalents (BERT / ResNet stage 3-4: 196 tiles of 256 rows fill 77 % of the CUs,
     // 224 tiles of 224 rows 88 %; BERT linears 16384x{2304,768}x768 and x768x3072 -5..-7 %, ResNet-50
     // fwd/dgrad conv sweep -1..-2 %, profiles/r4/ab/q224_*). ZOO_I2_Q224=0: always 256x256.
-    static const bool q224 = true;
-    if (q224 && epi != 4) {
-      static int ncu = 0;
-      if (!ncu) {
-        int dev = 0;
-        hipGetDevice(&dev);
-        hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (ncu <= 0) ncu = 256;
-      }
-      const long t256 = tiles(I2_256x256), t224 = tiles(I2_224x256);
-      const double c256 = (double)((t256 + ncu - 1) / ncu);
-      const double c224 = (double)((t224 + ncu - 1) / ncu) * (224.0 / 256.0);
-      if (c224 < 0.97 * c256) return I2_224x256;
+    // 192-wide tiles (12 waves) cost 3/4 of a round and split 768- and 2304-wide outputs exactly:
+    // BERT's 16384 x 768 x {768, 3072} and 16384 x 2304 x 768 linears 65.6-65.7 us vs 70.9-76.9 us
+    // (tools/gemm_bench.py --bert --tiles, profiles/r6/ab5_gemm_tiles_r6.log)
+    static int ncu = 0;
+    if (!ncu) {
+      int dev = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
+      if (ncu <= 0) ncu = 256;
     }
-    return I2_256x256;
+    auto rounds = [&](int t) { return (double)((tiles(t) + ncu - 1) / ncu) * (i2_bm(t) * i2_bn(t)) / (256.0 * 256.0); };
+    int best = I2_256x256;
+    double cbest = rounds(I2_256x256);
+    static const bool q224 = true;
+    if (q224 && epi != 4 && rounds(I2_224x256) < 0.97 * cbest) {
+      best = I2_224x256;
+      cbest = rounds(I2_224x256);
+    }
+    const int w192 = g_i2_w192;
+    if (w192 > 0 && g.K % 192 == 0 && (w192 > 1 || (epi != 2 && epi != 4)) && rounds(I2_256x192) < 0.97 * cbest)
+      best = I2_256x192;
+    return best;
   }
   return I2_128x128;
 }
@@ -915,6 +925,10 @@ extern "C" int zoo_igemm2_tiles_m(const ConvGeom* g, int epi) {
 extern "C" void zoo_igemm2_set(int mode, int tile) {
   if (mode >= 0) g_i2_mode = mode;
   if (tile >= 0) g_i2_tile = tile;
+}
+
+extern "C" void zoo_igemm2_w192_set(int mode) {
+  if (mode >= 0) g_i2_w192 = mode;
 }
 
 // band tiles on / off (-1: leave)

@@ -31,6 +31,8 @@ def main():
                     help="capture forward + backward + in-backward optimizer as one hipGraph per step")
     ap.add_argument("--i2-tile", type=int, default=0,
                     help="force one igemm2 tile for every linear (igemm2.hip I2Tile; 0 = per-shape choice)")
+    ap.add_argument("--i2-192", type=int, default=-1,
+                    help="256x192 igemm2 tiles: 0 off, 1 forward-type epilogues, 2 all (-1: default)")
     a = ap.parse_args()
     from zoo.common.nncontext import init_nncontext
     from zoo.pipeline.api.keras.layers import BERT
@@ -38,9 +40,10 @@ def main():
     from zoo.pipeline.engine import TrainingEngine
     from zoo.ops import softmax_cross_entropy
     init_nncontext("bert-train")
-    if a.i2_tile:
+    if a.i2_tile or a.i2_192 >= 0:
         from zoo.ops import native
         native().igemm2_set(-1, a.i2_tile)
+        native().igemm2_w192_set(a.i2_192)
     dev = torch.device("cuda")
     bert = BERT(vocab=30522, hidden_size=768, n_block=12, n_head=12, max_position_len=512, intermediate_size=3072,
                 output_all_block=False)

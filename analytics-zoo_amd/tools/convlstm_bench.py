@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--filters", type=int, default=32)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--dims", type=int, default=2, choices=[2, 3])
+    ap.add_argument("--modes", default=None, help="comma-separated subset of loop,seq,fused (profiling)")
     a = ap.parse_args()
     from zoo.pipeline.api.keras.layers import recurrent as R
     torch.manual_seed(0)
@@ -40,7 +41,10 @@ def main():
     outs = {}
     names = {0: "loop", 1: "seq", 2: "fused"}
     # ConvLSTM3D has no separate whole-sequence mode: SEQ without FUSED is its per-step loop
-    for mode in ((0, 1, 2) if a.dims == 2 else (0, 2)):
+    modes = (0, 1, 2) if a.dims == 2 else (0, 2)
+    if a.modes:
+        modes = [m for m in modes if names[m] in a.modes.split(",")]
+    for mode in modes:
         R._CONVLSTM_SEQ = mode > 0
         R._CONVLSTM_FUSED = mode == 2
 
@@ -61,10 +65,14 @@ def main():
         ms = (time.perf_counter() - t0) / a.iters * 1e3
         res["ms_%s" % names[mode]] = round(ms, 3)
         outs[mode] = (y.detach().float(), x.grad.detach().clone(), layer.Wh.grad.detach().clone())
+    if "ms_loop" not in res:
+        print(json.dumps(res), flush=True)
+        return
     if "ms_seq" in res:
         res["speedup_seq"] = round(res["ms_loop"] / res["ms_seq"], 2)
-    res["speedup"] = round(res["ms_loop"] / res["ms_fused"], 2)
-    for mode in [m for m in (1, 2) if m in outs]:
+    if "ms_fused" in res:
+        res["speedup"] = round(res["ms_loop"] / res["ms_fused"], 2)
+    for mode in [m for m in (1, 2) if m in outs and 0 in outs]:
         for k, n in enumerate(("y", "dx", "dWh")):
             a0, a1 = outs[0][k], outs[mode][k]
             res["rel_%s_%s" % (names[mode], n)] = round(float((a0 - a1).abs().max() /
