@@ -703,8 +703,12 @@ static int g_i2_tile = 0;  // 0 auto, else I2Tile
 // 12,239 / 12,205 on, same box (scripts/r4/knobs.sh); kept for the stride-1 band tests
 static int g_i2_band = 0;
 // 256x192 tiles for outputs that are a multiple of 192 wide: 0 off, 1 forward-type epilogues,
-// 2 also the backward epilogues (BN / GELU backward)
-static int g_i2_w192 = 1;
+// 2 also the backward epilogues (BN / GELU backward). Off by default: faster alone (BERT linears
+// 63.5 / 23.9 / 67.7 us vs 70.9 / 26.1 / 74.1 us) but the BERT training step loses 1.2 % with them
+// (15.58 ms off vs 15.76 mode 1 / 15.73 mode 2, profiles/r6/ab6_bert_*_r6.log): 256 tiles take
+// every CU, so the side-stream weight gradients beside the data-gradient chain find no free CU,
+// where the 224-row tiles leave 34 of them (setter zoo_igemm2_w192_set for serial / inference use)
+static int g_i2_w192 = 0;
 
 static int i2_mode() { return g_i2_mode; }
 static int i2_tile_force() { return g_i2_tile; }

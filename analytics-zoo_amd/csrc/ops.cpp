@@ -3318,7 +3318,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("igemm2_w192_set", [](int mode) { zoo_igemm2_w192_set(mode); },
-        "256x192 igemm2 tiles: 0 off, 1 forward-type epilogues (default), 2 also backward epilogues");
+        "256x192 igemm2 tiles: 0 off (default), 1 forward-type epilogues, 2 also backward epilogues");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
         "igemm2 A/B switch: mode 0 off / 1 on (-1 keep), tile 0 auto / I2Tile id (-1 keep)");
   m.def("c3_grid_for", [](int N, int H, int W) {

@@ -3,6 +3,7 @@
 critical-path attribution over the streams.
 
 Usage: prof_step.py <run_results.db> [marker_regex] [step_index_from_end] [--critical]
+       prof_step.py <run_results.db> --totals     (whole run: kernel time per kernel, top 30)
 
 The step boundary is the dispatch matching ``marker_regex`` (default: the first kernel of a
 step, ``nchw_to_s2d_kernel`` for the ResNet bench / ``embedding_fwd_kernel`` for BERT; with the
@@ -99,6 +100,18 @@ def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     critical = "--critical" in sys.argv
     db = args[0]
+    if "--totals" in sys.argv:
+        agg = defaultdict(lambda: [0.0, 0])
+        for r in load_rows(db):
+            k = re.sub(r"^void ", "", r["name"].split("(")[0])[:110]
+            agg[k][0] += r["dur"]
+            agg[k][1] += 1
+        total = sum(v[0] for v in agg.values())
+        print("| kernel | ms | calls | share |\n|---|---|---|---|")
+        for k, (d, n) in sorted(agg.items(), key=lambda kv: -kv[1][0])[:30]:
+            print("| `%s` | %.3f | %d | %.1f%% |" % (k, d / 1e6, n, 100.0 * d / max(total, 1)))
+        print("\ntotal kernel time %.3f ms over %d dispatches" % (total / 1e6, sum(v[1] for v in agg.values())))
+        return
     marker = re.compile(args[1] if len(args) > 1 else r"nchw_to_s2d_kernel|embedding_fwd_kernel")
     back = int(args[2]) if len(args) > 2 else 1
     rows = load_rows(db)
