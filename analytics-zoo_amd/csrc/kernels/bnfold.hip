@@ -93,9 +93,43 @@ __global__ __launch_bounds__(256) void bnpro_apply_any_kernel(const bf16_t* __re
   }
 }
 
+// the residual unit's apply where the consumer cannot take the EPI 4 prologue (pw.hip):
+// z = relu(A y + Cc + R), R = r or rA r + rC (rcoef = rA | - | rC of a projection shortcut's
+// BatchNorm), and the unit's 1-bit ReLU mask (bit e of byte i = element 8 i + e > 0)
+__global__ __launch_bounds__(256) void bnres_apply_kernel(const bf16_t* __restrict__ y, const float* __restrict__ coef,
+                                                          const bf16_t* __restrict__ r, const float* __restrict__ rcoef,
+                                                          bf16_t* __restrict__ z, uint8_t* __restrict__ mask, size_t n8,
+                                                          int K) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n8; i += (size_t)gridDim.x * blockDim.x) {
+    const int k0 = (int)((i * 8) % K);
+    float yv[8], rv[8], o[8];
+    unpack8(*reinterpret_cast<const uint4*>(y + i * 8), yv);
+    unpack8(*reinterpret_cast<const uint4*>(r + i * 8), rv);
+    unsigned bits = 0;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float res = rcoef ? rcoef[k0 + e] * rv[e] + rcoef[2 * K + k0 + e] : rv[e];
+      const float v = coef[k0 + e] * yv[e] + coef[2 * K + k0 + e] + res;
+      bits |= (v > 0.f ? 1u : 0u) << e;
+      o[e] = fmaxf(v, 0.f);
+    }
+    *reinterpret_cast<uint4*>(z + i * 8) = pack8(o);
+    if (mask) mask[i] = (uint8_t)bits;
+  }
+}
+
 }  // namespace zoo
 
 using namespace zoo;
+
+extern "C" hipError_t zoo_bnres_apply(const void* y, const float* coef, const void* r, const float* rcoef, void* z,
+                                      void* mask, size_t n, int K, hipStream_t st) {
+  const size_t n8 = n / 8;
+  const int blocks = (int)((n8 + 255) / 256 < 4096 ? (n8 + 255) / 256 : 4096);
+  hipLaunchKernelGGL(bnres_apply_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, st, (const bf16_t*)y, coef,
+                     (const bf16_t*)r, rcoef, (bf16_t*)z, (uint8_t*)mask, n8, K);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t zoo_bnfold_coef(int K, const float* gamma, const float* mean, const float* inv,
                                       const float* sums, long long M, float* coef, float* dgamma, float* dbeta,

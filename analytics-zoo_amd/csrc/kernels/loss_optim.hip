@@ -303,13 +303,15 @@ __global__ __launch_bounds__(256) void nchw_to_nhwc_kernel(const float* __restri
 __global__ __launch_bounds__(256) void nchw_to_s2d_kernel(const float* __restrict__ X, bf16_t* __restrict__ Y,
                                                           int N, int C, int H, int W, int Cp, int pad, int Hs,
                                                           int Ws) {
-  const size_t total = (size_t)N * Hs * Ws * 2;
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+  // 32-bit index math (the launcher checks total < 2^31): the 64-bit div / mod of a size_t index
+  // are emulated in dozens of instructions each and made this pass ~2.5x its bytes' time
+  const unsigned total = (unsigned)N * Hs * Ws * 2;
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int dy = (int)(i & 1);
-    size_t t = i >> 1;
-    const int j = (int)(t % Ws); t /= Ws;
-    const int ii = (int)(t % Hs);
-    const int n = (int)(t / Hs);
+    unsigned t = i >> 1;
+    const int j = (int)(t % (unsigned)Ws); t /= (unsigned)Ws;
+    const int ii = (int)(t % (unsigned)Hs);
+    const int n = (int)(t / (unsigned)Hs);
     const int h = 2 * ii + dy - pad;
     float v[8];
 #pragma unroll
@@ -331,14 +333,14 @@ __global__ __launch_bounds__(256) void nchw_to_s2d_kernel(const float* __restric
 __global__ __launch_bounds__(256) void nhwc_u8_to_s2d_kernel(const uint8_t* __restrict__ X, bf16_t* __restrict__ Y,
                                                              int N, int C, int H, int W, int pad, int Hs, int Ws,
                                                              float4 scale, float4 shift) {
-  const size_t total = (size_t)N * Hs * Ws * 2;
+  const unsigned total = (unsigned)N * Hs * Ws * 2;   // 32-bit index math, as nchw_to_s2d_kernel
   const float sc[4] = {scale.x, scale.y, scale.z, scale.w}, sh[4] = {shift.x, shift.y, shift.z, shift.w};
-  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+  for (unsigned i = blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gridDim.x * blockDim.x) {
     const int dy = (int)(i & 1);
-    size_t t = i >> 1;
-    const int j = (int)(t % Ws); t /= Ws;
-    const int ii = (int)(t % Hs);
-    const int n = (int)(t / Hs);
+    unsigned t = i >> 1;
+    const int j = (int)(t % (unsigned)Ws); t /= (unsigned)Ws;
+    const int ii = (int)(t % (unsigned)Hs);
+    const int n = (int)(t / (unsigned)Hs);
     const int h = 2 * ii + dy - pad;
     float v[8];
 #pragma unroll
@@ -494,6 +496,7 @@ extern "C" hipError_t zoo_nchw_to_nhwc(const float* X, void* Y, int N, int C, in
 
 extern "C" hipError_t zoo_nchw_to_s2d(const float* X, void* Y, int N, int C, int H, int W, int pad, int Hs, int Ws,
                                        hipStream_t st) {
+  if ((size_t)N * Hs * Ws * 2 >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit kernel index
   hipLaunchKernelGGL(nchw_to_s2d_kernel, dim3(egrid((size_t)N * Hs * Ws * 2)), dim3(256), 0, st, X, (bf16_t*)Y, N, C,
                      H, W, 4, pad, Hs, Ws);
   return hipGetLastError();
@@ -501,6 +504,7 @@ extern "C" hipError_t zoo_nchw_to_s2d(const float* X, void* Y, int N, int C, int
 
 extern "C" hipError_t zoo_nhwc_u8_to_s2d(const void* X, void* Y, int N, int C, int H, int W, int pad, int Hs, int Ws,
                                           const float* scale, const float* shift, hipStream_t st) {
+  if ((size_t)N * Hs * Ws * 2 >= (1ull << 31)) return hipErrorInvalidValue;   // 32-bit kernel index
   const float4 sc{scale[0], scale[1], scale[2], scale[3]}, sf{shift[0], shift[1], shift[2], shift[3]};
   hipLaunchKernelGGL(nhwc_u8_to_s2d_kernel, dim3(egrid((size_t)N * Hs * Ws * 2)), dim3(256), 0, st,
                      (const uint8_t*)X, (bf16_t*)Y, N, C, H, W, pad, Hs, Ws, sc, sf);

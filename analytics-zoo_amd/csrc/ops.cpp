@@ -137,6 +137,7 @@ hipError_t zoo_dropout_add(const void*, const void*, void*, size_t, float, uint6
 hipError_t zoo_nchw_to_s2d(const float*, void*, int, int, int, int, int, int, int, hipStream_t);
 hipError_t zoo_nhwc_u8_to_s2d(const void*, void*, int, int, int, int, int, int, int, const float*, const float*,
                               hipStream_t);
+hipError_t zoo_bnres_apply(const void*, const float*, const void*, const float*, void*, void*, size_t, int, hipStream_t);
 hipError_t zoo_bnfold_coef(int, const float*, const float*, const float*, const float*, long long, float*, float*,
                            float*, hipStream_t);
 hipError_t zoo_bnpro_apply(const void*, const void*, const float*, void*, size_t, int, int, hipStream_t);
@@ -490,8 +491,20 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
       bs.pro_dy = nullptr;
     }
   }
-  TORCH_CHECK(!(bs.pro_res && !zoo_pw_eligible(&g, route, &bs)),
-              "conv_fwd: the residual forward prologue runs on pw.hip only (1x1 stride-1, K <= 256)");
+  if (bs.pro_res && !zoo_pw_eligible(&g, route, &bs)) {
+    // the EPI 4 prologue runs only in pw.hip (e.g. not with deterministic partial statistics or
+    // a shape pw does not take): materialise z and the unit's mask, then convolve z
+    check_hip(zoo_bnres_apply(x.data_ptr(), bs.pro_coef, bs.pro_res, bs.pro_rcoef, pro_dy->data_ptr(), bs.pro_mask,
+                              x.numel(), C, cur_stream()),
+              "bnres_apply");
+    xin = *pro_dy;
+    bs.pro_fwd = 0;
+    bs.pro_coef = nullptr;
+    bs.pro_dy = nullptr;
+    bs.pro_res = nullptr;
+    bs.pro_rcoef = nullptr;
+    bs.pro_mask = nullptr;
+  }
   if (bs.pro_fwd && !zoo_pw_eligible(&g, route, &bs)) {
     // no prologue outside pw.hip: materialise z = relu(A y + Cc) into pro_dy and convolve that
     check_hip(zoo_bnpro_apply(x.data_ptr(), x.data_ptr(), bs.pro_coef, pro_dy->data_ptr(), x.numel(), C, 1,

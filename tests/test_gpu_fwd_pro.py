@@ -85,13 +85,15 @@ def test_resnet50_fwd_pro_matches_apply(gpu):
 
 
 @pytest.mark.parametrize("shortcut_bn", [False, True])
-def test_conv_fwd_pro_residual(gpu, shortcut_bn):
+@pytest.mark.parametrize("K", [64, 48])
+def test_conv_fwd_pro_residual(gpu, shortcut_bn, K):
     """Residual unit, consumer side (pw.hip EPI 4): the 1x1 conv forms the block output
     z = relu(A y + C + R), R the identity residual or a projection shortcut's BatchNorm of its raw
-    output, writes z and the 1-bit ReLU mask, and convolves z -- against fp32 PyTorch."""
+    output, writes z and the 1-bit ReLU mask, and convolves z -- against fp32 PyTorch. K = 48 is a
+    consumer pw.hip does not take: z and the mask come from the bnres_apply fallback pass."""
     from zoo.ops import _kern, native
     from zoo.ops.bn import stat_len
-    N, H, W, C, K = 2, 12, 12, 256, 64
+    N, H, W, C = 2, 12, 12, 256
     torch.manual_seed(7 + shortcut_bn)
 
     def bn_coef(t, gamma, beta):

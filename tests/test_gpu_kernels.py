@@ -1014,3 +1014,34 @@ def test_grouped_conv_kernels_vs_fp32(gpu, shape):
     assert rel(dw[:, :R * R * Cg], wr.grad.permute(0, 2, 3, 1).reshape(K, -1)) < 1e-3
     if ld > R * R * Cg:
         assert dw[:, R * R * Cg:].abs().max().item() == 0.0
+
+
+def _s2d_ref(xn, pad):
+    """NCHW fp32 -> zero-padded space-to-depth(2) NHWC: channel (dy*2+dx)*4 + c (c < 4, zero-filled)."""
+    N, C, H, W = xn.shape
+    Hs, Ws = (H + 2 * pad + 1) // 2, (W + 2 * pad + 1) // 2
+    xp = torch.zeros(N, 4, 2 * Hs, 2 * Ws, device=xn.device)
+    xp[:, :C, pad:pad + H, pad:pad + W] = xn
+    y = xp.view(N, 4, Hs, 2, Ws, 2).permute(0, 2, 4, 3, 5, 1)   # n, i, j, dy, dx, c
+    return y.reshape(N, Hs, Ws, 16)
+
+
+@pytest.mark.parametrize("shape", [(3, 3, 224, 224), (2, 3, 37, 50), (1, 2, 9, 8)])
+def test_s2d_input_passes_match_reference(gpu, shape):
+    """nchw_to_s2d (fp32 NCHW) and nhwc_u8_to_s2d (uint8 NHWC, normalisation fused) against the
+    plain-torch space-to-depth of the padded image (32-bit index math in both kernels)."""
+    from zoo import ops
+    N, C, H, W = shape
+    torch.manual_seed(3)
+    x = torch.randn(N, C, H, W, device=gpu)
+    y = ops.native().nchw_to_s2d(x.contiguous(), 3)
+    ref = _s2d_ref(x, 3)
+    assert y.shape == ref.shape
+    assert (y.float() - ref).abs().max().item() <= 1e-2 * ref.abs().max().item()
+    u8 = torch.randint(0, 256, (N, H, W, C), device=gpu, dtype=torch.uint8)
+    sc, sh = [0.017, 0.018, 0.0175, 1.0][:C], [-2.1, -2.0, -1.8, 0.0][:C]
+    yu = ops.native().nhwc_u8_to_s2d(u8.contiguous(), 3, sc, sh)
+    xn = (u8.float() * torch.tensor(sc, device=gpu) + torch.tensor(sh, device=gpu)).permute(0, 3, 1, 2)
+    refu = _s2d_ref(xn, 3)
+    assert yu.shape == refu.shape
+    assert (yu.float() - refu).abs().max().item() <= 1e-2 * refu.abs().max().item()
