@@ -59,16 +59,30 @@ constexpr int CL_PF = 4;      // activation chunks in flight per wave
 ZOO_DEV int cl_kcp(int KD) { return ((KD + 31) / 32 + CL_PF - 1) / CL_PF * CL_PF; }
 ZOO_DEV int cl_kdp(int KD) { return cl_kcp(KD) * 32 + 8; }   // LDS row pitch (+16 B: conflict-free)
 
-// acc[i] (rows 16 i .. 16 i + 15, this lane's pixel m) = W[rows] . X_patch(m)
-// LDSW: the workgroup's weights staged once in LDS (rows padded to cl_kdp); else read from L2
-template <int NI, bool LDSW>
-ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane, const bf16_t* wl) {
+// acc[j][i] (rows 16 i .. 16 i + 15, this lane's pixel m0 + 16 j) = W[rows] . X_patch(m0 + 16 j)
+// LDSW: the workgroup's weights staged once in LDS (rows padded to cl_kdp); else read from L2.
+// MJ pixel blocks per wave share every weight fragment: at large M (a 32^3 ConvLSTM3D volume,
+// 262k pixels per step) the kernel is bound by the L2 reads of weights the wave re-reads per
+// 32-deep chunk (221 KiB per 16 pixels); MJ = 2 halves them per MFMA
+template <int NI, int MJ, bool LDSW>
+ZOO_DEV void cl_gemm(const CLArgs& a, int m0, f32x4 (&acc)[MJ][NI], int lane, const bf16_t* wl) {
 #pragma unroll
-  for (int i = 0; i < NI; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < MJ; ++j)
+#pragma unroll
+    for (int i = 0; i < NI; ++i) acc[j][i] = f32x4{0.f, 0.f, 0.f, 0.f};
   if (!a.X) return;
-  const bool mok = m < a.M;
-  const int mm = mok ? m : 0;
-  const int x = mm % a.Wd, y = (mm / a.Wd) % a.H, z = (mm / (a.Wd * a.H)) % a.D, b = mm / (a.Wd * a.H * a.D);
+  bool mok[MJ];
+  int px[MJ], py[MJ], pz[MJ], pb[MJ];
+#pragma unroll
+  for (int j = 0; j < MJ; ++j) {
+    const int m = m0 + 16 * j;
+    mok[j] = m < a.M;
+    const int mm = mok[j] ? m : 0;
+    px[j] = mm % a.Wd;
+    py[j] = (mm / a.Wd) % a.H;
+    pz[j] = (mm / (a.Wd * a.H)) % a.D;
+    pb[j] = mm / (a.Wd * a.H * a.D);
+  }
   const int KD = a.Q * a.R * a.S * a.Cx, KC = (KD + 31) / 32, kdp = cl_kdp(KD);
   const int pq = a.Q / 2, ph = a.R / 2, pw = a.S / 2;
   const int kq = 8 * (lane >> 4), nr = lane & 15;
@@ -78,22 +92,24 @@ ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane, const b
   // branch-free: every lane loads from an in-bounds address (clamped) and zeroes the value when
   // the tap is outside the image / reduction -- a predicated load in a divergent branch made the
   // compiler wait for ALL outstanding loads (vmcnt(0)) before each chunk, serialising the prefetch
-  auto load_act = [=](int c) -> uint4 {
+  auto load_act = [=](int j, int c) -> uint4 {
     int k = c * 32 + kq;
-    const bool kin = mok && c < KC && k < KD;
+    const bool kin = mok[j] && c < KC && k < KD;
     k = kin ? k : 0;
     const int tap = k / Cx, ch = k - tap * Cx;
     const int q = tap / RS, rs = tap - q * RS;
     const int r = rs / S, s = rs - r * S;
-    const int zz = z + q - pq, yy = y + r - ph, xx = x + s - pw;
+    const int zz = pz[j] + q - pq, yy = py[j] + r - ph, xx = px[j] + s - pw;
     const bool ok = kin && zz >= 0 && zz < D && yy >= 0 && yy < H && xx >= 0 && xx < Wd;
-    const int zc = ok ? zz : z, yc = ok ? yy : y, xc = ok ? xx : x;
-    const uint4 v = *reinterpret_cast<const uint4*>(X + ((((size_t)b * D + zc) * H + yc) * Wd + xc) * Cx + ch);
+    const int zc = ok ? zz : pz[j], yc = ok ? yy : py[j], xc = ok ? xx : px[j];
+    const uint4 v = *reinterpret_cast<const uint4*>(X + ((((size_t)pb[j] * D + zc) * H + yc) * Wd + xc) * Cx + ch);
     return ok ? v : z4;
   };
-  uint4 pre[CL_PF];
+  uint4 pre[MJ][CL_PF];
 #pragma unroll
-  for (int u = 0; u < CL_PF; ++u) pre[u] = load_act(u);
+  for (int u = 0; u < CL_PF; ++u)
+#pragma unroll
+    for (int j = 0; j < MJ; ++j) pre[j][u] = load_act(j, u);
   // whole prefetch groups (chunks past KC read zeros): a straight-line body, so the in-order
   // vmcnt waits only for the chunk being consumed
   const int KCp = cl_kcp(KD);
@@ -101,26 +117,27 @@ ZOO_DEV void cl_gemm(const CLArgs& a, int m, f32x4 (&acc)[NI], int lane, const b
 #pragma unroll
     for (int u = 0; u < CL_PF; ++u) {
       const int c = c0 + u;
-      {
-        const bf16x8 bv = __builtin_bit_cast(bf16x8, pre[u]);
-        const int k = c * 32 + kq;
-        uint4 wv[NI];   // every row block's weight fragment first (one LDS wait), then the MFMAs
+      const int k = c * 32 + kq;
+      uint4 wv[NI];   // every row block's weight fragment first (one LDS wait), then the MFMAs
 #pragma unroll
-        for (int i = 0; i < NI; ++i) {
-          const int n = 16 * i + nr;
-          if (LDSW) {
-            wv[i] = *reinterpret_cast<const uint4*>(wl + (size_t)n * kdp + k);   // zero padded rows / k
-          } else {
-            const bool ok = n < a.Nr && k < KD;
-            const uint4 t = *reinterpret_cast<const uint4*>(a.Wt + (size_t)(ok ? n : 0) * a.ldw + (ok ? k : 0));
-            wv[i] = ok ? t : z4;
-          }
+      for (int i = 0; i < NI; ++i) {
+        const int n = 16 * i + nr;
+        if (LDSW) {
+          wv[i] = *reinterpret_cast<const uint4*>(wl + (size_t)n * kdp + k);   // zero padded rows / k
+        } else {
+          const bool ok = n < a.Nr && k < KD;
+          const uint4 t = *reinterpret_cast<const uint4*>(a.Wt + (size_t)(ok ? n : 0) * a.ldw + (ok ? k : 0));
+          wv[i] = ok ? t : z4;
         }
-        __builtin_amdgcn_sched_barrier(0);   // keep the fragment reads batched ahead of the MFMAs
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep the fragment reads batched ahead of the MFMAs
 #pragma unroll
-        for (int i = 0; i < NI; ++i) acc[i] = mfma16(__builtin_bit_cast(bf16x8, wv[i]), bv, acc[i]);
+      for (int j = 0; j < MJ; ++j) {
+        const bf16x8 bv = __builtin_bit_cast(bf16x8, pre[j][u]);
+#pragma unroll
+        for (int i = 0; i < NI; ++i) acc[j][i] = mfma16(__builtin_bit_cast(bf16x8, wv[i]), bv, acc[j][i]);
         // refill this slot after its use: the in-order vmcnt then waits only for this chunk's load
-        pre[u] = load_act(c + CL_PF);
+        pre[j][u] = load_act(j, c + CL_PF);
       }
     }
   }
@@ -160,102 +177,120 @@ ZOO_DEV void cl_stage(const CLArgs& a, bf16_t* wl) {
 // addresses, no branch) so their latency hides behind the reduction; loading them between the
 // stores of the epilogue made each channel wait for its own round trip (the stores may alias the
 // loads): 11 us of a 23 us step.
-template <int NI, bool LDSW>
+template <int NI, int MJ, bool LDSW>
 __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_fwd_kernel(CLArgs a) {
   extern __shared__ __attribute__((aligned(16))) char cl_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
-  const int mc = m < a.M ? m : a.M - 1, F = a.F;
+  const int m0 = (blockIdx.x * CL_WAVES + (threadIdx.x >> 6)) * 16 * MJ + (lane & 15);
+  const int F = a.F;
   const float* __restrict__ gx = a.gx;
   const float* __restrict__ cprev = a.cprev;
-  float4 g4[NI];
-  float cp[NI];
+  float4 g4[MJ][NI];
+  float cp[MJ][NI];
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int j = 4 * i + (lane >> 4);   // rows 16 i + 4 (lane >> 4) + q = gate q of channel j
-    const size_t e = (size_t)mc * F + (j < F ? j : F - 1);
-    g4[i] = *reinterpret_cast<const float4*>(gx + 4 * e);
-    cp[i] = cprev ? cprev[e] : 0.f;
+  for (int jb = 0; jb < MJ; ++jb) {
+    const int m = m0 + 16 * jb;
+    const int mc = m < a.M ? m : a.M - 1;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = 4 * i + (lane >> 4);   // rows 16 i + 4 (lane >> 4) + q = gate q of channel j
+      const size_t e = (size_t)mc * F + (j < F ? j : F - 1);
+      g4[jb][i] = *reinterpret_cast<const float4*>(gx + 4 * e);
+      cp[jb][i] = cprev ? cprev[e] : 0.f;
+    }
   }
   if (LDSW) cl_stage<NI>(a, wl);
-  f32x4 acc[NI];
-  cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
-  if (m >= a.M) return;
+  f32x4 acc[MJ][NI];
+  cl_gemm<NI, MJ, LDSW>(a, m0, acc, lane, wl);
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int j = 4 * i + (lane >> 4);
-    if (j >= F) continue;
-    const size_t e = (size_t)m * F + j;
-    const float ig = lstm_act(acc[i][0] + g4[i].x, a.iact), fg = lstm_act(acc[i][1] + g4[i].y, a.iact);
-    const float cg = lstm_act(acc[i][2] + g4[i].z, a.act), og = lstm_act(acc[i][3] + g4[i].w, a.iact);
-    const float cn = fg * cp[i] + ig * cg;
-    const float hn = og * lstm_act(cn, a.act);
-    a.c[e] = cn;
-    a.h[e] = hn;
-    a.hb[(size_t)m * a.ldh + j] = f2bf(hn);
-    *reinterpret_cast<float4*>(a.acts + 4 * e) = make_float4(ig, fg, cg, og);
+  for (int jb = 0; jb < MJ; ++jb) {
+    const int m = m0 + 16 * jb;
+    if (m >= a.M) continue;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = 4 * i + (lane >> 4);
+      if (j >= F) continue;
+      const size_t e = (size_t)m * F + j;
+      const float4 g = g4[jb][i];
+      const float ig = lstm_act(acc[jb][i][0] + g.x, a.iact), fg = lstm_act(acc[jb][i][1] + g.y, a.iact);
+      const float cg = lstm_act(acc[jb][i][2] + g.z, a.act), og = lstm_act(acc[jb][i][3] + g.w, a.iact);
+      const float cn = fg * cp[jb][i] + ig * cg;
+      const float hn = og * lstm_act(cn, a.act);
+      a.c[e] = cn;
+      a.h[e] = hn;
+      a.hb[(size_t)m * a.ldh + j] = f2bf(hn);
+      *reinterpret_cast<float4*>(a.acts + 4 * e) = make_float4(ig, fg, cg, og);
+    }
   }
 }
 
 // backward: operands of every (row block, channel) up front while NI <= 4 (the data-gradient rows
 // are the hidden channels: <= 64); wider row counts load them per row block
-template <int NI, bool LDSW>
+template <int NI, int MJ, bool LDSW>
 __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_bwd_kernel(CLArgs a) {
   extern __shared__ __attribute__((aligned(16))) char cl_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
-  constexpr bool PRE = NI <= 4;
-  constexpr int NP = PRE ? NI : 1;
+  constexpr bool PRE = NI * MJ <= 4;
+  constexpr int NP = PRE ? NI : 1, MP = PRE ? MJ : 1;
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * 16 * CL_WAVES + (threadIdx.x >> 6) * 16 + (lane & 15);
-  const int mc = m < a.M ? m : a.M - 1, F = a.F;
+  const int m0 = (blockIdx.x * CL_WAVES + (threadIdx.x >> 6)) * 16 * MJ + (lane & 15);
+  const int F = a.F;
   const float* __restrict__ acts = a.acts;
   const float* __restrict__ cc = a.cc;
   const float* __restrict__ dout = a.dout;
   const float* __restrict__ cprev = a.cprev;
   const float* __restrict__ dcin = a.dc_in ? a.dc : nullptr;
-  float4 av[NP][4];
-  float cv[NP][4], ov[NP][4], dv[NP][4], pv[NP][4];
-  auto load_ops = [&](int i, int slot) {
+  float4 av[MP][NP][4];
+  float cv[MP][NP][4], ov[MP][NP][4], dv[MP][NP][4], pv[MP][NP][4];
+  auto load_ops = [&](int jb, int i, int sj, int slot) {
+    const int m = m0 + 16 * jb;
+    const int mc = m < a.M ? m : a.M - 1;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int j = 16 * i + 4 * (lane >> 4) + q;   // row = hidden channel of the data gradient
       const size_t e = (size_t)mc * F + (j < F ? j : F - 1);
-      av[slot][q] = *reinterpret_cast<const float4*>(acts + 4 * e);
-      cv[slot][q] = cc[e];
-      ov[slot][q] = dout ? dout[e] : 0.f;
-      dv[slot][q] = dcin ? dcin[e] : 0.f;
-      pv[slot][q] = cprev ? cprev[e] : 0.f;
+      av[sj][slot][q] = *reinterpret_cast<const float4*>(acts + 4 * e);
+      cv[sj][slot][q] = cc[e];
+      ov[sj][slot][q] = dout ? dout[e] : 0.f;
+      dv[sj][slot][q] = dcin ? dcin[e] : 0.f;
+      pv[sj][slot][q] = cprev ? cprev[e] : 0.f;
     }
   };
   if constexpr (PRE) {
 #pragma unroll
-    for (int i = 0; i < NI; ++i) load_ops(i, i);
+    for (int jb = 0; jb < MJ; ++jb)
+#pragma unroll
+      for (int i = 0; i < NI; ++i) load_ops(jb, i, jb, i);
   }
   if (LDSW) cl_stage<NI>(a, wl);
-  f32x4 acc[NI];
-  cl_gemm<NI, LDSW>(a, m, acc, lane, wl);
-  if (m >= a.M) return;
+  f32x4 acc[MJ][NI];
+  cl_gemm<NI, MJ, LDSW>(a, m0, acc, lane, wl);
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const int slot = PRE ? i : 0;
-    if constexpr (!PRE) load_ops(i, 0);
+  for (int jb = 0; jb < MJ; ++jb) {
+    const int m = m0 + 16 * jb;
+    if (m >= a.M) continue;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = 16 * i + 4 * (lane >> 4) + q;
-      if (j >= F) continue;
-      const size_t e = (size_t)m * F + j;
-      const float ig = av[slot][q].x, fg = av[slot][q].y, cg = av[slot][q].z, og = av[slot][q].w;
-      const float tc = lstm_act(cv[slot][q], a.act);
-      const float dh = acc[i][q] + ov[slot][q];
-      const float dcv = dh * og * lstm_dact(tc, a.act) + dv[slot][q];
-      const float cp = pv[slot][q];
-      const float d0 = dcv * cg * lstm_dact(ig, a.iact), d1 = dcv * cp * lstm_dact(fg, a.iact);
-      const float d2 = dcv * ig * lstm_dact(cg, a.act), d3 = dh * tc * lstm_dact(og, a.iact);
-      *reinterpret_cast<float4*>(a.dg + 4 * e) = make_float4(d0, d1, d2, d3);
-      *reinterpret_cast<uint2*>(a.dgb + (size_t)m * a.ldg + 4 * j) =
-          make_uint2((uint32_t)f2bf(d0) | ((uint32_t)f2bf(d1) << 16), (uint32_t)f2bf(d2) | ((uint32_t)f2bf(d3) << 16));
-      a.dc[e] = dcv * fg;   // this lane read dc_{t+1}[e] before: in place
+    for (int i = 0; i < NI; ++i) {
+      const int slot = PRE ? i : 0, sj = PRE ? jb : 0;
+      if constexpr (!PRE) load_ops(jb, i, 0, 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 16 * i + 4 * (lane >> 4) + q;
+        if (j >= F) continue;
+        const size_t e = (size_t)m * F + j;
+        const float ig = av[sj][slot][q].x, fg = av[sj][slot][q].y, cg = av[sj][slot][q].z, og = av[sj][slot][q].w;
+        const float tc = lstm_act(cv[sj][slot][q], a.act);
+        const float dh = acc[jb][i][q] + ov[sj][slot][q];
+        const float dcv = dh * og * lstm_dact(tc, a.act) + dv[sj][slot][q];
+        const float cpv = pv[sj][slot][q];
+        const float d0 = dcv * cg * lstm_dact(ig, a.iact), d1 = dcv * cpv * lstm_dact(fg, a.iact);
+        const float d2 = dcv * ig * lstm_dact(cg, a.act), d3 = dh * tc * lstm_dact(og, a.iact);
+        *reinterpret_cast<float4*>(a.dg + 4 * e) = make_float4(d0, d1, d2, d3);
+        *reinterpret_cast<uint2*>(a.dgb + (size_t)m * a.ldg + 4 * j) =
+            make_uint2((uint32_t)f2bf(d0) | ((uint32_t)f2bf(d1) << 16), (uint32_t)f2bf(d2) | ((uint32_t)f2bf(d3) << 16));
+        a.dc[e] = dcv * fg;   // this lane read dc_{t+1}[e] before: in place
+      }
     }
   }
 }
@@ -263,10 +298,10 @@ __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_bwd_kernel(CLArgs a) {
 // weights in LDS while they fit 128 KiB per workgroup (one workgroup per CU at these grids); else from L2
 constexpr size_t CL_LDS_MAX = 128 * 1024;
 
-template <int NI, bool LDSW>
-static hipError_t cl_launch2(const CLArgs& a, int bwd, size_t smem, hipStream_t st) {
-  const dim3 grid((a.M + 16 * CL_WAVES - 1) / (16 * CL_WAVES));
-  auto kf = bwd ? &convlstm_bwd_kernel<NI, LDSW> : &convlstm_fwd_kernel<NI, LDSW>;
+template <int NI, int MJ, bool LDSW, bool BWD>
+static hipError_t cl_launch2(const CLArgs& a, size_t smem, hipStream_t st) {
+  const dim3 grid((a.M + 16 * MJ * CL_WAVES - 1) / (16 * MJ * CL_WAVES));
+  auto kf = BWD ? &convlstm_bwd_kernel<NI, MJ, LDSW> : &convlstm_fwd_kernel<NI, MJ, LDSW>;
   if (LDSW) {
     const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kf),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -276,12 +311,24 @@ static hipError_t cl_launch2(const CLArgs& a, int bwd, size_t smem, hipStream_t 
   return hipGetLastError();
 }
 
-template <int NI>
-static hipError_t cl_launch(const CLArgs& a, int bwd, hipStream_t st) {
+// pixel blocks per wave: 2 once the step has enough pixels to fill the chip with half the waves
+// (>= 64k: 512+ workgroups) and the weights do not fit in LDS (each wave then re-reads them from
+// L2 per chunk), while the registers allow it (forward <= 8 row blocks: 242 VGPRs; backward <= 4:
+// its epilogue operands spill beyond); small latency-bound steps keep one block per wave
+template <int NI, bool BWD>
+static hipError_t cl_launch_dir(const CLArgs& a, hipStream_t st) {
   const int KD = a.Q * a.R * a.S * a.Cx;
   const size_t smem = (size_t)16 * NI * ((((KD + 31) / 32 + CL_PF - 1) / CL_PF * CL_PF) * 32 + 8) * 2;
-  if (a.X && smem <= CL_LDS_MAX) return cl_launch2<NI, true>(a, bwd, smem, st);
-  return cl_launch2<NI, false>(a, bwd, 0, st);
+  if (a.X && smem <= CL_LDS_MAX) return cl_launch2<NI, 1, true, BWD>(a, smem, st);
+  if constexpr (NI <= (BWD ? 4 : 8)) {
+    if (a.X && a.M >= 65536) return cl_launch2<NI, 2, false, BWD>(a, 0, st);
+  }
+  return cl_launch2<NI, 1, false, BWD>(a, 0, st);
+}
+
+template <int NI>
+static hipError_t cl_launch(const CLArgs& a, int bwd, hipStream_t st) {
+  return bwd ? cl_launch_dir<NI, true>(a, st) : cl_launch_dir<NI, false>(a, st);
 }
 
 }  // namespace zoo

@@ -73,3 +73,28 @@ def test_convlstm2d_fused_odd_filters_and_wide_channels(gpu, monkeypatch):
     assert rel(xg.grad, xr.grad) < 5e-2
     assert rel(layer.Wh.grad, ref.Wh.grad) < 5e-2
     assert rel(layer.Wx.grad, ref.Wx.grad) < 5e-2
+
+
+def test_convlstm3d_large_volume_two_blocks_per_wave(gpu, monkeypatch):
+    """ConvLSTM3D over a 2 x 32^3 volume (65536 pixels per step: the step kernels run two 16-pixel
+    blocks per wave, convlstm.hip MJ = 2) against the per-step loop of the same layer on the GPU
+    (recurrent 3-D conv + gate kernel per step): output, input and recurrent-weight gradients."""
+    from zoo.pipeline.api.keras.layers import recurrent as R
+    torch.manual_seed(4)
+    T, B, C, S, f = 3, 2, 8, 32, 32
+    layer = R.ConvLSTM3D(f, 3, return_sequences=True, input_shape=(T, C, S, S, S))
+    layer._ensure_built((None, T, C, S, S, S))
+    layer = layer.to(gpu)
+    x = torch.randn(B, T, C, S, S, S, device=gpu)
+    outs = []
+    for fused in (False, True):
+        monkeypatch.setattr(R, "_CONVLSTM_FUSED", fused)
+        xg = x.clone().requires_grad_(True)
+        layer.zero_grad(set_to_none=True)
+        y = layer(xg)
+        y.float().square().mean().backward()
+        outs.append((y.detach().float(), xg.grad.detach(), layer.Wh.grad.detach().clone()))
+    (y0, dx0, dw0), (y1, dx1, dw1) = outs
+    assert rel(y1, y0) < 5e-3
+    assert rel(dx1, dx0) < 3e-2
+    assert rel(dw1, dw0) < 1e-2
