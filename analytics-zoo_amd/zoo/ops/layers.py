@@ -5,7 +5,7 @@ depthwise / pooling kernels), with fp32 PyTorch references for CPU tensors:
   resize_bilinear      ResizeBilinear        (BigDL nn.ResizeBilinear: TF-legacy sampling)
   upsample_nearest     UpSampling1D/2D/3D
   lstm_gates           ConvLSTM2D/3D gate step (fused activations + cell/hidden update)
-  conv3d_ndhwc         Convolution3D         (KD implicit-GEMM conv2d launches, fp32 sum)
+  conv3d_ndhwc         Convolution3D         (depth taps stacked on channels: one implicit-GEMM conv2d)
   pool3d_ndhwc         MaxPooling3D / AveragePooling3D (separable: HxW then D, native 2-D pools)
   pool1d_nwc           MaxPooling1D / AveragePooling1D (native 2-D pool with H = 1)
 
@@ -178,9 +178,13 @@ def lstm_gates(gx, gh, cprev, inner_activation="hard_sigmoid", activation="tanh"
 
 # ---------------------------------------------------------------------------- 3-D convolution
 def conv3d_ndhwc(x, w5, bias=None, stride=(1, 1, 1), pad=(0, 0, 0)):
-    """x [N, D, H, W, C]; w5 [K, KD, KH, KW, C] (channels-last filter). On the GPU: one
-    implicit-GEMM conv2d launch per depth tap over all output slices (batched as N*Do images),
-    summed in fp32; the backward is the conv2d's native dgrad/wgrad through autograd."""
+    """x [N, D, H, W, C]; w5 [K, KD, KH, KW, C] (channels-last filter). On the GPU: the KD
+    depth-shifted input slices are stacked along channels ([N*Do, H, W, KD*C], channel kd*C + c)
+    and convolved ONCE as a KH x KW conv2d with a KD*C-deep reduction, the depth taps summed in
+    the GEMM's fp32 accumulators; the backward is that conv2d's native dgrad / wgrad through
+    autograd (the stacking's gradient sums the slices back). Round 5 ran one conv2d per depth tap
+    with fp32 outputs summed by elementwise adds: 3 output tensors of 4 bytes per element and
+    their adds were a third of a ConvLSTM3D step (profiles/r6/ab7_convlstm3d_*_totals_r6.md)."""
     from zoo.ops.conv import conv2d_nhwc, pack_weight
     N, D, H, W, C = x.shape
     K, KD, KH, KW, _ = w5.shape
@@ -192,14 +196,13 @@ def conv3d_ndhwc(x, w5, bias=None, stride=(1, 1, 1), pad=(0, 0, 0)):
         return y.permute(0, 2, 3, 4, 1).to(x.dtype)
     xp = F.pad(x, (0, 0, 0, 0, 0, 0, pd, pd)) if pd else x
     Do = (D + 2 * pd - KD) // sd + 1
-    out = None
-    for kd in range(KD):
-        sl = xp[:, kd:kd + sd * (Do - 1) + 1:sd]                     # [N, Do, H, W, C]
-        wk = pack_weight(w5[:, kd])                                   # [K, ldb]
-        y = conv2d_nhwc(sl.reshape(N * Do, H, W, C), wk, bias if (kd == 0) else None, kernel=(KH, KW),
-                        stride=(sh, sw), pad=(ph, pw), out_f32=True)
-        out = y if out is None else out + y
-    return out.reshape(N, Do, out.shape[1], out.shape[2], K).to(x.dtype)
+    if KD == 1:
+        xs = xp[:, 0:sd * (Do - 1) + 1:sd]
+    else:
+        xs = torch.cat([xp[:, kd:kd + sd * (Do - 1) + 1:sd] for kd in range(KD)], dim=-1)   # [N, Do, H, W, KD*C]
+    wk = pack_weight(w5.permute(0, 2, 3, 1, 4).reshape(K, KH, KW, KD * C))
+    y = conv2d_nhwc(xs.reshape(N * Do, H, W, KD * C), wk, bias, kernel=(KH, KW), stride=(sh, sw), pad=(ph, pw))
+    return y.reshape(N, Do, y.shape[1], y.shape[2], K).to(x.dtype)
 
 
 # ---------------------------------------------------------------------------- pooling
