@@ -430,7 +430,8 @@ class _ConvLSTM3DFusedFn(torch.autograd.Function):
     """Whole ConvLSTM3D sequence, one launch per step each way: the convlstm.hip step kernels
     with a depth axis (no per-step pad / permute / conv3d glue). ``whp``: the recurrent weight
     [4f, f, k, k, k] in gate-interleaved row order; packed (and flipped for the backward) here
-    once per call. Recurrent weight gradient: one conv_wgrad per depth tap over all steps.
+    once per call. Recurrent weight gradient: one conv_wgrad over all steps, the depth taps stacked
+    on channels.
     Reference: InternalConvLSTM3D.scala (Zs/pipeline/api/keras/layers)."""
 
     @staticmethod
@@ -474,11 +475,12 @@ class _ConvLSTM3DFusedFn(torch.autograd.Function):
                 p = k // 2
                 hp = F.pad(hist[1:T], (0, 0, 0, 0, 0, 0, p, p))          # depth-padded inputs of steps 1..T-1
                 gy = dgb[1:T].reshape((T - 1) * B * D, H, W, K8)
-                for kd in range(k):
-                    xk = hp[:, :, kd:kd + D].reshape((T - 1) * B * D, H, W, cph)
-                    part = torch.zeros(K8, k * k * cph, dtype=torch.float32, device=dev)
-                    C_.conv_wgrad(xk.contiguous(), gy, part, k, k, 1, 1, p, p, 1, 1)
-                    dw5[:, kd] = part.view(K8, k, k, cph)
+                # the depth taps stacked on channels (channel kd * cph + c, as conv3d_ndhwc): ONE
+                # k x k weight gradient with a k * cph-deep input instead of one per depth tap
+                xk = torch.cat([hp[:, :, kd:kd + D] for kd in range(k)], dim=-1).reshape((T - 1) * B * D, H, W, k * cph)
+                part = torch.zeros(K8, k * k * k * cph, dtype=torch.float32, device=dev)
+                C_.conv_wgrad(xk, gy, part, k, k, 1, 1, p, p, 1, 1)
+                dw5 = part.view(K8, k, k, k, cph).permute(0, 3, 1, 2, 4)   # [K8][kh][kw][kd][c] -> [K8][kd][kh][kw][c]
             dw = dw5[:K, ..., :f].permute(0, 4, 1, 2, 3).to(whp.dtype)
         return dgxs, dw, None, None, None, None, None, None, None
 
