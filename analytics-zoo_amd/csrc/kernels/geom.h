@@ -79,6 +79,9 @@ struct BwdStats {
   const void* pro_res;
   const float* pro_rcoef;
   void* pro_mask;
+  // igemm2.hip EPI 3 with an activation: the pre-activation (bias added) is also stored here as
+  // bf16 -- the training forward of a GELU linear, whose backward needs it (nullptr: not stored)
+  void* act_pre;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

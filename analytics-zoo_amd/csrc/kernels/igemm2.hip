@@ -538,6 +538,11 @@ __global__ __launch_bounds__(64 * NWM * NWN, AM == I2_AM_BAND ? 1 : 2) void igem
         // lean bias / activation epilogue: the activation branch is per 8-column piece
 #pragma unroll
         for (int e = 0; e < 8; ++e) v[e] += bsv[e];
+        if (bs.act_pre) {   // training GELU linear: keep the pre-activation for the backward
+          const uint4 pk = pack8(v);
+          *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(bs.act_pre) + off) = pk;
+          unpack8(pk, v);   // the activation of the stored (rounded) value, as the separate pass did
+        }
         if (act == ACT_RELU) {
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);

@@ -282,7 +282,7 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
                        c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy,
                        bool resid_half, bool pro_fwd, c10::optional<torch::Tensor> pro_rcoef,
-                       c10::optional<torch::Tensor> pro_mask) {
+                       c10::optional<torch::Tensor> pro_mask, c10::optional<torch::Tensor> act_pre) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -522,6 +522,28 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
         resid->view({g.N, g.P / 2, g.Q / 2, K}));
     rp = resid_full.data_ptr();
     bs.resid_half = 0;
+  }
+  if (act_pre.has_value() && act_pre->defined()) {
+    // training forward of a GELU linear / conv: the output gelu(v) AND the pre-activation v (its
+    // backward's operand). The large-tile kernel stores both from its EPI 3 epilogue; any other
+    // kernel writes v and one pointwise pass applies GELU (the round-5 path)
+    req(*act_pre, at::kBFloat16, "act_pre");
+    TORCH_CHECK(act == 2 /* ACT_GELU */ && out_bf16 && !out_f32 && !sp && !(out.has_value() && out->defined()) &&
+                    act_pre->is_contiguous() && act_pre->numel() == (int64_t)g.N * g.P * g.Q * K,
+                "conv_fwd: act_pre takes a plain GELU conv with a bf16 output of the same size");
+    check_al16(act_pre->data_ptr(), "act_pre");
+    const int epi3 = zoo::igemm_epi(true, false, bp != nullptr, rp != nullptr, act, g.omap != 0, bs.sums != nullptr,
+                                    false);
+    if (epi3 == 3 && zoo_igemm2_tiles_m(&g, 3) > 0) {
+      bs.act_pre = act_pre->data_ptr();
+    } else {
+      check_hip(zoo_igemm(xin.data_ptr(), w.data_ptr(), act_pre->data_ptr(), nullptr, bp, rp, nullptr, &g, 0, &bs,
+                          cur_stream()),
+                "igemm");
+      auto ya = torch::empty({g.N, g.P, g.Q, K}, x.options());
+      check_hip(zoo_act(act_pre->data_ptr(), nullptr, ya.data_ptr(), ya.numel(), false, 4, 0.f, cur_stream()), "act");
+      return ya;
+    }
   }
   torch::Tensor y, yf;
   if (out.has_value() && out->defined()) {
@@ -3257,7 +3279,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("R"), py::arg("S"), py::arg("sh"), py::arg("sw"), py::arg("ph"), py::arg("pw"), py::arg("dh"), py::arg("dw"), py::arg("lh"), py::arg("lw"), py::arg("bias"), py::arg("resid"), py::arg("stats"), py::arg("act"), py::arg("out_f32"), py::arg("out_bf16"), py::arg("out_h"), py::arg("out_w"), py::arg("out"), py::arg("omap"), py::arg("bz"), py::arg("by"), py::arg("bmean"), py::arg("binv"), py::arg("bsums"),
         py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
         py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false,
-        py::arg("pro_fwd") = false, py::arg("pro_rcoef") = py::none(), py::arg("pro_mask") = py::none());
+        py::arg("pro_fwd") = false, py::arg("pro_rcoef") = py::none(), py::arg("pro_mask") = py::none(),
+        py::arg("act_pre") = py::none());
   m.def("bn_fwd_coef", [](torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean,
                           torch::Tensor rvar, torch::Tensor smean, torch::Tensor sinv, int64_t M, double eps,
                           double momentum) {

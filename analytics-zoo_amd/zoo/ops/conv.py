@@ -26,6 +26,9 @@ from zoo.ops._native import native
 from zoo.ops import _kern, wstream
 from zoo.parallel.flat import grad_slot
 
+# training GELU linears: pre-activation stored by the GEMM epilogue beside the output (False: the
+# GEMM writes v and a separate GELU pass forms the output -- the oracle / A/B of round 6)
+_GELU_DUAL = True
 ACT_CODES = {None: 0, "linear": 0, "relu": 1, "gelu": 2, "sigmoid": 3, "tanh": 4}
 
 
@@ -397,7 +400,7 @@ class _LinearNativeFn(torch.autograd.Function):
     """Transformer-size linear on the hand-written MFMA kernels (igemm / igemm2, zoo._C):
 
       forward   y = act(x W^T + b): GEMM with the bias (+ReLU) epilogue; GELU keeps its bf16
-                pre-activation and applies the native GELU pass (its backward needs it)
+                pre-activation beside the output from the same epilogue (its backward needs it)
       backward  one native pass computes the activation backward and the fp32 bias-gradient
                 column sums (straight into the engine's flat gradient); dX = dY W on the GEMM
                 with the residual gradient (GradAdd) added in its epilogue; W^T is the cached
@@ -415,9 +418,15 @@ class _LinearNativeFn(torch.autograd.Function):
         bf = None if bias is None else bias.detach().float().contiguous()
         x4 = x2.view(x2.shape[0], 1, 1, K)
         pre = None
-        if act == "gelu" and need_grad:
+        if act == "gelu" and need_grad and not _GELU_DUAL:
             pre = _kern.conv_fwd(x4, wb, 1, 1, bias=bf).view(-1, N)
             y = native().act_fwd_bwd(pre, None, 4, 0.0)
+        elif act == "gelu" and need_grad:
+            # one GEMM writes both gelu(v) and v (its backward's operand): igemm2.hip EPI 3 stores
+            # the pre-activation beside the output, no separate GELU pass over v
+            pre4 = torch.empty(x2.shape[0], 1, 1, N, dtype=torch.bfloat16, device=x2.device)
+            y = _kern.conv_fwd(x4, wb, 1, 1, bias=bf, act=ACT_CODES[act], act_pre=pre4).view(-1, N)
+            pre = pre4.view(-1, N)
         else:
             y = _kern.conv_fwd(x4, wb, 1, 1, bias=bf, act=ACT_CODES[act]).view(-1, N)
         ctx.gelu_link = ctx.gelu_src = None

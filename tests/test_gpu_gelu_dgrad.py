@@ -73,3 +73,29 @@ def test_block_matches_unfused(gpu, monkeypatch):
     for k in g0:
         r = ((g1[k] - g0[k]).norm() / g0[k].norm().clamp_min(1e-12)).item()
         assert r < 3e-2, (k, r)
+
+
+@pytest.mark.parametrize("M,K,N", [(16384, 768, 3072), (4096, 768, 3072), (512, 96, 136)])
+def test_gelu_linear_stores_pre_activation_from_the_epilogue(gpu, M, K, N):
+    """conv_fwd(act=GELU, act_pre=...): the output gelu(v) and the bf16 pre-activation v from one
+    GEMM (igemm2.hip EPI 3 dual store) -- no separate GELU pass in the trace on the large-tile
+    shapes; a shape that kernel does not take (512 x 96 x 136) runs GEMM + GELU pass instead.
+    Both against fp32 PyTorch."""
+    from torch.profiler import ProfilerActivity, profile
+    from zoo.ops import _kern
+    torch.manual_seed(2)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16()
+    b = torch.randn(N, device=gpu) * 0.1
+    pre = torch.empty(M, 1, 1, N, dtype=torch.bfloat16, device=gpu)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        y = _kern.conv_fwd(x.view(M, 1, 1, K), w, 1, 1, bias=b, act=2, act_pre=pre)
+        torch.cuda.synchronize()
+    names = [e.name for e in prof.events() if e.device_type.name == "CUDA"]
+    vref = x.float() @ w.float().t() + b
+    assert (pre.view(M, N).float() - vref).abs().max().item() <= 1e-2 * vref.abs().max().item()
+    yref = F.gelu(pre.view(M, N).float())                 # GELU of the stored (rounded) value
+    assert (y.view(M, N).float() - yref).abs().max().item() <= 1e-2 * yref.abs().max().item()
+    if M >= 4096:
+        assert any("igemm2_kernel" in n for n in names), names
+        assert not [n for n in names if "act_kernel" in n], names
