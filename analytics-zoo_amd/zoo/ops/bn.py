@@ -59,6 +59,11 @@ _PRO_K = tuple(int(v) for v in __import__("os").environ.get("ZOO_BN_FOLD_K", "64
 _PRO_NMAX = int(__import__("os").environ.get("ZOO_BN_FOLD_NMAX", "64"))
 
 
+# projection shortcut (stride 1, stage 1 of ResNet-50): its BatchNorm backward as the shortcut
+# dgrad's prologue instead of a bn_bwd_apply pass (oracle / A/B switch of round 6)
+_SC_FOLD = True
+
+
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
     # K = 64 / 128: the widths whose prologue tile stays spill-free in registers (pw.hip PRO); wider
     # units and the deterministic mode (partial statistics: no pw) keep bn_bwd_apply
@@ -331,12 +336,14 @@ class ShortcutBN:
     (bn_fwd_apply resid_bn) and its backward runs this BatchNorm's backward, handing the
     shortcut conv the gradient of its raw output. The shortcut's own apply pass and its
     normalised output tensor are never materialised."""
-    __slots__ = ("stats", "running_mean", "running_var", "smean", "sinv", "sync", "m_local")
+    __slots__ = ("stats", "running_mean", "running_var", "smean", "sinv", "sync", "m_local", "conv_geo", "fold")
 
     def __init__(self, running_mean, running_var):
         self.running_mean, self.running_var = running_mean, running_var
         self.stats = self.smean = self.sinv = None
         self.sync, self.m_local = False, 0
+        self.conv_geo = None   # (R, S, stride, pad, Cin) of the shortcut conv (set by its forward)
+        self.fold = None       # (y_raw, coef, dy_out): BN backward handed to the shortcut dgrad's prologue
 
 
 def _shortcut_bn_bwd(ctx, dres, K):
@@ -357,13 +364,25 @@ def _shortcut_bn_bwd(ctx, dres, K):
             dbet.add_(sums[:K])
         all_reduce_stats(sums[:2 * K], rb.m_local)
         dg = db = None
-    outs = C_.bn_bwd_apply(dres, None, yres, rb.smean, rb.sinv, gamma2.detach(), sums, False, dg, db)
+    geo = rb.conv_geo
+    if (_SC_FOLD and geo is not None and not rb.sync and gamma2.dtype == torch.float32 and gamma2.is_contiguous()
+            and _fold_ok(ctx, geo[0], geo[1], geo[2], geo[3], K, geo[4], gamma2)):
+        # the shortcut conv's dgrad forms d_raw = A dz + B y_raw + Cc in its operand prologue and
+        # writes it for its weight gradient (pw.hip PRO, as the block's own 1x1 units): the
+        # shortcut's bn_bwd_apply pass is gone (ResNet stage 1 block 1: 64 -> 256, 281 us at b256,
+        # profiles/r6/ab4_prof_rn_step_r6.md row 347). The returned gradient is dz; the shortcut's
+        # backward (_ConvStatsFn) finds the fold on the holder.
+        coef = C_.bnfold_coef(gamma2.detach(), rb.smean, rb.sinv, sums, yres.numel() // K, dg, db)
+        rb.fold = (yres, coef, torch.empty_like(dres))
+        out = dres
+    else:
+        out = C_.bn_bwd_apply(dres, None, yres, rb.smean, rb.sinv, gamma2.detach(), sums, False, dg, db)[0]
     if own_g:
         _notify(gamma2)
     if own_b:
         _notify(beta2)
     ctx.yres = ctx.resid_bn = None
-    return outs[0], (None if own_g else dgam), (None if own_b else dbet)
+    return out, (None if own_g else dgam), (None if own_b else dbet)
 
 
 class _ConvStatsFn(torch.autograd.Function):
@@ -381,10 +400,13 @@ class _ConvStatsFn(torch.autograd.Function):
         if holder.sync:
             all_reduce_stats(stats[:2 * K], holder.m_local)
         holder.stats = stats
+        holder.conv_geo = (R, S, tuple(stride), tuple(pad), x.shape[3])
+        holder.fold = None
         ctx.save_for_backward(x, w)
         ctx.meta = (R, S, stride, pad, x.shape)
         ctx.handoff_in = handoff_in
         ctx.dx_out = dx_out
+        ctx.holder = holder
         return y
 
     @staticmethod
@@ -397,6 +419,7 @@ class _ConvStatsFn(torch.autograd.Function):
             dy = dy.to(torch.bfloat16)
         K = w.shape[0]
         dx = None
+        fold, ctx.holder.fold = ctx.holder.fold, None
         if ctx.needs_input_grad[0]:
             add = None
             if ctx.handoff_in is not None:
@@ -404,7 +427,12 @@ class _ConvStatsFn(torch.autograd.Function):
                 ctx.handoff_in.grad = None
                 if add is None:
                     raise RuntimeError("GradHandoff: residual gradient missing (backward order violated)")
-            if (_HALF_RESID and add is None and ctx.dx_out is not None and (R, S) == (1, 1) and stride == (2, 2)
+            if fold is not None:
+                # dy is the block output's dz: the shortcut BN backward runs in this dgrad's prologue
+                dx = _kern.conv_dgrad(dy, bf16_weight(w), K, R, S, xshape[3], xshape[1], xshape[2], stride, pad,
+                                      resid=add, resid_inplace=add is not None, pro=fold)
+                dy = fold[2]
+            elif (_HALF_RESID and add is None and ctx.dx_out is not None and (R, S) == (1, 1) and stride == (2, 2)
                     and pad == (0, 0) and xshape[1] % 2 == 0 and xshape[2] % 2 == 0):
                 # 1x1 stride 2: the gradient is zero at every odd position -- hand the block's conv1
                 # the compact [N, H/2, W/2, C] values, its dgrad epilogue adds them at the even ones
@@ -418,6 +446,9 @@ class _ConvStatsFn(torch.autograd.Function):
                 # the other consumer of x (the block's conv1) adds it in its dgrad epilogue
                 ctx.dx_out.grad = dx
                 dx = None
+        elif fold is not None:
+            C_.bnpro_apply(dy, fold[0], fold[1], fold[2])   # no data gradient: d_raw for the wgrad alone
+            dy = fold[2]
         gw, own_w = _grad_target(w)
         with wstream.wgrad(dy.device, x, dy, on=own_w):
             C_.conv_wgrad(x, dy, gw, R, S, stride[0], stride[1], pad[0], pad[1], 1, 1)
