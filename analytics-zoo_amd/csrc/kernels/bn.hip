@@ -67,26 +67,45 @@ __global__ __launch_bounds__(256) void bn_reduce_kernel(const bf16_t* __restrict
         load8f(mean, chunk, mu);
         load8f(invstd, chunk, is);
       }
-      for (int r = r0 + my_row; r < r1; r += row_step) {
-        const size_t off = (size_t)r * C + chunk * 8;
-        float a[8];
-        unpack8(*reinterpret_cast<const uint4*>(A + off), a);
-        if (MODE == 0) {
+      // 4 rows per step, every load of the step issued before the first use: with one row per
+      // step a thread had 2 loads in flight and the pass ran at ~3.5 TB/s (234 us for the 256-wide
+      // stage-1 shortcut reduction, profiles/r6/ab4_prof_rn_step_r6.md row 345)
+      constexpr int U = 4;
+      const uint4 zero4 = make_uint4(0u, 0u, 0u, 0u);
+      for (int rb = r0 + my_row; rb < r1; rb += U * row_step) {
+        uint4 av[U], xv[U], zv[U];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) { s1[e] += a[e]; s2[e] += a[e] * a[e]; }
-        } else {
-          float x[8];
-          unpack8(*reinterpret_cast<const uint4*>(Xin + off), x);
-          if (Z) {
-            float z[8];
-            unpack8(*reinterpret_cast<const uint4*>(Z + off), z);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+        for (int u = 0; u < U; ++u) {
+          const int r = rb + u * row_step;
+          const bool ok = r < r1;
+          const size_t off = (size_t)(ok ? r : rb) * C + chunk * 8;
+          av[u] = ok ? *reinterpret_cast<const uint4*>(A + off) : zero4;
+          if (MODE == 1) {
+            xv[u] = ok ? *reinterpret_cast<const uint4*>(Xin + off) : zero4;
+            zv[u] = (ok && Z) ? *reinterpret_cast<const uint4*>(Z + off) : zero4;
           }
+        }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            s1[e] += a[e];
-            s2[e] += a[e] * (x[e] - mu[e]) * is[e];
+        for (int u = 0; u < U; ++u) {
+          float a[8];
+          unpack8(av[u], a);   // rows past r1 are zero: they add nothing
+          if (MODE == 0) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) { s1[e] += a[e]; s2[e] += a[e] * a[e]; }
+          } else {
+            float x[8];
+            unpack8(xv[u], x);
+            if (Z) {
+              float z[8];
+              unpack8(zv[u], z);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a[e] = z[e] > 0.f ? a[e] : 0.f;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              s1[e] += a[e];
+              s2[e] += a[e] * (x[e] - mu[e]) * is[e];
+            }
           }
         }
       }
