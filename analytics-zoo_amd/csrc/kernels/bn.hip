@@ -618,20 +618,35 @@ __global__ __launch_bounds__(256) void bn_relu_maxpool_bwd_reduce_kernel(
   load8f(save_invstd, chunk, is);
 #pragma unroll
   for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  // two pooled pieces per step, their six loads issued before either is used (one piece per step
+  // left three loads in flight per thread)
+  const int nj = Q << lg;
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
     const size_t base = (size_t)row * Q * C;
-    for (int j = threadIdx.x; j < (Q << lg); j += 256) {
-      const size_t off = base + (size_t)j * 8;
-      const uint2 ab = *reinterpret_cast<const uint2*>(arg + off);
-      float g[8], b[8];
-      unpack8(*reinterpret_cast<const uint4*>(dY + off), g);
-      unpack8(*reinterpret_cast<const uint4*>(best + off), b);
+    for (int j0 = threadIdx.x; j0 < nj; j0 += 512) {
+      uint2 ab[2];
+      uint4 gv[2], bv[2];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const uint32_t t = ((e < 4 ? ab.x : ab.y) >> (8 * (e & 3))) & 0xff;
-        const float d = t == kClipped ? 0.f : g[e];
-        s1[e] += d;
-        s2[e] += d * ((b[e] - mu[e]) * is[e]);
+      for (int u = 0; u < 2; ++u) {
+        const int j = j0 + 256 * u;
+        const bool ok = j < nj;
+        const size_t off = base + (size_t)(ok ? j : j0) * 8;
+        ab[u] = ok ? *reinterpret_cast<const uint2*>(arg + off) : make_uint2(0xffffffffu, 0xffffffffu);
+        gv[u] = *reinterpret_cast<const uint4*>(dY + off);
+        bv[u] = *reinterpret_cast<const uint4*>(best + off);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        float g[8], b[8];
+        unpack8(gv[u], g);
+        unpack8(bv[u], b);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t t = ((e < 4 ? ab[u].x : ab[u].y) >> (8 * (e & 3))) & 0xff;
+          const float d = t == kClipped ? 0.f : g[e];   // a piece past the row: all taps kClipped
+          s1[e] += d;
+          s2[e] += d * ((b[e] - mu[e]) * is[e]);
+        }
       }
     }
   }
