@@ -82,6 +82,11 @@ struct BwdStats {
   // igemm2.hip EPI 3 with an activation: the pre-activation (bias added) is also stored here as
   // bf16 -- the training forward of a GELU linear, whose backward needs it (nullptr: not stored)
   void* act_pre;
+  // pw.hip EPI 2 (short reductions): sums2[c] += sum over rows of out[m][c] * y2[m][c] -- the
+  // masked output gradient against a second pre-BN tensor (a fused projection shortcut's raw
+  // output, whose BatchNorm sees the same gradient), so its backward needs no reduction pass
+  const void* y2;
+  float* sums2;
 };
 
 // One flipped (sub-)filter of a batched flip (igemm.hip flip_weights_batched_kernel):

@@ -85,6 +85,11 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   const int N = p.N;
   float* patch = ssum + 2 * NP + w * 16 * PITCH;                   // wave-private fp32 16 x NP patch
   float* pco = ssum + 2 * NP + PW_NW * 16 * PITCH;                 // PRO: A | B | Cc, [3][K] (+ EPI 4: rA | - | rC)
+  float* ssum3 = pco + (PRO ? (EPI == 4 ? 6 : 3) * K : 0);         // [NP] sums against y2 (EPI 2)
+  // the y2 sums only in the short-reduction backward kernels (their registers have room; the
+  // 256-deep prologue kernels run at 256 VGPRs): the host does not route y2 calls elsewhere
+  constexpr bool Y2 = EPI == 2 && KT <= 2;
+  const bool y2on = Y2 && bs.y2 != nullptr;
 
   // ---- workgroup -> (channel group, pixel group); XCD-local channel groups ----
   const int b = blockIdx.x, G = gridDim.x;
@@ -102,6 +107,8 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
     *reinterpret_cast<uint4*>(wfr + (((n >> 4) * KT + kb) * 64 + (n & 15) + 16 * q) * 16) = v;
   }
   for (int c = tid; c < 2 * NP; c += NT) ssum[c] = 0.f;
+  if (y2on)
+    for (int c = tid; c < NP; c += NT) ssum3[c] = 0.f;
   if constexpr (PRO)
     for (int c = tid; c < 3 * K; c += NT) pco[c] = bs.pro_coef[c];
   if constexpr (PRO && EPI == 4)
@@ -128,9 +135,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
       }
     }
   }
-  float s1[8], s2[8];
+  float s1[8], s2[8], s3[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; }
+  for (int e = 0; e < 8; ++e) { s1[e] = 0.f; s2[e] = 0.f; s3[e] = 0.f; }
 
   const int ntiles = (p.M + TPM - 1) / TPM;
   const int gw = mg * PW_NW + w, GW = MG * PW_NW;
@@ -310,7 +317,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   auto process = [&](int t, bf16x8 (&cur)[MJ][KT], bf16x8 (&nxt)[MJ][KT], bf16x8 (&ycur)[YJ][YK],
                      bf16x8 (&ynxt)[YJ][YK]) {
     // (1) epilogue operands of THIS tile first (in-order vmcnt: they must not queue behind the prefetch)
-    uint4 ey[MJ][HP], er[MJ][HP];
+    uint4 ey[MJ][HP], er[MJ][HP], ey2[Y2 ? MJ : 1][Y2 ? HP : 1];
     unsigned em[MJ][HP];
     if constexpr (EPI == 2) {
 #pragma unroll
@@ -322,6 +329,9 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
           const size_t off = (size_t)m * N + c0;
           ey[j][h] = bnsum ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y) + off)
                            : make_uint4(0u, 0u, 0u, 0u);
+          if constexpr (Y2)
+            ey2[j][h] = y2on ? *reinterpret_cast<const uint4*>(reinterpret_cast<const bf16_t*>(bs.y2) + off)
+                             : make_uint4(0u, 0u, 0u, 0u);
           if (resid && bs.resid_half) {
             // half-resolution residual: even (h, w) only; the address stays in bounds for odd
             // positions (H, W even) and the value is dropped there, so the load is unconditional
@@ -414,6 +424,14 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
               s1[e] += q[e];
               s2[e] += q[e] * (yy[e] - cmu[e]) * civ[e];
             }
+            if constexpr (Y2) {
+              if (y2on) {
+                float y2v[8];
+                unpack8(ey2[j][h], y2v);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) s3[e] += q[e] * y2v[e];
+              }
+            }
           }
         }
       }
@@ -443,9 +461,14 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
       s1[e] += __shfl_xor(s1[e], o, 64);
       s2[e] += __shfl_xor(s2[e], o, 64);
     }
+    if (y2on) {
+#pragma unroll
+      for (int o = CPR; o < 64; o <<= 1) s3[e] += __shfl_xor(s3[e], o, 64);
+    }
     if (lane < CPR) {
       atomicAdd(ssum + ch * 8 + e, s1[e]);
       atomicAdd(ssum + NP + ch * 8 + e, s2[e]);
+      if (y2on) atomicAdd(ssum3 + ch * 8 + e, s3[e]);
     }
   }
   __syncthreads();
@@ -454,6 +477,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   for (int c = tid; c < NP; c += NT) {
     atomicAdd(dst + n0 + c, ssum[c]);
     atomicAdd(dst + N + n0 + c, ssum[NP + c]);
+    if (y2on) atomicAdd(bs.sums2 + n0 + c, ssum3[c]);
   }
 }
 
@@ -476,7 +500,7 @@ static int pw_ncu() {
 // [6][K] with a residual's affine in EPI 4)
 static size_t pw_smem(int NP, int K, bool pro, bool res = false) {
   return (size_t)NP * K * 2 + 2 * NP * 4 + (size_t)PW_NW * 16 * (NP + 4) * 4 +
-         (pro ? (size_t)(res ? 6 : 3) * K * 4 : 0);
+         (pro ? (size_t)(res ? 6 : 3) * K * 4 : 0) + (size_t)NP * 4;   // + [NP] second-BN sums (y2)
 }
 
 template <int NP, int TPM, int KT, int EPI, bool PRO>
@@ -576,6 +600,8 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   // with a residual operand (EPI 4) up to K = 256 in 64-channel groups
   if (bs && bs->pro_fwd && (route != 1 || g->Ktot > (bs->pro_res ? 256 : 128) || bs->pro_y)) return 0;
   if (bs && bs->pro_res && (g->K % 64 != 0 || g->Ktot % 64 != 0)) return 0;
+  // second-BN sums (BwdStats.y2): the short-reduction backward kernels only (pw_kernel Y2)
+  if (bs && bs->y2 && (route != 2 || !bs->sums || g->Ktot > 64)) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
   if (bs && bs->resid_half && (route != 2 || (g->H & 1) || (g->W & 1))) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;

@@ -272,6 +272,9 @@ ConvGeom make_geom(const torch::Tensor& x, int K, int R, int S, int sh, int sw, 
 static void check_al16(const void* p, const char* what);
 
 // x: [N,H,W,C] bf16; w: [K, ldb] bf16 (logical [K][R][S][C] rows, zero padded to ldb)
+void bn_reduce(torch::Tensor a, c10::optional<torch::Tensor> z, c10::optional<torch::Tensor> x,
+               c10::optional<torch::Tensor> mean, c10::optional<torch::Tensor> invstd, torch::Tensor out, int mode);
+
 torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, int sw, int ph, int pw, int dh, int dw,
                        int lh, int lw, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> resid,
                        c10::optional<torch::Tensor> stats, int act, bool out_f32, bool out_bf16, int out_h,
@@ -282,7 +285,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
                        c10::optional<torch::Tensor> bbeta, c10::optional<torch::Tensor> pro_y,
                        c10::optional<torch::Tensor> pro_coef, c10::optional<torch::Tensor> pro_dy,
                        bool resid_half, bool pro_fwd, c10::optional<torch::Tensor> pro_rcoef,
-                       c10::optional<torch::Tensor> pro_mask, c10::optional<torch::Tensor> act_pre) {
+                       c10::optional<torch::Tensor> pro_mask, c10::optional<torch::Tensor> act_pre,
+                       c10::optional<torch::Tensor> by2, c10::optional<torch::Tensor> bsums2) {
   req(x, at::kBFloat16, "x");
   req(w, at::kBFloat16, "w");
   TORCH_CHECK(x.dim() == 4 && w.dim() == 2, "conv_fwd: x must be NHWC 4-D, w 2-D [K, ldb]");
@@ -394,6 +398,15 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     TORCH_CHECK(!stats.has_value() || !stats->defined(), "stats and fused bn-backward are exclusive");
     TORCH_CHECK(out_bf16 && !out_f32, "fused bn-backward needs the bf16 output");
     bs.sums = bsums->data_ptr<float>();
+    if (by2.has_value() && by2->defined()) {
+      // a second BatchNorm on the same gradient (fused projection shortcut): sums2 += sum out * y2
+      TORCH_CHECK(!gelu && bsums2.has_value() && bsums2->defined(), "bn y2 needs the BN-backward epilogue and sums2");
+      req(*by2, at::kBFloat16, "bn y2");
+      req(*bsums2, at::kFloat, "bn sums2");
+      TORCH_CHECK(by2->numel() == full && bsums2->numel() >= K, "bn y2 must match the output, sums2 [K]");
+      bs.y2 = by2->data_ptr();
+      bs.sums2 = bsums2->data_ptr<float>();
+    }
   }
   bs.unbatched = 0;
   // BN-backward prologue: x is a unit's masked output gradient g; the GEMM operand is that unit's
@@ -523,6 +536,13 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     rp = resid_full.data_ptr();
     bs.resid_half = 0;
   }
+  // the y2 sums run in pw.hip's epilogue; any other kernel gets them from one reduction pass over
+  // its output afterwards
+  const bool y2_pass = bs.y2 != nullptr && !zoo_pw_eligible(&g, route, &bs);
+  if (y2_pass) {
+    bs.y2 = nullptr;
+    bs.sums2 = nullptr;
+  }
   if (act_pre.has_value() && act_pre->defined()) {
     // training forward of a GELU linear / conv: the output gelu(v) AND the pre-activation v (its
     // backward's operand). The large-tile kernel stores both from its EPI 3 epilogue; any other
@@ -562,6 +582,13 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
   if (g.stat_slots == zoo::kStatPartial) fold_partials(stat_dst, part, 2 * K, tiles_m);
   else if (g.stat_slots > 0)
     check_hip(zoo_stats_finalize(stat_dst, 2 * K, g.stat_slots, cur_stream()), "stats_finalize");
+  if (y2_pass) {
+    auto zero = torch::zeros({K}, x.options().dtype(at::kFloat));
+    auto one = torch::ones({K}, x.options().dtype(at::kFloat));
+    auto tmp = torch::zeros({2 * (int64_t)K}, x.options().dtype(at::kFloat));
+    bn_reduce(y, c10::nullopt, *by2, zero, one, tmp, 1);   // tmp[K..2K) = sum y * y2
+    bsums2->narrow(0, 0, K).add_(tmp.narrow(0, K, K));
+  }
   return out_bf16 ? y : yf;
 }
 
@@ -3280,7 +3307,7 @@ PYBIND11_MODULE(_C, m) {
         py::arg("bgamma") = py::none(), py::arg("bbeta") = py::none(), py::arg("pro_y") = py::none(),
         py::arg("pro_coef") = py::none(), py::arg("pro_dy") = py::none(), py::arg("resid_half") = false,
         py::arg("pro_fwd") = false, py::arg("pro_rcoef") = py::none(), py::arg("pro_mask") = py::none(),
-        py::arg("act_pre") = py::none());
+        py::arg("act_pre") = py::none(), py::arg("by2") = py::none(), py::arg("bsums2") = py::none());
   m.def("bn_fwd_coef", [](torch::Tensor stats, torch::Tensor gamma, torch::Tensor beta, torch::Tensor rmean,
                           torch::Tensor rvar, torch::Tensor smean, torch::Tensor sinv, int64_t M, double eps,
                           double momentum) {

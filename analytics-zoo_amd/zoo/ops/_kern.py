@@ -22,7 +22,7 @@ from zoo.ops._native import native
 def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bias=None, resid=None, stats=None,
              act=0, out_f32=False, out_bf16=True, out_hw=(0, 0), out=None, omap=None, bstats=None, pro=None,
              resid_half=False, pro_fwd=None, act_pre=None):
-    """``bstats = (z or None, y, mean, inv, sums[, gamma, beta])`` fuses the producing unit's
+    """``bstats = (z or None, y, mean, inv, sums[, gamma, beta[, y2, sums2]])`` fuses the producing unit's
     BN-backward reduction (and ReLU mask) into this conv's epilogue. The mask source: a bf16
     ``z`` (ReLU output), a uint8 ``z`` (1-bit mask of the forward apply), or -- z None and
     gamma given -- recomputed from ``y`` with the unit's affine (csrc/kernels/bnmask.h).
@@ -38,11 +38,13 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
     projection shortcut's BatchNorm) -- and its 1-bit ReLU mask goes to ``mask`` (pw.hip EPI 4).
     ``act_pre`` (GELU only): the pre-activation is also written there (bf16, the output's shape)
     -- from the large-tile kernel's epilogue, or by a separate GELU pass for other shapes."""
-    bz = by = bm = bi = bsum = bg = bb = None
+    bz = by = bm = bi = bsum = bg = bb = by2 = bsum2 = None
     if bstats is not None:
         bz, by, bm, bi, bsum = bstats[:5]
         if len(bstats) > 5:
             bg, bb = bstats[5], bstats[6]
+        if len(bstats) > 7:
+            by2, bsum2 = bstats[7], bstats[8]
     py, pc, pd = pro if pro is not None else (None, None, None)
     prc = pmask = None
     if pro_fwd is not None:
@@ -52,7 +54,7 @@ def conv_fwd(x, w, R, S, stride=(1, 1), pad=(0, 0), dil=(1, 1), ldil=(1, 1), bia
     return native().conv_fwd(x, w, R, S, stride[0], stride[1], pad[0], pad[1], dil[0], dil[1], ldil[0], ldil[1],
                              bias, resid, stats, act, out_f32, out_bf16, out_hw[0], out_hw[1], out,
                              list(omap) if omap else [], bz, by, bm, bi, bsum, bg, bb, py, pc, pd, bool(resid_half),
-                             pro_fwd is not None, prc, pmask, act_pre)
+                             pro_fwd is not None, prc, pmask, act_pre, by2, bsum2)
 
 
 # ---------------------------------------------------------------------------

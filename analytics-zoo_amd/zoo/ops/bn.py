@@ -62,6 +62,9 @@ _PRO_NMAX = int(__import__("os").environ.get("ZOO_BN_FOLD_NMAX", "64"))
 # projection shortcut (stride 1, stage 1 of ResNet-50): its BatchNorm backward as the shortcut
 # dgrad's prologue instead of a bn_bwd_apply pass (oracle / A/B switch of round 6)
 _SC_FOLD = True
+# ... and its BN-backward sums taken in the consumer's epilogue (BNProducer.y2) instead of a
+# bn_reduce pass over (dz, raw shortcut output)
+_SC_SUMS = True
 
 
 def _fold_ok(ctx, R, S, stride, pad, K, Cin, gamma):
@@ -119,7 +122,11 @@ class BNProducer:
     # stride-1 conv): the unit skips its apply pass and leaves ``pending = (y, coef, z)`` -- z an
     # unwritten tensor -- and the consumer's conv forms z = relu(A y + Cc) in its operand prologue
     # (pw.hip), writing z as it goes. 2 bytes per element of the z re-read saved, and a launch.
-    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused", "gamma", "beta", "mask", "fwd_pro", "pending")
+    # ``y2``: a fused projection shortcut's raw output. Its BatchNorm receives the same gradient as
+    # this unit's, so the consumer's epilogue also sums grad * y2 per channel into ``sums2`` and the
+    # shortcut's BN backward needs no reduction pass of its own (pw.hip BwdStats.y2).
+    __slots__ = ("relu", "y", "mean", "inv", "sums", "fused", "gamma", "beta", "mask", "fwd_pro", "pending",
+                 "y2", "sums2")
 
     def __init__(self, relu, y, mean, inv):
         self.relu, self.y, self.mean, self.inv = relu, y, mean, inv
@@ -128,21 +135,28 @@ class BNProducer:
         self.gamma = self.beta = self.mask = None
         self.fwd_pro = False
         self.pending = None
+        self.y2 = self.sums2 = None
 
     def bstats(self, z):
         self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
         self.fused = True
         if not self.relu:
-            return (None, self.y, self.mean, self.inv, self.sums)
-        if self.mask is not None:
-            return (self.mask, self.y, self.mean, self.inv, self.sums)
-        if self.gamma is not None:
-            return (None, self.y, self.mean, self.inv, self.sums, self.gamma, self.beta)
-        return (z, self.y, self.mean, self.inv, self.sums)
+            t = (None, self.y, self.mean, self.inv, self.sums)
+        elif self.mask is not None:
+            t = (self.mask, self.y, self.mean, self.inv, self.sums)
+        elif self.gamma is not None:
+            t = (None, self.y, self.mean, self.inv, self.sums, self.gamma, self.beta)
+        else:
+            t = (z, self.y, self.mean, self.inv, self.sums)
+        if self.y2 is not None:
+            self.sums2 = torch.zeros(self.y.shape[-1], dtype=torch.float32, device=self.y.device)
+            t = t + (None, None)[len(t) - 5:] + (self.y2, self.sums2)
+        return t
 
     def release(self):
         self.y = self.mean = self.inv = self.sums = None
         self.gamma = self.beta = self.mask = None
+        self.y2 = self.sums2 = None
         self.fused = False
 
 
@@ -228,6 +242,9 @@ class _ConvBNActFn(torch.autograd.Function):
             po.mask = mask
             if resid is None:
                 po.gamma, po.beta = gamma.detach(), beta.detach()
+            # the fused shortcut BatchNorm's sums come from the consumer's epilogue (not under SyncBN:
+            # there the two BNs all-reduce their own sums)
+            po.y2 = resid if (_SC_SUMS and rb is not None and not ctx.sync and not _deterministic()) else None
         if rb is not None:
             ctx.yres = resid        # shortcut conv output: its BN backward needs it
         ctx.save_for_backward(x, w, gamma, y, z if relu else None, smean, sinv)
@@ -264,8 +281,10 @@ class _ConvBNActFn(torch.autograd.Function):
                 outs = C_.bn_bwd_apply(dz, None, y, smean, sinv, gamma.detach(), sums, False, dg, db)
                 dy = outs[0]
             dresid = dz if has_resid else None
+            sc_sums = (sums, po.sums2) if po.sums2 is not None else None
             po.release()
         else:
+            sc_sums = None
             sums = workspace.zeros(stat_len(K), dz.device)
             C_.bn_reduce(dz, z, y, smean, sinv, sums, 1)
             dg, db = _sync_bwd(ctx, sums, K, y.numel() // K, dgam, dbet)
@@ -277,7 +296,7 @@ class _ConvBNActFn(torch.autograd.Function):
             dresid = None
         dgam2 = dbet2 = None
         if ctx.resid_bn is not None and dresid is not None:
-            dresid, dgam2, dbet2 = _shortcut_bn_bwd(ctx, dresid, K)
+            dresid, dgam2, dbet2 = _shortcut_bn_bwd(ctx, dresid, K, sc_sums)
         dx = None
         if ctx.needs_input_grad[0]:
             add, half = None, False
@@ -346,14 +365,21 @@ class ShortcutBN:
         self.fold = None       # (y_raw, coef, dy_out): BN backward handed to the shortcut dgrad's prologue
 
 
-def _shortcut_bn_bwd(ctx, dres, K):
+def _shortcut_bn_bwd(ctx, dres, K, pre=None):
     """BatchNorm backward of the fused shortcut: (sum dz, sum dz*xhat) over the raw
-    shortcut output, then dx = A dz + B x + D. Returns (d_raw, dgamma2, dbeta2)."""
+    shortcut output, then dx = A dz + B x + D. Returns (d_raw, dgamma2, dbeta2).
+    ``pre = (main sums, sum dz * y_raw)`` from the consumer's epilogue (BNProducer.y2): the
+    shortcut's sums follow without a pass, sum dz*xhat = inv (sum dz*y - mean sum dz)."""
     C_ = native()
     rb, yres = ctx.resid_bn, ctx.yres
     gamma2, beta2 = ctx.gamma2, ctx.beta2
     sums = workspace.zeros(stat_len(K), dres.device)
-    C_.bn_reduce(dres, None, yres, rb.smean, rb.sinv, sums, 1)
+    if pre is not None:
+        s1 = pre[0][:K]
+        sums[:K].copy_(s1)
+        sums[K:2 * K].copy_(rb.sinv * (pre[1] - rb.smean * s1))
+    else:
+        C_.bn_reduce(dres, None, yres, rb.smean, rb.sinv, sums, 1)
     dgam, own_g = _grad_target(gamma2)
     dbet, own_b = _grad_target(beta2)
     dg, db = dgam, dbet

@@ -72,3 +72,38 @@ def test_fused_shortcut_bn_matches_unfused(gpu, monkeypatch, kind, cin, width, s
         close(g1[k], g0[k], gr[k].float(), k)
     assert torch.allclose(s1[0], s0[0], rtol=1e-4, atol=1e-5)
     assert torch.allclose(s1[1], s0[1], rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("mask_form", ["bits", "z"])
+def test_consumer_epilogue_second_bn_sums(gpu, mask_form):
+    """BNProducer.y2: the consumer conv's BN-backward epilogue also sums out * y2 per channel
+    (pw.hip EPI 2 for the 1-bit mask form; the bf16-z form runs on another kernel and gets the
+    sums from one reduction pass) -- against fp32 torch, main BN sums included."""
+    from zoo.ops import _kern
+    from zoo.ops.bn import stat_len
+    torch.manual_seed(3)
+    N, H, W, Ci, Co = 2, 14, 14, 64, 256
+    x = (torch.randn(N, H, W, Ci, device=gpu) * 0.5).bfloat16()
+    w = (torch.randn(Co, Ci, device=gpu) * 0.1).bfloat16()
+    y = torch.randn(N, H, W, Co, device=gpu).bfloat16()
+    y2 = torch.randn(N, H, W, Co, device=gpu).bfloat16()
+    pre = torch.randn(N, H, W, Co, device=gpu)
+    keep = pre > 0
+    mean = torch.randn(Co, device=gpu) * 0.1
+    inv = torch.rand(Co, device=gpu) + 0.5
+    sums = torch.zeros(stat_len(Co), device=gpu)
+    sums2 = torch.zeros(Co, device=gpu)
+    if mask_form == "bits":
+        bits = (keep.view(-1, 8).int() << torch.arange(8, device=gpu)).sum(1).to(torch.uint8)
+        zarg = bits
+    else:
+        zarg = torch.where(keep, pre.abs() + 0.1, torch.zeros_like(pre)).bfloat16()
+    out = _kern.conv_fwd(x, w, 1, 1, bstats=(zarg, y, mean, inv, sums, None, None, y2, sums2))
+    o = (x.float().reshape(-1, Ci) @ w.float().t()).reshape(N, H, W, Co) * keep
+    ob = o.bfloat16().float()
+    assert _rel(out.float().cpu(), o.cpu()) < 1e-2
+    ref2 = (ob * y2.float()).reshape(-1, Co).sum(0)
+    ref_s1 = ob.reshape(-1, Co).sum(0)
+    ref_s2 = (ob * (y.float() - mean) * inv).reshape(-1, Co).sum(0)
+    assert _rel(sums2.cpu(), ref2.cpu()) < 2e-3
+    assert _rel(sums[:Co].cpu(), ref_s1.cpu()) < 2e-3 and _rel(sums[Co:2 * Co].cpu(), ref_s2.cpu()) < 2e-3
