@@ -88,7 +88,7 @@ __global__ __launch_bounds__(PW_NW * 64, 1) void pw_kernel(const bf16_t* __restr
   float* ssum3 = pco + (PRO ? (EPI == 4 ? 6 : 3) * K : 0);         // [NP] sums against y2 (EPI 2)
   // the y2 sums only in the short-reduction backward kernels (their registers have room; the
   // 256-deep prologue kernels run at 256 VGPRs): the host does not route y2 calls elsewhere
-  constexpr bool Y2 = EPI == 2 && KT <= 2;
+  constexpr bool Y2 = EPI == 2 && (KT <= 2 || (!PRO && KT <= 4));
   const bool y2on = Y2 && bs.y2 != nullptr;
 
   // ---- workgroup -> (channel group, pixel group); XCD-local channel groups ----
@@ -601,7 +601,7 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   if (bs && bs->pro_fwd && (route != 1 || g->Ktot > (bs->pro_res ? 256 : 128) || bs->pro_y)) return 0;
   if (bs && bs->pro_res && (g->K % 64 != 0 || g->Ktot % 64 != 0)) return 0;
   // second-BN sums (BwdStats.y2): the short-reduction backward kernels only (pw_kernel Y2)
-  if (bs && bs->y2 && (route != 2 || !bs->sums || g->Ktot > 64)) return 0;
+  if (bs && bs->y2 && (route != 2 || !bs->sums || g->Ktot > (bs->pro_y ? 64 : 128))) return 0;
   // a half-resolution residual (BwdStats::resid_half) needs the backward epilogue and even H, W
   if (bs && bs->resid_half && (route != 2 || (g->H & 1) || (g->W & 1))) return 0;
   return is1x1 && g->Ktot == g->C && g->M > 0 && pw_np(g->K, g->Ktot) > 0;

@@ -491,6 +491,21 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
     if (sp) sp = part.data_ptr<float>();
     else bs.sums = part.data_ptr<float>();
   }
+  // the y2 sums run in pw.hip's epilogue; any other kernel gets them from one reduction pass over
+  // its output afterwards. Decided before the prologue fallbacks below, so a y2 request never
+  // costs a call its prologue (y2 is dropped first)
+  bool y2_pass = false;
+  if (bs.y2) {
+    const void* y2p = bs.y2;
+    bs.y2 = nullptr;
+    const bool base_ok = zoo_pw_eligible(&g, route, &bs);
+    bs.y2 = y2p;
+    y2_pass = !(base_ok && zoo_pw_eligible(&g, route, &bs));
+    if (y2_pass) {
+      bs.y2 = nullptr;
+      bs.sums2 = nullptr;
+    }
+  }
   // the prologue runs only in pw.hip; any other kernel (including pw with the deterministic
   // partial statistics decided above) gets dy materialised first
   if (bs.pro_y) {
@@ -535,13 +550,6 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
         resid->view({g.N, g.P / 2, g.Q / 2, K}));
     rp = resid_full.data_ptr();
     bs.resid_half = 0;
-  }
-  // the y2 sums run in pw.hip's epilogue; any other kernel gets them from one reduction pass over
-  // its output afterwards
-  const bool y2_pass = bs.y2 != nullptr && !zoo_pw_eligible(&g, route, &bs);
-  if (y2_pass) {
-    bs.y2 = nullptr;
-    bs.sums2 = nullptr;
   }
   if (act_pre.has_value() && act_pre->defined()) {
     // training forward of a GELU linear / conv: the output gelu(v) AND the pre-activation v (its
