@@ -595,7 +595,7 @@ extern "C" int zoo_pw_eligible(const ConvGeom* g, int route, const BwdStats* bs)
   static const int fwd_kmax = 256;
   if (route == 1 && g->Ktot > fwd_kmax) return 0;
   // the BN-backward prologue keeps operand and y fragments of a K <= 128 tile in registers
-  if (bs && bs->pro_y && (route != 2 || g->Ktot > 256)) return 0;
+  if (bs && bs->pro_y && ((route != 2 && route != 1) || g->Ktot > 256)) return 0;
   // the forward consumer-side apply: plain forward epilogue, K <= 128 (register budget as above);
   // with a residual operand (EPI 4) up to K = 256 in 64-channel groups
   if (bs && bs->pro_fwd && (route != 1 || g->Ktot > (bs->pro_res ? 256 : 128) || bs->pro_y)) return 0;
@@ -635,11 +635,13 @@ extern "C" hipError_t zoo_pw(const void* X, const void* W, void* Y, const void* 
     return pw_dispatch<4, true>(*g, 64, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   if (epi == 1 && bs.pro_fwd)
     return pw_dispatch<1, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
-  if (epi == 1)
-    return pw_dispatch<1, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
+  // the BN-backward prologue runs in the backward-epilogue kernel also for a plain dgrad (no
+  // producer sums, no residual: a projection shortcut's dgrad, whose dx is handed to conv1)
   if (bs.pro_y)
     return pw_dispatch<2, true>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr,
                                 bs, st);
+  if (epi == 1)
+    return pw_dispatch<1, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, nullptr, stats, bs, st);
   return pw_dispatch<2, false>(*g, NP, (const bf16_t*)X, (const bf16_t*)W, (bf16_t*)Y, (const bf16_t*)resid, nullptr,
                                bs, st);
 }

@@ -431,6 +431,8 @@ torch::Tensor conv_fwd(torch::Tensor x, torch::Tensor w, int R, int S, int sh, i
       check_al16(pro_dy->data_ptr(), "pro_dy");
     }
     check_al16(pro_y->data_ptr(), "pro_y");
+    // the prologue kernel is the backward-epilogue one: it computes no forward statistics
+    TORCH_CHECK(!(stats.has_value() && stats->defined()), "conv_fwd: the BN-backward prologue takes no stats");
     bs.pro_y = pro_y->data_ptr();
     bs.pro_coef = pro_coef->data_ptr<float>();
     bs.pro_dy = opt_ptr<void>(pro_dy);

@@ -137,7 +137,10 @@ class BNProducer:
         self.pending = None
         self.y2 = self.sums2 = None
 
-    def bstats(self, z):
+    def bstats(self, z, y2_ok=True):
+        """``y2_ok``: the consumer's dgrad runs on pw.hip with room for the second sums (a 1x1
+        stride-1 dgrad with a <= 64-deep reduction when it has its own BN prologue, <= 128 without);
+        otherwise the shortcut keeps its own reduction pass (cheaper than the generic fallback)."""
         self.sums = workspace.zeros(stat_len(self.y.shape[-1]), self.y.device)
         self.fused = True
         if not self.relu:
@@ -148,7 +151,7 @@ class BNProducer:
             t = (None, self.y, self.mean, self.inv, self.sums, self.gamma, self.beta)
         else:
             t = (z, self.y, self.mean, self.inv, self.sums)
-        if self.y2 is not None:
+        if self.y2 is not None and y2_ok:
             self.sums2 = torch.zeros(self.y.shape[-1], dtype=torch.float32, device=self.y.device)
             t = t + (None, None)[len(t) - 5:] + (self.y2, self.sums2)
         return t
@@ -310,7 +313,8 @@ class _ConvBNActFn(torch.autograd.Function):
                 full[:, ::2, ::2] = add
                 add, half = full, False
             pin = ctx.producer_in
-            bst = pin.bstats(x) if (pin is not None and pin.y is not None) else None
+            y2_ok = (R, S) == (1, 1) and tuple(stride) == (1, 1) and K <= (64 if fold is not None else 128)
+            bst = pin.bstats(x, y2_ok) if (pin is not None and pin.y is not None) else None
             # a handed-off gradient is a temporary owned by this unit now: accumulate into it in place
             dx = _kern.conv_dgrad(dz if fold is not None else dy, bf16_weight(w), K, R, S, Cin, xshape[1],
                                   xshape[2], stride, pad, resid=add, bstats=bst, resid_inplace=add is not None,
