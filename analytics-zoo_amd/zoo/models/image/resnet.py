@@ -73,6 +73,9 @@ FWD_PRO = False
 # operand prologue (which writes the block output and its ReLU mask); the block's apply pass over
 # the full-width tensor is skipped (zoo.ops.bn _FWD_PRO_RES_K: the 256-wide stage-1 outputs)
 FWD_PRO_RES = True
+# ... also at the stage-1 -> stage-2 transition (the next block has a projection shortcut, stride
+# on conv2): the 256-wide stage-1 output apply pass (267 us at b256) goes too
+FWD_PRO_RES_DOWN = True
 
 
 def _bp():
@@ -96,9 +99,13 @@ class Bottleneck(nn.Module):
         self.down = ConvBN(cin, cout, 1, stride=stride, relu=False) if (stride != 1 or cin != cout) else None
 
     def consumes_block_output_1x1(self):
-        """The block's input feeds only its own 1x1 stride-1 conv1 (identity shortcut): the previous
+        """The block's input is formed by its own 1x1 stride-1 conv1: with an identity shortcut conv1
+        is its only reader; with a projection shortcut (SHORTCUT_FIRST order) conv1 runs first, its
+        prologue writes the input, and the shortcut conv reads it after. Either way the previous
         block's output apply can move into conv1's prologue."""
-        return self.down is None and self.conv1.k == 1 and self.conv1.stride == 1
+        if not (self.conv1.k == 1 and self.conv1.stride == 1):
+            return False
+        return self.down is None or (FWD_PRO_RES_DOWN and SHORTCUT_FIRST)
 
     def forward(self, x, prod=None, out_pro=False):
         """``prod``: BNProducer of ``x`` (the previous block's last unit). ``out_pro``: the next
