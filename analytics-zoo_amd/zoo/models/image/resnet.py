@@ -67,15 +67,18 @@ S2D_STEM = True
 SHORTCUT_FIRST = True
 # bottlenecks: conv2's BN + ReLU applied by conv3 (1x1) in its operand prologue, conv2's apply pass
 # skipped (BNProducer.fwd_pro, pw.hip forward prologue). Off: -0.3 % with the 64- and 128-wide
-# units, +-0 with the 64-wide ones alone (profiles/r5/ab_fwd_consumer_apply_r5.md)
+# units, +-0 with the 64-wide ones alone (profiles/r5/ab_fwd_consumer_apply_r5.md); on the
+# round-6 kernels -0.3 % again (profiles/r6/ab18_downfp*_r6.log)
 FWD_PRO = False
 # block outputs: the block's last BN + residual + ReLU applied by the NEXT block's 1x1 conv1 in its
 # operand prologue (which writes the block output and its ReLU mask); the block's apply pass over
 # the full-width tensor is skipped (zoo.ops.bn _FWD_PRO_RES_K: the 256-wide stage-1 outputs)
 FWD_PRO_RES = True
 # ... also at the stage-1 -> stage-2 transition (the next block has a projection shortcut, stride
-# on conv2): the 256-wide stage-1 output apply pass (267 us at b256) goes too
-FWD_PRO_RES_DOWN = True
+# on conv2). Off: that conv1 writes 128 channels, i.e. two 64-channel workgroup groups, so the
+# prologue's y + residual reads and BN math run twice; it measured -0.2 % against the 267 us
+# apply pass it removes (13,149 vs 13,173 img/s over 3 same-box pairs, profiles/r6/ab18_*_r6.log)
+FWD_PRO_RES_DOWN = False
 
 
 def _bp():
