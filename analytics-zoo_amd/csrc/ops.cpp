@@ -43,6 +43,7 @@ void zoo_c3_set(int);
 int zoo_c3_stamps(unsigned long long*, int);
 void zoo_igemm2_set(int, int);
 void zoo_igemm2_w192_set(int);
+void zoo_convlstm_pers_set(int);
 int zoo_pw_eligible(const ConvGeom*, int, const zoo::BwdStats*);
 void zoo_pw_set(int);
 void zoo_set_reserved_cus(int);
@@ -144,8 +145,8 @@ hipError_t zoo_bnpro_apply(const void*, const void*, const float*, void*, size_t
 hipError_t zoo_bn_fwd_coef(const float*, const float*, const float*, float*, float*, float*, float*, float*, int, int,
                            float, float, hipStream_t);
 hipError_t zoo_convlstm_step(const void*, const void*, int, int, int, int, int, int, int, int, int, int, int, int, int,
-                             const float*, const float*, float*, float*, float*, void*, int, const float*,
-                             const float*, float*, int, float*, void*, int, int, hipStream_t);
+                             const void*, int, const float*, float*, float*, float*, void*, int, const float*,
+                             const float*, float*, int, float*, void*, int, int, float*, hipStream_t);
 hipError_t zoo_bf16_to_f32(const void*, float*, size_t, int, hipStream_t);
 hipError_t zoo_f32_to_bf16(const float*, void*, size_t, hipStream_t);
 hipError_t zoo_sum_chunks_bf16(const void*, int, size_t, float*, void*, float, hipStream_t);
@@ -1756,9 +1757,9 @@ void convlstm_fwd_step(c10::optional<torch::Tensor> x, torch::Tensor wt, int64_t
     cp = cprev->data_ptr<float>();
   }
   check_hip(zoo_convlstm_step(opt_ptr<void>(x), wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1), 4 * F, F, iact, act,
-                              gx.data_ptr<float>(), cp, h.data_ptr<float>(), c.data_ptr<float>(),
+                              gx.data_ptr<float>(), 0, cp, h.data_ptr<float>(), c.data_ptr<float>(),
                               acts.data_ptr<float>(), hb.data_ptr(), hb.numel() / M, nullptr, nullptr, nullptr, 0,
-                              nullptr, nullptr, 0, 0, cur_stream()),
+                              nullptr, nullptr, 0, 0, nullptr, cur_stream()),
             "convlstm_fwd_step");
 }
 
@@ -1784,9 +1785,9 @@ void convlstm_bwd_step(c10::optional<torch::Tensor> x, torch::Tensor wt, int64_t
     return t->data_ptr<float>();
   };
   check_hip(zoo_convlstm_step(opt_ptr<void>(x), wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1), wt.size(0), F, iact,
-                              act, nullptr, opt(cprev, "cprev"), nullptr, nullptr, acts.data_ptr<float>(), nullptr, 0,
+                              act, nullptr, 0, opt(cprev, "cprev"), nullptr, nullptr, acts.data_ptr<float>(), nullptr, 0,
                               opt(dout, "dout"), cc.data_ptr<float>(), dc.data_ptr<float>(), dc_in ? 1 : 0,
-                              dg.data_ptr<float>(), dgb.data_ptr(), dgb.numel() / M, 1, cur_stream()),
+                              dg.data_ptr<float>(), dgb.data_ptr(), dgb.numel() / M, 1, nullptr, cur_stream()),
             "convlstm_bwd_step");
 }
 
@@ -1797,7 +1798,11 @@ void convlstm_bwd_step(c10::optional<torch::Tensor> x, torch::Tensor wt, int64_t
 void convlstm_fwd_seq(torch::Tensor gxs, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W, int64_t Q,
                       int64_t R, int64_t S, torch::Tensor hist, torch::Tensor hseq, torch::Tensor cseq,
                       torch::Tensor acts, int64_t iact, int64_t act) {
-  req(gxs, at::kFloat, "gxs"); req(hist, at::kBFloat16, "hist"); req(hseq, at::kFloat, "hseq");
+  TORCH_CHECK(gxs.is_cuda() && gxs.is_contiguous() &&
+                  (gxs.scalar_type() == at::kFloat || gxs.scalar_type() == at::kBFloat16),
+              "convlstm_fwd_seq: gxs contiguous fp32 / bf16");
+  const bool gxb = gxs.scalar_type() == at::kBFloat16;
+  req(hist, at::kBFloat16, "hist"); req(hseq, at::kFloat, "hseq");
   req(cseq, at::kFloat, "cseq"); req(acts, at::kFloat, "acts");
   const int64_t M = B * D * H * W, T = gxs.size(0);
   TORCH_CHECK(T > 0 && M > 0 && gxs.numel() % (4 * M * T) == 0, "convlstm_fwd_seq: gxs [T, M, F, 4]");
@@ -1813,20 +1818,27 @@ void convlstm_fwd_seq(torch::Tensor gxs, torch::Tensor wt, int64_t B, int64_t D,
   convlstm_geom(c10::optional<torch::Tensor>(x0), wt, B, D, H, W, Q, R, S, 4 * F, &Cx);
   const uint16_t* hp = reinterpret_cast<const uint16_t*>(hist.data_ptr());
   float* cs = cseq.data_ptr<float>();
+  // K-split partial sums of the large steps (convlstm.hip persistent kernel), reused by every step
+  auto part = torch::empty({M >= 65536 && T > 1 ? M * ((4 * F + 15) / 16 * 16) : 0}, hseq.options());
+  float* pp = part.numel() ? part.data_ptr<float>() : nullptr;
   for (int64_t s = 0; s < T; ++s) {
     check_hip(zoo_convlstm_step(s > 0 ? hp + s * M * cph : nullptr, wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1),
-                                4 * F, F, iact, act, gxs.data_ptr<float>() + s * M * 4 * F,
+                                4 * F, F, iact, act,
+                                static_cast<const char*>(gxs.data_ptr()) + s * M * 4 * F * gxs.element_size(), gxb ? 1 : 0,
                                 s > 0 ? cs + (s - 1) * M * F : nullptr, hseq.data_ptr<float>() + s * M * F,
                                 cs + s * M * F, acts.data_ptr<float>() + s * M * 4 * F,
                                 const_cast<uint16_t*>(hp) + (s + 1) * M * cph, cph, nullptr, nullptr, nullptr, 0,
-                                nullptr, nullptr, 0, 0, cur_stream()),
+                                nullptr, nullptr, 0, 0, pp, cur_stream()),
               "convlstm_fwd_seq");
   }
 }
 
 void convlstm_bwd_seq(torch::Tensor dout, bool rseq, torch::Tensor wt, int64_t B, int64_t D, int64_t H, int64_t W,
                       int64_t Q, int64_t R, int64_t S, torch::Tensor acts, torch::Tensor cseq, torch::Tensor dc,
-                      torch::Tensor dgxs, torch::Tensor dgb, int64_t iact, int64_t act) {
+                      c10::optional<torch::Tensor> dgxs_opt, torch::Tensor dgb, int64_t iact, int64_t act) {
+  // dgxs None: the fp32 gate gradients are not written (the caller takes dgb, the bf16 copy)
+  const bool dg32 = dgxs_opt.has_value() && dgxs_opt->defined();
+  torch::Tensor dgxs = dg32 ? *dgxs_opt : acts;
   req(dout, at::kFloat, "dout"); req(acts, at::kFloat, "acts"); req(cseq, at::kFloat, "cseq");
   req(dc, at::kFloat, "dc"); req(dgxs, at::kFloat, "dgxs"); req(dgb, at::kBFloat16, "dgb");
   const int64_t M = B * D * H * W, T = acts.size(0);
@@ -1844,13 +1856,16 @@ void convlstm_bwd_seq(torch::Tensor dout, bool rseq, torch::Tensor wt, int64_t B
   convlstm_geom(c10::optional<torch::Tensor>(x0), wt, B, D, H, W, Q, R, S, F, &Cx);
   uint16_t* gb = reinterpret_cast<uint16_t*>(dgb.data_ptr());
   const float* cs = cseq.data_ptr<float>();
+  auto part = torch::empty({M >= 65536 && T > 1 ? M * ((wt.size(0) + 15) / 16 * 16) : 0}, cseq.options());
+  float* pp = part.numel() ? part.data_ptr<float>() : nullptr;
   for (int64_t s = T - 1; s >= 0; --s) {
     const float* d = rseq ? dout.data_ptr<float>() + s * M * F : (s == T - 1 ? dout.data_ptr<float>() : nullptr);
     check_hip(zoo_convlstm_step(s < T - 1 ? gb + (s + 1) * M * K8 : nullptr, wt.data_ptr(), B, D, H, W, Cx, Q, R, S,
-                                wt.size(1), wt.size(0), F, iact, act, nullptr, s > 0 ? cs + (s - 1) * M * F : nullptr,
+                                wt.size(1), wt.size(0), F, iact, act, nullptr, 0, s > 0 ? cs + (s - 1) * M * F : nullptr,
                                 nullptr, nullptr, acts.data_ptr<float>() + s * M * 4 * F, nullptr, 0, d,
                                 cs + s * M * F, dc.data_ptr<float>(), s < T - 1 ? 1 : 0,
-                                dgxs.data_ptr<float>() + s * M * 4 * F, gb + s * M * K8, K8, 1, cur_stream()),
+                                dg32 ? dgxs.data_ptr<float>() + s * M * 4 * F : nullptr, gb + s * M * K8, K8, 1, pp,
+                                cur_stream()),
               "convlstm_bwd_seq");
   }
 }
@@ -3390,6 +3405,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("convlstm_bwd_seq", &convlstm_bwd_seq);
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
+  m.def("convlstm_pers_set", [](int on) { zoo_convlstm_pers_set(on); },
+        "persistent ConvLSTM step kernels for large steps: 1 K-split (default), 2 row groups only, 0 off (A/B switch)");
   m.def("igemm2_w192_set", [](int mode) { zoo_igemm2_w192_set(mode); },
         "256x192 igemm2 tiles: 0 off (default), 1 forward-type epilogues, 2 also backward epilogues");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },

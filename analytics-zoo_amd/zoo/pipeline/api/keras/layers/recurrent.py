@@ -432,6 +432,9 @@ class _ConvLSTM3DFusedFn(torch.autograd.Function):
     [4f, f, k, k, k] in gate-interleaved row order; packed (and flipped for the backward) here
     once per call. Recurrent weight gradient: one conv_wgrad over all steps, the depth taps stacked
     on channels.
+    ``gxs``: the input convolution's bf16 output [T, M, 4f] as is (the step kernel widens it; no
+    fp32 copy of the gate tensor), and its gradient is the step kernels' bf16 gate gradients (the
+    operand the recurrent data / weight gradients read anyway; no fp32 gate-gradient tensor).
     Reference: InternalConvLSTM3D.scala (Zs/pipeline/api/keras/layers)."""
 
     @staticmethod
@@ -463,11 +466,11 @@ class _ConvLSTM3DFusedFn(torch.autograd.Function):
         w5 = F.pad(whp.detach().permute(0, 2, 3, 4, 1), (0, cph - f, 0, 0, 0, 0, 0, 0, 0, K8 - K))
         wfl = w5.flip(1, 2, 3).permute(4, 1, 2, 3, 0).reshape(cph, k, k * k, K8)
         wfl = ops.pack_weight(wfl).to(torch.bfloat16)
-        dgxs = torch.empty(T, M, K, dtype=torch.float32, device=dev)
         dgb = torch.zeros(T, B, D, H, W, K8, dtype=torch.bfloat16, device=dev)
         dc = torch.empty(M, f, dtype=torch.float32, device=dev)
         dout = dout.contiguous().float()
-        C_.convlstm_bwd_seq(dout, bool(rseq), wfl, B, D, H, W, k, k, k, acts, cseq, dc, dgxs, dgb, 2, 1)
+        C_.convlstm_bwd_seq(dout, bool(rseq), wfl, B, D, H, W, k, k, k, acts, cseq, dc, None, dgb, 2, 1)
+        dgxs = dgb.view(T, M, K8)[..., :K]
         dw = None
         if ctx.needs_input_grad[1]:
             dw5 = torch.zeros(K8, k, k, k, cph, dtype=torch.float32, device=dev)
@@ -535,7 +538,8 @@ class ConvLSTM3D(Layer):
         wx = F.pad(Wx.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
         wh = F.pad(Whp.permute(0, 2, 3, 4, 1), (0, fp, 0, 0, 0, 0, 0, 0, 0, kp))
         bias = F.pad(b, (0, kp))
-        xs = conv3d_ndhwc(xn, wx, bias, stride=(1, 1, 1), pad=(p, p, p)).float()[..., :K]
+        xs = conv3d_ndhwc(xn, wx, bias, stride=(1, 1, 1), pad=(p, p, p))
+        xs = xs[..., :K] if il else xs.float()[..., :K]
         osp = tuple(xs.shape[1:4])
         P = osp[0] * osp[1] * osp[2]
         M = B * P

@@ -75,25 +75,36 @@ def test_convlstm2d_fused_odd_filters_and_wide_channels(gpu, monkeypatch):
     assert rel(layer.Wx.grad, ref.Wx.grad) < 5e-2
 
 
-def test_convlstm3d_large_volume_two_blocks_per_wave(gpu, monkeypatch):
-    """ConvLSTM3D over a 2 x 32^3 volume (65536 pixels per step: the step kernels run two 16-pixel
-    blocks per wave, convlstm.hip MJ = 2) against the per-step loop of the same layer on the GPU
-    (recurrent 3-D conv + gate kernel per step): output, input and recurrent-weight gradients."""
+@pytest.mark.parametrize("B,sp,f,pers", [(2, (32, 32, 32), 32, 0), (2, (32, 32, 32), 32, 1),
+                                         (2, (32, 32, 32), 32, 2), (1, (41, 40, 40), 32, 1),
+                                         (1, (41, 40, 40), 32, 2), (1, (41, 40, 40), 24, 1)])
+def test_convlstm3d_large_volume_two_blocks_per_wave(gpu, monkeypatch, B, sp, f, pers):
+    """ConvLSTM3D over >= 65536 pixels per step against the per-step loop of the same layer on the
+    GPU (recurrent 3-D conv + gate kernel per step): output, input and recurrent-weight gradients.
+    pers 0: the one-tile-per-workgroup step kernels with two 16-pixel blocks per wave (MJ = 2);
+    pers 1: the persistent K-split kernels (all rows, the reduction in two launches whose weights fit
+    LDS, fp32 partial sums between them); pers 2: the persistent row-group kernel (2 row groups whose
+    weights fit LDS). 41 x 40 x 40 leaves a partial last tile, 24 filters partial row blocks."""
+    from zoo.ops._kern import native
     from zoo.pipeline.api.keras.layers import recurrent as R
     torch.manual_seed(4)
-    T, B, C, S, f = 3, 2, 8, 32, 32
-    layer = R.ConvLSTM3D(f, 3, return_sequences=True, input_shape=(T, C, S, S, S))
-    layer._ensure_built((None, T, C, S, S, S))
+    T, C = 3, 8
+    layer = R.ConvLSTM3D(f, 3, return_sequences=True, input_shape=(T, C) + sp)
+    layer._ensure_built((None, T, C) + sp)
     layer = layer.to(gpu)
-    x = torch.randn(B, T, C, S, S, S, device=gpu)
+    x = torch.randn((B, T, C) + sp, device=gpu)
     outs = []
-    for fused in (False, True):
-        monkeypatch.setattr(R, "_CONVLSTM_FUSED", fused)
-        xg = x.clone().requires_grad_(True)
-        layer.zero_grad(set_to_none=True)
-        y = layer(xg)
-        y.float().square().mean().backward()
-        outs.append((y.detach().float(), xg.grad.detach(), layer.Wh.grad.detach().clone()))
+    native().convlstm_pers_set(pers)
+    try:
+        for fused in (False, True):
+            monkeypatch.setattr(R, "_CONVLSTM_FUSED", fused)
+            xg = x.clone().requires_grad_(True)
+            layer.zero_grad(set_to_none=True)
+            y = layer(xg)
+            y.float().square().mean().backward()
+            outs.append((y.detach().float(), xg.grad.detach(), layer.Wh.grad.detach().clone()))
+    finally:
+        native().convlstm_pers_set(1)
     (y0, dx0, dw0), (y1, dx1, dw1) = outs
     assert rel(y1, y0) < 5e-3
     assert rel(dx1, dx0) < 3e-2
