@@ -178,6 +178,12 @@ def _gate_perm(f, device):
     return (torch.arange(4, device=device)[None, :] * f + torch.arange(f, device=device)[:, None]).reshape(-1)
 
 
+def _gate_interleave(w, f):
+    """``w[_gate_perm(f)]`` as a reshape / transpose (no index kernels: the fancy index's backward
+    sorted the indices, a dozen small launches per call)."""
+    return w.reshape((4, f) + tuple(w.shape[1:])).transpose(0, 1).reshape(tuple(w.shape))
+
+
 class _ConvLSTMFusedFn(torch.autograd.Function):
     """Whole ConvLSTM2D sequence, ONE launch per step each way, issued by a C++ loop
     (convlstm_fwd_seq / convlstm_bwd_seq; csrc/kernels/convlstm.hip): the
@@ -354,8 +360,7 @@ class ConvLSTM2D(Layer):
         fused = _CONVLSTM_SEQ and _CONVLSTM_FUSED and f <= 64 and K % 8 == 0
         Wx, Wh, b = self.Wx, self.Wh, self.b
         if fused:   # gate-interleaved rows (the permutation's gradient flows back to the parameters)
-            perm = _gate_perm(f, x.device)
-            Wx, Wh, b = Wx[perm], Wh[perm], b[perm]
+            Wx, Wh, b = _gate_interleave(Wx, f), _gate_interleave(Wh, f), _gate_interleave(b, f)
         wx, cpx = self._packed(Wx)
         wh, cph = self._packed(Wh)
         bias = F.pad(b, (0, ops.ceil8(K) - K)).float()
@@ -466,7 +471,8 @@ class _ConvLSTM3DFusedFn(torch.autograd.Function):
         w5 = F.pad(whp.detach().permute(0, 2, 3, 4, 1), (0, cph - f, 0, 0, 0, 0, 0, 0, 0, K8 - K))
         wfl = w5.flip(1, 2, 3).permute(4, 1, 2, 3, 0).reshape(cph, k, k * k, K8)
         wfl = ops.pack_weight(wfl).to(torch.bfloat16)
-        dgb = torch.zeros(T, B, D, H, W, K8, dtype=torch.bfloat16, device=dev)
+        # every step kernel writes all K = 4f gate channels: zero-filled only for K8 > K padding
+        dgb = (torch.empty if K8 == K else torch.zeros)(T, B, D, H, W, K8, dtype=torch.bfloat16, device=dev)
         dc = torch.empty(M, f, dtype=torch.float32, device=dev)
         dout = dout.contiguous().float()
         C_.convlstm_bwd_seq(dout, bool(rseq), wfl, B, D, H, W, k, k, k, acts, cseq, dc, None, dgb, 2, 1)
@@ -527,14 +533,18 @@ class ConvLSTM3D(Layer):
             xt = x.transpose(0, 1)
             if self.go_backwards:
                 xt = xt.flip(0)
-            xn = xt.reshape(T * B, C, *sp).permute(0, 2, 3, 4, 1)
         else:
-            xn = x.reshape(B * T, C, *sp).permute(0, 2, 3, 4, 1)
-        xn = F.pad(xn, (0, cp)).to(torch.bfloat16)
+            xt = x
+        # [N, C, *sp] -> channels-last bf16 [N, *sp, C + cp] in ONE strided copy (reshape of the
+        # transposed input, pad and cast were three full passes over it)
+        xn = torch.empty((T * B,) + sp + (C + cp,), dtype=torch.bfloat16, device=x.device)
+        xv = xn.view((xt.shape[0], xt.shape[1]) + sp + (C + cp,))
+        if cp:
+            xv[..., C:].zero_()
+        xv[..., :C].copy_(xt.permute(0, 1, 3, 4, 5, 2))
         Wx, Whp, b = self.Wx, self.Wh, self.b
         if il:
-            perm = _gate_perm(f, x.device)
-            Wx, Whp, b = Wx[perm], Whp[perm], b[perm]
+            Wx, Whp, b = _gate_interleave(Wx, f), _gate_interleave(Whp, f), _gate_interleave(b, f)
         wx = F.pad(Wx.permute(0, 2, 3, 4, 1), (0, cp, 0, 0, 0, 0, 0, 0, 0, kp))
         wh = F.pad(Whp.permute(0, 2, 3, 4, 1), (0, fp, 0, 0, 0, 0, 0, 0, 0, kp))
         bias = F.pad(b, (0, kp))
