@@ -152,6 +152,19 @@ __global__ __launch_bounds__(256) void prob_nll_grad_kernel(const T* __restrict_
   }
 }
 
+// dlogits * (g / max(count, 1)) in the logits dtype: the softmax-xent backward in one pass (the
+// upstream gradient and the count are device scalars; was a div, a mul and a cast launch)
+template <typename T>
+__global__ __launch_bounds__(256) void xent_grad_scale_kernel(const T* __restrict__ dl, const float* __restrict__ g,
+                                                              const float* __restrict__ count, T* __restrict__ out,
+                                                              size_t n) {
+  const float s = g[0] / fmaxf(count[0], 1.f);
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    if constexpr (sizeof(T) == 4) out[i] = dl[i] * s;
+    else out[i] = f2bf(bf2f(dl[i]) * s);
+  }
+}
+
 // ---------------- optimizers over flat buffers ----------------
 // zero_g: the gradient slot is cleared after it is read (the engine's next step then needs no
 // fill launch over the flat gradient buffer)
@@ -399,6 +412,30 @@ extern "C" hipError_t zoo_softmax_xent(const void* logits, int is_f32, const int
   else
     hipLaunchKernelGGL(softmax_xent_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)logits, labels,
                        loss_sum, count, (bf16_t*)dlogits, B, NC, grad_scale, ignore_index, per_row);
+  return hipGetLastError();
+}
+
+// mean softmax cross-entropy in two launches: per-row terms (part: [B] losses, [B] counts), then
+// the ordered fold into out = [mean, count] (prob_nll_finalize_kernel); deterministic, no
+// accumulator fill, no clamp / div launches
+extern "C" hipError_t zoo_softmax_xent_mean(const void* logits, int is_f32, const int64_t* labels, float* part,
+                                            float* out, void* dlogits, int B, int NC, int ignore_index,
+                                            hipStream_t st) {
+  const hipError_t e = zoo_softmax_xent(logits, is_f32, labels, part, part + B, dlogits, B, NC, 1.f, ignore_index, 1, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(prob_nll_finalize_kernel, dim3(1), dim3(64), 0, st, part, B, out, 1);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t zoo_xent_grad_scale(const void* dl, int is_f32, const float* g, const float* count, void* out,
+                                          size_t n, hipStream_t st) {
+  const int blocks = egrid(n);
+  if (is_f32)
+    hipLaunchKernelGGL(xent_grad_scale_kernel<float>, dim3(blocks), dim3(256), 0, st, (const float*)dl, g, count,
+                       (float*)out, n);
+  else
+    hipLaunchKernelGGL(xent_grad_scale_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, (const bf16_t*)dl, g, count,
+                       (bf16_t*)out, n);
   return hipGetLastError();
 }
 

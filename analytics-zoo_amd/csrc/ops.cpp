@@ -123,6 +123,8 @@ hipError_t zoo_softmax_rows(const void*, void*, int, int, int, int, hipStream_t)
 hipError_t zoo_softmax_rows_bwd(const void*, const void*, void*, int, int, int, int, hipStream_t);
 hipError_t zoo_lrn(const void*, const void*, void*, size_t, int, int, float, float, float, int, int, hipStream_t);
 hipError_t zoo_gap_bwd(const void*, void*, int, int, int, hipStream_t);
+hipError_t zoo_softmax_xent_mean(const void*, int, const int64_t*, float*, float*, void*, int, int, int, hipStream_t);
+hipError_t zoo_xent_grad_scale(const void*, int, const float*, const float*, void*, size_t, hipStream_t);
 hipError_t zoo_softmax_xent(const void*, int, const int64_t*, float*, float*, void*, int, int, float, int, int,
                             hipStream_t);
 hipError_t zoo_sgd(float*, const float*, float*, void*, size_t, float, float, float, float, int, float, int,
@@ -1963,6 +1965,39 @@ std::vector<torch::Tensor> softmax_xent(torch::Tensor logits, torch::Tensor labe
   return {loss};
 }
 
+// {out [mean loss, count], unscaled dlogits}: two launches, deterministic (ordered fold)
+std::vector<torch::Tensor> softmax_xent_mean(torch::Tensor logits, torch::Tensor labels, int64_t ignore_index) {
+  TORCH_CHECK(logits.is_cuda() && logits.is_contiguous() && logits.dim() == 2, "softmax_xent_mean: 2-D GPU logits");
+  TORCH_CHECK(logits.scalar_type() == at::kFloat || logits.scalar_type() == at::kBFloat16, "logits dtype");
+  req(labels, at::kLong, "labels");
+  TORCH_CHECK(labels.numel() == logits.size(0) && logits.size(0) > 0 && logits.size(0) < (1LL << 30),
+              "softmax_xent_mean: labels size");
+  const int B = logits.size(0), NC = logits.size(1);
+  auto part = torch::empty({2 * B}, logits.options().dtype(at::kFloat));
+  auto out = torch::empty({2}, logits.options().dtype(at::kFloat));
+  auto dl = torch::empty_like(logits);
+  check_hip(zoo_softmax_xent_mean(logits.data_ptr(), logits.scalar_type() == at::kFloat, labels.data_ptr<int64_t>(),
+                                  part.data_ptr<float>(), out.data_ptr<float>(), dl.data_ptr(), B, NC,
+                                  (int)ignore_index, cur_stream()),
+            "softmax_xent_mean");
+  return {out, dl};
+}
+
+// dl * (g / max(count, 1)) in dl's dtype (g, count: device scalars)
+torch::Tensor xent_grad_scale(torch::Tensor dl, torch::Tensor g, torch::Tensor count) {
+  TORCH_CHECK(dl.is_cuda() && dl.is_contiguous(), "xent_grad_scale: contiguous GPU dl");
+  TORCH_CHECK(dl.scalar_type() == at::kFloat || dl.scalar_type() == at::kBFloat16, "xent_grad_scale: dtype");
+  req(g, at::kFloat, "g");
+  req(count, at::kFloat, "count");
+  TORCH_CHECK(g.numel() >= 1 && count.numel() >= 1, "xent_grad_scale: scalar g / count");
+  auto out = torch::empty_like(dl);
+  if (dl.numel())
+    check_hip(zoo_xent_grad_scale(dl.data_ptr(), dl.scalar_type() == at::kFloat, g.data_ptr<float>(),
+                                  count.data_ptr<float>(), out.data_ptr(), (size_t)dl.numel(), cur_stream()),
+              "xent_grad_scale");
+  return out;
+}
+
 // NLL of probabilities [B, NC] against int64 labels: {loss_sum, count} (+ unscaled dprobs)
 std::vector<torch::Tensor> prob_nll(torch::Tensor probs, torch::Tensor labels, bool want_grad, double eps,
                                     int64_t ignore_index) {
@@ -3451,6 +3486,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("gap_fwd", &gap_fwd);
   m.def("gap_bwd", &gap_bwd);
   m.def("softmax_xent", &softmax_xent);
+  m.def("softmax_xent_mean", &softmax_xent_mean);
+  m.def("xent_grad_scale", &xent_grad_scale);
   m.def("prob_nll_mean", &prob_nll_mean);
   m.def("optim_device_hparams", [](c10::optional<torch::Tensor> hp) {
           if (hp.has_value() && hp->defined()) {

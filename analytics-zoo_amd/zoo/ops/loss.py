@@ -12,10 +12,11 @@ import torch.nn.functional as F
 from zoo.ops._native import native
 
 
-class _SoftmaxXentFn(torch.autograd.Function):
+class _SoftmaxXentAtomicFn(torch.autograd.Function):
+    """The round-5 formulation (atomic sums, clamp / div / mul / cast launches): A/B oracle."""
+
     @staticmethod
     def forward(ctx, logits, labels, ignore_index):
-        B = logits.shape[0]
         outs = native().softmax_xent(logits, labels, True, 1.0, ignore_index)
         acc, dl = outs[0], outs[1]
         count = acc[1].clamp_min(1.0)
@@ -28,11 +29,32 @@ class _SoftmaxXentFn(torch.autograd.Function):
         return dl * (g / count).to(dl.dtype), None, None
 
 
+_XENT_MEAN = True   # A/B switch: False = _SoftmaxXentAtomicFn
+
+
+class _SoftmaxXentFn(torch.autograd.Function):
+    """Two launches forward (per-row terms + the ordered fold into [mean, count]: deterministic,
+    no accumulator fill / clamp / div launches), one backward (dlogits * g / count in the logits
+    dtype)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, ignore_index):
+        out, dl = native().softmax_xent_mean(logits, labels, ignore_index)
+        ctx.save_for_backward(dl, out)
+        return out[0]
+
+    @staticmethod
+    def backward(ctx, g):
+        dl, out = ctx.saved_tensors
+        return native().xent_grad_scale(dl, g.float().reshape(1).contiguous(), out[1:2]), None, None
+
+
 def softmax_cross_entropy(logits, labels, ignore_index=-100):
     """Mean cross-entropy of raw logits [B, C] against int64 labels [B]."""
     labels = labels.long()
-    if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16):
-        return _SoftmaxXentFn.apply(logits.contiguous(), labels.contiguous(), int(ignore_index))
+    if logits.is_cuda and logits.dtype in (torch.float32, torch.bfloat16) and logits.shape[0] > 0:
+        fn = _SoftmaxXentFn if _XENT_MEAN else _SoftmaxXentAtomicFn
+        return fn.apply(logits.contiguous(), labels.contiguous(), int(ignore_index))
     return F.cross_entropy(logits.float(), labels, ignore_index=ignore_index)
 
 

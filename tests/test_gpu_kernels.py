@@ -197,9 +197,15 @@ def test_pooling(gpu):
     assert rel(x2.grad, torch.full_like(x2.grad.float(), 1 / 49)) < 1e-2
 
 
+@pytest.mark.parametrize("mean", [True, False])
 @pytest.mark.parametrize("dt", [torch.float32, torch.bfloat16])
-def test_softmax_xent(gpu, dt):
+def test_softmax_xent(gpu, dt, mean, monkeypatch):
+    """mean: the two-launch ordered-fold loss + one-pass scaled backward (loss._SoftmaxXentFn);
+    False: the atomic-sum formulation it replaced. Against F.cross_entropy in fp32, with an ignored
+    row, an upstream gradient of 2.5, an all-ignored batch, and (mean) bit-identical reruns."""
+    import zoo.ops.loss as L
     from zoo.ops import softmax_cross_entropy
+    monkeypatch.setattr(L, "_XENT_MEAN", mean)
     logits = (torch.randn(33, 1000, device=gpu) * 3).to(dt).requires_grad_(True)
     lab = torch.randint(0, 1000, (33,), device=gpu)
     lab[3] = -100
@@ -207,9 +213,17 @@ def test_softmax_xent(gpu, dt):
     lr_ = logits.detach().float().requires_grad_(True)
     ref = F.cross_entropy(lr_, lab, ignore_index=-100)
     assert abs(l.item() - ref.item()) < 1e-3 * max(1.0, ref.item())
-    l.backward()
-    ref.backward()
+    (l * 2.5).backward()
+    (ref * 2.5).backward()
     assert rel(logits.grad, lr_.grad) < 2e-2
+    if mean:
+        l2 = softmax_cross_entropy(logits.detach(), lab)
+        assert l2.item() == l.item()
+    none = torch.full((5,), -100, dtype=torch.long, device=gpu)
+    z = logits.detach()[:5].clone().requires_grad_(True)
+    lz = softmax_cross_entropy(z, none)
+    lz.backward()
+    assert lz.item() == 0.0 and float(z.grad.float().abs().max()) == 0.0
 
 
 def test_fused_optimizers_match_cpu(gpu):
