@@ -628,7 +628,8 @@ static hipError_t cl_launch_dir(const CLArgs& a, hipStream_t st) {
   const size_t psmem = (size_t)16 * NI * cl_kdp<CL_PPF>(KD) * 2;   // all rows at the persistent padding
   // K-split: all rows, two halves of the reduction (tap-aligned gathers, partial-sum buffer given)
   if constexpr (NI <= (BWD ? 2 : 8) && (BWD || NI % 4 == 0)) {
-    if (a.X && a.M >= 65536 && smem > CL_LDS_MAX && g_cl_pers == 1 && a.part && (a.Cx & 31) == 0 &&
+    // from 32k pixels: one 128-pixel tile per workgroup of the 256-workgroup grid and up
+    if (a.X && a.M >= 32768 && smem > CL_LDS_MAX && g_cl_pers == 1 && a.part && (a.Cx & 31) == 0 &&
         (BWD || 4 * a.F == 16 * NI) && (a.ldh % 4) == 0) {
       const int KC = (KD + 31) / 32, KH = (KC + 1) / 2;
       const size_t ks = (size_t)16 * NI * cl_kdp<CL_PPF>(KH * 32) * 2;

@@ -1821,7 +1821,7 @@ void convlstm_fwd_seq(torch::Tensor gxs, torch::Tensor wt, int64_t B, int64_t D,
   const uint16_t* hp = reinterpret_cast<const uint16_t*>(hist.data_ptr());
   float* cs = cseq.data_ptr<float>();
   // K-split partial sums of the large steps (convlstm.hip persistent kernel), reused by every step
-  auto part = torch::empty({M >= 65536 && T > 1 ? M * ((4 * F + 15) / 16 * 16) : 0}, hseq.options());
+  auto part = torch::empty({M >= 32768 && T > 1 ? M * ((4 * F + 15) / 16 * 16) : 0}, hseq.options());
   float* pp = part.numel() ? part.data_ptr<float>() : nullptr;
   for (int64_t s = 0; s < T; ++s) {
     check_hip(zoo_convlstm_step(s > 0 ? hp + s * M * cph : nullptr, wt.data_ptr(), B, D, H, W, Cx, Q, R, S, wt.size(1),
@@ -1858,7 +1858,7 @@ void convlstm_bwd_seq(torch::Tensor dout, bool rseq, torch::Tensor wt, int64_t B
   convlstm_geom(c10::optional<torch::Tensor>(x0), wt, B, D, H, W, Q, R, S, F, &Cx);
   uint16_t* gb = reinterpret_cast<uint16_t*>(dgb.data_ptr());
   const float* cs = cseq.data_ptr<float>();
-  auto part = torch::empty({M >= 65536 && T > 1 ? M * ((wt.size(0) + 15) / 16 * 16) : 0}, cseq.options());
+  auto part = torch::empty({M >= 32768 && T > 1 ? M * ((wt.size(0) + 15) / 16 * 16) : 0}, cseq.options());
   float* pp = part.numel() ? part.data_ptr<float>() : nullptr;
   for (int64_t s = T - 1; s >= 0; --s) {
     const float* d = rseq ? dout.data_ptr<float>() + s * M * F : (s == T - 1 ? dout.data_ptr<float>() : nullptr);

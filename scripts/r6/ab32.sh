@@ -1,0 +1,12 @@
+#!/bin/bash
+# r6 run 32: K-split ConvLSTM step kernels from 32k pixels -- tests, 16^3 / 32^3 A/B
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+mkdir -p gpurun_out/r6
+T="timeout -k 10"
+$T 400 python -u -m pytest tests/test_gpu_convlstm_seq.py -x -q --timeout 200 --timeout-method thread -p no:cacheprovider > gpurun_out/r6/ab32_tests.log 2>&1
+rc=$?; tail -2 gpurun_out/r6/ab32_tests.log; [ $rc -ne 0 ] && exit $rc
+for r in 1 2; do
+  $T 300 python3 analytics-zoo_amd/tools/convlstm_bench.py --dims 3 --T 16 --hw 16 --modes loop,fused,fused_np --iters 10 >> gpurun_out/r6/ab32_cl3d.log 2>&1 || exit 42
+done
+$T 300 python3 analytics-zoo_amd/tools/convlstm_bench.py --dims 3 --T 16 --modes loop,fused --iters 5 >> gpurun_out/r6/ab32_cl3d.log 2>&1 || exit 43
+grep bench gpurun_out/r6/ab32_cl3d.log | cut -c1-260
