@@ -600,6 +600,9 @@ static hipError_t cl_launch2(const CLArgs& a, size_t smem, hipStream_t st) {
 // its epilogue operands spill beyond); small latency-bound steps keep one block per wave
 // persistent kernels for the large steps: 1 K-split (else row groups), 2 row groups only, 0 off (A/Bs)
 static int g_cl_pers = 1;
+// forward K-split also at >= 64k pixels (0: the row-group kernel there: its one launch without the
+// fp32 partial round trip ran the 32^3 forward step in 210 vs 260 us, ab22 / ab26 totals)
+static int g_cl_fks = 0;
 static int g_cl_ncu = 0;
 
 template <int NIG, int MJ, bool BWD, int PART = 0>
@@ -630,7 +633,7 @@ static hipError_t cl_launch_dir(const CLArgs& a, hipStream_t st) {
   if constexpr (NI <= (BWD ? 2 : 8) && (BWD || NI % 4 == 0)) {
     // from 32k pixels: one 128-pixel tile per workgroup of the 256-workgroup grid and up
     if (a.X && a.M >= 32768 && smem > CL_LDS_MAX && g_cl_pers == 1 && a.part && (a.Cx & 31) == 0 &&
-        (BWD || 4 * a.F == 16 * NI) && (a.ldh % 4) == 0) {
+        (BWD || 4 * a.F == 16 * NI) && (a.ldh % 4) == 0 && (BWD || a.M < 65536 || g_cl_fks)) {
       const int KC = (KD + 31) / 32, KH = (KC + 1) / 2;
       const size_t ks = (size_t)16 * NI * cl_kdp<CL_PPF>(KH * 32) * 2;
       if (ks <= CL_LDS_MAX) {
@@ -696,4 +699,7 @@ extern "C" hipError_t zoo_convlstm_step(const void* X, const void* Wt, int B, in
   }
 }
 
-extern "C" void zoo_convlstm_pers_set(int on) { g_cl_pers = on; }
+extern "C" void zoo_convlstm_pers_set(int on) {
+  g_cl_pers = on & 3;
+  g_cl_fks = (on >> 2) & 1;   // 4 | mode: forward K-split at every size (A/B)
+}

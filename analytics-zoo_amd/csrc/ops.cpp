@@ -3441,7 +3441,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("pw_set", [](int mode) { zoo_pw_set(mode); },
         "streaming 1x1 conv kernel (pw.hip): 1 on, 0 off (igemm / igemm2), -1 back to ZOO_PW");
   m.def("convlstm_pers_set", [](int on) { zoo_convlstm_pers_set(on); },
-        "persistent ConvLSTM step kernels for large steps: 1 K-split (default), 2 row groups only, 0 off (A/B switch)");
+        "persistent ConvLSTM step kernels for large steps: 1 K-split backward / forward below 64k pixels, row "
+        "groups above (default), 2 row groups only, 0 off, +4 forward K-split at every size (A/B switch)");
   m.def("igemm2_w192_set", [](int mode) { zoo_igemm2_w192_set(mode); },
         "256x192 igemm2 tiles: 0 off (default), 1 forward-type epilogues, 2 also backward epilogues");
   m.def("igemm2_set", [](int mode, int tile) { zoo_igemm2_set(mode, tile); },
