@@ -341,70 +341,75 @@ ZOO_DEV void cl_fwd_tile(const CLArgs& a, int m0, int lane, bf16_t* wl, int cofs
   }
 }
 
-// K-split forward step (all 4F = 16 NI rows in one wave, one pixel block): channel-blocked rows
-// (cl_stage CP: row 16 i + 4 quad + g = gate g of channel quad NI + i), so a lane's NI channels are
-// consecutive and the cell operands / results move as 16-byte vectors -- with the gate-interleaved
-// rows (channels quad + 4 i) every channel was its own 2 - 8 byte access, 56 memory instructions
-// per 16 pixels against the half reduction's 14 gathers. Launcher: F = 4 NI, NI % 4 == 0.
-template <int NI, int PF, int PART>
-ZOO_DEV void cl_fwd_tile_cp(const CLArgs& a, int m0, int lane, bf16_t* wl) {
+// Persistent forward step, channel-blocked rows (cl_stage CP: row 16 i + 4 quad + g = gate g of
+// channel cofs + quad NI + i), so a lane's NI channels are consecutive and the cell operands /
+// results move as 16-byte vectors -- with the gate-interleaved rows (channels quad + 4 i) every
+// channel was its own 2 - 8 byte access, 56 memory instructions per 16 pixels against the half
+// reduction's 14 gathers (K-split). Launcher: NI % 4 == 0, 4 F = 16 NI x row groups.
+template <int NI, int MJ, int PF, int PART>
+ZOO_DEV void cl_fwd_tile_cp(const CLArgs& a, int m0, int lane, bf16_t* wl, int cofs) {
   static_assert(NI % 4 == 0, "channel-blocked forward: 4 | NI");
-  f32x4 acc[1][NI];
+  f32x4 acc[MJ][NI];
   if constexpr (PART == 1) {
-    cl_gemm<NI, 1, true, PF, true>(a, m0, acc, lane, wl);
-    cl_part<NI, 1, 1>(a, m0, lane, acc);
+    cl_gemm<NI, MJ, true, PF, true>(a, m0, acc, lane, wl);
+    cl_part<NI, MJ, 1>(a, m0, lane, acc);
     return;
   }
   const int F = a.F;
-  const int m = m0, mc = m < a.M ? m : a.M - 1;
-  const int j0 = (lane >> 4) * NI;
-  float4 g4[NI];
-  float cp[NI];
-  {
+  const int j0 = cofs + (lane >> 4) * NI;   // the lane's NI consecutive channels
+  float4 g4[MJ][NI];
+  float cp[MJ][NI];
+#pragma unroll
+  for (int jb = 0; jb < MJ; ++jb) {
+    const int m = m0 + 16 * jb, mc = m < a.M ? m : a.M - 1;
     const size_t e0 = (size_t)mc * F + j0;
     if (a.gxb) {
 #pragma unroll
       for (int i = 0; i < NI; i += 2) {
         const uint4 u = *reinterpret_cast<const uint4*>(a.gxb + 4 * (e0 + i));
-        g4[i] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
-                            __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
-        g4[i + 1] = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
-                                __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u));
+        g4[jb][i] = make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u),
+                                __uint_as_float(u.y << 16), __uint_as_float(u.y & 0xffff0000u));
+        g4[jb][i + 1] = make_float4(__uint_as_float(u.z << 16), __uint_as_float(u.z & 0xffff0000u),
+                                    __uint_as_float(u.w << 16), __uint_as_float(u.w & 0xffff0000u));
       }
     } else {
 #pragma unroll
-      for (int i = 0; i < NI; ++i) g4[i] = *reinterpret_cast<const float4*>(a.gx + 4 * (e0 + i));
+      for (int i = 0; i < NI; ++i) g4[jb][i] = *reinterpret_cast<const float4*>(a.gx + 4 * (e0 + i));
     }
 #pragma unroll
     for (int i = 0; i < NI; i += 4) {
       const float4 c4 = a.cprev ? *reinterpret_cast<const float4*>(a.cprev + e0 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      cp[i] = c4.x;
-      cp[i + 1] = c4.y;
-      cp[i + 2] = c4.z;
-      cp[i + 3] = c4.w;
+      cp[jb][i] = c4.x;
+      cp[jb][i + 1] = c4.y;
+      cp[jb][i + 2] = c4.z;
+      cp[jb][i + 3] = c4.w;
     }
   }
-  cl_gemm<NI, 1, true, PF, true>(a, m0, acc, lane, wl);
-  if constexpr (PART == 2) cl_part<NI, 1, 2>(a, m0, lane, acc);
-  if (m >= a.M) return;
-  const size_t e = (size_t)m * F + j0;
-  float cn[NI], hn[NI];
+  cl_gemm<NI, MJ, true, PF, PART != 0>(a, m0, acc, lane, wl);
+  if constexpr (PART == 2) cl_part<NI, MJ, 2>(a, m0, lane, acc);
 #pragma unroll
-  for (int i = 0; i < NI; ++i) {
-    const float4 g = g4[i];
-    const float ig = lstm_act(acc[0][i][0] + g.x, a.iact), fg = lstm_act(acc[0][i][1] + g.y, a.iact);
-    const float cg = lstm_act(acc[0][i][2] + g.z, a.act), og = lstm_act(acc[0][i][3] + g.w, a.iact);
-    cn[i] = fg * cp[i] + ig * cg;
-    hn[i] = og * lstm_act(cn[i], a.act);
-    *reinterpret_cast<float4*>(a.acts + 4 * (e + i)) = make_float4(ig, fg, cg, og);
-  }
+  for (int jb = 0; jb < MJ; ++jb) {
+    const int m = m0 + 16 * jb;
+    if (m >= a.M) continue;
+    const size_t e = (size_t)m * F + j0;
+    float cn[NI], hn[NI];
 #pragma unroll
-  for (int i = 0; i < NI; i += 4) {
-    *reinterpret_cast<float4*>(a.c + e + i) = make_float4(cn[i], cn[i + 1], cn[i + 2], cn[i + 3]);
-    *reinterpret_cast<float4*>(a.h + e + i) = make_float4(hn[i], hn[i + 1], hn[i + 2], hn[i + 3]);
-    *reinterpret_cast<uint2*>(a.hb + (size_t)m * a.ldh + j0 + i) =
-        make_uint2((uint32_t)f2bf(hn[i]) | ((uint32_t)f2bf(hn[i + 1]) << 16),
-                   (uint32_t)f2bf(hn[i + 2]) | ((uint32_t)f2bf(hn[i + 3]) << 16));
+    for (int i = 0; i < NI; ++i) {
+      const float4 g = g4[jb][i];
+      const float ig = lstm_act(acc[jb][i][0] + g.x, a.iact), fg = lstm_act(acc[jb][i][1] + g.y, a.iact);
+      const float cg = lstm_act(acc[jb][i][2] + g.z, a.act), og = lstm_act(acc[jb][i][3] + g.w, a.iact);
+      cn[i] = fg * cp[jb][i] + ig * cg;
+      hn[i] = og * lstm_act(cn[i], a.act);
+      *reinterpret_cast<float4*>(a.acts + 4 * (e + i)) = make_float4(ig, fg, cg, og);
+    }
+#pragma unroll
+    for (int i = 0; i < NI; i += 4) {
+      *reinterpret_cast<float4*>(a.c + e + i) = make_float4(cn[i], cn[i + 1], cn[i + 2], cn[i + 3]);
+      *reinterpret_cast<float4*>(a.h + e + i) = make_float4(hn[i], hn[i + 1], hn[i + 2], hn[i + 3]);
+      *reinterpret_cast<uint2*>(a.hb + (size_t)m * a.ldh + j0 + i) =
+          make_uint2((uint32_t)f2bf(hn[i]) | ((uint32_t)f2bf(hn[i + 1]) << 16),
+                     (uint32_t)f2bf(hn[i + 2]) | ((uint32_t)f2bf(hn[i + 3]) << 16));
+    }
   }
 }
 
@@ -552,7 +557,7 @@ __global__ __launch_bounds__(64 * CL_WAVES) void convlstm_bwd_kernel(CLArgs a) {
 // against 3.5M MFMAs, profiles/r6/ab23_pmc*_sum_r6.txt); the first launch stores its fp32 sums, the
 // second adds them before the cell.
 constexpr int CL_PW = 8;
-template <int NI, int MJ, bool BWD, int PART>
+template <int NI, int MJ, bool BWD, int PART, bool CP>
 __global__ __launch_bounds__(64 * CL_PW) void convlstm_pers_kernel(CLArgs a, int RG) {
   extern __shared__ __attribute__((aligned(16))) char cl_smem[];
   bf16_t* wl = reinterpret_cast<bf16_t*>(cl_smem);
@@ -563,7 +568,7 @@ __global__ __launch_bounds__(64 * CL_PW) void convlstm_pers_kernel(CLArgs a, int
   CLArgs ag = a;
   ag.Wt = a.Wt + (size_t)r0 * a.ldw;
   ag.Nr = a.Nr - r0;
-  cl_stage<NI, CL_PPF, !BWD && PART != 0>(ag, wl);
+  cl_stage<NI, CL_PPF, CP>(ag, wl);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   constexpr int TPX = 16 * MJ * CL_PW;
   const int ntiles = (a.M + TPX - 1) / TPX;
@@ -571,8 +576,8 @@ __global__ __launch_bounds__(64 * CL_PW) void convlstm_pers_kernel(CLArgs a, int
     const int m0 = (t * CL_PW + wv) * 16 * MJ + (lane & 15);
     if constexpr (BWD)
       cl_bwd_tile<NI, MJ, true, false, CL_PPF, PART>(ag, m0, lane, wl, r0);
-    else if constexpr (PART != 0)
-      cl_fwd_tile_cp<NI, CL_PPF, PART>(ag, m0, lane, wl);
+    else if constexpr (CP)
+      cl_fwd_tile_cp<NI, MJ, CL_PPF, PART>(ag, m0, lane, wl, r0 / 4);
     else
       cl_fwd_tile<NI, MJ, true, false, CL_PPF, PART>(ag, m0, lane, wl, r0 / 4);
   }
@@ -603,11 +608,12 @@ static int g_cl_pers = 1;
 // forward K-split also at >= 64k pixels (0: the row-group kernel there: its one launch without the
 // fp32 partial round trip ran the 32^3 forward step in 210 vs 260 us, ab22 / ab26 totals)
 static int g_cl_fks = 0;
+static int g_cl_cp = 1;   // channel-blocked epilogue on the row-group forward (A/B: pers_set bit 3)
 static int g_cl_ncu = 0;
 
-template <int NIG, int MJ, bool BWD, int PART = 0>
+template <int NIG, int MJ, bool BWD, int PART = 0, bool CP = false>
 static hipError_t cl_launch_pers(const CLArgs& a, int RG, size_t smem, hipStream_t st) {
-  auto kf = &convlstm_pers_kernel<NIG, MJ, BWD, PART>;
+  auto kf = &convlstm_pers_kernel<NIG, MJ, BWD, PART, CP>;
   const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(kf),
                                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   if (e != hipSuccess) return e;
@@ -645,15 +651,21 @@ static hipError_t cl_launch_dir(const CLArgs& a, hipStream_t st) {
         a0.c_cnt = KH;
         a1.c_beg = KH;
         a1.c_cnt = KC - KH;
-        const hipError_t e = cl_launch_pers<NI, MJK, BWD, 1>(a0, 1, ks, st);
+        const hipError_t e = cl_launch_pers<NI, MJK, BWD, 1, !BWD>(a0, 1, ks, st);
         if (e != hipSuccess) return e;
-        return cl_launch_pers<NI, MJK, BWD, 2>(a1, 1, ks, st);
+        return cl_launch_pers<NI, MJK, BWD, 2, !BWD>(a1, 1, ks, st);
       }
     }
   }
   if (a.X && a.M >= 65536 && smem > CL_LDS_MAX && g_cl_pers) {
     if constexpr (NI % 2 == 0 && NI / 2 <= (BWD ? 1 : 5)) {   // register-bound: no spills
-      if (psmem / 2 <= CL_LDS_MAX) return cl_launch_pers<NI / 2, 2, BWD>(a, 2, psmem / 2, st);
+      if (psmem / 2 <= CL_LDS_MAX) {
+        if constexpr (!BWD && (NI / 2) % 4 == 0) {   // channel-blocked epilogue where the rows allow
+          if (4 * a.F == 16 * NI && (a.ldh % 4) == 0 && g_cl_cp)
+            return cl_launch_pers<NI / 2, 2, BWD, 0, true>(a, 2, psmem / 2, st);
+        }
+        return cl_launch_pers<NI / 2, 2, BWD>(a, 2, psmem / 2, st);
+      }
     }
     if constexpr (NI % 4 == 0 && NI / 4 <= (BWD ? 1 : 5)) {
       if (psmem / 4 <= CL_LDS_MAX) return cl_launch_pers<NI / 4, 2, BWD>(a, 4, psmem / 4, st);
@@ -702,4 +714,5 @@ extern "C" hipError_t zoo_convlstm_step(const void* X, const void* Wt, int B, in
 extern "C" void zoo_convlstm_pers_set(int on) {
   g_cl_pers = on & 3;
   g_cl_fks = (on >> 2) & 1;   // 4 | mode: forward K-split at every size (A/B)
+  g_cl_cp = ((on >> 3) & 1) ? 0 : 1;   // 8 | mode: gate-interleaved epilogue on the row-group forward
 }

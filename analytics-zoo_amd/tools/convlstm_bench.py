@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--dims", type=int, default=2, choices=[2, 3])
     ap.add_argument("--modes", default=None, help="comma-separated subset of loop,seq,fused (profiling); "
                     "fused_np = fused with the persistent step kernels off, fused_rg = row-group persistent only, "
-                    "fused_fks = forward K-split at every size (A/B)")
+                    "fused_fks = forward K-split at every size, fused_ncp = gate-interleaved row-group forward epilogue (A/B)")
     a = ap.parse_args()
     from zoo.pipeline.api.keras.layers import recurrent as R
     torch.manual_seed(0)
@@ -41,16 +41,16 @@ def main():
     res = {"bench": "convlstm%dd-fwd-bwd" % a.dims, "T": a.T, "batch": a.batch, "hw": a.hw, "cin": a.cin,
            "filters": a.filters}
     outs = {}
-    names = {0: "loop", 1: "seq", 2: "fused", 3: "fused_np", 4: "fused_rg", 5: "fused_fks"}
+    names = {0: "loop", 1: "seq", 2: "fused", 3: "fused_np", 4: "fused_rg", 5: "fused_fks", 6: "fused_ncp"}
     from zoo.ops._kern import native
     # ConvLSTM3D has no separate whole-sequence mode: SEQ without FUSED is its per-step loop
     modes = (0, 1, 2) if a.dims == 2 else (0, 2)
     if a.modes:
-        modes = [m for m in (0, 1, 2, 3, 4, 5) if names[m] in a.modes.split(",") and (m != 1 or a.dims == 2)]
+        modes = [m for m in (0, 1, 2, 3, 4, 5, 6) if names[m] in a.modes.split(",") and (m != 1 or a.dims == 2)]
     for mode in modes:
         R._CONVLSTM_SEQ = mode > 0
         R._CONVLSTM_FUSED = mode >= 2
-        native().convlstm_pers_set({3: 0, 4: 2, 5: 5}.get(mode, 1))
+        native().convlstm_pers_set({3: 0, 4: 2, 5: 5, 6: 9}.get(mode, 1))
 
         def step():
             x.grad = None
@@ -76,10 +76,10 @@ def main():
         res["speedup_seq"] = round(res["ms_loop"] / res["ms_seq"], 2)
     if "ms_fused" in res:
         res["speedup"] = round(res["ms_loop"] / res["ms_fused"], 2)
-    for n in ("np", "rg", "fks"):
+    for n in ("np", "rg", "fks", "ncp"):
         if "ms_fused_" + n in res:
             res["speedup_" + n] = round(res["ms_loop"] / res["ms_fused_" + n], 2)
-    for mode in [m for m in (1, 2, 3, 4, 5) if m in outs and 0 in outs]:
+    for mode in [m for m in (1, 2, 3, 4, 5, 6) if m in outs and 0 in outs]:
         for k, n in enumerate(("y", "dx", "dWh")):
             a0, a1 = outs[0][k], outs[mode][k]
             res["rel_%s_%s" % (names[mode], n)] = round(float((a0 - a1).abs().max() /

@@ -78,7 +78,8 @@ def test_convlstm2d_fused_odd_filters_and_wide_channels(gpu, monkeypatch):
 @pytest.mark.parametrize("B,sp,f,pers", [(2, (32, 32, 32), 32, 0), (2, (32, 32, 32), 32, 1),
                                          (2, (32, 32, 32), 32, 2), (1, (41, 40, 40), 32, 1),
                                          (1, (41, 40, 40), 32, 2), (1, (41, 40, 40), 24, 1),
-                                         (1, (32, 32, 32), 32, 1), (2, (32, 32, 32), 32, 5)])
+                                         (1, (32, 32, 32), 32, 1), (2, (32, 32, 32), 32, 5),
+                                         (2, (32, 32, 32), 32, 10)])
 def test_convlstm3d_large_volume_two_blocks_per_wave(gpu, monkeypatch, B, sp, f, pers):
     """ConvLSTM3D over >= 65536 pixels per step against the per-step loop of the same layer on the
     GPU (recurrent 3-D conv + gate kernel per step): output, input and recurrent-weight gradients.
@@ -87,7 +88,8 @@ def test_convlstm3d_large_volume_two_blocks_per_wave(gpu, monkeypatch, B, sp, f,
     LDS, fp32 partial sums between them); pers 2: the persistent row-group kernel (2 row groups whose
     weights fit LDS). 41 x 40 x 40 leaves a partial last tile, 24 filters partial row blocks;
     1 x 32^3 = 32768 pixels is the K-split path's lower bound (there the forward is K-split too; at
-    64k+ pixels it runs the row-group kernel unless pers 5 = 1 | 4 forces the forward K-split)."""
+    64k+ pixels it runs the row-group kernel unless pers 5 = 1 | 4 forces the forward K-split; the
+    row-group forward has the channel-blocked epilogue unless pers 10 = 2 | 8)."""
     from zoo.ops._kern import native
     from zoo.pipeline.api.keras.layers import recurrent as R
     torch.manual_seed(4)
