@@ -651,7 +651,11 @@ static hipError_t cl_launch_dir(const CLArgs& a, hipStream_t st) {
         a0.c_cnt = KH;
         a1.c_beg = KH;
         a1.c_cnt = KC - KH;
-        const hipError_t e = cl_launch_pers<NI, MJK, BWD, 1, !BWD>(a0, 1, ks, st);
+        // the first half has no epilogue operands: two pixel blocks per wave (more gathers in flight)
+        // once there are tiles for every workgroup (at 32k pixels 256-pixel tiles left half the
+        // CUs idle: 16^3 3.25 vs 2.97 ms; 32^3 18.41-18.49 vs 18.57-18.60 ms, ab35)
+        const hipError_t e = a.M >= 65536 ? cl_launch_pers<NI, 2, BWD, 1, !BWD>(a0, 1, ks, st)
+                                          : cl_launch_pers<NI, MJK, BWD, 1, !BWD>(a0, 1, ks, st);
         if (e != hipSuccess) return e;
         return cl_launch_pers<NI, MJK, BWD, 2, !BWD>(a1, 1, ks, st);
       }
